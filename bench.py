@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""GE2E training-step benchmark (BASELINE.json metric: embeddings/sec + GE2E steps/sec at
+N=64 x M=10, T=160, 40 mels, 3-layer LSTM 768 -> 256).
+
+One "step" = SpeechEmbedder forward + GE2E loss + backward + clip_grad_norm_ (3.0 / 1.0)
++ SGD on one N x M batch per GPU (GE2ETrainer.step, all HIP kernels).  Multi-GPU: one
+process per GPU (torchrun), speakers sharded across ranks (global batch = world * N
+speakers, exact single-batch semantics via ShardedGE2E), SUM all-reduce of gradients over
+RCCL; per-GPU work is fixed, so scaling is weak.
+
+Prints ONE JSON line on rank 0.  value = training embeddings/s of the whole job
+(world * N * M * steps / max-over-ranks time).  Extra fields: steps_per_sec,
+fwd_embeddings_per_sec (no-grad forward), roofline (dominant kernel, live HIP-event
+timing on the kernel's stream), cpu_baseline (the reference path on host cores,
+oracle/torch_port.py, rank 0 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MI355X_FP32_MFMA_TFLOPS = 157.3   # /opt/skills/guides/MI355X_MICROARCH.md, chip-level table
+MI355X_HBM_GBPS = 8000.0
+
+
+def step_flops(B, T, F, H, P, L):
+    """Algorithmic FLOPs: fwd = 2BTG[(F+H) + 2(2H)] ... as stated there:
+    fwd = sum over layers of 2*B*T*4H*(F_l + H) + 2*B*H*P; step = 3*fwd - 2*B*T*4H*F."""
+    G = 4 * H
+    fwd = sum(2 * B * T * G * ((F if l == 0 else H) + H) for l in range(L)) + 2 * B * H * P
+    return fwd, 3 * fwd - 2 * B * T * G * F
+
+
+def build_model(dims, dev, seed=0):
+    from pytorch_speaker_verification_amd.hparam import hparam as hp
+    from pytorch_speaker_verification_amd.speech_embedder_net import GE2ELoss, SpeechEmbedder
+    old = (hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj)
+    hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj = dims
+    try:
+        torch.manual_seed(seed)  # reference init (xavier_normal_ / zero bias / Linear default)
+        net = SpeechEmbedder()
+    finally:
+        hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj = old
+    return net.to(dev), GE2ELoss(dev)
+
+
+def time_step_kernel(B, H, dev, reps=64):
+    """Average duration of the forward recurrent-step kernel (K2), HIP events on the
+    stream it is launched on.  Returns (ms per launch, FLOPs per launch)."""
+    from pytorch_speaker_verification_amd._lib import call, ptr, stream_of
+    g = torch.Generator(device="cpu").manual_seed(7)
+    whh = (torch.randn(4 * H, H, generator=g) * 0.02).to(dev)
+    hprev = torch.randn(B, H, generator=g).to(dev)
+    cprev = torch.randn(B, H, generator=g).to(dev)
+    gates0 = torch.randn(B, 4 * H, generator=g).to(dev)
+    gates = gates0.clone()
+    c_t = torch.empty(B, H, device=dev)
+    h_t = torch.empty(B, H, device=dev)
+    s = torch.cuda.current_stream(dev)
+    for _ in range(8):
+        call("sv_lstm_step_fwd", ptr(hprev), ptr(whh), ptr(gates), ptr(cprev), ptr(c_t), ptr(h_t), B, H, stream_of(gates))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        call("sv_lstm_step_fwd", ptr(hprev), ptr(whh), ptr(gates), ptr(cprev), ptr(c_t), ptr(h_t), B, H, stream_of(gates))
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps, 2.0 * B * H * 4 * H
+
+
+def cpu_baseline(dims, N, M, T, seconds_budget=25.0):
+    """The reference's CPU path (stock PyTorch port, oracle/torch_port.py) on host cores,
+    one full training step of the same workload (bounded sample)."""
+    from oracle import torch_port
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    net = torch_port.SpeechEmbedderPort(*dims)
+    w = torch.nn.Parameter(torch.tensor(10.0))
+    b = torch.nn.Parameter(torch.tensor(-5.0))
+    opt = torch.optim.SGD([{"params": net.parameters()}, {"params": [w, b]}], lr=0.01)
+    g = torch.Generator().manual_seed(1235)
+    # warm oneDNN on a small batch first
+    xw = torch.randn(4 * 2, 16, dims[0], generator=g)
+    torch_port.train_step(net, w, b, opt, xw, 4, 2)
+    x = torch.randn(N * M, T, dims[0], generator=g)
+    t0 = time.perf_counter()
+    torch_port.train_step(net, w, b, opt, x, N, M)
+    dt = time.perf_counter() - t0
+    return {"value": round(N * M / dt, 3), "unit": "embeddings/s", "cores": threads, "kind": "port",
+            "steps_per_sec": round(1.0 / dt, 5), "sec_per_step": round(dt, 3),
+            "sample": f"1 full training step (fwd+GE2E+bwd+clip+SGD) of N={N}xM={M}, T={T}, fp32, "
+                      f"oracle/torch_port.py (nn.LSTM on oneDNN), {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--N", type=int, default=64)
+    ap.add_argument("--M", type=int, default=10)
+    ap.add_argument("--T", type=int, default=160)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fwd-steps", type=int, default=5)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from pytorch_speaker_verification_amd.ops import embedder_forward
+    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+
+    dims = (40, 768, 3, 256)
+    N, M, T = args.N, args.M, args.T
+    B = N * M
+    net, ge2e = build_model(dims, dev)
+    tr = GE2ETrainer(net, ge2e, lr=0.01)
+    g = torch.Generator(device="cpu").manual_seed(1234 + 1 + rank)   # SURVEY §8d seed 1234 + config index
+    x = torch.randn(B, T, dims[0], generator=g).to(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        tr.step(x, N, M)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = tr.step(x, N, M)
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    final_loss = float(loss)
+
+    # forward-only (inference) embeddings/s
+    layers = net.LSTM_stack.layer_params()
+    with torch.no_grad():
+        for _ in range(2):
+            embedder_forward(x, layers, net.projection.weight, net.projection.bias, save=False)
+        barrier()
+        tf0 = time.perf_counter()
+        for _ in range(args.fwd_steps):
+            embedder_forward(x, layers, net.projection.weight, net.projection.bias, save=False)
+        barrier()
+        tf = (time.perf_counter() - tf0) / args.fwd_steps
+
+    fwd_fl, st_fl = step_flops(B, T, dims[0], dims[1], dims[3], dims[2])
+    ms_step = dt / args.steps * 1e3
+    out = {
+        "metric": "embeddings/sec + GE2E steps/sec at N=64×M=10, 1/2/4/8 MI355X",
+        "value": round(world * B * args.steps / dt, 3),
+        "unit": "embeddings/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic x~N(0,1) frames, reference init (torch.manual_seed(0))",
+        "config": {"workload": f"GE2E train step N={N}xM={M} per GPU, T={T}, 40 mels, LSTM 3x768, proj 256",
+                   "global_batch": world * B, "speakers_global": world * N, "seq_len": T,
+                   "parallelism": f"dp{world} (speaker-sharded GE2E, RCCL grad all-reduce)"},
+        "steps_per_sec": round(args.steps / dt, 4),
+        "fwd_embeddings_per_sec": round(world * B / tf, 1),
+        "loss": round(final_loss, 5),
+        "step_tflops": round(st_fl / (ms_step * 1e-3) / 1e12, 2),
+        "step_mfma_frac": round(st_fl / (ms_step * 1e-3) / 1e12 / MI355X_FP32_MFMA_TFLOPS, 4),
+    }
+    if rank == 0:
+        ms_k, fl_k = time_step_kernel(B, dims[1], dev)
+        ach = fl_k / (ms_k * 1e-3) / 1e12
+        out["roofline"] = {"kernel": "lstm_step_fwd_kernel (K2, fp32 MFMA 32x32x2)", "bound": "mfma",
+                           "achieved": round(ach, 2), "peak": MI355X_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(ach / MI355X_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                           "avg_launch_us": round(ms_k * 1e3, 2), "flops_per_launch": fl_k}
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(dims, N, M, T)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,110 @@
+/* C ABI of libsv_ge2e.so -- the MI355X (gfx950) GE2E speaker-embedding training path.
+ *
+ * The reference (hwidong-na/PyTorch_Speaker_Verification) is pure Python over PyTorch and
+ * has no FFI of its own; each entry point below replaces the device work PyTorch launches
+ * implicitly at the cited reference line (SURVEY.md §2 "implicit op" table, §8 b).
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a caller-owned, contiguous, row-major DEVICE buffer (fp32), 16-byte
+ *     aligned; scalars such as w, b, gloss are device pointers to one float (no host sync);
+ *   - nothing is allocated, no global state is kept, no pointer is retained after return;
+ *     scratch comes from a caller workspace of the size the matching *_workspace* returns;
+ *   - every launch goes to `stream` (pass the current stream of the tensor's device: the
+ *     *_bwd functions are called from the autograd engine's worker thread);
+ *   - return 0 on success, a hipError_t (> 0) from a failed launch, or a negative
+ *     argument error (SV_EARG -1, SV_EALIGN -2, SV_ESHAPE -3).  Functions are reentrant.
+ */
+#ifndef SV_GE2E_H
+#define SV_GE2E_H
+
+#include <stddef.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SV_ABI_VERSION 1
+int sv_abi_version(void);
+
+/* ---- dense fp32 MFMA GEMM (used by every op below; exported for tests) -----------------
+ * C[M,N] = op(A) op(B) (+ bias0[n] + bias1[n]) (+ beta C).
+ * a_kcontig: A element (m,k) at A[m*lda+k], else at A[k*lda+m].
+ * b_kcontig: B element (k,n) at B[n*ldb+k], else at B[k*ldb+n].  */
+size_t sv_gemm_f32_workspace(int M, int N, int K);
+int sv_gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
+                float* C, long ldc, const float* bias0, const float* bias1, float beta, float* workspace,
+                hipStream_t stream);
+
+/* column sums of X[R,C] (deterministic two-level reduction) */
+size_t sv_colsum_workspace(int R, int C);
+int sv_colsum(const float* X, int R, int C, float* out, float* workspace, hipStream_t stream);
+
+/* ---- SpeechEmbedder LSTM stack (replaces nn.LSTM fwd, speech_embedder_net.py:19,28, and its
+ * autograd backward via train_speech_embedder.py:62).  Time-major layouts:
+ *   x_tm [T,B,F], gates [T,B,4H] (activated i,f,g,o), c_tm [T,B,H], h_tm [T+1,B,H] (h_tm[0]=0). */
+int sv_frames_to_time_major(const float* x, float* x_tm, int B, int T, int F, hipStream_t stream);
+int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, const float* w_ih, const float* w_hh,
+                      const float* b_ih, const float* b_hh, float* gates, float* c_tm, float* h_tm,
+                      hipStream_t stream);
+/* one forward recurrent step (K2): on entry gates_t [B,4H] = x_t W_ih^T + b_ih + b_hh, on exit the
+ * activated gates; h_prev / c_prev may be NULL (t = 0). */
+int sv_lstm_step_fwd(const float* h_prev, const float* w_hh, float* gates_t, const float* c_prev, float* c_t,
+                     float* h_t, int B, int H, hipStream_t stream);
+size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H);
+/* dh_up: gradient w.r.t. this layer's outputs; dh_up_full=1 -> [T,B,H], 0 -> [B,H] for t=T-1 only.
+ * Outputs dgates [T,B,4H], dx_tm [T,B,F] (may be NULL), dw_ih [4H,F], dw_hh [4H,H],
+ * db_ih [4H] and db_hh [4H] (may be NULL; both equal sum dgates). */
+int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* x_tm, const float* w_ih, const float* w_hh,
+                      const float* gates, const float* c_tm, const float* h_tm, const float* dh_up, int dh_up_full,
+                      float* dgates, float* dx_tm, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh,
+                      float* workspace, hipStream_t stream);
+
+/* ---- projection + L2 norm (speech_embedder_net.py:30-32) --------------------------------- */
+size_t sv_proj_norm_workspace(int B, int H, int P);
+int sv_proj_norm_fwd(const float* h_last, int B, int H, int P, const float* w_p, const float* b_p, float* y,
+                     float* emb, float* ynorm, float* workspace, hipStream_t stream);
+int sv_proj_norm_bwd(const float* demb, const float* emb, const float* ynorm, const float* h_last, int B, int H, int P,
+                     const float* w_p, float* dw_p, float* db_p, float* dh_last, float* workspace,
+                     hipStream_t stream);
+
+/* ---- GE2E loss (speech_embedder_net.py:43-49; utils.py:27-132) -----------------------------
+ * E is the local block [N_local, M, D] of a batch of N speakers; its first speaker is global
+ * speaker spk_offset.  ssum_all [N,D] = per-speaker sums (all-gathered when sharded).
+ * D % 4 == 0 and M >= 2.  dchat buffers are [Np, D] with Np = (N + 3) & ~3.
+ * The workspace carries state from fwd to bwd: keep it alive and untouched in between. */
+size_t sv_ge2e_workspace_size(int N_local, int M, int D, int N);
+int sv_ge2e_speaker_sums(const float* E, int N_local, int M, int D, float* ssum_local, hipStream_t stream);
+int sv_ge2e_fwd_rows(const float* E, int N_local, int M, int D, int spk_offset, int N, const float* ssum_all,
+                     const float* w, const float* b, float* per, float* loss_local, float* workspace,
+                     hipStream_t stream);
+int sv_ge2e_fwd(const float* E, int N, int M, int D, const float* w, const float* b, float* loss, float* per,
+                float* workspace, float* ssum, hipStream_t stream);
+/* dchat_partial [Np,D] and beta_partial [N]: this shard's contribution (sum over ranks before
+ * finalize); dwdb [2] = this shard's (dL/dw, dL/db).  gloss = upstream dL (NULL -> 1). */
+int sv_ge2e_bwd_rows(int N_local, int M, int D, int spk_offset, int N, const float* w, const float* b,
+                     const float* gloss, float* dchat_partial, float* beta_partial, float* dwdb, float* workspace,
+                     hipStream_t stream);
+int sv_ge2e_bwd_finalize(int N_local, int M, int D, int spk_offset, int N, const float* dchat, const float* beta,
+                         float* dE, float* workspace, hipStream_t stream);
+int sv_ge2e_bwd(int N, int M, int D, const float* w, const float* b, const float* gloss, float* dE, float* dwdb,
+                float* dchat, float* beta, float* workspace, hipStream_t stream);
+
+/* stand-alone helpers (utils.py): C = E.mean(1) [N,D]; cos [N,M,Nc] = get_cossim(E, C) with the
+ * diagonal from E's own leave-one-out centroids (utils.py:75,91,113), +1e-6; calc_loss on S [N,M,K]. */
+int sv_ge2e_centroids(const float* E, int N, int M, int D, float* C, hipStream_t stream);
+size_t sv_ge2e_cossim_workspace(int N, int M, int D, int Nc);
+int sv_ge2e_cossim(const float* E, int N, int M, int D, const float* C, int Nc, float* cos, float* workspace,
+                   hipStream_t stream);
+int sv_ge2e_calc_loss(const float* S, int N, int M, int K, float* per, float* loss, hipStream_t stream);
+
+/* ---- clip_grad_norm_ + SGD step over one flat parameter group (train_speech_embedder.py:63-65)
+ * p -= lr * min(1, max_norm / (|g|_2 + 1e-6)) * g; write_grad=1 also scales g in place. */
+size_t sv_clip_sgd_workspace(void);
+int sv_clip_sgd_step(float* params, float* grads, long n, float max_norm, float lr, int write_grad,
+                     float* total_norm_out, float* workspace, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SV_GE2E_H */

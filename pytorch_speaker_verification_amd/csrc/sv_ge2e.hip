@@ -1,0 +1,494 @@
+// GE2E loss (forward + closed-form backward) on gfx950.
+//
+// Replaces the reference's GE2ELoss.forward (speech_embedder_net.py:43-49) and the ATen
+// ops of utils.py:27-132 (get_centroids, get_utterance_centroids, get_cossim, calc_loss)
+// plus their autograd backward -- SURVEY §8 rows a-D .. a-G.
+//
+// Rows r = j*M + i of the local embedding block E[N_local, M, D] belong to speaker
+// s0 + j of the N speakers in the (possibly multi-GPU) batch.  Centroids come from the
+// speaker sums Ssum[N, D] (all-gathered across ranks in data-parallel runs).
+//
+//   cos[r, k]   = <E^_r, C^_k>                      (fp32 MFMA GEMM, C^ tiles in LDS)
+//   cos[r, s(r)] := <E^_r, U^_r>, U_r = (Ssum_s(r) - E_r) / (M - 1)   (leave-one-out)
+//   S = w (cos + 1e-6) + b;  per_r = log(sum_k e^S + 1e-6) - S[r, s(r)];  loss = sum per
+// with x^ = x / max(|x|, 1e-8) (torch cosine_similarity).
+#include <algorithm>
+#include "sv_common.h"
+#include "../../include/sv_ge2e.h"
+
+#define EPS_COS 1e-8f
+#define EPS_SIM 1e-6f
+#define EPS_LOG 1e-6f
+
+namespace {
+
+// workspace carve (all fp32), see sv_ge2e_workspace_size
+struct Ge2eWs {
+  float *Ehat, *Uhat, *En, *Un, *rawd, *cos, *logz, *Chat, *Cn, *dcos, *alpha, *G1, *dwdb_rows, *gemm;
+  size_t total;
+};
+
+size_t al(size_t n) { return (n + 63) & ~size_t(63); }  // 256-byte granules
+
+Ge2eWs carve(float* base, int Nl, int M, int D, int N) {
+  Ge2eWs w;
+  N = (N + 3) & ~3;  // speaker dimension padded to a multiple of 4 (zero rows/cols)
+  const size_t Bl = (size_t)Nl * M;
+  size_t off = 0;
+  auto take = [&](size_t n) {
+    float* p = base ? base + off : nullptr;
+    off += al(n);
+    return p;
+  };
+  w.Ehat = take(Bl * D);
+  w.Uhat = take(Bl * D);
+  w.En = take(Bl);
+  w.Un = take(Bl);
+  w.rawd = take(Bl);
+  w.cos = take(Bl * N);
+  w.logz = take(Bl);
+  w.Chat = take((size_t)N * D);
+  w.Cn = take(N);
+  w.dcos = take(Bl * N);
+  w.alpha = take(Bl);
+  w.G1 = take(Bl * D);
+  w.dwdb_rows = take(2 * Bl);
+  const size_t g1 = sv_gemm_f32_workspace((int)Bl, D, N);
+  const size_t g2 = sv_gemm_f32_workspace(N, D, (int)Bl);
+  w.gemm = take((std::max(g1, g2) + 3) / 4);
+  w.total = off * sizeof(float);
+  return w;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// K6a: per-speaker sums Ssum[j, :] = sum_i E[j, i, :]  (fixed order i = 0..M-1)
+__global__ void ge2e_sums_kernel(const float* __restrict__ E, int M, int D, float* __restrict__ ssum) {
+  const int j = blockIdx.x;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int i = 0; i < M; ++i) s += E[((long)j * M + i) * D + d];
+    ssum[(long)j * D + d] = s;
+  }
+}
+
+// block-wide sum (blockDim = 256)
+__device__ float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+// K6b: centroids C = Ssum / M (get_centroids, utils.py:27-29), C^ and |C|
+__global__ __launch_bounds__(256) void ge2e_centroid_kernel(const float* __restrict__ ssum, int N, int M, int D,
+                                                            float* __restrict__ Chat, float* __restrict__ Cn) {
+  __shared__ float red[4];
+  const int k = blockIdx.x;
+  if (k >= N) {  // padding rows of C^ (speaker dim rounded up to 4)
+    for (int d = threadIdx.x; d < D; d += 256) Chat[(long)k * D + d] = 0.f;
+    if (threadIdx.x == 0) Cn[k] = 0.f;
+    return;
+  }
+  float ss = 0.f;
+  for (int d = threadIdx.x; d < D; d += 256) {
+    const float c = ssum[(long)k * D + d] / (float)M;
+    ss += c * c;
+  }
+  const float n = sqrtf(block_sum256(ss, red));
+  const float inv = 1.0f / fmaxf(n, EPS_COS);
+  for (int d = threadIdx.x; d < D; d += 256) Chat[(long)k * D + d] = (ssum[(long)k * D + d] / (float)M) * inv;
+  if (threadIdx.x == 0) Cn[k] = n;
+}
+
+// K6c: per-row normalisation, leave-one-out centroid and the diagonal cosine.  One wave per row.
+__global__ __launch_bounds__(256) void ge2e_rowprep_kernel(const float* __restrict__ E, const float* __restrict__ ssum,
+                                                           int Bl, int M, int D, int s0, float* __restrict__ Ehat,
+                                                           float* __restrict__ Uhat, float* __restrict__ En,
+                                                           float* __restrict__ Un, float* __restrict__ rawd) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= Bl) return;
+  const int sg = s0 + r / M;
+  const float* e = E + (long)r * D;
+  const float* s = ssum + (long)sg * D;
+  const float invm1 = 1.0f / (float)(M - 1);
+  float ee = 0.f, uu = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const float x = e[d];
+    const float u = (s[d] - x) * invm1;
+    ee += x * x;
+    uu += u * u;
+  }
+  const float ne = sqrtf(wave_sum(ee)), nu = sqrtf(wave_sum(uu));
+  const float ie = 1.0f / fmaxf(ne, EPS_COS), iu = 1.0f / fmaxf(nu, EPS_COS);
+  float dot = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const float x = e[d] * ie;
+    const float u = ((s[d] - e[d]) * invm1) * iu;
+    Ehat[(long)r * D + d] = x;
+    Uhat[(long)r * D + d] = u;
+    dot += x * u;
+  }
+  dot = wave_sum(dot);
+  if (lane == 0) {
+    En[r] = ne;
+    Un[r] = nu;
+    rawd[r] = dot;
+  }
+}
+
+// K6d: row softmax-contrast loss.  One wave per row; lanes stride the N speakers.
+__global__ __launch_bounds__(256) void ge2e_rowloss_kernel(float* __restrict__ cos, const float* __restrict__ rawd,
+                                                           int Bl, int M, int N, int ldc, int s0,
+                                                           const float* __restrict__ wp,
+                                                           const float* __restrict__ bp, float* __restrict__ per,
+                                                           float* __restrict__ logz) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= Bl) return;
+  const int sg = s0 + r / M;
+  const float w = *wp, b = *bp;
+  float* c = cos + (long)r * ldc;
+  if (lane == 0) c[sg] = rawd[r];  // get_cossim's diagonal overwrite (utils.py:112-113)
+  float mx = -INFINITY;
+  for (int k = lane; k < N; k += 64) {
+    const float cr = (k == sg) ? rawd[r] : c[k];
+    mx = fmaxf(mx, w * (cr + EPS_SIM) + b);
+  }
+  mx = fmaxf(wave_max(mx), 0.f);
+  float z = 0.f;
+  for (int k = lane; k < N; k += 64) {
+    const float cr = (k == sg) ? rawd[r] : c[k];
+    z += __expf(w * (cr + EPS_SIM) + b - mx);
+  }
+  z = wave_sum(z);
+  // log(sum_k e^S + 1e-6) = mx + log(sum_k e^{S-mx} + 1e-6 e^{-mx}), mx >= 0
+  const float lz = mx + logf(z + EPS_LOG * __expf(-mx));
+  if (lane == 0) {
+    const float spos = w * (rawd[r] + EPS_SIM) + b;
+    per[r] = lz - spos;
+    logz[r] = lz;
+  }
+}
+
+// fixed-order sum of n floats into out[0] (single block of 256)
+__global__ __launch_bounds__(256) void sum_kernel(const float* __restrict__ x, int n, float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += x[i];
+  s = block_sum256(s, red);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+// ---------------------------------------------------------------------------
+// K7a: row backward.  dS = p - delta, dcos = w dS; writes dcos with the diagonal
+// zeroed (centroid side), alpha_r = sum_k dcos_rk raw_rk, and per-row dw/db partials.
+__global__ __launch_bounds__(256) void ge2e_rowbwd_kernel(const float* __restrict__ cos, const float* __restrict__ logz,
+                                                          int Bl, int M, int N, int ldc, int s0,
+                                                          const float* __restrict__ wp,
+                                                          const float* __restrict__ bp, const float* __restrict__ gl,
+                                                          float* __restrict__ dcos, float* __restrict__ alpha,
+                                                          float* __restrict__ dwdb) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= Bl) return;
+  const int sg = s0 + r / M;
+  const float w = *wp, b = *bp, g = gl ? *gl : 1.0f;
+  const float lz = logz[r];
+  const float* c = cos + (long)r * ldc;
+  float* dc = dcos + (long)r * ldc;
+  float a = 0.f, dw = 0.f, db = 0.f;
+  for (int k = lane; k < N; k += 64) {
+    const float cr = c[k];
+    const float cp = cr + EPS_SIM;
+    const float p = __expf(w * cp + b - lz);
+    const float ds = g * (p - (k == sg ? 1.0f : 0.0f));
+    const float dcv = w * ds;
+    a += dcv * cr;
+    dw += ds * cp;
+    db += ds;
+    dc[k] = (k == sg) ? 0.f : dcv;
+  }
+  for (int k = N + lane; k < ldc; k += 64) dc[k] = 0.f;
+  a = wave_sum(a);
+  dw = wave_sum(dw);
+  db = wave_sum(db);
+  if (lane == 0) {
+    alpha[r] = a;
+    dwdb[r] = dw;
+    dwdb[Bl + r] = db;
+  }
+}
+
+// K7b: beta_k = sum_r dcos_off[r,k] raw[r,k]  (column reduction, one thread per k)
+__global__ void ge2e_beta_kernel(const float* __restrict__ dcos, const float* __restrict__ cos, int Bl, int N,
+                                 int ldc, float* __restrict__ beta) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= N) return;
+  float s = 0.f;
+  for (int r = 0; r < Bl; ++r) s += dcos[(long)r * ldc + k] * cos[(long)r * ldc + k];
+  beta[k] = s;
+}
+
+// K7c: dw, db = fixed-order sums of the per-row partials
+__global__ __launch_bounds__(256) void ge2e_dwdb_kernel(const float* __restrict__ dwdb_rows, int Bl,
+                                                        float* __restrict__ out) {
+  __shared__ float red[4];
+  float a = 0.f, b = 0.f;
+  for (int i = threadIdx.x; i < Bl; i += 256) {
+    a += dwdb_rows[i];
+    b += dwdb_rows[Bl + i];
+  }
+  a = block_sum256(a, red);
+  b = block_sum256(b, red);
+  if (threadIdx.x == 0) {
+    out[0] = a;
+    out[1] = b;
+  }
+}
+
+// K7d: finalize dE for one local speaker per block:
+//   dC_j  = (dChat_j - beta_j C^_j [|C|>eps]) / max(|C_j|, eps)
+//   dU_r  = dcos_d (E^_r - raw_d U^_r [|U|>eps]) / max(|U_r|, eps)
+//   dE_r  = (G1_r + dcos_d U^_r - alpha_r E^_r [|E|>eps]) / max(|E_r|, eps)
+//           + dC_j / M + (sum_i' dU_ji' - dU_r) / (M - 1)
+// where dcos_d = w dS[r, s(r)] is recovered from alpha_r's definition inputs.
+__global__ __launch_bounds__(256) void ge2e_finalize_kernel(
+    int M, int D, int s0, const float* __restrict__ dchat, const float* __restrict__ beta,
+    const float* __restrict__ Chat, const float* __restrict__ Cn, const float* __restrict__ Ehat,
+    const float* __restrict__ Uhat, const float* __restrict__ En, const float* __restrict__ Un,
+    const float* __restrict__ rawd, const float* __restrict__ dcd, const float* __restrict__ alpha,
+    const float* __restrict__ G1, float* __restrict__ dE) {
+  const int j = blockIdx.x;
+  const int sg = s0 + j;
+  const float cn = Cn[sg];
+  const float icn = 1.0f / fmaxf(cn, EPS_COS);
+  const float pc = cn > EPS_COS ? 1.f : 0.f;
+  const float bj = beta[sg];
+  const float invM = 1.0f / (float)M, invm1 = 1.0f / (float)(M - 1);
+  for (int d = threadIdx.x; d < D; d += 256) {
+    const long cd = (long)sg * D + d;
+    const float dC = (dchat[cd] - bj * Chat[cd] * pc) * icn;
+    float sumdU = 0.f;
+    for (int i = 0; i < M; ++i) {
+      const int r = j * M + i;
+      const float iu = 1.0f / fmaxf(Un[r], EPS_COS);
+      const float pu = Un[r] > EPS_COS ? 1.f : 0.f;
+      sumdU += dcd[r] * (Ehat[(long)r * D + d] - rawd[r] * Uhat[(long)r * D + d] * pu) * iu;
+    }
+    for (int i = 0; i < M; ++i) {
+      const int r = j * M + i;
+      const long rd = (long)r * D + d;
+      const float iu = 1.0f / fmaxf(Un[r], EPS_COS);
+      const float pu = Un[r] > EPS_COS ? 1.f : 0.f;
+      const float dU = dcd[r] * (Ehat[rd] - rawd[r] * Uhat[rd] * pu) * iu;
+      const float ie = 1.0f / fmaxf(En[r], EPS_COS);
+      const float pe = En[r] > EPS_COS ? 1.f : 0.f;
+      const float gE = (G1[rd] + dcd[r] * Uhat[rd] - alpha[r] * Ehat[rd] * pe) * ie;
+      dE[rd] = gE + dC * invM + (sumdU - dU) * invm1;
+    }
+  }
+}
+
+// dcos on the diagonal (w dS[r, s(r)]) for the finalize step, recomputed from logz
+__global__ void ge2e_dcd_kernel(const float* __restrict__ rawd, const float* __restrict__ logz, int Bl,
+                                const float* __restrict__ wp, const float* __restrict__ bp,
+                                const float* __restrict__ gl, float* __restrict__ dcd) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= Bl) return;
+  const float w = *wp, b = *bp, g = gl ? *gl : 1.0f;
+  const float p = __expf(w * (rawd[r] + EPS_SIM) + b - logz[r]);
+  dcd[r] = w * g * (p - 1.0f);
+}
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" size_t sv_ge2e_workspace_size(int N_local, int M, int D, int N) {
+  return carve(nullptr, N_local, M, D, N).total;
+}
+
+static bool ge2e_args_ok(const float* E, int Nl, int M, int D, int s0, int N) {
+  return E && Nl > 0 && M >= 2 && D > 0 && D % 4 == 0 && N >= Nl && s0 >= 0 && s0 + Nl <= N;
+}
+
+extern "C" int sv_ge2e_speaker_sums(const float* E, int N_local, int M, int D, float* ssum_local, hipStream_t stream) {
+  if (!E || !ssum_local || N_local <= 0 || M <= 0 || D <= 0) return SV_EARG;
+  hipLaunchKernelGGL(ge2e_sums_kernel, dim3(N_local), dim3(256), 0, stream, E, M, D, ssum_local);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_ge2e_fwd_rows(const float* E, int N_local, int M, int D, int spk_offset, int N, const float* ssum_all,
+                                const float* w, const float* b, float* per, float* loss_local, float* workspace,
+                                hipStream_t stream) {
+  if (!ge2e_args_ok(E, N_local, M, D, spk_offset, N) || !ssum_all || !w || !b || !per || !workspace) return SV_EARG;
+  const Ge2eWs ws = carve(workspace, N_local, M, D, N);
+  const int Bl = N_local * M, Np = (N + 3) & ~3;
+  hipLaunchKernelGGL(ge2e_centroid_kernel, dim3(Np), dim3(256), 0, stream, ssum_all, N, M, D, ws.Chat, ws.Cn);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ge2e_rowprep_kernel, dim3((Bl + 3) / 4), dim3(256), 0, stream, E, ssum_all, Bl, M, D, spk_offset,
+                     ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd);
+  SV_LAUNCH_CHECK();
+  // cos = E^ C^T  (fp32 MFMA; rows of E^ and C^ are both D-contiguous)
+  int rc = sv_gemm_f32(1, 1, Bl, Np, D, ws.Ehat, D, ws.Chat, D, ws.cos, Np, nullptr, nullptr, 0.f, ws.gemm, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(ge2e_rowloss_kernel, dim3((Bl + 3) / 4), dim3(256), 0, stream, ws.cos, ws.rawd, Bl, M, N, Np,
+                     spk_offset, w, b, per, ws.logz);
+  SV_LAUNCH_CHECK();
+  if (loss_local) {
+    hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, stream, per, Bl, loss_local);
+    SV_LAUNCH_CHECK();
+  }
+  return SV_OK;
+}
+
+extern "C" int sv_ge2e_fwd(const float* E, int N, int M, int D, const float* w, const float* b, float* loss, float* per,
+                           float* workspace, float* ssum, hipStream_t stream) {
+  if (!ssum) return SV_EARG;
+  int rc = sv_ge2e_speaker_sums(E, N, M, D, ssum, stream);
+  if (rc) return rc;
+  return sv_ge2e_fwd_rows(E, N, M, D, 0, N, ssum, w, b, per, loss, workspace, stream);
+}
+
+extern "C" int sv_ge2e_bwd_rows(int N_local, int M, int D, int spk_offset, int N, const float* w, const float* b,
+                                const float* gloss, float* dchat_partial, float* beta_partial, float* dwdb,
+                                float* workspace, hipStream_t stream) {
+  if (N_local <= 0 || M < 2 || D <= 0 || N < N_local || !w || !b || !dchat_partial || !beta_partial || !dwdb ||
+      !workspace)
+    return SV_EARG;
+  const Ge2eWs ws = carve(workspace, N_local, M, D, N);
+  const int Bl = N_local * M, Np = (N + 3) & ~3;
+  hipLaunchKernelGGL(ge2e_rowbwd_kernel, dim3((Bl + 3) / 4), dim3(256), 0, stream, ws.cos, ws.logz, Bl, M, N, Np,
+                     spk_offset, w, b, gloss, ws.dcos, ws.alpha, ws.dwdb_rows);
+  SV_LAUNCH_CHECK();
+  // G1 = dcos_off C^   ([Bl, N] x [N, D]; C^ read as [K=N][D] row-contiguous)
+  int rc = sv_gemm_f32(1, 0, Bl, D, Np, ws.dcos, Np, ws.Chat, D, ws.G1, D, nullptr, nullptr, 0.f, ws.gemm, stream);
+  if (rc) return rc;
+  // dChat (before the norm Jacobian) = dcos_off^T E^   ([Np, Bl] x [Bl, D]); rows >= N are zero
+  rc = sv_gemm_f32(0, 0, Np, D, Bl, ws.dcos, Np, ws.Ehat, D, dchat_partial, D, nullptr, nullptr, 0.f, ws.gemm, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(ge2e_beta_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, ws.dcos, ws.cos, Bl, N, Np,
+                     beta_partial);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ge2e_dwdb_kernel, dim3(1), dim3(256), 0, stream, ws.dwdb_rows, Bl, dwdb);
+  SV_LAUNCH_CHECK();
+  // diagonal dcos into the (now free) dwdb_rows slot for the finalize step
+  hipLaunchKernelGGL(ge2e_dcd_kernel, dim3((Bl + 255) / 256), dim3(256), 0, stream, ws.rawd, ws.logz, Bl, w, b, gloss,
+                     ws.dwdb_rows);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_ge2e_bwd_finalize(int N_local, int M, int D, int spk_offset, int N, const float* dchat,
+                                    const float* beta, float* dE, float* workspace, hipStream_t stream) {
+  if (N_local <= 0 || M < 2 || D <= 0 || !dchat || !beta || !dE || !workspace) return SV_EARG;
+  const Ge2eWs ws = carve(workspace, N_local, M, D, N);
+  hipLaunchKernelGGL(ge2e_finalize_kernel, dim3(N_local), dim3(256), 0, stream, M, D, spk_offset, dchat, beta, ws.Chat,
+                     ws.Cn, ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, ws.dwdb_rows, ws.alpha, ws.G1, dE);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_ge2e_bwd(int N, int M, int D, const float* w, const float* b, const float* gloss, float* dE,
+                           float* dwdb, float* dchat, float* beta, float* workspace, hipStream_t stream) {
+  int rc = sv_ge2e_bwd_rows(N, M, D, 0, N, w, b, gloss, dchat, beta, dwdb, workspace, stream);
+  if (rc) return rc;
+  return sv_ge2e_bwd_finalize(N, M, D, 0, N, dchat, beta, dE, workspace, stream);
+}
+
+// ============================================================================
+// stand-alone forms of the reference helpers (utils.py): get_centroids, get_cossim
+// with arbitrary (e.g. enrollment) centroids, calc_loss on a given similarity matrix.
+// ============================================================================
+__global__ void ge2e_scale_kernel(float* __restrict__ x, long n, float s) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) x[i] *= s;
+}
+
+// cos[r, k] += 1e-6 for all k; cos[r, s(r)] = rawd[r] + 1e-6 when s(r) < Nc
+__global__ __launch_bounds__(256) void ge2e_cossim_fix_kernel(float* __restrict__ cos, const float* __restrict__ rawd,
+                                                              int Bl, int M, int Nc) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= Bl) return;
+  const int j = r / M;
+  float* c = cos + (long)r * Nc;
+  for (int k = lane; k < Nc; k += 64) c[k] = (k == j ? rawd[r] : c[k]) + EPS_SIM;
+}
+
+// calc_loss (utils.py:126-132) on S [N, M, K]: per[j,i] = log(sum_k e^S + 1e-6) - S[j,i,j]
+__global__ __launch_bounds__(256) void ge2e_calc_loss_kernel(const float* __restrict__ S, int Bl, int M, int K,
+                                                             float* __restrict__ per) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= Bl) return;
+  const float* s = S + (long)r * K;
+  float mx = -INFINITY;
+  for (int k = lane; k < K; k += 64) mx = fmaxf(mx, s[k]);
+  mx = fmaxf(wave_max(mx), 0.f);
+  float z = 0.f;
+  for (int k = lane; k < K; k += 64) z += __expf(s[k] - mx);
+  z = wave_sum(z);
+  if (lane == 0) per[r] = mx + logf(z + EPS_LOG * __expf(-mx)) - s[r / M];
+}
+
+extern "C" int sv_ge2e_centroids(const float* E, int N, int M, int D, float* C, hipStream_t stream) {
+  if (!E || !C || N <= 0 || M <= 0 || D <= 0) return SV_EARG;
+  hipLaunchKernelGGL(ge2e_sums_kernel, dim3(N), dim3(256), 0, stream, E, M, D, C);
+  SV_LAUNCH_CHECK();
+  const long n = (long)N * D;
+  hipLaunchKernelGGL(ge2e_scale_kernel, dim3((int)std::min<long>((n + 255) / 256, 1024)), dim3(256), 0, stream, C, n,
+                     1.0f / (float)M);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" size_t sv_ge2e_cossim_workspace(int N, int M, int D, int Nc) {
+  const size_t Bl = (size_t)N * M;
+  size_t n = al((size_t)N * D) + 2 * al(Bl * D) + 3 * al(Bl) + al((size_t)Nc * D) + al(Nc);
+  return n * sizeof(float) + sv_gemm_f32_workspace((int)Bl, Nc, D);
+}
+
+extern "C" int sv_ge2e_cossim(const float* E, int N, int M, int D, const float* C, int Nc, float* cos,
+                              float* workspace, hipStream_t stream) {
+  if (!E || !C || !cos || !workspace || N <= 0 || M < 2 || D <= 0 || D % 4 || Nc <= 0) return SV_EARG;
+  const int Bl = N * M;
+  float* p = workspace;
+  float* ssum = p; p += al((size_t)N * D);
+  float* Ehat = p; p += al((size_t)Bl * D);
+  float* Uhat = p; p += al((size_t)Bl * D);
+  float* En = p; p += al(Bl);
+  float* Un = p; p += al(Bl);
+  float* rawd = p; p += al(Bl);
+  float* Chat = p; p += al((size_t)Nc * D);
+  float* Cn = p; p += al(Nc);
+  float* gws = p;
+  hipLaunchKernelGGL(ge2e_sums_kernel, dim3(N), dim3(256), 0, stream, E, M, D, ssum);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ge2e_rowprep_kernel, dim3((Bl + 3) / 4), dim3(256), 0, stream, E, ssum, Bl, M, D, 0, Ehat, Uhat,
+                     En, Un, rawd);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ge2e_centroid_kernel, dim3(Nc), dim3(256), 0, stream, C, Nc, 1, D, Chat, Cn);
+  SV_LAUNCH_CHECK();
+  int rc = sv_gemm_f32(1, 1, Bl, Nc, D, Ehat, D, Chat, D, cos, Nc, nullptr, nullptr, 0.f, gws, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(ge2e_cossim_fix_kernel, dim3((Bl + 3) / 4), dim3(256), 0, stream, cos, rawd, Bl, M, Nc);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_ge2e_calc_loss(const float* S, int N, int M, int K, float* per, float* loss, hipStream_t stream) {
+  if (!S || !per || N <= 0 || M <= 0 || K < N) return SV_EARG;
+  const int Bl = N * M;
+  hipLaunchKernelGGL(ge2e_calc_loss_kernel, dim3((Bl + 3) / 4), dim3(256), 0, stream, S, Bl, M, K, per);
+  SV_LAUNCH_CHECK();
+  if (loss) {
+    hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, stream, per, Bl, loss);
+    SV_LAUNCH_CHECK();
+  }
+  return SV_OK;
+}

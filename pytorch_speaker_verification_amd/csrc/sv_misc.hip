@@ -1,0 +1,143 @@
+// Projection + L2 normalisation (speech_embedder_net.py:30-32, SURVEY §8 a-C) and the
+// fused gradient-clip + SGD update (train_speech_embedder.py:63-65, SURVEY §8 a-I).
+#include <algorithm>
+#include "sv_common.h"
+#include "../../include/sv_ge2e.h"
+
+// emb = y / |y|_2 (torch.norm, no eps).  One wave per row.
+__global__ __launch_bounds__(256) void rownorm_fwd_kernel(const float* __restrict__ y, int B, int P,
+                                                          float* __restrict__ emb, float* __restrict__ ynorm) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= B) return;
+  const float* yr = y + (long)r * P;
+  float ss = 0.f;
+  for (int p = lane; p < P; p += 64) ss += yr[p] * yr[p];
+  const float n = sqrtf(wave_sum(ss));
+  const float inv = 1.0f / n;
+  for (int p = lane; p < P; p += 64) emb[(long)r * P + p] = yr[p] * inv;
+  if (lane == 0) ynorm[r] = n;
+}
+
+// dy = (de - e <e, de>) / |y|
+__global__ __launch_bounds__(256) void rownorm_bwd_kernel(const float* __restrict__ demb, const float* __restrict__ emb,
+                                                          const float* __restrict__ ynorm, int B, int P,
+                                                          float* __restrict__ dy) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= B) return;
+  const float* de = demb + (long)r * P;
+  const float* e = emb + (long)r * P;
+  float dot = 0.f;
+  for (int p = lane; p < P; p += 64) dot += e[p] * de[p];
+  dot = wave_sum(dot);
+  const float inv = 1.0f / ynorm[r];
+  for (int p = lane; p < P; p += 64) dy[(long)r * P + p] = (de[p] - e[p] * dot) * inv;
+}
+
+extern "C" size_t sv_proj_norm_workspace(int B, int H, int P) {
+  size_t g = std::max(sv_gemm_f32_workspace(B, P, H), std::max(sv_gemm_f32_workspace(P, H, B), sv_gemm_f32_workspace(B, H, P)));
+  g = std::max(g, sv_colsum_workspace(B, P));
+  return ((size_t)B * P * sizeof(float) + 255) / 256 * 256 + g;
+}
+
+extern "C" int sv_proj_norm_fwd(const float* h_last, int B, int H, int P, const float* w_p, const float* b_p, float* y,
+                                float* emb, float* ynorm, float* workspace, hipStream_t stream) {
+  if (!h_last || !w_p || !y || !emb || !ynorm || B <= 0 || H <= 0 || P <= 0) return SV_EARG;
+  int rc = sv_gemm_f32(1, 1, B, P, H, h_last, H, w_p, H, y, P, b_p, nullptr, 0.f, workspace, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rownorm_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, y, B, P, emb, ynorm);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_proj_norm_bwd(const float* demb, const float* emb, const float* ynorm, const float* h_last, int B,
+                                int H, int P, const float* w_p, float* dw_p, float* db_p, float* dh_last,
+                                float* workspace, hipStream_t stream) {
+  if (!demb || !emb || !ynorm || !h_last || !w_p || !dw_p || !db_p || !dh_last || !workspace) return SV_EARG;
+  float* dy = workspace;
+  float* gws = workspace + ((size_t)B * P * sizeof(float) + 255) / 256 * 64;
+  hipLaunchKernelGGL(rownorm_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, demb, emb, ynorm, B, P, dy);
+  SV_LAUNCH_CHECK();
+  // dWp [P,H] = dy^T h_last  (A = dy as [K=B][M=P], B = h_last as [K=B][N=H])
+  int rc = sv_gemm_f32(0, 0, P, H, B, dy, P, h_last, H, dw_p, H, nullptr, nullptr, 0.f, gws, stream);
+  if (rc) return rc;
+  rc = sv_colsum(dy, B, P, db_p, gws, stream);
+  if (rc) return rc;
+  // dh_last [B,H] = dy Wp  (A = dy [B, K=P] k-contig, B = Wp as [K=P][N=H])
+  return sv_gemm_f32(1, 0, B, H, P, dy, P, w_p, H, dh_last, H, nullptr, nullptr, 0.f, gws, stream);
+}
+
+// ---------------------------------------------------------------------------
+// fused clip_grad_norm_(max_norm) + SGD(lr) over one flat parameter group.
+// pass 1: per-block partial sums of squares (fixed grid, fixed order)
+#define CLIP_BLOCKS 512
+__global__ __launch_bounds__(256) void sqsum_partial_kernel(const float* __restrict__ g, long n,
+                                                            float* __restrict__ partial) {
+  __shared__ float red[4];
+  float s = 0.f;
+  const long n4 = n / 4;
+  const f32x4* g4 = reinterpret_cast<const f32x4*>(g);
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const f32x4 v = g4[i];
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  for (long i = n4 * 4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) s += g[i] * g[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// pass 2: every block re-reduces the partials (fixed order, fp64), computes
+// coef = min(1, max_norm / (|g| + 1e-6)) and updates p -= lr * coef * g (optionally g *= coef).
+__global__ __launch_bounds__(256) void clip_sgd_kernel(float* __restrict__ p, float* __restrict__ g, long n,
+                                                       const float* __restrict__ partial, int npart, float max_norm,
+                                                       float lr, int write_grad, float* __restrict__ norm_out) {
+  __shared__ double redd[4];
+  __shared__ float coef_s;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < npart; i += 256) s += (double)partial[i];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) redd[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float total = (float)sqrt(redd[0] + redd[1] + redd[2] + redd[3]);
+    const float c = max_norm / (total + 1e-6f);
+    coef_s = c < 1.0f ? c : 1.0f;
+    if (norm_out && blockIdx.x == 0) norm_out[0] = total;
+  }
+  __syncthreads();
+  const float k = coef_s;
+  const float step = lr * k;
+  const long n4 = n / 4;
+  f32x4* p4 = reinterpret_cast<f32x4*>(p);
+  f32x4* g4 = reinterpret_cast<f32x4*>(g);
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const f32x4 gv = g4[i];
+    p4[i] = p4[i] - step * gv;
+    if (write_grad) g4[i] = gv * k;
+  }
+  for (long i = n4 * 4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float gv = g[i];
+    p[i] -= step * gv;
+    if (write_grad) g[i] = gv * k;
+  }
+}
+
+extern "C" size_t sv_clip_sgd_workspace(void) { return CLIP_BLOCKS * sizeof(float); }
+
+extern "C" int sv_clip_sgd_step(float* params, float* grads, long n, float max_norm, float lr, int write_grad,
+                                float* total_norm_out, float* workspace, hipStream_t stream) {
+  if (!params || !grads || !workspace || n <= 0) return SV_EARG;
+  if (((uintptr_t)params | (uintptr_t)grads) & 15) return SV_EALIGN;
+  const int blocks = (int)std::min<long>(CLIP_BLOCKS, (n / 4 + 255) / 256 + 1);
+  hipLaunchKernelGGL(sqsum_partial_kernel, dim3(blocks), dim3(256), 0, stream, grads, n, workspace);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(clip_sgd_kernel, dim3(blocks), dim3(256), 0, stream, params, grads, n, workspace, blocks, max_norm,
+                     lr, write_grad, total_norm_out);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_abi_version(void) { return SV_ABI_VERSION; }

@@ -1,0 +1,236 @@
+"""Torch-facing wrappers over the C ABI (include/sv_ge2e.h).
+
+PyTorch supplies device memory (caching allocator), the current HIP stream and autograd
+plumbing; every FLOP of the path runs in the HIP kernels of libsv_ge2e.so.
+
+  embedder_forward / embedder_backward   SpeechEmbedder.forward (speech_embedder_net.py:27-33)
+                                         and its backward: 3-layer LSTM + Linear + L2 norm
+  ge2e_forward / ge2e_backward           GE2ELoss.forward (speech_embedder_net.py:43-49)
+  EmbedderFunction, GE2EFunction         autograd.Function glue (loss.backward() works)
+  clip_sgd_step_                         clip_grad_norm_ + SGD.step (train_speech_embedder.py:63-65)
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import call, ptr, require_device, stream_of, lib
+
+
+def _ws(nbytes, device):
+    """Workspace of at least nbytes (fp32 storage, 256-byte aligned by the allocator)."""
+    n = max(1, (int(nbytes) + 3) // 4)
+    return torch.empty(n, dtype=torch.float32, device=device)
+
+
+# ----------------------------------------------------------------------------- LSTM stack
+class EmbedderState:
+    """Activations saved by the forward for the backward (all time-major, fp32)."""
+
+    def __init__(self):
+        self.x_tm = []      # per layer input [T,B,F_l]
+        self.gates = []     # per layer [T,B,4H] activated i,f,g,o
+        self.c_tm = []      # per layer [T,B,H]
+        self.h_tm = []      # per layer [T+1,B,H]
+        self.y = self.emb = self.ynorm = self.h_last = None
+        self.T = self.B = self.H = self.P = 0
+
+
+def embedder_forward(x, layers, w_p, b_p, save=True):
+    """x [B,T,F] float32 (batch_first); layers = [(w_ih, w_hh, b_ih, b_hh)] * L.
+    Returns (emb [B,P], state)."""
+    require_device(x, w_p, b_p, *[t for l in layers for t in l])
+    B, T, F = x.shape
+    H = layers[0][1].shape[1]
+    P = w_p.shape[0]
+    dev = x.device
+    s = stream_of(x)
+    st = EmbedderState()
+    st.T, st.B, st.H, st.P = T, B, H, P
+    x_tm = torch.empty((T, B, F), dtype=torch.float32, device=dev)
+    call("sv_frames_to_time_major", ptr(x), ptr(x_tm), B, T, F, s)
+    inp = x_tm
+    for (w_ih, w_hh, b_ih, b_hh) in layers:
+        Fl = inp.shape[2]
+        gates = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
+        c_tm = torch.empty((T, B, H), dtype=torch.float32, device=dev)
+        h_tm = torch.empty((T + 1, B, H), dtype=torch.float32, device=dev)
+        call("sv_lstm_layer_fwd", ptr(inp), T, B, Fl, H, ptr(w_ih), ptr(w_hh), ptr(b_ih), ptr(b_hh), ptr(gates),
+             ptr(c_tm), ptr(h_tm), s)
+        if save:
+            st.x_tm.append(inp)
+            st.gates.append(gates)
+            st.c_tm.append(c_tm)
+            st.h_tm.append(h_tm)
+        inp = h_tm[1:]
+    h_last = inp[T - 1]
+    y = torch.empty((B, P), dtype=torch.float32, device=dev)
+    emb = torch.empty((B, P), dtype=torch.float32, device=dev)
+    ynorm = torch.empty((B,), dtype=torch.float32, device=dev)
+    ws = _ws(lib().sv_proj_norm_workspace(B, H, P), dev)
+    call("sv_proj_norm_fwd", ptr(h_last), B, H, P, ptr(w_p), ptr(b_p), ptr(y), ptr(emb), ptr(ynorm), ptr(ws), s)
+    st.y, st.emb, st.ynorm, st.h_last = y, emb, ynorm, h_last
+    return emb, st
+
+
+def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False):
+    """Backward of embedder_forward.  ``grads`` (optional) is a list of preallocated
+    output tensors in parameter order [w_ih, w_hh, b_ih, b_hh]*L + [w_p, b_p]; returns it
+    (and dx [B,T,F] if need_dx)."""
+    demb = demb.contiguous()
+    require_device(demb)
+    T, B, H, P = st.T, st.B, st.H, st.P
+    dev = demb.device
+    s = stream_of(demb)
+    L = len(layers)
+    if grads is None:
+        grads = []
+        for (w_ih, w_hh, b_ih, b_hh) in layers:
+            grads += [torch.empty_like(w_ih), torch.empty_like(w_hh), torch.empty_like(b_ih), torch.empty_like(b_hh)]
+        grads += [torch.empty_like(w_p), torch.empty((P,), dtype=torch.float32, device=dev)]
+    dh_last = torch.empty((B, H), dtype=torch.float32, device=dev)
+    ws = _ws(lib().sv_proj_norm_workspace(B, H, P), dev)
+    call("sv_proj_norm_bwd", ptr(demb), ptr(st.emb), ptr(st.ynorm), ptr(st.h_last), B, H, P, ptr(w_p),
+         ptr(grads[4 * L]), ptr(grads[4 * L + 1]), ptr(dh_last), ptr(ws), s)
+    Fmax = max(st.x_tm[l].shape[2] for l in range(L))
+    ws = _ws(lib().sv_lstm_layer_bwd_workspace(T, B, Fmax, H), dev)
+    dgates = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
+    dh_up, full = dh_last, 0
+    dx_out = None
+    for l in range(L - 1, -1, -1):
+        w_ih, w_hh, _, _ = layers[l]
+        Fl = st.x_tm[l].shape[2]
+        want_dx = l > 0 or need_dx
+        dx = torch.empty((T, B, Fl), dtype=torch.float32, device=dev) if want_dx else None
+        call("sv_lstm_layer_bwd", T, B, Fl, H, ptr(st.x_tm[l]), ptr(w_ih), ptr(w_hh), ptr(st.gates[l]),
+             ptr(st.c_tm[l]), ptr(st.h_tm[l]), ptr(dh_up), full, ptr(dgates), ptr(dx), ptr(grads[4 * l]),
+             ptr(grads[4 * l + 1]), ptr(grads[4 * l + 2]), ptr(grads[4 * l + 3]), ptr(ws), s)
+        dh_up, full = dx, 1
+        if l == 0:
+            dx_out = dx
+    if need_dx:
+        dxb = torch.empty((B, T, dx_out.shape[2]), dtype=torch.float32, device=dev)
+        call("sv_frames_to_time_major", ptr(dx_out), ptr(dxb), T, B, dx_out.shape[2], s)  # [T,B,F] -> [B,T,F]
+        return grads, dxb
+    return grads
+
+
+class EmbedderFunction(torch.autograd.Function):
+    """emb = SpeechEmbedder.forward(x) with params (w_ih, w_hh, b_ih, b_hh)*L, w_p, b_p."""
+
+    @staticmethod
+    def forward(ctx, x, num_layers, *params):
+        L = num_layers
+        layers = [tuple(params[4 * l:4 * l + 4]) for l in range(L)]
+        w_p, b_p = params[4 * L], params[4 * L + 1]
+        emb, st = embedder_forward(x.contiguous(), layers, w_p, b_p, save=True)
+        ctx.st = st
+        ctx.L = L
+        ctx.save_for_backward(*params)
+        return emb
+
+    @staticmethod
+    def backward(ctx, demb):
+        params = ctx.saved_tensors
+        L = ctx.L
+        layers = [tuple(params[4 * l:4 * l + 4]) for l in range(L)]
+        need_dx = ctx.needs_input_grad[0]
+        out = embedder_backward(ctx.st, demb, layers, params[4 * L], need_dx=need_dx)
+        ctx.st = None
+        if need_dx:
+            grads, dx = out
+        else:
+            grads, dx = out, None
+        return (dx, None, *grads)
+
+
+# ----------------------------------------------------------------------------- GE2E
+class Ge2eState:
+    pass
+
+
+def _pad_d(E):
+    D = E.shape[-1]
+    if D % 4 == 0:
+        return E.contiguous(), D
+    Dp = (D + 3) // 4 * 4
+    Ep = torch.zeros(E.shape[:-1] + (Dp,), dtype=E.dtype, device=E.device)
+    Ep[..., :D] = E
+    return Ep, D
+
+
+def ge2e_forward(E, w, b):
+    """GE2E loss of E [N,M,D] with device scalars w, b.  Returns (loss 0-dim, per [N,M], state)."""
+    require_device(E, w, b)
+    if E.dim() != 3 or E.shape[1] < 2:
+        raise ValueError("GE2E expects embeddings [N, M, D] with M >= 2 (leave-one-out centroids)")
+    Ep, D0 = _pad_d(E)
+    N, M, D = Ep.shape
+    dev = E.device
+    s = stream_of(E)
+    st = Ge2eState()
+    st.ws = _ws(lib().sv_ge2e_workspace_size(N, M, D, N), dev)
+    st.ssum = torch.empty((N, D), dtype=torch.float32, device=dev)
+    st.N, st.M, st.D, st.D0 = N, M, D, D0
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    per = torch.empty((N, M), dtype=torch.float32, device=dev)
+    call("sv_ge2e_fwd", ptr(Ep), N, M, D, ptr(w.contiguous()), ptr(b.contiguous()), ptr(loss), ptr(per), ptr(st.ws),
+         ptr(st.ssum), s)
+    return loss, per, st
+
+
+def ge2e_backward(st, w, b, gloss=None):
+    """Returns (dE [N,M,D0], dw 0-dim, db 0-dim)."""
+    N, M, D = st.N, st.M, st.D
+    dev = st.ws.device
+    s = stream_of(st.ws)
+    Np = (N + 3) // 4 * 4
+    dE = torch.empty((N, M, D), dtype=torch.float32, device=dev)
+    dwdb = torch.empty((2,), dtype=torch.float32, device=dev)
+    dchat = torch.empty((Np, D), dtype=torch.float32, device=dev)
+    beta = torch.empty((N,), dtype=torch.float32, device=dev)
+    g = None if gloss is None else gloss.contiguous()
+    call("sv_ge2e_bwd", N, M, D, ptr(w.contiguous()), ptr(b.contiguous()), ptr(g), ptr(dE), ptr(dwdb), ptr(dchat),
+         ptr(beta), ptr(st.ws), s)
+    if st.D0 != D:
+        dE = dE[..., :st.D0].contiguous()
+    return dE, dwdb[0], dwdb[1]
+
+
+class GE2EFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, E, w, b):
+        loss, per, st = ge2e_forward(E, w, b)
+        ctx.st = st
+        ctx.save_for_backward(w, b)
+        ctx.mark_non_differentiable(per)
+        return loss, per
+
+    @staticmethod
+    def backward(ctx, gloss, _gper):
+        w, b = ctx.saved_tensors
+        dE, dw, db = ge2e_backward(ctx.st, w, b, gloss.reshape(()).to(torch.float32))
+        ctx.st = None
+        return dE, dw.reshape(w.shape), db.reshape(b.shape)
+
+
+# ----------------------------------------------------------------------------- clip + SGD
+def clip_sgd_step_(flat_params, flat_grads, max_norm, lr, write_grad=False, norm_out=None):
+    """In place: flat_params -= lr * min(1, max_norm/(|g|+1e-6)) * flat_grads."""
+    require_device(flat_params, flat_grads)
+    ws = _ws(lib().sv_clip_sgd_workspace(), flat_params.device)
+    call("sv_clip_sgd_step", ptr(flat_params), ptr(flat_grads), flat_params.numel(), float(max_norm), float(lr),
+         int(write_grad), ptr(norm_out), ptr(ws), stream_of(flat_params))
+
+
+def gemm_f32(A, B, a_kcontig=True, b_kcontig=True, bias=None):
+    """C = op(A) op(B) through sv_gemm_f32 (test hook).  With a_kcontig A is [M,K] else [K,M];
+    with b_kcontig B is [N,K] else [K,N]."""
+    require_device(A, B, bias)
+    M = A.shape[0] if a_kcontig else A.shape[1]
+    K = A.shape[1] if a_kcontig else A.shape[0]
+    N = B.shape[0] if b_kcontig else B.shape[1]
+    C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    ws = _ws(lib().sv_gemm_f32_workspace(M, N, K), A.device)
+    call("sv_gemm_f32", int(a_kcontig), int(b_kcontig), M, N, K, ptr(A), A.shape[1], ptr(B), B.shape[1], ptr(C), N,
+         ptr(bias), None, 0.0, ptr(ws), stream_of(A))
+    return C

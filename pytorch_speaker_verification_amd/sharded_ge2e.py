@@ -1,0 +1,96 @@
+"""Speaker-sharded GE2E across ranks ("exact-parity partitioning").
+
+Rank r owns speakers [r*N_local, (r+1)*N_local) with all their M utterances, so the
+leave-one-out centroids stay local.  Per step:
+
+  fwd  per-speaker sums (local)  --all_gather-->  Ssum [N, D]  --> local rows of S [N_local*M, N],
+       local loss (the global loss is the SUM over ranks; all_reduce only for reporting)
+  bwd  local rows give this shard's dC^ [Np, D] and beta [N] contributions --all_reduce(SUM)-->
+       finalize the local dE; (dw, db) stay per-rank partials and are summed together with
+       the network gradients by the caller.
+
+With world size 1 this is exactly the single-GPU GE2ELoss.  The per-shard arithmetic is
+a pluggable ``kernels`` object: the HIP kernels (``HipShardKernels``) in production; the
+CPU tests plug in a numpy restatement so the exchange protocol runs under gloo.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ._lib import call, lib, ptr, stream_of
+
+
+class HipShardKernels:
+    """Per-shard GE2E steps on the C ABI (sv_ge2e_speaker_sums / fwd_rows / bwd_rows / finalize)."""
+
+    def speaker_sums(self, E):
+        Nl, M, D = E.shape
+        out = torch.empty((Nl, D), dtype=torch.float32, device=E.device)
+        call("sv_ge2e_speaker_sums", ptr(E), Nl, M, D, ptr(out), stream_of(E))
+        return out
+
+    def fwd_rows(self, E, s0, N, ssum_all, w, b):
+        Nl, M, D = E.shape
+        ws = torch.empty(lib().sv_ge2e_workspace_size(Nl, M, D, N) // 4 + 1, dtype=torch.float32, device=E.device)
+        per = torch.empty((Nl, M), dtype=torch.float32, device=E.device)
+        loss = torch.empty((), dtype=torch.float32, device=E.device)
+        call("sv_ge2e_fwd_rows", ptr(E), Nl, M, D, s0, N, ptr(ssum_all), ptr(w), ptr(b), ptr(per), ptr(loss), ptr(ws),
+             stream_of(E))
+        return loss, per, {"ws": ws, "shape": (Nl, M, D), "s0": s0, "N": N}
+
+    def bwd_rows(self, st, w, b, gloss):
+        Nl, M, D = st["shape"]
+        N = st["N"]
+        Np = (N + 3) // 4 * 4
+        dev = st["ws"].device
+        # one buffer so the caller can all_reduce dC^ and beta together
+        red = torch.empty(Np * D + N, dtype=torch.float32, device=dev)
+        dwdb = torch.empty(2, dtype=torch.float32, device=dev)
+        call("sv_ge2e_bwd_rows", Nl, M, D, st["s0"], N, ptr(w), ptr(b), ptr(gloss), ptr(red), ptr(red[Np * D:]),
+             ptr(dwdb), ptr(st["ws"]), stream_of(red))
+        return red, dwdb
+
+    def finalize(self, st, red):
+        Nl, M, D = st["shape"]
+        N = st["N"]
+        Np = (N + 3) // 4 * 4
+        dE = torch.empty((Nl, M, D), dtype=torch.float32, device=red.device)
+        call("sv_ge2e_bwd_finalize", Nl, M, D, st["s0"], N, ptr(red), ptr(red[Np * D:]), ptr(dE), ptr(st["ws"]),
+             stream_of(red))
+        return dE
+
+
+class ShardedGE2E:
+    def __init__(self, kernels=None, group=None):
+        self.k = kernels if kernels is not None else HipShardKernels()
+        self.group = group
+        if dist.is_available() and dist.is_initialized():
+            self.rank = dist.get_rank(group)
+            self.world = dist.get_world_size(group)
+        else:
+            self.rank, self.world = 0, 1
+
+    def forward(self, E_local, w, b, reduce_loss=True):
+        """Returns (loss, per_local, state); loss is the global sum when reduce_loss."""
+        Nl, M, D = E_local.shape
+        N = Nl * self.world
+        s0 = Nl * self.rank
+        ssum_local = self.k.speaker_sums(E_local)
+        if self.world > 1:
+            ssum_all = ssum_local.new_empty((N, D))
+            dist.all_gather_into_tensor(ssum_all, ssum_local, group=self.group)
+        else:
+            ssum_all = ssum_local
+        loss, per, st = self.k.fwd_rows(E_local, s0, N, ssum_all, w, b)
+        if self.world > 1 and reduce_loss:
+            loss = loss.clone()
+            dist.all_reduce(loss, group=self.group)
+        return loss, per, st
+
+    def backward(self, st, w, b, gloss=None):
+        """Returns (dE_local, dwdb_partial[2]).  dwdb must still be summed over ranks."""
+        red, dwdb = self.k.bwd_rows(st, w, b, gloss)
+        if self.world > 1:
+            dist.all_reduce(red, group=self.group)
+        return self.k.finalize(st, red), dwdb

@@ -1,0 +1,95 @@
+"""Fused GE2E training step (the body of train_speech_embedder.py:44-65) on the HIP kernels.
+
+One ``GE2ETrainer.step(x)`` = SpeechEmbedder forward -> GE2E loss -> closed-form GE2E
+backward -> LSTM/projection backward -> (data-parallel: SUM all-reduce of gradients over
+RCCL) -> clip_grad_norm_(net, 3.0) + clip_grad_norm_([w, b], 1.0) + SGD(lr), with no
+autograd graph and no host synchronisation.  Numerically the same step as the reference
+loop body (the reference's random perm/unperm of rows is value-neutral: rows are
+independent, SURVEY §8 a-J).
+
+Parameters are flattened into one device buffer (the module's nn.Parameters become views
+of it, so state_dict(), optimizers and checkpoints keep working) so that the gradient
+all-reduce and the clip+SGD update each touch one contiguous buffer:
+
+    flat_p = [ net params (n, padded to n_pad = 4k) | w | b | pad ]   flat_g likewise.
+
+Data parallel: one process per GPU; rank r holds speakers [r*N, (r+1)*N) of a global
+batch of world*N speakers (ShardedGE2E), so the step is the single-GPU step of that
+global batch.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .ops import clip_sgd_step_, embedder_backward, embedder_forward
+from .sharded_ge2e import ShardedGE2E
+
+
+class GE2ETrainer:
+    def __init__(self, embedder, ge2e_loss, lr=0.01, clip_net=3.0, clip_wb=1.0, group=None, write_grads=True):
+        self.net = embedder
+        self.loss_mod = ge2e_loss
+        self.lr, self.clip_net, self.clip_wb = float(lr), float(clip_net), float(clip_wb)
+        self.group = group
+        self.write_grads = write_grads
+        self.ge2e = ShardedGE2E(group=group)
+        self._flatten()
+
+    # -------------------------------------------------------------------------------------
+    def _flatten(self):
+        params = self.net.flat_params()
+        dev = params[0].device
+        n = sum(p.numel() for p in params)
+        n_pad = (n + 3) // 4 * 4
+        self.n, self.n_pad = n, n_pad
+        flat_p = torch.zeros(n_pad + 4, dtype=torch.float32, device=dev)
+        flat_g = torch.zeros(n_pad + 4, dtype=torch.float32, device=dev)
+        off = 0
+        self.grad_views = []
+        with torch.no_grad():
+            for p in params:
+                k = p.numel()
+                flat_p[off:off + k].copy_(p.reshape(-1))
+                p.data = flat_p[off:off + k].view_as(p)
+                g = flat_g[off:off + k].view_as(p)
+                self.grad_views.append(g)
+                if self.write_grads:
+                    p.grad = g
+                off += k
+            w, b = self.loss_mod.w, self.loss_mod.b
+            flat_p[n_pad] = w.detach()
+            flat_p[n_pad + 1] = b.detach()
+            w.data = flat_p[n_pad:n_pad + 1].view(())
+            b.data = flat_p[n_pad + 1:n_pad + 2].view(())
+            if self.write_grads:
+                w.grad = flat_g[n_pad:n_pad + 1].view(())
+                b.grad = flat_g[n_pad + 1:n_pad + 2].view(())
+        self.flat_p, self.flat_g = flat_p, flat_g
+        self._ptrs = [p.data_ptr() for p in params]
+
+    def _check_layout(self):
+        if [p.data_ptr() for p in self.net.flat_params()] != self._ptrs:
+            self._flatten()  # the module was moved / reloaded since
+
+    # -------------------------------------------------------------------------------------
+    def step(self, x, N, M):
+        """x: [N*M, T, nmels] float32 on this rank's GPU (this rank's N speakers x M
+        utterances, speaker-major).  Returns the (global) loss as a 0-dim device tensor."""
+        self._check_layout()
+        net = self.net
+        layers = net.LSTM_stack.layer_params()
+        w_p, b_p = net.projection.weight, net.projection.bias
+        w, b = self.loss_mod.w, self.loss_mod.b
+        emb, st = embedder_forward(x.float().contiguous(), layers, w_p, b_p)
+        E = emb.view(N, M, emb.shape[1])
+        loss, _, gst = self.ge2e.forward(E, w, b)
+        dE, dwdb = self.ge2e.backward(gst, w, b)
+        self.flat_g[self.n_pad:self.n_pad + 2].copy_(dwdb)
+        embedder_backward(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views)
+        if self.ge2e.world > 1:
+            dist.all_reduce(self.flat_g, group=self.group)  # SUM, never mean (SURVEY §7 hard part 4)
+        n = self.n_pad
+        clip_sgd_step_(self.flat_p[:n], self.flat_g[:n], self.clip_net, self.lr, self.write_grads)
+        clip_sgd_step_(self.flat_p[n:n + 4], self.flat_g[n:n + 4], self.clip_wb, self.lr, self.write_grads)
+        return loss

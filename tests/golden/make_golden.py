@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE itself.
+
+Runs only in the build container, where the read-only reference is mounted at
+/root/reference (it never travels to the GPU box).  The reference is imported
+in-process, read-only, with the two shims SURVEY.md §8c lists:
+
+  1. ``yaml.load_all`` gets an explicit SafeLoader (``hparam.py:9`` omits it and
+     PyYAML >= 6 raises);
+  2. ``librosa`` is stubbed (only used by preprocessing, ``utils.py:8,138-164``).
+
+What is recorded (inputs + expected outputs; no reference source is copied):
+  kat0.npz            -- the reference's own ``utils.py:166-173`` example (KAT-0).
+  ge2e_*.npz          -- GE2E loss / per-embedding loss / dE / dw / db for seeded E.
+  cossim_ext.npz      -- get_cossim with external (enrollment) centroids, the
+                         ``train_speech_embedder.py:127-129`` call shape.
+  net_small.npz       -- full training step (fwd, GE2E, bwd, clip 3.0/1.0, SGD) of the
+                         reference SpeechEmbedder at small dims, 3 steps.
+  net_full_c1.npz     -- one step at the full dims (40->768x3->256), N=4 x M=5, T=160.
+  hparam.json         -- the parsed config/config.yaml as the reference sees it.
+
+Weights/inputs come from tests/golden/recipe.py (numpy PCG64), so fixtures hold the
+recipe parameters, not the weights.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+sys.path.insert(0, HERE)
+import recipe  # noqa: E402
+
+
+def import_reference():
+    import yaml
+    orig = yaml.load_all
+    yaml.load_all = lambda s, Loader=yaml.SafeLoader: orig(s, Loader=Loader)
+    sys.modules.setdefault("librosa", types.ModuleType("librosa"))
+    sys.dont_write_bytecode = True
+    cwd = os.getcwd()
+    os.chdir(REF)
+    sys.path.insert(0, REF)
+    try:
+        import hparam as ref_hparam  # noqa: F401
+        import utils as ref_utils
+        import speech_embedder_net as ref_net
+    finally:
+        os.chdir(cwd)
+    return ref_hparam, ref_utils, ref_net
+
+
+def ge2e_case(ref_utils, ref_net, E_np, w, b):
+    import torch
+    E = torch.tensor(E_np, requires_grad=True)
+    loss_mod = ref_net.GE2ELoss("cpu")
+    with torch.no_grad():
+        loss_mod.w.fill_(w)
+        loss_mod.b.fill_(b)
+    loss = loss_mod(E)
+    loss.backward()
+    with torch.no_grad():
+        C = ref_utils.get_centroids(E)
+        cos = ref_utils.get_cossim(E, C)
+        _, per = ref_utils.calc_loss(loss_mod.w * cos + loss_mod.b)
+    return dict(loss=np.float64(loss.item()), per=per.numpy(), cossim=cos.numpy(),
+                centroids=C.numpy(), dE=E.grad.numpy(),
+                dw=np.float64(loss_mod.w.grad.item()), db=np.float64(loss_mod.b.grad.item()))
+
+
+def train_steps(ref_net, ref_hparam, dims, wseed, wscale, xseed, N, M, T, steps, lr=0.01):
+    """Run the reference train() step body (train_speech_embedder.py:44-65) `steps` times
+    on fixed recipe input (the random perm/unperm is a no-op on values: rows are
+    independent, SURVEY §8 a-J)."""
+    import torch
+    hp = ref_hparam.hparam
+    old = (hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj)
+    hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj = dims
+    try:
+        net = ref_net.SpeechEmbedder()
+    finally:
+        hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj = old
+    sd = recipe.make_weights(wseed, *dims, scale=wscale)
+    net.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+    ge2e = ref_net.GE2ELoss("cpu")
+    opt = torch.optim.SGD([{"params": net.parameters()}, {"params": ge2e.parameters()}], lr=lr)
+    x = torch.tensor(recipe.make_frames(xseed, N * M, T, dims[0]))
+    rec = {"losses": [], "per": [], "emb": []}
+    for s in range(steps):
+        opt.zero_grad()
+        emb = net(x)
+        emb = emb.reshape(N, M, emb.size(1))
+        loss = ge2e(emb)
+        loss.backward()
+        if s == 0:
+            rec["grads"] = {k: p.grad.detach().numpy().copy() for k, p in net.named_parameters()}
+            rec["dw0"] = ge2e.w.grad.item()
+            rec["db0"] = ge2e.b.grad.item()
+        torch.nn.utils.clip_grad_norm_(net.parameters(), 3.0)
+        torch.nn.utils.clip_grad_norm_(ge2e.parameters(), 1.0)
+        opt.step()
+        rec["losses"].append(loss.item())
+        rec["emb"].append(emb.detach().numpy().copy())
+        if s == 0:
+            rec["params1"] = {k: p.detach().numpy().copy() for k, p in net.named_parameters()}
+            rec["wb1"] = (ge2e.w.item(), ge2e.b.item())
+    rec["params_final"] = {k: p.detach().numpy().copy() for k, p in net.named_parameters()}
+    rec["wb_final"] = (ge2e.w.item(), ge2e.b.item())
+    return rec
+
+
+def main():
+    if not os.path.isdir(REF):
+        print("reference not present; nothing to do")
+        return
+    import torch
+    torch.set_num_threads(os.cpu_count())
+    ref_hparam, ref_utils, ref_net = import_reference()
+
+    # ---- KAT-0: utils.py:166-173 -------------------------------------------------
+    E0 = np.array([[0, 1, 0], [0, 0, 1], [0, 1, 0], [0, 1, 0], [1, 0, 0], [1, 0, 0]],
+                  dtype=np.float32).reshape(3, 2, 3)
+    r = ge2e_case(ref_utils, ref_net, E0, 1.0, 0.0)
+    np.savez(os.path.join(HERE, "kat0.npz"), E=E0, w=1.0, b=0.0, **r)
+    print("kat0 loss", r["loss"])
+
+    # ---- GE2E vectors -----------------------------------------------------------
+    cases = [("n4m5", 5, 4, 5, 10.0, -5.0, True),
+             ("n4m5_flat", 6, 4, 5, 10.0, -5.0, False),
+             ("n8m10_wb", 7, 8, 10, 3.7, -1.2, True),
+             ("n64m10", 8, 64, 10, 10.0, -5.0, True),
+             ("n256m10", 9, 256, 10, 10.0, -5.0, True),
+             ("n3m2", 10, 3, 2, 10.0, -5.0, True)]
+    for tag, seed, n, m, w, b, clustered in cases:
+        E = recipe.make_embeddings(seed, n, m, 256, clustered)
+        r = ge2e_case(ref_utils, ref_net, E, w, b)
+        keep = dict(seed=seed, n=n, m=m, d=256, w=w, b=b, clustered=clustered,
+                    loss=r["loss"], per=r["per"], dw=r["dw"], db=r["db"])
+        if n * m <= 640:
+            keep.update(dE=r["dE"], cossim=r["cossim"], centroids=r["centroids"])
+        else:
+            keep.update(dE_norm=np.linalg.norm(r["dE"].astype(np.float64)),
+                        dE_head=r["dE"][:4], cossim_head=r["cossim"][:4],
+                        cossim_diag=np.stack([r["cossim"][j, :, j] for j in range(n)]))
+        if tag == "n4m5":  # the naive *_prior loop twins (utils.py:16-25,60-70,117-124)
+            import torch
+            Et = torch.tensor(E)
+            Cp = ref_utils.get_centroids_prior(Et)
+            cp = ref_utils.get_cossim_prior(Et, Cp)
+            lp, pp = ref_utils.calc_loss_prior(w * cp + b)
+            keep.update(prior_cossim=cp.numpy(), prior_loss=lp.item(), prior_per=pp.numpy())
+        np.savez_compressed(os.path.join(HERE, f"ge2e_{tag}.npz"), **keep)
+        print(tag, "loss", r["loss"], "dw", r["dw"], "db", r["db"])
+
+    # ---- get_cossim with external centroids (test() call shape) ----------------
+    import torch
+    Ev = recipe.make_embeddings(31, 4, 3, 256, True)
+    Ee = recipe.make_embeddings(32, 4, 3, 256, True)
+    Cen = ref_utils.get_centroids(torch.tensor(Ee))
+    cs = ref_utils.get_cossim(torch.tensor(Ev), Cen)
+    np.savez_compressed(os.path.join(HERE, "cossim_ext.npz"), verif=Ev, enroll=Ee,
+                        enroll_centroids=Cen.numpy(), cossim=cs.numpy())
+
+    # ---- full training step, small dims ----------------------------------------
+    dims = (40, 64, 3, 32)
+    rec = train_steps(ref_net, ref_hparam, dims, wseed=11, wscale=3.0, xseed=12,
+                      N=4, M=5, T=24, steps=3)
+    out = dict(dims=np.array(dims), wseed=11, wscale=3.0, xseed=12, N=4, M=5, T=24, steps=3,
+               losses=np.array(rec["losses"]), emb0=rec["emb"][0], emb_last=rec["emb"][-1],
+               dw0=rec["dw0"], db0=rec["db0"], wb1=np.array(rec["wb1"]),
+               wb_final=np.array(rec["wb_final"]))
+    for k, v in rec["grads"].items():
+        out["grad." + k] = v
+    for k, v in rec["params1"].items():
+        out["p1." + k] = v
+    for k, v in rec["params_final"].items():
+        out["pf." + k] = v
+    np.savez_compressed(os.path.join(HERE, "net_small.npz"), **out)
+    print("net_small losses", rec["losses"])
+
+    # ---- one step at the full dims (c1: N=4 x M=5, T=160) ----------------------
+    dims = (40, 768, 3, 256)
+    rec = train_steps(ref_net, ref_hparam, dims, wseed=21, wscale=2.0, xseed=22,
+                      N=4, M=5, T=160, steps=1)
+    out = dict(dims=np.array(dims), wseed=21, wscale=2.0, xseed=22, N=4, M=5, T=160,
+               loss=rec["losses"][0], emb=rec["emb"][0], dw0=rec["dw0"], db0=rec["db0"],
+               wb1=np.array(rec["wb1"]))
+    for k, g in rec["grads"].items():
+        out["gnorm." + k] = np.linalg.norm(g.astype(np.float64))
+        out["ghead." + k] = g.reshape(g.shape[0], -1)[:8, :8] if g.ndim == 2 else g[:64]
+    for k, p in rec["params1"].items():
+        out["p1head." + k] = p.reshape(p.shape[0], -1)[:8, :8] if p.ndim == 2 else p[:64]
+    np.savez_compressed(os.path.join(HERE, "net_full_c1.npz"), **out)
+    print("net_full_c1 loss", rec["losses"][0])
+
+    # ---- init RNG parity: reference SpeechEmbedder() under torch.manual_seed ------
+    hp = ref_hparam.hparam
+    old = (hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj)
+    hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj = (40, 64, 3, 32)
+    try:
+        torch.manual_seed(1234)
+        net = ref_net.SpeechEmbedder()
+    finally:
+        hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj = old
+    np.savez_compressed(os.path.join(HERE, "init_seed1234.npz"),
+                        **{k: v.detach().numpy() for k, v in net.state_dict().items()})
+
+    # ---- the parsed config -----------------------------------------------------
+    hp = ref_hparam.hparam
+    with open(os.path.join(HERE, "hparam.json"), "w") as f:
+        json.dump(json.loads(json.dumps(hp)), f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,110 @@
+"""GPU parity of the individual HIP kernels (through the C ABI) against the oracle and
+the reference's golden vectors.  Tolerances: fp32 path, relative 1e-4 on the loss
+(north_star), element-wise tolerances stated per test."""
+import numpy as np
+import pytest
+import torch
+
+import recipe
+from conftest import golden
+from oracle import ge2e_np
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("M,N,K", [(100, 72, 40), (256, 768, 640), (3072, 40, 2048), (640, 3072, 768), (8, 4, 4)])
+def test_gemm_f32_layouts(ak, bk, M, N, K):
+    from pytorch_speaker_verification_amd.ops import gemm_f32
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K + ak * 2 + bk)
+    A = torch.randn((M, K) if ak else (K, M), generator=g)
+    B = torch.randn((N, K) if bk else (K, N), generator=g)
+    ref = (A.double() if ak else A.double().T) @ (B.double().T if bk else B.double())
+    C = gemm_f32(A.to(DEV), B.to(DEV), bool(ak), bool(bk)).cpu().double()
+    err = (C - ref).abs().max().item()
+    assert err <= 2e-6 * K ** 0.5 * ref.abs().max().item() + 1e-5, err
+
+
+def _ge2e_gpu(E, w, b):
+    from pytorch_speaker_verification_amd import ops
+    Et = torch.tensor(E, device=DEV)
+    wt = torch.tensor(w, dtype=torch.float32, device=DEV)
+    bt = torch.tensor(b, dtype=torch.float32, device=DEV)
+    loss, per, st = ops.ge2e_forward(Et, wt, bt)
+    dE, dw, db = ops.ge2e_backward(st, wt, bt)
+    return float(loss), per.cpu().numpy(), dE.cpu().numpy(), float(dw), float(db)
+
+
+def test_ge2e_kat0():
+    k = golden("kat0.npz")
+    loss, per, dE, dw, db = _ge2e_gpu(k["E"], 1.0, 0.0)
+    assert abs(loss - float(k["loss"])) <= 1e-4 * abs(float(k["loss"]))
+    np.testing.assert_allclose(per, k["per"], atol=1e-5)
+    np.testing.assert_allclose(dE, k["dE"], atol=1e-5)
+    assert abs(dw - float(k["dw"])) < 1e-5 and abs(db - float(k["db"])) < 1e-5
+
+
+@pytest.mark.parametrize("tag", ["n4m5", "n4m5_flat", "n8m10_wb", "n64m10", "n256m10", "n3m2"])
+def test_ge2e_golden(tag):
+    g = golden(f"ge2e_{tag}.npz")
+    E = recipe.make_embeddings(int(g["seed"]), int(g["n"]), int(g["m"]), int(g["d"]), bool(g["clustered"]))
+    w, b = float(g["w"]), float(g["b"])
+    loss, per, dE, dw, db = _ge2e_gpu(E, w, b)
+    ref_loss = float(g["loss"])
+    assert abs(loss - ref_loss) <= 1e-4 * abs(ref_loss), (loss, ref_loss)       # fp32 loss within 1e-4 (rel)
+    np.testing.assert_allclose(per, g["per"], atol=1e-4)
+    o_dE, o_dw, o_db = ge2e_np.ge2e_backward(E, w, b)
+    scale = np.abs(o_dE).max()
+    np.testing.assert_allclose(dE, o_dE, atol=1e-4 * scale)
+    assert abs(dw - o_dw) <= 1e-4 * max(1.0, abs(o_dw))
+    assert abs(db - o_db) <= 1e-5 * E.shape[0] * E.shape[1]
+
+
+def test_ge2e_diagonal_index_set_exact():
+    """The leave-one-out (diagonal) entries are exactly the k == j entries: perturbing
+    one speaker's utterance changes only that speaker's diagonal centroid term."""
+    from pytorch_speaker_verification_amd.utils import get_centroids, get_cossim
+    E = recipe.make_embeddings(3, 6, 4, 256, True)
+    Et = torch.tensor(E, device=DEV)
+    C = get_centroids(Et)
+    cos = get_cossim(Et, C).cpu().numpy()
+    ref = ge2e_np.get_cossim(E, ge2e_np.get_centroids(E))
+    np.testing.assert_allclose(cos, ref, atol=2e-6)
+    # the diagonal differs from the plain centroid cosine everywhere (leave-one-out), off-diag equal
+    plain = np.einsum("jid,kd->jik", E / np.linalg.norm(E, axis=-1, keepdims=True),
+                      ge2e_np._unit(ge2e_np.get_centroids(E))[0]) + 1e-6
+    diff = np.abs(cos - plain) > 1e-4
+    assert np.array_equal(diff, np.broadcast_to(np.eye(6, dtype=bool)[:, None, :], diff.shape))
+
+
+def test_get_cossim_external_centroids_and_calc_loss():
+    from pytorch_speaker_verification_amd.utils import calc_loss, get_centroids, get_cossim
+    g = golden("cossim_ext.npz")
+    C = get_centroids(torch.tensor(g["enroll"], device=DEV))
+    np.testing.assert_allclose(C.cpu().numpy(), g["enroll_centroids"], atol=1e-6)
+    cos = get_cossim(torch.tensor(g["verif"], device=DEV), C)
+    np.testing.assert_allclose(cos.cpu().numpy(), g["cossim"], atol=2e-6)
+    k = golden("kat0.npz")
+    S = torch.tensor(k["cossim"], device=DEV)
+    loss, per = calc_loss(S)
+    assert abs(float(loss) - float(k["loss"])) < 1e-4 * float(k["loss"])
+    np.testing.assert_allclose(per.cpu().numpy(), k["per"], atol=1e-5)
+
+
+def test_clip_sgd_matches_torch():
+    from pytorch_speaker_verification_amd.ops import clip_sgd_step_
+    g = torch.Generator().manual_seed(5)
+    for n, max_norm in [(12134656, 3.0), (1003, 1.0), (2, 1.0), (4096, 1e6)]:
+        p = torch.randn(n, generator=g)
+        gr = torch.randn(n, generator=g) * 0.1
+        pr, grr = p.clone().double(), gr.clone().double()
+        norm = grr.norm()
+        coef = min(1.0, max_norm / (float(norm) + 1e-6))
+        pr -= 0.01 * coef * grr
+        pd, gd = p.to(DEV), gr.to(DEV)
+        out = torch.zeros(1, device=DEV)
+        clip_sgd_step_(pd, gd, max_norm, 0.01, write_grad=True, norm_out=out)
+        np.testing.assert_allclose(pd.cpu().double().numpy(), pr.numpy(), atol=1e-6)
+        np.testing.assert_allclose(gd.cpu().double().numpy(), (grr * coef).numpy(), atol=1e-6)
+        assert abs(float(out) - float(norm)) <= 1e-5 * float(norm)

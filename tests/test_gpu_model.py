@@ -1,0 +1,146 @@
+"""GPU parity of the full path (SpeechEmbedder + GE2ELoss + backward + clip/SGD) against
+the reference's golden vectors (small dims and the full 40->768x3->256 net at c1) and,
+at the full c2 size (N=64 x M=10, T=160), against stock PyTorch fp32 on the same GPU
+(nn.LSTM via MIOpen; oracle/torch_port.py) plus size-independent properties."""
+import numpy as np
+import pytest
+import torch
+
+import recipe
+from conftest import golden, model_dims
+from oracle import torch_port
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _build(dims, sd_np):
+    from pytorch_speaker_verification_amd.speech_embedder_net import GE2ELoss, SpeechEmbedder
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd_np[k]))
+    return net.to(DEV), GE2ELoss(DEV)
+
+
+def _rel(a, b):
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def test_small_net_autograd_path_matches_reference():
+    """The drop-in path: module forward, loss.backward(), torch clip + SGD (user code)."""
+    s = golden("net_small.npz")
+    dims = tuple(int(v) for v in s["dims"])
+    net, ge2e = _build(dims, recipe.make_weights(int(s["wseed"]), *dims, scale=float(s["wscale"])))
+    N, M, T = int(s["N"]), int(s["M"]), int(s["T"])
+    x = torch.tensor(recipe.make_frames(int(s["xseed"]), N * M, T, dims[0]), device=DEV)
+    opt = torch.optim.SGD([{"params": net.parameters()}, {"params": ge2e.parameters()}], lr=0.01)
+    losses = []
+    for step in range(3):
+        opt.zero_grad()
+        emb = net(x).reshape(N, M, -1)
+        if step == 0:
+            np.testing.assert_allclose(emb.detach().cpu().numpy(), s["emb0"], atol=2e-5)
+        loss = ge2e(emb)
+        loss.backward()
+        if step == 0:
+            for k, p in net.named_parameters():
+                assert _rel(p.grad.cpu().numpy(), s["grad." + k]) < 1e-4, k
+            assert abs(ge2e.w.grad.item() - float(s["dw0"])) <= 1e-4 * max(1, abs(float(s["dw0"])))
+        torch.nn.utils.clip_grad_norm_(net.parameters(), 3.0)
+        torch.nn.utils.clip_grad_norm_(ge2e.parameters(), 1.0)
+        opt.step()
+        losses.append(loss.item())
+    np.testing.assert_allclose(losses, s["losses"], rtol=1e-4)
+    for k, v in net.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), s["pf." + k], atol=2e-5)
+
+
+def test_small_net_fused_trainer_matches_reference():
+    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+    s = golden("net_small.npz")
+    dims = tuple(int(v) for v in s["dims"])
+    net, ge2e = _build(dims, recipe.make_weights(int(s["wseed"]), *dims, scale=float(s["wscale"])))
+    N, M, T = int(s["N"]), int(s["M"]), int(s["T"])
+    x = torch.tensor(recipe.make_frames(int(s["xseed"]), N * M, T, dims[0]), device=DEV)
+    tr = GE2ETrainer(net, ge2e, lr=0.01)
+    losses = [float(tr.step(x, N, M)) for _ in range(3)]
+    np.testing.assert_allclose(losses, s["losses"], rtol=1e-4)
+    for k, v in net.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), s["pf." + k], atol=2e-5)
+    np.testing.assert_allclose([ge2e.w.item(), ge2e.b.item()], s["wb_final"], atol=1e-5)
+
+
+def test_full_dims_c1_matches_reference():
+    s = golden("net_full_c1.npz")
+    dims = tuple(int(v) for v in s["dims"])
+    net, ge2e = _build(dims, recipe.make_weights(int(s["wseed"]), *dims, scale=float(s["wscale"])))
+    N, M, T = int(s["N"]), int(s["M"]), int(s["T"])
+    x = torch.tensor(recipe.make_frames(int(s["xseed"]), N * M, T, dims[0]), device=DEV)
+    emb = net(x).reshape(N, M, -1)
+    np.testing.assert_allclose(emb.detach().cpu().numpy(), s["emb"], atol=5e-5)
+    loss = ge2e(emb)
+    assert abs(loss.item() - float(s["loss"])) <= 1e-4 * abs(float(s["loss"]))
+    loss.backward()
+    for k, p in net.named_parameters():
+        g = p.grad.cpu().double()
+        assert abs(g.norm().item() - float(s["gnorm." + k])) <= 1e-3 * float(s["gnorm." + k]), k
+        head = g.reshape(g.shape[0], -1)[:8, :8].numpy() if g.dim() == 2 else g[:64].numpy()
+        ref = s["ghead." + k]
+        assert np.abs(head - ref).max() <= 2e-3 * max(np.abs(ref).max(), 1e-6) + 1e-7, k
+
+
+def test_full_size_c2_against_torch_gpu():
+    """c2 (N=64 x M=10, T=160) vs the stock-PyTorch fp32 port of the reference on the same GPU."""
+    dims, N, M, T = (40, 768, 3, 256), 64, 10, 160
+    sd = recipe.make_weights(2024, *dims, scale=3.0)
+    net, ge2e = _build(dims, sd)
+    port = torch_port.SpeechEmbedderPort(*dims)
+    torch_port.load_recipe_weights(port, sd)
+    port = port.to(DEV)
+    x = torch.tensor(recipe.make_frames(1236, N * M, T, dims[0]), device=DEV)
+    emb = net(x).reshape(N, M, -1)
+    emb_ref = port(x).reshape(N, M, -1)
+    assert _rel(emb.detach().cpu().numpy(), emb_ref.detach().cpu().numpy()) < 1e-4
+    # unit-norm rows (size-independent property of the projection + L2 norm)
+    np.testing.assert_allclose(emb.norm(dim=2).detach().cpu().numpy(), 1.0, atol=1e-5)
+    loss = ge2e(emb)
+    w = torch.tensor(10.0, device=DEV, requires_grad=True)
+    b = torch.tensor(-5.0, device=DEV, requires_grad=True)
+    loss_ref = torch_port.ge2e_loss(emb_ref, w, b)
+    assert abs(loss.item() - loss_ref.item()) <= 1e-4 * abs(loss_ref.item())
+    loss.backward()
+    loss_ref.backward()
+    pr = dict(port.named_parameters())
+    for k, p in net.named_parameters():
+        gr = pr[k].grad.cpu().numpy()
+        assert _rel(p.grad.cpu().numpy(), gr) < 2e-3, k
+    assert abs(ge2e.w.grad.item() - w.grad.item()) <= 1e-3 * max(1, abs(w.grad.item()))
+
+
+def test_batch_permutation_invariance():
+    """The reference permutes rows around the forward (train_speech_embedder.py:48-57);
+    rows are independent, so perm -> embed -> unperm equals embed."""
+    dims = (40, 128, 2, 64)
+    net, _ = _build(dims, recipe.make_weights(3, *dims, scale=2.0))
+    x = torch.tensor(recipe.make_frames(4, 24, 30, 40), device=DEV)
+    perm = torch.randperm(24, generator=torch.Generator().manual_seed(0)).to(DEV)
+    unperm = torch.empty_like(perm)
+    unperm[perm] = torch.arange(24, device=DEV)
+    a = net(x)
+    bb = net(x[perm])[unperm]
+    assert torch.equal(a, bb)
+
+
+def test_ragged_batch_and_seq_sizes():
+    """Non-multiple-of-tile batch / time / hidden sizes against the torch port."""
+    for dims, B, T in [((40, 96, 1, 24), 7, 5), ((40, 200, 2, 36), 33, 3), ((40, 64, 3, 32), 1, 1)]:
+        sd = recipe.make_weights(B * 13 + T, *dims, scale=2.0)
+        net, _ = _build(dims, sd)
+        port = torch_port.SpeechEmbedderPort(*dims)
+        torch_port.load_recipe_weights(port, sd)
+        x = torch.tensor(recipe.make_frames(B, B, T, dims[0]))
+        e = net(x.to(DEV)).detach().cpu().numpy()
+        er = port(x).detach().numpy()
+        np.testing.assert_allclose(e, er, atol=5e-5)

@@ -1,0 +1,65 @@
+"""Speaker-sharded GE2E exchange protocol under gloo, world size 2, on CPU.
+
+The product's ShardedGE2E runs its real collective sequence (all_gather of speaker sums,
+SUM all_reduce of the centroid-gradient buffer) with the oracle's per-shard numpy kernels
+plugged in; the concatenated shard results must equal the unsharded oracle."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import recipe
+from oracle import ge2e_np
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, N, M, D, w, b, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pytorch_speaker_verification_amd.sharded_ge2e import ShardedGE2E
+        E = recipe.make_embeddings(77, N, M, D, True).astype(np.float64)
+        Nl = N // world
+        El = torch.tensor(E[rank * Nl:(rank + 1) * Nl])
+        sh = ShardedGE2E(kernels=ge2e_np.NumpyShardKernels())
+        assert sh.world == world and sh.rank == rank
+        loss, per, st = sh.forward(El, torch.tensor(w), torch.tensor(b))
+        dE, dwdb = sh.backward(st, torch.tensor(w), torch.tensor(b))
+        dist.all_reduce(dwdb)
+        q.put((rank, float(loss), per.numpy(), dE.numpy(), dwdb.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_ge2e_gloo_world2():
+    N, M, D, w, b = 8, 5, 16, 7.5, -2.5
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, M, D, w, b, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    E = recipe.make_embeddings(77, N, M, D, True)
+    loss, per, _ = ge2e_np.ge2e_forward(E, w, b)
+    dE, dw, db = ge2e_np.ge2e_backward(E, w, b)
+    for r in range(world):
+        assert abs(res[r][1] - loss) < 1e-9 * max(1, abs(loss))  # all-reduced global loss
+    np.testing.assert_allclose(np.concatenate([r[2] for r in res]), per, atol=1e-10)
+    np.testing.assert_allclose(np.concatenate([r[3] for r in res]), dE, atol=1e-10)
+    np.testing.assert_allclose(res[0][4], [dw, db], atol=1e-10)
