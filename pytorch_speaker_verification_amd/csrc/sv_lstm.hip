@@ -68,12 +68,15 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 
 // out[M,N] (ld ldc) = sum_z slab[z][M,N] (+ beta*out), fixed summation order
 __global__ void slab_reduce_kernel(const float* __restrict__ slab, int nz, long zstride, float* __restrict__ out,
-                                   long ldc, int M, int N, float beta) {
+                                   long ldc, int M, int N, float beta, const float* __restrict__ bias0,
+                                   const float* __restrict__ bias1) {
   const long total = (long)M * N;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const int row = (int)(e / N), col = (int)(e % N);
     float s = 0.f;
     for (int z = 0; z < nz; ++z) s += slab[z * zstride + e];
+    if (bias0) s += bias0[col];
+    if (bias1) s += bias1[col];
     float* dst = out + (long)row * ldc + col;
     *dst = (beta != 0.f ? beta * *dst : 0.f) + s;
   }
@@ -289,7 +292,6 @@ extern "C" int sv_gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, co
     return dispatch_layout<128, 128, EPI_STORE>(ak, bk, A, lda, B, ldb, C, ldc, 0, M, N, K, 1, p.kchunk, bias0, bias1, beta, stream);
   }
   if (!workspace) return SV_EARG;
-  if (bias0 || bias1) return SV_EARG;  // split-K path is used for weight gradients only
   const long slab = (long)M * N;
   int rc;
   if (p.bm == 64)
@@ -299,7 +301,8 @@ extern "C" int sv_gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, co
   if (rc) return rc;
   const long total = slab;
   const int grid = (int)std::min<long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, stream, workspace, p.splitk, slab, C, ldc, M, N, beta);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, stream, workspace, p.splitk, slab, C, ldc, M, N, beta,
+                     bias0, bias1);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }

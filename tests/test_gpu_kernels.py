@@ -108,3 +108,14 @@ def test_clip_sgd_matches_torch():
         np.testing.assert_allclose(pd.cpu().double().numpy(), pr.numpy(), atol=1e-6)
         np.testing.assert_allclose(gd.cpu().double().numpy(), (grr * coef).numpy(), atol=1e-6)
         assert abs(float(out) - float(norm)) <= 1e-5 * float(norm)
+
+
+@pytest.mark.parametrize("M,N,K", [(640, 256, 768), (100, 36, 1024), (3000, 3072, 40)])
+def test_gemm_f32_bias_and_split_k(M, N, K):
+    """Bias epilogue on both the direct and the split-K (slab reduce) paths."""
+    from pytorch_speaker_verification_amd.ops import gemm_f32
+    g = torch.Generator().manual_seed(M + N + K)
+    A, B, bias = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g), torch.randn(N, generator=g)
+    ref = A.double() @ B.double().T + bias.double()
+    C = gemm_f32(A.to(DEV), B.to(DEV), True, True, bias=bias.to(DEV)).cpu().double()
+    assert (C - ref).abs().max().item() <= 2e-6 * K ** 0.5 * ref.abs().max().item() + 1e-5
