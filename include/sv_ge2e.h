@@ -44,21 +44,28 @@ int sv_colsum(const float* X, int R, int C, float* out, float* workspace, hipStr
  * autograd backward via train_speech_embedder.py:62).  Time-major layouts:
  *   x_tm [T,B,F], gates [T,B,4H] (activated i,f,g,o), c_tm [T,B,H], h_tm [T+1,B,H] (h_tm[0]=0). */
 int sv_frames_to_time_major(const float* x, float* x_tm, int B, int T, int F, hipStream_t stream);
+/* dst[c*ld_dst + r] = src[r*ld_src + c] for an R x C matrix */
+int sv_transpose(const float* src, long ld_src, int R, int C, float* dst, long ld_dst, hipStream_t stream);
+/* Transposed layouts use column blocks of Bp = (B + 3) & ~3 (padding columns zero).
+ * hT [H, (T+1)Bp] (may be NULL): h_t^T as column block t+1, block 0 = 0 -- the k-contiguous
+ * operand of the weight-gradient GEMMs (block t = h_{t-1}) and of the next layer's dW_ih. */
 int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, const float* w_ih, const float* w_hh,
-                      const float* b_ih, const float* b_hh, float* gates, float* c_tm, float* h_tm,
+                      const float* b_ih, const float* b_hh, float* gates, float* c_tm, float* h_tm, float* hT,
                       hipStream_t stream);
 /* one forward recurrent step (K2): on entry gates_t [B,4H] = x_t W_ih^T + b_ih + b_hh, on exit the
  * activated gates; h_prev / c_prev may be NULL (t = 0). */
 int sv_lstm_step_fwd(const float* h_prev, const float* w_hh, float* gates_t, const float* c_prev, float* c_t,
                      float* h_t, int B, int H, hipStream_t stream);
 size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H);
-/* dh_up: gradient w.r.t. this layer's outputs; dh_up_full=1 -> [T,B,H], 0 -> [B,H] for t=T-1 only.
- * Outputs dgates [T,B,4H], dx_tm [T,B,F] (may be NULL), dw_ih [4H,F], dw_hh [4H,H],
- * db_ih [4H] and db_hh [4H] (may be NULL; both equal sum dgates). */
-int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* x_tm, const float* w_ih, const float* w_hh,
-                      const float* gates, const float* c_tm, const float* h_tm, const float* dh_up, int dh_up_full,
-                      float* dgates, float* dx_tm, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh,
-                      float* workspace, hipStream_t stream);
+/* xT: the layer input transposed, [F, >= T*Bp] with row stride ld_xT (layer 0: the frames;
+ * layer l > 0: hT of layer l-1 offset by Bp columns).  hT: this layer's [H, (T+1)Bp] from the fwd.
+ * dh_up: gradient w.r.t. this layer's outputs; dh_up_full=1 -> [T,B,H], 0 -> [B,H] for t=T-1 only.
+ * Outputs dgates [T,B,4H], dgT [4H, T*Bp] (its transpose), dx_tm [T,B,F] (may be NULL),
+ * dw_ih [4H,F], dw_hh [4H,H], db_ih [4H] and db_hh [4H] (may be NULL; both = sum dgates). */
+int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* xT, long ld_xT, const float* w_ih, const float* w_hh,
+                      const float* gates, const float* c_tm, const float* hT, const float* dh_up, int dh_up_full,
+                      float* dgates, float* dgT, float* dx_tm, float* dw_ih, float* dw_hh, float* db_ih,
+                      float* db_hh, float* workspace, hipStream_t stream);
 
 /* ---- projection + L2 norm (speech_embedder_net.py:30-32) --------------------------------- */
 size_t sv_proj_norm_workspace(int B, int H, int P);

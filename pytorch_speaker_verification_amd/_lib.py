@@ -30,11 +30,12 @@ SIGNATURES = {
     "sv_colsum_workspace": (_c_size_t, [_c_int, _c_int]),
     "sv_colsum": (_c_int, [_P, _c_int, _c_int, _P, _P, _P]),
     "sv_frames_to_time_major": (_c_int, [_P, _P, _c_int, _c_int, _c_int, _P]),
-    "sv_lstm_layer_fwd": (_c_int, [_P, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "sv_transpose": (_c_int, [_P, _c_long, _c_int, _c_int, _P, _c_long, _P]),
+    "sv_lstm_layer_fwd": (_c_int, [_P, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_lstm_step_fwd": (_c_int, [_P, _P, _P, _P, _P, _P, _c_int, _c_int, _P]),
     "sv_lstm_layer_bwd_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
-    "sv_lstm_layer_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _c_int, _P, _P, _P,
-                                   _P, _P, _P, _P, _P]),
+    "sv_lstm_layer_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _P, _c_long, _P, _P, _P, _P, _P, _P, _c_int, _P,
+                                   _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_proj_norm_workspace": (_c_size_t, [_c_int, _c_int, _c_int]),
     "sv_proj_norm_fwd": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P]),
     "sv_proj_norm_bwd": (_c_int, [_P, _P, _P, _P, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P]),

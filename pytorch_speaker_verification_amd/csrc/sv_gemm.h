@@ -153,3 +153,97 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   if (q == 0) return orig;
   return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
 }
+
+// ===========================================================================
+// k-major tiles: both operands k-contiguous in HBM (element (r,k) at base[row(r)*ld + k])
+// and in LDS as [R][BK+4] (16-B aligned rows; the +4-float pad makes a 16-lane group's
+// ds_read_b128 of 16 distinct rows hit 16 distinct 16-B bank slots).  For the 32x32x2 f32
+// MFMA, lane (r = l&31, h = l>>5) reads 4 consecutive k at 8g + 4h with one ds_read_b128
+// and feeds MFMAs c = 0..3 with k_phys = 8g + 4h + c: the two lane halves together cover
+// k = 8g .. 8g+7 (a fixed permutation of the reduction order, identical for A and B).
+// ===========================================================================
+template <int R, int NT, int BK>
+struct KTileStage {
+  static constexpr int LD = BK + 4;
+  static constexpr int C4 = BK / 4;  // float4 per row
+  static constexpr int NV = (R * C4) / NT;
+  static_assert(NV >= 1 && NV * NT == R * C4, "tile/thread mismatch");
+  f32x4 v[NV];
+
+  template <class Map>
+  __device__ __forceinline__ void load(const float* __restrict__ base, long ld, const Map& map, int k0, int K,
+                                       int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int q = tid + NT * i;
+      const int r = q / C4, c = (q % C4) * 4;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (map.valid(r) && k0 + c < K) x = *reinterpret_cast<const f32x4*>(base + (long)map(r) * ld + k0 + c);
+      v[i] = x;
+    }
+  }
+  __device__ __forceinline__ void store(float* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int q = tid + NT * i;
+      *reinterpret_cast<f32x4*>(lds + (q / C4) * LD + (q % C4) * 4) = v[i];
+    }
+  }
+};
+
+template <int TM, int TN, int BK, int LD>
+__device__ __forceinline__ void mfma_ktile_km(const float* As, const float* Bs, int wm0, int wn0, int lane,
+                                              f32x16 (&acc)[TM][TN]) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int g = 0; g < BK / 8; ++g) {
+    f32x4 a[TM], b[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const f32x4*>(As + (wm0 + 32 * i + r) * LD + 8 * g + 4 * h);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const f32x4*>(Bs + (wn0 + 32 * j + r) * LD + 8 * g + 4 * h);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x2(a[i][c], b[j][c], acc[i][j]);
+  }
+}
+
+// lds must hold 2 * (BM + BN) * (BK + 4) floats
+template <int BM, int BN, int NT, int BK, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_km(const float* __restrict__ A, long lda, const MapA& mapA,
+                                                 const float* __restrict__ B, long ldb, const MapB& mapB, int kbeg,
+                                                 int kend, float* lds, int tid, int wm0, int wn0,
+                                                 f32x16 (&acc)[TM][TN]) {
+  using SA = KTileStage<BM, NT, BK>;
+  using SB = KTileStage<BN, NT, BK>;
+  constexpr int LD = BK + 4;
+  constexpr int BUF = (BM + BN) * LD;
+  const int lane = tid & 63;
+  SA sa;
+  SB sb;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk <= 0) return;
+  sa.load(A, lda, mapA, kbeg, kend, tid);
+  sb.load(B, ldb, mapB, kbeg, kend, tid);
+  sa.store(lds, tid);
+  sb.store(lds + BM * LD, tid);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    float* cur = lds + (kt & 1) * BUF;
+    float* nxt = lds + ((kt + 1) & 1) * BUF;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      sa.load(A, lda, mapA, kbeg + (kt + 1) * BK, kend, tid);
+      sb.load(B, ldb, mapB, kbeg + (kt + 1) * BK, kend, tid);
+    }
+    mfma_ktile_km<TM, TN, BK, LD>(cur, cur + BM * LD, wm0, wn0, lane, acc);
+    if (more) {
+      sa.store(nxt, tid);
+      sb.store(nxt + BM * LD, tid);
+    }
+    __syncthreads();
+  }
+}

@@ -10,9 +10,12 @@
 //   c_tm   [T, B, H]      cell state c_t
 //   h_tm   [T+1, B, H]    h_tm[0] = h_{-1} = 0, h_tm[t+1] = h_t
 //   dgates [T, B, 4H]     dL/d(pre-activation gates)
+#include <stdlib.h>
 #include "sv_common.h"
 #include "sv_gemm.h"
 #include "../../include/sv_ge2e.h"
+
+#define SV_BKM 32
 
 // ============================================================================
 // generic fp32 GEMM  C[M,N] = op(A) op(B) (+ bias) (+ beta C), or split-K slabs
@@ -114,10 +117,98 @@ __global__ void to_time_major_kernel(const float* __restrict__ x, float* __restr
   }
 }
 
+// k-major ("NT") GEMM: both operands k-contiguous; the fast path for every large GEMM
+template <int BM, int BN, int EPI>
+__global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ A, long lda, const float* __restrict__ B,
+                                                      long ldb, float* __restrict__ C, long ldc, long slab, int M,
+                                                      int N, int K, int kchunk, const float* __restrict__ bias0,
+                                                      const float* __restrict__ bias1, float beta) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int TM = BM / 64, TN = BN / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_m * ((N + BN - 1) / BN);
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int tm = id % tiles_m, tn = id / tiles_m;
+  const int kbeg = blockIdx.y * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  const int wm0 = (w >> 1) * (BM / 2), wn0 = (w & 1) * (BN / 2);
+  f32x16 acc[TM][TN];
+  zero_acc(acc);
+  gemm_mainloop_km<BM, BN, 256, SV_BKM, TM, TN>(A, lda, RowMapLinear{tm * BM, M}, B, ldb, RowMapLinear{tn * BN, N},
+                                                kbeg, kend, lds, tid, wm0, wn0, acc);
+  float* Cz = C + (EPI == EPI_SLAB ? (long)blockIdx.y * slab : 0);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = tn * BN + wn0 + 32 * j + (lane & 31);
+      if (col >= N) continue;
+      float badd = 0.f;
+      if (EPI == EPI_STORE) {
+        if (bias0) badd += bias0[col];
+        if (bias1) badd += bias1[col];
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = tm * BM + wm0 + 32 * i + acc_row(r, lane);
+        if (row >= M) continue;
+        float v = acc[i][j][r];
+        float* dst = Cz + (long)row * ldc + col;
+        if (EPI == EPI_STORE) {
+          v += badd;
+          if (beta != 0.f) v += beta * *dst;
+        }
+        *dst = v;
+      }
+    }
+}
+
+// row sums out[r] = sum_c X[r*ld + c], one block per row, fixed order
+__global__ __launch_bounds__(256) void rowsum_kernel(const float* __restrict__ X, long ld, int C,
+                                                     float* __restrict__ out0, float* __restrict__ out1) {
+  __shared__ float red[4];
+  const float* x = X + (long)blockIdx.x * ld;
+  float s = 0.f;
+  const int C4 = C / 4;
+  for (int c = threadIdx.x; c < C4; c += 256) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[c];
+    s += (v.x + v.y) + (v.z + v.w);
+  }
+  for (int c = C4 * 4 + threadIdx.x; c < C; c += 256) s += x[c];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = (red[0] + red[1]) + (red[2] + red[3]);
+    out0[blockIdx.x] = t;
+    if (out1) out1[blockIdx.x] = t;
+  }
+}
+
+// dst[c*ldd + r] = src[r*lds + c]  (R x C), 32x32 tiles through LDS
+__global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ src, long lds_, int R, int C,
+                                                        float* __restrict__ dst, long ldd) {
+  __shared__ float tile[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? src[(long)r * lds_ + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) dst[(long)c * ldd + r] = tile[tx][i];
+  }
+}
+
 // ============================================================================
 // K2: forward recurrent step.  Block = 64 batch rows x 32 hidden units (= 128 gate
-// columns: i,f,g,o of those units), 4 waves in 2x2; K = H.  Epilogue: + x-projection,
-// sigmoid/tanh, c_t = f c_{t-1} + i g, h_t = o tanh(c_t).
+// columns: i,f,g,o of those units), 4 waves in 2x2; K = H, k-major LDS tiles.
+// Epilogue: + x-projection, sigmoid/tanh, c_t = f c_{t-1} + i g, h_t = o tanh(c_t);
+// stores the activated gates (for BPTT), c_t, h_t and h_t^T (column block t+1 of
+// hT[H, (T+1) B], the k-contiguous operand of the weight-gradient GEMMs).
 // ============================================================================
 #define FWD_BM 64
 #define FWD_U 32
@@ -125,22 +216,24 @@ __global__ void to_time_major_kernel(const float* __restrict__ x, float* __restr
 __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(const float* __restrict__ hprev,
                                                             const float* __restrict__ whh, float* __restrict__ gates,
                                                             const float* __restrict__ cprev, float* __restrict__ cout,
-                                                            float* __restrict__ hout, int B, int H) {
+                                                            float* __restrict__ hout, float* __restrict__ hT, long ldhT,
+                                                            int t, int Bp, int B, int H) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int BN = 4 * FWD_U, LDP = BN + 4;
+  constexpr int BN = 4 * FWD_U, LDP = BN + 4, LDH = FWD_BM + 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int j0 = blockIdx.x * FWD_U, b0 = blockIdx.y * FWD_BM;
   const int wm0 = (w >> 1) * 32, wn0 = (w & 1) * 64;
   f32x16 acc[1][2];
   zero_acc(acc);
   if (hprev)
-    gemm_mainloop<FWD_BM, BN, 256, true, true, 1, 2>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
-                                                     RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc);
-  // pre-activations (recurrent part) -> LDS [64][LDP]
+    gemm_mainloop_km<FWD_BM, BN, 256, SV_BKM, 1, 2>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
+                                                    RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc);
+  float* pre = lds;                   // [64][LDP]
+  float* hs = lds + FWD_BM * LDP;     // [32][LDH]  h^T staging
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) lds[(wm0 + acc_row(r, lane)) * LDP + wn0 + 32 * j + (lane & 31)] = acc[0][j][r];
+    for (int r = 0; r < 16; ++r) pre[(wm0 + acc_row(r, lane)) * LDP + wn0 + 32 * j + (lane & 31)] = acc[0][j][r];
   __syncthreads();
   const long G = 4L * H;
   for (int e = tid; e < FWD_BM * FWD_U; e += 256) {
@@ -148,7 +241,7 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(const float* __restr
     const int gb = b0 + b, gj = j0 + u;
     if (gb >= B || gj >= H) continue;
     float* gp = gates + (long)gb * G + gj;
-    const float* pr = lds + b * LDP + u;
+    const float* pr = pre + b * LDP + u;
     const float pi = pr[0] + gp[0];
     const float pf = pr[FWD_U] + gp[H];
     const float pg = pr[2 * FWD_U] + gp[2 * H];
@@ -163,38 +256,53 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(const float* __restr
     gp[3 * H] = o;
     cout[(long)gb * H + gj] = c;
     hout[(long)gb * H + gj] = h;
+    hs[u * LDH + b] = h;
+  }
+  if (!hT) return;
+  __syncthreads();
+  // h^T: rows = hidden units, columns = (t+1)*B + b; batch index fastest (coalesced)
+  for (int e = tid; e < FWD_BM * FWD_U; e += 256) {
+    const int u = e / FWD_BM, b = e % FWD_BM;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    float* row = hT + (long)gj * ldhT;
+    row[(long)(t + 1) * Bp + gb] = hs[u * LDH + b];
+    if (t == 0) row[gb] = 0.f;  // column block 0 = h_{-1} = 0
   }
 }
 
 // ============================================================================
 // K3: backward recurrent step at time t.  Block = 64 batch rows x 32 hidden units;
 // wave w computes dG_{t+1}[:, gate w] . W_hh[gate w rows, units] (K = H each, an
-// in-block split of K = 4H by gate), partials summed in LDS in fixed order.
-// Epilogue: dh = that + dh_up; dc = dc_{t+1} f_{t+1} + dh o (1 - tanh^2 c);
-// dG_t = [dc g i(1-i), dc c_{t-1} f(1-f), dc i (1-g^2), dh tanh(c) o(1-o)].
+// in-block split of K = 4H by gate) from W_hh^T [H, 4H] (k-contiguous), partials summed
+// in LDS in fixed order.  Epilogue: dh = that + dh_up; dc = dc_{t+1} f_{t+1} + dh o
+// (1 - tanh^2 c); dG_t = [dc g i(1-i), dc c_{t-1} f(1-f), dc i (1-g^2), dh tanh(c) o(1-o)],
+// stored as dG[t] [B, 4H] and as column block t of dG^T [4H, T B].
 // ============================================================================
 #define BWD_BM 64
 #define BWD_U 32
 
 __global__ __launch_bounds__(256) void lstm_step_bwd_kernel(
-    const float* __restrict__ dgnext, const float* __restrict__ whh, const float* __restrict__ dhup,
+    const float* __restrict__ dgnext, const float* __restrict__ whhT, const float* __restrict__ dhup,
     const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
-    const float* __restrict__ c_prev, float* __restrict__ dg, float* __restrict__ dcf, int B, int H) {
+    const float* __restrict__ c_prev, float* __restrict__ dg, float* __restrict__ dcf, float* __restrict__ dgT,
+    long lddgT, int t, int Bp, int B, int H) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int LDA = TileLd<true, BWD_BM>::value, LDB = TileLd<false, BWD_U>::value;
-  constexpr int WBUF = 2 * SV_BK * (LDA + LDB);
+  constexpr int WBUF = 2 * (BWD_BM + BWD_U) * (SV_BKM + 4);
   constexpr int LDR = BWD_U + 1;
+  constexpr int LDT = BWD_BM + 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int j0 = blockIdx.x * BWD_U, b0 = blockIdx.y * BWD_BM;
   const long G = 4L * H;
   f32x16 acc[2][1];
   zero_acc(acc);
   if (dgnext)
-    gemm_mainloop<BWD_BM, BWD_U, 64, true, false, 2, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whh, H,
-                                                        RowMapLinear{j0, H}, w * H, (w + 1) * H, lds + w * WBUF,
-                                                        lane, 0, 0, acc);
+    gemm_mainloop_km<BWD_BM, BWD_U, 64, SV_BKM, 2, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
+                                                      RowMapLinear{j0, H}, w * H, (w + 1) * H, lds + w * WBUF, lane,
+                                                      0, 0, acc);
   __syncthreads();
-  float* red = lds;  // [4][64][LDR]
+  float* red = lds;                          // [4][64][LDR]
+  float* gT = lds + 4 * BWD_BM * LDR;        // [4*32][LDT] dG^T staging
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -217,12 +325,158 @@ __global__ __launch_bounds__(256) void lstm_step_bwd_kernel(
     float dc = dh * o * (1.f - tc * tc);
     if (dcf_next) dc += dcf_next[hi];
     const float cp = c_prev ? c_prev[hi] : 0.f;
+    const float d0 = dc * g * i * (1.f - i), d1 = dc * cp * f * (1.f - f);
+    const float d2 = dc * i * (1.f - g * g), d3 = dh * tc * o * (1.f - o);
     float* dp = dg + (long)gb * G + gj;
-    dp[0] = dc * g * i * (1.f - i);
-    dp[H] = dc * cp * f * (1.f - f);
-    dp[2 * H] = dc * i * (1.f - g * g);
-    dp[3 * H] = dh * tc * o * (1.f - o);
+    dp[0] = d0;
+    dp[H] = d1;
+    dp[2 * H] = d2;
+    dp[3 * H] = d3;
     dcf[hi] = dc * f;
+    gT[(0 * BWD_U + u) * LDT + b] = d0;
+    gT[(1 * BWD_U + u) * LDT + b] = d1;
+    gT[(2 * BWD_U + u) * LDT + b] = d2;
+    gT[(3 * BWD_U + u) * LDT + b] = d3;
+  }
+  if (!dgT) return;
+  __syncthreads();
+  for (int e = tid; e < 4 * BWD_U * BWD_BM; e += 256) {
+    const int gu = e / BWD_BM, b = e % BWD_BM;
+    const int gate = gu / BWD_U, u = gu % BWD_U;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    dgT[((long)gate * H + gj) * lddgT + (long)t * Bp + gb] = gT[gu * LDT + b];
+  }
+}
+
+// ============================================================================
+// 8-wave variants of K2/K3 (512 threads, 2 waves per SIMD so one wave's MFMAs cover the
+// other's LDS/global waits).
+//   K2v2: the 64 x 128 gate tile is split 2 (rows) x 4 (gate) over 8 waves, one 32x32
+//         accumulator each, all sharing the same staged A/B tiles.
+//   K3v2: 4 groups of 2 waves, group = gate (its K range of W_hh^T), waves split the rows.
+// ============================================================================
+__global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __restrict__ hprev,
+                                                               const float* __restrict__ whh,
+                                                               float* __restrict__ gates,
+                                                               const float* __restrict__ cprev,
+                                                               float* __restrict__ cout, float* __restrict__ hout,
+                                                               float* __restrict__ hT, long ldhT, int t, int Bp, int B,
+                                                               int H) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int BN = 4 * FWD_U, LDP = BN + 4, LDH = FWD_BM + 1;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j0 = blockIdx.x * FWD_U, b0 = blockIdx.y * FWD_BM;
+  const int wm0 = (w >> 2) * 32, wn0 = (w & 3) * 32;
+  f32x16 acc[1][1];
+  zero_acc(acc);
+  if (hprev)
+    gemm_mainloop_km<FWD_BM, BN, 512, SV_BKM, 1, 1>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
+                                                    RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc);
+  float* pre = lds;
+  float* hs = lds + FWD_BM * LDP;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) pre[(wm0 + acc_row(r, lane)) * LDP + wn0 + (lane & 31)] = acc[0][0][r];
+  __syncthreads();
+  const long G = 4L * H;
+  for (int e = tid; e < FWD_BM * FWD_U; e += 512) {
+    const int b = e / FWD_U, u = e % FWD_U;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    float* gp = gates + (long)gb * G + gj;
+    const float* pr = pre + b * LDP + u;
+    const float pi = pr[0] + gp[0];
+    const float pf = pr[FWD_U] + gp[H];
+    const float pg = pr[2 * FWD_U] + gp[2 * H];
+    const float po = pr[3 * FWD_U] + gp[3 * H];
+    const float i = sv_sigmoid(pi), f = sv_sigmoid(pf), g = tanhf(pg), o = sv_sigmoid(po);
+    const float cp = cprev ? cprev[(long)gb * H + gj] : 0.f;
+    const float c = f * cp + i * g;
+    const float h = o * tanhf(c);
+    gp[0] = i;
+    gp[H] = f;
+    gp[2 * H] = g;
+    gp[3 * H] = o;
+    cout[(long)gb * H + gj] = c;
+    hout[(long)gb * H + gj] = h;
+    hs[u * LDH + b] = h;
+  }
+  if (!hT) return;
+  __syncthreads();
+  for (int e = tid; e < FWD_BM * FWD_U; e += 512) {
+    const int u = e / FWD_BM, b = e % FWD_BM;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    float* row = hT + (long)gj * ldhT;
+    row[(long)(t + 1) * Bp + gb] = hs[u * LDH + b];
+    if (t == 0) row[gb] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
+    const float* __restrict__ dgnext, const float* __restrict__ whhT, const float* __restrict__ dhup,
+    const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
+    const float* __restrict__ c_prev, float* __restrict__ dg, float* __restrict__ dcf, float* __restrict__ dgT,
+    long lddgT, int t, int Bp, int B, int H) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int GBUF = 2 * (BWD_BM + BWD_U) * (SV_BKM + 4);
+  constexpr int LDR = BWD_U + 1;
+  constexpr int LDT = BWD_BM + 1;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int gate = w >> 1, gt = tid & 127;
+  const int j0 = blockIdx.x * BWD_U, b0 = blockIdx.y * BWD_BM;
+  const long G = 4L * H;
+  f32x16 acc[1][1];
+  zero_acc(acc);
+  if (dgnext)
+    gemm_mainloop_km<BWD_BM, BWD_U, 128, SV_BKM, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
+                                                       RowMapLinear{j0, H}, gate * H, (gate + 1) * H,
+                                                       lds + gate * GBUF, gt, (w & 1) * 32, 0, acc);
+  __syncthreads();
+  float* red = lds;                    // [4][64][LDR]
+  float* gT = lds + 4 * BWD_BM * LDR;  // [4*32][LDT]
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    red[(gate * BWD_BM + (w & 1) * 32 + acc_row(r, lane)) * LDR + (lane & 31)] = acc[0][0][r];
+  __syncthreads();
+  for (int e = tid; e < BWD_BM * BWD_U; e += 512) {
+    const int b = e / BWD_U, u = e % BWD_U;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    const long hi = (long)gb * H + gj;
+    float dh = red[(0 * BWD_BM + b) * LDR + u];
+    dh += red[(1 * BWD_BM + b) * LDR + u];
+    dh += red[(2 * BWD_BM + b) * LDR + u];
+    dh += red[(3 * BWD_BM + b) * LDR + u];
+    if (dhup) dh += dhup[hi];
+    const float* ap = acts + (long)gb * G + gj;
+    const float i = ap[0], f = ap[H], g = ap[2 * H], o = ap[3 * H];
+    const float c = c_t[hi];
+    const float tc = tanhf(c);
+    float dc = dh * o * (1.f - tc * tc);
+    if (dcf_next) dc += dcf_next[hi];
+    const float cp = c_prev ? c_prev[hi] : 0.f;
+    const float d0 = dc * g * i * (1.f - i), d1 = dc * cp * f * (1.f - f);
+    const float d2 = dc * i * (1.f - g * g), d3 = dh * tc * o * (1.f - o);
+    float* dp = dg + (long)gb * G + gj;
+    dp[0] = d0;
+    dp[H] = d1;
+    dp[2 * H] = d2;
+    dp[3 * H] = d3;
+    dcf[hi] = dc * f;
+    gT[(0 * BWD_U + u) * LDT + b] = d0;
+    gT[(1 * BWD_U + u) * LDT + b] = d1;
+    gT[(2 * BWD_U + u) * LDT + b] = d2;
+    gT[(3 * BWD_U + u) * LDT + b] = d3;
+  }
+  if (!dgT) return;
+  __syncthreads();
+  for (int e = tid; e < 4 * BWD_U * BWD_BM; e += 512) {
+    const int gu = e / BWD_BM, b = e % BWD_BM;
+    const int gte = gu / BWD_U, u = gu % BWD_U;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    dgT[((long)gte * H + gj) * lddgT + (long)t * Bp + gb] = gT[gu * LDT + b];
   }
 }
 
@@ -234,10 +488,16 @@ namespace {
 template <int BM, int BN, bool AK, bool BKC, int EPI>
 int launch_gemm_t(const float* A, long lda, const float* B, long ldb, float* C, long ldc, long slab, int M, int N,
                   int K, int splitk, int kchunk, const float* b0, const float* b1, float beta, hipStream_t s) {
-  constexpr int LDS_FLOATS = 2 * SV_BK * (TileLd<AK, BM>::value + TileLd<BKC, BN>::value);
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, AK, BKC, EPI>), dim3(tiles, splitk), dim3(256),
-                     LDS_FLOATS * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+  if (AK && BKC) {
+    constexpr int LDS_KM = 2 * (BM + BN) * (SV_BKM + 4);
+    hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float), s, A,
+                       lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+  } else {
+    constexpr int LDS_FLOATS = 2 * SV_BK * (TileLd<AK, BM>::value + TileLd<BKC, BN>::value);
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, AK, BKC, EPI>), dim3(tiles, splitk), dim3(256),
+                       LDS_FLOATS * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+  }
   SV_LAUNCH_CHECK();
   return SV_OK;
 }
@@ -256,16 +516,27 @@ struct GemmPlan {
   int bm, bn, splitk, kchunk;
 };
 
+// Tile 128x128 when there are enough tiles to fill the chip, else 64x64; split K only when
+// the tile count leaves resident slots (2 blocks/CU x 256 CUs) idle, and never below 512-deep
+// K chunks.  The split count is chosen so tiles*splitk fits the slots in whole rounds.
 GemmPlan plan_gemm(int M, int N, int K) {
   GemmPlan p;
-  const bool small = (long)((M + 127) / 128) * ((N + 127) / 128) < 128;
+  const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+  const bool small = t128 < 128;
   p.bm = small ? 64 : 128;
   p.bn = small ? 64 : 128;
   const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
+  const long slots = small ? 1024 : 512;
   int sk = 1;
-  while (tiles * sk < 512 && K / (sk * 2) >= 256 && sk < 32) sk *= 2;
-  p.splitk = sk;
-  p.kchunk = ((K + sk - 1) / sk + SV_BK - 1) / SV_BK * SV_BK;
+  if (tiles < slots) {
+    sk = (int)(slots / tiles);
+    const int kmax = K / 512;
+    if (sk > kmax) sk = kmax;
+    if (sk > 32) sk = 32;
+    if (sk < 1) sk = 1;
+  }
+  const int q = SV_BKM;
+  p.kchunk = ((K + sk - 1) / sk + q - 1) / q * q;
   p.splitk = (K + p.kchunk - 1) / p.kchunk;
   return p;
 }
@@ -317,6 +588,14 @@ extern "C" int sv_frames_to_time_major(const float* x, float* x_tm, int B, int T
   return SV_OK;
 }
 
+extern "C" int sv_transpose(const float* src, long ld_src, int R, int C, float* dst, long ld_dst, hipStream_t stream) {
+  if (!src || !dst || R <= 0 || C <= 0) return SV_EARG;
+  hipLaunchKernelGGL(transpose_kernel, dim3((C + 31) / 32, (R + 31) / 32), dim3(256), 0, stream, src, ld_src, R, C, dst,
+                     ld_dst);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
 static int colsum(const float* X, int R, int C, float* out0, float* out1, float* partial, hipStream_t s) {
   const int rows_per_chunk = 1024;
   const int nchunk = (R + rows_per_chunk - 1) / rows_per_chunk;
@@ -339,9 +618,53 @@ static bool lstm_dims_ok(int T, int B, int F, int H) {
   return T > 0 && B > 0 && F > 0 && H > 0 && F % 4 == 0 && H % 4 == 0;
 }
 
+namespace {
+constexpr int FWD_LDS_MAIN = 2 * (FWD_BM + 4 * FWD_U) * (SV_BKM + 4);
+constexpr int FWD_LDS_EPI = FWD_BM * (4 * FWD_U + 4) + FWD_U * (FWD_BM + 1);
+constexpr int FWD_LDS = (FWD_LDS_MAIN > FWD_LDS_EPI ? FWD_LDS_MAIN : FWD_LDS_EPI) * (int)sizeof(float);
+constexpr int BWD_LDS_MAIN = 4 * 2 * (BWD_BM + BWD_U) * (SV_BKM + 4);
+constexpr int BWD_LDS_EPI = 4 * BWD_BM * (BWD_U + 1) + 4 * BWD_U * (BWD_BM + 1);
+constexpr int BWD_LDS = (BWD_LDS_MAIN > BWD_LDS_EPI ? BWD_LDS_MAIN : BWD_LDS_EPI) * (int)sizeof(float);
+// step-kernel variant: 2 = 8-wave (default), 1 = 4-wave; SV_STEP_VARIANT overrides (A/B timing)
+int step_variant() {
+  static int v = [] {
+    const char* e = getenv("SV_STEP_VARIANT");
+    return (e && *e == '1') ? 1 : 2;
+  }();
+  return v;
+}
+void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh, float* g, const float* cp, float* c,
+                     float* h, float* hT, long ldhT, int t, int Bp, int B, int H) {
+  if (step_variant() == 2)
+    hipLaunchKernelGGL(lstm_step_fwd_v2_kernel, grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT, ldhT, t, Bp, B,
+                       H);
+  else
+    hipLaunchKernelGGL(lstm_step_fwd_kernel, grid, dim3(256), FWD_LDS, s, hp, whh, g, cp, c, h, hT, ldhT, t, Bp, B, H);
+}
+void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* whhT, const float* up, const float* dcfi,
+                     const float* acts, const float* ct, const float* cp, float* dg, float* dcfo, float* dgT,
+                     long lddgT, int t, int Bp, int B, int H) {
+  if (step_variant() == 2)
+    hipLaunchKernelGGL(lstm_step_bwd_v2_kernel, grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp, dg,
+                       dcfo, dgT, lddgT, t, Bp, B, H);
+  else
+    hipLaunchKernelGGL(lstm_step_bwd_kernel, grid, dim3(256), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp, dg, dcfo,
+                       dgT, lddgT, t, Bp, B, H);
+}
+}  // namespace
+
+extern "C" int sv_lstm_step_fwd(const float* h_prev, const float* w_hh, float* gates_t, const float* c_prev,
+                                float* c_t, float* h_t, int B, int H, hipStream_t stream) {
+  if (!w_hh || !gates_t || !c_t || !h_t || B <= 0 || H <= 0 || H % 4) return SV_EARG;
+  const dim3 grid((H + FWD_U - 1) / FWD_U, (B + FWD_BM - 1) / FWD_BM);
+  launch_fwd_step(grid, stream, h_prev, w_hh, gates_t, c_prev, c_t, h_t, nullptr, 0L, 0, B, B, H);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
 extern "C" int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, const float* w_ih, const float* w_hh,
                                  const float* b_ih, const float* b_hh, float* gates, float* c_tm, float* h_tm,
-                                 hipStream_t stream) {
+                                 float* hT, hipStream_t stream) {
   if (!x_tm || !w_ih || !w_hh || !gates || !c_tm || !h_tm) return SV_EARG;
   if (!lstm_dims_ok(T, B, F, H)) return SV_ESHAPE;
   const long BH = (long)B * H, BG = 4L * B * H;
@@ -350,83 +673,96 @@ extern "C" int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, 
   if (rc) return rc;
   hipError_t e = hipMemsetAsync(h_tm, 0, BH * sizeof(float), stream);
   if (e != hipSuccess) return (int)e;
-  constexpr int LDS_MAIN = 2 * SV_BK * (TileLd<true, FWD_BM>::value + TileLd<true, 4 * FWD_U>::value);
-  constexpr int LDS_EPI = FWD_BM * (4 * FWD_U + 4);
-  constexpr int LDS = (LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI) * sizeof(float);
   const dim3 grid((H + FWD_U - 1) / FWD_U, (B + FWD_BM - 1) / FWD_BM);
+  const int Bp = (B + 3) & ~3;
+  const long ldhT = (long)(T + 1) * Bp;
+  if (hT && Bp != B) {  // zero the padding columns of the transposed layout
+    e = hipMemsetAsync(hT, 0, (size_t)H * ldhT * sizeof(float), stream);
+    if (e != hipSuccess) return (int)e;
+  }
   for (int t = 0; t < T; ++t) {
-    hipLaunchKernelGGL(lstm_step_fwd_kernel, grid, dim3(256), LDS, stream, t ? h_tm + t * BH : nullptr, w_hh,
-                       gates + t * BG, t ? c_tm + (t - 1) * BH : nullptr, c_tm + t * BH, h_tm + (t + 1) * BH, B, H);
+    launch_fwd_step(grid, stream, t ? h_tm + t * BH : nullptr, w_hh, gates + t * BG, t ? c_tm + (t - 1) * BH : nullptr,
+                    c_tm + t * BH, h_tm + (t + 1) * BH, hT, ldhT, t, Bp, B, H);
     SV_LAUNCH_CHECK();
   }
   return SV_OK;
 }
 
-// one forward recurrent step (K2) on its own: gates_t holds x_t W_ih^T + b on entry
-extern "C" int sv_lstm_step_fwd(const float* h_prev, const float* w_hh, float* gates_t, const float* c_prev,
-                                float* c_t, float* h_t, int B, int H, hipStream_t stream) {
-  if (!w_hh || !gates_t || !c_t || !h_t || B <= 0 || H <= 0 || H % 4) return SV_EARG;
-  constexpr int LDS_MAIN = 2 * SV_BK * (TileLd<true, FWD_BM>::value + TileLd<true, 4 * FWD_U>::value);
-  constexpr int LDS_EPI = FWD_BM * (4 * FWD_U + 4);
-  constexpr int LDS = (LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI) * sizeof(float);
-  const dim3 grid((H + FWD_U - 1) / FWD_U, (B + FWD_BM - 1) / FWD_BM);
-  hipLaunchKernelGGL(lstm_step_fwd_kernel, grid, dim3(256), LDS, stream, h_prev, w_hh, gates_t, c_prev, c_t, h_t, B, H);
-  SV_LAUNCH_CHECK();
-  return SV_OK;
+namespace {
+struct BwdWs {
+  float *dcf0, *dcf1, *whhT, *wihT, *gws;
+  size_t total;
+};
+size_t al4(size_t n) { return (n + 63) & ~size_t(63); }
+BwdWs carve_bwd(float* base, int T, int B, int F, int H) {
+  BwdWs w;
+  size_t off = 0;
+  auto take = [&](size_t n) {
+    float* p = base ? base + off : nullptr;
+    off += al4(n);
+    return p;
+  };
+  w.dcf0 = take((size_t)B * H);
+  w.dcf1 = take((size_t)B * H);
+  w.whhT = take((size_t)4 * H * H);
+  w.wihT = take((size_t)4 * H * F);
+  const int TBp = T * ((B + 3) & ~3);
+  size_t g = sv_gemm_f32_workspace(4 * H, H, TBp);
+  g = std::max(g, sv_gemm_f32_workspace(4 * H, F, TBp));
+  g = std::max(g, sv_gemm_f32_workspace(T * B, F, 4 * H));
+  w.gws = take((g + 3) / 4);
+  w.total = off * sizeof(float);
+  return w;
 }
+}  // namespace
 
-extern "C" size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H) {
-  size_t dcf = 2ull * B * H * sizeof(float);
-  size_t g1 = sv_gemm_f32_workspace(4 * H, H, T * B);
-  size_t g2 = sv_gemm_f32_workspace(4 * H, F, T * B);
-  size_t g3 = sv_gemm_f32_workspace(T * B, F, 4 * H);
-  size_t cs = sv_colsum_workspace(T * B, 4 * H);
-  size_t m = g1;
-  if (g2 > m) m = g2;
-  if (g3 > m) m = g3;
-  if (cs > m) m = cs;
-  return dcf + ((m + 255) & ~size_t(255));
-}
+extern "C" size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H) { return carve_bwd(nullptr, T, B, F, H).total; }
 
-extern "C" int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* x_tm, const float* w_ih, const float* w_hh,
-                                 const float* gates, const float* c_tm, const float* h_tm, const float* dh_up,
-                                 int dh_up_full, float* dgates, float* dx_tm, float* dw_ih, float* dw_hh,
-                                 float* db_ih, float* db_hh, float* workspace, hipStream_t stream) {
-  if (!x_tm || !w_ih || !w_hh || !gates || !c_tm || !h_tm || !dgates || !dw_ih || !dw_hh || !db_ih || !workspace)
+extern "C" int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* xT, long ld_xT, const float* w_ih,
+                                 const float* w_hh, const float* gates, const float* c_tm, const float* hT,
+                                 const float* dh_up, int dh_up_full, float* dgates, float* dgT, float* dx_tm,
+                                 float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, float* workspace,
+                                 hipStream_t stream) {
+  if (!xT || !w_ih || !w_hh || !gates || !c_tm || !hT || !dgates || !dgT || !dw_ih || !dw_hh || !db_ih || !workspace)
     return SV_EARG;
-  if (!lstm_dims_ok(T, B, F, H)) return SV_ESHAPE;
+  if (!lstm_dims_ok(T, B, F, H) || ld_xT % 4) return SV_ESHAPE;
   const long BH = (long)B * H, BG = 4L * B * H;
-  float* dcf0 = workspace;
-  float* dcf1 = workspace + BH;
-  float* gws = workspace + 2 * BH;
-  gws = (float*)(((uintptr_t)gws + 255) & ~uintptr_t(255));
-  constexpr int LDS_MAIN = 4 * 2 * SV_BK * (TileLd<true, BWD_BM>::value + TileLd<false, BWD_U>::value);
-  constexpr int LDS_RED = 4 * BWD_BM * (BWD_U + 1);
-  constexpr int LDS = (LDS_MAIN > LDS_RED ? LDS_MAIN : LDS_RED) * sizeof(float);
+  const int Bp = (B + 3) & ~3;
+  const int TB = T * B, TBp = T * Bp;
+  const BwdWs ws = carve_bwd(workspace, T, B, F, H);
+  int rc = sv_transpose(w_hh, H, 4 * H, H, ws.whhT, 4L * H, stream);  // W_hh^T [H, 4H]
+  if (rc) return rc;
   const dim3 grid((H + BWD_U - 1) / BWD_U, (B + BWD_BM - 1) / BWD_BM);
+  if (Bp != B) {
+    hipError_t e = hipMemsetAsync(dgT, 0, (size_t)4 * H * TBp * sizeof(float), stream);
+    if (e != hipSuccess) return (int)e;
+  }
   for (int t = T - 1; t >= 0; --t) {
     const float* up = nullptr;
     if (dh_up) up = dh_up_full ? dh_up + t * BH : (t == T - 1 ? dh_up : nullptr);
-    float* dcf_out = (t & 1) ? dcf1 : dcf0;
-    const float* dcf_in = (t == T - 1) ? nullptr : ((t & 1) ? dcf0 : dcf1);
-    hipLaunchKernelGGL(lstm_step_bwd_kernel, grid, dim3(256), LDS, stream, t == T - 1 ? nullptr : dgates + (t + 1) * BG,
-                       w_hh, up, dcf_in, gates + t * BG, c_tm + t * BH, t ? c_tm + (t - 1) * BH : nullptr,
-                       dgates + t * BG, dcf_out, B, H);
+    float* dcf_out = (t & 1) ? ws.dcf1 : ws.dcf0;
+    const float* dcf_in = (t == T - 1) ? nullptr : ((t & 1) ? ws.dcf0 : ws.dcf1);
+    launch_bwd_step(grid, stream, t == T - 1 ? nullptr : dgates + (t + 1) * BG, ws.whhT, up, dcf_in, gates + t * BG,
+                    c_tm + t * BH, t ? c_tm + (t - 1) * BH : nullptr, dgates + t * BG, dcf_out, dgT, (long)TBp, t, Bp,
+                    B, H);
     SV_LAUNCH_CHECK();
   }
-  const int TB = T * B;
-  // dW_hh = sum_t dG_t^T h_{t-1}   (A = dG as [K=TB][M=4H], B = h_tm[0..T-1] as [K=TB][N=H])
-  int rc = sv_gemm_f32(0, 0, 4 * H, H, TB, dgates, 4L * H, h_tm, H, dw_hh, H, nullptr, nullptr, 0.f, gws, stream);
+  const long ldhT = (long)(T + 1) * Bp;
+  // dW_hh = sum_t dG_t^T h_{t-1}: A = dG^T [4H, T Bp], B = hT[:, 0:T Bp] (column block t = h_{t-1})
+  rc = sv_gemm_f32(1, 1, 4 * H, H, TBp, dgT, TBp, hT, ldhT, dw_hh, H, nullptr, nullptr, 0.f, ws.gws, stream);
   if (rc) return rc;
-  // dW_ih = sum_t dG_t^T x_t
-  rc = sv_gemm_f32(0, 0, 4 * H, F, TB, dgates, 4L * H, x_tm, F, dw_ih, F, nullptr, nullptr, 0.f, gws, stream);
+  // dW_ih = sum_t dG_t^T x_t: B = x^T [F, T Bp]
+  rc = sv_gemm_f32(1, 1, 4 * H, F, TBp, dgT, TBp, xT, ld_xT, dw_ih, F, nullptr, nullptr, 0.f, ws.gws, stream);
   if (rc) return rc;
-  // db_ih = db_hh = sum_{t,b} dG
-  rc = colsum(dgates, TB, 4 * H, db_ih, db_hh, gws, stream);
-  if (rc) return rc;
-  // dx = dG W_ih  (A = dG [TB, 4H] k-contig, B = W_ih as [K=4H][N=F] n-contig)
+  // db_ih = db_hh = row sums of dG^T
+  hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(256), 0, stream, dgT, (long)TBp, TBp, db_ih, db_hh);
+  SV_LAUNCH_CHECK();
+  // dx = dG W_ih: A = dG [TB, 4H], B = W_ih^T [F, 4H]
   if (dx_tm) {
-    rc = sv_gemm_f32(1, 0, TB, F, 4 * H, dgates, 4L * H, w_ih, F, dx_tm, F, nullptr, nullptr, 0.f, gws, stream);
+    rc = sv_transpose(w_ih, F, 4 * H, F, ws.wihT, 4L * H, stream);
+    if (rc) return rc;
+    rc = sv_gemm_f32(1, 1, TB, F, 4 * H, dgates, 4L * H, ws.wihT, 4L * H, dx_tm, F, nullptr, nullptr, 0.f, ws.gws,
+                     stream);
     if (rc) return rc;
   }
   return SV_OK;

@@ -31,6 +31,8 @@ class EmbedderState:
         self.gates = []     # per layer [T,B,4H] activated i,f,g,o
         self.c_tm = []      # per layer [T,B,H]
         self.h_tm = []      # per layer [T+1,B,H]
+        self.hT = []        # per layer [H,(T+1)B]  (h^T, column block t+1 = h_t, block 0 = 0)
+        self.xT0 = None     # layer-0 input transposed [F, T*B]
         self.y = self.emb = self.ynorm = self.h_last = None
         self.T = self.B = self.H = self.P = 0
 
@@ -48,19 +50,30 @@ def embedder_forward(x, layers, w_p, b_p, save=True):
     st.T, st.B, st.H, st.P = T, B, H, P
     x_tm = torch.empty((T, B, F), dtype=torch.float32, device=dev)
     call("sv_frames_to_time_major", ptr(x), ptr(x_tm), B, T, F, s)
+    Bp = (B + 3) // 4 * 4
+    if save:  # layer-0 input transposed, [F, T*Bp] (column block t = x_t^T, padding columns zero)
+        if Bp == B:
+            st.xT0 = torch.empty((F, T * B), dtype=torch.float32, device=dev)
+            call("sv_transpose", ptr(x_tm), F, T * B, F, ptr(st.xT0), T * B, s)
+        else:
+            st.xT0 = torch.zeros((F, T * Bp), dtype=torch.float32, device=dev)
+            for t in range(T):
+                call("sv_transpose", ptr(x_tm[t]), F, B, F, ptr(st.xT0) + 4 * t * Bp, T * Bp, s)
     inp = x_tm
     for (w_ih, w_hh, b_ih, b_hh) in layers:
         Fl = inp.shape[2]
         gates = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
         c_tm = torch.empty((T, B, H), dtype=torch.float32, device=dev)
         h_tm = torch.empty((T + 1, B, H), dtype=torch.float32, device=dev)
+        hT = torch.empty((H, (T + 1) * Bp), dtype=torch.float32, device=dev) if save else None
         call("sv_lstm_layer_fwd", ptr(inp), T, B, Fl, H, ptr(w_ih), ptr(w_hh), ptr(b_ih), ptr(b_hh), ptr(gates),
-             ptr(c_tm), ptr(h_tm), s)
+             ptr(c_tm), ptr(h_tm), ptr(hT), s)
         if save:
             st.x_tm.append(inp)
             st.gates.append(gates)
             st.c_tm.append(c_tm)
             st.h_tm.append(h_tm)
+            st.hT.append(hT)
         inp = h_tm[1:]
     h_last = inp[T - 1]
     y = torch.empty((B, P), dtype=torch.float32, device=dev)
@@ -94,6 +107,8 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False):
     Fmax = max(st.x_tm[l].shape[2] for l in range(L))
     ws = _ws(lib().sv_lstm_layer_bwd_workspace(T, B, Fmax, H), dev)
     dgates = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
+    Bp = (B + 3) // 4 * 4
+    dgT = torch.empty((4 * H, T * Bp), dtype=torch.float32, device=dev)
     dh_up, full = dh_last, 0
     dx_out = None
     for l in range(L - 1, -1, -1):
@@ -101,8 +116,12 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False):
         Fl = st.x_tm[l].shape[2]
         want_dx = l > 0 or need_dx
         dx = torch.empty((T, B, Fl), dtype=torch.float32, device=dev) if want_dx else None
-        call("sv_lstm_layer_bwd", T, B, Fl, H, ptr(st.x_tm[l]), ptr(w_ih), ptr(w_hh), ptr(st.gates[l]),
-             ptr(st.c_tm[l]), ptr(st.h_tm[l]), ptr(dh_up), full, ptr(dgates), ptr(dx), ptr(grads[4 * l]),
+        if l == 0:
+            xT, ld_xT = ptr(st.xT0), T * Bp
+        else:  # previous layer's h^T, column blocks 1..T (= h_0 .. h_{T-1})
+            xT, ld_xT = ptr(st.hT[l - 1]) + Bp * 4, (T + 1) * Bp
+        call("sv_lstm_layer_bwd", T, B, Fl, H, xT, ld_xT, ptr(w_ih), ptr(w_hh), ptr(st.gates[l]),
+             ptr(st.c_tm[l]), ptr(st.hT[l]), ptr(dh_up), full, ptr(dgates), ptr(dgT), ptr(dx), ptr(grads[4 * l]),
              ptr(grads[4 * l + 1]), ptr(grads[4 * l + 2]), ptr(grads[4 * l + 3]), ptr(ws), s)
         dh_up, full = dx, 1
         if l == 0:

@@ -44,7 +44,8 @@ def test_c_abi_library_exports_every_header_symbol():
     # workspace queries are host-only and callable without a GPU
     assert h.sv_ge2e_workspace_size(64, 10, 256, 64) > 0
     assert h.sv_lstm_layer_bwd_workspace(160, 640, 768, 768) > 0
-    assert h.sv_gemm_f32_workspace(3072, 768, 102400) == 4 * 3072 * 768 * 4
+    ws = h.sv_gemm_f32_workspace(3072, 768, 102400)  # split-K slabs
+    assert ws > 0 and ws % (3072 * 768 * 4) == 0
 
 
 def test_library_binds_torch_hip_runtime():
