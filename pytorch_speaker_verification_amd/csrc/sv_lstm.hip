@@ -356,6 +356,7 @@ __global__ __launch_bounds__(256) void lstm_step_bwd_kernel(
 //         accumulator each, all sharing the same staged A/B tiles.
 //   K3v2: 4 groups of 2 waves, group = gate (its K range of W_hh^T), waves split the rows.
 // ============================================================================
+template <int BKX>
 __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __restrict__ hprev,
                                                                const float* __restrict__ whh,
                                                                float* __restrict__ gates,
@@ -365,33 +366,45 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
                                                                int H) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int BN = 4 * FWD_U, LDP = BN + 4, LDH = FWD_BM + 1;
+  constexpr int PER = FWD_BM * FWD_U / 512;  // epilogue elements per thread
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int j0 = blockIdx.x * FWD_U, b0 = blockIdx.y * FWD_BM;
   const int wm0 = (w >> 2) * 32, wn0 = (w & 3) * 32;
+  const long G = 4L * H;
+  // the epilogue's inputs do not depend on the GEMM: issue their loads first
+  float xg[PER][4], cpv[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + 512 * k, b = e / FWD_U, u = e % FWD_U;
+    const int gb = b0 + b, gj = j0 + u;
+    const bool ok = gb < B && gj < H;
+    const float* gp = gates + (long)gb * G + gj;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xg[k][q] = ok ? gp[q * H] : 0.f;
+    cpv[k] = (ok && cprev) ? cprev[(long)gb * H + gj] : 0.f;
+  }
   f32x16 acc[1][1];
   zero_acc(acc);
   if (hprev)
-    gemm_mainloop_km<FWD_BM, BN, 512, SV_BKM, 1, 1>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
-                                                    RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc);
+    gemm_mainloop_km<FWD_BM, BN, 512, BKX, 1, 1>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
+                                                 RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc);
   float* pre = lds;
   float* hs = lds + FWD_BM * LDP;
 #pragma unroll
   for (int r = 0; r < 16; ++r) pre[(wm0 + acc_row(r, lane)) * LDP + wn0 + (lane & 31)] = acc[0][0][r];
   __syncthreads();
-  const long G = 4L * H;
-  for (int e = tid; e < FWD_BM * FWD_U; e += 512) {
-    const int b = e / FWD_U, u = e % FWD_U;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + 512 * k, b = e / FWD_U, u = e % FWD_U;
     const int gb = b0 + b, gj = j0 + u;
     if (gb >= B || gj >= H) continue;
     float* gp = gates + (long)gb * G + gj;
     const float* pr = pre + b * LDP + u;
-    const float pi = pr[0] + gp[0];
-    const float pf = pr[FWD_U] + gp[H];
-    const float pg = pr[2 * FWD_U] + gp[2 * H];
-    const float po = pr[3 * FWD_U] + gp[3 * H];
-    const float i = sv_sigmoid(pi), f = sv_sigmoid(pf), g = tanhf(pg), o = sv_sigmoid(po);
-    const float cp = cprev ? cprev[(long)gb * H + gj] : 0.f;
-    const float c = f * cp + i * g;
+    const float i = sv_sigmoid(pr[0] + xg[k][0]);
+    const float f = sv_sigmoid(pr[FWD_U] + xg[k][1]);
+    const float g = tanhf(pr[2 * FWD_U] + xg[k][2]);
+    const float o = sv_sigmoid(pr[3 * FWD_U] + xg[k][3]);
+    const float c = f * cpv[k] + i * g;
     const float h = o * tanhf(c);
     gp[0] = i;
     gp[H] = f;
@@ -422,10 +435,27 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
   constexpr int GBUF = 2 * (BWD_BM + BWD_U) * (SV_BKM + 4);
   constexpr int LDR = BWD_U + 1;
   constexpr int LDT = BWD_BM + 1;
+  constexpr int PER = BWD_BM * BWD_U / 512;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int gate = w >> 1, gt = tid & 127;
   const int j0 = blockIdx.x * BWD_U, b0 = blockIdx.y * BWD_BM;
   const long G = 4L * H;
+  // prefetch the epilogue's element-wise inputs (independent of the GEMM)
+  float av[PER][4], cv[PER], cpv[PER], dcfv[PER], upv[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + 512 * k, b = e / BWD_U, u = e % BWD_U;
+    const int gb = b0 + b, gj = j0 + u;
+    const bool ok = gb < B && gj < H;
+    const long hi = (long)gb * H + gj;
+    const float* ap = acts + (long)gb * G + gj;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) av[k][q] = ok ? ap[q * H] : 0.f;
+    cv[k] = ok ? c_t[hi] : 0.f;
+    cpv[k] = (ok && c_prev) ? c_prev[hi] : 0.f;
+    dcfv[k] = (ok && dcf_next) ? dcf_next[hi] : 0.f;
+    upv[k] = (ok && dhup) ? dhup[hi] : 0.f;
+  }
   f32x16 acc[1][1];
   zero_acc(acc);
   if (dgnext)
@@ -439,8 +469,9 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
   for (int r = 0; r < 16; ++r)
     red[(gate * BWD_BM + (w & 1) * 32 + acc_row(r, lane)) * LDR + (lane & 31)] = acc[0][0][r];
   __syncthreads();
-  for (int e = tid; e < BWD_BM * BWD_U; e += 512) {
-    const int b = e / BWD_U, u = e % BWD_U;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + 512 * k, b = e / BWD_U, u = e % BWD_U;
     const int gb = b0 + b, gj = j0 + u;
     if (gb >= B || gj >= H) continue;
     const long hi = (long)gb * H + gj;
@@ -448,15 +479,11 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
     dh += red[(1 * BWD_BM + b) * LDR + u];
     dh += red[(2 * BWD_BM + b) * LDR + u];
     dh += red[(3 * BWD_BM + b) * LDR + u];
-    if (dhup) dh += dhup[hi];
-    const float* ap = acts + (long)gb * G + gj;
-    const float i = ap[0], f = ap[H], g = ap[2 * H], o = ap[3 * H];
-    const float c = c_t[hi];
-    const float tc = tanhf(c);
-    float dc = dh * o * (1.f - tc * tc);
-    if (dcf_next) dc += dcf_next[hi];
-    const float cp = c_prev ? c_prev[hi] : 0.f;
-    const float d0 = dc * g * i * (1.f - i), d1 = dc * cp * f * (1.f - f);
+    dh += upv[k];
+    const float i = av[k][0], f = av[k][1], g = av[k][2], o = av[k][3];
+    const float tc = tanhf(cv[k]);
+    const float dc = dh * o * (1.f - tc * tc) + dcfv[k];
+    const float d0 = dc * g * i * (1.f - i), d1 = dc * cpv[k] * f * (1.f - f);
     const float d2 = dc * i * (1.f - g * g), d3 = dh * tc * o * (1.f - o);
     float* dp = dg + (long)gb * G + gj;
     dp[0] = d0;
@@ -626,25 +653,29 @@ constexpr int BWD_LDS_MAIN = 4 * 2 * (BWD_BM + BWD_U) * (SV_BKM + 4);
 constexpr int BWD_LDS_EPI = 4 * BWD_BM * (BWD_U + 1) + 4 * BWD_U * (BWD_BM + 1);
 constexpr int BWD_LDS = (BWD_LDS_MAIN > BWD_LDS_EPI ? BWD_LDS_MAIN : BWD_LDS_EPI) * (int)sizeof(float);
 // step-kernel variant: 2 = 8-wave (default), 1 = 4-wave; SV_STEP_VARIANT overrides (A/B timing)
+constexpr int FWD_LDS64 = 2 * (FWD_BM + 4 * FWD_U) * (64 + 4) * (int)sizeof(float);
 int step_variant() {
   static int v = [] {
     const char* e = getenv("SV_STEP_VARIANT");
-    return (e && *e == '1') ? 1 : 2;
+    return (e && (*e == '1' || *e == '3')) ? *e - '0' : 2;
   }();
   return v;
 }
 void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh, float* g, const float* cp, float* c,
                      float* h, float* hT, long ldhT, int t, int Bp, int B, int H) {
   if (step_variant() == 2)
-    hipLaunchKernelGGL(lstm_step_fwd_v2_kernel, grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT, ldhT, t, Bp, B,
-                       H);
+    hipLaunchKernelGGL(lstm_step_fwd_v2_kernel<SV_BKM>, grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT, ldhT, t,
+                       Bp, B, H);
+  else if (step_variant() == 3)
+    hipLaunchKernelGGL(lstm_step_fwd_v2_kernel<64>, grid, dim3(512), FWD_LDS64, s, hp, whh, g, cp, c, h, hT, ldhT, t,
+                       Bp, B, H);
   else
     hipLaunchKernelGGL(lstm_step_fwd_kernel, grid, dim3(256), FWD_LDS, s, hp, whh, g, cp, c, h, hT, ldhT, t, Bp, B, H);
 }
 void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* whhT, const float* up, const float* dcfi,
                      const float* acts, const float* ct, const float* cp, float* dg, float* dcfo, float* dgT,
                      long lddgT, int t, int Bp, int B, int H) {
-  if (step_variant() == 2)
+  if (step_variant() >= 2)
     hipLaunchKernelGGL(lstm_step_bwd_v2_kernel, grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp, dg,
                        dcfo, dgT, lddgT, t, Bp, B, H);
   else

@@ -61,6 +61,20 @@ class HipShardKernels:
         return dE
 
 
+def all_gather_rows(x, rank, world, group=None):
+    """Concatenate every rank's x [n, ...] along dim 0.  RCCL/NCCL: all_gather_into_tensor;
+    backends without a device all-gather (gloo with GPU tensors) get the equivalent SUM
+    all-reduce of a zero-padded buffer."""
+    n = x.shape[0]
+    out = x.new_zeros((n * world,) + tuple(x.shape[1:]))
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    else:
+        out[rank * n:(rank + 1) * n].copy_(x)
+        dist.all_reduce(out, group=group)
+    return out
+
+
 class ShardedGE2E:
     def __init__(self, kernels=None, group=None):
         self.k = kernels if kernels is not None else HipShardKernels()
@@ -78,8 +92,7 @@ class ShardedGE2E:
         s0 = Nl * self.rank
         ssum_local = self.k.speaker_sums(E_local)
         if self.world > 1:
-            ssum_all = ssum_local.new_empty((N, D))
-            dist.all_gather_into_tensor(ssum_all, ssum_local, group=self.group)
+            ssum_all = all_gather_rows(ssum_local, self.rank, self.world, self.group)
         else:
             ssum_all = ssum_local
         loss, per, st = self.k.fwd_rows(E_local, s0, N, ssum_all, w, b)

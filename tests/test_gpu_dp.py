@@ -1,0 +1,73 @@
+"""Data-parallel training step on the real kernels: 2 ranks (gloo, both on cuda:0 -- the GPU
+box has one GPU; RCCL needs one GPU per rank) each owning half the speakers must
+reproduce the single-process step on the whole batch (SURVEY §8e exact-parity partitioning)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import recipe
+from conftest import model_dims
+
+pytestmark = pytest.mark.gpu
+DIMS = (40, 64, 2, 32)
+NL, M, T, STEPS = 3, 4, 12, 2
+
+
+def _model():
+    from pytorch_speaker_verification_amd.speech_embedder_net import GE2ELoss, SpeechEmbedder
+    with model_dims(*DIMS):
+        net = SpeechEmbedder()
+    sd = recipe.make_weights(99, *DIMS, scale=3.0)
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    return net.to("cuda:0"), GE2ELoss("cuda:0")
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+        net, ge2e = _model()
+        x = torch.tensor(recipe.make_frames(5, world * NL * M, T, DIMS[0]), device="cuda:0")
+        xl = x[rank * NL * M:(rank + 1) * NL * M].contiguous()
+        tr = GE2ETrainer(net, ge2e, lr=0.01)
+        losses = [float(tr.step(xl, NL, M)) for _ in range(STEPS)]
+        q.put((rank, losses, {k: v.cpu().numpy() for k, v in net.state_dict().items()},
+               [ge2e.w.item(), ge2e.b.item()]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_two_ranks_equal_single_process():
+    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+    world = 2
+    net, ge2e = _model()
+    x = torch.tensor(recipe.make_frames(5, world * NL * M, T, DIMS[0]), device="cuda:0")
+    tr = GE2ETrainer(net, ge2e, lr=0.01)
+    ref_losses = [float(tr.step(x, world * NL, M)) for _ in range(STEPS)]
+    ref_sd = {k: v.cpu().numpy() for k, v in net.state_dict().items()}
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, losses, sd, wb in res:
+        np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
+        for k in ref_sd:
+            np.testing.assert_allclose(sd[k], ref_sd[k], atol=1e-5, err_msg=k)
+        np.testing.assert_allclose(wb, [ge2e.w.item(), ge2e.b.item()], atol=1e-6)
