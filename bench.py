@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 MI355X_FP32_MFMA_TFLOPS = 157.3   # /opt/skills/guides/MI355X_MICROARCH.md, chip-level table
 MI355X_HBM_GBPS = 8000.0
+MI355X_BF16_MFMA_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 
 
 def step_flops(B, T, F, H, P, L):
@@ -113,6 +114,7 @@ def main():
     ap.add_argument("--T", type=int, default=160)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fwd-steps", type=int, default=5)
+    ap.add_argument("--no-bf16", action="store_true", help="skip the config-c3 (bf16 operands) side measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,6 +191,30 @@ def main():
         "step_tflops": round(st_fl / (ms_step * 1e-3) / 1e12, 2),
         "step_mfma_frac": round(st_fl / (ms_step * 1e-3) / 1e12 / MI355X_FP32_MFMA_TFLOPS, 4),
     }
+    if not args.no_bf16:
+        # BASELINE config c3: same workload, bf16 GEMM operands (fp32 accumulate/state/loss)
+        net16, ge16 = build_model(dims, dev)
+        net16.precision = "bf16"
+        tr16 = GE2ETrainer(net16, ge16, lr=0.01)
+        for _ in range(args.warmup):
+            tr16.step(x, N, M)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            l16 = tr16.step(x, N, M)
+        barrier()
+        d16 = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([d16], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            d16 = float(t)
+        ms16 = d16 / args.steps * 1e3
+        out["bf16"] = {"config": "c3: same workload, bf16 GEMM operands, fp32 accumulate/state/loss",
+                       "value": round(world * B * args.steps / d16, 3), "unit": "embeddings/s",
+                       "ms_per_step": round(ms16, 3), "steps_per_sec": round(args.steps / d16, 4),
+                       "loss": round(float(l16), 5),
+                       "step_tflops": round(st_fl / (ms16 * 1e-3) / 1e12, 2),
+                       "step_mfma_frac": round(st_fl / (ms16 * 1e-3) / 1e12 / MI355X_BF16_MFMA_TFLOPS, 4)}
     if rank == 0:
         ms_k, fl_k = time_step_kernel(B, dims[1], dev)
         ach = fl_k / (ms_k * 1e-3) / 1e12

@@ -56,6 +56,12 @@ int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, const float
  * activated gates; h_prev / c_prev may be NULL (t = 0). */
 int sv_lstm_step_fwd(const float* h_prev, const float* w_hh, float* gates_t, const float* c_prev, float* c_t,
                      float* h_t, int B, int H, hipStream_t stream);
+/* one backward recurrent step (K3): dg_t [B,4H] = dL/d(gates_t) from dg_next [B,4H] (NULL at
+ * t = T-1), W_hh^T [H,4H], dh_up [B,H] (may be NULL), dcf_next = dc_{t+1} f_{t+1} (may be NULL),
+ * the activated gates, c_t, c_{t-1} (NULL at t = 0); writes dcf_t = dc_t f_t. */
+int sv_lstm_step_bwd(const float* dg_next, const float* w_hhT, const float* dh_up, const float* dcf_next,
+                     const float* acts_t, const float* c_t, const float* c_prev, float* dg_t, float* dcf_t, int B,
+                     int H, hipStream_t stream);
 size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H);
 /* xT: the layer input transposed, [F, >= T*Bp] with row stride ld_xT (layer 0: the frames;
  * layer l > 0: hT of layer l-1 offset by Bp columns).  hT: this layer's [H, (T+1)Bp] from the fwd.
@@ -104,6 +110,31 @@ size_t sv_ge2e_cossim_workspace(int N, int M, int D, int Nc);
 int sv_ge2e_cossim(const float* E, int N, int M, int D, const float* C, int Nc, float* cos, float* workspace,
                    hipStream_t stream);
 int sv_ge2e_calc_loss(const float* S, int N, int M, int K, float* per, float* loss, hipStream_t stream);
+
+/* ---- bf16-operand variant (BASELINE config c3, mixed precision) ------------------------------
+ * GEMM operands (weights, h, dgates) in bf16 (RNE casts), v_mfma_f32_32x32x16_bf16 with fp32
+ * accumulation; gates/cell state/biases/gradients/outputs fp32.  Same layouts as the fp32 entry
+ * points, except transposed layouts use column blocks of Bp = (B + 7) & ~7 and F, H, K and every
+ * bf16 leading dimension must be multiples of 8.  sv_bf16 = raw bf16 bits. */
+typedef unsigned short sv_bf16;
+size_t sv_gemm_bf16_workspace(int M, int N, int K);
+/* C[M,N] (fp32) = A[M,K] . B[N,K]^T (+ bias0 + bias1) (+ beta C); both operands k-contiguous */
+int sv_gemm_bf16(int M, int N, int K, const sv_bf16* A, long lda, const sv_bf16* B, long ldb, float* C, long ldc,
+                 const float* bias0, const float* bias1, float beta, float* workspace, hipStream_t stream);
+int sv_cast_bf16(const float* x, sv_bf16* y, long n, hipStream_t stream);
+int sv_transpose_cast_bf16(const float* src, long ld_src, int R, int C, sv_bf16* dst, long ld_dst,
+                           hipStream_t stream);
+/* x_bf [T,B,F]; writes gates/c_tm/h_tm (fp32) plus h_bf [T+1,B,H] and hT [H,(T+1)Bp] (bf16) */
+int sv_lstm_layer_fwd_bf16(const sv_bf16* x_bf, int T, int B, int F, int H, const sv_bf16* w_ih_bf,
+                           const sv_bf16* w_hh_bf, const float* b_ih, const float* b_hh, float* gates, float* c_tm,
+                           float* h_tm, sv_bf16* h_bf, sv_bf16* hT, hipStream_t stream);
+size_t sv_lstm_layer_bwd_bf16_workspace(int T, int B, int F, int H);
+/* wihT_bf [F,4H], whhT_bf [H,4H]; dg_bf [T,B,4H] and dgT_bf [4H,T*Bp] are bf16 outputs */
+int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const sv_bf16* xT_bf, long ld_xT, const sv_bf16* wihT_bf,
+                           const sv_bf16* whhT_bf, const float* gates, const float* c_tm, const sv_bf16* hT_bf,
+                           const float* dh_up, int dh_up_full, sv_bf16* dg_bf, sv_bf16* dgT_bf, float* dx_tm,
+                           float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, float* workspace,
+                           hipStream_t stream);
 
 /* ---- clip_grad_norm_ + SGD step over one flat parameter group (train_speech_embedder.py:63-65)
  * p -= lr * min(1, max_norm / (|g|_2 + 1e-6)) * g; write_grad=1 also scales g in place. */

@@ -33,6 +33,7 @@ SIGNATURES = {
     "sv_transpose": (_c_int, [_P, _c_long, _c_int, _c_int, _P, _c_long, _P]),
     "sv_lstm_layer_fwd": (_c_int, [_P, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_lstm_step_fwd": (_c_int, [_P, _P, _P, _P, _P, _P, _c_int, _c_int, _P]),
+    "sv_lstm_step_bwd": (_c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _P]),
     "sv_lstm_layer_bwd_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
     "sv_lstm_layer_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _P, _c_long, _P, _P, _P, _P, _P, _P, _c_int, _P,
                                    _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -50,6 +51,15 @@ SIGNATURES = {
     "sv_ge2e_cossim_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
     "sv_ge2e_cossim": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _c_int, _P, _P, _P]),
     "sv_ge2e_calc_loss": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _P, _P]),
+    "sv_gemm_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int]),
+    "sv_gemm_bf16": (_c_int, [_c_int, _c_int, _c_int, _P, _c_long, _P, _c_long, _P, _c_long, _P, _P, _c_float, _P,
+                              _P]),
+    "sv_cast_bf16": (_c_int, [_P, _P, _c_long, _P]),
+    "sv_transpose_cast_bf16": (_c_int, [_P, _c_long, _c_int, _c_int, _P, _c_long, _P]),
+    "sv_lstm_layer_fwd_bf16": (_c_int, [_P, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "sv_lstm_layer_bwd_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
+    "sv_lstm_layer_bwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _P, _c_long, _P, _P, _P, _P, _P, _P, _c_int,
+                                        _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_clip_sgd_workspace": (_c_size_t, []),
     "sv_clip_sgd_step": (_c_int, [_P, _P, _c_long, _c_float, _c_float, _c_int, _P, _P, _P]),
 }

@@ -1,0 +1,599 @@
+// bf16-operand variant of the LSTM stack (BASELINE config c3: "gate GEMMs on MFMA", mixed
+// precision).  GEMM operands (weights, h, dgates) are bf16 and feed v_mfma_f32_32x32x16_bf16
+// with fp32 accumulation; cell state, activations, biases, gradients, the projection, the
+// GE2E loss and the optimizer stay fp32.  Same algorithm, layouts and epilogues
+// as sv_lstm.hip; transposed layouts use column blocks of Bp = B rounded up to 8 so every
+// bf16 row stays 16-byte aligned.
+#include <algorithm>
+#include <stdlib.h>
+#include "sv_common.h"
+#include "sv_gemm.h"
+#include "../../include/sv_ge2e.h"
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned short bf16_t;  // storage type across the C ABI
+
+#define BBK 64  // k-tile (bf16 elements)
+
+__device__ __forceinline__ f32x16 mfma_bf16(bf16x8_t a, bf16x8_t b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// k-major bf16 tile: element (r,k) at base[row(r)*ld + k]; LDS [R][BK+8] (144-B rows: a 16-lane
+// group's ds_read_b128 of 16 distinct rows is conflict-free).  One 16-B chunk = 8 k per load.
+template <int R, int NT, int BK>
+struct BTileStage {
+  static constexpr int LD = BK + 8;
+  static constexpr int C8 = BK / 8;
+  static constexpr int NV = (R * C8) / NT;
+  static_assert(NV >= 1 && NV * NT == R * C8, "tile/thread mismatch");
+  uint4 v[NV];
+  template <class Map>
+  __device__ __forceinline__ void load(const bf16_t* __restrict__ base, long ld, const Map& map, int k0, int K,
+                                       int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int q = tid + NT * i;
+      const int r = q / C8, c = (q % C8) * 8;
+      uint4 x = {0u, 0u, 0u, 0u};
+      if (map.valid(r) && k0 + c < K) x = *reinterpret_cast<const uint4*>(base + (long)map(r) * ld + k0 + c);
+      v[i] = x;
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int q = tid + NT * i;
+      *reinterpret_cast<uint4*>(lds + (q / C8) * LD + (q % C8) * 8) = v[i];
+    }
+  }
+};
+
+// lane (r = l&31, h = l>>5) supplies A[r][16s + 8h + j] / B[16s + 8h + j][r], j = 0..7
+template <int TM, int TN, int BK, int LD>
+__device__ __forceinline__ void mfma_ktile_bf(const bf16_t* As, const bf16_t* Bs, int wm0, int wn0, int lane,
+                                              f32x16 (&acc)[TM][TN]) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < BK / 16; ++s) {
+    bf16x8_t a[TM], b[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8_t*>(As + (wm0 + 32 * i + r) * LD + 16 * s + 8 * h);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8_t*>(Bs + (wn0 + 32 * j + r) * LD + 16 * s + 8 * h);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(a[i], b[j], acc[i][j]);
+  }
+}
+
+// lds must hold 2 * (BM + BN) * (BK + 8) bf16
+template <int BM, int BN, int NT, int BK, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_bf(const bf16_t* __restrict__ A, long lda, const MapA& mapA,
+                                                 const bf16_t* __restrict__ B, long ldb, const MapB& mapB, int kbeg,
+                                                 int kend, bf16_t* lds, int tid, int wm0, int wn0,
+                                                 f32x16 (&acc)[TM][TN]) {
+  using SA = BTileStage<BM, NT, BK>;
+  using SB = BTileStage<BN, NT, BK>;
+  constexpr int LD = BK + 8;
+  constexpr int BUF = (BM + BN) * LD;
+  const int lane = tid & 63;
+  SA sa;
+  SB sb;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk <= 0) return;
+  sa.load(A, lda, mapA, kbeg, kend, tid);
+  sb.load(B, ldb, mapB, kbeg, kend, tid);
+  sa.store(lds, tid);
+  sb.store(lds + BM * LD, tid);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    bf16_t* cur = lds + (kt & 1) * BUF;
+    bf16_t* nxt = lds + ((kt + 1) & 1) * BUF;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      sa.load(A, lda, mapA, kbeg + (kt + 1) * BK, kend, tid);
+      sb.load(B, ldb, mapB, kbeg + (kt + 1) * BK, kend, tid);
+    }
+    mfma_ktile_bf<TM, TN, BK, LD>(cur, cur + BM * LD, wm0, wn0, lane, acc);
+    if (more) {
+      sa.store(nxt, tid);
+      sb.store(nxt + BM * LD, tid);
+    }
+    __syncthreads();
+  }
+}
+
+// Register-prefetch main loop for the latency-bound recurrent steps: every global load of a
+// super-chunk of SC k-tiles is issued up front (one HBM/L2 round trip per super-chunk instead
+// of one per k-tile), then the tiles are staged through two LDS buffers, one barrier each.
+template <int BM, int BN, int NT, int SC, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_bf_rp(const bf16_t* __restrict__ A, long lda, const MapA& mapA,
+                                                    const bf16_t* __restrict__ B, long ldb, const MapB& mapB,
+                                                    int kbeg, int kend, bf16_t* lds, int tid, int wm0, int wn0,
+                                                    f32x16 (&acc)[TM][TN]) {
+  using SA = BTileStage<BM, NT, BBK>;
+  using SB = BTileStage<BN, NT, BBK>;
+  constexpr int LD = BBK + 8;
+  constexpr int BUF = (BM + BN) * LD;
+  const int lane = tid & 63;
+  const int nk = (kend - kbeg + BBK - 1) / BBK;
+  int it = 0;
+  for (int c0 = 0; c0 < nk; c0 += SC) {
+    SA sa[SC];
+    SB sb[SC];
+#pragma unroll
+    for (int j = 0; j < SC; ++j) {
+      if (c0 + j < nk) {
+        sa[j].load(A, lda, mapA, kbeg + (c0 + j) * BBK, kend, tid);
+        sb[j].load(B, ldb, mapB, kbeg + (c0 + j) * BBK, kend, tid);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < SC; ++j) {
+      if (c0 + j < nk) {
+        bf16_t* buf = lds + (it & 1) * BUF;
+        sa[j].store(buf, tid);
+        sb[j].store(buf + BM * LD, tid);
+        __syncthreads();
+        mfma_ktile_bf<TM, TN, BBK, LD>(buf, buf + BM * LD, wm0, wn0, lane, acc);
+        ++it;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ bf16_t to_bf(float x) {
+  const __bf16 b = (__bf16)x;
+  return *reinterpret_cast<const bf16_t*>(&b);
+}
+
+// ============================================================================
+// GEMM: C[M,N] fp32 = A[M,K] . B[N,K]^T (bf16, both k-contiguous) (+bias) / split-K slabs
+// ============================================================================
+enum { BEPI_STORE = 0, BEPI_SLAB = 1 };
+
+template <int BM, int BN, int EPI>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict__ A, long lda,
+                                                        const bf16_t* __restrict__ B, long ldb, float* __restrict__ C,
+                                                        long ldc, long slab, int M, int N, int K, int kchunk,
+                                                        const float* __restrict__ bias0,
+                                                        const float* __restrict__ bias1, float beta) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t ldsb[];
+  constexpr int TM = BM / 64, TN = BN / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_m * ((N + BN - 1) / BN);
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int tm = id % tiles_m, tn = id / tiles_m;
+  const int kbeg = blockIdx.y * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  const int wm0 = (w >> 1) * (BM / 2), wn0 = (w & 1) * (BN / 2);
+  f32x16 acc[TM][TN];
+  zero_acc(acc);
+  gemm_mainloop_bf<BM, BN, 256, BBK, TM, TN>(A, lda, RowMapLinear{tm * BM, M}, B, ldb, RowMapLinear{tn * BN, N}, kbeg,
+                                             kend, ldsb, tid, wm0, wn0, acc);
+  float* Cz = C + (EPI == BEPI_SLAB ? (long)blockIdx.y * slab : 0);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = tn * BN + wn0 + 32 * j + (lane & 31);
+      if (col >= N) continue;
+      float badd = 0.f;
+      if (EPI == BEPI_STORE) {
+        if (bias0) badd += bias0[col];
+        if (bias1) badd += bias1[col];
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = tm * BM + wm0 + 32 * i + acc_row(r, lane);
+        if (row >= M) continue;
+        float v = acc[i][j][r];
+        float* dst = Cz + (long)row * ldc + col;
+        if (EPI == BEPI_STORE) {
+          v += badd;
+          if (beta != 0.f) v += beta * *dst;
+        }
+        *dst = v;
+      }
+    }
+}
+
+__global__ void slab_reduce_bf_kernel(const float* __restrict__ slab, int nz, long zstride, float* __restrict__ out,
+                                      long ldc, int M, int N, float beta, const float* __restrict__ bias0,
+                                      const float* __restrict__ bias1) {
+  const long total = (long)M * N;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int row = (int)(e / N), col = (int)(e % N);
+    float s = 0.f;
+    for (int z = 0; z < nz; ++z) s += slab[z * zstride + e];
+    if (bias0) s += bias0[col];
+    if (bias1) s += bias1[col];
+    float* dst = out + (long)row * ldc + col;
+    *dst = (beta != 0.f ? beta * *dst : 0.f) + s;
+  }
+}
+
+// x (fp32, n) -> y (bf16)
+__global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) y[i] = to_bf(x[i]);
+}
+
+// dst[c*ldd + r] = bf16(src[r*lds + c])
+__global__ __launch_bounds__(256) void transpose_cast_kernel(const float* __restrict__ src, long lds_, int R, int C,
+                                                             bf16_t* __restrict__ dst, long ldd) {
+  __shared__ float tile[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? src[(long)r * lds_ + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) dst[(long)c * ldd + r] = to_bf(tile[tx][i]);
+  }
+}
+
+// row sums of a bf16 matrix, fp32 accumulation, one block per row, fixed order
+__global__ __launch_bounds__(256) void rowsum_bf16_kernel(const bf16_t* __restrict__ X, long ld, int C,
+                                                          float* __restrict__ out0, float* __restrict__ out1) {
+  __shared__ float red[4];
+  const bf16_t* x = X + (long)blockIdx.x * ld;
+  float s = 0.f;
+  const int C8 = C / 8;
+  for (int c = threadIdx.x; c < C8; c += 256) {
+    const bf16x8_t v = reinterpret_cast<const bf16x8_t*>(x)[c];
+    float p = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p += (float)v[j];
+    s += p;
+  }
+  for (int c = C8 * 8 + threadIdx.x; c < C; c += 256) s += (float)*reinterpret_cast<const __bf16*>(x + c);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = (red[0] + red[1]) + (red[2] + red[3]);
+    out0[blockIdx.x] = t;
+    if (out1) out1[blockIdx.x] = t;
+  }
+}
+
+// ============================================================================
+// recurrent steps (same decomposition as the fp32 v2 kernels: 64 rows x 32 units, 8 waves)
+// ============================================================================
+#define BF_BM 64
+#define BF_U 32
+
+__global__ __launch_bounds__(512) void lstm_step_fwd_bf16_kernel(
+    const bf16_t* __restrict__ hprev_bf, const bf16_t* __restrict__ whh_bf, float* __restrict__ gates,
+    const float* __restrict__ cprev, float* __restrict__ cout, float* __restrict__ hout, bf16_t* __restrict__ hout_bf,
+    bf16_t* __restrict__ hT, long ldhT, int t, int Bp, int B, int H) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* ldsb = reinterpret_cast<bf16_t*>(smem);
+  constexpr int BN = 4 * BF_U, LDP = BN + 4, LDH = BF_BM + 1;
+  constexpr int PER = BF_BM * BF_U / 512;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j0 = blockIdx.x * BF_U, b0 = blockIdx.y * BF_BM;
+  const int wm0 = (w >> 2) * 32, wn0 = (w & 3) * 32;
+  const long G = 4L * H;
+  float xg[PER][4], cpv[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + 512 * k, b = e / BF_U, u = e % BF_U;
+    const int gb = b0 + b, gj = j0 + u;
+    const bool ok = gb < B && gj < H;
+    const float* gp = gates + (long)gb * G + gj;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xg[k][q] = ok ? gp[q * H] : 0.f;
+    cpv[k] = (ok && cprev) ? cprev[(long)gb * H + gj] : 0.f;
+  }
+  f32x16 acc[1][1];
+  zero_acc(acc);
+  if (hprev_bf)
+    gemm_mainloop_bf_rp<BF_BM, BN, 512, 12, 1, 1>(hprev_bf + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh_bf, H,
+                                                  RowMapGates<BF_U>{j0, H}, 0, H, ldsb, tid, wm0, wn0, acc);
+  float* pre = reinterpret_cast<float*>(smem);
+  float* hs = pre + BF_BM * LDP;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) pre[(wm0 + acc_row(r, lane)) * LDP + wn0 + (lane & 31)] = acc[0][0][r];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + 512 * k, b = e / BF_U, u = e % BF_U;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    float* gp = gates + (long)gb * G + gj;
+    const float* pr = pre + b * LDP + u;
+    const float i = sv_sigmoid(pr[0] + xg[k][0]);
+    const float f = sv_sigmoid(pr[BF_U] + xg[k][1]);
+    const float g = tanhf(pr[2 * BF_U] + xg[k][2]);
+    const float o = sv_sigmoid(pr[3 * BF_U] + xg[k][3]);
+    const float c = f * cpv[k] + i * g;
+    const float h = o * tanhf(c);
+    gp[0] = i;
+    gp[H] = f;
+    gp[2 * H] = g;
+    gp[3 * H] = o;
+    cout[(long)gb * H + gj] = c;
+    hout[(long)gb * H + gj] = h;
+    hout_bf[(long)gb * H + gj] = to_bf(h);
+    hs[u * LDH + b] = h;
+  }
+  if (!hT) return;
+  __syncthreads();
+  for (int e = tid; e < BF_BM * BF_U; e += 512) {
+    const int u = e / BF_BM, b = e % BF_BM;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    bf16_t* row = hT + (long)gj * ldhT;
+    row[(long)(t + 1) * Bp + gb] = to_bf(hs[u * LDH + b]);
+    if (t == 0) row[gb] = 0;
+  }
+}
+
+__global__ __launch_bounds__(512) void lstm_step_bwd_bf16_kernel(
+    const bf16_t* __restrict__ dgnext, const bf16_t* __restrict__ whhT, const float* __restrict__ dhup,
+    const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
+    const float* __restrict__ c_prev, bf16_t* __restrict__ dg, float* __restrict__ dcf, bf16_t* __restrict__ dgT,
+    long lddgT, int t, int Bp, int B, int H) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* ldsb = reinterpret_cast<bf16_t*>(smem);
+  constexpr int GBUF = 2 * (BF_BM + BF_U) * (BBK + 8);
+  constexpr int LDR = BF_U + 1;
+  constexpr int LDT = BF_BM + 1;
+  constexpr int PER = BF_BM * BF_U / 512;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int gate = w >> 1, gt = tid & 127;
+  const int j0 = blockIdx.x * BF_U, b0 = blockIdx.y * BF_BM;
+  const long G = 4L * H;
+  float av[PER][4], cv[PER], cpv[PER], dcfv[PER], upv[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + 512 * k, b = e / BF_U, u = e % BF_U;
+    const int gb = b0 + b, gj = j0 + u;
+    const bool ok = gb < B && gj < H;
+    const long hi = (long)gb * H + gj;
+    const float* ap = acts + (long)gb * G + gj;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) av[k][q] = ok ? ap[q * H] : 0.f;
+    cv[k] = ok ? c_t[hi] : 0.f;
+    cpv[k] = (ok && c_prev) ? c_prev[hi] : 0.f;
+    dcfv[k] = (ok && dcf_next) ? dcf_next[hi] : 0.f;
+    upv[k] = (ok && dhup) ? dhup[hi] : 0.f;
+  }
+  f32x16 acc[1][1];
+  zero_acc(acc);
+  if (dgnext)
+    gemm_mainloop_bf_rp<BF_BM, BF_U, 128, 6, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
+                                                   RowMapLinear{j0, H}, gate * H, (gate + 1) * H, ldsb + gate * GBUF,
+                                                   gt, (w & 1) * 32, 0, acc);
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // [4][64][LDR]
+  float* gTs = red + 4 * BF_BM * LDR;           // [4*32][LDT]
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    red[(gate * BF_BM + (w & 1) * 32 + acc_row(r, lane)) * LDR + (lane & 31)] = acc[0][0][r];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + 512 * k, b = e / BF_U, u = e % BF_U;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    const long hi = (long)gb * H + gj;
+    float dh = red[(0 * BF_BM + b) * LDR + u];
+    dh += red[(1 * BF_BM + b) * LDR + u];
+    dh += red[(2 * BF_BM + b) * LDR + u];
+    dh += red[(3 * BF_BM + b) * LDR + u];
+    dh += upv[k];
+    const float i = av[k][0], f = av[k][1], g = av[k][2], o = av[k][3];
+    const float tc = tanhf(cv[k]);
+    const float dc = dh * o * (1.f - tc * tc) + dcfv[k];
+    const float d0 = dc * g * i * (1.f - i), d1 = dc * cpv[k] * f * (1.f - f);
+    const float d2 = dc * i * (1.f - g * g), d3 = dh * tc * o * (1.f - o);
+    bf16_t* dp = dg + (long)gb * G + gj;
+    dp[0] = to_bf(d0);
+    dp[H] = to_bf(d1);
+    dp[2 * H] = to_bf(d2);
+    dp[3 * H] = to_bf(d3);
+    dcf[hi] = dc * f;
+    gTs[(0 * BF_U + u) * LDT + b] = d0;
+    gTs[(1 * BF_U + u) * LDT + b] = d1;
+    gTs[(2 * BF_U + u) * LDT + b] = d2;
+    gTs[(3 * BF_U + u) * LDT + b] = d3;
+  }
+  if (!dgT) return;
+  __syncthreads();
+  for (int e = tid; e < 4 * BF_U * BF_BM; e += 512) {
+    const int gu = e / BF_BM, b = e % BF_BM;
+    const int gte = gu / BF_U, u = gu % BF_U;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    dgT[((long)gte * H + gj) * lddgT + (long)t * Bp + gb] = to_bf(gTs[gu * LDT + b]);
+  }
+}
+
+// ============================================================================
+// host side
+// ============================================================================
+namespace {
+
+struct BPlan {
+  int bm, bn, splitk, kchunk;
+};
+
+BPlan plan_bf16(int M, int N, int K) {
+  BPlan p;
+  const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+  const bool small = t128 < 128;
+  p.bm = p.bn = small ? 64 : 128;
+  const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
+  const long slots = small ? 1024 : 512;
+  int sk = 1;
+  if (tiles < slots) {
+    sk = (int)(slots / tiles);
+    const int kmax = K / 1024;
+    if (sk > kmax) sk = kmax;
+    if (sk > 32) sk = 32;
+    if (sk < 1) sk = 1;
+  }
+  p.kchunk = ((K + sk - 1) / sk + BBK - 1) / BBK * BBK;
+  p.splitk = (K + p.kchunk - 1) / p.kchunk;
+  return p;
+}
+
+template <int BM, int BN, int EPI>
+void launch_bf(const bf16_t* A, long lda, const bf16_t* B, long ldb, float* C, long ldc, long slab, int M, int N, int K,
+               int splitk, int kchunk, const float* b0, const float* b1, float beta, hipStream_t s) {
+  constexpr int LDS = 2 * (BM + BN) * (BBK + 8) * (int)sizeof(bf16_t);
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, EPI>), dim3(tiles, splitk), dim3(256), LDS, s, A, lda, B, ldb, C, ldc,
+                     slab, M, N, K, kchunk, b0, b1, beta);
+}
+
+constexpr int BFWD_LDS_MAIN = 2 * (BF_BM + 4 * BF_U) * (BBK + 8) * 2;
+constexpr int BFWD_LDS_EPI = (BF_BM * (4 * BF_U + 4) + BF_U * (BF_BM + 1)) * 4;
+constexpr int BFWD_LDS = BFWD_LDS_MAIN > BFWD_LDS_EPI ? BFWD_LDS_MAIN : BFWD_LDS_EPI;
+constexpr int BBWD_LDS_MAIN = 4 * 2 * (BF_BM + BF_U) * (BBK + 8) * 2;
+constexpr int BBWD_LDS_EPI = (4 * BF_BM * (BF_U + 1) + 4 * BF_U * (BF_BM + 1)) * 4;
+constexpr int BBWD_LDS = BBWD_LDS_MAIN > BBWD_LDS_EPI ? BBWD_LDS_MAIN : BBWD_LDS_EPI;
+
+}  // namespace
+
+extern "C" size_t sv_gemm_bf16_workspace(int M, int N, int K) {
+  const BPlan p = plan_bf16(M, N, K);
+  return p.splitk > 1 ? (size_t)p.splitk * M * N * sizeof(float) : 0;
+}
+
+extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, const bf16_t* B, long ldb, float* C,
+                            long ldc, const float* bias0, const float* bias1, float beta, float* workspace,
+                            hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || !A || !B || !C) return SV_EARG;
+  if (K % 8 || lda % 8 || ldb % 8 || (((uintptr_t)A | (uintptr_t)B) & 15)) return SV_EALIGN;
+  const BPlan p = plan_bf16(M, N, K);
+  if (p.splitk == 1) {
+    if (p.bm == 64)
+      launch_bf<64, 64, BEPI_STORE>(A, lda, B, ldb, C, ldc, 0, M, N, K, 1, p.kchunk, bias0, bias1, beta, stream);
+    else
+      launch_bf<128, 128, BEPI_STORE>(A, lda, B, ldb, C, ldc, 0, M, N, K, 1, p.kchunk, bias0, bias1, beta, stream);
+    SV_LAUNCH_CHECK();
+    return SV_OK;
+  }
+  if (!workspace) return SV_EARG;
+  const long slab = (long)M * N;
+  if (p.bm == 64)
+    launch_bf<64, 64, BEPI_SLAB>(A, lda, B, ldb, workspace, N, slab, M, N, K, p.splitk, p.kchunk, nullptr, nullptr, 0.f,
+                                 stream);
+  else
+    launch_bf<128, 128, BEPI_SLAB>(A, lda, B, ldb, workspace, N, slab, M, N, K, p.splitk, p.kchunk, nullptr, nullptr,
+                                   0.f, stream);
+  SV_LAUNCH_CHECK();
+  const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
+  hipLaunchKernelGGL(slab_reduce_bf_kernel, dim3(grid), dim3(256), 0, stream, workspace, p.splitk, slab, C, ldc, M, N,
+                     beta, bias0, bias1);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_cast_bf16(const float* x, bf16_t* y, long n, hipStream_t stream) {
+  if (!x || !y || n <= 0) return SV_EARG;
+  const int grid = (int)std::min<long>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid), dim3(256), 0, stream, x, y, n);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_transpose_cast_bf16(const float* src, long ld_src, int R, int C, bf16_t* dst, long ld_dst,
+                                      hipStream_t stream) {
+  if (!src || !dst || R <= 0 || C <= 0) return SV_EARG;
+  hipLaunchKernelGGL(transpose_cast_kernel, dim3((C + 31) / 32, (R + 31) / 32), dim3(256), 0, stream, src, ld_src, R, C,
+                     dst, ld_dst);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_lstm_layer_fwd_bf16(const bf16_t* x_bf, int T, int B, int F, int H, const bf16_t* w_ih_bf,
+                                      const bf16_t* w_hh_bf, const float* b_ih, const float* b_hh, float* gates,
+                                      float* c_tm, float* h_tm, bf16_t* h_bf, bf16_t* hT, hipStream_t stream) {
+  if (!x_bf || !w_ih_bf || !w_hh_bf || !gates || !c_tm || !h_tm || !h_bf) return SV_EARG;
+  if (T <= 0 || B <= 0 || F <= 0 || H <= 0 || F % 8 || H % 8) return SV_ESHAPE;
+  const long BH = (long)B * H, BG = 4L * B * H;
+  int rc = sv_gemm_bf16(T * B, 4 * H, F, x_bf, F, w_ih_bf, F, gates, 4L * H, b_ih, b_hh, 0.f, nullptr, stream);
+  if (rc) return rc;
+  hipError_t e = hipMemsetAsync(h_tm, 0, BH * sizeof(float), stream);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemsetAsync(h_bf, 0, BH * sizeof(bf16_t), stream);
+  if (e != hipSuccess) return (int)e;
+  const int Bp = (B + 7) & ~7;
+  const long ldhT = (long)(T + 1) * Bp;
+  if (hT && Bp != B) {
+    e = hipMemsetAsync(hT, 0, (size_t)H * ldhT * sizeof(bf16_t), stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
+  for (int t = 0; t < T; ++t) {
+    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel, grid, dim3(512), BFWD_LDS, stream, t ? h_bf + t * BH : nullptr,
+                       w_hh_bf, gates + t * BG, t ? c_tm + (t - 1) * BH : nullptr, c_tm + t * BH, h_tm + (t + 1) * BH,
+                       h_bf + (t + 1) * BH, hT, ldhT, t, Bp, B, H);
+    SV_LAUNCH_CHECK();
+  }
+  return SV_OK;
+}
+
+extern "C" size_t sv_lstm_layer_bwd_bf16_workspace(int T, int B, int F, int H) {
+  const int TBp = T * ((B + 7) & ~7);
+  size_t g = sv_gemm_bf16_workspace(4 * H, H, TBp);
+  g = std::max(g, sv_gemm_bf16_workspace(4 * H, F, TBp));
+  g = std::max(g, sv_gemm_bf16_workspace(T * B, F, 4 * H));
+  return 2 * ((size_t)B * H * sizeof(float) + 256) + g + 256;
+}
+
+extern "C" int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const bf16_t* xT_bf, long ld_xT,
+                                      const bf16_t* wihT_bf, const bf16_t* whhT_bf, const float* gates,
+                                      const float* c_tm, const bf16_t* hT_bf, const float* dh_up, int dh_up_full,
+                                      bf16_t* dg_bf, bf16_t* dgT_bf, float* dx_tm, float* dw_ih, float* dw_hh,
+                                      float* db_ih, float* db_hh, float* workspace, hipStream_t stream) {
+  if (!xT_bf || !wihT_bf || !whhT_bf || !gates || !c_tm || !hT_bf || !dg_bf || !dgT_bf || !dw_ih || !dw_hh || !db_ih ||
+      !workspace)
+    return SV_EARG;
+  if (T <= 0 || B <= 0 || F <= 0 || H <= 0 || F % 8 || H % 8 || ld_xT % 8) return SV_ESHAPE;
+  const long BH = (long)B * H, BG = 4L * B * H;
+  const int Bp = (B + 7) & ~7;
+  const int TBp = T * Bp;
+  const size_t dcfsz = ((size_t)BH * sizeof(float) + 255) / 256 * 256 / sizeof(float);
+  float* dcf0 = workspace;
+  float* dcf1 = workspace + dcfsz;
+  float* gws = workspace + 2 * dcfsz;
+  if (Bp != B) {
+    hipError_t e = hipMemsetAsync(dgT_bf, 0, (size_t)4 * H * TBp * sizeof(bf16_t), stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
+  for (int t = T - 1; t >= 0; --t) {
+    const float* up = nullptr;
+    if (dh_up) up = dh_up_full ? dh_up + t * BH : (t == T - 1 ? dh_up : nullptr);
+    float* dcf_out = (t & 1) ? dcf1 : dcf0;
+    const float* dcf_in = (t == T - 1) ? nullptr : ((t & 1) ? dcf0 : dcf1);
+    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel, grid, dim3(512), BBWD_LDS, stream,
+                       t == T - 1 ? nullptr : dg_bf + (t + 1) * BG, whhT_bf, up, dcf_in, gates + t * BG, c_tm + t * BH,
+                       t ? c_tm + (t - 1) * BH : nullptr, dg_bf + t * BG, dcf_out, dgT_bf, (long)TBp, t, Bp, B, H);
+    SV_LAUNCH_CHECK();
+  }
+  const long ldhT = (long)(T + 1) * Bp;
+  int rc = sv_gemm_bf16(4 * H, H, TBp, dgT_bf, TBp, hT_bf, ldhT, dw_hh, H, nullptr, nullptr, 0.f, gws, stream);
+  if (rc) return rc;
+  rc = sv_gemm_bf16(4 * H, F, TBp, dgT_bf, TBp, xT_bf, ld_xT, dw_ih, F, nullptr, nullptr, 0.f, gws, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, stream, dgT_bf, (long)TBp, TBp, db_ih, db_hh);
+  SV_LAUNCH_CHECK();
+  if (dx_tm) {
+    rc = sv_gemm_bf16(T * B, F, 4 * H, dg_bf, 4L * H, wihT_bf, 4L * H, dx_tm, F, nullptr, nullptr, 0.f, gws, stream);
+    if (rc) return rc;
+  }
+  return SV_OK;
+}

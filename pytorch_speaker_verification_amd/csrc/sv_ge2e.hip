@@ -24,7 +24,7 @@ namespace {
 
 // workspace carve (all fp32), see sv_ge2e_workspace_size
 struct Ge2eWs {
-  float *Ehat, *Uhat, *En, *Un, *rawd, *cos, *logz, *Chat, *Cn, *dcos, *alpha, *G1, *dwdb_rows, *gemm;
+  float *Ehat, *Uhat, *En, *Un, *rawd, *cos, *logz, *Chat, *Cn, *dcos, *alpha, *G1, *dwdb_rows, *betap, *gemm;
   size_t total;
 };
 
@@ -53,6 +53,7 @@ Ge2eWs carve(float* base, int Nl, int M, int D, int N) {
   w.alpha = take(Bl);
   w.G1 = take(Bl * D);
   w.dwdb_rows = take(2 * Bl);
+  w.betap = take(((Bl + 63) / 64) * (size_t)N);
   const size_t g1 = sv_gemm_f32_workspace((int)Bl, D, N);
   const size_t g2 = sv_gemm_f32_workspace(N, D, (int)Bl);
   w.gemm = take((std::max(g1, g2) + 3) / 4);
@@ -224,13 +225,29 @@ __global__ __launch_bounds__(256) void ge2e_rowbwd_kernel(const float* __restric
   }
 }
 
-// K7b: beta_k = sum_r dcos_off[r,k] raw[r,k]  (column reduction, one thread per k)
-__global__ void ge2e_beta_kernel(const float* __restrict__ dcos, const float* __restrict__ cos, int Bl, int N,
-                                 int ldc, float* __restrict__ beta) {
+// K7b: beta_k = sum_r dcos_off[r,k] raw[r,k]  (column reduction over rows, two levels:
+// block (k-chunk of 64, row-chunk of 64) -> partial[row-chunk][k]; then a fixed-order sum)
+__global__ __launch_bounds__(256) void ge2e_beta_partial_kernel(const float* __restrict__ dcos,
+                                                                const float* __restrict__ cos, int Bl, int N, int ldc,
+                                                                float* __restrict__ partial) {
+  __shared__ float red[4][64];
+  const int k = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * 64 + w * 16;
+  float s = 0.f;
+  if (k < N)
+    for (int r = r0; r < min(r0 + 16, Bl); ++r) s += dcos[(long)r * ldc + k] * cos[(long)r * ldc + k];
+  red[w][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (w == 0 && k < N) partial[(long)blockIdx.y * N + k] = (red[0][threadIdx.x] + red[1][threadIdx.x]) +
+                                                            (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+__global__ void ge2e_beta_final_kernel(const float* __restrict__ partial, int nchunk, int N,
+                                       float* __restrict__ beta) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= N) return;
   float s = 0.f;
-  for (int r = 0; r < Bl; ++r) s += dcos[(long)r * ldc + k] * cos[(long)r * ldc + k];
+  for (int c = 0; c < nchunk; ++c) s += partial[(long)c * N + k];
   beta[k] = s;
 }
 
@@ -372,7 +389,11 @@ extern "C" int sv_ge2e_bwd_rows(int N_local, int M, int D, int spk_offset, int N
   // dChat (before the norm Jacobian) = dcos_off^T E^   ([Np, Bl] x [Bl, D]); rows >= N are zero
   rc = sv_gemm_f32(0, 0, Np, D, Bl, ws.dcos, Np, ws.Ehat, D, dchat_partial, D, nullptr, nullptr, 0.f, ws.gemm, stream);
   if (rc) return rc;
-  hipLaunchKernelGGL(ge2e_beta_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, ws.dcos, ws.cos, Bl, N, Np,
+  const int nchunk = (Bl + 63) / 64;
+  hipLaunchKernelGGL(ge2e_beta_partial_kernel, dim3((N + 63) / 64, nchunk), dim3(256), 0, stream, ws.dcos, ws.cos, Bl,
+                     N, Np, ws.betap);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ge2e_beta_final_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, ws.betap, nchunk, N,
                      beta_partial);
   SV_LAUNCH_CHECK();
   hipLaunchKernelGGL(ge2e_dwdb_kernel, dim3(1), dim3(256), 0, stream, ws.dwdb_rows, Bl, dwdb);

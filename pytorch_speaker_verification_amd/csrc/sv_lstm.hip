@@ -693,6 +693,18 @@ extern "C" int sv_lstm_step_fwd(const float* h_prev, const float* w_hh, float* g
   return SV_OK;
 }
 
+// one backward recurrent step (K3) on its own (timing / tests): dg_next may be NULL (t = T-1)
+extern "C" int sv_lstm_step_bwd(const float* dg_next, const float* w_hhT, const float* dh_up, const float* dcf_next,
+                                const float* acts_t, const float* c_t, const float* c_prev, float* dg_t, float* dcf_t,
+                                int B, int H, hipStream_t stream) {
+  if (!w_hhT || !acts_t || !c_t || !dg_t || !dcf_t || B <= 0 || H <= 0 || H % 4) return SV_EARG;
+  const dim3 grid((H + BWD_U - 1) / BWD_U, (B + BWD_BM - 1) / BWD_BM);
+  launch_bwd_step(grid, stream, dg_next, w_hhT, dh_up, dcf_next, acts_t, c_t, c_prev, dg_t, dcf_t, nullptr, 0L, 0, B, B,
+                  H);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
 extern "C" int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, const float* w_ih, const float* w_hh,
                                  const float* b_ih, const float* b_hh, float* gates, float* c_tm, float* h_tm,
                                  float* hT, hipStream_t stream) {

@@ -35,6 +35,7 @@ class EmbedderState:
         self.xT0 = None     # layer-0 input transposed [F, T*B]
         self.y = self.emb = self.ynorm = self.h_last = None
         self.T = self.B = self.H = self.P = 0
+        self.bf16 = False
 
 
 def embedder_forward(x, layers, w_p, b_p, save=True):
@@ -133,15 +134,117 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False):
     return grads
 
 
+# ----------------------------------------------------------------------------- bf16 operands
+def _bf(shape, dev):
+    return torch.empty(shape, dtype=torch.bfloat16, device=dev)
+
+
+def embedder_forward_bf16(x, layers, w_p, b_p, save=True):
+    """Mixed-precision forward (BASELINE config c3): bf16 GEMM operands, fp32 accumulation,
+    fp32 gates / cell state / projection / norm.  Same outputs as embedder_forward."""
+    require_device(x, w_p, b_p, *[t for l in layers for t in l])
+    B, T, F = x.shape
+    H = layers[0][1].shape[1]
+    P = w_p.shape[0]
+    dev = x.device
+    s = stream_of(x)
+    Bp = (B + 7) // 8 * 8
+    st = EmbedderState()
+    st.T, st.B, st.H, st.P, st.bf16 = T, B, H, P, True
+    x_tm = torch.empty((T, B, F), dtype=torch.float32, device=dev)
+    call("sv_frames_to_time_major", ptr(x), ptr(x_tm), B, T, F, s)
+    x_bf = _bf((T, B, F), dev)
+    call("sv_cast_bf16", ptr(x_tm), ptr(x_bf), x_tm.numel(), s)
+    if save:
+        st.xT0 = (torch.zeros if Bp != B else torch.empty)((F, T * Bp), dtype=torch.bfloat16, device=dev)
+        if Bp == B:
+            call("sv_transpose_cast_bf16", ptr(x_tm), F, T * B, F, ptr(st.xT0), T * B, s)
+        else:
+            for t in range(T):
+                call("sv_transpose_cast_bf16", ptr(x_tm[t]), F, B, F, ptr(st.xT0) + 2 * t * Bp, T * Bp, s)
+    inp = x_bf
+    st.wT = []
+    for (w_ih, w_hh, b_ih, b_hh) in layers:
+        Fl = inp.shape[2]
+        wih_bf, whh_bf = _bf(w_ih.shape, dev), _bf(w_hh.shape, dev)
+        call("sv_cast_bf16", ptr(w_ih), ptr(wih_bf), w_ih.numel(), s)
+        call("sv_cast_bf16", ptr(w_hh), ptr(whh_bf), w_hh.numel(), s)
+        gates = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
+        c_tm = torch.empty((T, B, H), dtype=torch.float32, device=dev)
+        h_tm = torch.empty((T + 1, B, H), dtype=torch.float32, device=dev)
+        h_bf = _bf((T + 1, B, H), dev)
+        hT = _bf((H, (T + 1) * Bp), dev) if save else None
+        call("sv_lstm_layer_fwd_bf16", ptr(inp), T, B, Fl, H, ptr(wih_bf), ptr(whh_bf), ptr(b_ih), ptr(b_hh),
+             ptr(gates), ptr(c_tm), ptr(h_tm), ptr(h_bf), ptr(hT), s)
+        if save:
+            st.x_tm.append(inp)
+            st.gates.append(gates)
+            st.c_tm.append(c_tm)
+            st.h_tm.append(h_tm)
+            st.hT.append(hT)
+        inp = h_bf[1:]
+    h_last = st.h_tm[-1][T] if save else h_tm[T]
+    y = torch.empty((B, P), dtype=torch.float32, device=dev)
+    emb = torch.empty((B, P), dtype=torch.float32, device=dev)
+    ynorm = torch.empty((B,), dtype=torch.float32, device=dev)
+    ws = _ws(lib().sv_proj_norm_workspace(B, H, P), dev)
+    call("sv_proj_norm_fwd", ptr(h_last), B, H, P, ptr(w_p), ptr(b_p), ptr(y), ptr(emb), ptr(ynorm), ptr(ws), s)
+    st.y, st.emb, st.ynorm, st.h_last = y, emb, ynorm, h_last
+    return emb, st
+
+
+def embedder_backward_bf16(st, demb, layers, w_p, grads=None):
+    demb = demb.contiguous()
+    require_device(demb)
+    T, B, H, P = st.T, st.B, st.H, st.P
+    dev = demb.device
+    s = stream_of(demb)
+    L = len(layers)
+    Bp = (B + 7) // 8 * 8
+    if grads is None:
+        grads = []
+        for (w_ih, w_hh, b_ih, b_hh) in layers:
+            grads += [torch.empty_like(w_ih), torch.empty_like(w_hh), torch.empty_like(b_ih), torch.empty_like(b_hh)]
+        grads += [torch.empty_like(w_p), torch.empty((P,), dtype=torch.float32, device=dev)]
+    dh_last = torch.empty((B, H), dtype=torch.float32, device=dev)
+    ws = _ws(lib().sv_proj_norm_workspace(B, H, P), dev)
+    call("sv_proj_norm_bwd", ptr(demb), ptr(st.emb), ptr(st.ynorm), ptr(st.h_last), B, H, P, ptr(w_p),
+         ptr(grads[4 * L]), ptr(grads[4 * L + 1]), ptr(dh_last), ptr(ws), s)
+    Fmax = max(st.x_tm[l].shape[2] for l in range(L))
+    ws = _ws(lib().sv_lstm_layer_bwd_bf16_workspace(T, B, Fmax, H), dev)
+    dg = _bf((T, B, 4 * H), dev)
+    dgT = _bf((4 * H, T * Bp), dev)
+    whhT = _bf((H, 4 * H), dev)
+    dh_up, full = dh_last, 0
+    for l in range(L - 1, -1, -1):
+        w_ih, w_hh, _, _ = layers[l]
+        Fl = st.x_tm[l].shape[2]
+        wihT = _bf((Fl, 4 * H), dev)
+        call("sv_transpose_cast_bf16", ptr(w_ih), Fl, 4 * H, Fl, ptr(wihT), 4 * H, s)
+        call("sv_transpose_cast_bf16", ptr(w_hh), H, 4 * H, H, ptr(whhT), 4 * H, s)
+        dx = torch.empty((T, B, Fl), dtype=torch.float32, device=dev) if l > 0 else None
+        if l == 0:
+            xT, ld_xT = ptr(st.xT0), T * Bp
+        else:
+            xT, ld_xT = ptr(st.hT[l - 1]) + 2 * Bp, (T + 1) * Bp
+        call("sv_lstm_layer_bwd_bf16", T, B, Fl, H, xT, ld_xT, ptr(wihT), ptr(whhT), ptr(st.gates[l]),
+             ptr(st.c_tm[l]), ptr(st.hT[l]), ptr(dh_up), full, ptr(dg), ptr(dgT), ptr(dx), ptr(grads[4 * l]),
+             ptr(grads[4 * l + 1]), ptr(grads[4 * l + 2]), ptr(grads[4 * l + 3]), ptr(ws), s)
+        dh_up, full = dx, 1
+    return grads
+
+
 class EmbedderFunction(torch.autograd.Function):
     """emb = SpeechEmbedder.forward(x) with params (w_ih, w_hh, b_ih, b_hh)*L, w_p, b_p."""
 
     @staticmethod
-    def forward(ctx, x, num_layers, *params):
+    def forward(ctx, x, num_layers, precision, *params):
         L = num_layers
         layers = [tuple(params[4 * l:4 * l + 4]) for l in range(L)]
         w_p, b_p = params[4 * L], params[4 * L + 1]
-        emb, st = embedder_forward(x.contiguous(), layers, w_p, b_p, save=True)
+        fwd = embedder_forward_bf16 if precision == "bf16" else embedder_forward
+        emb, st = fwd(x.contiguous(), layers, w_p, b_p, save=True)
+        ctx.precision = precision
         ctx.st = st
         ctx.L = L
         ctx.save_for_backward(*params)
@@ -153,13 +256,18 @@ class EmbedderFunction(torch.autograd.Function):
         L = ctx.L
         layers = [tuple(params[4 * l:4 * l + 4]) for l in range(L)]
         need_dx = ctx.needs_input_grad[0]
-        out = embedder_backward(ctx.st, demb, layers, params[4 * L], need_dx=need_dx)
+        if ctx.precision == "bf16":
+            if need_dx:
+                raise NotImplementedError("input gradients are only produced by the fp32 path")
+            out = embedder_backward_bf16(ctx.st, demb, layers, params[4 * L])
+        else:
+            out = embedder_backward(ctx.st, demb, layers, params[4 * L], need_dx=need_dx)
         ctx.st = None
         if need_dx:
             grads, dx = out
         else:
             grads, dx = out, None
-        return (dx, None, *grads)
+        return (dx, None, None, *grads)
 
 
 # ----------------------------------------------------------------------------- GE2E

@@ -60,6 +60,9 @@ class SpeechEmbedder(nn.Module):
             elif "weight" in name:
                 nn.init.xavier_normal_(param)
         self.projection = nn.Linear(hp.model.hidden, hp.model.proj)  # :25
+        # "f32" (exact fp32 MFMA, configs c1/c2) or "bf16" (bf16 GEMM operands, fp32
+        # accumulation / state / loss, config c3).  Not part of the state_dict.
+        self.precision = "f32"
 
     def flat_params(self):
         """Parameters in kernel order: (w_ih, w_hh, b_ih, b_hh) per layer, then w_p, b_p."""
@@ -68,7 +71,8 @@ class SpeechEmbedder(nn.Module):
 
     def forward(self, x):
         # x.float() (:28) -> LSTM -> last frame (:30) -> projection (:31) -> x/|x| (:32)
-        return EmbedderFunction.apply(x.float().contiguous(), self.LSTM_stack.num_layers, *self.flat_params())
+        return EmbedderFunction.apply(x.float().contiguous(), self.LSTM_stack.num_layers, self.precision,
+                                      *self.flat_params())
 
 
 class GE2ELoss(nn.Module):

@@ -22,7 +22,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from .ops import clip_sgd_step_, embedder_backward, embedder_forward
+from .ops import (clip_sgd_step_, embedder_backward, embedder_backward_bf16, embedder_forward,
+                  embedder_forward_bf16)
 from .sharded_ge2e import ShardedGE2E
 
 
@@ -81,12 +82,17 @@ class GE2ETrainer:
         layers = net.LSTM_stack.layer_params()
         w_p, b_p = net.projection.weight, net.projection.bias
         w, b = self.loss_mod.w, self.loss_mod.b
-        emb, st = embedder_forward(x.float().contiguous(), layers, w_p, b_p)
+        bf16 = getattr(net, "precision", "f32") == "bf16"
+        fwd = embedder_forward_bf16 if bf16 else embedder_forward
+        emb, st = fwd(x.float().contiguous(), layers, w_p, b_p)
         E = emb.view(N, M, emb.shape[1])
         loss, _, gst = self.ge2e.forward(E, w, b)
         dE, dwdb = self.ge2e.backward(gst, w, b)
         self.flat_g[self.n_pad:self.n_pad + 2].copy_(dwdb)
-        embedder_backward(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views)
+        if bf16:
+            embedder_backward_bf16(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views)
+        else:
+            embedder_backward(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views)
         if self.ge2e.world > 1:
             dist.all_reduce(self.flat_g, group=self.group)  # SUM, never mean (SURVEY §7 hard part 4)
         n = self.n_pad

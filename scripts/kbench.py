@@ -39,6 +39,20 @@ us = timeit(lambda: call("sv_lstm_step_fwd", ptr(hprev), ptr(whh), ptr(gates), p
 res["fwd_step_us"] = round(us, 2)
 res["fwd_step_tflops"] = round(2 * B * H * G / us / 1e6, 1)
 
+res["fwd_step_nogemm_us"] = round(timeit(lambda: call("sv_lstm_step_fwd", None, ptr(whh), ptr(gates), ptr(cprev),
+                                                       ptr(c_t), ptr(h_t), B, H, s)), 2)
+whhT = whh.t().contiguous()
+dgn = torch.randn(B, G, generator=g).to(dev) * 0.01
+acts = torch.rand(B, G, generator=g).to(dev)
+dgo = torch.empty(B, G, device=dev)
+dcf0, dcf1 = torch.randn(B, H, generator=g).to(dev), torch.empty(B, H, device=dev)
+bw = lambda: call("sv_lstm_step_bwd", ptr(dgn), ptr(whhT), ptr(hprev), ptr(dcf0), ptr(acts), ptr(cprev), ptr(cprev),  # noqa: E731
+                  ptr(dgo), ptr(dcf1), B, H, s)
+us = timeit(bw)
+res["bwd_step_us"] = round(us, 2)
+res["bwd_step_tflops"] = round(2 * B * H * G / us / 1e6, 1)
+res["bwd_step_nogemm_us"] = round(timeit(lambda: call("sv_lstm_step_bwd", None, ptr(whhT), ptr(hprev), ptr(dcf0),
+                                                       ptr(acts), ptr(cprev), ptr(cprev), ptr(dgo), ptr(dcf1), B, H, s)), 2)
 # one layer fwd + bwd at T=16 to time the bwd step kernel in place
 Ts = 16
 x_tm = torch.randn(Ts, B, F, generator=g).to(dev)

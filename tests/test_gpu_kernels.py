@@ -119,3 +119,21 @@ def test_gemm_f32_bias_and_split_k(M, N, K):
     ref = A.double() @ B.double().T + bias.double()
     C = gemm_f32(A.to(DEV), B.to(DEV), True, True, bias=bias.to(DEV)).cpu().double()
     assert (C - ref).abs().max().item() <= 2e-6 * K ** 0.5 * ref.abs().max().item() + 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(640, 3072, 768), (3072, 768, 10240), (100, 40, 72), (640, 256, 768)])
+def test_gemm_bf16(M, N, K):
+    """bf16 operands, fp32 accumulation: against fp64 on the same bf16-rounded inputs."""
+    from pytorch_speaker_verification_amd._lib import call, lib, ptr
+    g = torch.Generator().manual_seed(M + 3 * N + K)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    B = torch.randn(N, K, generator=g).bfloat16()
+    bias = torch.randn(N, generator=g)
+    ref = A.double() @ B.double().T + bias.double()
+    Ad, Bd, biasd = A.to(DEV), B.to(DEV), bias.to(DEV)
+    C = torch.empty(M, N, device=DEV)
+    ws = torch.empty(lib().sv_gemm_bf16_workspace(M, N, K) // 4 + 1, device=DEV)
+    call("sv_gemm_bf16", M, N, K, ptr(Ad), K, ptr(Bd), K, ptr(C), N, ptr(biasd), None, 0.0, ptr(ws),
+         torch.cuda.current_stream().cuda_stream)
+    err = (C.cpu().double() - ref).abs().max().item()
+    assert err <= 2e-6 * K ** 0.5 * ref.abs().max().item() + 1e-5, err
