@@ -79,6 +79,40 @@ def time_step_kernel(B, H, dev, reps=64):
     return e0.elapsed_time(e1) / reps, 2.0 * B * H * 4 * H
 
 
+def time_gemm_kernel(M, N, K, dev, reps=5):
+    """Average duration of the dominant kernel by total time, gemm_km_kernel<128,128> at the
+    K1 shape of layers 1-2 (x W_ih^T: M = T*B, N = 4H, K = H), HIP events on its stream."""
+    from pytorch_speaker_verification_amd._lib import call, ptr, stream_of
+    g = torch.Generator(device="cpu").manual_seed(8)
+    A = torch.randn(M, K, generator=g).to(dev)
+    Bm = (torch.randn(N, K, generator=g) * 0.03).to(dev)
+    C = torch.empty(M, N, device=dev)
+    s = torch.cuda.current_stream(dev)
+    f = lambda: call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, None,  # noqa: E731
+                     stream_of(C))
+    f()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        f()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps, 2.0 * M * N * K, 4.0 * (M * K + N * K + M * N)
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/), corrected as
+    MI355X_MICROARCH.md prescribes: FETCH_SIZE x 2 (gfx950 halves wide streaming reads) +
+    WRITE_SIZE, both in KiB."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d[kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(dims, N, M, T, seconds_budget=25.0):
     """The reference's CPU path (stock PyTorch port, oracle/torch_port.py) on host cores,
     one full training step of the same workload (bounded sample)."""
@@ -216,12 +250,22 @@ def main():
                        "step_tflops": round(st_fl / (ms16 * 1e-3) / 1e12, 2),
                        "step_mfma_frac": round(st_fl / (ms16 * 1e-3) / 1e12 / MI355X_BF16_MFMA_TFLOPS, 4)}
     if rank == 0:
-        ms_k, fl_k = time_step_kernel(B, dims[1], dev)
-        ach = fl_k / (ms_k * 1e-3) / 1e12
-        out["roofline"] = {"kernel": "lstm_step_fwd_kernel (K2, fp32 MFMA 32x32x2)", "bound": "mfma",
-                           "achieved": round(ach, 2), "peak": MI355X_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / MI355X_FP32_MFMA_TFLOPS, 4), "traffic": None,
-                           "avg_launch_us": round(ms_k * 1e3, 2), "flops_per_launch": fl_k}
+        H = dims[1]
+        ms_g, fl_g, by_g = time_gemm_kernel(T * B, 4 * H, H, dev)
+        ach = fl_g / (ms_g * 1e-3) / 1e12
+        out["roofline"] = {"kernel": "gemm_km_kernel<128,128> (K1/dW/dx NT GEMM, fp32 MFMA 32x32x2), K1 shape "
+                                     f"M={T * B} N={4 * H} K={H}",
+                           "bound": "mfma", "achieved": round(ach, 2), "peak": MI355X_FP32_MFMA_TFLOPS,
+                           "unit": "TFLOP/s", "frac": round(ach / MI355X_FP32_MFMA_TFLOPS, 4),
+                           "traffic": pmc_traffic("gemm_km_kernel<128,128>"), "algorithmic_bytes": by_g,
+                           "avg_launch_us": round(ms_g * 1e3, 2), "flops_per_launch": fl_g}
+        ms_k, fl_k = time_step_kernel(B, H, dev)
+        ach_k = fl_k / (ms_k * 1e-3) / 1e12
+        out["roofline_step_kernel"] = {"kernel": "lstm_step_fwd_v2_kernel (K2, fp32 MFMA 32x32x2)", "bound": "mfma",
+                                       "achieved": round(ach_k, 2), "peak": MI355X_FP32_MFMA_TFLOPS,
+                                       "unit": "TFLOP/s", "frac": round(ach_k / MI355X_FP32_MFMA_TFLOPS, 4),
+                                       "traffic": pmc_traffic("lstm_step_fwd_v2_kernel"),
+                                       "avg_launch_us": round(ms_k * 1e3, 2), "flops_per_launch": fl_k}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(dims, N, M, T)
         print(json.dumps(out), flush=True)

@@ -62,6 +62,15 @@ int sv_lstm_step_fwd(const float* h_prev, const float* w_hh, float* gates_t, con
 int sv_lstm_step_bwd(const float* dg_next, const float* w_hhT, const float* dh_up, const float* dcf_next,
                      const float* acts_t, const float* c_t, const float* c_prev, float* dg_t, float* dcf_t, int B,
                      int H, hipStream_t stream);
+/* Whole stack, layer-pipelined over streams: layer l runs on side[l] in chunks of `chunk`
+ * timesteps (chunk input-projection GEMM, then its steps) and waits only for layer l-1's same
+ * chunk, so the layers' kernels overlap.  Per-layer pointers come in host arrays of length L
+ * (layer 0 input width F, others H); ev = L*ceil(T/chunk)+1 caller-created events.  Starts after
+ * and joins back into `main` (all work ordered before the next op on `main`). */
+int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float* x_tm, const float* const* w_ih,
+                      const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
+                      float* const* gates, float* const* c_tm, float* const* h_tm, float* const* hT, int chunk,
+                      hipStream_t main, const hipStream_t* side, hipEvent_t* ev);
 size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H);
 /* xT: the layer input transposed, [F, >= T*Bp] with row stride ld_xT (layer 0: the frames;
  * layer l > 0: hT of layer l-1 offset by Bp columns).  hT: this layer's [H, (T+1)Bp] from the fwd.
@@ -128,6 +137,12 @@ int sv_transpose_cast_bf16(const float* src, long ld_src, int R, int C, sv_bf16*
 int sv_lstm_layer_fwd_bf16(const sv_bf16* x_bf, int T, int B, int F, int H, const sv_bf16* w_ih_bf,
                            const sv_bf16* w_hh_bf, const float* b_ih, const float* b_hh, float* gates, float* c_tm,
                            float* h_tm, sv_bf16* h_bf, sv_bf16* hT, hipStream_t stream);
+/* layer-pipelined stack forward in bf16 (as sv_lstm_stack_fwd; h_bf per layer [T+1,B,H]) */
+int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* x_bf, const sv_bf16* const* w_ih_bf,
+                           const sv_bf16* const* w_hh_bf, const float* const* b_ih, const float* const* b_hh,
+                           float* const* gates, float* const* c_tm, float* const* h_tm, sv_bf16* const* h_bf,
+                           sv_bf16* const* hT, int chunk, hipStream_t main, const hipStream_t* side,
+                           hipEvent_t* ev);
 size_t sv_lstm_layer_bwd_bf16_workspace(int T, int B, int F, int H);
 /* wihT_bf [F,4H], whhT_bf [H,4H]; dg_bf [T,B,4H] and dgT_bf [4H,T*Bp] are bf16 outputs */
 int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const sv_bf16* xT_bf, long ld_xT, const sv_bf16* wihT_bf,

@@ -164,10 +164,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
   extern __shared__ __attribute__((aligned(16))) bf16_t ldsb[];
   constexpr int TM = BM / 64, TN = BN / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int tiles_m = (M + BM - 1) / BM;
-  const int nwg = tiles_m * ((N + BN - 1) / BN);
+  // column tile fastest: the blocks an XCD runs together share one A row-panel (the large
+  // operand, read from HBM once) and sweep the small B operand, which stays cache-resident
+  const int tiles_n = (N + BN - 1) / BN;
+  const int nwg = tiles_n * ((M + BM - 1) / BM);
   const int id = xcd_remap(blockIdx.x, nwg);
-  const int tm = id % tiles_m, tn = id / tiles_m;
+  const int tn = id % tiles_n, tm = id / tiles_n;
   const int kbeg = blockIdx.y * kchunk;
   const int kend = min(K, kbeg + kchunk);
   const int wm0 = (w >> 1) * (BM / 2), wn0 = (w & 1) * (BN / 2);
@@ -270,6 +272,7 @@ __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const bf16_t* __restri
 #define BF_BM 64
 #define BF_U 32
 
+template <int SC>
 __global__ __launch_bounds__(512) void lstm_step_fwd_bf16_kernel(
     const bf16_t* __restrict__ hprev_bf, const bf16_t* __restrict__ whh_bf, float* __restrict__ gates,
     const float* __restrict__ cprev, float* __restrict__ cout, float* __restrict__ hout, bf16_t* __restrict__ hout_bf,
@@ -296,7 +299,7 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_bf16_kernel(
   f32x16 acc[1][1];
   zero_acc(acc);
   if (hprev_bf)
-    gemm_mainloop_bf_rp<BF_BM, BN, 512, 12, 1, 1>(hprev_bf + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh_bf, H,
+    gemm_mainloop_bf_rp<BF_BM, BN, 512, SC, 1, 1>(hprev_bf + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh_bf, H,
                                                   RowMapGates<BF_U>{j0, H}, 0, H, ldsb, tid, wm0, wn0, acc);
   float* pre = reinterpret_cast<float*>(smem);
   float* hs = pre + BF_BM * LDP;
@@ -463,6 +466,33 @@ constexpr int BBWD_LDS_MAIN = 4 * 2 * (BF_BM + BF_U) * (BBK + 8) * 2;
 constexpr int BBWD_LDS_EPI = (4 * BF_BM * (BF_U + 1) + 4 * BF_U * (BF_BM + 1)) * 4;
 constexpr int BBWD_LDS = BBWD_LDS_MAIN > BBWD_LDS_EPI ? BBWD_LDS_MAIN : BBWD_LDS_EPI;
 
+// forward step variant: register prefetch of all 12 k-tiles (1 block/CU) or super-chunks of
+// 6 (fewer VGPRs: 2 blocks/CU, so pipelined layers' steps can share a CU); SV_BF16_SC overrides
+int bf16_sc() {
+  static int v = [] {
+    const char* e = getenv("SV_BF16_SC");
+    const int x = e ? atoi(e) : 12;
+    return (x == 3 || x == 4 || x == 6) ? x : 12;
+  }();
+  return v;
+}
+void launch_fwd_bf16(dim3 grid, hipStream_t s, const bf16_t* hp, const bf16_t* whh, float* g, const float* cp,
+                     float* c, float* h, bf16_t* hb, bf16_t* hT, long ldhT, int t, int Bp, int B, int H) {
+  const int sc = bf16_sc();
+  if (sc == 6)
+    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<6>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
+                       t, Bp, B, H);
+  else if (sc == 4)
+    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<4>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
+                       t, Bp, B, H);
+  else if (sc == 3)
+    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<3>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
+                       t, Bp, B, H);
+  else
+    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<12>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
+                       t, Bp, B, H);
+}
+
 }  // namespace
 
 extern "C" size_t sv_gemm_bf16_workspace(int M, int N, int K) {
@@ -537,9 +567,9 @@ extern "C" int sv_lstm_layer_fwd_bf16(const bf16_t* x_bf, int T, int B, int F, i
   }
   const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
   for (int t = 0; t < T; ++t) {
-    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel, grid, dim3(512), BFWD_LDS, stream, t ? h_bf + t * BH : nullptr,
-                       w_hh_bf, gates + t * BG, t ? c_tm + (t - 1) * BH : nullptr, c_tm + t * BH, h_tm + (t + 1) * BH,
-                       h_bf + (t + 1) * BH, hT, ldhT, t, Bp, B, H);
+    launch_fwd_bf16(grid, stream, t ? h_bf + t * BH : nullptr, w_hh_bf, gates + t * BG,
+                    t ? c_tm + (t - 1) * BH : nullptr, c_tm + t * BH, h_tm + (t + 1) * BH, h_bf + (t + 1) * BH, hT,
+                    ldhT, t, Bp, B, H);
     SV_LAUNCH_CHECK();
   }
   return SV_OK;
@@ -595,5 +625,57 @@ extern "C" int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const bf16_t* 
     rc = sv_gemm_bf16(T * B, F, 4 * H, dg_bf, 4L * H, wihT_bf, 4L * H, dx_tm, F, nullptr, nullptr, 0.f, gws, stream);
     if (rc) return rc;
   }
+  return SV_OK;
+}
+
+// Layer-pipelined stack forward, bf16 operands (see sv_lstm_stack_fwd in sv_lstm.hip).
+extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf,
+                                      const bf16_t* const* w_ih_bf, const bf16_t* const* w_hh_bf,
+                                      const float* const* b_ih, const float* const* b_hh, float* const* gates,
+                                      float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
+                                      bf16_t* const* hT, int chunk, hipStream_t main, const hipStream_t* side,
+                                      hipEvent_t* ev) {
+  if (L <= 0 || !x_bf || !w_ih_bf || !w_hh_bf || !gates || !c_tm || !h_tm || !h_bf || !side || !ev || chunk <= 0)
+    return SV_EARG;
+  if (T <= 0 || B <= 0 || F <= 0 || H <= 0 || F % 8 || H % 8) return SV_ESHAPE;
+  const int nch = (T + chunk - 1) / chunk;
+  const long BH = (long)B * H, BG = 4L * B * H;
+  const int Bp = (B + 7) & ~7;
+  const long ldhT = (long)(T + 1) * Bp;
+  hipEvent_t ev_start = ev[L * nch];
+  hipError_t e = hipEventRecord(ev_start, main);
+  if (e != hipSuccess) return (int)e;
+  for (int l = 0; l < L; ++l) {
+    hipStream_t s = side[l];
+    if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
+    if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), s)) != hipSuccess) return (int)e;
+    if ((e = hipMemsetAsync(h_bf[l], 0, BH * sizeof(bf16_t), s)) != hipSuccess) return (int)e;
+    if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(bf16_t), s)) != hipSuccess)
+      return (int)e;
+  }
+  const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
+  for (int c = 0; c < nch + L - 1; ++c) {
+    for (int l = 0; l < L; ++l) {
+      const int cc = c - l;
+      if (cc < 0 || cc >= nch) continue;
+      hipStream_t s = side[l];
+      const int t0 = cc * chunk, t1 = std::min(T, t0 + chunk);
+      const int Fl = l == 0 ? F : H;
+      const bf16_t* in = l == 0 ? x_bf + (long)t0 * B * F : h_bf[l - 1] + (long)(t0 + 1) * BH;
+      if (l > 0 && (e = hipStreamWaitEvent(s, ev[(l - 1) * nch + cc], 0)) != hipSuccess) return (int)e;
+      int rc = sv_gemm_bf16((t1 - t0) * B, 4 * H, Fl, in, Fl, w_ih_bf[l], Fl, gates[l] + t0 * BG, 4L * H, b_ih[l],
+                            b_hh[l], 0.f, nullptr, s);
+      if (rc) return rc;
+      for (int t = t0; t < t1; ++t) {
+        launch_fwd_bf16(grid, s, t ? h_bf[l] + t * BH : nullptr, w_hh_bf[l], gates[l] + t * BG,
+                        t ? c_tm[l] + (t - 1) * BH : nullptr, c_tm[l] + t * BH, h_tm[l] + (t + 1) * BH,
+                        h_bf[l] + (t + 1) * BH, hT[l], ldhT, t, Bp, B, H);
+        SV_LAUNCH_CHECK();
+      }
+      if ((e = hipEventRecord(ev[l * nch + cc], s)) != hipSuccess) return (int)e;
+    }
+  }
+  for (int l = 0; l < L; ++l)
+    if ((e = hipStreamWaitEvent(main, ev[l * nch + nch - 1], 0)) != hipSuccess) return (int)e;
   return SV_OK;
 }

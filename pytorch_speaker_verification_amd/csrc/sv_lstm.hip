@@ -31,10 +31,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int TM = BM / 64, TN = BN / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int tiles_m = (M + BM - 1) / BM;
-  const int nwg = tiles_m * ((N + BN - 1) / BN);
+  // column tile fastest: the blocks an XCD runs together share one A row-panel (the large
+  // operand, read from HBM once) and sweep the small B operand, which stays cache-resident
+  const int tiles_n = (N + BN - 1) / BN;
+  const int nwg = tiles_n * ((M + BM - 1) / BM);
   const int id = xcd_remap(blockIdx.x, nwg);
-  const int tm = id % tiles_m, tn = id / tiles_m;
+  const int tn = id % tiles_n, tm = id / tiles_n;
   const int kbeg = blockIdx.y * kchunk;
   const int kend = min(K, kbeg + kchunk);
   const int wm0 = (w >> 1) * (BM / 2), wn0 = (w & 1) * (BN / 2);
@@ -126,10 +128,12 @@ __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ 
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int TM = BM / 64, TN = BN / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int tiles_m = (M + BM - 1) / BM;
-  const int nwg = tiles_m * ((N + BN - 1) / BN);
+  // column tile fastest: the blocks an XCD runs together share one A row-panel (the large
+  // operand, read from HBM once) and sweep the small B operand, which stays cache-resident
+  const int tiles_n = (N + BN - 1) / BN;
+  const int nwg = tiles_n * ((M + BM - 1) / BM);
   const int id = xcd_remap(blockIdx.x, nwg);
-  const int tm = id % tiles_m, tn = id / tiles_m;
+  const int tn = id % tiles_n, tm = id / tiles_n;
   const int kbeg = blockIdx.y * kchunk;
   const int kend = min(K, kbeg + kchunk);
   const int wm0 = (w >> 1) * (BM / 2), wn0 = (w & 1) * (BN / 2);
@@ -808,5 +812,62 @@ extern "C" int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* xT, lo
                      stream);
     if (rc) return rc;
   }
+  return SV_OK;
+}
+
+// ============================================================================
+// Layer-pipelined stack forward.  Layer l runs on side[l]; its timesteps are processed in
+// chunks of `chunk`: [chunk input-projection GEMM (K1) -> chunk step kernels (K2)].  Layer l
+// waits only for layer l-1 to finish the same chunk, so up to L layers' kernels run at once
+// and one layer's latency-bound step kernels overlap another's GEMM / steps (each K2 block
+// leaves room for a second resident block per CU).  Joins back into `main` before returning.
+// Host arrays (length L) carry the per-layer device pointers; ev needs L*ceil(T/chunk) + 1
+// caller-created events.
+// ============================================================================
+extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float* x_tm, const float* const* w_ih,
+                                 const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
+                                 float* const* gates, float* const* c_tm, float* const* h_tm, float* const* hT,
+                                 int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev) {
+  if (L <= 0 || !x_tm || !w_ih || !w_hh || !gates || !c_tm || !h_tm || !side || !ev || chunk <= 0) return SV_EARG;
+  if (!lstm_dims_ok(T, B, F, H)) return SV_ESHAPE;
+  const int nch = (T + chunk - 1) / chunk;
+  const long BH = (long)B * H, BG = 4L * B * H;
+  const int Bp = (B + 3) & ~3;
+  const long ldhT = (long)(T + 1) * Bp;
+  hipEvent_t ev_start = ev[L * nch];
+  hipError_t e = hipEventRecord(ev_start, main);
+  if (e != hipSuccess) return (int)e;
+  for (int l = 0; l < L; ++l) {
+    hipStream_t s = side[l];
+    if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
+    if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), s)) != hipSuccess) return (int)e;
+    if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(float), s)) != hipSuccess)
+      return (int)e;
+  }
+  const dim3 grid((H + FWD_U - 1) / FWD_U, (B + FWD_BM - 1) / FWD_BM);
+  // wavefront issue order: chunk c of layer l after chunk c of layer l-1 on the host too
+  for (int c = 0; c < nch + L - 1; ++c) {
+    for (int l = 0; l < L; ++l) {
+      const int cc = c - l;
+      if (cc < 0 || cc >= nch) continue;
+      hipStream_t s = side[l];
+      const int t0 = cc * chunk, t1 = std::min(T, t0 + chunk);
+      const int Fl = l == 0 ? F : H;
+      const float* in = l == 0 ? x_tm + (long)t0 * B * F : h_tm[l - 1] + (long)(t0 + 1) * BH;
+      if (l > 0 && (e = hipStreamWaitEvent(s, ev[(l - 1) * nch + cc], 0)) != hipSuccess) return (int)e;
+      int rc = sv_gemm_f32(1, 1, (t1 - t0) * B, 4 * H, Fl, in, Fl, w_ih[l], Fl, gates[l] + t0 * BG, 4L * H, b_ih[l],
+                           b_hh[l], 0.f, nullptr, s);
+      if (rc) return rc;
+      for (int t = t0; t < t1; ++t) {
+        launch_fwd_step(grid, s, t ? h_tm[l] + t * BH : nullptr, w_hh[l], gates[l] + t * BG,
+                        t ? c_tm[l] + (t - 1) * BH : nullptr, c_tm[l] + t * BH, h_tm[l] + (t + 1) * BH, hT[l], ldhT,
+                        t, Bp, B, H);
+        SV_LAUNCH_CHECK();
+      }
+      if ((e = hipEventRecord(ev[l * nch + cc], s)) != hipSuccess) return (int)e;
+    }
+  }
+  for (int l = 0; l < L; ++l)
+    if ((e = hipStreamWaitEvent(main, ev[l * nch + nch - 1], 0)) != hipSuccess) return (int)e;
   return SV_OK;
 }

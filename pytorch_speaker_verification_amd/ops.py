@@ -11,9 +11,39 @@ plumbing; every FLOP of the path runs in the HIP kernels of libsv_ge2e.so.
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import torch
 
 from ._lib import call, ptr, require_device, stream_of, lib
+
+PIPELINE_CHUNK = int(os.environ.get("SV_PIPELINE_CHUNK", "16"))  # 0 disables the layer pipeline
+
+
+class _StreamPool:
+    """Side streams + events for the layer-pipelined schedules (one set per device)."""
+    _pools = {}
+
+    @classmethod
+    def get(cls, device, n_streams, n_events):
+        key = (device.index, n_streams)
+        p = cls._pools.get(key)
+        if p is None or len(p[1]) < n_events:
+            streams = [torch.cuda.Stream(device=device) for _ in range(n_streams)]
+            events = []
+            with torch.cuda.device(device):
+                for _ in range(n_events):
+                    e = torch.cuda.Event()
+                    e.record()  # materialise the native event
+                    events.append(e)
+            p = (streams, events)
+            cls._pools[key] = p
+        return p
+
+
+def _parr(ts):
+    return (ctypes.c_void_p * len(ts))(*[ptr(t) if t is not None else None for t in ts])
 
 
 def _ws(nbytes, device):
@@ -61,7 +91,27 @@ def embedder_forward(x, layers, w_p, b_p, save=True):
             for t in range(T):
                 call("sv_transpose", ptr(x_tm[t]), F, B, F, ptr(st.xT0) + 4 * t * Bp, T * Bp, s)
     inp = x_tm
-    for (w_ih, w_hh, b_ih, b_hh) in layers:
+    L = len(layers)
+    if PIPELINE_CHUNK > 0 and L > 1:
+        gs = [torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev) for _ in range(L)]
+        cs = [torch.empty((T, B, H), dtype=torch.float32, device=dev) for _ in range(L)]
+        hs = [torch.empty((T + 1, B, H), dtype=torch.float32, device=dev) for _ in range(L)]
+        hTs = [torch.empty((H, (T + 1) * Bp), dtype=torch.float32, device=dev) if save else None for _ in range(L)]
+        nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
+        streams, events = _StreamPool.get(dev, L, L * nch + 1)
+        sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
+        ep = (ctypes.c_void_p * (L * nch + 1))(*[e.cuda_event for e in events[:L * nch + 1]])
+        call("sv_lstm_stack_fwd", L, T, B, F, H, ptr(x_tm), _parr([l[0] for l in layers]),
+             _parr([l[1] for l in layers]), _parr([l[2] for l in layers]), _parr([l[3] for l in layers]),
+             _parr(gs), _parr(cs), _parr(hs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep)
+        if save:
+            st.x_tm = [x_tm] + [h[1:] for h in hs[:-1]]
+            st.gates, st.c_tm, st.h_tm, st.hT = gs, cs, hs, hTs
+        layers_done = True
+        inp = hs[-1][1:]
+    else:
+        layers_done = False
+    for (w_ih, w_hh, b_ih, b_hh) in ([] if layers_done else layers):
         Fl = inp.shape[2]
         gates = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
         c_tm = torch.empty((T, B, H), dtype=torch.float32, device=dev)
@@ -163,26 +213,36 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True):
             for t in range(T):
                 call("sv_transpose_cast_bf16", ptr(x_tm[t]), F, B, F, ptr(st.xT0) + 2 * t * Bp, T * Bp, s)
     inp = x_bf
-    st.wT = []
+    L = len(layers)
+    wbf = []
     for (w_ih, w_hh, b_ih, b_hh) in layers:
-        Fl = inp.shape[2]
         wih_bf, whh_bf = _bf(w_ih.shape, dev), _bf(w_hh.shape, dev)
         call("sv_cast_bf16", ptr(w_ih), ptr(wih_bf), w_ih.numel(), s)
         call("sv_cast_bf16", ptr(w_hh), ptr(whh_bf), w_hh.numel(), s)
-        gates = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
-        c_tm = torch.empty((T, B, H), dtype=torch.float32, device=dev)
-        h_tm = torch.empty((T + 1, B, H), dtype=torch.float32, device=dev)
-        h_bf = _bf((T + 1, B, H), dev)
-        hT = _bf((H, (T + 1) * Bp), dev) if save else None
-        call("sv_lstm_layer_fwd_bf16", ptr(inp), T, B, Fl, H, ptr(wih_bf), ptr(whh_bf), ptr(b_ih), ptr(b_hh),
-             ptr(gates), ptr(c_tm), ptr(h_tm), ptr(h_bf), ptr(hT), s)
-        if save:
-            st.x_tm.append(inp)
-            st.gates.append(gates)
-            st.c_tm.append(c_tm)
-            st.h_tm.append(h_tm)
-            st.hT.append(hT)
-        inp = h_bf[1:]
+        wbf.append((wih_bf, whh_bf))
+    gs = [torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev) for _ in range(L)]
+    cs = [torch.empty((T, B, H), dtype=torch.float32, device=dev) for _ in range(L)]
+    hs = [torch.empty((T + 1, B, H), dtype=torch.float32, device=dev) for _ in range(L)]
+    hbs = [_bf((T + 1, B, H), dev) for _ in range(L)]
+    hTs = [_bf((H, (T + 1) * Bp), dev) if save else None for _ in range(L)]
+    if PIPELINE_CHUNK > 0 and L > 1:
+        nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
+        streams, events = _StreamPool.get(dev, L, L * nch + 1)
+        sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
+        ep = (ctypes.c_void_p * (L * nch + 1))(*[e.cuda_event for e in events[:L * nch + 1]])
+        call("sv_lstm_stack_fwd_bf16", L, T, B, F, H, ptr(x_bf), _parr([w[0] for w in wbf]),
+             _parr([w[1] for w in wbf]), _parr([l[2] for l in layers]), _parr([l[3] for l in layers]),
+             _parr(gs), _parr(cs), _parr(hs), _parr(hbs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep)
+    else:
+        for l, (w_ih, w_hh, b_ih, b_hh) in enumerate(layers):
+            Fl = inp.shape[2]
+            call("sv_lstm_layer_fwd_bf16", ptr(inp), T, B, Fl, H, ptr(wbf[l][0]), ptr(wbf[l][1]), ptr(b_ih),
+                 ptr(b_hh), ptr(gs[l]), ptr(cs[l]), ptr(hs[l]), ptr(hbs[l]), ptr(hTs[l]), s)
+            inp = hbs[l][1:]
+    if save:
+        st.x_tm = [x_bf] + [h[1:] for h in hbs[:-1]]
+        st.gates, st.c_tm, st.h_tm, st.hT = gs, cs, hs, hTs
+    h_tm = hs[-1]
     h_last = st.h_tm[-1][T] if save else h_tm[T]
     y = torch.empty((B, P), dtype=torch.float32, device=dev)
     emb = torch.empty((B, P), dtype=torch.float32, device=dev)

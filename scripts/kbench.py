@@ -95,3 +95,31 @@ res["gemm_Gx_us_tf"] = gemm(1, 1, T * B, G, H)
 res["gemm_dW_us_tf"] = gemm(1, 1, G, H, T * B)
 res["gemm_dx_us_tf"] = gemm(1, 1, T * B, H, G)
 print(json.dumps(res), flush=True)
+
+
+def torch_mm(M, N, K, dt):
+    A = torch.randn(M, K, device=dev).to(dt)
+    Bm = torch.randn(N, K, device=dev).to(dt)
+    us = timeit(lambda: torch.matmul(A, Bm.t()), reps=5, warm=2)
+    return round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)
+
+
+ref = {}
+for name, (M, N, K) in {"Gx": (T * B, G, H), "dW": (G, H, T * B), "dx": (T * B, H, G)}.items():
+    ref["torch_f32_" + name] = torch_mm(M, N, K, torch.float32)
+    ref["torch_bf16_" + name] = torch_mm(M, N, K, torch.bfloat16)
+
+
+def gemm_bf(M, N, K):
+    A = torch.randn(M, K, generator=g).bfloat16().to(dev)
+    Bm = torch.randn(N, K, generator=g).bfloat16().to(dev)
+    C = torch.empty(M, N, device=dev)
+    w = torch.empty(lib().sv_gemm_bf16_workspace(M, N, K) // 4 + 1, device=dev)
+    f = lambda: call("sv_gemm_bf16", M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, ptr(w), s)  # noqa: E731
+    us = timeit(f, reps=5, warm=1)
+    return round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)
+
+
+for name, (M, N, K) in {"Gx": (T * B, G, H), "dW": (G, H, T * B), "dx": (T * B, H, G)}.items():
+    ref["sv_bf16_" + name] = gemm_bf(M, N, K)
+print(json.dumps(ref), flush=True)
