@@ -119,6 +119,10 @@ size_t sv_ge2e_cossim_workspace(int N, int M, int D, int Nc);
 int sv_ge2e_cossim(const float* E, int N, int M, int D, const float* C, int Nc, float* cos, float* workspace,
                    hipStream_t stream);
 int sv_ge2e_calc_loss(const float* S, int N, int M, int K, float* per, float* loss, hipStream_t stream);
+/* EER sweep (train_speech_embedder.py:134-149): per threshold, #{S > thr} over all of S [N,M2,Nc]
+ * and over its diagonal k == j (exact integer counts, returned as float). */
+int sv_eer_counts(const float* S, int N, int M2, int Nc, const float* thresholds, int n_thr, float* cnt_all,
+                  float* cnt_diag, hipStream_t stream);
 
 /* ---- bf16-operand variant (BASELINE config c3, mixed precision) ------------------------------
  * GEMM operands (weights, h, dgates) in bf16 (RNE casts), v_mfma_f32_32x32x16_bf16 with fp32

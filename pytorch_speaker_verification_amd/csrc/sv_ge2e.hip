@@ -513,3 +513,46 @@ extern "C" int sv_ge2e_calc_loss(const float* S, int N, int M, int K, float* per
   }
   return SV_OK;
 }
+
+// ============================================================================
+// EER threshold sweep (train_speech_embedder.py:134-149): for each threshold, the number of
+// similarities above it (all entries and the diagonal k == j).  One block per threshold;
+// integer counts, so the result is exact.
+// ============================================================================
+__global__ __launch_bounds__(256) void eer_counts_kernel(const float* __restrict__ S, int N, int M2, int Nc,
+                                                         const float* __restrict__ thr, float* __restrict__ cnt_all,
+                                                         float* __restrict__ cnt_diag) {
+  __shared__ int red[2][4];
+  const float th = thr[blockIdx.x];
+  const long total = (long)N * M2 * Nc;
+  int a = 0, d = 0;
+  for (long e = threadIdx.x; e < total; e += 256) {
+    const int k = (int)(e % Nc);
+    const int j = (int)(e / ((long)M2 * Nc));
+    const int over = S[e] > th;
+    a += over;
+    d += (over && k == j);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    d += __shfl_xor(d, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = a;
+    red[1][threadIdx.x >> 6] = d;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    cnt_all[blockIdx.x] = (float)(red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    cnt_diag[blockIdx.x] = (float)(red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
+extern "C" int sv_eer_counts(const float* S, int N, int M2, int Nc, const float* thresholds, int n_thr,
+                             float* cnt_all, float* cnt_diag, hipStream_t stream) {
+  if (!S || !thresholds || !cnt_all || !cnt_diag || N <= 0 || M2 <= 0 || Nc < N || n_thr <= 0) return SV_EARG;
+  hipLaunchKernelGGL(eer_counts_kernel, dim3(n_thr), dim3(256), 0, stream, S, N, M2, Nc, thresholds, cnt_all, cnt_diag);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}

@@ -1,0 +1,65 @@
+"""Segment-level d-vectors for diarisation (reference dvector_create.py:38-73).
+
+The reference turns each VAD-concatenated segment's log-mel spectrogram [nmels, T] into
+24-frame windows at a 12-frame hop (0.24 s / 0.12 s, :48-52), embeds all windows with the
+SpeechEmbedder (:100) and averages consecutive window embeddings into ~0.4 s segments
+(align_embeddings, :55-73).  Audio I/O, VAD (webrtcvad) and the STFT (librosa) stay out of
+scope; this module starts from the log-mel frames.  The embedding is the short-sequence,
+large-batch forward of the same HIP LSTM kernels (T = 24).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .ops import embedder_forward
+
+WIN, HOP = 24, 12  # frames: int(.24/.01), int(.12/.01)
+
+
+def window_frames(logmel, win=WIN, hop=HOP):
+    """[nmels, T] -> [S, win, nmels]: windows starting every `hop` frames while j + win < T
+    (the strict '<' of dvector_create.py:50 drops a window that would end exactly at T)."""
+    logmel = np.asarray(logmel)
+    starts = [j for j in range(0, logmel.shape[1], hop) if j + win < logmel.shape[1]]
+    if not starts:
+        return np.zeros((0, win, logmel.shape[0]), dtype=np.float32)
+    return np.stack([logmel[:, j:j + win].T for j in starts]).astype(np.float32)
+
+
+@torch.no_grad()
+def embed_windows(net, windows, batch=16384):
+    """Embeddings [S, proj] of windows [S, win, nmels] with the module's weights (GPU)."""
+    dev = next(net.parameters()).device
+    layers = net.LSTM_stack.layer_params()
+    out = []
+    x = torch.as_tensor(windows, dtype=torch.float32)
+    for i in range(0, x.shape[0], batch):
+        xb = x[i:i + batch].to(dev).contiguous()
+        emb, _ = embedder_forward(xb, layers, net.projection.weight, net.projection.bias, save=False)
+        out.append(emb)
+    return torch.cat(out) if out else torch.zeros((0, net.projection.weight.shape[0]), device=dev)
+
+
+def partitions(n_windows, win_s=0.24, hop_s=0.12, seg_s=0.401):
+    """[start, end) window ranges averaged into one segment (dvector_create.py:56-69): a window i
+    joins segment j while it ends (i*hop + win) before j*seg; the loop's else appends the last."""
+    parts, start, end, j = [], 0, 0, 1
+    for i in range(n_windows):
+        if i * hop_s + win_s < j * seg_s:
+            end += 1
+        else:
+            parts.append((start, end))
+            start, end, j = end, end + 1, j + 1
+    parts.append((start, end))
+    return parts
+
+
+def align_embeddings(embeddings):
+    """Average window embeddings over partitions() -> [n_segments, D] float64 (:55-73)."""
+    e = np.asarray(embeddings)
+    parts = partitions(len(e))
+    out = np.zeros((len(parts), e.shape[1]))
+    for i, (a, b) in enumerate(parts):
+        out[i] = np.average(e[a:b], axis=0)
+    return out

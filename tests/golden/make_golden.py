@@ -114,6 +114,81 @@ def train_steps(ref_net, ref_hparam, dims, wseed, wscale, xseed, N, M, T, steps,
     return rec
 
 
+def eer_and_loader_fixtures(ref_hparam, ref_net):
+    import contextlib
+    import io
+    import random
+    import tempfile
+    import torch
+    hp = ref_hparam.hparam
+    sys.path.insert(0, REF)
+    cwd = os.getcwd()
+    os.chdir(REF)
+    try:
+        import data_load as ref_data
+        import train_speech_embedder as ref_train
+    finally:
+        os.chdir(cwd)
+    tmp = tempfile.mkdtemp(prefix="sv_golden_")
+    recipe.make_speaker_dir(os.path.join(tmp, "test"), 12, 77)
+    saved = {k: dict(v) for k, v in hp.items() if isinstance(v, dict)}
+    saved_top = {k: v for k, v in hp.items() if not isinstance(v, dict)}
+    try:
+        hp.training = False
+        hp.data.test_path = os.path.join(tmp, "test")
+        hp.data.train_path = os.path.join(tmp, "test")
+        hp.test.N, hp.test.M, hp.test.epochs, hp.test.num_workers = 4, 6, 2, 0
+        hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj = 40, 64, 3, 32
+        # (1) the preprocessed dataset under fixed seeds: shuffle=True and shuffle=False items
+        random.seed(123)
+        np.random.seed(123)
+        ds = ref_data.SpeakerDatasetTIMITPreprocessed()
+        files = sorted(os.listdir(hp.data.test_path))
+        items = [ds[i].numpy() for i in range(3)]
+        ds2 = ref_data.SpeakerDatasetTIMITPreprocessed(shuffle=False, utter_start=1)
+        items_ns = [ds2[i].numpy() for i in range(2)]
+        np.savez_compressed(os.path.join(HERE, "loader.npz"), seed=123, M=6, n_spk=12, data_seed=77,
+                            listdir=np.array(os.listdir(hp.data.test_path)), sorted_files=np.array(files),
+                            items=np.stack(items), items_noshuffle=np.stack(items_ns))
+        # (2) test(): EER on the synthetic test set with a recipe-weight checkpoint
+        net = ref_net.SpeechEmbedder()
+        sd = recipe.make_weights(41, 40, 64, 3, 32, scale=3.0)
+        net.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+        ckpt = os.path.join(tmp, "model.model")
+        torch.save(net.state_dict(), ckpt)
+        sims = []
+        orig = ref_train.get_cossim
+
+        def rec(a, b):
+            out = orig(a, b)
+            sims.append(out.detach().numpy().copy())
+            return out
+        ref_train.get_cossim = rec
+        random.seed(5)
+        np.random.seed(5)
+        torch.manual_seed(5)
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            ref_train.test(ckpt)
+        ref_train.get_cossim = orig
+        lines = [ln for ln in buf.getvalue().splitlines() if ln.startswith("EER")]
+        vals = np.array([[float(x) for x in
+                          ln.replace("EER :", "").replace("(thres:", " ").replace("FAR:", " ").replace("FRR:", " ")
+                          .replace(")", " ").replace(",", " ").split()] for ln in lines])
+        avg = float(buf.getvalue().strip().splitlines()[-1].split(":")[-1])
+        np.savez_compressed(os.path.join(HERE, "eer.npz"), sims=np.stack(sims), printed=vals, avg_eer=avg,
+                            wseed=41, dims=np.array([40, 64, 3, 32]), data_seed=77, n_spk=12, N=4, M=6, epochs=2,
+                            seed=5)
+        torch.save(net.state_dict(), os.path.join(HERE, "ref_small_checkpoint.pth"))
+        print("eer fixture: batches", len(sims), "avg", avg)
+    finally:
+        for k, v in saved.items():
+            hp[k].update(v)
+        for k, v in saved_top.items():
+            hp[k] = v
+        os.chdir(cwd)
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference not present; nothing to do")
@@ -209,6 +284,9 @@ def main():
         hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj = old
     np.savez_compressed(os.path.join(HERE, "init_seed1234.npz"),
                         **{k: v.detach().numpy() for k, v in net.state_dict().items()})
+
+    # ---- data loader + EER evaluation (train_speech_embedder.py:92-154) ---------
+    eer_and_loader_fixtures(ref_hparam, ref_net)
 
     # ---- the parsed config -----------------------------------------------------
     hp = ref_hparam.hparam

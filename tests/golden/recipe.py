@@ -66,3 +66,16 @@ def make_embeddings(seed: int, n: int, m: int, d: int, clustered: bool = True):
         e = rng.standard_normal((n, m, d))
     e = e / np.linalg.norm(e, axis=2, keepdims=True)
     return e.astype(np.float32)
+
+
+def make_speaker_dir(root, n_spk, seed):
+    """Synthetic preprocessed TIMIT-style data: speakerK.npy = [utterances, 40 mels, 180 frames]
+    (the data_preprocess.py:46-54 on-disk format)."""
+    import os
+    rng = np.random.default_rng(seed)
+    os.makedirs(root, exist_ok=True)
+    for k in range(n_spk):
+        n_utt = int(rng.integers(8, 14))
+        base = rng.standard_normal((1, 40, 1)) * 2.0
+        u = (base + rng.standard_normal((n_utt, 40, 180))).astype(np.float32)
+        np.save(os.path.join(root, f"speaker{k}.npy"), u)

@@ -1,0 +1,51 @@
+"""d-vector helpers (dvector_create.py:38-73).  The reference script runs its whole pipeline at
+import time (VAD + librosa + a checkpoint), so these are pinned by hand-computed known answers
+rather than by the reference itself ("parity unpinned" beyond these cases)."""
+import numpy as np
+import pytest
+import torch
+
+from pytorch_speaker_verification_amd import dvector
+
+
+def test_window_frames_counts_and_content():
+    m = np.arange(40 * 60, dtype=np.float32).reshape(40, 60)
+    w = dvector.window_frames(m)
+    # starts 0,12,24 (24+24=48<60); 36+24=60 is not < 60 -> stops
+    assert w.shape == (3, 24, 40)
+    np.testing.assert_array_equal(w[1], m[:, 12:36].T)
+    assert dvector.window_frames(np.zeros((40, 24))).shape == (0, 24, 40)
+
+
+def test_partitions_known_answer():
+    # window i ends at 0.12 i + 0.24; segment j closes at 0.401 j
+    assert dvector.partitions(6) == [(0, 2), (2, 5), (5, 6)]
+    assert dvector.partitions(1) == [(0, 1)]
+    e = np.arange(12, dtype=np.float64).reshape(6, 2)
+    np.testing.assert_allclose(dvector.align_embeddings(e), [[1, 2], [6, 7], [10, 11]])
+
+
+@pytest.mark.gpu
+def test_embed_windows_short_sequence_large_batch():
+    """T = 24 windows, thousands at once (the inference point of the kernel design space),
+    against the stock-PyTorch port."""
+    import recipe
+    from conftest import model_dims
+    from oracle import torch_port
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    dims = (40, 768, 3, 256)
+    sd = recipe.make_weights(9, *dims, scale=2.0)
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    net = net.cuda()
+    port = torch_port.SpeechEmbedderPort(*dims)
+    torch_port.load_recipe_weights(port, sd)
+    port = port.cuda()
+    x = recipe.make_frames(10, 3000, 24, 40)
+    e = dvector.embed_windows(net, x, batch=1024).cpu().numpy()
+    with torch.no_grad():
+        er = port(torch.tensor(x).cuda()).cpu().numpy()
+    np.testing.assert_allclose(e, er, atol=5e-5)

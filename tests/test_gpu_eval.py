@@ -1,0 +1,108 @@
+"""GPU: the EER sweep kernel (exact counts) and the drop-in test()/train() drivers end to end
+on synthetic preprocessed data, against the reference's own run (tests/golden/eer.npz)."""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+import recipe
+from conftest import golden
+from oracle import eer_np
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def test_eer_kernel_exact():
+    from pytorch_speaker_verification_amd.train_speech_embedder import eer_from_sim
+    e = golden("eer.npz")
+    for sim in e["sims"]:
+        got = eer_from_sim(torch.tensor(sim, device=DEV))
+        ref = eer_np.eer(sim)
+        assert got[1] == ref[1] and got[0] == ref[0] and got[2] == ref[2] and got[3] == ref[3]
+    rng = np.random.default_rng(3)
+    for N, M2 in [(4, 3), (16, 5), (64, 5)]:
+        sim = rng.uniform(0.3, 1.0, (N, M2, N)).astype(np.float32)
+        assert eer_from_sim(torch.tensor(sim, device=DEV)) == eer_np.eer(sim)
+
+
+def _hp_setup(hp, tmp, g):
+    saved = {k: dict(v) for k, v in hp.items() if isinstance(v, dict)}
+    saved_top = {k: v for k, v in hp.items() if not isinstance(v, dict)}
+    hp.device = "cuda"
+    hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj = [int(v) for v in g["dims"]]
+    return saved, saved_top
+
+
+def _hp_restore(hp, saved, saved_top):
+    for k, v in saved.items():
+        hp[k].update(v)
+    for k, v in saved_top.items():
+        hp[k] = v
+
+
+def test_test_driver_matches_reference(tmp_path, monkeypatch):
+    """Same synthetic data, checkpoint and seeds as the reference's test() run: identical batches
+    (RNG parity), per-batch similarity matrices within fp32 noise, same EER selection."""
+    from pytorch_speaker_verification_amd import train_speech_embedder as tse
+    from pytorch_speaker_verification_amd.hparam import hparam as hp
+    g = golden("eer.npz")
+    lg = golden("loader.npz")
+    d = tmp_path / "test"
+    recipe.make_speaker_dir(str(d), int(g["n_spk"]), int(g["data_seed"]))
+    order = [str(x) for x in lg["listdir"]]
+    real = os.listdir
+    monkeypatch.setattr(os, "listdir", lambda p=".": order if os.path.abspath(p) == str(d) else real(p))
+    ckpt = os.path.join(os.path.dirname(__file__), "golden", "ref_small_checkpoint.pth")
+    saved, saved_top = _hp_setup(hp, tmp_path, g)
+    sims = []
+    orig = tse.get_cossim
+    monkeypatch.setattr(tse, "get_cossim", lambda a, b: sims.append(orig(a, b)) or sims[-1])
+    try:
+        hp.training = False
+        hp.data.test_path = str(d)
+        hp.test.N, hp.test.M, hp.test.epochs, hp.test.num_workers = int(g["N"]), int(g["M"]), int(g["epochs"]), 0
+        random.seed(int(g["seed"]))
+        np.random.seed(int(g["seed"]))
+        torch.manual_seed(int(g["seed"]))
+        avg = tse.test(ckpt)
+    finally:
+        _hp_restore(hp, saved, saved_top)
+    got = np.stack([s.cpu().numpy() for s in sims])
+    np.testing.assert_allclose(got, g["sims"], atol=2e-5)
+    assert abs(avg - float(g["avg_eer"])) < 2e-2
+
+
+def test_train_driver_runs_and_checkpoints(tmp_path):
+    from pytorch_speaker_verification_amd import train_speech_embedder as tse
+    from pytorch_speaker_verification_amd.hparam import hparam as hp
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    g = golden("eer.npz")
+    d = tmp_path / "train"
+    recipe.make_speaker_dir(str(d), 12, 5)
+    saved, saved_top = _hp_setup(hp, tmp_path, g)
+    try:
+        hp.training = True
+        hp.data.train_path = str(d)
+        hp.train.N, hp.train.M, hp.train.epochs, hp.train.num_workers = 4, 5, 4, 0
+        hp.train.log_interval, hp.train.checkpoint_interval = 1, 2
+        hp.train.checkpoint_dir = str(tmp_path / "ckpt")
+        hp.train.log_file = str(tmp_path / "ckpt" / "Stats")
+        hp.train.restore = False
+        torch.manual_seed(0)
+        path = tse.train(str(tmp_path / "none.model"))
+        files = sorted(os.listdir(hp.train.checkpoint_dir))
+        sd = torch.load(path, weights_only=True)
+        net = SpeechEmbedder()
+        net.load_state_dict(sd)
+        lines = open(hp.train.log_file).read().strip().splitlines()
+    finally:
+        _hp_restore(hp, saved, saved_top)
+    assert "ckpt_epoch_2_batch_id_3.pth" in files and "ckpt_epoch_4_batch_id_3.pth" in files
+    assert os.path.basename(path) == "final_epoch_4_batch_id_3.model"
+    assert len(lines) == 12 and "Epoch:1[1/3],Iteration:1" in lines[0]
+    first = float(lines[0].split("Loss:")[1].split()[0])
+    last = float(lines[-1].split("Loss:")[1].split()[0])
+    assert np.isfinite(last) and last < first
