@@ -72,6 +72,17 @@ int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float* x_tm, cons
                       float* const* gates, float* const* c_tm, float* const* h_tm, float* const* hT, int chunk,
                       hipStream_t main, const hipStream_t* side, hipEvent_t* ev);
 size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H);
+/* Whole-stack backward, layer-pipelined over streams (top layer first): each layer's reverse
+ * chunks of steps, then (l > 0) the chunk's dx = dG W_ih GEMM that feeds layer l-1, then its
+ * weight-gradient GEMMs.  xT/ld_xT: per-layer transposed inputs; dx[l] [T,B,H] for l > 0;
+ * ev = L*ceil(T/chunk) + L + 1 caller events; joins back into `main`. */
+size_t sv_lstm_stack_bwd_workspace(int L, int T, int B, int F, int H);
+int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float* const* xT, const long* ld_xT,
+                      const float* const* w_ih, const float* const* w_hh, const float* const* gates,
+                      const float* const* c_tm, const float* const* hT, const float* dh_last, float* const* dgates,
+                      float* const* dgT, float* const* dx, float* const* dw_ih, float* const* dw_hh,
+                      float* const* db_ih, float* const* db_hh, float* workspace, int chunk, hipStream_t main,
+                      const hipStream_t* side, hipEvent_t* ev);
 /* xT: the layer input transposed, [F, >= T*Bp] with row stride ld_xT (layer 0: the frames;
  * layer l > 0: hT of layer l-1 offset by Bp columns).  hT: this layer's [H, (T+1)Bp] from the fwd.
  * dh_up: gradient w.r.t. this layer's outputs; dh_up_full=1 -> [T,B,H], 0 -> [B,H] for t=T-1 only.
@@ -154,6 +165,16 @@ int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const sv_bf16* xT_bf, lon
                            const float* dh_up, int dh_up_full, sv_bf16* dg_bf, sv_bf16* dgT_bf, float* dx_tm,
                            float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, float* workspace,
                            hipStream_t stream);
+
+/* layer-pipelined stack backward in bf16 (as sv_lstm_stack_bwd; fp32 master weights are
+ * transpose-cast per call; dg/dgT per layer bf16) */
+size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H);
+int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* const* xT, const long* ld_xT,
+                           const float* const* w_ih, const float* const* w_hh, const float* const* gates,
+                           const float* const* c_tm, const sv_bf16* const* hT, const float* dh_last,
+                           sv_bf16* const* dg, sv_bf16* const* dgT, float* const* dx, float* const* dw_ih,
+                           float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace, int chunk,
+                           hipStream_t main, const hipStream_t* side, hipEvent_t* ev);
 
 /* ---- clip_grad_norm_ + SGD step over one flat parameter group (train_speech_embedder.py:63-65)
  * p -= lr * min(1, max_norm / (|g|_2 + 1e-6)) * g; write_grad=1 also scales g in place. */

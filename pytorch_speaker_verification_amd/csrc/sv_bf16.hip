@@ -340,6 +340,7 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_bf16_kernel(
   }
 }
 
+template <int SC>
 __global__ __launch_bounds__(512) void lstm_step_bwd_bf16_kernel(
     const bf16_t* __restrict__ dgnext, const bf16_t* __restrict__ whhT, const float* __restrict__ dhup,
     const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
@@ -373,7 +374,7 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_bf16_kernel(
   f32x16 acc[1][1];
   zero_acc(acc);
   if (dgnext)
-    gemm_mainloop_bf_rp<BF_BM, BF_U, 128, 6, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
+    gemm_mainloop_bf_rp<BF_BM, BF_U, 128, SC, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
                                                    RowMapLinear{j0, H}, gate * H, (gate + 1) * H, ldsb + gate * GBUF,
                                                    gt, (w & 1) * 32, 0, acc);
   __syncthreads();
@@ -471,7 +472,7 @@ constexpr int BBWD_LDS = BBWD_LDS_MAIN > BBWD_LDS_EPI ? BBWD_LDS_MAIN : BBWD_LDS
 int bf16_sc() {
   static int v = [] {
     const char* e = getenv("SV_BF16_SC");
-    const int x = e ? atoi(e) : 12;
+    const int x = e ? atoi(e) : 3;
     return (x == 3 || x == 4 || x == 6) ? x : 12;
   }();
   return v;
@@ -491,6 +492,29 @@ void launch_fwd_bf16(dim3 grid, hipStream_t s, const bf16_t* hp, const bf16_t* w
   else
     hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<12>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
                        t, Bp, B, H);
+}
+
+int bf16_bsc() {
+  static int v = [] {
+    const char* e = getenv("SV_BF16_BSC");
+    const int x = e ? atoi(e) : 6;
+    return (x == 2 || x == 3) ? x : 6;
+  }();
+  return v;
+}
+void launch_bwd_bf16(dim3 grid, hipStream_t s, const bf16_t* dgn, const bf16_t* whhT, const float* up,
+                     const float* dcfi, const float* acts, const float* ct, const float* cp, bf16_t* dg, float* dcfo,
+                     bf16_t* dgT, long lddgT, int t, int Bp, int B, int H) {
+  const int sc = bf16_bsc();
+  if (sc == 2)
+    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<2>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
+                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  else if (sc == 3)
+    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<3>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
+                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  else
+    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<6>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
+                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
 }
 
 }  // namespace
@@ -609,9 +633,9 @@ extern "C" int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const bf16_t* 
     if (dh_up) up = dh_up_full ? dh_up + t * BH : (t == T - 1 ? dh_up : nullptr);
     float* dcf_out = (t & 1) ? dcf1 : dcf0;
     const float* dcf_in = (t == T - 1) ? nullptr : ((t & 1) ? dcf0 : dcf1);
-    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel, grid, dim3(512), BBWD_LDS, stream,
-                       t == T - 1 ? nullptr : dg_bf + (t + 1) * BG, whhT_bf, up, dcf_in, gates + t * BG, c_tm + t * BH,
-                       t ? c_tm + (t - 1) * BH : nullptr, dg_bf + t * BG, dcf_out, dgT_bf, (long)TBp, t, Bp, B, H);
+    launch_bwd_bf16(grid, stream, t == T - 1 ? nullptr : dg_bf + (t + 1) * BG, whhT_bf, up, dcf_in, gates + t * BG,
+                    c_tm + t * BH, t ? c_tm + (t - 1) * BH : nullptr, dg_bf + t * BG, dcf_out, dgT_bf, (long)TBp, t,
+                    Bp, B, H);
     SV_LAUNCH_CHECK();
   }
   const long ldhT = (long)(T + 1) * Bp;
@@ -677,5 +701,101 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
   }
   for (int l = 0; l < L; ++l)
     if ((e = hipStreamWaitEvent(main, ev[l * nch + nch - 1], 0)) != hipSuccess) return (int)e;
+  return SV_OK;
+}
+
+// Layer-pipelined stack backward, bf16 operands (see sv_lstm_stack_bwd in sv_lstm.hip).
+namespace {
+struct BBwdWs {
+  float *dcf0, *dcf1, *gws;
+  bf16_t *whhT, *wihT;
+  size_t total;
+};
+BBwdWs carve_bbwd(char* base, int T, int B, int F, int H) {
+  BBwdWs w;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off += (bytes + 255) & ~size_t(255);
+    return p;
+  };
+  w.dcf0 = (float*)take((size_t)B * H * 4);
+  w.dcf1 = (float*)take((size_t)B * H * 4);
+  w.whhT = (bf16_t*)take((size_t)4 * H * H * 2);
+  w.wihT = (bf16_t*)take((size_t)4 * H * F * 2);
+  const int TBp = T * ((B + 7) & ~7);
+  size_t g = sv_gemm_bf16_workspace(4 * H, H, TBp);
+  g = std::max(g, sv_gemm_bf16_workspace(4 * H, F, TBp));
+  g = std::max(g, sv_gemm_bf16_workspace(T * B, F, 4 * H));
+  w.gws = (float*)take(g);
+  w.total = off;
+  return w;
+}
+}  // namespace
+
+extern "C" size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H) {
+  return (size_t)L * carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
+}
+
+extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const bf16_t* const* xT, const long* ld_xT,
+                                      const float* const* w_ih, const float* const* w_hh, const float* const* gates,
+                                      const float* const* c_tm, const bf16_t* const* hT, const float* dh_last,
+                                      bf16_t* const* dg, bf16_t* const* dgT, float* const* dx, float* const* dw_ih,
+                                      float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace,
+                                      int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev) {
+  if (L <= 0 || !xT || !ld_xT || !w_ih || !w_hh || !gates || !c_tm || !hT || !dh_last || !dg || !dgT || !dx ||
+      !dw_ih || !dw_hh || !db_ih || !workspace || !side || !ev || chunk <= 0)
+    return SV_EARG;
+  if (T <= 0 || B <= 0 || F <= 0 || H <= 0 || F % 8 || H % 8) return SV_ESHAPE;
+  const int nch = (T + chunk - 1) / chunk;
+  const long BH = (long)B * H, BG = 4L * B * H;
+  const int Bp = (B + 7) & ~7;
+  const int TBp = T * Bp;
+  const long ldhT = (long)(T + 1) * Bp;
+  const size_t per = carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
+  hipEvent_t ev_start = ev[L * nch + L];
+  hipError_t e = hipEventRecord(ev_start, main);
+  if (e != hipSuccess) return (int)e;
+  const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
+  for (int l = L - 1; l >= 0; --l) {
+    hipStream_t s = side[l];
+    const int Fl = l == 0 ? F : H;
+    const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
+    if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
+    int rc = sv_transpose_cast_bf16(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, s);
+    if (rc) return rc;
+    if (l > 0 && (rc = sv_transpose_cast_bf16(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, s))) return rc;
+    if (Bp != B && (e = hipMemsetAsync(dgT[l], 0, (size_t)4 * H * TBp * sizeof(bf16_t), s)) != hipSuccess)
+      return (int)e;
+    for (int c = nch - 1; c >= 0; --c) {
+      const int t0 = c * chunk, t1 = std::min(T, t0 + chunk);
+      if (l < L - 1 && (e = hipStreamWaitEvent(s, ev[(l + 1) * nch + c], 0)) != hipSuccess) return (int)e;
+      for (int t = t1 - 1; t >= t0; --t) {
+        const float* up = (l == L - 1) ? (t == T - 1 ? dh_last : nullptr) : dx[l + 1] + t * BH;
+        float* dcf_out = (t & 1) ? ws.dcf1 : ws.dcf0;
+        const float* dcf_in = (t == T - 1) ? nullptr : ((t & 1) ? ws.dcf0 : ws.dcf1);
+        launch_bwd_bf16(grid, s, t == T - 1 ? nullptr : dg[l] + (t + 1) * BG, ws.whhT, up, dcf_in, gates[l] + t * BG,
+                        c_tm[l] + t * BH, t ? c_tm[l] + (t - 1) * BH : nullptr, dg[l] + t * BG, dcf_out, dgT[l],
+                        (long)TBp, t, Bp, B, H);
+        SV_LAUNCH_CHECK();
+      }
+      if (l > 0) {
+        rc = sv_gemm_bf16((t1 - t0) * B, Fl, 4 * H, dg[l] + t0 * BG, 4L * H, ws.wihT, 4L * H,
+                          dx[l] + (long)t0 * B * Fl, Fl, nullptr, nullptr, 0.f, ws.gws, s);
+        if (rc) return rc;
+      }
+      if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
+    }
+    rc = sv_gemm_bf16(4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws, s);
+    if (rc) return rc;
+    rc = sv_gemm_bf16(4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, ws.gws, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, s, dgT[l], (long)TBp, TBp, db_ih[l],
+                       db_hh ? db_hh[l] : nullptr);
+    SV_LAUNCH_CHECK();
+    if ((e = hipEventRecord(ev[L * nch + l], s)) != hipSuccess) return (int)e;
+  }
+  for (int l = 0; l < L; ++l)
+    if ((e = hipStreamWaitEvent(main, ev[L * nch + l], 0)) != hipSuccess) return (int)e;
   return SV_OK;
 }

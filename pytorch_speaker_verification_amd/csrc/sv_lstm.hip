@@ -871,3 +871,81 @@ extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float*
     if ((e = hipStreamWaitEvent(main, ev[l * nch + nch - 1], 0)) != hipSuccess) return (int)e;
   return SV_OK;
 }
+
+// ============================================================================
+// Layer-pipelined stack backward.  Layer l runs on side[l], top layer first in issue order:
+// its timesteps in reverse chunks of `chunk` (K3 steps, then -- for l > 0 -- the chunk's
+// dx = dG W_ih GEMM, which is the next-lower layer's dh_up for those timesteps), then its
+// dW_hh / dW_ih GEMMs and bias row sums.  Layer l-1 waits only for layer l's dx of the same
+// chunk, so one layer's (latency-bound) recurrence overlaps the upper layers' GEMMs.
+//   xT[l], ld_xT[l]: layer input transposed (layer 0: the frames; l > 0: hT[l-1] + Bp cols)
+//   dx[l] [T,B,H] for l > 0 (dh_up of layer l-1); dx[0] may be NULL
+//   workspace: L * sv_lstm_layer_bwd_workspace(T, B, max(F,H), H) bytes
+//   ev: L*ceil(T/chunk) + L + 1 caller-created events.  Joins back into `main`.
+// ============================================================================
+extern "C" size_t sv_lstm_stack_bwd_workspace(int L, int T, int B, int F, int H) {
+  return (size_t)L * ((carve_bwd(nullptr, T, B, std::max(F, H), H).total + 255) & ~size_t(255));
+}
+
+extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float* const* xT, const long* ld_xT,
+                                 const float* const* w_ih, const float* const* w_hh, const float* const* gates,
+                                 const float* const* c_tm, const float* const* hT, const float* dh_last,
+                                 float* const* dgates, float* const* dgT, float* const* dx, float* const* dw_ih,
+                                 float* const* dw_hh, float* const* db_ih, float* const* db_hh, float* workspace,
+                                 int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev) {
+  if (L <= 0 || !xT || !ld_xT || !w_ih || !w_hh || !gates || !c_tm || !hT || !dh_last || !dgates || !dgT || !dx ||
+      !dw_ih || !dw_hh || !db_ih || !workspace || !side || !ev || chunk <= 0)
+    return SV_EARG;
+  if (!lstm_dims_ok(T, B, F, H)) return SV_ESHAPE;
+  const int nch = (T + chunk - 1) / chunk;
+  const long BH = (long)B * H, BG = 4L * B * H;
+  const int Bp = (B + 3) & ~3;
+  const int TBp = T * Bp;
+  const long ldhT = (long)(T + 1) * Bp;
+  const size_t per = (carve_bwd(nullptr, T, B, std::max(F, H), H).total + 255) & ~size_t(255);
+  hipEvent_t ev_start = ev[L * nch + L];
+  hipError_t e = hipEventRecord(ev_start, main);
+  if (e != hipSuccess) return (int)e;
+  const dim3 grid((H + BWD_U - 1) / BWD_U, (B + BWD_BM - 1) / BWD_BM);
+  for (int l = L - 1; l >= 0; --l) {
+    hipStream_t s = side[l];
+    const int Fl = l == 0 ? F : H;
+    const BwdWs ws = carve_bwd((float*)((char*)workspace + per * l), T, B, std::max(F, H), H);
+    if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
+    int rc = sv_transpose(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, s);
+    if (rc) return rc;
+    if (l > 0 && (rc = sv_transpose(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, s))) return rc;
+    if (Bp != B && (e = hipMemsetAsync(dgT[l], 0, (size_t)4 * H * TBp * sizeof(float), s)) != hipSuccess) return (int)e;
+    for (int c = nch - 1; c >= 0; --c) {
+      const int t0 = c * chunk, t1 = std::min(T, t0 + chunk);
+      if (l < L - 1 && (e = hipStreamWaitEvent(s, ev[(l + 1) * nch + c], 0)) != hipSuccess) return (int)e;
+      for (int t = t1 - 1; t >= t0; --t) {
+        const float* up = (l == L - 1) ? (t == T - 1 ? dh_last : nullptr) : dx[l + 1] + t * BH;
+        float* dcf_out = (t & 1) ? ws.dcf1 : ws.dcf0;
+        const float* dcf_in = (t == T - 1) ? nullptr : ((t & 1) ? ws.dcf0 : ws.dcf1);
+        launch_bwd_step(grid, s, t == T - 1 ? nullptr : dgates[l] + (t + 1) * BG, ws.whhT, up, dcf_in,
+                        gates[l] + t * BG, c_tm[l] + t * BH, t ? c_tm[l] + (t - 1) * BH : nullptr, dgates[l] + t * BG,
+                        dcf_out, dgT[l], (long)TBp, t, Bp, B, H);
+        SV_LAUNCH_CHECK();
+      }
+      if (l > 0) {  // dh_up of layer l-1 for this chunk: dx = dG W_ih
+        rc = sv_gemm_f32(1, 1, (t1 - t0) * B, Fl, 4 * H, dgates[l] + t0 * BG, 4L * H, ws.wihT, 4L * H,
+                         dx[l] + (long)t0 * B * Fl, Fl, nullptr, nullptr, 0.f, ws.gws, s);
+        if (rc) return rc;
+      }
+      if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
+    }
+    rc = sv_gemm_f32(1, 1, 4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws, s);
+    if (rc) return rc;
+    rc = sv_gemm_f32(1, 1, 4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, ws.gws,
+                     s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(256), 0, s, dgT[l], (long)TBp, TBp, db_ih[l],
+                       db_hh ? db_hh[l] : nullptr);
+    SV_LAUNCH_CHECK();
+    if ((e = hipEventRecord(ev[L * nch + l], s)) != hipSuccess) return (int)e;
+  }
+  for (int l = 0; l < L; ++l)
+    if ((e = hipStreamWaitEvent(main, ev[L * nch + l], 0)) != hipSuccess) return (int)e;
+  return SV_OK;
+}

@@ -18,7 +18,7 @@ import torch
 
 from ._lib import call, ptr, require_device, stream_of, lib
 
-PIPELINE_CHUNK = int(os.environ.get("SV_PIPELINE_CHUNK", "16"))  # 0 disables the layer pipeline
+PIPELINE_CHUNK = int(os.environ.get("SV_PIPELINE_CHUNK", "32"))  # 0 disables the layer pipeline
 
 
 class _StreamPool:
@@ -156,9 +156,29 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False):
     call("sv_proj_norm_bwd", ptr(demb), ptr(st.emb), ptr(st.ynorm), ptr(st.h_last), B, H, P, ptr(w_p),
          ptr(grads[4 * L]), ptr(grads[4 * L + 1]), ptr(dh_last), ptr(ws), s)
     Fmax = max(st.x_tm[l].shape[2] for l in range(L))
+    Bp = (B + 3) // 4 * 4
+    if PIPELINE_CHUNK > 0 and L > 1 and not need_dx:
+        F0 = st.x_tm[0].shape[2]
+        ws = _ws(lib().sv_lstm_stack_bwd_workspace(L, T, B, F0, H), dev)
+        dgs = [torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev) for _ in range(L)]
+        dgTs = [torch.empty((4 * H, T * Bp), dtype=torch.float32, device=dev) for _ in range(L)]
+        dxs = [None] + [torch.empty((T, B, H), dtype=torch.float32, device=dev) for _ in range(L - 1)]
+        xT = [ptr(st.xT0)] + [ptr(st.hT[l - 1]) + Bp * 4 for l in range(1, L)]
+        ld = [T * Bp] + [(T + 1) * Bp] * (L - 1)
+        nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
+        nev = L * nch + L + 1
+        streams, events = _StreamPool.get(dev, L, nev)
+        sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
+        ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
+        call("sv_lstm_stack_bwd", L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
+             _parr([l[0] for l in layers]), _parr([l[1] for l in layers]), _parr(st.gates), _parr(st.c_tm),
+             _parr(st.hT), ptr(dh_last), _parr(dgs), _parr(dgTs), _parr(dxs),
+             _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
+             _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
+             PIPELINE_CHUNK, s, sp, ep)
+        return grads
     ws = _ws(lib().sv_lstm_layer_bwd_workspace(T, B, Fmax, H), dev)
     dgates = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
-    Bp = (B + 3) // 4 * 4
     dgT = torch.empty((4 * H, T * Bp), dtype=torch.float32, device=dev)
     dh_up, full = dh_last, 0
     dx_out = None
@@ -271,6 +291,26 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None):
     call("sv_proj_norm_bwd", ptr(demb), ptr(st.emb), ptr(st.ynorm), ptr(st.h_last), B, H, P, ptr(w_p),
          ptr(grads[4 * L]), ptr(grads[4 * L + 1]), ptr(dh_last), ptr(ws), s)
     Fmax = max(st.x_tm[l].shape[2] for l in range(L))
+    if PIPELINE_CHUNK > 0 and L > 1:
+        F0 = st.x_tm[0].shape[2]
+        ws = _ws(lib().sv_lstm_stack_bwd_bf16_workspace(L, T, B, F0, H), dev)
+        dgs = [_bf((T, B, 4 * H), dev) for _ in range(L)]
+        dgTs = [_bf((4 * H, T * Bp), dev) for _ in range(L)]
+        dxs = [None] + [torch.empty((T, B, H), dtype=torch.float32, device=dev) for _ in range(L - 1)]
+        xT = [ptr(st.xT0)] + [ptr(st.hT[l - 1]) + Bp * 2 for l in range(1, L)]
+        ld = [T * Bp] + [(T + 1) * Bp] * (L - 1)
+        nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
+        nev = L * nch + L + 1
+        streams, events = _StreamPool.get(dev, L, nev)
+        sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
+        ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
+        call("sv_lstm_stack_bwd_bf16", L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
+             _parr([l[0] for l in layers]), _parr([l[1] for l in layers]), _parr(st.gates), _parr(st.c_tm),
+             _parr(st.hT), ptr(dh_last), _parr(dgs), _parr(dgTs), _parr(dxs),
+             _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
+             _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
+             PIPELINE_CHUNK, s, sp, ep)
+        return grads
     ws = _ws(lib().sv_lstm_layer_bwd_bf16_workspace(T, B, Fmax, H), dev)
     dg = _bf((T, B, 4 * H), dev)
     dgT = _bf((4 * H, T * Bp), dev)
