@@ -149,6 +149,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fwd-steps", type=int, default=5)
     ap.add_argument("--no-bf16", action="store_true", help="skip the config-c3 (bf16 operands) side measurement")
+    ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32",
+                    help="precision of the headline line (default f32 = BASELINE configs[1]; bf16 = configs[2])")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -159,13 +161,14 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from pytorch_speaker_verification_amd.ops import embedder_forward
+    from pytorch_speaker_verification_amd.ops import embedder_forward, embedder_forward_bf16
     from pytorch_speaker_verification_amd.trainer import GE2ETrainer
 
     dims = (40, 768, 3, 256)
     N, M, T = args.N, args.M, args.T
     B = N * M
     net, ge2e = build_model(dims, dev)
+    net.precision = args.dtype
     tr = GE2ETrainer(net, ge2e, lr=0.01)
     g = torch.Generator(device="cpu").manual_seed(1234 + 1 + rank)   # SURVEY §8d seed 1234 + config index
     x = torch.randn(B, T, dims[0], generator=g).to(dev)
@@ -191,13 +194,14 @@ def main():
 
     # forward-only (inference) embeddings/s
     layers = net.LSTM_stack.layer_params()
+    fwd_fn = embedder_forward_bf16 if args.dtype == "bf16" else embedder_forward
     with torch.no_grad():
         for _ in range(2):
-            embedder_forward(x, layers, net.projection.weight, net.projection.bias, save=False)
+            fwd_fn(x, layers, net.projection.weight, net.projection.bias, save=False)
         barrier()
         tf0 = time.perf_counter()
         for _ in range(args.fwd_steps):
-            embedder_forward(x, layers, net.projection.weight, net.projection.bias, save=False)
+            fwd_fn(x, layers, net.projection.weight, net.projection.bias, save=False)
         barrier()
         tf = (time.perf_counter() - tf0) / args.fwd_steps
 
@@ -214,7 +218,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": args.dtype,
         "data": "synthetic x~N(0,1) frames, reference init (torch.manual_seed(0))",
         "config": {"workload": f"GE2E train step N={N}xM={M} per GPU, T={T}, 40 mels, LSTM 3x768, proj 256",
                    "global_batch": world * B, "speakers_global": world * N, "seq_len": T,
@@ -223,9 +227,10 @@ def main():
         "fwd_embeddings_per_sec": round(world * B / tf, 1),
         "loss": round(final_loss, 5),
         "step_tflops": round(st_fl / (ms_step * 1e-3) / 1e12, 2),
-        "step_mfma_frac": round(st_fl / (ms_step * 1e-3) / 1e12 / MI355X_FP32_MFMA_TFLOPS, 4),
+        "step_mfma_frac": round(st_fl / (ms_step * 1e-3) / 1e12 /
+                                (MI355X_FP32_MFMA_TFLOPS if args.dtype == "f32" else MI355X_BF16_MFMA_TFLOPS), 4),
     }
-    if not args.no_bf16:
+    if not args.no_bf16 and args.dtype == "f32":
         # BASELINE config c3: same workload, bf16 GEMM operands (fp32 accumulate/state/loss)
         net16, ge16 = build_model(dims, dev)
         net16.precision = "bf16"
