@@ -113,6 +113,111 @@ def pmc_traffic(kernel):
         return None
 
 
+def _timed(f, dev, reps):
+    s = torch.cuda.current_stream(dev)
+    f()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        f()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def hbm_kernels(tr, N, M, D, dev, reps=50):
+    """The HBM-bound kernels of the step, HIP events on their stream:
+    GE2E fwd+bwd (algorithmic bytes 3*B*D*4: read E twice, write dE) and clip+SGD over the
+    flat parameter buffer (read g, read p, write p)."""
+    g = torch.Generator(device="cpu").manual_seed(9)
+    E = torch.nn.functional.normalize(torch.randn(N, M, D, generator=g), dim=2).to(dev)
+    w, b = tr.loss_mod.w, tr.loss_mod.b
+
+    def ge2e():
+        _, _, st = tr.ge2e.forward(E, w, b)
+        tr.ge2e.backward(st, w, b)
+    ms_ge = _timed(ge2e, dev, reps)
+    by_ge = 3.0 * N * M * D * 4
+    n = tr.n_pad
+    pc, gc = tr.flat_p[:n].clone(), tr.flat_g[:n].clone().mul_(1e-3)
+    from pytorch_speaker_verification_amd.ops import clip_sgd_step_
+    ms_cl = _timed(lambda: clip_sgd_step_(pc, gc, 3.0, 0.0, False), dev, reps)
+    by_cl = 3.0 * n * 4
+    r = lambda by, ms: round(by / (ms * 1e-3) / 1e9, 1)  # noqa: E731
+    return {"ge2e_fwd_bwd": {"avg_us": round(ms_ge * 1e3, 2), "algorithmic_bytes": by_ge,
+                             "achieved_GBps": r(by_ge, ms_ge), "peak_GBps": MI355X_HBM_GBPS,
+                             "note": "launch-latency bound at this size (SURVEY §8d)"},
+            "clip_sgd": {"avg_us": round(ms_cl * 1e3, 2), "algorithmic_bytes": by_cl,
+                         "achieved_GBps": r(by_cl, ms_cl), "peak_GBps": MI355X_HBM_GBPS}}
+
+
+def _ge2e_torch(E, w, b):
+    """Plain torch GE2E loss (vectorised, autograd) for the vendor-library baseline."""
+    N, M, D = E.shape
+    C = E.mean(1)
+    U = (E.sum(1, keepdim=True) - E) / (M - 1)
+    nrm = lambda v: v / v.norm(dim=-1, keepdim=True).clamp_min(1e-8)  # noqa: E731
+    En = nrm(E)
+    cos = torch.einsum("nmd,kd->nmk", En, nrm(C))
+    diag = (En * nrm(U)).sum(2)
+    eye = torch.eye(N, device=E.device, dtype=torch.bool).unsqueeze(1)
+    cos = torch.where(eye, diag.unsqueeze(2), cos) + 1e-6
+    S = w * cos + b
+    pos = S.diagonal(dim1=0, dim2=2).transpose(0, 1)
+    return (torch.log(torch.exp(S).sum(2) + 1e-6) - pos).sum()
+
+
+def vendor_baseline(dims, N, M, T, dev, steps=3):
+    """Stock torch-ROCm on the same GPU: nn.LSTM (MIOpen RNN) + Linear + torch GE2E, autograd,
+    clip_grad_norm_ x2, SGD -- the reference's training step run by the vendor libraries."""
+    F, H, L, P = dims
+    try:
+        torch.manual_seed(0)
+        lstm = torch.nn.LSTM(F, H, num_layers=L, batch_first=True).to(dev)
+        proj = torch.nn.Linear(H, P).to(dev)
+        w = torch.nn.Parameter(torch.tensor(10.0, device=dev))
+        b = torch.nn.Parameter(torch.tensor(-5.0, device=dev))
+        net_params = list(lstm.parameters()) + list(proj.parameters())
+        opt = torch.optim.SGD([{"params": net_params}, {"params": [w, b]}], lr=0.01)
+        g = torch.Generator(device="cpu").manual_seed(1235)
+        x = torch.randn(N * M, T, F, generator=g).to(dev)
+
+        def step():
+            opt.zero_grad()
+            y, _ = lstm(x)
+            e = proj(y[:, -1])
+            e = e / e.norm(dim=1, keepdim=True)
+            loss = _ge2e_torch(e.view(N, M, P), w, b)
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(net_params, 3.0)
+            torch.nn.utils.clip_grad_norm_([w, b], 1.0)
+            opt.step()
+            return loss
+        step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        return {"value": round(N * M / dt, 3), "unit": "embeddings/s", "ms_per_step": round(dt * 1e3, 3),
+                "kind": "torch-rocm nn.LSTM (MIOpen) + autograd, fp32, same GPU",
+                "torch": torch.__version__}
+    except Exception as ex:  # report, never fail the bench on the vendor leg
+        return {"error": f"{type(ex).__name__}: {ex}"[:300]}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(dims, N, M, T, seconds_budget=25.0):
     """The reference's CPU path (stock PyTorch port, oracle/torch_port.py) on host cores,
     one full training step of the same workload (bounded sample)."""
@@ -133,6 +238,7 @@ def cpu_baseline(dims, N, M, T, seconds_budget=25.0):
     torch_port.train_step(net, w, b, opt, x, N, M)
     dt = time.perf_counter() - t0
     return {"value": round(N * M / dt, 3), "unit": "embeddings/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(),
             "steps_per_sec": round(1.0 / dt, 5), "sec_per_step": round(dt, 3),
             "sample": f"1 full training step (fwd+GE2E+bwd+clip+SGD) of N={N}xM={M}, T={T}, fp32, "
                       f"oracle/torch_port.py (nn.LSTM on oneDNN), {threads} threads"}
@@ -149,6 +255,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fwd-steps", type=int, default=5)
     ap.add_argument("--no-bf16", action="store_true", help="skip the config-c3 (bf16 operands) side measurement")
+    ap.add_argument("--no-vendor", action="store_true", help="skip the nn.LSTM/MIOpen same-GPU baseline")
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32",
                     help="precision of the headline line (default f32 = BASELINE configs[1]; bf16 = configs[2])")
     args = ap.parse_args()
@@ -271,6 +378,10 @@ def main():
                                        "unit": "TFLOP/s", "frac": round(ach_k / MI355X_FP32_MFMA_TFLOPS, 4),
                                        "traffic": pmc_traffic("lstm_step_fwd_v2_kernel"),
                                        "avg_launch_us": round(ms_k * 1e3, 2), "flops_per_launch": fl_k}
+        if world == 1:  # (the GE2E leg would issue collectives on rank 0 alone otherwise)
+            out["hbm_kernels"] = hbm_kernels(tr, N, M, dims[3], dev)
+        if not args.no_vendor and world == 1:
+            out["vendor_baseline"] = vendor_baseline(dims, N, M, T, dev)
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(dims, N, M, T)
         print(json.dumps(out), flush=True)

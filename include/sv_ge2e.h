@@ -73,9 +73,12 @@ int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float* x_tm, cons
                       hipStream_t main, const hipStream_t* side, hipEvent_t* ev);
 size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H);
 /* Whole-stack backward, layer-pipelined over streams (top layer first): each layer's reverse
- * chunks of steps, then (l > 0) the chunk's dx = dG W_ih GEMM that feeds layer l-1, then its
- * weight-gradient GEMMs.  xT/ld_xT: per-layer transposed inputs; dx[l] [T,B,H] for l > 0;
- * ev = L*ceil(T/chunk) + L + 1 caller events; joins back into `main`. */
+ * chunks of steps on side[l], then (l > 0) the chunk's dx = dG W_ih GEMM that feeds layer l-1;
+ * each finished chunk's share of dW_hh / dW_ih (K = its time columns, accumulated) runs on
+ * side[L + l] beside the recurrence, then the bias row sums.  side: 2*L caller streams.
+ * xT/ld_xT: per-layer transposed inputs; dx[l] [T,B,H] for l > 0;
+ * ev = L*ceil(T/chunk) + L + 1 caller events (ev[L*nch + l] = layer l's gradients done);
+ * joins back into `main`. */
 size_t sv_lstm_stack_bwd_workspace(int L, int T, int B, int F, int H);
 int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float* const* xT, const long* ld_xT,
                       const float* const* w_ih, const float* const* w_hh, const float* const* gates,
@@ -166,8 +169,8 @@ int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const sv_bf16* xT_bf, lon
                            float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, float* workspace,
                            hipStream_t stream);
 
-/* layer-pipelined stack backward in bf16 (as sv_lstm_stack_bwd; fp32 master weights are
- * transpose-cast per call; dg/dgT per layer bf16) */
+/* layer-pipelined stack backward in bf16 (as sv_lstm_stack_bwd, 2*L side streams; fp32
+ * master weights are transpose-cast per call; dg/dgT per layer bf16) */
 size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H);
 int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* const* xT, const long* ld_xT,
                            const float* const* w_ih, const float* const* w_hh, const float* const* gates,

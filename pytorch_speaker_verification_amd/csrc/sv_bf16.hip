@@ -707,7 +707,7 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
 // Layer-pipelined stack backward, bf16 operands (see sv_lstm_stack_bwd in sv_lstm.hip).
 namespace {
 struct BBwdWs {
-  float *dcf0, *dcf1, *gws;
+  float *dcf0, *dcf1, *gws, *gws2;
   bf16_t *whhT, *wihT;
   size_t total;
 };
@@ -728,6 +728,7 @@ BBwdWs carve_bbwd(char* base, int T, int B, int F, int H) {
   g = std::max(g, sv_gemm_bf16_workspace(4 * H, F, TBp));
   g = std::max(g, sv_gemm_bf16_workspace(T * B, F, 4 * H));
   w.gws = (float*)take(g);
+  w.gws2 = (float*)take(g);  // the weight-gradient stream's own split-K slabs (stack bwd)
   w.total = off;
   return w;
 }
@@ -758,7 +759,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
   if (e != hipSuccess) return (int)e;
   const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
   for (int l = L - 1; l >= 0; --l) {
-    hipStream_t s = side[l];
+    hipStream_t s = side[l], sw = side[L + l];
     const int Fl = l == 0 ? F : H;
     const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
     if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
@@ -785,15 +786,29 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
         if (rc) return rc;
       }
       if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
+      if (!dw_chunked_layer(l)) continue;
+      // the chunk's K-slice of the weight gradients, on the layer's weight-gradient stream
+      if ((e = hipStreamWaitEvent(sw, ev[l * nch + c], 0)) != hipSuccess) return (int)e;
+      const float beta = c == nch - 1 ? 0.f : 1.f;
+      const int Kc = (t1 - t0) * Bp;
+      rc = sv_gemm_bf16(4 * H, H, Kc, dgT[l] + (long)t0 * Bp, TBp, hT[l] + (long)t0 * Bp, ldhT, dw_hh[l], H, nullptr,
+                        nullptr, beta, ws.gws2, sw);
+      if (rc) return rc;
+      rc = sv_gemm_bf16(4 * H, Fl, Kc, dgT[l] + (long)t0 * Bp, TBp, xT[l] + (long)t0 * Bp, ld_xT[l], dw_ih[l], Fl,
+                        nullptr, nullptr, beta, ws.gws2, sw);
+      if (rc) return rc;
     }
-    rc = sv_gemm_bf16(4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws, s);
-    if (rc) return rc;
-    rc = sv_gemm_bf16(4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, ws.gws, s);
-    if (rc) return rc;
-    hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, s, dgT[l], (long)TBp, TBp, db_ih[l],
+    if (!dw_chunked_layer(l)) {
+      sw = s;
+      rc = sv_gemm_bf16(4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws, s);
+      if (rc) return rc;
+      rc = sv_gemm_bf16(4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, ws.gws, s);
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
                        db_hh ? db_hh[l] : nullptr);
     SV_LAUNCH_CHECK();
-    if ((e = hipEventRecord(ev[L * nch + l], s)) != hipSuccess) return (int)e;
+    if ((e = hipEventRecord(ev[L * nch + l], sw)) != hipSuccess) return (int)e;
   }
   for (int l = 0; l < L; ++l)
     if ((e = hipStreamWaitEvent(main, ev[L * nch + l], 0)) != hipSuccess) return (int)e;

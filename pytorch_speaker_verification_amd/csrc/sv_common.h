@@ -17,6 +17,9 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 #define SV_EALIGN -2
 #define SV_ESHAPE -3
 
+// stack-backward schedule switch (sv_lstm.hip; env SV_DW_CHUNKED)
+int dw_chunked_layer(int l);
+
 #define SV_LAUNCH_CHECK()                                  \
   do {                                                     \
     hipError_t e__ = hipGetLastError();                    \

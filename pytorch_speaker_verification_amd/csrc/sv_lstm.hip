@@ -430,13 +430,14 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
   }
 }
 
+template <int BKX>
 __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
     const float* __restrict__ dgnext, const float* __restrict__ whhT, const float* __restrict__ dhup,
     const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, float* __restrict__ dg, float* __restrict__ dcf, float* __restrict__ dgT,
     long lddgT, int t, int Bp, int B, int H) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int GBUF = 2 * (BWD_BM + BWD_U) * (SV_BKM + 4);
+  constexpr int GBUF = 2 * (BWD_BM + BWD_U) * (BKX + 4);
   constexpr int LDR = BWD_U + 1;
   constexpr int LDT = BWD_BM + 1;
   constexpr int PER = BWD_BM * BWD_U / 512;
@@ -463,9 +464,9 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
   f32x16 acc[1][1];
   zero_acc(acc);
   if (dgnext)
-    gemm_mainloop_km<BWD_BM, BWD_U, 128, SV_BKM, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
-                                                       RowMapLinear{j0, H}, gate * H, (gate + 1) * H,
-                                                       lds + gate * GBUF, gt, (w & 1) * 32, 0, acc);
+    gemm_mainloop_km<BWD_BM, BWD_U, 128, BKX, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
+                                                    RowMapLinear{j0, H}, gate * H, (gate + 1) * H, lds + gate * GBUF,
+                                                    gt, (w & 1) * 32, 0, acc);
   __syncthreads();
   float* red = lds;                    // [4][64][LDR]
   float* gT = lds + 4 * BWD_BM * LDR;  // [4*32][LDT]
@@ -645,6 +646,18 @@ extern "C" int sv_colsum(const float* X, int R, int C, float* out, float* worksp
   return colsum(X, R, C, out, nullptr, workspace, stream);
 }
 
+// stack bwd: weight-gradient GEMMs of layer l per finished chunk on a second stream, or
+// whole-T behind the layer's recurrence.  SV_DW_CHUNKED: 0 (default) none, 1 all layers,
+// 2 layer 0 only.  Measured at c2 (4 HW queues): 0 = 72.4 ms, 2 = 72.5, 1 = 76.5 -- the
+// chunk GEMMs slow the concurrent recurrences more than they shorten the tail.
+int dw_chunked_layer(int l) {
+  static int v = [] {
+    const char* e = getenv("SV_DW_CHUNKED");
+    return (e && *e >= '0' && *e <= '2') ? *e - '0' : 0;
+  }();
+  return v == 1 || (v == 2 && l == 0);
+}
+
 static bool lstm_dims_ok(int T, int B, int F, int H) {
   return T > 0 && B > 0 && F > 0 && H > 0 && F % 4 == 0 && H % 4 == 0;
 }
@@ -656,6 +669,18 @@ constexpr int FWD_LDS = (FWD_LDS_MAIN > FWD_LDS_EPI ? FWD_LDS_MAIN : FWD_LDS_EPI
 constexpr int BWD_LDS_MAIN = 4 * 2 * (BWD_BM + BWD_U) * (SV_BKM + 4);
 constexpr int BWD_LDS_EPI = 4 * BWD_BM * (BWD_U + 1) + 4 * BWD_U * (BWD_BM + 1);
 constexpr int BWD_LDS = (BWD_LDS_MAIN > BWD_LDS_EPI ? BWD_LDS_MAIN : BWD_LDS_EPI) * (int)sizeof(float);
+// BK = 16 variant of K3v2: 67 KB of LDS instead of 110 KB, so a K3 workgroup fits on a CU
+// beside a 128x128 GEMM workgroup (74 KB) of a concurrent stream (SV_BWD_BK=16; measured no
+// faster at c2, so BK = 32 stays the default)
+constexpr int BWD_LDS_MAIN16 = 4 * 2 * (BWD_BM + BWD_U) * (16 + 4);
+constexpr int BWD_LDS16 = (BWD_LDS_MAIN16 > BWD_LDS_EPI ? BWD_LDS_MAIN16 : BWD_LDS_EPI) * (int)sizeof(float);
+int bwd_bk() {
+  static int v = [] {
+    const char* e = getenv("SV_BWD_BK");
+    return (e && atoi(e) == 16) ? 16 : 32;
+  }();
+  return v;
+}
 // step-kernel variant: 2 = 8-wave (default), 1 = 4-wave; SV_STEP_VARIANT overrides (A/B timing)
 constexpr int FWD_LDS64 = 2 * (FWD_BM + 4 * FWD_U) * (64 + 4) * (int)sizeof(float);
 int step_variant() {
@@ -679,9 +704,12 @@ void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh
 void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* whhT, const float* up, const float* dcfi,
                      const float* acts, const float* ct, const float* cp, float* dg, float* dcfo, float* dgT,
                      long lddgT, int t, int Bp, int B, int H) {
-  if (step_variant() >= 2)
-    hipLaunchKernelGGL(lstm_step_bwd_v2_kernel, grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp, dg,
-                       dcfo, dgT, lddgT, t, Bp, B, H);
+  if (step_variant() >= 2 && bwd_bk() == 16)
+    hipLaunchKernelGGL(lstm_step_bwd_v2_kernel<16>, grid, dim3(512), BWD_LDS16, s, dgn, whhT, up, dcfi, acts, ct, cp,
+                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  else if (step_variant() >= 2)
+    hipLaunchKernelGGL(lstm_step_bwd_v2_kernel<SV_BKM>, grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
+                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
   else
     hipLaunchKernelGGL(lstm_step_bwd_kernel, grid, dim3(256), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp, dg, dcfo,
                        dgT, lddgT, t, Bp, B, H);
@@ -737,7 +765,7 @@ extern "C" int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, 
 
 namespace {
 struct BwdWs {
-  float *dcf0, *dcf1, *whhT, *wihT, *gws;
+  float *dcf0, *dcf1, *whhT, *wihT, *gws, *gws2;
   size_t total;
 };
 size_t al4(size_t n) { return (n + 63) & ~size_t(63); }
@@ -758,6 +786,7 @@ BwdWs carve_bwd(float* base, int T, int B, int F, int H) {
   g = std::max(g, sv_gemm_f32_workspace(4 * H, F, TBp));
   g = std::max(g, sv_gemm_f32_workspace(T * B, F, 4 * H));
   w.gws = take((g + 3) / 4);
+  w.gws2 = take((g + 3) / 4);  // the weight-gradient stream's own split-K slabs (stack bwd)
   w.total = off * sizeof(float);
   return w;
 }
@@ -875,9 +904,11 @@ extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float*
 // ============================================================================
 // Layer-pipelined stack backward.  Layer l runs on side[l], top layer first in issue order:
 // its timesteps in reverse chunks of `chunk` (K3 steps, then -- for l > 0 -- the chunk's
-// dx = dG W_ih GEMM, which is the next-lower layer's dh_up for those timesteps), then its
-// dW_hh / dW_ih GEMMs and bias row sums.  Layer l-1 waits only for layer l's dx of the same
-// chunk, so one layer's (latency-bound) recurrence overlaps the upper layers' GEMMs.
+// dx = dG W_ih GEMM, which is the next-lower layer's dh_up for those timesteps).  Each
+// finished chunk's K-slice of dW_hh / dW_ih (beta = 1 after the first) runs on the layer's
+// weight-gradient stream side[L + l], so no weight GEMM sits on a recurrence; the bias row
+// sums close the layer there.  Layer l-1 waits only for layer l's dx of the same chunk, so
+// one layer's (latency-bound) recurrence overlaps the upper layers' GEMMs.
 //   xT[l], ld_xT[l]: layer input transposed (layer 0: the frames; l > 0: hT[l-1] + Bp cols)
 //   dx[l] [T,B,H] for l > 0 (dh_up of layer l-1); dx[0] may be NULL
 //   workspace: L * sv_lstm_layer_bwd_workspace(T, B, max(F,H), H) bytes
@@ -908,7 +939,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
   if (e != hipSuccess) return (int)e;
   const dim3 grid((H + BWD_U - 1) / BWD_U, (B + BWD_BM - 1) / BWD_BM);
   for (int l = L - 1; l >= 0; --l) {
-    hipStream_t s = side[l];
+    hipStream_t s = side[l], sw = side[L + l];
     const int Fl = l == 0 ? F : H;
     const BwdWs ws = carve_bwd((float*)((char*)workspace + per * l), T, B, std::max(F, H), H);
     if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
@@ -934,16 +965,31 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
         if (rc) return rc;
       }
       if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
+      if (!dw_chunked_layer(l)) continue;
+      // this chunk's share of dW_hh / dW_ih (K = its time columns), accumulated on the layer's
+      // weight-gradient stream while the recurrence moves on to the next chunk
+      if ((e = hipStreamWaitEvent(sw, ev[l * nch + c], 0)) != hipSuccess) return (int)e;
+      const float beta = c == nch - 1 ? 0.f : 1.f;
+      const int Kc = (t1 - t0) * Bp;
+      rc = sv_gemm_f32(1, 1, 4 * H, H, Kc, dgT[l] + (long)t0 * Bp, TBp, hT[l] + (long)t0 * Bp, ldhT, dw_hh[l], H,
+                       nullptr, nullptr, beta, ws.gws2, sw);
+      if (rc) return rc;
+      rc = sv_gemm_f32(1, 1, 4 * H, Fl, Kc, dgT[l] + (long)t0 * Bp, TBp, xT[l] + (long)t0 * Bp, ld_xT[l], dw_ih[l],
+                       Fl, nullptr, nullptr, beta, ws.gws2, sw);
+      if (rc) return rc;
     }
-    rc = sv_gemm_f32(1, 1, 4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws, s);
-    if (rc) return rc;
-    rc = sv_gemm_f32(1, 1, 4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, ws.gws,
-                     s);
-    if (rc) return rc;
-    hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(256), 0, s, dgT[l], (long)TBp, TBp, db_ih[l],
+    if (!dw_chunked_layer(l)) {  // whole-T weight GEMMs behind the recurrence, on its stream
+      sw = s;
+      rc = sv_gemm_f32(1, 1, 4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws, s);
+      if (rc) return rc;
+      rc = sv_gemm_f32(1, 1, 4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f,
+                       ws.gws, s);
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
                        db_hh ? db_hh[l] : nullptr);
     SV_LAUNCH_CHECK();
-    if ((e = hipEventRecord(ev[L * nch + l], s)) != hipSuccess) return (int)e;
+    if ((e = hipEventRecord(ev[L * nch + l], sw)) != hipSuccess) return (int)e;
   }
   for (int l = 0; l < L; ++l)
     if ((e = hipStreamWaitEvent(main, ev[L * nch + l], 0)) != hipSuccess) return (int)e;

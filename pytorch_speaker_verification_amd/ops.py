@@ -136,10 +136,15 @@ def embedder_forward(x, layers, w_p, b_p, save=True):
     return emb, st
 
 
-def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False):
+def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_ready=None):
     """Backward of embedder_forward.  ``grads`` (optional) is a list of preallocated
     output tensors in parameter order [w_ih, w_hh, b_ih, b_hh]*L + [w_p, b_p]; returns it
-    (and dx [B,T,F] if need_dx)."""
+    (and dx [B,T,F] if need_dx).
+
+    ``grad_ready(k, event)`` (optional) is called as soon as a gradient group is enqueued:
+    k = L for the projection, then k = L-1 .. 0 for the LSTM layers; ``event`` is the HIP
+    event that completes it (None: the current stream).  The data-parallel trainer hangs its
+    per-layer all-reduce buckets on it so communication overlaps the rest of the BPTT."""
     demb = demb.contiguous()
     require_device(demb)
     T, B, H, P = st.T, st.B, st.H, st.P
@@ -155,6 +160,8 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False):
     ws = _ws(lib().sv_proj_norm_workspace(B, H, P), dev)
     call("sv_proj_norm_bwd", ptr(demb), ptr(st.emb), ptr(st.ynorm), ptr(st.h_last), B, H, P, ptr(w_p),
          ptr(grads[4 * L]), ptr(grads[4 * L + 1]), ptr(dh_last), ptr(ws), s)
+    if grad_ready:
+        grad_ready(L, None)
     Fmax = max(st.x_tm[l].shape[2] for l in range(L))
     Bp = (B + 3) // 4 * 4
     if PIPELINE_CHUNK > 0 and L > 1 and not need_dx:
@@ -167,8 +174,8 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False):
         ld = [T * Bp] + [(T + 1) * Bp] * (L - 1)
         nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
         nev = L * nch + L + 1
-        streams, events = _StreamPool.get(dev, L, nev)
-        sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
+        streams, events = _StreamPool.get(dev, 2 * L, nev)
+        sp = (ctypes.c_void_p * (2 * L))(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
         call("sv_lstm_stack_bwd", L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
              _parr([l[0] for l in layers]), _parr([l[1] for l in layers]), _parr(st.gates), _parr(st.c_tm),
@@ -176,6 +183,9 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False):
              _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
              _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
              PIPELINE_CHUNK, s, sp, ep)
+        if grad_ready:
+            for l in range(L - 1, -1, -1):
+                grad_ready(l, events[L * nch + l])
         return grads
     ws = _ws(lib().sv_lstm_layer_bwd_workspace(T, B, Fmax, H), dev)
     dgates = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
@@ -194,6 +204,8 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False):
         call("sv_lstm_layer_bwd", T, B, Fl, H, xT, ld_xT, ptr(w_ih), ptr(w_hh), ptr(st.gates[l]),
              ptr(st.c_tm[l]), ptr(st.hT[l]), ptr(dh_up), full, ptr(dgates), ptr(dgT), ptr(dx), ptr(grads[4 * l]),
              ptr(grads[4 * l + 1]), ptr(grads[4 * l + 2]), ptr(grads[4 * l + 3]), ptr(ws), s)
+        if grad_ready:
+            grad_ready(l, None)
         dh_up, full = dx, 1
         if l == 0:
             dx_out = dx
@@ -273,7 +285,9 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True):
     return emb, st
 
 
-def embedder_backward_bf16(st, demb, layers, w_p, grads=None):
+def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None):
+    """Backward of embedder_forward_bf16 (same ``grads`` / ``grad_ready`` contract as
+    embedder_backward)."""
     demb = demb.contiguous()
     require_device(demb)
     T, B, H, P = st.T, st.B, st.H, st.P
@@ -290,6 +304,8 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None):
     ws = _ws(lib().sv_proj_norm_workspace(B, H, P), dev)
     call("sv_proj_norm_bwd", ptr(demb), ptr(st.emb), ptr(st.ynorm), ptr(st.h_last), B, H, P, ptr(w_p),
          ptr(grads[4 * L]), ptr(grads[4 * L + 1]), ptr(dh_last), ptr(ws), s)
+    if grad_ready:
+        grad_ready(L, None)
     Fmax = max(st.x_tm[l].shape[2] for l in range(L))
     if PIPELINE_CHUNK > 0 and L > 1:
         F0 = st.x_tm[0].shape[2]
@@ -301,8 +317,8 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None):
         ld = [T * Bp] + [(T + 1) * Bp] * (L - 1)
         nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
         nev = L * nch + L + 1
-        streams, events = _StreamPool.get(dev, L, nev)
-        sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
+        streams, events = _StreamPool.get(dev, 2 * L, nev)
+        sp = (ctypes.c_void_p * (2 * L))(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
         call("sv_lstm_stack_bwd_bf16", L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
              _parr([l[0] for l in layers]), _parr([l[1] for l in layers]), _parr(st.gates), _parr(st.c_tm),
@@ -310,6 +326,9 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None):
              _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
              _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
              PIPELINE_CHUNK, s, sp, ep)
+        if grad_ready:
+            for l in range(L - 1, -1, -1):
+                grad_ready(l, events[L * nch + l])
         return grads
     ws = _ws(lib().sv_lstm_layer_bwd_bf16_workspace(T, B, Fmax, H), dev)
     dg = _bf((T, B, 4 * H), dev)
@@ -330,6 +349,8 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None):
         call("sv_lstm_layer_bwd_bf16", T, B, Fl, H, xT, ld_xT, ptr(wihT), ptr(whhT), ptr(st.gates[l]),
              ptr(st.c_tm[l]), ptr(st.hT[l]), ptr(dh_up), full, ptr(dg), ptr(dgT), ptr(dx), ptr(grads[4 * l]),
              ptr(grads[4 * l + 1]), ptr(grads[4 * l + 2]), ptr(grads[4 * l + 3]), ptr(ws), s)
+        if grad_ready:
+            grad_ready(l, None)
         dh_up, full = dx, 1
     return grads
 

@@ -15,7 +15,11 @@ all-reduce and the clip+SGD update each touch one contiguous buffer:
 
 Data parallel: one process per GPU; rank r holds speakers [r*N, (r+1)*N) of a global
 batch of world*N speakers (ShardedGE2E), so the step is the single-GPU step of that
-global batch.
+global batch.  The gradient SUM all-reduce is bucketed by readiness:
+bucket L = projection + pad + {w, b} (ready before the BPTT starts), then one bucket per
+LSTM layer, top layer first, each launched on a communication stream as soon as the
+backward's per-layer completion event fires, so RCCL traffic overlaps the lower layers'
+BPTT; the clip + SGD kernel waits for all buckets.
 """
 from __future__ import annotations
 
@@ -68,6 +72,14 @@ class GE2ETrainer:
                 b.grad = flat_g[n_pad + 1:n_pad + 2].view(())
         self.flat_p, self.flat_g = flat_p, flat_g
         self._ptrs = [p.data_ptr() for p in params]
+        # all-reduce buckets: [off(layer l), off(layer l+1)) per layer; the head bucket runs
+        # from the projection weight to the end (proj w, proj b, pad, w, b, pad)
+        offs = [0]
+        for p in params:
+            offs.append(offs[-1] + p.numel())
+        L = len(params) // 4
+        self.buckets = [(offs[4 * l], offs[4 * l + 4]) for l in range(L)] + [(offs[4 * L], n_pad + 4)]
+        self._comm = None
 
     def _check_layout(self):
         if [p.data_ptr() for p in self.net.flat_params()] != self._ptrs:
@@ -89,12 +101,26 @@ class GE2ETrainer:
         loss, _, gst = self.ge2e.forward(E, w, b)
         dE, dwdb = self.ge2e.backward(gst, w, b)
         self.flat_g[self.n_pad:self.n_pad + 2].copy_(dwdb)
-        if bf16:
-            embedder_backward_bf16(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views)
-        else:
-            embedder_backward(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views)
+        works = []
+        ready = None
         if self.ge2e.world > 1:
-            dist.all_reduce(self.flat_g, group=self.group)  # SUM, never mean (SURVEY §7 hard part 4)
+            main = torch.cuda.current_stream(x.device)
+            if self._comm is None:
+                self._comm = torch.cuda.Stream(device=x.device)
+            comm = self._comm
+
+            def ready(k, event):
+                lo, hi = self.buckets[k]
+                if event is None:
+                    comm.wait_stream(main)
+                else:
+                    comm.wait_event(event)
+                with torch.cuda.stream(comm):  # SUM, never mean (SURVEY §7 hard part 4)
+                    works.append(dist.all_reduce(self.flat_g[lo:hi], group=self.group, async_op=True))
+        bwd = embedder_backward_bf16 if bf16 else embedder_backward
+        bwd(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views, grad_ready=ready)
+        for wk in works:
+            wk.wait()  # the current (main) stream waits for every bucket
         n = self.n_pad
         clip_sgd_step_(self.flat_p[:n], self.flat_g[:n], self.clip_net, self.lr, self.write_grads)
         clip_sgd_step_(self.flat_p[n:n + 4], self.flat_g[n:n + 4], self.clip_wb, self.lr, self.write_grads)

@@ -28,13 +28,14 @@ def _model():
     return net.to("cuda:0"), GE2ELoss("cuda:0")
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, precision):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from pytorch_speaker_verification_amd.trainer import GE2ETrainer
         net, ge2e = _model()
+        net.precision = precision
         x = torch.tensor(recipe.make_frames(5, world * NL * M, T, DIMS[0]), device="cuda:0")
         xl = x[rank * NL * M:(rank + 1) * NL * M].contiguous()
         tr = GE2ETrainer(net, ge2e, lr=0.01)
@@ -45,10 +46,14 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_dp_two_ranks_equal_single_process():
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_dp_two_ranks_equal_single_process(precision):
+    """Also exercises the bucketed, event-driven gradient all-reduce (trainer.py): the
+    per-layer buckets are launched from the backward's completion events."""
     from pytorch_speaker_verification_amd.trainer import GE2ETrainer
     world = 2
     net, ge2e = _model()
+    net.precision = precision
     x = torch.tensor(recipe.make_frames(5, world * NL * M, T, DIMS[0]), device="cuda:0")
     tr = GE2ETrainer(net, ge2e, lr=0.01)
     ref_losses = [float(tr.step(x, world * NL, M)) for _ in range(STEPS)]
@@ -59,7 +64,7 @@ def test_dp_two_ranks_equal_single_process():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, precision)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
