@@ -145,6 +145,62 @@ __device__ __forceinline__ void gemm_mainloop_bf_rp(const bf16_t* __restrict__ A
   __syncthreads();
 }
 
+// Rolling-prefetch main loop (software pipeline of depth D k-tiles): the loads of tile
+// kt + D are issued into the registers tile kt has just left for LDS, so D tiles are always in
+// flight and only the first round trip is exposed (the super-chunk loop above exposes one per
+// super-chunk).  One LDS double buffer, one barrier per k-tile.
+template <int BM, int BN, int NT, int D, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_bf_pipe(const bf16_t* __restrict__ A, long lda, const MapA& mapA,
+                                                      const bf16_t* __restrict__ B, long ldb, const MapB& mapB,
+                                                      int kbeg, int kend, bf16_t* lds, int tid, int wm0, int wn0,
+                                                      f32x16 (&acc)[TM][TN]) {
+  using SA = BTileStage<BM, NT, BBK>;
+  using SB = BTileStage<BN, NT, BBK>;
+  constexpr int LD = BBK + 8;
+  constexpr int BUF = (BM + BN) * LD;
+  const int lane = tid & 63;
+  const int nk = (kend - kbeg + BBK - 1) / BBK;
+  SA sa[D];
+  SB sb[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (j < nk) {
+      sa[j].load(A, lda, mapA, kbeg + j * BBK, kend, tid);
+      sb[j].load(B, ldb, mapB, kbeg + j * BBK, kend, tid);
+    }
+  for (int k0 = 0; k0 < nk; k0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int kt = k0 + j;
+      if (kt < nk) {
+        bf16_t* buf = lds + (kt & 1) * BUF;
+        sa[j].store(buf, tid);
+        sb[j].store(buf + BM * LD, tid);
+        if (kt + D < nk) {
+          sa[j].load(A, lda, mapA, kbeg + (kt + D) * BBK, kend, tid);
+          sb[j].load(B, ldb, mapB, kbeg + (kt + D) * BBK, kend, tid);
+        }
+        __syncthreads();
+        mfma_ktile_bf<TM, TN, BBK, LD>(buf, buf + BM * LD, wm0, wn0, lane, acc);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// SC <= 12: super-chunk loop of SC tiles; SC = 100 + D: rolling pipeline of depth D
+template <int BM, int BN, int NT, int SC, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_step(const bf16_t* __restrict__ A, long lda, const MapA& mapA,
+                                                   const bf16_t* __restrict__ B, long ldb, const MapB& mapB,
+                                                   int kbeg, int kend, bf16_t* lds, int tid, int wm0, int wn0,
+                                                   f32x16 (&acc)[TM][TN]) {
+  if constexpr (SC > 100)
+    gemm_mainloop_bf_pipe<BM, BN, NT, SC - 100, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0,
+                                                        acc);
+  else
+    gemm_mainloop_bf_rp<BM, BN, NT, SC, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0, acc);
+}
+
 __device__ __forceinline__ bf16_t to_bf(float x) {
   const __bf16 b = (__bf16)x;
   return *reinterpret_cast<const bf16_t*>(&b);
@@ -299,8 +355,8 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_bf16_kernel(
   f32x16 acc[1][1];
   zero_acc(acc);
   if (hprev_bf)
-    gemm_mainloop_bf_rp<BF_BM, BN, 512, SC, 1, 1>(hprev_bf + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh_bf, H,
-                                                  RowMapGates<BF_U>{j0, H}, 0, H, ldsb, tid, wm0, wn0, acc);
+    gemm_mainloop_step<BF_BM, BN, 512, SC, 1, 1>(hprev_bf + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh_bf, H,
+                                                 RowMapGates<BF_U>{j0, H}, 0, H, ldsb, tid, wm0, wn0, acc);
   float* pre = reinterpret_cast<float*>(smem);
   float* hs = pre + BF_BM * LDP;
 #pragma unroll
@@ -340,6 +396,113 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_bf16_kernel(
   }
 }
 
+// ============================================================================
+// Wavefront forward over the whole stack: launch s runs layer l at time t = s - l for every
+// layer at once (blockIdx.z = layer), so one launch carries L recurrent steps and the L - 1
+// upper layers need no input-projection GEMM: their pre-activations are
+//   b_ih + b_hh + h^{l-1}_t W_ih^T + h^l_{t-1} W_hh^T
+// accumulated as two K segments of the same tile.  Layer 0 reads x W_ih^T + b from `gates`
+// (one T*B-row GEMM up front).  T + L - 1 launches replace L*T step launches + L*nch GEMMs.
+// ============================================================================
+#define SV_MAXL 4
+struct WaveFwdArgs {
+  const bf16_t* wih[SV_MAXL];
+  const bf16_t* whh[SV_MAXL];
+  const float* bih[SV_MAXL];
+  const float* bhh[SV_MAXL];
+  float* gates[SV_MAXL];
+  float* c[SV_MAXL];
+  float* h[SV_MAXL];
+  bf16_t* hb[SV_MAXL];
+  bf16_t* hT[SV_MAXL];
+  long ldhT;
+  int T, Bp, B, H;
+};
+
+template <int SC>
+__global__ __launch_bounds__(512) void lstm_wave_fwd_bf16_kernel(const WaveFwdArgs a, int s) {
+  const int l = blockIdx.z, t = s - l;
+  if (t < 0 || t >= a.T) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* ldsb = reinterpret_cast<bf16_t*>(smem);
+  constexpr int BN = 4 * BF_U, LDP = BN + 4, LDH = BF_BM + 1;
+  constexpr int PER = BF_BM * BF_U / 512;
+  const int B = a.B, H = a.H;
+  const long BH = (long)B * H, G = 4L * H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j0 = blockIdx.x * BF_U, b0 = blockIdx.y * BF_BM;
+  const int wm0 = (w >> 2) * 32, wn0 = (w & 3) * 32;
+  float* gates = a.gates[l] + (long)t * B * G;
+  const float* cprev = t ? a.c[l] + (long)(t - 1) * BH : nullptr;
+  float xg[PER][4], cpv[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + 512 * k, b = e / BF_U, u = e % BF_U;
+    const int gb = b0 + b, gj = j0 + u;
+    const bool ok = gb < B && gj < H;
+    if (l == 0) {
+      const float* gp = gates + (long)gb * G + gj;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xg[k][q] = ok ? gp[q * H] : 0.f;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xg[k][q] = ok ? a.bih[l][q * H + gj] + a.bhh[l][q * H + gj] : 0.f;
+    }
+    cpv[k] = (ok && cprev) ? cprev[(long)gb * H + gj] : 0.f;
+  }
+  f32x16 acc[1][1];
+  zero_acc(acc);
+  if (l > 0)  // h^{l-1}_t W_ih^T  (input width = H for every upper layer)
+    gemm_mainloop_step<BF_BM, BN, 512, SC, 1, 1>(a.hb[l - 1] + (long)(t + 1) * BH + (long)b0 * H, H,
+                                                 RowMapLinear{0, B - b0}, a.wih[l], H, RowMapGates<BF_U>{j0, H}, 0,
+                                                 H, ldsb, tid, wm0, wn0, acc);
+  if (t > 0)  // h^l_{t-1} W_hh^T
+    gemm_mainloop_step<BF_BM, BN, 512, SC, 1, 1>(a.hb[l] + (long)t * BH + (long)b0 * H, H, RowMapLinear{0, B - b0},
+                                                 a.whh[l], H, RowMapGates<BF_U>{j0, H}, 0, H, ldsb, tid, wm0, wn0,
+                                                 acc);
+  float* pre = reinterpret_cast<float*>(smem);
+  float* hs = pre + BF_BM * LDP;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) pre[(wm0 + acc_row(r, lane)) * LDP + wn0 + (lane & 31)] = acc[0][0][r];
+  __syncthreads();
+  float* cout = a.c[l] + (long)t * BH;
+  float* hout = a.h[l] + (long)(t + 1) * BH;
+  bf16_t* hout_bf = a.hb[l] + (long)(t + 1) * BH;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + 512 * k, b = e / BF_U, u = e % BF_U;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    float* gp = gates + (long)gb * G + gj;
+    const float* pr = pre + b * LDP + u;
+    const float i = sv_sigmoid(pr[0] + xg[k][0]);
+    const float f = sv_sigmoid(pr[BF_U] + xg[k][1]);
+    const float g = tanhf(pr[2 * BF_U] + xg[k][2]);
+    const float o = sv_sigmoid(pr[3 * BF_U] + xg[k][3]);
+    const float c = f * cpv[k] + i * g;
+    const float h = o * tanhf(c);
+    gp[0] = i;
+    gp[H] = f;
+    gp[2 * H] = g;
+    gp[3 * H] = o;
+    cout[(long)gb * H + gj] = c;
+    hout[(long)gb * H + gj] = h;
+    hout_bf[(long)gb * H + gj] = to_bf(h);
+    hs[u * LDH + b] = h;
+  }
+  bf16_t* hT = a.hT[l];
+  if (!hT) return;
+  __syncthreads();
+  for (int e = tid; e < BF_BM * BF_U; e += 512) {
+    const int u = e / BF_BM, b = e % BF_BM;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    bf16_t* row = hT + (long)gj * a.ldhT;
+    row[(long)(t + 1) * a.Bp + gb] = to_bf(hs[u * LDH + b]);
+    if (t == 0) row[gb] = 0;
+  }
+}
+
 template <int SC>
 __global__ __launch_bounds__(512) void lstm_step_bwd_bf16_kernel(
     const bf16_t* __restrict__ dgnext, const bf16_t* __restrict__ whhT, const float* __restrict__ dhup,
@@ -374,9 +537,9 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_bf16_kernel(
   f32x16 acc[1][1];
   zero_acc(acc);
   if (dgnext)
-    gemm_mainloop_bf_rp<BF_BM, BF_U, 128, SC, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
-                                                   RowMapLinear{j0, H}, gate * H, (gate + 1) * H, ldsb + gate * GBUF,
-                                                   gt, (w & 1) * 32, 0, acc);
+    gemm_mainloop_step<BF_BM, BF_U, 128, SC, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
+                                                  RowMapLinear{j0, H}, gate * H, (gate + 1) * H, ldsb + gate * GBUF,
+                                                  gt, (w & 1) * 32, 0, acc);
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);  // [4][64][LDR]
   float* gTs = red + 4 * BF_BM * LDR;           // [4*32][LDT]
@@ -473,14 +636,23 @@ int bf16_sc() {
   static int v = [] {
     const char* e = getenv("SV_BF16_SC");
     const int x = e ? atoi(e) : 3;
-    return (x == 3 || x == 4 || x == 6) ? x : 12;
+    return (x == 3 || x == 4 || x == 6 || x == 104 || x == 106 || x == 112) ? x : 12;
   }();
   return v;
 }
 void launch_fwd_bf16(dim3 grid, hipStream_t s, const bf16_t* hp, const bf16_t* whh, float* g, const float* cp,
                      float* c, float* h, bf16_t* hb, bf16_t* hT, long ldhT, int t, int Bp, int B, int H) {
   const int sc = bf16_sc();
-  if (sc == 6)
+  if (sc == 104)
+    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<104>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
+                       t, Bp, B, H);
+  else if (sc == 106)
+    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<106>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
+                       t, Bp, B, H);
+  else if (sc == 112)
+    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<112>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
+                       t, Bp, B, H);
+  else if (sc == 6)
     hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<6>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
                        t, Bp, B, H);
   else if (sc == 4)
@@ -494,11 +666,32 @@ void launch_fwd_bf16(dim3 grid, hipStream_t s, const bf16_t* hp, const bf16_t* w
                        t, Bp, B, H);
 }
 
+// stack forward schedule: layer-pipelined streams (0, default) or wavefront over layers (1).
+// Measured at c3: pipelined 22.25 ms/step, wavefront 25.5 (23.3 with the rolling prefetch):
+// a step launch starts with cold L2 (kernel-boundary invalidate), so its time scales with the
+// bytes each CU pulls from the Infinity Cache, and the wavefront moves 5x the bytes per launch.
+int wavefront_fwd() {
+  static int v = [] {
+    const char* e = getenv("SV_WAVEFRONT");
+    return (e && *e == '1') ? 1 : 0;
+  }();
+  return v;
+}
+void launch_wave_fwd_bf16(dim3 grid, hipStream_t s, const WaveFwdArgs& a, int st) {
+  const int sc = bf16_sc();
+  if (sc == 104)
+    hipLaunchKernelGGL(lstm_wave_fwd_bf16_kernel<104>, grid, dim3(512), BFWD_LDS, s, a, st);
+  else if (sc == 106)
+    hipLaunchKernelGGL(lstm_wave_fwd_bf16_kernel<106>, grid, dim3(512), BFWD_LDS, s, a, st);
+  else
+    hipLaunchKernelGGL(lstm_wave_fwd_bf16_kernel<3>, grid, dim3(512), BFWD_LDS, s, a, st);
+}
+
 int bf16_bsc() {
   static int v = [] {
     const char* e = getenv("SV_BF16_BSC");
     const int x = e ? atoi(e) : 6;
-    return (x == 2 || x == 3) ? x : 6;
+    return (x == 2 || x == 3 || x == 103 || x == 104 || x == 106) ? x : 6;
   }();
   return v;
 }
@@ -506,7 +699,16 @@ void launch_bwd_bf16(dim3 grid, hipStream_t s, const bf16_t* dgn, const bf16_t* 
                      const float* dcfi, const float* acts, const float* ct, const float* cp, bf16_t* dg, float* dcfo,
                      bf16_t* dgT, long lddgT, int t, int Bp, int B, int H) {
   const int sc = bf16_bsc();
-  if (sc == 2)
+  if (sc == 103)
+    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<103>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
+                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  else if (sc == 104)
+    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<104>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
+                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  else if (sc == 106)
+    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<106>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
+                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  else if (sc == 2)
     hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<2>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
                        dg, dcfo, dgT, lddgT, t, Bp, B, H);
   else if (sc == 3)
@@ -666,8 +868,43 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
   const long BH = (long)B * H, BG = 4L * B * H;
   const int Bp = (B + 7) & ~7;
   const long ldhT = (long)(T + 1) * Bp;
+  hipError_t e;
+  if (wavefront_fwd() && L <= SV_MAXL) {  // wavefront schedule, all on `main`
+    for (int l = 0; l < L; ++l) {
+      if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), main)) != hipSuccess) return (int)e;
+      if ((e = hipMemsetAsync(h_bf[l], 0, BH * sizeof(bf16_t), main)) != hipSuccess) return (int)e;
+      if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(bf16_t), main)) != hipSuccess)
+        return (int)e;
+    }
+    int rc = sv_gemm_bf16(T * B, 4 * H, F, x_bf, F, w_ih_bf[0], F, gates[0], 4L * H, b_ih[0], b_hh[0], 0.f, nullptr,
+                          main);
+    if (rc) return rc;
+    WaveFwdArgs a{};
+    for (int l = 0; l < L; ++l) {
+      a.wih[l] = w_ih_bf[l];
+      a.whh[l] = w_hh_bf[l];
+      a.bih[l] = b_ih[l];
+      a.bhh[l] = b_hh[l];
+      a.gates[l] = gates[l];
+      a.c[l] = c_tm[l];
+      a.h[l] = h_tm[l];
+      a.hb[l] = h_bf[l];
+      a.hT[l] = hT[l];
+    }
+    a.ldhT = ldhT;
+    a.T = T;
+    a.Bp = Bp;
+    a.B = B;
+    a.H = H;
+    const dim3 wgrid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM, L);
+    for (int st = 0; st < T + L - 1; ++st) {
+      launch_wave_fwd_bf16(wgrid, main, a, st);
+      SV_LAUNCH_CHECK();
+    }
+    return SV_OK;
+  }
   hipEvent_t ev_start = ev[L * nch];
-  hipError_t e = hipEventRecord(ev_start, main);
+  e = hipEventRecord(ev_start, main);
   if (e != hipSuccess) return (int)e;
   for (int l = 0; l < L; ++l) {
     hipStream_t s = side[l];
