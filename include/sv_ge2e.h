@@ -179,6 +179,13 @@ int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* con
                            float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace, int chunk,
                            hipStream_t main, const hipStream_t* side, hipEvent_t* ev);
 
+/* ---- persistent recurrences (one launch per layer for all T; sv_persist.hip).  The stack
+ * functions use them when sv_persist_fwd_ok(B, H) (grid co-resident on this device).
+ * sv_persist_status: 0 ok, 1 a hand-off wait timed out since the last call (device sync;
+ * clears the flag). */
+int sv_persist_fwd_ok(int B, int H);
+int sv_persist_status(void);
+
 /* ---- clip_grad_norm_ + SGD step over one flat parameter group (train_speech_embedder.py:63-65)
  * p -= lr * min(1, max_norm / (|g|_2 + 1e-6)) * g; write_grad=1 also scales g in place. */
 size_t sv_clip_sgd_workspace(void);

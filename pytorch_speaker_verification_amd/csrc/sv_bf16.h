@@ -1,0 +1,211 @@
+// bf16 GEMM building blocks shared by the step kernels (sv_bf16.hip) and the persistent
+// recurrences (sv_persist.hip): bf16 storage type, k-major LDS tile staging, the
+// v_mfma_f32_32x32x16_bf16 k-tile, and the main loops over them.
+#pragma once
+#include "sv_common.h"
+#include "sv_gemm.h"
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned short bf16_t;  // storage type across the C ABI
+
+#define BBK 64  // k-tile (bf16 elements)
+
+__device__ __forceinline__ f32x16 mfma_bf16(bf16x8_t a, bf16x8_t b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// k-major bf16 tile: element (r,k) at base[row(r)*ld + k]; LDS [R][BK+8] (144-B rows: a 16-lane
+// group's ds_read_b128 of 16 distinct rows is conflict-free).  One 16-B chunk = 8 k per load.
+template <int R, int NT, int BK>
+struct BTileStage {
+  static constexpr int LD = BK + 8;
+  static constexpr int C8 = BK / 8;
+  static constexpr int NV = (R * C8) / NT;
+  static_assert(NV >= 1 && NV * NT == R * C8, "tile/thread mismatch");
+  uint4 v[NV];
+  template <class Map>
+  __device__ __forceinline__ void load(const bf16_t* __restrict__ base, long ld, const Map& map, int k0, int K,
+                                       int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int q = tid + NT * i;
+      const int r = q / C8, c = (q % C8) * 8;
+      uint4 x = {0u, 0u, 0u, 0u};
+      if (map.valid(r) && k0 + c < K) x = *reinterpret_cast<const uint4*>(base + (long)map(r) * ld + k0 + c);
+      v[i] = x;
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int q = tid + NT * i;
+      *reinterpret_cast<uint4*>(lds + (q / C8) * LD + (q % C8) * 8) = v[i];
+    }
+  }
+};
+
+// lane (r = l&31, h = l>>5) supplies A[r][16s + 8h + j] / B[16s + 8h + j][r], j = 0..7
+template <int TM, int TN, int BK, int LD>
+__device__ __forceinline__ void mfma_ktile_bf(const bf16_t* As, const bf16_t* Bs, int wm0, int wn0, int lane,
+                                              f32x16 (&acc)[TM][TN]) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < BK / 16; ++s) {
+    bf16x8_t a[TM], b[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8_t*>(As + (wm0 + 32 * i + r) * LD + 16 * s + 8 * h);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8_t*>(Bs + (wn0 + 32 * j + r) * LD + 16 * s + 8 * h);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(a[i], b[j], acc[i][j]);
+  }
+}
+
+// lds must hold 2 * (BM + BN) * (BK + 8) bf16
+template <int BM, int BN, int NT, int BK, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_bf(const bf16_t* __restrict__ A, long lda, const MapA& mapA,
+                                                 const bf16_t* __restrict__ B, long ldb, const MapB& mapB, int kbeg,
+                                                 int kend, bf16_t* lds, int tid, int wm0, int wn0,
+                                                 f32x16 (&acc)[TM][TN]) {
+  using SA = BTileStage<BM, NT, BK>;
+  using SB = BTileStage<BN, NT, BK>;
+  constexpr int LD = BK + 8;
+  constexpr int BUF = (BM + BN) * LD;
+  const int lane = tid & 63;
+  SA sa;
+  SB sb;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk <= 0) return;
+  sa.load(A, lda, mapA, kbeg, kend, tid);
+  sb.load(B, ldb, mapB, kbeg, kend, tid);
+  sa.store(lds, tid);
+  sb.store(lds + BM * LD, tid);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    bf16_t* cur = lds + (kt & 1) * BUF;
+    bf16_t* nxt = lds + ((kt + 1) & 1) * BUF;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      sa.load(A, lda, mapA, kbeg + (kt + 1) * BK, kend, tid);
+      sb.load(B, ldb, mapB, kbeg + (kt + 1) * BK, kend, tid);
+    }
+    mfma_ktile_bf<TM, TN, BK, LD>(cur, cur + BM * LD, wm0, wn0, lane, acc);
+    if (more) {
+      sa.store(nxt, tid);
+      sb.store(nxt + BM * LD, tid);
+    }
+    __syncthreads();
+  }
+}
+
+// Register-prefetch main loop for the latency-bound recurrent steps: every global load of a
+// super-chunk of SC k-tiles is issued up front (one HBM/L2 round trip per super-chunk instead
+// of one per k-tile), then the tiles are staged through two LDS buffers, one barrier each.
+template <int BM, int BN, int NT, int SC, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_bf_rp(const bf16_t* __restrict__ A, long lda, const MapA& mapA,
+                                                    const bf16_t* __restrict__ B, long ldb, const MapB& mapB,
+                                                    int kbeg, int kend, bf16_t* lds, int tid, int wm0, int wn0,
+                                                    f32x16 (&acc)[TM][TN]) {
+  using SA = BTileStage<BM, NT, BBK>;
+  using SB = BTileStage<BN, NT, BBK>;
+  constexpr int LD = BBK + 8;
+  constexpr int BUF = (BM + BN) * LD;
+  const int lane = tid & 63;
+  const int nk = (kend - kbeg + BBK - 1) / BBK;
+  int it = 0;
+  for (int c0 = 0; c0 < nk; c0 += SC) {
+    SA sa[SC];
+    SB sb[SC];
+#pragma unroll
+    for (int j = 0; j < SC; ++j) {
+      if (c0 + j < nk) {
+        sa[j].load(A, lda, mapA, kbeg + (c0 + j) * BBK, kend, tid);
+        sb[j].load(B, ldb, mapB, kbeg + (c0 + j) * BBK, kend, tid);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < SC; ++j) {
+      if (c0 + j < nk) {
+        bf16_t* buf = lds + (it & 1) * BUF;
+        sa[j].store(buf, tid);
+        sb[j].store(buf + BM * LD, tid);
+        __syncthreads();
+        mfma_ktile_bf<TM, TN, BBK, LD>(buf, buf + BM * LD, wm0, wn0, lane, acc);
+        ++it;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Rolling-prefetch main loop (software pipeline of depth D k-tiles): the loads of tile
+// kt + D are issued into the registers tile kt has just left for LDS, so D tiles are always in
+// flight and only the first round trip is exposed (the super-chunk loop above exposes one per
+// super-chunk).  One LDS double buffer, one barrier per k-tile.
+template <int BM, int BN, int NT, int D, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_bf_pipe(const bf16_t* __restrict__ A, long lda, const MapA& mapA,
+                                                      const bf16_t* __restrict__ B, long ldb, const MapB& mapB,
+                                                      int kbeg, int kend, bf16_t* lds, int tid, int wm0, int wn0,
+                                                      f32x16 (&acc)[TM][TN]) {
+  using SA = BTileStage<BM, NT, BBK>;
+  using SB = BTileStage<BN, NT, BBK>;
+  constexpr int LD = BBK + 8;
+  constexpr int BUF = (BM + BN) * LD;
+  const int lane = tid & 63;
+  const int nk = (kend - kbeg + BBK - 1) / BBK;
+  SA sa[D];
+  SB sb[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (j < nk) {
+      sa[j].load(A, lda, mapA, kbeg + j * BBK, kend, tid);
+      sb[j].load(B, ldb, mapB, kbeg + j * BBK, kend, tid);
+    }
+  for (int k0 = 0; k0 < nk; k0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int kt = k0 + j;
+      if (kt < nk) {
+        bf16_t* buf = lds + (kt & 1) * BUF;
+        sa[j].store(buf, tid);
+        sb[j].store(buf + BM * LD, tid);
+        if (kt + D < nk) {
+          sa[j].load(A, lda, mapA, kbeg + (kt + D) * BBK, kend, tid);
+          sb[j].load(B, ldb, mapB, kbeg + (kt + D) * BBK, kend, tid);
+        }
+        __syncthreads();
+        mfma_ktile_bf<TM, TN, BBK, LD>(buf, buf + BM * LD, wm0, wn0, lane, acc);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// SC <= 12: super-chunk loop of SC tiles; SC = 100 + D: rolling pipeline of depth D
+template <int BM, int BN, int NT, int SC, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_step(const bf16_t* __restrict__ A, long lda, const MapA& mapA,
+                                                   const bf16_t* __restrict__ B, long ldb, const MapB& mapB,
+                                                   int kbeg, int kend, bf16_t* lds, int tid, int wm0, int wn0,
+                                                   f32x16 (&acc)[TM][TN]) {
+  if constexpr (SC > 100)
+    gemm_mainloop_bf_pipe<BM, BN, NT, SC - 100, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0,
+                                                        acc);
+  else
+    gemm_mainloop_bf_rp<BM, BN, NT, SC, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0, acc);
+}
+
+__device__ __forceinline__ bf16_t to_bf(float x) {
+  const __bf16 b = (__bf16)x;
+  return *reinterpret_cast<const bf16_t*>(&b);
+}
+
+// recurrent-step tile: 64 batch rows x 32 hidden units (x 4 gates = 128 gate columns)
+#define BF_BM 64
+#define BF_U 32
+
+// persistent forward recurrence of one layer (sv_persist.hip)
+extern "C" int sv_persist_fwd_ok(int B, int H);
+int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates, float* c_tm, float* h_tm,
+                        bf16_t* h_bf, bf16_t* hT, hipStream_t stream);

@@ -1,0 +1,52 @@
+"""Subprocess worker for test_gpu_persist.py: runs the bf16 stack forward + one training step
+under the schedule selected by the environment (SV_PERSIST / SV_WAVEFRONT are read once per
+process by the library) and saves every output to an .npz."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+sys.path.insert(0, HERE)
+
+import recipe  # noqa: E402
+from conftest import model_dims  # noqa: E402
+
+
+def main(out, dims, N, M, T, precision):
+    from pytorch_speaker_verification_amd._lib import lib
+    from pytorch_speaker_verification_amd.ops import embedder_forward_bf16, embedder_forward
+    from pytorch_speaker_verification_amd.speech_embedder_net import GE2ELoss, SpeechEmbedder
+    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+    dev = torch.device("cuda", 0)
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    sd = recipe.make_weights(7, *dims, scale=3.0)
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    net = net.to(dev)
+    net.precision = precision
+    x = torch.tensor(recipe.make_frames(11, N * M, T, dims[0]), device=dev)
+    layers = net.LSTM_stack.layer_params()
+    fwd = embedder_forward_bf16 if precision == "bf16" else embedder_forward
+    emb, st = fwd(x, layers, net.projection.weight, net.projection.bias)
+    res = {"emb": emb, "h_last": st.h_last}
+    for l in range(len(layers)):
+        res[f"gates{l}"] = st.gates[l]
+        res[f"c{l}"] = st.c_tm[l]
+    tr = GE2ETrainer(net, GE2ELoss(dev), lr=0.01)
+    res["loss"] = tr.step(x, N, M).reshape(1)
+    res["flat_p"] = tr.flat_p
+    torch.cuda.synchronize()
+    res = {k: v.detach().float().cpu().numpy() for k, v in res.items()}
+    res["status"] = np.array([lib().sv_persist_status()])
+    np.savez(out, **res)
+
+
+if __name__ == "__main__":
+    a = sys.argv
+    main(a[1], tuple(int(v) for v in a[2].split(",")), int(a[3]), int(a[4]), int(a[5]), a[6])

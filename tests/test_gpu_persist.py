@@ -1,0 +1,46 @@
+"""The persistent recurrence schedule (one launch per layer for all T, sv_persist.hip) must
+reproduce the per-step-launch schedule bit for bit: same tiles, same MFMA order, same K1 GEMMs
+(fp32 accumulation of identical products), only the launch structure and the h hand-off differ.
+Each schedule runs in its own process (the library reads SV_PERSIST once)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _run(tmp_path, tag, env_extra, dims, N, M, T, precision):
+    out = str(tmp_path / f"{tag}.npz")
+    env = dict(os.environ, **env_extra)
+    r = subprocess.run([sys.executable, os.path.join(HERE, "_schedule_worker.py"), out, ",".join(map(str, dims)),
+                        str(N), str(M), str(T), precision], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return dict(np.load(out))
+
+
+@pytest.mark.parametrize("dims,N,M,T", [((40, 768, 3, 256), 64, 10, 12),   # c3 grid: 24 x 10 workgroups
+                                        ((40, 96, 2, 32), 7, 5, 9)])       # ragged rows (B = 35)
+def test_persistent_fwd_bf16_equals_per_step(tmp_path, dims, N, M, T):
+    a = _run(tmp_path, "step", {"SV_PERSIST": "0", "SV_WAVEFRONT": "0"}, dims, N, M, T, "bf16")
+    b = _run(tmp_path, "persist", {"SV_PERSIST": "1"}, dims, N, M, T, "bf16")
+    assert int(b["status"][0]) == 0
+    for k in a:
+        if k == "status":
+            continue
+        np.testing.assert_array_equal(b[k], a[k], err_msg=k)
+
+
+def test_wavefront_fwd_bf16_equals_per_step(tmp_path):
+    """The wavefront schedule (all layers per launch, two K segments per tile) changes only the
+    accumulation split of the upper layers' pre-activations: fp32-rounding-level agreement."""
+    dims, N, M, T = (40, 96, 3, 32), 6, 4, 10
+    a = _run(tmp_path, "step", {"SV_PERSIST": "0", "SV_WAVEFRONT": "0"}, dims, N, M, T, "bf16")
+    b = _run(tmp_path, "wave", {"SV_PERSIST": "0", "SV_WAVEFRONT": "1"}, dims, N, M, T, "bf16")
+    for k in ("gates0", "c0"):
+        np.testing.assert_array_equal(b[k], a[k], err_msg=k)   # layer 0 is computed identically
+    for k in ("gates1", "gates2", "c2", "emb", "loss"):
+        np.testing.assert_allclose(b[k], a[k], rtol=2e-2, atol=2e-2, err_msg=k)
