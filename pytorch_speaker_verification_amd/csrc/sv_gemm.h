@@ -247,3 +247,58 @@ __device__ __forceinline__ void gemm_mainloop_km(const float* __restrict__ A, lo
     __syncthreads();
   }
 }
+
+// Rolling-prefetch variant of gemm_mainloop_km (software pipeline of depth D k-tiles): the
+// loads of tile kt + D go into the registers tile kt has just left for LDS, so D tiles are in
+// flight while one is multiplied.  For the per-step kernels, whose every launch starts from a
+// cold L2 and pulls its operands from the Infinity Cache.  lds as gemm_mainloop_km.
+template <int BM, int BN, int NT, int BK, int D, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_km_pipe(const float* __restrict__ A, long lda, const MapA& mapA,
+                                                      const float* __restrict__ B, long ldb, const MapB& mapB,
+                                                      int kbeg, int kend, float* lds, int tid, int wm0, int wn0,
+                                                      f32x16 (&acc)[TM][TN]) {
+  using SA = KTileStage<BM, NT, BK>;
+  using SB = KTileStage<BN, NT, BK>;
+  constexpr int LD = BK + 4;
+  constexpr int BUF = (BM + BN) * LD;
+  const int lane = tid & 63;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  SA sa[D];
+  SB sb[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (j < nk) {
+      sa[j].load(A, lda, mapA, kbeg + j * BK, kend, tid);
+      sb[j].load(B, ldb, mapB, kbeg + j * BK, kend, tid);
+    }
+  for (int k0 = 0; k0 < nk; k0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int kt = k0 + j;
+      if (kt < nk) {
+        float* buf = lds + (kt & 1) * BUF;
+        sa[j].store(buf, tid);
+        sb[j].store(buf + BM * LD, tid);
+        if (kt + D < nk) {
+          sa[j].load(A, lda, mapA, kbeg + (kt + D) * BK, kend, tid);
+          sb[j].load(B, ldb, mapB, kbeg + (kt + D) * BK, kend, tid);
+        }
+        __syncthreads();
+        mfma_ktile_km<TM, TN, BK, LD>(buf, buf + BM * LD, wm0, wn0, lane, acc);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// D == 1: the plain double-buffered loop; D > 1: the rolling pipeline
+template <int BM, int BN, int NT, int BK, int D, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_km_d(const float* __restrict__ A, long lda, const MapA& mapA,
+                                                   const float* __restrict__ B, long ldb, const MapB& mapB, int kbeg,
+                                                   int kend, float* lds, int tid, int wm0, int wn0,
+                                                   f32x16 (&acc)[TM][TN]) {
+  if constexpr (D > 1)
+    gemm_mainloop_km_pipe<BM, BN, NT, BK, D, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0, acc);
+  else
+    gemm_mainloop_km<BM, BN, NT, BK, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0, acc);
+}

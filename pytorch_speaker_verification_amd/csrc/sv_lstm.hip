@@ -120,7 +120,7 @@ __global__ void to_time_major_kernel(const float* __restrict__ x, float* __restr
 }
 
 // k-major ("NT") GEMM: both operands k-contiguous; the fast path for every large GEMM
-template <int BM, int BN, int EPI>
+template <int BM, int BN, int EPI, int D = 1>
 __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ A, long lda, const float* __restrict__ B,
                                                       long ldb, float* __restrict__ C, long ldc, long slab, int M,
                                                       int N, int K, int kchunk, const float* __restrict__ bias0,
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ 
   const int wm0 = (w >> 1) * (BM / 2), wn0 = (w & 1) * (BN / 2);
   f32x16 acc[TM][TN];
   zero_acc(acc);
-  gemm_mainloop_km<BM, BN, 256, SV_BKM, TM, TN>(A, lda, RowMapLinear{tm * BM, M}, B, ldb, RowMapLinear{tn * BN, N},
+  gemm_mainloop_km_d<BM, BN, 256, SV_BKM, D, TM, TN>(A, lda, RowMapLinear{tm * BM, M}, B, ldb, RowMapLinear{tn * BN, N},
                                                 kbeg, kend, lds, tid, wm0, wn0, acc);
   float* Cz = C + (EPI == EPI_SLAB ? (long)blockIdx.y * slab : 0);
 #pragma unroll
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(256) void lstm_step_bwd_kernel(
 //         accumulator each, all sharing the same staged A/B tiles.
 //   K3v2: 4 groups of 2 waves, group = gate (its K range of W_hh^T), waves split the rows.
 // ============================================================================
-template <int BKX>
+template <int BKX, int D = 1>
 __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __restrict__ hprev,
                                                                const float* __restrict__ whh,
                                                                float* __restrict__ gates,
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
   f32x16 acc[1][1];
   zero_acc(acc);
   if (hprev)
-    gemm_mainloop_km<FWD_BM, BN, 512, BKX, 1, 1>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
+    gemm_mainloop_km_d<FWD_BM, BN, 512, BKX, D, 1, 1>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
                                                  RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc);
   float* pre = lds;
   float* hs = lds + FWD_BM * LDP;
@@ -430,7 +430,82 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
   }
 }
 
-template <int BKX>
+// K2v4: the K2v2 body over a 64-row x U-unit tile with NW waves (2 x 4U/32 accumulators of
+// 32x32).  U = 16, NW = 4 gives 480 workgroups of 256 threads at c2, two per CU, so one
+// workgroup's barriers and epilogue are covered by the other's MFMAs (K2v2 has one per CU).
+template <int U, int NW, int BKX>
+__global__ __launch_bounds__(NW * 64) void lstm_step_fwd_v4_kernel(const float* __restrict__ hprev,
+                                                                   const float* __restrict__ whh,
+                                                                   float* __restrict__ gates,
+                                                                   const float* __restrict__ cprev,
+                                                                   float* __restrict__ cout, float* __restrict__ hout,
+                                                                   float* __restrict__ hT, long ldhT, int t, int Bp,
+                                                                   int B, int H) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int BM = 64, NT = NW * 64;
+  constexpr int BN = 4 * U, LDP = BN + 4, LDH = BM + 1;
+  constexpr int WN = BN / 32;  // waves across the gate columns
+  static_assert((BM / 32) * WN == NW, "wave grid");
+  constexpr int PER = BM * U / NT;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j0 = blockIdx.x * U, b0 = blockIdx.y * BM;
+  const int wm0 = (w / WN) * 32, wn0 = (w % WN) * 32;
+  const long G = 4L * H;
+  float xg[PER][4], cpv[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + NT * k, b = e / U, u = e % U;
+    const int gb = b0 + b, gj = j0 + u;
+    const bool ok = gb < B && gj < H;
+    const float* gp = gates + (long)gb * G + gj;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xg[k][q] = ok ? gp[q * H] : 0.f;
+    cpv[k] = (ok && cprev) ? cprev[(long)gb * H + gj] : 0.f;
+  }
+  f32x16 acc[1][1];
+  zero_acc(acc);
+  if (hprev)
+    gemm_mainloop_km<BM, BN, NT, BKX, 1, 1>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
+                                            RowMapGates<U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc);
+  float* pre = lds;
+  float* hs = lds + BM * LDP;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) pre[(wm0 + acc_row(r, lane)) * LDP + wn0 + (lane & 31)] = acc[0][0][r];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + NT * k, b = e / U, u = e % U;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    float* gp = gates + (long)gb * G + gj;
+    const float* pr = pre + b * LDP + u;
+    const float i = sv_sigmoid(pr[0] + xg[k][0]);
+    const float f = sv_sigmoid(pr[U] + xg[k][1]);
+    const float g = tanhf(pr[2 * U] + xg[k][2]);
+    const float o = sv_sigmoid(pr[3 * U] + xg[k][3]);
+    const float c = f * cpv[k] + i * g;
+    const float h = o * tanhf(c);
+    gp[0] = i;
+    gp[H] = f;
+    gp[2 * H] = g;
+    gp[3 * H] = o;
+    cout[(long)gb * H + gj] = c;
+    hout[(long)gb * H + gj] = h;
+    hs[u * LDH + b] = h;
+  }
+  if (!hT) return;
+  __syncthreads();
+  for (int e = tid; e < BM * U; e += NT) {
+    const int u = e / BM, b = e % BM;
+    const int gb = b0 + b, gj = j0 + u;
+    if (gb >= B || gj >= H) continue;
+    float* row = hT + (long)gj * ldhT;
+    row[(long)(t + 1) * Bp + gb] = hs[u * LDH + b];
+    if (t == 0) row[gb] = 0.f;
+  }
+}
+
+template <int BKX, int D = 1>
 __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
     const float* __restrict__ dgnext, const float* __restrict__ whhT, const float* __restrict__ dhup,
     const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
@@ -464,7 +539,7 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
   f32x16 acc[1][1];
   zero_acc(acc);
   if (dgnext)
-    gemm_mainloop_km<BWD_BM, BWD_U, 128, BKX, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
+    gemm_mainloop_km_d<BWD_BM, BWD_U, 128, BKX, D, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
                                                     RowMapLinear{j0, H}, gate * H, (gate + 1) * H, lds + gate * GBUF,
                                                     gt, (w & 1) * 32, 0, acc);
   __syncthreads();
@@ -517,14 +592,28 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
 // ============================================================================
 namespace {
 
+// prefetch depth of the NT GEMM main loop (SV_GEMM_PIPE = 1 or 2; measured equal at c2 --
+// the GEMMs are not latency-starved -- so 1, the lower-VGPR kernel, stays the default)
+int gemm_pipe() {
+  static int v = [] {
+    const char* e = getenv("SV_GEMM_PIPE");
+    return (e && *e == '2') ? 2 : 1;
+  }();
+  return v;
+}
+
 template <int BM, int BN, bool AK, bool BKC, int EPI>
 int launch_gemm_t(const float* A, long lda, const float* B, long ldb, float* C, long ldc, long slab, int M, int N,
                   int K, int splitk, int kchunk, const float* b0, const float* b1, float beta, hipStream_t s) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (AK && BKC) {
     constexpr int LDS_KM = 2 * (BM + BN) * (SV_BKM + 4);
-    hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float), s, A,
-                       lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+    if (gemm_pipe() == 2)
+      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 2>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float), s,
+                         A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+    else
+      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float), s, A,
+                         lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
   } else {
     constexpr int LDS_FLOATS = 2 * SV_BK * (TileLd<AK, BM>::value + TileLd<BKC, BN>::value);
     hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, AK, BKC, EPI>), dim3(tiles, splitk), dim3(256),
@@ -686,13 +775,45 @@ constexpr int FWD_LDS64 = 2 * (FWD_BM + 4 * FWD_U) * (64 + 4) * (int)sizeof(floa
 int step_variant() {
   static int v = [] {
     const char* e = getenv("SV_STEP_VARIANT");
-    return (e && (*e == '1' || *e == '3')) ? *e - '0' : 2;
+    return (e && (*e == '1' || *e == '3' || *e == '4')) ? *e - '0' : 2;
   }();
   return v;
 }
+// prefetch depth of the K2v2 / K3v2 main loops (1 = double buffer, 2 = default rolling
+// pipeline; SV_KM_PIPE = 1..4).  Measured at c2: K2 39.6 -> 36.4 us, K3 47.6 -> 43.1 us,
+// step 73.7 -> 70.4 ms with depth 2 (3: 71.3; 4: same kernels as 2)
+int km_pipe() {
+  static int v = [] {
+    const char* e = getenv("SV_KM_PIPE");
+    const int x = e ? atoi(e) : 2;
+    return (x >= 1 && x <= 4) ? x : 2;
+  }();
+  return v;
+}
+constexpr int FWD4_U = 16;
+constexpr int FWD4_LDS_MAIN = 2 * (64 + 4 * FWD4_U) * (SV_BKM + 4);
+constexpr int FWD4_LDS_EPI = 64 * (4 * FWD4_U + 4) + FWD4_U * (64 + 1);
+constexpr int FWD4_LDS = (FWD4_LDS_MAIN > FWD4_LDS_EPI ? FWD4_LDS_MAIN : FWD4_LDS_EPI) * (int)sizeof(float);
+// forward-step grid of the selected variant
+dim3 fwd_step_grid(int B, int H) {
+  if (step_variant() == 4) return dim3((H + FWD4_U - 1) / FWD4_U, (B + 63) / 64);
+  return dim3((H + FWD_U - 1) / FWD_U, (B + FWD_BM - 1) / FWD_BM);
+}
 void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh, float* g, const float* cp, float* c,
                      float* h, float* hT, long ldhT, int t, int Bp, int B, int H) {
-  if (step_variant() == 2)
+  if (step_variant() == 4)
+    hipLaunchKernelGGL((lstm_step_fwd_v4_kernel<FWD4_U, 4, SV_BKM>), grid, dim3(256), FWD4_LDS, s, hp, whh, g, cp, c, h,
+                       hT, ldhT, t, Bp, B, H);
+  else if (step_variant() == 2 && km_pipe() == 2)
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT,
+                       ldhT, t, Bp, B, H);
+  else if (step_variant() == 2 && km_pipe() == 3)
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 3>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT,
+                       ldhT, t, Bp, B, H);
+  else if (step_variant() == 2 && km_pipe() == 4)
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 4>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT,
+                       ldhT, t, Bp, B, H);
+  else if (step_variant() == 2)
     hipLaunchKernelGGL(lstm_step_fwd_v2_kernel<SV_BKM>, grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT, ldhT, t,
                        Bp, B, H);
   else if (step_variant() == 3)
@@ -707,6 +828,15 @@ void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* wh
   if (step_variant() >= 2 && bwd_bk() == 16)
     hipLaunchKernelGGL(lstm_step_bwd_v2_kernel<16>, grid, dim3(512), BWD_LDS16, s, dgn, whhT, up, dcfi, acts, ct, cp,
                        dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  else if (step_variant() >= 2 && km_pipe() == 2)
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
+                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  else if (step_variant() >= 2 && km_pipe() == 3)
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 3>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
+                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  else if (step_variant() >= 2 && km_pipe() == 4)
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 4>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
+                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H);
   else if (step_variant() >= 2)
     hipLaunchKernelGGL(lstm_step_bwd_v2_kernel<SV_BKM>, grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
                        dg, dcfo, dgT, lddgT, t, Bp, B, H);
@@ -719,7 +849,7 @@ void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* wh
 extern "C" int sv_lstm_step_fwd(const float* h_prev, const float* w_hh, float* gates_t, const float* c_prev,
                                 float* c_t, float* h_t, int B, int H, hipStream_t stream) {
   if (!w_hh || !gates_t || !c_t || !h_t || B <= 0 || H <= 0 || H % 4) return SV_EARG;
-  const dim3 grid((H + FWD_U - 1) / FWD_U, (B + FWD_BM - 1) / FWD_BM);
+  const dim3 grid = fwd_step_grid(B, H);
   launch_fwd_step(grid, stream, h_prev, w_hh, gates_t, c_prev, c_t, h_t, nullptr, 0L, 0, B, B, H);
   SV_LAUNCH_CHECK();
   return SV_OK;
@@ -748,7 +878,7 @@ extern "C" int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, 
   if (rc) return rc;
   hipError_t e = hipMemsetAsync(h_tm, 0, BH * sizeof(float), stream);
   if (e != hipSuccess) return (int)e;
-  const dim3 grid((H + FWD_U - 1) / FWD_U, (B + FWD_BM - 1) / FWD_BM);
+  const dim3 grid = fwd_step_grid(B, H);
   const int Bp = (B + 3) & ~3;
   const long ldhT = (long)(T + 1) * Bp;
   if (hT && Bp != B) {  // zero the padding columns of the transposed layout
@@ -873,7 +1003,7 @@ extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float*
     if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(float), s)) != hipSuccess)
       return (int)e;
   }
-  const dim3 grid((H + FWD_U - 1) / FWD_U, (B + FWD_BM - 1) / FWD_BM);
+  const dim3 grid = fwd_step_grid(B, H);
   // wavefront issue order: chunk c of layer l after chunk c of layer l-1 on the host too
   for (int c = 0; c < nch + L - 1; ++c) {
     for (int l = 0; l < L; ++l) {
