@@ -167,25 +167,28 @@ def _ge2e_torch(E, w, b):
     return (torch.log(torch.exp(S).sum(2) + 1e-6) - pos).sum()
 
 
-def vendor_baseline(dims, N, M, T, dev, steps=3):
+def vendor_baseline(dims, N, M, T, dev, steps=3, dtype="f32"):
     """Stock torch-ROCm on the same GPU: nn.LSTM (MIOpen RNN) + Linear + torch GE2E, autograd,
-    clip_grad_norm_ x2, SGD -- the reference's training step run by the vendor libraries."""
+    clip_grad_norm_ x2, SGD -- the reference's training step run by the vendor libraries.
+    dtype bf16: the LSTM and projection run entirely in bf16 (weights, states and gradients;
+    a lower precision than this repo's bf16 path, which keeps cell state and gradients fp32)."""
     F, H, L, P = dims
     try:
         torch.manual_seed(0)
-        lstm = torch.nn.LSTM(F, H, num_layers=L, batch_first=True).to(dev)
-        proj = torch.nn.Linear(H, P).to(dev)
+        wdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        lstm = torch.nn.LSTM(F, H, num_layers=L, batch_first=True).to(dev, wdt)
+        proj = torch.nn.Linear(H, P).to(dev, wdt)
         w = torch.nn.Parameter(torch.tensor(10.0, device=dev))
         b = torch.nn.Parameter(torch.tensor(-5.0, device=dev))
         net_params = list(lstm.parameters()) + list(proj.parameters())
         opt = torch.optim.SGD([{"params": net_params}, {"params": [w, b]}], lr=0.01)
         g = torch.Generator(device="cpu").manual_seed(1235)
-        x = torch.randn(N * M, T, F, generator=g).to(dev)
+        x = torch.randn(N * M, T, F, generator=g).to(dev, wdt)
 
         def step():
             opt.zero_grad()
             y, _ = lstm(x)
-            e = proj(y[:, -1])
+            e = proj(y[:, -1]).float()
             e = e / e.norm(dim=1, keepdim=True)
             loss = _ge2e_torch(e.view(N, M, P), w, b)
             loss.backward()
@@ -201,7 +204,7 @@ def vendor_baseline(dims, N, M, T, dev, steps=3):
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
         return {"value": round(N * M / dt, 3), "unit": "embeddings/s", "ms_per_step": round(dt * 1e3, 3),
-                "kind": "torch-rocm nn.LSTM (MIOpen) + autograd, fp32, same GPU",
+                "kind": f"torch-rocm nn.LSTM (MIOpen) + autograd, {dtype}, same GPU",
                 "torch": torch.__version__}
     except Exception as ex:  # report, never fail the bench on the vendor leg
         return {"error": f"{type(ex).__name__}: {ex}"[:300]}
@@ -255,10 +258,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fwd-steps", type=int, default=5)
     ap.add_argument("--no-bf16", action="store_true", help="skip the config-c3 (bf16 operands) side measurement")
+    ap.add_argument("--preset", choices=["c2", "c3", "c5"], default=None,
+                    help="BASELINE config per GPU: c2 = N64 M10 T160 f32, c3 = the same in bf16, "
+                         "c5 = N256/8 GPUs -> 32 speakers per GPU, M10, T180, bf16")
     ap.add_argument("--no-vendor", action="store_true", help="skip the nn.LSTM/MIOpen same-GPU baseline")
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32",
                     help="precision of the headline line (default f32 = BASELINE configs[1]; bf16 = configs[2])")
     args = ap.parse_args()
+    if args.preset == "c3":
+        args.dtype = "bf16"
+    elif args.preset == "c5":
+        args.N, args.M, args.T, args.dtype = 32, 10, 180, "bf16"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -381,7 +391,9 @@ def main():
         if world == 1:  # (the GE2E leg would issue collectives on rank 0 alone otherwise)
             out["hbm_kernels"] = hbm_kernels(tr, N, M, dims[3], dev)
         if not args.no_vendor and world == 1:
-            out["vendor_baseline"] = vendor_baseline(dims, N, M, T, dev)
+            out["vendor_baseline"] = vendor_baseline(dims, N, M, T, dev, dtype=args.dtype)
+            if "bf16" in out:
+                out["bf16"]["vendor_baseline"] = vendor_baseline(dims, N, M, T, dev, dtype="bf16")
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(dims, N, M, T)
         print(json.dumps(out), flush=True)

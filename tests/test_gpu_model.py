@@ -173,3 +173,29 @@ def test_bf16_path_c2_tolerance_and_training():
     tr = GE2ETrainer(net16b, ge16b, lr=0.01)
     losses = [float(tr.step(x, N, M)) for _ in range(4)]
     assert losses[-1] < losses[0], losses
+
+
+def test_c5_per_gpu_shape_bf16_and_f32():
+    """BASELINE config c5 on one GPU's shard: N = 256 speakers over 8 GPUs -> 32 speakers x
+    M = 10 per rank, T = 180, full dims.  The fused training step runs at that shape in bf16
+    and fp32 (the cross-rank exchange itself is covered by test_gpu_dp / the gloo protocol
+    test); the bf16 loss agrees with the fp32 loss to 1e-2 relative and both steps produce
+    finite, identical-shape parameter updates."""
+    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+    dims, N, M, T = (40, 768, 3, 256), 32, 10, 180
+    sd = recipe.make_weights(55, *dims, scale=3.0)
+    x = torch.tensor(recipe.make_frames(1238, N * M, T, dims[0]), device=DEV)
+    losses = {}
+    deltas = {}
+    for prec in ("f32", "bf16"):
+        net, ge = _build(dims, sd)
+        net.precision = prec
+        p0 = [p.detach().clone() for p in net.parameters()]
+        tr = GE2ETrainer(net, ge, lr=0.01)
+        losses[prec] = float(tr.step(x, N, M))
+        deltas[prec] = [(p.detach() - q) for p, q in zip(net.parameters(), p0)]
+        assert all(torch.isfinite(d).all() for d in deltas[prec])
+    assert abs(losses["bf16"] - losses["f32"]) <= 1e-2 * abs(losses["f32"]), losses
+    for d32, d16 in zip(deltas["f32"], deltas["bf16"]):
+        rel = float((d16 - d32).norm() / d32.norm().clamp_min(1e-30))
+        assert rel < 1e-1, rel
