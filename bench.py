@@ -299,8 +299,11 @@ def main():
         tr.step(x, N, M)
     barrier()
     t0 = time.perf_counter()
+    host_s = 0.0
     for _ in range(args.steps):
+        th = time.perf_counter()
         loss = tr.step(x, N, M)
+        host_s += time.perf_counter() - th
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
@@ -341,6 +344,7 @@ def main():
                    "global_batch": world * B, "speakers_global": world * N, "seq_len": T,
                    "parallelism": f"dp{world} (speaker-sharded GE2E, RCCL grad all-reduce)"},
         "steps_per_sec": round(args.steps / dt, 4),
+        "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 3),
         "fwd_embeddings_per_sec": round(world * B / tf, 1),
         "loss": round(final_loss, 5),
         "step_tflops": round(st_fl / (ms_step * 1e-3) / 1e12, 2),

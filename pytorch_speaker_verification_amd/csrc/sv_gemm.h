@@ -256,20 +256,23 @@ template <int BM, int BN, int NT, int BK, int D, int TM, int TN, class MapA, cla
 __device__ __forceinline__ void gemm_mainloop_km_pipe(const float* __restrict__ A, long lda, const MapA& mapA,
                                                       const float* __restrict__ B, long ldb, const MapB& mapB,
                                                       int kbeg, int kend, float* lds, int tid, int wm0, int wn0,
-                                                      f32x16 (&acc)[TM][TN]) {
+                                                      f32x16 (&acc)[TM][TN], int rot = 0) {
   using SA = KTileStage<BM, NT, BK>;
   using SB = KTileStage<BN, NT, BK>;
   constexpr int LD = BK + 4;
   constexpr int BUF = (BM + BN) * LD;
   const int lane = tid & 63;
   const int nk = (kend - kbeg + BK - 1) / BK;
+  // k-tile visiting order rotated by `rot` (workgroups sharing an operand panel start on
+  // different tiles instead of all hitting the same lines at once)
+  auto kof = [&](int kt) { return kbeg + ((kt + rot) % nk) * BK; };
   SA sa[D];
   SB sb[D];
 #pragma unroll
   for (int j = 0; j < D; ++j)
     if (j < nk) {
-      sa[j].load(A, lda, mapA, kbeg + j * BK, kend, tid);
-      sb[j].load(B, ldb, mapB, kbeg + j * BK, kend, tid);
+      sa[j].load(A, lda, mapA, kof(j), kend, tid);
+      sb[j].load(B, ldb, mapB, kof(j), kend, tid);
     }
   for (int k0 = 0; k0 < nk; k0 += D) {
 #pragma unroll
@@ -280,8 +283,8 @@ __device__ __forceinline__ void gemm_mainloop_km_pipe(const float* __restrict__ 
         sa[j].store(buf, tid);
         sb[j].store(buf + BM * LD, tid);
         if (kt + D < nk) {
-          sa[j].load(A, lda, mapA, kbeg + (kt + D) * BK, kend, tid);
-          sb[j].load(B, ldb, mapB, kbeg + (kt + D) * BK, kend, tid);
+          sa[j].load(A, lda, mapA, kof(kt + D), kend, tid);
+          sb[j].load(B, ldb, mapB, kof(kt + D), kend, tid);
         }
         __syncthreads();
         mfma_ktile_km<TM, TN, BK, LD>(buf, buf + BM * LD, wm0, wn0, lane, acc);
@@ -296,9 +299,10 @@ template <int BM, int BN, int NT, int BK, int D, int TM, int TN, class MapA, cla
 __device__ __forceinline__ void gemm_mainloop_km_d(const float* __restrict__ A, long lda, const MapA& mapA,
                                                    const float* __restrict__ B, long ldb, const MapB& mapB, int kbeg,
                                                    int kend, float* lds, int tid, int wm0, int wn0,
-                                                   f32x16 (&acc)[TM][TN]) {
+                                                   f32x16 (&acc)[TM][TN], int rot = 0) {
   if constexpr (D > 1)
-    gemm_mainloop_km_pipe<BM, BN, NT, BK, D, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0, acc);
+    gemm_mainloop_km_pipe<BM, BN, NT, BK, D, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0, acc,
+                                                     rot);
   else
     gemm_mainloop_km<BM, BN, NT, BK, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0, acc);
 }

@@ -367,7 +367,7 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
                                                                const float* __restrict__ cprev,
                                                                float* __restrict__ cout, float* __restrict__ hout,
                                                                float* __restrict__ hT, long ldhT, int t, int Bp, int B,
-                                                               int H) {
+                                                               int H, int krot = 0) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int BN = 4 * FWD_U, LDP = BN + 4, LDH = FWD_BM + 1;
   constexpr int PER = FWD_BM * FWD_U / 512;  // epilogue elements per thread
@@ -391,7 +391,8 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
   zero_acc(acc);
   if (hprev)
     gemm_mainloop_km_d<FWD_BM, BN, 512, BKX, D, 1, 1>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
-                                                 RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc);
+                                                 RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc,
+                                                 krot * (blockIdx.x + blockIdx.y));
   float* pre = lds;
   float* hs = lds + FWD_BM * LDP;
 #pragma unroll
@@ -510,7 +511,7 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
     const float* __restrict__ dgnext, const float* __restrict__ whhT, const float* __restrict__ dhup,
     const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, float* __restrict__ dg, float* __restrict__ dcf, float* __restrict__ dgT,
-    long lddgT, int t, int Bp, int B, int H) {
+    long lddgT, int t, int Bp, int B, int H, int krot = 0) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int GBUF = 2 * (BWD_BM + BWD_U) * (BKX + 4);
   constexpr int LDR = BWD_U + 1;
@@ -541,7 +542,7 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
   if (dgnext)
     gemm_mainloop_km_d<BWD_BM, BWD_U, 128, BKX, D, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
                                                     RowMapLinear{j0, H}, gate * H, (gate + 1) * H, lds + gate * GBUF,
-                                                    gt, (w & 1) * 32, 0, acc);
+                                                    gt, (w & 1) * 32, 0, acc, krot * (blockIdx.x + blockIdx.y));
   __syncthreads();
   float* red = lds;                    // [4][64][LDR]
   float* gT = lds + 4 * BWD_BM * LDR;  // [4*32][LDT]
@@ -782,6 +783,16 @@ int step_variant() {
 // prefetch depth of the K2v2 / K3v2 main loops (1 = double buffer, 2 = default rolling
 // pipeline; SV_KM_PIPE = 1..4).  Measured at c2: K2 39.6 -> 36.4 us, K3 47.6 -> 43.1 us,
 // step 73.7 -> 70.4 ms with depth 2 (3: 71.3; 4: same kernels as 2)
+// k-tile rotation of the K2v2 / K3v2 main loops (SV_KROT, default 0): rot = krot * (bx + by).
+// Measured slower (K3 41.7 -> 44.4 us at krot 1): workgroups sharing an operand panel gain from
+// reading the same lines at the same time (L2 hits), so the natural order stays.
+int k_rot() {
+  static int v = [] {
+    const char* e = getenv("SV_KROT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 int km_pipe() {
   static int v = [] {
     const char* e = getenv("SV_KM_PIPE");
@@ -806,13 +817,13 @@ void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh
                        hT, ldhT, t, Bp, B, H);
   else if (step_variant() == 2 && km_pipe() == 2)
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT,
-                       ldhT, t, Bp, B, H);
+                       ldhT, t, Bp, B, H, k_rot());
   else if (step_variant() == 2 && km_pipe() == 3)
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 3>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT,
-                       ldhT, t, Bp, B, H);
+                       ldhT, t, Bp, B, H, k_rot());
   else if (step_variant() == 2 && km_pipe() == 4)
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 4>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT,
-                       ldhT, t, Bp, B, H);
+                       ldhT, t, Bp, B, H, k_rot());
   else if (step_variant() == 2)
     hipLaunchKernelGGL(lstm_step_fwd_v2_kernel<SV_BKM>, grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT, ldhT, t,
                        Bp, B, H);
@@ -830,13 +841,13 @@ void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* wh
                        dg, dcfo, dgT, lddgT, t, Bp, B, H);
   else if (step_variant() >= 2 && km_pipe() == 2)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
-                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H);
+                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
   else if (step_variant() >= 2 && km_pipe() == 3)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 3>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
-                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H);
+                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
   else if (step_variant() >= 2 && km_pipe() == 4)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 4>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
-                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H);
+                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
   else if (step_variant() >= 2)
     hipLaunchKernelGGL(lstm_step_bwd_v2_kernel<SV_BKM>, grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
                        dg, dcfo, dgT, lddgT, t, Bp, B, H);
