@@ -252,7 +252,7 @@ __device__ __forceinline__ void gemm_mainloop_km(const float* __restrict__ A, lo
 // loads of tile kt + D go into the registers tile kt has just left for LDS, so D tiles are in
 // flight while one is multiplied.  For the per-step kernels, whose every launch starts from a
 // cold L2 and pulls its operands from the Infinity Cache.  lds as gemm_mainloop_km.
-template <int BM, int BN, int NT, int BK, int D, int TM, int TN, class MapA, class MapB>
+template <int BM, int BN, int NT, int BK, int D, int TM, int TN, class MapA, class MapB, bool DIAG = false>
 __device__ __forceinline__ void gemm_mainloop_km_pipe(const float* __restrict__ A, long lda, const MapA& mapA,
                                                       const float* __restrict__ B, long ldb, const MapB& mapB,
                                                       int kbeg, int kend, float* lds, int tid, int wm0, int wn0,
@@ -279,10 +279,13 @@ __device__ __forceinline__ void gemm_mainloop_km_pipe(const float* __restrict__ 
     for (int j = 0; j < D; ++j) {
       const int kt = k0 + j;
       if (kt < nk) {
-        float* buf = lds + (kt & 1) * BUF;
-        sa[j].store(buf, tid);
-        sb[j].store(buf + BM * LD, tid);
-        if (kt + D < nk) {
+        // DIAG (profiling only): every k-tile re-uses tile 0 from LDS, no further global loads
+        float* buf = lds + (DIAG ? 0 : (kt & 1) * BUF);
+        if (!DIAG || kt == 0) {
+          sa[j].store(buf, tid);
+          sb[j].store(buf + BM * LD, tid);
+        }
+        if (!DIAG && kt + D < nk) {
           sa[j].load(A, lda, mapA, kof(kt + D), kend, tid);
           sb[j].load(B, ldb, mapB, kof(kt + D), kend, tid);
         }
@@ -295,14 +298,14 @@ __device__ __forceinline__ void gemm_mainloop_km_pipe(const float* __restrict__ 
 }
 
 // D == 1: the plain double-buffered loop; D > 1: the rolling pipeline
-template <int BM, int BN, int NT, int BK, int D, int TM, int TN, class MapA, class MapB>
+template <int BM, int BN, int NT, int BK, int D, int TM, int TN, bool DIAG = false, class MapA, class MapB>
 __device__ __forceinline__ void gemm_mainloop_km_d(const float* __restrict__ A, long lda, const MapA& mapA,
                                                    const float* __restrict__ B, long ldb, const MapB& mapB, int kbeg,
                                                    int kend, float* lds, int tid, int wm0, int wn0,
                                                    f32x16 (&acc)[TM][TN], int rot = 0) {
   if constexpr (D > 1)
-    gemm_mainloop_km_pipe<BM, BN, NT, BK, D, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0, acc,
-                                                     rot);
+    gemm_mainloop_km_pipe<BM, BN, NT, BK, D, TM, TN, MapA, MapB, DIAG>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds,
+                                                                       tid, wm0, wn0, acc, rot);
   else
     gemm_mainloop_km<BM, BN, NT, BK, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0, acc);
 }

@@ -360,7 +360,7 @@ __global__ __launch_bounds__(256) void lstm_step_bwd_kernel(
 //         accumulator each, all sharing the same staged A/B tiles.
 //   K3v2: 4 groups of 2 waves, group = gate (its K range of W_hh^T), waves split the rows.
 // ============================================================================
-template <int BKX, int D = 1>
+template <int BKX, int D = 1, bool DIAG = false>
 __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __restrict__ hprev,
                                                                const float* __restrict__ whh,
                                                                float* __restrict__ gates,
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
   f32x16 acc[1][1];
   zero_acc(acc);
   if (hprev)
-    gemm_mainloop_km_d<FWD_BM, BN, 512, BKX, D, 1, 1>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
+    gemm_mainloop_km_d<FWD_BM, BN, 512, BKX, D, 1, 1, DIAG>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
                                                  RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc,
                                                  krot * (blockIdx.x + blockIdx.y));
   float* pre = lds;
@@ -506,7 +506,7 @@ __global__ __launch_bounds__(NW * 64) void lstm_step_fwd_v4_kernel(const float* 
   }
 }
 
-template <int BKX, int D = 1>
+template <int BKX, int D = 1, bool DIAG = false>
 __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
     const float* __restrict__ dgnext, const float* __restrict__ whhT, const float* __restrict__ dhup,
     const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
   f32x16 acc[1][1];
   zero_acc(acc);
   if (dgnext)
-    gemm_mainloop_km_d<BWD_BM, BWD_U, 128, BKX, D, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
+    gemm_mainloop_km_d<BWD_BM, BWD_U, 128, BKX, D, 1, 1, DIAG>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
                                                     RowMapLinear{j0, H}, gate * H, (gate + 1) * H, lds + gate * GBUF,
                                                     gt, (w & 1) * 32, 0, acc, krot * (blockIdx.x + blockIdx.y));
   __syncthreads();
@@ -793,6 +793,15 @@ int k_rot() {
   }();
   return v;
 }
+// profiling only (results invalid): SV_STEP_DIAG=1 runs K2/K3 with every k-tile re-using tile 0
+// from LDS (no further global loads) to separate memory from compute time
+int step_diag() {
+  static int v = [] {
+    const char* e = getenv("SV_STEP_DIAG");
+    return (e && *e == '1') ? 1 : 0;
+  }();
+  return v;
+}
 int km_pipe() {
   static int v = [] {
     const char* e = getenv("SV_KM_PIPE");
@@ -815,6 +824,9 @@ void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh
   if (step_variant() == 4)
     hipLaunchKernelGGL((lstm_step_fwd_v4_kernel<FWD4_U, 4, SV_BKM>), grid, dim3(256), FWD4_LDS, s, hp, whh, g, cp, c, h,
                        hT, ldhT, t, Bp, B, H);
+  else if (step_variant() == 2 && km_pipe() == 2 && step_diag())
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, true>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
+                       hT, ldhT, t, Bp, B, H, k_rot());
   else if (step_variant() == 2 && km_pipe() == 2)
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT,
                        ldhT, t, Bp, B, H, k_rot());
@@ -839,6 +851,9 @@ void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* wh
   if (step_variant() >= 2 && bwd_bk() == 16)
     hipLaunchKernelGGL(lstm_step_bwd_v2_kernel<16>, grid, dim3(512), BWD_LDS16, s, dgn, whhT, up, dcfi, acts, ct, cp,
                        dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  else if (step_variant() >= 2 && km_pipe() == 2 && step_diag())
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, true>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
+                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
   else if (step_variant() >= 2 && km_pipe() == 2)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
                        cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
