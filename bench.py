@@ -210,6 +210,28 @@ def vendor_baseline(dims, N, M, T, dev, steps=3, dtype="f32"):
         return {"error": f"{type(ex).__name__}: {ex}"[:300]}
 
 
+def f32_product_accuracy(dev, M=512, N=1024, K=768):
+    """Max error of one fp32 GEMM (K1 shape family) against fp64, per product mode, relative to
+    |A||B|^T -- the accuracy evidence for the bf16x6 mode."""
+    from pytorch_speaker_verification_amd._lib import call, ptr, stream_of
+    from pytorch_speaker_verification_amd.ops import set_f32_products
+    g = np.random.default_rng(11)
+    A = g.standard_normal((M, K)).astype(np.float32)
+    B = g.standard_normal((N, K)).astype(np.float32)
+    ref = A.astype(np.float64) @ B.astype(np.float64).T
+    scale = np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64).T
+    At, Bt = torch.tensor(A, device=dev), torch.tensor(B, device=dev)
+    out = {}
+    for mode in ("mfma_f32", "bf16x6"):
+        prev = set_f32_products(mode)
+        C = torch.empty(M, N, device=dev)
+        call("sv_gemm_f32", 1, 1, M, N, K, ptr(At), K, ptr(Bt), K, ptr(C), N, None, None, 0.0, None, stream_of(C))
+        err = np.abs(C.cpu().numpy().astype(np.float64) - ref) / scale
+        out[mode] = {"max": float(err.max()), "mean": float(err.mean())}
+        set_f32_products(prev)
+    return out
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -258,6 +280,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fwd-steps", type=int, default=5)
     ap.add_argument("--no-bf16", action="store_true", help="skip the config-c3 (bf16 operands) side measurement")
+    ap.add_argument("--no-f32x", action="store_true", help="skip the fp32-via-bf16x6 side measurement")
     ap.add_argument("--preset", choices=["c2", "c3", "c5"], default=None,
                     help="BASELINE config per GPU: c2 = N64 M10 T160 f32, c3 = the same in bf16, "
                          "c5 = N256/8 GPUs -> 32 speakers per GPU, M10, T180, bf16")
@@ -351,6 +374,34 @@ def main():
         "step_mfma_frac": round(st_fl / (ms_step * 1e-3) / 1e12 /
                                 (MI355X_FP32_MFMA_TFLOPS if args.dtype == "f32" else MI355X_BF16_MFMA_TFLOPS), 4),
     }
+    if not args.no_f32x and args.dtype == "f32":
+        # the same fp32 step with bf16x6 products (opt-in mode; exact-fp32 MFMA is the headline)
+        from pytorch_speaker_verification_amd.ops import set_f32_products
+        prev = set_f32_products("bf16x6")
+        try:
+            netx, gex = build_model(dims, dev)
+            trx = GE2ETrainer(netx, gex, lr=0.01)
+            for _ in range(args.warmup):
+                trx.step(x, N, M)
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                lx = trx.step(x, N, M)
+            barrier()
+            dx_ = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([dx_], device=dev, dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                dx_ = float(t)
+        finally:
+            set_f32_products(prev)
+        msx = dx_ / args.steps * 1e3
+        out["f32_bf16x6"] = {"config": "same workload, fp32 products formed as six bf16 MFMA products of a three-way "
+                                       "bf16 split (fp32 accumulation); opt-in via set_f32_products('bf16x6')",
+                             "value": round(world * B * args.steps / dx_, 3), "unit": "embeddings/s",
+                             "ms_per_step": round(msx, 3), "loss": round(float(lx), 5)}
+        if rank == 0:
+            out["f32_bf16x6"]["gemm_error_vs_fp64"] = f32_product_accuracy(dev)
     if not args.no_bf16 and args.dtype == "f32":
         # BASELINE config c3: same workload, bf16 GEMM operands (fp32 accumulate/state/loss)
         net16, ge16 = build_model(dims, dev)

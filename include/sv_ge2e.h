@@ -186,6 +186,14 @@ int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* con
 int sv_persist_fwd_ok(int B, int H);
 int sv_persist_status(void);
 
+/* ---- fp32 product mode of the fp32 path (process-wide; returns the previous mode):
+ *   0 (default) exact fp32 MFMA products (v_mfma_f32_32x32x2_f32);
+ *   1 "bf16x6": each fp32 operand split into three bf16 terms, six bf16 MFMA products per fp32
+ *     product, fp32 accumulation -- products carried to ~2^-25 relative, measured GEMM error vs
+ *     fp64 at or below the exact-MFMA path's (scripts/emu_check.py) -- on the NT GEMMs and K2;
+ *   2 / 3 diagnostics (split at LDS store / in registers everywhere). */
+int sv_set_f32_products(int mode);
+
 /* ---- clip_grad_norm_ + SGD step over one flat parameter group (train_speech_embedder.py:63-65)
  * p -= lr * min(1, max_norm / (|g|_2 + 1e-6)) * g; write_grad=1 also scales g in place. */
 size_t sv_clip_sgd_workspace(void);

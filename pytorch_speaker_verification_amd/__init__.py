@@ -6,6 +6,8 @@ The compute runs in libsv_ge2e.so (hand-written HIP, C ABI in include/sv_ge2e.h)
 """
 from .hparam import hparam  # noqa: F401
 from .speech_embedder_net import GE2ELoss, SpeechEmbedder, calc_loss, get_centroids, get_cossim  # noqa: F401
+from .ops import set_f32_products  # noqa: F401
 from .trainer import GE2ETrainer  # noqa: F401
 
-__all__ = ["hparam", "SpeechEmbedder", "GE2ELoss", "get_centroids", "get_cossim", "calc_loss", "GE2ETrainer"]
+__all__ = ["hparam", "SpeechEmbedder", "GE2ELoss", "get_centroids", "get_cossim", "calc_loss", "GE2ETrainer",
+           "set_f32_products"]

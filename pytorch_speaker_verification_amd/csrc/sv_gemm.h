@@ -211,8 +211,77 @@ __device__ __forceinline__ void mfma_ktile_km(const float* As, const float* Bs, 
   }
 }
 
+// ---------------------------------------------------------------------------
+// fp32 products on the bf16 MFMA pipe ("bf16x6" split): every fp32 operand x is split in
+// registers into three bf16 terms x = x0 + x1 + x2 (round-to-nearest at each level, so
+// |x1| <= 2^-9 |x|, |x2| <= 2^-18 |x|, residual <= 2^-27 |x|), and a*b is accumulated as
+//   a1 b1 + a2 b0 + a0 b2 + a1 b0 + a0 b1 + a0 b0
+// dropping a1 b2 + a2 b1 + a2 b2 (<= 2^-26 |ab|): each product is carried to ~2^-25
+// relative, below fp32's own rounding (2^-24), with fp32 accumulation in the MFMA -- an fp32
+// GEMM whose multiplies run on v_mfma_f32_32x32x16_bf16 (16x the fp32 MFMA rate, 6 MFMAs per
+// product: 2.67x the native fp32 MFMA throughput).  Reads the same k-major fp32 LDS tiles as
+// mfma_ktile_km: lane (r, h) takes k = 16 s + 8 h .. + 7 of its row (two ds_read_b128).
+typedef __bf16 sv_bf16x8v __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void sv_split3(const f32x4 lo, const f32x4 hi, sv_bf16x8v& p0, sv_bf16x8v& p1,
+                                          sv_bf16x8v& p2) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = j < 4 ? lo[j] : hi[j - 4];
+    const __bf16 b0 = (__bf16)x;
+    const float r1 = x - (float)b0;
+    const __bf16 b1 = (__bf16)r1;
+    const float r2 = r1 - (float)b1;
+    p0[j] = b0;
+    p1[j] = b1;
+    p2[j] = (__bf16)r2;
+  }
+}
+__device__ __forceinline__ f32x16 mfma_bf16x8(sv_bf16x8v a, sv_bf16x8v b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <int TM, int TN, int BK, int LD>
+__device__ __forceinline__ void mfma_ktile_km_x6(const float* As, const float* Bs, int wm0, int wn0, int lane,
+                                                 f32x16 (&acc)[TM][TN]) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < BK / 16; ++s) {
+    sv_bf16x8v a0[TM], a1[TM], a2[TM], b0[TN], b1[TN], b2[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* p = As + (wm0 + 32 * i + r) * LD + 16 * s + 8 * h;
+      sv_split3(*reinterpret_cast<const f32x4*>(p), *reinterpret_cast<const f32x4*>(p + 4), a0[i], a1[i], a2[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float* p = Bs + (wn0 + 32 * j + r) * LD + 16 * s + 8 * h;
+      sv_split3(*reinterpret_cast<const f32x4*>(p), *reinterpret_cast<const f32x4*>(p + 4), b0[j], b1[j], b2[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x16 c = acc[i][j];
+        c = mfma_bf16x8(a1[i], b1[j], c);
+        c = mfma_bf16x8(a2[i], b0[j], c);
+        c = mfma_bf16x8(a0[i], b2[j], c);
+        c = mfma_bf16x8(a1[i], b0[j], c);
+        c = mfma_bf16x8(a0[i], b1[j], c);
+        acc[i][j] = mfma_bf16x8(a0[i], b0[j], c);
+      }
+  }
+}
+// dispatch between the exact fp32 MFMA k-tile and the bf16x6 one
+template <bool X6, int TM, int TN, int BK, int LD>
+__device__ __forceinline__ void mfma_ktile_f32(const float* As, const float* Bs, int wm0, int wn0, int lane,
+                                               f32x16 (&acc)[TM][TN]) {
+  if constexpr (X6)
+    mfma_ktile_km_x6<TM, TN, BK, LD>(As, Bs, wm0, wn0, lane, acc);
+  else
+    mfma_ktile_km<TM, TN, BK, LD>(As, Bs, wm0, wn0, lane, acc);
+}
+
 // lds must hold 2 * (BM + BN) * (BK + 4) floats
-template <int BM, int BN, int NT, int BK, int TM, int TN, class MapA, class MapB>
+template <int BM, int BN, int NT, int BK, int TM, int TN, class MapA, class MapB, bool X6 = false>
 __device__ __forceinline__ void gemm_mainloop_km(const float* __restrict__ A, long lda, const MapA& mapA,
                                                  const float* __restrict__ B, long ldb, const MapB& mapB, int kbeg,
                                                  int kend, float* lds, int tid, int wm0, int wn0,
@@ -239,7 +308,7 @@ __device__ __forceinline__ void gemm_mainloop_km(const float* __restrict__ A, lo
       sa.load(A, lda, mapA, kbeg + (kt + 1) * BK, kend, tid);
       sb.load(B, ldb, mapB, kbeg + (kt + 1) * BK, kend, tid);
     }
-    mfma_ktile_km<TM, TN, BK, LD>(cur, cur + BM * LD, wm0, wn0, lane, acc);
+    mfma_ktile_f32<X6, TM, TN, BK, LD>(cur, cur + BM * LD, wm0, wn0, lane, acc);
     if (more) {
       sa.store(nxt, tid);
       sb.store(nxt + BM * LD, tid);
@@ -252,7 +321,8 @@ __device__ __forceinline__ void gemm_mainloop_km(const float* __restrict__ A, lo
 // loads of tile kt + D go into the registers tile kt has just left for LDS, so D tiles are in
 // flight while one is multiplied.  For the per-step kernels, whose every launch starts from a
 // cold L2 and pulls its operands from the Infinity Cache.  lds as gemm_mainloop_km.
-template <int BM, int BN, int NT, int BK, int D, int TM, int TN, class MapA, class MapB, bool DIAG = false>
+template <int BM, int BN, int NT, int BK, int D, int TM, int TN, class MapA, class MapB, bool DIAG = false,
+          bool X6 = false>
 __device__ __forceinline__ void gemm_mainloop_km_pipe(const float* __restrict__ A, long lda, const MapA& mapA,
                                                       const float* __restrict__ B, long ldb, const MapB& mapB,
                                                       int kbeg, int kend, float* lds, int tid, int wm0, int wn0,
@@ -290,7 +360,7 @@ __device__ __forceinline__ void gemm_mainloop_km_pipe(const float* __restrict__ 
           sb[j].load(B, ldb, mapB, kof(kt + D), kend, tid);
         }
         __syncthreads();
-        mfma_ktile_km<TM, TN, BK, LD>(buf, buf + BM * LD, wm0, wn0, lane, acc);
+        mfma_ktile_f32<X6, TM, TN, BK, LD>(buf, buf + BM * LD, wm0, wn0, lane, acc);
       }
     }
   }
@@ -298,14 +368,150 @@ __device__ __forceinline__ void gemm_mainloop_km_pipe(const float* __restrict__ 
 }
 
 // D == 1: the plain double-buffered loop; D > 1: the rolling pipeline
-template <int BM, int BN, int NT, int BK, int D, int TM, int TN, bool DIAG = false, class MapA, class MapB>
+template <int BM, int BN, int NT, int BK, int D, int TM, int TN, bool DIAG = false, bool X6 = false, class MapA,
+          class MapB>
 __device__ __forceinline__ void gemm_mainloop_km_d(const float* __restrict__ A, long lda, const MapA& mapA,
                                                    const float* __restrict__ B, long ldb, const MapB& mapB, int kbeg,
                                                    int kend, float* lds, int tid, int wm0, int wn0,
                                                    f32x16 (&acc)[TM][TN], int rot = 0) {
   if constexpr (D > 1)
-    gemm_mainloop_km_pipe<BM, BN, NT, BK, D, TM, TN, MapA, MapB, DIAG>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds,
-                                                                       tid, wm0, wn0, acc, rot);
+    gemm_mainloop_km_pipe<BM, BN, NT, BK, D, TM, TN, MapA, MapB, DIAG, X6>(A, lda, mapA, B, ldb, mapB, kbeg, kend,
+                                                                           lds, tid, wm0, wn0, acc, rot);
   else
-    gemm_mainloop_km<BM, BN, NT, BK, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0, acc);
+    gemm_mainloop_km<BM, BN, NT, BK, TM, TN, MapA, MapB, X6>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0,
+                                                             wn0, acc);
+}
+
+// ---------------------------------------------------------------------------
+// bf16x6 with the split done once per element, at LDS-store time ("X3" tiles): the fp32 tile
+// loaded from HBM is written to LDS as three bf16 planes [3][R][BK+8] (x = x0 + x1 + x2, each
+// level round-to-nearest), so each element is split by one thread instead of by every wave that
+// reads it, and the MFMA k-tile reads bf16 fragments straight from the planes.  Same products,
+// same accuracy as mfma_ktile_km_x6.
+typedef unsigned short sv_u16;
+__device__ __forceinline__ unsigned sv_pack_bf16(float lo, float hi) {
+  const __bf16 a = (__bf16)lo, b = (__bf16)hi;
+  return (unsigned)*reinterpret_cast<const sv_u16*>(&a) | ((unsigned)*reinterpret_cast<const sv_u16*>(&b) << 16);
+}
+__device__ __forceinline__ float sv_bf16_lo(unsigned p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float sv_bf16_hi(unsigned p) { return __uint_as_float(p & 0xffff0000u); }
+
+template <int R, int NT, int BK>
+struct KTileStageX3 {
+  static constexpr int LD = BK + 8;  // bf16 elements per plane row (16-B aligned, conflict-free b128)
+  static constexpr int C4 = BK / 4;
+  static constexpr int NV = (R * C4) / NT;
+  static_assert(NV >= 1 && NV * NT == R * C4, "tile/thread mismatch");
+  f32x4 v[NV];
+  template <class Map>
+  __device__ __forceinline__ void load(const float* __restrict__ base, long ld, const Map& map, int k0, int K,
+                                       int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int q = tid + NT * i;
+      const int r = q / C4, c = (q % C4) * 4;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (map.valid(r) && k0 + c < K) x = *reinterpret_cast<const f32x4*>(base + (long)map(r) * ld + k0 + c);
+      v[i] = x;
+    }
+  }
+  // planes: [3][R][LD] bf16
+  __device__ __forceinline__ void store(sv_u16* planes, int tid) const {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int q = tid + NT * i;
+      const int off = (q / C4) * LD + (q % C4) * 4;
+      unsigned p0[2], p1[2], p2[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float xa = v[i][2 * h], xb = v[i][2 * h + 1];
+        p0[h] = sv_pack_bf16(xa, xb);
+        const float ra = xa - sv_bf16_lo(p0[h]), rb = xb - sv_bf16_hi(p0[h]);
+        p1[h] = sv_pack_bf16(ra, rb);
+        p2[h] = sv_pack_bf16(ra - sv_bf16_lo(p1[h]), rb - sv_bf16_hi(p1[h]));
+      }
+      *reinterpret_cast<uint2*>(planes + off) = uint2{p0[0], p0[1]};
+      *reinterpret_cast<uint2*>(planes + R * LD + off) = uint2{p1[0], p1[1]};
+      *reinterpret_cast<uint2*>(planes + 2 * R * LD + off) = uint2{p2[0], p2[1]};
+    }
+  }
+};
+
+template <int TM, int TN, int BK, int RA, int RB>
+__device__ __forceinline__ void mfma_ktile_x3(const sv_u16* Ap, const sv_u16* Bp, int wm0, int wn0, int lane,
+                                              f32x16 (&acc)[TM][TN]) {
+  constexpr int LD = BK + 8;
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < BK / 16; ++s) {
+    sv_bf16x8v a0[TM], a1[TM], a2[TM], b0[TN], b1[TN], b2[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int o = (wm0 + 32 * i + r) * LD + 16 * s + 8 * h;
+      a0[i] = *reinterpret_cast<const sv_bf16x8v*>(Ap + o);
+      a1[i] = *reinterpret_cast<const sv_bf16x8v*>(Ap + RA * LD + o);
+      a2[i] = *reinterpret_cast<const sv_bf16x8v*>(Ap + 2 * RA * LD + o);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int o = (wn0 + 32 * j + r) * LD + 16 * s + 8 * h;
+      b0[j] = *reinterpret_cast<const sv_bf16x8v*>(Bp + o);
+      b1[j] = *reinterpret_cast<const sv_bf16x8v*>(Bp + RB * LD + o);
+      b2[j] = *reinterpret_cast<const sv_bf16x8v*>(Bp + 2 * RB * LD + o);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x16 c = acc[i][j];
+        c = mfma_bf16x8(a1[i], b1[j], c);
+        c = mfma_bf16x8(a2[i], b0[j], c);
+        c = mfma_bf16x8(a0[i], b2[j], c);
+        c = mfma_bf16x8(a1[i], b0[j], c);
+        c = mfma_bf16x8(a0[i], b1[j], c);
+        acc[i][j] = mfma_bf16x8(a0[i], b0[j], c);
+      }
+  }
+}
+
+// rolling-prefetch (depth D) main loop over X3 tiles.  lds (bytes): 2 stages x 3 planes x
+// (BM + BN) x (BK + 8) bf16 = 12 (BM + BN)(BK + 8) bytes.
+template <int BM, int BN, int NT, int BK, int D, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_x3(const float* __restrict__ A, long lda, const MapA& mapA,
+                                                 const float* __restrict__ B, long ldb, const MapB& mapB, int kbeg,
+                                                 int kend, void* lds_raw, int tid, int wm0, int wn0,
+                                                 f32x16 (&acc)[TM][TN]) {
+  using SA = KTileStageX3<BM, NT, BK>;
+  using SB = KTileStageX3<BN, NT, BK>;
+  constexpr int LD = BK + 8;
+  constexpr int PA = 3 * BM * LD, STAGE = 3 * (BM + BN) * LD;
+  sv_u16* lds = reinterpret_cast<sv_u16*>(lds_raw);
+  const int lane = tid & 63;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  SA sa[D];
+  SB sb[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (j < nk) {
+      sa[j].load(A, lda, mapA, kbeg + j * BK, kend, tid);
+      sb[j].load(B, ldb, mapB, kbeg + j * BK, kend, tid);
+    }
+  for (int k0 = 0; k0 < nk; k0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int kt = k0 + j;
+      if (kt < nk) {
+        sv_u16* buf = lds + (kt & 1) * STAGE;
+        sa[j].store(buf, tid);
+        sb[j].store(buf + PA, tid);
+        if (kt + D < nk) {
+          sa[j].load(A, lda, mapA, kbeg + (kt + D) * BK, kend, tid);
+          sb[j].load(B, ldb, mapB, kbeg + (kt + D) * BK, kend, tid);
+        }
+        __syncthreads();
+        mfma_ktile_x3<TM, TN, BK, BM, BN>(buf, buf + PA, wm0, wn0, lane, acc);
+      }
+    }
+  }
+  __syncthreads();
 }

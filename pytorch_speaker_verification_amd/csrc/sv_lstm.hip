@@ -11,6 +11,8 @@
 //   h_tm   [T+1, B, H]    h_tm[0] = h_{-1} = 0, h_tm[t+1] = h_t
 //   dgates [T, B, 4H]     dL/d(pre-activation gates)
 #include <stdlib.h>
+#include <algorithm>
+#include <atomic>
 #include "sv_common.h"
 #include "sv_gemm.h"
 #include "../../include/sv_ge2e.h"
@@ -120,7 +122,7 @@ __global__ void to_time_major_kernel(const float* __restrict__ x, float* __restr
 }
 
 // k-major ("NT") GEMM: both operands k-contiguous; the fast path for every large GEMM
-template <int BM, int BN, int EPI, int D = 1>
+template <int BM, int BN, int EPI, int D = 1, bool X6 = false, bool X3 = false>
 __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ A, long lda, const float* __restrict__ B,
                                                       long ldb, float* __restrict__ C, long ldc, long slab, int M,
                                                       int N, int K, int kchunk, const float* __restrict__ bias0,
@@ -139,8 +141,13 @@ __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ 
   const int wm0 = (w >> 1) * (BM / 2), wn0 = (w & 1) * (BN / 2);
   f32x16 acc[TM][TN];
   zero_acc(acc);
-  gemm_mainloop_km_d<BM, BN, 256, SV_BKM, D, TM, TN>(A, lda, RowMapLinear{tm * BM, M}, B, ldb, RowMapLinear{tn * BN, N},
-                                                kbeg, kend, lds, tid, wm0, wn0, acc);
+  if constexpr (X3)
+    gemm_mainloop_x3<BM, BN, 256, 16, 2, TM, TN>(A, lda, RowMapLinear{tm * BM, M}, B, ldb, RowMapLinear{tn * BN, N},
+                                                 kbeg, kend, lds, tid, wm0, wn0, acc);
+  else
+    gemm_mainloop_km_d<BM, BN, 256, SV_BKM, D, TM, TN, false, X6>(A, lda, RowMapLinear{tm * BM, M}, B, ldb,
+                                                                RowMapLinear{tn * BN, N}, kbeg, kend, lds, tid, wm0,
+                                                                wn0, acc);
   float* Cz = C + (EPI == EPI_SLAB ? (long)blockIdx.y * slab : 0);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -285,6 +292,7 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(const float* __restr
 // ============================================================================
 #define BWD_BM 64
 #define BWD_U 32
+#define X3_GBUF_BYTES (12 * (BWD_BM + BWD_U) * (16 + 8))  // one gate group's X3 double buffer
 
 __global__ __launch_bounds__(256) void lstm_step_bwd_kernel(
     const float* __restrict__ dgnext, const float* __restrict__ whhT, const float* __restrict__ dhup,
@@ -360,7 +368,7 @@ __global__ __launch_bounds__(256) void lstm_step_bwd_kernel(
 //         accumulator each, all sharing the same staged A/B tiles.
 //   K3v2: 4 groups of 2 waves, group = gate (its K range of W_hh^T), waves split the rows.
 // ============================================================================
-template <int BKX, int D = 1, bool DIAG = false>
+template <int BKX, int D = 1, bool DIAG = false, bool X6 = false, bool X3 = false>
 __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __restrict__ hprev,
                                                                const float* __restrict__ whh,
                                                                float* __restrict__ gates,
@@ -389,10 +397,15 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
   }
   f32x16 acc[1][1];
   zero_acc(acc);
-  if (hprev)
-    gemm_mainloop_km_d<FWD_BM, BN, 512, BKX, D, 1, 1, DIAG>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
-                                                 RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc,
-                                                 krot * (blockIdx.x + blockIdx.y));
+  if (hprev) {
+    if constexpr (X3)
+      gemm_mainloop_x3<FWD_BM, BN, 512, 32, 2, 1, 1>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
+                                                     RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc);
+    else
+      gemm_mainloop_km_d<FWD_BM, BN, 512, BKX, D, 1, 1, DIAG, X6>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0},
+                                                                 whh, H, RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid,
+                                                                 wm0, wn0, acc, krot * (blockIdx.x + blockIdx.y));
+  }
   float* pre = lds;
   float* hs = lds + FWD_BM * LDP;
 #pragma unroll
@@ -506,7 +519,7 @@ __global__ __launch_bounds__(NW * 64) void lstm_step_fwd_v4_kernel(const float* 
   }
 }
 
-template <int BKX, int D = 1, bool DIAG = false>
+template <int BKX, int D = 1, bool DIAG = false, bool X6 = false, bool X3 = false>
 __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
     const float* __restrict__ dgnext, const float* __restrict__ whhT, const float* __restrict__ dhup,
     const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
@@ -539,10 +552,17 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
   }
   f32x16 acc[1][1];
   zero_acc(acc);
-  if (dgnext)
-    gemm_mainloop_km_d<BWD_BM, BWD_U, 128, BKX, D, 1, 1, DIAG>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
-                                                    RowMapLinear{j0, H}, gate * H, (gate + 1) * H, lds + gate * GBUF,
-                                                    gt, (w & 1) * 32, 0, acc, krot * (blockIdx.x + blockIdx.y));
+  if (dgnext) {
+    if constexpr (X3)
+      gemm_mainloop_x3<BWD_BM, BWD_U, 128, 16, 2, 1, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
+                                                        RowMapLinear{j0, H}, gate * H, (gate + 1) * H,
+                                                        reinterpret_cast<char*>(lds) + gate * X3_GBUF_BYTES, gt,
+                                                        (w & 1) * 32, 0, acc);
+    else
+      gemm_mainloop_km_d<BWD_BM, BWD_U, 128, BKX, D, 1, 1, DIAG, X6>(
+          dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G, RowMapLinear{j0, H}, gate * H, (gate + 1) * H,
+          lds + gate * GBUF, gt, (w & 1) * 32, 0, acc, krot * (blockIdx.x + blockIdx.y));
+  }
   __syncthreads();
   float* red = lds;                    // [4][64][LDR]
   float* gT = lds + 4 * BWD_BM * LDR;  // [4*32][LDT]
@@ -593,6 +613,29 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
 // ============================================================================
 namespace {
 
+// fp32 GEMM multiplies on the bf16 MFMA pipe via the bf16x6 split (sv_gemm.h); SV_F32_EMU=1
+// Process-wide fp32 product mode (sv_set_f32_products; initial value from SV_F32_EMU):
+//   0  exact fp32 MFMA (v_mfma_f32_32x32x2_f32) everywhere -- the default
+//   1  bf16x6 split where it measured faster: NT GEMMs split in registers (x6), K2 split at the
+//      LDS store (x3), K3 exact
+//   2  x3 everywhere, 3  x6 everywhere (diagnostics)
+std::atomic<int> g_f32_mode{[] {
+  const char* e = getenv("SV_F32_EMU");
+  return (e && *e >= '0' && *e <= '3') ? *e - '0' : 0;
+}()};
+int gemm_x() {  // 0 exact, 1 x6, 2 x3
+  const int m = g_f32_mode.load(std::memory_order_relaxed);
+  return m == 1 || m == 3 ? 1 : m == 2 ? 2 : 0;
+}
+int k2_x() {
+  const int m = g_f32_mode.load(std::memory_order_relaxed);
+  return m == 1 || m == 2 ? 2 : m == 3 ? 1 : 0;
+}
+int k3_x() {
+  const int m = g_f32_mode.load(std::memory_order_relaxed);
+  return m == 2 ? 2 : m == 3 ? 1 : 0;
+}
+
 // prefetch depth of the NT GEMM main loop (SV_GEMM_PIPE = 1 or 2; measured equal at c2 --
 // the GEMMs are not latency-starved -- so 1, the lower-VGPR kernel, stays the default)
 int gemm_pipe() {
@@ -609,7 +652,13 @@ int launch_gemm_t(const float* A, long lda, const float* B, long ldb, float* C, 
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (AK && BKC) {
     constexpr int LDS_KM = 2 * (BM + BN) * (SV_BKM + 4);
-    if (gemm_pipe() == 2)
+    if (gemm_x() == 2)
+      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 1, false, true>), dim3(tiles, splitk), dim3(256),
+                         12 * (BM + BN) * (16 + 8), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+    else if (gemm_x() == 1)
+      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 1, true>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float),
+                         s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+    else if (gemm_pipe() == 2)
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 2>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float), s,
                          A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
     else
@@ -664,6 +713,12 @@ GemmPlan plan_gemm(int M, int N, int K) {
 }
 
 }  // namespace
+
+// fp32 product mode (see g_f32_mode): returns the previous mode, or SV_EARG for an unknown one
+extern "C" int sv_set_f32_products(int mode) {
+  if (mode < 0 || mode > 3) return SV_EARG;
+  return g_f32_mode.exchange(mode);
+}
 
 extern "C" size_t sv_gemm_f32_workspace(int M, int N, int K) {
   const GemmPlan p = plan_gemm(M, N, K);
@@ -772,6 +827,10 @@ int bwd_bk() {
   return v;
 }
 // step-kernel variant: 2 = 8-wave (default), 1 = 4-wave; SV_STEP_VARIANT overrides (A/B timing)
+constexpr int FWD_X3_MAIN = 12 * (FWD_BM + 4 * FWD_U) * (32 + 8);
+constexpr int FWD_X3_LDS = FWD_X3_MAIN > FWD_LDS ? FWD_X3_MAIN : FWD_LDS;
+constexpr int BWD_X3_MAIN = 4 * X3_GBUF_BYTES;
+constexpr int BWD_X3_LDS = BWD_X3_MAIN > BWD_LDS ? BWD_X3_MAIN : BWD_LDS;
 constexpr int FWD_LDS64 = 2 * (FWD_BM + 4 * FWD_U) * (64 + 4) * (int)sizeof(float);
 int step_variant() {
   static int v = [] {
@@ -824,6 +883,12 @@ void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh
   if (step_variant() == 4)
     hipLaunchKernelGGL((lstm_step_fwd_v4_kernel<FWD4_U, 4, SV_BKM>), grid, dim3(256), FWD4_LDS, s, hp, whh, g, cp, c, h,
                        hT, ldhT, t, Bp, B, H);
+  else if (step_variant() == 2 && k2_x() == 2)
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, false, false, true>), grid, dim3(512), FWD_X3_LDS, s, hp,
+                       whh, g, cp, c, h, hT, ldhT, t, Bp, B, H, k_rot());
+  else if (step_variant() == 2 && km_pipe() == 2 && k2_x() == 1)
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, false, true>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp,
+                       c, h, hT, ldhT, t, Bp, B, H, k_rot());
   else if (step_variant() == 2 && km_pipe() == 2 && step_diag())
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, true>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
                        hT, ldhT, t, Bp, B, H, k_rot());
@@ -851,6 +916,12 @@ void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* wh
   if (step_variant() >= 2 && bwd_bk() == 16)
     hipLaunchKernelGGL(lstm_step_bwd_v2_kernel<16>, grid, dim3(512), BWD_LDS16, s, dgn, whhT, up, dcfi, acts, ct, cp,
                        dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  else if (step_variant() >= 2 && k3_x() == 2)
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, false, false, true>), grid, dim3(512), BWD_X3_LDS, s, dgn,
+                       whhT, up, dcfi, acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
+  else if (step_variant() >= 2 && km_pipe() == 2 && k3_x() == 1)
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, false, true>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up,
+                       dcfi, acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
   else if (step_variant() >= 2 && km_pipe() == 2 && step_diag())
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, true>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
                        acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());

@@ -20,6 +20,16 @@ from ._lib import call, ptr, require_device, stream_of, lib
 
 PIPELINE_CHUNK = int(os.environ.get("SV_PIPELINE_CHUNK", "32"))  # 0 disables the layer pipeline
 
+F32_PRODUCT_MODES = {"mfma_f32": 0, "bf16x6": 1}
+
+
+def set_f32_products(mode):
+    """Select how the fp32 path forms its products (process-wide, like a BLAS math mode):
+    "mfma_f32" (default, exact fp32 MFMA) or "bf16x6" (three-way bf16 split, six bf16 MFMA
+    products per fp32 product, fp32 accumulation; include/sv_ge2e.h).  Returns the previous mode."""
+    prev = lib().sv_set_f32_products(F32_PRODUCT_MODES[mode])
+    return {v: k for k, v in F32_PRODUCT_MODES.items()}.get(prev, str(prev))
+
 
 class _StreamPool:
     """Side streams + events for the layer-pipelined schedules (one set per device)."""

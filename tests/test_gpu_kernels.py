@@ -137,3 +137,54 @@ def test_gemm_bf16(M, N, K):
          torch.cuda.current_stream().cuda_stream)
     err = (C.cpu().double() - ref).abs().max().item()
     assert err <= 2e-6 * K ** 0.5 * ref.abs().max().item() + 1e-5, err
+
+
+def test_f32_products_bf16x6_accuracy_and_step():
+    """The opt-in bf16x6 fp32-product mode: GEMM error against fp64 no larger than the exact
+    fp32-MFMA path's (x1.25 margin), and a full training step that agrees with the exact path
+    to fp32 level (loss 1e-5 relative, parameters 1e-5 relative)."""
+    from pytorch_speaker_verification_amd._lib import call, ptr, stream_of
+    from pytorch_speaker_verification_amd.ops import set_f32_products
+    g = np.random.default_rng(3)
+    M, N, K = 256, 512, 768
+    A = g.standard_normal((M, K)).astype(np.float32)
+    B = g.standard_normal((N, K)).astype(np.float32)
+    ref = A.astype(np.float64) @ B.astype(np.float64).T
+    scale = np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64).T
+    errs = {}
+    for mode in ("mfma_f32", "bf16x6"):
+        prev = set_f32_products(mode)
+        try:
+            C = torch.empty(M, N, device=DEV)
+            call("sv_gemm_f32", 1, 1, M, N, K, ptr(torch.tensor(A, device=DEV)), K, ptr(torch.tensor(B, device=DEV)),
+                 K, ptr(C), N, None, None, 0.0, None, stream_of(C))
+            errs[mode] = float((np.abs(C.cpu().numpy() - ref) / scale).max())
+        finally:
+            set_f32_products(prev)
+    assert errs["bf16x6"] <= 1.25 * errs["mfma_f32"], errs
+    assert errs["bf16x6"] < 1e-6, errs
+
+    from conftest import model_dims
+    from pytorch_speaker_verification_amd.speech_embedder_net import GE2ELoss, SpeechEmbedder
+    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+    dims, Ns, Ms, T = (40, 128, 3, 64), 6, 4, 20
+    sd = recipe.make_weights(77, *dims, scale=3.0)
+    x = torch.tensor(recipe.make_frames(78, Ns * Ms, T, dims[0]), device=DEV)
+    res = {}
+    for mode in ("mfma_f32", "bf16x6"):
+        with model_dims(*dims):
+            net = SpeechEmbedder()
+        with torch.no_grad():
+            for k, v in net.state_dict().items():
+                v.copy_(torch.as_tensor(sd[k]))
+        net = net.to(DEV)
+        prev = set_f32_products(mode)
+        try:
+            tr = GE2ETrainer(net, GE2ELoss(DEV), lr=0.01)
+            loss = float(tr.step(x, Ns, Ms))
+            res[mode] = (loss, tr.flat_p.detach().cpu().numpy().copy())
+        finally:
+            set_f32_products(prev)
+    (l0, p0), (l1, p1) = res["mfma_f32"], res["bf16x6"]
+    assert abs(l1 - l0) <= 1e-5 * abs(l0), (l0, l1)
+    assert np.abs(p1 - p0).max() <= 1e-5 * np.abs(p0).max()
