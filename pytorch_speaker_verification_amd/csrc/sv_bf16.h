@@ -103,7 +103,7 @@ __device__ __forceinline__ void gemm_mainloop_bf(const bf16_t* __restrict__ A, l
 // Register-prefetch main loop for the latency-bound recurrent steps: every global load of a
 // super-chunk of SC k-tiles is issued up front (one HBM/L2 round trip per super-chunk instead
 // of one per k-tile), then the tiles are staged through two LDS buffers, one barrier each.
-template <int BM, int BN, int NT, int SC, int TM, int TN, class MapA, class MapB>
+template <int BM, int BN, int NT, int SC, int TM, int TN, class MapA, class MapB, bool DIAG = false>
 __device__ __forceinline__ void gemm_mainloop_bf_rp(const bf16_t* __restrict__ A, long lda, const MapA& mapA,
                                                     const bf16_t* __restrict__ B, long ldb, const MapB& mapB,
                                                     int kbeg, int kend, bf16_t* lds, int tid, int wm0, int wn0,
@@ -118,19 +118,24 @@ __device__ __forceinline__ void gemm_mainloop_bf_rp(const bf16_t* __restrict__ A
   for (int c0 = 0; c0 < nk; c0 += SC) {
     SA sa[SC];
     SB sb[SC];
+    // DIAG (profiling only): only the first super-chunk is fetched; later k-tiles re-use LDS
+    if (!DIAG || c0 == 0) {
 #pragma unroll
-    for (int j = 0; j < SC; ++j) {
-      if (c0 + j < nk) {
-        sa[j].load(A, lda, mapA, kbeg + (c0 + j) * BBK, kend, tid);
-        sb[j].load(B, ldb, mapB, kbeg + (c0 + j) * BBK, kend, tid);
+      for (int j = 0; j < SC; ++j) {
+        if (c0 + j < nk) {
+          sa[j].load(A, lda, mapA, kbeg + (c0 + j) * BBK, kend, tid);
+          sb[j].load(B, ldb, mapB, kbeg + (c0 + j) * BBK, kend, tid);
+        }
       }
     }
 #pragma unroll
     for (int j = 0; j < SC; ++j) {
       if (c0 + j < nk) {
-        bf16_t* buf = lds + (it & 1) * BUF;
-        sa[j].store(buf, tid);
-        sb[j].store(buf + BM * LD, tid);
+        bf16_t* buf = lds + (DIAG ? 0 : (it & 1) * BUF);
+        if (!DIAG || c0 == 0) {
+          sa[j].store(buf, tid);
+          sb[j].store(buf + BM * LD, tid);
+        }
         __syncthreads();
         mfma_ktile_bf<TM, TN, BBK, LD>(buf, buf + BM * LD, wm0, wn0, lane, acc);
         ++it;
@@ -183,13 +188,17 @@ __device__ __forceinline__ void gemm_mainloop_bf_pipe(const bf16_t* __restrict__
   __syncthreads();
 }
 
-// SC <= 12: super-chunk loop of SC tiles; SC = 100 + D: rolling pipeline of depth D
+// SC <= 12: super-chunk loop of SC tiles; SC = 100 + D: rolling pipeline of depth D;
+// SC = 200 + x: diagnostic super-chunk loop that fetches only its first super-chunk
 template <int BM, int BN, int NT, int SC, int TM, int TN, class MapA, class MapB>
 __device__ __forceinline__ void gemm_mainloop_step(const bf16_t* __restrict__ A, long lda, const MapA& mapA,
                                                    const bf16_t* __restrict__ B, long ldb, const MapB& mapB,
                                                    int kbeg, int kend, bf16_t* lds, int tid, int wm0, int wn0,
                                                    f32x16 (&acc)[TM][TN]) {
-  if constexpr (SC > 100)
+  if constexpr (SC > 200)
+    gemm_mainloop_bf_rp<BM, BN, NT, SC - 200, TM, TN, MapA, MapB, true>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds,
+                                                                        tid, wm0, wn0, acc);
+  else if constexpr (SC > 100)
     gemm_mainloop_bf_pipe<BM, BN, NT, SC - 100, TM, TN>(A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0,
                                                         acc);
   else

@@ -440,14 +440,17 @@ int bf16_sc() {
   static int v = [] {
     const char* e = getenv("SV_BF16_SC");
     const int x = e ? atoi(e) : 3;
-    return (x == 3 || x == 4 || x == 6 || x == 104 || x == 106 || x == 112) ? x : 12;
+    return (x == 3 || x == 4 || x == 6 || x == 104 || x == 106 || x == 112 || x == 203) ? x : 12;
   }();
   return v;
 }
 void launch_fwd_bf16(dim3 grid, hipStream_t s, const bf16_t* hp, const bf16_t* whh, float* g, const float* cp,
                      float* c, float* h, bf16_t* hb, bf16_t* hT, long ldhT, int t, int Bp, int B, int H) {
   const int sc = bf16_sc();
-  if (sc == 104)
+  if (sc == 203)
+    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<203>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
+                       t, Bp, B, H);
+  else if (sc == 104)
     hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<104>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
                        t, Bp, B, H);
   else if (sc == 106)
@@ -507,7 +510,7 @@ int bf16_bsc() {
   static int v = [] {
     const char* e = getenv("SV_BF16_BSC");
     const int x = e ? atoi(e) : 6;
-    return (x == 2 || x == 3 || x == 103 || x == 104 || x == 106) ? x : 6;
+    return (x == 2 || x == 3 || x == 103 || x == 104 || x == 106 || x == 206) ? x : 6;
   }();
   return v;
 }
@@ -515,7 +518,10 @@ void launch_bwd_bf16(dim3 grid, hipStream_t s, const bf16_t* dgn, const bf16_t* 
                      const float* dcfi, const float* acts, const float* ct, const float* cp, bf16_t* dg, float* dcfo,
                      bf16_t* dgT, long lddgT, int t, int Bp, int B, int H) {
   const int sc = bf16_bsc();
-  if (sc == 103)
+  if (sc == 206)
+    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<206>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
+                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  else if (sc == 103)
     hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<103>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
                        dg, dcfo, dgT, lddgT, t, Bp, B, H);
   else if (sc == 104)
