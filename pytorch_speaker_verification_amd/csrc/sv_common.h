@@ -19,6 +19,7 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
 // stack-backward schedule switch (sv_lstm.hip; env SV_DW_CHUNKED)
 int dw_chunked_layer(int l);
+int dx_side();
 
 #define SV_LAUNCH_CHECK()                                  \
   do {                                                     \

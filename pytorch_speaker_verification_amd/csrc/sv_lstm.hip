@@ -795,6 +795,16 @@ extern "C" int sv_colsum(const float* X, int R, int C, float* out, float* worksp
 // whole-T behind the layer's recurrence.  SV_DW_CHUNKED: 0 (default) none, 1 all layers,
 // 2 layer 0 only.  Measured at c2 (4 HW queues): 0 = 72.4 ms, 2 = 72.5, 1 = 76.5 -- the
 // chunk GEMMs slow the concurrent recurrences more than they shorten the tail.
+// stack bwd: each chunk's dx GEMM on the layer's second stream (SV_DX_SIDE=1) instead of
+// behind the chunk on the recurrence stream (0, default; measured at c2: 69.3 vs 72.3 ms)
+int dx_side() {
+  static int v = [] {
+    const char* e = getenv("SV_DX_SIDE");
+    return (e && *e == '1') ? 1 : 0;
+  }();
+  return v;
+}
+
 int dw_chunked_layer(int l) {
   static int v = [] {
     const char* e = getenv("SV_DW_CHUNKED");
@@ -914,8 +924,8 @@ void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* wh
                      const float* acts, const float* ct, const float* cp, float* dg, float* dcfo, float* dgT,
                      long lddgT, int t, int Bp, int B, int H) {
   if (step_variant() >= 2 && bwd_bk() == 16)
-    hipLaunchKernelGGL(lstm_step_bwd_v2_kernel<16>, grid, dim3(512), BWD_LDS16, s, dgn, whhT, up, dcfi, acts, ct, cp,
-                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<16, 2>), grid, dim3(512), BWD_LDS16, s, dgn, whhT, up, dcfi, acts, ct,
+                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, 0);
   else if (step_variant() >= 2 && k3_x() == 2)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, false, false, true>), grid, dim3(512), BWD_X3_LDS, s, dgn,
                        whhT, up, dcfi, acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
@@ -1186,12 +1196,24 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
                         dcf_out, dgT[l], (long)TBp, t, Bp, B, H);
         SV_LAUNCH_CHECK();
       }
-      if (l > 0) {  // dh_up of layer l-1 for this chunk: dx = dG W_ih
+      if (l > 0 && dx_side()) {  // dx on the layer's second stream: the recurrence goes on at once
+        if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
+        if ((e = hipStreamWaitEvent(side[L + l], ev[l * nch + c], 0)) != hipSuccess) return (int)e;
         rc = sv_gemm_f32(1, 1, (t1 - t0) * B, Fl, 4 * H, dgates[l] + t0 * BG, 4L * H, ws.wihT, 4L * H,
-                         dx[l] + (long)t0 * B * Fl, Fl, nullptr, nullptr, 0.f, ws.gws, s);
+                         dx[l] + (long)t0 * B * Fl, Fl, nullptr, nullptr, 0.f, ws.gws2, side[L + l]);
         if (rc) return rc;
+        // re-record: layer l-1 (issued after this loop) waits for the dx of this chunk
+        if ((e = hipEventRecord(ev[l * nch + c], side[L + l])) != hipSuccess) return (int)e;
+        if (c == 0 && (e = hipStreamWaitEvent(s, ev[l * nch + c], 0)) != hipSuccess) return (int)e;
+        if (!dw_chunked_layer(l)) continue;
+      } else {
+        if (l > 0) {  // dh_up of layer l-1 for this chunk: dx = dG W_ih
+          rc = sv_gemm_f32(1, 1, (t1 - t0) * B, Fl, 4 * H, dgates[l] + t0 * BG, 4L * H, ws.wihT, 4L * H,
+                           dx[l] + (long)t0 * B * Fl, Fl, nullptr, nullptr, 0.f, ws.gws, s);
+          if (rc) return rc;
+        }
+        if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
       }
-      if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
       if (!dw_chunked_layer(l)) continue;
       // this chunk's share of dW_hh / dW_ih (K = its time columns), accumulated on the layer's
       // weight-gradient stream while the recurrence moves on to the next chunk
