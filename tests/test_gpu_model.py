@@ -199,3 +199,47 @@ def test_c5_per_gpu_shape_bf16_and_f32():
     for d32, d16 in zip(deltas["f32"], deltas["bf16"]):
         rel = float((d16 - d32).norm() / d32.norm().clamp_min(1e-30))
         assert rel < 1e-1, rel
+
+
+@pytest.mark.parametrize("dims,N,M,T", [((40, 96, 2, 24), 3, 3, 5),     # B = 9: odd, below every tile
+                                        ((40, 64, 3, 32), 2, 2, 1),     # T = 1, M = 2 (leave-one-out of one)
+                                        ((40, 72, 2, 20), 5, 7, 37)])   # H = 72, D = 20, T > pipeline chunk
+def test_ragged_training_step_against_torch_port(dims, N, M, T):
+    """Fused trainer steps (fp32) at ragged sizes against the stock PyTorch port on the host:
+    loss, and parameters after two clipped SGD steps."""
+    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+    sd = recipe.make_weights(N * 31 + M * 7 + T, *dims, scale=2.0)
+    x = recipe.make_frames(N + M + T, N * M, T, dims[0])
+    net, ge2e = _build(dims, sd)
+    tr = GE2ETrainer(net, ge2e, lr=0.01)
+    xd = torch.tensor(x, device=DEV)
+    losses = [float(tr.step(xd, N, M)) for _ in range(2)]
+    port = torch_port.SpeechEmbedderPort(*dims)
+    torch_port.load_recipe_weights(port, sd)
+    w = torch.nn.Parameter(torch.tensor(10.0))
+    b = torch.nn.Parameter(torch.tensor(-5.0))
+    opt = torch.optim.SGD([{"params": port.parameters()}, {"params": [w, b]}], lr=0.01)
+    ref = [float(torch_port.train_step(port, w, b, opt, torch.tensor(x), N, M)) for _ in range(2)]
+    np.testing.assert_allclose(losses, ref, rtol=1e-4)
+    got = {k: v.detach().cpu().numpy() for k, v in net.state_dict().items()}
+    for k, v in port.state_dict().items():
+        np.testing.assert_allclose(got[k], v.numpy(), atol=5e-5, err_msg=k)
+    np.testing.assert_allclose([ge2e.w.item(), ge2e.b.item()], [w.item(), b.item()], atol=1e-5)
+
+
+@pytest.mark.parametrize("dims,N,M,T", [((40, 96, 2, 24), 3, 3, 5), ((40, 64, 3, 32), 2, 2, 1),
+                                        ((40, 72, 2, 20), 5, 7, 37)])
+def test_ragged_training_step_bf16(dims, N, M, T):
+    """The bf16-operand step at the same ragged sizes (Bp padding to 8, partial k-tiles, T = 1,
+    two pipeline chunks): loss within 1e-2 relative of the fp32 HIP step, finite updates."""
+    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+    sd = recipe.make_weights(N * 31 + M * 7 + T, *dims, scale=2.0)
+    xd = torch.tensor(recipe.make_frames(N + M + T, N * M, T, dims[0]), device=DEV)
+    out = {}
+    for prec in ("f32", "bf16"):
+        net, ge2e = _build(dims, sd)
+        net.precision = prec
+        tr = GE2ETrainer(net, ge2e, lr=0.01)
+        out[prec] = [float(tr.step(xd, N, M)) for _ in range(2)]
+        assert all(torch.isfinite(p).all() for p in net.parameters())
+    np.testing.assert_allclose(out["bf16"], out["f32"], rtol=1e-2)
