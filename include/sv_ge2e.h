@@ -179,8 +179,11 @@ int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* con
                            float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace, int chunk,
                            hipStream_t main, const hipStream_t* side, hipEvent_t* ev);
 
-/* ---- persistent recurrences (one launch per layer for all T; sv_persist.hip).  The stack
- * functions use them when sv_persist_fwd_ok(B, H) (grid co-resident on this device).
+/* ---- persistent recurrences (one launch per layer for all T; sv_persist.hip).  The bf16 stack
+ * forward uses them (by default when H = 768: W_hh held in registers) when sv_persist_fwd_ok(B, H)
+ * (grid co-resident on this device).  Their arrival counters are one device-global block: calls
+ * that run persistent recurrences must not execute concurrently on one device (the stack
+ * functions serialise them on their `main` stream).
  * sv_persist_status: 0 ok, 1 a hand-off wait timed out since the last call (device sync;
  * clears the flag). */
 int sv_persist_fwd_ok(int B, int H);

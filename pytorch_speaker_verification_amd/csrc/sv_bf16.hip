@@ -484,17 +484,16 @@ int wavefront_fwd() {
   }();
   return v;
 }
-// stack forward recurrences: per-step launches, layer-pipelined (0, default) or one persistent
-// launch per layer (1; SV_PERSIST).  Measured at c3 (3-layer forward, T = 160): per-step 7.8 ms,
-// persistent 8.5 ms -- of which the hand-off waits cost 0.45 ms, the epilogues (HBM traffic of
-// the fp32 gate pre-activations / activations) ~2.6 ms and the step GEMMs ~3.2 ms; the per-step
-// schedule wins because it overlaps the layers, which co-resident persistent grids cannot.
-int persist_fwd() {
+// stack forward recurrences: one persistent launch per layer (W_hh held in registers,
+// sv_persist.hip) or per-step launches, layer-pipelined.  SV_PERSIST: unset = persistent when
+// H = 768 (the W-stationary kernel; measured c3 21.5 vs 22.2 ms), 1 = always persistent
+// (H != 768 falls back to the LDS-staged persistent kernel), 0 = per-step.
+int persist_fwd(int H) {
   static int v = [] {
     const char* e = getenv("SV_PERSIST");
-    return (e && *e == '1') ? 1 : 0;
+    return e ? (*e == '1' ? 1 : 0) : -1;
   }();
-  return v;
+  return v < 0 ? (H == 768) : v;
 }
 void launch_wave_fwd_bf16(dim3 grid, hipStream_t s, const WaveFwdArgs& a, int st) {
   const int sc = bf16_sc();
@@ -691,7 +690,7 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
   const int Bp = (B + 7) & ~7;
   const long ldhT = (long)(T + 1) * Bp;
   hipError_t e;
-  if (persist_fwd() && sv_persist_fwd_ok(B, H)) {
+  if (persist_fwd(H) && sv_persist_fwd_ok(B, H)) {
     // persistent schedule on `main`: per layer the whole-T K1 GEMM, then one launch for the
     // recurrence (sv_persist.hip); layers run one after another
     for (int l = 0; l < L; ++l) {

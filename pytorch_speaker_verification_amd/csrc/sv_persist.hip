@@ -4,7 +4,7 @@
 // misses per bf16 step launch ~ the per-XCD W_hh + h footprint).  Here each workgroup keeps the
 // same (row block, unit block) tile for the whole sequence: its W_hh slice stays in the XCD's
 // L2, its cell state stays in registers, and only h_{t-1} crosses workgroups.  Selected by
-// SV_PERSIST=1 (see persist_fwd() in sv_bf16.hip for the measured trade-off).
+// (see persist_fwd() in sv_bf16.hip for when the stack forward uses it).
 //
 // Hand-off of h between timesteps (MI355X_MICROARCH.md, inter-workgroup visibility, hand-off
 // table row 1): every store of the handed-off bytes (h_bf[t+1], 4-B packed pairs) is an `sc1`
@@ -221,6 +221,165 @@ __global__ __launch_bounds__(512) void lstm_persist_fwd_bf16_kernel(const bf16_t
 }
 
 // ============================================================================
+// W-stationary variant (H = 16 NS): 4 waves, wave g owns gate g of the tile's 32 units for all
+// 64 rows (two 32x32 accumulators) and keeps its W_hh rows -- 32 x H bf16, the MFMA B
+// fragments of every k-step -- in registers for the whole sequence.  Per step only h_{t-1}
+// (64 rows x H) is staged into LDS (two halves of sc1 buffer loads); each wave reads it as A
+// fragments: 1 LDS fragment per MFMA instead of 2, no W traffic at all after the prologue.
+// ============================================================================
+template <int NS>
+__global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf16_t* __restrict__ whh_bf,
+                                                                       float* __restrict__ gates,
+                                                                       float* __restrict__ c_tm,
+                                                                       float* __restrict__ h_tm, bf16_t* h_bf,
+                                                                       bf16_t* __restrict__ hT, long ldhT, int T,
+                                                                       int Bp, int B, int H, unsigned* cnt) {
+  constexpr int K = NS * 16, LDA = K + 8, HALF = NS / 2 * 16;
+  constexpr int LDP = 4 * BF_U + 4, LDH = BF_BM + 1;
+  constexpr int PER = BF_BM * BF_U / 256;  // epilogue elements per thread
+  static_assert(NS % 2 == 0, "two staging halves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);                          // [64][LDA]
+  float* pre = reinterpret_cast<float*>(smem + BF_BM * LDA * 2);         // [64][LDP]
+  float* hs = pre + BF_BM * LDP;                                         // [32][LDH]
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int j0 = blockIdx.x * BF_U, b0 = blockIdx.y * BF_BM;
+  const long G = 4L * H, BH = (long)B * H;
+  unsigned* my_cnt = cnt + blockIdx.y * SV_PCNT_STRIDE;
+  const unsigned producers = gridDim.x;
+  // this wave's W_hh fragments: B[k][n] = W[g H + j0 + n][k], lane (n = r, k = 16 s + 8 hh .. +7)
+  bf16x8_t wreg[NS];
+  {
+    const bool wok = j0 + r < H;
+    const bf16_t* wrow = whh_bf + ((long)g * H + j0 + r) * K + 8 * hh;
+#pragma unroll
+    for (int s2 = 0; s2 < NS; ++s2) {
+      bf16x8_t z = {};
+      wreg[s2] = wok ? *reinterpret_cast<const bf16x8_t*>(wrow + 16 * s2) : z;
+    }
+  }
+  float cst[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) cst[k] = 0.f;
+  // staging map of one half (64 rows x HALF bf16 = 64 * HALF / 8 16-B chunks over 256 threads)
+  constexpr int CH = BF_BM * HALF / 8 / 256;
+  // x W_ih^T + b of step t (K1 output), prefetched one step ahead: independent of the recurrence
+  float xg[PER][4];
+  auto load_xg = [&](int tt) {
+    const float* gt = gates + (long)tt * B * G;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = tid + 256 * k, b = e / BF_U, u = e % BF_U;
+      const int gb = b0 + b, gj = j0 + u;
+      const bool ok = gb < B && gj < H;
+      const float* gp = gt + (long)gb * G + gj;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xg[k][q] = ok ? gp[q * H] : 0.f;
+    }
+  };
+  load_xg(0);
+  for (int t = 0; t < T; ++t) {
+    float* gt = gates + (long)t * B * G;
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+    if (t > 0) {
+      if (tid == 0) persist_wait(my_cnt, producers * (unsigned)t);
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t ra = sv_rsrc(h_bf + (long)t * BH, (unsigned)(BH * 2));
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        uint4 v[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {  // chunk q: row q / (HALF/8), column chunk q % (HALF/8)
+          const int q = tid + 256 * i, row = q / (HALF / 8), c = (q % (HALF / 8)) * 8 + half * HALF;
+          const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(
+              ra, ((unsigned)(b0 + row) * (unsigned)H + (unsigned)c) * 2u, 0, 16 /* sc1 */);
+          v[i] = uint4{x.x, x.y, x.z, x.w};
+        }
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int q = tid + 256 * i, row = q / (HALF / 8), c = (q % (HALF / 8)) * 8 + half * HALF;
+          *reinterpret_cast<uint4*>(As + row * LDA + c) = v[i];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2) {
+        const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(As + r * LDA + 16 * s2 + 8 * hh);
+        const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(As + (32 + r) * LDA + 16 * s2 + 8 * hh);
+        acc0 = mfma_bf16(a0, wreg[s2], acc0);
+        acc1 = mfma_bf16(a1, wreg[s2], acc1);
+      }
+    }
+    // gate exchange: wave g's [64 rows][32 units] -> pre[row][g * 32 + unit]
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      pre[acc_row(i, lane) * LDP + g * BF_U + r] = acc0[i];
+      pre[(32 + acc_row(i, lane)) * LDP + g * BF_U + r] = acc1[i];
+    }
+    __syncthreads();
+    float* ct = c_tm + (long)t * BH;
+    float* ht = h_tm + (long)(t + 1) * BH;
+    bf16_t* hb = h_bf + (long)(t + 1) * BH;
+    float act[PER][4], hv[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = tid + 256 * k, b = e / BF_U, u = e % BF_U;
+      const int gb = b0 + b, gj = j0 + u;
+      const bool ok = gb < B && gj < H;
+      const float* pr = pre + b * LDP + u;
+      act[k][0] = sv_sigmoid(pr[0] + xg[k][0]);
+      act[k][1] = sv_sigmoid(pr[BF_U] + xg[k][1]);
+      act[k][2] = tanhf(pr[2 * BF_U] + xg[k][2]);
+      act[k][3] = sv_sigmoid(pr[3 * BF_U] + xg[k][3]);
+      const float c = act[k][1] * cst[k] + act[k][0] * act[k][2];
+      const float h = act[k][3] * tanhf(c);
+      cst[k] = c;
+      hv[k] = h;
+      // the hand-off first: lanes (u, u+1) pair up, the even lane stores both (4-B sc1 store)
+      const unsigned hbits = to_bf(h);
+      const unsigned nb = __shfl_down(hbits, 1, 64);
+      if (ok && !(u & 1))
+        __hip_atomic_store(reinterpret_cast<unsigned*>(hb + (long)gb * H + gj), hbits | (nb << 16),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      hs[u * LDH + b] = h;
+    }
+    __syncthreads();  // hs complete
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = tid + 256 * k, b = e / BF_U, u = e % BF_U;
+      const int gb = b0 + b, gj = j0 + u;
+      if (gb < B && gj < H) {
+        float* gp = gt + (long)gb * G + gj;
+        gp[0] = act[k][0];
+        gp[H] = act[k][1];
+        gp[2 * H] = act[k][2];
+        gp[3 * H] = act[k][3];
+        ct[(long)gb * H + gj] = cst[k];
+        ht[(long)gb * H + gj] = hv[k];
+      }
+    }
+    if (hT) {
+      for (int e = tid; e < BF_BM * BF_U; e += 256) {
+        const int u = e / BF_BM, b = e % BF_BM;
+        const int gb = b0 + b, gj = j0 + u;
+        if (gb >= B || gj >= H) continue;
+        bf16_t* row = hT + (long)gj * ldhT;
+        row[(long)(t + 1) * Bp + gb] = to_bf(hs[u * LDH + b]);
+        if (t == 0) row[gb] = 0;
+      }
+    }
+    // publish h_t (every store of this step drained first), then prefetch the next x-projection
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t + 1 < T) load_xg(t + 1);
+  }
+}
+
+// ============================================================================
 // host side
 // ============================================================================
 namespace {
@@ -233,6 +392,15 @@ int cu_count() {
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
   return n;
+}
+// W_hh held in registers (lstm_persist2_fwd_bf16_kernel) when H = 768; SV_PERSIST_W=0 forces the
+// LDS-staged persistent kernel
+int persist_wregs() {
+  static int v = [] {
+    const char* e = getenv("SV_PERSIST_W");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return v;
 }
 unsigned* pcnt_ptr() {
   void* p = nullptr;
@@ -272,8 +440,15 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
     const char* v = getenv("SV_PERSIST_DEBUG");
     return v ? atoi(v) : 0;
   }();
-  hipLaunchKernelGGL(lstm_persist_fwd_bf16_kernel<4>, grid, dim3(512), PFWD_LDS, stream, whh_bf, gates, c_tm, h_tm,
-                     h_bf, hT, ldhT, T, Bp, B, H, cnt, dbg);
+  if (H == 768 && persist_wregs()) {
+    constexpr int NS = 48, LDA = NS * 16 + 8;
+    constexpr size_t lds = (size_t)BF_BM * LDA * 2 + (size_t)(BF_BM * (4 * BF_U + 4) + BF_U * (BF_BM + 1)) * 4;
+    hipLaunchKernelGGL(lstm_persist2_fwd_bf16_kernel<NS>, grid, dim3(256), lds, stream, whh_bf, gates, c_tm, h_tm,
+                       h_bf, hT, ldhT, T, Bp, B, H, cnt);
+  } else {
+    hipLaunchKernelGGL(lstm_persist_fwd_bf16_kernel<4>, grid, dim3(512), PFWD_LDS, stream, whh_bf, gates, c_tm, h_tm,
+                       h_bf, hT, ldhT, T, Bp, B, H, cnt, dbg);
+  }
   SV_LAUNCH_CHECK();
   return SV_OK;
 }
