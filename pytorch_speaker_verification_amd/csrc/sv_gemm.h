@@ -136,14 +136,15 @@ __device__ __forceinline__ void gemm_mainloop(const float* __restrict__ A, long 
   }
 }
 
-template <int TM, int TN>
-__device__ __forceinline__ void zero_acc(f32x16 (&acc)[TM][TN]) {
+template <int TM, int TN, class AccT>
+__device__ __forceinline__ void zero_acc(AccT (&acc)[TM][TN]) {
+  constexpr int NR = sizeof(AccT) / sizeof(float);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
 }
 
 // bijective XCD-aware block remap (cdna_hip_programming.md §5, T1): blocks that the
@@ -152,6 +153,24 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
   if (q == 0) return orig;
   return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+}
+
+// XCD-aware 2-D tile map for the per-step kernels (grid nbx unit-blocks x nby row-blocks):
+// the dispatcher deals linear block L to XCD L % 8; give each XCD a compact rectangle of
+// (nby/2) x (nbx/4) tiles so the operand panels it reads (row-blocks of the left operand,
+// unit-blocks of W) are shared through its own L2 instead of every XCD pulling every row-block
+// from the Infinity Cache.  Falls back to the identity map when the grid does not split.
+// Enabled by `on` (runtime switch, so one binary can A/B it).
+__device__ __forceinline__ void xcd_tile_map(int on, int& bx, int& by) {
+  const int nbx = gridDim.x, nby = gridDim.y;
+  bx = blockIdx.x;
+  by = blockIdx.y;
+  if (!on || (nbx & 3) || (nby & 1)) return;
+  const int L = blockIdx.x + nbx * blockIdx.y;
+  const int xcd = L & 7, slot = L >> 3;
+  const int ru = nbx >> 2, rr = nby >> 1;  // rectangle: rr row-blocks x ru unit-blocks
+  bx = (xcd & 3) * ru + slot % ru;
+  by = (xcd >> 2) * rr + slot / ru;
 }
 
 // ===========================================================================
@@ -170,16 +189,24 @@ struct KTileStage {
   static_assert(NV >= 1 && NV * NT == R * C4, "tile/thread mismatch");
   f32x4 v[NV];
 
+  // Buffer loads relative to the tile's first row (a uniform base, so the resource lives in
+  // SGPRs): an element outside the tile (row past the map's limit, or k >= K) gets an offset
+  // past num_records and reads 0 -- branch-free, unlike guarded global loads, which the
+  // compiler wraps in one exec-mask branch per load.  Needs the tile's row span x ld x 4 bytes
+  // below 2^31 (checked in launch_gemm_t; the step kernels' spans are a few MB).
   template <class Map>
   __device__ __forceinline__ void load(const float* __restrict__ base, long ld, const Map& map, int k0, int K,
                                        int tid) {
+    const int m0 = map(0);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base + (long)m0 * ld), 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int q = tid + NT * i;
       const int r = q / C4, c = (q % C4) * 4;
-      f32x4 x = {0.f, 0.f, 0.f, 0.f};
-      if (map.valid(r) && k0 + c < K) x = *reinterpret_cast<const f32x4*>(base + (long)map(r) * ld + k0 + c);
-      v[i] = x;
+      const bool ok = map.valid(r) && k0 + c < K;
+      const int off = ok ? (int)(((long)(map(r) - m0) * ld + k0 + c) * 4) : 0x7FFFFFF0;
+      v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
     }
   }
   __device__ __forceinline__ void store(float* lds, int tid) const {
@@ -270,7 +297,37 @@ __device__ __forceinline__ void mfma_ktile_km_x6(const float* As, const float* B
       }
   }
 }
-// dispatch between the exact fp32 MFMA k-tile and the bf16x6 one
+// The same k-major tiles on v_mfma_f32_16x16x4_f32 (exact f32, 32-cycle issue; per the
+// microarch guide the 16x16 shapes hold a higher clock than the 32x32 ones under sustained
+// load).  Operand map: lane (r = l&15, q = l>>4) reads 4 consecutive k at 16g + 4q with one
+// ds_read_b128 and feeds MFMAs c = 0..3 with k_phys = 16g + 4q + c (a fixed permutation of the
+// reduction order, identical for A and B).  Here TM/TN count 16-row blocks; accumulator reg r
+// of lane l holds C[row 4(l>>4) + r][col l&15].
+__device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+template <int TM, int TN, int BK, int LD>
+__device__ __forceinline__ void mfma_ktile_km16(const float* As, const float* Bs, int wm0, int wn0, int lane,
+                                                f32x4 (&acc)[TM][TN]) {
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int g = 0; g < BK / 16; ++g) {
+    f32x4 a[TM], b[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const f32x4*>(As + (wm0 + 16 * i + r) * LD + 16 * g + 4 * q);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const f32x4*>(Bs + (wn0 + 16 * j + r) * LD + 16 * g + 4 * q);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x4(a[i][c], b[j][c], acc[i][j]);
+  }
+}
+
+// dispatch between the exact fp32 MFMA k-tile and the bf16x6 one; the 16x16 accumulator type
+// selects the 16x16x4 k-tile
 template <bool X6, int TM, int TN, int BK, int LD>
 __device__ __forceinline__ void mfma_ktile_f32(const float* As, const float* Bs, int wm0, int wn0, int lane,
                                                f32x16 (&acc)[TM][TN]) {
@@ -279,13 +336,19 @@ __device__ __forceinline__ void mfma_ktile_f32(const float* As, const float* Bs,
   else
     mfma_ktile_km<TM, TN, BK, LD>(As, Bs, wm0, wn0, lane, acc);
 }
+template <bool X6, int TM, int TN, int BK, int LD>
+__device__ __forceinline__ void mfma_ktile_f32(const float* As, const float* Bs, int wm0, int wn0, int lane,
+                                               f32x4 (&acc)[TM][TN]) {
+  static_assert(!X6, "bf16x6 runs on the 32x32 tiles");
+  mfma_ktile_km16<TM, TN, BK, LD>(As, Bs, wm0, wn0, lane, acc);
+}
 
 // lds must hold 2 * (BM + BN) * (BK + 4) floats
-template <int BM, int BN, int NT, int BK, int TM, int TN, class MapA, class MapB, bool X6 = false>
+template <int BM, int BN, int NT, int BK, int TM, int TN, class MapA, class MapB, bool X6 = false, class AccT>
 __device__ __forceinline__ void gemm_mainloop_km(const float* __restrict__ A, long lda, const MapA& mapA,
                                                  const float* __restrict__ B, long ldb, const MapB& mapB, int kbeg,
                                                  int kend, float* lds, int tid, int wm0, int wn0,
-                                                 f32x16 (&acc)[TM][TN]) {
+                                                 AccT (&acc)[TM][TN]) {
   using SA = KTileStage<BM, NT, BK>;
   using SB = KTileStage<BN, NT, BK>;
   constexpr int LD = BK + 4;
@@ -322,11 +385,11 @@ __device__ __forceinline__ void gemm_mainloop_km(const float* __restrict__ A, lo
 // flight while one is multiplied.  For the per-step kernels, whose every launch starts from a
 // cold L2 and pulls its operands from the Infinity Cache.  lds as gemm_mainloop_km.
 template <int BM, int BN, int NT, int BK, int D, int TM, int TN, class MapA, class MapB, bool DIAG = false,
-          bool X6 = false>
+          bool X6 = false, class AccT>
 __device__ __forceinline__ void gemm_mainloop_km_pipe(const float* __restrict__ A, long lda, const MapA& mapA,
                                                       const float* __restrict__ B, long ldb, const MapB& mapB,
                                                       int kbeg, int kend, float* lds, int tid, int wm0, int wn0,
-                                                      f32x16 (&acc)[TM][TN], int rot = 0) {
+                                                      AccT (&acc)[TM][TN], int rot = 0) {
   using SA = KTileStage<BM, NT, BK>;
   using SB = KTileStage<BN, NT, BK>;
   constexpr int LD = BK + 4;
@@ -367,14 +430,111 @@ __device__ __forceinline__ void gemm_mainloop_km_pipe(const float* __restrict__ 
   __syncthreads();
 }
 
-// D == 1: the plain double-buffered loop; D > 1: the rolling pipeline
+// Software-pipelined variant with one barrier per k-tile and a prefetched local read
+// (32x32x2 exact fp32 only).  Tile kt+1 waits in a register stage and is written to the
+// other LDS buffer during tile kt, after the first k-group's MFMAs are issued; with S stages
+// its global loads were issued S tiles earlier.  The MFMA fragments of k-group g+1 are read
+// while group g multiplies, and the barrier sits before the last k-group's MFMAs, which then
+// cover the LDS latency of the next tile's first fragments.  Safety: the barrier in tile kt
+// orders (a) every read of tile kt (issued before it, completed by the waitcnt a barrier
+// implies) before the writes of tile kt+2 into the same buffer, and (b) the writes of tile
+// kt+1 before its reads.  Template D = SV_PLR + S.
+constexpr int SV_PLR = 100;
+template <int BM, int BN, int NT, int BK, int S, int TM, int TN, class MapA, class MapB>
+__device__ __forceinline__ void gemm_mainloop_km_plr(const float* __restrict__ A, long lda, const MapA& mapA,
+                                                     const float* __restrict__ B, long ldb, const MapB& mapB,
+                                                     int kbeg, int kend, float* lds, int tid, int wm0, int wn0,
+                                                     f32x16 (&acc)[TM][TN]) {
+  using SA = KTileStage<BM, NT, BK>;
+  using SB = KTileStage<BN, NT, BK>;
+  constexpr int LD = BK + 4;
+  constexpr int BUF = (BM + BN) * LD;
+  constexpr int G = BK / 8;
+  static_assert(G % 2 == 0 && S >= 1, "k-groups are consumed in pairs");
+  const int lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk <= 0) return;
+  SA sa[S];
+  SB sb[S];
+  // tile 0 straight to LDS buffer 0; tile k >= 1 lives in stage (k - 1) % S
+  sa[0].load(A, lda, mapA, kbeg, kend, tid);
+  sb[0].load(B, ldb, mapB, kbeg, kend, tid);
+  sa[0].store(lds, tid);
+  sb[0].store(lds + BM * LD, tid);
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    sa[j].load(A, lda, mapA, kbeg + (j + 1) * BK, kend, tid);
+    sb[j].load(B, ldb, mapB, kbeg + (j + 1) * BK, kend, tid);
+  }
+  __syncthreads();
+  auto rd = [&](const float* buf, int g, f32x4 (&a)[TM], f32x4 (&b)[TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const f32x4*>(buf + (wm0 + 32 * i + r) * LD + 8 * g + 4 * h);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      b[j] = *reinterpret_cast<const f32x4*>(buf + BM * LD + (wn0 + 32 * j + r) * LD + 8 * g + 4 * h);
+  };
+  auto mm = [&](const f32x4 (&a)[TM], const f32x4 (&b)[TN]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x2(a[i][c], b[j][c], acc[i][j]);
+  };
+  f32x4 a0[TM], b0[TN], a1[TM], b1[TN];
+  rd(lds, 0, a0, b0);
+  for (int k0 = 0; k0 < nk; k0 += S) {
+#pragma unroll
+    for (int js = 0; js < S; ++js) {
+      const int kt = k0 + js;
+      if (kt < nk) {
+        const float* cur = lds + (kt & 1) * BUF;
+        float* nxt = lds + ((kt + 1) & 1) * BUF;
+#pragma unroll
+        for (int g = 0; g < G; g += 2) {
+          // even group in (a0, b0), odd group in (a1, b1)
+          rd(cur, g + 1, a1, b1);
+          mm(a0, b0);
+          if (g == 0) {
+            // after the first group's MFMAs are issued, so the LDS counter the next fragment
+            // reads wait on does not include these writes.  Unconditional: past the last
+            // tile the stage re-stores data nobody reads and the loads are guarded off
+            // (k0 >= kend).
+            sa[js].store(nxt, tid);
+            sb[js].store(nxt + BM * LD, tid);
+            sa[js].load(A, lda, mapA, kbeg + (kt + 1 + S) * BK, kend, tid);
+            sb[js].load(B, ldb, mapB, kbeg + (kt + 1 + S) * BK, kend, tid);
+          }
+          if (g + 2 < G) {
+            rd(cur, g + 2, a0, b0);
+          } else {
+            __builtin_amdgcn_sched_barrier(0);
+            __syncthreads();
+            __builtin_amdgcn_sched_barrier(0);
+            rd(nxt, 0, a0, b0);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          mm(a1, b1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// D == 1: the plain double-buffered loop; D > 1: the rolling pipeline; D == SV_PLR + S: the
+// pipelined-local-read loop above with S register stages
 template <int BM, int BN, int NT, int BK, int D, int TM, int TN, bool DIAG = false, bool X6 = false, class MapA,
-          class MapB>
+          class MapB, class AccT>
 __device__ __forceinline__ void gemm_mainloop_km_d(const float* __restrict__ A, long lda, const MapA& mapA,
                                                    const float* __restrict__ B, long ldb, const MapB& mapB, int kbeg,
                                                    int kend, float* lds, int tid, int wm0, int wn0,
-                                                   f32x16 (&acc)[TM][TN], int rot = 0) {
-  if constexpr (D > 1)
+                                                   AccT (&acc)[TM][TN], int rot = 0) {
+  if constexpr (D >= SV_PLR)
+    gemm_mainloop_km_plr<BM, BN, NT, BK, (D > SV_PLR ? D - SV_PLR : 1), TM, TN, MapA, MapB>(
+        A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0, acc);
+  else if constexpr (D > 1)
     gemm_mainloop_km_pipe<BM, BN, NT, BK, D, TM, TN, MapA, MapB, DIAG, X6>(A, lda, mapA, B, ldb, mapB, kbeg, kend,
                                                                            lds, tid, wm0, wn0, acc, rot);
   else

@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <algorithm>
 #include <atomic>
+#include <type_traits>
 #include "sv_common.h"
 #include "sv_gemm.h"
 #include "../../include/sv_ge2e.h"
@@ -121,14 +122,18 @@ __global__ void to_time_major_kernel(const float* __restrict__ x, float* __restr
   }
 }
 
-// k-major ("NT") GEMM: both operands k-contiguous; the fast path for every large GEMM
-template <int BM, int BN, int EPI, int D = 1, bool X6 = false, bool X3 = false>
+// k-major ("NT") GEMM: both operands k-contiguous; the fast path for every large GEMM.
+// M16 selects the v_mfma_f32_16x16x4_f32 k-tile (each wave's 64x64 as 4x4 blocks of 16x16).
+template <int BM, int BN, int EPI, int D = 1, bool X6 = false, bool X3 = false, bool M16 = false, bool DIAG = false>
 __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ A, long lda, const float* __restrict__ B,
                                                       long ldb, float* __restrict__ C, long ldc, long slab, int M,
                                                       int N, int K, int kchunk, const float* __restrict__ bias0,
                                                       const float* __restrict__ bias1, float beta) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int BLK = M16 ? 16 : 32;                     // MFMA output block edge
+  constexpr int TM = BM / 2 / BLK, TN = BN / 2 / BLK;    // blocks per wave (2x2 waves)
+  using AccT = typename std::conditional<M16, f32x4, f32x16>::type;
+  constexpr int NR = M16 ? 4 : 16;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // column tile fastest: the blocks an XCD runs together share one A row-panel (the large
   // operand, read from HBM once) and sweep the small B operand, which stays cache-resident
@@ -139,13 +144,13 @@ __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ 
   const int kbeg = blockIdx.y * kchunk;
   const int kend = min(K, kbeg + kchunk);
   const int wm0 = (w >> 1) * (BM / 2), wn0 = (w & 1) * (BN / 2);
-  f32x16 acc[TM][TN];
+  AccT acc[TM][TN];
   zero_acc(acc);
   if constexpr (X3)
     gemm_mainloop_x3<BM, BN, 256, 16, 2, TM, TN>(A, lda, RowMapLinear{tm * BM, M}, B, ldb, RowMapLinear{tn * BN, N},
                                                  kbeg, kend, lds, tid, wm0, wn0, acc);
   else
-    gemm_mainloop_km_d<BM, BN, 256, SV_BKM, D, TM, TN, false, X6>(A, lda, RowMapLinear{tm * BM, M}, B, ldb,
+    gemm_mainloop_km_d<BM, BN, 256, SV_BKM, D, TM, TN, DIAG, X6>(A, lda, RowMapLinear{tm * BM, M}, B, ldb,
                                                                 RowMapLinear{tn * BN, N}, kbeg, kend, lds, tid, wm0,
                                                                 wn0, acc);
   float* Cz = C + (EPI == EPI_SLAB ? (long)blockIdx.y * slab : 0);
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ 
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int col = tn * BN + wn0 + 32 * j + (lane & 31);
+      const int col = tn * BN + wn0 + BLK * j + (lane & (BLK - 1));
       if (col >= N) continue;
       float badd = 0.f;
       if (EPI == EPI_STORE) {
@@ -161,8 +166,8 @@ __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ 
         if (bias1) badd += bias1[col];
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = tm * BM + wm0 + 32 * i + acc_row(r, lane);
+      for (int r = 0; r < NR; ++r) {
+        const int row = tm * BM + wm0 + BLK * i + (M16 ? 4 * (lane >> 4) + r : acc_row(r, lane));
         if (row >= M) continue;
         float v = acc[i][j][r];
         float* dst = Cz + (long)row * ldc + col;
@@ -380,7 +385,9 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
   constexpr int BN = 4 * FWD_U, LDP = BN + 4, LDH = FWD_BM + 1;
   constexpr int PER = FWD_BM * FWD_U / 512;  // epilogue elements per thread
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int j0 = blockIdx.x * FWD_U, b0 = blockIdx.y * FWD_BM;
+  int bx, by;
+  xcd_tile_map(krot >> 1, bx, by);
+  const int j0 = bx * FWD_U, b0 = by * FWD_BM;
   const int wm0 = (w >> 2) * 32, wn0 = (w & 3) * 32;
   const long G = 4L * H;
   // the epilogue's inputs do not depend on the GEMM: issue their loads first
@@ -404,7 +411,7 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
     else
       gemm_mainloop_km_d<FWD_BM, BN, 512, BKX, D, 1, 1, DIAG, X6>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0},
                                                                  whh, H, RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid,
-                                                                 wm0, wn0, acc, krot * (blockIdx.x + blockIdx.y));
+                                                                 wm0, wn0, acc, (krot & 1) * (bx + by));
   }
   float* pre = lds;
   float* hs = lds + FWD_BM * LDP;
@@ -532,7 +539,9 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
   constexpr int PER = BWD_BM * BWD_U / 512;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int gate = w >> 1, gt = tid & 127;
-  const int j0 = blockIdx.x * BWD_U, b0 = blockIdx.y * BWD_BM;
+  int bx, by;
+  xcd_tile_map(krot >> 1, bx, by);
+  const int j0 = bx * BWD_U, b0 = by * BWD_BM;
   const long G = 4L * H;
   // prefetch the epilogue's element-wise inputs (independent of the GEMM)
   float av[PER][4], cv[PER], cpv[PER], dcfv[PER], upv[PER];
@@ -561,7 +570,7 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
     else
       gemm_mainloop_km_d<BWD_BM, BWD_U, 128, BKX, D, 1, 1, DIAG, X6>(
           dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G, RowMapLinear{j0, H}, gate * H, (gate + 1) * H,
-          lds + gate * GBUF, gt, (w & 1) * 32, 0, acc, krot * (blockIdx.x + blockIdx.y));
+          lds + gate * GBUF, gt, (w & 1) * 32, 0, acc, (krot & 1) * (bx + by));
   }
   __syncthreads();
   float* red = lds;                    // [4][64][LDR]
@@ -641,7 +650,16 @@ int k3_x() {
 int gemm_pipe() {
   static int v = [] {
     const char* e = getenv("SV_GEMM_PIPE");
-    return (e && *e == '2') ? 2 : 1;
+    return (e && *e >= '2' && *e <= '4') ? *e - '0' : 1;
+  }();
+  return v;
+}
+
+// exact-fp32 NT GEMM on the 16x16x4 MFMA (SV_GEMM_M16=1) instead of 32x32x2
+int gemm_m16() {
+  static int v = [] {
+    const char* e = getenv("SV_GEMM_M16");
+    return (e && *e == '1') ? 1 : 0;
   }();
   return v;
 }
@@ -651,6 +669,8 @@ int launch_gemm_t(const float* A, long lda, const float* B, long ldb, float* C, 
                   int K, int splitk, int kchunk, const float* b0, const float* b1, float beta, hipStream_t s) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (AK && BKC) {
+    // KTileStage's buffer loads address a tile's rows with 32-bit byte offsets
+    if ((long)BM * lda * 4 >= (1L << 31) || (long)BN * ldb * 4 >= (1L << 31)) return SV_ESHAPE;
     constexpr int LDS_KM = 2 * (BM + BN) * (SV_BKM + 4);
     if (gemm_x() == 2)
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 1, false, true>), dim3(tiles, splitk), dim3(256),
@@ -658,6 +678,15 @@ int launch_gemm_t(const float* A, long lda, const float* B, long ldb, float* C, 
     else if (gemm_x() == 1)
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 1, true>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float),
                          s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+    else if (gemm_m16())
+      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 1, false, false, true>), dim3(tiles, splitk), dim3(256),
+                         LDS_KM * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+    else if (gemm_pipe() == 3)
+      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, SV_PLR>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float),
+                         s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+    else if (gemm_pipe() == 4)  // profiling only (results invalid): LDS + MFMA without global loads
+      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 2, false, false, false, true>), dim3(tiles, splitk), dim3(256),
+                         LDS_KM * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
     else if (gemm_pipe() == 2)
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 2>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float), s,
                          A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
@@ -849,16 +878,23 @@ int step_variant() {
   }();
   return v;
 }
-// prefetch depth of the K2v2 / K3v2 main loops (1 = double buffer, 2 = default rolling
-// pipeline; SV_KM_PIPE = 1..4).  Measured at c2: K2 39.6 -> 36.4 us, K3 47.6 -> 43.1 us,
-// step 73.7 -> 70.4 ms with depth 2 (3: 71.3; 4: same kernels as 2)
+// main loop of the K2v2 / K3v2 step kernels (SV_KM_PIPE): 1 = double buffer, 2..4 = rolling
+// register prefetch of that depth, 5 / 6 = pipelined local read with 1 / 2 register stages
+// (gemm_mainloop_km_plr; one barrier per k-tile, LDS writes issued behind the first k-group's
+// MFMAs).  Measured at c2 with the branch-free buffer loads: K2 41.7 / 35.6 us, K3 41.5 / 40.8
+// us, step 69.3-69.6 / 67.2 ms for 2 / 5 (before the buffer loads depth 2 was the best: K2 39.6
+// -> 36.4, K3 47.6 -> 43.1 us against the double buffer).
 // k-tile rotation of the K2v2 / K3v2 main loops (SV_KROT, default 0): rot = krot * (bx + by).
 // Measured slower (K3 41.7 -> 44.4 us at krot 1): workgroups sharing an operand panel gain from
 // reading the same lines at the same time (L2 hits), so the natural order stays.
+// schedule flags of the fp32 step kernels (their `krot` argument): bit 0 rotates the k-tile
+// order per workgroup (SV_KROT=1), bit 1 maps blocks to XCD-compact tile rectangles
+// (xcd_tile_map; SV_XCD_STEP=1)
 int k_rot() {
   static int v = [] {
     const char* e = getenv("SV_KROT");
-    return e ? atoi(e) : 0;
+    const char* x = getenv("SV_XCD_STEP");
+    return ((e && *e == '1') ? 1 : 0) | ((x && *x == '1') ? 2 : 0);
   }();
   return v;
 }
@@ -874,8 +910,8 @@ int step_diag() {
 int km_pipe() {
   static int v = [] {
     const char* e = getenv("SV_KM_PIPE");
-    const int x = e ? atoi(e) : 2;
-    return (x >= 1 && x <= 4) ? x : 2;
+    const int x = e ? atoi(e) : 5;
+    return (x >= 1 && x <= 6) ? x : 5;
   }();
   return v;
 }
@@ -896,10 +932,10 @@ void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh
   else if (step_variant() == 2 && k2_x() == 2)
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, false, false, true>), grid, dim3(512), FWD_X3_LDS, s, hp,
                        whh, g, cp, c, h, hT, ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2 && km_pipe() == 2 && k2_x() == 1)
+  else if (step_variant() == 2 && k2_x() == 1)
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, false, true>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp,
                        c, h, hT, ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2 && km_pipe() == 2 && step_diag())
+  else if (step_variant() == 2 && step_diag())
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, true>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
                        hT, ldhT, t, Bp, B, H, k_rot());
   else if (step_variant() == 2 && km_pipe() == 2)
@@ -911,6 +947,12 @@ void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh
   else if (step_variant() == 2 && km_pipe() == 4)
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 4>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT,
                        ldhT, t, Bp, B, H, k_rot());
+  else if (step_variant() == 2 && km_pipe() == 5)
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, SV_PLR + 1>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
+                       hT, ldhT, t, Bp, B, H, k_rot());
+  else if (step_variant() == 2 && km_pipe() == 6)
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, SV_PLR + 2>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
+                       hT, ldhT, t, Bp, B, H, k_rot());
   else if (step_variant() == 2)
     hipLaunchKernelGGL(lstm_step_fwd_v2_kernel<SV_BKM>, grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT, ldhT, t,
                        Bp, B, H);
@@ -929,10 +971,10 @@ void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* wh
   else if (step_variant() >= 2 && k3_x() == 2)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, false, false, true>), grid, dim3(512), BWD_X3_LDS, s, dgn,
                        whhT, up, dcfi, acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && km_pipe() == 2 && k3_x() == 1)
+  else if (step_variant() >= 2 && k3_x() == 1)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, false, true>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up,
                        dcfi, acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && km_pipe() == 2 && step_diag())
+  else if (step_variant() >= 2 && step_diag())
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, true>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
                        acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
   else if (step_variant() >= 2 && km_pipe() == 2)
@@ -944,6 +986,12 @@ void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* wh
   else if (step_variant() >= 2 && km_pipe() == 4)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 4>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
                        cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
+  else if (step_variant() >= 2 && km_pipe() == 5)
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 1>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
+                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
+  else if (step_variant() >= 2 && km_pipe() == 6)
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 2>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
+                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
   else if (step_variant() >= 2)
     hipLaunchKernelGGL(lstm_step_bwd_v2_kernel<SV_BKM>, grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
                        dg, dcfo, dgT, lddgT, t, Bp, B, H);

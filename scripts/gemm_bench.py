@@ -1,0 +1,68 @@
+"""fp32 / bf16 GEMM timing at the c2 shapes (ours via the C ABI, and torch.matmul =
+hipBLASLt for comparison).  HIP events on the launch stream; prints one JSON line.
+Usage: python scripts/gemm_bench.py [--torch] [--reps N]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_speaker_verification_amd._lib import call, lib, ptr  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--torch", action="store_true")
+ap.add_argument("--bf16", action="store_true")
+ap.add_argument("--reps", type=int, default=8)
+args = ap.parse_args()
+dev = torch.device("cuda", 0)
+s = torch.cuda.current_stream(dev).cuda_stream
+B, T, H = 640, 160, 768
+G = 4 * H
+SHAPES = {"Gx": (T * B, G, H), "dW": (G, H, T * B), "dx": (T * B, H, G)}
+
+
+def timeit(fn, reps, warm=2):
+    for _ in range(warm):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+res = {"env": {k: v for k, v in os.environ.items() if k.startswith("SV_")}}
+for name, (M, N, K) in SHAPES.items():
+    A = torch.randn(M, K, device=dev)
+    Bm = torch.randn(N, K, device=dev)
+    C = torch.empty(M, N, device=dev)
+    w = torch.empty(lib().sv_gemm_f32_workspace(M, N, K) // 4 + 1, device=dev)
+    f = lambda: call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, ptr(w), s)  # noqa: E731
+    us = timeit(f, args.reps)
+    res["sv_f32_" + name] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
+    if args.torch:
+        ref = torch.matmul(A.double(), Bm.double().t()) if name == "Gx" else None
+        us = timeit(lambda: torch.matmul(A, Bm.t()), args.reps)
+        res["torch_f32_" + name] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
+        if ref is not None:
+            f()
+            torch.cuda.synchronize()
+            sc = (A.abs().double() @ Bm.abs().double().t())
+            res["sv_f32_Gx_err"] = float(((C.double() - ref).abs() / sc).max())
+            res["torch_f32_Gx_err"] = float(((torch.matmul(A, Bm.t()).double() - ref).abs() / sc).max())
+            del ref, sc
+    if args.bf16:
+        Ab, Bb = A.bfloat16(), Bm.bfloat16()
+        wb = torch.empty(lib().sv_gemm_bf16_workspace(M, N, K) // 4 + 1, device=dev)
+        us = timeit(lambda: call("sv_gemm_bf16", M, N, K, ptr(Ab), K, ptr(Bb), K, ptr(C), N, None, None, 0.0, ptr(wb), s),
+                    args.reps)
+        res["sv_bf16_" + name] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
+        if args.torch:
+            us = timeit(lambda: torch.matmul(Ab, Bb.t()), args.reps)
+            res["torch_bf16_" + name] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
+    del A, Bm, C, w
+print(json.dumps(res), flush=True)
