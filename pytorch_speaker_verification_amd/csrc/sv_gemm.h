@@ -440,7 +440,7 @@ __device__ __forceinline__ void gemm_mainloop_km_pipe(const float* __restrict__ 
 // implies) before the writes of tile kt+2 into the same buffer, and (b) the writes of tile
 // kt+1 before its reads.  Template D = SV_PLR + S.
 constexpr int SV_PLR = 100;
-template <int BM, int BN, int NT, int BK, int S, int TM, int TN, class MapA, class MapB>
+template <int BM, int BN, int NT, int BK, int S, int TM, int TN, class MapA, class MapB, bool NOLOAD = false>
 __device__ __forceinline__ void gemm_mainloop_km_plr(const float* __restrict__ A, long lda, const MapA& mapA,
                                                      const float* __restrict__ B, long ldb, const MapB& mapB,
                                                      int kbeg, int kend, float* lds, int tid, int wm0, int wn0,
@@ -503,8 +503,10 @@ __device__ __forceinline__ void gemm_mainloop_km_plr(const float* __restrict__ A
             // (k0 >= kend).
             sa[js].store(nxt, tid);
             sb[js].store(nxt + BM * LD, tid);
-            sa[js].load(A, lda, mapA, kbeg + (kt + 1 + S) * BK, kend, tid);
-            sb[js].load(B, ldb, mapB, kbeg + (kt + 1 + S) * BK, kend, tid);
+            if constexpr (!NOLOAD) {  // NOLOAD (profiling only): LDS traffic without global loads
+              sa[js].load(A, lda, mapA, kbeg + (kt + 1 + S) * BK, kend, tid);
+              sb[js].load(B, ldb, mapB, kbeg + (kt + 1 + S) * BK, kend, tid);
+            }
           }
           if (g + 2 < G) {
             rd(cur, g + 2, a0, b0);
@@ -532,7 +534,7 @@ __device__ __forceinline__ void gemm_mainloop_km_d(const float* __restrict__ A, 
                                                    int kend, float* lds, int tid, int wm0, int wn0,
                                                    AccT (&acc)[TM][TN], int rot = 0) {
   if constexpr (D >= SV_PLR)
-    gemm_mainloop_km_plr<BM, BN, NT, BK, (D > SV_PLR ? D - SV_PLR : 1), TM, TN, MapA, MapB>(
+    gemm_mainloop_km_plr<BM, BN, NT, BK, (D > SV_PLR ? D - SV_PLR : 1), TM, TN, MapA, MapB, DIAG>(
         A, lda, mapA, B, ldb, mapB, kbeg, kend, lds, tid, wm0, wn0, acc);
   else if constexpr (D > 1)
     gemm_mainloop_km_pipe<BM, BN, NT, BK, D, TM, TN, MapA, MapB, DIAG, X6>(A, lda, mapA, B, ldb, mapB, kbeg, kend,

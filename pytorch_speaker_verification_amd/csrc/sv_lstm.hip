@@ -128,7 +128,7 @@ template <int BM, int BN, int EPI, int D = 1, bool X6 = false, bool X3 = false, 
 __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ A, long lda, const float* __restrict__ B,
                                                       long ldb, float* __restrict__ C, long ldc, long slab, int M,
                                                       int N, int K, int kchunk, const float* __restrict__ bias0,
-                                                      const float* __restrict__ bias1, float beta) {
+                                                      const float* __restrict__ bias1, float beta, int gm) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int BLK = M16 ? 16 : 32;                     // MFMA output block edge
   constexpr int TM = BM / 2 / BLK, TN = BN / 2 / BLK;    // blocks per wave (2x2 waves)
@@ -137,10 +137,18 @@ __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // column tile fastest: the blocks an XCD runs together share one A row-panel (the large
   // operand, read from HBM once) and sweep the small B operand, which stays cache-resident
-  const int tiles_n = (N + BN - 1) / BN;
-  const int nwg = tiles_n * ((M + BM - 1) / BM);
+  // gm > 1: grouped order -- an XCD's consecutive tiles sweep gm row panels per column tile, so
+  // the column panels it streams are reused gm times from its L2 instead of once
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_n * tiles_m;
   const int id = xcd_remap(blockIdx.x, nwg);
-  const int tn = id % tiles_n, tm = id / tiles_n;
+  int tn = id % tiles_n, tm = id / tiles_n;
+  if (gm > 1) {
+    const int gsz = gm * tiles_n, first = (id / gsz) * gm;
+    const int g = min(tiles_m - first, gm), r = id % gsz;
+    tm = first + r % g;
+    tn = r / g;
+  }
   const int kbeg = blockIdx.y * kchunk;
   const int kend = min(K, kbeg + kchunk);
   const int wm0 = (w >> 1) * (BM / 2), wn0 = (w & 1) * (BN / 2);
@@ -664,6 +672,16 @@ int gemm_m16() {
   return v;
 }
 
+// grouped tile order of the NT GEMM (SV_GEMM_GM row panels per group; 1 = row-panel order)
+int gemm_gm() {
+  static int v = [] {
+    const char* e = getenv("SV_GEMM_GM");
+    const int x = e ? atoi(e) : 1;
+    return (x >= 1 && x <= 64) ? x : 1;
+  }();
+  return v;
+}
+
 template <int BM, int BN, bool AK, bool BKC, int EPI>
 int launch_gemm_t(const float* A, long lda, const float* B, long ldb, float* C, long ldc, long slab, int M, int N,
                   int K, int splitk, int kchunk, const float* b0, const float* b1, float beta, hipStream_t s) {
@@ -674,25 +692,25 @@ int launch_gemm_t(const float* A, long lda, const float* B, long ldb, float* C, 
     constexpr int LDS_KM = 2 * (BM + BN) * (SV_BKM + 4);
     if (gemm_x() == 2)
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 1, false, true>), dim3(tiles, splitk), dim3(256),
-                         12 * (BM + BN) * (16 + 8), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+                         12 * (BM + BN) * (16 + 8), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
     else if (gemm_x() == 1)
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 1, true>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float),
-                         s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+                         s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
     else if (gemm_m16())
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 1, false, false, true>), dim3(tiles, splitk), dim3(256),
-                         LDS_KM * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+                         LDS_KM * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
     else if (gemm_pipe() == 3)
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, SV_PLR>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float),
-                         s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+                         s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
     else if (gemm_pipe() == 4)  // profiling only (results invalid): LDS + MFMA without global loads
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 2, false, false, false, true>), dim3(tiles, splitk), dim3(256),
-                         LDS_KM * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+                         LDS_KM * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
     else if (gemm_pipe() == 2)
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 2>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float), s,
-                         A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+                         A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
     else
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float), s, A,
-                         lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
+                         lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
   } else {
     constexpr int LDS_FLOATS = 2 * SV_BK * (TileLd<AK, BM>::value + TileLd<BKC, BN>::value);
     hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, AK, BKC, EPI>), dim3(tiles, splitk), dim3(256),
@@ -878,12 +896,15 @@ int step_variant() {
   }();
   return v;
 }
-// main loop of the K2v2 / K3v2 step kernels (SV_KM_PIPE): 1 = double buffer, 2..4 = rolling
-// register prefetch of that depth, 5 / 6 = pipelined local read with 1 / 2 register stages
-// (gemm_mainloop_km_plr; one barrier per k-tile, LDS writes issued behind the first k-group's
-// MFMAs).  Measured at c2 with the branch-free buffer loads: K2 41.7 / 35.6 us, K3 41.5 / 40.8
-// us, step 69.3-69.6 / 67.2 ms for 2 / 5 (before the buffer loads depth 2 was the best: K2 39.6
-// -> 36.4, K3 47.6 -> 43.1 us against the double buffer).
+// main loop of the K2v2 / K3v2 step kernels (SV_KM_PIPE for K2, SV_K3_PIPE for K3): 1 = double
+// buffer, 2..4 = rolling register prefetch of that depth, 5..8 = pipelined local read with 1..4
+// register stages (gemm_mainloop_km_plr; one barrier per k-tile, LDS writes issued behind the
+// first k-group's MFMAs).  Measured at c2 with the branch-free buffer loads (us, two runs):
+//   K2: depth 2 41.7 | PLR 1 / 2 / 3 / 4 stages 35.1-35.6 / 37.1-37.6 / 38.6 / 37.7
+//   K3: depth 2 41.5 | PLR 1 / 2 / 3 / 4 stages 40.1-40.8 / 37.2-38.0 / 41.3 / 38.3
+// (odd stage counts > 1 lose the compile-time LDS buffer parity).  Defaults K2 5, K3 6: c2 step
+// 69.3 -> 66.4-67.0 ms.  Before the buffer loads depth 2 was the best (K2 39.6 -> 36.4, K3 47.6
+// -> 43.1 us against the double buffer).
 // k-tile rotation of the K2v2 / K3v2 main loops (SV_KROT, default 0): rot = krot * (bx + by).
 // Measured slower (K3 41.7 -> 44.4 us at krot 1): workgroups sharing an operand panel gain from
 // reading the same lines at the same time (L2 hits), so the natural order stays.
@@ -899,19 +920,29 @@ int k_rot() {
   return v;
 }
 // profiling only (results invalid): SV_STEP_DIAG=1 runs K2/K3 with every k-tile re-using tile 0
-// from LDS (no further global loads) to separate memory from compute time
+// from LDS (no further global loads) to separate memory from compute time; =2: the default
+// pipelined-local-read loop with its LDS stores but no global loads past the prologue
 int step_diag() {
   static int v = [] {
     const char* e = getenv("SV_STEP_DIAG");
-    return (e && *e == '1') ? 1 : 0;
+    return (e && (*e == '1' || *e == '2')) ? *e - '0' : 0;
   }();
   return v;
 }
-int km_pipe() {
+int km_pipe() {  // K2
   static int v = [] {
     const char* e = getenv("SV_KM_PIPE");
     const int x = e ? atoi(e) : 5;
-    return (x >= 1 && x <= 6) ? x : 5;
+    return (x >= 1 && x <= 8) ? x : 5;
+  }();
+  return v;
+}
+int k3_pipe() {  // K3: SV_K3_PIPE, else SV_KM_PIPE, else 6
+  static int v = [] {
+    const char* e = getenv("SV_K3_PIPE");
+    if (!e) e = getenv("SV_KM_PIPE");
+    const int x = e ? atoi(e) : 6;
+    return (x >= 1 && x <= 8) ? x : 6;
   }();
   return v;
 }
@@ -935,6 +966,9 @@ void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh
   else if (step_variant() == 2 && k2_x() == 1)
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, false, true>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp,
                        c, h, hT, ldhT, t, Bp, B, H, k_rot());
+  else if (step_variant() == 2 && step_diag() == 2)
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, SV_PLR + 2, true>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp,
+                       c, h, hT, ldhT, t, Bp, B, H, k_rot());
   else if (step_variant() == 2 && step_diag())
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, true>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
                        hT, ldhT, t, Bp, B, H, k_rot());
@@ -952,6 +986,12 @@ void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh
                        hT, ldhT, t, Bp, B, H, k_rot());
   else if (step_variant() == 2 && km_pipe() == 6)
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, SV_PLR + 2>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
+                       hT, ldhT, t, Bp, B, H, k_rot());
+  else if (step_variant() == 2 && km_pipe() == 7)
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, SV_PLR + 3>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
+                       hT, ldhT, t, Bp, B, H, k_rot());
+  else if (step_variant() == 2 && km_pipe() == 8)
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, SV_PLR + 4>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
                        hT, ldhT, t, Bp, B, H, k_rot());
   else if (step_variant() == 2)
     hipLaunchKernelGGL(lstm_step_fwd_v2_kernel<SV_BKM>, grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT, ldhT, t,
@@ -974,23 +1014,32 @@ void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* wh
   else if (step_variant() >= 2 && k3_x() == 1)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, false, true>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up,
                        dcfi, acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
+  else if (step_variant() >= 2 && step_diag() == 2)
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 2, true>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up,
+                       dcfi, acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
   else if (step_variant() >= 2 && step_diag())
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, true>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
                        acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && km_pipe() == 2)
+  else if (step_variant() >= 2 && k3_pipe() == 2)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
                        cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && km_pipe() == 3)
+  else if (step_variant() >= 2 && k3_pipe() == 3)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 3>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
                        cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && km_pipe() == 4)
+  else if (step_variant() >= 2 && k3_pipe() == 4)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 4>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
                        cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && km_pipe() == 5)
+  else if (step_variant() >= 2 && k3_pipe() == 5)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 1>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
                        acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && km_pipe() == 6)
+  else if (step_variant() >= 2 && k3_pipe() == 6)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 2>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
+                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
+  else if (step_variant() >= 2 && k3_pipe() == 7)
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 3>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
+                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
+  else if (step_variant() >= 2 && k3_pipe() == 8)
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 4>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
                        acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
   else if (step_variant() >= 2)
     hipLaunchKernelGGL(lstm_step_bwd_v2_kernel<SV_BKM>, grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
