@@ -406,12 +406,19 @@ BPlan plan_bf16(int M, int N, int K) {
   const long tiles = (long)((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
   const long slots = small ? 1024 : 512;
   int sk = 1;
-  if (tiles < slots) {
-    sk = (int)(slots / tiles);
-    const int kmax = K / 1024;
-    if (sk > kmax) sk = kmax;
-    if (sk > 32) sk = 32;
-    if (sk < 1) sk = 1;
+  if (tiles < slots) {  // the wave-quantised split-K model of plan_gemm (sv_lstm.hip), at ~600 TF/s
+    const double rate = 600e12 / (double)slots, hbm = 5e12;
+    const int kmax = std::max(1, std::min(32, K / 1024));
+    double best = 1e30;
+    for (int c = 1; c <= kmax; ++c) {
+      const long rounds = (tiles * c + slots - 1) / slots;
+      const double kc = (double)K / c;
+      const double t = rounds * (2.0 * p.bm * p.bn * kc / rate) + (c > 1 ? 2.0 * c * M * N * 4.0 / hbm + 5e-6 : 0.0);
+      if (t < best * 0.999) {
+        best = t;
+        sk = c;
+      }
+    }
   }
   p.kchunk = ((K + sk - 1) / sk + BBK - 1) / BBK * BBK;
   p.splitk = (K + p.kchunk - 1) / p.kchunk;

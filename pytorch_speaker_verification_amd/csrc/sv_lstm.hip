@@ -658,7 +658,7 @@ int k3_x() {
 int gemm_pipe() {
   static int v = [] {
     const char* e = getenv("SV_GEMM_PIPE");
-    return (e && *e >= '2' && *e <= '4') ? *e - '0' : 1;
+    return (e && *e >= '2' && *e <= '5') ? *e - '0' : 1;
   }();
   return v;
 }
@@ -702,6 +702,10 @@ int launch_gemm_t(const float* A, long lda, const float* B, long ldb, float* C, 
     else if (gemm_pipe() == 3)
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, SV_PLR>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float),
                          s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
+    else if (gemm_pipe() == 5)  // profiling only (results invalid): PLR loop with LDS stores, no global loads
+      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, SV_PLR + 1, false, false, false, true>), dim3(tiles, splitk),
+                         dim3(256), LDS_KM * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1,
+                         beta, gemm_gm());
     else if (gemm_pipe() == 4)  // profiling only (results invalid): LDS + MFMA without global loads
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 2, false, false, false, true>), dim3(tiles, splitk), dim3(256),
                          LDS_KM * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
@@ -734,9 +738,12 @@ struct GemmPlan {
   int bm, bn, splitk, kchunk;
 };
 
-// Tile 128x128 when there are enough tiles to fill the chip, else 64x64; split K only when
-// the tile count leaves resident slots (2 blocks/CU x 256 CUs) idle, and never below 512-deep
-// K chunks.  The split count is chosen so tiles*splitk fits the slots in whole rounds.
+// Tile 128x128 when there are enough tiles to fill the chip, else 64x64.  When the tiles leave
+// resident slots (2 blocks/CU x 256 CUs, 4 for 64x64) idle, split K: the split count minimises
+// a wave-quantised time model, rounds(tiles*sk / slots) x (time of one K/sk chunk) + the slab
+// traffic of the split (sk x M x N x 4 B written and read back), over sk <= 32 with K chunks of
+// at least 512.  At the dW shape (144 tiles, K = 102400) this picks 32 splits = 9 full rounds of
+// 512 blocks (the old 512/144 = 3 left 80 CUs with one block and the rest with two).
 GemmPlan plan_gemm(int M, int N, int K) {
   GemmPlan p;
   const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
@@ -747,11 +754,19 @@ GemmPlan plan_gemm(int M, int N, int K) {
   const long slots = small ? 1024 : 512;
   int sk = 1;
   if (tiles < slots) {
-    sk = (int)(slots / tiles);
-    const int kmax = K / 512;
-    if (sk > kmax) sk = kmax;
-    if (sk > 32) sk = 32;
-    if (sk < 1) sk = 1;
+    // per-block rate at ~120 TF/s shared by all resident blocks; HBM ~5 TB/s for the slabs
+    const double rate = 120e12 / (double)slots, hbm = 5e12;
+    const int kmax = std::max(1, std::min(32, K / 512));
+    double best = 1e30;
+    for (int c = 1; c <= kmax; ++c) {
+      const long rounds = (tiles * c + slots - 1) / slots;
+      const double kc = (double)K / c;
+      const double t = rounds * (2.0 * p.bm * p.bn * kc / rate) + (c > 1 ? 2.0 * c * M * N * 4.0 / hbm + 5e-6 : 0.0);
+      if (t < best * 0.999) {
+        best = t;
+        sk = c;
+      }
+    }
   }
   const int q = SV_BKM;
   p.kchunk = ((K + sk - 1) / sk + q - 1) / q * q;
