@@ -210,6 +210,22 @@ __device__ __forceinline__ bf16_t to_bf(float x) {
   return *reinterpret_cast<const bf16_t*>(&b);
 }
 
+// LSTM cell backward of one element, shared by the per-step and the persistent bf16 backward
+// kernels so both round identically (contraction off: every product and sum rounded as written)
+//   in: dh (recurrent + upstream), activated gates i f g o, c_t, c_{t-1}, dcf_in = dc_{t+1} f_{t+1}
+//   out: d[4] = gate pre-activation gradients (i f g o), return dc_t f_t
+__device__ __forceinline__ float lstm_cell_bwd(float dh, float i, float f, float g, float o, float c, float cp,
+                                               float dcf_in, float (&d)[4]) {
+#pragma clang fp contract(off)
+  const float tc = tanhf(c);
+  const float dc = dh * o * (1.f - tc * tc) + dcf_in;
+  d[0] = dc * g * i * (1.f - i);
+  d[1] = dc * cp * f * (1.f - f);
+  d[2] = dc * i * (1.f - g * g);
+  d[3] = dh * tc * o * (1.f - o);
+  return dc * f;
+}
+
 // recurrent-step tile: 64 batch rows x 32 hidden units (x 4 gates = 128 gate columns)
 #define BF_BM 64
 #define BF_U 32
@@ -218,3 +234,8 @@ __device__ __forceinline__ bf16_t to_bf(float x) {
 extern "C" int sv_persist_fwd_ok(int B, int H);
 int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates, float* c_tm, float* h_tm,
                         bf16_t* h_bf, bf16_t* hT, hipStream_t stream);
+// persistent backward recurrence of one layer (sv_persist.hip)
+extern "C" int sv_persist_bwd_ok(int B, int H);
+extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H);
+int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* acts, const float* c_tm,
+                        const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream);

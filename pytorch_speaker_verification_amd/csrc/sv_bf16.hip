@@ -362,17 +362,14 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_bf16_kernel(
     dh += red[(2 * BF_BM + b) * LDR + u];
     dh += red[(3 * BF_BM + b) * LDR + u];
     dh += upv[k];
-    const float i = av[k][0], f = av[k][1], g = av[k][2], o = av[k][3];
-    const float tc = tanhf(cv[k]);
-    const float dc = dh * o * (1.f - tc * tc) + dcfv[k];
-    const float d0 = dc * g * i * (1.f - i), d1 = dc * cpv[k] * f * (1.f - f);
-    const float d2 = dc * i * (1.f - g * g), d3 = dh * tc * o * (1.f - o);
+    float dd[4];
+    dcf[hi] = lstm_cell_bwd(dh, av[k][0], av[k][1], av[k][2], av[k][3], cv[k], cpv[k], dcfv[k], dd);
+    const float d0 = dd[0], d1 = dd[1], d2 = dd[2], d3 = dd[3];
     bf16_t* dp = dg + (long)gb * G + gj;
     dp[0] = to_bf(d0);
     dp[H] = to_bf(d1);
     dp[2 * H] = to_bf(d2);
     dp[3 * H] = to_bf(d3);
-    dcf[hi] = dc * f;
     gTs[(0 * BF_U + u) * LDT + b] = d0;
     gTs[(1 * BF_U + u) * LDT + b] = d1;
     gTs[(2 * BF_U + u) * LDT + b] = d2;
@@ -501,6 +498,26 @@ int persist_fwd(int H) {
     return e ? (*e == '1' ? 1 : 0) : -1;
   }();
   return v < 0 ? (H == 768) : v;
+}
+// stack backward recurrences: one persistent launch per layer (W_hh held in registers,
+// sv_persist.hip) or per-step launches, layer-pipelined.  SV_PERSIST_BWD: unset = persistent
+// when H = 768, 1 = whenever sv_persist_bwd_ok, 0 = per-step.
+int persist_bwd(int H) {
+  static int v = [] {
+    const char* e = getenv("SV_PERSIST_BWD");
+    return e ? (*e == '1' ? 1 : 0) : -1;
+  }();
+  return v < 0 ? (H == 768) : v;
+}
+// persistent backward: the layer's dW GEMMs on `main` after its dx GEMM (0, default; measured
+// c3 16.6 ms/step) or on its weight-gradient stream, overlapping the next layer's recurrence
+// (SV_PBWD_DW_SIDE=1: 16.8 ms -- the GEMM workgroups contend with the co-resident recurrence)
+int pbwd_dw_side() {
+  static int v = [] {
+    const char* e = getenv("SV_PBWD_DW_SIDE");
+    return (e && *e == '1') ? 1 : 0;
+  }();
+  return v;
 }
 void launch_wave_fwd_bf16(dim3 grid, hipStream_t s, const WaveFwdArgs& a, int st) {
   const int sc = bf16_sc();
@@ -817,8 +834,11 @@ BBwdWs carve_bbwd(char* base, int T, int B, int F, int H) {
 }
 }  // namespace
 
+// L per-layer regions, then the persistent backward's hand-off scratch (shared by the layers,
+// whose recurrences run one after another)
 extern "C" size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H) {
-  return (size_t)L * carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
+  const size_t per = (size_t)L * carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
+  return per + (sv_persist_bwd_ok(B, H) ? sv_persist_bwd_scratch(T, B, H) : 0);
 }
 
 extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const bf16_t* const* xT, const long* ld_xT,
@@ -840,6 +860,43 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
   hipEvent_t ev_start = ev[L * nch + L];
   hipError_t e = hipEventRecord(ev_start, main);
   if (e != hipSuccess) return (int)e;
+  if (persist_bwd(H) && sv_persist_bwd_ok(B, H)) {
+    // persistent schedule: per layer (top first) the whole-T recurrence in one launch
+    // (sv_persist.hip) and the whole-T dx GEMM on `main`; the layer's weight gradients on its
+    // weight-gradient stream (SV_PBWD_DW_SIDE=0: on `main` after the dx GEMM)
+    for (int l = L - 1; l >= 0; --l) {
+      const int Fl = l == 0 ? F : H;
+      const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
+      hipStream_t sw = pbwd_dw_side() ? side[L + l] : main;
+      int rc = sv_transpose_cast_bf16(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, main);
+      if (rc) return rc;
+      if (l > 0 && (rc = sv_transpose_cast_bf16(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, main))) return rc;
+      const float* up = l == L - 1 ? dh_last : dx[l + 1];
+      bf16_t* dgf = (bf16_t*)((char*)workspace + per * L);
+      if ((rc = sv_persist_bwd_bf16(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1, dg[l], dgT[l], dgf, main)))
+        return rc;
+      if (l > 0 && (rc = sv_gemm_bf16(T * B, Fl, 4 * H, dg[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr, nullptr,
+                                       0.f, ws.gws, main)))
+        return rc;
+      if (sw != main) {
+        if ((e = hipEventRecord(ev[l * nch], main)) != hipSuccess) return (int)e;
+        if ((e = hipStreamWaitEvent(sw, ev[l * nch], 0)) != hipSuccess) return (int)e;
+      }
+      float* gw = sw != main ? ws.gws2 : ws.gws;
+      rc = sv_gemm_bf16(4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, gw, sw);
+      if (rc) return rc;
+      rc = sv_gemm_bf16(4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, gw, sw);
+      if (rc) return rc;
+      hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
+                         db_hh ? db_hh[l] : nullptr);
+      SV_LAUNCH_CHECK();
+      if ((e = hipEventRecord(ev[L * nch + l], sw)) != hipSuccess) return (int)e;  // grad_ready of layer l
+    }
+    if (pbwd_dw_side())
+      for (int l = 0; l < L; ++l)
+        if ((e = hipStreamWaitEvent(main, ev[L * nch + l], 0)) != hipSuccess) return (int)e;
+    return SV_OK;
+  }
   const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
   for (int l = L - 1; l >= 0; --l) {
     hipStream_t s = side[l], sw = side[L + l];

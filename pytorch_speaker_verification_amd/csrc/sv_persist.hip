@@ -101,6 +101,21 @@ __device__ __forceinline__ void persist_mainloop(__amdgpu_buffer_rsrc_t ra, int 
   __syncthreads();
 }
 
+// Tile order of the W-stationary kernels (1-D grid of nub x nrb workgroups).  Workgroup i is
+// dispatched to XCD i % 8; with xcd = 1 each XCD gets a contiguous range of logical tiles, so
+// the workgroups that share a row block (and read the same handed-off rows) sit mostly on one
+// XCD and the second and later readers hit that XCD's L2 instead of the fabric.
+__device__ __forceinline__ void persist_tile(int xcd, int nub, int& ub, int& rb) {
+  const int i = blockIdx.x, n = gridDim.x;
+  int L = i;
+  if (xcd) {
+    const int x = i & 7, q = n >> 3, r = n & 7;
+    L = x * q + min(x, r) + (i >> 3);
+  }
+  ub = L % nub;
+  rb = L / nub;
+}
+
 // lane 0 of the workgroup: wait until *c >= target (bounded; a timeout raises sv_perr and every
 // later wait returns at once, so a broken launch drains instead of hanging the GPU)
 __device__ __forceinline__ void persist_wait(unsigned* c, unsigned target) {
@@ -233,7 +248,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
                                                                        float* __restrict__ c_tm,
                                                                        float* __restrict__ h_tm, bf16_t* h_bf,
                                                                        bf16_t* __restrict__ hT, long ldhT, int T,
-                                                                       int Bp, int B, int H, unsigned* cnt) {
+                                                                       int Bp, int B, int H, unsigned* cnt, int nub,
+                                                                       int xcd) {
   constexpr int K = NS * 16, LDA = K + 8, HALF = NS / 2 * 16;
   constexpr int LDP = 4 * BF_U + 4, LDH = BF_BM + 1;
   constexpr int PER = BF_BM * BF_U / 256;  // epilogue elements per thread
@@ -244,10 +260,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
   float* hs = pre + BF_BM * LDP;                                         // [32][LDH]
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int j0 = blockIdx.x * BF_U, b0 = blockIdx.y * BF_BM;
+  int ub, rb;
+  persist_tile(xcd, nub, ub, rb);
+  const int j0 = ub * BF_U, b0 = rb * BF_BM;
   const long G = 4L * H, BH = (long)B * H;
-  unsigned* my_cnt = cnt + blockIdx.y * SV_PCNT_STRIDE;
-  const unsigned producers = gridDim.x;
+  unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
+  const unsigned producers = nub;
   // this wave's W_hh fragments: B[k][n] = W[g H + j0 + n][k], lane (n = r, k = 16 s + 8 hh .. +7)
   bf16x8_t wreg[NS];
   {
@@ -380,6 +398,222 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
 }
 
 // ============================================================================
+// W-stationary backward recurrence of one layer (reverse time, all T steps).  Tile (b0, j0):
+// 64 batch rows x 32 hidden units.  Wave g owns gate g's K range of the recurrent product
+//   dh_rec[b][j] = sum_g sum_k dG_{t+1}[b][g H + k] * W_hh[g H + k][j]
+// and keeps its W_hh slice (K = H rows x 32 units, the MFMA B fragments of every k-step) in
+// registers for the whole sequence.  Each wave's A operand (64 rows x H of dG_{t+1}, used by no
+// other wave of the workgroup) streams from the hand-off buffer straight into registers, P
+// fragment pairs in flight.  The hand-off buffer `dgf` holds dG in MFMA A-fragment order --
+// [slot t][row block][gate][row half][k-step][lane][8] -- so every wave load instruction reads
+// one contiguous KB (row-major rows would give 32-B pieces of 32 rows per instruction, which
+// measured at under a third of the CU's L2 read rate).  The four per-gate partials meet in LDS
+// and are summed in gate order 0..3 (the per-step kernel's order, each gate accumulated over k
+// in one accumulator as there), so results are bit-identical to lstm_step_bwd_bf16_kernel.
+// dc * f (the cell-gradient carry) and c_{t-1} stay in registers; the elementwise operands of
+// step t load as 16-B vectors behind the first A fragments.  Only the hand-off stores precede
+// the arrival; dG_t row-major (the dx GEMM's operand) and transposed (dgT, the dW GEMMs')
+// are stored after it, off the critical chain.
+//   acts [T,B,4H] activated gates, c_tm [T,B,H]; dhup: [T,B,H] (up_full) or [B,H] at t = T-1.
+// Hand-off: hand-off table row 1 of MI355X_MICROARCH.md, as the forward kernel above.
+// ============================================================================
+template <int NS, int P>
+__global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
+    const bf16_t* __restrict__ whhT, const float* __restrict__ acts, const float* __restrict__ c_tm,
+    const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
+    bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd, int dbg) {
+  constexpr int LDR = BF_U + 4;          // red [4][64][LDR] fp32 (16-B aligned rows)
+  constexpr int LDG = 4 * BF_U + 8;      // dgs [64][LDG] bf16 (row-major dG tile)
+  constexpr int LDT = BF_BM + 8;         // gts [128][LDT] bf16 (transposed dG tile)
+  constexpr int FRAG = NS * 64 * 8;      // dgf elements of one (row block, gate, row half)
+  static_assert(P >= 1 && P <= NS, "prefetch depth");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red = reinterpret_cast<float*>(smem);
+  bf16_t* dgs = reinterpret_cast<bf16_t*>(smem + 4 * BF_BM * LDR * 4);
+  bf16_t* gts = dgs + BF_BM * LDG;
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  int ub, rb;
+  persist_tile(xcd, nub, ub, rb);
+  const int j0 = ub * BF_U, b0 = rb * BF_BM;
+  const int nrb = gridDim.x / nub;
+  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
+  const long FS = (long)nrb * BF_BM * G;  // dgf slot (elements)
+  unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
+  const unsigned producers = nub;
+  // W_hh fragments of gate g: B[k][n] = W_hh[g H + k][j0 + n] = whhT[j0 + n][g H + k]
+  bf16x8_t wreg[NS];
+  {
+    const bool wok = j0 + r < H;
+    const bf16_t* wrow = whhT + (long)(j0 + r) * G + (long)g * H + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      bf16x8_t z = {};
+      wreg[s] = wok ? *reinterpret_cast<const bf16x8_t*>(wrow + 16 * s) : z;
+    }
+  }
+  // elementwise map: thread -> 4 consecutive units (u4) x rows brow, brow + 32
+  const int u4 = (tid & 7) * 4, brow = tid >> 3;
+  float4 av[2][4], cv[2], cpv[2], upv[2];
+  float dcf[2][4];
+  // step tt's operands except c_tt (carried): 16-B buffer loads, rows past B read zeros (offsets
+  // beyond the slice's range), as do absent operands (zero-size ranges)
+  auto ld4 = [](__amdgpu_buffer_rsrc_t rs, long off_elems) {
+    const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(off_elems * 4), 0, 0);
+    return float4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
+  };
+  const long Bv = B;
+  auto load_ew = [&](int tt) {
+    const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
+    const __amdgpu_buffer_rsrc_t ra_ = sv_rsrc(acts + (long)tt * BG, (unsigned)(BG * 4));
+    const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(tt > 0 ? tt - 1 : 0) * BH, tt > 0 ? (unsigned)(BH * 4) : 0u);
+    const __amdgpu_buffer_rsrc_t ru_ = sv_rsrc(up ? up : c_tm, up ? (unsigned)(BH * 4) : 0u);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const long gb = b0 + brow + 32 * k;
+      const long gbv = gb < Bv ? gb : Bv + 64;  // rows past B: offsets past every range
+#pragma unroll
+      for (int q = 0; q < 4; ++q) av[k][q] = ld4(ra_, gbv * G + q * H + j0 + u4);
+      cpv[k] = ld4(rc_, gbv * H + j0 + u4);
+      upv[k] = ld4(ru_, gbv * H + j0 + u4);
+    }
+  };
+  {
+    const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(T - 1) * BH, (unsigned)(BH * 4));
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const long gb = b0 + brow + 32 * k;
+      cv[k] = ld4(rc_, (gb < Bv ? gb : Bv + 64) * H + j0 + u4);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) dcf[k][v] = 0.f;
+    }
+  }
+  for (int t = T - 1; t >= 0; --t) {
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+    if (t < T - 1 && !(dbg & 4)) {
+      if (tid == 0 && !(dbg & 1)) persist_wait(my_cnt, producers * (unsigned)(T - 1 - t));
+      __syncthreads();
+      // A fragments of dG_{t+1}: (row half m, k-step s) is the KB at ((rb 4 + g) 2 + m) FRAG + s 512
+      const __amdgpu_buffer_rsrc_t ra = sv_rsrc(dgf + (long)(t + 1) * FS, (unsigned)(FS * 2));
+      constexpr unsigned kstep = 1024u;
+      const unsigned base0 = ((unsigned)((rb * 4 + g) * 2) * (unsigned)FRAG + (unsigned)lane * 8u) * 2u;
+      const unsigned base1 = base0 + (unsigned)FRAG * 2u;
+      u32x4_t fa[P][2];
+#pragma unroll
+      for (int s = 0; s < P; ++s) {
+        fa[s][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base0 + kstep * s, 0, 16 /* sc1 */);
+        fa[s][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, base1 + kstep * s, 0, 16 /* sc1 */);
+      }
+      if (!(dbg & 16)) load_ew(t);
+      // the scheduler would sink every load next to its MFMA (one exposed round trip per
+      // k-step); scheduling barriers pin the P-deep software pipeline in program order
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const u32x4_t x0 = fa[s % P][0], x1 = fa[s % P][1];
+        acc0 = mfma_bf16(__builtin_bit_cast(bf16x8_t, x0), wreg[s], acc0);
+        acc1 = mfma_bf16(__builtin_bit_cast(bf16x8_t, x1), wreg[s], acc1);
+        if (s + P < NS) {
+          fa[s % P][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base0 + kstep * (s + P), 0, 16);
+          fa[s % P][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, base1 + kstep * (s + P), 0, 16);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if (!(dbg & 16) || t == T - 1) {
+      load_ew(t);
+    }
+    // per-gate partials -> red[g][row][unit]
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      red[(g * BF_BM + acc_row(i, lane)) * LDR + r] = acc0[i];
+      red[(g * BF_BM + 32 + acc_row(i, lane)) * LDR + r] = acc1[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int b = brow + 32 * k;
+      const float4 r0 = *reinterpret_cast<const float4*>(red + (0 * BF_BM + b) * LDR + u4);
+      const float4 r1 = *reinterpret_cast<const float4*>(red + (1 * BF_BM + b) * LDR + u4);
+      const float4 r2 = *reinterpret_cast<const float4*>(red + (2 * BF_BM + b) * LDR + u4);
+      const float4 r3 = *reinterpret_cast<const float4*>(red + (3 * BF_BM + b) * LDR + u4);
+      const float rs0[4] = {r0.x, r0.y, r0.z, r0.w}, rs1[4] = {r1.x, r1.y, r1.z, r1.w};
+      const float rs2[4] = {r2.x, r2.y, r2.z, r2.w}, rs3[4] = {r3.x, r3.y, r3.z, r3.w};
+      const float ups[4] = {upv[k].x, upv[k].y, upv[k].z, upv[k].w};
+      const float cs[4] = {cv[k].x, cv[k].y, cv[k].z, cv[k].w}, cps[4] = {cpv[k].x, cpv[k].y, cpv[k].z, cpv[k].w};
+      const float a0[4] = {av[k][0].x, av[k][0].y, av[k][0].z, av[k][0].w};
+      const float a1[4] = {av[k][1].x, av[k][1].y, av[k][1].z, av[k][1].w};
+      const float a2[4] = {av[k][2].x, av[k][2].y, av[k][2].z, av[k][2].w};
+      const float a3[4] = {av[k][3].x, av[k][3].y, av[k][3].z, av[k][3].w};
+      unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float dh = rs0[v];
+        dh += rs1[v];
+        dh += rs2[v];
+        dh += rs3[v];
+        dh += ups[v];
+        float dd[4];
+        dcf[k][v] = lstm_cell_bwd(dh, a0[v], a1[v], a2[v], a3[v], cs[v], cps[v], dcf[k][v], dd);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bf16_t e = to_bf(dd[q]);
+          gts[(q * BF_U + u4 + v) * LDT + b] = e;
+          pk[q][v >> 1] |= (unsigned)e << (16 * (v & 1));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(dgs + b * LDG + q * BF_U + u4) = uint2{pk[q][0], pk[q][1]};
+      cv[k] = cpv[k];  // c_{t-1} is the next step's c_t
+    }
+    __syncthreads();
+    // the hand-off: dG_t in fragment order, 16 KB per workgroup as 16 contiguous KB pieces,
+    // 16-B sc1 stores (dbg & 8, profiling only: no global stores at all)
+    if (!(dbg & 8)) {
+      const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 2));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = tid + 256 * i, c = p >> 6, l = p & 63;
+        const int gq = c >> 2, m = (c >> 1) & 1, sl = c & 1;
+        const uint4 v = *reinterpret_cast<const uint4*>(dgs + (32 * m + (l & 31)) * LDG + gq * BF_U + 16 * sl +
+                                                        8 * (l >> 5));
+        const unsigned off =
+            ((unsigned)((rb * 4 + gq) * 2 + m) * (unsigned)FRAG + (unsigned)(2 * ub + sl) * 512u + (unsigned)l * 8u) *
+            2u;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
+      }
+    }
+    // publish dG_t: every store of the hand-off drained, barrier, one lane arrives
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dbg & 8) continue;
+    // dG_t row-major (64 rows x 4 gates x 4 chunks of 8 units) and transposed (128 gate-unit
+    // rows x 8 chunks of 8 batch columns; padding columns get zeros): 16-B plain stores
+    bf16_t* dgt = dg + (long)t * BG;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = tid + 256 * i, row = q >> 4, gq = (q >> 2) & 3, c = q & 3;
+      const int gb = b0 + row, gj = j0 + 8 * c;
+      if (gb < B && gj < H)
+        *reinterpret_cast<uint4*>(dgt + (long)gb * G + (long)gq * H + gj) =
+            *reinterpret_cast<const uint4*>(dgs + row * LDG + gq * BF_U + 8 * c);
+    }
+    if (dgT) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = tid + 256 * i, gu = q >> 3, c = q & 7;
+        const int gq = gu / BF_U, gj = j0 + gu % BF_U, gb = b0 + 8 * c;
+        if (gb < Bp && gj < H)
+          *reinterpret_cast<uint4*>(dgT + ((long)gq * H + gj) * lddgT + (long)t * Bp + gb) =
+              *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
+      }
+    }
+  }
+}
+
+// ============================================================================
 // host side
 // ============================================================================
 namespace {
@@ -395,6 +629,14 @@ int cu_count() {
 }
 // W_hh held in registers (lstm_persist2_fwd_bf16_kernel) when H = 768; SV_PERSIST_W=0 forces the
 // LDS-staged persistent kernel
+// XCD-grouped tile order for the W-stationary kernels (persist_tile); SV_PXCD=0: linear order
+int persist_xcd() {
+  static int v = [] {
+    const char* e = getenv("SV_PXCD");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return v;
+}
 int persist_wregs() {
   static int v = [] {
     const char* e = getenv("SV_PERSIST_W");
@@ -443,11 +685,84 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
   if (H == 768 && persist_wregs()) {
     constexpr int NS = 48, LDA = NS * 16 + 8;
     constexpr size_t lds = (size_t)BF_BM * LDA * 2 + (size_t)(BF_BM * (4 * BF_U + 4) + BF_U * (BF_BM + 1)) * 4;
-    hipLaunchKernelGGL(lstm_persist2_fwd_bf16_kernel<NS>, grid, dim3(256), lds, stream, whh_bf, gates, c_tm, h_tm,
-                       h_bf, hT, ldhT, T, Bp, B, H, cnt);
+    hipLaunchKernelGGL(lstm_persist2_fwd_bf16_kernel<NS>, dim3(grid.x * grid.y), dim3(256), lds, stream, whh_bf,
+                       gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, (int)grid.x, persist_xcd());
   } else {
     hipLaunchKernelGGL(lstm_persist_fwd_bf16_kernel<4>, grid, dim3(512), PFWD_LDS, stream, whh_bf, gates, c_tm, h_tm,
                        h_bf, hT, ldhT, T, Bp, B, H, cnt, dbg);
+  }
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+// ---- W-stationary persistent backward recurrence ----
+namespace {
+constexpr size_t PBWD_LDS = (size_t)4 * BF_BM * (BF_U + 4) * 4 + (size_t)BF_BM * (4 * BF_U + 8) * 2 +
+                            (size_t)4 * BF_U * (BF_BM + 8) * 2;
+// A-fragment prefetch depth (pairs of 16-B loads in flight per lane); SV_PBWD_P overrides
+int pbwd_depth() {
+  static int v = [] {
+    const char* e = getenv("SV_PBWD_P");
+    const int x = e ? atoi(e) : 8;
+    return (x == 4 || x == 8 || x == 12 || x == 16) ? x : 8;
+  }();
+  return v;
+}
+// SV_PBWD_DEBUG (profiling only, results invalid): 1 = no hand-off waits, 4 = no recurrent GEMM, 8 = no global stores, 16 = no
+// elementwise operand loads after the first step
+int pbwd_debug() {
+  static int v = [] {
+    const char* e = getenv("SV_PBWD_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+template <int NS, int P>
+void launch_pbwd(dim3 grid, hipStream_t s, const bf16_t* whhT, const float* acts, const float* c_tm, const float* dhup,
+                 int up_full, bf16_t* dg, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B, int H,
+                 unsigned* cnt) {
+  hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P>), dim3(grid.x * grid.y), dim3(256), PBWD_LDS, s, whhT,
+                     acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x, persist_xcd(),
+                     pbwd_debug());
+}
+}  // namespace
+
+// can the persistent backward recurrence run these dims (W_hh slice in registers: H in {64, 96, 768})?
+extern "C" int sv_persist_bwd_ok(int B, int H) {
+  return (H == 768 || H == 64 || H == 96) && sv_persist_fwd_ok(B, H) && (long)B * 4 * H * 2 < (1L << 31);
+}
+
+// fragment-order hand-off scratch of the persistent backward (bytes; T slots of nrb*64 x 4H bf16)
+extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H) {
+  return (size_t)T * (size_t)((B + BF_BM - 1) / BF_BM) * BF_BM * 4 * H * sizeof(bf16_t);
+}
+
+// one layer's backward recurrence for all t (reverse), on `stream`: dG (bf16, row-major and
+// transposed) from the activations, cell states and the upstream dh (dhup [T,B,H] if up_full,
+// else [B,H] at t = T-1 only, or NULL).  dgT: [4H][T*Bp] (padding columns written as zeros).
+// dgf: sv_persist_bwd_scratch(T, B, H) bytes.
+int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* acts, const float* c_tm,
+                        const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream) {
+  if (!sv_persist_bwd_ok(B, H)) return SV_ESHAPE;
+  if (!dgf || ((uintptr_t)dgf & 15)) return SV_EARG;
+  unsigned* cnt = pcnt_ptr();
+  if (!cnt) return SV_EARG;
+  const int Bp = (B + 7) & ~7;
+  const long lddgT = (long)T * Bp;
+  const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
+  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)grid.y * SV_PCNT_STRIDE * sizeof(unsigned), stream);
+  if (e != hipSuccess) return (int)e;
+  if (H == 768) {
+    switch (pbwd_depth()) {
+      case 4: launch_pbwd<48, 4>(grid, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt); break;
+      case 12: launch_pbwd<48, 12>(grid, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt); break;
+      case 16: launch_pbwd<48, 16>(grid, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt); break;
+      default: launch_pbwd<48, 8>(grid, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt);
+    }
+  } else if (H == 96) {
+    launch_pbwd<6, 4>(grid, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt);
+  } else {
+    launch_pbwd<4, 4>(grid, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt);
   }
   SV_LAUNCH_CHECK();
   return SV_OK;

@@ -41,6 +41,7 @@ def main(out, dims, N, M, T, precision):
     tr = GE2ETrainer(net, GE2ELoss(dev), lr=0.01)
     res["loss"] = tr.step(x, N, M).reshape(1)
     res["flat_p"] = tr.flat_p
+    res["flat_g"] = tr.flat_g
     torch.cuda.synchronize()
     res = {k: v.detach().float().cpu().numpy() for k, v in res.items()}
     res["status"] = np.array([lib().sv_persist_status()])

@@ -44,3 +44,19 @@ def test_wavefront_fwd_bf16_equals_per_step(tmp_path):
         np.testing.assert_array_equal(b[k], a[k], err_msg=k)   # layer 0 is computed identically
     for k in ("gates1", "gates2", "c2", "emb", "loss"):
         np.testing.assert_allclose(b[k], a[k], rtol=2e-2, atol=2e-2, err_msg=k)
+
+
+@pytest.mark.parametrize("dims,N,M,T", [((40, 768, 3, 256), 64, 10, 12),   # c3 grid: 24 x 10 workgroups
+                                        ((40, 96, 2, 32), 7, 5, 9),        # ragged rows (B = 35)
+                                        ((40, 64, 3, 32), 4, 5, 7)])       # H = 64: 2 unit blocks
+def test_persistent_bwd_bf16_equals_per_step(tmp_path, dims, N, M, T):
+    """W-stationary persistent backward recurrence (one launch per layer, dG handed off through
+    HBM) vs per-step launches: the same per-gate MFMA order and the same gate-order sum, so the
+    parameters after one training step are bit-identical."""
+    a = _run(tmp_path, "step", {"SV_PERSIST_BWD": "0"}, dims, N, M, T, "bf16")
+    b = _run(tmp_path, "persist", {"SV_PERSIST_BWD": "1"}, dims, N, M, T, "bf16")
+    c = _run(tmp_path, "persist_side", {"SV_PERSIST_BWD": "1", "SV_PBWD_DW_SIDE": "1"}, dims, N, M, T, "bf16")
+    assert int(b["status"][0]) == 0 and int(c["status"][0]) == 0
+    for k in ("loss", "flat_g", "flat_p"):
+        np.testing.assert_array_equal(b[k], a[k], err_msg=k)
+        np.testing.assert_array_equal(c[k], a[k], err_msg=k)
