@@ -181,12 +181,16 @@ int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* con
 
 /* ---- persistent recurrences (one launch per layer for all T; sv_persist.hip).  The bf16 stack
  * forward uses them (by default when H = 768: W_hh held in registers) when sv_persist_fwd_ok(B, H)
- * (grid co-resident on this device).  Their arrival counters are one device-global block: calls
+ * (grid co-resident on this device); the bf16 stack backward likewise when sv_persist_bwd_ok(B, H)
+ * (H in {64, 96, 768}; by default when H = 768), handing dG off through a fragment-order scratch
+ * of sv_persist_bwd_scratch(T, B, H) bytes that sv_lstm_stack_bwd_bf16_workspace includes.  Their arrival counters are one device-global block: calls
  * that run persistent recurrences must not execute concurrently on one device (the stack
  * functions serialise them on their `main` stream).
  * sv_persist_status: 0 ok, 1 a hand-off wait timed out since the last call (device sync;
  * clears the flag). */
 int sv_persist_fwd_ok(int B, int H);
+int sv_persist_bwd_ok(int B, int H);
+size_t sv_persist_bwd_scratch(int T, int B, int H);
 int sv_persist_status(void);
 
 /* ---- fp32 product mode of the fp32 path (process-wide; returns the previous mode):

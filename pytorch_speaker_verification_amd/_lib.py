@@ -71,6 +71,8 @@ SIGNATURES = {
     "sv_lstm_stack_bwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P]),
     "sv_set_f32_products": (_c_int, [_c_int]),
     "sv_persist_fwd_ok": (_c_int, [_c_int, _c_int]),
+    "sv_persist_bwd_ok": (_c_int, [_c_int, _c_int]),
+    "sv_persist_bwd_scratch": (_c_size_t, [_c_int, _c_int, _c_int]),
     "sv_persist_status": (_c_int, []),
     "sv_clip_sgd_workspace": (_c_size_t, []),
     "sv_clip_sgd_step": (_c_int, [_P, _P, _c_long, _c_float, _c_float, _c_int, _P, _P, _P]),
