@@ -210,6 +210,21 @@ __device__ __forceinline__ bf16_t to_bf(float x) {
   return *reinterpret_cast<const bf16_t*>(&b);
 }
 
+// LSTM cell forward of one element, shared by the bf16 step, wavefront and persistent kernels
+// (contraction off, so every schedule rounds identically): pre-activations (recurrent part p +
+// input part x) -> activated gates a[4] = i f g o, returns c_t, sets h_t
+__device__ __forceinline__ float lstm_cell_fwd(const float (&p)[4], const float (&x)[4], float c_prev, float (&a)[4],
+                                               float& h) {
+#pragma clang fp contract(off)
+  a[0] = sv_sigmoid(p[0] + x[0]);
+  a[1] = sv_sigmoid(p[1] + x[1]);
+  a[2] = tanhf(p[2] + x[2]);
+  a[3] = sv_sigmoid(p[3] + x[3]);
+  const float c = a[1] * c_prev + a[0] * a[2];
+  h = a[3] * tanhf(c);
+  return c;
+}
+
 // LSTM cell backward of one element, shared by the per-step and the persistent bf16 backward
 // kernels so both round identically (contraction off: every product and sum rounded as written)
 //   in: dh (recurrent + upstream), activated gates i f g o, c_t, c_{t-1}, dcf_in = dc_{t+1} f_{t+1}

@@ -173,16 +173,13 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_bf16_kernel(
     if (gb >= B || gj >= H) continue;
     float* gp = gates + (long)gb * G + gj;
     const float* pr = pre + b * LDP + u;
-    const float i = sv_sigmoid(pr[0] + xg[k][0]);
-    const float f = sv_sigmoid(pr[BF_U] + xg[k][1]);
-    const float g = tanhf(pr[2 * BF_U] + xg[k][2]);
-    const float o = sv_sigmoid(pr[3 * BF_U] + xg[k][3]);
-    const float c = f * cpv[k] + i * g;
-    const float h = o * tanhf(c);
-    gp[0] = i;
-    gp[H] = f;
-    gp[2 * H] = g;
-    gp[3 * H] = o;
+    const float pv[4] = {pr[0], pr[BF_U], pr[2 * BF_U], pr[3 * BF_U]};
+    float av[4], h;
+    const float c = lstm_cell_fwd(pv, xg[k], cpv[k], av, h);
+    gp[0] = av[0];
+    gp[H] = av[1];
+    gp[2 * H] = av[2];
+    gp[3 * H] = av[3];
     cout[(long)gb * H + gj] = c;
     hout[(long)gb * H + gj] = h;
     hout_bf[(long)gb * H + gj] = to_bf(h);
@@ -279,16 +276,13 @@ __global__ __launch_bounds__(512) void lstm_wave_fwd_bf16_kernel(const WaveFwdAr
     if (gb >= B || gj >= H) continue;
     float* gp = gates + (long)gb * G + gj;
     const float* pr = pre + b * LDP + u;
-    const float i = sv_sigmoid(pr[0] + xg[k][0]);
-    const float f = sv_sigmoid(pr[BF_U] + xg[k][1]);
-    const float g = tanhf(pr[2 * BF_U] + xg[k][2]);
-    const float o = sv_sigmoid(pr[3 * BF_U] + xg[k][3]);
-    const float c = f * cpv[k] + i * g;
-    const float h = o * tanhf(c);
-    gp[0] = i;
-    gp[H] = f;
-    gp[2 * H] = g;
-    gp[3 * H] = o;
+    const float pv[4] = {pr[0], pr[BF_U], pr[2 * BF_U], pr[3 * BF_U]};
+    float av[4], h;
+    const float c = lstm_cell_fwd(pv, xg[k], cpv[k], av, h);
+    gp[0] = av[0];
+    gp[H] = av[1];
+    gp[2 * H] = av[2];
+    gp[3 * H] = av[3];
     cout[(long)gb * H + gj] = c;
     hout[(long)gb * H + gj] = h;
     hout_bf[(long)gb * H + gj] = to_bf(h);

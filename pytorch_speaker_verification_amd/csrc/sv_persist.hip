@@ -193,12 +193,10 @@ __global__ __launch_bounds__(512) void lstm_persist_fwd_bf16_kernel(const bf16_t
       const int gb = b0 + b, gj = j0 + u;
       const bool ok = gb < B && gj < H;
       const float* pr = pre + b * LDP + u;
-      const float i = sv_sigmoid(pr[0] + xg[k][0]);
-      const float f = sv_sigmoid(pr[BF_U] + xg[k][1]);
-      const float g = tanhf(pr[2 * BF_U] + xg[k][2]);
-      const float o = sv_sigmoid(pr[3 * BF_U] + xg[k][3]);
-      const float c = f * cst[k] + i * g;
-      const float h = o * tanhf(c);
+      const float pv[4] = {pr[0], pr[BF_U], pr[2 * BF_U], pr[3 * BF_U]};
+      float av[4], h;
+      const float c = lstm_cell_fwd(pv, xg[k], cst[k], av, h);
+      const float i = av[0], f = av[1], g = av[2], o = av[3];
       cst[k] = c;
       // h_bf hand-off: lanes (u, u+1) pair up, the even lane stores both as one 4-B sc1 store
       const unsigned hbits = to_bf(h);
@@ -241,6 +239,9 @@ __global__ __launch_bounds__(512) void lstm_persist_fwd_bf16_kernel(const bf16_t
 // fragments of every k-step -- in registers for the whole sequence.  Per step only h_{t-1}
 // (64 rows x H) is staged into LDS (two halves of sc1 buffer loads); each wave reads it as A
 // fragments: 1 LDS fragment per MFMA instead of 2, no W traffic at all after the prologue.
+// Epilogue: each thread owns 4 consecutive units of 2 rows (16-B operand loads and stores);
+// only the h_bf hand-off (16-B sc1 stores from an LDS-staged tile) precedes the arrival, the
+// activations, c, h and hT (16-B transposed chunks) are stored after it.
 // ============================================================================
 template <int NS>
 __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf16_t* __restrict__ whh_bf,
@@ -251,19 +252,21 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
                                                                        int Bp, int B, int H, unsigned* cnt, int nub,
                                                                        int xcd) {
   constexpr int K = NS * 16, LDA = K + 8, HALF = NS / 2 * 16;
-  constexpr int LDP = 4 * BF_U + 4, LDH = BF_BM + 1;
-  constexpr int PER = BF_BM * BF_U / 256;  // epilogue elements per thread
+  constexpr int LDP = 4 * BF_U + 4;      // pre [64][LDP] fp32
+  constexpr int LDB = BF_U + 8;          // hsb [64][LDB] bf16 (h tile, row-major)
+  constexpr int LDT = BF_BM + 8;         // hts [32][LDT] bf16 (h tile, transposed)
   static_assert(NS % 2 == 0, "two staging halves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);                          // [64][LDA]
   float* pre = reinterpret_cast<float*>(smem + BF_BM * LDA * 2);         // [64][LDP]
-  float* hs = pre + BF_BM * LDP;                                         // [32][LDH]
+  bf16_t* hsb = reinterpret_cast<bf16_t*>(pre + BF_BM * LDP);            // [64][LDB]
+  bf16_t* hts = hsb + BF_BM * LDB;                                       // [32][LDT]
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   int ub, rb;
   persist_tile(xcd, nub, ub, rb);
   const int j0 = ub * BF_U, b0 = rb * BF_BM;
-  const long G = 4L * H, BH = (long)B * H;
+  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
   unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
   const unsigned producers = nub;
   // this wave's W_hh fragments: B[k][n] = W[g H + j0 + n][k], lane (n = r, k = 16 s + 8 hh .. +7)
@@ -277,28 +280,34 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
       wreg[s2] = wok ? *reinterpret_cast<const bf16x8_t*>(wrow + 16 * s2) : z;
     }
   }
-  float cst[PER];
+  // elementwise map: thread -> 4 consecutive units (u4) x rows brow, brow + 32
+  const int u4 = (tid & 7) * 4, brow = tid >> 3;
+  const long Bv = B;
+  float cst[2][4];
 #pragma unroll
-  for (int k = 0; k < PER; ++k) cst[k] = 0.f;
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) cst[k][v] = 0.f;
   // staging map of one half (64 rows x HALF bf16 = 64 * HALF / 8 16-B chunks over 256 threads)
   constexpr int CH = BF_BM * HALF / 8 / 256;
-  // x W_ih^T + b of step t (K1 output), prefetched one step ahead: independent of the recurrence
-  float xg[PER][4];
+  // x W_ih^T + b of step t (K1 output), prefetched one step ahead: 16-B buffer loads, rows past B
+  // read zeros
+  float4 xg[2][4];
   auto load_xg = [&](int tt) {
-    const float* gt = gates + (long)tt * B * G;
+    const __amdgpu_buffer_rsrc_t rx = sv_rsrc(gates + (long)tt * BG, (unsigned)(BG * 4));
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = tid + 256 * k, b = e / BF_U, u = e % BF_U;
-      const int gb = b0 + b, gj = j0 + u;
-      const bool ok = gb < B && gj < H;
-      const float* gp = gt + (long)gb * G + gj;
+    for (int k = 0; k < 2; ++k) {
+      const long gb = b0 + brow + 32 * k;
+      const long gbv = gb < Bv ? gb : Bv + 64;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) xg[k][q] = ok ? gp[q * H] : 0.f;
+      for (int q = 0; q < 4; ++q) {
+        const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(rx, (unsigned)((gbv * G + q * H + j0 + u4) * 4), 0, 0);
+        xg[k][q] = float4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
+      }
     }
   };
   load_xg(0);
   for (int t = 0; t < T; ++t) {
-    float* gt = gates + (long)t * B * G;
     f32x16 acc0, acc1;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
@@ -338,62 +347,73 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
       pre[(32 + acc_row(i, lane)) * LDP + g * BF_U + r] = acc1[i];
     }
     __syncthreads();
-    float* ct = c_tm + (long)t * BH;
-    float* ht = h_tm + (long)(t + 1) * BH;
-    bf16_t* hb = h_bf + (long)(t + 1) * BH;
-    float act[PER][4], hv[PER];
+    float4 act[2][4], cv[2], hv[2];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = tid + 256 * k, b = e / BF_U, u = e % BF_U;
-      const int gb = b0 + b, gj = j0 + u;
-      const bool ok = gb < B && gj < H;
-      const float* pr = pre + b * LDP + u;
-      act[k][0] = sv_sigmoid(pr[0] + xg[k][0]);
-      act[k][1] = sv_sigmoid(pr[BF_U] + xg[k][1]);
-      act[k][2] = tanhf(pr[2 * BF_U] + xg[k][2]);
-      act[k][3] = sv_sigmoid(pr[3 * BF_U] + xg[k][3]);
-      const float c = act[k][1] * cst[k] + act[k][0] * act[k][2];
-      const float h = act[k][3] * tanhf(c);
-      cst[k] = c;
-      hv[k] = h;
-      // the hand-off first: lanes (u, u+1) pair up, the even lane stores both (4-B sc1 store)
-      const unsigned hbits = to_bf(h);
-      const unsigned nb = __shfl_down(hbits, 1, 64);
-      if (ok && !(u & 1))
-        __hip_atomic_store(reinterpret_cast<unsigned*>(hb + (long)gb * H + gj), hbits | (nb << 16),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      hs[u * LDH + b] = h;
+    for (int k = 0; k < 2; ++k) {
+      const int b = brow + 32 * k;
+      float4 pq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pq[q] = *reinterpret_cast<const float4*>(pre + b * LDP + q * BF_U + u4);
+      float ao[4][4], co[4], ho[4];
+      unsigned pk[2] = {0u, 0u};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float pv[4] = {pq[0][v], pq[1][v], pq[2][v], pq[3][v]};
+        const float xv[4] = {xg[k][0][v], xg[k][1][v], xg[k][2][v], xg[k][3][v]};
+        float a4[4], h;
+        const float c = lstm_cell_fwd(pv, xv, cst[k][v], a4, h);
+        cst[k][v] = c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ao[q][v] = a4[q];
+        co[v] = c;
+        ho[v] = h;
+        const bf16_t e = to_bf(h);
+        hts[(u4 + v) * LDT + b] = e;
+        pk[v >> 1] |= (unsigned)e << (16 * (v & 1));
+      }
+      *reinterpret_cast<uint2*>(hsb + b * LDB + u4) = uint2{pk[0], pk[1]};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) act[k][q] = float4{ao[q][0], ao[q][1], ao[q][2], ao[q][3]};
+      cv[k] = float4{co[0], co[1], co[2], co[3]};
+      hv[k] = float4{ho[0], ho[1], ho[2], ho[3]};
     }
-    __syncthreads();  // hs complete
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = tid + 256 * k, b = e / BF_U, u = e % BF_U;
-      const int gb = b0 + b, gj = j0 + u;
-      if (gb < B && gj < H) {
-        float* gp = gt + (long)gb * G + gj;
-        gp[0] = act[k][0];
-        gp[H] = act[k][1];
-        gp[2 * H] = act[k][2];
-        gp[3 * H] = act[k][3];
-        ct[(long)gb * H + gj] = cst[k];
-        ht[(long)gb * H + gj] = hv[k];
+    __syncthreads();  // hsb, hts complete
+    // the hand-off: h_t bf16, 64 rows x 4 chunks of 8 units, one 16-B sc1 store per thread
+    {
+      const int row = tid >> 2, c = tid & 3, gb = b0 + row;
+      const __amdgpu_buffer_rsrc_t rw = sv_rsrc(h_bf + (long)(t + 1) * BH, (unsigned)(BH * 2));
+      if (gb < B && j0 + 8 * c < H) {
+        const uint4 v = *reinterpret_cast<const uint4*>(hsb + row * LDB + 8 * c);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw,
+                                               ((unsigned)gb * (unsigned)H + (unsigned)(j0 + 8 * c)) * 2u, 0,
+                                               16 /* sc1 */);
       }
     }
-    if (hT) {
-      for (int e = tid; e < BF_BM * BF_U; e += 256) {
-        const int u = e / BF_BM, b = e % BF_BM;
-        const int gb = b0 + b, gj = j0 + u;
-        if (gb >= B || gj >= H) continue;
-        bf16_t* row = hT + (long)gj * ldhT;
-        row[(long)(t + 1) * Bp + gb] = to_bf(hs[u * LDH + b]);
-        if (t == 0) row[gb] = 0;
-      }
-    }
-    // publish h_t (every store of this step drained first), then prefetch the next x-projection
+    // publish h_t: the hand-off stores drained, barrier, one lane arrives
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // off the critical chain: the next x-projection, then activations, c, h and hT of step t
     if (t + 1 < T) load_xg(t + 1);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const long gb = b0 + brow + 32 * k;
+      if (gb < Bv) {
+        float* gp = gates + (long)t * BG + gb * G + j0 + u4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(gp + q * H) = act[k][q];
+        *reinterpret_cast<float4*>(c_tm + (long)t * BH + gb * H + j0 + u4) = cv[k];
+        *reinterpret_cast<float4*>(h_tm + (long)(t + 1) * BH + gb * H + j0 + u4) = hv[k];
+      }
+    }
+    if (hT) {  // 32 unit rows x 8 chunks of 8 batch columns (padding columns get zeros)
+      const int u = tid >> 3, c = tid & 7, gb = b0 + 8 * c;
+      if (gb < Bp && j0 + u < H) {
+        bf16_t* row = hT + (long)(j0 + u) * ldhT;
+        *reinterpret_cast<uint4*>(row + (long)(t + 1) * Bp + gb) = *reinterpret_cast<const uint4*>(hts + u * LDT + 8 * c);
+        if (t == 0) *reinterpret_cast<uint4*>(row + gb) = uint4{0u, 0u, 0u, 0u};
+      }
+    }
   }
 }
 
@@ -684,7 +704,8 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
   }();
   if (H == 768 && persist_wregs()) {
     constexpr int NS = 48, LDA = NS * 16 + 8;
-    constexpr size_t lds = (size_t)BF_BM * LDA * 2 + (size_t)(BF_BM * (4 * BF_U + 4) + BF_U * (BF_BM + 1)) * 4;
+    constexpr size_t lds = (size_t)BF_BM * LDA * 2 + (size_t)BF_BM * (4 * BF_U + 4) * 4 +
+                           (size_t)BF_BM * (BF_U + 8) * 2 + (size_t)BF_U * (BF_BM + 8) * 2;
     hipLaunchKernelGGL(lstm_persist2_fwd_bf16_kernel<NS>, dim3(grid.x * grid.y), dim3(256), lds, stream, whh_bf,
                        gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, (int)grid.x, persist_xcd());
   } else {
