@@ -508,6 +508,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
       for (int v = 0; v < 4; ++v) dcf[k][v] = 0.f;
     }
   }
+  load_ew(T - 1);
   for (int t = T - 1; t >= 0; --t) {
     f32x16 acc0, acc1;
 #pragma unroll
@@ -526,7 +527,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
         fa[s][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base0 + kstep * s, 0, 16 /* sc1 */);
         fa[s][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, base1 + kstep * s, 0, 16 /* sc1 */);
       }
-      if (!(dbg & 16)) load_ew(t);
       // the scheduler would sink every load next to its MFMA (one exposed round trip per
       // k-step); scheduling barriers pin the P-deep software pipeline in program order
       __builtin_amdgcn_sched_barrier(0);
@@ -541,8 +541,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-    } else if (!(dbg & 16) || t == T - 1) {
-      load_ew(t);
     }
     // per-gate partials -> red[g][row][unit]
 #pragma unroll
@@ -608,6 +606,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // step t-1's elementwise operands, in flight during the stores below and the next hand-off
+    // wait (dbg & 16, profiling only: skipped)
+    if (t > 0 && !(dbg & 16)) load_ew(t - 1);
     if (dbg & 8) continue;
     // dG_t row-major (64 rows x 4 gates x 4 chunks of 8 units) and transposed (128 gate-unit
     // rows x 8 chunks of 8 batch columns; padding columns get zeros): 16-B plain stores
