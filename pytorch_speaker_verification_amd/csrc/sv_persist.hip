@@ -243,7 +243,7 @@ __global__ __launch_bounds__(512) void lstm_persist_fwd_bf16_kernel(const bf16_t
 // only the h_bf hand-off (16-B sc1 stores from an LDS-staged tile) precedes the arrival, the
 // activations, c, h and hT (16-B transposed chunks) are stored after it.
 // ============================================================================
-template <int NS>
+template <int NS, int BM>
 __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf16_t* __restrict__ whh_bf,
                                                                        float* __restrict__ gates,
                                                                        float* __restrict__ c_tm,
@@ -252,20 +252,22 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
                                                                        int Bp, int B, int H, unsigned* cnt, int nub,
                                                                        int xcd) {
   constexpr int K = NS * 16, LDA = K + 8, HALF = NS / 2 * 16;
-  constexpr int LDP = 4 * BF_U + 4;      // pre [64][LDP] fp32
-  constexpr int LDB = BF_U + 8;          // hsb [64][LDB] bf16 (h tile, row-major)
-  constexpr int LDT = BF_BM + 8;         // hts [32][LDT] bf16 (h tile, transposed)
+  constexpr int LDP = 4 * BF_U + 4;      // pre [BM][LDP] fp32
+  constexpr int LDB = BF_U + 8;          // hsb [BM][LDB] bf16 (h tile, row-major)
+  constexpr int LDT = BM + 8;            // hts [32][LDT] bf16 (h tile, transposed)
+  constexpr int KR = BM / 32;            // 32-row halves of the tile (rows per thread)
   static_assert(NS % 2 == 0, "two staging halves");
+  static_assert(BM == 32 || BM == 64, "row tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* As = reinterpret_cast<bf16_t*>(smem);                          // [64][LDA]
-  float* pre = reinterpret_cast<float*>(smem + BF_BM * LDA * 2);         // [64][LDP]
-  bf16_t* hsb = reinterpret_cast<bf16_t*>(pre + BF_BM * LDP);            // [64][LDB]
-  bf16_t* hts = hsb + BF_BM * LDB;                                       // [32][LDT]
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);                          // [BM][LDA]
+  float* pre = reinterpret_cast<float*>(smem + BM * LDA * 2);            // [BM][LDP]
+  bf16_t* hsb = reinterpret_cast<bf16_t*>(pre + BM * LDP);               // [BM][LDB]
+  bf16_t* hts = hsb + BM * LDB;                                          // [32][LDT]
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   int ub, rb;
   persist_tile(xcd, nub, ub, rb);
-  const int j0 = ub * BF_U, b0 = rb * BF_BM;
+  const int j0 = ub * BF_U, b0 = rb * BM;
   const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
   unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
   const unsigned producers = nub;
@@ -280,23 +282,23 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
       wreg[s2] = wok ? *reinterpret_cast<const bf16x8_t*>(wrow + 16 * s2) : z;
     }
   }
-  // elementwise map: thread -> 4 consecutive units (u4) x rows brow, brow + 32
+  // elementwise map: thread -> 4 consecutive units (u4) x rows brow (+ 32)
   const int u4 = (tid & 7) * 4, brow = tid >> 3;
   const long Bv = B;
-  float cst[2][4];
+  float cst[KR][4];
 #pragma unroll
-  for (int k = 0; k < 2; ++k)
+  for (int k = 0; k < KR; ++k)
 #pragma unroll
     for (int v = 0; v < 4; ++v) cst[k][v] = 0.f;
-  // staging map of one half (64 rows x HALF bf16 = 64 * HALF / 8 16-B chunks over 256 threads)
-  constexpr int CH = BF_BM * HALF / 8 / 256;
+  // staging map of one half (BM rows x HALF bf16 = BM * HALF / 8 16-B chunks over 256 threads)
+  constexpr int CH = BM * HALF / 8 / 256;
   // x W_ih^T + b of step t (K1 output), prefetched one step ahead: 16-B buffer loads, rows past B
   // read zeros
-  float4 xg[2][4];
+  float4 xg[KR][4];
   auto load_xg = [&](int tt) {
     const __amdgpu_buffer_rsrc_t rx = sv_rsrc(gates + (long)tt * BG, (unsigned)(BG * 4));
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < KR; ++k) {
       const long gb = b0 + brow + 32 * k;
       const long gbv = gb < Bv ? gb : Bv + 64;
 #pragma unroll
@@ -335,21 +337,23 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
 #pragma unroll
       for (int s2 = 0; s2 < NS; ++s2) {
         const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(As + r * LDA + 16 * s2 + 8 * hh);
-        const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(As + (32 + r) * LDA + 16 * s2 + 8 * hh);
         acc0 = mfma_bf16(a0, wreg[s2], acc0);
-        acc1 = mfma_bf16(a1, wreg[s2], acc1);
+        if constexpr (BM == 64) {
+          const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(As + (32 + r) * LDA + 16 * s2 + 8 * hh);
+          acc1 = mfma_bf16(a1, wreg[s2], acc1);
+        }
       }
     }
-    // gate exchange: wave g's [64 rows][32 units] -> pre[row][g * 32 + unit]
+    // gate exchange: wave g's [BM rows][32 units] -> pre[row][g * 32 + unit]
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       pre[acc_row(i, lane) * LDP + g * BF_U + r] = acc0[i];
-      pre[(32 + acc_row(i, lane)) * LDP + g * BF_U + r] = acc1[i];
+      if constexpr (BM == 64) pre[(32 + acc_row(i, lane)) * LDP + g * BF_U + r] = acc1[i];
     }
     __syncthreads();
-    float4 act[2][4], cv[2], hv[2];
+    float4 act[KR][4], cv[KR], hv[KR];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < KR; ++k) {
       const int b = brow + 32 * k;
       float4 pq[4];
 #pragma unroll
@@ -378,11 +382,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
       hv[k] = float4{ho[0], ho[1], ho[2], ho[3]};
     }
     __syncthreads();  // hsb, hts complete
-    // the hand-off: h_t bf16, 64 rows x 4 chunks of 8 units, one 16-B sc1 store per thread
+    // the hand-off: h_t bf16, BM rows x 4 chunks of 8 units, 16-B sc1 stores
     {
       const int row = tid >> 2, c = tid & 3, gb = b0 + row;
       const __amdgpu_buffer_rsrc_t rw = sv_rsrc(h_bf + (long)(t + 1) * BH, (unsigned)(BH * 2));
-      if (gb < B && j0 + 8 * c < H) {
+      if (row < BM && gb < B && j0 + 8 * c < H) {
         const uint4 v = *reinterpret_cast<const uint4*>(hsb + row * LDB + 8 * c);
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw,
                                                ((unsigned)gb * (unsigned)H + (unsigned)(j0 + 8 * c)) * 2u, 0,
@@ -396,7 +400,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
     // off the critical chain: the next x-projection, then activations, c, h and hT of step t
     if (t + 1 < T) load_xg(t + 1);
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < KR; ++k) {
       const long gb = b0 + brow + 32 * k;
       if (gb < Bv) {
         float* gp = gates + (long)t * BG + gb * G + j0 + u4;
@@ -406,9 +410,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
         *reinterpret_cast<float4*>(h_tm + (long)(t + 1) * BH + gb * H + j0 + u4) = hv[k];
       }
     }
-    if (hT) {  // 32 unit rows x 8 chunks of 8 batch columns (padding columns get zeros)
-      const int u = tid >> 3, c = tid & 7, gb = b0 + 8 * c;
-      if (gb < Bp && j0 + u < H) {
+    if (hT) {  // 32 unit rows x BM/8 chunks of 8 batch columns (padding columns get zeros)
+      constexpr int CPR = BM / 8;
+      const int u = tid / CPR, c = tid % CPR, gb = b0 + 8 * c;
+      if (u < BF_U && gb < Bp && j0 + u < H) {
         bf16_t* row = hT + (long)(j0 + u) * ldhT;
         *reinterpret_cast<uint4*>(row + (long)(t + 1) * Bp + gb) = *reinterpret_cast<const uint4*>(hts + u * LDT + 8 * c);
         if (t == 0) *reinterpret_cast<uint4*>(row + gb) = uint4{0u, 0u, 0u, 0u};
@@ -437,28 +442,30 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
 //   acts [T,B,4H] activated gates, c_tm [T,B,H]; dhup: [T,B,H] (up_full) or [B,H] at t = T-1.
 // Hand-off: hand-off table row 1 of MI355X_MICROARCH.md, as the forward kernel above.
 // ============================================================================
-template <int NS, int P>
+template <int NS, int P, int BM>
 __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     const bf16_t* __restrict__ whhT, const float* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
     bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd, int dbg) {
-  constexpr int LDR = BF_U + 4;          // red [4][64][LDR] fp32 (16-B aligned rows)
-  constexpr int LDG = 4 * BF_U + 8;      // dgs [64][LDG] bf16 (row-major dG tile)
-  constexpr int LDT = BF_BM + 8;         // gts [128][LDT] bf16 (transposed dG tile)
+  constexpr int LDR = BF_U + 4;          // red [4][BM][LDR] fp32 (16-B aligned rows)
+  constexpr int LDG = 4 * BF_U + 8;      // dgs [BM][LDG] bf16 (row-major dG tile)
+  constexpr int LDT = BM + 8;            // gts [128][LDT] bf16 (transposed dG tile)
   constexpr int FRAG = NS * 64 * 8;      // dgf elements of one (row block, gate, row half)
+  constexpr int KR = BM / 32;            // 32-row halves of the tile
   static_assert(P >= 1 && P <= NS, "prefetch depth");
+  static_assert(BM == 32 || BM == 64, "row tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem);
-  bf16_t* dgs = reinterpret_cast<bf16_t*>(smem + 4 * BF_BM * LDR * 4);
-  bf16_t* gts = dgs + BF_BM * LDG;
+  bf16_t* dgs = reinterpret_cast<bf16_t*>(smem + 4 * BM * LDR * 4);
+  bf16_t* gts = dgs + BM * LDG;
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   int ub, rb;
   persist_tile(xcd, nub, ub, rb);
-  const int j0 = ub * BF_U, b0 = rb * BF_BM;
+  const int j0 = ub * BF_U, b0 = rb * BM;
   const int nrb = gridDim.x / nub;
   const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
-  const long FS = (long)nrb * BF_BM * G;  // dgf slot (elements)
+  const long FS = (long)nrb * BM * G;  // dgf slot (elements)
   unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
   const unsigned producers = nub;
   // W_hh fragments of gate g: B[k][n] = W_hh[g H + k][j0 + n] = whhT[j0 + n][g H + k]
@@ -474,8 +481,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
   }
   // elementwise map: thread -> 4 consecutive units (u4) x rows brow, brow + 32
   const int u4 = (tid & 7) * 4, brow = tid >> 3;
-  float4 av[2][4], cv[2], cpv[2], upv[2];
-  float dcf[2][4];
+  float4 av[KR][4], cv[KR], cpv[KR], upv[KR];
+  float dcf[KR][4];
   // step tt's operands except c_tt (carried): 16-B buffer loads, rows past B read zeros (offsets
   // beyond the slice's range), as do absent operands (zero-size ranges)
   auto ld4 = [](__amdgpu_buffer_rsrc_t rs, long off_elems) {
@@ -489,7 +496,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(tt > 0 ? tt - 1 : 0) * BH, tt > 0 ? (unsigned)(BH * 4) : 0u);
     const __amdgpu_buffer_rsrc_t ru_ = sv_rsrc(up ? up : c_tm, up ? (unsigned)(BH * 4) : 0u);
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < KR; ++k) {
       const long gb = b0 + brow + 32 * k;
       const long gbv = gb < Bv ? gb : Bv + 64;  // rows past B: offsets past every range
 #pragma unroll
@@ -501,7 +508,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
   {
     const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(T - 1) * BH, (unsigned)(BH * 4));
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < KR; ++k) {
       const long gb = b0 + brow + 32 * k;
       cv[k] = ld4(rc_, (gb < Bv ? gb : Bv + 64) * H + j0 + u4);
 #pragma unroll
@@ -519,25 +526,25 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
       // A fragments of dG_{t+1}: (row half m, k-step s) is the KB at ((rb 4 + g) 2 + m) FRAG + s 512
       const __amdgpu_buffer_rsrc_t ra = sv_rsrc(dgf + (long)(t + 1) * FS, (unsigned)(FS * 2));
       constexpr unsigned kstep = 1024u;
-      const unsigned base0 = ((unsigned)((rb * 4 + g) * 2) * (unsigned)FRAG + (unsigned)lane * 8u) * 2u;
+      const unsigned base0 = ((unsigned)((rb * 4 + g) * KR) * (unsigned)FRAG + (unsigned)lane * 8u) * 2u;
       const unsigned base1 = base0 + (unsigned)FRAG * 2u;
       u32x4_t fa[P][2];
 #pragma unroll
       for (int s = 0; s < P; ++s) {
         fa[s][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base0 + kstep * s, 0, 16 /* sc1 */);
-        fa[s][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, base1 + kstep * s, 0, 16 /* sc1 */);
+        if constexpr (BM == 64) fa[s][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, base1 + kstep * s, 0, 16);
       }
       // the scheduler would sink every load next to its MFMA (one exposed round trip per
       // k-step); scheduling barriers pin the P-deep software pipeline in program order
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        const u32x4_t x0 = fa[s % P][0], x1 = fa[s % P][1];
-        acc0 = mfma_bf16(__builtin_bit_cast(bf16x8_t, x0), wreg[s], acc0);
-        acc1 = mfma_bf16(__builtin_bit_cast(bf16x8_t, x1), wreg[s], acc1);
+        acc0 = mfma_bf16(__builtin_bit_cast(bf16x8_t, fa[s % P][0]), wreg[s], acc0);
+        if constexpr (BM == 64) acc1 = mfma_bf16(__builtin_bit_cast(bf16x8_t, fa[s % P][1]), wreg[s], acc1);
         if (s + P < NS) {
           fa[s % P][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base0 + kstep * (s + P), 0, 16);
-          fa[s % P][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, base1 + kstep * (s + P), 0, 16);
+          if constexpr (BM == 64)
+            fa[s % P][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, base1 + kstep * (s + P), 0, 16);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -545,17 +552,17 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     // per-gate partials -> red[g][row][unit]
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      red[(g * BF_BM + acc_row(i, lane)) * LDR + r] = acc0[i];
-      red[(g * BF_BM + 32 + acc_row(i, lane)) * LDR + r] = acc1[i];
+      red[(g * BM + acc_row(i, lane)) * LDR + r] = acc0[i];
+      if constexpr (BM == 64) red[(g * BM + 32 + acc_row(i, lane)) * LDR + r] = acc1[i];
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < KR; ++k) {
       const int b = brow + 32 * k;
-      const float4 r0 = *reinterpret_cast<const float4*>(red + (0 * BF_BM + b) * LDR + u4);
-      const float4 r1 = *reinterpret_cast<const float4*>(red + (1 * BF_BM + b) * LDR + u4);
-      const float4 r2 = *reinterpret_cast<const float4*>(red + (2 * BF_BM + b) * LDR + u4);
-      const float4 r3 = *reinterpret_cast<const float4*>(red + (3 * BF_BM + b) * LDR + u4);
+      const float4 r0 = *reinterpret_cast<const float4*>(red + (0 * BM + b) * LDR + u4);
+      const float4 r1 = *reinterpret_cast<const float4*>(red + (1 * BM + b) * LDR + u4);
+      const float4 r2 = *reinterpret_cast<const float4*>(red + (2 * BM + b) * LDR + u4);
+      const float4 r3 = *reinterpret_cast<const float4*>(red + (3 * BM + b) * LDR + u4);
       const float rs0[4] = {r0.x, r0.y, r0.z, r0.w}, rs1[4] = {r1.x, r1.y, r1.z, r1.w};
       const float rs2[4] = {r2.x, r2.y, r2.z, r2.w}, rs3[4] = {r3.x, r3.y, r3.z, r3.w};
       const float ups[4] = {upv[k].x, upv[k].y, upv[k].z, upv[k].w};
@@ -586,18 +593,18 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
       cv[k] = cpv[k];  // c_{t-1} is the next step's c_t
     }
     __syncthreads();
-    // the hand-off: dG_t in fragment order, 16 KB per workgroup as 16 contiguous KB pieces,
-    // 16-B sc1 stores (dbg & 8, profiling only: no global stores at all)
+    // the hand-off: dG_t in fragment order, BM/4 KB per workgroup as contiguous KB pieces
+    // (gate, row half, k-step), 16-B sc1 stores (dbg & 8, profiling only: no global stores)
     if (!(dbg & 8)) {
       const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 2));
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 2 * KR; ++i) {
         const int p = tid + 256 * i, c = p >> 6, l = p & 63;
-        const int gq = c >> 2, m = (c >> 1) & 1, sl = c & 1;
+        const int gq = c / (2 * KR), m = (c >> 1) % KR, sl = c & 1;
         const uint4 v = *reinterpret_cast<const uint4*>(dgs + (32 * m + (l & 31)) * LDG + gq * BF_U + 16 * sl +
                                                         8 * (l >> 5));
         const unsigned off =
-            ((unsigned)((rb * 4 + gq) * 2 + m) * (unsigned)FRAG + (unsigned)(2 * ub + sl) * 512u + (unsigned)l * 8u) *
+            ((unsigned)((rb * 4 + gq) * KR + m) * (unsigned)FRAG + (unsigned)(2 * ub + sl) * 512u + (unsigned)l * 8u) *
             2u;
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
       }
@@ -610,11 +617,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     // wait (dbg & 16, profiling only: skipped)
     if (t > 0 && !(dbg & 16)) load_ew(t - 1);
     if (dbg & 8) continue;
-    // dG_t row-major (64 rows x 4 gates x 4 chunks of 8 units) and transposed (128 gate-unit
-    // rows x 8 chunks of 8 batch columns; padding columns get zeros): 16-B plain stores
+    // dG_t row-major (BM rows x 4 gates x 4 chunks of 8 units) and transposed (128 gate-unit
+    // rows x BM/8 chunks of 8 batch columns; padding columns get zeros): 16-B plain stores
     bf16_t* dgt = dg + (long)t * BG;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < BM / 16; ++i) {
       const int q = tid + 256 * i, row = q >> 4, gq = (q >> 2) & 3, c = q & 3;
       const int gb = b0 + row, gj = j0 + 8 * c;
       if (gb < B && gj < H)
@@ -623,8 +630,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     }
     if (dgT) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = tid + 256 * i, gu = q >> 3, c = q & 7;
+      for (int i = 0; i < BM / 16; ++i) {
+        const int q = tid + 256 * i, gu = q / (BM / 8), c = q % (BM / 8);
         const int gq = gu / BF_U, gj = j0 + gu % BF_U, gb = b0 + 8 * c;
         if (gb < Bp && gj < H)
           *reinterpret_cast<uint4*>(dgT + ((long)gq * H + gj) * lddgT + (long)t * Bp + gb) =
@@ -687,6 +694,17 @@ extern "C" int sv_persist_status(void) {
   return (int)v;
 }
 
+// row tile of the W-stationary kernels: 32 rows when twice the 64-row grid still fits on the
+// device (B <= 320 at H = 768: c5's per-GPU batch), else 64; SV_PBM=64 forces 64
+int persist_bm(int B, int H) {
+  static int force64 = [] {
+    const char* e = getenv("SV_PBM");
+    return (e && atoi(e) == 64) ? 1 : 0;
+  }();
+  const long grid32 = (long)((H + BF_U - 1) / BF_U) * ((B + 31) / 32);
+  return (!force64 && grid32 <= cu_count() && (B + 31) / 32 <= SV_PCNT_ROWS) ? 32 : 64;
+}
+
 // one layer's recurrence (K2 for all t) after its K1 has filled `gates`; on `stream`
 int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates, float* c_tm, float* h_tm,
                         bf16_t* h_bf, bf16_t* hT, hipStream_t stream) {
@@ -695,7 +713,9 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
   if (!cnt) return SV_EARG;
   const int Bp = (B + 7) & ~7;
   const long ldhT = (long)(T + 1) * Bp;
-  const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
+  const bool wst = H == 768 && persist_wregs();
+  const int bm = wst ? persist_bm(B, H) : BF_BM;
+  const dim3 grid((H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)grid.y * SV_PCNT_STRIDE * sizeof(unsigned), stream);
   if (e != hipSuccess) return (int)e;
   // SV_PERSIST_DEBUG (profiling only, results invalid): 1 = skip the hand-off waits, 2 = skip the GEMM
@@ -703,12 +723,16 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
     const char* v = getenv("SV_PERSIST_DEBUG");
     return v ? atoi(v) : 0;
   }();
-  if (H == 768 && persist_wregs()) {
+  if (wst) {
     constexpr int NS = 48, LDA = NS * 16 + 8;
-    constexpr size_t lds = (size_t)BF_BM * LDA * 2 + (size_t)BF_BM * (4 * BF_U + 4) * 4 +
-                           (size_t)BF_BM * (BF_U + 8) * 2 + (size_t)BF_U * (BF_BM + 8) * 2;
-    hipLaunchKernelGGL(lstm_persist2_fwd_bf16_kernel<NS>, dim3(grid.x * grid.y), dim3(256), lds, stream, whh_bf,
-                       gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, (int)grid.x, persist_xcd());
+    const size_t lds = (size_t)bm * LDA * 2 + (size_t)bm * (4 * BF_U + 4) * 4 + (size_t)bm * (BF_U + 8) * 2 +
+                       (size_t)BF_U * (bm + 8) * 2;
+    if (bm == 32)
+      hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 32>), dim3(grid.x * grid.y), dim3(256), lds, stream,
+                         whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, (int)grid.x, persist_xcd());
+    else
+      hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 64>), dim3(grid.x * grid.y), dim3(256), lds, stream,
+                         whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, (int)grid.x, persist_xcd());
   } else {
     hipLaunchKernelGGL(lstm_persist_fwd_bf16_kernel<4>, grid, dim3(512), PFWD_LDS, stream, whh_bf, gates, c_tm, h_tm,
                        h_bf, hT, ldhT, T, Bp, B, H, cnt, dbg);
@@ -719,16 +743,8 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
 
 // ---- W-stationary persistent backward recurrence ----
 namespace {
-constexpr size_t PBWD_LDS = (size_t)4 * BF_BM * (BF_U + 4) * 4 + (size_t)BF_BM * (4 * BF_U + 8) * 2 +
-                            (size_t)4 * BF_U * (BF_BM + 8) * 2;
-// A-fragment prefetch depth (pairs of 16-B loads in flight per lane); SV_PBWD_P overrides
-int pbwd_depth() {
-  static int v = [] {
-    const char* e = getenv("SV_PBWD_P");
-    const int x = e ? atoi(e) : 8;
-    return (x == 4 || x == 8 || x == 12 || x == 16) ? x : 8;
-  }();
-  return v;
+constexpr size_t pbwd_lds(int bm) {
+  return (size_t)4 * bm * (BF_U + 4) * 4 + (size_t)bm * (4 * BF_U + 8) * 2 + (size_t)4 * BF_U * (bm + 8) * 2;
 }
 // SV_PBWD_DEBUG (profiling only, results invalid): 1 = no hand-off waits, 4 = no recurrent GEMM, 8 = no global stores, 16 = no
 // elementwise operand loads after the first step
@@ -740,12 +756,17 @@ int pbwd_debug() {
   return v;
 }
 template <int NS, int P>
-void launch_pbwd(dim3 grid, hipStream_t s, const bf16_t* whhT, const float* acts, const float* c_tm, const float* dhup,
-                 int up_full, bf16_t* dg, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B, int H,
-                 unsigned* cnt) {
-  hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P>), dim3(grid.x * grid.y), dim3(256), PBWD_LDS, s, whhT,
-                     acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x, persist_xcd(),
-                     pbwd_debug());
+void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const float* acts, const float* c_tm,
+                 const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B,
+                 int H, unsigned* cnt) {
+  if (bm == 32)
+    hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P, 32>), dim3(grid.x * grid.y), dim3(256), pbwd_lds(32), s,
+                       whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x,
+                       persist_xcd(), pbwd_debug());
+  else
+    hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P, 64>), dim3(grid.x * grid.y), dim3(256), pbwd_lds(64), s,
+                       whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x,
+                       persist_xcd(), pbwd_debug());
 }
 }  // namespace
 
@@ -754,7 +775,8 @@ extern "C" int sv_persist_bwd_ok(int B, int H) {
   return (H == 768 || H == 64 || H == 96) && sv_persist_fwd_ok(B, H) && (long)B * 4 * H * 2 < (1L << 31);
 }
 
-// fragment-order hand-off scratch of the persistent backward (bytes; T slots of nrb*64 x 4H bf16)
+// fragment-order hand-off scratch of the persistent backward (bytes; T slots of nrb*BM x 4H
+// bf16; the 64-row count bounds the 32-row one)
 extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H) {
   return (size_t)T * (size_t)((B + BF_BM - 1) / BF_BM) * BF_BM * 4 * H * sizeof(bf16_t);
 }
@@ -771,21 +793,17 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* ac
   if (!cnt) return SV_EARG;
   const int Bp = (B + 7) & ~7;
   const long lddgT = (long)T * Bp;
-  const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
+  const int bm = persist_bm(B, H);
+  const dim3 grid((H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)grid.y * SV_PCNT_STRIDE * sizeof(unsigned), stream);
   if (e != hipSuccess) return (int)e;
-  if (H == 768) {
-    switch (pbwd_depth()) {
-      case 4: launch_pbwd<48, 4>(grid, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt); break;
-      case 12: launch_pbwd<48, 12>(grid, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt); break;
-      case 16: launch_pbwd<48, 16>(grid, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt); break;
-      default: launch_pbwd<48, 8>(grid, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt);
-    }
-  } else if (H == 96) {
-    launch_pbwd<6, 4>(grid, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt);
-  } else {
-    launch_pbwd<4, 4>(grid, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt);
-  }
+  // A-fragment prefetch depth 8 at H = 768 (measured: 4 / 16 no better)
+  if (H == 768)
+    launch_pbwd<48, 8>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt);
+  else if (H == 96)
+    launch_pbwd<6, 4>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt);
+  else
+    launch_pbwd<4, 4>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }

@@ -23,6 +23,7 @@ def _run(tmp_path, tag, env_extra, dims, N, M, T, precision):
 
 
 @pytest.mark.parametrize("dims,N,M,T", [((40, 768, 3, 256), 64, 10, 12),   # c3 grid: 24 x 10 workgroups
+                                        ((40, 768, 2, 256), 16, 10, 7),    # B = 160: 32-row tiles
                                         ((40, 96, 2, 32), 7, 5, 9)])       # ragged rows (B = 35)
 def test_persistent_fwd_bf16_equals_per_step(tmp_path, dims, N, M, T):
     a = _run(tmp_path, "step", {"SV_PERSIST": "0", "SV_WAVEFRONT": "0"}, dims, N, M, T, "bf16")
@@ -47,6 +48,7 @@ def test_wavefront_fwd_bf16_equals_per_step(tmp_path):
 
 
 @pytest.mark.parametrize("dims,N,M,T", [((40, 768, 3, 256), 64, 10, 12),   # c3 grid: 24 x 10 workgroups
+                                        ((40, 768, 2, 256), 16, 10, 7),    # B = 160: 32-row tiles
                                         ((40, 96, 2, 32), 7, 5, 9),        # ragged rows (B = 35)
                                         ((40, 64, 3, 32), 4, 5, 7)])       # H = 64: 2 unit blocks
 def test_persistent_bwd_bf16_equals_per_step(tmp_path, dims, N, M, T):
