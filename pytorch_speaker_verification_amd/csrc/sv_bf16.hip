@@ -10,6 +10,7 @@
 #include "sv_gemm.h"
 #include "../../include/sv_ge2e.h"
 #include "sv_bf16.h"
+#include "sv_gemm256.h"
 
 
 // ============================================================================
@@ -389,8 +390,26 @@ struct BPlan {
   int bm, bn, splitk, kchunk;
 };
 
+// 256 x 256 glds kernel (sv_gemm256.h) for shapes it tiles exactly; SV_GEMM256=0 disables it
+bool gemm256_ok(int M, int N, int K) {
+  static int on = [] {
+    const char* e = getenv("SV_GEMM256");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on && M % G256_BM == 0 && N % G256_BM == 0 && K % G256_BK == 0;
+}
+
 BPlan plan_bf16(int M, int N, int K) {
   BPlan p;
+  if (gemm256_ok(M, N, K)) {  // one workgroup per CU: split K only to fill the 256 CUs
+    const long tiles = (long)(M / G256_BM) * (N / G256_BM);
+    int sk = 1;
+    if (tiles < 256) sk = (int)std::max(1L, std::min(256L / tiles, (long)K / 1024));
+    p.bm = p.bn = G256_BM;
+    p.kchunk = ((K + sk - 1) / sk + G256_BK - 1) / G256_BK * G256_BK;
+    p.splitk = (K + p.kchunk - 1) / p.kchunk;
+    return p;
+  }
   const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
   const bool small = t128 < 128;
   p.bm = p.bn = small ? 64 : 128;
@@ -571,6 +590,25 @@ extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, cons
   if (M <= 0 || N <= 0 || K <= 0 || !A || !B || !C) return SV_EARG;
   if (K % 8 || lda % 8 || ldb % 8 || (((uintptr_t)A | (uintptr_t)B) & 15)) return SV_EALIGN;
   const BPlan p = plan_bf16(M, N, K);
+  if (p.bm == G256_BM) {
+    const int tiles = (M / G256_BM) * (N / G256_BM);
+    const long slab = (long)M * N;
+    if (p.splitk == 1) {
+      hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_STORE>), dim3(tiles, 1), dim3(512), G256_LDS, stream, A, lda, B,
+                         ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1, beta);
+      SV_LAUNCH_CHECK();
+      return SV_OK;
+    }
+    if (!workspace) return SV_EARG;
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_SLAB>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream, A, lda,
+                       B, ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr, 0.f);
+    SV_LAUNCH_CHECK();
+    const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
+    hipLaunchKernelGGL(slab_reduce_bf_kernel, dim3(grid), dim3(256), 0, stream, workspace, p.splitk, slab, C, ldc, M, N,
+                       beta, bias0, bias1);
+    SV_LAUNCH_CHECK();
+    return SV_OK;
+  }
   if (p.splitk == 1) {
     if (p.bm == 64)
       launch_bf<64, 64, BEPI_STORE>(A, lda, B, ldb, C, ldc, 0, M, N, K, 1, p.kchunk, bias0, bias1, beta, stream);

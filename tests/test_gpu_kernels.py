@@ -121,7 +121,8 @@ def test_gemm_f32_bias_and_split_k(M, N, K):
     assert (C - ref).abs().max().item() <= 2e-6 * K ** 0.5 * ref.abs().max().item() + 1e-5
 
 
-@pytest.mark.parametrize("M,N,K", [(640, 3072, 768), (3072, 768, 10240), (100, 40, 72), (640, 256, 768)])
+@pytest.mark.parametrize("M,N,K", [(640, 3072, 768), (3072, 768, 10240), (100, 40, 72), (640, 256, 768),
+                                   (1024, 768, 3072), (2560, 3072, 768), (512, 256, 4096)])
 def test_gemm_bf16(M, N, K):
     """bf16 operands, fp32 accumulation: against fp64 on the same bf16-rounded inputs."""
     from pytorch_speaker_verification_amd._lib import call, lib, ptr
