@@ -71,8 +71,14 @@ def test_dp_two_ranks_equal_single_process(precision):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    # the weight gradients are summed in a different order (per-rank GEMMs + all-reduce vs one
+    # GEMM over the whole batch), so the updated fp32 weights differ by fp32 ulps; in bf16 such a
+    # difference can flip the bf16 rounding of a weight operand at the next step (a 2^-8 relative
+    # change of that element), which moves the step-2 loss by ~1e-4 relative
+    loss_rtol = 1e-5 if precision == "f32" else 1e-3
     for rank, losses, sd, wb in res:
-        np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
+        np.testing.assert_allclose(losses[:1], ref_losses[:1], rtol=1e-5)
+        np.testing.assert_allclose(losses, ref_losses, rtol=loss_rtol)
         for k in ref_sd:
             np.testing.assert_allclose(sd[k], ref_sd[k], atol=1e-5, err_msg=k)
         np.testing.assert_allclose(wb, [ge2e.w.item(), ge2e.b.item()], atol=1e-6)
