@@ -247,8 +247,10 @@ __device__ __forceinline__ float lstm_cell_bwd(float dh, float i, float f, float
 
 // persistent forward recurrence of one layer (sv_persist.hip)
 extern "C" int sv_persist_fwd_ok(int B, int H);
+int sv_persist_fwd_fusex_ok(int H, int F);
 int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates, float* c_tm, float* h_tm,
-                        bf16_t* h_bf, bf16_t* hT, hipStream_t stream);
+                        bf16_t* h_bf, bf16_t* hT, hipStream_t stream, const bf16_t* x_bf = nullptr, int F = 0,
+                        const bf16_t* wih_bf = nullptr, const float* b_ih = nullptr, const float* b_hh = nullptr);
 // persistent backward recurrence of one layer (sv_persist.hip)
 extern "C" int sv_persist_bwd_ok(int B, int H);
 extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H);

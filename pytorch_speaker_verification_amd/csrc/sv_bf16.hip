@@ -756,8 +756,15 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
         return (int)e;
       const int Fl = l == 0 ? F : H;
       const bf16_t* in = l == 0 ? x_bf : h_bf[l - 1] + BH;
-      int rc = sv_gemm_bf16(T * B, 4 * H, Fl, in, Fl, w_ih_bf[l], Fl, gates[l], 4L * H, b_ih[l], b_hh[l], 0.f,
-                            nullptr, main);
+      int rc;
+      if (l == 0 && sv_persist_fwd_fusex_ok(H, F)) {  // layer 0's input projection inside the recurrence
+        if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, x_bf, F,
+                                      w_ih_bf[l], b_ih[l], b_hh[l])))
+          return rc;
+        continue;
+      }
+      rc = sv_gemm_bf16(T * B, 4 * H, Fl, in, Fl, w_ih_bf[l], Fl, gates[l], 4L * H, b_ih[l], b_hh[l], 0.f, nullptr,
+                        main);
       if (rc) return rc;
       if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main)))
         return rc;

@@ -243,14 +243,22 @@ __global__ __launch_bounds__(512) void lstm_persist_fwd_bf16_kernel(const bf16_t
 // only the h_bf hand-off (16-B sc1 stores from an LDS-staged tile) precedes the arrival, the
 // activations, c, h and hT (16-B transposed chunks) are stored after it.
 // ============================================================================
-template <int NS, int BM>
+// XF > 0 (layer 0, F = 8 * XF <= 48 input features): the input projection x_t W_ih^T + b_ih + b_hh
+// is computed in the kernel from x_bf [T,B,F] and W_ih [4H,F] (held in registers beside W_hh:
+// 3 k-steps of 16, zero-padded), so the layer needs no K1 GEMM and its step loads 80 B per row
+// instead of 4 x 4H fp32 pre-activations; the sum (MFMA over the zero-padded k range, then the
+// two biases) matches the K1 GEMM's bit for bit.
+template <int NS, int BM, int XF>
 __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf16_t* __restrict__ whh_bf,
                                                                        float* __restrict__ gates,
                                                                        float* __restrict__ c_tm,
                                                                        float* __restrict__ h_tm, bf16_t* h_bf,
                                                                        bf16_t* __restrict__ hT, long ldhT, int T,
                                                                        int Bp, int B, int H, unsigned* cnt, int nub,
-                                                                       int xcd) {
+                                                                       int xcd, const bf16_t* __restrict__ x_bf,
+                                                                       const bf16_t* __restrict__ wih_bf,
+                                                                       const float* __restrict__ b_ih,
+                                                                       const float* __restrict__ b_hh) {
   constexpr int K = NS * 16, LDA = K + 8, HALF = NS / 2 * 16;
   constexpr int LDP = 4 * BF_U + 4;      // pre [BM][LDP] fp32
   constexpr int LDB = BF_U + 8;          // hsb [BM][LDB] bf16 (h tile, row-major)
@@ -282,6 +290,42 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
       wreg[s2] = wok ? *reinterpret_cast<const bf16x8_t*>(wrow + 16 * s2) : z;
     }
   }
+  // fused input projection (XF > 0): W_ih fragments of this wave's 32 gate columns (k = 16 s +
+  // 8 hh .. +7, zero past F = 8 XF) and the column's bias b_ih + b_hh
+  constexpr int XS = (XF + 1) / 2;  // k-steps of 16
+  constexpr int F = 8 * XF;
+  bf16x8_t wx[XS > 0 ? XS : 1];
+  float xbias = 0.f;
+  if constexpr (XF > 0) {
+    const int col = g * H + j0 + r;
+    const bool wok = j0 + r < H;
+#pragma unroll
+    for (int s2 = 0; s2 < XS; ++s2) {
+      bf16x8_t z = {};
+      wx[s2] = (wok && 16 * s2 + 8 * hh < F) ? *reinterpret_cast<const bf16x8_t*>(wih_bf + (long)col * F + 16 * s2 + 8 * hh)
+                                             : z;
+    }
+    if (wok) {
+      if (b_ih) xbias += b_ih[col];
+      if (b_hh) xbias += b_hh[col];
+    }
+  }
+  // x_t A fragments (rows b0 + r (+32), k = 16 s + 8 hh), prefetched a step ahead; rows past B
+  // and k past F read zeros
+  u32x4_t xa[XS > 0 ? XS : 1][BM / 32];
+  auto load_x = [&](int tt) {
+    if constexpr (XF > 0) {
+      const __amdgpu_buffer_rsrc_t rxs = sv_rsrc(x_bf + (long)tt * B * F, (unsigned)((long)B * F * 2));
+#pragma unroll
+      for (int s2 = 0; s2 < XS; ++s2)
+#pragma unroll
+        for (int m = 0; m < BM / 32; ++m) {
+          const unsigned off = 16 * s2 + 8 * hh < F ? ((unsigned)(b0 + 32 * m + r) * (unsigned)F + 16 * s2 + 8 * hh) * 2u
+                                                    : 0xFFFFFFF0u;
+          xa[s2][m] = __builtin_amdgcn_raw_buffer_load_b128(rxs, off, 0, 0);
+        }
+    }
+  };
   // elementwise map: thread -> 4 consecutive units (u4) x rows brow (+ 32)
   const int u4 = (tid & 7) * 4, brow = tid >> 3;
   const long Bv = B;
@@ -296,6 +340,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
   // read zeros
   float4 xg[KR][4];
   auto load_xg = [&](int tt) {
+    if constexpr (XF > 0) {
+      load_x(tt);
+      return;
+    }
     const __amdgpu_buffer_rsrc_t rx = sv_rsrc(gates + (long)tt * BG, (unsigned)(BG * 4));
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
@@ -344,6 +392,21 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
         }
       }
     }
+    if constexpr (XF > 0) {  // pre-activation = recurrent part + (x_t W_ih^T + b_ih + b_hh)
+      f32x16 x0, x1;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) x0[i] = x1[i] = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < XS; ++s2) {
+        x0 = mfma_bf16(__builtin_bit_cast(bf16x8_t, xa[s2][0]), wx[s2], x0);
+        if constexpr (BM == 64) x1 = mfma_bf16(__builtin_bit_cast(bf16x8_t, xa[s2][1]), wx[s2], x1);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        acc0[i] += x0[i] + xbias;
+        if constexpr (BM == 64) acc1[i] += x1[i] + xbias;
+      }
+    }
     // gate exchange: wave g's [BM rows][32 units] -> pre[row][g * 32 + unit]
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -363,7 +426,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const float pv[4] = {pq[0][v], pq[1][v], pq[2][v], pq[3][v]};
-        const float xv[4] = {xg[k][0][v], xg[k][1][v], xg[k][2][v], xg[k][3][v]};
+        float xv[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (XF == 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) xv[q] = xg[k][q][v];
+        }
         float a4[4], h;
         const float c = lstm_cell_fwd(pv, xv, cst[k][v], a4, h);
         cst[k][v] = c;
@@ -694,6 +761,7 @@ extern "C" int sv_persist_status(void) {
   return (int)v;
 }
 
+namespace {
 // row tile of the W-stationary kernels: 32 rows when twice the 64-row grid still fits on the
 // device (B <= 320 at H = 768: c5's per-GPU batch), else 64; SV_PBM=64 forces 64
 int persist_bm(int B, int H) {
@@ -705,10 +773,26 @@ int persist_bm(int B, int H) {
   return (!force64 && grid32 <= cu_count() && (B + 31) / 32 <= SV_PCNT_ROWS) ? 32 : 64;
 }
 
-// one layer's recurrence (K2 for all t) after its K1 has filled `gates`; on `stream`
+// SV_PFUSEX=0: layer 0 keeps its K1 GEMM instead of the in-kernel input projection
+int persist_fusex() {
+  static int v = [] {
+    const char* e = getenv("SV_PFUSEX");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return v;
+}
+}  // namespace
+
+// can the persistent forward compute layer 0's input projection in-kernel (F = 40 features)?
+int sv_persist_fwd_fusex_ok(int H, int F) { return H == 768 && F == 40 && persist_wregs() && persist_fusex(); }
+
+// one layer's recurrence (K2 for all t) after its K1 has filled `gates`; on `stream`.  With x_bf
+// (layer 0, sv_persist_fwd_fusex_ok): no K1 -- the kernel forms x_t W_ih^T + b_ih + b_hh itself.
 int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates, float* c_tm, float* h_tm,
-                        bf16_t* h_bf, bf16_t* hT, hipStream_t stream) {
+                        bf16_t* h_bf, bf16_t* hT, hipStream_t stream, const bf16_t* x_bf, int F,
+                        const bf16_t* wih_bf, const float* b_ih, const float* b_hh) {
   if (!sv_persist_fwd_ok(B, H)) return SV_ESHAPE;
+  if (x_bf && (!wih_bf || !sv_persist_fwd_fusex_ok(H, F))) return SV_EARG;
   unsigned* cnt = pcnt_ptr();
   if (!cnt) return SV_EARG;
   const int Bp = (B + 7) & ~7;
@@ -727,12 +811,20 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
     constexpr int NS = 48, LDA = NS * 16 + 8;
     const size_t lds = (size_t)bm * LDA * 2 + (size_t)bm * (4 * BF_U + 4) * 4 + (size_t)bm * (BF_U + 8) * 2 +
                        (size_t)BF_U * (bm + 8) * 2;
-    if (bm == 32)
-      hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 32>), dim3(grid.x * grid.y), dim3(256), lds, stream,
-                         whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, (int)grid.x, persist_xcd());
+    const dim3 g1(grid.x * grid.y);
+    const int nub = (int)grid.x, xcd = persist_xcd();
+    if (x_bf && bm == 32)
+      hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 32, 5>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
+                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, x_bf, wih_bf, b_ih, b_hh);
+    else if (x_bf)
+      hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 64, 5>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
+                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, x_bf, wih_bf, b_ih, b_hh);
+    else if (bm == 32)
+      hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 32, 0>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
+                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, nullptr, nullptr, nullptr, nullptr);
     else
-      hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 64>), dim3(grid.x * grid.y), dim3(256), lds, stream,
-                         whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, (int)grid.x, persist_xcd());
+      hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 64, 0>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
+                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, nullptr, nullptr, nullptr, nullptr);
   } else {
     hipLaunchKernelGGL(lstm_persist_fwd_bf16_kernel<4>, grid, dim3(512), PFWD_LDS, stream, whh_bf, gates, c_tm, h_tm,
                        h_bf, hT, ldhT, T, Bp, B, H, cnt, dbg);
