@@ -522,6 +522,15 @@ int persist_bwd(int H) {
   }();
   return v < 0 ? (H == 768) : v;
 }
+// persistent backward: bias gradients summed inside the recurrence (1, default) or by a row sum
+// over dG^T afterwards (SV_PBWD_DB=0)
+int pbwd_db() {
+  static int v = [] {
+    const char* e = getenv("SV_PBWD_DB");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return v;
+}
 // persistent backward: the layer's dW GEMMs on `main` after its dx GEMM (0, default; measured
 // c3 16.6 ms/step) or on its weight-gradient stream, overlapping the next layer's recurrence
 // (SV_PBWD_DW_SIDE=1: 16.8 ms -- the GEMM workgroups contend with the co-resident recurrence)
@@ -912,7 +921,9 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       if (l > 0 && (rc = sv_transpose_cast_bf16(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, main))) return rc;
       const float* up = l == L - 1 ? dh_last : dx[l + 1];
       bf16_t* dgf = (bf16_t*)((char*)workspace + per * L);
-      if ((rc = sv_persist_bwd_bf16(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1, dg[l], dgT[l], dgf, main)))
+      const bool dbk = pbwd_db();  // bias gradients summed in the recurrence, else by rowsum over dG^T
+      if ((rc = sv_persist_bwd_bf16(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1, dg[l], dgT[l], dgf, main,
+                                    dbk ? db_ih[l] : nullptr, dbk && db_hh ? db_hh[l] : nullptr)))
         return rc;
       if (l > 0 && (rc = sv_gemm_bf16(T * B, Fl, 4 * H, dg[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr, nullptr,
                                        0.f, ws.gws, main)))
@@ -926,9 +937,11 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       if (rc) return rc;
       rc = sv_gemm_bf16(4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, gw, sw);
       if (rc) return rc;
-      hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
-                         db_hh ? db_hh[l] : nullptr);
-      SV_LAUNCH_CHECK();
+      if (!dbk) {
+        hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
+                           db_hh ? db_hh[l] : nullptr);
+        SV_LAUNCH_CHECK();
+      }
       if ((e = hipEventRecord(ev[L * nch + l], sw)) != hipSuccess) return (int)e;  // grad_ready of layer l
     }
     if (pbwd_dw_side())

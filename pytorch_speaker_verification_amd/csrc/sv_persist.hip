@@ -513,7 +513,7 @@ template <int NS, int P, int BM>
 __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     const bf16_t* __restrict__ whhT, const float* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
-    bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd, int dbg) {
+    bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd, int dbg, float* __restrict__ dbp) {
   constexpr int LDR = BF_U + 4;          // red [4][BM][LDR] fp32 (16-B aligned rows)
   constexpr int LDG = 4 * BF_U + 8;      // dgs [BM][LDG] bf16 (row-major dG tile)
   constexpr int LDT = BM + 8;            // gts [128][LDT] bf16 (transposed dG tile)
@@ -550,6 +550,14 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
   const int u4 = (tid & 7) * 4, brow = tid >> 3;
   float4 av[KR][4], cv[KR], cpv[KR], upv[KR];
   float dcf[KR][4];
+  // bias-gradient partial sums over t of this thread's bf16 dG values (dbp: per row block)
+  float dbs[KR][4][4];
+#pragma unroll
+  for (int k = 0; k < KR; ++k)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) dbs[k][q][v] = 0.f;
   // step tt's operands except c_tt (carried): 16-B buffer loads, rows past B read zeros (offsets
   // beyond the slice's range), as do absent operands (zero-size ranges)
   auto ld4 = [](__amdgpu_buffer_rsrc_t rs, long off_elems) {
@@ -653,6 +661,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
           const bf16_t e = to_bf(dd[q]);
           gts[(q * BF_U + u4 + v) * LDT + b] = e;
           pk[q][v >> 1] |= (unsigned)e << (16 * (v & 1));
+          dbs[k][q][v] += __uint_as_float((unsigned)e << 16);
         }
       }
 #pragma unroll
@@ -706,6 +715,36 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
       }
     }
   }
+  // bias gradients: this tile's column sums (rows in order 0..BM-1), one partial per row block;
+  // sv_persist_db_finalize adds the row blocks in order
+  if (dbp) {
+    __syncthreads();
+    float* dsum = red;  // [BM][4 * BF_U] fp32 (fits in the red region)
+#pragma unroll
+    for (int k = 0; k < KR; ++k)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<float4*>(dsum + (brow + 32 * k) * (4 * BF_U) + q * BF_U + u4) =
+            float4{dbs[k][q][0], dbs[k][q][1], dbs[k][q][2], dbs[k][q][3]};
+    __syncthreads();
+    if (tid < 4 * BF_U) {
+      const int q = tid / BF_U, gj = j0 + tid % BF_U;
+      float sum = 0.f;
+      for (int b = 0; b < BM; ++b) sum += dsum[b * (4 * BF_U) + tid];
+      if (gj < H) dbp[(long)rb * G + (long)q * H + gj] = sum;
+    }
+  }
+}
+
+// db_ih = db_hh = sum over row blocks (in order) of the persistent backward's partials [nrb][G]
+__global__ void persist_db_finalize_kernel(const float* __restrict__ dbp, int nrb, int G, float* __restrict__ db_ih,
+                                           float* __restrict__ db_hh) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= G) return;
+  float s = 0.f;
+  for (int r = 0; r < nrb; ++r) s += dbp[(long)r * G + c];
+  db_ih[c] = s;
+  if (db_hh) db_hh[c] = s;
 }
 
 // ============================================================================
@@ -850,15 +889,15 @@ int pbwd_debug() {
 template <int NS, int P>
 void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const float* acts, const float* c_tm,
                  const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B,
-                 int H, unsigned* cnt) {
+                 int H, unsigned* cnt, float* dbp) {
   if (bm == 32)
     hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P, 32>), dim3(grid.x * grid.y), dim3(256), pbwd_lds(32), s,
                        whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x,
-                       persist_xcd(), pbwd_debug());
+                       persist_xcd(), pbwd_debug(), dbp);
   else
     hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P, 64>), dim3(grid.x * grid.y), dim3(256), pbwd_lds(64), s,
                        whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x,
-                       persist_xcd(), pbwd_debug());
+                       persist_xcd(), pbwd_debug(), dbp);
 }
 }  // namespace
 
@@ -870,7 +909,8 @@ extern "C" int sv_persist_bwd_ok(int B, int H) {
 // fragment-order hand-off scratch of the persistent backward (bytes; T slots of nrb*BM x 4H
 // bf16; the 64-row count bounds the 32-row one)
 extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H) {
-  return (size_t)T * (size_t)((B + BF_BM - 1) / BF_BM) * BF_BM * 4 * H * sizeof(bf16_t);
+  const size_t frag = (size_t)T * (size_t)((B + BF_BM - 1) / BF_BM) * BF_BM * 4 * H * sizeof(bf16_t);
+  return frag + (size_t)((B + 31) / 32) * 4 * H * sizeof(float);  // + bias-gradient partials
 }
 
 // one layer's backward recurrence for all t (reverse), on `stream`: dG (bf16, row-major and
@@ -878,7 +918,8 @@ extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H) {
 // else [B,H] at t = T-1 only, or NULL).  dgT: [4H][T*Bp] (padding columns written as zeros).
 // dgf: sv_persist_bwd_scratch(T, B, H) bytes.
 int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* acts, const float* c_tm,
-                        const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream) {
+                        const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream,
+                        float* db_ih, float* db_hh) {
   if (!sv_persist_bwd_ok(B, H)) return SV_ESHAPE;
   if (!dgf || ((uintptr_t)dgf & 15)) return SV_EARG;
   unsigned* cnt = pcnt_ptr();
@@ -887,15 +928,27 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* ac
   const long lddgT = (long)T * Bp;
   const int bm = persist_bm(B, H);
   const dim3 grid((H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
+  // bias-gradient partials [nrb][4H] after the fragment-order slots (db_ih NULL: not computed)
+  float* dbp = db_ih ? reinterpret_cast<float*>(reinterpret_cast<char*>(dgf) +
+                                                (size_t)T * ((B + BF_BM - 1) / BF_BM) * BF_BM * 4 * H * sizeof(bf16_t))
+                     : nullptr;
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)grid.y * SV_PCNT_STRIDE * sizeof(unsigned), stream);
   if (e != hipSuccess) return (int)e;
   // A-fragment prefetch depth 8 at H = 768 (measured: 4 / 16 no better)
   if (H == 768)
-    launch_pbwd<48, 8>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt);
+    launch_pbwd<48, 8>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt,
+                          dbp);
   else if (H == 96)
-    launch_pbwd<6, 4>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt);
+    launch_pbwd<6, 4>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt,
+                          dbp);
   else
-    launch_pbwd<4, 4>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt);
+    launch_pbwd<4, 4>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt,
+                          dbp);
   SV_LAUNCH_CHECK();
+  if (dbp) {
+    hipLaunchKernelGGL(persist_db_finalize_kernel, dim3((4 * H + 255) / 256), dim3(256), 0, stream, dbp, (int)grid.y,
+                       4 * H, db_ih, db_hh);
+    SV_LAUNCH_CHECK();
+  }
   return SV_OK;
 }

@@ -42,6 +42,8 @@ def main(out, dims, N, M, T, precision):
     res["loss"] = tr.step(x, N, M).reshape(1)
     res["flat_p"] = tr.flat_p
     res["flat_g"] = tr.flat_g
+    for name, prm in net.named_parameters():
+        res["grad_" + name] = prm.grad
     torch.cuda.synchronize()
     res = {k: v.detach().float().cpu().numpy() for k, v in res.items()}
     res["status"] = np.array([lib().sv_persist_status()])
