@@ -642,6 +642,42 @@ extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, cons
   return SV_OK;
 }
 
+// dx = dG . W_ih with dG read from the persistent backward's fragment-order hand-off buffer
+// (no row-major dG copy): M = T * B rows (t, b), K = 4H; needs B % 32, M % 256, N % 256, H % 64
+bool gemm_afrag_ok(int T, int B, int N, int H) {
+  static int on = [] {
+    const char* e = getenv("SV_DX_AFRAG");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on && gemm256_ok(T * B, N, 4 * H) && B % 32 == 0 && H % G256_BK == 0;
+}
+// (the split-K plan of sv_gemm_bf16 for the same shape, so both forms sum in the same order)
+int gemm_bf16_afrag(int T, int B, int H, int N, const bf16_t* dgf, int bm, const bf16_t* Bop, long ldb, float* C,
+                    long ldc, float* workspace, hipStream_t stream) {
+  const int M = T * B, K = 4 * H;
+  const int tiles = (M / G256_BM) * (N / G256_BM);
+  const long fs = (long)((B + bm - 1) / bm) * bm * 4 * H;
+  const G256AFrag af{dgf, fs, B, bm, H};
+  const BPlan p = plan_bf16(M, N, K);
+  if (p.splitk == 1) {
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_STORE, 1>), dim3(tiles, 1), dim3(512), G256_LDS, stream,
+                       (const bf16_t*)nullptr, 0L, Bop, ldb, C, ldc, 0L, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
+    SV_LAUNCH_CHECK();
+    return SV_OK;
+  }
+  if (!workspace) return SV_EARG;
+  const long slab = (long)M * N;
+  hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_SLAB, 1>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream,
+                     (const bf16_t*)nullptr, 0L, Bop, ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr,
+                     0.f, af);
+  SV_LAUNCH_CHECK();
+  const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
+  hipLaunchKernelGGL(slab_reduce_bf_kernel, dim3(grid), dim3(256), 0, stream, workspace, p.splitk, slab, C, ldc, M, N,
+                     0.f, nullptr, nullptr);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
 extern "C" int sv_cast_bf16(const float* x, bf16_t* y, long n, hipStream_t stream) {
   if (!x || !y || n <= 0) return SV_EARG;
   const int grid = (int)std::min<long>((n + 255) / 256, 8192);
@@ -922,12 +958,17 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       const float* up = l == L - 1 ? dh_last : dx[l + 1];
       bf16_t* dgf = (bf16_t*)((char*)workspace + per * L);
       const bool dbk = pbwd_db();  // bias gradients summed in the recurrence, else by rowsum over dG^T
-      if ((rc = sv_persist_bwd_bf16(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1, dg[l], dgT[l], dgf, main,
-                                    dbk ? db_ih[l] : nullptr, dbk && db_hh ? db_hh[l] : nullptr)))
+      const bool afr = l > 0 && gemm_afrag_ok(T, B, Fl, H);  // dx reads dgf: no row-major dG
+      if ((rc = sv_persist_bwd_bf16(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1, afr ? nullptr : dg[l],
+                                    dgT[l], dgf, main, dbk ? db_ih[l] : nullptr, dbk && db_hh ? db_hh[l] : nullptr)))
         return rc;
-      if (l > 0 && (rc = sv_gemm_bf16(T * B, Fl, 4 * H, dg[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr, nullptr,
-                                       0.f, ws.gws, main)))
+      if (afr) {
+        if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H), ws.wihT, 4L * H, dx[l], Fl, ws.gws, main)))
+          return rc;
+      } else if (l > 0 && (rc = sv_gemm_bf16(T * B, Fl, 4 * H, dg[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr,
+                                              nullptr, 0.f, ws.gws, main))) {
         return rc;
+      }
       if (sw != main) {
         if ((e = hipEventRecord(ev[l * nch], main)) != hipSuccess) return (int)e;
         if ((e = hipStreamWaitEvent(sw, ev[l * nch], 0)) != hipSuccess) return (int)e;

@@ -46,12 +46,25 @@ struct G256Stage {
 
 enum { G256_STORE = 0, G256_SLAB = 1 };
 
-template <int EPI>
+// A operand in the persistent backward's fragment-order hand-off layout (sv_persist.hip, dgf):
+// row m = t * bsl + b of A is (time slot t, batch row b); its 32-row group and 16-wide k-step s
+// of gate g form one contiguous KB [lane][8] at slot t, block ((b / bm) * 4 + g) * (bm / 32) +
+// (b / 32) % (bm / 32), k-step s.  A k-tile of 64 never crosses a gate (kg % 64 == 0), so a
+// 256 x 64 A tile is 8 row groups x 4 k-steps = 32 whole KB: one per wave instruction, copied
+// to LDS as is, and each lane's MFMA fragment is its own 16 B of one KB (conflict-free reads).
+struct G256AFrag {
+  const bf16_t* base;  // dgf
+  long fs;             // slot size (elements)
+  int bsl, bm, kg;     // batch rows per slot, row-block size of the layout, gate K (= H)
+};
+
+template <int EPI, int AF = 0>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16_t* __restrict__ A, long lda,
                                                               const bf16_t* __restrict__ B, long ldb,
                                                               float* __restrict__ C, long ldc, long slab, int M, int N,
                                                               int K, int kchunk, const float* __restrict__ bias0,
-                                                              const float* __restrict__ bias1, float beta) {
+                                                              const float* __restrict__ bias1, float beta,
+                                                              G256AFrag af = G256AFrag{}) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -63,9 +76,33 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16_t* __r
   const int nk = (min(K, kbeg + kchunk) - kbeg) / G256_BK;
   const int wr = w >> 2, wc = w & 3;  // wave's 128 x 64 output block: rows wr*128, cols wc*64
   G256Stage sa, sb;
-  sa.init(A, lda, tm * G256_BM, kbeg, tid);
+  if constexpr (!AF) sa.init(A, lda, tm * G256_BM, kbeg, tid);
   sb.init(B, ldb, tn * G256_BM, kbeg, tid);
   constexpr int OPB = G256_BM * G256_BK * 2;  // bytes per operand per stage
+  // fragment-order A (AF): wave w's instruction i copies KB c = 4 w + i = (row group c / 4,
+  // k-step c % 4) of the tile
+  long af_row[4];  // element offset of this lane's 16 B in row group c / 4 at gate 0, k-step 0
+  if constexpr (AF) {
+    const int KR = af.bm / 32, frag = af.kg / 16 * 512;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 4 * w + i, row = tm * G256_BM + 32 * (c >> 2);
+      const int t = row / af.bsl, b = row % af.bsl;
+      af_row[i] = (long)t * af.fs + (long)(((b / af.bm) * 4) * KR + (b / 32) % KR) * frag + (c & 3) * 512 + lane * 8;
+    }
+  }
+  auto issue_a = [&](char* lds, int kt) {
+    if constexpr (AF) {
+      const int k0 = kbeg + kt * G256_BK, g = k0 / af.kg, s0 = (k0 % af.kg) / 16;
+      const long goff = (long)g * (af.bm / 32) * (af.kg / 16 * 512) + (long)s0 * 512;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds((glb_vptr_t)(af.base + af_row[i] + goff),
+                                         (lds_vptr_t)(lds + (4 * w + i) * 1024), 16, 0, 0);
+    } else {
+      sa.issue(lds, kt, w);
+    }
+  };
   f32x16 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -74,7 +111,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16_t* __r
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
   if (nk > 0) {
-    sa.issue(smem, 0, w);
+    issue_a(smem, 0);
     sb.issue(smem + OPB, 0, w);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -83,7 +120,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16_t* __r
     char* cur = smem + (kt & 1) * 2 * OPB;
     if (kt + 1 < nk) {
       char* nxt = smem + ((kt + 1) & 1) * 2 * OPB;
-      sa.issue(nxt, kt + 1, w);
+      issue_a(nxt, kt + 1);
       sb.issue(nxt + OPB, kt + 1, w);
     }
     const char* As = cur;
@@ -93,8 +130,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16_t* __r
       bf16x8_t a[4], b[2];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int row = wr * 128 + 32 * i + r;
-        a[i] = *reinterpret_cast<const bf16x8_t*>(As + row * 128 + g256_phys_slot(row, 2 * s + hh) * 16);
+        if constexpr (AF) {
+          a[i] = *reinterpret_cast<const bf16x8_t*>(As + ((wr * 4 + i) * 4 + s) * 1024 + lane * 16);
+        } else {
+          const int row = wr * 128 + 32 * i + r;
+          a[i] = *reinterpret_cast<const bf16x8_t*>(As + row * 128 + g256_phys_slot(row, 2 * s + hh) * 16);
+        }
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {

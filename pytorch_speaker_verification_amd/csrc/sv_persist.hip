@@ -695,12 +695,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     if (dbg & 8) continue;
     // dG_t row-major (BM rows x 4 gates x 4 chunks of 8 units) and transposed (128 gate-unit
     // rows x BM/8 chunks of 8 batch columns; padding columns get zeros): 16-B plain stores
-    bf16_t* dgt = dg + (long)t * BG;
+    bf16_t* dgt = dg ? dg + (long)t * BG : nullptr;  // NULL: the dx GEMM reads dgf itself
 #pragma unroll
     for (int i = 0; i < BM / 16; ++i) {
       const int q = tid + 256 * i, row = q >> 4, gq = (q >> 2) & 3, c = q & 3;
       const int gb = b0 + row, gj = j0 + 8 * c;
-      if (gb < B && gj < H)
+      if (dgt && gb < B && gj < H)
         *reinterpret_cast<uint4*>(dgt + (long)gb * G + (long)gq * H + gj) =
             *reinterpret_cast<const uint4*>(dgs + row * LDG + gq * BF_U + 8 * c);
     }
@@ -900,6 +900,9 @@ void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const flo
                        persist_xcd(), pbwd_debug(), dbp);
 }
 }  // namespace
+
+// row tile the persistent kernels use for this batch (the dgf layout's row-block size)
+int sv_persist_bm(int B, int H) { return persist_bm(B, H); }
 
 // can the persistent backward recurrence run these dims (W_hh slice in registers: H in {64, 96, 768})?
 extern "C" int sv_persist_bwd_ok(int B, int H) {
