@@ -959,7 +959,8 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       bf16_t* dgf = (bf16_t*)((char*)workspace + per * L);
       const bool dbk = pbwd_db();  // bias gradients summed in the recurrence, else by rowsum over dG^T
       const bool afr = l > 0 && gemm_afrag_ok(T, B, Fl, H);  // dx reads dgf: no row-major dG
-      if ((rc = sv_persist_bwd_bf16(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1, afr ? nullptr : dg[l],
+      if ((rc = sv_persist_bwd_bf16(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1,
+                                    (afr || l == 0) ? nullptr : dg[l],  // layer 0 has no dx GEMM
                                     dgT[l], dgf, main, dbk ? db_ih[l] : nullptr, dbk && db_hh ? db_hh[l] : nullptr)))
         return rc;
       if (afr) {

@@ -29,6 +29,9 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 #define SV_PCNT_STRIDE 32    // one 128-B line per counter
 __device__ unsigned sv_pcnt[SV_PCNT_ROWS * SV_PCNT_STRIDE];
 __device__ unsigned sv_perr;
+// per-workgroup phase cycle counts of the persistent backward (profiling, SV_PBWD_DEBUG & 32)
+#define SV_NSTAMP 8
+__device__ unsigned long long sv_pstamp[1024 * SV_NSTAMP];
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t sv_rsrc(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
@@ -591,6 +594,17 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     }
   }
   load_ew(T - 1);
+  // phase stamps (dbg & 32): wait, GEMM + partial exchange, cell epilogue, hand-off + arrival,
+  // post-arrival issue
+  const bool stamp = dbg & 32;
+  unsigned long long ph[5] = {0, 0, 0, 0, 0}, tlast = stamp ? __builtin_amdgcn_s_memtime() : 0;
+  auto mark = [&](int i) {
+    if (stamp) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      ph[i] += now - tlast;
+      tlast = now;
+    }
+  };
   for (int t = T - 1; t >= 0; --t) {
     f32x16 acc0, acc1;
 #pragma unroll
@@ -598,6 +612,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     if (t < T - 1 && !(dbg & 4)) {
       if (tid == 0 && !(dbg & 1)) persist_wait(my_cnt, producers * (unsigned)(T - 1 - t));
       __syncthreads();
+      mark(0);
       // A fragments of dG_{t+1}: (row half m, k-step s) is the KB at ((rb 4 + g) 2 + m) FRAG + s 512
       const __amdgpu_buffer_rsrc_t ra = sv_rsrc(dgf + (long)(t + 1) * FS, (unsigned)(FS * 2));
       constexpr unsigned kstep = 1024u;
@@ -631,6 +646,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
       if constexpr (BM == 64) red[(g * BM + 32 + acc_row(i, lane)) * LDR + r] = acc1[i];
     }
     __syncthreads();
+    mark(1);
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       const int b = brow + 32 * k;
@@ -669,6 +685,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
       cv[k] = cpv[k];  // c_{t-1} is the next step's c_t
     }
     __syncthreads();
+    mark(2);
     // the hand-off: dG_t in fragment order, BM/4 KB per workgroup as contiguous KB pieces
     // (gate, row half, k-step), 16-B sc1 stores (dbg & 8, profiling only: no global stores)
     if (!(dbg & 8)) {
@@ -689,6 +706,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mark(3);
     // step t-1's elementwise operands, in flight during the stores below and the next hand-off
     // wait (dbg & 16, profiling only: skipped)
     if (t > 0 && !(dbg & 16)) load_ew(t - 1);
@@ -714,7 +732,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
               *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
       }
     }
+    mark(4);
   }
+  if (stamp && tid == 0 && blockIdx.x < 1024)
+    for (int i = 0; i < 5; ++i) sv_pstamp[blockIdx.x * SV_NSTAMP + i] = ph[i];
   // bias gradients: this tile's column sums (rows in order 0..BM-1), one partial per row block;
   // sv_persist_db_finalize adds the row blocks in order
   if (dbp) {
@@ -954,4 +975,11 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* ac
     SV_LAUNCH_CHECK();
   }
   return SV_OK;
+}
+
+// copy the persistent backward's phase stamps (SV_PBWD_DEBUG & 32) of the first n workgroups
+extern "C" int sv_persist_stamps(unsigned long long* out, int n) {
+  if (!out || n <= 0 || n > 1024) return SV_EARG;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(sv_pstamp), (size_t)n * SV_NSTAMP * sizeof(unsigned long long));
 }

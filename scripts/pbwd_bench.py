@@ -30,3 +30,14 @@ e1.record()
 e1.synchronize()
 print(json.dumps({"persist_bwd": os.environ.get("SV_PERSIST_BWD", "-"), "P": os.environ.get("SV_PBWD_P", "8"),
                   "bwd_ms": round(e0.elapsed_time(e1) / n, 3), "status": lib().sv_persist_status()}), flush=True)
+if int(os.environ.get("SV_PBWD_DEBUG", "0")) & 32:
+    import ctypes
+    import numpy as np
+    n = 240
+    buf = (ctypes.c_ulonglong * (n * 8))()
+    lib().sv_persist_stamps(buf, n)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 8)[:, :5].astype(np.float64)
+    names = ["wait", "gemm+exchange", "cell epilogue", "hand-off+arrive", "post-arrival issue"]
+    per = a.mean(0) / 159.0  # per step (the last layer's launch, T-1 = 159 GEMM steps)
+    print(json.dumps({"cycles_per_step": {k: round(v, 1) for k, v in zip(names, per)},
+                      "total": round(per.sum(), 1)}), flush=True)
