@@ -192,6 +192,10 @@ int sv_persist_fwd_ok(int B, int H);
 int sv_persist_bwd_ok(int B, int H);
 size_t sv_persist_bwd_scratch(int T, int B, int H);
 int sv_persist_status(void);
+/* profiling: per-phase cycle counts of the persistent backward's first n (<= 1024) workgroups, 8
+ * per workgroup (wait, GEMM + partial exchange, cell epilogue, hand-off + arrival, post-arrival
+ * issue, 3 unused), recorded when SV_PBWD_DEBUG has bit 32; synchronises the device */
+int sv_persist_stamps(unsigned long long* out, int n);
 
 /* ---- fp32 product mode of the fp32 path (process-wide; returns the previous mode):
  *   0 (default) exact fp32 MFMA products (v_mfma_f32_32x32x2_f32);
