@@ -74,6 +74,7 @@ SIGNATURES = {
     "sv_persist_bwd_ok": (_c_int, [_c_int, _c_int]),
     "sv_persist_bwd_scratch": (_c_size_t, [_c_int, _c_int, _c_int]),
     "sv_persist_status": (_c_int, []),
+    "sv_persist_stamps": (_c_int, [_P, _c_int]),
     "sv_clip_sgd_workspace": (_c_size_t, []),
     "sv_clip_sgd_step": (_c_int, [_P, _P, _c_long, _c_float, _c_float, _c_int, _P, _P, _P]),
 }
