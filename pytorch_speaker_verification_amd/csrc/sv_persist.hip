@@ -359,7 +359,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
       }
     }
   };
-  load_xg(0);
   for (int t = 0; t < T; ++t) {
     f32x16 acc0, acc1;
 #pragma unroll
@@ -385,6 +384,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
         }
       }
       __syncthreads();
+      // this step's x-projection, in flight behind the recurrent MFMAs (which read only LDS);
+      // loaded in the step that uses it, so it is no loop-carried register set (those were
+      // copied right after the loads, exposing the whole round trip)
+      load_xg(t);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s2 = 0; s2 < NS; ++s2) {
         const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(As + r * LDA + 16 * s2 + 8 * hh);
@@ -394,6 +398,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
           acc1 = mfma_bf16(a1, wreg[s2], acc1);
         }
       }
+    } else {
+      load_xg(0);
     }
     if constexpr (XF > 0) {  // pre-activation = recurrent part + (x_t W_ih^T + b_ih + b_hh)
       f32x16 x0, x1;
@@ -467,8 +473,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // off the critical chain: the next x-projection, then activations, c, h and hT of step t
-    if (t + 1 < T) load_xg(t + 1);
+    // off the critical chain: activations, c, h and hT of step t
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       const long gb = b0 + brow + 32 * k;
