@@ -511,9 +511,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
 // and are summed in gate order 0..3 (the per-step kernel's order, each gate accumulated over k
 // in one accumulator as there), so results are bit-identical to lstm_step_bwd_bf16_kernel.
 // dc * f (the cell-gradient carry) and c_{t-1} stay in registers; the elementwise operands of
-// step t load as 16-B vectors behind the first A fragments.  Only the hand-off stores precede
-// the arrival; dG_t row-major (the dx GEMM's operand) and transposed (dgT, the dW GEMMs')
-// are stored after it, off the critical chain.
+// step t-1 load as 16-B vectors right after step t's arrival.  Only the hand-off stores precede
+// the arrival; dG_t row-major (the dx GEMM's operand, skipped when the dx GEMM reads dgf) and
+// transposed (dgT, the dW GEMMs') are stored after it.
 //   acts [T,B,4H] activated gates, c_tm [T,B,H]; dhup: [T,B,H] (up_full) or [B,H] at t = T-1.
 // Hand-off: hand-off table row 1 of MI355X_MICROARCH.md, as the forward kernel above.
 // ============================================================================
