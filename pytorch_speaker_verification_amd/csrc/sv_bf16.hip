@@ -984,11 +984,16 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
                            db_hh ? db_hh[l] : nullptr);
         SV_LAUNCH_CHECK();
       }
-      if ((e = hipEventRecord(ev[L * nch + l], sw)) != hipSuccess) return (int)e;  // grad_ready of layer l
+      if (sw != main && (e = hipEventRecord(ev[L * nch + l], sw)) != hipSuccess) return (int)e;
     }
     if (pbwd_dw_side())
       for (int l = 0; l < L; ++l)
         if ((e = hipStreamWaitEvent(main, ev[L * nch + l], 0)) != hipSuccess) return (int)e;
+    // the per-layer completion events (grad_ready: a caller's bucketed all-reduce) all fire after
+    // the last recurrence, so collectives never share the device with a persistent launch (whose
+    // grid must be co-resident; a concurrent RCCL kernel would hold CUs it waits for)
+    for (int l = 0; l < L; ++l)
+      if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
     return SV_OK;
   }
   const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
