@@ -314,8 +314,6 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None):
     ws = _ws(lib().sv_proj_norm_workspace(B, H, P), dev)
     call("sv_proj_norm_bwd", ptr(demb), ptr(st.emb), ptr(st.ynorm), ptr(st.h_last), B, H, P, ptr(w_p),
          ptr(grads[4 * L]), ptr(grads[4 * L + 1]), ptr(dh_last), ptr(ws), s)
-    if grad_ready:
-        grad_ready(L, None)
     Fmax = max(st.x_tm[l].shape[2] for l in range(L))
     if PIPELINE_CHUNK > 0 and L > 1:
         F0 = st.x_tm[0].shape[2]
@@ -337,9 +335,14 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None):
              _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
              PIPELINE_CHUNK, s, sp, ep)
         if grad_ready:
+            # the projection bucket is enqueued behind the stack backward: with the persistent
+            # recurrences a collective must not run beside them (sv_lstm_stack_bwd_bf16)
+            grad_ready(L, None)
             for l in range(L - 1, -1, -1):
                 grad_ready(l, events[L * nch + l])
         return grads
+    if grad_ready:
+        grad_ready(L, None)
     ws = _ws(lib().sv_lstm_layer_bwd_bf16_workspace(T, B, Fmax, H), dev)
     dg = _bf((T, B, 4 * H), dev)
     dgT = _bf((4 * H, T * Bp), dev)
