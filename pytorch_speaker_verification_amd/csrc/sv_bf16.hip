@@ -399,6 +399,15 @@ bool gemm256_ok(int M, int N, int K) {
   return on && M % G256_BM == 0 && N % G256_BM == 0 && K % G256_BK == 0;
 }
 
+// SV_GEMM256P=1: the four-stage, three-in-flight variant of the 256 x 256 kernel (same results)
+bool gemm256p() {
+  static int on = [] {
+    const char* e = getenv("SV_GEMM256P");
+    return (e && *e == '1') ? 1 : 0;
+  }();
+  return on;
+}
+
 BPlan plan_bf16(int M, int N, int K) {
   BPlan p;
   if (gemm256_ok(M, N, K)) {  // one workgroup per CU: split K only to fill the 256 CUs
@@ -603,13 +612,21 @@ extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, cons
     const int tiles = (M / G256_BM) * (N / G256_BM);
     const long slab = (long)M * N;
     if (p.splitk == 1) {
-      hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_STORE>), dim3(tiles, 1), dim3(512), G256_LDS, stream, A, lda, B,
+      if (gemm256p())
+        hipLaunchKernelGGL((gemm_bf16_256p_kernel<G256_STORE>), dim3(tiles, 1), dim3(512), G256_LDS, stream, A, lda, B,
+                         ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1, beta);
+      else
+        hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_STORE>), dim3(tiles, 1), dim3(512), G256_LDS, stream, A, lda, B,
                          ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1, beta);
       SV_LAUNCH_CHECK();
       return SV_OK;
     }
     if (!workspace) return SV_EARG;
-    hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_SLAB>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream, A, lda,
+    if (gemm256p())
+      hipLaunchKernelGGL((gemm_bf16_256p_kernel<G256_SLAB>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream, A, lda,
+                       B, ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr, 0.f);
+    else
+      hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_SLAB>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream, A, lda,
                        B, ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr, 0.f);
     SV_LAUNCH_CHECK();
     const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
@@ -660,14 +677,23 @@ int gemm_bf16_afrag(int T, int B, int H, int N, const bf16_t* dgf, int bm, const
   const G256AFrag af{dgf, fs, B, bm, H};
   const BPlan p = plan_bf16(M, N, K);
   if (p.splitk == 1) {
-    hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_STORE, 1>), dim3(tiles, 1), dim3(512), G256_LDS, stream,
+    if (gemm256p())
+      hipLaunchKernelGGL((gemm_bf16_256p_kernel<G256_STORE, 1>), dim3(tiles, 1), dim3(512), G256_LDS, stream,
+                       (const bf16_t*)nullptr, 0L, Bop, ldb, C, ldc, 0L, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
+    else
+      hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_STORE, 1>), dim3(tiles, 1), dim3(512), G256_LDS, stream,
                        (const bf16_t*)nullptr, 0L, Bop, ldb, C, ldc, 0L, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
     SV_LAUNCH_CHECK();
     return SV_OK;
   }
   if (!workspace) return SV_EARG;
   const long slab = (long)M * N;
-  hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_SLAB, 1>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream,
+  if (gemm256p())
+    hipLaunchKernelGGL((gemm_bf16_256p_kernel<G256_SLAB, 1>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream,
+                     (const bf16_t*)nullptr, 0L, Bop, ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr,
+                     0.f, af);
+  else
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_SLAB, 1>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream,
                      (const bf16_t*)nullptr, 0L, Bop, ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr,
                      0.f, af);
   SV_LAUNCH_CHECK();

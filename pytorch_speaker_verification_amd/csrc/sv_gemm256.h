@@ -58,6 +58,38 @@ struct G256AFrag {
   int bsl, bm, kg;     // batch rows per slot, row-block size of the layout, gate K (= H)
 };
 
+// C tile store of a wave's 4 x 2 accumulators (bias / beta for G256_STORE, slab per k-split for
+// G256_SLAB)
+template <int EPI>
+__device__ __forceinline__ void g256_epilogue_impl(f32x16 (&acc)[4][2], float* C, long ldc, long slab, int tm, int tn,
+                                                   int wr, int wc, int lane, const float* bias0, const float* bias1,
+                                                   float beta) {
+  const int r = lane & 31;
+  float* Cz = C + (EPI == G256_SLAB ? (long)blockIdx.y * slab : 0);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = tn * G256_BM + wc * 64 + 32 * j + r;
+    float badd = 0.f;
+    if (EPI == G256_STORE) {
+      if (bias0) badd += bias0[col];
+      if (bias1) badd += bias1[col];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = tm * G256_BM + wr * 128 + 32 * i + acc_row(e, lane);
+        float* dst = Cz + (long)row * ldc + col;
+        float v = acc[i][j][e];
+        if (EPI == G256_STORE) {
+          v += badd;
+          if (beta != 0.f) v += beta * *dst;
+        }
+        *dst = v;
+      }
+  }
+}
+
 template <int EPI, int AF = 0>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16_t* __restrict__ A, long lda,
                                                               const bf16_t* __restrict__ B, long ldb,
@@ -151,27 +183,123 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16_t* __r
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  float* Cz = C + (EPI == G256_SLAB ? (long)blockIdx.y * slab : 0);
+  g256_epilogue_impl<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
+}
+
+// ---- deeper pipeline (SV_GEMM256P=1): k-tiles of 32 in four LDS stages, three in flight ----
+// Same tile, waves and MFMA order as gemm_bf16_256_kernel (so bit-identical results); the k-tile
+// is halved so four stages fit the same 128 KB, and tile kt + 3 is issued while tile kt is
+// computed.  The wait before each tile's barrier is a counted vmcnt (the two younger tiles stay
+// in flight across it) and the barrier is a raw s_barrier (a __syncthreads would drain every
+// outstanding LDS-DMA, cdna_hip_programming.md "Pipelining across barriers").  Row stride 64 B:
+// physical slot = slot ^ ((row >> 2) & 3) puts each ds_read_b128 lane group on 16 distinct slots.
+#define G256P_BK 32
+__device__ __forceinline__ int g256p_phys_slot(int row, int slot) { return slot ^ ((row >> 2) & 3); }
+
+template <int EPI, int AF = 0>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_256p_kernel(const bf16_t* __restrict__ A, long lda,
+                                                               const bf16_t* __restrict__ B, long ldb,
+                                                               float* __restrict__ C, long ldc, long slab, int M, int N,
+                                                               int K, int kchunk, const float* __restrict__ bias0,
+                                                               const float* __restrict__ bias1, float beta,
+                                                               G256AFrag af = G256AFrag{}) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int tiles_n = N / G256_BM;
+  const int nwg = tiles_n * (M / G256_BM);
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int tn = id % tiles_n, tm = id / tiles_n;
+  const int kbeg = blockIdx.y * kchunk;
+  const int nk = (min(K, kbeg + kchunk) - kbeg) / G256P_BK;
+  const int wr = w >> 2, wc = w & 3;
+  constexpr int OPB = G256_BM * G256P_BK * 2;  // 16 KB per operand per stage
+  constexpr int STG = 2 * OPB;
+  // per-thread 16-B chunks of a [256][32] operand tile: q = tid + 512 i -> row q >> 2, slot q & 3
+  const bf16_t* srcA[2];
+  const bf16_t* srcB[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = tn * G256_BM + wc * 64 + 32 * j + r;
-    float badd = 0.f;
-    if (EPI == G256_STORE) {
-      if (bias0) badd += bias0[col];
-      if (bias1) badd += bias1[col];
+  for (int i = 0; i < 2; ++i) {
+    const int q = tid + 512 * i, row = q >> 2, ls = g256p_phys_slot(row, q & 3);
+    if constexpr (!AF) srcA[i] = A + (long)(tm * G256_BM + row) * lda + kbeg + ls * 8;
+    srcB[i] = B + (long)(tn * G256_BM + row) * ldb + kbeg + ls * 8;
+  }
+  // fragment-order A: wave w's instruction i copies KB c = 2 w + i = (row group c / 2, k-step c % 2)
+  long af_row[2];
+  if constexpr (AF) {
+    const int KR = af.bm / 32, frag = af.kg / 16 * 512;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = 2 * w + i, row = tm * G256_BM + 32 * (c >> 1);
+      const int t = row / af.bsl, b = row % af.bsl;
+      af_row[i] = (long)t * af.fs + (long)(((b / af.bm) * 4) * KR + (b / 32) % KR) * frag + (c & 1) * 512 + lane * 8;
+    }
+  }
+  auto issue = [&](int kt) {
+    char* st = smem + (kt & 3) * STG;
+    if constexpr (AF) {
+      const int k0 = kbeg + kt * G256P_BK, g = k0 / af.kg, s0 = (k0 % af.kg) / 16;
+      const long goff = (long)g * (af.bm / 32) * (af.kg / 16 * 512) + (long)s0 * 512;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_global_load_lds((glb_vptr_t)(af.base + af_row[i] + goff),
+                                         (lds_vptr_t)(st + (2 * w + i) * 1024), 16, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_global_load_lds((glb_vptr_t)(srcA[i] + kt * G256P_BK),
+                                         (lds_vptr_t)(st + (w * 64 + 512 * i) * 16), 16, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((glb_vptr_t)(srcB[i] + kt * G256P_BK),
+                                       (lds_vptr_t)(st + OPB + (w * 64 + 512 * i) * 16), 16, 0, 0);
+  };
+  f32x16 acc[4][2];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = tm * G256_BM + wr * 128 + 32 * i + acc_row(e, lane);
-        float* dst = Cz + (long)row * ldc + col;
-        float v = acc[i][j][e];
-        if (EPI == G256_STORE) {
-          v += badd;
-          if (beta != 0.f) v += beta * *dst;
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+    if (p < nk) issue(p);
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt landed (this wave's 4 DMAs per tile; the younger tiles stay in flight), then every
+    // wave's: the barrier also ends every read of stage (kt + 3) & 3 = (kt - 1) & 3
+    const int ahead = min(nk - 1 - kt, 2);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 3 < nk) issue(kt + 3);
+    const char* As = smem + (kt & 3) * STG;
+    const char* Bs = As + OPB;
+#pragma unroll
+    for (int s = 0; s < G256P_BK / 16; ++s) {
+      bf16x8_t a[4], b[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (AF) {
+          a[i] = *reinterpret_cast<const bf16x8_t*>(As + ((wr * 4 + i) * 2 + s) * 1024 + lane * 16);
+        } else {
+          const int row = wr * 128 + 32 * i + r;
+          a[i] = *reinterpret_cast<const bf16x8_t*>(As + row * 64 + g256p_phys_slot(row, 2 * s + hh) * 16);
         }
-        *dst = v;
       }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wc * 64 + 32 * j + r;
+        b[j] = *reinterpret_cast<const bf16x8_t*>(Bs + row * 64 + g256p_phys_slot(row, 2 * s + hh) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf16(a[i], b[j], acc[i][j]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
+  g256_epilogue_impl<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
 }
