@@ -225,7 +225,7 @@ def f32_product_accuracy(dev, M=512, N=1024, K=768):
     for mode in ("mfma_f32", "bf16x6"):
         prev = set_f32_products(mode)
         C = torch.empty(M, N, device=dev)
-        call("sv_gemm_f32", 1, 1, M, N, K, ptr(At), K, ptr(Bt), K, ptr(C), N, None, None, 0.0, None, stream_of(C))
+        call("sv_gemm_f32", 1, 1, M, N, K, ptr(At), K, ptr(Bt), K, ptr(C), N, None, None, 0.0, None, 0, stream_of(C))
         err = np.abs(C.cpu().numpy().astype(np.float64) - ref) / scale
         out[mode] = {"max": float(err.max()), "mean": float(err.mean())}
         set_f32_products(prev)

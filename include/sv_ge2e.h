@@ -9,6 +9,8 @@
  *     aligned; scalars such as w, b, gloss are device pointers to one float (no host sync);
  *   - nothing is allocated, no global state is kept, no pointer is retained after return;
  *     scratch comes from a caller workspace of the size the matching *_workspace* returns;
+ *     modes are explicit arguments (`products`), cross-workgroup counters live in a caller
+ *     sync block (sv_sync_size), so calls with distinct buffers may run concurrently;
  *   - every launch goes to `stream` (pass the current stream of the tensor's device: the
  *     *_bwd functions are called from the autograd engine's worker thread);
  *   - return 0 on success, a hipError_t (> 0) from a failed launch, or a negative
@@ -24,8 +26,18 @@
 extern "C" {
 #endif
 
-#define SV_ABI_VERSION 1
+#define SV_ABI_VERSION 2
 int sv_abi_version(void);
+
+/* ---- fp32 product modes (`products` argument of sv_gemm_f32 / sv_lstm_stack_fwd / _bwd; every
+ * other fp32 entry point runs mode 0):
+ *   0 exact fp32 MFMA products (v_mfma_f32_32x32x2_f32);
+ *   1 "bf16x6": each fp32 operand split into three bf16 terms, six bf16 MFMA products per fp32
+ *     product, fp32 accumulation -- products carried to ~2^-25 relative, measured GEMM error vs
+ *     fp64 at or below the exact-MFMA path's (scripts/emu_check.py) -- on the NT GEMMs and K2;
+ *   2 / 3 diagnostics (split at LDS store / in registers everywhere). */
+#define SV_F32_EXACT 0
+#define SV_F32_BF16X6 1
 
 /* ---- dense fp32 MFMA GEMM (used by every op below; exported for tests) -----------------
  * C[M,N] = op(A) op(B) (+ bias0[n] + bias1[n]) (+ beta C).
@@ -34,7 +46,7 @@ int sv_abi_version(void);
 size_t sv_gemm_f32_workspace(int M, int N, int K);
 int sv_gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
                 float* C, long ldc, const float* bias0, const float* bias1, float beta, float* workspace,
-                hipStream_t stream);
+                int products, hipStream_t stream);
 
 /* column sums of X[R,C] (deterministic two-level reduction) */
 size_t sv_colsum_workspace(int R, int C);
@@ -70,7 +82,7 @@ int sv_lstm_step_bwd(const float* dg_next, const float* w_hhT, const float* dh_u
 int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float* x_tm, const float* const* w_ih,
                       const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                       float* const* gates, float* const* c_tm, float* const* h_tm, float* const* hT, int chunk,
-                      hipStream_t main, const hipStream_t* side, hipEvent_t* ev);
+                      hipStream_t main, const hipStream_t* side, hipEvent_t* ev, int products);
 size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H);
 /* Whole-stack backward, layer-pipelined over streams (top layer first): each layer's reverse
  * chunks of steps on side[l], then (l > 0) the chunk's dx = dG W_ih GEMM that feeds layer l-1;
@@ -85,7 +97,7 @@ int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float* const* xT,
                       const float* const* c_tm, const float* const* hT, const float* dh_last, float* const* dgates,
                       float* const* dgT, float* const* dx, float* const* dw_ih, float* const* dw_hh,
                       float* const* db_ih, float* const* db_hh, float* workspace, int chunk, hipStream_t main,
-                      const hipStream_t* side, hipEvent_t* ev);
+                      const hipStream_t* side, hipEvent_t* ev, int products);
 /* xT: the layer input transposed, [F, >= T*Bp] with row stride ld_xT (layer 0: the frames;
  * layer l > 0: hT of layer l-1 offset by Bp columns).  hT: this layer's [H, (T+1)Bp] from the fwd.
  * dh_up: gradient w.r.t. this layer's outputs; dh_up_full=1 -> [T,B,H], 0 -> [B,H] for t=T-1 only.
@@ -155,12 +167,13 @@ int sv_transpose_cast_bf16(const float* src, long ld_src, int R, int C, sv_bf16*
 int sv_lstm_layer_fwd_bf16(const sv_bf16* x_bf, int T, int B, int F, int H, const sv_bf16* w_ih_bf,
                            const sv_bf16* w_hh_bf, const float* b_ih, const float* b_hh, float* gates, float* c_tm,
                            float* h_tm, sv_bf16* h_bf, sv_bf16* hT, hipStream_t stream);
-/* layer-pipelined stack forward in bf16 (as sv_lstm_stack_fwd; h_bf per layer [T+1,B,H]) */
+/* layer-pipelined stack forward in bf16 (as sv_lstm_stack_fwd; h_bf per layer [T+1,B,H]).
+ * sync: the caller's sync block (below; required when the persistent recurrences run). */
 int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* x_bf, const sv_bf16* const* w_ih_bf,
                            const sv_bf16* const* w_hh_bf, const float* const* b_ih, const float* const* b_hh,
                            float* const* gates, float* const* c_tm, float* const* h_tm, sv_bf16* const* h_bf,
                            sv_bf16* const* hT, int chunk, hipStream_t main, const hipStream_t* side,
-                           hipEvent_t* ev);
+                           hipEvent_t* ev, void* sync);
 size_t sv_lstm_layer_bwd_bf16_workspace(int T, int B, int F, int H);
 /* wihT_bf [F,4H], whhT_bf [H,4H]; dg_bf [T,B,4H] and dgT_bf [4H,T*Bp] are bf16 outputs */
 int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const sv_bf16* xT_bf, long ld_xT, const sv_bf16* wihT_bf,
@@ -177,39 +190,35 @@ int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* con
                            const float* const* c_tm, const sv_bf16* const* hT, const float* dh_last,
                            sv_bf16* const* dg, sv_bf16* const* dgT, float* const* dx, float* const* dw_ih,
                            float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace, int chunk,
-                           hipStream_t main, const hipStream_t* side, hipEvent_t* ev);
+                           hipStream_t main, const hipStream_t* side, hipEvent_t* ev, void* sync);
 
 /* ---- persistent recurrences (one launch per layer for all T; sv_persist.hip).  The bf16 stack
- * forward uses them (by default when H = 768: W_hh held in registers) when sv_persist_fwd_ok(B, H)
- * (grid co-resident on this device); the bf16 stack backward likewise when sv_persist_bwd_ok(B, H)
- * (H in {64, 96, 768}; by default when H = 768), handing dG off through a fragment-order scratch
- * of sv_persist_bwd_scratch(T, B, H) bytes that sv_lstm_stack_bwd_bf16_workspace includes.  Their arrival counters are one device-global block: calls
- * that run persistent recurrences must not execute concurrently on one device (the stack
- * functions serialise them on their `main` stream).
- * sv_persist_status: 0 ok, 1 a hand-off wait timed out since the last call (device sync;
- * clears the flag). */
+ * forward uses them (by default when H = 768: W_hh held in registers) when the grid is
+ * co-resident on the device of `main` (sv_persist_fwd_ok answers for the current device); the
+ * bf16 stack backward likewise (H in {64, 96, 768}; by default when H = 768), handing dG off
+ * through a fragment-order scratch of sv_persist_bwd_scratch(T, B, H) bytes that
+ * sv_lstm_stack_bwd_bf16_workspace includes.
+ * Sync block: caller-owned device memory of sv_sync_size() bytes, zeroed once before first use;
+ * it holds the recurrences' arrival counters and, in its first u32 word, a STICKY status:
+ *   0 ok; bit 0 / bit 1 set = a forward / backward hand-off wait timed out (a co-residency
+ *   failure: another kernel or process held the CUs).  A timed-out launch drains instead of
+ *   hanging; every later wait on the same block returns at once; all outputs written since are
+ *   invalid.  The caller reads the word (async copy) and clears it.
+ * Calls that share one block must be ordered (one stream); distinct blocks may run concurrently.
+ * sv_status_poison: x[0..n) := NaN if the block's status is set (stream-ordered, no host sync). */
+size_t sv_sync_size(void);
 int sv_persist_fwd_ok(int B, int H);
 int sv_persist_bwd_ok(int B, int H);
 size_t sv_persist_bwd_scratch(int T, int B, int H);
-int sv_persist_status(void);
-/* profiling: per-phase cycle counts of the persistent backward's first n (<= 1024) workgroups, 8
- * per workgroup (wait, GEMM + partial exchange, cell epilogue, hand-off + arrival, post-arrival
- * issue, 3 unused), recorded when SV_PBWD_DEBUG has bit 32; synchronises the device */
-int sv_persist_stamps(unsigned long long* out, int n);
-
-/* ---- fp32 product mode of the fp32 path (process-wide; returns the previous mode):
- *   0 (default) exact fp32 MFMA products (v_mfma_f32_32x32x2_f32);
- *   1 "bf16x6": each fp32 operand split into three bf16 terms, six bf16 MFMA products per fp32
- *     product, fp32 accumulation -- products carried to ~2^-25 relative, measured GEMM error vs
- *     fp64 at or below the exact-MFMA path's (scripts/emu_check.py) -- on the NT GEMMs and K2;
- *   2 / 3 diagnostics (split at LDS store / in registers everywhere). */
-int sv_set_f32_products(int mode);
+int sv_status_poison(const void* sync, float* x, int n, hipStream_t stream);
 
 /* ---- clip_grad_norm_ + SGD step over one flat parameter group (train_speech_embedder.py:63-65)
- * p -= lr * min(1, max_norm / (|g|_2 + 1e-6)) * g; write_grad=1 also scales g in place. */
+ * p -= lr * min(1, max_norm / (|g|_2 + 1e-6)) * g; write_grad=1 also scales g in place.
+ * sync (may be NULL): a persistent-recurrence sync block; if its status is set the step is
+ * skipped (p and g untouched, total_norm_out = NaN): never a step on invalid gradients. */
 size_t sv_clip_sgd_workspace(void);
 int sv_clip_sgd_step(float* params, float* grads, long n, float max_norm, float lr, int write_grad,
-                     float* total_norm_out, float* workspace, hipStream_t stream);
+                     float* total_norm_out, const void* sync, float* workspace, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -26,7 +26,7 @@ SIGNATURES = {
     "sv_abi_version": (_c_int, []),
     "sv_gemm_f32_workspace": (_c_size_t, [_c_int, _c_int, _c_int]),
     "sv_gemm_f32": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _c_long, _P, _c_long, _P, _c_long, _P, _P,
-                             _c_float, _P, _P]),
+                             _c_float, _P, _c_int, _P]),
     "sv_colsum_workspace": (_c_size_t, [_c_int, _c_int]),
     "sv_colsum": (_c_int, [_P, _c_int, _c_int, _P, _P, _P]),
     "sv_frames_to_time_major": (_c_int, [_P, _P, _c_int, _c_int, _c_int, _P]),
@@ -35,9 +35,9 @@ SIGNATURES = {
     "sv_lstm_step_fwd": (_c_int, [_P, _P, _P, _P, _P, _P, _c_int, _c_int, _P]),
     "sv_lstm_step_bwd": (_c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _P]),
     "sv_lstm_stack_fwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                   _c_int, _P, _P, _P]),
+                                   _c_int, _P, _P, _P, _c_int]),
     "sv_lstm_stack_bwd_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int, _c_int]),
-    "sv_lstm_stack_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P]),
+    "sv_lstm_stack_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P, _c_int]),
     "sv_lstm_layer_bwd_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
     "sv_lstm_layer_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _P, _c_long, _P, _P, _P, _P, _P, _P, _c_int, _P,
                                    _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -62,21 +62,20 @@ SIGNATURES = {
     "sv_transpose_cast_bf16": (_c_int, [_P, _c_long, _c_int, _c_int, _P, _c_long, _P]),
     "sv_lstm_layer_fwd_bf16": (_c_int, [_P, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_lstm_stack_fwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                        _P, _c_int, _P, _P, _P]),
+                                        _P, _c_int, _P, _P, _P, _P]),
     "sv_lstm_layer_bwd_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
     "sv_lstm_layer_bwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _P, _c_long, _P, _P, _P, _P, _P, _P, _c_int,
                                         _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_eer_counts": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _c_int, _P, _P, _P]),
     "sv_lstm_stack_bwd_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int, _c_int]),
-    "sv_lstm_stack_bwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P]),
-    "sv_set_f32_products": (_c_int, [_c_int]),
+    "sv_lstm_stack_bwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P, _P]),
+    "sv_sync_size": (_c_size_t, []),
     "sv_persist_fwd_ok": (_c_int, [_c_int, _c_int]),
     "sv_persist_bwd_ok": (_c_int, [_c_int, _c_int]),
     "sv_persist_bwd_scratch": (_c_size_t, [_c_int, _c_int, _c_int]),
-    "sv_persist_status": (_c_int, []),
-    "sv_persist_stamps": (_c_int, [_P, _c_int]),
+    "sv_status_poison": (_c_int, [_P, _P, _c_int, _P]),
     "sv_clip_sgd_workspace": (_c_size_t, []),
-    "sv_clip_sgd_step": (_c_int, [_P, _P, _c_long, _c_float, _c_float, _c_int, _P, _P, _P]),
+    "sv_clip_sgd_step": (_c_int, [_P, _P, _c_long, _c_float, _c_float, _c_int, _P, _P, _P, _P]),
 }
 
 ERRORS = {-1: "invalid argument (SV_EARG)", -2: "misaligned pointer/leading dim (SV_EALIGN)",
@@ -126,6 +125,79 @@ def ptr(t):
 def stream_of(t):
     """hipStream_t of the current stream on the tensor's device."""
     return torch.cuda.current_stream(t.device).cuda_stream
+
+
+class PersistentRecurrenceError(RuntimeError):
+    """A persistent recurrence's hand-off wait timed out (its grid was not co-resident: another
+    kernel or process held CUs it needed).  Outputs since then are invalid; the trainer's
+    clip + SGD step skipped the update (include/sv_ge2e.h, sync block)."""
+
+
+# status word layout of the sync block (include/sv_ge2e.h; sv_bf16.h SV_SYNC_*)
+SYNC_STAMP_WORD = 32 + 4 * 64 * 32
+SYNC_NSTAMP = 8
+
+
+class PersistStatus:
+    """A caller-owned sync block for the persistent recurrences (sv_sync_size bytes, zeroed once)
+    plus a non-blocking check of its sticky status word: ``arm()`` after enqueueing work that
+    uses the block issues an async device->pinned copy of the word behind it; ``poll()`` raises
+    PersistentRecurrenceError for any completed copy that saw a nonzero status (``wait=True``
+    first waits for all of them)."""
+
+    def __init__(self, device):
+        words = (int(lib().sv_sync_size()) + 3) // 4
+        self.block = torch.zeros(words, dtype=torch.int32, device=device)
+        self._pending = []
+
+    def ptr(self):
+        return self.block.data_ptr()
+
+    def arm(self):
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        host.copy_(self.block[:1], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.block.device))
+        self._pending.append((ev, host))
+
+    def poll(self, wait=False):
+        keep = []
+        bad = 0
+        for ev, host in self._pending:
+            if wait:
+                ev.synchronize()
+            if ev.query():
+                bad |= int(host[0])
+            else:
+                keep.append((ev, host))
+        self._pending = keep
+        if bad:
+            which = " and ".join(n for b, n in ((1, "forward"), (2, "backward")) if bad & b)
+            raise PersistentRecurrenceError(
+                f"a persistent {which} recurrence timed out waiting for a hand-off (status {bad}): its grid was not "
+                "co-resident; the step's outputs are invalid and its parameter update was skipped")
+
+    def clear(self):
+        """Forget pending checks and zero the status word (stream-ordered)."""
+        self._pending = []
+        self.block[:1].zero_()
+
+    def stamps(self, n):
+        """Per-phase cycle stamps of the persistent backward's first n workgroups (SV_PBWD_DEBUG & 32)."""
+        st = self.block[SYNC_STAMP_WORD:SYNC_STAMP_WORD + 2 * SYNC_NSTAMP * n]
+        return st.view(torch.int64).view(n, SYNC_NSTAMP).cpu()
+
+
+def compute_device(t):
+    """The GPU a tensor's op runs on: its own device if it is on one, else (a CPU tensor, as in
+    the reference's CPU-resident evaluation, train_speech_embedder.py:100-102,120-121) the
+    current HIP device -- the data makes a round trip there and back; there is no CPU path."""
+    if t.is_cuda:
+        return t.device
+    if not torch.cuda.is_available():
+        raise RuntimeError("pytorch_speaker_verification_amd ops run on the GPU only (HIP kernels, no CPU "
+                           f"fallback) and no GPU is visible (got a {t.device} tensor)")
+    return torch.device("cuda", torch.cuda.current_device())
 
 
 def require_device(*tensors):

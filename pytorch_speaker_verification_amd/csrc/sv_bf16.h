@@ -245,16 +245,40 @@ __device__ __forceinline__ float lstm_cell_bwd(float dh, float i, float f, float
 #define BF_BM 64
 #define BF_U 32
 
-// persistent forward recurrence of one layer (sv_persist.hip)
+// Caller-owned synchronisation block of the persistent recurrences (sv_sync_size() bytes,
+// zeroed once by the caller; include/sv_ge2e.h).  u32 words:
+//   [0]                       sticky status: 0 ok, bit 0 / bit 1 = a forward / backward hand-off
+//                             wait timed out (every later wait on this block returns at once, so
+//                             the launch drains; outputs since then are invalid)
+//   [SV_SYNC_CNT ..)          arrival counters: SV_SYNC_CHANNELS channels x SV_PCNT_ROWS row
+//                             blocks x SV_PCNT_STRIDE words (one 128-B line per counter); each
+//                             launch zeroes the rows it uses of its channel
+//   [SV_SYNC_STAMP ..)        u64 phase stamps of the persistent backward (profiling)
+#define SV_PCNT_ROWS 64
+#define SV_PCNT_STRIDE 32
+#define SV_SYNC_CHANNELS 4
+#define SV_SYNC_CNT 32
+#define SV_NSTAMP 8
+#define SV_NSTAMP_WG 1024
+#define SV_SYNC_STAMP (SV_SYNC_CNT + SV_SYNC_CHANNELS * SV_PCNT_ROWS * SV_PCNT_STRIDE)
+#define SV_SYNC_WORDS (SV_SYNC_STAMP + 2 * SV_NSTAMP_WG * SV_NSTAMP)
+
+// persistent forward recurrence of one layer (sv_persist.hip); sync: the caller's block, chan: its
+// counter channel
 extern "C" int sv_persist_fwd_ok(int B, int H);
 int sv_persist_fwd_fusex_ok(int H, int F);
 int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates, float* c_tm, float* h_tm,
-                        bf16_t* h_bf, bf16_t* hT, hipStream_t stream, const bf16_t* x_bf = nullptr, int F = 0,
-                        const bf16_t* wih_bf = nullptr, const float* b_ih = nullptr, const float* b_hh = nullptr);
+                        bf16_t* h_bf, bf16_t* hT, hipStream_t stream, unsigned* sync, int chan = 0,
+                        const bf16_t* x_bf = nullptr, int F = 0, const bf16_t* wih_bf = nullptr,
+                        const float* b_ih = nullptr, const float* b_hh = nullptr);
 // persistent backward recurrence of one layer (sv_persist.hip)
 extern "C" int sv_persist_bwd_ok(int B, int H);
 extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H);
-int sv_persist_bm(int B, int H);
+int sv_persist_bm(int B, int H, int cus);
 int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* acts, const float* c_tm,
                         const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream,
-                        float* db_ih = nullptr, float* db_hh = nullptr);
+                        unsigned* sync, float* db_ih = nullptr, float* db_hh = nullptr);
+// CUs of the device `stream` belongs to (cached per device); dims fit co-resident on `cus` CUs
+int sv_stream_cus(hipStream_t stream);
+int sv_persist_fwd_fits(int B, int H, int cus);
+int sv_persist_bwd_fits(int B, int H, int cus);

@@ -808,16 +808,18 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
                                       const float* const* b_ih, const float* const* b_hh, float* const* gates,
                                       float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
                                       bf16_t* const* hT, int chunk, hipStream_t main, const hipStream_t* side,
-                                      hipEvent_t* ev) {
+                                      hipEvent_t* ev, void* sync_block) {
   if (L <= 0 || !x_bf || !w_ih_bf || !w_hh_bf || !gates || !c_tm || !h_tm || !h_bf || !side || !ev || chunk <= 0)
     return SV_EARG;
+  unsigned* sync = reinterpret_cast<unsigned*>(sync_block);
   if (T <= 0 || B <= 0 || F <= 0 || H <= 0 || F % 8 || H % 8) return SV_ESHAPE;
   const int nch = (T + chunk - 1) / chunk;
   const long BH = (long)B * H, BG = 4L * B * H;
   const int Bp = (B + 7) & ~7;
   const long ldhT = (long)(T + 1) * Bp;
   hipError_t e;
-  if (persist_fwd(H) && sv_persist_fwd_ok(B, H)) {
+  if (persist_fwd(H) && sv_persist_fwd_fits(B, H, sv_stream_cus(main))) {
+    if (!sync) return SV_EARG;
     // persistent schedule on `main`: per layer the whole-T K1 GEMM, then one launch for the
     // recurrence (sv_persist.hip); layers run one after another
     for (int l = 0; l < L; ++l) {
@@ -829,15 +831,15 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
       const bf16_t* in = l == 0 ? x_bf : h_bf[l - 1] + BH;
       int rc;
       if (l == 0 && sv_persist_fwd_fusex_ok(H, F)) {  // layer 0's input projection inside the recurrence
-        if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, x_bf, F,
-                                      w_ih_bf[l], b_ih[l], b_hh[l])))
+        if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, sync, 0,
+                                      x_bf, F, w_ih_bf[l], b_ih[l], b_hh[l])))
           return rc;
         continue;
       }
       rc = sv_gemm_bf16(T * B, 4 * H, Fl, in, Fl, w_ih_bf[l], Fl, gates[l], 4L * H, b_ih[l], b_hh[l], 0.f, nullptr,
                         main);
       if (rc) return rc;
-      if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main)))
+      if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, sync)))
         return rc;
     }
     return SV_OK;
@@ -948,7 +950,7 @@ BBwdWs carve_bbwd(char* base, int T, int B, int F, int H) {
 // whose recurrences run one after another)
 extern "C" size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H) {
   const size_t per = (size_t)L * carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
-  return per + (sv_persist_bwd_ok(B, H) ? sv_persist_bwd_scratch(T, B, H) : 0);
+  return per + (sv_persist_bwd_fits(B, H, 1 << 30) ? sv_persist_bwd_scratch(T, B, H) : 0);
 }
 
 extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const bf16_t* const* xT, const long* ld_xT,
@@ -956,10 +958,12 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
                                       const float* const* c_tm, const bf16_t* const* hT, const float* dh_last,
                                       bf16_t* const* dg, bf16_t* const* dgT, float* const* dx, float* const* dw_ih,
                                       float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace,
-                                      int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev) {
+                                      int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev,
+                                      void* sync_block) {
   if (L <= 0 || !xT || !ld_xT || !w_ih || !w_hh || !gates || !c_tm || !hT || !dh_last || !dg || !dgT || !dx ||
       !dw_ih || !dw_hh || !db_ih || !workspace || !side || !ev || chunk <= 0)
     return SV_EARG;
+  unsigned* sync = reinterpret_cast<unsigned*>(sync_block);
   if (T <= 0 || B <= 0 || F <= 0 || H <= 0 || F % 8 || H % 8) return SV_ESHAPE;
   const int nch = (T + chunk - 1) / chunk;
   const long BH = (long)B * H, BG = 4L * B * H;
@@ -970,7 +974,8 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
   hipEvent_t ev_start = ev[L * nch + L];
   hipError_t e = hipEventRecord(ev_start, main);
   if (e != hipSuccess) return (int)e;
-  if (persist_bwd(H) && sv_persist_bwd_ok(B, H)) {
+  if (persist_bwd(H) && sv_persist_bwd_fits(B, H, sv_stream_cus(main))) {
+    if (!sync) return SV_EARG;
     // persistent schedule: per layer (top first) the whole-T recurrence in one launch
     // (sv_persist.hip) and the whole-T dx GEMM on `main`; the layer's weight gradients on its
     // weight-gradient stream (SV_PBWD_DW_SIDE=0: on `main` after the dx GEMM)
@@ -987,10 +992,11 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       const bool afr = l > 0 && gemm_afrag_ok(T, B, Fl, H);  // dx reads dgf: no row-major dG
       if ((rc = sv_persist_bwd_bf16(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1,
                                     (afr || l == 0) ? nullptr : dg[l],  // layer 0 has no dx GEMM
-                                    dgT[l], dgf, main, dbk ? db_ih[l] : nullptr, dbk && db_hh ? db_hh[l] : nullptr)))
+                                    dgT[l], dgf, main, sync, dbk ? db_ih[l] : nullptr,
+                                    dbk && db_hh ? db_hh[l] : nullptr)))
         return rc;
       if (afr) {
-        if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H), ws.wihT, 4L * H, dx[l], Fl, ws.gws, main)))
+        if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H, sv_stream_cus(main)), ws.wihT, 4L * H, dx[l], Fl, ws.gws, main)))
           return rc;
       } else if (l > 0 && (rc = sv_gemm_bf16(T * B, Fl, 4 * H, dg[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr,
                                               nullptr, 0.f, ws.gws, main))) {

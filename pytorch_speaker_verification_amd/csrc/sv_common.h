@@ -17,6 +17,17 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 #define SV_EALIGN -2
 #define SV_ESHAPE -3
 
+// fp32 GEMM of the C ABI's sv_gemm_f32 (include/sv_ge2e.h) under the calling thread's current
+// product mode; F32ProductScope sets that mode for one entry point's duration
+int gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
+             float* C, long ldc, const float* bias0, const float* bias1, float beta, float* workspace,
+             hipStream_t stream);
+struct F32ProductScope {
+  int prev;
+  explicit F32ProductScope(int mode);
+  ~F32ProductScope();
+};
+
 // stack-backward schedule switch (sv_lstm.hip; env SV_DW_CHUNKED)
 int dw_chunked_layer(int l);
 int dx_side();

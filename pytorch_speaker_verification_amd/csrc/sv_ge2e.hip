@@ -352,7 +352,7 @@ extern "C" int sv_ge2e_fwd_rows(const float* E, int N_local, int M, int D, int s
                      ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd);
   SV_LAUNCH_CHECK();
   // cos = E^ C^T  (fp32 MFMA; rows of E^ and C^ are both D-contiguous)
-  int rc = sv_gemm_f32(1, 1, Bl, Np, D, ws.Ehat, D, ws.Chat, D, ws.cos, Np, nullptr, nullptr, 0.f, ws.gemm, stream);
+  int rc = gemm_f32(1, 1, Bl, Np, D, ws.Ehat, D, ws.Chat, D, ws.cos, Np, nullptr, nullptr, 0.f, ws.gemm, stream);
   if (rc) return rc;
   hipLaunchKernelGGL(ge2e_rowloss_kernel, dim3((Bl + 3) / 4), dim3(256), 0, stream, ws.cos, ws.rawd, Bl, M, N, Np,
                      spk_offset, w, b, per, ws.logz);
@@ -384,10 +384,10 @@ extern "C" int sv_ge2e_bwd_rows(int N_local, int M, int D, int spk_offset, int N
                      spk_offset, w, b, gloss, ws.dcos, ws.alpha, ws.dwdb_rows);
   SV_LAUNCH_CHECK();
   // G1 = dcos_off C^   ([Bl, N] x [N, D]; C^ read as [K=N][D] row-contiguous)
-  int rc = sv_gemm_f32(1, 0, Bl, D, Np, ws.dcos, Np, ws.Chat, D, ws.G1, D, nullptr, nullptr, 0.f, ws.gemm, stream);
+  int rc = gemm_f32(1, 0, Bl, D, Np, ws.dcos, Np, ws.Chat, D, ws.G1, D, nullptr, nullptr, 0.f, ws.gemm, stream);
   if (rc) return rc;
   // dChat (before the norm Jacobian) = dcos_off^T E^   ([Np, Bl] x [Bl, D]); rows >= N are zero
-  rc = sv_gemm_f32(0, 0, Np, D, Bl, ws.dcos, Np, ws.Ehat, D, dchat_partial, D, nullptr, nullptr, 0.f, ws.gemm, stream);
+  rc = gemm_f32(0, 0, Np, D, Bl, ws.dcos, Np, ws.Ehat, D, dchat_partial, D, nullptr, nullptr, 0.f, ws.gemm, stream);
   if (rc) return rc;
   const int nchunk = (Bl + 63) / 64;
   hipLaunchKernelGGL(ge2e_beta_partial_kernel, dim3((N + 63) / 64, nchunk), dim3(256), 0, stream, ws.dcos, ws.cos, Bl,
@@ -495,7 +495,7 @@ extern "C" int sv_ge2e_cossim(const float* E, int N, int M, int D, const float* 
   SV_LAUNCH_CHECK();
   hipLaunchKernelGGL(ge2e_centroid_kernel, dim3(Nc), dim3(256), 0, stream, C, Nc, 1, D, Chat, Cn);
   SV_LAUNCH_CHECK();
-  int rc = sv_gemm_f32(1, 1, Bl, Nc, D, Ehat, D, Chat, D, cos, Nc, nullptr, nullptr, 0.f, gws, stream);
+  int rc = gemm_f32(1, 1, Bl, Nc, D, Ehat, D, Chat, D, cos, Nc, nullptr, nullptr, 0.f, gws, stream);
   if (rc) return rc;
   hipLaunchKernelGGL(ge2e_cossim_fix_kernel, dim3((Bl + 3) / 4), dim3(256), 0, stream, cos, rawd, Bl, M, Nc);
   SV_LAUNCH_CHECK();

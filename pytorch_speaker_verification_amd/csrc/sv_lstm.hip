@@ -630,26 +630,24 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
 // ============================================================================
 namespace {
 
-// fp32 GEMM multiplies on the bf16 MFMA pipe via the bf16x6 split (sv_gemm.h); SV_F32_EMU=1
-// Process-wide fp32 product mode (sv_set_f32_products; initial value from SV_F32_EMU):
+// fp32 product mode of the calling thread's current entry point (the `products` argument of
+// sv_gemm_f32 / sv_lstm_stack_fwd / sv_lstm_stack_bwd, set for the duration of that call by
+// F32ProductScope; every other entry point runs exact):
 //   0  exact fp32 MFMA (v_mfma_f32_32x32x2_f32) everywhere -- the default
 //   1  bf16x6 split where it measured faster: NT GEMMs split in registers (x6), K2 split at the
 //      LDS store (x3), K3 exact
 //   2  x3 everywhere, 3  x6 everywhere (diagnostics)
-std::atomic<int> g_f32_mode{[] {
-  const char* e = getenv("SV_F32_EMU");
-  return (e && *e >= '0' && *e <= '3') ? *e - '0' : 0;
-}()};
+thread_local int t_f32_mode = 0;
 int gemm_x() {  // 0 exact, 1 x6, 2 x3
-  const int m = g_f32_mode.load(std::memory_order_relaxed);
+  const int m = t_f32_mode;
   return m == 1 || m == 3 ? 1 : m == 2 ? 2 : 0;
 }
 int k2_x() {
-  const int m = g_f32_mode.load(std::memory_order_relaxed);
+  const int m = t_f32_mode;
   return m == 1 || m == 2 ? 2 : m == 3 ? 1 : 0;
 }
 int k3_x() {
-  const int m = g_f32_mode.load(std::memory_order_relaxed);
+  const int m = t_f32_mode;
   return m == 2 ? 2 : m == 3 ? 1 : 0;
 }
 
@@ -776,11 +774,8 @@ GemmPlan plan_gemm(int M, int N, int K) {
 
 }  // namespace
 
-// fp32 product mode (see g_f32_mode): returns the previous mode, or SV_EARG for an unknown one
-extern "C" int sv_set_f32_products(int mode) {
-  if (mode < 0 || mode > 3) return SV_EARG;
-  return g_f32_mode.exchange(mode);
-}
+F32ProductScope::F32ProductScope(int mode) : prev(t_f32_mode) { t_f32_mode = mode; }
+F32ProductScope::~F32ProductScope() { t_f32_mode = prev; }
 
 extern "C" size_t sv_gemm_f32_workspace(int M, int N, int K) {
   const GemmPlan p = plan_gemm(M, N, K);
@@ -789,7 +784,15 @@ extern "C" size_t sv_gemm_f32_workspace(int M, int N, int K) {
 
 extern "C" int sv_gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, const float* A, long lda, const float* B,
                            long ldb, float* C, long ldc, const float* bias0, const float* bias1, float beta,
-                           float* workspace, hipStream_t stream) {
+                           float* workspace, int products, hipStream_t stream) {
+  if (products < 0 || products > 3) return SV_EARG;
+  F32ProductScope scope(products);
+  return gemm_f32(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C, ldc, bias0, bias1, beta, workspace, stream);
+}
+
+int gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
+             float* C, long ldc, const float* bias0, const float* bias1, float beta, float* workspace,
+             hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || !A || !B || !C) return SV_EARG;
   if (a_kcontig ? (K % 4 || lda % 4) : (M % 4 || lda % 4)) return SV_EALIGN;
   if (b_kcontig ? (K % 4 || ldb % 4) : (N % 4 || ldb % 4)) return SV_EALIGN;
@@ -1093,7 +1096,7 @@ extern "C" int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, 
   if (!lstm_dims_ok(T, B, F, H)) return SV_ESHAPE;
   const long BH = (long)B * H, BG = 4L * B * H;
   // K1: all-timestep input projection  gates = x W_ih^T + b_ih + b_hh
-  int rc = sv_gemm_f32(1, 1, T * B, 4 * H, F, x_tm, F, w_ih, F, gates, 4L * H, b_ih, b_hh, 0.f, nullptr, stream);
+  int rc = gemm_f32(1, 1, T * B, 4 * H, F, x_tm, F, w_ih, F, gates, 4L * H, b_ih, b_hh, 0.f, nullptr, stream);
   if (rc) return rc;
   hipError_t e = hipMemsetAsync(h_tm, 0, BH * sizeof(float), stream);
   if (e != hipSuccess) return (int)e;
@@ -1174,10 +1177,10 @@ extern "C" int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* xT, lo
   }
   const long ldhT = (long)(T + 1) * Bp;
   // dW_hh = sum_t dG_t^T h_{t-1}: A = dG^T [4H, T Bp], B = hT[:, 0:T Bp] (column block t = h_{t-1})
-  rc = sv_gemm_f32(1, 1, 4 * H, H, TBp, dgT, TBp, hT, ldhT, dw_hh, H, nullptr, nullptr, 0.f, ws.gws, stream);
+  rc = gemm_f32(1, 1, 4 * H, H, TBp, dgT, TBp, hT, ldhT, dw_hh, H, nullptr, nullptr, 0.f, ws.gws, stream);
   if (rc) return rc;
   // dW_ih = sum_t dG_t^T x_t: B = x^T [F, T Bp]
-  rc = sv_gemm_f32(1, 1, 4 * H, F, TBp, dgT, TBp, xT, ld_xT, dw_ih, F, nullptr, nullptr, 0.f, ws.gws, stream);
+  rc = gemm_f32(1, 1, 4 * H, F, TBp, dgT, TBp, xT, ld_xT, dw_ih, F, nullptr, nullptr, 0.f, ws.gws, stream);
   if (rc) return rc;
   // db_ih = db_hh = row sums of dG^T
   hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(256), 0, stream, dgT, (long)TBp, TBp, db_ih, db_hh);
@@ -1186,7 +1189,7 @@ extern "C" int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* xT, lo
   if (dx_tm) {
     rc = sv_transpose(w_ih, F, 4 * H, F, ws.wihT, 4L * H, stream);
     if (rc) return rc;
-    rc = sv_gemm_f32(1, 1, TB, F, 4 * H, dgates, 4L * H, ws.wihT, 4L * H, dx_tm, F, nullptr, nullptr, 0.f, ws.gws,
+    rc = gemm_f32(1, 1, TB, F, 4 * H, dgates, 4L * H, ws.wihT, 4L * H, dx_tm, F, nullptr, nullptr, 0.f, ws.gws,
                      stream);
     if (rc) return rc;
   }
@@ -1205,8 +1208,11 @@ extern "C" int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* xT, lo
 extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float* x_tm, const float* const* w_ih,
                                  const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                                  float* const* gates, float* const* c_tm, float* const* h_tm, float* const* hT,
-                                 int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev) {
+                                 int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev,
+                                 int products) {
   if (L <= 0 || !x_tm || !w_ih || !w_hh || !gates || !c_tm || !h_tm || !side || !ev || chunk <= 0) return SV_EARG;
+  if (products < 0 || products > 3) return SV_EARG;
+  F32ProductScope scope(products);
   if (!lstm_dims_ok(T, B, F, H)) return SV_ESHAPE;
   const int nch = (T + chunk - 1) / chunk;
   const long BH = (long)B * H, BG = 4L * B * H;
@@ -1233,7 +1239,7 @@ extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float*
       const int Fl = l == 0 ? F : H;
       const float* in = l == 0 ? x_tm + (long)t0 * B * F : h_tm[l - 1] + (long)(t0 + 1) * BH;
       if (l > 0 && (e = hipStreamWaitEvent(s, ev[(l - 1) * nch + cc], 0)) != hipSuccess) return (int)e;
-      int rc = sv_gemm_f32(1, 1, (t1 - t0) * B, 4 * H, Fl, in, Fl, w_ih[l], Fl, gates[l] + t0 * BG, 4L * H, b_ih[l],
+      int rc = gemm_f32(1, 1, (t1 - t0) * B, 4 * H, Fl, in, Fl, w_ih[l], Fl, gates[l] + t0 * BG, 4L * H, b_ih[l],
                            b_hh[l], 0.f, nullptr, s);
       if (rc) return rc;
       for (int t = t0; t < t1; ++t) {
@@ -1272,10 +1278,13 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
                                  const float* const* c_tm, const float* const* hT, const float* dh_last,
                                  float* const* dgates, float* const* dgT, float* const* dx, float* const* dw_ih,
                                  float* const* dw_hh, float* const* db_ih, float* const* db_hh, float* workspace,
-                                 int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev) {
+                                 int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev,
+                                 int products) {
   if (L <= 0 || !xT || !ld_xT || !w_ih || !w_hh || !gates || !c_tm || !hT || !dh_last || !dgates || !dgT || !dx ||
       !dw_ih || !dw_hh || !db_ih || !workspace || !side || !ev || chunk <= 0)
     return SV_EARG;
+  if (products < 0 || products > 3) return SV_EARG;
+  F32ProductScope scope(products);
   if (!lstm_dims_ok(T, B, F, H)) return SV_ESHAPE;
   const int nch = (T + chunk - 1) / chunk;
   const long BH = (long)B * H, BG = 4L * B * H;
@@ -1311,7 +1320,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
       if (l > 0 && dx_side()) {  // dx on the layer's second stream: the recurrence goes on at once
         if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
         if ((e = hipStreamWaitEvent(side[L + l], ev[l * nch + c], 0)) != hipSuccess) return (int)e;
-        rc = sv_gemm_f32(1, 1, (t1 - t0) * B, Fl, 4 * H, dgates[l] + t0 * BG, 4L * H, ws.wihT, 4L * H,
+        rc = gemm_f32(1, 1, (t1 - t0) * B, Fl, 4 * H, dgates[l] + t0 * BG, 4L * H, ws.wihT, 4L * H,
                          dx[l] + (long)t0 * B * Fl, Fl, nullptr, nullptr, 0.f, ws.gws2, side[L + l]);
         if (rc) return rc;
         // re-record: layer l-1 (issued after this loop) waits for the dx of this chunk
@@ -1320,7 +1329,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
         if (!dw_chunked_layer(l)) continue;
       } else {
         if (l > 0) {  // dh_up of layer l-1 for this chunk: dx = dG W_ih
-          rc = sv_gemm_f32(1, 1, (t1 - t0) * B, Fl, 4 * H, dgates[l] + t0 * BG, 4L * H, ws.wihT, 4L * H,
+          rc = gemm_f32(1, 1, (t1 - t0) * B, Fl, 4 * H, dgates[l] + t0 * BG, 4L * H, ws.wihT, 4L * H,
                            dx[l] + (long)t0 * B * Fl, Fl, nullptr, nullptr, 0.f, ws.gws, s);
           if (rc) return rc;
         }
@@ -1332,18 +1341,18 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
       if ((e = hipStreamWaitEvent(sw, ev[l * nch + c], 0)) != hipSuccess) return (int)e;
       const float beta = c == nch - 1 ? 0.f : 1.f;
       const int Kc = (t1 - t0) * Bp;
-      rc = sv_gemm_f32(1, 1, 4 * H, H, Kc, dgT[l] + (long)t0 * Bp, TBp, hT[l] + (long)t0 * Bp, ldhT, dw_hh[l], H,
+      rc = gemm_f32(1, 1, 4 * H, H, Kc, dgT[l] + (long)t0 * Bp, TBp, hT[l] + (long)t0 * Bp, ldhT, dw_hh[l], H,
                        nullptr, nullptr, beta, ws.gws2, sw);
       if (rc) return rc;
-      rc = sv_gemm_f32(1, 1, 4 * H, Fl, Kc, dgT[l] + (long)t0 * Bp, TBp, xT[l] + (long)t0 * Bp, ld_xT[l], dw_ih[l],
+      rc = gemm_f32(1, 1, 4 * H, Fl, Kc, dgT[l] + (long)t0 * Bp, TBp, xT[l] + (long)t0 * Bp, ld_xT[l], dw_ih[l],
                        Fl, nullptr, nullptr, beta, ws.gws2, sw);
       if (rc) return rc;
     }
     if (!dw_chunked_layer(l)) {  // whole-T weight GEMMs behind the recurrence, on its stream
       sw = s;
-      rc = sv_gemm_f32(1, 1, 4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws, s);
+      rc = gemm_f32(1, 1, 4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws, s);
       if (rc) return rc;
-      rc = sv_gemm_f32(1, 1, 4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f,
+      rc = gemm_f32(1, 1, 4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f,
                        ws.gws, s);
       if (rc) return rc;
     }

@@ -44,7 +44,7 @@ extern "C" size_t sv_proj_norm_workspace(int B, int H, int P) {
 extern "C" int sv_proj_norm_fwd(const float* h_last, int B, int H, int P, const float* w_p, const float* b_p, float* y,
                                 float* emb, float* ynorm, float* workspace, hipStream_t stream) {
   if (!h_last || !w_p || !y || !emb || !ynorm || B <= 0 || H <= 0 || P <= 0) return SV_EARG;
-  int rc = sv_gemm_f32(1, 1, B, P, H, h_last, H, w_p, H, y, P, b_p, nullptr, 0.f, workspace, stream);
+  int rc = gemm_f32(1, 1, B, P, H, h_last, H, w_p, H, y, P, b_p, nullptr, 0.f, workspace, stream);
   if (rc) return rc;
   hipLaunchKernelGGL(rownorm_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, y, B, P, emb, ynorm);
   SV_LAUNCH_CHECK();
@@ -60,12 +60,12 @@ extern "C" int sv_proj_norm_bwd(const float* demb, const float* emb, const float
   hipLaunchKernelGGL(rownorm_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, demb, emb, ynorm, B, P, dy);
   SV_LAUNCH_CHECK();
   // dWp [P,H] = dy^T h_last  (A = dy as [K=B][M=P], B = h_last as [K=B][N=H])
-  int rc = sv_gemm_f32(0, 0, P, H, B, dy, P, h_last, H, dw_p, H, nullptr, nullptr, 0.f, gws, stream);
+  int rc = gemm_f32(0, 0, P, H, B, dy, P, h_last, H, dw_p, H, nullptr, nullptr, 0.f, gws, stream);
   if (rc) return rc;
   rc = sv_colsum(dy, B, P, db_p, gws, stream);
   if (rc) return rc;
   // dh_last [B,H] = dy Wp  (A = dy [B, K=P] k-contig, B = Wp as [K=P][N=H])
-  return sv_gemm_f32(1, 0, B, H, P, dy, P, w_p, H, dh_last, H, nullptr, nullptr, 0.f, gws, stream);
+  return gemm_f32(1, 0, B, H, P, dy, P, w_p, H, dh_last, H, nullptr, nullptr, 0.f, gws, stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -91,9 +91,16 @@ __global__ __launch_bounds__(256) void sqsum_partial_kernel(const float* __restr
 
 // pass 2: every block re-reduces the partials (fixed order, fp64), computes
 // coef = min(1, max_norm / (|g| + 1e-6)) and updates p -= lr * coef * g (optionally g *= coef).
+// status (optional, a persistent-recurrence sync block's status word): nonzero -> the gradients
+// came from a timed-out recurrence: no update at all (parameters and gradients untouched).
 __global__ __launch_bounds__(256) void clip_sgd_kernel(float* __restrict__ p, float* __restrict__ g, long n,
                                                        const float* __restrict__ partial, int npart, float max_norm,
-                                                       float lr, int write_grad, float* __restrict__ norm_out) {
+                                                       float lr, int write_grad, float* __restrict__ norm_out,
+                                                       const unsigned* __restrict__ status) {
+  if (status && *status) {
+    if (norm_out && blockIdx.x == 0 && threadIdx.x == 0) norm_out[0] = __builtin_nanf("");
+    return;
+  }
   __shared__ double redd[4];
   __shared__ float coef_s;
   double s = 0.0;
@@ -128,14 +135,14 @@ __global__ __launch_bounds__(256) void clip_sgd_kernel(float* __restrict__ p, fl
 extern "C" size_t sv_clip_sgd_workspace(void) { return CLIP_BLOCKS * sizeof(float); }
 
 extern "C" int sv_clip_sgd_step(float* params, float* grads, long n, float max_norm, float lr, int write_grad,
-                                float* total_norm_out, float* workspace, hipStream_t stream) {
+                                float* total_norm_out, const void* sync, float* workspace, hipStream_t stream) {
   if (!params || !grads || !workspace || n <= 0) return SV_EARG;
   if (((uintptr_t)params | (uintptr_t)grads) & 15) return SV_EALIGN;
   const int blocks = (int)std::min<long>(CLIP_BLOCKS, (n / 4 + 255) / 256 + 1);
   hipLaunchKernelGGL(sqsum_partial_kernel, dim3(blocks), dim3(256), 0, stream, grads, n, workspace);
   SV_LAUNCH_CHECK();
   hipLaunchKernelGGL(clip_sgd_kernel, dim3(blocks), dim3(256), 0, stream, params, grads, n, workspace, blocks, max_norm,
-                     lr, write_grad, total_norm_out);
+                     lr, write_grad, total_norm_out, reinterpret_cast<const unsigned*>(sync));
   SV_LAUNCH_CHECK();
   return SV_OK;
 }

@@ -14,24 +14,22 @@
 // step, the workgroup barrier releases the other waves, and every load of h_bf is a
 // buffer_load_dwordx4 `sc1`.  Each h_bf slot is written once per launch (slot t+1 at step t).
 //
-// Residency: the grid must be co-resident (one 512-thread workgroup per CU at most), which the
-// host checks against the CU count; the spin is bounded (a timeout sets the status flag and
-// the kernel drains instead of hanging), and the recurrences of different layers never run
-// concurrently (the host serialises them on one stream).
+// Residency: the grid must be co-resident (one workgroup per CU at most), which the host checks
+// against the CU count of the stream's device; the spin is bounded: a timeout sets the sticky
+// status word of the caller's sync block (sv_sync_size, include/sv_ge2e.h) and every later wait
+// on that block returns at once, so the launch drains instead of hanging, and the caller sees
+// the status (the trainer raises and its clip + SGD kernel skips the update).  Counters and
+// status live in the caller's block, not in device globals: calls with different blocks may
+// run concurrently; launches sharing one block (the layers of a stack call) are serialised on
+// one stream.
 #include <algorithm>
+#include <atomic>
 #include <stdlib.h>
 #include "sv_bf16.h"
 #include "../../include/sv_ge2e.h"
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
-#define SV_PCNT_ROWS 64      // max row blocks per launch
-#define SV_PCNT_STRIDE 32    // one 128-B line per counter
-__device__ unsigned sv_pcnt[SV_PCNT_ROWS * SV_PCNT_STRIDE];
-__device__ unsigned sv_perr;
-// per-workgroup phase cycle counts of the persistent backward (profiling, SV_PBWD_DEBUG & 32)
-#define SV_NSTAMP 8
-__device__ unsigned long long sv_pstamp[1024 * SV_NSTAMP];
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t sv_rsrc(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
@@ -119,19 +117,24 @@ __device__ __forceinline__ void persist_tile(int xcd, int nub, int& ub, int& rb)
   rb = L / nub;
 }
 
-// lane 0 of the workgroup: wait until *c >= target (bounded; a timeout raises sv_perr and every
-// later wait returns at once, so a broken launch drains instead of hanging the GPU)
-__device__ __forceinline__ void persist_wait(unsigned* c, unsigned target) {
+// lane 0 of the workgroup: wait until *c >= target.  Bounded: after `limit` polls the wait sets
+// `code` in the sync block's status word and returns; once the status is nonzero every wait on
+// the block returns at once, so a broken launch drains instead of hanging the GPU.
+__device__ __forceinline__ void persist_wait(unsigned* c, unsigned target, unsigned* status, unsigned limit,
+                                             unsigned code) {
   unsigned spins = 0;
   while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    if (__hip_atomic_load(&sv_perr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     __builtin_amdgcn_s_sleep(2);
-    if (++spins > (1u << 21)) {
-      __hip_atomic_store(&sv_perr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (++spins > limit) {
+      __hip_atomic_fetch_or(status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
   }
 }
+// test-only fault injection (SV_PERSIST_FAULT=1, read by the host): workgroup 0 withholds its
+// first arrival, so its row block's consumers time out (short spin limit) and the status is set
+__device__ __forceinline__ bool persist_arrive_ok(int fault, int first) { return !(fault && first && blockIdx.x == 0); }
 
 // ============================================================================
 // bf16 forward recurrence of one layer, all T steps.  Tile (b0, j0): 64 batch rows x 32
@@ -147,6 +150,7 @@ __global__ __launch_bounds__(512) void lstm_persist_fwd_bf16_kernel(const bf16_t
                                                                     float* __restrict__ h_tm, bf16_t* h_bf,
                                                                     bf16_t* __restrict__ hT, long ldhT, int T,
                                                                     int Bp, int B, int H, unsigned* cnt,
+                                                                    unsigned* status, unsigned limit, int fault,
                                                                     int dbg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* ldsb = reinterpret_cast<bf16_t*>(smem);
@@ -178,7 +182,7 @@ __global__ __launch_bounds__(512) void lstm_persist_fwd_bf16_kernel(const bf16_t
     f32x16 acc[1][1];
     zero_acc(acc);
     if (t > 0 && !(dbg & 2)) {
-      if (tid == 0 && !(dbg & 1)) persist_wait(my_cnt, producers * (unsigned)t);
+      if (tid == 0 && !(dbg & 1)) persist_wait(my_cnt, producers * (unsigned)t, status, limit, 1u);
       __syncthreads();
       const __amdgpu_buffer_rsrc_t ra = sv_rsrc(h_bf + (long)t * BH, (unsigned)(BH * 2));
       persist_mainloop<BF_BM, BN, 512, D>(ra, b0, H, whh_bf, H, RowMapGates<BF_U>{j0, H}, H, ldsb, tid, wm0, wn0,
@@ -232,7 +236,8 @@ __global__ __launch_bounds__(512) void lstm_persist_fwd_bf16_kernel(const bf16_t
     // publish: every wave drains its stores, barrier, one lane arrives on the row block
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0 && persist_arrive_ok(fault, t == 0))
+      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -258,7 +263,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
                                                                        float* __restrict__ h_tm, bf16_t* h_bf,
                                                                        bf16_t* __restrict__ hT, long ldhT, int T,
                                                                        int Bp, int B, int H, unsigned* cnt, int nub,
-                                                                       int xcd, const bf16_t* __restrict__ x_bf,
+                                                                       int xcd, unsigned* status, unsigned limit,
+                                                                       int fault, const bf16_t* __restrict__ x_bf,
                                                                        const bf16_t* __restrict__ wih_bf,
                                                                        const float* __restrict__ b_ih,
                                                                        const float* __restrict__ b_hh) {
@@ -364,7 +370,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
     if (t > 0) {
-      if (tid == 0) persist_wait(my_cnt, producers * (unsigned)t);
+      if (tid == 0) persist_wait(my_cnt, producers * (unsigned)t, status, limit, 1u);
       __syncthreads();
       const __amdgpu_buffer_rsrc_t ra = sv_rsrc(h_bf + (long)t * BH, (unsigned)(BH * 2));
 #pragma unroll
@@ -472,7 +478,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
     // publish h_t: the hand-off stores drained, barrier, one lane arrives
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0 && persist_arrive_ok(fault, t == 0))
+      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // off the critical chain: activations, c, h and hT of step t
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
@@ -521,7 +528,8 @@ template <int NS, int P, int BM>
 __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     const bf16_t* __restrict__ whhT, const float* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
-    bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd, int dbg, float* __restrict__ dbp) {
+    bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit,
+    int fault, int dbg, float* __restrict__ dbp, unsigned long long* __restrict__ stamps) {
   constexpr int LDR = BF_U + 4;          // red [4][BM][LDR] fp32 (16-B aligned rows)
   constexpr int LDG = 4 * BF_U + 8;      // dgs [BM][LDG] bf16 (row-major dG tile)
   constexpr int LDT = BM + 8;            // gts [128][LDT] bf16 (transposed dG tile)
@@ -615,7 +623,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
     if (t < T - 1 && !(dbg & 4)) {
-      if (tid == 0 && !(dbg & 1)) persist_wait(my_cnt, producers * (unsigned)(T - 1 - t));
+      if (tid == 0 && !(dbg & 1)) persist_wait(my_cnt, producers * (unsigned)(T - 1 - t), status, limit, 2u);
       __syncthreads();
       mark(0);
       // A fragments of dG_{t+1}: (row half m, k-step s) is the KB at ((rb 4 + g) 2 + m) FRAG + s 512
@@ -710,7 +718,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     // publish dG_t: every store of the hand-off drained, barrier, one lane arrives
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
+      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     mark(3);
     // step t-1's elementwise operands, in flight during the stores below and the next hand-off
     // wait (dbg & 16, profiling only: skipped)
@@ -739,8 +748,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     }
     mark(4);
   }
-  if (stamp && tid == 0 && blockIdx.x < 1024)
-    for (int i = 0; i < 5; ++i) sv_pstamp[blockIdx.x * SV_NSTAMP + i] = ph[i];
+  if (stamp && tid == 0 && blockIdx.x < SV_NSTAMP_WG)
+    for (int i = 0; i < 5; ++i) stamps[blockIdx.x * SV_NSTAMP + i] = ph[i];
   // bias gradients: this tile's column sums (rows in order 0..BM-1), one partial per row block;
   // sv_persist_db_finalize adds the row blocks in order
   if (dbp) {
@@ -781,11 +790,19 @@ constexpr int PFWD_LDS_MAIN = 2 * (BF_BM + 4 * BF_U) * (BBK + 8) * 2;
 constexpr int PFWD_LDS_EPI = (BF_BM * (4 * BF_U + 4) + BF_U * (BF_BM + 1)) * 4;
 constexpr int PFWD_LDS = PFWD_LDS_MAIN > PFWD_LDS_EPI ? PFWD_LDS_MAIN : PFWD_LDS_EPI;
 
-int cu_count() {
-  int dev = 0, n = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
+// CU count per device, cached (device attributes do not change while the process runs)
+std::atomic<int> g_cus[64];
+int device_cus(int dev) {
+  if (dev < 0 || dev >= 64) return 0;
+  int n = g_cus[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
   if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  g_cus[dev].store(n, std::memory_order_relaxed);
   return n;
+}
+int current_cus() {
+  int dev = 0;
+  return hipGetDevice(&dev) == hipSuccess ? device_cus(dev) : 0;
 }
 // W_hh held in registers (lstm_persist2_fwd_bf16_kernel) when H = 768; SV_PERSIST_W=0 forces the
 // LDS-staged persistent kernel
@@ -804,38 +821,54 @@ int persist_wregs() {
   }();
   return v;
 }
-unsigned* pcnt_ptr() {
-  void* p = nullptr;
-  return hipGetSymbolAddress(&p, HIP_SYMBOL(sv_pcnt)) == hipSuccess ? (unsigned*)p : nullptr;
+// test-only fault injection: SV_PERSIST_FAULT=1 (every persistent launch) or =2 (backward
+// launches only) makes workgroup 0 withhold its first arrival and shortens the spin limit, so the
+// launch times out deterministically and quickly
+int persist_fault() {
+  static int v = [] {
+    const char* e = getenv("SV_PERSIST_FAULT");
+    return (e && (*e == '1' || *e == '2')) ? *e - '0' : 0;
+  }();
+  return v;
+}
+int fwd_fault() { return persist_fault() == 1; }
+// polls before a hand-off wait gives up (each poll = one L2 round trip + s_sleep 2: ~2^21 polls
+// is seconds, far beyond any legitimate wait)
+unsigned persist_limit() { return persist_fault() ? (1u << 12) : (1u << 21); }
+unsigned* sync_cnt(unsigned* sync, int chan) {
+  return sync + SV_SYNC_CNT + (size_t)chan * SV_PCNT_ROWS * SV_PCNT_STRIDE;
 }
 }  // namespace
 
-// can the persistent forward recurrence run these dims co-resident on this device?
-extern "C" int sv_persist_fwd_ok(int B, int H) {
-  const long grid = (long)((H + BF_U - 1) / BF_U) * ((B + BF_BM - 1) / BF_BM);
-  return H % 8 == 0 && (B + BF_BM - 1) / BF_BM <= SV_PCNT_ROWS && grid <= cu_count() && (long)B * H * 2 < (1L << 31);
+int sv_stream_cus(hipStream_t stream) {
+  int dev = -1;
+  if (stream && hipStreamGetDevice(stream, &dev) == hipSuccess) return device_cus(dev);
+  return current_cus();
 }
 
-// status of the persistent kernels since the last call (0 = ok, 1 = a hand-off wait timed out);
-// synchronises the device, clears the flag
-extern "C" int sv_persist_status(void) {
-  unsigned v = 0, z = 0;
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(sv_perr), sizeof(v)) != hipSuccess) return -1;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(sv_perr), &z, sizeof(z)) != hipSuccess) return -1;
-  return (int)v;
+extern "C" size_t sv_sync_size(void) { return (size_t)SV_SYNC_WORDS * sizeof(unsigned); }
+
+// can the persistent forward recurrence run these dims co-resident on a device of `cus` CUs?
+int sv_persist_fwd_fits(int B, int H, int cus) {
+  const long grid = (long)((H + BF_U - 1) / BF_U) * ((B + BF_BM - 1) / BF_BM);
+  return H % 8 == 0 && (B + BF_BM - 1) / BF_BM <= SV_PCNT_ROWS && grid <= cus && (long)B * H * 2 < (1L << 31);
 }
+int sv_persist_bwd_fits(int B, int H, int cus) {
+  return (H == 768 || H == 64 || H == 96) && sv_persist_fwd_fits(B, H, cus) && (long)B * 4 * H * 2 < (1L << 31);
+}
+// ... on the current device
+extern "C" int sv_persist_fwd_ok(int B, int H) { return sv_persist_fwd_fits(B, H, current_cus()); }
 
 namespace {
 // row tile of the W-stationary kernels: 32 rows when twice the 64-row grid still fits on the
 // device (B <= 320 at H = 768: c5's per-GPU batch), else 64; SV_PBM=64 forces 64
-int persist_bm(int B, int H) {
+int persist_bm(int B, int H, int cus) {
   static int force64 = [] {
     const char* e = getenv("SV_PBM");
     return (e && atoi(e) == 64) ? 1 : 0;
   }();
   const long grid32 = (long)((H + BF_U - 1) / BF_U) * ((B + 31) / 32);
-  return (!force64 && grid32 <= cu_count() && (B + 31) / 32 <= SV_PCNT_ROWS) ? 32 : 64;
+  return (!force64 && grid32 <= cus && (B + 31) / 32 <= SV_PCNT_ROWS) ? 32 : 64;
 }
 
 // SV_PFUSEX=0: layer 0 keeps its K1 GEMM instead of the in-kernel input projection
@@ -854,16 +887,18 @@ int sv_persist_fwd_fusex_ok(int H, int F) { return H == 768 && F == 40 && persis
 // one layer's recurrence (K2 for all t) after its K1 has filled `gates`; on `stream`.  With x_bf
 // (layer 0, sv_persist_fwd_fusex_ok): no K1 -- the kernel forms x_t W_ih^T + b_ih + b_hh itself.
 int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates, float* c_tm, float* h_tm,
-                        bf16_t* h_bf, bf16_t* hT, hipStream_t stream, const bf16_t* x_bf, int F,
-                        const bf16_t* wih_bf, const float* b_ih, const float* b_hh) {
-  if (!sv_persist_fwd_ok(B, H)) return SV_ESHAPE;
+                        bf16_t* h_bf, bf16_t* hT, hipStream_t stream, unsigned* sync, int chan, const bf16_t* x_bf,
+                        int F, const bf16_t* wih_bf, const float* b_ih, const float* b_hh) {
+  const int cus = sv_stream_cus(stream);
+  if (!sv_persist_fwd_fits(B, H, cus)) return SV_ESHAPE;
+  if (!sync || chan < 0 || chan >= SV_SYNC_CHANNELS) return SV_EARG;
   if (x_bf && (!wih_bf || !sv_persist_fwd_fusex_ok(H, F))) return SV_EARG;
-  unsigned* cnt = pcnt_ptr();
-  if (!cnt) return SV_EARG;
+  unsigned* cnt = sync_cnt(sync, chan);
+  unsigned* status = sync;
   const int Bp = (B + 7) & ~7;
   const long ldhT = (long)(T + 1) * Bp;
   const bool wst = H == 768 && persist_wregs();
-  const int bm = wst ? persist_bm(B, H) : BF_BM;
+  const int bm = wst ? persist_bm(B, H, cus) : BF_BM;
   const dim3 grid((H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)grid.y * SV_PCNT_STRIDE * sizeof(unsigned), stream);
   if (e != hipSuccess) return (int)e;
@@ -872,6 +907,8 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
     const char* v = getenv("SV_PERSIST_DEBUG");
     return v ? atoi(v) : 0;
   }();
+  const unsigned limit = persist_limit();
+  const int fault = fwd_fault();
   if (wst) {
     constexpr int NS = 48, LDA = NS * 16 + 8;
     const size_t lds = (size_t)bm * LDA * 2 + (size_t)bm * (4 * BF_U + 4) * 4 + (size_t)bm * (BF_U + 8) * 2 +
@@ -880,19 +917,23 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
     const int nub = (int)grid.x, xcd = persist_xcd();
     if (x_bf && bm == 32)
       hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 32, 5>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
-                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, x_bf, wih_bf, b_ih, b_hh);
+                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, x_bf, wih_bf, b_ih,
+                         b_hh);
     else if (x_bf)
       hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 64, 5>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
-                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, x_bf, wih_bf, b_ih, b_hh);
+                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, x_bf, wih_bf, b_ih,
+                         b_hh);
     else if (bm == 32)
       hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 32, 0>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
-                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, nullptr, nullptr, nullptr, nullptr);
+                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, nullptr, nullptr,
+                         nullptr, nullptr);
     else
       hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 64, 0>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
-                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, nullptr, nullptr, nullptr, nullptr);
+                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, nullptr, nullptr,
+                         nullptr, nullptr);
   } else {
     hipLaunchKernelGGL(lstm_persist_fwd_bf16_kernel<4>, grid, dim3(512), PFWD_LDS, stream, whh_bf, gates, c_tm, h_tm,
-                       h_bf, hT, ldhT, T, Bp, B, H, cnt, dbg);
+                       h_bf, hT, ldhT, T, Bp, B, H, cnt, status, limit, fault, dbg);
   }
   SV_LAUNCH_CHECK();
   return SV_OK;
@@ -904,7 +945,7 @@ constexpr size_t pbwd_lds(int bm) {
   return (size_t)4 * bm * (BF_U + 4) * 4 + (size_t)bm * (4 * BF_U + 8) * 2 + (size_t)4 * BF_U * (bm + 8) * 2;
 }
 // SV_PBWD_DEBUG (profiling only, results invalid): 1 = no hand-off waits, 4 = no recurrent GEMM, 8 = no global stores, 16 = no
-// elementwise operand loads after the first step
+// elementwise operand loads after the first step, 32 = per-phase cycle stamps into the sync block
 int pbwd_debug() {
   static int v = [] {
     const char* e = getenv("SV_PBWD_DEBUG");
@@ -915,25 +956,25 @@ int pbwd_debug() {
 template <int NS, int P>
 void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const float* acts, const float* c_tm,
                  const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B,
-                 int H, unsigned* cnt, float* dbp) {
+                 int H, unsigned* cnt, unsigned* sync, float* dbp) {
+  unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + SV_SYNC_STAMP);
   if (bm == 32)
     hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P, 32>), dim3(grid.x * grid.y), dim3(256), pbwd_lds(32), s,
                        whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x,
-                       persist_xcd(), pbwd_debug(), dbp);
+                       persist_xcd(), sync, persist_limit(), persist_fault(), pbwd_debug(), dbp, stamps);
   else
     hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P, 64>), dim3(grid.x * grid.y), dim3(256), pbwd_lds(64), s,
                        whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x,
-                       persist_xcd(), pbwd_debug(), dbp);
+                       persist_xcd(), sync, persist_limit(), persist_fault(), pbwd_debug(), dbp, stamps);
 }
 }  // namespace
 
-// row tile the persistent kernels use for this batch (the dgf layout's row-block size)
-int sv_persist_bm(int B, int H) { return persist_bm(B, H); }
+// row tile the persistent kernels use for this batch on a device of `cus` CUs (the dgf layout's
+// row-block size)
+int sv_persist_bm(int B, int H, int cus) { return persist_bm(B, H, cus); }
 
 // can the persistent backward recurrence run these dims (W_hh slice in registers: H in {64, 96, 768})?
-extern "C" int sv_persist_bwd_ok(int B, int H) {
-  return (H == 768 || H == 64 || H == 96) && sv_persist_fwd_ok(B, H) && (long)B * 4 * H * 2 < (1L << 31);
-}
+extern "C" int sv_persist_bwd_ok(int B, int H) { return sv_persist_bwd_fits(B, H, current_cus()); }
 
 // fragment-order hand-off scratch of the persistent backward (bytes; T slots of nrb*BM x 4H
 // bf16; the 64-row count bounds the 32-row one)
@@ -945,17 +986,17 @@ extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H) {
 // one layer's backward recurrence for all t (reverse), on `stream`: dG (bf16, row-major and
 // transposed) from the activations, cell states and the upstream dh (dhup [T,B,H] if up_full,
 // else [B,H] at t = T-1 only, or NULL).  dgT: [4H][T*Bp] (padding columns written as zeros).
-// dgf: sv_persist_bwd_scratch(T, B, H) bytes.
+// dgf: sv_persist_bwd_scratch(T, B, H) bytes.  Counter channel 0 of `sync`.
 int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* acts, const float* c_tm,
                         const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream,
-                        float* db_ih, float* db_hh) {
-  if (!sv_persist_bwd_ok(B, H)) return SV_ESHAPE;
-  if (!dgf || ((uintptr_t)dgf & 15)) return SV_EARG;
-  unsigned* cnt = pcnt_ptr();
-  if (!cnt) return SV_EARG;
+                        unsigned* sync, float* db_ih, float* db_hh) {
+  const int cus = sv_stream_cus(stream);
+  if (!sv_persist_bwd_fits(B, H, cus)) return SV_ESHAPE;
+  if (!dgf || ((uintptr_t)dgf & 15) || !sync) return SV_EARG;
+  unsigned* cnt = sync_cnt(sync, 0);
   const int Bp = (B + 7) & ~7;
   const long lddgT = (long)T * Bp;
-  const int bm = persist_bm(B, H);
+  const int bm = persist_bm(B, H, cus);
   const dim3 grid((H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
   // bias-gradient partials [nrb][4H] after the fragment-order slots (db_ih NULL: not computed)
   float* dbp = db_ih ? reinterpret_cast<float*>(reinterpret_cast<char*>(dgf) +
@@ -965,14 +1006,14 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* ac
   if (e != hipSuccess) return (int)e;
   // A-fragment prefetch depth 8 at H = 768 (measured: 4 / 16 no better)
   if (H == 768)
-    launch_pbwd<48, 8>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt,
-                          dbp);
+    launch_pbwd<48, 8>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, sync,
+                       dbp);
   else if (H == 96)
-    launch_pbwd<6, 4>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt,
-                          dbp);
+    launch_pbwd<6, 4>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, sync,
+                      dbp);
   else
-    launch_pbwd<4, 4>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt,
-                          dbp);
+    launch_pbwd<4, 4>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, sync,
+                      dbp);
   SV_LAUNCH_CHECK();
   if (dbp) {
     hipLaunchKernelGGL(persist_db_finalize_kernel, dim3((4 * H + 255) / 256), dim3(256), 0, stream, dbp, (int)grid.y,
@@ -982,9 +1023,16 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* ac
   return SV_OK;
 }
 
-// copy the persistent backward's phase stamps (SV_PBWD_DEBUG & 32) of the first n workgroups
-extern "C" int sv_persist_stamps(unsigned long long* out, int n) {
-  if (!out || n <= 0 || n > 1024) return SV_EARG;
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(sv_pstamp), (size_t)n * SV_NSTAMP * sizeof(unsigned long long));
+// (status guard) loss := NaN when the sync block's status is set: a training step whose
+// recurrences timed out reports a NaN loss instead of a finite wrong one
+__global__ void status_poison_kernel(const unsigned* __restrict__ status, float* __restrict__ x, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) x[i] = __builtin_nanf("");
+}
+extern "C" int sv_status_poison(const void* sync, float* x, int n, hipStream_t stream) {
+  if (!sync || !x || n <= 0) return SV_EARG;
+  hipLaunchKernelGGL(status_poison_kernel, dim3((n + 255) / 256), dim3(256), 0, stream,
+                     reinterpret_cast<const unsigned*>(sync), x, n);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
 }

@@ -16,19 +16,57 @@ import os
 
 import torch
 
-from ._lib import call, ptr, require_device, stream_of, lib
+from ._lib import PersistStatus, call, ptr, require_device, stream_of, lib
 
 PIPELINE_CHUNK = int(os.environ.get("SV_PIPELINE_CHUNK", "32"))  # 0 disables the layer pipeline
 
+# how the fp32 path forms its products (the `products` argument of the C ABI, include/sv_ge2e.h):
+# "mfma_f32" (default, exact fp32 MFMA) or "bf16x6" (three-way bf16 split, six bf16 MFMA products
+# per fp32 product, fp32 accumulation).  Per call, never process-wide.
 F32_PRODUCT_MODES = {"mfma_f32": 0, "bf16x6": 1}
 
 
-def set_f32_products(mode):
-    """Select how the fp32 path forms its products (process-wide, like a BLAS math mode):
-    "mfma_f32" (default, exact fp32 MFMA) or "bf16x6" (three-way bf16 split, six bf16 MFMA
-    products per fp32 product, fp32 accumulation; include/sv_ge2e.h).  Returns the previous mode."""
-    prev = lib().sv_set_f32_products(F32_PRODUCT_MODES[mode])
-    return {v: k for k, v in F32_PRODUCT_MODES.items()}.get(prev, str(prev))
+def _products(mode):
+    try:
+        return F32_PRODUCT_MODES[mode or "mfma_f32"]
+    except KeyError:
+        raise ValueError(f"unknown fp32 product mode {mode!r} (expected one of {sorted(F32_PRODUCT_MODES)})") from None
+
+
+# sync blocks of bf16 calls made without a caller-owned one (autograd path): their status is
+# checked (non-blocking) at the next call and by check_persistent_status()
+_UNCHECKED = []
+
+
+def _own_status(status, device):
+    if status is not None:
+        return status, False
+    check_persistent_status()
+    return PersistStatus(device), True
+
+
+def _release_status(st, own):
+    if own:
+        st.arm()
+        _UNCHECKED.append(st)
+
+
+def check_persistent_status(wait=False):
+    """Raise PersistentRecurrenceError if a persistent recurrence of an earlier call (made
+    without a caller-owned sync block) timed out; wait=True waits for all of them first."""
+    global _UNCHECKED
+    pending = _UNCHECKED
+    _UNCHECKED = []
+    err = None
+    for st in pending:
+        try:
+            st.poll(wait=wait)
+        except RuntimeError as e:
+            err = err or e
+        if st._pending:
+            _UNCHECKED.append(st)
+    if err:
+        raise err
 
 
 class _StreamPool:
@@ -78,9 +116,10 @@ class EmbedderState:
         self.bf16 = False
 
 
-def embedder_forward(x, layers, w_p, b_p, save=True):
+def embedder_forward(x, layers, w_p, b_p, save=True, products="mfma_f32"):
     """x [B,T,F] float32 (batch_first); layers = [(w_ih, w_hh, b_ih, b_hh)] * L.
-    Returns (emb [B,P], state)."""
+    Returns (emb [B,P], state).  products: fp32 product mode of the stack (F32_PRODUCT_MODES)."""
+    prod = _products(products)
     require_device(x, w_p, b_p, *[t for l in layers for t in l])
     B, T, F = x.shape
     H = layers[0][1].shape[1]
@@ -113,7 +152,7 @@ def embedder_forward(x, layers, w_p, b_p, save=True):
         ep = (ctypes.c_void_p * (L * nch + 1))(*[e.cuda_event for e in events[:L * nch + 1]])
         call("sv_lstm_stack_fwd", L, T, B, F, H, ptr(x_tm), _parr([l[0] for l in layers]),
              _parr([l[1] for l in layers]), _parr([l[2] for l in layers]), _parr([l[3] for l in layers]),
-             _parr(gs), _parr(cs), _parr(hs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep)
+             _parr(gs), _parr(cs), _parr(hs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep, prod)
         if save:
             st.x_tm = [x_tm] + [h[1:] for h in hs[:-1]]
             st.gates, st.c_tm, st.h_tm, st.hT = gs, cs, hs, hTs
@@ -121,6 +160,8 @@ def embedder_forward(x, layers, w_p, b_p, save=True):
         inp = hs[-1][1:]
     else:
         layers_done = False
+    if not layers_done and prod:
+        raise ValueError("the bf16x6 product mode runs on the layer-pipelined stack only (SV_PIPELINE_CHUNK > 0, L > 1)")
     for (w_ih, w_hh, b_ih, b_hh) in ([] if layers_done else layers):
         Fl = inp.shape[2]
         gates = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
@@ -146,7 +187,7 @@ def embedder_forward(x, layers, w_p, b_p, save=True):
     return emb, st
 
 
-def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_ready=None):
+def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_ready=None, products="mfma_f32"):
     """Backward of embedder_forward.  ``grads`` (optional) is a list of preallocated
     output tensors in parameter order [w_ih, w_hh, b_ih, b_hh]*L + [w_p, b_p]; returns it
     (and dx [B,T,F] if need_dx).
@@ -155,6 +196,7 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
     k = L for the projection, then k = L-1 .. 0 for the LSTM layers; ``event`` is the HIP
     event that completes it (None: the current stream).  The data-parallel trainer hangs its
     per-layer all-reduce buckets on it so communication overlaps the rest of the BPTT."""
+    prod = _products(products)
     demb = demb.contiguous()
     require_device(demb)
     T, B, H, P = st.T, st.B, st.H, st.P
@@ -172,6 +214,8 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
          ptr(grads[4 * L]), ptr(grads[4 * L + 1]), ptr(dh_last), ptr(ws), s)
     if grad_ready:
         grad_ready(L, None)
+    if prod and not (PIPELINE_CHUNK > 0 and L > 1 and not need_dx):
+        raise ValueError("the bf16x6 product mode runs on the layer-pipelined stack only")
     Fmax = max(st.x_tm[l].shape[2] for l in range(L))
     Bp = (B + 3) // 4 * 4
     if PIPELINE_CHUNK > 0 and L > 1 and not need_dx:
@@ -192,7 +236,7 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
              _parr(st.hT), ptr(dh_last), _parr(dgs), _parr(dgTs), _parr(dxs),
              _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
              _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
-             PIPELINE_CHUNK, s, sp, ep)
+             PIPELINE_CHUNK, s, sp, ep, prod)
         if grad_ready:
             for l in range(L - 1, -1, -1):
                 grad_ready(l, events[L * nch + l])
@@ -231,9 +275,11 @@ def _bf(shape, dev):
     return torch.empty(shape, dtype=torch.bfloat16, device=dev)
 
 
-def embedder_forward_bf16(x, layers, w_p, b_p, save=True):
+def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None):
     """Mixed-precision forward (BASELINE config c3): bf16 GEMM operands, fp32 accumulation,
-    fp32 gates / cell state / projection / norm.  Same outputs as embedder_forward."""
+    fp32 gates / cell state / projection / norm.  Same outputs as embedder_forward.
+    status: the caller's PersistStatus (sync block of the persistent recurrences); None = a
+    fresh one, checked at the next call / check_persistent_status()."""
     require_device(x, w_p, b_p, *[t for l in layers for t in l])
     B, T, F = x.shape
     H = layers[0][1].shape[1]
@@ -272,9 +318,11 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True):
         streams, events = _StreamPool.get(dev, L, L * nch + 1)
         sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * (L * nch + 1))(*[e.cuda_event for e in events[:L * nch + 1]])
+        sync, own = _own_status(status, dev)
         call("sv_lstm_stack_fwd_bf16", L, T, B, F, H, ptr(x_bf), _parr([w[0] for w in wbf]),
              _parr([w[1] for w in wbf]), _parr([l[2] for l in layers]), _parr([l[3] for l in layers]),
-             _parr(gs), _parr(cs), _parr(hs), _parr(hbs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep)
+             _parr(gs), _parr(cs), _parr(hs), _parr(hbs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep, sync.ptr())
+        _release_status(sync, own)
     else:
         for l, (w_ih, w_hh, b_ih, b_hh) in enumerate(layers):
             Fl = inp.shape[2]
@@ -295,9 +343,9 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True):
     return emb, st
 
 
-def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None):
+def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, status=None):
     """Backward of embedder_forward_bf16 (same ``grads`` / ``grad_ready`` contract as
-    embedder_backward)."""
+    embedder_backward; ``status`` as embedder_forward_bf16)."""
     demb = demb.contiguous()
     require_device(demb)
     T, B, H, P = st.T, st.B, st.H, st.P
@@ -328,12 +376,14 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None):
         streams, events = _StreamPool.get(dev, 2 * L, nev)
         sp = (ctypes.c_void_p * (2 * L))(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
+        sync, own = _own_status(status, dev)
         call("sv_lstm_stack_bwd_bf16", L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
              _parr([l[0] for l in layers]), _parr([l[1] for l in layers]), _parr(st.gates), _parr(st.c_tm),
              _parr(st.hT), ptr(dh_last), _parr(dgs), _parr(dgTs), _parr(dxs),
              _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
              _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
-             PIPELINE_CHUNK, s, sp, ep)
+             PIPELINE_CHUNK, s, sp, ep, sync.ptr())
+        _release_status(sync, own)
         if grad_ready:
             # the projection bucket is enqueued behind the stack backward: with the persistent
             # recurrences a collective must not run beside them (sv_lstm_stack_bwd_bf16)
@@ -372,13 +422,15 @@ class EmbedderFunction(torch.autograd.Function):
     """emb = SpeechEmbedder.forward(x) with params (w_ih, w_hh, b_ih, b_hh)*L, w_p, b_p."""
 
     @staticmethod
-    def forward(ctx, x, num_layers, precision, *params):
+    def forward(ctx, x, num_layers, precision, products, *params):
         L = num_layers
         layers = [tuple(params[4 * l:4 * l + 4]) for l in range(L)]
         w_p, b_p = params[4 * L], params[4 * L + 1]
-        fwd = embedder_forward_bf16 if precision == "bf16" else embedder_forward
-        emb, st = fwd(x.contiguous(), layers, w_p, b_p, save=True)
-        ctx.precision = precision
+        if precision == "bf16":
+            emb, st = embedder_forward_bf16(x.contiguous(), layers, w_p, b_p, save=True)
+        else:
+            emb, st = embedder_forward(x.contiguous(), layers, w_p, b_p, save=True, products=products)
+        ctx.precision, ctx.products = precision, products
         ctx.st = st
         ctx.L = L
         ctx.save_for_backward(*params)
@@ -395,13 +447,13 @@ class EmbedderFunction(torch.autograd.Function):
                 raise NotImplementedError("input gradients are only produced by the fp32 path")
             out = embedder_backward_bf16(ctx.st, demb, layers, params[4 * L])
         else:
-            out = embedder_backward(ctx.st, demb, layers, params[4 * L], need_dx=need_dx)
+            out = embedder_backward(ctx.st, demb, layers, params[4 * L], need_dx=need_dx, products=ctx.products)
         ctx.st = None
         if need_dx:
             grads, dx = out
         else:
             grads, dx = out, None
-        return (dx, None, None, *grads)
+        return (dx, None, None, None, *grads)
 
 
 # ----------------------------------------------------------------------------- GE2E
@@ -475,15 +527,17 @@ class GE2EFunction(torch.autograd.Function):
 
 
 # ----------------------------------------------------------------------------- clip + SGD
-def clip_sgd_step_(flat_params, flat_grads, max_norm, lr, write_grad=False, norm_out=None):
-    """In place: flat_params -= lr * min(1, max_norm/(|g|+1e-6)) * flat_grads."""
+def clip_sgd_step_(flat_params, flat_grads, max_norm, lr, write_grad=False, norm_out=None, status=None):
+    """In place: flat_params -= lr * min(1, max_norm/(|g|+1e-6)) * flat_grads.  With ``status``
+    (a PersistStatus) the update is skipped on the device when its status word is set."""
     require_device(flat_params, flat_grads)
     ws = _ws(lib().sv_clip_sgd_workspace(), flat_params.device)
     call("sv_clip_sgd_step", ptr(flat_params), ptr(flat_grads), flat_params.numel(), float(max_norm), float(lr),
-         int(write_grad), ptr(norm_out), ptr(ws), stream_of(flat_params))
+         int(write_grad), ptr(norm_out), status.ptr() if status is not None else None, ptr(ws),
+         stream_of(flat_params))
 
 
-def gemm_f32(A, B, a_kcontig=True, b_kcontig=True, bias=None):
+def gemm_f32(A, B, a_kcontig=True, b_kcontig=True, bias=None, products="mfma_f32"):
     """C = op(A) op(B) through sv_gemm_f32 (test hook).  With a_kcontig A is [M,K] else [K,M];
     with b_kcontig B is [N,K] else [K,N]."""
     require_device(A, B, bias)
@@ -493,5 +547,5 @@ def gemm_f32(A, B, a_kcontig=True, b_kcontig=True, bias=None):
     C = torch.empty((M, N), dtype=torch.float32, device=A.device)
     ws = _ws(lib().sv_gemm_f32_workspace(M, N, K), A.device)
     call("sv_gemm_f32", int(a_kcontig), int(b_kcontig), M, N, K, ptr(A), A.shape[1], ptr(B), B.shape[1], ptr(C), N,
-         ptr(bias), None, 0.0, ptr(ws), stream_of(A))
+         ptr(bias), None, 0.0, ptr(ws), _products(products), stream_of(A))
     return C

@@ -4,7 +4,9 @@ Same public surface -- ``SpeechEmbedder()``, ``GE2ELoss(device)``, and the re-ex
 ``get_centroids``, ``get_cossim``, ``calc_loss`` (:13) -- same parameter names, init and
 state_dict keys, so checkpoints and the reference's train_speech_embedder.py work
 unchanged.  The arithmetic runs in the gfx950 HIP kernels of libsv_ge2e.so
-(pytorch_speaker_verification_amd.ops); modules must live on the GPU.
+(pytorch_speaker_verification_amd.ops).  A module left on the CPU (the reference's test() never
+moves its net, train_speech_embedder.py:100-102,120-121) still computes there: its inputs and
+parameters make a differentiable round trip to the current GPU and the result comes back.
 """
 from __future__ import annotations
 
@@ -13,6 +15,7 @@ import math
 import torch
 import torch.nn as nn
 
+from ._lib import compute_device
 from .hparam import hparam as hp
 from .ops import EmbedderFunction, GE2EFunction
 from .utils import calc_loss, get_centroids, get_cossim  # noqa: F401  (re-exports, as :13)
@@ -63,6 +66,8 @@ class SpeechEmbedder(nn.Module):
         # "f32" (exact fp32 MFMA, configs c1/c2) or "bf16" (bf16 GEMM operands, fp32
         # accumulation / state / loss, config c3).  Not part of the state_dict.
         self.precision = "f32"
+        # fp32 product mode of the f32 path: "mfma_f32" (exact) or "bf16x6" (ops.F32_PRODUCT_MODES)
+        self.f32_products = "mfma_f32"
 
     def flat_params(self):
         """Parameters in kernel order: (w_ih, w_hh, b_ih, b_hh) per layer, then w_p, b_p."""
@@ -71,8 +76,14 @@ class SpeechEmbedder(nn.Module):
 
     def forward(self, x):
         # x.float() (:28) -> LSTM -> last frame (:30) -> projection (:31) -> x/|x| (:32)
-        return EmbedderFunction.apply(x.float().contiguous(), self.LSTM_stack.num_layers, self.precision,
-                                      *self.flat_params())
+        params = self.flat_params()
+        dev = compute_device(params[0])
+        host = None if params[0].is_cuda else params[0].device
+        if host is not None:  # CPU-resident module: differentiable copies to the GPU and back
+            params = [p.to(dev) for p in params]
+        out = EmbedderFunction.apply(x.float().to(dev).contiguous(), self.LSTM_stack.num_layers, self.precision,
+                                     self.f32_products, *params)
+        return out if host is None else out.to(host)
 
 
 class GE2ELoss(nn.Module):
@@ -88,5 +99,9 @@ class GE2ELoss(nn.Module):
         self.device = device
 
     def forward(self, embeddings):
-        loss, _ = GE2EFunction.apply(embeddings.contiguous(), self.w, self.b)
-        return loss
+        dev = compute_device(self.w)
+        if self.w.is_cuda:
+            loss, _ = GE2EFunction.apply(embeddings.to(dev).contiguous(), self.w, self.b)
+            return loss
+        loss, _ = GE2EFunction.apply(embeddings.to(dev).contiguous(), self.w.to(dev), self.b.to(dev))
+        return loss.to(self.w.device)

@@ -20,12 +20,20 @@ bucket L = projection + pad + {w, b} (ready before the BPTT starts), then one bu
 LSTM layer, top layer first, each launched on a communication stream as soon as the
 backward's per-layer completion event fires, so RCCL traffic overlaps the lower layers'
 BPTT; the clip + SGD kernel waits for all buckets.
+
+Failure surfacing (the reference never steps on wrong gradients, train_speech_embedder.py:61-65):
+the persistent bf16 recurrences synchronise through this trainer's own sync block
+(``self.status``, include/sv_ge2e.h).  If a hand-off wait times out, the block's sticky status
+is set, the clip + SGD kernels skip the update on the device, the returned loss is NaN, and the
+next ``step()`` (or ``check()``) raises PersistentRecurrenceError -- read through an async
+device-to-pinned copy, so the steady state never synchronises the host.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
+from ._lib import PersistStatus, call, ptr, stream_of
 from .ops import (clip_sgd_step_, embedder_backward, embedder_backward_bf16, embedder_forward,
                   embedder_forward_bf16)
 from .sharded_ge2e import ShardedGE2E
@@ -40,6 +48,7 @@ class GE2ETrainer:
         self.write_grads = write_grads
         self.ge2e = ShardedGE2E(group=group)
         self._flatten()
+        self.status = PersistStatus(self.flat_p.device)
 
     # -------------------------------------------------------------------------------------
     def _flatten(self):
@@ -71,6 +80,11 @@ class GE2ETrainer:
                 w.grad = flat_g[n_pad:n_pad + 1].view(())
                 b.grad = flat_g[n_pad + 1:n_pad + 2].view(())
         self.flat_p, self.flat_g = flat_p, flat_g
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            # every rank starts from rank 0's parameters (as DDP does), so SUM-reduced gradients
+            # update identical replicas even if the ranks' inits differed
+            dist.broadcast(flat_p, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0,
+                           group=self.group)
         self._ptrs = [p.data_ptr() for p in params]
         # all-reduce buckets: [off(layer l), off(layer l+1)) per layer; the head bucket runs
         # from the projection weight to the end (proj w, proj b, pad, w, b, pad)
@@ -86,17 +100,26 @@ class GE2ETrainer:
             self._flatten()  # the module was moved / reloaded since
 
     # -------------------------------------------------------------------------------------
+    def check(self):
+        """Wait for every step enqueued so far and raise PersistentRecurrenceError if one of
+        them had a persistent-recurrence timeout."""
+        self.status.poll(wait=True)
+
     def step(self, x, N, M):
         """x: [N*M, T, nmels] float32 on this rank's GPU (this rank's N speakers x M
         utterances, speaker-major).  Returns the (global) loss as a 0-dim device tensor."""
+        self.status.poll()  # raises if an earlier step's recurrences timed out
         self._check_layout()
         net = self.net
         layers = net.LSTM_stack.layer_params()
         w_p, b_p = net.projection.weight, net.projection.bias
         w, b = self.loss_mod.w, self.loss_mod.b
         bf16 = getattr(net, "precision", "f32") == "bf16"
-        fwd = embedder_forward_bf16 if bf16 else embedder_forward
-        emb, st = fwd(x.float().contiguous(), layers, w_p, b_p)
+        products = getattr(net, "f32_products", "mfma_f32")
+        if bf16:
+            emb, st = embedder_forward_bf16(x.float().contiguous(), layers, w_p, b_p, status=self.status)
+        else:
+            emb, st = embedder_forward(x.float().contiguous(), layers, w_p, b_p, products=products)
         E = emb.view(N, M, emb.shape[1])
         loss, _, gst = self.ge2e.forward(E, w, b)
         dE, dwdb = self.ge2e.backward(gst, w, b)
@@ -117,11 +140,19 @@ class GE2ETrainer:
                     comm.wait_event(event)
                 with torch.cuda.stream(comm):  # SUM, never mean (SURVEY §7 hard part 4)
                     works.append(dist.all_reduce(self.flat_g[lo:hi], group=self.group, async_op=True))
-        bwd = embedder_backward_bf16 if bf16 else embedder_backward
-        bwd(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views, grad_ready=ready)
+        if bf16:
+            embedder_backward_bf16(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views, grad_ready=ready,
+                                   status=self.status)
+        else:
+            embedder_backward(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views, grad_ready=ready,
+                              products=products)
         for wk in works:
             wk.wait()  # the current (main) stream waits for every bucket
         n = self.n_pad
-        clip_sgd_step_(self.flat_p[:n], self.flat_g[:n], self.clip_net, self.lr, self.write_grads)
-        clip_sgd_step_(self.flat_p[n:n + 4], self.flat_g[n:n + 4], self.clip_wb, self.lr, self.write_grads)
+        st_ = self.status if bf16 else None  # (the fp32 path has no persistent recurrences)
+        clip_sgd_step_(self.flat_p[:n], self.flat_g[:n], self.clip_net, self.lr, self.write_grads, status=st_)
+        clip_sgd_step_(self.flat_p[n:n + 4], self.flat_g[n:n + 4], self.clip_wb, self.lr, self.write_grads, status=st_)
+        if bf16:
+            call("sv_status_poison", self.status.ptr(), ptr(loss), 1, stream_of(loss))
+            self.status.arm()
         return loss

@@ -1,6 +1,6 @@
-"""fp32 GEMM accuracy / speed of the exact fp32 MFMA path vs the bf16x6 split (SV_F32_EMU=1):
+"""fp32 GEMM accuracy / speed of the exact fp32 MFMA path vs the bf16x6 split (products mode 1; SV_F32_PRODUCTS selects it here):
 errors against an fp64 reference on the same fp32 inputs, and the K1-shape throughput.
-Run once per setting (the library reads SV_F32_EMU once per process)."""
+"""
 import json
 import os
 import sys
@@ -13,7 +13,8 @@ from pytorch_speaker_verification_amd._lib import call, lib, ptr  # noqa: E402
 
 dev = torch.device("cuda", 0)
 s = torch.cuda.current_stream(dev).cuda_stream
-out = {"emu": os.environ.get("SV_F32_EMU", "0")}
+MODE = int(os.environ.get("SV_F32_PRODUCTS", "0"))
+out = {"products": MODE}
 g = np.random.default_rng(5)
 for name, (M, N, K, scale) in {"gx": (2048, 3072, 768, 1.0), "dw": (3072, 768, 20480, 1.0),
                                "mixed": (1024, 1024, 4096, 0.0)}.items():
@@ -25,7 +26,7 @@ for name, (M, N, K, scale) in {"gx": (2048, 3072, 768, 1.0), "dw": (3072, 768, 2
     At, Bt = torch.tensor(A, device=dev), torch.tensor(B, device=dev)
     C = torch.empty(M, N, device=dev)
     ws = torch.empty(lib().sv_gemm_f32_workspace(M, N, K) // 4 + 1, device=dev)
-    call("sv_gemm_f32", 1, 1, M, N, K, ptr(At), K, ptr(Bt), K, ptr(C), N, None, None, 0.0, ptr(ws), s)
+    call("sv_gemm_f32", 1, 1, M, N, K, ptr(At), K, ptr(Bt), K, ptr(C), N, None, None, 0.0, ptr(ws), MODE, s)
     ref = A.astype(np.float64) @ B.astype(np.float64).T
     absref = np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64).T   # |A||B|^T: the error scale
     err = np.abs(C.cpu().numpy().astype(np.float64) - ref) / absref
@@ -34,7 +35,7 @@ M, N, K = 102400, 3072, 768
 A = torch.randn(M, K, device=dev)
 Bm = torch.randn(N, K, device=dev) * 0.03
 C = torch.empty(M, N, device=dev)
-f = lambda: call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, None, s)  # noqa
+f = lambda: call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, None, MODE, s)  # noqa
 f()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()

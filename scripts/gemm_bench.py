@@ -41,7 +41,7 @@ for name, (M, N, K) in SHAPES.items():
     Bm = torch.randn(N, K, device=dev)
     C = torch.empty(M, N, device=dev)
     w = torch.empty(lib().sv_gemm_f32_workspace(M, N, K) // 4 + 1, device=dev)
-    f = lambda: call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, ptr(w), s)  # noqa: E731
+    f = lambda: call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, ptr(w), 0, s)  # noqa: E731
     us = timeit(f, args.reps)
     res["sv_f32_" + name] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
     if args.torch:

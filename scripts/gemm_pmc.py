@@ -17,7 +17,7 @@ for (M, N, K) in ((T * B, G, H), (T * B, H, G)):
     Bm = torch.randn(N, K, device=dev)
     C = torch.empty(M, N, device=dev)
     for _ in range(3):
-        call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, None, s)
+        call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, None, 0, s)
     if os.environ.get("WITH_TORCH", "1") == "1":
         for _ in range(3):
             torch.matmul(A, Bm.t(), out=C)

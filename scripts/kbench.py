@@ -86,7 +86,7 @@ def gemm(ak, bk, M, N, K):
     wsz = lib().sv_gemm_f32_workspace(M, N, K)
     w = torch.empty(wsz // 4 + 1, device=dev)
     f = lambda: call("sv_gemm_f32", ak, bk, M, N, K, ptr(A), A.shape[1], ptr(Bm), Bm.shape[1], ptr(C), N, None, None,  # noqa: E731
-                     0.0, ptr(w), s)
+                     0.0, ptr(w), int(os.environ.get("SV_F32_PRODUCTS", "0")), s)
     us = timeit(f, reps=5, warm=1)
     return round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)
 

@@ -1,7 +1,6 @@
 """Debug aid: run the bf16 stack backward under the schedule in the environment and save
 dG (row-major + transposed), dx and the weight gradients per layer.  Usage:
   python scripts/pbwd_debug.py out.npz   (then compare two runs with --cmp a.npz b.npz)"""
-import ctypes
 import os
 import sys
 
@@ -18,7 +17,7 @@ def run(out):
     import recipe
     from conftest import model_dims
     from pytorch_speaker_verification_amd import ops
-    from pytorch_speaker_verification_amd._lib import lib
+    from pytorch_speaker_verification_amd._lib import PersistStatus
     from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
     dims, N, M, T = (40, 768, 3, 256), 64, 10, 12
     dev = torch.device("cuda", 0)
@@ -31,7 +30,8 @@ def run(out):
     net = net.to(dev)
     x = torch.tensor(recipe.make_frames(11, N * M, T, dims[0]), device=dev)
     layers = net.LSTM_stack.layer_params()
-    emb, st = ops.embedder_forward_bf16(x, layers, net.projection.weight, net.projection.bias)
+    ps = PersistStatus(dev)
+    emb, st = ops.embedder_forward_bf16(x, layers, net.projection.weight, net.projection.bias, status=ps)
     torch.manual_seed(3)
     demb = torch.randn_like(emb)
     cap = []
@@ -42,12 +42,12 @@ def run(out):
         cap.append(t)
         return t
     ops._bf = spy
-    grads = ops.embedder_backward_bf16(st, demb, layers, net.projection.weight)
+    grads = ops.embedder_backward_bf16(st, demb, layers, net.projection.weight, status=ps)
     torch.cuda.synchronize()
     res = {f"buf{i}": c.float().cpu().numpy() for i, c in enumerate(cap)}
     for i, g in enumerate(grads):
         res[f"g{i}"] = g.float().cpu().numpy()
-    res["status"] = np.array([lib().sv_persist_status()])
+    res["status"] = np.array([int(ps.block[0])])
     np.savez(out, **res)
 
 

@@ -24,7 +24,7 @@ A = torch.randn(M, K, generator=g).to(dev)
 Bm = torch.randn(N, K, generator=g).to(dev)
 C = torch.empty(M, N, device=dev)
 for _ in range(3):
-    call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, None, s)
+    call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, None, 0, s)
 torch.cuda.synchronize()
 print("done")
 

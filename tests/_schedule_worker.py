@@ -17,7 +17,7 @@ from conftest import model_dims  # noqa: E402
 
 
 def main(out, dims, N, M, T, precision):
-    from pytorch_speaker_verification_amd._lib import lib
+    from pytorch_speaker_verification_amd._lib import PersistStatus
     from pytorch_speaker_verification_amd.ops import embedder_forward_bf16, embedder_forward
     from pytorch_speaker_verification_amd.speech_embedder_net import GE2ELoss, SpeechEmbedder
     from pytorch_speaker_verification_amd.trainer import GE2ETrainer
@@ -32,8 +32,11 @@ def main(out, dims, N, M, T, precision):
     net.precision = precision
     x = torch.tensor(recipe.make_frames(11, N * M, T, dims[0]), device=dev)
     layers = net.LSTM_stack.layer_params()
-    fwd = embedder_forward_bf16 if precision == "bf16" else embedder_forward
-    emb, st = fwd(x, layers, net.projection.weight, net.projection.bias)
+    status = PersistStatus(dev)
+    if precision == "bf16":
+        emb, st = embedder_forward_bf16(x, layers, net.projection.weight, net.projection.bias, status=status)
+    else:
+        emb, st = embedder_forward(x, layers, net.projection.weight, net.projection.bias)
     res = {"emb": emb, "h_last": st.h_last}
     for l in range(len(layers)):
         res[f"gates{l}"] = st.gates[l]
@@ -46,7 +49,7 @@ def main(out, dims, N, M, T, precision):
         res["grad_" + name] = prm.grad
     torch.cuda.synchronize()
     res = {k: v.detach().float().cpu().numpy() for k, v in res.items()}
-    res["status"] = np.array([lib().sv_persist_status()])
+    res["status"] = np.array([int(status.block[0]) | int(tr.status.block[0])])
     np.savez(out, **res)
 
 

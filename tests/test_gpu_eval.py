@@ -71,8 +71,12 @@ def test_test_driver_matches_reference(tmp_path, monkeypatch):
     finally:
         _hp_restore(hp, saved, saved_top)
     got = np.stack([s.cpu().numpy() for s in sims])
-    np.testing.assert_allclose(got, g["sims"], atol=2e-5)
-    assert abs(avg - float(g["avg_eer"])) < 2e-2
+    err = float(np.abs(got - g["sims"]).max())
+    print(f"\nMEASURED test_driver.sims_abs {err:.3e}")
+    assert err <= 4e-6, err  # 10x the deviation measured on MI355X (4.2e-7)
+    # the EER is a threshold pick over a 0.01 grid, recorded as the reference's printed "{:.4f}"
+    # line (:154): the same selection reproduces that line exactly
+    assert f"{avg:.4f}" == f"{float(g['avg_eer']):.4f}", (avg, float(g["avg_eer"]))
 
 
 def test_train_driver_runs_and_checkpoints(tmp_path):

@@ -145,7 +145,7 @@ def test_f32_products_bf16x6_accuracy_and_step():
     fp32-MFMA path's (x1.25 margin), and a full training step that agrees with the exact path
     to fp32 level (loss 1e-5 relative, parameters 1e-5 relative)."""
     from pytorch_speaker_verification_amd._lib import call, ptr, stream_of
-    from pytorch_speaker_verification_amd.ops import set_f32_products
+    from pytorch_speaker_verification_amd.ops import F32_PRODUCT_MODES
     g = np.random.default_rng(3)
     M, N, K = 256, 512, 768
     A = g.standard_normal((M, K)).astype(np.float32)
@@ -154,14 +154,10 @@ def test_f32_products_bf16x6_accuracy_and_step():
     scale = np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64).T
     errs = {}
     for mode in ("mfma_f32", "bf16x6"):
-        prev = set_f32_products(mode)
-        try:
-            C = torch.empty(M, N, device=DEV)
-            call("sv_gemm_f32", 1, 1, M, N, K, ptr(torch.tensor(A, device=DEV)), K, ptr(torch.tensor(B, device=DEV)),
-                 K, ptr(C), N, None, None, 0.0, None, stream_of(C))
-            errs[mode] = float((np.abs(C.cpu().numpy() - ref) / scale).max())
-        finally:
-            set_f32_products(prev)
+        C = torch.empty(M, N, device=DEV)
+        call("sv_gemm_f32", 1, 1, M, N, K, ptr(torch.tensor(A, device=DEV)), K, ptr(torch.tensor(B, device=DEV)),
+             K, ptr(C), N, None, None, 0.0, None, F32_PRODUCT_MODES[mode], stream_of(C))
+        errs[mode] = float((np.abs(C.cpu().numpy() - ref) / scale).max())
     assert errs["bf16x6"] <= 1.25 * errs["mfma_f32"], errs
     assert errs["bf16x6"] < 1e-6, errs
 
@@ -179,13 +175,10 @@ def test_f32_products_bf16x6_accuracy_and_step():
             for k, v in net.state_dict().items():
                 v.copy_(torch.as_tensor(sd[k]))
         net = net.to(DEV)
-        prev = set_f32_products(mode)
-        try:
-            tr = GE2ETrainer(net, GE2ELoss(DEV), lr=0.01)
-            loss = float(tr.step(x, Ns, Ms))
-            res[mode] = (loss, tr.flat_p.detach().cpu().numpy().copy())
-        finally:
-            set_f32_products(prev)
+        net.f32_products = mode  # a per-module setting, passed to the C ABI per call
+        tr = GE2ETrainer(net, GE2ELoss(DEV), lr=0.01)
+        loss = float(tr.step(x, Ns, Ms))
+        res[mode] = (loss, tr.flat_p.detach().cpu().numpy().copy())
     (l0, p0), (l1, p1) = res["mfma_f32"], res["bf16x6"]
     assert abs(l1 - l0) <= 1e-5 * abs(l0), (l0, l1)
     assert np.abs(p1 - p0).max() <= 1e-5 * np.abs(p0).max()

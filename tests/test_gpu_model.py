@@ -28,6 +28,12 @@ def _rel(a, b):
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
 
 
+def _check(name, value, tol):
+    """Tolerances are ~10x the deviation measured on MI355X."""
+    print(f"\nMEASURED {name} {value:.3e} (tol {tol:.1e})")
+    assert value <= tol, (name, value, tol)
+
+
 def test_small_net_autograd_path_matches_reference():
     """The drop-in path: module forward, loss.backward(), torch clip + SGD (user code)."""
     s = golden("net_small.npz")
@@ -79,16 +85,19 @@ def test_full_dims_c1_matches_reference():
     N, M, T = int(s["N"]), int(s["M"]), int(s["T"])
     x = torch.tensor(recipe.make_frames(int(s["xseed"]), N * M, T, dims[0]), device=DEV)
     emb = net(x).reshape(N, M, -1)
-    np.testing.assert_allclose(emb.detach().cpu().numpy(), s["emb"], atol=5e-5)
+    _check("c1.emb_abs", float(np.abs(emb.detach().cpu().numpy() - s["emb"]).max()), 2e-6)
     loss = ge2e(emb)
-    assert abs(loss.item() - float(s["loss"])) <= 1e-4 * abs(float(s["loss"]))
+    _check("c1.loss_rel", abs(loss.item() - float(s["loss"])) / abs(float(s["loss"])), 2e-6)
     loss.backward()
+    gn, gh = 0.0, 0.0
     for k, p in net.named_parameters():
         g = p.grad.cpu().double()
-        assert abs(g.norm().item() - float(s["gnorm." + k])) <= 1e-3 * float(s["gnorm." + k]), k
+        gn = max(gn, abs(g.norm().item() - float(s["gnorm." + k])) / float(s["gnorm." + k]))
         head = g.reshape(g.shape[0], -1)[:8, :8].numpy() if g.dim() == 2 else g[:64].numpy()
         ref = s["ghead." + k]
-        assert np.abs(head - ref).max() <= 2e-3 * max(np.abs(ref).max(), 1e-6) + 1e-7, k
+        gh = max(gh, float(np.abs(head - ref).max()) / max(np.abs(ref).max(), 1e-6))
+    _check("c1.grad_norm_rel", gn, 2e-5)
+    _check("c1.grad_head_rel", gh, 5e-5)
 
 
 def test_full_size_c2_against_torch_gpu():
@@ -102,21 +111,20 @@ def test_full_size_c2_against_torch_gpu():
     x = torch.tensor(recipe.make_frames(1236, N * M, T, dims[0]), device=DEV)
     emb = net(x).reshape(N, M, -1)
     emb_ref = port(x).reshape(N, M, -1)
-    assert _rel(emb.detach().cpu().numpy(), emb_ref.detach().cpu().numpy()) < 1e-4
+    _check("c2.emb_rel_vs_miopen", _rel(emb.detach().cpu().numpy(), emb_ref.detach().cpu().numpy()), 1e-5)
     # unit-norm rows (size-independent property of the projection + L2 norm)
     np.testing.assert_allclose(emb.norm(dim=2).detach().cpu().numpy(), 1.0, atol=1e-5)
     loss = ge2e(emb)
     w = torch.tensor(10.0, device=DEV, requires_grad=True)
     b = torch.tensor(-5.0, device=DEV, requires_grad=True)
     loss_ref = torch_port.ge2e_loss(emb_ref, w, b)
-    assert abs(loss.item() - loss_ref.item()) <= 1e-4 * abs(loss_ref.item())
+    _check("c2.loss_rel_vs_miopen", abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()), 1e-6)
     loss.backward()
     loss_ref.backward()
     pr = dict(port.named_parameters())
-    for k, p in net.named_parameters():
-        gr = pr[k].grad.cpu().numpy()
-        assert _rel(p.grad.cpu().numpy(), gr) < 2e-3, k
-    assert abs(ge2e.w.grad.item() - w.grad.item()) <= 1e-3 * max(1, abs(w.grad.item()))
+    g = max(_rel(p.grad.cpu().numpy(), pr[k].grad.cpu().numpy()) for k, p in net.named_parameters())
+    _check("c2.grad_rel_vs_miopen", g, 4e-5)
+    _check("c2.dw_vs_miopen", abs(ge2e.w.grad.item() - w.grad.item()) / max(1, abs(w.grad.item())), 2.5e-5)
 
 
 def test_batch_permutation_invariance():
@@ -146,59 +154,43 @@ def test_ragged_batch_and_seq_sizes():
         np.testing.assert_allclose(e, er, atol=5e-5)
 
 
-def test_bf16_path_c2_tolerance_and_training():
-    """Config c3: bf16 GEMM operands.  Embeddings / loss / gradients against the fp32 HIP path
-    on identical inputs (diversified weights, so the embeddings are not near-collinear);
-    measured tolerances are written here: emb 2e-2 max-abs, loss 1e-2 rel, grads 5e-2 rel
-    (norm).  Then a few fused bf16 training steps must lower the loss like the fp32 steps."""
+def test_bf16_training_lowers_loss_c2():
+    """Config c3 trains: a few fused bf16 steps at the full c2 size lower the loss (the
+    per-step numerics are pinned to the bf16 oracle in test_gpu_precision.py)."""
     from pytorch_speaker_verification_amd.trainer import GE2ETrainer
     dims, N, M, T = (40, 768, 3, 256), 64, 10, 160
     sd = recipe.make_weights(2025, *dims, scale=3.0)
     x = torch.tensor(recipe.make_frames(1237, N * M, T, dims[0]), device=DEV)
-    net32, ge32 = _build(dims, sd)
-    net16, ge16 = _build(dims, sd)
-    net16.precision = "bf16"
-    e32 = net32(x).reshape(N, M, -1)
-    e16 = net16(x).reshape(N, M, -1)
-    assert float((e16 - e32).abs().max()) < 2e-2
-    l32, l16 = ge32(e32), ge16(e16)
-    assert abs(l16.item() - l32.item()) <= 1e-2 * abs(l32.item())
-    l32.backward()
-    l16.backward()
-    for (k, p32), p16 in zip(net32.named_parameters(), net16.parameters()):
-        d = float((p16.grad - p32.grad).norm() / p32.grad.norm().clamp_min(1e-30))
-        assert d < 5e-2, (k, d)
     net16b, ge16b = _build(dims, sd)
     net16b.precision = "bf16"
     tr = GE2ETrainer(net16b, ge16b, lr=0.01)
     losses = [float(tr.step(x, N, M)) for _ in range(4)]
+    tr.check()
     assert losses[-1] < losses[0], losses
 
 
-def test_c5_per_gpu_shape_bf16_and_f32():
-    """BASELINE config c5 on one GPU's shard: N = 256 speakers over 8 GPUs -> 32 speakers x
-    M = 10 per rank, T = 180, full dims.  The fused training step runs at that shape in bf16
-    and fp32 (the cross-rank exchange itself is covered by test_gpu_dp / the gloo protocol
-    test); the bf16 loss agrees with the fp32 loss to 1e-2 relative and both steps produce
-    finite, identical-shape parameter updates."""
+def test_c5_per_gpu_shape_f32():
+    """BASELINE config c5's per-rank shape (N = 256 over 8 GPUs -> 32 x M = 10, T = 180) in
+    fp32 against the stock-PyTorch port on the same GPU (the bf16 form is pinned to the bf16
+    oracle in test_gpu_precision.py; the cross-rank exchange by test_gpu_dp / the gloo test)."""
     from pytorch_speaker_verification_amd.trainer import GE2ETrainer
     dims, N, M, T = (40, 768, 3, 256), 32, 10, 180
     sd = recipe.make_weights(55, *dims, scale=3.0)
-    x = torch.tensor(recipe.make_frames(1238, N * M, T, dims[0]), device=DEV)
-    losses = {}
-    deltas = {}
-    for prec in ("f32", "bf16"):
-        net, ge = _build(dims, sd)
-        net.precision = prec
-        p0 = [p.detach().clone() for p in net.parameters()]
-        tr = GE2ETrainer(net, ge, lr=0.01)
-        losses[prec] = float(tr.step(x, N, M))
-        deltas[prec] = [(p.detach() - q) for p, q in zip(net.parameters(), p0)]
-        assert all(torch.isfinite(d).all() for d in deltas[prec])
-    assert abs(losses["bf16"] - losses["f32"]) <= 1e-2 * abs(losses["f32"]), losses
-    for d32, d16 in zip(deltas["f32"], deltas["bf16"]):
-        rel = float((d16 - d32).norm() / d32.norm().clamp_min(1e-30))
-        assert rel < 1e-1, rel
+    xh = recipe.make_frames(1238, N * M, T, dims[0])
+    net, ge = _build(dims, sd)
+    tr = GE2ETrainer(net, ge, lr=0.01)
+    loss = float(tr.step(torch.tensor(xh, device=DEV), N, M))
+    port = torch_port.SpeechEmbedderPort(*dims)
+    torch_port.load_recipe_weights(port, sd)
+    port = port.to(DEV)
+    w = torch.nn.Parameter(torch.tensor(10.0, device=DEV))
+    b = torch.nn.Parameter(torch.tensor(-5.0, device=DEV))
+    opt = torch.optim.SGD([{"params": port.parameters()}, {"params": [w, b]}], lr=0.01)
+    ref = float(torch_port.train_step(port, w, b, opt, torch.tensor(xh, device=DEV), N, M))
+    _check("c5_rank.f32_loss_rel_vs_miopen", abs(loss - ref) / abs(ref), 1e-6)
+    got = {k: v.detach() for k, v in net.state_dict().items()}
+    d = max(float((got[k] - v.detach()).abs().max()) for k, v in port.state_dict().items())
+    _check("c5_rank.f32_param_abs_vs_miopen", d, 3e-7)
 
 
 @pytest.mark.parametrize("dims,N,M,T", [((40, 96, 2, 24), 3, 3, 5),     # B = 9: odd, below every tile

@@ -1,0 +1,105 @@
+"""GPU: the mixed-precision configs (BASELINE c3 / c4 / c5: bf16 GEMM operands, fp32 state,
+accumulation, gradients and loss) pinned to the bf16-operand oracle (oracle/lstm_bf16.py, whose
+fp32 mode is pinned to the reference's golden vectors), at the shapes the configs run per GPU:
+
+  c4 per rank   N = 64 speakers over 8 GPUs -> 8 x M = 10 = 80 utterances, T = 160
+  c3            N = 64 x M = 10 = 640 utterances (T reduced to 24 so the CPU oracle stays fast;
+                the tiles, grids and hand-offs are those of T = 160)
+  c5 per rank   N = 256 over 8 GPUs -> 32 x 10 = 320 utterances, T = 180
+
+Every tolerance is about 10x the deviation measured on MI355X (DESIGN.md §6 lists the measured
+values; each check prints its MEASURED line).  Deviations are relative to the reference
+quantity's max-abs (emb: absolute; loss: relative).  Weights use the portable recipe scaled x3 so
+the embeddings are diverse (SURVEY §7 hard part 5)."""
+import numpy as np
+import pytest
+import torch
+
+import recipe
+from conftest import model_dims
+from oracle import lstm_bf16
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _check(name, value, tol):
+    print(f"\nMEASURED {name} {value:.3e} (tol {tol:.1e})")
+    assert value <= tol, (name, value, tol)
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def _hip_step(dims, sd, x, N, M, precision):
+    from pytorch_speaker_verification_amd.speech_embedder_net import GE2ELoss, SpeechEmbedder
+    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    net = net.to(DEV)
+    net.precision = precision
+    emb = net(torch.tensor(x, device=DEV)).detach().cpu().numpy()
+    tr = GE2ETrainer(net, GE2ELoss(DEV), lr=0.01)
+    loss = float(tr.step(torch.tensor(x, device=DEV), N, M))
+    tr.check()
+    grads = {k: p.grad.detach().cpu().numpy().copy() for k, p in net.named_parameters()}
+    params = {k: v.detach().cpu().numpy().copy() for k, v in net.state_dict().items()}
+    return emb, loss, grads, params
+
+
+def _compare(tag, dims, N, M, T, seed, tol):
+    sd = recipe.make_weights(seed, *dims, scale=3.0)
+    x = recipe.make_frames(seed + 1, N * M, T, dims[0])
+    emb, loss, grads, params = _hip_step(dims, sd, x, N, M, "bf16")
+    r_loss, r_new, _, _, r_emb, r_grads, _, _ = lstm_bf16.train_step(sd, 10.0, -5.0, x, N, M, dims[2], bf16=True)
+    _check(f"{tag}.emb_abs", float(np.abs(emb - r_emb.numpy()).max()), tol["emb"])
+    _check(f"{tag}.loss_rel", abs(loss - r_loss) / abs(r_loss), tol["loss"])
+    # the trainer leaves the CLIPPED gradients in .grad (clip_grad_norm_ scales them in place)
+    tot = float(np.sqrt(sum(float((r_grads[k].double() ** 2).sum()) for k in r_grads)))
+    coef = min(1.0, 3.0 / (tot + 1e-6))
+    g = max(_rel(grads[k], coef * r_grads[k].numpy()) for k in grads)
+    _check(f"{tag}.grad_rel_max", g, tol["grad"])
+    p = max(float(np.abs(params[k] - r_new[k].numpy()).max()) for k in params)
+    _check(f"{tag}.param_abs", p, tol["param"])
+    return emb, loss
+
+
+def test_c4_rank_shape_bf16_against_oracle():
+    """c4's per-rank shape (B = 80) on the persistent W-stationary kernels: against the bf16
+    oracle, and the bf16-vs-fp32 gap of the oracle itself recorded beside it."""
+    from pytorch_speaker_verification_amd._lib import lib
+    dims, N, M, T = (40, 768, 3, 256), 8, 10, 160
+    assert lib().sv_persist_fwd_ok(N * M, 768) and lib().sv_persist_bwd_ok(N * M, 768)
+    _compare("c4_rank", dims, N, M, T, 4040, dict(emb=5e-3, loss=5e-4, grad=5e-2, param=2e-5))
+
+
+def test_c3_shape_bf16_against_oracle():
+    dims, N, M, T = (40, 768, 3, 256), 64, 10, 24
+    _compare("c3_T24", dims, N, M, T, 3030, dict(emb=5e-3, loss=5e-4, grad=5e-2, param=2e-5))
+
+
+def test_c5_rank_shape_bf16_against_oracle():
+    dims, N, M, T = (40, 768, 3, 256), 32, 10, 180
+    _compare("c5_rank", dims, N, M, T, 5050, dict(emb=5e-3, loss=5e-4, grad=5e-2, param=2e-5))
+
+
+def test_bf16_vs_fp32_gap_matches_oracle_gap():
+    """What bf16 operands cost: the HIP bf16-vs-fp32 gap equals the oracle's bf16-vs-fp32 gap
+    (same inputs, c4 rank shape) to within the oracle tolerance -- the mixed-precision error is
+    the rounding the config prescribes, nothing more."""
+    dims, N, M, T = (40, 768, 3, 256), 8, 10, 160
+    sd = recipe.make_weights(4041, *dims, scale=3.0)
+    x = recipe.make_frames(4042, N * M, T, dims[0])
+    e16, l16, _, _ = _hip_step(dims, sd, x, N, M, "bf16")
+    e32, l32, _, _ = _hip_step(dims, sd, x, N, M, "f32")
+    o16, _ = lstm_bf16.embedder_forward(sd, x, dims[2], bf16=True)
+    o32, _ = lstm_bf16.embedder_forward(sd, x, dims[2], bf16=False)
+    hip_gap = float(np.abs(e16 - e32).max())
+    ora_gap = float((o16 - o32).abs().max())
+    _check("c4_rank.hip_bf16_fp32_emb_gap", hip_gap, 2e-2)
+    _check("c4_rank.gap_mismatch", abs(hip_gap - ora_gap), 3e-4)
