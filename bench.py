@@ -1,24 +1,38 @@
 #!/usr/bin/env python3
 """GE2E training-step benchmark (BASELINE.json metric: embeddings/sec + GE2E steps/sec at
-N=64 x M=10, T=160, 40 mels, 3-layer LSTM 768 -> 256).
+N=64 x M=10, T=160, 40 mels, 3-layer LSTM 768 -> 256, at 1/2/4/8 MI355X).
 
 One "step" = SpeechEmbedder forward + GE2E loss + backward + clip_grad_norm_ (3.0 / 1.0)
-+ SGD on one N x M batch per GPU (GE2ETrainer.step, all HIP kernels).  Multi-GPU: one
-process per GPU (torchrun), speakers sharded across ranks (global batch = world * N
-speakers, exact single-batch semantics via ShardedGE2E), SUM all-reduce of gradients over
-RCCL; per-GPU work is fixed, so scaling is weak.
++ SGD on one N x M batch (GE2ETrainer.step, all HIP kernels), inputs already in HBM.
 
-Prints ONE JSON line on rank 0.  value = training embeddings/s of the whole job
-(world * N * M * steps / max-over-ranks time).  Extra fields: steps_per_sec,
-fwd_embeddings_per_sec (no-grad forward), roofline (dominant kernel, live HIP-event
-timing on the kernel's stream), cpu_baseline (the reference path on host cores,
-oracle/torch_port.py, rank 0 only).
+Multi-GPU: one process per GPU.  ``python bench.py --gpus N`` launches the N ranks itself
+(torch.distributed.run, 127.0.0.1) before this process touches the GPU; under an external
+launcher (WORLD_SIZE set) it runs as one rank.  Speakers are sharded across ranks (exact
+single-batch semantics via ShardedGE2E), gradients SUM-all-reduced over RCCL.
+
+Headline line (rank 0 prints ONE JSON line): config c2 (fp32, the reference's precision) with
+N = 64 speakers PER GPU -> weak scaling; value = world * N * M * steps / max-over-ranks time.
+Side measurements in the same line:
+  bf16            c3: the same per-GPU workload with bf16 GEMM operands (weak scaling)
+  c4              (world > 1) c3's global batch N = 64 x M = 10 split over the ranks, bf16:
+                  strong scaling, value = 640 * steps / time
+  c5              (world > 1) N = 256 x M = 10, T = 180 split over the ranks, bf16 (strong)
+  c4_rank_shape / c5_rank_shape   (world = 1) one rank's share of c4 / c5 at 8 GPUs, alone
+  roofline        the in-step dominant kernel of the headline step: the fp32 backward
+                  recurrent step K3 (lstm_step_bwd_v2_kernel), timed by HIP events recorded on
+                  its own stream around each chunk of its launches INSIDE the timed steps
+  roofline_bf16   the same for c3's dominant kernels, the persistent bf16 recurrences
+  roofline_gemm / roofline_step_kernel   secondary: the K1-shape fp32 GEMM and K2 in isolation
+  cpu_baseline    the reference's CPU path (oracle/torch_port.py, nn.LSTM on oneDNN) on every
+                  host CPU this process may use, median of 3 steps at c2, plus c1
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,11 +46,13 @@ sys.path.insert(0, ROOT)
 MI355X_FP32_MFMA_TFLOPS = 157.3   # /opt/skills/guides/MI355X_MICROARCH.md, chip-level table
 MI355X_HBM_GBPS = 8000.0
 MI355X_BF16_MFMA_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
+METRIC = "embeddings/sec + GE2E steps/sec at N=64×M=10, 1/2/4/8 MI355X"
+DIMS = (40, 768, 3, 256)          # nmels, hidden, layers, proj (config/config.yaml)
 
 
 def step_flops(B, T, F, H, P, L):
-    """Algorithmic FLOPs: fwd = 2BTG[(F+H) + 2(2H)] ... as stated there:
-    fwd = sum over layers of 2*B*T*4H*(F_l + H) + 2*B*H*P; step = 3*fwd - 2*B*T*4H*F."""
+    """Algorithmic FLOPs (SURVEY §8d): fwd = sum over layers of 2*B*T*4H*(F_l + H) + 2*B*H*P;
+    step = 3*fwd - 2*B*T*4H*F."""
     G = 4 * H
     fwd = sum(2 * B * T * G * ((F if l == 0 else H) + H) for l in range(L)) + 2 * B * H * P
     return fwd, 3 * fwd - 2 * B * T * G * F
@@ -55,60 +71,94 @@ def build_model(dims, dev, seed=0):
     return net.to(dev), GE2ELoss(dev)
 
 
-def time_step_kernel(B, H, dev, reps=64):
-    """Average duration of the forward recurrent-step kernel (K2), HIP events on the
-    stream it is launched on.  Returns (ms per launch, FLOPs per launch)."""
-    from pytorch_speaker_verification_amd._lib import call, ptr, stream_of
-    g = torch.Generator(device="cpu").manual_seed(7)
-    whh = (torch.randn(4 * H, H, generator=g) * 0.02).to(dev)
-    hprev = torch.randn(B, H, generator=g).to(dev)
-    cprev = torch.randn(B, H, generator=g).to(dev)
-    gates0 = torch.randn(B, 4 * H, generator=g).to(dev)
-    gates = gates0.clone()
-    c_t = torch.empty(B, H, device=dev)
-    h_t = torch.empty(B, H, device=dev)
-    s = torch.cuda.current_stream(dev)
-    for _ in range(8):
-        call("sv_lstm_step_fwd", ptr(hprev), ptr(whh), ptr(gates), ptr(cprev), ptr(c_t), ptr(h_t), B, H, stream_of(gates))
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(reps):
-        call("sv_lstm_step_fwd", ptr(hprev), ptr(whh), ptr(gates), ptr(cprev), ptr(c_t), ptr(h_t), B, H, stream_of(gates))
-    e1.record(s)
-    e1.synchronize()
-    return e0.elapsed_time(e1) / reps, 2.0 * B * H * 4 * H
+class Ctx:
+    def __init__(self, world, rank, dev):
+        self.world, self.rank, self.dev = world, rank, dev
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(self, v):
+        if self.world == 1:
+            return v
+        t = torch.tensor([v], device=self.dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t)
 
 
-def time_gemm_kernel(M, N, K, dev, reps=5):
-    """Average duration of the dominant kernel by total time, gemm_km_kernel<128,128> at the
-    K1 shape of layers 1-2 (x W_ih^T: M = T*B, N = 4H, K = H), HIP events on its stream."""
-    from pytorch_speaker_verification_amd._lib import call, ptr, stream_of
-    g = torch.Generator(device="cpu").manual_seed(8)
-    A = torch.randn(M, K, generator=g).to(dev)
-    Bm = (torch.randn(N, K, generator=g) * 0.03).to(dev)
-    C = torch.empty(M, N, device=dev)
-    s = torch.cuda.current_stream(dev)
-    f = lambda: call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, None,  # noqa: E731
-                     stream_of(C))
-    f()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(reps):
-        f()
-    e1.record(s)
-    e1.synchronize()
-    return e0.elapsed_time(e1) / reps, 2.0 * M * N * K, 4.0 * (M * K + N * K + M * N)
+_T0 = time.perf_counter()
+
+
+def log(msg):
+    """Progress to stderr (rank 0), so a long run is visibly alive."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+def _events(n):
+    """Timing events with their native HIP event materialised (torch creates it lazily, at the
+    first record; the C ABI records them itself)."""
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
+    for e in evs:
+        e.record()
+    return evs
+
+
+def run_steps(ctx, N, M, T, precision, steps, warmup, seed, probe=None, products="mfma_f32"):
+    """Time `steps` fused training steps of this rank's N x M batch.  probe = None, "fwd_bwd"
+    (bf16: events around each layer's persistent recurrences) or "bwd_chunks" (fp32: events
+    around each chunk of K3 launches).  Returns (max-over-ranks seconds, loss, host enqueue s,
+    per-step probe event lists, trainer)."""
+    from pytorch_speaker_verification_amd.ops import PIPELINE_CHUNK
+    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+    log(f"run N={N} M={M} T={T} {precision} {products} steps={steps} warmup={warmup}")
+    net, ge2e = build_model(DIMS, ctx.dev)
+    net.precision = precision
+    net.f32_products = products
+    tr = GE2ETrainer(net, ge2e, lr=0.01)
+    g = torch.Generator(device="cpu").manual_seed(seed + ctx.rank)
+    x = torch.randn(N * M, T, DIMS[0], generator=g).to(ctx.dev)
+    for _ in range(warmup):
+        tr.step(x, N, M)
+    L = DIMS[2]
+    nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
+    probes = []
+    for _ in range(steps if probe else 0):
+        if probe == "fwd_bwd":
+            probes.append({"fwd": _events(2 * L), "bwd": _events(2 * L)})
+        else:
+            probes.append({"bwd": _events(2 * L * nch)})
+    ctx.barrier()
+    t0 = time.perf_counter()
+    host = 0.0
+    for k in range(steps):
+        th = time.perf_counter()
+        loss = tr.step(x, N, M, probe=probes[k] if probe else None)
+        host += time.perf_counter() - th
+    ctx.barrier()
+    dt = ctx.max_over_ranks(time.perf_counter() - t0)
+    tr.check()  # raises if a persistent recurrence timed out during the timed steps
+    log(f"  {dt / steps * 1e3:.3f} ms/step")
+    return dt, float(loss), host, probes, tr
+
+
+def probe_ms(probes, key):
+    """Sum over the (before, after) event pairs of one step's probe list, averaged over steps."""
+    tot = 0.0
+    for p in probes:
+        ev = p[key]
+        tot += sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(len(ev) // 2))
+    return tot / max(1, len(probes))
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/), corrected as
-    MI355X_MICROARCH.md prescribes: FETCH_SIZE x 2 (gfx950 halves wide streaming reads) +
-    WRITE_SIZE, both in KiB."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json),
+    corrected as MI355X_MICROARCH.md prescribes (FETCH_SIZE x 2 + WRITE_SIZE, both KiB)."""
     try:
-        with open(path) as f:
-            d = json.load(f)
-        return d[kernel]["hbm_bytes_per_launch"]
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            return json.load(f)[kernel]["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         return None
 
@@ -125,10 +175,35 @@ def _timed(f, dev, reps):
     return e0.elapsed_time(e1) / reps
 
 
+def time_step_kernel(B, H, dev, reps=64):
+    """K2 (fp32 forward recurrent step) in isolation, HIP events on its stream."""
+    from pytorch_speaker_verification_amd._lib import call, ptr, stream_of
+    g = torch.Generator(device="cpu").manual_seed(7)
+    whh = (torch.randn(4 * H, H, generator=g) * 0.02).to(dev)
+    hprev, cprev = torch.randn(B, H, generator=g).to(dev), torch.randn(B, H, generator=g).to(dev)
+    gates = torch.randn(B, 4 * H, generator=g).to(dev)
+    c_t, h_t = torch.empty(B, H, device=dev), torch.empty(B, H, device=dev)
+    f = lambda: call("sv_lstm_step_fwd", ptr(hprev), ptr(whh), ptr(gates), ptr(cprev), ptr(c_t), ptr(h_t), B, H,  # noqa
+                     stream_of(gates))
+    return _timed(f, dev, reps), 2.0 * B * H * 4 * H
+
+
+def time_gemm_kernel(M, N, K, dev, reps=5):
+    """gemm_km_kernel<128,128> at the K1 shape of layers 1-2 in isolation, HIP events on its stream."""
+    from pytorch_speaker_verification_amd._lib import call, ptr, stream_of
+    g = torch.Generator(device="cpu").manual_seed(8)
+    A = torch.randn(M, K, generator=g).to(dev)
+    Bm = (torch.randn(N, K, generator=g) * 0.03).to(dev)
+    C = torch.empty(M, N, device=dev)
+    f = lambda: call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, None, 0,  # noqa
+                     stream_of(C))
+    return _timed(f, dev, reps), 2.0 * M * N * K, 4.0 * (M * K + N * K + M * N)
+
+
 def hbm_kernels(tr, N, M, D, dev, reps=50):
-    """The HBM-bound kernels of the step, HIP events on their stream:
-    GE2E fwd+bwd (algorithmic bytes 3*B*D*4: read E twice, write dE) and clip+SGD over the
-    flat parameter buffer (read g, read p, write p)."""
+    """The HBM-bound kernels of the step: GE2E fwd+bwd (algorithmic bytes 3*B*D*4)
+    and clip+SGD over the flat parameter buffer (read g, read p, write p)."""
+    from pytorch_speaker_verification_amd.ops import clip_sgd_step_
     g = torch.Generator(device="cpu").manual_seed(9)
     E = torch.nn.functional.normalize(torch.randn(N, M, D, generator=g), dim=2).to(dev)
     w, b = tr.loss_mod.w, tr.loss_mod.b
@@ -140,7 +215,6 @@ def hbm_kernels(tr, N, M, D, dev, reps=50):
     by_ge = 3.0 * N * M * D * 4
     n = tr.n_pad
     pc, gc = tr.flat_p[:n].clone(), tr.flat_g[:n].clone().mul_(1e-3)
-    from pytorch_speaker_verification_amd.ops import clip_sgd_step_
     ms_cl = _timed(lambda: clip_sgd_step_(pc, gc, 3.0, 0.0, False), dev, reps)
     by_cl = 3.0 * n * 4
     r = lambda by, ms: round(by / (ms * 1e-3) / 1e9, 1)  # noqa: E731
@@ -167,12 +241,12 @@ def _ge2e_torch(E, w, b):
     return (torch.log(torch.exp(S).sum(2) + 1e-6) - pos).sum()
 
 
-def vendor_baseline(dims, N, M, T, dev, steps=3, dtype="f32"):
+def vendor_baseline(N, M, T, dev, steps=3, dtype="f32"):
     """Stock torch-ROCm on the same GPU: nn.LSTM (MIOpen RNN) + Linear + torch GE2E, autograd,
     clip_grad_norm_ x2, SGD -- the reference's training step run by the vendor libraries.
-    dtype bf16: the LSTM and projection run entirely in bf16 (weights, states and gradients;
-    a lower precision than this repo's bf16 path, which keeps cell state and gradients fp32)."""
-    F, H, L, P = dims
+    dtype bf16: the LSTM and projection run entirely in bf16 (a lower precision than this
+    repo's bf16 path, which keeps cell state and gradients fp32)."""
+    F, H, L, P = DIMS
     try:
         torch.manual_seed(0)
         wdt = torch.bfloat16 if dtype == "bf16" else torch.float32
@@ -204,8 +278,7 @@ def vendor_baseline(dims, N, M, T, dev, steps=3, dtype="f32"):
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
         return {"value": round(N * M / dt, 3), "unit": "embeddings/s", "ms_per_step": round(dt * 1e3, 3),
-                "kind": f"torch-rocm nn.LSTM (MIOpen) + autograd, {dtype}, same GPU",
-                "torch": torch.__version__}
+                "kind": f"torch-rocm nn.LSTM (MIOpen) + autograd, {dtype}, same GPU", "torch": torch.__version__}
     except Exception as ex:  # report, never fail the bench on the vendor leg
         return {"error": f"{type(ex).__name__}: {ex}"[:300]}
 
@@ -214,7 +287,7 @@ def f32_product_accuracy(dev, M=512, N=1024, K=768):
     """Max error of one fp32 GEMM (K1 shape family) against fp64, per product mode, relative to
     |A||B|^T -- the accuracy evidence for the bf16x6 mode."""
     from pytorch_speaker_verification_amd._lib import call, ptr, stream_of
-    from pytorch_speaker_verification_amd.ops import set_f32_products
+    from pytorch_speaker_verification_amd.ops import F32_PRODUCT_MODES
     g = np.random.default_rng(11)
     A = g.standard_normal((M, K)).astype(np.float32)
     B = g.standard_normal((N, K)).astype(np.float32)
@@ -222,13 +295,11 @@ def f32_product_accuracy(dev, M=512, N=1024, K=768):
     scale = np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64).T
     At, Bt = torch.tensor(A, device=dev), torch.tensor(B, device=dev)
     out = {}
-    for mode in ("mfma_f32", "bf16x6"):
-        prev = set_f32_products(mode)
+    for mode, code in F32_PRODUCT_MODES.items():
         C = torch.empty(M, N, device=dev)
-        call("sv_gemm_f32", 1, 1, M, N, K, ptr(At), K, ptr(Bt), K, ptr(C), N, None, None, 0.0, None, 0, stream_of(C))
+        call("sv_gemm_f32", 1, 1, M, N, K, ptr(At), K, ptr(Bt), K, ptr(C), N, None, None, 0.0, None, code, stream_of(C))
         err = np.abs(C.cpu().numpy().astype(np.float64) - ref) / scale
         out[mode] = {"max": float(err.max()), "mean": float(err.mean())}
-        set_f32_products(prev)
     return out
 
 
@@ -243,30 +314,81 @@ def _cpu_model():
     return None
 
 
-def cpu_baseline(dims, N, M, T, seconds_budget=25.0):
-    """The reference's CPU path (stock PyTorch port, oracle/torch_port.py) on host cores,
-    one full training step of the same workload (bounded sample)."""
+def cpu_share():
+    """CPUs this job may actually use: the cgroup CPU quota (cpu.max) when one is set -- on the
+    GPU box the host grants each GPU job a share of its cores this way, while the affinity mask
+    and os.cpu_count() show the whole machine -- else the affinity mask."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
+def cpu_baseline(N, M, T, reps=3):
+    """The reference's CPU path (stock PyTorch port, oracle/torch_port.py) on every host CPU this
+    job may use (cpu_share: the cgroup quota the host grants it), median of `reps` full training
+    steps of the same workload, plus the c1 config (N=4 x M=5)."""
     from oracle import torch_port
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads, aff, quota = cpu_share()
     torch.set_num_threads(threads)
-    torch.manual_seed(0)
-    net = torch_port.SpeechEmbedderPort(*dims)
-    w = torch.nn.Parameter(torch.tensor(10.0))
-    b = torch.nn.Parameter(torch.tensor(-5.0))
-    opt = torch.optim.SGD([{"params": net.parameters()}, {"params": [w, b]}], lr=0.01)
-    g = torch.Generator().manual_seed(1235)
-    # warm oneDNN on a small batch first
-    xw = torch.randn(4 * 2, 16, dims[0], generator=g)
-    torch_port.train_step(net, w, b, opt, xw, 4, 2)
-    x = torch.randn(N * M, T, dims[0], generator=g)
-    t0 = time.perf_counter()
-    torch_port.train_step(net, w, b, opt, x, N, M)
-    dt = time.perf_counter() - t0
+
+    def one(Nc, Mc, Tc, r):
+        torch.manual_seed(0)
+        net = torch_port.SpeechEmbedderPort(*DIMS)
+        w = torch.nn.Parameter(torch.tensor(10.0))
+        b = torch.nn.Parameter(torch.tensor(-5.0))
+        opt = torch.optim.SGD([{"params": net.parameters()}, {"params": [w, b]}], lr=0.01)
+        g = torch.Generator().manual_seed(1235)
+        torch_port.train_step(net, w, b, opt, torch.randn(8, 16, DIMS[0], generator=g), 4, 2)  # warm oneDNN
+        x = torch.randn(Nc * Mc, Tc, DIMS[0], generator=g)
+        ts = []
+        for _ in range(r):
+            t0 = time.perf_counter()
+            torch_port.train_step(net, w, b, opt, x, Nc, Mc)
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)), ts
+    log(f"cpu baseline on {threads} threads")
+    dt, ts = one(N, M, T, reps)
+    dt1, _ = one(4, 5, 160, 5)
+    log(f"  cpu {dt:.2f} s/step, c1 {dt1:.3f} s/step")
     return {"value": round(N * M / dt, 3), "unit": "embeddings/s", "cores": threads, "kind": "port",
-            "cpu_model": _cpu_model(),
+            "host_cpus": os.cpu_count(), "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+            "torch_threads": torch.get_num_threads(), "cpu_model": _cpu_model(),
             "steps_per_sec": round(1.0 / dt, 5), "sec_per_step": round(dt, 3),
-            "sample": f"1 full training step (fwd+GE2E+bwd+clip+SGD) of N={N}xM={M}, T={T}, fp32, "
-                      f"oracle/torch_port.py (nn.LSTM on oneDNN), {threads} threads"}
+            "sec_per_step_samples": [round(t, 3) for t in ts],
+            "c1": {"workload": "N=4xM=5, T=160, fp32 (BASELINE configs[0])", "sec_per_step": round(dt1, 4),
+                   "value": round(20 / dt1, 2), "unit": "embeddings/s"},
+            "sample": f"median of {reps} full training steps (fwd+GE2E+bwd+clip+SGD) of N={N}xM={M}, T={T}, fp32, "
+                      f"oracle/torch_port.py (nn.LSTM on oneDNN) on {threads} threads = every CPU this job may use "
+                      f"(cgroup quota {quota}, affinity {aff}, host {os.cpu_count()}); c1: median of 5"}
+
+
+def _launch_ranks(args):
+    """--gpus N without an external launcher: start N ranks (torch.distributed.run) as a child
+    process before this process initialises the GPU, and return its exit code."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def roofline_entry(kernel, flops, ms, peak, traffic, launches, note):
+    ach = flops / (ms * 1e-3) / 1e12
+    return {"kernel": kernel, "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4), "traffic": traffic, "avg_launch_us": round(ms * 1e3, 2),
+            "flops_per_launch": flops, "launches_timed": launches, "timing": note}
 
 
 def main():
@@ -279,178 +401,170 @@ def main():
     ap.add_argument("--T", type=int, default=160)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fwd-steps", type=int, default=5)
-    ap.add_argument("--no-bf16", action="store_true", help="skip the config-c3 (bf16 operands) side measurement")
+    ap.add_argument("--no-bf16", action="store_true", help="skip the bf16 side measurements (c3/c4/c5)")
     ap.add_argument("--no-f32x", action="store_true", help="skip the fp32-via-bf16x6 side measurement")
-    ap.add_argument("--preset", choices=["c2", "c3", "c5"], default=None,
-                    help="BASELINE config per GPU: c2 = N64 M10 T160 f32, c3 = the same in bf16, "
-                         "c5 = N256/8 GPUs -> 32 speakers per GPU, M10, T180, bf16")
     ap.add_argument("--no-vendor", action="store_true", help="skip the nn.LSTM/MIOpen same-GPU baseline")
-    ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32",
-                    help="precision of the headline line (default f32 = BASELINE configs[1]; bf16 = configs[2])")
+    ap.add_argument("--preset", choices=["c2", "c3", "c4", "c5"], default=None,
+                    help="headline config: c2 = N64 M10 T160 f32 per GPU (default), c3 = the same in bf16, "
+                         "c4 = N64 M10 T160 bf16 split over the GPUs (strong scaling), c5 = N256 M10 T180 bf16 "
+                         "split over the GPUs")
+    ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32")
     args = ap.parse_args()
-    if args.preset == "c3":
-        args.dtype = "bf16"
-    elif args.preset == "c5":
-        args.N, args.M, args.T, args.dtype = 32, 10, 180, "bf16"
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    ctx = Ctx(world, rank, dev)
+    F, H, L, P = DIMS
 
-    from pytorch_speaker_verification_amd.ops import embedder_forward, embedder_forward_bf16
-    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
-
-    dims = (40, 768, 3, 256)
-    N, M, T = args.N, args.M, args.T
+    # ---- headline -------------------------------------------------------------------------
+    strong = args.preset in ("c4", "c5")
+    dtype = "bf16" if args.preset in ("c3", "c4", "c5") else args.dtype
+    if args.preset == "c5":
+        Ng, M, T = 256, 10, 180
+    else:
+        Ng, M, T = args.N, args.M, args.T
+    N = max(1, Ng // world) if strong else Ng
     B = N * M
-    net, ge2e = build_model(dims, dev)
-    net.precision = args.dtype
-    tr = GE2ETrainer(net, ge2e, lr=0.01)
-    g = torch.Generator(device="cpu").manual_seed(1234 + 1 + rank)   # SURVEY §8d seed 1234 + config index
-    x = torch.randn(B, T, dims[0], generator=g).to(dev)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        tr.step(x, N, M)
-    barrier()
-    t0 = time.perf_counter()
-    host_s = 0.0
-    for _ in range(args.steps):
-        th = time.perf_counter()
-        loss = tr.step(x, N, M)
-        host_s += time.perf_counter() - th
-    barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t)
-    final_loss = float(loss)
-
-    # forward-only (inference) embeddings/s
-    layers = net.LSTM_stack.layer_params()
-    fwd_fn = embedder_forward_bf16 if args.dtype == "bf16" else embedder_forward
-    with torch.no_grad():
-        for _ in range(2):
-            fwd_fn(x, layers, net.projection.weight, net.projection.bias, save=False)
-        barrier()
-        tf0 = time.perf_counter()
-        for _ in range(args.fwd_steps):
-            fwd_fn(x, layers, net.projection.weight, net.projection.bias, save=False)
-        barrier()
-        tf = (time.perf_counter() - tf0) / args.fwd_steps
-
-    fwd_fl, st_fl = step_flops(B, T, dims[0], dims[1], dims[3], dims[2])
+    dt, loss, host, probes, tr = run_steps(ctx, N, M, T, dtype, args.steps, args.warmup, 1235,
+                                           probe="bwd_chunks" if dtype == "f32" else "fwd_bwd")
     ms_step = dt / args.steps * 1e3
+    fwd_fl, st_fl = step_flops(B, T, F, H, P, L)
+    peak = MI355X_FP32_MFMA_TFLOPS if dtype == "f32" else MI355X_BF16_MFMA_TFLOPS
+    emb_total = world * B
     out = {
-        "metric": "embeddings/sec + GE2E steps/sec at N=64×M=10, 1/2/4/8 MI355X",
-        "value": round(world * B * args.steps / dt, 3),
+        "metric": METRIC,
+        "value": round(emb_total * args.steps / dt, 3),
         "unit": "embeddings/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
-        "dtype": args.dtype,
+        "dtype": dtype,
         "data": "synthetic x~N(0,1) frames, reference init (torch.manual_seed(0))",
-        "config": {"workload": f"GE2E train step N={N}xM={M} per GPU, T={T}, 40 mels, LSTM 3x768, proj 256",
-                   "global_batch": world * B, "speakers_global": world * N, "seq_len": T,
+        "config": {"workload": (f"GE2E train step, global N={N * world}xM={M} split over {world} GPU(s)" if strong else
+                                f"GE2E train step N={N}xM={M} per GPU") + f", T={T}, 40 mels, LSTM 3x768, proj 256",
+                   "preset": args.preset or ("c3" if dtype == "bf16" else "c2"),
+                   "global_batch": emb_total, "speakers_global": N * world, "per_gpu_batch": B, "seq_len": T,
                    "parallelism": f"dp{world} (speaker-sharded GE2E, RCCL grad all-reduce)"},
         "steps_per_sec": round(args.steps / dt, 4),
-        "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 3),
-        "fwd_embeddings_per_sec": round(world * B / tf, 1),
-        "loss": round(final_loss, 5),
-        "step_tflops": round(st_fl / (ms_step * 1e-3) / 1e12, 2),
-        "step_mfma_frac": round(st_fl / (ms_step * 1e-3) / 1e12 /
-                                (MI355X_FP32_MFMA_TFLOPS if args.dtype == "f32" else MI355X_BF16_MFMA_TFLOPS), 4),
+        "host_enqueue_ms_per_step": round(host / args.steps * 1e3, 3),
+        "loss": round(loss, 5),
+        "step_tflops_per_gpu": round(st_fl / (ms_step * 1e-3) / 1e12, 2),
+        "step_mfma_frac": round(st_fl / (ms_step * 1e-3) / 1e12 / peak, 4),
     }
-    if not args.no_f32x and args.dtype == "f32":
-        # the same fp32 step with bf16x6 products (opt-in mode; exact-fp32 MFMA is the headline)
-        from pytorch_speaker_verification_amd.ops import set_f32_products
-        prev = set_f32_products("bf16x6")
-        try:
-            netx, gex = build_model(dims, dev)
-            trx = GE2ETrainer(netx, gex, lr=0.01)
-            for _ in range(args.warmup):
-                trx.step(x, N, M)
-            barrier()
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                lx = trx.step(x, N, M)
-            barrier()
-            dx_ = time.perf_counter() - t0
-            if world > 1:
-                t = torch.tensor([dx_], device=dev, dtype=torch.float64)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                dx_ = float(t)
-        finally:
-            set_f32_products(prev)
-        msx = dx_ / args.steps * 1e3
-        out["f32_bf16x6"] = {"config": "same workload, fp32 products formed as six bf16 MFMA products of a three-way "
-                                       "bf16 split (fp32 accumulation); opt-in via set_f32_products('bf16x6')",
-                             "value": round(world * B * args.steps / dx_, 3), "unit": "embeddings/s",
-                             "ms_per_step": round(msx, 3), "loss": round(float(lx), 5)}
-        if rank == 0:
-            out["f32_bf16x6"]["gemm_error_vs_fp64"] = f32_product_accuracy(dev)
-    if not args.no_bf16 and args.dtype == "f32":
-        # BASELINE config c3: same workload, bf16 GEMM operands (fp32 accumulate/state/loss)
-        net16, ge16 = build_model(dims, dev)
-        net16.precision = "bf16"
-        tr16 = GE2ETrainer(net16, ge16, lr=0.01)
-        for _ in range(args.warmup):
-            tr16.step(x, N, M)
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            l16 = tr16.step(x, N, M)
-        barrier()
-        d16 = time.perf_counter() - t0
+    if dtype == "f32":
+        # K3, the headline step's dominant kernel: per-chunk HIP-event spans on its own stream over
+        # the timed steps / its L*T launches per step
+        ms_k3 = probe_ms(probes, "bwd") / (L * T)
+        out["roofline"] = roofline_entry(
+            "lstm_step_bwd_v2_kernel (K3, fp32 MFMA 32x32x2, backward recurrent step)", 2.0 * B * H * 4 * H, ms_k3,
+            MI355X_FP32_MFMA_TFLOPS, pmc_traffic("lstm_step_bwd_v2_kernel"), L * T * args.steps,
+            "in-step: HIP events recorded on the recurrence's stream around each 32-step chunk of K3 launches inside "
+            "the timed steps (sum of chunk spans / launches; includes the inter-launch gaps of the chunk)")
+    else:
+        fl = 2.0 * B * T * H * 4 * H
+        out["roofline"] = roofline_entry(
+            "lstm_persist2_bwd_bf16_kernel (persistent backward recurrence, one launch per layer, bf16 MFMA)", fl,
+            probe_ms(probes, "bwd") / L, MI355X_BF16_MFMA_TFLOPS, pmc_traffic("lstm_persist2_bwd_bf16_kernel"),
+            L * args.steps, "in-step: HIP events around each layer's launch inside the timed steps")
+        out["roofline_fwd"] = roofline_entry(
+            "lstm_persist2_fwd_bf16_kernel (persistent forward recurrence)", fl, probe_ms(probes, "fwd") / L,
+            MI355X_BF16_MFMA_TFLOPS, pmc_traffic("lstm_persist2_fwd_bf16_kernel"), L * args.steps,
+            "in-step, as roofline")
+
+    # forward-only (inference) embeddings/s at the headline shape
+    from pytorch_speaker_verification_amd.ops import embedder_forward, embedder_forward_bf16
+    g = torch.Generator(device="cpu").manual_seed(1235 + rank)
+    x = torch.randn(B, T, F, generator=g).to(dev)
+    net = tr.net
+    layers = net.LSTM_stack.layer_params()
+    fwd_fn = embedder_forward_bf16 if dtype == "bf16" else embedder_forward
+    with torch.no_grad():
+        for _ in range(2):
+            fwd_fn(x, layers, net.projection.weight, net.projection.bias, save=False)
+        ctx.barrier()
+        tf0 = time.perf_counter()
+        for _ in range(args.fwd_steps):
+            fwd_fn(x, layers, net.projection.weight, net.projection.bias, save=False)
+        ctx.barrier()
+        tf = ctx.max_over_ranks((time.perf_counter() - tf0) / args.fwd_steps)
+    out["fwd_embeddings_per_sec"] = round(emb_total / tf, 1)
+
+    # ---- side measurements ----------------------------------------------------------------
+    def side(name, Nl, Ml, Tl, prec, strong_, descr, probe=None, products="mfma_f32"):
+        d, l_, _, pr, _ = run_steps(ctx, Nl, Ml, Tl, prec, args.steps, args.warmup, 2235, probe=probe,
+                                    products=products)
+        ms = d / args.steps * 1e3
+        _, fl = step_flops(Nl * Ml, Tl, F, H, P, L)
+        tot = Nl * Ml * world
+        o = {"config": descr, "value": round(tot * args.steps / d, 3), "unit": "embeddings/s",
+             "ms_per_step": round(ms, 3), "steps_per_sec": round(args.steps / d, 4), "loss": round(l_, 5),
+             "scaling": "strong" if strong_ else "weak", "per_gpu_batch": Nl * Ml, "seq_len": Tl,
+             "step_tflops_per_gpu": round(fl / (ms * 1e-3) / 1e12, 2),
+             "step_mfma_frac": round(fl / (ms * 1e-3) / 1e12 /
+                                     (MI355X_FP32_MFMA_TFLOPS if prec == "f32" else MI355X_BF16_MFMA_TFLOPS), 4)}
+        out[name] = o
+        return o, pr
+
+    if not args.no_bf16 and args.preset is None and dtype == "f32":
+        o, pr = side("bf16", N, M, T, "bf16", False, "c3: the headline workload with bf16 GEMM operands, fp32 "
+                     "accumulate/state/loss", probe="fwd_bwd")
+        fl = 2.0 * B * T * H * 4 * H
+        out["roofline_bf16"] = roofline_entry(
+            "lstm_persist2_bwd_bf16_kernel (c3's dominant kernel: persistent backward recurrence)", fl,
+            probe_ms(pr, "bwd") / L, MI355X_BF16_MFMA_TFLOPS, pmc_traffic("lstm_persist2_bwd_bf16_kernel"),
+            L * args.steps, "in-step: HIP events around each layer's launch inside the timed c3 steps")
+        out["roofline_bf16_fwd"] = roofline_entry(
+            "lstm_persist2_fwd_bf16_kernel (persistent forward recurrence)", fl, probe_ms(pr, "fwd") / L,
+            MI355X_BF16_MFMA_TFLOPS, pmc_traffic("lstm_persist2_fwd_bf16_kernel"), L * args.steps, "in-step")
         if world > 1:
-            t = torch.tensor([d16], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            d16 = float(t)
-        ms16 = d16 / args.steps * 1e3
-        out["bf16"] = {"config": "c3: same workload, bf16 GEMM operands, fp32 accumulate/state/loss",
-                       "value": round(world * B * args.steps / d16, 3), "unit": "embeddings/s",
-                       "ms_per_step": round(ms16, 3), "steps_per_sec": round(args.steps / d16, 4),
-                       "loss": round(float(l16), 5),
-                       "step_tflops": round(st_fl / (ms16 * 1e-3) / 1e12, 2),
-                       "step_mfma_frac": round(st_fl / (ms16 * 1e-3) / 1e12 / MI355X_BF16_MFMA_TFLOPS, 4)}
+            side("c4", max(1, 64 // world), 10, 160, "bf16", True,
+                 f"c4: N=64xM=10, T=160, bf16, split over {world} GPUs ({max(1, 64 // world)} speakers per rank); "
+                 "value = 640 embeddings per step / time")
+            side("c5", max(1, 256 // world), 10, 180, "bf16", True,
+                 f"c5: N=256xM=10, T=180, bf16, split over {world} GPUs ({max(1, 256 // world)} speakers per rank)")
+        else:
+            side("c4_rank_shape", 8, 10, 160, "bf16", True,
+                 "one rank's share of c4 at 8 GPUs (N=8xM=10, T=160, bf16) run alone on this GPU: the per-rank "
+                 "step time of the 8-GPU strong-scaling config (value counts this GPU's 80 embeddings)")
+            side("c5_rank_shape", 32, 10, 180, "bf16", True,
+                 "one rank's share of c5 at 8 GPUs (N=32xM=10, T=180, bf16) run alone on this GPU")
+    if not args.no_f32x and dtype == "f32" and world == 1:
+        o, _ = side("f32_bf16x6", N, M, T, "f32", False,
+                    "same workload, fp32 products formed as six bf16 MFMA products of a three-way bf16 split (fp32 "
+                    "accumulation); opt-in per module: net.f32_products = 'bf16x6'", products="bf16x6")
+        o["gemm_error_vs_fp64"] = f32_product_accuracy(dev)
     if rank == 0:
-        H = dims[1]
-        ms_g, fl_g, by_g = time_gemm_kernel(T * B, 4 * H, H, dev)
-        ach = fl_g / (ms_g * 1e-3) / 1e12
-        out["roofline"] = {"kernel": "gemm_km_kernel<128,128> (K1/dW/dx NT GEMM, fp32 MFMA 32x32x2), K1 shape "
-                                     f"M={T * B} N={4 * H} K={H}",
-                           "bound": "mfma", "achieved": round(ach, 2), "peak": MI355X_FP32_MFMA_TFLOPS,
-                           "unit": "TFLOP/s", "frac": round(ach / MI355X_FP32_MFMA_TFLOPS, 4),
-                           "traffic": pmc_traffic("gemm_km_kernel<128,128>"), "algorithmic_bytes": by_g,
-                           "avg_launch_us": round(ms_g * 1e3, 2), "flops_per_launch": fl_g}
-        ms_k, fl_k = time_step_kernel(B, H, dev)
-        ach_k = fl_k / (ms_k * 1e-3) / 1e12
-        out["roofline_step_kernel"] = {"kernel": "lstm_step_fwd_v2_kernel (K2, fp32 MFMA 32x32x2)", "bound": "mfma",
-                                       "achieved": round(ach_k, 2), "peak": MI355X_FP32_MFMA_TFLOPS,
-                                       "unit": "TFLOP/s", "frac": round(ach_k / MI355X_FP32_MFMA_TFLOPS, 4),
-                                       "traffic": pmc_traffic("lstm_step_fwd_v2_kernel"),
-                                       "avg_launch_us": round(ms_k * 1e3, 2), "flops_per_launch": fl_k}
-        if world == 1:  # (the GE2E leg would issue collectives on rank 0 alone otherwise)
-            out["hbm_kernels"] = hbm_kernels(tr, N, M, dims[3], dev)
-        if not args.no_vendor and world == 1:
-            out["vendor_baseline"] = vendor_baseline(dims, N, M, T, dev, dtype=args.dtype)
-            if "bf16" in out:
-                out["bf16"]["vendor_baseline"] = vendor_baseline(dims, N, M, T, dev, dtype="bf16")
-        if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(dims, N, M, T)
+        ms_g, fl_g, by_g = time_gemm_kernel(160 * 640, 4 * H, H, dev)
+        out["roofline_gemm"] = dict(roofline_entry(
+            f"gemm_km_kernel<128,128> (K1/dW/dx NT GEMM, fp32 MFMA 32x32x2), K1 shape M={160 * 640} N={4 * H} K={H}",
+            fl_g, ms_g, MI355X_FP32_MFMA_TFLOPS, pmc_traffic("gemm_km_kernel<128,128>"), 5,
+            "isolated launches, HIP events on its stream"), algorithmic_bytes=by_g)
+        ms_k, fl_k = time_step_kernel(640, H, dev)
+        out["roofline_step_kernel"] = roofline_entry(
+            "lstm_step_fwd_v2_kernel (K2, fp32 forward recurrent step) at B=640", fl_k, ms_k,
+            MI355X_FP32_MFMA_TFLOPS, pmc_traffic("lstm_step_fwd_v2_kernel"), 64, "isolated launches")
+        if world == 1:
+            log("hbm kernels / vendor baseline")
+            out["hbm_kernels"] = hbm_kernels(tr, N, M, P, dev)
+            if not args.no_vendor:
+                out["vendor_baseline"] = vendor_baseline(N, M, T, dev, dtype=dtype)
+                if "bf16" in out:
+                    out["bf16"]["vendor_baseline"] = vendor_baseline(N, M, T, dev, dtype="bf16")
+            if not args.no_cpu_baseline:
+                out["cpu_baseline"] = cpu_baseline(N, M, T)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

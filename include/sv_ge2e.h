@@ -90,14 +90,16 @@ size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H);
  * side[L + l] beside the recurrence, then the bias row sums.  side: 2*L caller streams.
  * xT/ld_xT: per-layer transposed inputs; dx[l] [T,B,H] for l > 0;
  * ev = L*ceil(T/chunk) + L + 1 caller events (ev[L*nch + l] = layer l's gradients done);
- * joins back into `main`. */
+ * joins back into `main`.  probe (may be NULL): 2*L*ceil(T/chunk) caller events recorded on the
+ * layer's stream around each chunk's recurrent-step (K3) launches, probe[2(l nch + c)] before,
+ * [+1] after -- in-step kernel timing for the bench's roofline. */
 size_t sv_lstm_stack_bwd_workspace(int L, int T, int B, int F, int H);
 int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float* const* xT, const long* ld_xT,
                       const float* const* w_ih, const float* const* w_hh, const float* const* gates,
                       const float* const* c_tm, const float* const* hT, const float* dh_last, float* const* dgates,
                       float* const* dgT, float* const* dx, float* const* dw_ih, float* const* dw_hh,
                       float* const* db_ih, float* const* db_hh, float* workspace, int chunk, hipStream_t main,
-                      const hipStream_t* side, hipEvent_t* ev, int products);
+                      const hipStream_t* side, hipEvent_t* ev, int products, hipEvent_t* probe);
 /* xT: the layer input transposed, [F, >= T*Bp] with row stride ld_xT (layer 0: the frames;
  * layer l > 0: hT of layer l-1 offset by Bp columns).  hT: this layer's [H, (T+1)Bp] from the fwd.
  * dh_up: gradient w.r.t. this layer's outputs; dh_up_full=1 -> [T,B,H], 0 -> [B,H] for t=T-1 only.
@@ -168,12 +170,14 @@ int sv_lstm_layer_fwd_bf16(const sv_bf16* x_bf, int T, int B, int F, int H, cons
                            const sv_bf16* w_hh_bf, const float* b_ih, const float* b_hh, float* gates, float* c_tm,
                            float* h_tm, sv_bf16* h_bf, sv_bf16* hT, hipStream_t stream);
 /* layer-pipelined stack forward in bf16 (as sv_lstm_stack_fwd; h_bf per layer [T+1,B,H]).
- * sync: the caller's sync block (below; required when the persistent recurrences run). */
+ * sync: the caller's sync block (below; required when the persistent recurrences run).
+ * probe (may be NULL): 2*L caller events recorded around each layer's persistent recurrence
+ * launch (before / after; only when the persistent schedule runs) -- in-step kernel timing. */
 int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* x_bf, const sv_bf16* const* w_ih_bf,
                            const sv_bf16* const* w_hh_bf, const float* const* b_ih, const float* const* b_hh,
                            float* const* gates, float* const* c_tm, float* const* h_tm, sv_bf16* const* h_bf,
                            sv_bf16* const* hT, int chunk, hipStream_t main, const hipStream_t* side,
-                           hipEvent_t* ev, void* sync);
+                           hipEvent_t* ev, void* sync, hipEvent_t* probe);
 size_t sv_lstm_layer_bwd_bf16_workspace(int T, int B, int F, int H);
 /* wihT_bf [F,4H], whhT_bf [H,4H]; dg_bf [T,B,4H] and dgT_bf [4H,T*Bp] are bf16 outputs */
 int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const sv_bf16* xT_bf, long ld_xT, const sv_bf16* wihT_bf,
@@ -183,14 +187,15 @@ int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const sv_bf16* xT_bf, lon
                            hipStream_t stream);
 
 /* layer-pipelined stack backward in bf16 (as sv_lstm_stack_bwd, 2*L side streams; fp32
- * master weights are transpose-cast per call; dg/dgT per layer bf16) */
+ * master weights are transpose-cast per call; dg/dgT per layer bf16).  probe: as the bf16 stack
+ * forward's, around each layer's persistent backward recurrence. */
 size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H);
 int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* const* xT, const long* ld_xT,
                            const float* const* w_ih, const float* const* w_hh, const float* const* gates,
                            const float* const* c_tm, const sv_bf16* const* hT, const float* dh_last,
                            sv_bf16* const* dg, sv_bf16* const* dgT, float* const* dx, float* const* dw_ih,
                            float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace, int chunk,
-                           hipStream_t main, const hipStream_t* side, hipEvent_t* ev, void* sync);
+                           hipStream_t main, const hipStream_t* side, hipEvent_t* ev, void* sync, hipEvent_t* probe);
 
 /* ---- persistent recurrences (one launch per layer for all T; sv_persist.hip).  The bf16 stack
  * forward uses them (by default when H = 768: W_hh held in registers) when the grid is

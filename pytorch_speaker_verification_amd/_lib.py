@@ -37,7 +37,8 @@ SIGNATURES = {
     "sv_lstm_stack_fwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                    _c_int, _P, _P, _P, _c_int]),
     "sv_lstm_stack_bwd_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int, _c_int]),
-    "sv_lstm_stack_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P, _c_int]),
+    "sv_lstm_stack_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P, _c_int,
+                                                                                          _P]),
     "sv_lstm_layer_bwd_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
     "sv_lstm_layer_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _P, _c_long, _P, _P, _P, _P, _P, _P, _c_int, _P,
                                    _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -62,13 +63,14 @@ SIGNATURES = {
     "sv_transpose_cast_bf16": (_c_int, [_P, _c_long, _c_int, _c_int, _P, _c_long, _P]),
     "sv_lstm_layer_fwd_bf16": (_c_int, [_P, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_lstm_stack_fwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                        _P, _c_int, _P, _P, _P, _P]),
+                                        _P, _c_int, _P, _P, _P, _P, _P]),
     "sv_lstm_layer_bwd_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
     "sv_lstm_layer_bwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _P, _c_long, _P, _P, _P, _P, _P, _P, _c_int,
                                         _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_eer_counts": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _c_int, _P, _P, _P]),
     "sv_lstm_stack_bwd_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int, _c_int]),
-    "sv_lstm_stack_bwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P, _P]),
+    "sv_lstm_stack_bwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P, _P,
+                                                                                               _P]),
     "sv_sync_size": (_c_size_t, []),
     "sv_persist_fwd_ok": (_c_int, [_c_int, _c_int]),
     "sv_persist_bwd_ok": (_c_int, [_c_int, _c_int]),

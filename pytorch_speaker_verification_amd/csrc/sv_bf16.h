@@ -270,14 +270,16 @@ int sv_persist_fwd_fusex_ok(int H, int F);
 int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates, float* c_tm, float* h_tm,
                         bf16_t* h_bf, bf16_t* hT, hipStream_t stream, unsigned* sync, int chan = 0,
                         const bf16_t* x_bf = nullptr, int F = 0, const bf16_t* wih_bf = nullptr,
-                        const float* b_ih = nullptr, const float* b_hh = nullptr);
+                        const float* b_ih = nullptr, const float* b_hh = nullptr, hipEvent_t pre = nullptr,
+                        hipEvent_t post = nullptr);
 // persistent backward recurrence of one layer (sv_persist.hip)
 extern "C" int sv_persist_bwd_ok(int B, int H);
 extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H);
 int sv_persist_bm(int B, int H, int cus);
 int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* acts, const float* c_tm,
                         const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream,
-                        unsigned* sync, float* db_ih = nullptr, float* db_hh = nullptr);
+                        unsigned* sync, float* db_ih = nullptr, float* db_hh = nullptr, hipEvent_t pre = nullptr,
+                        hipEvent_t post = nullptr);
 // CUs of the device `stream` belongs to (cached per device); dims fit co-resident on `cus` CUs
 int sv_stream_cus(hipStream_t stream);
 int sv_persist_fwd_fits(int B, int H, int cus);

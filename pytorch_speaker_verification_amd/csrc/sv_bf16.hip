@@ -808,7 +808,7 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
                                       const float* const* b_ih, const float* const* b_hh, float* const* gates,
                                       float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
                                       bf16_t* const* hT, int chunk, hipStream_t main, const hipStream_t* side,
-                                      hipEvent_t* ev, void* sync_block) {
+                                      hipEvent_t* ev, void* sync_block, hipEvent_t* probe) {
   if (L <= 0 || !x_bf || !w_ih_bf || !w_hh_bf || !gates || !c_tm || !h_tm || !h_bf || !side || !ev || chunk <= 0)
     return SV_EARG;
   unsigned* sync = reinterpret_cast<unsigned*>(sync_block);
@@ -832,14 +832,17 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
       int rc;
       if (l == 0 && sv_persist_fwd_fusex_ok(H, F)) {  // layer 0's input projection inside the recurrence
         if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, sync, 0,
-                                      x_bf, F, w_ih_bf[l], b_ih[l], b_hh[l])))
+                                      x_bf, F, w_ih_bf[l], b_ih[l], b_hh[l], probe ? probe[2 * l] : nullptr,
+                                      probe ? probe[2 * l + 1] : nullptr)))
           return rc;
         continue;
       }
       rc = sv_gemm_bf16(T * B, 4 * H, Fl, in, Fl, w_ih_bf[l], Fl, gates[l], 4L * H, b_ih[l], b_hh[l], 0.f, nullptr,
                         main);
       if (rc) return rc;
-      if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, sync)))
+      if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, sync, 0,
+                                    nullptr, 0, nullptr, nullptr, nullptr, probe ? probe[2 * l] : nullptr,
+                                    probe ? probe[2 * l + 1] : nullptr)))
         return rc;
     }
     return SV_OK;
@@ -959,7 +962,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
                                       bf16_t* const* dg, bf16_t* const* dgT, float* const* dx, float* const* dw_ih,
                                       float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace,
                                       int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev,
-                                      void* sync_block) {
+                                      void* sync_block, hipEvent_t* probe) {
   if (L <= 0 || !xT || !ld_xT || !w_ih || !w_hh || !gates || !c_tm || !hT || !dh_last || !dg || !dgT || !dx ||
       !dw_ih || !dw_hh || !db_ih || !workspace || !side || !ev || chunk <= 0)
     return SV_EARG;
@@ -993,7 +996,8 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       if ((rc = sv_persist_bwd_bf16(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1,
                                     (afr || l == 0) ? nullptr : dg[l],  // layer 0 has no dx GEMM
                                     dgT[l], dgf, main, sync, dbk ? db_ih[l] : nullptr,
-                                    dbk && db_hh ? db_hh[l] : nullptr)))
+                                    dbk && db_hh ? db_hh[l] : nullptr, probe ? probe[2 * l] : nullptr,
+                                    probe ? probe[2 * l + 1] : nullptr)))
         return rc;
       if (afr) {
         if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H, sv_stream_cus(main)), ws.wihT, 4L * H, dx[l], Fl, ws.gws, main)))

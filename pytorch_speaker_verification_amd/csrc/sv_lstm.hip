@@ -1279,7 +1279,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
                                  float* const* dgates, float* const* dgT, float* const* dx, float* const* dw_ih,
                                  float* const* dw_hh, float* const* db_ih, float* const* db_hh, float* workspace,
                                  int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev,
-                                 int products) {
+                                 int products, hipEvent_t* probe) {
   if (L <= 0 || !xT || !ld_xT || !w_ih || !w_hh || !gates || !c_tm || !hT || !dh_last || !dgates || !dgT || !dx ||
       !dw_ih || !dw_hh || !db_ih || !workspace || !side || !ev || chunk <= 0)
     return SV_EARG;
@@ -1308,6 +1308,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
     for (int c = nch - 1; c >= 0; --c) {
       const int t0 = c * chunk, t1 = std::min(T, t0 + chunk);
       if (l < L - 1 && (e = hipStreamWaitEvent(s, ev[(l + 1) * nch + c], 0)) != hipSuccess) return (int)e;
+      if (probe && (e = hipEventRecord(probe[2 * (l * nch + c)], s)) != hipSuccess) return (int)e;
       for (int t = t1 - 1; t >= t0; --t) {
         const float* up = (l == L - 1) ? (t == T - 1 ? dh_last : nullptr) : dx[l + 1] + t * BH;
         float* dcf_out = (t & 1) ? ws.dcf1 : ws.dcf0;
@@ -1317,6 +1318,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
                         dcf_out, dgT[l], (long)TBp, t, Bp, B, H);
         SV_LAUNCH_CHECK();
       }
+      if (probe && (e = hipEventRecord(probe[2 * (l * nch + c) + 1], s)) != hipSuccess) return (int)e;
       if (l > 0 && dx_side()) {  // dx on the layer's second stream: the recurrence goes on at once
         if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
         if ((e = hipStreamWaitEvent(side[L + l], ev[l * nch + c], 0)) != hipSuccess) return (int)e;

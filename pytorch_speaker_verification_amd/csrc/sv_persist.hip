@@ -888,7 +888,8 @@ int sv_persist_fwd_fusex_ok(int H, int F) { return H == 768 && F == 40 && persis
 // (layer 0, sv_persist_fwd_fusex_ok): no K1 -- the kernel forms x_t W_ih^T + b_ih + b_hh itself.
 int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates, float* c_tm, float* h_tm,
                         bf16_t* h_bf, bf16_t* hT, hipStream_t stream, unsigned* sync, int chan, const bf16_t* x_bf,
-                        int F, const bf16_t* wih_bf, const float* b_ih, const float* b_hh) {
+                        int F, const bf16_t* wih_bf, const float* b_ih, const float* b_hh, hipEvent_t pre,
+                        hipEvent_t post) {
   const int cus = sv_stream_cus(stream);
   if (!sv_persist_fwd_fits(B, H, cus)) return SV_ESHAPE;
   if (!sync || chan < 0 || chan >= SV_SYNC_CHANNELS) return SV_EARG;
@@ -909,6 +910,7 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
   }();
   const unsigned limit = persist_limit();
   const int fault = fwd_fault();
+  if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   if (wst) {
     constexpr int NS = 48, LDA = NS * 16 + 8;
     const size_t lds = (size_t)bm * LDA * 2 + (size_t)bm * (4 * BF_U + 4) * 4 + (size_t)bm * (BF_U + 8) * 2 +
@@ -936,6 +938,7 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
                        h_bf, hT, ldhT, T, Bp, B, H, cnt, status, limit, fault, dbg);
   }
   SV_LAUNCH_CHECK();
+  if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
   return SV_OK;
 }
 
@@ -989,7 +992,7 @@ extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H) {
 // dgf: sv_persist_bwd_scratch(T, B, H) bytes.  Counter channel 0 of `sync`.
 int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* acts, const float* c_tm,
                         const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream,
-                        unsigned* sync, float* db_ih, float* db_hh) {
+                        unsigned* sync, float* db_ih, float* db_hh, hipEvent_t pre, hipEvent_t post) {
   const int cus = sv_stream_cus(stream);
   if (!sv_persist_bwd_fits(B, H, cus)) return SV_ESHAPE;
   if (!dgf || ((uintptr_t)dgf & 15) || !sync) return SV_EARG;
@@ -1004,6 +1007,7 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* ac
                      : nullptr;
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)grid.y * SV_PCNT_STRIDE * sizeof(unsigned), stream);
   if (e != hipSuccess) return (int)e;
+  if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   // A-fragment prefetch depth 8 at H = 768 (measured: 4 / 16 no better)
   if (H == 768)
     launch_pbwd<48, 8>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, sync,
@@ -1015,6 +1019,7 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* ac
     launch_pbwd<4, 4>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, sync,
                       dbp);
   SV_LAUNCH_CHECK();
+  if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
   if (dbp) {
     hipLaunchKernelGGL(persist_db_finalize_kernel, dim3((4 * H + 255) / 256), dim3(256), 0, stream, dbp, (int)grid.y,
                        4 * H, db_ih, db_hh);

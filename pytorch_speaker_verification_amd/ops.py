@@ -94,6 +94,13 @@ def _parr(ts):
     return (ctypes.c_void_p * len(ts))(*[ptr(t) if t is not None else None for t in ts])
 
 
+def _evarr(events):
+    """Host array of native HIP events (timing probes), or NULL."""
+    if not events:
+        return None
+    return (ctypes.c_void_p * len(events))(*[e.cuda_event for e in events])
+
+
 def _ws(nbytes, device):
     """Workspace of at least nbytes (fp32 storage, 256-byte aligned by the allocator)."""
     n = max(1, (int(nbytes) + 3) // 4)
@@ -187,7 +194,8 @@ def embedder_forward(x, layers, w_p, b_p, save=True, products="mfma_f32"):
     return emb, st
 
 
-def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_ready=None, products="mfma_f32"):
+def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_ready=None, products="mfma_f32",
+                      probe=None):
     """Backward of embedder_forward.  ``grads`` (optional) is a list of preallocated
     output tensors in parameter order [w_ih, w_hh, b_ih, b_hh]*L + [w_p, b_p]; returns it
     (and dx [B,T,F] if need_dx).
@@ -195,7 +203,10 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
     ``grad_ready(k, event)`` (optional) is called as soon as a gradient group is enqueued:
     k = L for the projection, then k = L-1 .. 0 for the LSTM layers; ``event`` is the HIP
     event that completes it (None: the current stream).  The data-parallel trainer hangs its
-    per-layer all-reduce buckets on it so communication overlaps the rest of the BPTT."""
+    per-layer all-reduce buckets on it so communication overlaps the rest of the BPTT.
+
+    ``probe`` (optional): 2*L*ceil(T/chunk) timing events recorded around each chunk's
+    recurrent-step launches (include/sv_ge2e.h, sv_lstm_stack_bwd)."""
     prod = _products(products)
     demb = demb.contiguous()
     require_device(demb)
@@ -236,7 +247,7 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
              _parr(st.hT), ptr(dh_last), _parr(dgs), _parr(dgTs), _parr(dxs),
              _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
              _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
-             PIPELINE_CHUNK, s, sp, ep, prod)
+             PIPELINE_CHUNK, s, sp, ep, prod, _evarr(probe))
         if grad_ready:
             for l in range(L - 1, -1, -1):
                 grad_ready(l, events[L * nch + l])
@@ -275,11 +286,12 @@ def _bf(shape, dev):
     return torch.empty(shape, dtype=torch.bfloat16, device=dev)
 
 
-def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None):
+def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=None):
     """Mixed-precision forward (BASELINE config c3): bf16 GEMM operands, fp32 accumulation,
     fp32 gates / cell state / projection / norm.  Same outputs as embedder_forward.
     status: the caller's PersistStatus (sync block of the persistent recurrences); None = a
-    fresh one, checked at the next call / check_persistent_status()."""
+    fresh one, checked at the next call / check_persistent_status().  probe: 2*L timing events
+    around the layers' persistent recurrences (include/sv_ge2e.h)."""
     require_device(x, w_p, b_p, *[t for l in layers for t in l])
     B, T, F = x.shape
     H = layers[0][1].shape[1]
@@ -321,7 +333,8 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None):
         sync, own = _own_status(status, dev)
         call("sv_lstm_stack_fwd_bf16", L, T, B, F, H, ptr(x_bf), _parr([w[0] for w in wbf]),
              _parr([w[1] for w in wbf]), _parr([l[2] for l in layers]), _parr([l[3] for l in layers]),
-             _parr(gs), _parr(cs), _parr(hs), _parr(hbs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep, sync.ptr())
+             _parr(gs), _parr(cs), _parr(hs), _parr(hbs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep, sync.ptr(),
+             _evarr(probe))
         _release_status(sync, own)
     else:
         for l, (w_ih, w_hh, b_ih, b_hh) in enumerate(layers):
@@ -343,7 +356,7 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None):
     return emb, st
 
 
-def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, status=None):
+def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, status=None, probe=None):
     """Backward of embedder_forward_bf16 (same ``grads`` / ``grad_ready`` contract as
     embedder_backward; ``status`` as embedder_forward_bf16)."""
     demb = demb.contiguous()
@@ -382,7 +395,7 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
              _parr(st.hT), ptr(dh_last), _parr(dgs), _parr(dgTs), _parr(dxs),
              _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
              _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
-             PIPELINE_CHUNK, s, sp, ep, sync.ptr())
+             PIPELINE_CHUNK, s, sp, ep, sync.ptr(), _evarr(probe))
         _release_status(sync, own)
         if grad_ready:
             # the projection bucket is enqueued behind the stack backward: with the persistent

@@ -105,9 +105,12 @@ class GE2ETrainer:
         them had a persistent-recurrence timeout."""
         self.status.poll(wait=True)
 
-    def step(self, x, N, M):
+    def step(self, x, N, M, probe=None):
         """x: [N*M, T, nmels] float32 on this rank's GPU (this rank's N speakers x M
-        utterances, speaker-major).  Returns the (global) loss as a 0-dim device tensor."""
+        utterances, speaker-major).  Returns the (global) loss as a 0-dim device tensor.
+        probe (bench only): {"fwd": events, "bwd": events} timing events handed to the stack
+        forward (bf16) / backward (include/sv_ge2e.h)."""
+        probe = probe or {}
         self.status.poll()  # raises if an earlier step's recurrences timed out
         self._check_layout()
         net = self.net
@@ -117,7 +120,8 @@ class GE2ETrainer:
         bf16 = getattr(net, "precision", "f32") == "bf16"
         products = getattr(net, "f32_products", "mfma_f32")
         if bf16:
-            emb, st = embedder_forward_bf16(x.float().contiguous(), layers, w_p, b_p, status=self.status)
+            emb, st = embedder_forward_bf16(x.float().contiguous(), layers, w_p, b_p, status=self.status,
+                                            probe=probe.get("fwd"))
         else:
             emb, st = embedder_forward(x.float().contiguous(), layers, w_p, b_p, products=products)
         E = emb.view(N, M, emb.shape[1])
@@ -142,10 +146,10 @@ class GE2ETrainer:
                     works.append(dist.all_reduce(self.flat_g[lo:hi], group=self.group, async_op=True))
         if bf16:
             embedder_backward_bf16(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views, grad_ready=ready,
-                                   status=self.status)
+                                   status=self.status, probe=probe.get("bwd"))
         else:
             embedder_backward(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views, grad_ready=ready,
-                              products=products)
+                              products=products, probe=probe.get("bwd"))
         for wk in works:
             wk.wait()  # the current (main) stream waits for every bucket
         n = self.n_pad

@@ -1,0 +1,54 @@
+"""Fold rocprofv3 FETCH_SIZE / WRITE_SIZE passes (separate runs, gpurun_out/pmc_traffic/*) into
+profiles/pmc_traffic.json: per kernel family, the average HBM bytes per launch corrected as
+MI355X_MICROARCH.md prescribes (2 x FETCH_SIZE + WRITE_SIZE, counters in KiB).
+Usage: python scripts/pmc_traffic.py <dir with f32_fetch/f32_write/bf16_fetch/bf16_write csvs>"""
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAMILIES = {  # json key -> kernel-name prefix
+    "lstm_step_bwd_v2_kernel": "void lstm_step_bwd_v2_kernel<",
+    "lstm_step_fwd_v2_kernel": "void lstm_step_fwd_v2_kernel<32, 101",
+    "lstm_persist2_bwd_bf16_kernel": "void lstm_persist2_bwd_bf16_kernel<",
+    "lstm_persist2_fwd_bf16_kernel": "void lstm_persist2_fwd_bf16_kernel<48, 64, 0>",
+}
+
+
+def per_launch(path, counter):
+    acc = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        for key, pre in FAMILIES.items():
+            if r["Kernel_Name"].startswith(pre):
+                s, n = acc.get(key, (0.0, 0))
+                acc[key] = (s + float(r["Counter_Value"]), n + 1)
+    return {k: s / n for k, (s, n) in acc.items()}
+
+
+def main(d):
+    out_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    data = json.load(open(out_path)) if os.path.exists(out_path) else {}
+    for tag in ("f32", "bf16"):
+        fs = glob.glob(os.path.join(d, f"{tag}_fetch*", "**", "*counter_collection.csv"), recursive=True)
+        ws = glob.glob(os.path.join(d, f"{tag}_write*", "**", "*counter_collection.csv"), recursive=True)
+        if not fs or not ws:
+            continue
+        fetch, write = per_launch(fs[0], "FETCH_SIZE"), per_launch(ws[0], "WRITE_SIZE")
+        for k in fetch:
+            if k in write:
+                data[k] = {"FETCH_SIZE_KiB": round(fetch[k], 1), "WRITE_SIZE_KiB": round(write[k], 1),
+                           "hbm_bytes_per_launch": int(1024 * (2 * fetch[k] + write[k])),
+                           "source": f"rocprofv3 --pmc over bench.py ({tag} step, in-step launches)"}
+    data["_note"] = ("rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE in separate runs; hbm_bytes = 2*FETCH_SIZE + "
+                     "WRITE_SIZE (gfx950 halves wide reads, MI355X_MICROARCH.md §HBM); FETCH_SIZE counts L2 misses "
+                     "incl. Infinity-Cache hits.  In-step entries: scripts/gpu_pmc_traffic.sh + scripts/pmc_traffic.py")
+    json.dump(data, open(out_path, "w"), indent=1)
+    print(json.dumps({k: v.get("hbm_bytes_per_launch") for k, v in data.items() if isinstance(v, dict)}))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
