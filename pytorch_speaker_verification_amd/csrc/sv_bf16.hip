@@ -521,6 +521,15 @@ int persist_fwd(int H) {
   }();
   return v < 0 ? (H == 768) : v;
 }
+// stack forward for small batches: the layer-wavefront launch (sv_wave.hip) whenever all layers'
+// grids fit co-resident (B <= 96 at H = 768 on 256 CUs); SV_WAVE2=0 keeps one launch per layer
+int wave2_fwd() {
+  static int v = [] {
+    const char* e = getenv("SV_WAVE2");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return v;
+}
 // stack backward recurrences: one persistent launch per layer (W_hh held in registers,
 // sv_persist.hip) or per-step launches, layer-pipelined.  SV_PERSIST_BWD: unset = persistent
 // when H = 768, 1 = whenever sv_persist_bwd_ok, 0 = per-step.
@@ -818,6 +827,20 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
   const int Bp = (B + 7) & ~7;
   const long ldhT = (long)(T + 1) * Bp;
   hipError_t e;
+  if (persist_fwd(H) && wave2_fwd() && sv_wave_fwd_fits(L, B, F, H, sv_stream_cus(main))) {
+    // layer-wavefront schedule (sv_wave.hip): every layer's recurrence and input projection in
+    // one launch on `main`
+    if (!sync) return SV_EARG;
+    for (int l = 0; l < L; ++l) {
+      if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), main)) != hipSuccess) return (int)e;
+      if ((e = hipMemsetAsync(h_bf[l], 0, BH * sizeof(bf16_t), main)) != hipSuccess) return (int)e;
+      if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(bf16_t), main)) != hipSuccess)
+        return (int)e;
+    }
+    return sv_wave_fwd_bf16(L, T, B, F, H, x_bf, w_ih_bf, w_hh_bf, b_ih, b_hh, gates, c_tm, h_tm, h_bf, hT, sync, main,
+                            sv_persist_limit(), sv_persist_fault(0), probe ? probe[0] : nullptr,
+                            probe ? probe[1] : nullptr);
+  }
   if (persist_fwd(H) && sv_persist_fwd_fits(B, H, sv_stream_cus(main))) {
     if (!sync) return SV_EARG;
     // persistent schedule on `main`: per layer the whole-T K1 GEMM, then one launch for the

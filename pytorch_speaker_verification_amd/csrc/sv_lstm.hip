@@ -870,6 +870,17 @@ int dx_side() {
   return v;
 }
 
+// stack bwd: the layer's whole-T weight-gradient GEMMs on its weight-gradient stream side[L + l]
+// (created low-priority by the caller) instead of behind the recurrence on side[l]: the next
+// layer's recurrence (high-priority stream) then takes CUs ahead of them (SV_DW_LOWPRIO=1)
+int dw_lowprio() {
+  static int v = [] {
+    const char* e = getenv("SV_DW_LOWPRIO");
+    return (e && *e == '1') ? 1 : 0;
+  }();
+  return v;
+}
+
 int dw_chunked_layer(int l) {
   static int v = [] {
     const char* e = getenv("SV_DW_CHUNKED");
@@ -1351,11 +1362,16 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
       if (rc) return rc;
     }
     if (!dw_chunked_layer(l)) {  // whole-T weight GEMMs behind the recurrence, on its stream
-      sw = s;
-      rc = gemm_f32(1, 1, 4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws, s);
+      if (dw_lowprio()) {        // ... or on the weight-gradient stream, after the last chunk's dx
+        if ((e = hipStreamWaitEvent(sw, ev[l * nch], 0)) != hipSuccess) return (int)e;
+      } else {
+        sw = s;
+      }
+      float* gw = sw == s ? ws.gws : ws.gws2;
+      rc = gemm_f32(1, 1, 4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, gw, sw);
       if (rc) return rc;
-      rc = gemm_f32(1, 1, 4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f,
-                       ws.gws, s);
+      rc = gemm_f32(1, 1, 4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, gw,
+                    sw);
       if (rc) return rc;
     }
     hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],

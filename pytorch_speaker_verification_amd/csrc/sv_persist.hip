@@ -840,6 +840,9 @@ unsigned* sync_cnt(unsigned* sync, int chan) {
 }
 }  // namespace
 
+unsigned sv_persist_limit() { return persist_limit(); }
+int sv_persist_fault(int bwd) { return bwd ? persist_fault() != 0 : fwd_fault(); }
+
 int sv_stream_cus(hipStream_t stream) {
   int dev = -1;
   if (stream && hipStreamGetDevice(stream, &dev) == hipSuccess) return device_cus(dev);

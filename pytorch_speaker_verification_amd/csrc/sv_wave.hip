@@ -1,0 +1,323 @@
+// Layer-wavefront persistent recurrences for small per-GPU batches (BASELINE c4: 8 speakers x
+// 10 utterances = 80 rows per rank at 8 GPUs).
+//
+// Why: at B = 80 one layer's W-stationary recurrence (sv_persist.hip) is 3 row blocks x 24 unit
+// blocks = 72 workgroups on 256 CUs, and the three layers run one after another, each behind its
+// own input-projection GEMM.  Here ONE launch runs all layers: layer l's step t needs only layer
+// l's h_{t-1} and layer l-1's h_t, so the layers advance as a wavefront (layer l one step behind
+// layer l-1) on 3 x 72 = 216 co-resident workgroups, and the input projection x_t W_ih^T of the
+// upper layers is computed in the recurrence itself (no K1 GEMM): T + L - 1 dependent steps
+// instead of L x T.
+//
+// Workgroup (layer l, unit block ub, row block rb): 256 threads = 4 waves, one per SIMD (512
+// registers each).  Wave g owns gate g of the tile's 32 units and holds BOTH its weight slices in
+// registers for the whole launch: W_hh^l rows [g H + j0, +32) x K = H (48 bf16x8 MFMA B
+// fragments) and W_ih^l's (48; layer 0: 3 over F = 40 features).  Per step it contracts
+// h_{t-1}^l and x_t^l = h_t^{l-1} (layer 0: the frames, read straight from global) into ONE
+// 32 x 32 accumulator with v_mfma_f32_32x32x16_bf16 (96 MFMAs), adds b_ih + b_hh, and the gate
+// tiles meet in LDS for the cell update (the shared contraction-free lstm_cell_fwd; 4 units x 1
+// row per thread).  Both A tiles (32 rows x H bf16) are staged into LDS with `sc1` loads.
+// Hand-off of h_t^l: hand-off table row 1 of MI355X_MICROARCH.md, exactly as sv_persist.hip
+// (16-B `sc1` stores of an LDS-staged bf16 tile, every storing wave drains vmcnt, workgroup
+// barrier, one lane adds to its (layer, row block) counter in the caller's sync block; consumers
+// poll with `sc1` loads, bounded, with the same sticky timeout status).
+// Outputs are those of the per-layer schedule (activated gates, c, h fp32; h bf16 slots; hT), so
+// the backward runs unchanged.
+#include <algorithm>
+#include <stdlib.h>
+#include "sv_bf16.h"
+#include "../../include/sv_ge2e.h"
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+namespace {
+constexpr int WV_L = 3;       // layers of one wavefront launch (hp.model.num_layer)
+constexpr int WV_BM = 32;     // rows per workgroup
+constexpr int WV_NS = 48;     // k-steps of 16 over H = 768
+constexpr int WV_XS = 3;      // k-steps of 16 over layer 0's F = 40 features (zero-padded to 48)
+constexpr int WV_F = 40;
+constexpr int WV_LDA = WV_NS * 16 + 8;  // As row stride (bf16): 1552-B rows, conflict-free b128 reads
+constexpr int WV_LDP = 4 * BF_U + 4;    // pre tile [32][LDP] fp32
+constexpr int WV_LDB = BF_U + 8;        // hsb [32][LDB] bf16
+constexpr int WV_LDT = WV_BM + 8;       // hts [32][LDT] bf16
+constexpr int WV_NT = 256;              // threads per workgroup
+constexpr size_t WV_LDS = 2 * (size_t)WV_BM * WV_LDA * 2 + (size_t)WV_BM * WV_LDP * 4 + (size_t)WV_BM * WV_LDB * 2 +
+                          (size_t)BF_U * WV_LDT * 2;
+}  // namespace
+
+struct WaveFwd2Args {
+  const bf16_t* whh[WV_L];   // [4H][H] bf16
+  const bf16_t* wih[WV_L];   // [4H][F_l] bf16
+  const float* bih[WV_L];
+  const float* bhh[WV_L];
+  float* gates[WV_L];        // [T][B][4H] activated
+  float* c[WV_L];            // [T][B][H]
+  float* h[WV_L];            // [T+1][B][H] (slot 0 = 0, written by the host)
+  bf16_t* hb[WV_L];          // [T+1][B][H] bf16 (slot 0 = 0)
+  bf16_t* hT[WV_L];          // [H][(T+1)Bp] or NULL
+  const bf16_t* x_bf;        // [T][B][F]
+  unsigned* cnt[WV_L];       // per-layer row-block counters (sync block channels)
+  unsigned* status;
+  unsigned limit;
+  long ldhT;
+  int T, Bp, B, H, nub, nrb, fault;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wv_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void wv_wait(unsigned* c, unsigned target, unsigned* status, unsigned limit) {
+  unsigned spins = 0;
+  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > limit) {
+      __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+}
+
+// stage one 32-row x H bf16 tile of a hand-off buffer slot into LDS (sc1 loads, issued in four
+// groups of 3 per thread to bound live registers; rows past B read zeros: their offsets fall
+// past the descriptor's range)
+__device__ __forceinline__ void wv_stage(const bf16_t* slot, int B, int H, int b0, bf16_t* As, int tid) {
+  const __amdgpu_buffer_rsrc_t ra = wv_rsrc(slot, (unsigned)((long)B * H * 2));
+  constexpr int C8 = WV_NS * 16 / 8;          // 16-B chunks per row (96)
+  constexpr int PER = WV_BM * C8 / WV_NT;     // 12 per thread
+  constexpr int GRP = 3;
+#pragma unroll
+  for (int i0 = 0; i0 < PER; i0 += GRP) {
+    uint4 v[GRP];
+#pragma unroll
+    for (int i = 0; i < GRP; ++i) {
+      const int q = tid + WV_NT * (i0 + i), row = q / C8, c = (q % C8) * 8;
+      const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(
+          ra, ((unsigned)(b0 + row) * (unsigned)H + (unsigned)c) * 2u, 0, 16 /* sc1 */);
+      v[i] = uint4{x.x, x.y, x.z, x.w};
+    }
+#pragma unroll
+    for (int i = 0; i < GRP; ++i) {
+      const int q = tid + WV_NT * (i0 + i), row = q / C8, c = (q % C8) * 8;
+      *reinterpret_cast<uint4*>(As + row * WV_LDA + c) = v[i];
+    }
+  }
+}
+
+// acc += A(32 x H, LDS rows at Ar, this lane's k-offset folded in) . W (48 B fragments): A
+// fragments software-pipelined one group of 4 ahead of the MFMAs (group schedule barriers keep
+// the 4 ds_read_b128 of group k+1 in front of group k's MFMAs, so LDS latency hides behind them)
+__device__ __forceinline__ void wv_mfma_lds(const bf16_t* Ar, const bf16x8_t (&W)[WV_NS], f32x16& acc) {
+  bf16x8_t cur[4], nxt[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) cur[j] = *reinterpret_cast<const bf16x8_t*>(Ar + 16 * j);
+#pragma unroll
+  for (int s0 = 0; s0 < WV_NS; s0 += 4) {
+    if (s0 + 4 < WV_NS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nxt[j] = *reinterpret_cast<const bf16x8_t*>(Ar + 16 * (s0 + 4 + j));
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // the 4 DS reads of the next group
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = mfma_bf16(cur[j], W[s0 + j], acc);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);    // then this group's 4 MFMAs
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void lstm_wave2_fwd_bf16_kernel(const WaveFwd2Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* As_h = reinterpret_cast<bf16_t*>(smem);                         // [32][LDA]
+  bf16_t* As_x = As_h + WV_BM * WV_LDA;                                   // [32][LDA]
+  float* pre = reinterpret_cast<float*>(As_x + WV_BM * WV_LDA);           // [32][LDP]
+  bf16_t* hsb = reinterpret_cast<bf16_t*>(pre + WV_BM * WV_LDP);          // [32][LDB]
+  bf16_t* hts = hsb + WV_BM * WV_LDB;                                     // [32][LDT]
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int H = a.H, B = a.B, T = a.T, nub = a.nub;
+  // workgroup -> (layer, unit block, row block): XCD-contiguous logical order, unit block fastest
+  int ub, rb, l;
+  {
+    const int i = blockIdx.x, n = gridDim.x;
+    const int x = i & 7, q = n >> 3, rr = n & 7;
+    const int L = x * q + min(x, rr) + (i >> 3);
+    ub = L % nub;
+    rb = (L / nub) % a.nrb;
+    l = L / (nub * a.nrb);
+  }
+  const int j0 = ub * BF_U, b0 = rb * WV_BM;
+  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
+  unsigned* my_cnt = a.cnt[l] + rb * SV_PCNT_STRIDE;
+  unsigned* below = l > 0 ? a.cnt[l - 1] + rb * SV_PCNT_STRIDE : nullptr;
+  const unsigned producers = nub;
+  // weight fragments of gate g: B[k][n] = W[g H + j0 + n][k], lane (n = r, k = 16 s + 8 hh .. +7)
+  const bool wok = j0 + r < H;
+  bf16x8_t wh[WV_NS], wx[WV_NS];
+  {
+    const bf16_t* rh = a.whh[l] + ((long)g * H + j0 + r) * H + 8 * hh;
+    const int K = l == 0 ? WV_F : H;
+    const bf16_t* rx = a.wih[l] + ((long)g * H + j0 + r) * K + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < WV_NS; ++s) {
+      bf16x8_t z = {};
+      wh[s] = wok ? *reinterpret_cast<const bf16x8_t*>(rh + 16 * s) : z;
+      wx[s] = (wok && 16 * s + 8 * hh < K) ? *reinterpret_cast<const bf16x8_t*>(rx + 16 * s) : z;
+    }
+  }
+  float xbias = 0.f;
+  if (wok) {
+    const int col = g * H + j0 + r;
+    xbias = a.bih[l][col] + a.bhh[l][col];
+  }
+  // epilogue map: thread -> 4 consecutive units (u4) of row brow
+  const int u4 = (tid & 7) * 4, brow = tid >> 3;
+  const long gb = b0 + brow;
+  float cst[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < T; ++t) {
+    if (tid == 0) {
+      if (t > 0) wv_wait(my_cnt, producers * (unsigned)t, a.status, a.limit);
+      if (below) wv_wait(below, producers * (unsigned)(t + 1), a.status, a.limit);
+    }
+    __syncthreads();
+    if (t > 0) wv_stage(a.hb[l] + (long)t * BH, B, H, b0, As_h, tid);
+    if (l > 0) wv_stage(a.hb[l - 1] + (long)(t + 1) * BH, B, H, b0, As_x, tid);
+    __syncthreads();
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    if (l > 0) {
+      wv_mfma_lds(As_x + r * WV_LDA + 8 * hh, wx, acc);
+    } else {  // layer 0: x_t (F = 40) from global; rows past B and k past F read zeros
+      const __amdgpu_buffer_rsrc_t rxs = wv_rsrc(a.x_bf + (long)t * B * WV_F, (unsigned)((long)B * WV_F * 2));
+#pragma unroll
+      for (int s = 0; s < WV_XS; ++s) {
+        const unsigned off = 16 * s + 8 * hh < WV_F
+                                 ? ((unsigned)(b0 + r) * (unsigned)WV_F + 16 * s + 8 * hh) * 2u
+                                 : 0xFFFFFFF0u;
+        const u32x4_t xa = __builtin_amdgcn_raw_buffer_load_b128(rxs, off, 0, 0);
+        acc = mfma_bf16(__builtin_bit_cast(bf16x8_t, xa), wx[s], acc);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] += xbias;
+    if (t > 0) wv_mfma_lds(As_h + r * WV_LDA + 8 * hh, wh, acc);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) pre[acc_row(i, lane) * WV_LDP + g * BF_U + r] = acc[i];
+    __syncthreads();
+    // cell update: 4 units x 1 row per thread
+    float4 act[4], cv, hv;
+    {
+      float4 pq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pq[q] = *reinterpret_cast<const float4*>(pre + brow * WV_LDP + q * BF_U + u4);
+      float ao[4][4], co[4], ho[4];
+      unsigned pk[2] = {0u, 0u};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float pv[4] = {pq[0][v], pq[1][v], pq[2][v], pq[3][v]};
+        const float xv[4] = {0.f, 0.f, 0.f, 0.f};
+        float a4[4], h;
+        const float c = lstm_cell_fwd(pv, xv, cst[v], a4, h);
+        cst[v] = c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ao[q][v] = a4[q];
+        co[v] = c;
+        ho[v] = h;
+        const bf16_t e = to_bf(h);
+        hts[(u4 + v) * WV_LDT + brow] = e;
+        pk[v >> 1] |= (unsigned)e << (16 * (v & 1));
+      }
+      *reinterpret_cast<uint2*>(hsb + brow * WV_LDB + u4) = uint2{pk[0], pk[1]};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) act[q] = float4{ao[q][0], ao[q][1], ao[q][2], ao[q][3]};
+      cv = float4{co[0], co[1], co[2], co[3]};
+      hv = float4{ho[0], ho[1], ho[2], ho[3]};
+    }
+    __syncthreads();  // hsb, hts complete
+    // the hand-off: h_t bf16, 32 rows x 4 chunks of 8 units, 16-B sc1 stores
+    if (tid < WV_BM * 4) {
+      const int row = tid >> 2, c = tid & 3, gr = b0 + row;
+      const __amdgpu_buffer_rsrc_t rw = wv_rsrc(a.hb[l] + (long)(t + 1) * BH, (unsigned)(BH * 2));
+      if (gr < B && j0 + 8 * c < H) {
+        const uint4 v = *reinterpret_cast<const uint4*>(hsb + row * WV_LDB + 8 * c);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw,
+                                               ((unsigned)gr * (unsigned)H + (unsigned)(j0 + 8 * c)) * 2u, 0,
+                                               16 /* sc1 */);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0 && !(a.fault && t == 0 && blockIdx.x == 0))
+      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // off the critical chain: activations, c, h and hT of step t
+    if (gb < B && j0 + u4 < H) {
+      float* gp = a.gates[l] + (long)t * BG + gb * G + j0 + u4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(gp + q * H) = act[q];
+      *reinterpret_cast<float4*>(a.c[l] + (long)t * BH + gb * H + j0 + u4) = cv;
+      *reinterpret_cast<float4*>(a.h[l] + (long)(t + 1) * BH + gb * H + j0 + u4) = hv;
+    }
+    if (a.hT[l] && tid < BF_U * (WV_BM / 8)) {  // 32 unit rows x 4 chunks of 8 batch columns
+      const int u = tid >> 2, c = tid & 3, gc = b0 + 8 * c;
+      if (gc < a.Bp && j0 + u < H) {
+        bf16_t* row = a.hT[l] + (long)(j0 + u) * a.ldhT;
+        *reinterpret_cast<uint4*>(row + (long)(t + 1) * a.Bp + gc) = *reinterpret_cast<const uint4*>(hts + u * WV_LDT + 8 * c);
+        if (t == 0) *reinterpret_cast<uint4*>(row + gc) = uint4{0u, 0u, 0u, 0u};
+      }
+    }
+  }
+}
+
+// ---- host ----
+// can the layer-wavefront forward run these dims co-resident on a device of `cus` CUs?
+int sv_wave_fwd_fits(int L, int B, int F, int H, int cus) {
+  const int nub = (H + BF_U - 1) / BF_U, nrb = (B + WV_BM - 1) / WV_BM;
+  return L == WV_L && H == WV_NS * 16 && F == WV_F && nrb <= SV_PCNT_ROWS && (long)L * nub * nrb <= cus &&
+         (long)B * H * 2 < (1L << 31);
+}
+
+// all L layers' recurrences of the bf16 stack forward in one launch (no K1 GEMMs): writes what the
+// per-layer schedule writes.  h_tm / h_bf slot 0 and padded hT columns must be zero (the caller's
+// memsets).  Counter channels 0..L-1 of `sync`.
+int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, const bf16_t* const* w_ih_bf,
+                     const bf16_t* const* w_hh_bf, const float* const* b_ih, const float* const* b_hh,
+                     float* const* gates, float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
+                     bf16_t* const* hT, unsigned* sync, hipStream_t stream, unsigned limit, int fault, hipEvent_t pre,
+                     hipEvent_t post) {
+  if (!sv_wave_fwd_fits(L, B, F, H, sv_stream_cus(stream))) return SV_ESHAPE;
+  if (!sync || !x_bf) return SV_EARG;
+  WaveFwd2Args a{};
+  a.nub = (H + BF_U - 1) / BF_U;
+  a.nrb = (B + WV_BM - 1) / WV_BM;
+  for (int l = 0; l < L; ++l) {
+    a.whh[l] = w_hh_bf[l];
+    a.wih[l] = w_ih_bf[l];
+    a.bih[l] = b_ih[l];
+    a.bhh[l] = b_hh[l];
+    a.gates[l] = gates[l];
+    a.c[l] = c_tm[l];
+    a.h[l] = h_tm[l];
+    a.hb[l] = h_bf[l];
+    a.hT[l] = hT[l];
+    a.cnt[l] = sync + SV_SYNC_CNT + (size_t)l * SV_PCNT_ROWS * SV_PCNT_STRIDE;
+    hipError_t e = hipMemsetAsync(a.cnt[l], 0, (size_t)a.nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  a.x_bf = x_bf;
+  a.status = sync;
+  a.limit = limit;
+  a.fault = fault;
+  a.T = T;
+  a.B = B;
+  a.H = H;
+  a.Bp = (B + 7) & ~7;
+  a.ldhT = (long)(T + 1) * a.Bp;
+  hipError_t e;
+  if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(lstm_wave2_fwd_bf16_kernel, dim3(L * a.nub * a.nrb), dim3(WV_NT), WV_LDS, stream, a);
+  SV_LAUNCH_CHECK();
+  if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
+  return SV_OK;
+}

@@ -73,12 +73,20 @@ class _StreamPool:
     """Side streams + events for the layer-pipelined schedules (one set per device)."""
     _pools = {}
 
+    # SV_STREAM_PRIO=1: the backward pool's recurrence streams (first half) high priority, its
+    # weight-gradient streams (second half) low priority (see SV_DW_LOWPRIO in sv_lstm.hip)
+    PRIO = os.environ.get("SV_STREAM_PRIO", "0") == "1"
+
     @classmethod
-    def get(cls, device, n_streams, n_events):
+    def get(cls, device, n_streams, n_events, split_prio=False):
         key = (device.index, n_streams)
         p = cls._pools.get(key)
         if p is None or len(p[1]) < n_events:
-            streams = [torch.cuda.Stream(device=device) for _ in range(n_streams)]
+            if split_prio and cls.PRIO:
+                streams = [torch.cuda.Stream(device=device, priority=-1 if i < n_streams // 2 else 0)
+                           for i in range(n_streams)]
+            else:
+                streams = [torch.cuda.Stream(device=device) for _ in range(n_streams)]
             events = []
             with torch.cuda.device(device):
                 for _ in range(n_events):
@@ -239,7 +247,7 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
         ld = [T * Bp] + [(T + 1) * Bp] * (L - 1)
         nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
         nev = L * nch + L + 1
-        streams, events = _StreamPool.get(dev, 2 * L, nev)
+        streams, events = _StreamPool.get(dev, 2 * L, nev, split_prio=True)
         sp = (ctypes.c_void_p * (2 * L))(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
         call("sv_lstm_stack_bwd", L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),

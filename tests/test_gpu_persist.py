@@ -73,3 +73,24 @@ def test_persistent_bwd_bf16_equals_per_step(tmp_path, dims, N, M, T):
                 np.testing.assert_array_equal(other[k], a[k], err_msg=k)
     for other in (b, c):
         np.testing.assert_allclose(other["flat_p"], a["flat_p"], rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("N,M,T", [(8, 10, 20),    # c4's per-rank shape: 3 x 3 x 24 = 216 workgroups
+                                   (7, 5, 9)])     # ragged rows (B = 35, 2 row blocks)
+def test_wavefront_fwd_bf16_against_per_layer(tmp_path, N, M, T):
+    """Layer-wavefront forward (sv_wave.hip: all layers in one launch, input projection in the
+    recurrence) vs the per-layer persistent schedule (K1 GEMM + one launch per layer): the same
+    bf16 products, summed in another order (x and h parts in one accumulator), so agreement to
+    bf16-operand level; then the training step through it."""
+    dims = (40, 768, 3, 256)
+    a = _run(tmp_path, "layer", {"SV_WAVE2": "0"}, dims, N, M, T, "bf16")
+    b = _run(tmp_path, "wave", {"SV_WAVE2": "1"}, dims, N, M, T, "bf16")
+    assert int(a["status"][0]) == 0 and int(b["status"][0]) == 0
+    for k in ("gates0", "c0", "gates1", "c1", "gates2", "c2"):
+        d = float(np.abs(b[k] - a[k]).max())
+        print(f"\nMEASURED wave2_vs_layer.{k} {d:.3e}")
+        assert d < 2e-2, (k, d)
+    d = float(np.abs(b["emb"] - a["emb"]).max())
+    print(f"\nMEASURED wave2_vs_layer.emb {d:.3e}")
+    assert d < 5e-3, d
+    np.testing.assert_allclose(b["loss"], a["loss"], rtol=1e-3)
