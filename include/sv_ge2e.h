@@ -140,6 +140,15 @@ int sv_ge2e_bwd_finalize(int N_local, int M, int D, int spk_offset, int N, const
 int sv_ge2e_bwd(int N, int M, int D, const float* w, const float* b, const float* gloss, float* dE, float* dwdb,
                 float* dchat, float* beta, float* workspace, hipStream_t stream);
 
+/* fused single-GPU training form (all N speakers local, gloss = 1): forward + closed-form
+ * backward in three launches (per-speaker prep; a wave per row with every centroid staged in LDS:
+ * cosines, shuffle softmax, row backward; a workgroup per (speaker, 64-wide d slice): centroid
+ * gradients and the speaker's dE).  Needs N <= 128, 2 <= M <= 16, D <= 256, D % 4 == 0 (sv_ge2e_train_ok);
+ * workspace: sv_ge2e_workspace_size(N, M, D, N). */
+int sv_ge2e_train_ok(int N, int M, int D);
+int sv_ge2e_train(const float* E, int N, int M, int D, const float* w, const float* b, float* loss, float* per,
+                  float* dE, float* dwdb, float* workspace, hipStream_t stream);
+
 /* stand-alone helpers (utils.py): C = E.mean(1) [N,D]; cos [N,M,Nc] = get_cossim(E, C) with the
  * diagonal from E's own leave-one-out centroids (utils.py:75,91,113), +1e-6; calc_loss on S [N,M,K]. */
 int sv_ge2e_centroids(const float* E, int N, int M, int D, float* C, hipStream_t stream);

@@ -24,7 +24,7 @@ namespace {
 
 // workspace carve (all fp32), see sv_ge2e_workspace_size
 struct Ge2eWs {
-  float *Ehat, *Uhat, *En, *Un, *rawd, *cos, *logz, *Chat, *Cn, *dcos, *alpha, *G1, *dwdb_rows, *betap, *gemm;
+  float *Ehat, *Uhat, *En, *Un, *rawd, *cos, *logz, *Chat, *Cn, *dcos, *alpha, *G1, *dwdb_rows, *betap, *dcd, *gemm;
   size_t total;
 };
 
@@ -54,6 +54,7 @@ Ge2eWs carve(float* base, int Nl, int M, int D, int N) {
   w.G1 = take(Bl * D);
   w.dwdb_rows = take(2 * Bl);
   w.betap = take(((Bl + 63) / 64) * (size_t)N);
+  w.dcd = take(Bl);
   const size_t g1 = sv_gemm_f32_workspace((int)Bl, D, N);
   const size_t g2 = sv_gemm_f32_workspace(N, D, (int)Bl);
   w.gemm = take((std::max(g1, g2) + 3) / 4);
@@ -420,6 +421,361 @@ extern "C" int sv_ge2e_bwd(int N, int M, int D, const float* w, const float* b, 
   int rc = sv_ge2e_bwd_rows(N, M, D, 0, N, w, b, gloss, dchat, beta, dwdb, workspace, stream);
   if (rc) return rc;
   return sv_ge2e_bwd_finalize(N, M, D, 0, N, dchat, beta, dE, workspace, stream);
+}
+
+// ============================================================================
+// Fused single-GPU training path: GE2E forward + closed-form backward in three launches
+// (sv_ge2e_train), for N <= 128 speakers, M <= 16, D <= 256 (every c1-c5 single-GPU shape):
+//   F1 ge2e_prep_kernel   one workgroup per speaker: its sum, centroid C^ and |C| (LDS
+//                         reduction), and per utterance row E^, U^ (leave-one-out), the norms and
+//                         the diagonal cosine (a wave per row, shuffle reductions)
+//   F2 ge2e_rows_kernel   one wave per row, C^ of every speaker staged in LDS once per
+//                         workgroup: the row's N cosines (lanes over speakers, ds_read_b128 of
+//                         conflict-free padded C^ rows, E^ broadcast), the diagonal overwrite, the
+//                         shuffle softmax (max, log-sum-exp, per-row loss), dS = p - delta,
+//                         dcos, alpha, dw/db row partials and G1 = sum_k dcos_k C^_k
+//   F3 ge2e_cols_kernel   one workgroup per (speaker k, 64-wide d slice): beta_k and
+//                         dC^_k = sum_r dcos[r,k] E^_r over every row, then dC_k and the speaker's
+//                         rows of dE (the split path's finalize); workgroup (0, 0) also sums the
+//                         loss and dw, db in fixed order
+// The arithmetic is the split path's (same formulas, fixed-order sums; the cosines by FMA dot
+// products instead of the MFMA GEMM), so results agree to fp32 rounding.
+// ============================================================================
+#define GF_NMAX 128
+#define GF_DMAX 256
+#define GF_MMAX 16
+
+__global__ __launch_bounds__(256) void ge2e_prep_kernel(const float* __restrict__ E, int M, int D,
+                                                        float* __restrict__ Chat, float* __restrict__ Cn,
+                                                        float* __restrict__ Ehat, float* __restrict__ Uhat,
+                                                        float* __restrict__ En, float* __restrict__ Un,
+                                                        float* __restrict__ rawd) {
+  // one pass over the speaker's rows: wave w holds rows w, w + 4, ... (lane: d = 4 lane .. + 3,
+  // D <= 256), their per-wave partial sums meet in LDS (added in wave order, rows in order)
+  constexpr int RW = (GF_MMAX + 3) / 4;
+  __shared__ float4 ps[4][64];
+  __shared__ float red[4];
+  const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bool dok = 4 * lane < D;
+  const float* Ej = E + (long)j * M * D;
+  float4 e[RW];
+  float4 part = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    const int i = w + 4 * q;
+    e[q] = (i < M && dok) ? *reinterpret_cast<const float4*>(Ej + (long)i * D + 4 * lane) : float4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    part.x += e[q].x;
+    part.y += e[q].y;
+    part.z += e[q].z;
+    part.w += e[q].w;
+  }
+  ps[w][lane] = part;
+  __syncthreads();
+  const float4 p0 = ps[0][lane], p1 = ps[1][lane], p2 = ps[2][lane], p3 = ps[3][lane];
+  const float4 sum = float4{((p0.x + p1.x) + p2.x) + p3.x, ((p0.y + p1.y) + p2.y) + p3.y,
+                            ((p0.z + p1.z) + p2.z) + p3.z, ((p0.w + p1.w) + p2.w) + p3.w};
+  const float fm = (float)M;
+  const float4 c = float4{sum.x / fm, sum.y / fm, sum.z / fm, sum.w / fm};
+  const float cn = sqrtf(wave_sum(c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w));
+  const float icn = 1.0f / fmaxf(cn, EPS_COS);
+  if (w == 0) {
+    if (dok) *reinterpret_cast<float4*>(Chat + (long)j * D + 4 * lane) = float4{c.x * icn, c.y * icn, c.z * icn, c.w * icn};
+    if (lane == 0) Cn[j] = cn;
+  }
+  const float invm1 = 1.0f / (float)(M - 1);
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    const int i = w + 4 * q;
+    if (i >= M) break;
+    const long r = (long)j * M + i;
+    const float4 x = e[q];
+    const float4 u = float4{(sum.x - x.x) * invm1, (sum.y - x.y) * invm1, (sum.z - x.z) * invm1, (sum.w - x.w) * invm1};
+    const float ne = sqrtf(wave_sum(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w));
+    const float nu = sqrtf(wave_sum(u.x * u.x + u.y * u.y + u.z * u.z + u.w * u.w));
+    const float ie = 1.0f / fmaxf(ne, EPS_COS), iu = 1.0f / fmaxf(nu, EPS_COS);
+    const float4 xh = float4{x.x * ie, x.y * ie, x.z * ie, x.w * ie};
+    const float4 uh = float4{u.x * iu, u.y * iu, u.z * iu, u.w * iu};
+    if (dok) {
+      *reinterpret_cast<float4*>(Ehat + r * D + 4 * lane) = xh;
+      *reinterpret_cast<float4*>(Uhat + r * D + 4 * lane) = uh;
+    }
+    const float dot = wave_sum(xh.x * uh.x + xh.y * uh.y + xh.z * uh.z + xh.w * uh.w);
+    if (lane == 0) {
+      En[r] = ne;
+      Un[r] = nu;
+      rawd[r] = dot;
+    }
+  }
+  (void)red;
+}
+
+// F2: 8 rows per workgroup (two per wave, sharing every C^ read).  Cs [N][D + 4] fp32 in LDS
+// (16-B padded rows: the 16 lanes of a ds_read_b128 group hit disjoint banks); the rows' E^ in
+// Es [8][D]; per-row dcos vectors in Vs [8][N].
+__global__ __launch_bounds__(256) void ge2e_rows_kernel(const float* __restrict__ Chat, const float* __restrict__ Ehat,
+                                                        const float* __restrict__ rawd, int Bl, int M, int N, int D,
+                                                        int ldc, const float* __restrict__ wp,
+                                                        const float* __restrict__ bp, float* __restrict__ per,
+                                                        float* __restrict__ cos, float* __restrict__ dcos,
+                                                        float* __restrict__ alpha, float* __restrict__ dcd,
+                                                        float* __restrict__ dwdb_rows, float* __restrict__ G1) {
+  extern __shared__ __attribute__((aligned(16))) float gsm[];
+  const int LDC = D + 4;
+  float* Cs = gsm;                    // [N][LDC]
+  float* Es = Cs + (size_t)N * LDC;   // [8][D]
+  float* Vs = Es + 8 * D;             // [8][N]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int D4 = D / 4, NQ = N * D4;
+  for (int q0 = tid; q0 < NQ; q0 += 256 * 8) {  // 8 loads in flight per thread
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int q = q0 + 256 * u;
+      if (q < NQ) v[u] = *reinterpret_cast<const float4*>(Chat + (long)(q / D4) * D + (q % D4) * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int q = q0 + 256 * u;
+      if (q < NQ) *reinterpret_cast<float4*>(Cs + (q / D4) * LDC + (q % D4) * 4) = v[u];
+    }
+  }
+  const int r0 = blockIdx.x * 8 + 2 * w;   // this wave's rows r0, r0 + 1
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (r0 + h < Bl)
+      for (int c = lane * 4; c < D; c += 256)
+        *reinterpret_cast<float4*>(Es + (2 * w + h) * D + c) = *reinterpret_cast<const float4*>(Ehat + (long)(r0 + h) * D + c);
+  __syncthreads();
+  if (r0 >= Bl) return;
+  const float wv = *wp, bv = *bp;
+  // cosines: lane k (and k + 64) over D, both rows at once, E^ broadcast
+  float cv[2][2] = {{0.f, 0.f}, {0.f, 0.f}};  // [row][speaker half]
+  const float* e0 = Es + (2 * w) * D;
+  const float* e1 = e0 + D;
+#pragma unroll
+  for (int hk = 0; hk < 2; ++hk) {
+    const int k = lane + 64 * hk;
+    if (k < N) {
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll 8
+      for (int c = 0; c < D; c += 4) {
+        const float4 cc = *reinterpret_cast<const float4*>(Cs + k * LDC + c);
+        const float4 x0 = *reinterpret_cast<const float4*>(e0 + c);
+        const float4 x1 = *reinterpret_cast<const float4*>(e1 + c);
+        a0 += x0.x * cc.x;
+        a0 += x0.y * cc.y;
+        a0 += x0.z * cc.z;
+        a0 += x0.w * cc.w;
+        a1 += x1.x * cc.x;
+        a1 += x1.y * cc.y;
+        a1 += x1.z * cc.z;
+        a1 += x1.w * cc.w;
+      }
+      cv[0][hk] = a0;
+      cv[1][hk] = a1;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = r0 + h;
+    if (r >= Bl) break;
+    const int sg = r / M;
+    const float rd = rawd[r];
+#pragma unroll
+    for (int hk = 0; hk < 2; ++hk)
+      if (lane + 64 * hk == sg) cv[h][hk] = rd;  // get_cossim's diagonal overwrite (utils.py:112-113)
+    // row softmax: S = w (cos + 1e-6) + b;  lz = log(sum_k e^S + 1e-6)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int hk = 0; hk < 2; ++hk)
+      if (lane + 64 * hk < N) mx = fmaxf(mx, wv * (cv[h][hk] + EPS_SIM) + bv);
+    mx = fmaxf(wave_max(mx), 0.f);
+    float z = 0.f;
+#pragma unroll
+    for (int hk = 0; hk < 2; ++hk)
+      if (lane + 64 * hk < N) z += __expf(wv * (cv[h][hk] + EPS_SIM) + bv - mx);
+    z = wave_sum(z);
+    const float lz = mx + logf(z + EPS_LOG * __expf(-mx));
+    // row backward (gloss = 1): dS = p - delta, dcos = w dS
+    float a = 0.f, dw = 0.f, db = 0.f;
+#pragma unroll
+    for (int hk = 0; hk < 2; ++hk) {
+      const int k = lane + 64 * hk;
+      if (k < N) {
+        const float cp = cv[h][hk] + EPS_SIM;
+        const float p = __expf(wv * cp + bv - lz);
+        const float ds = p - (k == sg ? 1.0f : 0.0f);
+        const float dcv = wv * ds;
+        a += dcv * cv[h][hk];
+        dw += ds * cp;
+        db += ds;
+        const float off = (k == sg) ? 0.f : dcv;
+        Vs[(2 * w + h) * N + k] = off;
+        cos[(long)r * ldc + k] = cv[h][hk];
+        dcos[(long)r * ldc + k] = off;
+        if (k == sg) dcd[r] = dcv;
+      }
+    }
+    a = wave_sum(a);
+    dw = wave_sum(dw);
+    db = wave_sum(db);
+    if (lane == 0) {
+      per[r] = lz - (wv * (rd + EPS_SIM) + bv);
+      alpha[r] = a;
+      dwdb_rows[r] = dw;
+      dwdb_rows[Bl + r] = db;
+    }
+  }
+  // G1_r = sum_k dcos_off[r,k] C^_k for both rows: lanes over d (4 each), speakers in order
+  __builtin_amdgcn_wave_barrier();
+  const bool two = r0 + 1 < Bl;
+  for (int c = lane * 4; c < D; c += 256) {
+    float4 g0 = float4{0.f, 0.f, 0.f, 0.f}, g1 = g0;
+#pragma unroll 8
+    for (int k = 0; k < N; ++k) {
+      const float d0 = Vs[(2 * w) * N + k], d1 = Vs[(2 * w + 1) * N + k];
+      const float4 cc = *reinterpret_cast<const float4*>(Cs + k * LDC + c);
+      g0.x += d0 * cc.x;
+      g0.y += d0 * cc.y;
+      g0.z += d0 * cc.z;
+      g0.w += d0 * cc.w;
+      g1.x += d1 * cc.x;
+      g1.y += d1 * cc.y;
+      g1.z += d1 * cc.z;
+      g1.w += d1 * cc.w;
+    }
+    *reinterpret_cast<float4*>(G1 + (long)r0 * D + c) = g0;
+    if (two) *reinterpret_cast<float4*>(G1 + (long)(r0 + 1) * D + c) = g1;
+  }
+}
+
+// F3: workgroup (speaker k, d slice q of 64): beta_k, dC^_k[slice], dC_k[slice], then dE of
+// speaker k's rows over the slice.  Rows in a fixed order: wave w takes rows w, w + 4, ... (16
+// rows' loads in flight); the four wave partials are added in wave order.
+__global__ __launch_bounds__(256) void ge2e_cols_kernel(int Bl, int M, int N, int D, int ldc,
+                                                        const float* __restrict__ Chat, const float* __restrict__ Cn,
+                                                        const float* __restrict__ Ehat, const float* __restrict__ Uhat,
+                                                        const float* __restrict__ En, const float* __restrict__ Un,
+                                                        const float* __restrict__ rawd, const float* __restrict__ cos,
+                                                        const float* __restrict__ dcos,
+                                                        const float* __restrict__ alpha, const float* __restrict__ dcd,
+                                                        const float* __restrict__ G1, const float* __restrict__ per,
+                                                        const float* __restrict__ dwdb_rows, float* __restrict__ dE,
+                                                        float* __restrict__ loss, float* __restrict__ dwdb) {
+  __shared__ float part[4][64];
+  __shared__ float bpart[4];
+  __shared__ float dCs[64];
+  const int k = blockIdx.x, q = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int d = q * 64 + lane;
+  const bool dok = d < D;
+  constexpr int U = 16;
+  float acc = 0.f, bsum = 0.f;
+  int r = w;
+  for (; r + 4 * (U - 1) < Bl; r += 4 * U) {
+    float dc[U], ev[U], cv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long rr = r + 4 * u;
+      dc[u] = dcos[rr * ldc + k];
+      cv[u] = cos[rr * ldc + k];
+      ev[u] = dok ? Ehat[rr * D + d] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc += dc[u] * ev[u];
+      bsum += dc[u] * cv[u];
+    }
+  }
+  for (; r < Bl; r += 4) {
+    const float dc = dcos[(long)r * ldc + k];
+    if (dok) acc += dc * Ehat[(long)r * D + d];
+    bsum += dc * cos[(long)r * ldc + k];
+  }
+  part[w][lane] = acc;
+  if (lane == 0) bpart[w] = bsum;
+  __syncthreads();
+  const float cn = Cn[k];
+  const float icn = 1.0f / fmaxf(cn, EPS_COS);
+  const float pc = cn > EPS_COS ? 1.f : 0.f;
+  const float beta = ((bpart[0] + bpart[1]) + bpart[2]) + bpart[3];
+  if (tid < 64 && dok) {
+    const float dch = ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
+    dCs[tid] = (dch - beta * Chat[(long)k * D + d] * pc) * icn;
+  }
+  __syncthreads();
+  // dE of speaker k's rows over the slice: wave w takes rows w, w + 4, ...; sum_i dU by all
+  // four waves (each over all M rows, the same fixed order)
+  if (dok) {
+    const float dC = dCs[lane];
+    const float invM = 1.0f / (float)M, invm1 = 1.0f / (float)(M - 1);
+    float sumdU = 0.f;
+    for (int i = 0; i < M; ++i) {
+      const int rr = k * M + i;
+      const float iu = 1.0f / fmaxf(Un[rr], EPS_COS);
+      const float pu = Un[rr] > EPS_COS ? 1.f : 0.f;
+      sumdU += dcd[rr] * (Ehat[(long)rr * D + d] - rawd[rr] * Uhat[(long)rr * D + d] * pu) * iu;
+    }
+    for (int i = w; i < M; i += 4) {
+      const int rr = k * M + i;
+      const long rd = (long)rr * D + d;
+      const float iu = 1.0f / fmaxf(Un[rr], EPS_COS);
+      const float pu = Un[rr] > EPS_COS ? 1.f : 0.f;
+      const float dU = dcd[rr] * (Ehat[rd] - rawd[rr] * Uhat[rd] * pu) * iu;
+      const float ie = 1.0f / fmaxf(En[rr], EPS_COS);
+      const float pe = En[rr] > EPS_COS ? 1.f : 0.f;
+      const float gE = (G1[rd] + dcd[rr] * Uhat[rd] - alpha[rr] * Ehat[rd] * pe) * ie;
+      dE[rd] = gE + dC * invM + (sumdU - dU) * invm1;
+    }
+  }
+  if (k == 0 && q == 0) {  // loss = sum per, dw, db: fixed-order block sums
+    __shared__ float red[4];
+    float l = 0.f, a = 0.f, b = 0.f;
+    for (int i = tid; i < Bl; i += 256) {
+      l += per[i];
+      a += dwdb_rows[i];
+      b += dwdb_rows[Bl + i];
+    }
+    l = block_sum256(l, red);
+    a = block_sum256(a, red);
+    b = block_sum256(b, red);
+    if (tid == 0) {
+      loss[0] = l;
+      dwdb[0] = a;
+      dwdb[1] = b;
+    }
+  }
+}
+
+// can the fused 3-launch path run this shape?
+extern "C" int sv_ge2e_train_ok(int N, int M, int D) {
+  return N > 0 && N <= GF_NMAX && M >= 2 && M <= GF_MMAX && D > 0 && D <= GF_DMAX && D % 4 == 0;
+}
+
+// fused forward + backward of GE2ELoss for one GPU holding all N speakers (gloss = 1, the
+// training step's): loss, per [N,M], dE [N,M,D], dwdb [2] = (dL/dw, dL/db)
+extern "C" int sv_ge2e_train(const float* E, int N, int M, int D, const float* w, const float* b, float* loss,
+                             float* per, float* dE, float* dwdb, float* workspace, hipStream_t stream) {
+  if (!E || !w || !b || !loss || !per || !dE || !dwdb || !workspace) return SV_EARG;
+  if (!sv_ge2e_train_ok(N, M, D)) return SV_ESHAPE;
+  if (((uintptr_t)E | (uintptr_t)workspace) & 15) return SV_EALIGN;
+  const Ge2eWs ws = carve(workspace, N, M, D, N);
+  const int Bl = N * M, Np = (N + 3) & ~3;
+  hipLaunchKernelGGL(ge2e_prep_kernel, dim3(N), dim3(256), 0, stream, E, M, D, ws.Chat, ws.Cn, ws.Ehat, ws.Uhat,
+                     ws.En, ws.Un, ws.rawd);
+  SV_LAUNCH_CHECK();
+  const size_t lds = ((size_t)N * (D + 4) + 8 * (size_t)D + 8 * (size_t)N) * sizeof(float);
+  hipLaunchKernelGGL(ge2e_rows_kernel, dim3((Bl + 7) / 8), dim3(256), lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N,
+                     D, Np, w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ge2e_cols_kernel, dim3(N, (D + 63) / 64), dim3(256), 0, stream, Bl, M, N, D, Np, ws.Chat, ws.Cn,
+                     ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.G1, per,
+                     ws.dwdb_rows, dE, loss, dwdb);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
 }
 
 // ============================================================================

@@ -530,6 +530,32 @@ def ge2e_backward(st, w, b, gloss=None):
     return dE, dwdb[0], dwdb[1]
 
 
+def ge2e_train(E, w, b):
+    """Fused GE2E forward + closed-form backward for one GPU holding all N speakers (the training
+    step's gloss = 1): returns (loss 0-dim, per [N,M], dE [N,M,D], dwdb [2]) from three launches
+    (include/sv_ge2e.h, sv_ge2e_train).  Shapes outside sv_ge2e_train_ok take the split path."""
+    require_device(E, w, b)
+    Ep, D0 = _pad_d(E)
+    N, M, D = Ep.shape
+    if M < 2:
+        raise ValueError("GE2E expects embeddings [N, M, D] with M >= 2 (leave-one-out centroids)")
+    if not lib().sv_ge2e_train_ok(N, M, D):
+        loss, per, st = ge2e_forward(E, w, b)
+        dE, dw, db = ge2e_backward(st, w, b)
+        return loss, per, dE, torch.stack([dw, db])
+    dev = E.device
+    ws = _ws(lib().sv_ge2e_workspace_size(N, M, D, N), dev)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    per = torch.empty((N, M), dtype=torch.float32, device=dev)
+    dE = torch.empty((N, M, D), dtype=torch.float32, device=dev)
+    dwdb = torch.empty((2,), dtype=torch.float32, device=dev)
+    call("sv_ge2e_train", ptr(Ep), N, M, D, ptr(w.contiguous()), ptr(b.contiguous()), ptr(loss), ptr(per), ptr(dE),
+         ptr(dwdb), ptr(ws), stream_of(Ep))
+    if D0 != D:
+        dE = dE[..., :D0].contiguous()
+    return loss, per, dE, dwdb
+
+
 class GE2EFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, E, w, b):

@@ -101,6 +101,18 @@ class ShardedGE2E:
             dist.all_reduce(loss, group=self.group)
         return loss, per, st
 
+    def train(self, E_local, w, b):
+        """Forward + backward for the training step (gloss = 1): (global loss, dE_local,
+        dwdb_partial[2]).  One rank holding every speaker uses the fused 3-launch kernel
+        (ops.ge2e_train); sharded runs take the exchange protocol above."""
+        if self.world == 1 and isinstance(self.k, HipShardKernels):
+            from .ops import ge2e_train
+            loss, _, dE, dwdb = ge2e_train(E_local, w, b)
+            return loss, dE, dwdb
+        loss, _, st = self.forward(E_local, w, b)
+        dE, dwdb = self.backward(st, w, b)
+        return loss, dE, dwdb
+
     def backward(self, st, w, b, gloss=None):
         """Returns (dE_local, dwdb_partial[2]).  dwdb must still be summed over ranks."""
         red, dwdb = self.k.bwd_rows(st, w, b, gloss)

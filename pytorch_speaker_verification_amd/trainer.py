@@ -125,8 +125,7 @@ class GE2ETrainer:
         else:
             emb, st = embedder_forward(x.float().contiguous(), layers, w_p, b_p, products=products)
         E = emb.view(N, M, emb.shape[1])
-        loss, _, gst = self.ge2e.forward(E, w, b)
-        dE, dwdb = self.ge2e.backward(gst, w, b)
+        loss, dE, dwdb = self.ge2e.train(E, w, b)
         self.flat_g[self.n_pad:self.n_pad + 2].copy_(dwdb)
         works = []
         ready = None
