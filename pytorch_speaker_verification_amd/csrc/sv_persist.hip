@@ -264,7 +264,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
                                                                        bf16_t* __restrict__ hT, long ldhT, int T,
                                                                        int Bp, int B, int H, unsigned* cnt, int nub,
                                                                        int xcd, unsigned* status, unsigned limit,
-                                                                       int fault, const bf16_t* __restrict__ x_bf,
+                                                                       int fault, int pipe,
+                                                                       const bf16_t* __restrict__ x_bf,
                                                                        const bf16_t* __restrict__ wih_bf,
                                                                        const float* __restrict__ b_ih,
                                                                        const float* __restrict__ b_hh) {
@@ -298,6 +299,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
       bf16x8_t z = {};
       wreg[s2] = wok ? *reinterpret_cast<const bf16x8_t*>(wrow + 16 * s2) : z;
     }
+    // the weights live in AGPRs (MFMA reads B from them directly): the VGPRs stay free for the
+    // x-projection prefetch and the A-fragment ring of the recurrent MFMAs
+#pragma unroll
+    for (int s2 = 0; s2 < NS; ++s2) asm volatile("" : "+a"(wreg[s2]));
   }
   // fused input projection (XF > 0): W_ih fragments of this wave's 32 gate columns (k = 16 s +
   // 8 hh .. +7, zero past F = 8 XF) and the column's bias b_ih + b_hh
@@ -395,13 +400,22 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
       // copied right after the loads, exposing the whole round trip)
       load_xg(t);
       __builtin_amdgcn_sched_barrier(0);
+      if (pipe) {  // A fragments P k-steps ahead of the MFMAs (sv_bf16.h)
+        f32x16 accs[KR];
+        accs[0] = acc0;
+        if constexpr (BM == 64) accs[KR - 1] = acc1;
+        mfma_lds_pipe<NS, KR, (BM == 64 ? 3 : 4)>(As + r * LDA + 8 * hh, 32 * LDA, wreg, accs);
+        acc0 = accs[0];
+        if constexpr (BM == 64) acc1 = accs[KR - 1];
+      } else {
 #pragma unroll
-      for (int s2 = 0; s2 < NS; ++s2) {
-        const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(As + r * LDA + 16 * s2 + 8 * hh);
-        acc0 = mfma_bf16(a0, wreg[s2], acc0);
-        if constexpr (BM == 64) {
-          const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(As + (32 + r) * LDA + 16 * s2 + 8 * hh);
-          acc1 = mfma_bf16(a1, wreg[s2], acc1);
+        for (int s2 = 0; s2 < NS; ++s2) {
+          const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(As + r * LDA + 16 * s2 + 8 * hh);
+          acc0 = mfma_bf16(a0, wreg[s2], acc0);
+          if constexpr (BM == 64) {
+            const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(As + (32 + r) * LDA + 16 * s2 + 8 * hh);
+            acc1 = mfma_bf16(a1, wreg[s2], acc1);
+          }
         }
       }
     } else {
@@ -524,7 +538,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
 //   acts [T,B,4H] activated gates, c_tm [T,B,H]; dhup: [T,B,H] (up_full) or [B,H] at t = T-1.
 // Hand-off: hand-off table row 1 of MI355X_MICROARCH.md, as the forward kernel above.
 // ============================================================================
-template <int NS, int P, int BM>
+template <int NS, int P, int BM, bool agpr_w = true>
 __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     const bf16_t* __restrict__ whhT, const float* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
@@ -560,6 +574,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     for (int s = 0; s < NS; ++s) {
       bf16x8_t z = {};
       wreg[s] = wok ? *reinterpret_cast<const bf16x8_t*>(wrow + 16 * s) : z;
+    }
+    if (agpr_w) {  // weights in AGPRs (MFMA B operand): VGPRs free for the A stream and operands
+#pragma unroll
+      for (int s = 0; s < NS; ++s) asm volatile("" : "+a"(wreg[s]));
     }
   }
   // elementwise map: thread -> 4 consecutive units (u4) x rows brow, brow + 32
@@ -913,6 +931,11 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
   }();
   const unsigned limit = persist_limit();
   const int fault = fwd_fault();
+  // SV_PFWD_PIPE=0: the recurrent MFMAs read each A fragment right before use (no LDS pipeline)
+  static const int pipe = [] {
+    const char* v = getenv("SV_PFWD_PIPE");
+    return (v && *v == '0') ? 0 : 1;
+  }();
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   if (wst) {
     constexpr int NS = 48, LDA = NS * 16 + 8;
@@ -922,19 +945,19 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
     const int nub = (int)grid.x, xcd = persist_xcd();
     if (x_bf && bm == 32)
       hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 32, 5>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
-                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, x_bf, wih_bf, b_ih,
+                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, pipe, x_bf, wih_bf, b_ih,
                          b_hh);
     else if (x_bf)
       hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 64, 5>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
-                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, x_bf, wih_bf, b_ih,
+                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, pipe, x_bf, wih_bf, b_ih,
                          b_hh);
     else if (bm == 32)
       hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 32, 0>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
-                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, nullptr, nullptr,
+                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, pipe, nullptr, nullptr,
                          nullptr, nullptr);
     else
       hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 64, 0>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
-                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, nullptr, nullptr,
+                         h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, pipe, nullptr, nullptr,
                          nullptr, nullptr);
   } else {
     hipLaunchKernelGGL(lstm_persist_fwd_bf16_kernel<4>, grid, dim3(512), PFWD_LDS, stream, whh_bf, gates, c_tm, h_tm,
@@ -959,19 +982,32 @@ int pbwd_debug() {
   }();
   return v;
 }
+// SV_PBWD_AGPR=0: leave the weight fragments' register class to the compiler
+int pbwd_agpr() {
+  static int v = [] {
+    const char* e = getenv("SV_PBWD_AGPR");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return v;
+}
 template <int NS, int P>
 void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const float* acts, const float* c_tm,
                  const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B,
                  int H, unsigned* cnt, unsigned* sync, float* dbp) {
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + SV_SYNC_STAMP);
-  if (bm == 32)
-    hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P, 32>), dim3(grid.x * grid.y), dim3(256), pbwd_lds(32), s,
-                       whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x,
-                       persist_xcd(), sync, persist_limit(), persist_fault(), pbwd_debug(), dbp, stamps);
+#define SV_PBWD_LAUNCH(BMV, AG)                                                                                   \
+  hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P, BMV, AG>), dim3(grid.x * grid.y), dim3(256), pbwd_lds(BMV), s, \
+                     whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x, persist_xcd(), \
+                     sync, persist_limit(), persist_fault(), pbwd_debug(), dbp, stamps)
+  if (bm == 32 && pbwd_agpr())
+    SV_PBWD_LAUNCH(32, true);
+  else if (bm == 32)
+    SV_PBWD_LAUNCH(32, false);
+  else if (pbwd_agpr())
+    SV_PBWD_LAUNCH(64, true);
   else
-    hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P, 64>), dim3(grid.x * grid.y), dim3(256), pbwd_lds(64), s,
-                       whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x,
-                       persist_xcd(), sync, persist_limit(), persist_fault(), pbwd_debug(), dbp, stamps);
+    SV_PBWD_LAUNCH(64, false);
+#undef SV_PBWD_LAUNCH
 }
 }  // namespace
 
