@@ -98,6 +98,7 @@ __global__ void colsum_partial_kernel(const float* __restrict__ X, int R, int C,
   if (col >= C) return;
   const int r0 = chunk * rows_per_chunk, r1 = min(R, r0 + rows_per_chunk);
   float s = 0.f;
+#pragma unroll 8
   for (int r = r0; r < r1; ++r) s += X[(long)r * C + col];
   partial[(long)chunk * C + col] = s;
 }
@@ -838,8 +839,17 @@ extern "C" int sv_transpose(const float* src, long ld_src, int R, int C, float* 
   return SV_OK;
 }
 
+// rows per partial-sum chunk: about 1024 workgroups in all, chunks of 32..1024 rows, so a small R
+// (the projection's B rows) still spreads over many workgroups instead of one thread walking
+// every row, and a large R keeps the final pass short
+static int colsum_rows(int R, int C) {
+  const int target = std::max(1, 1024 / ((C + 255) / 256));
+  int rpc = (R + target - 1) / target;
+  rpc = (rpc + 31) / 32 * 32;
+  return std::min(1024, std::max(32, rpc));
+}
 static int colsum(const float* X, int R, int C, float* out0, float* out1, float* partial, hipStream_t s) {
-  const int rows_per_chunk = 1024;
+  const int rows_per_chunk = colsum_rows(R, C);
   const int nchunk = (R + rows_per_chunk - 1) / rows_per_chunk;
   hipLaunchKernelGGL(colsum_partial_kernel, dim3((C + 255) / 256, nchunk), dim3(256), 0, s, X, R, C, rows_per_chunk,
                      partial);
@@ -849,7 +859,10 @@ static int colsum(const float* X, int R, int C, float* out0, float* out1, float*
   return SV_OK;
 }
 
-extern "C" size_t sv_colsum_workspace(int R, int C) { return (size_t)((R + 1023) / 1024) * C * sizeof(float); }
+extern "C" size_t sv_colsum_workspace(int R, int C) {
+  const int rpc = colsum_rows(R, C);
+  return (size_t)((R + rpc - 1) / rpc) * C * sizeof(float);
+}
 
 extern "C" int sv_colsum(const float* X, int R, int C, float* out, float* workspace, hipStream_t stream) {
   if (!X || !out || !workspace || R <= 0 || C <= 0) return SV_EARG;
