@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SV_ABI_VERSION 2
+#define SV_ABI_VERSION 3
 int sv_abi_version(void);
 
 /* ---- fp32 product modes (`products` argument of sv_gemm_f32 / sv_lstm_stack_fwd / _bwd; every
@@ -161,22 +161,29 @@ int sv_ge2e_calc_loss(const float* S, int N, int M, int K, float* per, float* lo
 int sv_eer_counts(const float* S, int N, int M2, int Nc, const float* thresholds, int n_thr, float* cnt_all,
                   float* cnt_diag, hipStream_t stream);
 
-/* ---- bf16-operand variant (BASELINE config c3, mixed precision) ------------------------------
- * GEMM operands (weights, h, dgates) in bf16 (RNE casts), v_mfma_f32_32x32x16_bf16 with fp32
- * accumulation; gates/cell state/biases/gradients/outputs fp32.  Same layouts as the fp32 entry
- * points, except transposed layouts use column blocks of Bp = (B + 7) & ~7 and F, H, K and every
- * bf16 leading dimension must be multiples of 8.  sv_bf16 = raw bf16 bits. */
+/* ---- bf16 mixed-precision variant (BASELINE config c3) ---------------------------------------
+ * GEMM operands (weights, h, dgates) in bf16 (RNE casts), bf16 MFMA with fp32 accumulation;
+ * the stored x-projection (K1 output incl. biases) and the saved activated gates are bf16 (ABI
+ * v3: `gates` is sv_bf16 [T,B,4H] -- in: bf16(x W_ih^T + b_ih + b_hh), out: bf16 activations;
+ * the cell update itself runs on the fp32 sums and fp32 activations); cell state, biases,
+ * gradients and outputs fp32.  Same layouts as the fp32 entry points, except transposed layouts
+ * use column blocks of Bp = (B + 7) & ~7 and F, H, K and every bf16 leading dimension must be
+ * multiples of 8.  sv_bf16 = raw bf16 bits. */
 typedef unsigned short sv_bf16;
 size_t sv_gemm_bf16_workspace(int M, int N, int K);
 /* C[M,N] (fp32) = A[M,K] . B[N,K]^T (+ bias0 + bias1) (+ beta C); both operands k-contiguous */
 int sv_gemm_bf16(int M, int N, int K, const sv_bf16* A, long lda, const sv_bf16* B, long ldb, float* C, long ldc,
                  const float* bias0, const float* bias1, float beta, float* workspace, hipStream_t stream);
+/* C[M,N] (bf16) = bf16(A[M,K] . B[N,K]^T + bias0 + bias1): fp32 accumulation, one rounding (the
+ * x-projection store of the bf16 LSTM); ldc % 4 == 0 for the 256 x 256 kernel, else a slower one */
+int sv_gemm_bf16_bf(int M, int N, int K, const sv_bf16* A, long lda, const sv_bf16* B, long ldb, sv_bf16* C,
+                    long ldc, const float* bias0, const float* bias1, hipStream_t stream);
 int sv_cast_bf16(const float* x, sv_bf16* y, long n, hipStream_t stream);
 int sv_transpose_cast_bf16(const float* src, long ld_src, int R, int C, sv_bf16* dst, long ld_dst,
                            hipStream_t stream);
-/* x_bf [T,B,F]; writes gates/c_tm/h_tm (fp32) plus h_bf [T+1,B,H] and hT [H,(T+1)Bp] (bf16) */
+/* x_bf [T,B,F]; writes gates (bf16), c_tm/h_tm (fp32) plus h_bf [T+1,B,H] and hT [H,(T+1)Bp] (bf16) */
 int sv_lstm_layer_fwd_bf16(const sv_bf16* x_bf, int T, int B, int F, int H, const sv_bf16* w_ih_bf,
-                           const sv_bf16* w_hh_bf, const float* b_ih, const float* b_hh, float* gates, float* c_tm,
+                           const sv_bf16* w_hh_bf, const float* b_ih, const float* b_hh, sv_bf16* gates, float* c_tm,
                            float* h_tm, sv_bf16* h_bf, sv_bf16* hT, hipStream_t stream);
 /* layer-pipelined stack forward in bf16 (as sv_lstm_stack_fwd; h_bf per layer [T+1,B,H]).
  * sync: the caller's sync block (below; required when the persistent recurrences run).
@@ -184,13 +191,13 @@ int sv_lstm_layer_fwd_bf16(const sv_bf16* x_bf, int T, int B, int F, int H, cons
  * launch (before / after; only when the persistent schedule runs) -- in-step kernel timing. */
 int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* x_bf, const sv_bf16* const* w_ih_bf,
                            const sv_bf16* const* w_hh_bf, const float* const* b_ih, const float* const* b_hh,
-                           float* const* gates, float* const* c_tm, float* const* h_tm, sv_bf16* const* h_bf,
+                           sv_bf16* const* gates, float* const* c_tm, float* const* h_tm, sv_bf16* const* h_bf,
                            sv_bf16* const* hT, int chunk, hipStream_t main, const hipStream_t* side,
                            hipEvent_t* ev, void* sync, hipEvent_t* probe);
 size_t sv_lstm_layer_bwd_bf16_workspace(int T, int B, int F, int H);
 /* wihT_bf [F,4H], whhT_bf [H,4H]; dg_bf [T,B,4H] and dgT_bf [4H,T*Bp] are bf16 outputs */
 int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const sv_bf16* xT_bf, long ld_xT, const sv_bf16* wihT_bf,
-                           const sv_bf16* whhT_bf, const float* gates, const float* c_tm, const sv_bf16* hT_bf,
+                           const sv_bf16* whhT_bf, const sv_bf16* gates, const float* c_tm, const sv_bf16* hT_bf,
                            const float* dh_up, int dh_up_full, sv_bf16* dg_bf, sv_bf16* dgT_bf, float* dx_tm,
                            float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, float* workspace,
                            hipStream_t stream);
@@ -200,7 +207,7 @@ int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const sv_bf16* xT_bf, lon
  * forward's, around each layer's persistent backward recurrence. */
 size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H);
 int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* const* xT, const long* ld_xT,
-                           const float* const* w_ih, const float* const* w_hh, const float* const* gates,
+                           const float* const* w_ih, const float* const* w_hh, const sv_bf16* const* gates,
                            const float* const* c_tm, const sv_bf16* const* hT, const float* dh_last,
                            sv_bf16* const* dg, sv_bf16* const* dgT, float* const* dx, float* const* dw_ih,
                            float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace, int chunk,

@@ -1,16 +1,19 @@
 """ORACLE (test infrastructure only) -- the SpeechEmbedder training step in fp32 with the
-mixed-precision operand rounding of BASELINE config c3 (bf16 GEMM operands, fp32 accumulation,
-fp32 cell state / activations / gradients / loss), restated on plain torch-CPU float32 ops.
+mixed-precision rounding of BASELINE config c3 (bf16 GEMM operands, fp32 accumulation; bf16
+storage of the x-projection and of the saved activations; fp32 cell state / gradients / loss),
+restated on plain torch-CPU float32 ops.
 
 Follows the same reference lines as lstm_np.py (speech_embedder_net.py:19,27-33 for nn.LSTM +
 last frame + Linear + L2 norm; utils.py:27-132 + speech_embedder_net.py:43-49 for GE2E;
 train_speech_embedder.py:54-65 for the step).  The only difference from the reference's fp32
 arithmetic is the operand quantiser ``q`` applied where the c3 path feeds a GEMM:
 
-  forward   gates_t = q(x_t) q(W_ih)^T + b_ih + b_hh + q(h_{t-1}) q(W_hh)^T      (every layer;
-            layer l > 0 reads q(h) of layer l-1); c, h, the activations fp32; the projection
-            and the norm fp32 (they read the fp32 h of the last layer)
-  backward  dh_rec = q(dG_{t+1}) q(W_hh); dW_ih += q(dG_t)^T q(x_t); dW_hh += q(dG_t)^T q(h_{t-1});
+  forward   gates_t = q(q(x_t) q(W_ih)^T + b_ih + b_hh) + q(h_{t-1}) q(W_hh)^T   (every layer;
+            layer l > 0 reads q(h) of layer l-1; the x-projection incl. biases is stored in
+            bf16, ABI v3); c, h and the activations that form them fp32; the projection and
+            the norm fp32 (they read the fp32 h of the last layer)
+  backward  the saved activations q(i), q(f), q(g), q(o) (bf16 storage) with fp32 c;
+            dh_rec = q(dG_{t+1}) q(W_hh); dW_ih += q(dG_t)^T q(x_t); dW_hh += q(dG_t)^T q(h_{t-1});
             db += q(dG_t) (fp32 sum of the rounded values); dx_t = q(dG_t) q(W_ih) (fp32, added to
             the layer below's dh in fp32)
 
@@ -55,7 +58,7 @@ def embedder_forward(params, x, L, bf16=True):
         H = Whh.shape[1]
         qWih, qWhh = q(Wih), q(Whh)
         xq = q(inp)
-        gx = (xq.reshape(B * T, -1) @ qWih.T).reshape(B, T, 4 * H) + (bih + bhh)
+        gx = q((xq.reshape(B * T, -1) @ qWih.T).reshape(B, T, 4 * H) + (bih + bhh))
         h = torch.zeros(B, H)
         c = torch.zeros(B, H)
         hs = torch.empty(B, T, H)
@@ -68,7 +71,7 @@ def embedder_forward(params, x, L, bf16=True):
             c = f * c + i * gg
             h = o * torch.tanh(c)
             hs[:, t], cs[:, t] = h, c
-            acts[:, t] = torch.cat([i, f, gg, o], dim=1)
+            acts[:, t] = q(torch.cat([i, f, gg, o], dim=1))
         caches.append((xq, hs, cs, acts))
         inp = hs
     last = inp[:, -1]

@@ -61,6 +61,7 @@ SIGNATURES = {
     "sv_gemm_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int]),
     "sv_gemm_bf16": (_c_int, [_c_int, _c_int, _c_int, _P, _c_long, _P, _c_long, _P, _c_long, _P, _P, _c_float, _P,
                               _P]),
+    "sv_gemm_bf16_bf": (_c_int, [_c_int, _c_int, _c_int, _P, _c_long, _P, _c_long, _P, _c_long, _P, _P, _P]),
     "sv_cast_bf16": (_c_int, [_P, _P, _c_long, _P]),
     "sv_transpose_cast_bf16": (_c_int, [_P, _c_long, _c_int, _c_int, _P, _c_long, _P]),
     "sv_lstm_layer_fwd_bf16": (_c_int, [_P, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -235,6 +235,17 @@ __device__ __forceinline__ bf16_t to_bf(float x) {
   const __bf16 b = (__bf16)x;
   return *reinterpret_cast<const bf16_t*>(&b);
 }
+__device__ __forceinline__ float from_bf(bf16_t x) { return __uint_as_float((unsigned)x << 16); }
+// x rounded to bf16 (nearest even) and back: the stored x-projection of the bf16 path
+__device__ __forceinline__ float round_bf(float x) { return from_bf(to_bf(x)); }
+// 4 consecutive bf16 <-> 4 floats (8-B loads / stores of activations and x-projections)
+__device__ __forceinline__ uint2 pack_bf4(float a, float b, float c, float d) {
+  return uint2{(unsigned)to_bf(a) | ((unsigned)to_bf(b) << 16), (unsigned)to_bf(c) | ((unsigned)to_bf(d) << 16)};
+}
+__device__ __forceinline__ float4 unpack_bf4(uint2 p) {
+  return float4{__uint_as_float(p.x << 16), __uint_as_float(p.x & 0xffff0000u), __uint_as_float(p.y << 16),
+                __uint_as_float(p.y & 0xffff0000u)};
+}
 
 // LSTM cell forward of one element, shared by the bf16 step, wavefront and persistent kernels
 // (contraction off, so every schedule rounds identically): pre-activations (recurrent part p +
@@ -293,7 +304,7 @@ __device__ __forceinline__ float lstm_cell_bwd(float dh, float i, float f, float
 // counter channel
 extern "C" int sv_persist_fwd_ok(int B, int H);
 int sv_persist_fwd_fusex_ok(int H, int F);
-int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates, float* c_tm, float* h_tm,
+int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates, float* c_tm, float* h_tm,
                         bf16_t* h_bf, bf16_t* hT, hipStream_t stream, unsigned* sync, int chan = 0,
                         const bf16_t* x_bf = nullptr, int F = 0, const bf16_t* wih_bf = nullptr,
                         const float* b_ih = nullptr, const float* b_hh = nullptr, hipEvent_t pre = nullptr,
@@ -302,7 +313,7 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates,
 extern "C" int sv_persist_bwd_ok(int B, int H);
 extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H);
 int sv_persist_bm(int B, int H, int cus);
-int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* acts, const float* c_tm,
+int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
                         const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream,
                         unsigned* sync, float* db_ih = nullptr, float* db_hh = nullptr, hipEvent_t pre = nullptr,
                         hipEvent_t post = nullptr);
@@ -317,6 +328,6 @@ int sv_persist_fault(int bwd);
 int sv_wave_fwd_fits(int L, int B, int F, int H, int cus);
 int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, const bf16_t* const* w_ih_bf,
                      const bf16_t* const* w_hh_bf, const float* const* b_ih, const float* const* b_hh,
-                     float* const* gates, float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
+                     bf16_t* const* gates, float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
                      bf16_t* const* hT, unsigned* sync, hipStream_t stream, unsigned limit, int fault, hipEvent_t pre,
                      hipEvent_t post);

@@ -16,11 +16,11 @@
 // ============================================================================
 // GEMM: C[M,N] fp32 = A[M,K] . B[N,K]^T (bf16, both k-contiguous) (+bias) / split-K slabs
 // ============================================================================
-enum { BEPI_STORE = 0, BEPI_SLAB = 1 };
+enum { BEPI_STORE = 0, BEPI_SLAB = 1, BEPI_STORE_BF16 = 2 };
 
 template <int BM, int BN, int EPI>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict__ A, long lda,
-                                                        const bf16_t* __restrict__ B, long ldb, float* __restrict__ C,
+                                                        const bf16_t* __restrict__ B, long ldb, void* __restrict__ Cv,
                                                         long ldc, long slab, int M, int N, int K, int kchunk,
                                                         const float* __restrict__ bias0,
                                                         const float* __restrict__ bias1, float beta) {
@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
   zero_acc(acc);
   gemm_mainloop_bf<BM, BN, 256, BBK, TM, TN>(A, lda, RowMapLinear{tm * BM, M}, B, ldb, RowMapLinear{tn * BN, N}, kbeg,
                                              kend, ldsb, tid, wm0, wn0, acc);
-  float* Cz = C + (EPI == BEPI_SLAB ? (long)blockIdx.y * slab : 0);
+  float* Cz = reinterpret_cast<float*>(Cv) + (EPI == BEPI_SLAB ? (long)blockIdx.y * slab : 0);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
       const int col = tn * BN + wn0 + 32 * j + (lane & 31);
       if (col >= N) continue;
       float badd = 0.f;
-      if (EPI == BEPI_STORE) {
+      if (EPI != BEPI_SLAB) {
         if (bias0) badd += bias0[col];
         if (bias1) badd += bias1[col];
       }
@@ -57,6 +57,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
         const int row = tm * BM + wm0 + 32 * i + acc_row(r, lane);
         if (row >= M) continue;
         float v = acc[i][j][r];
+        if (EPI == BEPI_STORE_BF16) {
+          reinterpret_cast<bf16_t*>(Cv)[(long)row * ldc + col] = to_bf(v + badd);
+          continue;
+        }
         float* dst = Cz + (long)row * ldc + col;
         if (EPI == BEPI_STORE) {
           v += badd;
@@ -69,7 +73,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
 
 __global__ void slab_reduce_bf_kernel(const float* __restrict__ slab, int nz, long zstride, float* __restrict__ out,
                                       long ldc, int M, int N, float beta, const float* __restrict__ bias0,
-                                      const float* __restrict__ bias1) {
+                                      const float* __restrict__ bias1, bf16_t* __restrict__ outb = nullptr) {
   const long total = (long)M * N;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const int row = (int)(e / N), col = (int)(e % N);
@@ -77,6 +81,10 @@ __global__ void slab_reduce_bf_kernel(const float* __restrict__ slab, int nz, lo
     for (int z = 0; z < nz; ++z) s += slab[z * zstride + e];
     if (bias0) s += bias0[col];
     if (bias1) s += bias1[col];
+    if (outb) {  // bf16 output (beta unused)
+      outb[(long)row * ldc + col] = to_bf(s);
+      continue;
+    }
     float* dst = out + (long)row * ldc + col;
     *dst = (beta != 0.f ? beta * *dst : 0.f) + s;
   }
@@ -135,7 +143,7 @@ __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const bf16_t* __restri
 
 template <int SC>
 __global__ __launch_bounds__(512) void lstm_step_fwd_bf16_kernel(
-    const bf16_t* __restrict__ hprev_bf, const bf16_t* __restrict__ whh_bf, float* __restrict__ gates,
+    const bf16_t* __restrict__ hprev_bf, const bf16_t* __restrict__ whh_bf, bf16_t* __restrict__ gates,
     const float* __restrict__ cprev, float* __restrict__ cout, float* __restrict__ hout, bf16_t* __restrict__ hout_bf,
     bf16_t* __restrict__ hT, long ldhT, int t, int Bp, int B, int H) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -152,9 +160,9 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_bf16_kernel(
     const int e = tid + 512 * k, b = e / BF_U, u = e % BF_U;
     const int gb = b0 + b, gj = j0 + u;
     const bool ok = gb < B && gj < H;
-    const float* gp = gates + (long)gb * G + gj;
+    const bf16_t* gp = gates + (long)gb * G + gj;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) xg[k][q] = ok ? gp[q * H] : 0.f;
+    for (int q = 0; q < 4; ++q) xg[k][q] = ok ? from_bf(gp[q * H]) : 0.f;
     cpv[k] = (ok && cprev) ? cprev[(long)gb * H + gj] : 0.f;
   }
   f32x16 acc[1][1];
@@ -172,15 +180,15 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_bf16_kernel(
     const int e = tid + 512 * k, b = e / BF_U, u = e % BF_U;
     const int gb = b0 + b, gj = j0 + u;
     if (gb >= B || gj >= H) continue;
-    float* gp = gates + (long)gb * G + gj;
+    bf16_t* gp = gates + (long)gb * G + gj;
     const float* pr = pre + b * LDP + u;
     const float pv[4] = {pr[0], pr[BF_U], pr[2 * BF_U], pr[3 * BF_U]};
     float av[4], h;
     const float c = lstm_cell_fwd(pv, xg[k], cpv[k], av, h);
-    gp[0] = av[0];
-    gp[H] = av[1];
-    gp[2 * H] = av[2];
-    gp[3 * H] = av[3];
+    gp[0] = to_bf(av[0]);
+    gp[H] = to_bf(av[1]);
+    gp[2 * H] = to_bf(av[2]);
+    gp[3 * H] = to_bf(av[3]);
     cout[(long)gb * H + gj] = c;
     hout[(long)gb * H + gj] = h;
     hout_bf[(long)gb * H + gj] = to_bf(h);
@@ -212,7 +220,7 @@ struct WaveFwdArgs {
   const bf16_t* whh[SV_MAXL];
   const float* bih[SV_MAXL];
   const float* bhh[SV_MAXL];
-  float* gates[SV_MAXL];
+  bf16_t* gates[SV_MAXL];  // layer 0: the x-projection in, then bf16 activations; others: out
   float* c[SV_MAXL];
   float* h[SV_MAXL];
   bf16_t* hb[SV_MAXL];
@@ -234,7 +242,7 @@ __global__ __launch_bounds__(512) void lstm_wave_fwd_bf16_kernel(const WaveFwdAr
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int j0 = blockIdx.x * BF_U, b0 = blockIdx.y * BF_BM;
   const int wm0 = (w >> 2) * 32, wn0 = (w & 3) * 32;
-  float* gates = a.gates[l] + (long)t * B * G;
+  bf16_t* gates = a.gates[l] + (long)t * B * G;
   const float* cprev = t ? a.c[l] + (long)(t - 1) * BH : nullptr;
   float xg[PER][4], cpv[PER];
 #pragma unroll
@@ -243,9 +251,9 @@ __global__ __launch_bounds__(512) void lstm_wave_fwd_bf16_kernel(const WaveFwdAr
     const int gb = b0 + b, gj = j0 + u;
     const bool ok = gb < B && gj < H;
     if (l == 0) {
-      const float* gp = gates + (long)gb * G + gj;
+      const bf16_t* gp = gates + (long)gb * G + gj;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) xg[k][q] = ok ? gp[q * H] : 0.f;
+      for (int q = 0; q < 4; ++q) xg[k][q] = ok ? from_bf(gp[q * H]) : 0.f;
     } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q) xg[k][q] = ok ? a.bih[l][q * H + gj] + a.bhh[l][q * H + gj] : 0.f;
@@ -275,15 +283,15 @@ __global__ __launch_bounds__(512) void lstm_wave_fwd_bf16_kernel(const WaveFwdAr
     const int e = tid + 512 * k, b = e / BF_U, u = e % BF_U;
     const int gb = b0 + b, gj = j0 + u;
     if (gb >= B || gj >= H) continue;
-    float* gp = gates + (long)gb * G + gj;
+    bf16_t* gp = gates + (long)gb * G + gj;
     const float* pr = pre + b * LDP + u;
     const float pv[4] = {pr[0], pr[BF_U], pr[2 * BF_U], pr[3 * BF_U]};
     float av[4], h;
     const float c = lstm_cell_fwd(pv, xg[k], cpv[k], av, h);
-    gp[0] = av[0];
-    gp[H] = av[1];
-    gp[2 * H] = av[2];
-    gp[3 * H] = av[3];
+    gp[0] = to_bf(av[0]);
+    gp[H] = to_bf(av[1]);
+    gp[2 * H] = to_bf(av[2]);
+    gp[3 * H] = to_bf(av[3]);
     cout[(long)gb * H + gj] = c;
     hout[(long)gb * H + gj] = h;
     hout_bf[(long)gb * H + gj] = to_bf(h);
@@ -305,7 +313,7 @@ __global__ __launch_bounds__(512) void lstm_wave_fwd_bf16_kernel(const WaveFwdAr
 template <int SC>
 __global__ __launch_bounds__(512) void lstm_step_bwd_bf16_kernel(
     const bf16_t* __restrict__ dgnext, const bf16_t* __restrict__ whhT, const float* __restrict__ dhup,
-    const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
+    const float* __restrict__ dcf_next, const bf16_t* __restrict__ acts, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, bf16_t* __restrict__ dg, float* __restrict__ dcf, bf16_t* __restrict__ dgT,
     long lddgT, int t, int Bp, int B, int H) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -325,9 +333,9 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_bf16_kernel(
     const int gb = b0 + b, gj = j0 + u;
     const bool ok = gb < B && gj < H;
     const long hi = (long)gb * H + gj;
-    const float* ap = acts + (long)gb * G + gj;
+    const bf16_t* ap = acts + (long)gb * G + gj;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) av[k][q] = ok ? ap[q * H] : 0.f;
+    for (int q = 0; q < 4; ++q) av[k][q] = ok ? from_bf(ap[q * H]) : 0.f;
     cv[k] = ok ? c_t[hi] : 0.f;
     cpv[k] = (ok && c_prev) ? c_prev[hi] : 0.f;
     dcfv[k] = (ok && dcf_next) ? dcf_next[hi] : 0.f;
@@ -408,6 +416,51 @@ bool gemm256p() {
   return on;
 }
 
+// the 256 x 256 tile's schedule: 2 = 8-phase (default), 1 = four-stage (SV_GEMM256P=1),
+// 0 = two-stage (SV_GEMM8P=0); the 8-phase epilogue stores 16 B per lane, so it needs 16-B
+// aligned C rows and biases
+int g256_variant(const void* C, long ldc, const float* bias0, const float* bias1) {
+  static int v = [] {
+    if (gemm256p()) return 1;
+    const char* e = getenv("SV_GEMM8P");
+    return (e && *e == '0') ? 0 : 2;
+  }();
+  if (v == 2 && ((((uintptr_t)C | (uintptr_t)bias0 | (uintptr_t)bias1) & 15) || ldc % 4)) return 0;
+  return v;
+}
+
+template <int EPI, int AF>
+void launch_g8(dim3 grid, hipStream_t stream, const bf16_t* A, long lda, const bf16_t* B, long ldb, void* C, long ldc,
+               long slab, int M, int N, int K, int kchunk, const float* bias0, const float* bias1, float beta,
+               G256AFrag af = G256AFrag{}) {
+  // SV_G8_SCHED: 0 (default) fills issued over phases 0 and 1, B nh0 re-read in phase 3; 1 both
+  // fills in phase 0 with B nh0 kept in registers (measured 3-4 % slower on K1 / dx)
+  static const int sched = [] {
+    const char* e = getenv("SV_G8_SCHED");
+    return e ? atoi(e) : 0;
+  }();
+  if (sched == 0)
+    hipLaunchKernelGGL((gemm_bf16_8p_kernel<EPI, AF, 0>), grid, dim3(512), G256_LDS, stream, A, lda, B, ldb, C, ldc,
+                       slab, M, N, K, kchunk, bias0, bias1, beta, af);
+  else
+    hipLaunchKernelGGL((gemm_bf16_8p_kernel<EPI, AF, 1>), grid, dim3(512), G256_LDS, stream, A, lda, B, ldb, C, ldc,
+                       slab, M, N, K, kchunk, bias0, bias1, beta, af);
+}
+
+template <int EPI, int AF>
+void launch_g256(int variant, dim3 grid, hipStream_t stream, const bf16_t* A, long lda, const bf16_t* B, long ldb,
+                 void* C, long ldc, long slab, int M, int N, int K, int kchunk, const float* bias0,
+                 const float* bias1, float beta, G256AFrag af = G256AFrag{}) {
+  if (variant == 2)
+    launch_g8<EPI, AF>(grid, stream, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, bias0, bias1, beta, af);
+  else if (variant == 1)
+    hipLaunchKernelGGL((gemm_bf16_256p_kernel<EPI, AF>), grid, dim3(512), G256_LDS, stream, A, lda, B, ldb, (float*)C,
+                       ldc, slab, M, N, K, kchunk, bias0, bias1, beta, af);
+  else
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, AF>), grid, dim3(512), G256_LDS, stream, A, lda, B, ldb, (float*)C,
+                       ldc, slab, M, N, K, kchunk, bias0, bias1, beta, af);
+}
+
 BPlan plan_bf16(int M, int N, int K) {
   BPlan p;
   if (gemm256_ok(M, N, K)) {  // one workgroup per CU: split K only to fill the 256 CUs
@@ -445,7 +498,7 @@ BPlan plan_bf16(int M, int N, int K) {
 }
 
 template <int BM, int BN, int EPI>
-void launch_bf(const bf16_t* A, long lda, const bf16_t* B, long ldb, float* C, long ldc, long slab, int M, int N, int K,
+void launch_bf(const bf16_t* A, long lda, const bf16_t* B, long ldb, void* C, long ldc, long slab, int M, int N, int K,
                int splitk, int kchunk, const float* b0, const float* b1, float beta, hipStream_t s) {
   constexpr int LDS = 2 * (BM + BN) * (BBK + 8) * (int)sizeof(bf16_t);
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
@@ -470,7 +523,7 @@ int bf16_sc() {
   }();
   return v;
 }
-void launch_fwd_bf16(dim3 grid, hipStream_t s, const bf16_t* hp, const bf16_t* whh, float* g, const float* cp,
+void launch_fwd_bf16(dim3 grid, hipStream_t s, const bf16_t* hp, const bf16_t* whh, bf16_t* g, const float* cp,
                      float* c, float* h, bf16_t* hb, bf16_t* hT, long ldhT, int t, int Bp, int B, int H) {
   const int sc = bf16_sc();
   if (sc == 203)
@@ -578,7 +631,7 @@ int bf16_bsc() {
   return v;
 }
 void launch_bwd_bf16(dim3 grid, hipStream_t s, const bf16_t* dgn, const bf16_t* whhT, const float* up,
-                     const float* dcfi, const float* acts, const float* ct, const float* cp, bf16_t* dg, float* dcfo,
+                     const float* dcfi, const bf16_t* acts, const float* ct, const float* cp, bf16_t* dg, float* dcfo,
                      bf16_t* dgT, long lddgT, int t, int Bp, int B, int H) {
   const int sc = bf16_bsc();
   if (sc == 206)
@@ -621,22 +674,14 @@ extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, cons
     const int tiles = (M / G256_BM) * (N / G256_BM);
     const long slab = (long)M * N;
     if (p.splitk == 1) {
-      if (gemm256p())
-        hipLaunchKernelGGL((gemm_bf16_256p_kernel<G256_STORE>), dim3(tiles, 1), dim3(512), G256_LDS, stream, A, lda, B,
-                         ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1, beta);
-      else
-        hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_STORE>), dim3(tiles, 1), dim3(512), G256_LDS, stream, A, lda, B,
-                         ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1, beta);
+      launch_g256<G256_STORE, 0>(g256_variant(C, ldc, bias0, bias1), dim3(tiles, 1), stream, A, lda, B, ldb, C, ldc, 0L,
+                                 M, N, K, p.kchunk, bias0, bias1, beta);
       SV_LAUNCH_CHECK();
       return SV_OK;
     }
     if (!workspace) return SV_EARG;
-    if (gemm256p())
-      hipLaunchKernelGGL((gemm_bf16_256p_kernel<G256_SLAB>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream, A, lda,
-                       B, ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr, 0.f);
-    else
-      hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_SLAB>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream, A, lda,
-                       B, ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr, 0.f);
+    launch_g256<G256_SLAB, 0>(g256_variant(workspace, N, nullptr, nullptr), dim3(tiles, p.splitk), stream, A, lda, B,
+                              ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr, 0.f);
     SV_LAUNCH_CHECK();
     const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
     hipLaunchKernelGGL(slab_reduce_bf_kernel, dim3(grid), dim3(256), 0, stream, workspace, p.splitk, slab, C, ldc, M, N,
@@ -668,6 +713,32 @@ extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, cons
   return SV_OK;
 }
 
+// C[M,N] bf16 = bf16(A . B^T + bias0 + bias1) (fp32 accumulation, one rounding): the bf16
+// path's x-projection (K1), stored in the gates buffer the recurrence then overwrites with its
+// bf16 activations.  The 8-phase 256 x 256 kernel where the shape tiles (no split-K), else the
+// 128 x 128 / 64 x 64 kernel without split-K -- one kernel per shape, so every schedule that
+// forms the same projection rounds it identically.
+extern "C" int sv_gemm_bf16_bf(int M, int N, int K, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C,
+                               long ldc, const float* bias0, const float* bias1, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || !A || !B || !C) return SV_EARG;
+  if (K % 8 || lda % 8 || ldb % 8 || (((uintptr_t)A | (uintptr_t)B) & 15)) return SV_EALIGN;
+  const BPlan p = plan_bf16(M, N, K);
+  if (p.bm == G256_BM && p.splitk == 1 && g256_variant(nullptr, 0, bias0, bias1) == 2 && ldc % 4 == 0 &&
+      !((uintptr_t)C & 7)) {
+    const int tiles = (M / G256_BM) * (N / G256_BM);
+    launch_g8<G8_STORE_BF16, 0>(dim3(tiles, 1), stream, A, lda, B, ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1,
+                                0.f);
+  } else if ((long)((M + 127) / 128) * ((N + 127) / 128) < 128) {
+    launch_bf<64, 64, BEPI_STORE_BF16>(A, lda, B, ldb, C, ldc, 0, M, N, K, 1, ((K + BBK - 1) / BBK) * BBK, bias0,
+                                       bias1, 0.f, stream);
+  } else {
+    launch_bf<128, 128, BEPI_STORE_BF16>(A, lda, B, ldb, C, ldc, 0, M, N, K, 1, ((K + BBK - 1) / BBK) * BBK, bias0,
+                                         bias1, 0.f, stream);
+  }
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
 // dx = dG . W_ih with dG read from the persistent backward's fragment-order hand-off buffer
 // (no row-major dG copy): M = T * B rows (t, b), K = 4H; needs B % 32, M % 256, N % 256, H % 64
 bool gemm_afrag_ok(int T, int B, int N, int H) {
@@ -686,25 +757,15 @@ int gemm_bf16_afrag(int T, int B, int H, int N, const bf16_t* dgf, int bm, const
   const G256AFrag af{dgf, fs, B, bm, H};
   const BPlan p = plan_bf16(M, N, K);
   if (p.splitk == 1) {
-    if (gemm256p())
-      hipLaunchKernelGGL((gemm_bf16_256p_kernel<G256_STORE, 1>), dim3(tiles, 1), dim3(512), G256_LDS, stream,
-                       (const bf16_t*)nullptr, 0L, Bop, ldb, C, ldc, 0L, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
-    else
-      hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_STORE, 1>), dim3(tiles, 1), dim3(512), G256_LDS, stream,
-                       (const bf16_t*)nullptr, 0L, Bop, ldb, C, ldc, 0L, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
+    launch_g256<G256_STORE, 1>(g256_variant(C, ldc, nullptr, nullptr), dim3(tiles, 1), stream, nullptr, 0L, Bop, ldb, C,
+                               ldc, 0L, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
     SV_LAUNCH_CHECK();
     return SV_OK;
   }
   if (!workspace) return SV_EARG;
   const long slab = (long)M * N;
-  if (gemm256p())
-    hipLaunchKernelGGL((gemm_bf16_256p_kernel<G256_SLAB, 1>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream,
-                     (const bf16_t*)nullptr, 0L, Bop, ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr,
-                     0.f, af);
-  else
-    hipLaunchKernelGGL((gemm_bf16_256_kernel<G256_SLAB, 1>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream,
-                     (const bf16_t*)nullptr, 0L, Bop, ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr,
-                     0.f, af);
+  launch_g256<G256_SLAB, 1>(g256_variant(workspace, N, nullptr, nullptr), dim3(tiles, p.splitk), stream, nullptr, 0L,
+                            Bop, ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
   SV_LAUNCH_CHECK();
   const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
   hipLaunchKernelGGL(slab_reduce_bf_kernel, dim3(grid), dim3(256), 0, stream, workspace, p.splitk, slab, C, ldc, M, N,
@@ -731,12 +792,12 @@ extern "C" int sv_transpose_cast_bf16(const float* src, long ld_src, int R, int 
 }
 
 extern "C" int sv_lstm_layer_fwd_bf16(const bf16_t* x_bf, int T, int B, int F, int H, const bf16_t* w_ih_bf,
-                                      const bf16_t* w_hh_bf, const float* b_ih, const float* b_hh, float* gates,
+                                      const bf16_t* w_hh_bf, const float* b_ih, const float* b_hh, bf16_t* gates,
                                       float* c_tm, float* h_tm, bf16_t* h_bf, bf16_t* hT, hipStream_t stream) {
   if (!x_bf || !w_ih_bf || !w_hh_bf || !gates || !c_tm || !h_tm || !h_bf) return SV_EARG;
   if (T <= 0 || B <= 0 || F <= 0 || H <= 0 || F % 8 || H % 8) return SV_ESHAPE;
   const long BH = (long)B * H, BG = 4L * B * H;
-  int rc = sv_gemm_bf16(T * B, 4 * H, F, x_bf, F, w_ih_bf, F, gates, 4L * H, b_ih, b_hh, 0.f, nullptr, stream);
+  int rc = sv_gemm_bf16_bf(T * B, 4 * H, F, x_bf, F, w_ih_bf, F, gates, 4L * H, b_ih, b_hh, stream);
   if (rc) return rc;
   hipError_t e = hipMemsetAsync(h_tm, 0, BH * sizeof(float), stream);
   if (e != hipSuccess) return (int)e;
@@ -767,7 +828,7 @@ extern "C" size_t sv_lstm_layer_bwd_bf16_workspace(int T, int B, int F, int H) {
 }
 
 extern "C" int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const bf16_t* xT_bf, long ld_xT,
-                                      const bf16_t* wihT_bf, const bf16_t* whhT_bf, const float* gates,
+                                      const bf16_t* wihT_bf, const bf16_t* whhT_bf, const bf16_t* gates,
                                       const float* c_tm, const bf16_t* hT_bf, const float* dh_up, int dh_up_full,
                                       bf16_t* dg_bf, bf16_t* dgT_bf, float* dx_tm, float* dw_ih, float* dw_hh,
                                       float* db_ih, float* db_hh, float* workspace, hipStream_t stream) {
@@ -814,7 +875,7 @@ extern "C" int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const bf16_t* 
 // Layer-pipelined stack forward, bf16 operands (see sv_lstm_stack_fwd in sv_lstm.hip).
 extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf,
                                       const bf16_t* const* w_ih_bf, const bf16_t* const* w_hh_bf,
-                                      const float* const* b_ih, const float* const* b_hh, float* const* gates,
+                                      const float* const* b_ih, const float* const* b_hh, bf16_t* const* gates,
                                       float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
                                       bf16_t* const* hT, int chunk, hipStream_t main, const hipStream_t* side,
                                       hipEvent_t* ev, void* sync_block, hipEvent_t* probe) {
@@ -860,8 +921,7 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
           return rc;
         continue;
       }
-      rc = sv_gemm_bf16(T * B, 4 * H, Fl, in, Fl, w_ih_bf[l], Fl, gates[l], 4L * H, b_ih[l], b_hh[l], 0.f, nullptr,
-                        main);
+      rc = sv_gemm_bf16_bf(T * B, 4 * H, Fl, in, Fl, w_ih_bf[l], Fl, gates[l], 4L * H, b_ih[l], b_hh[l], main);
       if (rc) return rc;
       if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, sync, 0,
                                     nullptr, 0, nullptr, nullptr, nullptr, probe ? probe[2 * l] : nullptr,
@@ -877,8 +937,7 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
       if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(bf16_t), main)) != hipSuccess)
         return (int)e;
     }
-    int rc = sv_gemm_bf16(T * B, 4 * H, F, x_bf, F, w_ih_bf[0], F, gates[0], 4L * H, b_ih[0], b_hh[0], 0.f, nullptr,
-                          main);
+    int rc = sv_gemm_bf16_bf(T * B, 4 * H, F, x_bf, F, w_ih_bf[0], F, gates[0], 4L * H, b_ih[0], b_hh[0], main);
     if (rc) return rc;
     WaveFwdArgs a{};
     for (int l = 0; l < L; ++l) {
@@ -925,8 +984,8 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
       const int Fl = l == 0 ? F : H;
       const bf16_t* in = l == 0 ? x_bf + (long)t0 * B * F : h_bf[l - 1] + (long)(t0 + 1) * BH;
       if (l > 0 && (e = hipStreamWaitEvent(s, ev[(l - 1) * nch + cc], 0)) != hipSuccess) return (int)e;
-      int rc = sv_gemm_bf16((t1 - t0) * B, 4 * H, Fl, in, Fl, w_ih_bf[l], Fl, gates[l] + t0 * BG, 4L * H, b_ih[l],
-                            b_hh[l], 0.f, nullptr, s);
+      int rc = sv_gemm_bf16_bf((t1 - t0) * B, 4 * H, Fl, in, Fl, w_ih_bf[l], Fl, gates[l] + t0 * BG, 4L * H, b_ih[l],
+                               b_hh[l], s);
       if (rc) return rc;
       for (int t = t0; t < t1; ++t) {
         launch_fwd_bf16(grid, s, t ? h_bf[l] + t * BH : nullptr, w_hh_bf[l], gates[l] + t * BG,
@@ -980,7 +1039,7 @@ extern "C" size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, i
 }
 
 extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const bf16_t* const* xT, const long* ld_xT,
-                                      const float* const* w_ih, const float* const* w_hh, const float* const* gates,
+                                      const float* const* w_ih, const float* const* w_hh, const bf16_t* const* gates,
                                       const float* const* c_tm, const bf16_t* const* hT, const float* dh_last,
                                       bf16_t* const* dg, bf16_t* const* dgT, float* const* dx, float* const* dw_ih,
                                       float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace,

@@ -303,3 +303,207 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256p_kernel(const bf16_t* __
   }
   g256_epilogue_impl<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
 }
+
+// ---- 8-phase schedule (default; SV_GEMM8P=0 keeps gemm_bf16_256_kernel) ----
+// Same 256 x 256 x 64 tile, LDS images and DMA map as gemm_bf16_256_kernel, computed with
+// v_mfma_f32_16x16x32_bf16 in the phase schedule of cdna_hip_programming.md §5 ("The 256² 8-phase
+// template"): a k-tile is four phases, each one C quadrant (64 rows x 32 columns of the wave's
+// 128 x 64) over K = 64 = 16 MFMAs, bracketed by raw s_barriers.  The two wave groups (wr = 0 / 1,
+// one wave of each per SIMD) run one barrier apart, so one group's fragment reads and DMA issue
+// overlap the other group's MFMAs (s_setprio 1 around the MFMA cluster).
+//   phase 0: quadrant (0,0): read B nh0 (4 ds_read_b128) + A mh0 (8); issue A of k-tile kt + 1
+//   phase 1: quadrant (0,1): read B nh1 (4);                          issue B of k-tile kt + 1
+//   phase 2: quadrant (1,1): read A mh1 (8)
+//   phase 3: quadrant (1,0): read B nh0 (4);  s_waitcnt vmcnt(0) (k-tile kt + 1 landed)
+// Slot accounting (a slot = the span between two barriers; a group reads in every other slot and
+// computes in the next): a stage is re-filled >= 2 slots after its last read (A: last read in
+// phase 2, re-issued in the next k-tile's phase 0; B: phase 3 -> phase 1), so every read of it
+// has retired (the reader's lgkmcnt(0) precedes the barrier that ends its MFMA slot); the fill
+// of k-tile kt + 1 is waited for by every issuing wave before the barrier that ends its phase-3
+// read slot, which both groups pass before reading kt + 1.
+// The MFMA takes the B tile as its first operand, so each lane's 4 accumulator elements are 4
+// consecutive C columns of one row (16-B stores): acc[mt][nt][v] = C[16 mt + fr][16 nt + 4 fq + v].
+// The fragment reads are conflict-free on the swizzled image (slot ^ ((row >> 1) & 7)).
+typedef float g8_f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ g8_f32x4 mfma16_bf16(bf16x8_t a, bf16x8_t b, g8_f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+enum { G8_STORE = 0, G8_SLAB = 1, G8_STORE_BF16 = 2 };
+
+template <int EPI>
+__device__ __forceinline__ void g8_epilogue(g8_f32x4 (&acc)[8][4], void* Cv, long ldc, long slab, int tm, int tn,
+                                            int wr, int wc, int lane, const float* bias0, const float* bias1,
+                                            float beta) {
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int col = tn * G256_BM + wc * 64 + 16 * nt + 4 * fq;
+    g8_f32x4 badd = {0.f, 0.f, 0.f, 0.f};
+    if (EPI != G8_SLAB) {
+      if (bias0) badd += *reinterpret_cast<const g8_f32x4*>(bias0 + col);
+      if (bias1) badd += *reinterpret_cast<const g8_f32x4*>(bias1 + col);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const long row = (long)tm * G256_BM + wr * 128 + 16 * mt + fr;
+      g8_f32x4 v = acc[mt][nt];
+      if constexpr (EPI == G8_STORE_BF16) {
+        v += badd;
+        bf16_t* dst = reinterpret_cast<bf16_t*>(Cv) + row * ldc + col;
+        const unsigned lo = (unsigned)to_bf(v[0]) | ((unsigned)to_bf(v[1]) << 16);
+        const unsigned hi = (unsigned)to_bf(v[2]) | ((unsigned)to_bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(dst) = uint2{lo, hi};
+      } else {
+        float* dst = reinterpret_cast<float*>(Cv) + (EPI == G8_SLAB ? (long)blockIdx.y * slab : 0) + row * ldc + col;
+        if (EPI == G8_STORE) {
+          v += badd;
+          if (beta != 0.f) v += beta * *reinterpret_cast<const g8_f32x4*>(dst);
+        }
+        *reinterpret_cast<g8_f32x4*>(dst) = v;
+      }
+    }
+  }
+}
+
+// SCHED 1: B nh0 stays in registers from phase 0 to phase 3 (no phase-3 re-read), so both
+// operands' fills can be issued in phase 0 (B's last read is then phase 1, A's phase 2: both
+// >= 2 slots before the next k-tile's phase 0) and stay in flight for three phases.
+template <int EPI, int AF = 0, int SCHED = 0>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_8p_kernel(const bf16_t* __restrict__ A, long lda,
+                                                             const bf16_t* __restrict__ B, long ldb, void* __restrict__ C,
+                                                             long ldc, long slab, int M, int N, int K, int kchunk,
+                                                             const float* __restrict__ bias0,
+                                                             const float* __restrict__ bias1, float beta,
+                                                             G256AFrag af = G256AFrag{}) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int tiles_n = N / G256_BM;
+  const int nwg = tiles_n * (M / G256_BM);
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int tn = id % tiles_n, tm = id / tiles_n;
+  const int kbeg = blockIdx.y * kchunk;
+  const int nk = (min(K, kbeg + kchunk) - kbeg) / G256_BK;
+  const int wr = w >> 2, wc = w & 3;  // wave's 128 x 64 output block: rows wr*128, cols wc*64
+  G256Stage sa, sb;
+  if constexpr (!AF) sa.init(A, lda, tm * G256_BM, kbeg, tid);
+  sb.init(B, ldb, tn * G256_BM, kbeg, tid);
+  constexpr int OPB = G256_BM * G256_BK * 2;  // bytes per operand per stage
+  long af_row[4];
+  if constexpr (AF) {
+    const int KR = af.bm / 32, frag = af.kg / 16 * 512;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 4 * w + i, row = tm * G256_BM + 32 * (c >> 2);
+      const int t = row / af.bsl, b = row % af.bsl;
+      af_row[i] = (long)t * af.fs + (long)(((b / af.bm) * 4) * KR + (b / 32) % KR) * frag + (c & 3) * 512 + lane * 8;
+    }
+  }
+  auto issue_a = [&](char* lds, int kt) {
+    if constexpr (AF) {
+      const int k0 = kbeg + kt * G256_BK, g = k0 / af.kg, s0 = (k0 % af.kg) / 16;
+      const long goff = (long)g * (af.bm / 32) * (af.kg / 16 * 512) + (long)s0 * 512;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds((glb_vptr_t)(af.base + af_row[i] + goff),
+                                         (lds_vptr_t)(lds + (4 * w + i) * 1024), 16, 0, 0);
+    } else {
+      sa.issue(lds, kt, w);
+    }
+  };
+  // fragment of A m-tile mt (16 rows of the wave's 128), k-substep ks (32 of the tile's 64)
+  auto read_a = [&](const char* As, int mt, int ks) -> bf16x8_t {
+    const int row = wr * 128 + 16 * mt + fr;
+    if constexpr (AF) {  // KB (row group, k-step of 16) = [32 rows + 32 * k-half][16 B]
+      return *reinterpret_cast<const bf16x8_t*>(As + ((row >> 5) * 4 + 2 * ks + (fq >> 1)) * 1024 +
+                                                ((row & 31) + 32 * (fq & 1)) * 16);
+    } else {
+      return *reinterpret_cast<const bf16x8_t*>(As + row * 128 + g256_phys_slot(row, 4 * ks + fq) * 16);
+    }
+  };
+  auto read_b = [&](const char* Bs, int nt, int ks) -> bf16x8_t {
+    const int row = wc * 64 + 16 * nt + fr;
+    return *reinterpret_cast<const bf16x8_t*>(Bs + row * 128 + g256_phys_slot(row, 4 * ks + fq) * 16);
+  };
+  g8_f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = g8_f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) {
+    issue_a(smem, 0);
+    sb.issue(smem + OPB, 0, w);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (wr == 1) {  // the second group runs one barrier behind
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  bf16x8_t a[4][2], b0[2][2], b1[2][2];
+  auto mma = [&](int mh, int nh, const bf16x8_t (&bq)[2][2]) {
+    __builtin_amdgcn_s_barrier();  // end of the read slot
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 * mh + i][2 * nh + j] = mfma16_bf16(bq[j][ks], a[i][ks], acc[4 * mh + i][2 * nh + j]);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();  // end of the MFMA slot
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* As = smem + (kt & 1) * 2 * OPB;
+    const char* Bs = As + OPB;
+    char* nxt = smem + ((kt + 1) & 1) * 2 * OPB;
+    const bool more = kt + 1 < nk;
+    // phase 0: quadrant (0, 0)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) b0[j][ks] = read_b(Bs, j, ks);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) a[i][ks] = read_a(As, i, ks);
+    if (more) issue_a(nxt, kt + 1);
+    if (SCHED == 1 && more) sb.issue(nxt + OPB, kt + 1, w);
+    mma(0, 0, b0);
+    // phase 1: quadrant (0, 1)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) b1[j][ks] = read_b(Bs, 2 + j, ks);
+    if (SCHED == 0 && more) sb.issue(nxt + OPB, kt + 1, w);
+    mma(0, 1, b1);
+    // phase 2: quadrant (1, 1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) a[i][ks] = read_a(As, 4 + i, ks);
+    mma(1, 1, b1);
+    // phase 3: quadrant (1, 0); k-tile kt + 1 landed before this read slot ends
+    if constexpr (SCHED == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) b0[j][ks] = read_b(Bs, j, ks);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    mma(1, 0, b0);
+  }
+  if (wr == 0) {  // balance the second group's extra barrier
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  g8_epilogue<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
+}

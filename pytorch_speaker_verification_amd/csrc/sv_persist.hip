@@ -29,6 +29,7 @@
 #include "../../include/sv_ge2e.h"
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t sv_rsrc(const void* p, unsigned bytes) {
@@ -139,13 +140,13 @@ __device__ __forceinline__ bool persist_arrive_ok(int fault, int first) { return
 // ============================================================================
 // bf16 forward recurrence of one layer, all T steps.  Tile (b0, j0): 64 batch rows x 32
 // units x 4 gates; 8 waves, one 32x32 accumulator each (as lstm_step_fwd_bf16_kernel).
-//   gates [T,B,4H]: in = x W_ih^T + b_ih + b_hh (K1), out = activated i,f,g,o
+//   gates [T,B,4H] bf16: in = bf16(x W_ih^T + b_ih + b_hh) (K1), out = bf16 activated i,f,g,o
 //   c_tm [T,B,H], h_tm [T+1,B,H] (slot 0 = 0), h_bf [T+1,B,H] (slot 0 = 0, the hand-off),
 //   hT [H,(T+1)Bp] or NULL.  cnt: this launch's zeroed row-block counters.
 // ============================================================================
 template <int D>
 __global__ __launch_bounds__(512) void lstm_persist_fwd_bf16_kernel(const bf16_t* __restrict__ whh_bf,
-                                                                    float* __restrict__ gates,
+                                                                    bf16_t* __restrict__ gates,
                                                                     float* __restrict__ c_tm,
                                                                     float* __restrict__ h_tm, bf16_t* h_bf,
                                                                     bf16_t* __restrict__ hT, long ldhT, int T,
@@ -168,16 +169,16 @@ __global__ __launch_bounds__(512) void lstm_persist_fwd_bf16_kernel(const bf16_t
   float* pre = reinterpret_cast<float*>(smem);
   float* hs = pre + BF_BM * LDP;
   for (int t = 0; t < T; ++t) {
-    float* gt = gates + (long)t * B * G;
+    bf16_t* gt = gates + (long)t * B * G;
     float xg[PER][4];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int e = tid + 512 * k, b = e / BF_U, u = e % BF_U;
       const int gb = b0 + b, gj = j0 + u;
       const bool ok = gb < B && gj < H;
-      const float* gp = gt + (long)gb * G + gj;
+      const bf16_t* gp = gt + (long)gb * G + gj;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) xg[k][q] = ok ? gp[q * H] : 0.f;
+      for (int q = 0; q < 4; ++q) xg[k][q] = ok ? from_bf(gp[q * H]) : 0.f;
     }
     f32x16 acc[1][1];
     zero_acc(acc);
@@ -209,11 +210,11 @@ __global__ __launch_bounds__(512) void lstm_persist_fwd_bf16_kernel(const bf16_t
       const unsigned hbits = to_bf(h);
       const unsigned nb = __shfl_down(hbits, 1, 64);
       if (ok) {
-        float* gp = gt + (long)gb * G + gj;
-        gp[0] = i;
-        gp[H] = f;
-        gp[2 * H] = g;
-        gp[3 * H] = o;
+        bf16_t* gp = gt + (long)gb * G + gj;
+        gp[0] = to_bf(i);
+        gp[H] = to_bf(f);
+        gp[2 * H] = to_bf(g);
+        gp[3 * H] = to_bf(o);
         ct[(long)gb * H + gj] = c;
         ht[(long)gb * H + gj] = h;
         if (!(u & 1))
@@ -255,10 +256,10 @@ __global__ __launch_bounds__(512) void lstm_persist_fwd_bf16_kernel(const bf16_t
 // is computed in the kernel from x_bf [T,B,F] and W_ih [4H,F] (held in registers beside W_hh:
 // 3 k-steps of 16, zero-padded), so the layer needs no K1 GEMM and its step loads 80 B per row
 // instead of 4 x 4H fp32 pre-activations; the sum (MFMA over the zero-padded k range, then the
-// two biases) matches the K1 GEMM's bit for bit.
+// two biases, rounded to bf16 as the K1 GEMM stores it) matches the K1 path bit for bit.
 template <int NS, int BM, int XF>
 __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf16_t* __restrict__ whh_bf,
-                                                                       float* __restrict__ gates,
+                                                                       bf16_t* __restrict__ gates,
                                                                        float* __restrict__ c_tm,
                                                                        float* __restrict__ h_tm, bf16_t* h_bf,
                                                                        bf16_t* __restrict__ hT, long ldhT, int T,
@@ -350,23 +351,22 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
     for (int v = 0; v < 4; ++v) cst[k][v] = 0.f;
   // staging map of one half (BM rows x HALF bf16 = BM * HALF / 8 16-B chunks over 256 threads)
   constexpr int CH = BM * HALF / 8 / 256;
-  // x W_ih^T + b of step t (K1 output), prefetched one step ahead: 16-B buffer loads, rows past B
-  // read zeros
-  float4 xg[KR][4];
+  // bf16(x W_ih^T + b) of step t (K1 output): 8-B buffer loads of 4 units, rows past B read zeros
+  uint2 xg[KR][4];
   auto load_xg = [&](int tt) {
     if constexpr (XF > 0) {
       load_x(tt);
       return;
     }
-    const __amdgpu_buffer_rsrc_t rx = sv_rsrc(gates + (long)tt * BG, (unsigned)(BG * 4));
+    const __amdgpu_buffer_rsrc_t rx = sv_rsrc(gates + (long)tt * BG, (unsigned)(BG * 2));
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       const long gb = b0 + brow + 32 * k;
       const long gbv = gb < Bv ? gb : Bv + 64;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(rx, (unsigned)((gbv * G + q * H + j0 + u4) * 4), 0, 0);
-        xg[k][q] = float4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
+        const u32x2_t x = __builtin_amdgcn_raw_buffer_load_b64(rx, (unsigned)((gbv * G + q * H + j0 + u4) * 2), 0, 0);
+        xg[k][q] = uint2{x.x, x.y};
       }
     }
   };
@@ -432,8 +432,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        acc0[i] += x0[i] + xbias;
-        if constexpr (BM == 64) acc1[i] += x1[i] + xbias;
+        acc0[i] += round_bf(x0[i] + xbias);
+        if constexpr (BM == 64) acc1[i] += round_bf(x1[i] + xbias);
       }
     }
     // gate exchange: wave g's [BM rows][32 units] -> pre[row][g * 32 + unit]
@@ -443,7 +443,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
       if constexpr (BM == 64) pre[(32 + acc_row(i, lane)) * LDP + g * BF_U + r] = acc1[i];
     }
     __syncthreads();
-    float4 act[KR][4], cv[KR], hv[KR];
+    uint2 act[KR][4];
+    float4 cv[KR], hv[KR];
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       const int b = brow + 32 * k;
@@ -452,13 +453,18 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
       for (int q = 0; q < 4; ++q) pq[q] = *reinterpret_cast<const float4*>(pre + b * LDP + q * BF_U + u4);
       float ao[4][4], co[4], ho[4];
       unsigned pk[2] = {0u, 0u};
+      float4 xf[4];
+      if constexpr (XF == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xf[q] = unpack_bf4(xg[k][q]);
+      }
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const float pv[4] = {pq[0][v], pq[1][v], pq[2][v], pq[3][v]};
         float xv[4] = {0.f, 0.f, 0.f, 0.f};
         if constexpr (XF == 0) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) xv[q] = xg[k][q][v];
+          for (int q = 0; q < 4; ++q) xv[q] = xf[q][v];
         }
         float a4[4], h;
         const float c = lstm_cell_fwd(pv, xv, cst[k][v], a4, h);
@@ -473,7 +479,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
       }
       *reinterpret_cast<uint2*>(hsb + b * LDB + u4) = uint2{pk[0], pk[1]};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) act[k][q] = float4{ao[q][0], ao[q][1], ao[q][2], ao[q][3]};
+      for (int q = 0; q < 4; ++q) act[k][q] = pack_bf4(ao[q][0], ao[q][1], ao[q][2], ao[q][3]);
       cv[k] = float4{co[0], co[1], co[2], co[3]};
       hv[k] = float4{ho[0], ho[1], ho[2], ho[3]};
     }
@@ -499,9 +505,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
     for (int k = 0; k < KR; ++k) {
       const long gb = b0 + brow + 32 * k;
       if (gb < Bv) {
-        float* gp = gates + (long)t * BG + gb * G + j0 + u4;
+        bf16_t* gp = gates + (long)t * BG + gb * G + j0 + u4;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(gp + q * H) = act[k][q];
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(gp + q * H) = act[k][q];
         *reinterpret_cast<float4*>(c_tm + (long)t * BH + gb * H + j0 + u4) = cv[k];
         *reinterpret_cast<float4*>(h_tm + (long)(t + 1) * BH + gb * H + j0 + u4) = hv[k];
       }
@@ -535,12 +541,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
 // step t-1 load as 16-B vectors right after step t's arrival.  Only the hand-off stores precede
 // the arrival; dG_t row-major (the dx GEMM's operand, skipped when the dx GEMM reads dgf) and
 // transposed (dgT, the dW GEMMs') are stored after it.
-//   acts [T,B,4H] activated gates, c_tm [T,B,H]; dhup: [T,B,H] (up_full) or [B,H] at t = T-1.
+//   acts [T,B,4H] bf16 activated gates, c_tm [T,B,H]; dhup: [T,B,H] (up_full) or [B,H] at t = T-1.
 // Hand-off: hand-off table row 1 of MI355X_MICROARCH.md, as the forward kernel above.
 // ============================================================================
 template <int NS, int P, int BM, bool agpr_w = true>
 __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
-    const bf16_t* __restrict__ whhT, const float* __restrict__ acts, const float* __restrict__ c_tm,
+    const bf16_t* __restrict__ whhT, const bf16_t* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
     bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit,
     int fault, int dbg, float* __restrict__ dbp, unsigned long long* __restrict__ stamps) {
@@ -582,7 +588,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
   }
   // elementwise map: thread -> 4 consecutive units (u4) x rows brow, brow + 32
   const int u4 = (tid & 7) * 4, brow = tid >> 3;
-  float4 av[KR][4], cv[KR], cpv[KR], upv[KR];
+  uint2 av[KR][4];  // 4 units of each gate, bf16
+  float4 cv[KR], cpv[KR], upv[KR];
   float dcf[KR][4];
   // bias-gradient partial sums over t of this thread's bf16 dG values (dbp: per row block)
   float dbs[KR][4][4];
@@ -601,7 +608,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
   const long Bv = B;
   auto load_ew = [&](int tt) {
     const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
-    const __amdgpu_buffer_rsrc_t ra_ = sv_rsrc(acts + (long)tt * BG, (unsigned)(BG * 4));
+    const __amdgpu_buffer_rsrc_t ra_ = sv_rsrc(acts + (long)tt * BG, (unsigned)(BG * 2));
     const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(tt > 0 ? tt - 1 : 0) * BH, tt > 0 ? (unsigned)(BH * 4) : 0u);
     const __amdgpu_buffer_rsrc_t ru_ = sv_rsrc(up ? up : c_tm, up ? (unsigned)(BH * 4) : 0u);
 #pragma unroll
@@ -609,7 +616,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
       const long gb = b0 + brow + 32 * k;
       const long gbv = gb < Bv ? gb : Bv + 64;  // rows past B: offsets past every range
 #pragma unroll
-      for (int q = 0; q < 4; ++q) av[k][q] = ld4(ra_, gbv * G + q * H + j0 + u4);
+      for (int q = 0; q < 4; ++q) {
+        const u32x2_t x = __builtin_amdgcn_raw_buffer_load_b64(ra_, (unsigned)((gbv * G + q * H + j0 + u4) * 2), 0, 0);
+        av[k][q] = uint2{x.x, x.y};
+      }
       cpv[k] = ld4(rc_, gbv * H + j0 + u4);
       upv[k] = ld4(ru_, gbv * H + j0 + u4);
     }
@@ -689,10 +699,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
       const float rs2[4] = {r2.x, r2.y, r2.z, r2.w}, rs3[4] = {r3.x, r3.y, r3.z, r3.w};
       const float ups[4] = {upv[k].x, upv[k].y, upv[k].z, upv[k].w};
       const float cs[4] = {cv[k].x, cv[k].y, cv[k].z, cv[k].w}, cps[4] = {cpv[k].x, cpv[k].y, cpv[k].z, cpv[k].w};
-      const float a0[4] = {av[k][0].x, av[k][0].y, av[k][0].z, av[k][0].w};
-      const float a1[4] = {av[k][1].x, av[k][1].y, av[k][1].z, av[k][1].w};
-      const float a2[4] = {av[k][2].x, av[k][2].y, av[k][2].z, av[k][2].w};
-      const float a3[4] = {av[k][3].x, av[k][3].y, av[k][3].z, av[k][3].w};
+      const float4 f0 = unpack_bf4(av[k][0]), f1 = unpack_bf4(av[k][1]), f2 = unpack_bf4(av[k][2]),
+                   f3 = unpack_bf4(av[k][3]);
+      const float a0[4] = {f0.x, f0.y, f0.z, f0.w};
+      const float a1[4] = {f1.x, f1.y, f1.z, f1.w};
+      const float a2[4] = {f2.x, f2.y, f2.z, f2.w};
+      const float a3[4] = {f3.x, f3.y, f3.z, f3.w};
       unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
@@ -907,7 +919,7 @@ int sv_persist_fwd_fusex_ok(int H, int F) { return H == 768 && F == 40 && persis
 
 // one layer's recurrence (K2 for all t) after its K1 has filled `gates`; on `stream`.  With x_bf
 // (layer 0, sv_persist_fwd_fusex_ok): no K1 -- the kernel forms x_t W_ih^T + b_ih + b_hh itself.
-int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, float* gates, float* c_tm, float* h_tm,
+int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates, float* c_tm, float* h_tm,
                         bf16_t* h_bf, bf16_t* hT, hipStream_t stream, unsigned* sync, int chan, const bf16_t* x_bf,
                         int F, const bf16_t* wih_bf, const float* b_ih, const float* b_hh, hipEvent_t pre,
                         hipEvent_t post) {
@@ -991,7 +1003,7 @@ int pbwd_agpr() {
   return v;
 }
 template <int NS, int P>
-void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const float* acts, const float* c_tm,
+void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
                  const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B,
                  int H, unsigned* cnt, unsigned* sync, float* dbp) {
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + SV_SYNC_STAMP);
@@ -1029,7 +1041,7 @@ extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H) {
 // transposed) from the activations, cell states and the upstream dh (dhup [T,B,H] if up_full,
 // else [B,H] at t = T-1 only, or NULL).  dgT: [4H][T*Bp] (padding columns written as zeros).
 // dgf: sv_persist_bwd_scratch(T, B, H) bytes.  Counter channel 0 of `sync`.
-int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const float* acts, const float* c_tm,
+int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
                         const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream,
                         unsigned* sync, float* db_ih, float* db_hh, hipEvent_t pre, hipEvent_t post) {
   const int cus = sv_stream_cus(stream);

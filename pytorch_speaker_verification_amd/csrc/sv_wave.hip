@@ -50,7 +50,7 @@ struct WaveFwd2Args {
   const bf16_t* wih[WV_L];   // [4H][F_l] bf16
   const float* bih[WV_L];
   const float* bhh[WV_L];
-  float* gates[WV_L];        // [T][B][4H] activated
+  bf16_t* gates[WV_L];       // [T][B][4H] activated, bf16
   float* c[WV_L];            // [T][B][H]
   float* h[WV_L];            // [T+1][B][H] (slot 0 = 0, written by the host)
   bf16_t* hb[WV_L];          // [T+1][B][H] bf16 (slot 0 = 0)
@@ -200,14 +200,16 @@ __global__ __launch_bounds__(256, 1) void lstm_wave2_fwd_bf16_kernel(const WaveF
         acc = mfma_bf16(__builtin_bit_cast(bf16x8_t, xa), wx[s], acc);
       }
     }
+    // the x-projection incl. biases rounded to bf16, as the per-layer schedule's K1 GEMM stores it
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] += xbias;
+    for (int i = 0; i < 16; ++i) acc[i] = round_bf(acc[i] + xbias);
     if (t > 0) wv_mfma_lds(As_h + r * WV_LDA + 8 * hh, wh, acc);
 #pragma unroll
     for (int i = 0; i < 16; ++i) pre[acc_row(i, lane) * WV_LDP + g * BF_U + r] = acc[i];
     __syncthreads();
     // cell update: 4 units x 1 row per thread
-    float4 act[4], cv, hv;
+    uint2 act[4];
+    float4 cv, hv;
     {
       float4 pq[4];
 #pragma unroll
@@ -231,7 +233,7 @@ __global__ __launch_bounds__(256, 1) void lstm_wave2_fwd_bf16_kernel(const WaveF
       }
       *reinterpret_cast<uint2*>(hsb + brow * WV_LDB + u4) = uint2{pk[0], pk[1]};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) act[q] = float4{ao[q][0], ao[q][1], ao[q][2], ao[q][3]};
+      for (int q = 0; q < 4; ++q) act[q] = pack_bf4(ao[q][0], ao[q][1], ao[q][2], ao[q][3]);
       cv = float4{co[0], co[1], co[2], co[3]};
       hv = float4{ho[0], ho[1], ho[2], ho[3]};
     }
@@ -253,9 +255,9 @@ __global__ __launch_bounds__(256, 1) void lstm_wave2_fwd_bf16_kernel(const WaveF
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // off the critical chain: activations, c, h and hT of step t
     if (gb < B && j0 + u4 < H) {
-      float* gp = a.gates[l] + (long)t * BG + gb * G + j0 + u4;
+      bf16_t* gp = a.gates[l] + (long)t * BG + gb * G + j0 + u4;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(gp + q * H) = act[q];
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(gp + q * H) = act[q];
       *reinterpret_cast<float4*>(a.c[l] + (long)t * BH + gb * H + j0 + u4) = cv;
       *reinterpret_cast<float4*>(a.h[l] + (long)(t + 1) * BH + gb * H + j0 + u4) = hv;
     }
@@ -283,7 +285,7 @@ int sv_wave_fwd_fits(int L, int B, int F, int H, int cus) {
 // memsets).  Counter channels 0..L-1 of `sync`.
 int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, const bf16_t* const* w_ih_bf,
                      const bf16_t* const* w_hh_bf, const float* const* b_ih, const float* const* b_hh,
-                     float* const* gates, float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
+                     bf16_t* const* gates, float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
                      bf16_t* const* hT, unsigned* sync, hipStream_t stream, unsigned limit, int fault, hipEvent_t pre,
                      hipEvent_t post) {
   if (!sv_wave_fwd_fits(L, B, F, H, sv_stream_cus(stream))) return SV_ESHAPE;

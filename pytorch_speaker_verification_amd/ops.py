@@ -296,7 +296,8 @@ def _bf(shape, dev):
 
 def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=None):
     """Mixed-precision forward (BASELINE config c3): bf16 GEMM operands, fp32 accumulation,
-    fp32 gates / cell state / projection / norm.  Same outputs as embedder_forward.
+    bf16 storage of the x-projection and of the activated gates saved for the backward, fp32
+    cell state / projection / norm.  Same outputs as embedder_forward.
     status: the caller's PersistStatus (sync block of the persistent recurrences); None = a
     fresh one, checked at the next call / check_persistent_status().  probe: 2*L timing events
     around the layers' persistent recurrences (include/sv_ge2e.h)."""
@@ -328,7 +329,7 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=Non
         call("sv_cast_bf16", ptr(w_ih), ptr(wih_bf), w_ih.numel(), s)
         call("sv_cast_bf16", ptr(w_hh), ptr(whh_bf), w_hh.numel(), s)
         wbf.append((wih_bf, whh_bf))
-    gs = [torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev) for _ in range(L)]
+    gs = [_bf((T, B, 4 * H), dev) for _ in range(L)]  # bf16 x-projection in, bf16 activations out
     cs = [torch.empty((T, B, H), dtype=torch.float32, device=dev) for _ in range(L)]
     hs = [torch.empty((T + 1, B, H), dtype=torch.float32, device=dev) for _ in range(L)]
     hbs = [_bf((T + 1, B, H), dev) for _ in range(L)]

@@ -15,6 +15,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--torch", action="store_true")
 ap.add_argument("--bf16", action="store_true")
 ap.add_argument("--reps", type=int, default=8)
+ap.add_argument("--check", action="store_true", help="bf16: error vs fp32 torch on the same bf16 inputs, "
+                "and bitwise repeatability over --reps runs (a race screen)")
+ap.add_argument("--shapes", default="Gx,dW,dx")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 s = torch.cuda.current_stream(dev).cuda_stream
@@ -37,6 +40,8 @@ def timeit(fn, reps, warm=2):
 
 res = {"env": {k: v for k, v in os.environ.items() if k.startswith("SV_")}}
 for name, (M, N, K) in SHAPES.items():
+    if name not in args.shapes.split(","):
+        continue
     A = torch.randn(M, K, device=dev)
     Bm = torch.randn(N, K, device=dev)
     C = torch.empty(M, N, device=dev)
@@ -61,8 +66,28 @@ for name, (M, N, K) in SHAPES.items():
         us = timeit(lambda: call("sv_gemm_bf16", M, N, K, ptr(Ab), K, ptr(Bb), K, ptr(C), N, None, None, 0.0, ptr(wb), s),
                     args.reps)
         res["sv_bf16_" + name] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
+        if args.check:
+            call("sv_gemm_bf16", M, N, K, ptr(Ab), K, ptr(Bb), K, ptr(C), N, None, None, 0.0, ptr(wb), s)
+            torch.cuda.synchronize()
+            first = C.clone()
+            same = True
+            for _ in range(max(args.reps, 8)):
+                C.fill_(float("nan"))
+                call("sv_gemm_bf16", M, N, K, ptr(Ab), K, ptr(Bb), K, ptr(C), N, None, None, 0.0, ptr(wb), s)
+                torch.cuda.synchronize()
+                same = same and bool(torch.equal(C, first))
+            ref = torch.matmul(Ab.float(), Bb.float().t())
+            sc = torch.matmul(Ab.float().abs(), Bb.float().abs().t())
+            res["sv_bf16_err_" + name] = float(((first - ref).abs() / sc).max())
+            res["sv_bf16_repeat_" + name] = same
+            del ref, sc, first
         if args.torch:
             us = timeit(lambda: torch.matmul(Ab, Bb.t()), args.reps)
             res["torch_bf16_" + name] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
+            try:  # bf16 operands, fp32 output (what our K1/dx/dW write)
+                us = timeit(lambda: torch.mm(Ab, Bb.t(), out_dtype=torch.float32), args.reps)
+                res["torch_bf16_f32out_" + name] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
+            except (TypeError, RuntimeError) as e:
+                res["torch_bf16_f32out_" + name] = str(e)[:80]
     del A, Bm, C, w
 print(json.dumps(res), flush=True)

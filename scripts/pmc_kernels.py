@@ -34,7 +34,7 @@ x_bf = torch.randn(Tb, B, H, generator=g).bfloat16().to(dev)
 wih_bf = (torch.randn(G, H, generator=g) * 0.03).bfloat16().to(dev)
 whh_bf = (torch.randn(G, H, generator=g) * 0.03).bfloat16().to(dev)
 bias = torch.zeros(G, device=dev)
-gts = torch.empty(Tb, B, G, device=dev)
+gts = torch.empty(Tb, B, G, dtype=torch.bfloat16, device=dev)  # bf16 gates (ABI v3)
 ctm = torch.empty(Tb, B, H, device=dev)
 htm = torch.empty(Tb + 1, B, H, device=dev)
 hbf = torch.empty(Tb + 1, B, H, dtype=torch.bfloat16, device=dev)
