@@ -433,13 +433,17 @@ template <int EPI, int AF>
 void launch_g8(dim3 grid, hipStream_t stream, const bf16_t* A, long lda, const bf16_t* B, long ldb, void* C, long ldc,
                long slab, int M, int N, int K, int kchunk, const float* bias0, const float* bias1, float beta,
                G256AFrag af = G256AFrag{}) {
-  // SV_G8_SCHED: 0 (default) fills issued over phases 0 and 1, B nh0 re-read in phase 3; 1 both
-  // fills in phase 0 with B nh0 kept in registers (measured 3-4 % slower on K1 / dx)
+  // SV_G8_SCHED: 2 (default) two fills per phase (gemm_bf16_8q_kernel); 0 a k-tile's fills in
+  // phases 0 and 1, B nh0 re-read in phase 3; 1 all fills in phase 0.  Measured (c3 shapes, us):
+  // dW 414 / 446 / 445, dx 440 / 471 / 480, K1 (bf16 out) 615 / 626 / --
   static const int sched = [] {
     const char* e = getenv("SV_G8_SCHED");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
-  if (sched == 0)
+  if (sched == 2)
+    hipLaunchKernelGGL((gemm_bf16_8q_kernel<EPI, AF>), grid, dim3(512), G256_LDS, stream, A, lda, B, ldb, C, ldc, slab,
+                       M, N, K, kchunk, bias0, bias1, beta, af);
+  else if (sched == 0)
     hipLaunchKernelGGL((gemm_bf16_8p_kernel<EPI, AF, 0>), grid, dim3(512), G256_LDS, stream, A, lda, B, ldb, C, ldc,
                        slab, M, N, K, kchunk, bias0, bias1, beta, af);
   else

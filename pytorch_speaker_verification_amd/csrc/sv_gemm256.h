@@ -507,3 +507,184 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8p_kernel(const bf16_t* __re
   }
   g8_epilogue<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
 }
+
+// ---- 8-phase schedule with the fills spread two per phase (SV_G8_SCHED=2) ----
+// The 8-phase kernel above issues a k-tile's 8 fills per wave in one or two phases, and an
+// LDS-DMA issue inside a phase that also reads fragments costs 100-185 cycles
+// (MI355X_MICROARCH.md, "LDS-DMA piece"), so those read slots outlast the other group's 16 MFMAs.
+// Here every phase issues exactly two 64-row chunks (chunk i = operand rows 64 i .. 64 i + 63;
+// for A that is wave group i / 2's m-half i % 2, for B the column block of waves wc = i), and
+// B nh0 stays in registers (B read in phases 0-1 only).  Per wave, in the phases of k-tile kt:
+//   p0: B2(kt+1) B3(kt+1)   p1: A1(kt+1) A0(kt+2)   p2: A3(kt+1) A2(kt+2)   p3: B0(kt+2) B1(kt+2)
+// Each chunk is re-filled >= 2 slots after its last read of the tile two back (A0 / A2: phase 0,
+// A1 / A3: phase 2, B: phase 1).  Waits (counted, before the phase's issue): p3 vmcnt(4) -- every
+// B chunk and A0 / A2 of kt+1 landed (the 4 younger ops are A1 / A0 / A3 / A2 of p1-p2); p1
+// vmcnt(5) -- A1 / A3 of kt landed (younger: A2(kt+1) and the four B fills of kt+1), so the
+// m-half-1 fragments read in p2 are ordered by the barrier that ends the p1 read slot.  Near the
+// end of K, where fewer younger ops exist, the waits fall back to vmcnt(0).
+template <int EPI, int AF = 0>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __restrict__ A, long lda,
+                                                             const bf16_t* __restrict__ B, long ldb, void* __restrict__ C,
+                                                             long ldc, long slab, int M, int N, int K, int kchunk,
+                                                             const float* __restrict__ bias0,
+                                                             const float* __restrict__ bias1, float beta,
+                                                             G256AFrag af = G256AFrag{}) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int tiles_n = N / G256_BM;
+  const int nwg = tiles_n * (M / G256_BM);
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int tn = id % tiles_n, tm = id / tiles_n;
+  const int kbeg = blockIdx.y * kchunk;
+  const int nk = (min(K, kbeg + kchunk) - kbeg) / G256_BK;
+  const int wr = w >> 2, wc = w & 3;
+  G256Stage sa, sb;
+  if constexpr (!AF) sa.init(A, lda, tm * G256_BM, kbeg, tid);
+  sb.init(B, ldb, tn * G256_BM, kbeg, tid);
+  constexpr int OPB = G256_BM * G256_BK * 2;
+  // fragment-order A: chunk i of wave w is KB c = (2 i + w / 4) * 4 + w % 4 (row group 2 i + w / 4,
+  // k-step w % 4), so a chunk is the 64 rows 64 i .. 64 i + 63 as for the row-major operand
+  long af_row[4];
+  if constexpr (AF) {
+    const int KR = af.bm / 32, frag = af.kg / 16 * 512;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rg = 2 * i + (w >> 2), row = tm * G256_BM + 32 * rg;
+      const int t = row / af.bsl, b = row % af.bsl;
+      af_row[i] = (long)t * af.fs + (long)(((b / af.bm) * 4) * KR + (b / 32) % KR) * frag + (w & 3) * 512 + lane * 8;
+    }
+  }
+  auto stage = [&](int kt) { return smem + (kt & 1) * 2 * OPB; };
+  auto fill_a = [&](int kt, int i) {
+    char* lds = stage(kt);
+    if constexpr (AF) {
+      const int k0 = kbeg + kt * G256_BK, g = k0 / af.kg, s0 = (k0 % af.kg) / 16;
+      const long goff = (long)g * (af.bm / 32) * (af.kg / 16 * 512) + (long)s0 * 512;
+      __builtin_amdgcn_global_load_lds((glb_vptr_t)(af.base + af_row[i] + goff),
+                                       (lds_vptr_t)(lds + ((2 * i + (w >> 2)) * 4 + (w & 3)) * 1024), 16, 0, 0);
+    } else {
+      __builtin_amdgcn_global_load_lds((glb_vptr_t)(sa.src[i] + kt * G256_BK), (lds_vptr_t)(lds + (w * 64 + 512 * i) * 16),
+                                       16, 0, 0);
+    }
+  };
+  auto fill_b = [&](int kt, int i) {
+    __builtin_amdgcn_global_load_lds((glb_vptr_t)(sb.src[i] + kt * G256_BK),
+                                     (lds_vptr_t)(stage(kt) + OPB + (w * 64 + 512 * i) * 16), 16, 0, 0);
+  };
+  auto read_a = [&](const char* As, int mt, int ks) -> bf16x8_t {
+    const int row = wr * 128 + 16 * mt + fr;
+    if constexpr (AF) {
+      return *reinterpret_cast<const bf16x8_t*>(As + ((row >> 5) * 4 + 2 * ks + (fq >> 1)) * 1024 +
+                                                ((row & 31) + 32 * (fq & 1)) * 16);
+    } else {
+      return *reinterpret_cast<const bf16x8_t*>(As + row * 128 + g256_phys_slot(row, 4 * ks + fq) * 16);
+    }
+  };
+  auto read_b = [&](const char* Bs, int nt, int ks) -> bf16x8_t {
+    const int row = wc * 64 + 16 * nt + fr;
+    return *reinterpret_cast<const bf16x8_t*>(Bs + row * 128 + g256_phys_slot(row, 4 * ks + fq) * 16);
+  };
+  g8_f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = g8_f32x4{0.f, 0.f, 0.f, 0.f};
+  // prologue: k-tile 0 whole, then k-tile 1's fills that the steady state issues in the phases of
+  // k-tile -1 (A0 / A2 / B0 / B1); k-tile 0 landed
+  if (nk > 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fill_b(0, i);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fill_a(0, i);
+  }
+  if (nk > 1) {
+    fill_a(1, 0);
+    fill_a(1, 2);
+    fill_b(1, 0);
+    fill_b(1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (wr == 1) {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  bf16x8_t a[4][2], b0[2][2], b1[2][2];
+  auto mma = [&](int mh, int nh, const bf16x8_t (&bq)[2][2]) {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 * mh + i][2 * nh + j] = mfma16_bf16(bq[j][ks], a[i][ks], acc[4 * mh + i][2 * nh + j]);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* As = stage(kt);
+    const char* Bs = As + OPB;
+    const bool m1 = kt + 1 < nk, m2 = kt + 2 < nk;
+    // phase 0: quadrant (0, 0)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) b0[j][ks] = read_b(Bs, j, ks);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) a[i][ks] = read_a(As, i, ks);
+    if (m1) {
+      fill_b(kt + 1, 2);
+      fill_b(kt + 1, 3);
+    }
+    mma(0, 0, b0);
+    // phase 1: quadrant (0, 1); A1 / A3 of kt landed
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) b1[j][ks] = read_b(Bs, 2 + j, ks);
+    if (m1)
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (m1) fill_a(kt + 1, 1);
+    if (m2) fill_a(kt + 2, 0);
+    mma(0, 1, b1);
+    // phase 2: quadrant (1, 1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) a[i][ks] = read_a(As, 4 + i, ks);
+    if (m1) fill_a(kt + 1, 3);
+    if (m2) fill_a(kt + 2, 2);
+    mma(1, 1, b1);
+    // phase 3: quadrant (1, 0); every B chunk and A0 / A2 of kt + 1 landed
+    if (m2)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (m1)
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (m2) {
+      fill_b(kt + 2, 0);
+      fill_b(kt + 2, 1);
+    }
+    mma(1, 0, b0);
+  }
+  if (wr == 0) {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  g8_epilogue<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
+}

@@ -66,6 +66,16 @@ for name, (M, N, K) in SHAPES.items():
         us = timeit(lambda: call("sv_gemm_bf16", M, N, K, ptr(Ab), K, ptr(Bb), K, ptr(C), N, None, None, 0.0, ptr(wb), s),
                     args.reps)
         res["sv_bf16_" + name] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
+        if name == "Gx":  # the bf16 path's K1: bf16 output incl. biases
+            Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            us = timeit(lambda: call("sv_gemm_bf16_bf", M, N, K, ptr(Ab), K, ptr(Bb), K, ptr(Cb), N, None, None, s),
+                        args.reps)
+            res["sv_bf16_bfout_Gx"] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
+            if args.check:
+                ref = torch.matmul(Ab.float(), Bb.float().t())
+                res["sv_bf16_bfout_err_Gx"] = float(((Cb.float() - ref).abs() / (ref.abs() + 1e-3)).max())
+                del ref
+            del Cb
         if args.check:
             call("sv_gemm_bf16", M, N, K, ptr(Ab), K, ptr(Bb), K, ptr(C), N, None, None, 0.0, ptr(wb), s)
             torch.cuda.synchronize()
