@@ -30,6 +30,7 @@
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t sv_rsrc(const void* p, unsigned bytes) {
@@ -544,7 +545,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
 //   acts [T,B,4H] bf16 activated gates, c_tm [T,B,H]; dhup: [T,B,H] (up_full) or [B,H] at t = T-1.
 // Hand-off: hand-off table row 1 of MI355X_MICROARCH.md, as the forward kernel above.
 // ============================================================================
-template <int NS, int P, int BM, bool agpr_w = true>
+template <int NS, int P, int BM, bool agpr_w = true, bool EWD = true>
 __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     const bf16_t* __restrict__ whhT, const bf16_t* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
@@ -561,6 +562,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
   float* red = reinterpret_cast<float*>(smem);
   bf16_t* dgs = reinterpret_cast<bf16_t*>(smem + 4 * BM * LDR * 4);
   bf16_t* gts = dgs + BM * LDG;
+  // step operands staged by LDS-DMA (EWD): activations [BM][16 x 16 B] (gate blocks rotated by
+  // row), c_{t-1} and dh_up [BM][32] fp32
+  char* ewa = reinterpret_cast<char*>(gts + 4 * BF_U * LDT);
+  float* ewc = reinterpret_cast<float*>(ewa + BM * 256);
+  float* ewu = ewc + BM * BF_U;
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   int ub, rb;
@@ -606,7 +612,39 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     return float4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
   };
   const long Bv = B;
+  // EWD: step tt's operands into LDS by buffer_load ... lds (no destination registers, so the
+  // issuing wave does not wait for them; rows past B and absent operands read zeros).  Wave g's
+  // instruction j stages 1 KB at LDS position p = (g * n + j) * 64 + lane (16-B units):
+  //   acts: row p / 16, slot s = p % 16 holds gate ((s / 4) - row) & 3, 8-unit chunk s % 4
+  //   c_{t-1}, dh_up: row p / 8, 4-unit chunk p % 8
+  auto load_ew_lds = [&](int tt) {
+    const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
+    const __amdgpu_buffer_rsrc_t ra_ = sv_rsrc(acts + (long)tt * BG, (unsigned)(BG * 2));
+    const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(tt > 0 ? tt - 1 : 0) * BH, tt > 0 ? (unsigned)(BH * 4) : 0u);
+    const __amdgpu_buffer_rsrc_t ru_ = sv_rsrc(up ? up : c_tm, up ? (unsigned)(BH * 4) : 0u);
+    constexpr int NA = BM / 16, NC = BM / 32;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int p = (g * NA + j) * 64 + lane, row = p >> 4, sl = p & 15;
+      const int q = ((sl >> 2) - row) & 3, c = sl & 3;
+      const long gb = b0 + row, gbv = gb < Bv ? gb : Bv + 64;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_, (lds_ptr_t)(ewa + (g * NA + j) * 1024), 16,
+                                               (unsigned)((gbv * G + q * H + j0 + 8 * c) * 2), 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int p = (g * NC + j) * 64 + lane, row = p >> 3, c = p & 7;
+      const long gb = b0 + row, gbv = gb < Bv ? gb : Bv + 64;
+      const unsigned off = (unsigned)((gbv * H + j0 + 4 * c) * 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rc_, (lds_ptr_t)((char*)ewc + (g * NC + j) * 1024), 16, off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ru_, (lds_ptr_t)((char*)ewu + (g * NC + j) * 1024), 16, off, 0, 0, 0);
+    }
+  };
   auto load_ew = [&](int tt) {
+    if (EWD) {
+      load_ew_lds(tt);
+      return;
+    }
     const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
     const __amdgpu_buffer_rsrc_t ra_ = sv_rsrc(acts + (long)tt * BG, (unsigned)(BG * 2));
     const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(tt > 0 ? tt - 1 : 0) * BH, tt > 0 ? (unsigned)(BH * 4) : 0u);
@@ -686,8 +724,20 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
       red[(g * BM + acc_row(i, lane)) * LDR + r] = acc0[i];
       if constexpr (BM == 64) red[(g * BM + 32 + acc_row(i, lane)) * LDR + r] = acc1[i];
     }
+    if (EWD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
     __syncthreads();
     mark(1);
+    if (EWD) {  // step t's operands from the LDS image (every wave's DMA retired before the barrier)
+#pragma unroll
+      for (int k = 0; k < KR; ++k) {
+        const int b = brow + 32 * k;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          av[k][q] = *reinterpret_cast<const uint2*>(ewa + b * 256 + (((q + b) & 3) * 4 + (u4 >> 3)) * 16 + (u4 & 7) * 2);
+        cpv[k] = *reinterpret_cast<const float4*>(ewc + b * BF_U + u4);
+        upv[k] = *reinterpret_cast<const float4*>(ewu + b * BF_U + u4);
+      }
+    }
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       const int b = brow + 32 * k;
@@ -983,7 +1033,8 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
 // ---- W-stationary persistent backward recurrence ----
 namespace {
 constexpr size_t pbwd_lds(int bm) {
-  return (size_t)4 * bm * (BF_U + 4) * 4 + (size_t)bm * (4 * BF_U + 8) * 2 + (size_t)4 * BF_U * (bm + 8) * 2;
+  return (size_t)4 * bm * (BF_U + 4) * 4 + (size_t)bm * (4 * BF_U + 8) * 2 + (size_t)4 * BF_U * (bm + 8) * 2 +
+         (size_t)bm * 512;  // + the LDS-DMA operand image (EWD)
 }
 // SV_PBWD_DEBUG (profiling only, results invalid): 1 = no hand-off waits, 4 = no recurrent GEMM, 8 = no global stores, 16 = no
 // elementwise operand loads after the first step, 32 = per-phase cycle stamps into the sync block
@@ -1007,18 +1058,27 @@ void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const bf1
                  const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B,
                  int H, unsigned* cnt, unsigned* sync, float* dbp) {
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + SV_SYNC_STAMP);
-#define SV_PBWD_LAUNCH(BMV, AG)                                                                                   \
-  hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P, BMV, AG>), dim3(grid.x * grid.y), dim3(256), pbwd_lds(BMV), s, \
+#define SV_PBWD_LAUNCH(BMV, AG, EW)                                                                               \
+  hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P, BMV, AG, EW>), dim3(grid.x * grid.y), dim3(256), pbwd_lds(BMV), s, \
                      whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x, persist_xcd(), \
                      sync, persist_limit(), persist_fault(), pbwd_debug(), dbp, stamps)
-  if (bm == 32 && pbwd_agpr())
-    SV_PBWD_LAUNCH(32, true);
+  // SV_PBWD_EWD=0: step operands loaded to registers after the arrival (the former schedule)
+  static const int ewd = [] {
+    const char* e = getenv("SV_PBWD_EWD");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  if (bm == 32 && !pbwd_agpr())
+    SV_PBWD_LAUNCH(32, false, true);
+  else if (bm == 32 && ewd)
+    SV_PBWD_LAUNCH(32, true, true);
   else if (bm == 32)
-    SV_PBWD_LAUNCH(32, false);
-  else if (pbwd_agpr())
-    SV_PBWD_LAUNCH(64, true);
+    SV_PBWD_LAUNCH(32, true, false);
+  else if (!pbwd_agpr())
+    SV_PBWD_LAUNCH(64, false, true);
+  else if (ewd)
+    SV_PBWD_LAUNCH(64, true, true);
   else
-    SV_PBWD_LAUNCH(64, false);
+    SV_PBWD_LAUNCH(64, true, false);
 #undef SV_PBWD_LAUNCH
 }
 }  // namespace
