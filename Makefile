@@ -9,9 +9,12 @@ LIB := $(PKG)/libsv_ge2e.so
 
 all: $(LIB)
 
+# the wide-tile persistent backward keeps its MFMA accumulators in VGPRs (all AGPRs hold weights)
+build/sv_persist3.o: EXTRA := -mllvm -amdgpu-mfma-vgpr-form=1
+
 build/%.o: $(PKG)/csrc/%.hip $(wildcard $(PKG)/csrc/*.h) include/sv_ge2e.h
 	@mkdir -p build
-	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+	$(HIPCC) $(CXXFLAGS) $(EXTRA) -c $< -o $@
 
 $(LIB): $(OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)

@@ -317,6 +317,11 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
                         const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream,
                         unsigned* sync, float* db_ih = nullptr, float* db_hh = nullptr, hipEvent_t pre = nullptr,
                         hipEvent_t post = nullptr);
+// launcher of the wide-tile persistent backward (sv_persist3.hip; grid = nub x nrb workgroups)
+int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whhT, const bf16_t* acts,
+                           const float* c_tm, const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT,
+                           bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int xcd, unsigned* sync,
+                           unsigned limit, int fault, int dbg, float* dbp);
 // CUs of the device `stream` belongs to (cached per device); dims fit co-resident on `cus` CUs
 int sv_stream_cus(hipStream_t stream);
 int sv_persist_fwd_fits(int B, int H, int cus);

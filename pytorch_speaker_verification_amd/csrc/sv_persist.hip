@@ -28,14 +28,7 @@
 #include "sv_bf16.h"
 #include "../../include/sv_ge2e.h"
 
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sv_rsrc(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
-}
+#include "sv_persist_dev.h"
 
 // A-operand tile of a handed-off buffer: [R][BK] bf16 rows (row stride ld elements) read with
 // buffer_load_dwordx4 sc1 (bypasses the CU's L1, L2-served; rows past the buffer end read 0)
@@ -103,40 +96,6 @@ __device__ __forceinline__ void persist_mainloop(__amdgpu_buffer_rsrc_t ra, int 
   }
   __syncthreads();
 }
-
-// Tile order of the W-stationary kernels (1-D grid of nub x nrb workgroups).  Workgroup i is
-// dispatched to XCD i % 8; with xcd = 1 each XCD gets a contiguous range of logical tiles, so
-// the workgroups that share a row block (and read the same handed-off rows) sit mostly on one
-// XCD and the second and later readers hit that XCD's L2 instead of the fabric.
-__device__ __forceinline__ void persist_tile(int xcd, int nub, int& ub, int& rb) {
-  const int i = blockIdx.x, n = gridDim.x;
-  int L = i;
-  if (xcd) {
-    const int x = i & 7, q = n >> 3, r = n & 7;
-    L = x * q + min(x, r) + (i >> 3);
-  }
-  ub = L % nub;
-  rb = L / nub;
-}
-
-// lane 0 of the workgroup: wait until *c >= target.  Bounded: after `limit` polls the wait sets
-// `code` in the sync block's status word and returns; once the status is nonzero every wait on
-// the block returns at once, so a broken launch drains instead of hanging the GPU.
-__device__ __forceinline__ void persist_wait(unsigned* c, unsigned target, unsigned* status, unsigned limit,
-                                             unsigned code) {
-  unsigned spins = 0;
-  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    __builtin_amdgcn_s_sleep(2);
-    if (++spins > limit) {
-      __hip_atomic_fetch_or(status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-  }
-}
-// test-only fault injection (SV_PERSIST_FAULT=1, read by the host): workgroup 0 withholds its
-// first arrival, so its row block's consumers time out (short spin limit) and the status is set
-__device__ __forceinline__ bool persist_arrive_ok(int fault, int first) { return !(fault && first && blockIdx.x == 0); }
 
 // ============================================================================
 // bf16 forward recurrence of one layer, all T steps.  Tile (b0, j0): 64 batch rows x 32
@@ -1085,7 +1044,20 @@ void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const bf1
 
 // row tile the persistent kernels use for this batch on a device of `cus` CUs (the dgf layout's
 // row-block size)
-int sv_persist_bm(int B, int H, int cus) { return persist_bm(B, H, cus); }
+// wide-tile backward (lstm_persist3_bwd_bf16_kernel): H = 768, (H / 64) x (B / 32) co-resident,
+// and only where the 32-unit tile would need 64-row blocks (B > 320 on 256 CUs: c3); at smaller
+// B the 32 x 32 tile's twice-as-many workgroups win (c5 rank 8.30 vs 9.48 ms, c4 rank 4.36 vs
+// 5.65).  SV_PBWD3=0 keeps the 32-unit tile everywhere.
+int pbwd3_ok(int B, int H, int cus) {
+  static int on = [] {
+    const char* e = getenv("SV_PBWD3");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  const int nrb = (B + 31) / 32;
+  return on && H == 768 && nrb <= SV_PCNT_ROWS && (long)(H / 64) * nrb <= cus && persist_bm(B, H, cus) == 64;
+}
+// row-block size of the backward's fragment-order hand-off (the dx GEMM's A layout)
+int sv_persist_bm(int B, int H, int cus) { return pbwd3_ok(B, H, cus) ? 32 : persist_bm(B, H, cus); }
 
 // can the persistent backward recurrence run these dims (W_hh slice in registers: H in {64, 96, 768})?
 extern "C" int sv_persist_bwd_ok(int B, int H) { return sv_persist_bwd_fits(B, H, current_cus()); }
@@ -1110,8 +1082,9 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
   unsigned* cnt = sync_cnt(sync, 0);
   const int Bp = (B + 7) & ~7;
   const long lddgT = (long)T * Bp;
-  const int bm = persist_bm(B, H, cus);
-  const dim3 grid((H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
+  const bool wide = pbwd3_ok(B, H, cus);
+  const int bm = wide ? 32 : persist_bm(B, H, cus);
+  const dim3 grid(wide ? H / 64 : (H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
   // bias-gradient partials [nrb][4H] after the fragment-order slots (db_ih NULL: not computed)
   float* dbp = db_ih ? reinterpret_cast<float*>(reinterpret_cast<char*>(dgf) +
                                                 (size_t)T * ((B + BF_BM - 1) / BF_BM) * BF_BM * 4 * H * sizeof(bf16_t))
@@ -1120,7 +1093,11 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   // A-fragment prefetch depth 8 at H = 768 (measured: 4 / 16 no better)
-  if (H == 768)
+  if (wide) {
+    sv_persist3_bwd_launch(dim3(grid.x * grid.y), (int)grid.x, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT,
+                           dgf, T, Bp, B, H, cnt, persist_xcd(), sync, persist_limit(), persist_fault(), pbwd_debug(),
+                           dbp);
+  } else if (H == 768)
     launch_pbwd<48, 8>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, sync,
                        dbp);
   else if (H == 96)

@@ -1,0 +1,289 @@
+// Wide-tile persistent backward recurrence (see the kernel comment).  Its own translation unit:
+// built with -mllvm -amdgpu-mfma-vgpr-form=1 (Makefile) so the two accumulators are VGPRs and
+// all 256 AGPRs hold W_hh fragments.
+#include <stdlib.h>
+#include "sv_persist_dev.h"
+#include "../../include/sv_ge2e.h"
+
+// ============================================================================
+// Wide-tile W-stationary backward (H = 768, default; SV_PBWD3=0 keeps the 32-unit tile above).
+// Tile: 32 batch rows x 64 hidden units, so the grid is (H / 64) x (B / 32) -- 240 workgroups at
+// c3 as before -- but each workgroup streams HALF the hand-off bytes per step: wave g's A operand
+// is 32 rows x H of dG_{t+1} (48 KB, one fragment per k-step) and every fragment feeds two MFMAs,
+// one per 32-unit half of W_hh (2 x 48 B fragments = 384 registers: 256 AGPRs + 128 VGPRs).  The
+// per-step operand stream of the 32-unit tile (393 KB per CU from the hand-off buffer, the
+// kernel's dominant phase) becomes 196 KB.  Everything else is the 32-unit kernel's: the same
+// per-gate k order and gate-order sum (bit-identical dG), fragment-order hand-off (row blocks of
+// 32), operands staged by LDS-DMA after the arrival, bias partials per row block.
+// ============================================================================
+// NL: the last NL k-steps of the second W_hh half are read from LDS (staged once, 16 B per lane per
+// fragment, prefetched two k-steps ahead) -- the registers cannot hold all 2 x NS fragments beside
+// the step's working set
+template <int NS, int P, int NL>
+__global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
+    const bf16_t* __restrict__ whhT, const bf16_t* __restrict__ acts, const float* __restrict__ c_tm,
+    const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
+    bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit,
+    int fault, int dbg, float* __restrict__ dbp, unsigned long long* __restrict__ stamps) {
+  constexpr int BM = 32, U = 64, KR = 2;  // rows, units, row passes of the epilogue (16 rows each)
+  constexpr int LDR = U + 4;              // red [4][BM][LDR] fp32
+  constexpr int LDG = 4 * U + 8;          // dgs [BM][LDG] bf16 (row-major dG tile)
+  constexpr int LDT = BM + 8;             // gts [4U][LDT] bf16 (transposed dG tile)
+  constexpr int FRAG = NS * 64 * 8;       // dgf elements of one (row block, gate)
+  static_assert(P >= 1 && P <= NS, "prefetch depth");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red = reinterpret_cast<float*>(smem);
+  bf16_t* dgs = reinterpret_cast<bf16_t*>(smem + 4 * BM * LDR * 4);
+  bf16_t* gts = dgs + BM * LDG;
+  char* ewa = reinterpret_cast<char*>(gts + 4 * U * LDT);  // [BM][512 B]: gate q at ((q + row) & 3) * 128
+  float* ewc = reinterpret_cast<float*>(ewa + BM * 512);    // [BM][U] c_{t-1}
+  float* ewu = ewc + BM * U;                                // [BM][U] dh_up
+  char* wl = reinterpret_cast<char*>(ewu + BM * U);         // [4 waves][NL][64 lanes][16 B]
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  int ub, rb;
+  persist_tile(xcd, nub, ub, rb);
+  const int j0 = ub * U, b0 = rb * BM;
+  const int nrb = gridDim.x / nub;
+  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
+  const long FS = (long)nrb * BM * G;
+  unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
+  const unsigned producers = nub;
+  // W_hh fragments of gate g for units j0 + r (wa) and j0 + 32 + r (wb)
+  constexpr int NR = NS - NL;  // second-half fragments kept in registers
+  bf16x8_t wa[NS], wb[NR];
+  {
+    const bf16_t* ra = whhT + (long)(j0 + r) * G + (long)g * H + 8 * hh;
+    const bf16_t* rbp = ra + 32 * G;
+    const bool oka = j0 + r < H, okb = j0 + 32 + r < H;
+    const bf16x8_t z = {};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) wa[s] = oka ? *reinterpret_cast<const bf16x8_t*>(ra + 16 * s) : z;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) wb[s] = okb ? *reinterpret_cast<const bf16x8_t*>(rbp + 16 * s) : z;
+#pragma unroll
+    for (int s = NR; s < NS; ++s)
+      *reinterpret_cast<bf16x8_t*>(wl + ((g * NL + s - NR) * 64 + lane) * 16) =
+          okb ? *reinterpret_cast<const bf16x8_t*>(rbp + 16 * s) : z;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) asm volatile("" : "+a"(wa[s]));
+#pragma unroll
+    for (int s = 0; s < 64 - NS; ++s) asm volatile("" : "+a"(wb[s]));  // the AGPRs left: 64 - NS fragments
+  }
+  auto wl_read = [&](int j) { return *reinterpret_cast<const bf16x8_t*>(wl + ((g * NL + j) * 64 + lane) * 16); };
+  // elementwise map: thread -> 4 consecutive units (u4) x rows brow, brow + 16
+  const int u4 = (tid & 15) * 4, brow = tid >> 4;
+  float4 cv[KR];
+  float dcf[KR][4];
+  // bias-gradient partial sums of this thread's bf16 dG values over t and its two rows
+  float dbs[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) dbs[q][v] = 0.f;
+  const long Bv = B;
+  // step tt's operands into LDS (buffer_load ... lds; rows past B and absent operands read zeros)
+  auto load_ew = [&](int tt) {
+    const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
+    const __amdgpu_buffer_rsrc_t ra_ = sv_rsrc(acts + (long)tt * BG, (unsigned)(BG * 2));
+    const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(tt > 0 ? tt - 1 : 0) * BH, tt > 0 ? (unsigned)(BH * 4) : 0u);
+    const __amdgpu_buffer_rsrc_t ru_ = sv_rsrc(up ? up : c_tm, up ? (unsigned)(BH * 4) : 0u);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = (g * 4 + j) * 64 + lane, row = p >> 5, sl = p & 31;
+      const int q = ((sl >> 3) - row) & 3, c = sl & 7;
+      const long gb = b0 + row, gbv = gb < Bv ? gb : Bv + 64;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_, (lds_ptr_t)(ewa + (g * 4 + j) * 1024), 16,
+                                               (unsigned)((gbv * G + q * H + j0 + 8 * c) * 2), 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int p = (g * 2 + j) * 64 + lane, row = p >> 4, c = p & 15;
+      const long gb = b0 + row, gbv = gb < Bv ? gb : Bv + 64;
+      const unsigned off = (unsigned)((gbv * H + j0 + 4 * c) * 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rc_, (lds_ptr_t)((char*)ewc + (g * 2 + j) * 1024), 16, off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ru_, (lds_ptr_t)((char*)ewu + (g * 2 + j) * 1024), 16, off, 0, 0, 0);
+    }
+  };
+  {
+    const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(T - 1) * BH, (unsigned)(BH * 4));
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const long gb = b0 + brow + 16 * k;
+      const u32x4_t x =
+          __builtin_amdgcn_raw_buffer_load_b128(rc_, (unsigned)(((gb < Bv ? gb : Bv + 64) * H + j0 + u4) * 4), 0, 0);
+      cv[k] = float4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) dcf[k][v] = 0.f;
+    }
+  }
+  load_ew(T - 1);
+  const bool stamp = dbg & 32;
+  unsigned long long ph[5] = {0, 0, 0, 0, 0}, tlast = stamp ? __builtin_amdgcn_s_memtime() : 0;
+  auto mark = [&](int i) {
+    if (stamp) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      ph[i] += now - tlast;
+      tlast = now;
+    }
+  };
+  for (int t = T - 1; t >= 0; --t) {
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+    if (t < T - 1 && !(dbg & 4)) {
+      if (tid == 0 && !(dbg & 1)) persist_wait(my_cnt, producers * (unsigned)(T - 1 - t), status, limit, 2u);
+      __syncthreads();
+      mark(0);
+      // A fragments of dG_{t+1}: k-step s is the KB at (rb 4 + g) FRAG + s 512
+      const __amdgpu_buffer_rsrc_t ra = sv_rsrc(dgf + (long)(t + 1) * FS, (unsigned)(FS * 2));
+      constexpr unsigned kstep = 1024u;
+      const unsigned base0 = ((unsigned)(rb * 4 + g) * (unsigned)FRAG + (unsigned)lane * 8u) * 2u;
+      u32x4_t fa[P];
+#pragma unroll
+      for (int s = 0; s < P; ++s) fa[s] = __builtin_amdgcn_raw_buffer_load_b128(ra, base0 + kstep * s, 0, 16 /* sc1 */);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8_t wq[2];  // LDS-resident fragments, two k-steps ahead
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const bf16x8_t a = __builtin_bit_cast(bf16x8_t, fa[s % P]);
+        acc0 = mfma_bf16(a, wa[s], acc0);
+        acc1 = mfma_bf16(a, s < NR ? wb[s < NR ? s : 0] : wq[s & 1], acc1);
+        if (s + 2 >= NR && s + 2 < NS) wq[s & 1] = wl_read(s + 2 - NR);  // k-step s + 2 (same parity)
+        if (s + P < NS) fa[s % P] = __builtin_amdgcn_raw_buffer_load_b128(ra, base0 + kstep * (s + P), 0, 16);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // per-gate partials -> red[g][row][unit]
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      red[(g * BM + acc_row(i, lane)) * LDR + r] = acc0[i];
+      red[(g * BM + acc_row(i, lane)) * LDR + 32 + r] = acc1[i];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
+    __syncthreads();
+    mark(1);
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int b = brow + 16 * k;
+      const float4 r0 = *reinterpret_cast<const float4*>(red + (0 * BM + b) * LDR + u4);
+      const float4 r1 = *reinterpret_cast<const float4*>(red + (1 * BM + b) * LDR + u4);
+      const float4 r2 = *reinterpret_cast<const float4*>(red + (2 * BM + b) * LDR + u4);
+      const float4 r3 = *reinterpret_cast<const float4*>(red + (3 * BM + b) * LDR + u4);
+      const float4 cpv = *reinterpret_cast<const float4*>(ewc + b * U + u4);
+      const float4 upv = *reinterpret_cast<const float4*>(ewu + b * U + u4);
+      float4 f[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        f[q] = unpack_bf4(*reinterpret_cast<const uint2*>(ewa + b * 512 + ((q + b) & 3) * 128 + (u4 >> 3) * 16 +
+                                                          (u4 & 7) * 2));
+      const float rs0[4] = {r0.x, r0.y, r0.z, r0.w}, rs1[4] = {r1.x, r1.y, r1.z, r1.w};
+      const float rs2[4] = {r2.x, r2.y, r2.z, r2.w}, rs3[4] = {r3.x, r3.y, r3.z, r3.w};
+      const float ups[4] = {upv.x, upv.y, upv.z, upv.w};
+      const float cs[4] = {cv[k].x, cv[k].y, cv[k].z, cv[k].w}, cps[4] = {cpv.x, cpv.y, cpv.z, cpv.w};
+      const float a0[4] = {f[0].x, f[0].y, f[0].z, f[0].w}, a1[4] = {f[1].x, f[1].y, f[1].z, f[1].w};
+      const float a2[4] = {f[2].x, f[2].y, f[2].z, f[2].w}, a3[4] = {f[3].x, f[3].y, f[3].z, f[3].w};
+      unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float dh = rs0[v];
+        dh += rs1[v];
+        dh += rs2[v];
+        dh += rs3[v];
+        dh += ups[v];
+        float dd[4];
+        dcf[k][v] = lstm_cell_bwd(dh, a0[v], a1[v], a2[v], a3[v], cs[v], cps[v], dcf[k][v], dd);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bf16_t e = to_bf(dd[q]);
+          gts[(q * U + u4 + v) * LDT + b] = e;
+          pk[q][v >> 1] |= (unsigned)e << (16 * (v & 1));
+          dbs[q][v] += __uint_as_float((unsigned)e << 16);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(dgs + b * LDG + q * U + u4) = uint2{pk[q][0], pk[q][1]};
+      cv[k] = cpv;  // c_{t-1} is the next step's c_t
+    }
+    __syncthreads();
+    mark(2);
+    // the hand-off: 16 KB of dG_t per workgroup in fragment order (gate, k-step), 16-B sc1 stores
+    if (!(dbg & 8)) {
+      const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 2));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = tid + 256 * i, c = p >> 6, l = p & 63;
+        const int gq = c >> 2, sl = c & 3;
+        const uint4 v = *reinterpret_cast<const uint4*>(dgs + (l & 31) * LDG + gq * U + 16 * sl + 8 * (l >> 5));
+        const unsigned off =
+            ((unsigned)(rb * 4 + gq) * (unsigned)FRAG + (unsigned)(j0 / 16 + sl) * 512u + (unsigned)l * 8u) * 2u;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
+      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mark(3);
+    if (t > 0) load_ew(t - 1);
+    if (dbg & 8) continue;
+    bf16_t* dgt = dg ? dg + (long)t * BG : nullptr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = tid + 256 * i, row = q >> 5, gq = (q >> 3) & 3, c = q & 7;
+      const int gb = b0 + row, gj = j0 + 8 * c;
+      if (dgt && gb < B && gj < H)
+        *reinterpret_cast<uint4*>(dgt + (long)gb * G + (long)gq * H + gj) =
+            *reinterpret_cast<const uint4*>(dgs + row * LDG + gq * U + 8 * c);
+    }
+    if (dgT) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = tid + 256 * i, gu = q >> 2, c = q & 3;
+        const int gq = gu / U, gj = j0 + gu % U, gb = b0 + 8 * c;
+        if (gb < Bp && gj < H)
+          *reinterpret_cast<uint4*>(dgT + ((long)gq * H + gj) * lddgT + (long)t * Bp + gb) =
+              *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
+      }
+    }
+    mark(4);
+  }
+  if (stamp && tid == 0 && blockIdx.x < SV_NSTAMP_WG)
+    for (int i = 0; i < 5; ++i) stamps[blockIdx.x * SV_NSTAMP + i] = ph[i];
+  if (dbp) {
+    __syncthreads();
+    float* dsum = red;  // [16][4U] fp32: row pairs (brow, brow + 16)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(dsum + brow * (4 * U) + q * U + u4) = float4{dbs[q][0], dbs[q][1], dbs[q][2], dbs[q][3]};
+    __syncthreads();
+    {
+      const int q = tid / U, gj = j0 + tid % U;
+      float sum = 0.f;
+      for (int b = 0; b < 16; ++b) sum += dsum[b * (4 * U) + tid];
+      if (gj < H) dbp[(long)rb * G + (long)q * H + gj] = sum;
+    }
+  }
+}
+
+int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whhT, const bf16_t* acts,
+                           const float* c_tm, const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT,
+                           bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int xcd, unsigned* sync,
+                           unsigned limit, int fault, int dbg, float* dbp) {
+  constexpr int NL = 12;
+  constexpr size_t lds = (size_t)4 * 32 * 68 * 4 + (size_t)32 * 264 * 2 + (size_t)256 * 40 * 2 + (size_t)32 * 512 +
+                         (size_t)2 * 32 * 64 * 4 + (size_t)4 * NL * 1024;
+  unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + SV_SYNC_STAMP);
+  // SV_PBWD3_P: A-fragment prefetch depth (8 default, 4)
+  static const int P = [] {
+    const char* e = getenv("SV_PBWD3_P");
+    return (e && atoi(e) == 4) ? 4 : 8;
+  }();
+  if (P == 4)
+    hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 4, NL>), grid, dim3(256), lds, stream, whhT, acts, c_tm, dhup,
+                       up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbg, dbp, stamps);
+  else
+    hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL>), grid, dim3(256), lds, stream, whhT, acts, c_tm, dhup,
+                       up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbg, dbp, stamps);
+  return (int)hipGetLastError();
+}
