@@ -19,7 +19,7 @@
 // NL: the last NL k-steps of the second W_hh half are read from LDS (staged once, 16 B per lane per
 // fragment, prefetched two k-steps ahead) -- the registers cannot hold all 2 x NS fragments beside
 // the step's working set
-template <int NS, int P, int NL>
+template <int NS, int P, int NL, bool DEFER>
 __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     const bf16_t* __restrict__ whhT, const bf16_t* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
@@ -83,26 +83,56 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     for (int v = 0; v < 4; ++v) dbs[q][v] = 0.f;
   const long Bv = B;
   // step tt's operands into LDS (buffer_load ... lds; rows past B and absent operands read zeros)
-  auto load_ew = [&](int tt) {
-    const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
-    const __amdgpu_buffer_rsrc_t ra_ = sv_rsrc(acts + (long)tt * BG, (unsigned)(BG * 2));
-    const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(tt > 0 ? tt - 1 : 0) * BH, tt > 0 ? (unsigned)(BH * 4) : 0u);
-    const __amdgpu_buffer_rsrc_t ru_ = sv_rsrc(up ? up : c_tm, up ? (unsigned)(BH * 4) : 0u);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int p = (g * 4 + j) * 64 + lane, row = p >> 5, sl = p & 31;
+  // piece i (0..7) of step tt's operand DMA: 0-3 activations, 4-5 c_{t-1}, 6-7 dh_up
+  auto ew_piece = [&](int tt, int i) {
+    if (i < 4) {
+      const __amdgpu_buffer_rsrc_t ra_ = sv_rsrc(acts + (long)tt * BG, (unsigned)(BG * 2));
+      const int p = (g * 4 + i) * 64 + lane, row = p >> 5, sl = p & 31;
       const int q = ((sl >> 3) - row) & 3, c = sl & 7;
       const long gb = b0 + row, gbv = gb < Bv ? gb : Bv + 64;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_, (lds_ptr_t)(ewa + (g * 4 + j) * 1024), 16,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_, (lds_ptr_t)(ewa + (g * 4 + i) * 1024), 16,
                                                (unsigned)((gbv * G + q * H + j0 + 8 * c) * 2), 0, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    } else {
+      const int j = i & 1;
       const int p = (g * 2 + j) * 64 + lane, row = p >> 4, c = p & 15;
       const long gb = b0 + row, gbv = gb < Bv ? gb : Bv + 64;
       const unsigned off = (unsigned)((gbv * H + j0 + 4 * c) * 4);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rc_, (lds_ptr_t)((char*)ewc + (g * 2 + j) * 1024), 16, off, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ru_, (lds_ptr_t)((char*)ewu + (g * 2 + j) * 1024), 16, off, 0, 0, 0);
+      if (i < 6) {
+        const __amdgpu_buffer_rsrc_t rc_ =
+            sv_rsrc(c_tm + (long)(tt > 0 ? tt - 1 : 0) * BH, tt > 0 ? (unsigned)(BH * 4) : 0u);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rc_, (lds_ptr_t)((char*)ewc + (g * 2 + j) * 1024), 16, off, 0, 0, 0);
+      } else {
+        const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
+        const __amdgpu_buffer_rsrc_t ru_ = sv_rsrc(up ? up : c_tm, up ? (unsigned)(BH * 4) : 0u);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ru_, (lds_ptr_t)((char*)ewu + (g * 2 + j) * 1024), 16, off, 0, 0, 0);
+      }
+    }
+  };
+  auto load_ew = [&](int tt) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ew_piece(tt, i);
+  };
+  // store i (0..7) of step tt's dG tile from LDS: 0-3 row-major dG (when dg), 4-7 dG^T (when dgT)
+  auto store_piece = [&](int tt, int i) {
+    // buffer stores with 32-bit offsets (no 64-bit addresses kept live across the k-loop)
+    if (i < 4) {
+      if (!dg) return;
+      const __amdgpu_buffer_rsrc_t rs = sv_rsrc(dg + (long)tt * BG, (unsigned)(BG * 2));
+      const int q = tid + 256 * i, row = q >> 5, gq = (q >> 3) & 3, c = q & 7;
+      const int gb = b0 + row, gj = j0 + 8 * c;
+      const uint4 v = *reinterpret_cast<const uint4*>(dgs + row * LDG + gq * U + 8 * c);
+      if (gb < B && gj < H)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rs,
+                                               (unsigned)(((long)gb * G + (long)gq * H + gj) * 2), 0, 0);
+    } else {
+      if (!dgT) return;
+      const __amdgpu_buffer_rsrc_t rs = sv_rsrc(dgT + (long)tt * Bp, (unsigned)(4L * H * lddgT * 2 - (long)tt * Bp * 2));
+      const int q = tid + 256 * (i - 4), gu = q >> 2, c = q & 3;
+      const int gq = gu / U, gj = j0 + gu % U, gb = b0 + 8 * c;
+      const uint4 v = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
+      if (gb < Bp && gj < H)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rs,
+                                               (unsigned)((((long)gq * H + gj) * lddgT + gb) * 2), 0, 0);
     }
   };
   {
@@ -151,8 +181,18 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
         acc1 = mfma_bf16(a, s < NR ? wb[s < NR ? s : 0] : wq[s & 1], acc1);
         if (s + 2 >= NR && s + 2 < NS) wq[s & 1] = wl_read(s + 2 - NR);  // k-step s + 2 (same parity)
         if (s + P < NS) fa[s % P] = __builtin_amdgcn_raw_buffer_load_b128(ra, base0 + kstep * (s + P), 0, 16);
+        // DEFER: the previous step's leftovers ride in this latency-bound loop instead of delaying
+        // the next wait -- this step's operand DMA (k-steps 1-8), step t+1's dG / dG^T stores
+        // (k-steps 10-17, from the LDS tiles the epilogue below overwrites)
+        if (DEFER && s >= 1 && s <= 8) ew_piece(t, s - 1);
+        if (DEFER && s >= 10 && s <= 17 && !(dbg & 8)) store_piece(t + 1, s - 10);
         __builtin_amdgcn_sched_barrier(0);
       }
+    } else if (DEFER && t < T - 1) {  // no recurrent GEMM (dbg & 4): the leftovers here
+      load_ew(t);
+      if (!(dbg & 8))
+#pragma unroll
+        for (int i = 0; i < 8; ++i) store_piece(t + 1, i);
     }
     // per-gate partials -> red[g][row][unit]
 #pragma unroll
@@ -225,26 +265,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     mark(3);
-    if (t > 0) load_ew(t - 1);
-    if (dbg & 8) continue;
-    bf16_t* dgt = dg ? dg + (long)t * BG : nullptr;
+    if (!DEFER || t == 0) {  // DEFER: all but the last step's leftovers go into the next k-loop
+      if (!DEFER && t > 0) load_ew(t - 1);
+      if (!(dbg & 8))
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = tid + 256 * i, row = q >> 5, gq = (q >> 3) & 3, c = q & 7;
-      const int gb = b0 + row, gj = j0 + 8 * c;
-      if (dgt && gb < B && gj < H)
-        *reinterpret_cast<uint4*>(dgt + (long)gb * G + (long)gq * H + gj) =
-            *reinterpret_cast<const uint4*>(dgs + row * LDG + gq * U + 8 * c);
-    }
-    if (dgT) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = tid + 256 * i, gu = q >> 2, c = q & 3;
-        const int gq = gu / U, gj = j0 + gu % U, gb = b0 + 8 * c;
-        if (gb < Bp && gj < H)
-          *reinterpret_cast<uint4*>(dgT + ((long)gq * H + gj) * lddgT + (long)t * Bp + gb) =
-              *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
-      }
+        for (int i = 0; i < 8; ++i) store_piece(t, i);
     }
     mark(4);
   }
@@ -274,16 +299,20 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
   constexpr size_t lds = (size_t)4 * 32 * 68 * 4 + (size_t)32 * 264 * 2 + (size_t)256 * 40 * 2 + (size_t)32 * 512 +
                          (size_t)2 * 32 * 64 * 4 + (size_t)4 * NL * 1024;
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + SV_SYNC_STAMP);
-  // SV_PBWD3_P: A-fragment prefetch depth (8 default, 4)
-  static const int P = [] {
-    const char* e = getenv("SV_PBWD3_P");
-    return (e && atoi(e) == 4) ? 4 : 8;
+  // SV_PBWD3_DEFER=1: the operand DMA and the dG / dG^T stores inside the next step's k-loop
+  // instead of after the arrival.  Measured slower (c3 bwd 1205 vs 1086 us per layer; the k-loop
+  // phase 5.2k -> 9.0k cycles: the fragment waits count the older stores) -- kept off.
+  static const int defer = [] {
+    const char* e = getenv("SV_PBWD3_DEFER");
+    return (e && *e == '1') ? 1 : 0;
   }();
-  if (P == 4)
-    hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 4, NL>), grid, dim3(256), lds, stream, whhT, acts, c_tm, dhup,
-                       up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbg, dbp, stamps);
+  if (defer)
+    hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL, true>), grid, dim3(256), lds, stream, whhT, acts, c_tm,
+                       dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbg, dbp,
+                       stamps);
   else
-    hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL>), grid, dim3(256), lds, stream, whhT, acts, c_tm, dhup,
-                       up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbg, dbp, stamps);
+    hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL, false>), grid, dim3(256), lds, stream, whhT, acts,
+                       c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbg,
+                       dbp, stamps);
   return (int)hipGetLastError();
 }
