@@ -322,6 +322,10 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
                            const float* c_tm, const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT,
                            bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int xcd, unsigned* sync,
                            unsigned limit, int fault, int dbg, float* dbp);
+// launcher of the wide-tile persistent forward (sv_persist3.hip; no fused input projection)
+int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whh_bf, bf16_t* gates, float* c_tm,
+                           float* h_tm, bf16_t* h_bf, bf16_t* hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt,
+                           int xcd, unsigned* status, unsigned limit, int fault);
 // CUs of the device `stream` belongs to (cached per device); dims fit co-resident on `cus` CUs
 int sv_stream_cus(hipStream_t stream);
 int sv_persist_fwd_fits(int B, int H, int cus);

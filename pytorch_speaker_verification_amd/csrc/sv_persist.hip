@@ -928,6 +928,7 @@ int sv_persist_fwd_fusex_ok(int H, int F) { return H == 768 && F == 40 && persis
 
 // one layer's recurrence (K2 for all t) after its K1 has filled `gates`; on `stream`.  With x_bf
 // (layer 0, sv_persist_fwd_fusex_ok): no K1 -- the kernel forms x_t W_ih^T + b_ih + b_hh itself.
+int pbwd3_ok(int B, int H, int cus);
 int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates, float* c_tm, float* h_tm,
                         bf16_t* h_bf, bf16_t* hT, hipStream_t stream, unsigned* sync, int chan, const bf16_t* x_bf,
                         int F, const bf16_t* wih_bf, const float* b_ih, const float* b_hh, hipEvent_t pre,
@@ -941,8 +942,15 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
   const int Bp = (B + 7) & ~7;
   const long ldhT = (long)(T + 1) * Bp;
   const bool wst = H == 768 && persist_wregs();
-  const int bm = wst ? persist_bm(B, H, cus) : BF_BM;
-  const dim3 grid((H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
+  // wide tile (32 rows x 64 units, sv_persist3.hip) where the wide backward runs, for the layers
+  // whose input projection comes from K1 (SV_PFWD3=0 keeps the 32-unit tile)
+  static const int pf3 = [] {
+    const char* v = getenv("SV_PFWD3");
+    return (v && *v == '0') ? 0 : 1;
+  }();
+  const bool wide = wst && !x_bf && pf3 && pbwd3_ok(B, H, cus);
+  const int bm = wide ? 32 : wst ? persist_bm(B, H, cus) : BF_BM;
+  const dim3 grid(wide ? H / 64 : (H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)grid.y * SV_PCNT_STRIDE * sizeof(unsigned), stream);
   if (e != hipSuccess) return (int)e;
   // SV_PERSIST_DEBUG (profiling only, results invalid): 1 = skip the hand-off waits, 2 = skip the GEMM
@@ -958,7 +966,11 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
     return (v && *v == '0') ? 0 : 1;
   }();
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
-  if (wst) {
+  if (wide) {
+    const int rc = sv_persist3_fwd_launch(dim3(grid.x * grid.y), (int)grid.x, stream, whh_bf, gates, c_tm, h_tm, h_bf,
+                                          hT, ldhT, T, Bp, B, H, cnt, persist_xcd(), status, limit, fault);
+    if (rc) return rc;
+  } else if (wst) {
     constexpr int NS = 48, LDA = NS * 16 + 8;
     const size_t lds = (size_t)bm * LDA * 2 + (size_t)bm * (4 * BF_U + 4) * 4 + (size_t)bm * (BF_U + 8) * 2 +
                        (size_t)BF_U * (bm + 8) * 2;

@@ -316,3 +316,222 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
                        dbp, stamps);
   return (int)hipGetLastError();
 }
+
+// ============================================================================
+// Wide-tile W-stationary forward (H = 768, layers without the fused input projection; the same
+// conditions as the wide backward).  Tile: 32 batch rows x 64 hidden units x 4 gates; wave g
+// holds gate g's W_hh rows for the 64 units (two halves of 48 MFMA B fragments: 256 AGPRs +
+// VGPRs + NL LDS-resident fragments) for the whole sequence.  Per step only h_{t-1} of the 32
+// rows (48 KB, half the 64 x 32 tile's staging) is staged into LDS with sc1 loads, and every A
+// fragment read from LDS feeds two MFMAs.  Same per-gate k order, cell helper and hand-off as
+// lstm_persist2_fwd_bf16_kernel (bit-identical outputs).
+// ============================================================================
+template <int NS, int NL, int PA>
+__global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
+    const bf16_t* __restrict__ whh_bf, bf16_t* __restrict__ gates, float* __restrict__ c_tm, float* __restrict__ h_tm,
+    bf16_t* h_bf, bf16_t* __restrict__ hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd,
+    unsigned* status, unsigned limit, int fault) {
+  constexpr int BM = 32, U = 64, KR = 2;
+  constexpr int K = NS * 16, LDA = K + 8;
+  constexpr int LDP = 4 * U + 4;  // pre [BM][LDP] fp32
+  constexpr int LDB = U + 8;      // hsb [BM][LDB] bf16
+  constexpr int LDT = BM + 8;     // hts [U][LDT] bf16
+  constexpr int NR = NS - NL;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);                // [BM][LDA]
+  float* pre = reinterpret_cast<float*>(smem + BM * LDA * 2);  // [BM][LDP]
+  bf16_t* hsb = reinterpret_cast<bf16_t*>(pre + BM * LDP);     // [BM][LDB]
+  bf16_t* hts = hsb + BM * LDB;                                // [U][LDT]
+  char* wl = reinterpret_cast<char*>(hts + U * LDT);           // [4 waves][NL][64 lanes][16 B]
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  int ub, rb;
+  persist_tile(xcd, nub, ub, rb);
+  const int j0 = ub * U, b0 = rb * BM;
+  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
+  unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
+  const unsigned producers = nub;
+  // W_hh fragments of gate g: B[k][n] = W[g H + j0 + n][k], lane (n = r, k = 16 s + 8 hh .. +7)
+  bf16x8_t wa[NS], wb[NR];
+  {
+    const bf16_t* ra = whh_bf + ((long)g * H + j0 + r) * K + 8 * hh;
+    const bf16_t* rbp = ra + 32L * K;
+    const bool oka = j0 + r < H, okb = j0 + 32 + r < H;
+    const bf16x8_t z = {};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) wa[s] = oka ? *reinterpret_cast<const bf16x8_t*>(ra + 16 * s) : z;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) wb[s] = okb ? *reinterpret_cast<const bf16x8_t*>(rbp + 16 * s) : z;
+#pragma unroll
+    for (int s = NR; s < NS; ++s)
+      *reinterpret_cast<bf16x8_t*>(wl + ((g * NL + s - NR) * 64 + lane) * 16) =
+          okb ? *reinterpret_cast<const bf16x8_t*>(rbp + 16 * s) : z;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) asm volatile("" : "+a"(wa[s]));
+#pragma unroll
+    for (int s = 0; s < 64 - NS; ++s) asm volatile("" : "+a"(wb[s]));
+  }
+  auto wl_read = [&](int j) { return *reinterpret_cast<const bf16x8_t*>(wl + ((g * NL + j) * 64 + lane) * 16); };
+  // elementwise map: thread -> 4 consecutive units (u4) x rows brow, brow + 16
+  const int u4 = (tid & 15) * 4, brow = tid >> 4;
+  const long Bv = B;
+  float cst[KR][4];
+#pragma unroll
+  for (int k = 0; k < KR; ++k)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) cst[k][v] = 0.f;
+  // staging map: BM rows x K bf16 = 3072 16-B chunks, 12 per thread in two halves of 6
+  constexpr int HALF = K / 2, CH = BM * HALF / 8 / 256;
+  uint2 xg[KR][4];
+  auto load_xg = [&](int tt) {
+    const __amdgpu_buffer_rsrc_t rx = sv_rsrc(gates + (long)tt * BG, (unsigned)(BG * 2));
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const long gb = b0 + brow + 16 * k;
+      const long gbv = gb < Bv ? gb : Bv + 64;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const u32x2_t x = __builtin_amdgcn_raw_buffer_load_b64(rx, (unsigned)((gbv * G + q * H + j0 + u4) * 2), 0, 0);
+        xg[k][q] = uint2{x.x, x.y};
+      }
+    }
+  };
+  for (int t = 0; t < T; ++t) {
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+    if (t > 0) {
+      if (tid == 0) persist_wait(my_cnt, producers * (unsigned)t, status, limit, 1u);
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t ra = sv_rsrc(h_bf + (long)t * BH, (unsigned)(BH * 2));
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        uint4 v[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int q = tid + 256 * i, row = q / (HALF / 8), c = (q % (HALF / 8)) * 8 + half * HALF;
+          const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(
+              ra, ((unsigned)(b0 + row) * (unsigned)H + (unsigned)c) * 2u, 0, 16 /* sc1 */);
+          v[i] = uint4{x.x, x.y, x.z, x.w};
+        }
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int q = tid + 256 * i, row = q / (HALF / 8), c = (q % (HALF / 8)) * 8 + half * HALF;
+          *reinterpret_cast<uint4*>(As + row * LDA + c) = v[i];
+        }
+      }
+      __syncthreads();
+      load_xg(t);
+      __builtin_amdgcn_sched_barrier(0);
+      // A fragments PA k-steps ahead; the LDS-resident W fragments two ahead
+      const bf16_t* A0 = As + r * LDA + 8 * hh;
+      bf16x8_t fa[PA], wq[2];
+#pragma unroll
+      for (int p = 0; p < PA; ++p) fa[p] = *reinterpret_cast<const bf16x8_t*>(A0 + 16 * p);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        acc0 = mfma_bf16(fa[s % PA], wa[s], acc0);
+        acc1 = mfma_bf16(fa[s % PA], s < NR ? wb[s < NR ? s : 0] : wq[s & 1], acc1);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        if (s + PA < NS) {
+          fa[s % PA] = *reinterpret_cast<const bf16x8_t*>(A0 + 16 * (s + PA));
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        if (s + 2 >= NR && s + 2 < NS) {
+          wq[s & 1] = wl_read(s + 2 - NR);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      }
+    } else {
+      load_xg(0);
+    }
+    // gate exchange: wave g's [32 rows][64 units] -> pre[row][g * 64 + unit]
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      pre[acc_row(i, lane) * LDP + g * U + r] = acc0[i];
+      pre[acc_row(i, lane) * LDP + g * U + 32 + r] = acc1[i];
+    }
+    __syncthreads();
+    uint2 act[KR][4];
+    float4 cv[KR], hv[KR];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int b = brow + 16 * k;
+      float4 pq[4], xf[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        pq[q] = *reinterpret_cast<const float4*>(pre + b * LDP + q * U + u4);
+        xf[q] = unpack_bf4(xg[k][q]);
+      }
+      float ao[4][4], co[4], ho[4];
+      unsigned pk[2] = {0u, 0u};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float pv[4] = {pq[0][v], pq[1][v], pq[2][v], pq[3][v]};
+        const float xv[4] = {xf[0][v], xf[1][v], xf[2][v], xf[3][v]};
+        float a4[4], h;
+        const float c = lstm_cell_fwd(pv, xv, cst[k][v], a4, h);
+        cst[k][v] = c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ao[q][v] = a4[q];
+        co[v] = c;
+        ho[v] = h;
+        const bf16_t e = to_bf(h);
+        hts[(u4 + v) * LDT + b] = e;
+        pk[v >> 1] |= (unsigned)e << (16 * (v & 1));
+      }
+      *reinterpret_cast<uint2*>(hsb + b * LDB + u4) = uint2{pk[0], pk[1]};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) act[k][q] = pack_bf4(ao[q][0], ao[q][1], ao[q][2], ao[q][3]);
+      cv[k] = float4{co[0], co[1], co[2], co[3]};
+      hv[k] = float4{ho[0], ho[1], ho[2], ho[3]};
+    }
+    __syncthreads();  // hsb, hts complete
+    // the hand-off: h_t bf16, 32 rows x 8 chunks of 8 units, one 16-B sc1 store per thread
+    {
+      const int row = tid >> 3, c = tid & 7, gb = b0 + row;
+      const __amdgpu_buffer_rsrc_t rw = sv_rsrc(h_bf + (long)(t + 1) * BH, (unsigned)(BH * 2));
+      if (gb < B && j0 + 8 * c < H) {
+        const uint4 v = *reinterpret_cast<const uint4*>(hsb + row * LDB + 8 * c);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw,
+                                               ((unsigned)gb * (unsigned)H + (unsigned)(j0 + 8 * c)) * 2u, 0,
+                                               16 /* sc1 */);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0 && persist_arrive_ok(fault, t == 0))
+      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // off the critical chain: activations, c, h and hT of step t
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const long gb = b0 + brow + 16 * k;
+      if (gb < Bv) {
+        bf16_t* gp = gates + (long)t * BG + gb * G + j0 + u4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(gp + q * H) = act[k][q];
+        *reinterpret_cast<float4*>(c_tm + (long)t * BH + gb * H + j0 + u4) = cv[k];
+        *reinterpret_cast<float4*>(h_tm + (long)(t + 1) * BH + gb * H + j0 + u4) = hv[k];
+      }
+    }
+    if (hT) {  // 64 unit rows x 4 chunks of 8 batch columns (padding columns get zeros)
+      const int u = tid >> 2, c = tid & 3, gb = b0 + 8 * c;
+      if (gb < Bp && j0 + u < H) {
+        bf16_t* row = hT + (long)(j0 + u) * ldhT;
+        *reinterpret_cast<uint4*>(row + (long)(t + 1) * Bp + gb) = *reinterpret_cast<const uint4*>(hts + u * LDT + 8 * c);
+        if (t == 0) *reinterpret_cast<uint4*>(row + gb) = uint4{0u, 0u, 0u, 0u};
+      }
+    }
+  }
+}
+
+int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whh_bf, bf16_t* gates, float* c_tm,
+                           float* h_tm, bf16_t* h_bf, bf16_t* hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt,
+                           int xcd, unsigned* status, unsigned limit, int fault) {
+  constexpr int NL = 12;
+  constexpr size_t lds = (size_t)32 * (768 + 8) * 2 + (size_t)32 * (4 * 64 + 4) * 4 + (size_t)32 * 72 * 2 +
+                         (size_t)64 * 40 * 2 + (size_t)4 * NL * 1024;
+  hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4>), grid, dim3(256), lds, stream, whh_bf, gates, c_tm,
+                     h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault);
+  return (int)hipGetLastError();
+}
