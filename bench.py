@@ -19,8 +19,8 @@ Side measurements in the same line:
   c5              (world > 1) N = 256 x M = 10, T = 180 split over the ranks, bf16 (strong)
   c4_rank_shape / c5_rank_shape   (world = 1) one rank's share of c4 / c5 at 8 GPUs, alone
   roofline        the in-step dominant kernel of the headline step: the fp32 backward
-                  recurrent step K3 (lstm_step_bwd_v2_kernel), timed by HIP events recorded on
-                  its own stream around each chunk of its launches INSIDE the timed steps
+                  recurrent step K3 (lstm_step_bwd_v2_kernel), timed by HIP event pairs recorded
+                  on its own stream around one launch per chunk INSIDE the timed steps
   roofline_bf16   the same for c3's dominant kernels, the persistent bf16 recurrences
   roofline_gemm / roofline_step_kernel   secondary: the K1-shape fp32 GEMM and K2 in isolation
   cpu_baseline    the reference's CPU path (oracle/torch_port.py, nn.LSTM on oneDNN) on every
@@ -109,7 +109,7 @@ def _events(n):
 def run_steps(ctx, N, M, T, precision, steps, warmup, seed, probe=None, products="mfma_f32"):
     """Time `steps` fused training steps of this rank's N x M batch.  probe = None, "fwd_bwd"
     (bf16: events around each layer's persistent recurrences) or "bwd_chunks" (fp32: events
-    around each chunk of K3 launches).  Returns (max-over-ranks seconds, loss, host enqueue s,
+    around one K3 launch per chunk).  Returns (max-over-ranks seconds, loss, host enqueue s,
     per-step probe event lists, trainer)."""
     from pytorch_speaker_verification_amd.ops import PIPELINE_CHUNK
     from pytorch_speaker_verification_amd.trainer import GE2ETrainer
@@ -151,6 +151,18 @@ def probe_ms(probes, key):
         ev = p[key]
         tot += sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(len(ev) // 2))
     return tot / max(1, len(probes))
+
+
+def persist_kernels(B, H=768, cus=256):
+    """(bwd, fwd) names of the persistent bf16 recurrence kernels the library picks for the upper
+    layers at batch B (sv_persist.hip: the wide 32 x 64 tile where the 32-unit tile would need
+    64-row blocks; SV_PBWD3 / SV_PFWD3 = 0 keep the 32-unit tile)."""
+    wide = (H == 768 and (B + 31) // 32 * (H // 32) > cus and (B + 31) // 32 * (H // 64) <= cus
+            and os.environ.get("SV_PBWD3", "1") != "0")
+    bwd = "lstm_persist3_bwd_bf16_kernel" if wide else "lstm_persist2_bwd_bf16_kernel"
+    fwd = "lstm_persist3_fwd_bf16_kernel" if wide and os.environ.get("SV_PFWD3", "1") != "0" else \
+        "lstm_persist2_fwd_bf16_kernel"
+    return bwd, fwd
 
 
 def pmc_traffic(kernel):
@@ -472,22 +484,25 @@ def main():
     if dtype == "f32":
         # K3, the headline step's dominant kernel: per-chunk HIP-event spans on its own stream over
         # the timed steps / its L*T launches per step
-        ms_k3 = probe_ms(probes, "bwd") / (L * T)
+        from pytorch_speaker_verification_amd.ops import PIPELINE_CHUNK
+        ms_k3 = probe_ms(probes, "bwd") / (L * ((T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK))  # one launch per chunk
         out["roofline"] = roofline_entry(
             "lstm_step_bwd_v2_kernel (K3, fp32 MFMA 32x32x2, backward recurrent step)", 2.0 * B * H * 4 * H, ms_k3,
             MI355X_FP32_MFMA_TFLOPS, pmc_traffic("lstm_step_bwd_v2_kernel"), L * T * args.steps,
-            "in-step: HIP events recorded on the recurrence's stream around each 32-step chunk of K3 launches inside "
-            "the timed steps (sum of chunk spans / launches; includes the inter-launch gaps of the chunk)")
+            "in-step: HIP event pairs on the recurrence's stream around one K3 launch per 32-step chunk (its second "
+            "launch) inside the timed steps; average over the sampled launches")
     else:
         fl = 2.0 * B * T * H * 4 * H
+        kb, kf = persist_kernels(B)
         out["roofline"] = roofline_entry(
-            "lstm_persist2_bwd_bf16_kernel (persistent backward recurrence, one launch per layer, bf16 MFMA)", fl,
-            probe_ms(probes, "bwd") / L, MI355X_BF16_MFMA_TFLOPS, pmc_traffic("lstm_persist2_bwd_bf16_kernel"),
+            f"{kb} (persistent backward recurrence, one launch per layer, bf16 MFMA)", fl,
+            probe_ms(probes, "bwd") / L, MI355X_BF16_MFMA_TFLOPS, pmc_traffic(kb),
             L * args.steps, "in-step: HIP events around each layer's launch inside the timed steps")
         out["roofline_fwd"] = roofline_entry(
-            "lstm_persist2_fwd_bf16_kernel (persistent forward recurrence)", fl, probe_ms(probes, "fwd") / L,
-            MI355X_BF16_MFMA_TFLOPS, pmc_traffic("lstm_persist2_fwd_bf16_kernel"), L * args.steps,
-            "in-step, as roofline")
+            f"{kf} (persistent forward recurrence; layer 0: lstm_persist2_fwd_bf16_kernel with the fused input "
+            "projection)", fl, probe_ms(probes, "fwd") / L,
+            MI355X_BF16_MFMA_TFLOPS, pmc_traffic(kf), L * args.steps,
+            "in-step, as roofline (average over the L layers' launches)")
 
     # forward-only (inference) embeddings/s at the headline shape
     from pytorch_speaker_verification_amd.ops import embedder_forward, embedder_forward_bf16
@@ -527,13 +542,15 @@ def main():
         o, pr = side("bf16", N, M, T, "bf16", False, "c3: the headline workload with bf16 GEMM operands, fp32 "
                      "accumulate/state/loss", probe="fwd_bwd")
         fl = 2.0 * B * T * H * 4 * H
+        kb, kf = persist_kernels(B)
         out["roofline_bf16"] = roofline_entry(
-            "lstm_persist2_bwd_bf16_kernel (c3's dominant kernel: persistent backward recurrence)", fl,
-            probe_ms(pr, "bwd") / L, MI355X_BF16_MFMA_TFLOPS, pmc_traffic("lstm_persist2_bwd_bf16_kernel"),
+            f"{kb} (c3's dominant kernel: persistent backward recurrence)", fl,
+            probe_ms(pr, "bwd") / L, MI355X_BF16_MFMA_TFLOPS, pmc_traffic(kb),
             L * args.steps, "in-step: HIP events around each layer's launch inside the timed c3 steps")
         out["roofline_bf16_fwd"] = roofline_entry(
-            "lstm_persist2_fwd_bf16_kernel (persistent forward recurrence)", fl, probe_ms(pr, "fwd") / L,
-            MI355X_BF16_MFMA_TFLOPS, pmc_traffic("lstm_persist2_fwd_bf16_kernel"), L * args.steps, "in-step")
+            f"{kf} (persistent forward recurrence; layer 0: the fused-projection 32-unit kernel)", fl,
+            probe_ms(pr, "fwd") / L, MI355X_BF16_MFMA_TFLOPS, pmc_traffic(kf), L * args.steps,
+            "in-step (average over the L layers' launches)")
         if world > 1:
             side("c4", max(1, 64 // world), 10, 160, "bf16", True,
                  f"c4: N=64xM=10, T=160, bf16, split over {world} GPUs ({max(1, 64 // world)} speakers per rank); "

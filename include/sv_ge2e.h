@@ -91,8 +91,9 @@ size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H);
  * xT/ld_xT: per-layer transposed inputs; dx[l] [T,B,H] for l > 0;
  * ev = L*ceil(T/chunk) + L + 1 caller events (ev[L*nch + l] = layer l's gradients done);
  * joins back into `main`.  probe (may be NULL): 2*L*ceil(T/chunk) caller events recorded on the
- * layer's stream around each chunk's recurrent-step (K3) launches, probe[2(l nch + c)] before,
- * [+1] after -- in-step kernel timing for the bench's roofline. */
+ * layer's stream around ONE recurrent-step (K3) launch of each chunk (its second),
+ * probe[2(l nch + c)] before, [+1] after -- a per-launch in-step sample of K3's duration for the
+ * bench's roofline. */
 size_t sv_lstm_stack_bwd_workspace(int L, int T, int B, int F, int H);
 int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float* const* xT, const long* ld_xT,
                       const float* const* w_ih, const float* const* w_hh, const float* const* gates,

@@ -1332,17 +1332,20 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
     for (int c = nch - 1; c >= 0; --c) {
       const int t0 = c * chunk, t1 = std::min(T, t0 + chunk);
       if (l < L - 1 && (e = hipStreamWaitEvent(s, ev[(l + 1) * nch + c], 0)) != hipSuccess) return (int)e;
-      if (probe && (e = hipEventRecord(probe[2 * (l * nch + c)], s)) != hipSuccess) return (int)e;
+      // timing probe: one K3 launch per chunk (the chunk's second, behind a running K3 on its
+      // stream; the first if the chunk has one) bracketed by the caller's event pair
+      const int tp = t1 - t0 > 1 ? t1 - 2 : t0;
       for (int t = t1 - 1; t >= t0; --t) {
         const float* up = (l == L - 1) ? (t == T - 1 ? dh_last : nullptr) : dx[l + 1] + t * BH;
         float* dcf_out = (t & 1) ? ws.dcf1 : ws.dcf0;
         const float* dcf_in = (t == T - 1) ? nullptr : ((t & 1) ? ws.dcf0 : ws.dcf1);
+        if (probe && t == tp && (e = hipEventRecord(probe[2 * (l * nch + c)], s)) != hipSuccess) return (int)e;
         launch_bwd_step(grid, s, t == T - 1 ? nullptr : dgates[l] + (t + 1) * BG, ws.whhT, up, dcf_in,
                         gates[l] + t * BG, c_tm[l] + t * BH, t ? c_tm[l] + (t - 1) * BH : nullptr, dgates[l] + t * BG,
                         dcf_out, dgT[l], (long)TBp, t, Bp, B, H);
         SV_LAUNCH_CHECK();
+        if (probe && t == tp && (e = hipEventRecord(probe[2 * (l * nch + c) + 1], s)) != hipSuccess) return (int)e;
       }
-      if (probe && (e = hipEventRecord(probe[2 * (l * nch + c) + 1], s)) != hipSuccess) return (int)e;
       if (l > 0 && dx_side()) {  // dx on the layer's second stream: the recurrence goes on at once
         if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
         if ((e = hipStreamWaitEvent(side[L + l], ev[l * nch + c], 0)) != hipSuccess) return (int)e;

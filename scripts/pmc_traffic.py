@@ -14,6 +14,9 @@ FAMILIES = {  # json key -> kernel-name prefix
     "lstm_step_fwd_v2_kernel": "void lstm_step_fwd_v2_kernel<32, 101",
     "lstm_persist2_bwd_bf16_kernel": "void lstm_persist2_bwd_bf16_kernel<",
     "lstm_persist2_fwd_bf16_kernel": "void lstm_persist2_fwd_bf16_kernel<48, 64, 0>",
+    "lstm_persist3_bwd_bf16_kernel": "void lstm_persist3_bwd_bf16_kernel<",
+    "lstm_persist3_fwd_bf16_kernel": "void lstm_persist3_fwd_bf16_kernel<",
+    "gemm_bf16_8q_kernel": "void gemm_bf16_8q_kernel<",
 }
 
 
