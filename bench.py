@@ -128,8 +128,10 @@ def run_steps(ctx, N, M, T, precision, steps, warmup, seed, probe=None, products
     for _ in range(steps if probe else 0):
         if probe == "fwd_bwd":
             probes.append({"fwd": _events(2 * L), "bwd": _events(2 * L)})
-        else:
-            probes.append({"bwd": _events(2 * L * nch)})
+        else:  # fp32: events + the kernel's own real-time stamps around one K3 launch per chunk
+            ks = torch.zeros(2 * L * T, dtype=torch.int64, device=ctx.dev)
+            ks[0::2] = -1  # (UINT64_MAX, 0) pairs: atomic min / max targets
+            probes.append({"bwd": _events(2 * L * nch), "kstamp": ks})
     ctx.barrier()
     t0 = time.perf_counter()
     host = 0.0
@@ -142,6 +144,16 @@ def run_steps(ctx, N, M, T, precision, steps, warmup, seed, probe=None, products
     tr.check()  # raises if a persistent recurrence timed out during the timed steps
     log(f"  {dt / steps * 1e3:.3f} ms/step")
     return dt, float(loss), host, probes, tr
+
+
+def kstamp_us(probes):
+    """Average execution span (us) of the timed steps' K3 launches from the kernels' own real-time
+    stamps (100 MHz GPU clock, first-workgroup start to last-workgroup end)."""
+    spans = []
+    for p in probes:
+        ks = p["kstamp"].cpu().view(-1, 2)
+        spans += [int(e - s_) / 100.0 for s_, e in ks.tolist() if e > 0]
+    return sum(spans) / max(1, len(spans)), len(spans)
 
 
 def probe_ms(probes, key):
@@ -166,10 +178,11 @@ def persist_kernels(B, H=768, cus=256):
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json),
-    corrected as MI355X_MICROARCH.md prescribes (FETCH_SIZE x 2 + WRITE_SIZE, both KiB)."""
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (bench_pmc_traffic.json at the
+    repo root: profiles/ does not travel to the GPU box), corrected as MI355X_MICROARCH.md
+    prescribes (FETCH_SIZE x 2 + WRITE_SIZE, both KiB)."""
     try:
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+        with open(os.path.join(ROOT, "bench_pmc_traffic.json")) as f:
             return json.load(f)[kernel]["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         return None
@@ -485,12 +498,16 @@ def main():
         # K3, the headline step's dominant kernel: per-chunk HIP-event spans on its own stream over
         # the timed steps / its L*T launches per step
         from pytorch_speaker_verification_amd.ops import PIPELINE_CHUNK
-        ms_k3 = probe_ms(probes, "bwd") / (L * ((T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK))  # one launch per chunk
+        us_k3, n_k3 = kstamp_us(probes)
+        ms_ev = probe_ms(probes, "bwd") / (L * ((T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK))
         out["roofline"] = roofline_entry(
-            "lstm_step_bwd_v2_kernel (K3, fp32 MFMA 32x32x2, backward recurrent step)", 2.0 * B * H * 4 * H, ms_k3,
-            MI355X_FP32_MFMA_TFLOPS, pmc_traffic("lstm_step_bwd_v2_kernel"), L * T * args.steps,
-            "in-step: HIP event pairs on the recurrence's stream around one K3 launch per 32-step chunk (its second "
-            "launch) inside the timed steps; average over the sampled launches")
+            "lstm_step_bwd_v2_kernel (K3, fp32 MFMA 32x32x2, backward recurrent step)", 2.0 * B * H * 4 * H,
+            us_k3 * 1e-3, MI355X_FP32_MFMA_TFLOPS, pmc_traffic("lstm_step_bwd_v2_kernel"), n_k3,
+            "in-step: every K3 launch of the timed steps, timed by the kernel's own start / end stamps on the GPU's "
+            "100 MHz real-time clock (execution span, as rocprofv3 measures it; HIP event pairs on the stream also "
+            "count the wait for CUs held by the concurrent GEMMs: stream_span_us, HIP events around one launch per "
+            "32-step chunk)")
+        out["roofline"]["stream_span_us"] = round(ms_ev * 1e3, 2)
     else:
         fl = 2.0 * B * T * H * 4 * H
         kb, kf = persist_kernels(B)

@@ -92,15 +92,18 @@ size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H);
  * ev = L*ceil(T/chunk) + L + 1 caller events (ev[L*nch + l] = layer l's gradients done);
  * joins back into `main`.  probe (may be NULL): 2*L*ceil(T/chunk) caller events recorded on the
  * layer's stream around ONE recurrent-step (K3) launch of each chunk (its second),
- * probe[2(l nch + c)] before, [+1] after -- a per-launch in-step sample of K3's duration for the
- * bench's roofline. */
+ * probe[2(l nch + c)] before, [+1] after (stream view: includes any wait for CUs); kstamp (may be
+ * NULL): 2*L*T u64, each pair preset by the caller to {UINT64_MAX, 0}, which K3 launch (l, t)
+ * sets to its first-workgroup start / last-workgroup end on the GPU's 100 MHz real-time clock
+ * (the kernel's own execution span, as a profiler measures it) -- the bench's in-step roofline. */
 size_t sv_lstm_stack_bwd_workspace(int L, int T, int B, int F, int H);
 int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float* const* xT, const long* ld_xT,
                       const float* const* w_ih, const float* const* w_hh, const float* const* gates,
                       const float* const* c_tm, const float* const* hT, const float* dh_last, float* const* dgates,
                       float* const* dgT, float* const* dx, float* const* dw_ih, float* const* dw_hh,
                       float* const* db_ih, float* const* db_hh, float* workspace, int chunk, hipStream_t main,
-                      const hipStream_t* side, hipEvent_t* ev, int products, hipEvent_t* probe);
+                      const hipStream_t* side, hipEvent_t* ev, int products, hipEvent_t* probe,
+                      unsigned long long* kstamp);
 /* xT: the layer input transposed, [F, >= T*Bp] with row stride ld_xT (layer 0: the frames;
  * layer l > 0: hT of layer l-1 offset by Bp columns).  hT: this layer's [H, (T+1)Bp] from the fwd.
  * dh_up: gradient w.r.t. this layer's outputs; dh_up_full=1 -> [T,B,H], 0 -> [B,H] for t=T-1 only.

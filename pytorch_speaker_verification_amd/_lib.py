@@ -38,7 +38,7 @@ SIGNATURES = {
                                    _c_int, _P, _P, _P, _c_int]),
     "sv_lstm_stack_bwd_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "sv_lstm_stack_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P, _c_int,
-                                                                                          _P]),
+                                                                                          _P, _P]),
     "sv_lstm_layer_bwd_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
     "sv_lstm_layer_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _P, _c_long, _P, _P, _P, _P, _P, _P, _c_int, _P,
                                    _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -540,7 +540,10 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
     const float* __restrict__ dgnext, const float* __restrict__ whhT, const float* __restrict__ dhup,
     const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, float* __restrict__ dg, float* __restrict__ dcf, float* __restrict__ dgT,
-    long lddgT, int t, int Bp, int B, int H, int krot = 0) {
+    long lddgT, int t, int Bp, int B, int H, int krot = 0, unsigned long long* __restrict__ ts = nullptr) {
+  // ts (timing sample, bench only): [start, end] of this launch on the 100 MHz real-time clock,
+  // first workgroup start (min) and last workgroup end (max), vector atomics
+  if (ts && threadIdx.x == 0) atomicMin(ts, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int GBUF = 2 * (BWD_BM + BWD_U) * (BKX + 4);
   constexpr int LDR = BWD_U + 1;
@@ -615,14 +618,20 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
     gT[(2 * BWD_U + u) * LDT + b] = d2;
     gT[(3 * BWD_U + u) * LDT + b] = d3;
   }
-  if (!dgT) return;
-  __syncthreads();
-  for (int e = tid; e < 4 * BWD_U * BWD_BM; e += 512) {
-    const int gu = e / BWD_BM, b = e % BWD_BM;
-    const int gte = gu / BWD_U, u = gu % BWD_U;
-    const int gb = b0 + b, gj = j0 + u;
-    if (gb >= B || gj >= H) continue;
-    dgT[((long)gte * H + gj) * lddgT + (long)t * Bp + gb] = gT[gu * LDT + b];
+  if (dgT) {
+    __syncthreads();
+    for (int e = tid; e < 4 * BWD_U * BWD_BM; e += 512) {
+      const int gu = e / BWD_BM, b = e % BWD_BM;
+      const int gte = gu / BWD_U, u = gu % BWD_U;
+      const int gb = b0 + b, gj = j0 + u;
+      if (gb >= B || gj >= H) continue;
+      dgT[((long)gte * H + gj) * lddgT + (long)t * Bp + gb] = gT[gu * LDT + b];
+    }
+  }
+  if (ts) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(ts + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
 }
 
@@ -1046,7 +1055,7 @@ void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh
 }
 void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* whhT, const float* up, const float* dcfi,
                      const float* acts, const float* ct, const float* cp, float* dg, float* dcfo, float* dgT,
-                     long lddgT, int t, int Bp, int B, int H) {
+                     long lddgT, int t, int Bp, int B, int H, unsigned long long* ts = nullptr) {
   if (step_variant() >= 2 && bwd_bk() == 16)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<16, 2>), grid, dim3(512), BWD_LDS16, s, dgn, whhT, up, dcfi, acts, ct,
                        cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, 0);
@@ -1074,9 +1083,9 @@ void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* wh
   else if (step_variant() >= 2 && k3_pipe() == 5)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 1>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
                        acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && k3_pipe() == 6)
+  else if (step_variant() >= 2 && k3_pipe() == 6)  // the default K3
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 2>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
-                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
+                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot(), ts);
   else if (step_variant() >= 2 && k3_pipe() == 7)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 3>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
                        acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
@@ -1303,7 +1312,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
                                  float* const* dgates, float* const* dgT, float* const* dx, float* const* dw_ih,
                                  float* const* dw_hh, float* const* db_ih, float* const* db_hh, float* workspace,
                                  int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev,
-                                 int products, hipEvent_t* probe) {
+                                 int products, hipEvent_t* probe, unsigned long long* kstamp) {
   if (L <= 0 || !xT || !ld_xT || !w_ih || !w_hh || !gates || !c_tm || !hT || !dh_last || !dgates || !dgT || !dx ||
       !dw_ih || !dw_hh || !db_ih || !workspace || !side || !ev || chunk <= 0)
     return SV_EARG;
@@ -1342,7 +1351,8 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
         if (probe && t == tp && (e = hipEventRecord(probe[2 * (l * nch + c)], s)) != hipSuccess) return (int)e;
         launch_bwd_step(grid, s, t == T - 1 ? nullptr : dgates[l] + (t + 1) * BG, ws.whhT, up, dcf_in,
                         gates[l] + t * BG, c_tm[l] + t * BH, t ? c_tm[l] + (t - 1) * BH : nullptr, dgates[l] + t * BG,
-                        dcf_out, dgT[l], (long)TBp, t, Bp, B, H);
+                        dcf_out, dgT[l], (long)TBp, t, Bp, B, H,
+                        kstamp ? kstamp + 2 * ((long)l * T + t) : nullptr);
         SV_LAUNCH_CHECK();
         if (probe && t == tp && (e = hipEventRecord(probe[2 * (l * nch + c) + 1], s)) != hipSuccess) return (int)e;
       }

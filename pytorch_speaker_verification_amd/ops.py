@@ -203,7 +203,7 @@ def embedder_forward(x, layers, w_p, b_p, save=True, products="mfma_f32"):
 
 
 def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_ready=None, products="mfma_f32",
-                      probe=None):
+                      probe=None, kstamp=None):
     """Backward of embedder_forward.  ``grads`` (optional) is a list of preallocated
     output tensors in parameter order [w_ih, w_hh, b_ih, b_hh]*L + [w_p, b_p]; returns it
     (and dx [B,T,F] if need_dx).
@@ -213,8 +213,10 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
     event that completes it (None: the current stream).  The data-parallel trainer hangs its
     per-layer all-reduce buckets on it so communication overlaps the rest of the BPTT.
 
-    ``probe`` (optional): 2*L*ceil(T/chunk) timing events recorded around each chunk's
-    recurrent-step launches (include/sv_ge2e.h, sv_lstm_stack_bwd)."""
+    ``probe`` (optional): 2*L*ceil(T/chunk) timing events recorded around one recurrent-step
+    launch per chunk; ``kstamp`` (optional): int64 device tensor of 2*L*T slots, pairs preset
+    to (-1, 0), set by every recurrent-step launch (l, t) to its start / end on the GPU's 100 MHz
+    real-time clock (include/sv_ge2e.h, sv_lstm_stack_bwd)."""
     prod = _products(products)
     demb = demb.contiguous()
     require_device(demb)
@@ -255,7 +257,7 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
              _parr(st.hT), ptr(dh_last), _parr(dgs), _parr(dgTs), _parr(dxs),
              _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
              _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
-             PIPELINE_CHUNK, s, sp, ep, prod, _evarr(probe))
+             PIPELINE_CHUNK, s, sp, ep, prod, _evarr(probe), ptr(kstamp) if kstamp is not None else None)
         if grad_ready:
             for l in range(L - 1, -1, -1):
                 grad_ready(l, events[L * nch + l])

@@ -148,7 +148,7 @@ class GE2ETrainer:
                                    status=self.status, probe=probe.get("bwd"))
         else:
             embedder_backward(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views, grad_ready=ready,
-                              products=products, probe=probe.get("bwd"))
+                              products=products, probe=probe.get("bwd"), kstamp=probe.get("kstamp"))
         for wk in works:
             wk.wait()  # the current (main) stream waits for every bucket
         n = self.n_pad

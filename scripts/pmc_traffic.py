@@ -1,5 +1,5 @@
 """Fold rocprofv3 FETCH_SIZE / WRITE_SIZE passes (separate runs, gpurun_out/pmc_traffic/*) into
-profiles/pmc_traffic.json: per kernel family, the average HBM bytes per launch corrected as
+bench_pmc_traffic.json: per kernel family, the average HBM bytes per launch corrected as
 MI355X_MICROARCH.md prescribes (2 x FETCH_SIZE + WRITE_SIZE, counters in KiB).
 Usage: python scripts/pmc_traffic.py <dir with f32_fetch/f32_write/bf16_fetch/bf16_write csvs>"""
 import csv
@@ -33,7 +33,7 @@ def per_launch(path, counter):
 
 
 def main(d):
-    out_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    out_path = os.path.join(ROOT, "bench_pmc_traffic.json")  # read by bench.py (profiles/ stays here)
     data = json.load(open(out_path)) if os.path.exists(out_path) else {}
     for tag in ("f32", "bf16"):
         fs = glob.glob(os.path.join(d, f"{tag}_fetch*", "**", "*counter_collection.csv"), recursive=True)
