@@ -1,5 +1,6 @@
-"""GPU: the mixed-precision configs (BASELINE c3 / c4 / c5: bf16 GEMM operands, fp32 state,
-accumulation, gradients and loss) pinned to the bf16-operand oracle (oracle/lstm_bf16.py, whose
+"""GPU: the mixed-precision configs (BASELINE c3 / c4 / c5: bf16 GEMM operands, bf16 storage of the
+x-projection and saved activations, fp32 state, accumulation, gradients and loss) pinned to the
+bf16 oracle (oracle/lstm_bf16.py, whose
 fp32 mode is pinned to the reference's golden vectors), at the shapes the configs run per GPU:
 
   c4 per rank   N = 64 speakers over 8 GPUs -> 8 x M = 10 = 80 utterances, T = 160
@@ -75,7 +76,9 @@ def test_c4_rank_shape_bf16_against_oracle():
     from pytorch_speaker_verification_amd._lib import lib
     dims, N, M, T = (40, 768, 3, 256), 8, 10, 160
     assert lib().sv_persist_fwd_ok(N * M, 768) and lib().sv_persist_bwd_ok(N * M, 768)
-    _compare("c4_rank", dims, N, M, T, 4040, dict(emb=5e-3, loss=5e-4, grad=5e-2, param=2e-5))
+    # loss 2e-3: measured 2.9e-4 since the x-projection is stored in bf16 (the wavefront rounds it
+    # inside its accumulator, so fp32-order flips of that rounding reach the loss at B = 80)
+    _compare("c4_rank", dims, N, M, T, 4040, dict(emb=5e-3, loss=2e-3, grad=5e-2, param=2e-5))
 
 
 def test_c3_shape_bf16_against_oracle():
