@@ -325,7 +325,9 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
 // launcher of the wide-tile persistent forward (sv_persist3.hip; no fused input projection)
 int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whh_bf, bf16_t* gates, float* c_tm,
                            float* h_tm, bf16_t* h_bf, bf16_t* hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt,
-                           int xcd, unsigned* status, unsigned limit, int fault);
+                           int xcd, unsigned* status, unsigned limit, int fault, const bf16_t* x_bf = nullptr,
+                           int F = 0, const bf16_t* wih_bf = nullptr, const float* b_ih = nullptr,
+                           const float* b_hh = nullptr);
 // CUs of the device `stream` belongs to (cached per device); dims fit co-resident on `cus` CUs
 int sv_stream_cus(hipStream_t stream);
 int sv_persist_fwd_fits(int B, int H, int cus);

@@ -942,13 +942,13 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
   const int Bp = (B + 7) & ~7;
   const long ldhT = (long)(T + 1) * Bp;
   const bool wst = H == 768 && persist_wregs();
-  // wide tile (32 rows x 64 units, sv_persist3.hip) where the wide backward runs, for the layers
-  // whose input projection comes from K1 (SV_PFWD3=0 keeps the 32-unit tile)
+  // wide tile (32 rows x 64 units, sv_persist3.hip) where the wide backward runs, with or without
+  // the fused layer-0 projection (SV_PFWD3=0 keeps the 32-unit tile)
   static const int pf3 = [] {
     const char* v = getenv("SV_PFWD3");
     return (v && *v == '0') ? 0 : 1;
   }();
-  const bool wide = wst && !x_bf && pf3 && pbwd3_ok(B, H, cus);
+  const bool wide = wst && pf3 && pbwd3_ok(B, H, cus);
   const int bm = wide ? 32 : wst ? persist_bm(B, H, cus) : BF_BM;
   const dim3 grid(wide ? H / 64 : (H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)grid.y * SV_PCNT_STRIDE * sizeof(unsigned), stream);
@@ -968,7 +968,8 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   if (wide) {
     const int rc = sv_persist3_fwd_launch(dim3(grid.x * grid.y), (int)grid.x, stream, whh_bf, gates, c_tm, h_tm, h_bf,
-                                          hT, ldhT, T, Bp, B, H, cnt, persist_xcd(), status, limit, fault);
+                                          hT, ldhT, T, Bp, B, H, cnt, persist_xcd(), status, limit, fault, x_bf, F,
+                                          wih_bf, b_ih, b_hh);
     if (rc) return rc;
   } else if (wst) {
     constexpr int NS = 48, LDA = NS * 16 + 8;

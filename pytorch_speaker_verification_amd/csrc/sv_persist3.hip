@@ -326,11 +326,15 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
 // fragment read from LDS feeds two MFMAs.  Same per-gate k order, cell helper and hand-off as
 // lstm_persist2_fwd_bf16_kernel (bit-identical outputs).
 // ============================================================================
-template <int NS, int NL, int PA>
+// XF > 0 (layer 0, F = 8 XF <= 48 features): the input projection formed in the kernel from x_bf
+// [T,B,F] and W_ih [4H,F] (both halves' fragments in registers), rounded to bf16 with its biases as
+// the K1 path stores it -- lstm_persist2_fwd_bf16_kernel's fused form.
+template <int NS, int NL, int PA, int XF>
 __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
     const bf16_t* __restrict__ whh_bf, bf16_t* __restrict__ gates, float* __restrict__ c_tm, float* __restrict__ h_tm,
     bf16_t* h_bf, bf16_t* __restrict__ hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd,
-    unsigned* status, unsigned limit, int fault) {
+    unsigned* status, unsigned limit, int fault, const bf16_t* __restrict__ x_bf, const bf16_t* __restrict__ wih_bf,
+    const float* __restrict__ b_ih, const float* __restrict__ b_hh) {
   constexpr int BM = 32, U = 64, KR = 2;
   constexpr int K = NS * 16, LDA = K + 8;
   constexpr int LDP = 4 * U + 4;  // pre [BM][LDP] fp32
@@ -372,6 +376,37 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
     for (int s = 0; s < 64 - NS; ++s) asm volatile("" : "+a"(wb[s]));
   }
   auto wl_read = [&](int j) { return *reinterpret_cast<const bf16x8_t*>(wl + ((g * NL + j) * 64 + lane) * 16); };
+  // fused input projection (XF > 0): W_ih fragments of both 32-column halves of gate g (zero past
+  // F) and the columns' biases
+  constexpr int XS = (XF + 1) / 2, F = 8 * XF;
+  bf16x8_t wxa[XS > 0 ? XS : 1], wxb[XS > 0 ? XS : 1];
+  float xba = 0.f, xbb = 0.f;
+  if constexpr (XF > 0) {
+    const int ca = g * H + j0 + r, cb = ca + 32;
+    const bf16x8_t z = {};
+#pragma unroll
+    for (int s2 = 0; s2 < XS; ++s2) {
+      const bool kok = 16 * s2 + 8 * hh < F;
+      wxa[s2] = (kok && j0 + r < H) ? *reinterpret_cast<const bf16x8_t*>(wih_bf + (long)ca * F + 16 * s2 + 8 * hh) : z;
+      wxb[s2] =
+          (kok && j0 + 32 + r < H) ? *reinterpret_cast<const bf16x8_t*>(wih_bf + (long)cb * F + 16 * s2 + 8 * hh) : z;
+    }
+    if (j0 + r < H) xba = (b_ih ? b_ih[ca] : 0.f) + (b_hh ? b_hh[ca] : 0.f);
+    if (j0 + 32 + r < H) xbb = (b_ih ? b_ih[cb] : 0.f) + (b_hh ? b_hh[cb] : 0.f);
+  }
+  // x_t A fragments (rows b0 + r, k = 16 s + 8 hh); rows past B and k past F read zeros
+  u32x4_t xa[XS > 0 ? XS : 1];
+  auto load_x = [&](int tt) {
+    if constexpr (XF > 0) {
+      const __amdgpu_buffer_rsrc_t rxs = sv_rsrc(x_bf + (long)tt * B * F, (unsigned)((long)B * F * 2));
+#pragma unroll
+      for (int s2 = 0; s2 < XS; ++s2) {
+        const unsigned off =
+            16 * s2 + 8 * hh < F ? ((unsigned)(b0 + r) * (unsigned)F + 16 * s2 + 8 * hh) * 2u : 0xFFFFFFF0u;
+        xa[s2] = __builtin_amdgcn_raw_buffer_load_b128(rxs, off, 0, 0);
+      }
+    }
+  };
   // elementwise map: thread -> 4 consecutive units (u4) x rows brow, brow + 16
   const int u4 = (tid & 15) * 4, brow = tid >> 4;
   const long Bv = B;
@@ -384,6 +419,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
   constexpr int HALF = K / 2, CH = BM * HALF / 8 / 256;
   uint2 xg[KR][4];
   auto load_xg = [&](int tt) {
+    if constexpr (XF > 0) {
+      load_x(tt);
+      return;
+    }
     const __amdgpu_buffer_rsrc_t rx = sv_rsrc(gates + (long)tt * BG, (unsigned)(BG * 2));
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
@@ -445,6 +484,21 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
     } else {
       load_xg(0);
     }
+    if constexpr (XF > 0) {  // pre-activation = recurrent part + bf16(x_t W_ih^T + b_ih + b_hh)
+      f32x16 x0, x1;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) x0[i] = x1[i] = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < XS; ++s2) {
+        x0 = mfma_bf16(__builtin_bit_cast(bf16x8_t, xa[s2]), wxa[s2], x0);
+        x1 = mfma_bf16(__builtin_bit_cast(bf16x8_t, xa[s2]), wxb[s2], x1);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        acc0[i] += round_bf(x0[i] + xba);
+        acc1[i] += round_bf(x1[i] + xbb);
+      }
+    }
     // gate exchange: wave g's [32 rows][64 units] -> pre[row][g * 64 + unit]
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -461,7 +515,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         pq[q] = *reinterpret_cast<const float4*>(pre + b * LDP + q * U + u4);
-        xf[q] = unpack_bf4(xg[k][q]);
+        xf[q] = XF > 0 ? float4{0.f, 0.f, 0.f, 0.f} : unpack_bf4(xg[k][q]);
       }
       float ao[4][4], co[4], ho[4];
       unsigned pk[2] = {0u, 0u};
@@ -527,11 +581,21 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
 
 int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whh_bf, bf16_t* gates, float* c_tm,
                            float* h_tm, bf16_t* h_bf, bf16_t* hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt,
-                           int xcd, unsigned* status, unsigned limit, int fault) {
-  constexpr int NL = 12;
-  constexpr size_t lds = (size_t)32 * (768 + 8) * 2 + (size_t)32 * (4 * 64 + 4) * 4 + (size_t)32 * 72 * 2 +
-                         (size_t)64 * 40 * 2 + (size_t)4 * NL * 1024;
-  hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4>), grid, dim3(256), lds, stream, whh_bf, gates, c_tm,
-                     h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault);
+                           int xcd, unsigned* status, unsigned limit, int fault, const bf16_t* x_bf, int F,
+                           const bf16_t* wih_bf, const float* b_ih, const float* b_hh) {
+  constexpr size_t base = (size_t)32 * (768 + 8) * 2 + (size_t)32 * (4 * 64 + 4) * 4 + (size_t)32 * 72 * 2 +
+                          (size_t)64 * 40 * 2;
+  if (x_bf) {  // layer 0, F = 40: the W_ih fragments take registers, so more W_hh fragments live in LDS
+    if (F != 40 || !wih_bf) return SV_EARG;
+    constexpr int NL = 16;
+    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 5>), grid, dim3(256), base + (size_t)4 * NL * 1024,
+                       stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
+                       fault, x_bf, wih_bf, b_ih, b_hh);
+  } else {
+    constexpr int NL = 12;
+    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0>), grid, dim3(256), base + (size_t)4 * NL * 1024,
+                       stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
+                       fault, nullptr, nullptr, nullptr, nullptr);
+  }
   return (int)hipGetLastError();
 }
