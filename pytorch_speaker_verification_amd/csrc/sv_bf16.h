@@ -327,7 +327,7 @@ int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
                            float* h_tm, bf16_t* h_bf, bf16_t* hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt,
                            int xcd, unsigned* status, unsigned limit, int fault, const bf16_t* x_bf = nullptr,
                            int F = 0, const bf16_t* wih_bf = nullptr, const float* b_ih = nullptr,
-                           const float* b_hh = nullptr);
+                           const float* b_hh = nullptr, int dbg = 0);
 // CUs of the device `stream` belongs to (cached per device); dims fit co-resident on `cus` CUs
 int sv_stream_cus(hipStream_t stream);
 int sv_persist_fwd_fits(int B, int H, int cus);

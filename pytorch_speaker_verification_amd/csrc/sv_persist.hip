@@ -969,7 +969,7 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
   if (wide) {
     const int rc = sv_persist3_fwd_launch(dim3(grid.x * grid.y), (int)grid.x, stream, whh_bf, gates, c_tm, h_tm, h_bf,
                                           hT, ldhT, T, Bp, B, H, cnt, persist_xcd(), status, limit, fault, x_bf, F,
-                                          wih_bf, b_ih, b_hh);
+                                          wih_bf, b_ih, b_hh, dbg);
     if (rc) return rc;
   } else if (wst) {
     constexpr int NS = 48, LDA = NS * 16 + 8;

@@ -329,12 +329,16 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
 // XF > 0 (layer 0, F = 8 XF <= 48 features): the input projection formed in the kernel from x_bf
 // [T,B,F] and W_ih [4H,F] (both halves' fragments in registers), rounded to bf16 with its biases as
 // the K1 path stores it -- lstm_persist2_fwd_bf16_kernel's fused form.
-template <int NS, int NL, int PA, int XF>
+// SPLIT: the second half of h_{t-1} is loaded while the first half's MFMAs run (its registers
+// stay live across them; only where the register budget allows, XF = 0)
+template <int NS, int NL, int PA, int XF, bool SPLIT = false>
 __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
     const bf16_t* __restrict__ whh_bf, bf16_t* __restrict__ gates, float* __restrict__ c_tm, float* __restrict__ h_tm,
     bf16_t* h_bf, bf16_t* __restrict__ hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd,
     unsigned* status, unsigned limit, int fault, const bf16_t* __restrict__ x_bf, const bf16_t* __restrict__ wih_bf,
-    const float* __restrict__ b_ih, const float* __restrict__ b_hh) {
+    const float* __restrict__ b_ih, const float* __restrict__ b_hh, int dbg) {
+  // dbg (SV_PERSIST_DEBUG, profiling only, results invalid): 1 no hand-off waits, 2 no recurrent
+  // MFMAs, 8 no post-arrival stores
   constexpr int BM = 32, U = 64, KR = 2;
   constexpr int K = NS * 16, LDA = K + 8;
   constexpr int LDP = 4 * U + 4;  // pre [BM][LDP] fp32
@@ -440,12 +444,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
     if (t > 0) {
-      if (tid == 0) persist_wait(my_cnt, producers * (unsigned)t, status, limit, 1u);
+      if (tid == 0 && !(dbg & 1)) persist_wait(my_cnt, producers * (unsigned)t, status, limit, 1u);
       __syncthreads();
       const __amdgpu_buffer_rsrc_t ra = sv_rsrc(h_bf + (long)t * BH, (unsigned)(BH * 2));
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        uint4 v[CH];
+      auto stage_load = [&](int half, uint4 (&v)[CH]) {
 #pragma unroll
         for (int i = 0; i < CH; ++i) {
           const int q = tid + 256 * i, row = q / (HALF / 8), c = (q % (HALF / 8)) * 8 + half * HALF;
@@ -453,33 +455,60 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
               ra, ((unsigned)(b0 + row) * (unsigned)H + (unsigned)c) * 2u, 0, 16 /* sc1 */);
           v[i] = uint4{x.x, x.y, x.z, x.w};
         }
+      };
+      auto stage_store = [&](int half, const uint4 (&v)[CH]) {
 #pragma unroll
         for (int i = 0; i < CH; ++i) {
           const int q = tid + 256 * i, row = q / (HALF / 8), c = (q % (HALF / 8)) * 8 + half * HALF;
           *reinterpret_cast<uint4*>(As + row * LDA + c) = v[i];
         }
-      }
-      __syncthreads();
-      load_xg(t);
-      __builtin_amdgcn_sched_barrier(0);
-      // A fragments PA k-steps ahead; the LDS-resident W fragments two ahead
+      };
       const bf16_t* A0 = As + r * LDA + 8 * hh;
-      bf16x8_t fa[PA], wq[2];
+      bf16x8_t wq[2];
+      // k-steps [s0, s1) from the staged A tile: A fragments PA ahead (within the range), the
+      // LDS-resident W fragments two ahead
+      auto mma_range = [&](int s0, int s1) {
+        bf16x8_t fa[PA];
 #pragma unroll
-      for (int p = 0; p < PA; ++p) fa[p] = *reinterpret_cast<const bf16x8_t*>(A0 + 16 * p);
+        for (int p = 0; p < PA; ++p) fa[p] = *reinterpret_cast<const bf16x8_t*>(A0 + 16 * (s0 + p));
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        acc0 = mfma_bf16(fa[s % PA], wa[s], acc0);
-        acc1 = mfma_bf16(fa[s % PA], s < NR ? wb[s < NR ? s : 0] : wq[s & 1], acc1);
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        if (s + PA < NS) {
-          fa[s % PA] = *reinterpret_cast<const bf16x8_t*>(A0 + 16 * (s + PA));
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        for (int s = s0; s < s1; ++s) {
+          acc0 = mfma_bf16(fa[(s - s0) % PA], wa[s], acc0);
+          acc1 = mfma_bf16(fa[(s - s0) % PA], s < NR ? wb[s < NR ? s : 0] : wq[s & 1], acc1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          if (s + PA < s1) {
+            fa[(s - s0) % PA] = *reinterpret_cast<const bf16x8_t*>(A0 + 16 * (s + PA));
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          if (s + 2 >= NR && s + 2 < NS) {
+            wq[s & 1] = wl_read(s + 2 - NR);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
         }
-        if (s + 2 >= NR && s + 2 < NS) {
-          wq[s & 1] = wl_read(s + 2 - NR);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      };
+      if constexpr (SPLIT) {
+        uint4 v0[CH], v1[CH];
+        stage_load(0, v0);
+        stage_store(0, v0);
+        stage_load(1, v1);  // in flight during the first half's MFMAs
+        __syncthreads();
+        load_xg(t);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!(dbg & 2)) mma_range(0, NS / 2);
+        stage_store(1, v1);
+        __syncthreads();
+        if (!(dbg & 2)) mma_range(NS / 2, NS);
+      } else {
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          uint4 v[CH];
+          stage_load(half, v);
+          stage_store(half, v);
         }
+        __syncthreads();
+        load_xg(t);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!(dbg & 2)) mma_range(0, NS);
       }
     } else {
       load_xg(0);
@@ -557,6 +586,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
     if (tid == 0 && persist_arrive_ok(fault, t == 0))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // off the critical chain: activations, c, h and hT of step t
+    if (dbg & 8) continue;
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       const long gb = b0 + brow + 16 * k;
@@ -582,7 +612,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
 int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whh_bf, bf16_t* gates, float* c_tm,
                            float* h_tm, bf16_t* h_bf, bf16_t* hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt,
                            int xcd, unsigned* status, unsigned limit, int fault, const bf16_t* x_bf, int F,
-                           const bf16_t* wih_bf, const float* b_ih, const float* b_hh) {
+                           const bf16_t* wih_bf, const float* b_ih, const float* b_hh, int dbg) {
   constexpr size_t base = (size_t)32 * (768 + 8) * 2 + (size_t)32 * (4 * 64 + 4) * 4 + (size_t)32 * 72 * 2 +
                           (size_t)64 * 40 * 2;
   if (x_bf) {  // layer 0, F = 40: the W_ih fragments take registers, so more W_hh fragments live in LDS
@@ -590,12 +620,25 @@ int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
     constexpr int NL = 16;
     hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 5>), grid, dim3(256), base + (size_t)4 * NL * 1024,
                        stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
-                       fault, x_bf, wih_bf, b_ih, b_hh);
+                       fault, x_bf, wih_bf, b_ih, b_hh, dbg);
   } else {
-    constexpr int NL = 12;
-    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0>), grid, dim3(256), base + (size_t)4 * NL * 1024,
-                       stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
-                       fault, nullptr, nullptr, nullptr, nullptr);
+    // SV_PFWD3_SPLIT=1: the second half of h_{t-1} loads during the first half's MFMAs (measured
+    // no faster: c3 forward 4.77 vs 4.67 ms, step 11.46 vs 11.47 ms -- kept off)
+    static const int split = [] {
+      const char* e = getenv("SV_PFWD3_SPLIT");
+      return (e && *e == '1') ? 1 : 0;
+    }();
+    if (split) {
+      constexpr int NL = 16;
+      hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0, true>), grid, dim3(256),
+                         base + (size_t)4 * NL * 1024, stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H,
+                         cnt, nub, xcd, status, limit, fault, nullptr, nullptr, nullptr, nullptr, dbg);
+    } else {
+      constexpr int NL = 12;
+      hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0>), grid, dim3(256), base + (size_t)4 * NL * 1024,
+                         stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
+                         fault, nullptr, nullptr, nullptr, nullptr, dbg);
+    }
   }
   return (int)hipGetLastError();
 }
