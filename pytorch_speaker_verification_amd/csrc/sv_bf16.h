@@ -247,18 +247,29 @@ __device__ __forceinline__ float4 unpack_bf4(uint2 p) {
                 __uint_as_float(p.y & 0xffff0000u)};
 }
 
+// Activations of the mixed-precision (bf16) path: v_exp_f32 + v_rcp_f32 forms (about 5 VALU
+// instructions each instead of the accurate library tanh / division sequences, which made the
+// cell update of the persistent recurrences VALU-bound: 144 -> ~40 instructions per element).
+// Absolute error a few fp32 ulps of 1 (tanh near 0 included: 2 s(2x) - 1 cancels to an absolute,
+// not relative, error), far below the bf16 rounding of the stored activations; the fp32 path
+// keeps the accurate functions.
+__device__ __forceinline__ float bf_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float bf_tanh(float x) {
+  return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f;
+}
+
 // LSTM cell forward of one element, shared by the bf16 step, wavefront and persistent kernels
 // (contraction off, so every schedule rounds identically): pre-activations (recurrent part p +
 // input part x) -> activated gates a[4] = i f g o, returns c_t, sets h_t
 __device__ __forceinline__ float lstm_cell_fwd(const float (&p)[4], const float (&x)[4], float c_prev, float (&a)[4],
                                                float& h) {
 #pragma clang fp contract(off)
-  a[0] = sv_sigmoid(p[0] + x[0]);
-  a[1] = sv_sigmoid(p[1] + x[1]);
-  a[2] = tanhf(p[2] + x[2]);
-  a[3] = sv_sigmoid(p[3] + x[3]);
+  a[0] = bf_sigmoid(p[0] + x[0]);
+  a[1] = bf_sigmoid(p[1] + x[1]);
+  a[2] = bf_tanh(p[2] + x[2]);
+  a[3] = bf_sigmoid(p[3] + x[3]);
   const float c = a[1] * c_prev + a[0] * a[2];
-  h = a[3] * tanhf(c);
+  h = a[3] * bf_tanh(c);
   return c;
 }
 
@@ -269,7 +280,7 @@ __device__ __forceinline__ float lstm_cell_fwd(const float (&p)[4], const float 
 __device__ __forceinline__ float lstm_cell_bwd(float dh, float i, float f, float g, float o, float c, float cp,
                                                float dcf_in, float (&d)[4]) {
 #pragma clang fp contract(off)
-  const float tc = tanhf(c);
+  const float tc = bf_tanh(c);
   const float dc = dh * o * (1.f - tc * tc) + dcf_in;
   d[0] = dc * g * i * (1.f - i);
   d[1] = dc * cp * f * (1.f - f);
