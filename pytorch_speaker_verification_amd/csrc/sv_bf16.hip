@@ -727,8 +727,8 @@ extern "C" int sv_gemm_bf16_bf(int M, int N, int K, const bf16_t* A, long lda, c
   if (M <= 0 || N <= 0 || K <= 0 || !A || !B || !C) return SV_EARG;
   if (K % 8 || lda % 8 || ldb % 8 || (((uintptr_t)A | (uintptr_t)B) & 15)) return SV_EALIGN;
   const BPlan p = plan_bf16(M, N, K);
-  if (p.bm == G256_BM && p.splitk == 1 && g256_variant(nullptr, 0, bias0, bias1) == 2 && ldc % 4 == 0 &&
-      !((uintptr_t)C & 7)) {
+  if (p.bm == G256_BM && p.splitk == 1 && g256_variant(nullptr, 0, bias0, bias1) == 2 && ldc % 8 == 0 &&
+      !((uintptr_t)C & 15)) {
     const int tiles = (M / G256_BM) * (N / G256_BM);
     launch_g8<G8_STORE_BF16, 0>(dim3(tiles, 1), stream, A, lda, B, ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1,
                                 0.f);

@@ -522,6 +522,39 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8p_kernel(const bf16_t* __re
 // vmcnt(5) -- A1 / A3 of kt landed (younger: A2(kt+1) and the four B fills of kt+1), so the
 // m-half-1 fragments read in p2 are ordered by the barrier that ends the p1 read slot.  Near the
 // end of K, where fewer younger ops exist, the waits fall back to vmcnt(0).
+// bf16 C through LDS: each wave's 128 x 64 tile (16 KB; the 128 KB of stages are free after the
+// k-loop) is written as 8-B fragments, then stored as whole 128-B row pieces with one 16-B store
+// per lane (16 store instructions per wave instead of 32 scattered 8-B ones: the store tail of a
+// 256 x 256 tile is issue-bound, MI355X_MICROARCH.md "attention epilogue store tail")
+__device__ __forceinline__ void g8_epilogue_bf16_lds(g8_f32x4 (&acc)[8][4], bf16_t* C, long ldc, int tm, int tn,
+                                                     int wr, int wc, int w, int lane, const float* bias0,
+                                                     const float* bias1, char* smem) {
+  const int fr = lane & 15, fq = lane >> 4;
+  char* tile = smem + w * 16384;  // [128 rows][128 B]
+  __syncthreads();                // every wave's last stage reads retired
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int col = tn * G256_BM + wc * 64 + 16 * nt + 4 * fq;
+    g8_f32x4 badd = {0.f, 0.f, 0.f, 0.f};
+    if (bias0) badd += *reinterpret_cast<const g8_f32x4*>(bias0 + col);
+    if (bias1) badd += *reinterpret_cast<const g8_f32x4*>(bias1 + col);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const g8_f32x4 v = acc[mt][nt] + badd;
+      const unsigned lo = (unsigned)to_bf(v[0]) | ((unsigned)to_bf(v[1]) << 16);
+      const unsigned hi = (unsigned)to_bf(v[2]) | ((unsigned)to_bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(tile + (16 * mt + fr) * 128 + (16 * nt + 4 * fq) * 2) = uint2{lo, hi};
+    }
+  }
+  // same wave reads back: LDS is ordered within a wave (the compiler waits lgkmcnt)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = 8 * i + (lane >> 3), c = lane & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(tile + row * 128 + c * 16);
+    *reinterpret_cast<uint4*>(C + ((long)tm * G256_BM + wr * 128 + row) * ldc + tn * G256_BM + wc * 64 + 8 * c) = v;
+  }
+}
+
 template <int EPI, int AF = 0>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __restrict__ A, long lda,
                                                              const bf16_t* __restrict__ B, long ldb, void* __restrict__ C,
@@ -686,5 +719,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   }
-  g8_epilogue<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
+  if constexpr (EPI == G8_STORE_BF16)
+    g8_epilogue_bf16_lds(acc, reinterpret_cast<bf16_t*>(C), ldc, tm, tn, wr, wc, w, lane, bias0, bias1, smem);
+  else
+    g8_epilogue<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
 }
