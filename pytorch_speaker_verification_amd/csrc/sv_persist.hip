@@ -760,31 +760,34 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     mark(3);
-    // step t-1's elementwise operands, in flight during the stores below and the next hand-off
-    // wait (dbg & 16, profiling only: skipped)
-    if (t > 0 && !(dbg & 16)) load_ew(t - 1);
-    if (dbg & 8) continue;
     // dG_t row-major (BM rows x 4 gates x 4 chunks of 8 units) and transposed (128 gate-unit
     // rows x BM/8 chunks of 8 batch columns; padding columns get zeros): 16-B plain stores
-    bf16_t* dgt = dg ? dg + (long)t * BG : nullptr;  // NULL: the dx GEMM reads dgf itself
-#pragma unroll
-    for (int i = 0; i < BM / 16; ++i) {
-      const int q = tid + 256 * i, row = q >> 4, gq = (q >> 2) & 3, c = q & 3;
-      const int gb = b0 + row, gj = j0 + 8 * c;
-      if (dgt && gb < B && gj < H)
-        *reinterpret_cast<uint4*>(dgt + (long)gb * G + (long)gq * H + gj) =
-            *reinterpret_cast<const uint4*>(dgs + row * LDG + gq * BF_U + 8 * c);
-    }
-    if (dgT) {
+    // (dbg & 8, profiling only: skipped).  Before the operand DMA below: LDS reads issued behind
+    // an LDS-DMA wait for it to land (the compiler puts vmcnt(0) before them)
+    if (!(dbg & 8)) {
+      bf16_t* dgt = dg ? dg + (long)t * BG : nullptr;  // NULL: the dx GEMM reads dgf itself
 #pragma unroll
       for (int i = 0; i < BM / 16; ++i) {
-        const int q = tid + 256 * i, gu = q / (BM / 8), c = q % (BM / 8);
-        const int gq = gu / BF_U, gj = j0 + gu % BF_U, gb = b0 + 8 * c;
-        if (gb < Bp && gj < H)
-          *reinterpret_cast<uint4*>(dgT + ((long)gq * H + gj) * lddgT + (long)t * Bp + gb) =
-              *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
+        const int q = tid + 256 * i, row = q >> 4, gq = (q >> 2) & 3, c = q & 3;
+        const int gb = b0 + row, gj = j0 + 8 * c;
+        if (dgt && gb < B && gj < H)
+          *reinterpret_cast<uint4*>(dgt + (long)gb * G + (long)gq * H + gj) =
+              *reinterpret_cast<const uint4*>(dgs + row * LDG + gq * BF_U + 8 * c);
+      }
+      if (dgT) {
+#pragma unroll
+        for (int i = 0; i < BM / 16; ++i) {
+          const int q = tid + 256 * i, gu = q / (BM / 8), c = q % (BM / 8);
+          const int gq = gu / BF_U, gj = j0 + gu % BF_U, gb = b0 + 8 * c;
+          if (gb < Bp && gj < H)
+            *reinterpret_cast<uint4*>(dgT + ((long)gq * H + gj) * lddgT + (long)t * Bp + gb) =
+                *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
+        }
       }
     }
+    // step t-1's elementwise operands, in flight during the next hand-off wait (dbg & 16,
+    // profiling only: skipped)
+    if (t > 0 && !(dbg & 16)) load_ew(t - 1);
     mark(4);
   }
   if (stamp && tid == 0 && blockIdx.x < SV_NSTAMP_WG)

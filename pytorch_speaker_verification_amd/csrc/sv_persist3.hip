@@ -266,11 +266,13 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     mark(3);
     if (!DEFER || t == 0) {  // DEFER: all but the last step's leftovers go into the next k-loop
-      // (dbg, profiling only: 64 skips the operand DMA, 128 the dG / dG^T stores)
-      if (!DEFER && t > 0 && !(dbg & 64)) load_ew(t - 1);
+      // (dbg, profiling only: 64 skips the operand DMA, 128 the dG / dG^T stores).  The stores
+      // first: their LDS reads issued behind an LDS-DMA would wait for it to land (the compiler
+      // cannot tell the DMA's LDS range from the tiles', so it puts vmcnt(0) before every read)
       if (!(dbg & 8) && !(dbg & 128))
 #pragma unroll
         for (int i = 0; i < 8; ++i) store_piece(t, i);
+      if (!DEFER && t > 0 && !(dbg & 64)) load_ew(t - 1);
     }
     mark(4);
   }
