@@ -161,7 +161,11 @@ def probe_ms(probes, key):
     tot = 0.0
     for p in probes:
         ev = p[key]
-        tot += sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(len(ev) // 2))
+        for i in range(len(ev) // 2):
+            try:   # a schedule that runs all layers in one launch records only the first pair
+                tot += ev[2 * i].elapsed_time(ev[2 * i + 1])
+            except RuntimeError:
+                pass
     return tot / max(1, len(probes))
 
 

@@ -353,3 +353,29 @@ int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, cons
                      bf16_t* const* gates, float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
                      bf16_t* const* hT, unsigned* sync, hipStream_t stream, unsigned limit, int fault, hipEvent_t pre,
                      hipEvent_t post);
+// layer-wavefront backward (sv_persist3.hip / sv_persist.hip): all L = 3 layers' recurrences and
+// their upstream gradients dx in one launch, for the small per-GPU batches (B <= 80 at H = 768)
+constexpr int WB_L = 3;
+struct WaveBwdArgs {
+  const bf16_t* whhT[WB_L];  // [H][4H] bf16 (W_hh^T)
+  const bf16_t* wihT[WB_L];  // [H][4H] bf16 (W_ih^T; layers >= 1)
+  const bf16_t* acts[WB_L];  // [T][B][4H] bf16
+  const float* c[WB_L];      // [T][B][H]
+  float* dx[WB_L];           // [T][B][H] (layers >= 1): this layer's dx = layer l-1's dh_up
+  bf16_t* dgf[WB_L];         // fragment-order dG hand-off, [T][nrb][4][32 rows][H] bf16
+  bf16_t* dgT[WB_L];         // [4H][T Bp]
+  float* dbp[WB_L];          // [nrb][4H] bias partials or NULL
+  unsigned* cnt[WB_L];
+  const float* dh_last;      // [B][H]: the top layer's dh_up at t = T-1
+  unsigned* status;
+  unsigned limit;
+  long lddgT;
+  int T, Bp, B, H, nub, nrb, fault;
+};
+int sv_wave_bwd_launch(const WaveBwdArgs& a, hipStream_t stream);
+int sv_wave_bwd_fits(int L, int B, int H, int cus);
+size_t sv_wave_bwd_scratch(int L, int T, int B, int H);
+int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, const bf16_t* const* wihT,
+                     const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
+                     bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
+                     float* const* db_hh, hipEvent_t pre, hipEvent_t post);

@@ -1039,7 +1039,9 @@ BBwdWs carve_bbwd(char* base, int T, int B, int F, int H) {
 // whose recurrences run one after another)
 extern "C" size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H) {
   const size_t per = (size_t)L * carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
-  return per + (sv_persist_bwd_fits(B, H, 1 << 30) ? sv_persist_bwd_scratch(T, B, H) : 0);
+  size_t scratch = sv_persist_bwd_fits(B, H, 1 << 30) ? sv_persist_bwd_scratch(T, B, H) : 0;
+  if (sv_wave_bwd_fits(L, B, H, 1 << 30)) scratch = std::max(scratch, sv_wave_bwd_scratch(L, T, B, H));
+  return per + scratch;
 }
 
 extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const bf16_t* const* xT, const long* ld_xT,
@@ -1063,6 +1065,51 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
   hipEvent_t ev_start = ev[L * nch + L];
   hipError_t e = hipEventRecord(ev_start, main);
   if (e != hipSuccess) return (int)e;
+  if (persist_bwd(H) && sv_wave_bwd_fits(L, B, H, sv_stream_cus(main))) {
+    if (!sync) return SV_EARG;
+    // layer-wavefront schedule: every layer's recurrence and upstream gradient dx in one launch
+    // (sv_persist3.hip, no dx GEMMs), then per layer the weight gradients on its weight-gradient
+    // stream (SV_PBWD_DW_SIDE=0: on `main`)
+    const bf16_t* whhT_l[WB_L];
+    const bf16_t* wihT_l[WB_L];
+    for (int l = 0; l < L; ++l) {
+      const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
+      int rc = sv_transpose_cast_bf16(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, main);
+      if (rc) return rc;
+      if (l > 0 && (rc = sv_transpose_cast_bf16(w_ih[l], H, 4 * H, H, ws.wihT, 4L * H, main))) return rc;
+      whhT_l[l] = ws.whhT;
+      wihT_l[l] = l > 0 ? ws.wihT : nullptr;
+    }
+    const bool dbk = pbwd_db();
+    int rc = sv_wave_bwd_bf16(L, T, B, H, whhT_l, wihT_l, gates, c_tm, dh_last, dx, dgT, (char*)workspace + per * L,
+                              sync, main, dbk ? db_ih : nullptr, dbk ? db_hh : nullptr, probe ? probe[0] : nullptr,
+                              probe ? probe[1] : nullptr);
+    if (rc) return rc;
+    if ((e = hipEventRecord(ev[0], main)) != hipSuccess) return (int)e;
+    for (int l = L - 1; l >= 0; --l) {
+      const int Fl = l == 0 ? F : H;
+      const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
+      hipStream_t sw = pbwd_dw_side() ? side[L + l] : main;
+      if (sw != main && (e = hipStreamWaitEvent(sw, ev[0], 0)) != hipSuccess) return (int)e;
+      float* gw = sw != main ? ws.gws2 : ws.gws;
+      if ((rc = sv_gemm_bf16(4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, gw, sw)))
+        return rc;
+      if ((rc = sv_gemm_bf16(4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, gw, sw)))
+        return rc;
+      if (!dbk) {
+        hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
+                           db_hh ? db_hh[l] : nullptr);
+        SV_LAUNCH_CHECK();
+      }
+      if (sw != main) {
+        if ((e = hipEventRecord(ev[L * nch + l], sw)) != hipSuccess) return (int)e;
+        if ((e = hipStreamWaitEvent(main, ev[L * nch + l], 0)) != hipSuccess) return (int)e;
+      }
+    }
+    for (int l = 0; l < L; ++l)
+      if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
+    return SV_OK;
+  }
   if (persist_bwd(H) && sv_persist_bwd_fits(B, H, sv_stream_cus(main))) {
     if (!sync) return SV_EARG;
     // persistent schedule: per layer (top first) the whole-T recurrence in one launch

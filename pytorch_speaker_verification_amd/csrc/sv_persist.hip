@@ -1132,6 +1132,80 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
   return SV_OK;
 }
 
+// ---- layer-wavefront backward (lstm_wave_bwd_bf16_kernel, sv_persist3.hip) ----
+// L = 3, H = 768 and all L x (H/32) x (B/32) workgroups co-resident (c4's 80 rows per rank: 216
+// of 256 CUs).  SV_WAVE_BWD=0 keeps the per-layer schedule.
+int sv_wave_bwd_fits(int L, int B, int H, int cus) {
+  static int on = [] {
+    const char* e = getenv("SV_WAVE_BWD");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  const int nrb = (B + 31) / 32;
+  return on && L == WB_L && H == 768 && nrb <= SV_PCNT_ROWS && (long)L * (H / 32) * nrb <= cus &&
+         (long)(B + 64) * 4 * H * 2 < (1L << 31);
+}
+namespace {
+size_t wave_frag_bytes(int T, int B, int H) {
+  return ((size_t)T * ((B + 31) / 32) * 32 * 4 * H * sizeof(bf16_t) + 255) & ~size_t(255);
+}
+size_t wave_dbp_bytes(int B, int H) { return ((size_t)((B + 31) / 32) * 4 * H * sizeof(float) + 255) & ~size_t(255); }
+}  // namespace
+// per layer: the fragment-order dG hand-off ([T][nrb][4][32][H] bf16) and the bias partials
+size_t sv_wave_bwd_scratch(int L, int T, int B, int H) {
+  return (size_t)L * (wave_frag_bytes(T, B, H) + wave_dbp_bytes(B, H));
+}
+// dx[l] (l >= 1): layer l's upstream gradient for layer l-1, [T][B][H] fp32 (written whole);
+// dgT[l]: [4H][T*Bp] (padding columns written as zeros); db_ih NULL: bias gradients not computed.
+// Counter channels 0..L-1 of `sync`.
+int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, const bf16_t* const* wihT,
+                     const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
+                     bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
+                     float* const* db_hh, hipEvent_t pre, hipEvent_t post) {
+  if (!sv_wave_bwd_fits(L, B, H, sv_stream_cus(stream))) return SV_ESHAPE;
+  if (!scratch || ((uintptr_t)scratch & 15) || !sync || !dh_last || !whhT || !wihT || !acts || !c_tm || !dx || !dgT)
+    return SV_EARG;
+  WaveBwdArgs a{};
+  a.nub = H / 32;
+  a.nrb = (B + 31) / 32;
+  char* p = static_cast<char*>(scratch);
+  for (int l = 0; l < L; ++l) {
+    if (!whhT[l] || !acts[l] || !c_tm[l] || !dgT[l] || (l > 0 && (!wihT[l] || !dx[l]))) return SV_EARG;
+    a.whhT[l] = whhT[l];
+    a.wihT[l] = l > 0 ? wihT[l] : nullptr;
+    a.acts[l] = acts[l];
+    a.c[l] = c_tm[l];
+    a.dx[l] = l > 0 ? dx[l] : nullptr;
+    a.dgT[l] = dgT[l];
+    a.dgf[l] = reinterpret_cast<bf16_t*>(p);
+    p += wave_frag_bytes(T, B, H);
+    a.dbp[l] = db_ih ? reinterpret_cast<float*>(p) : nullptr;
+    p += wave_dbp_bytes(B, H);
+    a.cnt[l] = sync_cnt(sync, l);
+    hipError_t e = hipMemsetAsync(a.cnt[l], 0, (size_t)a.nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  a.dh_last = dh_last;
+  a.status = sync;
+  a.limit = persist_limit();
+  a.fault = persist_fault() != 0;
+  a.T = T;
+  a.B = B;
+  a.Bp = (B + 7) & ~7;
+  a.H = H;
+  a.lddgT = (long)T * a.Bp;
+  hipError_t e;
+  if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
+  sv_wave_bwd_launch(a, stream);
+  SV_LAUNCH_CHECK();
+  if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
+  for (int l = 0; l < L && db_ih; ++l) {
+    hipLaunchKernelGGL(persist_db_finalize_kernel, dim3((4 * H + 255) / 256), dim3(256), 0, stream, a.dbp[l], a.nrb,
+                       4 * H, db_ih[l], db_hh ? db_hh[l] : nullptr);
+    SV_LAUNCH_CHECK();
+  }
+  return SV_OK;
+}
+
 // (status guard) loss := NaN when the sync block's status is set: a training step whose
 // recurrences timed out reports a NaN loss instead of a finite wrong one
 __global__ void status_poison_kernel(const unsigned* __restrict__ status, float* __restrict__ x, int n) {

@@ -645,3 +645,284 @@ int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
   }
   return (int)hipGetLastError();
 }
+
+// ============================================================================
+// Layer-wavefront backward for small per-GPU batches (c4's 80 rows per rank): ONE launch runs the
+// backward recurrences of all L layers.  The per-layer schedule at B = 80 runs 72 workgroups per
+// layer, one layer after another, each followed by its dx = dG W_ih GEMM; here workgroup (l, ub,
+// rb) -- 32 rows x 32 units, 4 waves, one per gate -- holds BOTH of its gate's weight slices, W_hh^T
+// (for dh_rec = dG_{t+1} W_hh) and W_ih^T (for layer l-1's upstream gradient dx_{t+1} =
+// dG_{t+1} W_ih), and streams dG_{t+1} once for both: two accumulators per A fragment (the wide
+// backward's register plan: 256 AGPRs + VGPRs + NL LDS-resident fragments).  Layer l's iteration t
+// computes dh_rec_t and dx_{t+1}, hands dx_{t+1} (fp32, 16-B sc1 stores) to layer l-1 with its dG_t,
+// and consumes dx_t from layer l+1's iteration t-1 as dh_up: so layer l runs two iterations behind
+// layer l+1, and the chain is T + 2(L-1) + 1 dependent steps (layers >= 1 run one extra iteration,
+// t = -1, that only forms dx_0).  One counter per (layer, row block) counts finished iterations;
+// both hand-offs of an iteration are drained before its arrival (hand-off table row 1).
+//   own layer:   iteration t needs dG_{t+1}  -> counter >= nub (T - 1 - t)
+//   layer above: iteration t needs dx_t      -> its counter >= nub (T - t + 1)
+// Outputs as the per-layer schedule (dG^T per layer, bias partials, the dx buffers), except the
+// in-kernel dx sums the gates' k-ordered partials in gate order (the dx GEMM sums K = 4H in
+// k-tile order): bf16-level agreement, not bitwise.
+// ============================================================================
+template <int NS, int P, int NL>
+__global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBwdArgs a) {
+  constexpr int BM = 32, U = 32;
+  constexpr int LDR = U + 4;         // red0 / red1 [4][BM][LDR] fp32
+  constexpr int LDG = 4 * U + 8;     // dgs [BM][LDG] bf16
+  constexpr int LDT = BM + 8;        // gts [4U][LDT] bf16
+  constexpr int FRAG = NS * 64 * 8;  // dgf elements of one (row block, gate)
+  constexpr int NR = NS - NL;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red0 = reinterpret_cast<float*>(smem);
+  float* red1 = red0 + 4 * BM * LDR;
+  bf16_t* dgs = reinterpret_cast<bf16_t*>(red1 + 4 * BM * LDR);
+  bf16_t* gts = dgs + BM * LDG;
+  char* ewa = reinterpret_cast<char*>(gts + 4 * U * LDT);  // [BM][256 B]: gate q's 64 B at ((q + row) & 3) * 64
+  float* ewc = reinterpret_cast<float*>(ewa + BM * 256);    // [BM][U] c_{t-1}
+  char* wl = reinterpret_cast<char*>(ewc + BM * U);         // [4 waves][NL][64 lanes][16 B]
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int T = a.T, B = a.B, H = a.H, nub = a.nub, nrb = a.nrb;
+  int ub, rb, l;
+  {
+    const int i = blockIdx.x, n = gridDim.x;
+    const int x = i & 7, q = n >> 3, rr = n & 7;
+    const int Lg = x * q + min(x, rr) + (i >> 3);
+    ub = Lg % nub;
+    rb = (Lg / nub) % nrb;
+    l = Lg / (nub * nrb);
+  }
+  const int j0 = ub * U, b0 = rb * BM;
+  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
+  const long FS = (long)nrb * BM * G;
+  const bool has_dx = l > 0, has_up = l < WB_L - 1;
+  unsigned* my_cnt = a.cnt[l] + rb * SV_PCNT_STRIDE;
+  unsigned* up_cnt = has_up ? a.cnt[l + 1] + rb * SV_PCNT_STRIDE : nullptr;
+  const unsigned producers = nub;
+  // gate g's fragments: W_hh^T (wa) and W_ih^T (wb, layers >= 1): B[k][n] = W[g H + k][j0 + n]
+  bf16x8_t wa[NS], wb[NR];
+  {
+    const bf16_t* ra = a.whhT[l] + (long)(j0 + r) * G + (long)g * H + 8 * hh;
+    const bf16_t* rbp = has_dx ? a.wihT[l] + (long)(j0 + r) * G + (long)g * H + 8 * hh : ra;
+    const bool ok = j0 + r < H;
+    const bf16x8_t z = {};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) wa[s] = ok ? *reinterpret_cast<const bf16x8_t*>(ra + 16 * s) : z;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) wb[s] = (ok && has_dx) ? *reinterpret_cast<const bf16x8_t*>(rbp + 16 * s) : z;
+#pragma unroll
+    for (int s = NR; s < NS; ++s)
+      *reinterpret_cast<bf16x8_t*>(wl + ((g * NL + s - NR) * 64 + lane) * 16) =
+          (ok && has_dx) ? *reinterpret_cast<const bf16x8_t*>(rbp + 16 * s) : z;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) asm volatile("" : "+a"(wa[s]));
+#pragma unroll
+    for (int s = 0; s < 64 - NS; ++s) asm volatile("" : "+a"(wb[s]));
+  }
+  auto wl_read = [&](int j) { return *reinterpret_cast<const bf16x8_t*>(wl + ((g * NL + j) * 64 + lane) * 16); };
+  // elementwise map: thread -> 4 consecutive units (u4) of row brow
+  const int u4 = (tid & 7) * 4, brow = tid >> 3;
+  const long gb = b0 + brow, Bv = B;
+  const long gbv = gb < Bv ? gb : Bv + 64;  // rows past B: offsets past every range
+  float4 cv;
+  float dcf[4] = {0.f, 0.f, 0.f, 0.f};
+  float dbs[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) dbs[q][v] = 0.f;
+  // step tt's activations and c_{tt-1} into LDS (LDS-DMA; not hand-off data)
+  auto load_ew = [&](int tt) {
+    const __amdgpu_buffer_rsrc_t ra_ = sv_rsrc(a.acts[l] + (long)tt * BG, (unsigned)(BG * 2));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int p = (g * 2 + j) * 64 + lane, row = p >> 4, sl = p & 15;
+      const int q = ((sl >> 2) - row) & 3, c = sl & 3;
+      const long rg = b0 + row, rgv = rg < Bv ? rg : Bv + 64;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_, (lds_ptr_t)(ewa + (g * 2 + j) * 1024), 16,
+                                               (unsigned)((rgv * G + q * H + j0 + 8 * c) * 2), 0, 0, 0);
+    }
+    const __amdgpu_buffer_rsrc_t rc_ =
+        sv_rsrc(a.c[l] + (long)(tt > 0 ? tt - 1 : 0) * BH, tt > 0 ? (unsigned)(BH * 4) : 0u);
+    {
+      const int p = g * 64 + lane, row = p >> 3, c = p & 7;
+      const long rg = b0 + row, rgv = rg < Bv ? rg : Bv + 64;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rc_, (lds_ptr_t)((char*)ewc + g * 1024), 16,
+                                               (unsigned)((rgv * H + j0 + 4 * c) * 4), 0, 0, 0);
+    }
+  };
+  {
+    const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(a.c[l] + (long)(T - 1) * BH, (unsigned)(BH * 4));
+    const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(rc_, (unsigned)((gbv * H + j0 + u4) * 4), 0, 0);
+    cv = float4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
+  }
+  load_ew(T - 1);
+  const int t_end = has_dx ? -1 : 0;
+  for (int t = T - 1; t >= t_end; --t) {
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+    if (tid == 0) {
+      if (t < T - 1) persist_wait(my_cnt, producers * (unsigned)(T - 1 - t), a.status, a.limit, 2u);
+      if (has_up && t >= 0) persist_wait(up_cnt, producers * (unsigned)(T - t + 1), a.status, a.limit, 2u);
+    }
+    __syncthreads();
+    if (t < T - 1) {
+      // A fragments of dG_{t+1} (this layer's hand-off slot): k-step s at (rb 4 + g) FRAG + s 512
+      const __amdgpu_buffer_rsrc_t ra = sv_rsrc(a.dgf[l] + (long)(t + 1) * FS, (unsigned)(FS * 2));
+      constexpr unsigned kstep = 1024u;
+      const unsigned base0 = ((unsigned)(rb * 4 + g) * (unsigned)FRAG + (unsigned)lane * 8u) * 2u;
+      u32x4_t fa[P];
+#pragma unroll
+      for (int s = 0; s < P; ++s) fa[s] = __builtin_amdgcn_raw_buffer_load_b128(ra, base0 + kstep * s, 0, 16 /* sc1 */);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8_t wq[2];
+      if (has_dx) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const bf16x8_t av = __builtin_bit_cast(bf16x8_t, fa[s % P]);
+          acc0 = mfma_bf16(av, wa[s], acc0);  // unused at t = -1
+          acc1 = mfma_bf16(av, s < NR ? wb[s < NR ? s : 0] : wq[s & 1], acc1);
+          if (s + 2 >= NR && s + 2 < NS) wq[s & 1] = wl_read(s + 2 - NR);
+          if (s + P < NS) fa[s % P] = __builtin_amdgcn_raw_buffer_load_b128(ra, base0 + kstep * (s + P), 0, 16);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          acc0 = mfma_bf16(__builtin_bit_cast(bf16x8_t, fa[s % P]), wa[s], acc0);
+          if (s + P < NS) fa[s % P] = __builtin_amdgcn_raw_buffer_load_b128(ra, base0 + kstep * (s + P), 0, 16);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    // per-gate partials: red0 = dh_rec, red1 = dx
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      red0[(g * BM + acc_row(i, lane)) * LDR + r] = acc0[i];
+      red1[(g * BM + acc_row(i, lane)) * LDR + r] = acc1[i];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
+    __syncthreads();
+    // dh_up_t (hand-off from the layer above, sc1 loads) or the top layer's dh_last
+    float4 upv = float4{0.f, 0.f, 0.f, 0.f};
+    if (t >= 0) {
+      const float* up = has_up ? a.dx[l + 1] + (long)t * BH : (t == T - 1 ? a.dh_last : nullptr);
+      if (up) {
+        const __amdgpu_buffer_rsrc_t ru = sv_rsrc(up, (unsigned)(BH * 4));
+        const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(ru, (unsigned)((gbv * H + j0 + u4) * 4), 0,
+                                                                16 /* sc1: hand-off */);
+        upv = float4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
+      }
+    }
+    // dx_{t+1} of this layer: gate partials summed in gate order, 16-B sc1 stores (hand-off)
+    if (has_dx && t < T - 1) {
+      const int b = brow;
+      const float4 p0 = *reinterpret_cast<const float4*>(red1 + (0 * BM + b) * LDR + u4);
+      const float4 p1 = *reinterpret_cast<const float4*>(red1 + (1 * BM + b) * LDR + u4);
+      const float4 p2 = *reinterpret_cast<const float4*>(red1 + (2 * BM + b) * LDR + u4);
+      const float4 p3 = *reinterpret_cast<const float4*>(red1 + (3 * BM + b) * LDR + u4);
+      float dxv[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float s_ = p0[v];
+        s_ += p1[v];
+        s_ += p2[v];
+        s_ += p3[v];
+        dxv[v] = s_;
+      }
+      const __amdgpu_buffer_rsrc_t rw = sv_rsrc(a.dx[l] + (long)(t + 1) * BH, (unsigned)(BH * 4));
+      if (gb < Bv && j0 + u4 < H)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4_t{__float_as_uint(dxv[0]), __float_as_uint(dxv[1]), __float_as_uint(dxv[2]), __float_as_uint(dxv[3])},
+            rw, (unsigned)((gb * H + j0 + u4) * 4), 0, 16 /* sc1 */);
+    }
+    if (t >= 0) {  // the cell backward of step t
+      const int b = brow;
+      const float4 r0 = *reinterpret_cast<const float4*>(red0 + (0 * BM + b) * LDR + u4);
+      const float4 r1 = *reinterpret_cast<const float4*>(red0 + (1 * BM + b) * LDR + u4);
+      const float4 r2 = *reinterpret_cast<const float4*>(red0 + (2 * BM + b) * LDR + u4);
+      const float4 r3 = *reinterpret_cast<const float4*>(red0 + (3 * BM + b) * LDR + u4);
+      const float4 cpv = *reinterpret_cast<const float4*>(ewc + b * U + u4);
+      float4 f[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        f[q] = unpack_bf4(*reinterpret_cast<const uint2*>(ewa + b * 256 + ((q + b) & 3) * 64 + (u4 >> 3) * 16 +
+                                                          (u4 & 7) * 2));
+      unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float dh = r0[v];
+        dh += r1[v];
+        dh += r2[v];
+        dh += r3[v];
+        dh += upv[v];
+        float dd[4];
+        dcf[v] = lstm_cell_bwd(dh, f[0][v], f[1][v], f[2][v], f[3][v], cv[v], cpv[v], dcf[v], dd);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bf16_t e = to_bf(dd[q]);
+          gts[(q * U + u4 + v) * LDT + b] = e;
+          pk[q][v >> 1] |= (unsigned)e << (16 * (v & 1));
+          dbs[q][v] += __uint_as_float((unsigned)e << 16);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(dgs + b * LDG + q * U + u4) = uint2{pk[q][0], pk[q][1]};
+      cv = cpv;
+    }
+    __syncthreads();
+    // the dG_t hand-off: 8 KB per workgroup in fragment order (gate, 2 k-steps), 16-B sc1 stores
+    if (t >= 0) {
+      const __amdgpu_buffer_rsrc_t rw = sv_rsrc(a.dgf[l] + (long)t * FS, (unsigned)(FS * 2));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int p = tid + 256 * i, c = p >> 6, ln = p & 63;
+        const int gq = c >> 1, sl = c & 1;
+        const uint4 v = *reinterpret_cast<const uint4*>(dgs + (ln & 31) * LDG + gq * U + 16 * sl + 8 * (ln >> 5));
+        const unsigned off =
+            ((unsigned)(rb * 4 + gq) * (unsigned)FRAG + (unsigned)(2 * ub + sl) * 512u + (unsigned)ln * 8u) * 2u;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0 && persist_arrive_ok(a.fault, t == T - 1))
+      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t >= 0 && a.dgT[l]) {  // dG_t^T (the dW GEMMs' operand), then the next step's operands
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int q = tid + 256 * i, gu = q >> 2, c = q & 3;
+        const int gq = gu / U, gj = j0 + gu % U, gc = b0 + 8 * c;
+        if (gc < a.Bp && gj < H)
+          *reinterpret_cast<uint4*>(a.dgT[l] + ((long)gq * H + gj) * a.lddgT + (long)t * a.Bp + gc) =
+              *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
+      }
+    }
+    if (t > 0) load_ew(t - 1);
+  }
+  // bias gradients: this tile's column sums over its rows (in order), one partial per row block
+  if (a.dbp[l]) {
+    __syncthreads();
+    float* dsum = red0;  // [BM][4U] fp32
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(dsum + brow * (4 * U) + q * U + u4) = float4{dbs[q][0], dbs[q][1], dbs[q][2], dbs[q][3]};
+    __syncthreads();
+    if (tid < 4 * U) {
+      const int q = tid / U, gj = j0 + tid % U;
+      float sum = 0.f;
+      for (int b = 0; b < BM; ++b) sum += dsum[b * (4 * U) + tid];
+      if (gj < H) a.dbp[l][(long)rb * G + (long)q * H + gj] = sum;
+    }
+  }
+}
+
+int sv_wave_bwd_launch(const WaveBwdArgs& a, hipStream_t stream) {
+  constexpr int NL = 12;
+  constexpr size_t lds = (size_t)2 * 4 * 32 * 36 * 4 + (size_t)32 * 136 * 2 + (size_t)128 * 40 * 2 + (size_t)32 * 256 +
+                         (size_t)32 * 32 * 4 + (size_t)4 * NL * 1024;
+  hipLaunchKernelGGL((lstm_wave_bwd_bf16_kernel<48, 8, NL>), dim3(WB_L * a.nub * a.nrb), dim3(256), lds, stream, a);
+  return (int)hipGetLastError();
+}

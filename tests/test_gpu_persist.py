@@ -94,3 +94,27 @@ def test_wavefront_fwd_bf16_against_per_layer(tmp_path, N, M, T):
     print(f"\nMEASURED wave2_vs_layer.emb {d:.3e}")
     assert d < 5e-3, d
     np.testing.assert_allclose(b["loss"], a["loss"], rtol=1e-3)
+
+
+@pytest.mark.parametrize("N,M,T", [(8, 10, 20),    # c4's per-rank shape: 3 x 24 x 3 = 216 workgroups
+                                   (7, 5, 9)])     # ragged rows (B = 35: padded dG^T columns)
+def test_wavefront_bwd_bf16_against_per_layer(tmp_path, N, M, T):
+    """Layer-wavefront backward (lstm_wave_bwd_bf16_kernel: all layers' recurrences and dx in one
+    launch) vs the per-layer schedule (one persistent launch + dx GEMM per layer).  The layers'
+    dh_rec sums are ordered alike; dx is summed per gate then across gates (the GEMM: over K in
+    k-tile order), so the lower layers see fp32-reordered upstream gradients that bf16 rounding of
+    dG can amplify to a few bf16 ulps: agreement at bf16-operand level."""
+    dims = (40, 768, 3, 256)
+    a = _run(tmp_path, "layer", {"SV_WAVE_BWD": "0"}, dims, N, M, T, "bf16")
+    b = _run(tmp_path, "wave", {"SV_WAVE_BWD": "1"}, dims, N, M, T, "bf16")
+    assert int(a["status"][0]) == 0 and int(b["status"][0]) == 0
+    np.testing.assert_array_equal(b["loss"], a["loss"])   # the forward is unchanged
+    grads = [k for k in a if k.startswith("grad_")]
+    assert len(grads) == 4 * dims[2] + 2
+    worst = 0.0
+    for k in grads:
+        d = float(np.abs(b[k] - a[k]).max() / max(np.abs(a[k]).max(), 1e-30))
+        worst = max(worst, d)
+        print(f"\nMEASURED wave_bwd_vs_layer.{k} {d:.3e}")
+        assert d < 2e-2, (k, d)
+    print(f"\nMEASURED wave_bwd_vs_layer.worst {worst:.3e}")
