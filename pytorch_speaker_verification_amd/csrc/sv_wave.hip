@@ -61,6 +61,8 @@ struct WaveFwd2Args {
   unsigned limit;
   long ldhT;
   int T, Bp, B, H, nub, nrb, fault;
+  int stamp;  // SV_WAVE3_STAMP=1 (profiling): per-phase s_memtime cycle sums into the sync block
+  int dbg;    // SV_WAVE3_DEBUG (diagnostics)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wv_rsrc(const void* p, unsigned bytes) {
@@ -272,6 +274,290 @@ __global__ __launch_bounds__(256, 1) void lstm_wave2_fwd_bf16_kernel(const WaveF
   }
 }
 
+// ---- wave3: the same wavefront with LDS-DMA operand staging ----
+// lstm_wave2_fwd_bf16_kernel stages both A tiles through registers in groups of 3 loads (eight
+// dependent global round trips per step).  Here each tile is ONE batch of 12 buffer_load ... lds
+// per thread straight into LDS, in MFMA fragment order ([k-step][lane] 16-B chunks: every
+// ds_read_b128 of a fragment is one contiguous 1 KB), and the two tiles live in distinct static
+// LDS arrays so the compiler's LDS-DMA wait tracking keeps reads of one tile from waiting on the
+// other's DMA.  Per step t of layer l:
+//   x_t = h_t^{l-1}: its DMA was issued at the end of step t-1 (once layer l-1's step t arrived)
+//   wait own h_{t-1}; issue its DMA; x-part MFMAs from the x tile (overlapping the h DMA);
+//   bf16 rounding with the biases; h-part MFMAs; cell update; hand-off; arrival;
+//   off-critical stores; wait layer l-1's step t+1; issue x_{t+1}'s DMA.
+// Same products in the same order as wave2 (bit-identical outputs).
+namespace {
+// LDS image of one 32-row x H bf16 tile (H = 768), two regions:
+//   A: units [0, 512) as 32 rows of 1024 B + 16 B pad (a 1040-B row stride);
+//   B: units [512, 768) as 32 rows of 512 B, unpadded, the 16-B chunk c of row r at slot
+//      c ^ (r & 15) (an XOR swizzle in place of a pad: one DMA instruction fills two whole rows).
+// Fragment reads (lanes 0-15 = rows 0-15 at one k offset) are conflict-free in both; every DMA
+// instruction reads whole 128-B lines (one 1 KB row piece, or two 512-B ones).
+constexpr int W3_RA = 1040, W3_RB = 512;
+constexpr int W3_TILE = WV_BM * (W3_RA + W3_RB);
+constexpr int W3_DMA = WV_BM / 4 + WV_BM / 8;  // DMA instructions per wave per tile (8 A + 4 B)
+}  // namespace
+
+// stage a 32-row tile of slot `ts` of `ra` (a [T+1][B][H] bf16 buffer, H = 768; the descriptor is
+// built once, outside the time loop, so it stays scalar): wave w stages rows 8 w .. 8 w + 7; rows
+// past B read zeros
+__device__ __forceinline__ void w3_dma(__amdgpu_buffer_rsrc_t ra, int ts, int B, int H, int b0, char* tile, int g,
+                                       int lane, int fmask) {
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  // an opaque zero keeps the 24 per-instruction addresses from being hoisted out of the time loop
+  // (held live across it they pushed weight fragments into scratch)
+  int z = 0;
+  asm volatile("" : "+v"(z));
+  g += z;
+  const unsigned slot = (unsigned)ts * (unsigned)B * (unsigned)H * 2u;
+  auto row_base = [&](int row) {
+    return b0 + row < B ? slot + (unsigned)(b0 + row) * (unsigned)H * 2u : 0xFFFFE000u;
+  };
+#pragma unroll
+  for (int j = 0; j < WV_BM / 4; ++j) {  // region A: one row per instruction
+    const int row = g * (WV_BM / 4) + j;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + row * W3_RA), 16, row_base(row) + 16u * lane, 0,
+                                             0, 16 /* sc1 */);
+  }
+#pragma unroll
+  for (int j = 0; j < WV_BM / 8; ++j) {  // region B: rows 2p, 2p + 1 per instruction, swizzled
+    const int p = g * (WV_BM / 8) + j, row = 2 * p + (lane >> 5), sl = lane & 31;
+    const unsigned c = 64u + (unsigned)(sl ^ (row & fmask));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + WV_BM * W3_RA + p * 1024), 16,
+                                             row_base(row) + 16u * c, 0, 0, 16 /* sc1 */);
+  }
+}
+
+// acc += A (the tile's LDS image) . W: fragments read 4 ahead, as wv_mfma_lds
+__device__ __forceinline__ void w3_mfma_lds(const char* tile, int lane, const bf16x8_t (&W)[WV_NS], f32x16& acc,
+                                            int fmask) {
+  const int r = lane & 31, hh = lane >> 5;
+  const char* pa = tile + r * W3_RA + hh * 16;
+  // region B: chunk 2 s' + hh of row r at slot (2 s' + hh) ^ (r & 15) = 2 s' ^ F, F = (r & 15) ^ hh
+  const unsigned fb = (unsigned)(((r & fmask) ^ hh) << 4);
+  const char* pb = tile + WV_BM * W3_RA + r * W3_RB;
+  auto frag = [&](int s) {
+    if (s < 32) return *reinterpret_cast<const bf16x8_t*>(pa + 32 * s);
+    return *reinterpret_cast<const bf16x8_t*>(pb + ((unsigned)(32 * (s - 32)) ^ fb));
+  };
+  bf16x8_t cur[4], nxt[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) cur[j] = frag(j);
+#pragma unroll
+  for (int s0 = 0; s0 < WV_NS; s0 += 4) {
+    if (s0 + 4 < WV_NS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nxt[j] = frag(s0 + 4 + j);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = mfma_bf16(cur[j], W[s0 + j], acc);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+  }
+}
+
+template <bool L0, bool STAMP>
+__device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int rb, char* tile_x, char* tile_h,
+                                       float* pre, bf16_t* hsb, bf16_t* hts) {
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int H = a.H, B = a.B, T = a.T, nub = a.nub;
+  const int fmask = (a.dbg & 2) ? 0 : 15;  // debug: SV_WAVE3_DEBUG=2 drops the region-B swizzle
+  const int j0 = ub * BF_U, b0 = rb * WV_BM;
+  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
+  unsigned* my_cnt = a.cnt[l] + rb * SV_PCNT_STRIDE;
+  unsigned* below = L0 ? nullptr : a.cnt[l - 1] + rb * SV_PCNT_STRIDE;
+  const unsigned producers = nub;
+  const bool wok = j0 + r < H;
+  bf16x8_t wh[WV_NS], wx[WV_NS];
+  {
+    const bf16_t* rh = a.whh[l] + ((long)g * H + j0 + r) * H + 8 * hh;
+    const int K = L0 ? WV_F : H;
+    const bf16_t* rx = a.wih[l] + ((long)g * H + j0 + r) * K + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < WV_NS; ++s) {
+      bf16x8_t z = {};
+      wh[s] = wok ? *reinterpret_cast<const bf16x8_t*>(rh + 16 * s) : z;
+      wx[s] = (wok && 16 * s + 8 * hh < K) ? *reinterpret_cast<const bf16x8_t*>(rx + 16 * s) : z;
+    }
+  }
+  float xbias = 0.f;
+  if (wok) {
+    const int col = g * H + j0 + r;
+    xbias = a.bih[l][col] + a.bhh[l][col];
+  }
+  const int u4 = (tid & 7) * 4, brow = tid >> 3;
+  const long gb = b0 + brow;
+  float cst[4] = {0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t rxs = wv_rsrc(a.x_bf, (unsigned)((long)T * B * WV_F * 2));
+  const unsigned hbytes = (unsigned)((long)(T + 1) * BH * 2);
+  const __amdgpu_buffer_rsrc_t rown = wv_rsrc(a.hb[l], hbytes);
+  const __amdgpu_buffer_rsrc_t rbel = wv_rsrc(L0 ? a.hb[l] : a.hb[l - 1], hbytes);
+  if constexpr (!L0) {  // x_0 = h_0^{l-1}
+    if (tid == 0) wv_wait(below, producers, a.status, a.limit);
+    __syncthreads();
+    w3_dma(rbel, 1, B, H, b0, tile_x, g, lane, fmask);
+  }
+  // raw barriers (no fence) where a DMA is in flight: __syncthreads' release fence would drain it
+  auto raw_barrier = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // STAMP is a template parameter, not a runtime test: a branch between an MFMA and the reads of
+  // its accumulators made the compiler's hazard padding too short (the first AGPR read returned a
+  // stale a15: rows 27 and 31 of every tile wrong)
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+  auto mark = [&](int i) {
+    if constexpr (STAMP) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      ph[i] += now - tlast;
+      tlast = now;
+    }
+  };
+  for (int t = 0; t < T; ++t) {
+    // h_{t-1} (t = 0: slot 0, zeros -- the h-part then adds exact zeros, so every step has the
+    // same DMA / wait shape and the compiler can count the waits)
+    if (tid == 0 && t > 0) wv_wait(my_cnt, producers * (unsigned)t, a.status, a.limit);
+    if (a.dbg & 1)
+      __syncthreads();  // debug: drain everything (the x DMA too) here
+    else
+      raw_barrier();
+    mark(0);
+    w3_dma(rown, t, B, H, b0, tile_h, g, lane, fmask);
+    mark(1);
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    if constexpr (!L0) {
+      // this wave's x DMA and everything older (the 12 h DMAs are the newest), then all waves'
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      raw_barrier();
+      w3_mfma_lds(tile_x, lane, wx, acc, fmask);
+    } else {
+      u32x4_t xa[WV_XS];
+#pragma unroll
+      for (int s = 0; s < WV_XS; ++s) {  // rows past B: zeros (offset past the step's rows)
+        const unsigned off = 16 * s + 8 * hh < WV_F
+                                 ? ((unsigned)t * (unsigned)(B * WV_F) + (unsigned)min(b0 + r, B) * (unsigned)WV_F +
+                                    (b0 + r < B ? 16 * s + 8 * hh : 0)) * 2u
+                                 : 0xFFFFFFF0u;
+        xa[s] = __builtin_amdgcn_raw_buffer_load_b128(rxs, b0 + r < B ? off : 0xFFFFFFF0u, 0, 0);
+      }
+#pragma unroll
+      for (int s = 0; s < WV_XS; ++s) acc = mfma_bf16(__builtin_bit_cast(bf16x8_t, xa[s]), wx[s], acc);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = round_bf(acc[i] + xbias);
+    mark(2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    w3_mfma_lds(tile_h, lane, wh, acc, fmask);
+    mark(3);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) pre[acc_row(i, lane) * WV_LDP + g * BF_U + r] = acc[i];
+    __syncthreads();
+    uint2 act[4];
+    float4 cv, hv;
+    {
+      float4 pq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pq[q] = *reinterpret_cast<const float4*>(pre + brow * WV_LDP + q * BF_U + u4);
+      float ao[4][4], co[4], ho[4];
+      unsigned pk[2] = {0u, 0u};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float pv[4] = {pq[0][v], pq[1][v], pq[2][v], pq[3][v]};
+        const float xv[4] = {0.f, 0.f, 0.f, 0.f};
+        float a4[4], h;
+        const float c = lstm_cell_fwd(pv, xv, cst[v], a4, h);
+        cst[v] = c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ao[q][v] = a4[q];
+        co[v] = c;
+        ho[v] = h;
+        const bf16_t e = to_bf(h);
+        hts[(u4 + v) * WV_LDT + brow] = e;
+        pk[v >> 1] |= (unsigned)e << (16 * (v & 1));
+      }
+      *reinterpret_cast<uint2*>(hsb + brow * WV_LDB + u4) = uint2{pk[0], pk[1]};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) act[q] = pack_bf4(ao[q][0], ao[q][1], ao[q][2], ao[q][3]);
+      cv = float4{co[0], co[1], co[2], co[3]};
+      hv = float4{ho[0], ho[1], ho[2], ho[3]};
+    }
+    __syncthreads();
+    mark(4);
+    if (tid < WV_BM * 4) {
+      const int row = tid >> 2, c = tid & 3, gr = b0 + row;
+      const __amdgpu_buffer_rsrc_t rw = wv_rsrc(a.hb[l] + (long)(t + 1) * BH, (unsigned)(BH * 2));
+      if (gr < B && j0 + 8 * c < H) {
+        const uint4 v = *reinterpret_cast<const uint4*>(hsb + row * WV_LDB + 8 * c);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw,
+                                               ((unsigned)gr * (unsigned)H + (unsigned)(j0 + 8 * c)) * 2u, 0,
+                                               16 /* sc1 */);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0 && !(a.fault && t == 0 && blockIdx.x == 0))
+      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mark(5);
+    // off the critical chain: activations, c, h and hT of step t (before the next x DMA, so the
+    // counted wait above sees only DMAs behind it)
+    if (gb < B && j0 + u4 < H) {
+      bf16_t* gp = a.gates[l] + (long)t * BG + gb * G + j0 + u4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(gp + q * H) = act[q];
+      *reinterpret_cast<float4*>(a.c[l] + (long)t * BH + gb * H + j0 + u4) = cv;
+      *reinterpret_cast<float4*>(a.h[l] + (long)(t + 1) * BH + gb * H + j0 + u4) = hv;
+    }
+    if (a.hT[l] && tid < BF_U * (WV_BM / 8)) {
+      const int u = tid >> 2, c = tid & 3, gc = b0 + 8 * c;
+      if (gc < a.Bp && j0 + u < H) {
+        bf16_t* row = a.hT[l] + (long)(j0 + u) * a.ldhT;
+        *reinterpret_cast<uint4*>(row + (long)(t + 1) * a.Bp + gc) = *reinterpret_cast<const uint4*>(hts + u * WV_LDT + 8 * c);
+        if (t == 0) *reinterpret_cast<uint4*>(row + gc) = uint4{0u, 0u, 0u, 0u};
+      }
+    }
+    if (!L0 && t + 1 < T) {  // x_{t+1}: tile_x is free (every wave is past this step's x-part)
+      if (tid == 0) wv_wait(below, producers * (unsigned)(t + 2), a.status, a.limit);
+      raw_barrier();
+      w3_dma(rbel, t + 2, B, H, b0, tile_x, g, lane, fmask);
+    }
+    mark(6);
+  }
+  if (STAMP && tid == 0 && blockIdx.x < SV_NSTAMP_WG) {
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(a.status + SV_SYNC_STAMP) + blockIdx.x * SV_NSTAMP;
+    for (int i = 0; i < 7; ++i) st[i] = ph[i];
+  }
+}
+
+template <bool STAMP>
+__global__ __launch_bounds__(256, 1) void lstm_wave3_fwd_bf16_kernel(const WaveFwd2Args a) {
+  __shared__ __attribute__((aligned(16))) char tile_x[W3_TILE];
+  __shared__ __attribute__((aligned(16))) char tile_h[W3_TILE];
+  __shared__ __attribute__((aligned(16))) float pre[WV_BM * WV_LDP];
+  __shared__ __attribute__((aligned(16))) bf16_t hsb[WV_BM * WV_LDB];
+  __shared__ __attribute__((aligned(16))) bf16_t hts[BF_U * WV_LDT];
+  const int nub = a.nub;
+  int ub, rb, l;
+  {
+    const int i = blockIdx.x, n = gridDim.x;
+    const int x = i & 7, q = n >> 3, rr = n & 7;
+    const int L = x * q + min(x, rr) + (i >> 3);
+    ub = L % nub;
+    rb = (L / nub) % a.nrb;
+    l = L / (nub * a.nrb);
+  }
+  if (l == 0)
+    w3_run<true, STAMP>(a, l, ub, rb, tile_x, tile_h, pre, hsb, hts);
+  else
+    w3_run<false, STAMP>(a, l, ub, rb, tile_x, tile_h, pre, hsb, hts);
+}
+
 // ---- host ----
 // can the layer-wavefront forward run these dims co-resident on a device of `cus` CUs?
 int sv_wave_fwd_fits(int L, int B, int F, int H, int cus) {
@@ -318,7 +604,26 @@ int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, cons
   a.ldhT = (long)(T + 1) * a.Bp;
   hipError_t e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(lstm_wave2_fwd_bf16_kernel, dim3(L * a.nub * a.nrb), dim3(WV_NT), WV_LDS, stream, a);
+  // SV_WAVE3=0: the register-staged wave2 kernel (same outputs bit for bit)
+  static const int wave3 = [] {
+    const char* e = getenv("SV_WAVE3");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  static const int w3stamp = [] {
+    const char* e = getenv("SV_WAVE3_STAMP");
+    return (e && *e == '1') ? 1 : 0;
+  }();
+  a.stamp = w3stamp;
+  static const int w3dbg = [] {
+    const char* e = getenv("SV_WAVE3_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  a.dbg = w3dbg;
+  if (wave3 && (long)(T + 1) * B * H * 2 < (1L << 32) - (1L << 20))
+    hipLaunchKernelGGL(a.stamp ? lstm_wave3_fwd_bf16_kernel<true> : lstm_wave3_fwd_bf16_kernel<false>,
+                       dim3(L * a.nub * a.nrb), dim3(WV_NT), 0, stream, a);
+  else
+    hipLaunchKernelGGL(lstm_wave2_fwd_bf16_kernel, dim3(L * a.nub * a.nrb), dim3(WV_NT), WV_LDS, stream, a);
   SV_LAUNCH_CHECK();
   if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
   return SV_OK;

@@ -118,3 +118,16 @@ def test_wavefront_bwd_bf16_against_per_layer(tmp_path, N, M, T):
         print(f"\nMEASURED wave_bwd_vs_layer.{k} {d:.3e}")
         assert d < 2e-2, (k, d)
     print(f"\nMEASURED wave_bwd_vs_layer.worst {worst:.3e}")
+
+
+@pytest.mark.parametrize("N,M,T", [(8, 10, 20), (7, 5, 9)])
+def test_wave3_fwd_equals_wave2(tmp_path, N, M, T):
+    """The LDS-DMA-staged wavefront forward (wave3) forms the same products in the same order as
+    the register-staged one (wave2; its step-0 h-part adds exact zeros): bit-identical outputs."""
+    dims = (40, 768, 3, 256)
+    a = _run(tmp_path, "w2", {"SV_WAVE3": "0"}, dims, N, M, T, "bf16")
+    b = _run(tmp_path, "w3", {"SV_WAVE3": "1"}, dims, N, M, T, "bf16")
+    assert int(a["status"][0]) == 0 and int(b["status"][0]) == 0
+    for k in a:
+        if k != "status":
+            np.testing.assert_array_equal(b[k], a[k], err_msg=k)
