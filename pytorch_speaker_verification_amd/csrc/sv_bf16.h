@@ -207,8 +207,8 @@ __device__ __forceinline__ void gemm_mainloop_step(const bf16_t* __restrict__ A,
 
 // acc[m] += A_m . W over NS k-steps of 16, A_m = LDS rows (A0 + m * mstride; this lane's row and
 // k-offset folded in), W = this wave's B fragments in registers.  The A fragments run P k-steps
-// ahead of the MFMAs in a register ring: group scheduling barriers keep each step's NACC MFMAs
-// in front of the ds_read_b128s of step s + P, so every read is waited for P steps later
+// ahead of the MFMAs in a register ring: a scheduling barrier per step keeps each step's NACC
+// MFMAs in front of the ds_read_b128s of step s + P, so every read is waited for P steps later
 // (lgkmcnt(P-1 ...)) and the LDS latency hides behind the MFMAs instead of being paid per MFMA.
 template <int NS, int NACC, int P>
 __device__ __forceinline__ void mfma_lds_pipe(const bf16_t* A0, int mstride, const bf16x8_t (&W)[NS],
@@ -222,12 +222,13 @@ __device__ __forceinline__ void mfma_lds_pipe(const bf16_t* A0, int mstride, con
   for (int s = 0; s < NS; ++s) {
 #pragma unroll
     for (int m = 0; m < NACC; ++m) acc[m] = mfma_bf16(f[s % P][m], W[s], acc[m]);
-    __builtin_amdgcn_sched_group_barrier(0x008, NACC, 0);
     if (s + P < NS) {
 #pragma unroll
       for (int m = 0; m < NACC; ++m) f[s % P][m] = *reinterpret_cast<const bf16x8_t*>(A0 + m * mstride + 16 * (s + P));
-      __builtin_amdgcn_sched_group_barrier(0x100, NACC, 0);
     }
+    // a full scheduling barrier per k-step (group barriers let the scheduler satisfy "NACC DS
+    // reads here" with the reads the next MFMAs need, i.e. prefetch distance 0)
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 

@@ -334,7 +334,10 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
 // the K1 path stores it -- lstm_persist2_fwd_bf16_kernel's fused form.
 // SPLIT: the second half of h_{t-1} is loaded while the first half's MFMAs run (its registers
 // stay live across them; only where the register budget allows, XF = 0)
-template <int NS, int NL, int PA, int XF, bool SPLIT = false>
+// MODE: 0 register staging of h_{t-1} (two halves), 1 the same with the second half in flight
+// during the first half's MFMAs (SPLIT), 2 LDS-DMA staging into the row-contiguous tile image of
+// sv_persist_dev.h's w3_dma (one batch of 12 DMA instructions per wave, no register round trip)
+template <int NS, int NL, int PA, int XF, int MODE = 0>
 __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
     const bf16_t* __restrict__ whh_bf, bf16_t* __restrict__ gates, float* __restrict__ c_tm, float* __restrict__ h_tm,
     bf16_t* h_bf, bf16_t* __restrict__ hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd,
@@ -344,6 +347,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
   // MFMAs, 8 no post-arrival stores
   constexpr int BM = 32, U = 64, KR = 2;
   constexpr int K = NS * 16, LDA = K + 8;
+  constexpr bool SPLIT = MODE == 1, DMA = MODE == 2;
+  static_assert(!DMA || (BM * LDA * 2 == W3_TILE && NS == 48), "DMA tile image = the As region");
   constexpr int LDP = 4 * U + 4;  // pre [BM][LDP] fp32
   constexpr int LDB = U + 8;      // hsb [BM][LDB] bf16
   constexpr int LDT = BM + 8;     // hts [U][LDT] bf16
@@ -442,6 +447,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
       }
     }
   };
+  const __amdgpu_buffer_rsrc_t rh_all = sv_rsrc(h_bf, (unsigned)((long)(T + 1) * BH * 2));
   for (int t = 0; t < T; ++t) {
     f32x16 acc0, acc1;
 #pragma unroll
@@ -467,29 +473,39 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
         }
       };
       const bf16_t* A0 = As + r * LDA + 8 * hh;
+      const W3Frag dfrag(reinterpret_cast<const char*>(As), lane);
+      auto afrag = [&](int s) {
+        if constexpr (DMA) return dfrag(s);
+        return *reinterpret_cast<const bf16x8_t*>(A0 + 16 * s);
+      };
       bf16x8_t wq[2];
       // k-steps [s0, s1) from the staged A tile: A fragments PA ahead (within the range), the
       // LDS-resident W fragments two ahead
       auto mma_range = [&](int s0, int s1) {
         bf16x8_t fa[PA];
 #pragma unroll
-        for (int p = 0; p < PA; ++p) fa[p] = *reinterpret_cast<const bf16x8_t*>(A0 + 16 * (s0 + p));
+        for (int p = 0; p < PA; ++p) fa[p] = afrag(s0 + p);
 #pragma unroll
         for (int s = s0; s < s1; ++s) {
           acc0 = mfma_bf16(fa[(s - s0) % PA], wa[s], acc0);
           acc1 = mfma_bf16(fa[(s - s0) % PA], s < NR ? wb[s < NR ? s : 0] : wq[s & 1], acc1);
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-          if (s + PA < s1) {
-            fa[(s - s0) % PA] = *reinterpret_cast<const bf16x8_t*>(A0 + 16 * (s + PA));
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          }
-          if (s + 2 >= NR && s + 2 < NS) {
-            wq[s & 1] = wl_read(s + 2 - NR);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          }
+          if (s + PA < s1) fa[(s - s0) % PA] = afrag(s + PA);
+          if (s + 2 >= NR && s + 2 < NS) wq[s & 1] = wl_read(s + 2 - NR);
+          // a full scheduling barrier per k-step: with group barriers the scheduler satisfied
+          // "one DS read here" with the read the next MFMA needs, sinking every fragment read to
+          // just before its use (prefetch distance 0, one exposed LDS latency per k-step)
+          __builtin_amdgcn_sched_barrier(0);
         }
       };
-      if constexpr (SPLIT) {
+      if constexpr (DMA) {
+        w3_dma(rh_all, t, B, H, b0, reinterpret_cast<char*>(As), g, lane);
+        load_xg(t);
+        // the tile's DMA (older than the x-projection loads), then every wave's
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XF > 0 ? XS : KR * 4) : "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (!(dbg & 2)) mma_range(0, NS);
+      } else if constexpr (SPLIT) {
         uint4 v0[CH], v1[CH];
         stage_load(0, v0);
         stage_store(0, v0);
@@ -618,12 +634,30 @@ int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
                            const bf16_t* wih_bf, const float* b_ih, const float* b_hh, int dbg) {
   constexpr size_t base = (size_t)32 * (768 + 8) * 2 + (size_t)32 * (4 * 64 + 4) * 4 + (size_t)32 * 72 * 2 +
                           (size_t)64 * 40 * 2;
+  // SV_PFWD3_DMA=1: h_{t-1} staged by LDS-DMA (sv_persist_dev.h's w3_dma) instead of through
+  // registers; same products in the same order (bit-identical).  Measured slower at c3 (forward
+  // 921 vs 843 µs per layer, step 10.54-10.70 vs 10.32 ms) -- kept off
+  static const int dma_env = [] {
+    const char* e = getenv("SV_PFWD3_DMA");
+    return (e && *e == '1') ? 1 : 0;
+  }();
+  const bool dma = dma_env && (long)(T + 1) * B * H * 2 < (1L << 32) - (1L << 20);
   if (x_bf) {  // layer 0, F = 40: the W_ih fragments take registers, so more W_hh fragments live in LDS
     if (F != 40 || !wih_bf) return SV_EARG;
     constexpr int NL = 16;
-    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 5>), grid, dim3(256), base + (size_t)4 * NL * 1024,
+    if (dma)
+      hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 5, 2>), grid, dim3(256),
+                         base + (size_t)4 * NL * 1024, stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H,
+                         cnt, nub, xcd, status, limit, fault, x_bf, wih_bf, b_ih, b_hh, dbg);
+    else
+      hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 5>), grid, dim3(256), base + (size_t)4 * NL * 1024,
+                         stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
+                         fault, x_bf, wih_bf, b_ih, b_hh, dbg);
+  } else if (dma) {
+    constexpr int NL = 12;
+    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0, 2>), grid, dim3(256), base + (size_t)4 * NL * 1024,
                        stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
-                       fault, x_bf, wih_bf, b_ih, b_hh, dbg);
+                       fault, nullptr, nullptr, nullptr, nullptr, dbg);
   } else {
     // SV_PFWD3_SPLIT=1: the second half of h_{t-1} loads during the first half's MFMAs (measured
     // no faster: c3 forward 4.77 vs 4.67 ms, step 11.46 vs 11.47 ms -- kept off)
@@ -633,7 +667,7 @@ int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
     }();
     if (split) {
       constexpr int NL = 16;
-      hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0, true>), grid, dim3(256),
+      hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0, 1>), grid, dim3(256),
                          base + (size_t)4 * NL * 1024, stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H,
                          cnt, nub, xcd, status, limit, fault, nullptr, nullptr, nullptr, nullptr, dbg);
     } else {

@@ -45,3 +45,60 @@ __device__ __forceinline__ void persist_wait(unsigned* c, unsigned target, unsig
 // first arrival, so its row block's consumers time out (short spin limit) and the status is set
 __device__ __forceinline__ bool persist_arrive_ok(int fault, int first) { return !(fault && first && blockIdx.x == 0); }
 
+// LDS-DMA image of one 32-row x H bf16 tile (H = 768; sv_wave.hip's wave3 forward and
+// sv_persist3.hip's wide forward), two regions:
+//   A: units [0, 512) as 32 rows of 1024 B + 16 B pad (a 1040-B row stride);
+//   B: units [512, 768) as 32 rows of 512 B, unpadded, the 16-B chunk c of row r at slot
+//      c ^ (r & 15) (an XOR swizzle in place of a pad: one DMA instruction fills two whole rows).
+// Fragment reads (lanes 0-15 = rows 0-15 at one k offset) are conflict-free in both; every DMA
+// instruction reads whole 128-B lines (one 1 KB row piece, or two 512-B ones).
+constexpr int W3_RA = 1040, W3_RB = 512;
+constexpr int W3_TILE = 32 * (W3_RA + W3_RB);
+constexpr int W3_DMA = 12;  // DMA instructions per wave per tile (8 A + 4 B)
+
+// stage a 32-row tile of slot `ts` of `ra` (a [T+1][B][H] bf16 buffer, H = 768; the descriptor is
+// built once, outside the time loop, so it stays scalar): wave w stages rows 8 w .. 8 w + 7; rows
+// past B read zeros
+__device__ __forceinline__ void w3_dma(__amdgpu_buffer_rsrc_t ra, int ts, int B, int H, int b0, char* tile, int g,
+                                       int lane) {
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  // an opaque zero keeps the 24 per-instruction addresses from being hoisted out of the time loop
+  // (held live across it they pushed weight fragments into scratch)
+  int z = 0;
+  asm volatile("" : "+v"(z));
+  g += z;
+  const unsigned slot = (unsigned)ts * (unsigned)B * (unsigned)H * 2u;
+  auto row_base = [&](int row) {
+    return b0 + row < B ? slot + (unsigned)(b0 + row) * (unsigned)H * 2u : 0xFFFFE000u;
+  };
+#pragma unroll
+  for (int j = 0; j < 32 / 4; ++j) {  // region A: one row per instruction
+    const int row = g * (32 / 4) + j;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + row * W3_RA), 16, row_base(row) + 16u * lane, 0,
+                                             0, 16 /* sc1 */);
+  }
+#pragma unroll
+  for (int j = 0; j < 32 / 8; ++j) {  // region B: rows 2p, 2p + 1 per instruction, swizzled
+    const int p = g * (32 / 8) + j, row = 2 * p + (lane >> 5), sl = lane & 31;
+    const unsigned c = 64u + (unsigned)(sl ^ (row & 15));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + 32 * W3_RA + p * 1024), 16,
+                                             row_base(row) + 16u * c, 0, 0, 16 /* sc1 */);
+  }
+}
+
+// byte offset of A fragment s (k-step, 16 bf16) of lane (r, hh) in a w3_dma tile image
+struct W3Frag {
+  const char* pa;
+  const char* pb;
+  unsigned fb;
+  __device__ __forceinline__ W3Frag(const char* tile, int lane) {
+    const int r = lane & 31, hh = lane >> 5;
+    pa = tile + r * W3_RA + hh * 16;
+    fb = (unsigned)(((r & 15) ^ hh) << 4);
+    pb = tile + 32 * W3_RA + r * W3_RB;
+  }
+  __device__ __forceinline__ bf16x8_t operator()(int s) const {
+    if (s < 32) return *reinterpret_cast<const bf16x8_t*>(pa + 32 * s);
+    return *reinterpret_cast<const bf16x8_t*>(pb + ((unsigned)(32 * (s - 32)) ^ fb));
+  }
+};

@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <stdlib.h>
 #include "sv_bf16.h"
+#include "sv_persist_dev.h"
 #include "../../include/sv_ge2e.h"
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -286,75 +287,18 @@ __global__ __launch_bounds__(256, 1) void lstm_wave2_fwd_bf16_kernel(const WaveF
 //   bf16 rounding with the biases; h-part MFMAs; cell update; hand-off; arrival;
 //   off-critical stores; wait layer l-1's step t+1; issue x_{t+1}'s DMA.
 // Same products in the same order as wave2 (bit-identical outputs).
-namespace {
-// LDS image of one 32-row x H bf16 tile (H = 768), two regions:
-//   A: units [0, 512) as 32 rows of 1024 B + 16 B pad (a 1040-B row stride);
-//   B: units [512, 768) as 32 rows of 512 B, unpadded, the 16-B chunk c of row r at slot
-//      c ^ (r & 15) (an XOR swizzle in place of a pad: one DMA instruction fills two whole rows).
-// Fragment reads (lanes 0-15 = rows 0-15 at one k offset) are conflict-free in both; every DMA
-// instruction reads whole 128-B lines (one 1 KB row piece, or two 512-B ones).
-constexpr int W3_RA = 1040, W3_RB = 512;
-constexpr int W3_TILE = WV_BM * (W3_RA + W3_RB);
-constexpr int W3_DMA = WV_BM / 4 + WV_BM / 8;  // DMA instructions per wave per tile (8 A + 4 B)
-}  // namespace
-
-// stage a 32-row tile of slot `ts` of `ra` (a [T+1][B][H] bf16 buffer, H = 768; the descriptor is
-// built once, outside the time loop, so it stays scalar): wave w stages rows 8 w .. 8 w + 7; rows
-// past B read zeros
-__device__ __forceinline__ void w3_dma(__amdgpu_buffer_rsrc_t ra, int ts, int B, int H, int b0, char* tile, int g,
-                                       int lane, int fmask) {
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  // an opaque zero keeps the 24 per-instruction addresses from being hoisted out of the time loop
-  // (held live across it they pushed weight fragments into scratch)
-  int z = 0;
-  asm volatile("" : "+v"(z));
-  g += z;
-  const unsigned slot = (unsigned)ts * (unsigned)B * (unsigned)H * 2u;
-  auto row_base = [&](int row) {
-    return b0 + row < B ? slot + (unsigned)(b0 + row) * (unsigned)H * 2u : 0xFFFFE000u;
-  };
-#pragma unroll
-  for (int j = 0; j < WV_BM / 4; ++j) {  // region A: one row per instruction
-    const int row = g * (WV_BM / 4) + j;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + row * W3_RA), 16, row_base(row) + 16u * lane, 0,
-                                             0, 16 /* sc1 */);
-  }
-#pragma unroll
-  for (int j = 0; j < WV_BM / 8; ++j) {  // region B: rows 2p, 2p + 1 per instruction, swizzled
-    const int p = g * (WV_BM / 8) + j, row = 2 * p + (lane >> 5), sl = lane & 31;
-    const unsigned c = 64u + (unsigned)(sl ^ (row & fmask));
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + WV_BM * W3_RA + p * 1024), 16,
-                                             row_base(row) + 16u * c, 0, 0, 16 /* sc1 */);
-  }
-}
-
 // acc += A (the tile's LDS image) . W: fragments read 4 ahead, as wv_mfma_lds
-__device__ __forceinline__ void w3_mfma_lds(const char* tile, int lane, const bf16x8_t (&W)[WV_NS], f32x16& acc,
-                                            int fmask) {
-  const int r = lane & 31, hh = lane >> 5;
-  const char* pa = tile + r * W3_RA + hh * 16;
-  // region B: chunk 2 s' + hh of row r at slot (2 s' + hh) ^ (r & 15) = 2 s' ^ F, F = (r & 15) ^ hh
-  const unsigned fb = (unsigned)(((r & fmask) ^ hh) << 4);
-  const char* pb = tile + WV_BM * W3_RA + r * W3_RB;
-  auto frag = [&](int s) {
-    if (s < 32) return *reinterpret_cast<const bf16x8_t*>(pa + 32 * s);
-    return *reinterpret_cast<const bf16x8_t*>(pb + ((unsigned)(32 * (s - 32)) ^ fb));
-  };
-  bf16x8_t cur[4], nxt[4];
+__device__ __forceinline__ void w3_mfma_lds(const char* tile, int lane, const bf16x8_t (&W)[WV_NS], f32x16& acc) {
+  const W3Frag frag(tile, lane);
+  constexpr int P = 4;  // fragments in flight; one full scheduling barrier per k-step keeps them so
+  bf16x8_t f[P];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) cur[j] = frag(j);
+  for (int j = 0; j < P; ++j) f[j] = frag(j);
 #pragma unroll
-  for (int s0 = 0; s0 < WV_NS; s0 += 4) {
-    if (s0 + 4 < WV_NS) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) nxt[j] = frag(s0 + 4 + j);
-      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc = mfma_bf16(cur[j], W[s0 + j], acc);
-    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+  for (int s = 0; s < WV_NS; ++s) {
+    acc = mfma_bf16(f[s % P], W[s], acc);
+    if (s + P < WV_NS) f[s % P] = frag(s + P);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -364,7 +308,6 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int H = a.H, B = a.B, T = a.T, nub = a.nub;
-  const int fmask = (a.dbg & 2) ? 0 : 15;  // debug: SV_WAVE3_DEBUG=2 drops the region-B swizzle
   const int j0 = ub * BF_U, b0 = rb * WV_BM;
   const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
   unsigned* my_cnt = a.cnt[l] + rb * SV_PCNT_STRIDE;
@@ -398,7 +341,7 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
   if constexpr (!L0) {  // x_0 = h_0^{l-1}
     if (tid == 0) wv_wait(below, producers, a.status, a.limit);
     __syncthreads();
-    w3_dma(rbel, 1, B, H, b0, tile_x, g, lane, fmask);
+    w3_dma(rbel, 1, B, H, b0, tile_x, g, lane);
   }
   // raw barriers (no fence) where a DMA is in flight: __syncthreads' release fence would drain it
   auto raw_barrier = [] {
@@ -426,7 +369,7 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
     else
       raw_barrier();
     mark(0);
-    w3_dma(rown, t, B, H, b0, tile_h, g, lane, fmask);
+    w3_dma(rown, t, B, H, b0, tile_h, g, lane);
     mark(1);
     f32x16 acc;
 #pragma unroll
@@ -435,7 +378,7 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
       // this wave's x DMA and everything older (the 12 h DMAs are the newest), then all waves'
       asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
       raw_barrier();
-      w3_mfma_lds(tile_x, lane, wx, acc, fmask);
+      w3_mfma_lds(tile_x, lane, wx, acc);
     } else {
       u32x4_t xa[WV_XS];
 #pragma unroll
@@ -454,7 +397,7 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
     mark(2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     raw_barrier();
-    w3_mfma_lds(tile_h, lane, wh, acc, fmask);
+    w3_mfma_lds(tile_h, lane, wh, acc);
     mark(3);
 #pragma unroll
     for (int i = 0; i < 16; ++i) pre[acc_row(i, lane) * WV_LDP + g * BF_U + r] = acc[i];
@@ -525,7 +468,7 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
     if (!L0 && t + 1 < T) {  // x_{t+1}: tile_x is free (every wave is past this step's x-part)
       if (tid == 0) wv_wait(below, producers * (unsigned)(t + 2), a.status, a.limit);
       raw_barrier();
-      w3_dma(rbel, t + 2, B, H, b0, tile_x, g, lane, fmask);
+      w3_dma(rbel, t + 2, B, H, b0, tile_x, g, lane);
     }
     mark(6);
   }
