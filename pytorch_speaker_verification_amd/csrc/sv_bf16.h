@@ -290,6 +290,48 @@ __device__ __forceinline__ float lstm_cell_bwd(float dh, float i, float f, float
   return dc * f;
 }
 
+// Two elements at once in packed fp32 (v_pk_mul_f32 / v_pk_add_f32: one VALU issue for both):
+// the same per-element operations in the same order as lstm_cell_bwd (contraction off, the
+// transcendentals per element), so results are bit-identical to it.
+typedef float f2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2_t bf_tanh2(f2_t x) {
+#pragma clang fp contract(off)
+  const f2_t y = -2.0f * x;
+  const f2_t e = f2_t{__expf(y.x), __expf(y.y)};
+  const f2_t d = 1.0f + e;
+  const f2_t r = f2_t{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  return 2.0f * r - 1.0f;
+}
+__device__ __forceinline__ f2_t bf_sigmoid2(f2_t x) {
+#pragma clang fp contract(off)
+  const f2_t y = -x;
+  const f2_t d = 1.0f + f2_t{__expf(y.x), __expf(y.y)};
+  return f2_t{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+// lstm_cell_fwd on two elements (same operations, same order: bit-identical)
+__device__ __forceinline__ f2_t lstm_cell_fwd2(const f2_t (&p)[4], const f2_t (&x)[4], f2_t c_prev, f2_t (&a)[4],
+                                               f2_t& h) {
+#pragma clang fp contract(off)
+  a[0] = bf_sigmoid2(p[0] + x[0]);
+  a[1] = bf_sigmoid2(p[1] + x[1]);
+  a[2] = bf_tanh2(p[2] + x[2]);
+  a[3] = bf_sigmoid2(p[3] + x[3]);
+  const f2_t c = a[1] * c_prev + a[0] * a[2];
+  h = a[3] * bf_tanh2(c);
+  return c;
+}
+__device__ __forceinline__ f2_t lstm_cell_bwd2(f2_t dh, f2_t i, f2_t f, f2_t g, f2_t o, f2_t c, f2_t cp, f2_t dcf_in,
+                                               f2_t (&d)[4]) {
+#pragma clang fp contract(off)
+  const f2_t tc = bf_tanh2(c);
+  const f2_t dc = dh * o * (1.f - tc * tc) + dcf_in;
+  d[0] = dc * g * i * (1.f - i);
+  d[1] = dc * cp * f * (1.f - f);
+  d[2] = dc * i * (1.f - g * g);
+  d[3] = dh * tc * o * (1.f - o);
+  return dc * f;
+}
+
 // recurrent-step tile: 64 batch rows x 32 hidden units (x 4 gates = 128 gate columns)
 #define BF_BM 64
 #define BF_U 32

@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     for (int s = 0; s < 64 - NS; ++s) asm volatile("" : "+a"(wb[s]));  // the AGPRs left: 64 - NS fragments
   }
   auto wl_read = [&](int j) { return *reinterpret_cast<const bf16x8_t*>(wl + ((g * NL + j) * 64 + lane) * 16); };
-  // elementwise map: thread -> 4 consecutive units (u4) x rows brow, brow + 16
+  // elementwise map: thread -> 4 consecutive units (u4) x rows 2 brow, 2 brow + 1
   const int u4 = (tid & 15) * 4, brow = tid >> 4;
   float4 cv[KR];
   float dcf[KR][4];
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
       const __amdgpu_buffer_rsrc_t rs = sv_rsrc(dgT + (long)tt * Bp, (unsigned)(4L * H * lddgT * 2 - (long)tt * Bp * 2));
       const int q = tid + 256 * (i - 4), gu = q >> 2, c = q & 3;
       const int gq = gu / U, gj = j0 + gu % U, gb = b0 + 8 * c;
-      const uint4 v = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
+      const uint4 v = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * (c ^ ((gu % U) >> 4 & 3)));
       if (gb < Bp && gj < H)
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rs,
                                                (unsigned)((((long)gq * H + gj) * lddgT + gb) * 2), 0, 0);
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(T - 1) * BH, (unsigned)(BH * 4));
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      const long gb = b0 + brow + 16 * k;
+      const long gb = b0 + 2 * brow + k;
       const u32x4_t x =
           __builtin_amdgcn_raw_buffer_load_b128(rc_, (unsigned)(((gb < Bv ? gb : Bv + 64) * H + j0 + u4) * 4), 0, 0);
       cv[k] = float4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
@@ -203,47 +203,52 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
     __syncthreads();
     mark(1);
+    {
+      // thread: rows 2 brow and 2 brow + 1 (k = 0, 1) x units u4 .. u4 + 3; a unit's two rows land
+      // in the transposed tile as one 4-B write (16 per thread instead of 32 2-B ones), at a chunk
+      // swizzle that makes those writes conflict-free
+      unsigned e0s[4][2] = {};  // row 2 brow's bf16 dG, (q, unit pair)
 #pragma unroll
-    for (int k = 0; k < KR; ++k) {
-      const int b = brow + 16 * k;
-      const float4 r0 = *reinterpret_cast<const float4*>(red + (0 * BM + b) * LDR + u4);
-      const float4 r1 = *reinterpret_cast<const float4*>(red + (1 * BM + b) * LDR + u4);
-      const float4 r2 = *reinterpret_cast<const float4*>(red + (2 * BM + b) * LDR + u4);
-      const float4 r3 = *reinterpret_cast<const float4*>(red + (3 * BM + b) * LDR + u4);
-      const float4 cpv = *reinterpret_cast<const float4*>(ewc + b * U + u4);
-      const float4 upv = *reinterpret_cast<const float4*>(ewu + b * U + u4);
-      float4 f[4];
+      for (int k = 0; k < KR; ++k) {
+        const int b = 2 * brow + k;
+        const float4 r0 = *reinterpret_cast<const float4*>(red + (0 * BM + b) * LDR + u4);
+        const float4 r1 = *reinterpret_cast<const float4*>(red + (1 * BM + b) * LDR + u4);
+        const float4 r2 = *reinterpret_cast<const float4*>(red + (2 * BM + b) * LDR + u4);
+        const float4 r3 = *reinterpret_cast<const float4*>(red + (3 * BM + b) * LDR + u4);
+        const float4 cpv = *reinterpret_cast<const float4*>(ewc + b * U + u4);
+        const float4 upv = *reinterpret_cast<const float4*>(ewu + b * U + u4);
+        float4 f[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        f[q] = unpack_bf4(*reinterpret_cast<const uint2*>(ewa + b * 512 + ((q + b) & 3) * 128 + (u4 >> 3) * 16 +
-                                                          (u4 & 7) * 2));
-      const float rs0[4] = {r0.x, r0.y, r0.z, r0.w}, rs1[4] = {r1.x, r1.y, r1.z, r1.w};
-      const float rs2[4] = {r2.x, r2.y, r2.z, r2.w}, rs3[4] = {r3.x, r3.y, r3.z, r3.w};
-      const float ups[4] = {upv.x, upv.y, upv.z, upv.w};
-      const float cs[4] = {cv[k].x, cv[k].y, cv[k].z, cv[k].w}, cps[4] = {cpv.x, cpv.y, cpv.z, cpv.w};
-      const float a0[4] = {f[0].x, f[0].y, f[0].z, f[0].w}, a1[4] = {f[1].x, f[1].y, f[1].z, f[1].w};
-      const float a2[4] = {f[2].x, f[2].y, f[2].z, f[2].w}, a3[4] = {f[3].x, f[3].y, f[3].z, f[3].w};
-      unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
+        for (int q = 0; q < 4; ++q)
+          f[q] = unpack_bf4(*reinterpret_cast<const uint2*>(ewa + b * 512 + ((q + b) & 3) * 128 + (u4 >> 3) * 16 +
+                                                            (u4 & 7) * 2));
+        unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        float dh = rs0[v];
-        dh += rs1[v];
-        dh += rs2[v];
-        dh += rs3[v];
-        dh += ups[v];
-        float dd[4];
-        dcf[k][v] = lstm_cell_bwd(dh, a0[v], a1[v], a2[v], a3[v], cs[v], cps[v], dcf[k][v], dd);
+        for (int v = 0; v < 4; ++v) {
+          float dh = r0[v];
+          dh += r1[v];
+          dh += r2[v];
+          dh += r3[v];
+          dh += upv[v];
+          float dd[4];
+          dcf[k][v] = lstm_cell_bwd(dh, f[0][v], f[1][v], f[2][v], f[3][v], cv[k][v], cpv[v], dcf[k][v], dd);
+          const int u = u4 + v, sw = (2 * brow) ^ (((u >> 4) & 3) << 3);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bf16_t e = to_bf(dd[q]);
-          gts[(q * U + u4 + v) * LDT + b] = e;
-          pk[q][v >> 1] |= (unsigned)e << (16 * (v & 1));
-          dbs[q][v] += __uint_as_float((unsigned)e << 16);
+          for (int q = 0; q < 4; ++q) {
+            const unsigned e = to_bf(dd[q]);
+            pk[q][v >> 1] |= e << (16 * (v & 1));
+            dbs[q][v] += __uint_as_float(e << 16);
+            if (k == 0)
+              e0s[q][v >> 1] |= e << (16 * (v & 1));
+            else if (!(dbg & 256))  // (profiling: 256 skips the transposed-tile writes)
+              *reinterpret_cast<unsigned*>(gts + (q * U + u) * LDT + sw) =
+                  ((e0s[q][v >> 1] >> (16 * (v & 1))) & 0xffffu) | (e << 16);
+          }
         }
-      }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(dgs + b * LDG + q * U + u4) = uint2{pk[q][0], pk[q][1]};
-      cv[k] = cpv;  // c_{t-1} is the next step's c_t
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(dgs + b * LDG + q * U + u4) = uint2{pk[q][0], pk[q][1]};
+        cv[k] = cpv;  // c_{t-1} is the next step's c_t
+      }
     }
     __syncthreads();
     mark(2);
@@ -280,7 +285,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     for (int i = 0; i < 5; ++i) stamps[blockIdx.x * SV_NSTAMP + i] = ph[i];
   if (dbp) {
     __syncthreads();
-    float* dsum = red;  // [16][4U] fp32: row pairs (brow, brow + 16)
+    float* dsum = red;  // [16][4U] fp32: row pairs (2 brow, 2 brow + 1)
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       *reinterpret_cast<float4*>(dsum + brow * (4 * U) + q * U + u4) = float4{dbs[q][0], dbs[q][1], dbs[q][2], dbs[q][3]};
@@ -568,19 +573,29 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
       float ao[4][4], co[4], ho[4];
       unsigned pk[2] = {0u, 0u};
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const float pv[4] = {pq[0][v], pq[1][v], pq[2][v], pq[3][v]};
-        const float xv[4] = {xf[0][v], xf[1][v], xf[2][v], xf[3][v]};
-        float a4[4], h;
-        const float c = lstm_cell_fwd(pv, xv, cst[k][v], a4, h);
-        cst[k][v] = c;
+      for (int vp = 0; vp < 2; ++vp) {  // unit pairs in packed fp32
+        const int v0 = 2 * vp, v1 = v0 + 1;
+        const f2_t pv[4] = {f2_t{pq[0][v0], pq[0][v1]}, f2_t{pq[1][v0], pq[1][v1]}, f2_t{pq[2][v0], pq[2][v1]},
+                            f2_t{pq[3][v0], pq[3][v1]}};
+        const f2_t xv[4] = {f2_t{xf[0][v0], xf[0][v1]}, f2_t{xf[1][v0], xf[1][v1]}, f2_t{xf[2][v0], xf[2][v1]},
+                            f2_t{xf[3][v0], xf[3][v1]}};
+        f2_t a4[4], h;
+        const f2_t c = lstm_cell_fwd2(pv, xv, f2_t{cst[k][v0], cst[k][v1]}, a4, h);
+        cst[k][v0] = c.x;
+        cst[k][v1] = c.y;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ao[q][v] = a4[q];
-        co[v] = c;
-        ho[v] = h;
-        const bf16_t e = to_bf(h);
-        hts[(u4 + v) * LDT + b] = e;
-        pk[v >> 1] |= (unsigned)e << (16 * (v & 1));
+        for (int q = 0; q < 4; ++q) {
+          ao[q][v0] = a4[q].x;
+          ao[q][v1] = a4[q].y;
+        }
+        co[v0] = c.x;
+        co[v1] = c.y;
+        ho[v0] = h.x;
+        ho[v1] = h.y;
+        const bf16_t e0 = to_bf(h.x), e1 = to_bf(h.y);
+        hts[(u4 + v0) * LDT + b] = e0;
+        hts[(u4 + v1) * LDT + b] = e1;
+        pk[vp] = (unsigned)e0 | ((unsigned)e1 << 16);
       }
       *reinterpret_cast<uint2*>(hsb + b * LDB + u4) = uint2{pk[0], pk[1]};
 #pragma unroll
