@@ -424,7 +424,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
       }
     }
   };
-  // elementwise map: thread -> 4 consecutive units (u4) x rows brow, brow + 16
+  // elementwise map: thread -> 4 consecutive units (u4) x rows 2 brow, 2 brow + 1
   const int u4 = (tid & 15) * 4, brow = tid >> 4;
   const long Bv = B;
   float cst[KR][4];
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
     const __amdgpu_buffer_rsrc_t rx = sv_rsrc(gates + (long)tt * BG, (unsigned)(BG * 2));
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      const long gb = b0 + brow + 16 * k;
+      const long gb = b0 + 2 * brow + k;
       const long gbv = gb < Bv ? gb : Bv + 64;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -561,9 +561,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
     __syncthreads();
     uint2 act[KR][4];
     float4 cv[KR], hv[KR];
+    unsigned hk0[2] = {0u, 0u};  // row 2 brow's bf16 h (unit pairs), joined with row 2 brow + 1's
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      const int b = brow + 16 * k;
+      const int b = 2 * brow + k;
       float4 pq[4], xf[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -593,9 +594,16 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
         ho[v0] = h.x;
         ho[v1] = h.y;
         const bf16_t e0 = to_bf(h.x), e1 = to_bf(h.y);
-        hts[(u4 + v0) * LDT + b] = e0;
-        hts[(u4 + v1) * LDT + b] = e1;
         pk[vp] = (unsigned)e0 | ((unsigned)e1 << 16);
+        if (k == 0) {
+          hk0[vp] = pk[vp];
+        } else {  // a unit's two rows as one 4-B write into the transposed tile (chunk swizzle)
+          const int ua = u4 + v0, ub_ = u4 + v1;
+          *reinterpret_cast<unsigned*>(hts + ua * LDT + ((2 * brow) ^ (((ua >> 4) & 3) << 3))) =
+              (hk0[vp] & 0xffffu) | ((unsigned)e0 << 16);
+          *reinterpret_cast<unsigned*>(hts + ub_ * LDT + ((2 * brow) ^ (((ub_ >> 4) & 3) << 3))) =
+              (hk0[vp] >> 16) | ((unsigned)e1 << 16);
+        }
       }
       *reinterpret_cast<uint2*>(hsb + b * LDB + u4) = uint2{pk[0], pk[1]};
 #pragma unroll
@@ -623,7 +631,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
     if (dbg & 8) continue;
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      const long gb = b0 + brow + 16 * k;
+      const long gb = b0 + 2 * brow + k;
       if (gb < Bv) {
         bf16_t* gp = gates + (long)t * BG + gb * G + j0 + u4;
 #pragma unroll
@@ -636,7 +644,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
       const int u = tid >> 2, c = tid & 3, gb = b0 + 8 * c;
       if (gb < Bp && j0 + u < H) {
         bf16_t* row = hT + (long)(j0 + u) * ldhT;
-        *reinterpret_cast<uint4*>(row + (long)(t + 1) * Bp + gb) = *reinterpret_cast<const uint4*>(hts + u * LDT + 8 * c);
+        *reinterpret_cast<uint4*>(row + (long)(t + 1) * Bp + gb) =
+            *reinterpret_cast<const uint4*>(hts + u * LDT + 8 * (c ^ ((u >> 4) & 3)));
         if (t == 0) *reinterpret_cast<uint4*>(row + gb) = uint4{0u, 0u, 0u, 0u};
       }
     }
