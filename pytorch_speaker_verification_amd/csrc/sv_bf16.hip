@@ -73,12 +73,17 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
 
 __global__ void slab_reduce_bf_kernel(const float* __restrict__ slab, int nz, long zstride, float* __restrict__ out,
                                       long ldc, int M, int N, float beta, const float* __restrict__ bias0,
-                                      const float* __restrict__ bias1, bf16_t* __restrict__ outb = nullptr) {
+                                      const float* __restrict__ bias1, bf16_t* __restrict__ outb = nullptr,
+                                      float* __restrict__ out2 = nullptr, long ldc2 = 0, int n1 = 0) {
   const long total = (long)M * N;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const int row = (int)(e / N), col = (int)(e % N);
     float s = 0.f;
     for (int z = 0; z < nz; ++z) s += slab[z * zstride + e];
+    if (out2 && col >= n1) {  // fused pair: columns past n1 belong to the second product
+      out2[(long)row * ldc2 + col - n1] = s;
+      continue;
+    }
     if (bias0) s += bias0[col];
     if (bias1) s += bias1[col];
     if (outb) {  // bf16 output (beta unused)
@@ -663,6 +668,49 @@ void launch_bwd_bf16(dim3 grid, hipStream_t s, const bf16_t* dgn, const bf16_t* 
 
 }  // namespace
 
+extern "C" size_t sv_gemm_bf16_workspace(int M, int N, int K);
+extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, const bf16_t* B, long ldb, float* C,
+                            long ldc, const float* bias0, const float* bias1, float beta, float* workspace,
+                            hipStream_t stream);
+// C1 = A . B1^T and C2 = A . B2^T (fp32 out, no bias / beta) in one launch over the shared A:
+// the split-K plan of sv_gemm_bf16(M, N1, K), so each product sums exactly as the single GEMM
+// does (bit-identical); falls back to two calls where the fused form does not apply.
+// workspace: sv_gemm_bf16_dual_workspace bytes
+size_t sv_gemm_bf16_dual_workspace(int M, int N1, int N2, int K) {
+  const BPlan p = plan_bf16(M, N1, K);
+  const size_t fused = p.splitk > 1 ? (size_t)p.splitk * M * (N1 + N2) * sizeof(float) : 0;
+  return std::max(fused, std::max(sv_gemm_bf16_workspace(M, N1, K), sv_gemm_bf16_workspace(M, N2, K)));
+}
+int sv_gemm_bf16_dual(int M, int N1, int N2, int K, const bf16_t* A, long lda, const bf16_t* B1, long ldb1, float* C1,
+                      long ldc1, const bf16_t* B2, long ldb2, float* C2, long ldc2, float* workspace,
+                      hipStream_t stream) {
+  static const int on = [] {
+    const char* e = getenv("SV_DW_DUAL");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  const BPlan p = plan_bf16(M, N1, K);
+  const bool fused = on && p.bm == G256_BM && p.splitk > 1 && gemm256_ok(M, N1 + N2, K) && N1 % G256_BM == 0 &&
+                     N2 % G256_BM == 0 && workspace && g256_variant(workspace, N1 + N2, nullptr, nullptr) == 2 &&
+                     ldb1 % 8 == 0 && ldb2 % 8 == 0 && lda % 8 == 0 && !(((uintptr_t)A | (uintptr_t)B1 | (uintptr_t)B2) & 15);
+  if (!fused) {
+    int rc = sv_gemm_bf16(M, N1, K, A, lda, B1, ldb1, C1, ldc1, nullptr, nullptr, 0.f, workspace, stream);
+    if (rc) return rc;
+    return sv_gemm_bf16(M, N2, K, A, lda, B2, ldb2, C2, ldc2, nullptr, nullptr, 0.f, workspace, stream);
+  }
+  const int N = N1 + N2;
+  const int tiles = (M / G256_BM) * (N / G256_BM);
+  const long slab = (long)M * N;
+  hipLaunchKernelGGL((gemm_bf16_8q_kernel<G8_SLAB, 0>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream, A, lda, B1,
+                     ldb1, (void*)workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr, 0.f, G256AFrag{},
+                     G256Dual{B2, ldb2, N1});
+  SV_LAUNCH_CHECK();
+  const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
+  hipLaunchKernelGGL(slab_reduce_bf_kernel, dim3(grid), dim3(256), 0, stream, workspace, p.splitk, slab, C1, ldc1, M, N,
+                     0.f, nullptr, nullptr, nullptr, C2, ldc2, N1);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
 extern "C" size_t sv_gemm_bf16_workspace(int M, int N, int K) {
   const BPlan p = plan_bf16(M, N, K);
   return p.splitk > 1 ? (size_t)p.splitk * M * N * sizeof(float) : 0;
@@ -1028,6 +1076,7 @@ BBwdWs carve_bbwd(char* base, int T, int B, int F, int H) {
   size_t g = sv_gemm_bf16_workspace(4 * H, H, TBp);
   g = std::max(g, sv_gemm_bf16_workspace(4 * H, F, TBp));
   g = std::max(g, sv_gemm_bf16_workspace(T * B, F, 4 * H));
+  g = std::max(g, sv_gemm_bf16_dual_workspace(4 * H, H, F, TBp));
   w.gws = (float*)take(g);
   w.gws2 = (float*)take(g);  // the weight-gradient stream's own split-K slabs (stack bwd)
   w.total = off;
@@ -1092,9 +1141,8 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       hipStream_t sw = pbwd_dw_side() ? side[L + l] : main;
       if (sw != main && (e = hipStreamWaitEvent(sw, ev[0], 0)) != hipSuccess) return (int)e;
       float* gw = sw != main ? ws.gws2 : ws.gws;
-      if ((rc = sv_gemm_bf16(4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, gw, sw)))
-        return rc;
-      if ((rc = sv_gemm_bf16(4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, gw, sw)))
+      if ((rc = sv_gemm_bf16_dual(4 * H, H, Fl, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, xT[l], ld_xT[l], dw_ih[l],
+                                  Fl, gw, sw)))
         return rc;
       if (!dbk) {
         hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
@@ -1144,9 +1192,9 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
         if ((e = hipStreamWaitEvent(sw, ev[l * nch], 0)) != hipSuccess) return (int)e;
       }
       float* gw = sw != main ? ws.gws2 : ws.gws;
-      rc = sv_gemm_bf16(4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, gw, sw);
-      if (rc) return rc;
-      rc = sv_gemm_bf16(4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, gw, sw);
+      // dW_hh and dW_ih in one pass over dG^T (falls back to two GEMMs for layer 0's F = 40)
+      rc = sv_gemm_bf16_dual(4 * H, H, Fl, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, xT[l], ld_xT[l], dw_ih[l], Fl, gw,
+                             sw);
       if (rc) return rc;
       if (!dbk) {
         hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],

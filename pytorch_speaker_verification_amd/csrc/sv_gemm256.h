@@ -52,6 +52,13 @@ enum { G256_STORE = 0, G256_SLAB = 1 };
 // (b / 32) % (bm / 32), k-step s.  A k-tile of 64 never crosses a gate (kg % 64 == 0), so a
 // 256 x 64 A tile is 8 row groups x 4 k-steps = 32 whole KB: one per wave instruction, copied
 // to LDS as is, and each lane's MFMA fragment is its own 16 B of one KB (conflict-free reads).
+// second B operand of a fused pair of GEMMs sharing A (C = A . [B ; B2]^T): N-tiles at and past
+// n1 read B2 (the backward's dW_hh and dW_ih of one layer: one pass over dG^T for both)
+struct G256Dual {
+  const bf16_t* B2;
+  long ldb2;
+  int n1;
+};
 struct G256AFrag {
   const bf16_t* base;  // dgf
   long fs;             // slot size (elements)
@@ -561,7 +568,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
                                                              long ldc, long slab, int M, int N, int K, int kchunk,
                                                              const float* __restrict__ bias0,
                                                              const float* __restrict__ bias1, float beta,
-                                                             G256AFrag af = G256AFrag{}) {
+                                                             G256AFrag af = G256AFrag{}, G256Dual dual = G256Dual{}) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
@@ -574,7 +581,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
   const int wr = w >> 2, wc = w & 3;
   G256Stage sa, sb;
   if constexpr (!AF) sa.init(A, lda, tm * G256_BM, kbeg, tid);
-  sb.init(B, ldb, tn * G256_BM, kbeg, tid);
+  if (dual.B2 && tn * G256_BM >= dual.n1)
+    sb.init(dual.B2, dual.ldb2, tn * G256_BM - dual.n1, kbeg, tid);
+  else
+    sb.init(B, ldb, tn * G256_BM, kbeg, tid);
   constexpr int OPB = G256_BM * G256_BK * 2;
   // fragment-order A: chunk i of wave w is KB c = (2 i + w / 4) * 4 + w % 4 (row group 2 i + w / 4,
   // k-step w % 4), so a chunk is the 64 rows 64 i .. 64 i + 63 as for the row-major operand
