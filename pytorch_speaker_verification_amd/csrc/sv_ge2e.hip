@@ -479,42 +479,56 @@ __global__ __launch_bounds__(256) void ge2e_prep_kernel(const float* __restrict_
                             ((p0.z + p1.z) + p2.z) + p3.z, ((p0.w + p1.w) + p2.w) + p3.w};
   const float fm = (float)M;
   const float4 c = float4{sum.x / fm, sum.y / fm, sum.z / fm, sum.w / fm};
-  const float cn = sqrtf(wave_sum(c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w));
+  const float invm1 = 1.0f / (float)(M - 1);
+  // every lane-partial first (|c|^2; per row |e|^2, |u|^2, e.u), then ONE butterfly over all of
+  // them: the 3 RW + 1 shuffle chains are independent, so their LDS latencies overlap
+  float v[3 * RW + 1];
+  float4 uu[RW];
+  v[3 * RW] = c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w;
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    const float4 x = e[q];
+    uu[q] = float4{(sum.x - x.x) * invm1, (sum.y - x.y) * invm1, (sum.z - x.z) * invm1, (sum.w - x.w) * invm1};
+    const float4 u = uu[q];
+    v[3 * q] = x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+    v[3 * q + 1] = u.x * u.x + u.y * u.y + u.z * u.z + u.w * u.w;
+    v[3 * q + 2] = x.x * u.x + x.y * u.y + x.z * u.z + x.w * u.w;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+#pragma unroll
+    for (int i = 0; i < 3 * RW + 1; ++i) v[i] += __shfl_xor(v[i], o, 64);
+  }
+  const float cn = sqrtf(v[3 * RW]);
   const float icn = 1.0f / fmaxf(cn, EPS_COS);
   if (w == 0) {
     if (dok) *reinterpret_cast<float4*>(Chat + (long)j * D + 4 * lane) = float4{c.x * icn, c.y * icn, c.z * icn, c.w * icn};
     if (lane == 0) Cn[j] = cn;
   }
-  const float invm1 = 1.0f / (float)(M - 1);
 #pragma unroll
   for (int q = 0; q < RW; ++q) {
     const int i = w + 4 * q;
     if (i >= M) break;
     const long r = (long)j * M + i;
-    const float4 x = e[q];
-    const float4 u = float4{(sum.x - x.x) * invm1, (sum.y - x.y) * invm1, (sum.z - x.z) * invm1, (sum.w - x.w) * invm1};
-    const float ne = sqrtf(wave_sum(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w));
-    const float nu = sqrtf(wave_sum(u.x * u.x + u.y * u.y + u.z * u.z + u.w * u.w));
+    const float4 x = e[q], u = uu[q];
+    const float ne = sqrtf(v[3 * q]), nu = sqrtf(v[3 * q + 1]);
     const float ie = 1.0f / fmaxf(ne, EPS_COS), iu = 1.0f / fmaxf(nu, EPS_COS);
-    const float4 xh = float4{x.x * ie, x.y * ie, x.z * ie, x.w * ie};
-    const float4 uh = float4{u.x * iu, u.y * iu, u.z * iu, u.w * iu};
     if (dok) {
-      *reinterpret_cast<float4*>(Ehat + r * D + 4 * lane) = xh;
-      *reinterpret_cast<float4*>(Uhat + r * D + 4 * lane) = uh;
+      *reinterpret_cast<float4*>(Ehat + r * D + 4 * lane) = float4{x.x * ie, x.y * ie, x.z * ie, x.w * ie};
+      *reinterpret_cast<float4*>(Uhat + r * D + 4 * lane) = float4{u.x * iu, u.y * iu, u.z * iu, u.w * iu};
     }
-    const float dot = wave_sum(xh.x * uh.x + xh.y * uh.y + xh.z * uh.z + xh.w * uh.w);
     if (lane == 0) {
       En[r] = ne;
       Un[r] = nu;
-      rawd[r] = dot;
+      rawd[r] = v[3 * q + 2] * ie * iu;  // cos(e, u) = e.u / (|e| |u|)
     }
   }
   (void)red;
 }
 
-// F2: 8 rows per workgroup (two per wave, sharing every C^ read).  Cs [N][D + 4] fp32 in LDS
-// (16-B padded rows: the 16 lanes of a ds_read_b128 group hit disjoint banks); the rows' E^ in
-// Es [8][D]; per-row dcos vectors in Vs [8][N].
+// F2: 4 rows per workgroup, one per wave (160 workgroups at c2, so the rows' serial work is
+// spread over more CUs).  Cs [N][D + 4] fp32 in LDS (16-B padded rows: the 16 lanes of a
+// ds_read_b128 group hit disjoint banks); the rows' E^ in Es [4][D]; per-row dcos in Vs [4][N].
 __global__ __launch_bounds__(256) void ge2e_rows_kernel(const float* __restrict__ Chat, const float* __restrict__ Ehat,
                                                         const float* __restrict__ rawd, int Bl, int M, int N, int D,
                                                         int ldc, const float* __restrict__ wp,
@@ -525,137 +539,137 @@ __global__ __launch_bounds__(256) void ge2e_rows_kernel(const float* __restrict_
   extern __shared__ __attribute__((aligned(16))) float gsm[];
   const int LDC = D + 4;
   float* Cs = gsm;                    // [N][LDC]
-  float* Es = Cs + (size_t)N * LDC;   // [8][D]
-  float* Vs = Es + 8 * D;             // [8][N]
+  float* Es = Cs + (size_t)N * LDC;   // [4][D]
+  float* Vs = Es + 4 * D;             // [4][N]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int D4 = D / 4, NQ = N * D4;
-  for (int q0 = tid; q0 < NQ; q0 += 256 * 8) {  // 8 loads in flight per thread
-    float4 v[8];
+  // global -> LDS copy of C^ (distinct address spaces: the unrolled loads issue back to back)
+#pragma unroll 8
+  for (int q = tid; q < NQ; q += 256) {
+    const int row = q / D4, col = (q - row * D4) * 4;
+    *reinterpret_cast<float4*>(Cs + row * LDC + col) = *reinterpret_cast<const float4*>(Chat + (long)row * D + col);
+  }
+  const int r = blockIdx.x * 4 + w;   // this wave's row
+  if (r < Bl)
+    for (int c = lane * 4; c < D; c += 256)
+      *reinterpret_cast<float4*>(Es + w * D + c) = *reinterpret_cast<const float4*>(Ehat + (long)r * D + c);
+  __syncthreads();
+  if (r >= Bl) return;
+  const float wv = *wp, bv = *bp;
+  const int sg = r / M;
+  const float rd = rawd[r];
+  // cosines: KS speaker lanes x DS d-slices (DS = 1 for N > 32: lane k and k + 64 over all of
+  // D; small N splits D so the wave's lanes all work, the slices then meet by a butterfly), E^
+  // broadcast; four independent partial sums (d mod 4), added pairwise at the end
+  int DS = N <= 8 ? 8 : N <= 16 ? 4 : N <= 32 ? 2 : 1;
+  while (DS > 1 && D % (4 * DS)) DS >>= 1;
+  const int KS = 64 / DS, dlen = D / DS;
+  const int kl = lane & (KS - 1), d0 = (lane / KS) * dlen;
+  float cv[2] = {0.f, 0.f};
+  const float* e0 = Es + w * D;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int q = q0 + 256 * u;
-      if (q < NQ) v[u] = *reinterpret_cast<const float4*>(Chat + (long)(q / D4) * D + (q % D4) * 4);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int q = q0 + 256 * u;
-      if (q < NQ) *reinterpret_cast<float4*>(Cs + (q / D4) * LDC + (q % D4) * 4) = v[u];
+  for (int hk = 0; hk < 2; ++hk) {
+    const int k = kl + 64 * hk;
+    if (k < N) {
+      float4 a = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+      for (int c = d0; c < d0 + dlen; c += 4) {
+        const float4 cc = *reinterpret_cast<const float4*>(Cs + k * LDC + c);
+        const float4 x0 = *reinterpret_cast<const float4*>(e0 + c);
+        a.x += x0.x * cc.x;
+        a.y += x0.y * cc.y;
+        a.z += x0.z * cc.z;
+        a.w += x0.w * cc.w;
+      }
+      cv[hk] = (a.x + a.y) + (a.z + a.w);
     }
   }
-  const int r0 = blockIdx.x * 8 + 2 * w;   // this wave's rows r0, r0 + 1
+  for (int o = KS; o < 64; o <<= 1) cv[0] += __shfl_xor(cv[0], o, 64);  // lane k < KS: speaker k
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
-    if (r0 + h < Bl)
-      for (int c = lane * 4; c < D; c += 256)
-        *reinterpret_cast<float4*>(Es + (2 * w + h) * D + c) = *reinterpret_cast<const float4*>(Ehat + (long)(r0 + h) * D + c);
-  __syncthreads();
-  if (r0 >= Bl) return;
-  const float wv = *wp, bv = *bp;
-  // cosines: lane k (and k + 64) over D, both rows at once, E^ broadcast
-  float cv[2][2] = {{0.f, 0.f}, {0.f, 0.f}};  // [row][speaker half]
-  const float* e0 = Es + (2 * w) * D;
-  const float* e1 = e0 + D;
+  for (int hk = 0; hk < 2; ++hk)
+    if (lane + 64 * hk == sg) cv[hk] = rd;  // get_cossim's diagonal overwrite (utils.py:112-113)
+  // row softmax: S = w (cos + 1e-6) + b;  lz = log(sum_k e^S + 1e-6)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int hk = 0; hk < 2; ++hk)
+    if (lane + 64 * hk < N) mx = fmaxf(mx, wv * (cv[hk] + EPS_SIM) + bv);
+  mx = fmaxf(wave_max(mx), 0.f);
+  float z = 0.f;
+#pragma unroll
+  for (int hk = 0; hk < 2; ++hk)
+    if (lane + 64 * hk < N) z += __expf(wv * (cv[hk] + EPS_SIM) + bv - mx);
+  z = wave_sum(z);
+  const float lz = mx + logf(z + EPS_LOG * __expf(-mx));
+  // row backward (gloss = 1): dS = p - delta, dcos = w dS
+  float a = 0.f, dw = 0.f, db = 0.f;
 #pragma unroll
   for (int hk = 0; hk < 2; ++hk) {
     const int k = lane + 64 * hk;
     if (k < N) {
-      float a0 = 0.f, a1 = 0.f;
-#pragma unroll 8
-      for (int c = 0; c < D; c += 4) {
-        const float4 cc = *reinterpret_cast<const float4*>(Cs + k * LDC + c);
-        const float4 x0 = *reinterpret_cast<const float4*>(e0 + c);
-        const float4 x1 = *reinterpret_cast<const float4*>(e1 + c);
-        a0 += x0.x * cc.x;
-        a0 += x0.y * cc.y;
-        a0 += x0.z * cc.z;
-        a0 += x0.w * cc.w;
-        a1 += x1.x * cc.x;
-        a1 += x1.y * cc.y;
-        a1 += x1.z * cc.z;
-        a1 += x1.w * cc.w;
-      }
-      cv[0][hk] = a0;
-      cv[1][hk] = a1;
+      const float cp = cv[hk] + EPS_SIM;
+      const float p = __expf(wv * cp + bv - lz);
+      const float ds = p - (k == sg ? 1.0f : 0.0f);
+      const float dcv = wv * ds;
+      a += dcv * cv[hk];
+      dw += ds * cp;
+      db += ds;
+      const float off = (k == sg) ? 0.f : dcv;
+      Vs[w * N + k] = off;
+      cos[(long)r * ldc + k] = cv[hk];
+      dcos[(long)r * ldc + k] = off;
+      if (k == sg) dcd[r] = dcv;
     }
   }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int r = r0 + h;
-    if (r >= Bl) break;
-    const int sg = r / M;
-    const float rd = rawd[r];
-#pragma unroll
-    for (int hk = 0; hk < 2; ++hk)
-      if (lane + 64 * hk == sg) cv[h][hk] = rd;  // get_cossim's diagonal overwrite (utils.py:112-113)
-    // row softmax: S = w (cos + 1e-6) + b;  lz = log(sum_k e^S + 1e-6)
-    float mx = -INFINITY;
-#pragma unroll
-    for (int hk = 0; hk < 2; ++hk)
-      if (lane + 64 * hk < N) mx = fmaxf(mx, wv * (cv[h][hk] + EPS_SIM) + bv);
-    mx = fmaxf(wave_max(mx), 0.f);
-    float z = 0.f;
-#pragma unroll
-    for (int hk = 0; hk < 2; ++hk)
-      if (lane + 64 * hk < N) z += __expf(wv * (cv[h][hk] + EPS_SIM) + bv - mx);
-    z = wave_sum(z);
-    const float lz = mx + logf(z + EPS_LOG * __expf(-mx));
-    // row backward (gloss = 1): dS = p - delta, dcos = w dS
-    float a = 0.f, dw = 0.f, db = 0.f;
-#pragma unroll
-    for (int hk = 0; hk < 2; ++hk) {
-      const int k = lane + 64 * hk;
-      if (k < N) {
-        const float cp = cv[h][hk] + EPS_SIM;
-        const float p = __expf(wv * cp + bv - lz);
-        const float ds = p - (k == sg ? 1.0f : 0.0f);
-        const float dcv = wv * ds;
-        a += dcv * cv[h][hk];
-        dw += ds * cp;
-        db += ds;
-        const float off = (k == sg) ? 0.f : dcv;
-        Vs[(2 * w + h) * N + k] = off;
-        cos[(long)r * ldc + k] = cv[h][hk];
-        dcos[(long)r * ldc + k] = off;
-        if (k == sg) dcd[r] = dcv;
-      }
-    }
-    a = wave_sum(a);
-    dw = wave_sum(dw);
-    db = wave_sum(db);
-    if (lane == 0) {
-      per[r] = lz - (wv * (rd + EPS_SIM) + bv);
-      alpha[r] = a;
-      dwdb_rows[r] = dw;
-      dwdb_rows[Bl + r] = db;
-    }
+  a = wave_sum(a);
+  dw = wave_sum(dw);
+  db = wave_sum(db);
+  if (lane == 0) {
+    per[r] = lz - (wv * (rd + EPS_SIM) + bv);
+    alpha[r] = a;
+    dwdb_rows[r] = dw;
+    dwdb_rows[Bl + r] = db;
   }
-  // G1_r = sum_k dcos_off[r,k] C^_k for both rows: lanes over d (4 each), speakers in order
+  // G1_r = sum_k dcos_off[r,k] C^_k: lanes over d (4 each), even / odd speakers in two
+  // accumulators, added at the end
   __builtin_amdgcn_wave_barrier();
-  const bool two = r0 + 1 < Bl;
+  const float* vr = Vs + w * N;
   for (int c = lane * 4; c < D; c += 256) {
     float4 g0 = float4{0.f, 0.f, 0.f, 0.f}, g1 = g0;
-#pragma unroll 8
-    for (int k = 0; k < N; ++k) {
-      const float d0 = Vs[(2 * w) * N + k], d1 = Vs[(2 * w + 1) * N + k];
-      const float4 cc = *reinterpret_cast<const float4*>(Cs + k * LDC + c);
-      g0.x += d0 * cc.x;
-      g0.y += d0 * cc.y;
-      g0.z += d0 * cc.z;
-      g0.w += d0 * cc.w;
-      g1.x += d1 * cc.x;
-      g1.y += d1 * cc.y;
-      g1.z += d1 * cc.z;
-      g1.w += d1 * cc.w;
+    int k = 0;
+#pragma unroll 4
+    for (; k + 1 < N; k += 2) {
+      const float d0 = vr[k], d1 = vr[k + 1];
+      const float4 c0 = *reinterpret_cast<const float4*>(Cs + k * LDC + c);
+      const float4 c1 = *reinterpret_cast<const float4*>(Cs + (k + 1) * LDC + c);
+      g0.x += d0 * c0.x;
+      g0.y += d0 * c0.y;
+      g0.z += d0 * c0.z;
+      g0.w += d0 * c0.w;
+      g1.x += d1 * c1.x;
+      g1.y += d1 * c1.y;
+      g1.z += d1 * c1.z;
+      g1.w += d1 * c1.w;
     }
-    *reinterpret_cast<float4*>(G1 + (long)r0 * D + c) = g0;
-    if (two) *reinterpret_cast<float4*>(G1 + (long)(r0 + 1) * D + c) = g1;
+    if (k < N) {
+      const float d0 = vr[k];
+      const float4 c0 = *reinterpret_cast<const float4*>(Cs + k * LDC + c);
+      g0.x += d0 * c0.x;
+      g0.y += d0 * c0.y;
+      g0.z += d0 * c0.z;
+      g0.w += d0 * c0.w;
+    }
+    *reinterpret_cast<float4*>(G1 + (long)r * D + c) = float4{g0.x + g1.x, g0.y + g1.y, g0.z + g1.z, g0.w + g1.w};
   }
 }
 
-// F3: workgroup (speaker k, d slice q of 64): beta_k, dC^_k[slice], dC_k[slice], then dE of
-// speaker k's rows over the slice.  Rows in a fixed order: wave w takes rows w, w + 4, ... (16
-// rows' loads in flight); the four wave partials are added in wave order.
-__global__ __launch_bounds__(256) void ge2e_cols_kernel(int Bl, int M, int N, int D, int ldc,
+// F3: workgroup (speaker k, d slice q of 64), GF_COLW waves: beta_k, dC^_k[slice], dC_k[slice],
+// then dE of speaker k's rows over the slice.  The row sum runs with lane = 16 s + t: t covers
+// 4 consecutive d (16-B loads), s one of 4 row sub-groups, so a wave's batch of GF_COLU loads
+// spans 4 GF_COLU rows and the whole c2 batch (640 rows) is one round trip to L2; rows in a fixed
+// order per (wave, sub-group), the sub-groups then the waves added in a fixed order.
+#define GF_COLW 16
+#define GF_COLU 10
+__global__ __launch_bounds__(64 * GF_COLW) void ge2e_cols_kernel(int Bl, int M, int N, int D, int ldc,
                                                         const float* __restrict__ Chat, const float* __restrict__ Cn,
                                                         const float* __restrict__ Ehat, const float* __restrict__ Uhat,
                                                         const float* __restrict__ En, const float* __restrict__ Un,
@@ -665,87 +679,115 @@ __global__ __launch_bounds__(256) void ge2e_cols_kernel(int Bl, int M, int N, in
                                                         const float* __restrict__ G1, const float* __restrict__ per,
                                                         const float* __restrict__ dwdb_rows, float* __restrict__ dE,
                                                         float* __restrict__ loss, float* __restrict__ dwdb) {
-  __shared__ float part[4][64];
-  __shared__ float bpart[4];
+  constexpr int NW = GF_COLW, U = GF_COLU;
+  __shared__ __attribute__((aligned(16))) float part[NW][64];
+  __shared__ float bpart[NW];
   __shared__ float dCs[64];
+  __shared__ float dUs[GF_MMAX][64];
+  __shared__ float red3[3][NW];
   const int k = blockIdx.x, q = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int d = q * 64 + lane;
-  const bool dok = d < D;
-  constexpr int U = 16;
-  float acc = 0.f, bsum = 0.f;
-  int r = w;
-  for (; r + 4 * (U - 1) < Bl; r += 4 * U) {
-    float dc[U], ev[U], cv[U];
+  const int s = lane >> 4, t = lane & 15;
+  const int d4 = q * 64 + 4 * t;  // D % 4 == 0: the 4 values are all in range or all out
+  const bool d4ok = d4 < D;
+  float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  for (int r = 4 * w + s; r < Bl; r += 4 * NW * U) {
+    float dc[U], cv[U];
+    float4 ev[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long rr = r + 4 * u;
-      dc[u] = dcos[rr * ldc + k];
-      cv[u] = cos[rr * ldc + k];
-      ev[u] = dok ? Ehat[rr * D + d] : 0.f;
+      const unsigned rr = r + 4 * NW * u;  // 32-bit offsets: SGPR base + VGPR offset addressing
+      const bool ok = rr < (unsigned)Bl;
+      dc[u] = ok ? dcos[rr * (unsigned)ldc + k] : 0.f;
+      cv[u] = ok ? cos[rr * (unsigned)ldc + k] : 0.f;
+      ev[u] = (ok && d4ok) ? *reinterpret_cast<const float4*>(Ehat + (rr * (unsigned)D + d4)) : float4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      acc += dc[u] * ev[u];
+      acc.x += dc[u] * ev[u].x;
+      acc.y += dc[u] * ev[u].y;
+      acc.z += dc[u] * ev[u].z;
+      acc.w += dc[u] * ev[u].w;
       bsum += dc[u] * cv[u];
     }
   }
-  for (; r < Bl; r += 4) {
-    const float dc = dcos[(long)r * ldc + k];
-    if (dok) acc += dc * Ehat[(long)r * D + d];
-    bsum += dc * cos[(long)r * ldc + k];
+#pragma unroll
+  for (int o = 16; o <= 32; o <<= 1) {
+    acc.x += __shfl_xor(acc.x, o, 64);
+    acc.y += __shfl_xor(acc.y, o, 64);
+    acc.z += __shfl_xor(acc.z, o, 64);
+    acc.w += __shfl_xor(acc.w, o, 64);
+    bsum += __shfl_xor(bsum, o, 64);
   }
-  part[w][lane] = acc;
+  if (lane < 16) *reinterpret_cast<float4*>(&part[w][4 * t]) = acc;
   if (lane == 0) bpart[w] = bsum;
+  // this wave's dE row (speaker k's utterance w): operands loaded before the barrier, dU shared
+  // through LDS so the sum over the speaker's M rows needs no second trip to memory
+  const int d = q * 64 + lane;
+  const bool dok = d < D;
+  const bool mine = dok && w < M;
+  float dU = 0.f, gE = 0.f;
+  long rdx = 0;
+  if (mine) {
+    const int rr = k * M + w;
+    rdx = (long)rr * D + d;
+    const float un = Un[rr], en = En[rr], dd = dcd[rr];
+    const float iu = 1.0f / fmaxf(un, EPS_COS);
+    const float pu = un > EPS_COS ? 1.f : 0.f;
+    const float eh = Ehat[rdx], uh = Uhat[rdx];
+    dU = dd * (eh - rawd[rr] * uh * pu) * iu;
+    const float ie = 1.0f / fmaxf(en, EPS_COS);
+    const float pe = en > EPS_COS ? 1.f : 0.f;
+    gE = (G1[rdx] + dd * uh - alpha[rr] * eh * pe) * ie;
+    dUs[w][lane] = dU;
+  }
   __syncthreads();
   const float cn = Cn[k];
   const float icn = 1.0f / fmaxf(cn, EPS_COS);
   const float pc = cn > EPS_COS ? 1.f : 0.f;
-  const float beta = ((bpart[0] + bpart[1]) + bpart[2]) + bpart[3];
+  float beta = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) beta += bpart[i];
   if (tid < 64 && dok) {
-    const float dch = ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
+    float dch = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) dch += part[i][tid];
     dCs[tid] = (dch - beta * Chat[(long)k * D + d] * pc) * icn;
   }
   __syncthreads();
-  // dE of speaker k's rows over the slice: wave w takes rows w, w + 4, ...; sum_i dU by all
-  // four waves (each over all M rows, the same fixed order)
-  if (dok) {
-    const float dC = dCs[lane];
+  if (mine) {
     const float invM = 1.0f / (float)M, invm1 = 1.0f / (float)(M - 1);
     float sumdU = 0.f;
-    for (int i = 0; i < M; ++i) {
-      const int rr = k * M + i;
-      const float iu = 1.0f / fmaxf(Un[rr], EPS_COS);
-      const float pu = Un[rr] > EPS_COS ? 1.f : 0.f;
-      sumdU += dcd[rr] * (Ehat[(long)rr * D + d] - rawd[rr] * Uhat[(long)rr * D + d] * pu) * iu;
-    }
-    for (int i = w; i < M; i += 4) {
-      const int rr = k * M + i;
-      const long rd = (long)rr * D + d;
-      const float iu = 1.0f / fmaxf(Un[rr], EPS_COS);
-      const float pu = Un[rr] > EPS_COS ? 1.f : 0.f;
-      const float dU = dcd[rr] * (Ehat[rd] - rawd[rr] * Uhat[rd] * pu) * iu;
-      const float ie = 1.0f / fmaxf(En[rr], EPS_COS);
-      const float pe = En[rr] > EPS_COS ? 1.f : 0.f;
-      const float gE = (G1[rd] + dcd[rr] * Uhat[rd] - alpha[rr] * Ehat[rd] * pe) * ie;
-      dE[rd] = gE + dC * invM + (sumdU - dU) * invm1;
-    }
+    for (int i = 0; i < M; ++i) sumdU += dUs[i][lane];
+    dE[rdx] = gE + dCs[lane] * invM + (sumdU - dU) * invm1;
   }
-  if (k == 0 && q == 0) {  // loss = sum per, dw, db: fixed-order block sums
-    __shared__ float red[4];
+  if (k == 0 && q == 0) {  // loss = sum per, dw, db: fixed-order block sums (block-uniform branch)
     float l = 0.f, a = 0.f, b = 0.f;
-    for (int i = tid; i < Bl; i += 256) {
+    for (int i = tid; i < Bl; i += 64 * NW) {
       l += per[i];
       a += dwdb_rows[i];
       b += dwdb_rows[Bl + i];
     }
-    l = block_sum256(l, red);
-    a = block_sum256(a, red);
-    b = block_sum256(b, red);
+    l = wave_sum(l);
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) {
+      red3[0][w] = l;
+      red3[1][w] = a;
+      red3[2][w] = b;
+    }
+    __syncthreads();
     if (tid == 0) {
-      loss[0] = l;
-      dwdb[0] = a;
-      dwdb[1] = b;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+      for (int i = 0; i < NW; ++i) {
+        s0 += red3[0][i];
+        s1 += red3[1][i];
+        s2 += red3[2][i];
+      }
+      loss[0] = s0;
+      dwdb[0] = s1;
+      dwdb[1] = s2;
     }
   }
 }
@@ -767,11 +809,11 @@ extern "C" int sv_ge2e_train(const float* E, int N, int M, int D, const float* w
   hipLaunchKernelGGL(ge2e_prep_kernel, dim3(N), dim3(256), 0, stream, E, M, D, ws.Chat, ws.Cn, ws.Ehat, ws.Uhat,
                      ws.En, ws.Un, ws.rawd);
   SV_LAUNCH_CHECK();
-  const size_t lds = ((size_t)N * (D + 4) + 8 * (size_t)D + 8 * (size_t)N) * sizeof(float);
-  hipLaunchKernelGGL(ge2e_rows_kernel, dim3((Bl + 7) / 8), dim3(256), lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N,
+  const size_t lds = ((size_t)N * (D + 4) + 4 * (size_t)D + 4 * (size_t)N) * sizeof(float);
+  hipLaunchKernelGGL(ge2e_rows_kernel, dim3((Bl + 3) / 4), dim3(256), lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N,
                      D, Np, w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1);
   SV_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ge2e_cols_kernel, dim3(N, (D + 63) / 64), dim3(256), 0, stream, Bl, M, N, D, Np, ws.Chat, ws.Cn,
+  hipLaunchKernelGGL(ge2e_cols_kernel, dim3(N, (D + 63) / 64), dim3(64 * GF_COLW), 0, stream, Bl, M, N, D, Np, ws.Chat, ws.Cn,
                      ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.G1, per,
                      ws.dwdb_rows, dE, loss, dwdb);
   SV_LAUNCH_CHECK();
