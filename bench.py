@@ -245,6 +245,22 @@ def hbm_kernels(tr, N, M, D, dev, reps=50):
         tr.ge2e.backward(st, w, b)
     ms_ge = _timed(ge2e, dev, reps)
     ms_split = _timed(ge2e_split, dev, reps)
+    # the same 3 launches captured once in a HIP graph and replayed: the device-side time
+    # without the per-call host path (ctypes + argument marshalling) that bounds the eager loop
+    graph_us = None
+    try:
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            ge2e()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            ge2e()
+        graph_us = round(_timed(gr.replay, dev, reps) * 1e3, 2)
+    except Exception as ex:  # capture is a measurement aid only: report why it is absent
+        graph_us = f"capture failed: {type(ex).__name__}"
     by_ge = 3.0 * N * M * D * 4
     n = tr.n_pad
     pc, gc = tr.flat_p[:n].clone(), tr.flat_g[:n].clone().mul_(1e-3)
@@ -253,8 +269,10 @@ def hbm_kernels(tr, N, M, D, dev, reps=50):
     r = lambda by, ms: round(by / (ms * 1e-3) / 1e9, 1)  # noqa: E731
     return {"ge2e_fwd_bwd": {"avg_us": round(ms_ge * 1e3, 2), "algorithmic_bytes": by_ge,
                              "achieved_GBps": r(by_ge, ms_ge), "peak_GBps": MI355X_HBM_GBPS,
-                             "split_path_us": round(ms_split * 1e3, 2),
-                             "note": "fused 3-launch kernel (sv_ge2e_train); launch-latency bound at this size"},
+                             "split_path_us": round(ms_split * 1e3, 2), "hip_graph_replay_us": graph_us,
+                             "note": "fused 3-launch kernel (sv_ge2e_train); avg_us is the eager per-call loop "
+                                     "(host-path bound), hip_graph_replay_us the same launches replayed from a "
+                                     "HIP graph; launch-latency bound at this size"},
             "clip_sgd": {"avg_us": round(ms_cl * 1e3, 2), "algorithmic_bytes": by_cl,
                          "achieved_GBps": r(by_cl, ms_cl), "peak_GBps": MI355X_HBM_GBPS}}
 
@@ -273,6 +291,40 @@ def _ge2e_torch(E, w, b):
     S = w * cos + b
     pos = S.diagonal(dim1=0, dim2=2).transpose(0, 1)
     return (torch.log(torch.exp(S).sum(2) + 1e-6) - pos).sum()
+
+
+
+def dvector_inference(net, dev, S=16384, T=24, reps=3):
+    """d-vector extraction (dvector_create.py:96-101): S windows of T = 24 frames
+    (240 ms at a 10 ms hop) embedded by the trained net, no autograd state (dvector.embed_windows,
+    fp32 MFMA path), windows already in HBM; MIOpen nn.LSTM + Linear on the same windows beside it."""
+    from pytorch_speaker_verification_amd.dvector import embed_windows
+    F, H, L, P = DIMS
+    g = torch.Generator(device="cpu").manual_seed(24)
+    xw = torch.randn(S, T, F, generator=g).to(dev)
+    flops = sum(2.0 * S * T * 4 * H * ((F if l == 0 else H) + H) for l in range(L)) + 2.0 * S * H * P
+
+    def ours():
+        return embed_windows(net, xw, batch=S)
+    res = {"workload": f"{S} windows x T={T} x {F} mel, fp32 (dvector_create.py:96-101)"}
+    with torch.no_grad():
+        ms = _timed(ours, dev, reps)
+        res.update(ms_per_batch=round(ms, 3), windows_per_sec=round(S / (ms * 1e-3), 1),
+                   tflops=round(flops / (ms * 1e-3) / 1e12, 2),
+                   mfma_frac=round(flops / (ms * 1e-3) / 1e12 / MI355X_FP32_MFMA_TFLOPS, 4))
+        try:
+            lstm = torch.nn.LSTM(F, H, num_layers=L, batch_first=True).to(dev)
+            proj = torch.nn.Linear(H, P).to(dev)
+
+            def vendor():
+                y, _ = lstm(xw)
+                e = proj(y[:, -1])
+                return e / e.norm(dim=1, keepdim=True)
+            msv = _timed(vendor, dev, reps)
+            res["vendor_miopen"] = {"ms_per_batch": round(msv, 3), "windows_per_sec": round(S / (msv * 1e-3), 1)}
+        except Exception as ex:
+            res["vendor_miopen"] = f"unavailable: {type(ex).__name__}"
+    return res
 
 
 def vendor_baseline(N, M, T, dev, steps=3, dtype="f32"):
@@ -602,6 +654,8 @@ def main():
         if world == 1:
             log("hbm kernels / vendor baseline")
             out["hbm_kernels"] = hbm_kernels(tr, N, M, P, dev)
+            log("d-vector inference")
+            out["dvector_inference"] = dvector_inference(tr.net, dev)
             if not args.no_vendor:
                 out["vendor_baseline"] = vendor_baseline(N, M, T, dev, dtype=dtype)
                 if "bf16" in out:

@@ -526,10 +526,11 @@ __global__ __launch_bounds__(256) void ge2e_prep_kernel(const float* __restrict_
   (void)red;
 }
 
-// F2: 4 rows per workgroup, one per wave (160 workgroups at c2, so the rows' serial work is
-// spread over more CUs).  Cs [N][D + 4] fp32 in LDS (16-B padded rows: the 16 lanes of a
-// ds_read_b128 group hit disjoint banks); the rows' E^ in Es [4][D]; per-row dcos in Vs [4][N].
-__global__ __launch_bounds__(256) void ge2e_rows_kernel(const float* __restrict__ Chat, const float* __restrict__ Ehat,
+// F2: GF_ROWW rows per workgroup, one per wave (160 workgroups of 4 waves at c2: each row's
+// serial work in its own wave; 8 waves per workgroup measured slower: 11.2 vs 10.0 us at c2).  Cs [N][D + 4] fp32 in LDS (16-B padded rows: the 16 lanes of a
+// ds_read_b128 group hit disjoint banks); the rows' E^ in Es [GF_ROWW][D]; per-row dcos in Vs [GF_ROWW][N].
+#define GF_ROWW 4
+__global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __restrict__ Chat, const float* __restrict__ Ehat,
                                                         const float* __restrict__ rawd, int Bl, int M, int N, int D,
                                                         int ldc, const float* __restrict__ wp,
                                                         const float* __restrict__ bp, float* __restrict__ per,
@@ -539,17 +540,17 @@ __global__ __launch_bounds__(256) void ge2e_rows_kernel(const float* __restrict_
   extern __shared__ __attribute__((aligned(16))) float gsm[];
   const int LDC = D + 4;
   float* Cs = gsm;                    // [N][LDC]
-  float* Es = Cs + (size_t)N * LDC;   // [4][D]
-  float* Vs = Es + 4 * D;             // [4][N]
+  float* Es = Cs + (size_t)N * LDC;   // [GF_ROWW][D]
+  float* Vs = Es + GF_ROWW * D;       // [GF_ROWW][N]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int D4 = D / 4, NQ = N * D4;
   // global -> LDS copy of C^ (distinct address spaces: the unrolled loads issue back to back)
 #pragma unroll 8
-  for (int q = tid; q < NQ; q += 256) {
+  for (int q = tid; q < NQ; q += 64 * GF_ROWW) {
     const int row = q / D4, col = (q - row * D4) * 4;
     *reinterpret_cast<float4*>(Cs + row * LDC + col) = *reinterpret_cast<const float4*>(Chat + (long)row * D + col);
   }
-  const int r = blockIdx.x * 4 + w;   // this wave's row
+  const int r = blockIdx.x * GF_ROWW + w;   // this wave's row
   if (r < Bl)
     for (int c = lane * 4; c < D; c += 256)
       *reinterpret_cast<float4*>(Es + w * D + c) = *reinterpret_cast<const float4*>(Ehat + (long)r * D + c);
@@ -809,8 +810,8 @@ extern "C" int sv_ge2e_train(const float* E, int N, int M, int D, const float* w
   hipLaunchKernelGGL(ge2e_prep_kernel, dim3(N), dim3(256), 0, stream, E, M, D, ws.Chat, ws.Cn, ws.Ehat, ws.Uhat,
                      ws.En, ws.Un, ws.rawd);
   SV_LAUNCH_CHECK();
-  const size_t lds = ((size_t)N * (D + 4) + 4 * (size_t)D + 4 * (size_t)N) * sizeof(float);
-  hipLaunchKernelGGL(ge2e_rows_kernel, dim3((Bl + 3) / 4), dim3(256), lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N,
+  const size_t lds = ((size_t)N * (D + 4) + GF_ROWW * (size_t)D + GF_ROWW * (size_t)N) * sizeof(float);
+  hipLaunchKernelGGL(ge2e_rows_kernel, dim3((Bl + GF_ROWW - 1) / GF_ROWW), dim3(64 * GF_ROWW), lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N,
                      D, Np, w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1);
   SV_LAUNCH_CHECK();
   hipLaunchKernelGGL(ge2e_cols_kernel, dim3(N, (D + 63) / 64), dim3(64 * GF_COLW), 0, stream, Bl, M, N, D, Np, ws.Chat, ws.Cn,

@@ -75,10 +75,16 @@ def test_dp_two_ranks_equal_single_process(precision):
     # GEMM over the whole batch), so the updated fp32 weights differ by fp32 ulps; in bf16 such a
     # difference can flip the bf16 rounding of a weight operand at the next step (a 2^-8 relative
     # change of that element), which moves the step-2 loss by ~1e-4 relative
-    loss_rtol = 1e-5 if precision == "f32" else 1e-3
+    # (the same flips move single weights after the update; measured on MI355X, bf16: params
+    # max-abs 1.04e-5, losses 7.3e-4 relative over the steps; f32: 1.2e-7 / 1.1e-7)
+    loss_rtol = 1e-5 if precision == "f32" else 3e-3
+    p_atol = 1e-5 if precision == "f32" else 5e-5
     for rank, losses, sd, wb in res:
+        dev_p = max(float(np.abs(sd[k] - ref_sd[k]).max()) for k in ref_sd)
+        print(f"\nMEASURED dp2_vs_single.{precision} rank {rank} params max-abs {dev_p:.2e} "
+              f"loss rel {float(np.max(np.abs(np.array(losses) / np.array(ref_losses) - 1))):.2e}")
         np.testing.assert_allclose(losses[:1], ref_losses[:1], rtol=1e-5)
         np.testing.assert_allclose(losses, ref_losses, rtol=loss_rtol)
         for k in ref_sd:
-            np.testing.assert_allclose(sd[k], ref_sd[k], atol=1e-5, err_msg=k)
+            np.testing.assert_allclose(sd[k], ref_sd[k], atol=p_atol, err_msg=k)
         np.testing.assert_allclose(wb, [ge2e.w.item(), ge2e.b.item()], atol=1e-6)
