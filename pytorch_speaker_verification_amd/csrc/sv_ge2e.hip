@@ -527,8 +527,9 @@ __global__ __launch_bounds__(256) void ge2e_prep_kernel(const float* __restrict_
 }
 
 // F2: GF_ROWW rows per workgroup, one per wave (160 workgroups of 4 waves at c2: each row's
-// serial work in its own wave; 8 waves per workgroup measured slower: 11.2 vs 10.0 us at c2).  Cs [N][D + 4] fp32 in LDS (16-B padded rows: the 16 lanes of a
-// ds_read_b128 group hit disjoint banks); the rows' E^ in Es [GF_ROWW][D]; per-row dcos in Vs [GF_ROWW][N].
+// serial work in its own wave; 8 waves per workgroup measured slower, 11.2 vs 10.0 us at c2).
+// Cs [N][D + 4] fp32 in LDS (16-B padded rows: the 16 lanes of a ds_read_b128 group hit
+// disjoint banks); the rows' E^ in Es [GF_ROWW][D]; per-row dcos in Vs [GF_ROWW][N].
 #define GF_ROWW 4
 __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __restrict__ Chat, const float* __restrict__ Ehat,
                                                         const float* __restrict__ rawd, int Bl, int M, int N, int D,
