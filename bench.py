@@ -270,9 +270,9 @@ def hbm_kernels(tr, N, M, D, dev, reps=50):
     return {"ge2e_fwd_bwd": {"avg_us": round(ms_ge * 1e3, 2), "algorithmic_bytes": by_ge,
                              "achieved_GBps": r(by_ge, ms_ge), "peak_GBps": MI355X_HBM_GBPS,
                              "split_path_us": round(ms_split * 1e3, 2), "hip_graph_replay_us": graph_us,
-                             "note": "fused 3-launch kernel (sv_ge2e_train); avg_us is the eager per-call loop "
-                                     "(host-path bound), hip_graph_replay_us the same launches replayed from a "
-                                     "HIP graph; launch-latency bound at this size"},
+                             "note": "fused 3-launch kernel (sv_ge2e_train); avg_us: the trainer's eager per-call loop, "
+                                     "hip_graph_replay_us: the same launches replayed from a HIP graph (adds the "
+                                     "graph launch); launch- and L2-latency bound at this size"},
             "clip_sgd": {"avg_us": round(ms_cl * 1e3, 2), "algorithmic_bytes": by_cl,
                          "achieved_GBps": r(by_cl, ms_cl), "peak_GBps": MI355X_HBM_GBPS}}
 
@@ -323,7 +323,7 @@ def dvector_inference(net, dev, S=16384, T=24, reps=3):
             msv = _timed(vendor, dev, reps)
             res["vendor_miopen"] = {"ms_per_batch": round(msv, 3), "windows_per_sec": round(S / (msv * 1e-3), 1)}
         except Exception as ex:
-            res["vendor_miopen"] = f"unavailable: {type(ex).__name__}"
+            res["vendor_miopen"] = f"unavailable: {type(ex).__name__}: {str(ex)[:160]}"
     return res
 
 
