@@ -316,10 +316,13 @@ def dvector_inference(net, dev, S=16384, T=24, reps=3):
             lstm = torch.nn.LSTM(F, H, num_layers=L, batch_first=True).to(dev)
             proj = torch.nn.Linear(H, P).to(dev)
 
-            def vendor():
-                y, _ = lstm(xw)
-                e = proj(y[:, -1])
-                return e / e.norm(dim=1, keepdim=True)
+            def vendor():  # in chunks of 4096 windows: one 16384-window call fails inside MIOpen
+                outs = []
+                for i in range(0, S, 4096):
+                    y, _ = lstm(xw[i:i + 4096])
+                    e = proj(y[:, -1])
+                    outs.append(e / e.norm(dim=1, keepdim=True))
+                return torch.cat(outs)
             msv = _timed(vendor, dev, reps)
             res["vendor_miopen"] = {"ms_per_batch": round(msv, 3), "windows_per_sec": round(S / (msv * 1e-3), 1)}
         except Exception as ex:

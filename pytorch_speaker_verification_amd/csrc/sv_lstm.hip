@@ -194,13 +194,25 @@ __global__ __launch_bounds__(256) void rowsum_kernel(const float* __restrict__ X
                                                      float* __restrict__ out0, float* __restrict__ out1) {
   __shared__ float red[4];
   const float* x = X + (long)blockIdx.x * ld;
-  float s = 0.f;
+  // four independent 16-B loads in flight per thread per trip (a row is 400 KB at c2: one
+  // dependent load per trip left the kernel at ~5 TB/s), summed in a fixed order
   const int C4 = C / 4;
-  for (int c = threadIdx.x; c < C4; c += 256) {
-    const f32x4 v = reinterpret_cast<const f32x4*>(x)[c];
-    s += (v.x + v.y) + (v.z + v.w);
+  const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int c = threadIdx.x;
+  for (; c + 768 < C4; c += 1024) {
+    const f32x4 v0 = x4[c], v1 = x4[c + 256], v2 = x4[c + 512], v3 = x4[c + 768];
+    s0 += (v0.x + v0.y) + (v0.z + v0.w);
+    s1 += (v1.x + v1.y) + (v1.z + v1.w);
+    s2 += (v2.x + v2.y) + (v2.z + v2.w);
+    s3 += (v3.x + v3.y) + (v3.z + v3.w);
   }
-  for (int c = C4 * 4 + threadIdx.x; c < C; c += 256) s += x[c];
+  for (; c < C4; c += 256) {
+    const f32x4 v = x4[c];
+    s0 += (v.x + v.y) + (v.z + v.w);
+  }
+  float s = (s0 + s1) + (s2 + s3);
+  for (int c1 = C4 * 4 + threadIdx.x; c1 < C; c1 += 256) s += x[c1];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
