@@ -312,6 +312,11 @@ def dvector_inference(net, dev, S=16384, T=24, reps=3):
         res.update(ms_per_batch=round(ms, 3), windows_per_sec=round(S / (ms * 1e-3), 1),
                    tflops=round(flops / (ms * 1e-3) / 1e12, 2),
                    mfma_frac=round(flops / (ms * 1e-3) / 1e12 / MI355X_FP32_MFMA_TFLOPS, 4))
+        # the c3 mixed-precision forward on the same windows (bf16 operands, fp32 state)
+        ms16 = _timed(lambda: embed_windows(net, xw, batch=S, precision="bf16"), dev, reps)
+        res["bf16"] = {"ms_per_batch": round(ms16, 3), "windows_per_sec": round(S / (ms16 * 1e-3), 1),
+                       "tflops": round(flops / (ms16 * 1e-3) / 1e12, 2),
+                       "mfma_frac": round(flops / (ms16 * 1e-3) / 1e12 / MI355X_BF16_MFMA_TFLOPS, 4)}
         try:
             lstm = torch.nn.LSTM(F, H, num_layers=L, batch_first=True).to(dev)
             proj = torch.nn.Linear(H, P).to(dev)

@@ -12,7 +12,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .ops import embedder_forward
+from .ops import embedder_forward, embedder_forward_bf16
 
 WIN, HOP = 24, 12  # frames: int(.24/.01), int(.12/.01)
 
@@ -28,15 +28,20 @@ def window_frames(logmel, win=WIN, hop=HOP):
 
 
 @torch.no_grad()
-def embed_windows(net, windows, batch=16384):
-    """Embeddings [S, proj] of windows [S, win, nmels] with the module's weights (GPU)."""
+def embed_windows(net, windows, batch=16384, precision="f32"):
+    """Embeddings [S, proj] of windows [S, win, nmels] with the module's weights (GPU).
+    precision "bf16": the c3 mixed-precision forward (bf16 GEMM operands, fp32 accumulation and
+    state), no activations saved."""
+    if precision not in ("f32", "bf16"):
+        raise ValueError(f"precision must be 'f32' or 'bf16', got {precision!r}")
     dev = next(net.parameters()).device
     layers = net.LSTM_stack.layer_params()
     out = []
     x = torch.as_tensor(windows, dtype=torch.float32)
     for i in range(0, x.shape[0], batch):
         xb = x[i:i + batch].to(dev).contiguous()
-        emb, _ = embedder_forward(xb, layers, net.projection.weight, net.projection.bias, save=False)
+        fwd = embedder_forward_bf16 if precision == "bf16" else embedder_forward
+        emb, _ = fwd(xb, layers, net.projection.weight, net.projection.bias, save=False)
         out.append(emb)
     return torch.cat(out) if out else torch.zeros((0, net.projection.weight.shape[0]), device=dev)
 

@@ -49,3 +49,34 @@ def test_embed_windows_short_sequence_large_batch():
     with torch.no_grad():
         er = port(torch.tensor(x).cuda()).cpu().numpy()
     np.testing.assert_allclose(e, er, atol=5e-5)
+
+
+@pytest.mark.gpu
+def test_embed_windows_bf16_against_bf16_oracle():
+    """bf16 d-vectors (the c3 mixed-precision forward at T = 24, 512 windows) against the
+    bf16-operand oracle (oracle/lstm_bf16.py) and the fp32 path.  Measured on MI355X with these
+    (scale-2) weights: 4.9e-4 vs the oracle, 1.0e-3 vs fp32 (random-init net, 16384 windows:
+    1.4e-4 vs fp32, min cosine 0.9999997); tolerance 5e-3, the c3/c4 embedding bound."""
+    import recipe
+    from conftest import model_dims
+    from oracle import lstm_bf16
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    dims = (40, 768, 3, 256)
+    sd = recipe.make_weights(9, *dims, scale=2.0)
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    net = net.cuda()
+    x = recipe.make_frames(11, 512, 24, 40)
+    e16 = dvector.embed_windows(net, x, batch=512, precision="bf16").cpu().numpy()
+    e32 = dvector.embed_windows(net, x, batch=512).cpu().numpy()
+    eo, _ = lstm_bf16.embedder_forward(sd, x, 3, bf16=True)
+    eo = eo.numpy()
+    d_or = float(np.abs(e16 - eo).max())
+    d_32 = float(np.abs(e16 - e32).max())
+    print(f"\nMEASURED dvector_bf16 vs bf16 oracle max-abs {d_or:.2e}; vs fp32 {d_32:.2e}")
+    assert d_or <= 5e-3 and d_32 <= 5e-3, (d_or, d_32)
+    with pytest.raises(ValueError):
+        dvector.embed_windows(net, x[:4], precision="fp16")
