@@ -80,3 +80,9 @@ def test_embed_windows_bf16_against_bf16_oracle():
     assert d_or <= 5e-3 and d_32 <= 5e-3, (d_or, d_32)
     with pytest.raises(ValueError):
         dvector.embed_windows(net, x[:4], precision="fp16")
+
+
+def test_embed_windows_rejects_unknown_precision():
+    """The precision switch is validated before any device work (CPU-only check)."""
+    with pytest.raises(ValueError):
+        dvector.embed_windows(None, np.zeros((1, 24, 40), np.float32), precision="fp16")
