@@ -189,35 +189,40 @@ __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ 
     }
 }
 
-// row sums out[r] = sum_c X[r*ld + c], one block per row, fixed order
-__global__ __launch_bounds__(256) void rowsum_kernel(const float* __restrict__ X, long ld, int C,
-                                                     float* __restrict__ out0, float* __restrict__ out1) {
-  __shared__ float red[4];
+// row sums out[r] = sum_c X[r*ld + c], one block of RS_T threads per row, fixed order.
+// 512-thread blocks: 4 per CU resident, so the 4H = 3072 rows of c2 run as 3 full rounds of
+// 1024 blocks (256-thread blocks left a half-empty second round: 3072 / 2048)
+#define RS_T 512
+__global__ __launch_bounds__(RS_T) void rowsum_kernel(const float* __restrict__ X, long ld, int C,
+                                                      float* __restrict__ out0, float* __restrict__ out1) {
+  __shared__ float red[RS_T / 64];
   const float* x = X + (long)blockIdx.x * ld;
-  // four independent 16-B loads in flight per thread per trip (a row is 400 KB at c2: one
-  // dependent load per trip left the kernel at ~5 TB/s), summed in a fixed order
+  // four independent 16-B loads in flight per thread per trip (a row is 400 KB at c2), summed
+  // in a fixed order
   const int C4 = C / 4;
   const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   int c = threadIdx.x;
-  for (; c + 768 < C4; c += 1024) {
-    const f32x4 v0 = x4[c], v1 = x4[c + 256], v2 = x4[c + 512], v3 = x4[c + 768];
+  for (; c + 3 * RS_T < C4; c += 4 * RS_T) {
+    const f32x4 v0 = x4[c], v1 = x4[c + RS_T], v2 = x4[c + 2 * RS_T], v3 = x4[c + 3 * RS_T];
     s0 += (v0.x + v0.y) + (v0.z + v0.w);
     s1 += (v1.x + v1.y) + (v1.z + v1.w);
     s2 += (v2.x + v2.y) + (v2.z + v2.w);
     s3 += (v3.x + v3.y) + (v3.z + v3.w);
   }
-  for (; c < C4; c += 256) {
+  for (; c < C4; c += RS_T) {
     const f32x4 v = x4[c];
     s0 += (v.x + v.y) + (v.z + v.w);
   }
   float s = (s0 + s1) + (s2 + s3);
-  for (int c1 = C4 * 4 + threadIdx.x; c1 < C; c1 += 256) s += x[c1];
+  for (int c1 = C4 * 4 + threadIdx.x; c1 < C; c1 += RS_T) s += x[c1];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float t = (red[0] + red[1]) + (red[2] + red[3]);
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < RS_T / 64; ++i) t += red[i];
     out0[blockIdx.x] = t;
     if (out1) out1[blockIdx.x] = t;
   }
@@ -1228,7 +1233,7 @@ extern "C" int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* xT, lo
   rc = gemm_f32(1, 1, 4 * H, F, TBp, dgT, TBp, xT, ld_xT, dw_ih, F, nullptr, nullptr, 0.f, ws.gws, stream);
   if (rc) return rc;
   // db_ih = db_hh = row sums of dG^T
-  hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(256), 0, stream, dgT, (long)TBp, TBp, db_ih, db_hh);
+  hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(RS_T), 0, stream, dgT, (long)TBp, TBp, db_ih, db_hh);
   SV_LAUNCH_CHECK();
   // dx = dG W_ih: A = dG [TB, 4H], B = W_ih^T [F, 4H]
   if (dx_tm) {
@@ -1412,7 +1417,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
                     sw);
       if (rc) return rc;
     }
-    hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
+    hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(RS_T), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
                        db_hh ? db_hh[l] : nullptr);
     SV_LAUNCH_CHECK();
     if ((e = hipEventRecord(ev[L * nch + l], sw)) != hipSuccess) return (int)e;
