@@ -1,4 +1,6 @@
-# Builds the gfx950 HIP library behind the C ABI in include/sv_ge2e.h.
+# Builds the gfx950 HIP library behind the C ABI in include/sv_ge2e.h, plus its fault-injection
+# test build (libsv_ge2e_faultinj.so: the same sources with -DSV_FAULT_INJECTION, which exports
+# sv_test_set_fault; only tests/test_gpu_status.py loads it).
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CXXFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
@@ -6,8 +8,11 @@ PKG := pytorch_speaker_verification_amd
 SRC := $(wildcard $(PKG)/csrc/*.hip)
 OBJ := $(patsubst $(PKG)/csrc/%.hip,build/%.o,$(SRC))
 LIB := $(PKG)/libsv_ge2e.so
+# only sv_persist.hip reads SV_FAULT_INJECTION; the other objects are shared
+FAULT_OBJ := $(patsubst build/sv_persist.o,build/faultinj/sv_persist.o,$(OBJ))
+FAULT_LIB := $(PKG)/libsv_ge2e_faultinj.so
 
-all: $(LIB)
+all: $(LIB) $(FAULT_LIB)
 
 # the wide-tile persistent backward keeps its MFMA accumulators in VGPRs (all AGPRs hold weights)
 build/sv_persist3.o: EXTRA := -mllvm -amdgpu-mfma-vgpr-form=1
@@ -16,10 +21,17 @@ build/%.o: $(PKG)/csrc/%.hip $(wildcard $(PKG)/csrc/*.h) include/sv_ge2e.h
 	@mkdir -p build
 	$(HIPCC) $(CXXFLAGS) $(EXTRA) -c $< -o $@
 
+build/faultinj/sv_persist.o: $(PKG)/csrc/sv_persist.hip $(wildcard $(PKG)/csrc/*.h) include/sv_ge2e.h
+	@mkdir -p build/faultinj
+	$(HIPCC) $(CXXFLAGS) -DSV_FAULT_INJECTION -c $< -o $@
+
 $(LIB): $(OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)
 
+$(FAULT_LIB): $(FAULT_OBJ)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(FAULT_OBJ)
+
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(FAULT_LIB)
 
 .PHONY: all clean

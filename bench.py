@@ -172,12 +172,10 @@ def probe_ms(probes, key):
 def persist_kernels(B, H=768, cus=256):
     """(bwd, fwd) names of the persistent bf16 recurrence kernels the library picks for the upper
     layers at batch B (sv_persist.hip: the wide 32 x 64 tile where the 32-unit tile would need
-    64-row blocks; SV_PBWD3 / SV_PFWD3 = 0 keep the 32-unit tile)."""
-    wide = (H == 768 and (B + 31) // 32 * (H // 32) > cus and (B + 31) // 32 * (H // 64) <= cus
-            and os.environ.get("SV_PBWD3", "1") != "0")
+    64-row blocks)."""
+    wide = H == 768 and (B + 31) // 32 * (H // 32) > cus and (B + 31) // 32 * (H // 64) <= cus
     bwd = "lstm_persist3_bwd_bf16_kernel" if wide else "lstm_persist2_bwd_bf16_kernel"
-    fwd = "lstm_persist3_fwd_bf16_kernel" if wide and os.environ.get("SV_PFWD3", "1") != "0" else \
-        "lstm_persist2_fwd_bf16_kernel"
+    fwd = "lstm_persist3_fwd_bf16_kernel" if wide else "lstm_persist2_fwd_bf16_kernel"
     return bwd, fwd
 
 

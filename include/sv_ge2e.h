@@ -9,8 +9,9 @@
  *     aligned; scalars such as w, b, gloss are device pointers to one float (no host sync);
  *   - nothing is allocated, no global state is kept, no pointer is retained after return;
  *     scratch comes from a caller workspace of the size the matching *_workspace* returns;
- *     modes are explicit arguments (`products`), cross-workgroup counters live in a caller
- *     sync block (sv_sync_size), so calls with distinct buffers may run concurrently;
+ *     modes are explicit arguments (`products`, `schedule`; the library reads no environment
+ *     variables), cross-workgroup counters live in a caller sync block (sv_sync_size), so calls
+ *     with distinct buffers may run concurrently;
  *   - every launch goes to `stream` (pass the current stream of the tensor's device: the
  *     *_bwd functions are called from the autograd engine's worker thread);
  *   - return 0 on success, a hipError_t (> 0) from a failed launch, or a negative
@@ -26,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SV_ABI_VERSION 3
+#define SV_ABI_VERSION 4
 int sv_abi_version(void);
 
 /* ---- fp32 product modes (`products` argument of sv_gemm_f32 / sv_lstm_stack_fwd / _bwd; every
@@ -38,6 +39,23 @@ int sv_abi_version(void);
  *   2 / 3 diagnostics (split at LDS store / in registers everywhere). */
 #define SV_F32_EXACT 0
 #define SV_F32_BF16X6 1
+
+/* ---- schedule flags of the bf16 stack entry points (`schedule` argument of
+ * sv_lstm_stack_fwd_bf16 / sv_lstm_stack_bwd_bf16; 0 = the measured default):
+ *   SV_SCHED_AUTO       the layer wavefront (all layers in one launch) where every layer's grid
+ *                       fits co-resident, else one persistent recurrence launch per layer at
+ *                       H = 768, else per-step launches;
+ *   SV_SCHED_PER_LAYER  never the layer wavefront (it sums the upper layers' products in another
+ *                       order: results agree at bf16 level, not bit for bit);
+ *   SV_SCHED_PER_STEP   per-step launches, layer-pipelined over the side streams (bit-identical
+ *                       to the persistent per-layer schedule);
+ *   SV_SCHED_PERSIST    persistent per-layer recurrences for any H they support (64, 96, 768),
+ *                       not only H = 768. */
+#define SV_SCHED_AUTO 0
+#define SV_SCHED_PER_LAYER 1
+#define SV_SCHED_PER_STEP 2
+#define SV_SCHED_PERSIST 4
+#define SV_SCHED_MASK 7
 
 /* ---- dense fp32 MFMA GEMM (used by every op below; exported for tests) -----------------
  * C[M,N] = op(A) op(B) (+ bias0[n] + bias1[n]) (+ beta C).
@@ -86,8 +104,7 @@ int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float* x_tm, cons
 size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H);
 /* Whole-stack backward, layer-pipelined over streams (top layer first): each layer's reverse
  * chunks of steps on side[l], then (l > 0) the chunk's dx = dG W_ih GEMM that feeds layer l-1;
- * each finished chunk's share of dW_hh / dW_ih (K = its time columns, accumulated) runs on
- * side[L + l] beside the recurrence, then the bias row sums.  side: 2*L caller streams.
+ * then the layer's whole-T dW_hh / dW_ih GEMMs and bias row sums on side[l].  side: L streams.
  * xT/ld_xT: per-layer transposed inputs; dx[l] [T,B,H] for l > 0;
  * ev = L*ceil(T/chunk) + L + 1 caller events (ev[L*nch + l] = layer l's gradients done);
  * joins back into `main`.  probe (may be NULL): 2*L*ceil(T/chunk) caller events recorded on the
@@ -160,6 +177,19 @@ size_t sv_ge2e_cossim_workspace(int N, int M, int D, int Nc);
 int sv_ge2e_cossim(const float* E, int N, int M, int D, const float* C, int Nc, float* cos, float* workspace,
                    hipStream_t stream);
 int sv_ge2e_calc_loss(const float* S, int N, int M, int K, float* per, float* loss, hipStream_t stream);
+/* their backward passes (the autograd of utils.py:28, :72-115, :126-132):
+ *   dE = dC / M broadcast over the M utterances;
+ *   cossim: dE [N,M,D], dC [Nc,D] from dcos [N,M,Nc] -- gradient through the cosines against C_k
+ *   (k != j) and, on the diagonal, through E's own leave-one-out centroid U_ji = (sum_i' E_ji' -
+ *   E_ji) / (M - 1), as index_put's backward routes it (the overwritten entries give C nothing);
+ *   calc_loss: dS [N,M,K] from gloss (device scalar, NULL = 0) and gper [N,M] (NULL = 0):
+ *   dS_jik = (gloss + gper_ji) (e^{S_jik} / (sum_k e^{S_jik} + 1e-6) - [k == j]). */
+int sv_ge2e_centroids_bwd(const float* dC, int N, int M, int D, float* dE, hipStream_t stream);
+size_t sv_ge2e_cossim_bwd_workspace(int N, int M, int D, int Nc);
+int sv_ge2e_cossim_bwd(const float* E, int N, int M, int D, const float* C, int Nc, const float* dcos, float* dE,
+                       float* dC, float* workspace, hipStream_t stream);
+int sv_ge2e_calc_loss_bwd(const float* S, int N, int M, int K, const float* gloss, const float* gper, float* dS,
+                          hipStream_t stream);
 /* EER sweep (train_speech_embedder.py:134-149): per threshold, #{S > thr} over all of S [N,M2,Nc]
  * and over its diagonal k == j (exact integer counts, returned as float). */
 int sv_eer_counts(const float* S, int N, int M2, int Nc, const float* thresholds, int n_thr, float* cnt_all,
@@ -189,15 +219,15 @@ int sv_transpose_cast_bf16(const float* src, long ld_src, int R, int C, sv_bf16*
 int sv_lstm_layer_fwd_bf16(const sv_bf16* x_bf, int T, int B, int F, int H, const sv_bf16* w_ih_bf,
                            const sv_bf16* w_hh_bf, const float* b_ih, const float* b_hh, sv_bf16* gates, float* c_tm,
                            float* h_tm, sv_bf16* h_bf, sv_bf16* hT, hipStream_t stream);
-/* layer-pipelined stack forward in bf16 (as sv_lstm_stack_fwd; h_bf per layer [T+1,B,H]).
- * sync: the caller's sync block (below; required when the persistent recurrences run).
+/* stack forward in bf16 (as sv_lstm_stack_fwd; h_bf per layer [T+1,B,H]) under `schedule`
+ * (SV_SCHED_*).  sync: the caller's sync block (below; required when the persistent recurrences run).
  * probe (may be NULL): 2*L caller events recorded around each layer's persistent recurrence
  * launch (before / after; only when the persistent schedule runs) -- in-step kernel timing. */
 int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* x_bf, const sv_bf16* const* w_ih_bf,
                            const sv_bf16* const* w_hh_bf, const float* const* b_ih, const float* const* b_hh,
                            sv_bf16* const* gates, float* const* c_tm, float* const* h_tm, sv_bf16* const* h_bf,
                            sv_bf16* const* hT, int chunk, hipStream_t main, const hipStream_t* side,
-                           hipEvent_t* ev, void* sync, hipEvent_t* probe);
+                           hipEvent_t* ev, void* sync, hipEvent_t* probe, int schedule);
 size_t sv_lstm_layer_bwd_bf16_workspace(int T, int B, int F, int H);
 /* wihT_bf [F,4H], whhT_bf [H,4H]; dg_bf [T,B,4H] and dgT_bf [4H,T*Bp] are bf16 outputs */
 int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const sv_bf16* xT_bf, long ld_xT, const sv_bf16* wihT_bf,
@@ -206,8 +236,8 @@ int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const sv_bf16* xT_bf, lon
                            float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, float* workspace,
                            hipStream_t stream);
 
-/* layer-pipelined stack backward in bf16 (as sv_lstm_stack_bwd, 2*L side streams; fp32
- * master weights are transpose-cast per call; dg/dgT per layer bf16).  probe: as the bf16 stack
+/* stack backward in bf16 under `schedule` (as sv_lstm_stack_bwd, L side streams; fp32 master
+ * weights are transpose-cast per call; dg/dgT per layer bf16).  probe: as the bf16 stack
  * forward's, around each layer's persistent backward recurrence. */
 size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H);
 int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* const* xT, const long* ld_xT,
@@ -215,7 +245,8 @@ int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* con
                            const float* const* c_tm, const sv_bf16* const* hT, const float* dh_last,
                            sv_bf16* const* dg, sv_bf16* const* dgT, float* const* dx, float* const* dw_ih,
                            float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace, int chunk,
-                           hipStream_t main, const hipStream_t* side, hipEvent_t* ev, void* sync, hipEvent_t* probe);
+                           hipStream_t main, const hipStream_t* side, hipEvent_t* ev, void* sync, hipEvent_t* probe,
+                           int schedule);
 
 /* ---- persistent recurrences (one launch per layer for all T; sv_persist.hip).  The bf16 stack
  * forward uses them (by default when H = 768: W_hh held in registers) when the grid is
@@ -236,6 +267,13 @@ int sv_persist_fwd_ok(int B, int H);
 int sv_persist_bwd_ok(int B, int H);
 size_t sv_persist_bwd_scratch(int T, int B, int H);
 int sv_status_poison(const void* sync, float* x, int n, hipStream_t stream);
+/* data-parallel status agreement (a rank whose recurrence timed out must stop every rank's
+ * update): sv_status_to_flag writes the status's forward / backward bits as 0/1 floats into
+ * flag[0..1], two words of the gradient buffer that the SUM all-reduce carries; sv_status_merge
+ * ORs the bits whose reduced flag is nonzero back into the block's status, so sv_clip_sgd_step
+ * skips the update on every rank alike. */
+int sv_status_to_flag(const void* sync, float* flag, hipStream_t stream);
+int sv_status_merge(void* sync, const float* flag, hipStream_t stream);
 
 /* ---- clip_grad_norm_ + SGD step over one flat parameter group (train_speech_embedder.py:63-65)
  * p -= lr * min(1, max_norm / (|g|_2 + 1e-6)) * g; write_grad=1 also scales g in place.

@@ -13,6 +13,27 @@ import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsv_ge2e.so")
+# the fault-injection test build (Makefile `faultinj`): the same library plus sv_test_set_fault;
+# only tests load it, through use_library() before the first call
+FAULT_LIB_PATH = os.path.join(_HERE, "libsv_ge2e_faultinj.so")
+ABI_VERSION = 4
+
+# schedule flags of the bf16 stack (include/sv_ge2e.h SV_SCHED_*), by name
+SCHEDULES = {"auto": 0, "per_layer": 1, "per_step": 2, "persist": 5}  # persist: per-layer persistent, any H
+
+
+def schedule_flags(schedule):
+    """'auto' | 'per_layer' | 'per_step' | 'persist' (or an int of SV_SCHED_* flags) -> int."""
+    if schedule is None:
+        return 0
+    if isinstance(schedule, int):
+        if schedule & ~7:
+            raise ValueError(f"unknown schedule flags {schedule:#x}")
+        return schedule
+    try:
+        return SCHEDULES[schedule]
+    except KeyError:
+        raise ValueError(f"unknown schedule {schedule!r} (expected one of {sorted(SCHEDULES)})") from None
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -58,6 +79,10 @@ SIGNATURES = {
     "sv_ge2e_cossim_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
     "sv_ge2e_cossim": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _c_int, _P, _P, _P]),
     "sv_ge2e_calc_loss": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _P, _P]),
+    "sv_ge2e_centroids_bwd": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _P]),
+    "sv_ge2e_cossim_bwd_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
+    "sv_ge2e_cossim_bwd": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _c_int, _P, _P, _P, _P, _P]),
+    "sv_ge2e_calc_loss_bwd": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _P, _P, _P]),
     "sv_gemm_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int]),
     "sv_gemm_bf16": (_c_int, [_c_int, _c_int, _c_int, _P, _c_long, _P, _c_long, _P, _c_long, _P, _P, _c_float, _P,
                               _P]),
@@ -66,19 +91,21 @@ SIGNATURES = {
     "sv_transpose_cast_bf16": (_c_int, [_P, _c_long, _c_int, _c_int, _P, _c_long, _P]),
     "sv_lstm_layer_fwd_bf16": (_c_int, [_P, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_lstm_stack_fwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                        _P, _c_int, _P, _P, _P, _P, _P]),
+                                        _P, _c_int, _P, _P, _P, _P, _P, _c_int]),
     "sv_lstm_layer_bwd_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
     "sv_lstm_layer_bwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _P, _c_long, _P, _P, _P, _P, _P, _P, _c_int,
                                         _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_eer_counts": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _c_int, _P, _P, _P]),
     "sv_lstm_stack_bwd_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "sv_lstm_stack_bwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P, _P,
-                                                                                               _P]),
+                                                                                               _P, _c_int]),
     "sv_sync_size": (_c_size_t, []),
     "sv_persist_fwd_ok": (_c_int, [_c_int, _c_int]),
     "sv_persist_bwd_ok": (_c_int, [_c_int, _c_int]),
     "sv_persist_bwd_scratch": (_c_size_t, [_c_int, _c_int, _c_int]),
     "sv_status_poison": (_c_int, [_P, _P, _c_int, _P]),
+    "sv_status_to_flag": (_c_int, [_P, _P, _P]),
+    "sv_status_merge": (_c_int, [_P, _P, _P]),
     "sv_clip_sgd_workspace": (_c_size_t, []),
     "sv_clip_sgd_step": (_c_int, [_P, _P, _c_long, _c_float, _c_float, _c_int, _P, _P, _P, _P]),
 }
@@ -91,6 +118,15 @@ _lib = None
 
 class NativeLibraryError(RuntimeError):
     pass
+
+
+def use_library(path):
+    """Load ``path`` instead of the shipped library (tests: the fault-injection build).  Must run
+    before the first call into the library in this process."""
+    global LIB_PATH
+    if _lib is not None and os.path.abspath(path) != os.path.abspath(LIB_PATH):
+        raise NativeLibraryError(f"{LIB_PATH} is already loaded")
+    LIB_PATH = path
 
 
 def lib():
@@ -109,6 +145,11 @@ def lib():
             f = getattr(h, name)
             f.restype = res
             f.argtypes = args
+        if h.sv_abi_version() != ABI_VERSION:
+            raise NativeLibraryError(f"{LIB_PATH} has ABI {h.sv_abi_version()}, expected {ABI_VERSION}: rebuild it")
+        if hasattr(h, "sv_test_set_fault"):
+            h.sv_test_set_fault.restype = _c_int
+            h.sv_test_set_fault.argtypes = [_c_int]
         _lib = h
     return _lib
 
@@ -136,11 +177,6 @@ class PersistentRecurrenceError(RuntimeError):
     """A persistent recurrence's hand-off wait timed out (its grid was not co-resident: another
     kernel or process held CUs it needed).  Outputs since then are invalid; the trainer's
     clip + SGD step skipped the update (include/sv_ge2e.h, sync block)."""
-
-
-# status word layout of the sync block (include/sv_ge2e.h; sv_bf16.h SV_SYNC_*)
-SYNC_STAMP_WORD = 32 + 4 * 64 * 32
-SYNC_NSTAMP = 8
 
 
 class PersistStatus:
@@ -186,11 +222,6 @@ class PersistStatus:
         """Forget pending checks and zero the status word (stream-ordered)."""
         self._pending = []
         self.block[:1].zero_()
-
-    def stamps(self, n):
-        """Per-phase cycle stamps of the persistent backward's first n workgroups (SV_PBWD_DEBUG & 32)."""
-        st = self.block[SYNC_STAMP_WORD:SYNC_STAMP_WORD + 2 * SYNC_NSTAMP * n]
-        return st.view(torch.int64).view(n, SYNC_NSTAMP).cpu()
 
 
 def compute_device(t):

@@ -390,7 +390,7 @@ int sv_persist_bwd_fits(int B, int H, int cus);
 unsigned sv_persist_limit();
 int sv_persist_fault(int bwd);
 // layer-wavefront forward (sv_wave.hip): all L layers in one launch for small B
-int sv_wave_fwd_fits(int L, int B, int F, int H, int cus);
+int sv_wave_fwd_fits(int L, int T, int B, int F, int H, int cus);
 int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, const bf16_t* const* w_ih_bf,
                      const bf16_t* const* w_hh_bf, const float* const* b_ih, const float* const* b_hh,
                      bf16_t* const* gates, float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,

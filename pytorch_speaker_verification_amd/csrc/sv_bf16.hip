@@ -5,7 +5,6 @@
 // as sv_lstm.hip; transposed layouts use column blocks of Bp = B rounded up to 8 so every
 // bf16 row stays 16-byte aligned.
 #include <algorithm>
-#include <stdlib.h>
 #include "sv_common.h"
 #include "sv_gemm.h"
 #include "../../include/sv_ge2e.h"
@@ -211,110 +210,6 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_bf16_kernel(
   }
 }
 
-// ============================================================================
-// Wavefront forward over the whole stack: launch s runs layer l at time t = s - l for every
-// layer at once (blockIdx.z = layer), so one launch carries L recurrent steps and the L - 1
-// upper layers need no input-projection GEMM: their pre-activations are
-//   b_ih + b_hh + h^{l-1}_t W_ih^T + h^l_{t-1} W_hh^T
-// accumulated as two K segments of the same tile.  Layer 0 reads x W_ih^T + b from `gates`
-// (one T*B-row GEMM up front).  T + L - 1 launches replace L*T step launches + L*nch GEMMs.
-// ============================================================================
-#define SV_MAXL 4
-struct WaveFwdArgs {
-  const bf16_t* wih[SV_MAXL];
-  const bf16_t* whh[SV_MAXL];
-  const float* bih[SV_MAXL];
-  const float* bhh[SV_MAXL];
-  bf16_t* gates[SV_MAXL];  // layer 0: the x-projection in, then bf16 activations; others: out
-  float* c[SV_MAXL];
-  float* h[SV_MAXL];
-  bf16_t* hb[SV_MAXL];
-  bf16_t* hT[SV_MAXL];
-  long ldhT;
-  int T, Bp, B, H;
-};
-
-template <int SC>
-__global__ __launch_bounds__(512) void lstm_wave_fwd_bf16_kernel(const WaveFwdArgs a, int s) {
-  const int l = blockIdx.z, t = s - l;
-  if (t < 0 || t >= a.T) return;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* ldsb = reinterpret_cast<bf16_t*>(smem);
-  constexpr int BN = 4 * BF_U, LDP = BN + 4, LDH = BF_BM + 1;
-  constexpr int PER = BF_BM * BF_U / 512;
-  const int B = a.B, H = a.H;
-  const long BH = (long)B * H, G = 4L * H;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int j0 = blockIdx.x * BF_U, b0 = blockIdx.y * BF_BM;
-  const int wm0 = (w >> 2) * 32, wn0 = (w & 3) * 32;
-  bf16_t* gates = a.gates[l] + (long)t * B * G;
-  const float* cprev = t ? a.c[l] + (long)(t - 1) * BH : nullptr;
-  float xg[PER][4], cpv[PER];
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int e = tid + 512 * k, b = e / BF_U, u = e % BF_U;
-    const int gb = b0 + b, gj = j0 + u;
-    const bool ok = gb < B && gj < H;
-    if (l == 0) {
-      const bf16_t* gp = gates + (long)gb * G + gj;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) xg[k][q] = ok ? from_bf(gp[q * H]) : 0.f;
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) xg[k][q] = ok ? a.bih[l][q * H + gj] + a.bhh[l][q * H + gj] : 0.f;
-    }
-    cpv[k] = (ok && cprev) ? cprev[(long)gb * H + gj] : 0.f;
-  }
-  f32x16 acc[1][1];
-  zero_acc(acc);
-  if (l > 0)  // h^{l-1}_t W_ih^T  (input width = H for every upper layer)
-    gemm_mainloop_step<BF_BM, BN, 512, SC, 1, 1>(a.hb[l - 1] + (long)(t + 1) * BH + (long)b0 * H, H,
-                                                 RowMapLinear{0, B - b0}, a.wih[l], H, RowMapGates<BF_U>{j0, H}, 0,
-                                                 H, ldsb, tid, wm0, wn0, acc);
-  if (t > 0)  // h^l_{t-1} W_hh^T
-    gemm_mainloop_step<BF_BM, BN, 512, SC, 1, 1>(a.hb[l] + (long)t * BH + (long)b0 * H, H, RowMapLinear{0, B - b0},
-                                                 a.whh[l], H, RowMapGates<BF_U>{j0, H}, 0, H, ldsb, tid, wm0, wn0,
-                                                 acc);
-  float* pre = reinterpret_cast<float*>(smem);
-  float* hs = pre + BF_BM * LDP;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) pre[(wm0 + acc_row(r, lane)) * LDP + wn0 + (lane & 31)] = acc[0][0][r];
-  __syncthreads();
-  float* cout = a.c[l] + (long)t * BH;
-  float* hout = a.h[l] + (long)(t + 1) * BH;
-  bf16_t* hout_bf = a.hb[l] + (long)(t + 1) * BH;
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int e = tid + 512 * k, b = e / BF_U, u = e % BF_U;
-    const int gb = b0 + b, gj = j0 + u;
-    if (gb >= B || gj >= H) continue;
-    bf16_t* gp = gates + (long)gb * G + gj;
-    const float* pr = pre + b * LDP + u;
-    const float pv[4] = {pr[0], pr[BF_U], pr[2 * BF_U], pr[3 * BF_U]};
-    float av[4], h;
-    const float c = lstm_cell_fwd(pv, xg[k], cpv[k], av, h);
-    gp[0] = to_bf(av[0]);
-    gp[H] = to_bf(av[1]);
-    gp[2 * H] = to_bf(av[2]);
-    gp[3 * H] = to_bf(av[3]);
-    cout[(long)gb * H + gj] = c;
-    hout[(long)gb * H + gj] = h;
-    hout_bf[(long)gb * H + gj] = to_bf(h);
-    hs[u * LDH + b] = h;
-  }
-  bf16_t* hT = a.hT[l];
-  if (!hT) return;
-  __syncthreads();
-  for (int e = tid; e < BF_BM * BF_U; e += 512) {
-    const int u = e / BF_BM, b = e % BF_BM;
-    const int gb = b0 + b, gj = j0 + u;
-    if (gb >= B || gj >= H) continue;
-    bf16_t* row = hT + (long)gj * a.ldhT;
-    row[(long)(t + 1) * a.Bp + gb] = to_bf(hs[u * LDH + b]);
-    if (t == 0) row[gb] = 0;
-  }
-}
-
 template <int SC>
 __global__ __launch_bounds__(512) void lstm_step_bwd_bf16_kernel(
     const bf16_t* __restrict__ dgnext, const bf16_t* __restrict__ whhT, const float* __restrict__ dhup,
@@ -403,68 +298,31 @@ struct BPlan {
   int bm, bn, splitk, kchunk;
 };
 
-// 256 x 256 glds kernel (sv_gemm256.h) for shapes it tiles exactly; SV_GEMM256=0 disables it
-bool gemm256_ok(int M, int N, int K) {
-  static int on = [] {
-    const char* e = getenv("SV_GEMM256");
-    return (e && *e == '0') ? 0 : 1;
-  }();
-  return on && M % G256_BM == 0 && N % G256_BM == 0 && K % G256_BK == 0;
+// 256 x 256 kernels (sv_gemm256.h) for shapes they tile exactly
+bool gemm256_ok(int M, int N, int K) { return M % G256_BM == 0 && N % G256_BM == 0 && K % G256_BK == 0; }
+
+// the 256 x 256 tile's schedule: the 8-phase kernel (gemm_bf16_8q_kernel) where its 16-B
+// epilogue stores are aligned (C rows, biases), else the two-stage gemm_bf16_256_kernel
+bool g8_ok(const void* C, long ldc, const float* bias0, const float* bias1) {
+  return !((((uintptr_t)C | (uintptr_t)bias0 | (uintptr_t)bias1) & 15) || ldc % 4);
 }
 
-// SV_GEMM256P=1: the four-stage, three-in-flight variant of the 256 x 256 kernel (same results)
-bool gemm256p() {
-  static int on = [] {
-    const char* e = getenv("SV_GEMM256P");
-    return (e && *e == '1') ? 1 : 0;
-  }();
-  return on;
-}
-
-// the 256 x 256 tile's schedule: 2 = 8-phase (default), 1 = four-stage (SV_GEMM256P=1),
-// 0 = two-stage (SV_GEMM8P=0); the 8-phase epilogue stores 16 B per lane, so it needs 16-B
-// aligned C rows and biases
-int g256_variant(const void* C, long ldc, const float* bias0, const float* bias1) {
-  static int v = [] {
-    if (gemm256p()) return 1;
-    const char* e = getenv("SV_GEMM8P");
-    return (e && *e == '0') ? 0 : 2;
-  }();
-  if (v == 2 && ((((uintptr_t)C | (uintptr_t)bias0 | (uintptr_t)bias1) & 15) || ldc % 4)) return 0;
-  return v;
-}
-
+// the 8-phase kernel with two LDS-DMA fills per phase.  Measured against one or two fill phases
+// per k-tile (c3 shapes, us): dW 414 vs 445-446, dx 440 vs 471-480, K1 (bf16 out) 615 vs 626.
 template <int EPI, int AF>
 void launch_g8(dim3 grid, hipStream_t stream, const bf16_t* A, long lda, const bf16_t* B, long ldb, void* C, long ldc,
                long slab, int M, int N, int K, int kchunk, const float* bias0, const float* bias1, float beta,
                G256AFrag af = G256AFrag{}) {
-  // SV_G8_SCHED: 2 (default) two fills per phase (gemm_bf16_8q_kernel); 0 a k-tile's fills in
-  // phases 0 and 1, B nh0 re-read in phase 3; 1 all fills in phase 0.  Measured (c3 shapes, us):
-  // dW 414 / 446 / 445, dx 440 / 471 / 480, K1 (bf16 out) 615 / 626 / --
-  static const int sched = [] {
-    const char* e = getenv("SV_G8_SCHED");
-    return e ? atoi(e) : 2;
-  }();
-  if (sched == 2)
-    hipLaunchKernelGGL((gemm_bf16_8q_kernel<EPI, AF>), grid, dim3(512), G256_LDS, stream, A, lda, B, ldb, C, ldc, slab,
-                       M, N, K, kchunk, bias0, bias1, beta, af);
-  else if (sched == 0)
-    hipLaunchKernelGGL((gemm_bf16_8p_kernel<EPI, AF, 0>), grid, dim3(512), G256_LDS, stream, A, lda, B, ldb, C, ldc,
-                       slab, M, N, K, kchunk, bias0, bias1, beta, af);
-  else
-    hipLaunchKernelGGL((gemm_bf16_8p_kernel<EPI, AF, 1>), grid, dim3(512), G256_LDS, stream, A, lda, B, ldb, C, ldc,
-                       slab, M, N, K, kchunk, bias0, bias1, beta, af);
+  hipLaunchKernelGGL((gemm_bf16_8q_kernel<EPI, AF>), grid, dim3(512), G256_LDS, stream, A, lda, B, ldb, C, ldc, slab,
+                     M, N, K, kchunk, bias0, bias1, beta, af);
 }
 
 template <int EPI, int AF>
-void launch_g256(int variant, dim3 grid, hipStream_t stream, const bf16_t* A, long lda, const bf16_t* B, long ldb,
-                 void* C, long ldc, long slab, int M, int N, int K, int kchunk, const float* bias0,
-                 const float* bias1, float beta, G256AFrag af = G256AFrag{}) {
-  if (variant == 2)
+void launch_g256(bool g8, dim3 grid, hipStream_t stream, const bf16_t* A, long lda, const bf16_t* B, long ldb, void* C,
+                 long ldc, long slab, int M, int N, int K, int kchunk, const float* bias0, const float* bias1,
+                 float beta, G256AFrag af = G256AFrag{}) {
+  if (g8)
     launch_g8<EPI, AF>(grid, stream, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, bias0, bias1, beta, af);
-  else if (variant == 1)
-    hipLaunchKernelGGL((gemm_bf16_256p_kernel<EPI, AF>), grid, dim3(512), G256_LDS, stream, A, lda, B, ldb, (float*)C,
-                       ldc, slab, M, N, K, kchunk, bias0, bias1, beta, af);
   else
     hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, AF>), grid, dim3(512), G256_LDS, stream, A, lda, B, ldb, (float*)C,
                        ldc, slab, M, N, K, kchunk, bias0, bias1, beta, af);
@@ -522,148 +380,32 @@ constexpr int BBWD_LDS_MAIN = 4 * 2 * (BF_BM + BF_U) * (BBK + 8) * 2;
 constexpr int BBWD_LDS_EPI = (4 * BF_BM * (BF_U + 1) + 4 * BF_U * (BF_BM + 1)) * 4;
 constexpr int BBWD_LDS = BBWD_LDS_MAIN > BBWD_LDS_EPI ? BBWD_LDS_MAIN : BBWD_LDS_EPI;
 
-// forward step variant: register prefetch of all 12 k-tiles (1 block/CU) or super-chunks of
-// 6 (fewer VGPRs: 2 blocks/CU, so pipelined layers' steps can share a CU); SV_BF16_SC overrides
-int bf16_sc() {
-  static int v = [] {
-    const char* e = getenv("SV_BF16_SC");
-    const int x = e ? atoi(e) : 3;
-    return (x == 3 || x == 4 || x == 6 || x == 104 || x == 106 || x == 112 || x == 203) ? x : 12;
-  }();
-  return v;
-}
+// per-step forward kernel: register prefetch in super-chunks of 3 k-tiles (measured against 4, 6,
+// 12 and rolling prefetch depths 4 / 6 at c3: none faster)
 void launch_fwd_bf16(dim3 grid, hipStream_t s, const bf16_t* hp, const bf16_t* whh, bf16_t* g, const float* cp,
                      float* c, float* h, bf16_t* hb, bf16_t* hT, long ldhT, int t, int Bp, int B, int H) {
-  const int sc = bf16_sc();
-  if (sc == 203)
-    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<203>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
-                       t, Bp, B, H);
-  else if (sc == 104)
-    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<104>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
-                       t, Bp, B, H);
-  else if (sc == 106)
-    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<106>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
-                       t, Bp, B, H);
-  else if (sc == 112)
-    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<112>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
-                       t, Bp, B, H);
-  else if (sc == 6)
-    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<6>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
-                       t, Bp, B, H);
-  else if (sc == 4)
-    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<4>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
-                       t, Bp, B, H);
-  else if (sc == 3)
-    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<3>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
-                       t, Bp, B, H);
-  else
-    hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<12>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
-                       t, Bp, B, H);
+  hipLaunchKernelGGL(lstm_step_fwd_bf16_kernel<3>, grid, dim3(512), BFWD_LDS, s, hp, whh, g, cp, c, h, hb, hT, ldhT,
+                     t, Bp, B, H);
 }
 
-// stack forward schedule: layer-pipelined streams (0, default) or wavefront over layers (1).
-// Measured at c3: pipelined 22.25 ms/step, wavefront 25.5 (23.3 with the rolling prefetch):
-// a step launch starts with cold L2 (kernel-boundary invalidate), so its time scales with the
-// bytes each CU pulls from the Infinity Cache, and the wavefront moves 5x the bytes per launch.
-int wavefront_fwd() {
-  static int v = [] {
-    const char* e = getenv("SV_WAVEFRONT");
-    return (e && *e == '1') ? 1 : 0;
-  }();
-  return v;
+// bf16 stack schedule (the `schedule` flags of sv_lstm_stack_{fwd,bwd}_bf16, include/sv_ge2e.h):
+// persistent recurrences (one launch per layer, W_hh held in registers, sv_persist.hip) at
+// H = 768 (measured c3 21.5 vs 22.2 ms per-step) or wherever they fit with SV_SCHED_PERSIST;
+// per-step launches, layer-pipelined, with SV_SCHED_PER_STEP (bit-identical results).
+bool sched_persist(int schedule, int H) {
+  return !(schedule & SV_SCHED_PER_STEP) && ((schedule & SV_SCHED_PERSIST) || H == 768);
 }
-// stack forward recurrences: one persistent launch per layer (W_hh held in registers,
-// sv_persist.hip) or per-step launches, layer-pipelined.  SV_PERSIST: unset = persistent when
-// H = 768 (the W-stationary kernel; measured c3 21.5 vs 22.2 ms), 1 = always persistent
-// (H != 768 falls back to the LDS-staged persistent kernel), 0 = per-step.
-int persist_fwd(int H) {
-  static int v = [] {
-    const char* e = getenv("SV_PERSIST");
-    return e ? (*e == '1' ? 1 : 0) : -1;
-  }();
-  return v < 0 ? (H == 768) : v;
-}
-// stack forward for small batches: the layer-wavefront launch (sv_wave.hip) whenever all layers'
-// grids fit co-resident (B <= 96 at H = 768 on 256 CUs); SV_WAVE2=0 keeps one launch per layer
-int wave2_fwd() {
-  static int v = [] {
-    const char* e = getenv("SV_WAVE2");
-    return (e && *e == '0') ? 0 : 1;
-  }();
-  return v;
-}
-// stack backward recurrences: one persistent launch per layer (W_hh held in registers,
-// sv_persist.hip) or per-step launches, layer-pipelined.  SV_PERSIST_BWD: unset = persistent
-// when H = 768, 1 = whenever sv_persist_bwd_ok, 0 = per-step.
-int persist_bwd(int H) {
-  static int v = [] {
-    const char* e = getenv("SV_PERSIST_BWD");
-    return e ? (*e == '1' ? 1 : 0) : -1;
-  }();
-  return v < 0 ? (H == 768) : v;
-}
-// persistent backward: bias gradients summed inside the recurrence (1, default) or by a row sum
-// over dG^T afterwards (SV_PBWD_DB=0)
-int pbwd_db() {
-  static int v = [] {
-    const char* e = getenv("SV_PBWD_DB");
-    return (e && *e == '0') ? 0 : 1;
-  }();
-  return v;
-}
-// persistent backward: the layer's dW GEMMs on `main` after its dx GEMM (0, default; measured
-// c3 16.6 ms/step) or on its weight-gradient stream, overlapping the next layer's recurrence
-// (SV_PBWD_DW_SIDE=1: 16.8 ms -- the GEMM workgroups contend with the co-resident recurrence)
-int pbwd_dw_side() {
-  static int v = [] {
-    const char* e = getenv("SV_PBWD_DW_SIDE");
-    return (e && *e == '1') ? 1 : 0;
-  }();
-  return v;
-}
-void launch_wave_fwd_bf16(dim3 grid, hipStream_t s, const WaveFwdArgs& a, int st) {
-  const int sc = bf16_sc();
-  if (sc == 104)
-    hipLaunchKernelGGL(lstm_wave_fwd_bf16_kernel<104>, grid, dim3(512), BFWD_LDS, s, a, st);
-  else if (sc == 106)
-    hipLaunchKernelGGL(lstm_wave_fwd_bf16_kernel<106>, grid, dim3(512), BFWD_LDS, s, a, st);
-  else
-    hipLaunchKernelGGL(lstm_wave_fwd_bf16_kernel<3>, grid, dim3(512), BFWD_LDS, s, a, st);
-}
+// the layer wavefronts (every layer in one launch, sv_wave.hip / sv_persist3.hip) where all
+// layers' grids fit co-resident, unless SV_SCHED_PER_LAYER (bf16-level different sums)
+bool sched_wave(int schedule, int H) { return sched_persist(schedule, H) && !(schedule & SV_SCHED_PER_LAYER); }
 
-int bf16_bsc() {
-  static int v = [] {
-    const char* e = getenv("SV_BF16_BSC");
-    const int x = e ? atoi(e) : 6;
-    return (x == 2 || x == 3 || x == 103 || x == 104 || x == 106 || x == 206) ? x : 6;
-  }();
-  return v;
-}
+// per-step backward kernel: register prefetch in super-chunks of 6 k-tiles (measured against
+// 2, 3 and rolling depths 3 / 4 / 6 at c3)
 void launch_bwd_bf16(dim3 grid, hipStream_t s, const bf16_t* dgn, const bf16_t* whhT, const float* up,
                      const float* dcfi, const bf16_t* acts, const float* ct, const float* cp, bf16_t* dg, float* dcfo,
                      bf16_t* dgT, long lddgT, int t, int Bp, int B, int H) {
-  const int sc = bf16_bsc();
-  if (sc == 206)
-    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<206>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
-                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
-  else if (sc == 103)
-    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<103>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
-                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
-  else if (sc == 104)
-    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<104>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
-                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
-  else if (sc == 106)
-    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<106>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
-                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
-  else if (sc == 2)
-    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<2>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
-                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
-  else if (sc == 3)
-    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<3>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
-                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
-  else
-    hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<6>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
-                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
+  hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<6>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
+                     dg, dcfo, dgT, lddgT, t, Bp, B, H);
 }
 
 }  // namespace
@@ -684,13 +426,9 @@ size_t sv_gemm_bf16_dual_workspace(int M, int N1, int N2, int K) {
 int sv_gemm_bf16_dual(int M, int N1, int N2, int K, const bf16_t* A, long lda, const bf16_t* B1, long ldb1, float* C1,
                       long ldc1, const bf16_t* B2, long ldb2, float* C2, long ldc2, float* workspace,
                       hipStream_t stream) {
-  static const int on = [] {
-    const char* e = getenv("SV_DW_DUAL");
-    return (e && *e == '0') ? 0 : 1;
-  }();
   const BPlan p = plan_bf16(M, N1, K);
-  const bool fused = on && p.bm == G256_BM && p.splitk > 1 && gemm256_ok(M, N1 + N2, K) && N1 % G256_BM == 0 &&
-                     N2 % G256_BM == 0 && workspace && g256_variant(workspace, N1 + N2, nullptr, nullptr) == 2 &&
+  const bool fused = p.bm == G256_BM && p.splitk > 1 && gemm256_ok(M, N1 + N2, K) && N1 % G256_BM == 0 &&
+                     N2 % G256_BM == 0 && workspace && g8_ok(workspace, N1 + N2, nullptr, nullptr) &&
                      ldb1 % 8 == 0 && ldb2 % 8 == 0 && lda % 8 == 0 && !(((uintptr_t)A | (uintptr_t)B1 | (uintptr_t)B2) & 15);
   if (!fused) {
     int rc = sv_gemm_bf16(M, N1, K, A, lda, B1, ldb1, C1, ldc1, nullptr, nullptr, 0.f, workspace, stream);
@@ -726,13 +464,13 @@ extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, cons
     const int tiles = (M / G256_BM) * (N / G256_BM);
     const long slab = (long)M * N;
     if (p.splitk == 1) {
-      launch_g256<G256_STORE, 0>(g256_variant(C, ldc, bias0, bias1), dim3(tiles, 1), stream, A, lda, B, ldb, C, ldc, 0L,
+      launch_g256<G256_STORE, 0>(g8_ok(C, ldc, bias0, bias1), dim3(tiles, 1), stream, A, lda, B, ldb, C, ldc, 0L,
                                  M, N, K, p.kchunk, bias0, bias1, beta);
       SV_LAUNCH_CHECK();
       return SV_OK;
     }
     if (!workspace) return SV_EARG;
-    launch_g256<G256_SLAB, 0>(g256_variant(workspace, N, nullptr, nullptr), dim3(tiles, p.splitk), stream, A, lda, B,
+    launch_g256<G256_SLAB, 0>(g8_ok(workspace, N, nullptr, nullptr), dim3(tiles, p.splitk), stream, A, lda, B,
                               ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr, 0.f);
     SV_LAUNCH_CHECK();
     const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
@@ -775,7 +513,7 @@ extern "C" int sv_gemm_bf16_bf(int M, int N, int K, const bf16_t* A, long lda, c
   if (M <= 0 || N <= 0 || K <= 0 || !A || !B || !C) return SV_EARG;
   if (K % 8 || lda % 8 || ldb % 8 || (((uintptr_t)A | (uintptr_t)B) & 15)) return SV_EALIGN;
   const BPlan p = plan_bf16(M, N, K);
-  if (p.bm == G256_BM && p.splitk == 1 && g256_variant(nullptr, 0, bias0, bias1) == 2 && ldc % 8 == 0 &&
+  if (p.bm == G256_BM && p.splitk == 1 && g8_ok(nullptr, 0, bias0, bias1) && ldc % 8 == 0 &&
       !((uintptr_t)C & 15)) {
     const int tiles = (M / G256_BM) * (N / G256_BM);
     launch_g8<G8_STORE_BF16, 0>(dim3(tiles, 1), stream, A, lda, B, ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1,
@@ -794,11 +532,7 @@ extern "C" int sv_gemm_bf16_bf(int M, int N, int K, const bf16_t* A, long lda, c
 // dx = dG . W_ih with dG read from the persistent backward's fragment-order hand-off buffer
 // (no row-major dG copy): M = T * B rows (t, b), K = 4H; needs B % 32, M % 256, N % 256, H % 64
 bool gemm_afrag_ok(int T, int B, int N, int H) {
-  static int on = [] {
-    const char* e = getenv("SV_DX_AFRAG");
-    return (e && *e == '0') ? 0 : 1;
-  }();
-  return on && gemm256_ok(T * B, N, 4 * H) && B % 32 == 0 && H % G256_BK == 0;
+  return gemm256_ok(T * B, N, 4 * H) && B % 32 == 0 && H % G256_BK == 0;
 }
 // (the split-K plan of sv_gemm_bf16 for the same shape, so both forms sum in the same order)
 int gemm_bf16_afrag(int T, int B, int H, int N, const bf16_t* dgf, int bm, const bf16_t* Bop, long ldb, float* C,
@@ -809,14 +543,14 @@ int gemm_bf16_afrag(int T, int B, int H, int N, const bf16_t* dgf, int bm, const
   const G256AFrag af{dgf, fs, B, bm, H};
   const BPlan p = plan_bf16(M, N, K);
   if (p.splitk == 1) {
-    launch_g256<G256_STORE, 1>(g256_variant(C, ldc, nullptr, nullptr), dim3(tiles, 1), stream, nullptr, 0L, Bop, ldb, C,
+    launch_g256<G256_STORE, 1>(g8_ok(C, ldc, nullptr, nullptr), dim3(tiles, 1), stream, nullptr, 0L, Bop, ldb, C,
                                ldc, 0L, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
     SV_LAUNCH_CHECK();
     return SV_OK;
   }
   if (!workspace) return SV_EARG;
   const long slab = (long)M * N;
-  launch_g256<G256_SLAB, 1>(g256_variant(workspace, N, nullptr, nullptr), dim3(tiles, p.splitk), stream, nullptr, 0L,
+  launch_g256<G256_SLAB, 1>(g8_ok(workspace, N, nullptr, nullptr), dim3(tiles, p.splitk), stream, nullptr, 0L,
                             Bop, ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
   SV_LAUNCH_CHECK();
   const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
@@ -924,15 +658,20 @@ extern "C" int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const bf16_t* 
   return SV_OK;
 }
 
-// Layer-pipelined stack forward, bf16 operands (see sv_lstm_stack_fwd in sv_lstm.hip).
+// Stack forward, bf16 operands.  `schedule` (include/sv_ge2e.h): the layer wavefront (one launch
+// for every layer's recurrence and input projection, sv_wave.hip) where the grids fit; else per
+// layer its K1 GEMM and one persistent recurrence launch (layer 0's projection in-kernel); else
+// (SV_SCHED_PER_STEP, or H without a persistent kernel) the layer-pipelined per-step schedule of
+// sv_lstm_stack_fwd (sv_lstm.hip).
 extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf,
                                       const bf16_t* const* w_ih_bf, const bf16_t* const* w_hh_bf,
                                       const float* const* b_ih, const float* const* b_hh, bf16_t* const* gates,
                                       float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
                                       bf16_t* const* hT, int chunk, hipStream_t main, const hipStream_t* side,
-                                      hipEvent_t* ev, void* sync_block, hipEvent_t* probe) {
+                                      hipEvent_t* ev, void* sync_block, hipEvent_t* probe, int schedule) {
   if (L <= 0 || !x_bf || !w_ih_bf || !w_hh_bf || !gates || !c_tm || !h_tm || !h_bf || !side || !ev || chunk <= 0)
     return SV_EARG;
+  if (schedule & ~SV_SCHED_MASK) return SV_EARG;
   unsigned* sync = reinterpret_cast<unsigned*>(sync_block);
   if (T <= 0 || B <= 0 || F <= 0 || H <= 0 || F % 8 || H % 8) return SV_ESHAPE;
   const int nch = (T + chunk - 1) / chunk;
@@ -940,32 +679,32 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
   const int Bp = (B + 7) & ~7;
   const long ldhT = (long)(T + 1) * Bp;
   hipError_t e;
-  if (persist_fwd(H) && wave2_fwd() && sv_wave_fwd_fits(L, B, F, H, sv_stream_cus(main))) {
+  auto zero_state = [&](int l, hipStream_t s) -> int {
+    if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), s)) != hipSuccess) return (int)e;
+    if ((e = hipMemsetAsync(h_bf[l], 0, BH * sizeof(bf16_t), s)) != hipSuccess) return (int)e;
+    if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(bf16_t), s)) != hipSuccess)
+      return (int)e;
+    return SV_OK;
+  };
+  int rc;
+  if (sched_wave(schedule, H) && sv_wave_fwd_fits(L, T, B, F, H, sv_stream_cus(main))) {
     // layer-wavefront schedule (sv_wave.hip): every layer's recurrence and input projection in
     // one launch on `main`
     if (!sync) return SV_EARG;
-    for (int l = 0; l < L; ++l) {
-      if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), main)) != hipSuccess) return (int)e;
-      if ((e = hipMemsetAsync(h_bf[l], 0, BH * sizeof(bf16_t), main)) != hipSuccess) return (int)e;
-      if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(bf16_t), main)) != hipSuccess)
-        return (int)e;
-    }
+    for (int l = 0; l < L; ++l)
+      if ((rc = zero_state(l, main))) return rc;
     return sv_wave_fwd_bf16(L, T, B, F, H, x_bf, w_ih_bf, w_hh_bf, b_ih, b_hh, gates, c_tm, h_tm, h_bf, hT, sync, main,
                             sv_persist_limit(), sv_persist_fault(0), probe ? probe[0] : nullptr,
                             probe ? probe[1] : nullptr);
   }
-  if (persist_fwd(H) && sv_persist_fwd_fits(B, H, sv_stream_cus(main))) {
+  if (sched_persist(schedule, H) && sv_persist_fwd_fits(B, H, sv_stream_cus(main))) {
     if (!sync) return SV_EARG;
     // persistent schedule on `main`: per layer the whole-T K1 GEMM, then one launch for the
     // recurrence (sv_persist.hip); layers run one after another
     for (int l = 0; l < L; ++l) {
-      if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), main)) != hipSuccess) return (int)e;
-      if ((e = hipMemsetAsync(h_bf[l], 0, BH * sizeof(bf16_t), main)) != hipSuccess) return (int)e;
-      if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(bf16_t), main)) != hipSuccess)
-        return (int)e;
+      if ((rc = zero_state(l, main))) return rc;
       const int Fl = l == 0 ? F : H;
       const bf16_t* in = l == 0 ? x_bf : h_bf[l - 1] + BH;
-      int rc;
       if (l == 0 && sv_persist_fwd_fusex_ok(H, F)) {  // layer 0's input projection inside the recurrence
         if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, sync, 0,
                                       x_bf, F, w_ih_bf[l], b_ih[l], b_hh[l], probe ? probe[2 * l] : nullptr,
@@ -982,49 +721,13 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
     }
     return SV_OK;
   }
-  if (wavefront_fwd() && L <= SV_MAXL) {  // wavefront schedule, all on `main`
-    for (int l = 0; l < L; ++l) {
-      if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), main)) != hipSuccess) return (int)e;
-      if ((e = hipMemsetAsync(h_bf[l], 0, BH * sizeof(bf16_t), main)) != hipSuccess) return (int)e;
-      if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(bf16_t), main)) != hipSuccess)
-        return (int)e;
-    }
-    int rc = sv_gemm_bf16_bf(T * B, 4 * H, F, x_bf, F, w_ih_bf[0], F, gates[0], 4L * H, b_ih[0], b_hh[0], main);
-    if (rc) return rc;
-    WaveFwdArgs a{};
-    for (int l = 0; l < L; ++l) {
-      a.wih[l] = w_ih_bf[l];
-      a.whh[l] = w_hh_bf[l];
-      a.bih[l] = b_ih[l];
-      a.bhh[l] = b_hh[l];
-      a.gates[l] = gates[l];
-      a.c[l] = c_tm[l];
-      a.h[l] = h_tm[l];
-      a.hb[l] = h_bf[l];
-      a.hT[l] = hT[l];
-    }
-    a.ldhT = ldhT;
-    a.T = T;
-    a.Bp = Bp;
-    a.B = B;
-    a.H = H;
-    const dim3 wgrid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM, L);
-    for (int st = 0; st < T + L - 1; ++st) {
-      launch_wave_fwd_bf16(wgrid, main, a, st);
-      SV_LAUNCH_CHECK();
-    }
-    return SV_OK;
-  }
   hipEvent_t ev_start = ev[L * nch];
   e = hipEventRecord(ev_start, main);
   if (e != hipSuccess) return (int)e;
   for (int l = 0; l < L; ++l) {
     hipStream_t s = side[l];
     if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
-    if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), s)) != hipSuccess) return (int)e;
-    if ((e = hipMemsetAsync(h_bf[l], 0, BH * sizeof(bf16_t), s)) != hipSuccess) return (int)e;
-    if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(bf16_t), s)) != hipSuccess)
-      return (int)e;
+    if ((rc = zero_state(l, s))) return rc;
   }
   const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
   for (int c = 0; c < nch + L - 1; ++c) {
@@ -1036,8 +739,8 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
       const int Fl = l == 0 ? F : H;
       const bf16_t* in = l == 0 ? x_bf + (long)t0 * B * F : h_bf[l - 1] + (long)(t0 + 1) * BH;
       if (l > 0 && (e = hipStreamWaitEvent(s, ev[(l - 1) * nch + cc], 0)) != hipSuccess) return (int)e;
-      int rc = sv_gemm_bf16_bf((t1 - t0) * B, 4 * H, Fl, in, Fl, w_ih_bf[l], Fl, gates[l] + t0 * BG, 4L * H, b_ih[l],
-                               b_hh[l], s);
+      rc = sv_gemm_bf16_bf((t1 - t0) * B, 4 * H, Fl, in, Fl, w_ih_bf[l], Fl, gates[l] + t0 * BG, 4L * H, b_ih[l],
+                           b_hh[l], s);
       if (rc) return rc;
       for (int t = t0; t < t1; ++t) {
         launch_fwd_bf16(grid, s, t ? h_bf[l] + t * BH : nullptr, w_hh_bf[l], gates[l] + t * BG,
@@ -1056,7 +759,7 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
 // Layer-pipelined stack backward, bf16 operands (see sv_lstm_stack_bwd in sv_lstm.hip).
 namespace {
 struct BBwdWs {
-  float *dcf0, *dcf1, *gws, *gws2;
+  float *dcf0, *dcf1, *gws;
   bf16_t *whhT, *wihT;
   size_t total;
 };
@@ -1078,7 +781,6 @@ BBwdWs carve_bbwd(char* base, int T, int B, int F, int H) {
   g = std::max(g, sv_gemm_bf16_workspace(T * B, F, 4 * H));
   g = std::max(g, sv_gemm_bf16_dual_workspace(4 * H, H, F, TBp));
   w.gws = (float*)take(g);
-  w.gws2 = (float*)take(g);  // the weight-gradient stream's own split-K slabs (stack bwd)
   w.total = off;
   return w;
 }
@@ -1099,10 +801,11 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
                                       bf16_t* const* dg, bf16_t* const* dgT, float* const* dx, float* const* dw_ih,
                                       float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace,
                                       int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev,
-                                      void* sync_block, hipEvent_t* probe) {
+                                      void* sync_block, hipEvent_t* probe, int schedule) {
   if (L <= 0 || !xT || !ld_xT || !w_ih || !w_hh || !gates || !c_tm || !hT || !dh_last || !dg || !dgT || !dx ||
       !dw_ih || !dw_hh || !db_ih || !workspace || !side || !ev || chunk <= 0)
     return SV_EARG;
+  if (schedule & ~SV_SCHED_MASK) return SV_EARG;
   unsigned* sync = reinterpret_cast<unsigned*>(sync_block);
   if (T <= 0 || B <= 0 || F <= 0 || H <= 0 || F % 8 || H % 8) return SV_ESHAPE;
   const int nch = (T + chunk - 1) / chunk;
@@ -1114,11 +817,11 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
   hipEvent_t ev_start = ev[L * nch + L];
   hipError_t e = hipEventRecord(ev_start, main);
   if (e != hipSuccess) return (int)e;
-  if (persist_bwd(H) && sv_wave_bwd_fits(L, B, H, sv_stream_cus(main))) {
+  if (sched_wave(schedule, H) && sv_wave_bwd_fits(L, B, H, sv_stream_cus(main))) {
     if (!sync) return SV_EARG;
     // layer-wavefront schedule: every layer's recurrence and upstream gradient dx in one launch
-    // (sv_persist3.hip, no dx GEMMs), then per layer the weight gradients on its weight-gradient
-    // stream (SV_PBWD_DW_SIDE=0: on `main`)
+    // (sv_persist3.hip, no dx GEMMs; bias gradients summed in the kernel), then per layer the
+    // weight gradients on `main`
     const bf16_t* whhT_l[WB_L];
     const bf16_t* wihT_l[WB_L];
     for (int l = 0; l < L; ++l) {
@@ -1129,83 +832,54 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       whhT_l[l] = ws.whhT;
       wihT_l[l] = l > 0 ? ws.wihT : nullptr;
     }
-    const bool dbk = pbwd_db();
     int rc = sv_wave_bwd_bf16(L, T, B, H, whhT_l, wihT_l, gates, c_tm, dh_last, dx, dgT, (char*)workspace + per * L,
-                              sync, main, dbk ? db_ih : nullptr, dbk ? db_hh : nullptr, probe ? probe[0] : nullptr,
-                              probe ? probe[1] : nullptr);
+                              sync, main, db_ih, db_hh, probe ? probe[0] : nullptr, probe ? probe[1] : nullptr);
     if (rc) return rc;
-    if ((e = hipEventRecord(ev[0], main)) != hipSuccess) return (int)e;
     for (int l = L - 1; l >= 0; --l) {
       const int Fl = l == 0 ? F : H;
       const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
-      hipStream_t sw = pbwd_dw_side() ? side[L + l] : main;
-      if (sw != main && (e = hipStreamWaitEvent(sw, ev[0], 0)) != hipSuccess) return (int)e;
-      float* gw = sw != main ? ws.gws2 : ws.gws;
       if ((rc = sv_gemm_bf16_dual(4 * H, H, Fl, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, xT[l], ld_xT[l], dw_ih[l],
-                                  Fl, gw, sw)))
+                                  Fl, ws.gws, main)))
         return rc;
-      if (!dbk) {
-        hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
-                           db_hh ? db_hh[l] : nullptr);
-        SV_LAUNCH_CHECK();
-      }
-      if (sw != main) {
-        if ((e = hipEventRecord(ev[L * nch + l], sw)) != hipSuccess) return (int)e;
-        if ((e = hipStreamWaitEvent(main, ev[L * nch + l], 0)) != hipSuccess) return (int)e;
-      }
     }
     for (int l = 0; l < L; ++l)
       if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
     return SV_OK;
   }
-  if (persist_bwd(H) && sv_persist_bwd_fits(B, H, sv_stream_cus(main))) {
+  if (sched_persist(schedule, H) && sv_persist_bwd_fits(B, H, sv_stream_cus(main))) {
     if (!sync) return SV_EARG;
-    // persistent schedule: per layer (top first) the whole-T recurrence in one launch
-    // (sv_persist.hip) and the whole-T dx GEMM on `main`; the layer's weight gradients on its
-    // weight-gradient stream (SV_PBWD_DW_SIDE=0: on `main` after the dx GEMM)
+    // persistent schedule on `main`: per layer (top first) the whole-T recurrence in one launch
+    // (sv_persist.hip; bias gradients summed in the kernel), the whole-T dx GEMM straight from its
+    // fragment-order hand-off, then the layer's weight gradients (measured: on a side stream
+    // beside the next layer's recurrence 16.8 vs 16.6 ms at c3 -- the GEMM workgroups contend
+    // with the co-resident recurrence)
     for (int l = L - 1; l >= 0; --l) {
       const int Fl = l == 0 ? F : H;
       const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
-      hipStream_t sw = pbwd_dw_side() ? side[L + l] : main;
       int rc = sv_transpose_cast_bf16(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, main);
       if (rc) return rc;
       if (l > 0 && (rc = sv_transpose_cast_bf16(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, main))) return rc;
       const float* up = l == L - 1 ? dh_last : dx[l + 1];
       bf16_t* dgf = (bf16_t*)((char*)workspace + per * L);
-      const bool dbk = pbwd_db();  // bias gradients summed in the recurrence, else by rowsum over dG^T
       const bool afr = l > 0 && gemm_afrag_ok(T, B, Fl, H);  // dx reads dgf: no row-major dG
       if ((rc = sv_persist_bwd_bf16(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1,
                                     (afr || l == 0) ? nullptr : dg[l],  // layer 0 has no dx GEMM
-                                    dgT[l], dgf, main, sync, dbk ? db_ih[l] : nullptr,
-                                    dbk && db_hh ? db_hh[l] : nullptr, probe ? probe[2 * l] : nullptr,
-                                    probe ? probe[2 * l + 1] : nullptr)))
+                                    dgT[l], dgf, main, sync, db_ih[l], db_hh ? db_hh[l] : nullptr,
+                                    probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr)))
         return rc;
       if (afr) {
-        if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H, sv_stream_cus(main)), ws.wihT, 4L * H, dx[l], Fl, ws.gws, main)))
+        if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H, sv_stream_cus(main)), ws.wihT, 4L * H, dx[l],
+                                  Fl, ws.gws, main)))
           return rc;
       } else if (l > 0 && (rc = sv_gemm_bf16(T * B, Fl, 4 * H, dg[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr,
                                               nullptr, 0.f, ws.gws, main))) {
         return rc;
       }
-      if (sw != main) {
-        if ((e = hipEventRecord(ev[l * nch], main)) != hipSuccess) return (int)e;
-        if ((e = hipStreamWaitEvent(sw, ev[l * nch], 0)) != hipSuccess) return (int)e;
-      }
-      float* gw = sw != main ? ws.gws2 : ws.gws;
       // dW_hh and dW_ih in one pass over dG^T (falls back to two GEMMs for layer 0's F = 40)
-      rc = sv_gemm_bf16_dual(4 * H, H, Fl, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, xT[l], ld_xT[l], dw_ih[l], Fl, gw,
-                             sw);
+      rc = sv_gemm_bf16_dual(4 * H, H, Fl, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, xT[l], ld_xT[l], dw_ih[l], Fl,
+                             ws.gws, main);
       if (rc) return rc;
-      if (!dbk) {
-        hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
-                           db_hh ? db_hh[l] : nullptr);
-        SV_LAUNCH_CHECK();
-      }
-      if (sw != main && (e = hipEventRecord(ev[L * nch + l], sw)) != hipSuccess) return (int)e;
     }
-    if (pbwd_dw_side())
-      for (int l = 0; l < L; ++l)
-        if ((e = hipStreamWaitEvent(main, ev[L * nch + l], 0)) != hipSuccess) return (int)e;
     // the per-layer completion events (grad_ready: a caller's bucketed all-reduce) all fire after
     // the last recurrence, so collectives never share the device with a persistent launch (whose
     // grid must be co-resident; a concurrent RCCL kernel would hold CUs it waits for)
@@ -1213,9 +887,10 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
     return SV_OK;
   }
+  // per-step schedule, layer-pipelined (sv_lstm_stack_bwd, sv_lstm.hip): each layer on side[l]
   const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
   for (int l = L - 1; l >= 0; --l) {
-    hipStream_t s = side[l], sw = side[L + l];
+    hipStream_t s = side[l];
     const int Fl = l == 0 ? F : H;
     const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
     if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
@@ -1242,29 +917,15 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
         if (rc) return rc;
       }
       if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
-      if (!dw_chunked_layer(l)) continue;
-      // the chunk's K-slice of the weight gradients, on the layer's weight-gradient stream
-      if ((e = hipStreamWaitEvent(sw, ev[l * nch + c], 0)) != hipSuccess) return (int)e;
-      const float beta = c == nch - 1 ? 0.f : 1.f;
-      const int Kc = (t1 - t0) * Bp;
-      rc = sv_gemm_bf16(4 * H, H, Kc, dgT[l] + (long)t0 * Bp, TBp, hT[l] + (long)t0 * Bp, ldhT, dw_hh[l], H, nullptr,
-                        nullptr, beta, ws.gws2, sw);
-      if (rc) return rc;
-      rc = sv_gemm_bf16(4 * H, Fl, Kc, dgT[l] + (long)t0 * Bp, TBp, xT[l] + (long)t0 * Bp, ld_xT[l], dw_ih[l], Fl,
-                        nullptr, nullptr, beta, ws.gws2, sw);
-      if (rc) return rc;
     }
-    if (!dw_chunked_layer(l)) {
-      sw = s;
-      rc = sv_gemm_bf16(4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws, s);
-      if (rc) return rc;
-      rc = sv_gemm_bf16(4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, ws.gws, s);
-      if (rc) return rc;
-    }
-    hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
+    rc = sv_gemm_bf16(4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws, s);
+    if (rc) return rc;
+    rc = sv_gemm_bf16(4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, ws.gws, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(4 * H), dim3(256), 0, s, dgT[l], (long)TBp, TBp, db_ih[l],
                        db_hh ? db_hh[l] : nullptr);
     SV_LAUNCH_CHECK();
-    if ((e = hipEventRecord(ev[L * nch + l], sw)) != hipSuccess) return (int)e;
+    if ((e = hipEventRecord(ev[L * nch + l], s)) != hipSuccess) return (int)e;
   }
   for (int l = 0; l < L; ++l)
     if ((e = hipStreamWaitEvent(main, ev[L * nch + l], 0)) != hipSuccess) return (int)e;

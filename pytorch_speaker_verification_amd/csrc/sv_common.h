@@ -28,10 +28,6 @@ struct F32ProductScope {
   ~F32ProductScope();
 };
 
-// stack-backward schedule switch (sv_lstm.hip; env SV_DW_CHUNKED)
-int dw_chunked_layer(int l);
-int dx_side();
-
 #define SV_LAUNCH_CHECK()                                  \
   do {                                                     \
     hipError_t e__ = hipGetLastError();                    \

@@ -914,6 +914,216 @@ extern "C" int sv_ge2e_calc_loss(const float* S, int N, int M, int K, float* per
   return SV_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Backward passes of the stand-alone helpers (the autograd graphs of utils.py:28, :72-115,
+// :126-132), so a loss composed from them as in speech_embedder_net.py:45-48 trains.
+// ---------------------------------------------------------------------------
+// get_centroids: E.mean(1) -> dE[j,i,:] = dC[j,:] / M  (mean's backward divides by M)
+__global__ void ge2e_centroids_bwd_kernel(const float* __restrict__ dC, int N, int M, int D, float* __restrict__ dE) {
+  const long total = (long)N * M * D;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int d = (int)(e % D);
+    const long j = e / ((long)M * D);
+    dE[e] = dC[j * D + d] / (float)M;
+  }
+}
+
+// get_cossim row pass, one wave per row r = (j, i): the upstream dcos row with the diagonal k = j
+// taken out (the index_put overwrote cos[j, :, j], so C_j gets nothing from it) -> dcoff, its
+// diagonal value -> dcd, the raw off-diagonal cosines (cosr, from the MFMA GEMM) with the
+// diagonal replaced by the leave-one-out one -> alpha_r = sum_k dcos[r,k] cos_raw[r,k]
+__global__ __launch_bounds__(256) void ge2e_cossim_bwd_rows_kernel(const float* __restrict__ dcos,
+                                                                   const float* __restrict__ cosr,
+                                                                   const float* __restrict__ rawd, int Bl, int M, int Nc,
+                                                                   int ldc, float* __restrict__ dcoff,
+                                                                   float* __restrict__ dcd, float* __restrict__ alpha) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= Bl) return;
+  const int j = r / M;
+  const float* g = dcos + (long)r * Nc;
+  const float* c = cosr + (long)r * ldc;
+  float* o = dcoff + (long)r * ldc;
+  float a = 0.f;
+  for (int k = lane; k < ldc; k += 64) {
+    const float gk = k < Nc ? g[k] : 0.f;
+    a += gk * (k == j ? rawd[r] : c[k]);
+    o[k] = k == j ? 0.f : gk;
+  }
+  a = wave_sum(a);
+  if (lane == 0) {
+    alpha[r] = a;
+    dcd[r] = g[j];
+  }
+}
+
+// get_cossim, dE for one speaker per block (the finalize step without the centroid term):
+//   dU_r = dcd_r (E^_r - raw_r U^_r [|U|>eps]) / max(|U_r|, eps)
+//   dE_r = (G1_r + dcd_r U^_r - alpha_r E^_r [|E|>eps]) / max(|E_r|, eps) + (sum_i' dU_ji' - dU_r) / (M - 1)
+__global__ __launch_bounds__(256) void ge2e_cossim_bwd_de_kernel(
+    int M, int D, const float* __restrict__ Ehat, const float* __restrict__ Uhat, const float* __restrict__ En,
+    const float* __restrict__ Un, const float* __restrict__ rawd, const float* __restrict__ dcd,
+    const float* __restrict__ alpha, const float* __restrict__ G1, float* __restrict__ dE) {
+  const int j = blockIdx.x;
+  const float invm1 = 1.0f / (float)(M - 1);
+  for (int d = threadIdx.x; d < D; d += 256) {
+    float sumdU = 0.f;
+    for (int i = 0; i < M; ++i) {
+      const int r = j * M + i;
+      const float iu = 1.0f / fmaxf(Un[r], EPS_COS);
+      const float pu = Un[r] > EPS_COS ? 1.f : 0.f;
+      sumdU += dcd[r] * (Ehat[(long)r * D + d] - rawd[r] * Uhat[(long)r * D + d] * pu) * iu;
+    }
+    for (int i = 0; i < M; ++i) {
+      const int r = j * M + i;
+      const long rd = (long)r * D + d;
+      const float iu = 1.0f / fmaxf(Un[r], EPS_COS);
+      const float pu = Un[r] > EPS_COS ? 1.f : 0.f;
+      const float dU = dcd[r] * (Ehat[rd] - rawd[r] * Uhat[rd] * pu) * iu;
+      const float ie = 1.0f / fmaxf(En[r], EPS_COS);
+      const float pe = En[r] > EPS_COS ? 1.f : 0.f;
+      dE[rd] = (G1[rd] + dcd[r] * Uhat[rd] - alpha[r] * Ehat[rd] * pe) * ie + (sumdU - dU) * invm1;
+    }
+  }
+}
+
+// get_cossim, dC_k = (dChat_k - beta_k C^_k [|C|>eps]) / max(|C_k|, eps), one centroid per block
+__global__ __launch_bounds__(256) void ge2e_cossim_bwd_dc_kernel(int D, const float* __restrict__ dchat,
+                                                                 const float* __restrict__ beta,
+                                                                 const float* __restrict__ Chat,
+                                                                 const float* __restrict__ Cn, float* __restrict__ dC) {
+  const int k = blockIdx.x;
+  const float cn = Cn[k];
+  const float icn = 1.0f / fmaxf(cn, EPS_COS);
+  const float pc = cn > EPS_COS ? 1.f : 0.f;
+  for (int d = threadIdx.x; d < D; d += 256) {
+    const long cd = (long)k * D + d;
+    dC[cd] = (dchat[cd] - beta[k] * Chat[cd] * pc) * icn;
+  }
+}
+
+// calc_loss backward, one wave per row: dS_k = g_r (e^{S_k - mx} / (z + 1e-6 e^{-mx}) - [k == j]),
+// g_r = gloss + gper_r, with the forward's max shift (ge2e_calc_loss_kernel)
+__global__ __launch_bounds__(256) void ge2e_calc_loss_bwd_kernel(const float* __restrict__ S, int Bl, int M, int K,
+                                                                 const float* __restrict__ gloss,
+                                                                 const float* __restrict__ gper, float* __restrict__ dS) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= Bl) return;
+  const int j = r / M;
+  const float* s = S + (long)r * K;
+  float mx = -INFINITY;
+  for (int k = lane; k < K; k += 64) mx = fmaxf(mx, s[k]);
+  mx = fmaxf(wave_max(mx), 0.f);
+  float z = 0.f;
+  for (int k = lane; k < K; k += 64) z += __expf(s[k] - mx);
+  z = wave_sum(z);
+  const float inv = 1.0f / (z + EPS_LOG * __expf(-mx));
+  const float g = (gloss ? *gloss : 0.f) + (gper ? gper[r] : 0.f);
+  for (int k = lane; k < K; k += 64) dS[(long)r * K + k] = g * (__expf(s[k] - mx) * inv - (k == j ? 1.f : 0.f));
+}
+
+extern "C" int sv_ge2e_centroids_bwd(const float* dC, int N, int M, int D, float* dE, hipStream_t stream) {
+  if (!dC || !dE || N <= 0 || M <= 0 || D <= 0) return SV_EARG;
+  const long n = (long)N * M * D;
+  hipLaunchKernelGGL(ge2e_centroids_bwd_kernel, dim3((int)std::min<long>((n + 255) / 256, 4096)), dim3(256), 0, stream,
+                     dC, N, M, D, dE);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+namespace {
+struct CosBwdWs {
+  float *ssum, *Ehat, *Uhat, *En, *Un, *rawd, *alpha, *dcd, *Chat, *Cn, *cosr, *dcoff, *G1, *dchat, *betap, *beta, *gemm;
+  size_t total;
+};
+CosBwdWs carve_cos_bwd(float* base, int N, int M, int D, int Nc) {
+  CosBwdWs w;
+  const size_t Bl = (size_t)N * M;
+  const int Ncp = (Nc + 3) & ~3;
+  size_t off = 0;
+  auto take = [&](size_t n) {
+    float* p = base ? base + off : nullptr;
+    off += al(n);
+    return p;
+  };
+  w.ssum = take((size_t)N * D);
+  w.Ehat = take(Bl * D);
+  w.Uhat = take(Bl * D);
+  w.En = take(Bl);
+  w.Un = take(Bl);
+  w.rawd = take(Bl);
+  w.alpha = take(Bl);
+  w.dcd = take(Bl);
+  w.Chat = take((size_t)Ncp * D);
+  w.Cn = take(Ncp);
+  w.cosr = take(Bl * Ncp);
+  w.dcoff = take(Bl * Ncp);
+  w.G1 = take(Bl * D);
+  w.dchat = take((size_t)Ncp * D);
+  w.betap = take(((Bl + 63) / 64) * (size_t)Ncp);
+  w.beta = take(Ncp);
+  size_t g = sv_gemm_f32_workspace((int)Bl, Ncp, D);
+  g = std::max(g, sv_gemm_f32_workspace((int)Bl, D, Ncp));
+  g = std::max(g, sv_gemm_f32_workspace(Ncp, D, (int)Bl));
+  w.gemm = take((g + 3) / 4);
+  w.total = off * sizeof(float);
+  return w;
+}
+}  // namespace
+
+extern "C" size_t sv_ge2e_cossim_bwd_workspace(int N, int M, int D, int Nc) {
+  return carve_cos_bwd(nullptr, N, M, D, Nc).total;
+}
+
+extern "C" int sv_ge2e_cossim_bwd(const float* E, int N, int M, int D, const float* C, int Nc, const float* dcos,
+                                  float* dE, float* dC, float* workspace, hipStream_t stream) {
+  if (!E || !C || !dcos || !dE || !dC || !workspace || N <= 0 || M < 2 || D <= 0 || D % 4 || Nc < N) return SV_EARG;
+  const int Bl = N * M, Ncp = (Nc + 3) & ~3;
+  const CosBwdWs ws = carve_cos_bwd(workspace, N, M, D, Nc);
+  hipLaunchKernelGGL(ge2e_sums_kernel, dim3(N), dim3(256), 0, stream, E, M, D, ws.ssum);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ge2e_rowprep_kernel, dim3((Bl + 3) / 4), dim3(256), 0, stream, E, ws.ssum, Bl, M, D, 0, ws.Ehat,
+                     ws.Uhat, ws.En, ws.Un, ws.rawd);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ge2e_centroid_kernel, dim3(Ncp), dim3(256), 0, stream, C, Nc, 1, D, ws.Chat, ws.Cn);
+  SV_LAUNCH_CHECK();
+  // the raw cosines E^ C^T (padding columns zero)
+  int rc = gemm_f32(1, 1, Bl, Ncp, D, ws.Ehat, D, ws.Chat, D, ws.cosr, Ncp, nullptr, nullptr, 0.f, ws.gemm, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(ge2e_cossim_bwd_rows_kernel, dim3((Bl + 3) / 4), dim3(256), 0, stream, dcos, ws.cosr, ws.rawd, Bl,
+                     M, Nc, Ncp, ws.dcoff, ws.dcd, ws.alpha);
+  SV_LAUNCH_CHECK();
+  // G1 = dcoff C^ ([Bl, Ncp] x [Ncp, D]);  dChat = dcoff^T E^ ([Ncp, Bl] x [Bl, D])
+  rc = gemm_f32(1, 0, Bl, D, Ncp, ws.dcoff, Ncp, ws.Chat, D, ws.G1, D, nullptr, nullptr, 0.f, ws.gemm, stream);
+  if (rc) return rc;
+  rc = gemm_f32(0, 0, Ncp, D, Bl, ws.dcoff, Ncp, ws.Ehat, D, ws.dchat, D, nullptr, nullptr, 0.f, ws.gemm, stream);
+  if (rc) return rc;
+  const int nchunk = (Bl + 63) / 64;
+  hipLaunchKernelGGL(ge2e_beta_partial_kernel, dim3((Nc + 63) / 64, nchunk), dim3(256), 0, stream, ws.dcoff, ws.cosr,
+                     Bl, Nc, Ncp, ws.betap);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ge2e_beta_final_kernel, dim3((Nc + 255) / 256), dim3(256), 0, stream, ws.betap, nchunk, Nc,
+                     ws.beta);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ge2e_cossim_bwd_de_kernel, dim3(N), dim3(256), 0, stream, M, D, ws.Ehat, ws.Uhat, ws.En, ws.Un,
+                     ws.rawd, ws.dcd, ws.alpha, ws.G1, dE);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ge2e_cossim_bwd_dc_kernel, dim3(Nc), dim3(256), 0, stream, D, ws.dchat, ws.beta, ws.Chat, ws.Cn,
+                     dC);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_ge2e_calc_loss_bwd(const float* S, int N, int M, int K, const float* gloss, const float* gper,
+                                     float* dS, hipStream_t stream) {
+  if (!S || !dS || N <= 0 || M <= 0 || K < N) return SV_EARG;
+  const int Bl = N * M;
+  hipLaunchKernelGGL(ge2e_calc_loss_bwd_kernel, dim3((Bl + 3) / 4), dim3(256), 0, stream, S, Bl, M, K, gloss, gper, dS);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
 // ============================================================================
 // EER threshold sweep (train_speech_embedder.py:134-149): for each threshold, the number of
 // similarities above it (all entries and the diagonal k == j).  One block per threshold;

@@ -192,126 +192,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16_t* __r
   }
   g256_epilogue_impl<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
 }
-
-// ---- deeper pipeline (SV_GEMM256P=1): k-tiles of 32 in four LDS stages, three in flight ----
-// Same tile, waves and MFMA order as gemm_bf16_256_kernel (so bit-identical results); the k-tile
-// is halved so four stages fit the same 128 KB, and tile kt + 3 is issued while tile kt is
-// computed.  The wait before each tile's barrier is a counted vmcnt (the two younger tiles stay
-// in flight across it) and the barrier is a raw s_barrier (a __syncthreads would drain every
-// outstanding LDS-DMA, cdna_hip_programming.md "Pipelining across barriers").  Row stride 64 B:
-// physical slot = slot ^ ((row >> 2) & 3) puts each ds_read_b128 lane group on 16 distinct slots.
-#define G256P_BK 32
-__device__ __forceinline__ int g256p_phys_slot(int row, int slot) { return slot ^ ((row >> 2) & 3); }
-
-template <int EPI, int AF = 0>
-__global__ __launch_bounds__(512, 1) void gemm_bf16_256p_kernel(const bf16_t* __restrict__ A, long lda,
-                                                               const bf16_t* __restrict__ B, long ldb,
-                                                               float* __restrict__ C, long ldc, long slab, int M, int N,
-                                                               int K, int kchunk, const float* __restrict__ bias0,
-                                                               const float* __restrict__ bias1, float beta,
-                                                               G256AFrag af = G256AFrag{}) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r = lane & 31, hh = lane >> 5;
-  const int tiles_n = N / G256_BM;
-  const int nwg = tiles_n * (M / G256_BM);
-  const int id = xcd_remap(blockIdx.x, nwg);
-  const int tn = id % tiles_n, tm = id / tiles_n;
-  const int kbeg = blockIdx.y * kchunk;
-  const int nk = (min(K, kbeg + kchunk) - kbeg) / G256P_BK;
-  const int wr = w >> 2, wc = w & 3;
-  constexpr int OPB = G256_BM * G256P_BK * 2;  // 16 KB per operand per stage
-  constexpr int STG = 2 * OPB;
-  // per-thread 16-B chunks of a [256][32] operand tile: q = tid + 512 i -> row q >> 2, slot q & 3
-  const bf16_t* srcA[2];
-  const bf16_t* srcB[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = tid + 512 * i, row = q >> 2, ls = g256p_phys_slot(row, q & 3);
-    if constexpr (!AF) srcA[i] = A + (long)(tm * G256_BM + row) * lda + kbeg + ls * 8;
-    srcB[i] = B + (long)(tn * G256_BM + row) * ldb + kbeg + ls * 8;
-  }
-  // fragment-order A: wave w's instruction i copies KB c = 2 w + i = (row group c / 2, k-step c % 2)
-  long af_row[2];
-  if constexpr (AF) {
-    const int KR = af.bm / 32, frag = af.kg / 16 * 512;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = 2 * w + i, row = tm * G256_BM + 32 * (c >> 1);
-      const int t = row / af.bsl, b = row % af.bsl;
-      af_row[i] = (long)t * af.fs + (long)(((b / af.bm) * 4) * KR + (b / 32) % KR) * frag + (c & 1) * 512 + lane * 8;
-    }
-  }
-  auto issue = [&](int kt) {
-    char* st = smem + (kt & 3) * STG;
-    if constexpr (AF) {
-      const int k0 = kbeg + kt * G256P_BK, g = k0 / af.kg, s0 = (k0 % af.kg) / 16;
-      const long goff = (long)g * (af.bm / 32) * (af.kg / 16 * 512) + (long)s0 * 512;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        __builtin_amdgcn_global_load_lds((glb_vptr_t)(af.base + af_row[i] + goff),
-                                         (lds_vptr_t)(st + (2 * w + i) * 1024), 16, 0, 0);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        __builtin_amdgcn_global_load_lds((glb_vptr_t)(srcA[i] + kt * G256P_BK),
-                                         (lds_vptr_t)(st + (w * 64 + 512 * i) * 16), 16, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((glb_vptr_t)(srcB[i] + kt * G256P_BK),
-                                       (lds_vptr_t)(st + OPB + (w * 64 + 512 * i) * 16), 16, 0, 0);
-  };
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-#pragma unroll
-  for (int p = 0; p < 3; ++p)
-    if (p < nk) issue(p);
-  for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed (this wave's 4 DMAs per tile; the younger tiles stay in flight), then every
-    // wave's: the barrier also ends every read of stage (kt + 3) & 3 = (kt - 1) & 3
-    const int ahead = min(nk - 1 - kt, 2);
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + 3 < nk) issue(kt + 3);
-    const char* As = smem + (kt & 3) * STG;
-    const char* Bs = As + OPB;
-#pragma unroll
-    for (int s = 0; s < G256P_BK / 16; ++s) {
-      bf16x8_t a[4], b[2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if constexpr (AF) {
-          a[i] = *reinterpret_cast<const bf16x8_t*>(As + ((wr * 4 + i) * 2 + s) * 1024 + lane * 16);
-        } else {
-          const int row = wr * 128 + 32 * i + r;
-          a[i] = *reinterpret_cast<const bf16x8_t*>(As + row * 64 + g256p_phys_slot(row, 2 * s + hh) * 16);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = wc * 64 + 32 * j + r;
-        b[j] = *reinterpret_cast<const bf16x8_t*>(Bs + row * 64 + g256p_phys_slot(row, 2 * s + hh) * 16);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf16(a[i], b[j], acc[i][j]);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  g256_epilogue_impl<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
-}
-
-// ---- 8-phase schedule (default; SV_GEMM8P=0 keeps gemm_bf16_256_kernel) ----
+// ---- 8-phase schedule (gemm_bf16_256_kernel is kept for C rows that are not 16-B aligned) ----
 // Same 256 x 256 x 64 tile, LDS images and DMA map as gemm_bf16_256_kernel, computed with
 // v_mfma_f32_16x16x32_bf16 in the phase schedule of cdna_hip_programming.md §5 ("The 256² 8-phase
 // template"): a k-tile is four phases, each one C quadrant (64 rows x 32 columns of the wave's
@@ -374,149 +255,8 @@ __device__ __forceinline__ void g8_epilogue(g8_f32x4 (&acc)[8][4], void* Cv, lon
   }
 }
 
-// SCHED 1: B nh0 stays in registers from phase 0 to phase 3 (no phase-3 re-read), so both
-// operands' fills can be issued in phase 0 (B's last read is then phase 1, A's phase 2: both
-// >= 2 slots before the next k-tile's phase 0) and stay in flight for three phases.
-template <int EPI, int AF = 0, int SCHED = 0>
-__global__ __launch_bounds__(512, 1) void gemm_bf16_8p_kernel(const bf16_t* __restrict__ A, long lda,
-                                                             const bf16_t* __restrict__ B, long ldb, void* __restrict__ C,
-                                                             long ldc, long slab, int M, int N, int K, int kchunk,
-                                                             const float* __restrict__ bias0,
-                                                             const float* __restrict__ bias1, float beta,
-                                                             G256AFrag af = G256AFrag{}) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int tiles_n = N / G256_BM;
-  const int nwg = tiles_n * (M / G256_BM);
-  const int id = xcd_remap(blockIdx.x, nwg);
-  const int tn = id % tiles_n, tm = id / tiles_n;
-  const int kbeg = blockIdx.y * kchunk;
-  const int nk = (min(K, kbeg + kchunk) - kbeg) / G256_BK;
-  const int wr = w >> 2, wc = w & 3;  // wave's 128 x 64 output block: rows wr*128, cols wc*64
-  G256Stage sa, sb;
-  if constexpr (!AF) sa.init(A, lda, tm * G256_BM, kbeg, tid);
-  sb.init(B, ldb, tn * G256_BM, kbeg, tid);
-  constexpr int OPB = G256_BM * G256_BK * 2;  // bytes per operand per stage
-  long af_row[4];
-  if constexpr (AF) {
-    const int KR = af.bm / 32, frag = af.kg / 16 * 512;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = 4 * w + i, row = tm * G256_BM + 32 * (c >> 2);
-      const int t = row / af.bsl, b = row % af.bsl;
-      af_row[i] = (long)t * af.fs + (long)(((b / af.bm) * 4) * KR + (b / 32) % KR) * frag + (c & 3) * 512 + lane * 8;
-    }
-  }
-  auto issue_a = [&](char* lds, int kt) {
-    if constexpr (AF) {
-      const int k0 = kbeg + kt * G256_BK, g = k0 / af.kg, s0 = (k0 % af.kg) / 16;
-      const long goff = (long)g * (af.bm / 32) * (af.kg / 16 * 512) + (long)s0 * 512;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        __builtin_amdgcn_global_load_lds((glb_vptr_t)(af.base + af_row[i] + goff),
-                                         (lds_vptr_t)(lds + (4 * w + i) * 1024), 16, 0, 0);
-    } else {
-      sa.issue(lds, kt, w);
-    }
-  };
-  // fragment of A m-tile mt (16 rows of the wave's 128), k-substep ks (32 of the tile's 64)
-  auto read_a = [&](const char* As, int mt, int ks) -> bf16x8_t {
-    const int row = wr * 128 + 16 * mt + fr;
-    if constexpr (AF) {  // KB (row group, k-step of 16) = [32 rows + 32 * k-half][16 B]
-      return *reinterpret_cast<const bf16x8_t*>(As + ((row >> 5) * 4 + 2 * ks + (fq >> 1)) * 1024 +
-                                                ((row & 31) + 32 * (fq & 1)) * 16);
-    } else {
-      return *reinterpret_cast<const bf16x8_t*>(As + row * 128 + g256_phys_slot(row, 4 * ks + fq) * 16);
-    }
-  };
-  auto read_b = [&](const char* Bs, int nt, int ks) -> bf16x8_t {
-    const int row = wc * 64 + 16 * nt + fr;
-    return *reinterpret_cast<const bf16x8_t*>(Bs + row * 128 + g256_phys_slot(row, 4 * ks + fq) * 16);
-  };
-  g8_f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = g8_f32x4{0.f, 0.f, 0.f, 0.f};
-  if (nk > 0) {
-    issue_a(smem, 0);
-    sb.issue(smem + OPB, 0, w);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  if (wr == 1) {  // the second group runs one barrier behind
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  bf16x8_t a[4][2], b0[2][2], b1[2][2];
-  auto mma = [&](int mh, int nh, const bf16x8_t (&bq)[2][2]) {
-    __builtin_amdgcn_s_barrier();  // end of the read slot
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_setprio(1);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[4 * mh + i][2 * nh + j] = mfma16_bf16(bq[j][ks], a[i][ks], acc[4 * mh + i][2 * nh + j]);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();  // end of the MFMA slot
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* As = smem + (kt & 1) * 2 * OPB;
-    const char* Bs = As + OPB;
-    char* nxt = smem + ((kt + 1) & 1) * 2 * OPB;
-    const bool more = kt + 1 < nk;
-    // phase 0: quadrant (0, 0)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) b0[j][ks] = read_b(Bs, j, ks);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) a[i][ks] = read_a(As, i, ks);
-    if (more) issue_a(nxt, kt + 1);
-    if (SCHED == 1 && more) sb.issue(nxt + OPB, kt + 1, w);
-    mma(0, 0, b0);
-    // phase 1: quadrant (0, 1)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) b1[j][ks] = read_b(Bs, 2 + j, ks);
-    if (SCHED == 0 && more) sb.issue(nxt + OPB, kt + 1, w);
-    mma(0, 1, b1);
-    // phase 2: quadrant (1, 1)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) a[i][ks] = read_a(As, 4 + i, ks);
-    mma(1, 1, b1);
-    // phase 3: quadrant (1, 0); k-tile kt + 1 landed before this read slot ends
-    if constexpr (SCHED == 0) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) b0[j][ks] = read_b(Bs, j, ks);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    mma(1, 0, b0);
-  }
-  if (wr == 0) {  // balance the second group's extra barrier
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  g8_epilogue<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
-}
-
-// ---- 8-phase schedule with the fills spread two per phase (SV_G8_SCHED=2) ----
-// The 8-phase kernel above issues a k-tile's 8 fills per wave in one or two phases, and an
+// ---- 8-phase schedule with the fills spread two per phase ----
+// Issuing a k-tile's 8 fills per wave in one or two phases measured slower: an
 // LDS-DMA issue inside a phase that also reads fragments costs 100-185 cycles
 // (MI355X_MICROARCH.md, "LDS-DMA piece"), so those read slots outlast the other group's 16 MFMAs.
 // Here every phase issues exactly two 64-row chunks (chunk i = operand rows 64 i .. 64 i + 63;

@@ -124,42 +124,32 @@ __global__ void to_time_major_kernel(const float* __restrict__ x, float* __restr
 }
 
 // k-major ("NT") GEMM: both operands k-contiguous; the fast path for every large GEMM.
-// M16 selects the v_mfma_f32_16x16x4_f32 k-tile (each wave's 64x64 as 4x4 blocks of 16x16).
-template <int BM, int BN, int EPI, int D = 1, bool X6 = false, bool X3 = false, bool M16 = false, bool DIAG = false>
+// X6 / X3: the bf16x6 / bf16x3 product forms of the `products` argument (sv_lstm_stack_fwd).
+template <int BM, int BN, int EPI, int D = 1, bool X6 = false, bool X3 = false>
 __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ A, long lda, const float* __restrict__ B,
                                                       long ldb, float* __restrict__ C, long ldc, long slab, int M,
                                                       int N, int K, int kchunk, const float* __restrict__ bias0,
-                                                      const float* __restrict__ bias1, float beta, int gm) {
+                                                      const float* __restrict__ bias1, float beta) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int BLK = M16 ? 16 : 32;                     // MFMA output block edge
+  constexpr int BLK = 32;                                // MFMA output block edge
   constexpr int TM = BM / 2 / BLK, TN = BN / 2 / BLK;    // blocks per wave (2x2 waves)
-  using AccT = typename std::conditional<M16, f32x4, f32x16>::type;
-  constexpr int NR = M16 ? 4 : 16;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // column tile fastest: the blocks an XCD runs together share one A row-panel (the large
   // operand, read from HBM once) and sweep the small B operand, which stays cache-resident
-  // gm > 1: grouped order -- an XCD's consecutive tiles sweep gm row panels per column tile, so
-  // the column panels it streams are reused gm times from its L2 instead of once
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
   const int nwg = tiles_n * tiles_m;
   const int id = xcd_remap(blockIdx.x, nwg);
-  int tn = id % tiles_n, tm = id / tiles_n;
-  if (gm > 1) {
-    const int gsz = gm * tiles_n, first = (id / gsz) * gm;
-    const int g = min(tiles_m - first, gm), r = id % gsz;
-    tm = first + r % g;
-    tn = r / g;
-  }
+  const int tn = id % tiles_n, tm = id / tiles_n;
   const int kbeg = blockIdx.y * kchunk;
   const int kend = min(K, kbeg + kchunk);
   const int wm0 = (w >> 1) * (BM / 2), wn0 = (w & 1) * (BN / 2);
-  AccT acc[TM][TN];
+  f32x16 acc[TM][TN];
   zero_acc(acc);
   if constexpr (X3)
     gemm_mainloop_x3<BM, BN, 256, 16, 2, TM, TN>(A, lda, RowMapLinear{tm * BM, M}, B, ldb, RowMapLinear{tn * BN, N},
                                                  kbeg, kend, lds, tid, wm0, wn0, acc);
   else
-    gemm_mainloop_km_d<BM, BN, 256, SV_BKM, D, TM, TN, DIAG, X6>(A, lda, RowMapLinear{tm * BM, M}, B, ldb,
+    gemm_mainloop_km_d<BM, BN, 256, SV_BKM, D, TM, TN, false, X6>(A, lda, RowMapLinear{tm * BM, M}, B, ldb,
                                                                 RowMapLinear{tn * BN, N}, kbeg, kend, lds, tid, wm0,
                                                                 wn0, acc);
   float* Cz = C + (EPI == EPI_SLAB ? (long)blockIdx.y * slab : 0);
@@ -175,8 +165,8 @@ __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ 
         if (bias1) badd += bias1[col];
       }
 #pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const int row = tm * BM + wm0 + BLK * i + (M16 ? 4 * (lane >> 4) + r : acc_row(r, lane));
+      for (int r = 0; r < 16; ++r) {
+        const int row = tm * BM + wm0 + BLK * i + acc_row(r, lane);
         if (row >= M) continue;
         float v = acc[i][j][r];
         float* dst = Cz + (long)row * ldc + col;
@@ -255,64 +245,6 @@ __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict_
 #define FWD_BM 64
 #define FWD_U 32
 
-__global__ __launch_bounds__(256) void lstm_step_fwd_kernel(const float* __restrict__ hprev,
-                                                            const float* __restrict__ whh, float* __restrict__ gates,
-                                                            const float* __restrict__ cprev, float* __restrict__ cout,
-                                                            float* __restrict__ hout, float* __restrict__ hT, long ldhT,
-                                                            int t, int Bp, int B, int H) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int BN = 4 * FWD_U, LDP = BN + 4, LDH = FWD_BM + 1;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int j0 = blockIdx.x * FWD_U, b0 = blockIdx.y * FWD_BM;
-  const int wm0 = (w >> 1) * 32, wn0 = (w & 1) * 64;
-  f32x16 acc[1][2];
-  zero_acc(acc);
-  if (hprev)
-    gemm_mainloop_km<FWD_BM, BN, 256, SV_BKM, 1, 2>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
-                                                    RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc);
-  float* pre = lds;                   // [64][LDP]
-  float* hs = lds + FWD_BM * LDP;     // [32][LDH]  h^T staging
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) pre[(wm0 + acc_row(r, lane)) * LDP + wn0 + 32 * j + (lane & 31)] = acc[0][j][r];
-  __syncthreads();
-  const long G = 4L * H;
-  for (int e = tid; e < FWD_BM * FWD_U; e += 256) {
-    const int b = e / FWD_U, u = e % FWD_U;
-    const int gb = b0 + b, gj = j0 + u;
-    if (gb >= B || gj >= H) continue;
-    float* gp = gates + (long)gb * G + gj;
-    const float* pr = pre + b * LDP + u;
-    const float pi = pr[0] + gp[0];
-    const float pf = pr[FWD_U] + gp[H];
-    const float pg = pr[2 * FWD_U] + gp[2 * H];
-    const float po = pr[3 * FWD_U] + gp[3 * H];
-    const float i = sv_sigmoid(pi), f = sv_sigmoid(pf), g = tanhf(pg), o = sv_sigmoid(po);
-    const float cp = cprev ? cprev[(long)gb * H + gj] : 0.f;
-    const float c = f * cp + i * g;
-    const float h = o * tanhf(c);
-    gp[0] = i;
-    gp[H] = f;
-    gp[2 * H] = g;
-    gp[3 * H] = o;
-    cout[(long)gb * H + gj] = c;
-    hout[(long)gb * H + gj] = h;
-    hs[u * LDH + b] = h;
-  }
-  if (!hT) return;
-  __syncthreads();
-  // h^T: rows = hidden units, columns = (t+1)*B + b; batch index fastest (coalesced)
-  for (int e = tid; e < FWD_BM * FWD_U; e += 256) {
-    const int u = e / FWD_BM, b = e % FWD_BM;
-    const int gb = b0 + b, gj = j0 + u;
-    if (gb >= B || gj >= H) continue;
-    float* row = hT + (long)gj * ldhT;
-    row[(long)(t + 1) * Bp + gb] = hs[u * LDH + b];
-    if (t == 0) row[gb] = 0.f;  // column block 0 = h_{-1} = 0
-  }
-}
-
 // ============================================================================
 // K3: backward recurrent step at time t.  Block = 64 batch rows x 32 hidden units;
 // wave w computes dG_{t+1}[:, gate w] . W_hh[gate w rows, units] (K = H each, an
@@ -325,73 +257,6 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(const float* __restr
 #define BWD_U 32
 #define X3_GBUF_BYTES (12 * (BWD_BM + BWD_U) * (16 + 8))  // one gate group's X3 double buffer
 
-__global__ __launch_bounds__(256) void lstm_step_bwd_kernel(
-    const float* __restrict__ dgnext, const float* __restrict__ whhT, const float* __restrict__ dhup,
-    const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
-    const float* __restrict__ c_prev, float* __restrict__ dg, float* __restrict__ dcf, float* __restrict__ dgT,
-    long lddgT, int t, int Bp, int B, int H) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int WBUF = 2 * (BWD_BM + BWD_U) * (SV_BKM + 4);
-  constexpr int LDR = BWD_U + 1;
-  constexpr int LDT = BWD_BM + 1;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int j0 = blockIdx.x * BWD_U, b0 = blockIdx.y * BWD_BM;
-  const long G = 4L * H;
-  f32x16 acc[2][1];
-  zero_acc(acc);
-  if (dgnext)
-    gemm_mainloop_km<BWD_BM, BWD_U, 64, SV_BKM, 2, 1>(dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G,
-                                                      RowMapLinear{j0, H}, w * H, (w + 1) * H, lds + w * WBUF, lane,
-                                                      0, 0, acc);
-  __syncthreads();
-  float* red = lds;                          // [4][64][LDR]
-  float* gT = lds + 4 * BWD_BM * LDR;        // [4*32][LDT] dG^T staging
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) red[(w * BWD_BM + 32 * i + acc_row(r, lane)) * LDR + (lane & 31)] = acc[i][0][r];
-  __syncthreads();
-  for (int e = tid; e < BWD_BM * BWD_U; e += 256) {
-    const int b = e / BWD_U, u = e % BWD_U;
-    const int gb = b0 + b, gj = j0 + u;
-    if (gb >= B || gj >= H) continue;
-    const long hi = (long)gb * H + gj;
-    float dh = red[(0 * BWD_BM + b) * LDR + u];
-    dh += red[(1 * BWD_BM + b) * LDR + u];
-    dh += red[(2 * BWD_BM + b) * LDR + u];
-    dh += red[(3 * BWD_BM + b) * LDR + u];
-    if (dhup) dh += dhup[hi];
-    const float* ap = acts + (long)gb * G + gj;
-    const float i = ap[0], f = ap[H], g = ap[2 * H], o = ap[3 * H];
-    const float c = c_t[hi];
-    const float tc = tanhf(c);
-    float dc = dh * o * (1.f - tc * tc);
-    if (dcf_next) dc += dcf_next[hi];
-    const float cp = c_prev ? c_prev[hi] : 0.f;
-    const float d0 = dc * g * i * (1.f - i), d1 = dc * cp * f * (1.f - f);
-    const float d2 = dc * i * (1.f - g * g), d3 = dh * tc * o * (1.f - o);
-    float* dp = dg + (long)gb * G + gj;
-    dp[0] = d0;
-    dp[H] = d1;
-    dp[2 * H] = d2;
-    dp[3 * H] = d3;
-    dcf[hi] = dc * f;
-    gT[(0 * BWD_U + u) * LDT + b] = d0;
-    gT[(1 * BWD_U + u) * LDT + b] = d1;
-    gT[(2 * BWD_U + u) * LDT + b] = d2;
-    gT[(3 * BWD_U + u) * LDT + b] = d3;
-  }
-  if (!dgT) return;
-  __syncthreads();
-  for (int e = tid; e < 4 * BWD_U * BWD_BM; e += 256) {
-    const int gu = e / BWD_BM, b = e % BWD_BM;
-    const int gate = gu / BWD_U, u = gu % BWD_U;
-    const int gb = b0 + b, gj = j0 + u;
-    if (gb >= B || gj >= H) continue;
-    dgT[((long)gate * H + gj) * lddgT + (long)t * Bp + gb] = gT[gu * LDT + b];
-  }
-}
-
 // ============================================================================
 // 8-wave variants of K2/K3 (512 threads, 2 waves per SIMD so one wave's MFMAs cover the
 // other's LDS/global waits).
@@ -399,21 +264,19 @@ __global__ __launch_bounds__(256) void lstm_step_bwd_kernel(
 //         accumulator each, all sharing the same staged A/B tiles.
 //   K3v2: 4 groups of 2 waves, group = gate (its K range of W_hh^T), waves split the rows.
 // ============================================================================
-template <int BKX, int D = 1, bool DIAG = false, bool X6 = false, bool X3 = false>
+template <int BKX, int D = 1, bool X6 = false, bool X3 = false>
 __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __restrict__ hprev,
                                                                const float* __restrict__ whh,
                                                                float* __restrict__ gates,
                                                                const float* __restrict__ cprev,
                                                                float* __restrict__ cout, float* __restrict__ hout,
                                                                float* __restrict__ hT, long ldhT, int t, int Bp, int B,
-                                                               int H, int krot = 0) {
+                                                               int H) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int BN = 4 * FWD_U, LDP = BN + 4, LDH = FWD_BM + 1;
   constexpr int PER = FWD_BM * FWD_U / 512;  // epilogue elements per thread
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int bx, by;
-  xcd_tile_map(krot >> 1, bx, by);
-  const int j0 = bx * FWD_U, b0 = by * FWD_BM;
+  const int j0 = blockIdx.x * FWD_U, b0 = blockIdx.y * FWD_BM;
   const int wm0 = (w >> 2) * 32, wn0 = (w & 3) * 32;
   const long G = 4L * H;
   // the epilogue's inputs do not depend on the GEMM: issue their loads first
@@ -435,9 +298,9 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
       gemm_mainloop_x3<FWD_BM, BN, 512, 32, 2, 1, 1>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
                                                      RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc);
     else
-      gemm_mainloop_km_d<FWD_BM, BN, 512, BKX, D, 1, 1, DIAG, X6>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0},
-                                                                 whh, H, RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid,
-                                                                 wm0, wn0, acc, (krot & 1) * (bx + by));
+      gemm_mainloop_km_d<FWD_BM, BN, 512, BKX, D, 1, 1, false, X6>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0},
+                                                                  whh, H, RowMapGates<FWD_U>{j0, H}, 0, H, lds, tid,
+                                                                  wm0, wn0, acc);
   }
   float* pre = lds;
   float* hs = lds + FWD_BM * LDP;
@@ -477,87 +340,12 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
   }
 }
 
-// K2v4: the K2v2 body over a 64-row x U-unit tile with NW waves (2 x 4U/32 accumulators of
-// 32x32).  U = 16, NW = 4 gives 480 workgroups of 256 threads at c2, two per CU, so one
-// workgroup's barriers and epilogue are covered by the other's MFMAs (K2v2 has one per CU).
-template <int U, int NW, int BKX>
-__global__ __launch_bounds__(NW * 64) void lstm_step_fwd_v4_kernel(const float* __restrict__ hprev,
-                                                                   const float* __restrict__ whh,
-                                                                   float* __restrict__ gates,
-                                                                   const float* __restrict__ cprev,
-                                                                   float* __restrict__ cout, float* __restrict__ hout,
-                                                                   float* __restrict__ hT, long ldhT, int t, int Bp,
-                                                                   int B, int H) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int BM = 64, NT = NW * 64;
-  constexpr int BN = 4 * U, LDP = BN + 4, LDH = BM + 1;
-  constexpr int WN = BN / 32;  // waves across the gate columns
-  static_assert((BM / 32) * WN == NW, "wave grid");
-  constexpr int PER = BM * U / NT;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int j0 = blockIdx.x * U, b0 = blockIdx.y * BM;
-  const int wm0 = (w / WN) * 32, wn0 = (w % WN) * 32;
-  const long G = 4L * H;
-  float xg[PER][4], cpv[PER];
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int e = tid + NT * k, b = e / U, u = e % U;
-    const int gb = b0 + b, gj = j0 + u;
-    const bool ok = gb < B && gj < H;
-    const float* gp = gates + (long)gb * G + gj;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) xg[k][q] = ok ? gp[q * H] : 0.f;
-    cpv[k] = (ok && cprev) ? cprev[(long)gb * H + gj] : 0.f;
-  }
-  f32x16 acc[1][1];
-  zero_acc(acc);
-  if (hprev)
-    gemm_mainloop_km<BM, BN, NT, BKX, 1, 1>(hprev + (long)b0 * H, H, RowMapLinear{0, B - b0}, whh, H,
-                                            RowMapGates<U>{j0, H}, 0, H, lds, tid, wm0, wn0, acc);
-  float* pre = lds;
-  float* hs = lds + BM * LDP;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) pre[(wm0 + acc_row(r, lane)) * LDP + wn0 + (lane & 31)] = acc[0][0][r];
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int e = tid + NT * k, b = e / U, u = e % U;
-    const int gb = b0 + b, gj = j0 + u;
-    if (gb >= B || gj >= H) continue;
-    float* gp = gates + (long)gb * G + gj;
-    const float* pr = pre + b * LDP + u;
-    const float i = sv_sigmoid(pr[0] + xg[k][0]);
-    const float f = sv_sigmoid(pr[U] + xg[k][1]);
-    const float g = tanhf(pr[2 * U] + xg[k][2]);
-    const float o = sv_sigmoid(pr[3 * U] + xg[k][3]);
-    const float c = f * cpv[k] + i * g;
-    const float h = o * tanhf(c);
-    gp[0] = i;
-    gp[H] = f;
-    gp[2 * H] = g;
-    gp[3 * H] = o;
-    cout[(long)gb * H + gj] = c;
-    hout[(long)gb * H + gj] = h;
-    hs[u * LDH + b] = h;
-  }
-  if (!hT) return;
-  __syncthreads();
-  for (int e = tid; e < BM * U; e += NT) {
-    const int u = e / BM, b = e % BM;
-    const int gb = b0 + b, gj = j0 + u;
-    if (gb >= B || gj >= H) continue;
-    float* row = hT + (long)gj * ldhT;
-    row[(long)(t + 1) * Bp + gb] = hs[u * LDH + b];
-    if (t == 0) row[gb] = 0.f;
-  }
-}
-
-template <int BKX, int D = 1, bool DIAG = false, bool X6 = false, bool X3 = false>
+template <int BKX, int D = 1, bool X6 = false, bool X3 = false>
 __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
     const float* __restrict__ dgnext, const float* __restrict__ whhT, const float* __restrict__ dhup,
     const float* __restrict__ dcf_next, const float* __restrict__ acts, const float* __restrict__ c_t,
     const float* __restrict__ c_prev, float* __restrict__ dg, float* __restrict__ dcf, float* __restrict__ dgT,
-    long lddgT, int t, int Bp, int B, int H, int krot = 0, unsigned long long* __restrict__ ts = nullptr) {
+    long lddgT, int t, int Bp, int B, int H, unsigned long long* __restrict__ ts = nullptr) {
   // ts (timing sample, bench only): [start, end] of this launch on the 100 MHz real-time clock,
   // first workgroup start (min) and last workgroup end (max), vector atomics
   if (ts && threadIdx.x == 0) atomicMin(ts, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -568,9 +356,7 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
   constexpr int PER = BWD_BM * BWD_U / 512;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int gate = w >> 1, gt = tid & 127;
-  int bx, by;
-  xcd_tile_map(krot >> 1, bx, by);
-  const int j0 = bx * BWD_U, b0 = by * BWD_BM;
+  const int j0 = blockIdx.x * BWD_U, b0 = blockIdx.y * BWD_BM;
   const long G = 4L * H;
   // prefetch the epilogue's element-wise inputs (independent of the GEMM)
   float av[PER][4], cv[PER], cpv[PER], dcfv[PER], upv[PER];
@@ -597,9 +383,9 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
                                                         reinterpret_cast<char*>(lds) + gate * X3_GBUF_BYTES, gt,
                                                         (w & 1) * 32, 0, acc);
     else
-      gemm_mainloop_km_d<BWD_BM, BWD_U, 128, BKX, D, 1, 1, DIAG, X6>(
+      gemm_mainloop_km_d<BWD_BM, BWD_U, 128, BKX, D, 1, 1, false, X6>(
           dgnext + (long)b0 * G, G, RowMapLinear{0, B - b0}, whhT, G, RowMapLinear{j0, H}, gate * H, (gate + 1) * H,
-          lds + gate * GBUF, gt, (w & 1) * 32, 0, acc, (krot & 1) * (bx + by));
+          lds + gate * GBUF, gt, (w & 1) * 32, 0, acc);
   }
   __syncthreads();
   float* red = lds;                    // [4][64][LDR]
@@ -678,35 +464,6 @@ int k3_x() {
   return m == 2 ? 2 : m == 3 ? 1 : 0;
 }
 
-// prefetch depth of the NT GEMM main loop (SV_GEMM_PIPE = 1 or 2; measured equal at c2 --
-// the GEMMs are not latency-starved -- so 1, the lower-VGPR kernel, stays the default)
-int gemm_pipe() {
-  static int v = [] {
-    const char* e = getenv("SV_GEMM_PIPE");
-    return (e && *e >= '2' && *e <= '5') ? *e - '0' : 1;
-  }();
-  return v;
-}
-
-// exact-fp32 NT GEMM on the 16x16x4 MFMA (SV_GEMM_M16=1) instead of 32x32x2
-int gemm_m16() {
-  static int v = [] {
-    const char* e = getenv("SV_GEMM_M16");
-    return (e && *e == '1') ? 1 : 0;
-  }();
-  return v;
-}
-
-// grouped tile order of the NT GEMM (SV_GEMM_GM row panels per group; 1 = row-panel order)
-int gemm_gm() {
-  static int v = [] {
-    const char* e = getenv("SV_GEMM_GM");
-    const int x = e ? atoi(e) : 1;
-    return (x >= 1 && x <= 64) ? x : 1;
-  }();
-  return v;
-}
-
 template <int BM, int BN, bool AK, bool BKC, int EPI>
 int launch_gemm_t(const float* A, long lda, const float* B, long ldb, float* C, long ldc, long slab, int M, int N,
                   int K, int splitk, int kchunk, const float* b0, const float* b1, float beta, hipStream_t s) {
@@ -717,29 +474,13 @@ int launch_gemm_t(const float* A, long lda, const float* B, long ldb, float* C, 
     constexpr int LDS_KM = 2 * (BM + BN) * (SV_BKM + 4);
     if (gemm_x() == 2)
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 1, false, true>), dim3(tiles, splitk), dim3(256),
-                         12 * (BM + BN) * (16 + 8), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
+                         12 * (BM + BN) * (16 + 8), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
     else if (gemm_x() == 1)
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 1, true>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float),
-                         s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
-    else if (gemm_m16())
-      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 1, false, false, true>), dim3(tiles, splitk), dim3(256),
-                         LDS_KM * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
-    else if (gemm_pipe() == 3)
-      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, SV_PLR>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float),
-                         s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
-    else if (gemm_pipe() == 5)  // profiling only (results invalid): PLR loop with LDS stores, no global loads
-      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, SV_PLR + 1, false, false, false, true>), dim3(tiles, splitk),
-                         dim3(256), LDS_KM * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1,
-                         beta, gemm_gm());
-    else if (gemm_pipe() == 4)  // profiling only (results invalid): LDS + MFMA without global loads
-      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 2, false, false, false, true>), dim3(tiles, splitk), dim3(256),
-                         LDS_KM * sizeof(float), s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
-    else if (gemm_pipe() == 2)
-      hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI, 2>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float), s,
-                         A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
+                         s, A, lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
     else
       hipLaunchKernelGGL((gemm_km_kernel<BM, BN, EPI>), dim3(tiles, splitk), dim3(256), LDS_KM * sizeof(float), s, A,
-                         lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta, gemm_gm());
+                         lda, B, ldb, C, ldc, slab, M, N, K, kchunk, b0, b1, beta);
   } else {
     constexpr int LDS_FLOATS = 2 * SV_BK * (TileLd<AK, BM>::value + TileLd<BKC, BN>::value);
     hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, AK, BKC, EPI>), dim3(tiles, splitk), dim3(256),
@@ -895,39 +636,6 @@ extern "C" int sv_colsum(const float* X, int R, int C, float* out, float* worksp
   return colsum(X, R, C, out, nullptr, workspace, stream);
 }
 
-// stack bwd: weight-gradient GEMMs of layer l per finished chunk on a second stream, or
-// whole-T behind the layer's recurrence.  SV_DW_CHUNKED: 0 (default) none, 1 all layers,
-// 2 layer 0 only.  Measured at c2 (4 HW queues): 0 = 72.4 ms, 2 = 72.5, 1 = 76.5 -- the
-// chunk GEMMs slow the concurrent recurrences more than they shorten the tail.
-// stack bwd: each chunk's dx GEMM on the layer's second stream (SV_DX_SIDE=1) instead of
-// behind the chunk on the recurrence stream (0, default; measured at c2: 69.3 vs 72.3 ms)
-int dx_side() {
-  static int v = [] {
-    const char* e = getenv("SV_DX_SIDE");
-    return (e && *e == '1') ? 1 : 0;
-  }();
-  return v;
-}
-
-// stack bwd: the layer's whole-T weight-gradient GEMMs on its weight-gradient stream side[L + l]
-// (created low-priority by the caller) instead of behind the recurrence on side[l]: the next
-// layer's recurrence (high-priority stream) then takes CUs ahead of them (SV_DW_LOWPRIO=1)
-int dw_lowprio() {
-  static int v = [] {
-    const char* e = getenv("SV_DW_LOWPRIO");
-    return (e && *e == '1') ? 1 : 0;
-  }();
-  return v;
-}
-
-int dw_chunked_layer(int l) {
-  static int v = [] {
-    const char* e = getenv("SV_DW_CHUNKED");
-    return (e && *e >= '0' && *e <= '2') ? *e - '0' : 0;
-  }();
-  return v == 1 || (v == 2 && l == 0);
-}
-
 static bool lstm_dims_ok(int T, int B, int F, int H) {
   return T > 0 && B > 0 && F > 0 && H > 0 && F % 4 == 0 && H % 4 == 0;
 }
@@ -939,182 +647,40 @@ constexpr int FWD_LDS = (FWD_LDS_MAIN > FWD_LDS_EPI ? FWD_LDS_MAIN : FWD_LDS_EPI
 constexpr int BWD_LDS_MAIN = 4 * 2 * (BWD_BM + BWD_U) * (SV_BKM + 4);
 constexpr int BWD_LDS_EPI = 4 * BWD_BM * (BWD_U + 1) + 4 * BWD_U * (BWD_BM + 1);
 constexpr int BWD_LDS = (BWD_LDS_MAIN > BWD_LDS_EPI ? BWD_LDS_MAIN : BWD_LDS_EPI) * (int)sizeof(float);
-// BK = 16 variant of K3v2: 67 KB of LDS instead of 110 KB, so a K3 workgroup fits on a CU
-// beside a 128x128 GEMM workgroup (74 KB) of a concurrent stream (SV_BWD_BK=16; measured no
-// faster at c2, so BK = 32 stays the default)
-constexpr int BWD_LDS_MAIN16 = 4 * 2 * (BWD_BM + BWD_U) * (16 + 4);
-constexpr int BWD_LDS16 = (BWD_LDS_MAIN16 > BWD_LDS_EPI ? BWD_LDS_MAIN16 : BWD_LDS_EPI) * (int)sizeof(float);
-int bwd_bk() {
-  static int v = [] {
-    const char* e = getenv("SV_BWD_BK");
-    return (e && atoi(e) == 16) ? 16 : 32;
-  }();
-  return v;
-}
-// step-kernel variant: 2 = 8-wave (default), 1 = 4-wave; SV_STEP_VARIANT overrides (A/B timing)
+// step-kernel main loops: pipelined local read (gemm_mainloop_km_plr; one barrier per k-tile, LDS
+// writes issued behind the first k-group's MFMAs) with 1 register stage for K2 and 2 for K3.
+// Measured at c2 against the rolling register prefetch of depth 2 (us): K2 35.1-35.6 vs 41.7,
+// K3 37.2-38.0 vs 41.5; c2 step 69.3 -> 66.4-67.0 ms.  The x6 / x3 forms are the bf16x6 product
+// mode's (`products`, F32ProductScope): K2 split at the LDS store (x3), K3 exact.
 constexpr int FWD_X3_MAIN = 12 * (FWD_BM + 4 * FWD_U) * (32 + 8);
 constexpr int FWD_X3_LDS = FWD_X3_MAIN > FWD_LDS ? FWD_X3_MAIN : FWD_LDS;
 constexpr int BWD_X3_MAIN = 4 * X3_GBUF_BYTES;
 constexpr int BWD_X3_LDS = BWD_X3_MAIN > BWD_LDS ? BWD_X3_MAIN : BWD_LDS;
-constexpr int FWD_LDS64 = 2 * (FWD_BM + 4 * FWD_U) * (64 + 4) * (int)sizeof(float);
-int step_variant() {
-  static int v = [] {
-    const char* e = getenv("SV_STEP_VARIANT");
-    return (e && (*e == '1' || *e == '3' || *e == '4')) ? *e - '0' : 2;
-  }();
-  return v;
-}
-// main loop of the K2v2 / K3v2 step kernels (SV_KM_PIPE for K2, SV_K3_PIPE for K3): 1 = double
-// buffer, 2..4 = rolling register prefetch of that depth, 5..8 = pipelined local read with 1..4
-// register stages (gemm_mainloop_km_plr; one barrier per k-tile, LDS writes issued behind the
-// first k-group's MFMAs).  Measured at c2 with the branch-free buffer loads (us, two runs):
-//   K2: depth 2 41.7 | PLR 1 / 2 / 3 / 4 stages 35.1-35.6 / 37.1-37.6 / 38.6 / 37.7
-//   K3: depth 2 41.5 | PLR 1 / 2 / 3 / 4 stages 40.1-40.8 / 37.2-38.0 / 41.3 / 38.3
-// (odd stage counts > 1 lose the compile-time LDS buffer parity).  Defaults K2 5, K3 6: c2 step
-// 69.3 -> 66.4-67.0 ms.  Before the buffer loads depth 2 was the best (K2 39.6 -> 36.4, K3 47.6
-// -> 43.1 us against the double buffer).
-// k-tile rotation of the K2v2 / K3v2 main loops (SV_KROT, default 0): rot = krot * (bx + by).
-// Measured slower (K3 41.7 -> 44.4 us at krot 1): workgroups sharing an operand panel gain from
-// reading the same lines at the same time (L2 hits), so the natural order stays.
-// schedule flags of the fp32 step kernels (their `krot` argument): bit 0 rotates the k-tile
-// order per workgroup (SV_KROT=1), bit 1 maps blocks to XCD-compact tile rectangles
-// (xcd_tile_map; SV_XCD_STEP=1)
-int k_rot() {
-  static int v = [] {
-    const char* e = getenv("SV_KROT");
-    const char* x = getenv("SV_XCD_STEP");
-    return ((e && *e == '1') ? 1 : 0) | ((x && *x == '1') ? 2 : 0);
-  }();
-  return v;
-}
-// profiling only (results invalid): SV_STEP_DIAG=1 runs K2/K3 with every k-tile re-using tile 0
-// from LDS (no further global loads) to separate memory from compute time; =2: the default
-// pipelined-local-read loop with its LDS stores but no global loads past the prologue
-int step_diag() {
-  static int v = [] {
-    const char* e = getenv("SV_STEP_DIAG");
-    return (e && (*e == '1' || *e == '2')) ? *e - '0' : 0;
-  }();
-  return v;
-}
-int km_pipe() {  // K2
-  static int v = [] {
-    const char* e = getenv("SV_KM_PIPE");
-    const int x = e ? atoi(e) : 5;
-    return (x >= 1 && x <= 8) ? x : 5;
-  }();
-  return v;
-}
-int k3_pipe() {  // K3: SV_K3_PIPE, else SV_KM_PIPE, else 6
-  static int v = [] {
-    const char* e = getenv("SV_K3_PIPE");
-    if (!e) e = getenv("SV_KM_PIPE");
-    const int x = e ? atoi(e) : 6;
-    return (x >= 1 && x <= 8) ? x : 6;
-  }();
-  return v;
-}
-constexpr int FWD4_U = 16;
-constexpr int FWD4_LDS_MAIN = 2 * (64 + 4 * FWD4_U) * (SV_BKM + 4);
-constexpr int FWD4_LDS_EPI = 64 * (4 * FWD4_U + 4) + FWD4_U * (64 + 1);
-constexpr int FWD4_LDS = (FWD4_LDS_MAIN > FWD4_LDS_EPI ? FWD4_LDS_MAIN : FWD4_LDS_EPI) * (int)sizeof(float);
-// forward-step grid of the selected variant
-dim3 fwd_step_grid(int B, int H) {
-  if (step_variant() == 4) return dim3((H + FWD4_U - 1) / FWD4_U, (B + 63) / 64);
-  return dim3((H + FWD_U - 1) / FWD_U, (B + FWD_BM - 1) / FWD_BM);
-}
+dim3 fwd_step_grid(int B, int H) { return dim3((H + FWD_U - 1) / FWD_U, (B + FWD_BM - 1) / FWD_BM); }
 void launch_fwd_step(dim3 grid, hipStream_t s, const float* hp, const float* whh, float* g, const float* cp, float* c,
                      float* h, float* hT, long ldhT, int t, int Bp, int B, int H) {
-  if (step_variant() == 4)
-    hipLaunchKernelGGL((lstm_step_fwd_v4_kernel<FWD4_U, 4, SV_BKM>), grid, dim3(256), FWD4_LDS, s, hp, whh, g, cp, c, h,
-                       hT, ldhT, t, Bp, B, H);
-  else if (step_variant() == 2 && k2_x() == 2)
-    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, false, false, true>), grid, dim3(512), FWD_X3_LDS, s, hp,
-                       whh, g, cp, c, h, hT, ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2 && k2_x() == 1)
-    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, false, true>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp,
-                       c, h, hT, ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2 && step_diag() == 2)
-    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, SV_PLR + 2, true>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp,
-                       c, h, hT, ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2 && step_diag())
+  if (k2_x() == 2)
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, false, true>), grid, dim3(512), FWD_X3_LDS, s, hp, whh, g,
+                       cp, c, h, hT, ldhT, t, Bp, B, H);
+  else if (k2_x() == 1)
     hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2, true>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
-                       hT, ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2 && km_pipe() == 2)
-    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 2>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT,
-                       ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2 && km_pipe() == 3)
-    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 3>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT,
-                       ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2 && km_pipe() == 4)
-    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, 4>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT,
-                       ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2 && km_pipe() == 5)
-    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, SV_PLR + 1>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
-                       hT, ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2 && km_pipe() == 6)
-    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, SV_PLR + 2>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
-                       hT, ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2 && km_pipe() == 7)
-    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, SV_PLR + 3>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
-                       hT, ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2 && km_pipe() == 8)
-    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, SV_PLR + 4>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
-                       hT, ldhT, t, Bp, B, H, k_rot());
-  else if (step_variant() == 2)
-    hipLaunchKernelGGL(lstm_step_fwd_v2_kernel<SV_BKM>, grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h, hT, ldhT, t,
-                       Bp, B, H);
-  else if (step_variant() == 3)
-    hipLaunchKernelGGL(lstm_step_fwd_v2_kernel<64>, grid, dim3(512), FWD_LDS64, s, hp, whh, g, cp, c, h, hT, ldhT, t,
-                       Bp, B, H);
+                       hT, ldhT, t, Bp, B, H);
   else
-    hipLaunchKernelGGL(lstm_step_fwd_kernel, grid, dim3(256), FWD_LDS, s, hp, whh, g, cp, c, h, hT, ldhT, t, Bp, B, H);
+    hipLaunchKernelGGL((lstm_step_fwd_v2_kernel<SV_BKM, SV_PLR + 1>), grid, dim3(512), FWD_LDS, s, hp, whh, g, cp, c, h,
+                       hT, ldhT, t, Bp, B, H);
 }
 void launch_bwd_step(dim3 grid, hipStream_t s, const float* dgn, const float* whhT, const float* up, const float* dcfi,
                      const float* acts, const float* ct, const float* cp, float* dg, float* dcfo, float* dgT,
                      long lddgT, int t, int Bp, int B, int H, unsigned long long* ts = nullptr) {
-  if (step_variant() >= 2 && bwd_bk() == 16)
-    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<16, 2>), grid, dim3(512), BWD_LDS16, s, dgn, whhT, up, dcfi, acts, ct,
-                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, 0);
-  else if (step_variant() >= 2 && k3_x() == 2)
-    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, false, false, true>), grid, dim3(512), BWD_X3_LDS, s, dgn,
-                       whhT, up, dcfi, acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && k3_x() == 1)
-    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, false, true>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up,
-                       dcfi, acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && step_diag() == 2)
-    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 2, true>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up,
-                       dcfi, acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && step_diag())
+  if (k3_x() == 2)
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, false, true>), grid, dim3(512), BWD_X3_LDS, s, dgn, whhT, up,
+                       dcfi, acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, ts);
+  else if (k3_x() == 1)
     hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2, true>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
-                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && k3_pipe() == 2)
-    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 2>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
-                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && k3_pipe() == 3)
-    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 3>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
-                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && k3_pipe() == 4)
-    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, 4>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct,
-                       cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && k3_pipe() == 5)
-    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 1>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
-                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && k3_pipe() == 6)  // the default K3
-    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 2>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
-                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot(), ts);
-  else if (step_variant() >= 2 && k3_pipe() == 7)
-    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 3>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
-                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2 && k3_pipe() == 8)
-    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 4>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
-                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, k_rot());
-  else if (step_variant() >= 2)
-    hipLaunchKernelGGL(lstm_step_bwd_v2_kernel<SV_BKM>, grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
-                       dg, dcfo, dgT, lddgT, t, Bp, B, H);
+                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, ts);
   else
-    hipLaunchKernelGGL(lstm_step_bwd_kernel, grid, dim3(256), BWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp, dg, dcfo,
-                       dgT, lddgT, t, Bp, B, H);
+    hipLaunchKernelGGL((lstm_step_bwd_v2_kernel<SV_BKM, SV_PLR + 2>), grid, dim3(512), BWD_LDS, s, dgn, whhT, up, dcfi,
+                       acts, ct, cp, dg, dcfo, dgT, lddgT, t, Bp, B, H, ts);
 }
 }  // namespace
 
@@ -1167,7 +733,7 @@ extern "C" int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, 
 
 namespace {
 struct BwdWs {
-  float *dcf0, *dcf1, *whhT, *wihT, *gws, *gws2;
+  float *dcf0, *dcf1, *whhT, *wihT, *gws;
   size_t total;
 };
 size_t al4(size_t n) { return (n + 63) & ~size_t(63); }
@@ -1188,7 +754,6 @@ BwdWs carve_bwd(float* base, int T, int B, int F, int H) {
   g = std::max(g, sv_gemm_f32_workspace(4 * H, F, TBp));
   g = std::max(g, sv_gemm_f32_workspace(T * B, F, 4 * H));
   w.gws = take((g + 3) / 4);
-  w.gws2 = take((g + 3) / 4);  // the weight-gradient stream's own split-K slabs (stack bwd)
   w.total = off * sizeof(float);
   return w;
 }
@@ -1309,14 +874,13 @@ extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float*
 // ============================================================================
 // Layer-pipelined stack backward.  Layer l runs on side[l], top layer first in issue order:
 // its timesteps in reverse chunks of `chunk` (K3 steps, then -- for l > 0 -- the chunk's
-// dx = dG W_ih GEMM, which is the next-lower layer's dh_up for those timesteps).  Each
-// finished chunk's K-slice of dW_hh / dW_ih (beta = 1 after the first) runs on the layer's
-// weight-gradient stream side[L + l], so no weight GEMM sits on a recurrence; the bias row
-// sums close the layer there.  Layer l-1 waits only for layer l's dx of the same chunk, so
-// one layer's (latency-bound) recurrence overlaps the upper layers' GEMMs.
+// dx = dG W_ih GEMM, which is the next-lower layer's dh_up for those timesteps), then its
+// whole-T weight-gradient GEMMs and bias row sums behind the recurrence on the same stream.
+// Layer l-1 waits only for layer l's dx of the same chunk, so one layer's (latency-bound)
+// recurrence overlaps the upper layers' GEMMs.
 //   xT[l], ld_xT[l]: layer input transposed (layer 0: the frames; l > 0: hT[l-1] + Bp cols)
 //   dx[l] [T,B,H] for l > 0 (dh_up of layer l-1); dx[0] may be NULL
-//   workspace: L * sv_lstm_layer_bwd_workspace(T, B, max(F,H), H) bytes
+//   workspace: sv_lstm_stack_bwd_workspace bytes; side: L streams
 //   ev: L*ceil(T/chunk) + L + 1 caller-created events.  Joins back into `main`.
 // ============================================================================
 extern "C" size_t sv_lstm_stack_bwd_workspace(int L, int T, int B, int F, int H) {
@@ -1347,7 +911,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
   if (e != hipSuccess) return (int)e;
   const dim3 grid((H + BWD_U - 1) / BWD_U, (B + BWD_BM - 1) / BWD_BM);
   for (int l = L - 1; l >= 0; --l) {
-    hipStream_t s = side[l], sw = side[L + l];
+    hipStream_t s = side[l];
     const int Fl = l == 0 ? F : H;
     const BwdWs ws = carve_bwd((float*)((char*)workspace + per * l), T, B, std::max(F, H), H);
     if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
@@ -1373,54 +937,22 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
         SV_LAUNCH_CHECK();
         if (probe && t == tp && (e = hipEventRecord(probe[2 * (l * nch + c) + 1], s)) != hipSuccess) return (int)e;
       }
-      if (l > 0 && dx_side()) {  // dx on the layer's second stream: the recurrence goes on at once
-        if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
-        if ((e = hipStreamWaitEvent(side[L + l], ev[l * nch + c], 0)) != hipSuccess) return (int)e;
+      if (l > 0) {  // dh_up of layer l-1 for this chunk: dx = dG W_ih
         rc = gemm_f32(1, 1, (t1 - t0) * B, Fl, 4 * H, dgates[l] + t0 * BG, 4L * H, ws.wihT, 4L * H,
-                         dx[l] + (long)t0 * B * Fl, Fl, nullptr, nullptr, 0.f, ws.gws2, side[L + l]);
+                      dx[l] + (long)t0 * B * Fl, Fl, nullptr, nullptr, 0.f, ws.gws, s);
         if (rc) return rc;
-        // re-record: layer l-1 (issued after this loop) waits for the dx of this chunk
-        if ((e = hipEventRecord(ev[l * nch + c], side[L + l])) != hipSuccess) return (int)e;
-        if (c == 0 && (e = hipStreamWaitEvent(s, ev[l * nch + c], 0)) != hipSuccess) return (int)e;
-        if (!dw_chunked_layer(l)) continue;
-      } else {
-        if (l > 0) {  // dh_up of layer l-1 for this chunk: dx = dG W_ih
-          rc = gemm_f32(1, 1, (t1 - t0) * B, Fl, 4 * H, dgates[l] + t0 * BG, 4L * H, ws.wihT, 4L * H,
-                           dx[l] + (long)t0 * B * Fl, Fl, nullptr, nullptr, 0.f, ws.gws, s);
-          if (rc) return rc;
-        }
-        if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
       }
-      if (!dw_chunked_layer(l)) continue;
-      // this chunk's share of dW_hh / dW_ih (K = its time columns), accumulated on the layer's
-      // weight-gradient stream while the recurrence moves on to the next chunk
-      if ((e = hipStreamWaitEvent(sw, ev[l * nch + c], 0)) != hipSuccess) return (int)e;
-      const float beta = c == nch - 1 ? 0.f : 1.f;
-      const int Kc = (t1 - t0) * Bp;
-      rc = gemm_f32(1, 1, 4 * H, H, Kc, dgT[l] + (long)t0 * Bp, TBp, hT[l] + (long)t0 * Bp, ldhT, dw_hh[l], H,
-                       nullptr, nullptr, beta, ws.gws2, sw);
-      if (rc) return rc;
-      rc = gemm_f32(1, 1, 4 * H, Fl, Kc, dgT[l] + (long)t0 * Bp, TBp, xT[l] + (long)t0 * Bp, ld_xT[l], dw_ih[l],
-                       Fl, nullptr, nullptr, beta, ws.gws2, sw);
-      if (rc) return rc;
+      if ((e = hipEventRecord(ev[l * nch + c], s)) != hipSuccess) return (int)e;
     }
-    if (!dw_chunked_layer(l)) {  // whole-T weight GEMMs behind the recurrence, on its stream
-      if (dw_lowprio()) {        // ... or on the weight-gradient stream, after the last chunk's dx
-        if ((e = hipStreamWaitEvent(sw, ev[l * nch], 0)) != hipSuccess) return (int)e;
-      } else {
-        sw = s;
-      }
-      float* gw = sw == s ? ws.gws : ws.gws2;
-      rc = gemm_f32(1, 1, 4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, gw, sw);
-      if (rc) return rc;
-      rc = gemm_f32(1, 1, 4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, gw,
-                    sw);
-      if (rc) return rc;
-    }
-    hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(RS_T), 0, sw, dgT[l], (long)TBp, TBp, db_ih[l],
+    // whole-T weight gradients behind the recurrence, on its stream
+    rc = gemm_f32(1, 1, 4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws, s);
+    if (rc) return rc;
+    rc = gemm_f32(1, 1, 4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f, ws.gws, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(RS_T), 0, s, dgT[l], (long)TBp, TBp, db_ih[l],
                        db_hh ? db_hh[l] : nullptr);
     SV_LAUNCH_CHECK();
-    if ((e = hipEventRecord(ev[L * nch + l], sw)) != hipSuccess) return (int)e;
+    if ((e = hipEventRecord(ev[L * nch + l], s)) != hipSuccess) return (int)e;
   }
   for (int l = 0; l < L; ++l)
     if ((e = hipStreamWaitEvent(main, ev[L * nch + l], 0)) != hipSuccess) return (int)e;

@@ -24,7 +24,6 @@
 // one stream.
 #include <algorithm>
 #include <atomic>
-#include <stdlib.h>
 #include "sv_bf16.h"
 #include "../../include/sv_ge2e.h"
 
@@ -846,33 +845,18 @@ int current_cus() {
   int dev = 0;
   return hipGetDevice(&dev) == hipSuccess ? device_cus(dev) : 0;
 }
-// W_hh held in registers (lstm_persist2_fwd_bf16_kernel) when H = 768; SV_PERSIST_W=0 forces the
-// LDS-staged persistent kernel
-// XCD-grouped tile order for the W-stationary kernels (persist_tile); SV_PXCD=0: linear order
-int persist_xcd() {
-  static int v = [] {
-    const char* e = getenv("SV_PXCD");
-    return (e && *e == '0') ? 0 : 1;
-  }();
-  return v;
-}
-int persist_wregs() {
-  static int v = [] {
-    const char* e = getenv("SV_PERSIST_W");
-    return (e && *e == '0') ? 0 : 1;
-  }();
-  return v;
-}
-// test-only fault injection: SV_PERSIST_FAULT=1 (every persistent launch) or =2 (backward
-// launches only) makes workgroup 0 withhold its first arrival and shortens the spin limit, so the
-// launch times out deterministically and quickly
-int persist_fault() {
-  static int v = [] {
-    const char* e = getenv("SV_PERSIST_FAULT");
-    return (e && (*e == '1' || *e == '2')) ? *e - '0' : 0;
-  }();
-  return v;
-}
+// XCD-grouped tile order for the W-stationary kernels (persist_tile)
+constexpr int kPersistXcd = 1;
+#ifdef SV_FAULT_INJECTION
+// test build only (libsv_ge2e_faultinj.so, `make faultinj`): sv_test_set_fault(1) (every
+// persistent launch) or (2) (backward launches only) makes workgroup 0 withhold its first arrival
+// and shortens the spin limit, so the launch times out deterministically and quickly.  The
+// shipped library has no such state: persist_fault() is the constant 0.
+std::atomic<int> g_fault{0};
+int persist_fault() { return g_fault.load(std::memory_order_relaxed); }
+#else
+constexpr int persist_fault() { return 0; }
+#endif
 int fwd_fault() { return persist_fault() == 1; }
 // polls before a hand-off wait gives up (each poll = one L2 round trip + s_sleep 2: ~2^21 polls
 // is seconds, far beyond any legitimate wait)
@@ -881,6 +865,14 @@ unsigned* sync_cnt(unsigned* sync, int chan) {
   return sync + SV_SYNC_CNT + (size_t)chan * SV_PCNT_ROWS * SV_PCNT_STRIDE;
 }
 }  // namespace
+
+#ifdef SV_FAULT_INJECTION
+extern "C" int sv_test_set_fault(int mode) {
+  if (mode < 0 || mode > 2) return SV_EARG;
+  g_fault.store(mode, std::memory_order_relaxed);
+  return SV_OK;
+}
+#endif
 
 unsigned sv_persist_limit() { return persist_limit(); }
 int sv_persist_fault(int bwd) { return bwd ? persist_fault() != 0 : fwd_fault(); }
@@ -906,28 +898,16 @@ extern "C" int sv_persist_fwd_ok(int B, int H) { return sv_persist_fwd_fits(B, H
 
 namespace {
 // row tile of the W-stationary kernels: 32 rows when twice the 64-row grid still fits on the
-// device (B <= 320 at H = 768: c5's per-GPU batch), else 64; SV_PBM=64 forces 64
+// device (B <= 320 at H = 768: c5's per-GPU batch; measured 13.4 -> 10.1 ms at the c5 rank
+// shape), else 64
 int persist_bm(int B, int H, int cus) {
-  static int force64 = [] {
-    const char* e = getenv("SV_PBM");
-    return (e && atoi(e) == 64) ? 1 : 0;
-  }();
   const long grid32 = (long)((H + BF_U - 1) / BF_U) * ((B + 31) / 32);
-  return (!force64 && grid32 <= cus && (B + 31) / 32 <= SV_PCNT_ROWS) ? 32 : 64;
-}
-
-// SV_PFUSEX=0: layer 0 keeps its K1 GEMM instead of the in-kernel input projection
-int persist_fusex() {
-  static int v = [] {
-    const char* e = getenv("SV_PFUSEX");
-    return (e && *e == '0') ? 0 : 1;
-  }();
-  return v;
+  return (grid32 <= cus && (B + 31) / 32 <= SV_PCNT_ROWS) ? 32 : 64;
 }
 }  // namespace
 
 // can the persistent forward compute layer 0's input projection in-kernel (F = 40 features)?
-int sv_persist_fwd_fusex_ok(int H, int F) { return H == 768 && F == 40 && persist_wregs() && persist_fusex(); }
+int sv_persist_fwd_fusex_ok(int H, int F) { return H == 768 && F == 40; }
 
 // one layer's recurrence (K2 for all t) after its K1 has filled `gates`; on `stream`.  With x_bf
 // (layer 0, sv_persist_fwd_fusex_ok): no K1 -- the kernel forms x_t W_ih^T + b_ih + b_hh itself.
@@ -944,34 +924,21 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
   unsigned* status = sync;
   const int Bp = (B + 7) & ~7;
   const long ldhT = (long)(T + 1) * Bp;
-  const bool wst = H == 768 && persist_wregs();
+  const bool wst = H == 768;  // W_hh held in registers (else the LDS-staged persistent kernel)
   // wide tile (32 rows x 64 units, sv_persist3.hip) where the wide backward runs, with or without
-  // the fused layer-0 projection (SV_PFWD3=0 keeps the 32-unit tile)
-  static const int pf3 = [] {
-    const char* v = getenv("SV_PFWD3");
-    return (v && *v == '0') ? 0 : 1;
-  }();
-  const bool wide = wst && pf3 && pbwd3_ok(B, H, cus);
+  // the fused layer-0 projection
+  const bool wide = wst && pbwd3_ok(B, H, cus);
   const int bm = wide ? 32 : wst ? persist_bm(B, H, cus) : BF_BM;
   const dim3 grid(wide ? H / 64 : (H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)grid.y * SV_PCNT_STRIDE * sizeof(unsigned), stream);
   if (e != hipSuccess) return (int)e;
-  // SV_PERSIST_DEBUG (profiling only, results invalid): 1 = skip the hand-off waits, 2 = skip the GEMM
-  static const int dbg = [] {
-    const char* v = getenv("SV_PERSIST_DEBUG");
-    return v ? atoi(v) : 0;
-  }();
   const unsigned limit = persist_limit();
   const int fault = fwd_fault();
-  // SV_PFWD_PIPE=0: the recurrent MFMAs read each A fragment right before use (no LDS pipeline)
-  static const int pipe = [] {
-    const char* v = getenv("SV_PFWD_PIPE");
-    return (v && *v == '0') ? 0 : 1;
-  }();
+  constexpr int dbg = 0, pipe = 1;  // no diagnostic skips; LDS-pipelined A fragments
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   if (wide) {
     const int rc = sv_persist3_fwd_launch(dim3(grid.x * grid.y), (int)grid.x, stream, whh_bf, gates, c_tm, h_tm, h_bf,
-                                          hT, ldhT, T, Bp, B, H, cnt, persist_xcd(), status, limit, fault, x_bf, F,
+                                          hT, ldhT, T, Bp, B, H, cnt, kPersistXcd, status, limit, fault, x_bf, F,
                                           wih_bf, b_ih, b_hh, dbg);
     if (rc) return rc;
   } else if (wst) {
@@ -979,7 +946,7 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
     const size_t lds = (size_t)bm * LDA * 2 + (size_t)bm * (4 * BF_U + 4) * 4 + (size_t)bm * (BF_U + 8) * 2 +
                        (size_t)BF_U * (bm + 8) * 2;
     const dim3 g1(grid.x * grid.y);
-    const int nub = (int)grid.x, xcd = persist_xcd();
+    const int nub = (int)grid.x, xcd = kPersistXcd;
     if (x_bf && bm == 32)
       hipLaunchKernelGGL((lstm_persist2_fwd_bf16_kernel<NS, 32, 5>), g1, dim3(256), lds, stream, whh_bf, gates, c_tm,
                          h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, pipe, x_bf, wih_bf, b_ih,
@@ -1011,23 +978,7 @@ constexpr size_t pbwd_lds(int bm) {
   return (size_t)4 * bm * (BF_U + 4) * 4 + (size_t)bm * (4 * BF_U + 8) * 2 + (size_t)4 * BF_U * (bm + 8) * 2 +
          (size_t)bm * 512;  // + the LDS-DMA operand image (EWD)
 }
-// SV_PBWD_DEBUG (profiling only, results invalid): 1 = no hand-off waits, 4 = no recurrent GEMM, 8 = no global stores, 16 = no
-// elementwise operand loads after the first step, 32 = per-phase cycle stamps into the sync block
-int pbwd_debug() {
-  static int v = [] {
-    const char* e = getenv("SV_PBWD_DEBUG");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-// SV_PBWD_AGPR=0: leave the weight fragments' register class to the compiler
-int pbwd_agpr() {
-  static int v = [] {
-    const char* e = getenv("SV_PBWD_AGPR");
-    return (e && *e == '0') ? 0 : 1;
-  }();
-  return v;
-}
+constexpr int kPbwdDebug = 0;  // the kernels' diagnostic skips, all off in the product library
 template <int NS, int P>
 void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
                  const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B,
@@ -1035,25 +986,13 @@ void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const bf1
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + SV_SYNC_STAMP);
 #define SV_PBWD_LAUNCH(BMV, AG, EW)                                                                               \
   hipLaunchKernelGGL((lstm_persist2_bwd_bf16_kernel<NS, P, BMV, AG, EW>), dim3(grid.x * grid.y), dim3(256), pbwd_lds(BMV), s, \
-                     whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x, persist_xcd(), \
-                     sync, persist_limit(), persist_fault(), pbwd_debug(), dbp, stamps)
-  // SV_PBWD_EWD=0: step operands loaded to registers after the arrival (the former schedule)
-  static const int ewd = [] {
-    const char* e = getenv("SV_PBWD_EWD");
-    return (e && *e == '0') ? 0 : 1;
-  }();
-  if (bm == 32 && !pbwd_agpr())
-    SV_PBWD_LAUNCH(32, false, true);
-  else if (bm == 32 && ewd)
+                     whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, (int)grid.x, kPersistXcd, \
+                     sync, persist_limit(), persist_fault(), kPbwdDebug, dbp, stamps)
+  // weight fragments in AGPRs, step operands staged by LDS-DMA (EWD)
+  if (bm == 32)
     SV_PBWD_LAUNCH(32, true, true);
-  else if (bm == 32)
-    SV_PBWD_LAUNCH(32, true, false);
-  else if (!pbwd_agpr())
-    SV_PBWD_LAUNCH(64, false, true);
-  else if (ewd)
-    SV_PBWD_LAUNCH(64, true, true);
   else
-    SV_PBWD_LAUNCH(64, true, false);
+    SV_PBWD_LAUNCH(64, true, true);
 #undef SV_PBWD_LAUNCH
 }
 }  // namespace
@@ -1063,14 +1002,10 @@ void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const bf1
 // wide-tile backward (lstm_persist3_bwd_bf16_kernel): H = 768, (H / 64) x (B / 32) co-resident,
 // and only where the 32-unit tile would need 64-row blocks (B > 320 on 256 CUs: c3); at smaller
 // B the 32 x 32 tile's twice-as-many workgroups win (c5 rank 8.30 vs 9.48 ms, c4 rank 4.36 vs
-// 5.65).  SV_PBWD3=0 keeps the 32-unit tile everywhere.
+// 5.65).
 int pbwd3_ok(int B, int H, int cus) {
-  static int on = [] {
-    const char* e = getenv("SV_PBWD3");
-    return (e && *e == '0') ? 0 : 1;
-  }();
   const int nrb = (B + 31) / 32;
-  return on && H == 768 && nrb <= SV_PCNT_ROWS && (long)(H / 64) * nrb <= cus && persist_bm(B, H, cus) == 64;
+  return H == 768 && nrb <= SV_PCNT_ROWS && (long)(H / 64) * nrb <= cus && persist_bm(B, H, cus) == 64;
 }
 // row-block size of the backward's fragment-order hand-off (the dx GEMM's A layout)
 int sv_persist_bm(int B, int H, int cus) { return pbwd3_ok(B, H, cus) ? 32 : persist_bm(B, H, cus); }
@@ -1110,9 +1045,10 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   // A-fragment prefetch depth 8 at H = 768 (measured: 4 / 16 no better)
   if (wide) {
-    sv_persist3_bwd_launch(dim3(grid.x * grid.y), (int)grid.x, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT,
-                           dgf, T, Bp, B, H, cnt, persist_xcd(), sync, persist_limit(), persist_fault(), pbwd_debug(),
-                           dbp);
+    const int rc = sv_persist3_bwd_launch(dim3(grid.x * grid.y), (int)grid.x, stream, whhT, acts, c_tm, dhup, up_full,
+                                          dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, kPersistXcd, sync, persist_limit(),
+                                          persist_fault(), kPbwdDebug, dbp);
+    if (rc) return rc;
   } else if (H == 768)
     launch_pbwd<48, 8>(grid, bm, stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, sync,
                        dbp);
@@ -1134,14 +1070,10 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
 
 // ---- layer-wavefront backward (lstm_wave_bwd_bf16_kernel, sv_persist3.hip) ----
 // L = 3, H = 768 and all L x (H/32) x (B/32) workgroups co-resident (c4's 80 rows per rank: 216
-// of 256 CUs).  SV_WAVE_BWD=0 keeps the per-layer schedule.
+// of 256 CUs).  SV_SCHED_PER_LAYER keeps the per-layer schedule.
 int sv_wave_bwd_fits(int L, int B, int H, int cus) {
-  static int on = [] {
-    const char* e = getenv("SV_WAVE_BWD");
-    return (e && *e == '0') ? 0 : 1;
-  }();
   const int nrb = (B + 31) / 32;
-  return on && L == WB_L && H == 768 && nrb <= SV_PCNT_ROWS && (long)L * (H / 32) * nrb <= cus &&
+  return L == WB_L && H == 768 && nrb <= SV_PCNT_ROWS && (long)L * (H / 32) * nrb <= cus &&
          (long)(B + 64) * 4 * H * 2 < (1L << 31);
 }
 namespace {
@@ -1195,8 +1127,8 @@ int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, cons
   a.lddgT = (long)T * a.Bp;
   hipError_t e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
-  sv_wave_bwd_launch(a, stream);
-  SV_LAUNCH_CHECK();
+  const int rc = sv_wave_bwd_launch(a, stream);
+  if (rc) return rc;
   if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
   for (int l = 0; l < L && db_ih; ++l) {
     hipLaunchKernelGGL(persist_db_finalize_kernel, dim3((4 * H + 255) / 256), dim3(256), 0, stream, a.dbp[l], a.nrb,
@@ -1216,6 +1148,35 @@ extern "C" int sv_status_poison(const void* sync, float* x, int n, hipStream_t s
   if (!sync || !x || n <= 0) return SV_EARG;
   hipLaunchKernelGGL(status_poison_kernel, dim3((n + 255) / 256), dim3(256), 0, stream,
                      reinterpret_cast<const unsigned*>(sync), x, n);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+// data-parallel status agreement: flag[0..1] := the status's forward / backward bits as floats
+// (two words of the SUM-reduced gradient buffer: a sum over ranks stays nonzero iff any rank set
+// the bit), then status |= the reduced bits on every rank
+__global__ void status_to_flag_kernel(const unsigned* __restrict__ status, float* __restrict__ flag) {
+  if (threadIdx.x == 0) {
+    const unsigned s = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = (s & 1u) ? 1.f : 0.f;
+    flag[1] = (s & 2u) ? 1.f : 0.f;
+  }
+}
+__global__ void status_merge_kernel(unsigned* __restrict__ status, const float* __restrict__ flag) {
+  if (threadIdx.x == 0) {
+    const unsigned bits = (flag[0] != 0.f ? 1u : 0u) | (flag[1] != 0.f ? 2u : 0u);
+    if (bits) __hip_atomic_fetch_or(status, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+extern "C" int sv_status_to_flag(const void* sync, float* flag, hipStream_t stream) {
+  if (!sync || !flag) return SV_EARG;
+  hipLaunchKernelGGL(status_to_flag_kernel, dim3(1), dim3(64), 0, stream, reinterpret_cast<const unsigned*>(sync), flag);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+extern "C" int sv_status_merge(void* sync, const float* flag, hipStream_t stream) {
+  if (!sync || !flag) return SV_EARG;
+  hipLaunchKernelGGL(status_merge_kernel, dim3(1), dim3(64), 0, stream, reinterpret_cast<unsigned*>(sync), flag);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }

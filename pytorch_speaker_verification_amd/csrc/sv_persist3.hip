@@ -1,7 +1,6 @@
 // Wide-tile persistent backward recurrence (see the kernel comment).  Its own translation unit:
 // built with -mllvm -amdgpu-mfma-vgpr-form=1 (Makefile) so the two accumulators are VGPRs and
 // all 256 AGPRs hold W_hh fragments.
-#include <stdlib.h>
 #include "sv_persist_dev.h"
 #include "../../include/sv_ge2e.h"
 
@@ -307,21 +306,11 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
   constexpr size_t lds = (size_t)4 * 32 * 68 * 4 + (size_t)32 * 264 * 2 + (size_t)256 * 40 * 2 + (size_t)32 * 512 +
                          (size_t)2 * 32 * 64 * 4 + (size_t)4 * NL * 1024;
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + SV_SYNC_STAMP);
-  // SV_PBWD3_DEFER=1: the operand DMA and the dG / dG^T stores inside the next step's k-loop
-  // instead of after the arrival.  Measured slower (c3 bwd 1205 vs 1086 us per layer; the k-loop
-  // phase 5.2k -> 9.0k cycles: the fragment waits count the older stores) -- kept off.
-  static const int defer = [] {
-    const char* e = getenv("SV_PBWD3_DEFER");
-    return (e && *e == '1') ? 1 : 0;
-  }();
-  if (defer)
-    hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL, true>), grid, dim3(256), lds, stream, whhT, acts, c_tm,
-                       dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbg, dbp,
-                       stamps);
-  else
-    hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL, false>), grid, dim3(256), lds, stream, whhT, acts,
-                       c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbg,
-                       dbp, stamps);
+  // (the DEFER form -- the operand DMA and the dG / dG^T stores inside the next step's k-loop --
+  // measured slower: c3 bwd 1205 vs 1086 us per layer; the fragment waits count the older stores)
+  hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL, false>), grid, dim3(256), lds, stream, whhT, acts, c_tm,
+                     dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbg, dbp,
+                     stamps);
   return (int)hipGetLastError();
 }
 
@@ -658,48 +647,20 @@ int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
                            const bf16_t* wih_bf, const float* b_ih, const float* b_hh, int dbg) {
   constexpr size_t base = (size_t)32 * (768 + 8) * 2 + (size_t)32 * (4 * 64 + 4) * 4 + (size_t)32 * 72 * 2 +
                           (size_t)64 * 40 * 2;
-  // SV_PFWD3_DMA=1: h_{t-1} staged by LDS-DMA (sv_persist_dev.h's w3_dma) instead of through
-  // registers; same products in the same order (bit-identical).  Measured slower at c3 (forward
-  // 921 vs 843 µs per layer, step 10.54-10.70 vs 10.32 ms) -- kept off
-  static const int dma_env = [] {
-    const char* e = getenv("SV_PFWD3_DMA");
-    return (e && *e == '1') ? 1 : 0;
-  }();
-  const bool dma = dma_env && (long)(T + 1) * B * H * 2 < (1L << 32) - (1L << 20);
+  // MODE 0: h_{t-1} staged through registers in two halves.  Measured alternatives (bit-identical
+  // results): LDS-DMA staging (MODE 2) 921 vs 843 us per layer at c3; the second half in flight
+  // during the first half's MFMAs (MODE 1) 4.77 vs 4.67 ms for the 3-layer forward
   if (x_bf) {  // layer 0, F = 40: the W_ih fragments take registers, so more W_hh fragments live in LDS
     if (F != 40 || !wih_bf) return SV_EARG;
     constexpr int NL = 16;
-    if (dma)
-      hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 5, 2>), grid, dim3(256),
-                         base + (size_t)4 * NL * 1024, stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H,
-                         cnt, nub, xcd, status, limit, fault, x_bf, wih_bf, b_ih, b_hh, dbg);
-    else
-      hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 5>), grid, dim3(256), base + (size_t)4 * NL * 1024,
-                         stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
-                         fault, x_bf, wih_bf, b_ih, b_hh, dbg);
-  } else if (dma) {
+    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 5>), grid, dim3(256), base + (size_t)4 * NL * 1024,
+                       stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
+                       fault, x_bf, wih_bf, b_ih, b_hh, dbg);
+  } else {
     constexpr int NL = 12;
-    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0, 2>), grid, dim3(256), base + (size_t)4 * NL * 1024,
+    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0>), grid, dim3(256), base + (size_t)4 * NL * 1024,
                        stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
                        fault, nullptr, nullptr, nullptr, nullptr, dbg);
-  } else {
-    // SV_PFWD3_SPLIT=1: the second half of h_{t-1} loads during the first half's MFMAs (measured
-    // no faster: c3 forward 4.77 vs 4.67 ms, step 11.46 vs 11.47 ms -- kept off)
-    static const int split = [] {
-      const char* e = getenv("SV_PFWD3_SPLIT");
-      return (e && *e == '1') ? 1 : 0;
-    }();
-    if (split) {
-      constexpr int NL = 16;
-      hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0, 1>), grid, dim3(256),
-                         base + (size_t)4 * NL * 1024, stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H,
-                         cnt, nub, xcd, status, limit, fault, nullptr, nullptr, nullptr, nullptr, dbg);
-    } else {
-      constexpr int NL = 12;
-      hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0>), grid, dim3(256), base + (size_t)4 * NL * 1024,
-                         stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
-                         fault, nullptr, nullptr, nullptr, nullptr, dbg);
-    }
   }
   return (int)hipGetLastError();
 }

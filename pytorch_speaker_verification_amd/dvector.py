@@ -12,7 +12,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .ops import embedder_forward, embedder_forward_bf16
+from .ops import check_persistent_status, embedder_forward, embedder_forward_bf16
 
 WIN, HOP = 24, 12  # frames: int(.24/.01), int(.12/.01)
 
@@ -31,7 +31,8 @@ def window_frames(logmel, win=WIN, hop=HOP):
 def embed_windows(net, windows, batch=16384, precision="f32"):
     """Embeddings [S, proj] of windows [S, win, nmels] with the module's weights (GPU).
     precision "bf16": the c3 mixed-precision forward (bf16 GEMM operands, fp32 accumulation and
-    state), no activations saved."""
+    state), no activations saved; raises PersistentRecurrenceError if one of its persistent
+    recurrences timed out."""
     if precision not in ("f32", "bf16"):
         raise ValueError(f"precision must be 'f32' or 'bf16', got {precision!r}")
     dev = next(net.parameters()).device
@@ -43,6 +44,10 @@ def embed_windows(net, windows, batch=16384, precision="f32"):
         fwd = embedder_forward_bf16 if precision == "bf16" else embedder_forward
         emb, _ = fwd(xb, layers, net.projection.weight, net.projection.bias, save=False)
         out.append(emb)
+    if precision == "bf16":
+        # a persistent recurrence that timed out (its grid not co-resident) must not return
+        # silently wrong embeddings: wait for this call's status words and raise
+        check_persistent_status(wait=True)
     return torch.cat(out) if out else torch.zeros((0, net.projection.weight.shape[0]), device=dev)
 
 

@@ -12,13 +12,14 @@ plumbing; every FLOP of the path runs in the HIP kernels of libsv_ge2e.so.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
-from ._lib import PersistStatus, call, ptr, require_device, stream_of, lib
+from ._lib import PersistStatus, call, lib, ptr, require_device, schedule_flags, stream_of
 
-PIPELINE_CHUNK = int(os.environ.get("SV_PIPELINE_CHUNK", "32"))  # 0 disables the layer pipeline
+# timesteps per chunk of the layer-pipelined schedules (measured at c2: 16 / 24 / 32 / 48 / 64 ->
+# 69.3 / 69.7 / 69.1 / 69.5 / 69.6 ms per step)
+PIPELINE_CHUNK = 32
 
 # how the fp32 path forms its products (the `products` argument of the C ABI, include/sv_ge2e.h):
 # "mfma_f32" (default, exact fp32 MFMA) or "bf16x6" (three-way bf16 split, six bf16 MFMA products
@@ -73,20 +74,12 @@ class _StreamPool:
     """Side streams + events for the layer-pipelined schedules (one set per device)."""
     _pools = {}
 
-    # SV_STREAM_PRIO=1: the backward pool's recurrence streams (first half) high priority, its
-    # weight-gradient streams (second half) low priority (see SV_DW_LOWPRIO in sv_lstm.hip)
-    PRIO = os.environ.get("SV_STREAM_PRIO", "0") == "1"
-
     @classmethod
-    def get(cls, device, n_streams, n_events, split_prio=False):
+    def get(cls, device, n_streams, n_events):
         key = (device.index, n_streams)
         p = cls._pools.get(key)
         if p is None or len(p[1]) < n_events:
-            if split_prio and cls.PRIO:
-                streams = [torch.cuda.Stream(device=device, priority=-1 if i < n_streams // 2 else 0)
-                           for i in range(n_streams)]
-            else:
-                streams = [torch.cuda.Stream(device=device) for _ in range(n_streams)]
+            streams = [torch.cuda.Stream(device=device) for _ in range(n_streams)]
             events = []
             with torch.cuda.device(device):
                 for _ in range(n_events):
@@ -249,8 +242,8 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
         ld = [T * Bp] + [(T + 1) * Bp] * (L - 1)
         nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
         nev = L * nch + L + 1
-        streams, events = _StreamPool.get(dev, 2 * L, nev, split_prio=True)
-        sp = (ctypes.c_void_p * (2 * L))(*[st_.cuda_stream for st_ in streams])
+        streams, events = _StreamPool.get(dev, L, nev)
+        sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
         call("sv_lstm_stack_bwd", L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
              _parr([l[0] for l in layers]), _parr([l[1] for l in layers]), _parr(st.gates), _parr(st.c_tm),
@@ -296,13 +289,15 @@ def _bf(shape, dev):
     return torch.empty(shape, dtype=torch.bfloat16, device=dev)
 
 
-def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=None):
+def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=None, schedule="auto"):
     """Mixed-precision forward (BASELINE config c3): bf16 GEMM operands, fp32 accumulation,
     bf16 storage of the x-projection and of the activated gates saved for the backward, fp32
     cell state / projection / norm.  Same outputs as embedder_forward.
     status: the caller's PersistStatus (sync block of the persistent recurrences); None = a
     fresh one, checked at the next call / check_persistent_status().  probe: 2*L timing events
-    around the layers' persistent recurrences (include/sv_ge2e.h)."""
+    around the layers' persistent recurrences (include/sv_ge2e.h).  schedule: 'auto' (default),
+    'per_layer', 'per_step' or 'persist' (the SV_SCHED_* flags of include/sv_ge2e.h)."""
+    sched = schedule_flags(schedule)
     require_device(x, w_p, b_p, *[t for l in layers for t in l])
     B, T, F = x.shape
     H = layers[0][1].shape[1]
@@ -345,7 +340,7 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=Non
         call("sv_lstm_stack_fwd_bf16", L, T, B, F, H, ptr(x_bf), _parr([w[0] for w in wbf]),
              _parr([w[1] for w in wbf]), _parr([l[2] for l in layers]), _parr([l[3] for l in layers]),
              _parr(gs), _parr(cs), _parr(hs), _parr(hbs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep, sync.ptr(),
-             _evarr(probe))
+             _evarr(probe), sched)
         _release_status(sync, own)
     else:
         for l, (w_ih, w_hh, b_ih, b_hh) in enumerate(layers):
@@ -367,9 +362,11 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=Non
     return emb, st
 
 
-def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, status=None, probe=None):
+def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, status=None, probe=None,
+                           schedule="auto"):
     """Backward of embedder_forward_bf16 (same ``grads`` / ``grad_ready`` contract as
-    embedder_backward; ``status`` as embedder_forward_bf16)."""
+    embedder_backward; ``status`` and ``schedule`` as embedder_forward_bf16)."""
+    sched = schedule_flags(schedule)
     demb = demb.contiguous()
     require_device(demb)
     T, B, H, P = st.T, st.B, st.H, st.P
@@ -397,8 +394,8 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
         ld = [T * Bp] + [(T + 1) * Bp] * (L - 1)
         nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
         nev = L * nch + L + 1
-        streams, events = _StreamPool.get(dev, 2 * L, nev)
-        sp = (ctypes.c_void_p * (2 * L))(*[st_.cuda_stream for st_ in streams])
+        streams, events = _StreamPool.get(dev, L, nev)
+        sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
         sync, own = _own_status(status, dev)
         call("sv_lstm_stack_bwd_bf16", L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
@@ -406,7 +403,7 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
              _parr(st.hT), ptr(dh_last), _parr(dgs), _parr(dgTs), _parr(dxs),
              _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
              _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
-             PIPELINE_CHUNK, s, sp, ep, sync.ptr(), _evarr(probe))
+             PIPELINE_CHUNK, s, sp, ep, sync.ptr(), _evarr(probe), sched)
         _release_status(sync, own)
         if grad_ready:
             # the projection bucket is enqueued behind the stack backward: with the persistent
@@ -442,19 +439,37 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
     return grads
 
 
+def _flat_grads(params, dev):
+    """Gradient tensors shaped like params, as views of one flat buffer (returned last)."""
+    n = sum(p.numel() for p in params)
+    flat = torch.empty(n, dtype=torch.float32, device=dev)
+    out, off = [], 0
+    for p in params:
+        out.append(flat[off:off + p.numel()].view(p.shape))
+        off += p.numel()
+    return out, flat
+
+
 class EmbedderFunction(torch.autograd.Function):
-    """emb = SpeechEmbedder.forward(x) with params (w_ih, w_hh, b_ih, b_hh)*L, w_p, b_p."""
+    """emb = SpeechEmbedder.forward(x) with params (w_ih, w_hh, b_ih, b_hh)*L, w_p, b_p.
+
+    bf16: the forward and backward share one sync block; if a persistent recurrence of either
+    timed out, every returned gradient is NaN (sv_status_poison), so an optimizer step on them
+    cannot pass unnoticed, and check_persistent_status() raises."""
 
     @staticmethod
-    def forward(ctx, x, num_layers, precision, products, *params):
+    def forward(ctx, x, num_layers, precision, products, schedule, *params):
         L = num_layers
         layers = [tuple(params[4 * l:4 * l + 4]) for l in range(L)]
         w_p, b_p = params[4 * L], params[4 * L + 1]
+        ctx.status = None
         if precision == "bf16":
-            emb, st = embedder_forward_bf16(x.contiguous(), layers, w_p, b_p, save=True)
+            ctx.status = PersistStatus(x.device)
+            emb, st = embedder_forward_bf16(x.contiguous(), layers, w_p, b_p, save=True, status=ctx.status,
+                                            schedule=schedule)
         else:
             emb, st = embedder_forward(x.contiguous(), layers, w_p, b_p, save=True, products=products)
-        ctx.precision, ctx.products = precision, products
+        ctx.precision, ctx.products, ctx.schedule = precision, products, schedule
         ctx.st = st
         ctx.L = L
         ctx.save_for_backward(*params)
@@ -469,7 +484,13 @@ class EmbedderFunction(torch.autograd.Function):
         if ctx.precision == "bf16":
             if need_dx:
                 raise NotImplementedError("input gradients are only produced by the fp32 path")
-            out = embedder_backward_bf16(ctx.st, demb, layers, params[4 * L])
+            grads, flat = _flat_grads(params, demb.device)
+            out = embedder_backward_bf16(ctx.st, demb, layers, params[4 * L], grads=grads, status=ctx.status,
+                                         schedule=ctx.schedule)
+            call("sv_status_poison", ctx.status.ptr(), ptr(flat), flat.numel(), stream_of(flat))
+            ctx.status.arm()
+            _UNCHECKED.append(ctx.status)
+            ctx.status = None
         else:
             out = embedder_backward(ctx.st, demb, layers, params[4 * L], need_dx=need_dx, products=ctx.products)
         ctx.st = None
@@ -477,7 +498,7 @@ class EmbedderFunction(torch.autograd.Function):
             grads, dx = out
         else:
             grads, dx = out, None
-        return (dx, None, None, None, *grads)
+        return (dx, None, None, None, None, *grads)
 
 
 # ----------------------------------------------------------------------------- GE2E

@@ -62,14 +62,15 @@ class HipShardKernels:
 
 
 def all_gather_rows(x, rank, world, group=None):
-    """Concatenate every rank's x [n, ...] along dim 0.  RCCL/NCCL: all_gather_into_tensor;
-    backends without a device all-gather (gloo with GPU tensors) get the equivalent SUM
+    """Concatenate every rank's x [n, ...] along dim 0 with all_gather_into_tensor (RCCL; gloo
+    for CPU tensors).  Gloo has no device all-gather for GPU tensors: there the equivalent SUM
     all-reduce of a zero-padded buffer."""
     n = x.shape[0]
-    out = x.new_zeros((n * world,) + tuple(x.shape[1:]))
-    if dist.get_backend(group) == "nccl":
+    if dist.get_backend(group) == "nccl" or not x.is_cuda:
+        out = x.new_empty((n * world,) + tuple(x.shape[1:]))
         dist.all_gather_into_tensor(out, x.contiguous(), group=group)
     else:
+        out = x.new_zeros((n * world,) + tuple(x.shape[1:]))
         out[rank * n:(rank + 1) * n].copy_(x)
         dist.all_reduce(out, group=group)
     return out
@@ -101,15 +102,17 @@ class ShardedGE2E:
             dist.all_reduce(loss, group=self.group)
         return loss, per, st
 
-    def train(self, E_local, w, b):
-        """Forward + backward for the training step (gloss = 1): (global loss, dE_local,
-        dwdb_partial[2]).  One rank holding every speaker uses the fused 3-launch kernel
-        (ops.ge2e_train); sharded runs take the exchange protocol above."""
+    def train(self, E_local, w, b, reduce_loss=True):
+        """Forward + backward for the training step (gloss = 1): (loss, dE_local, dwdb_partial[2]);
+        the loss is the global sum when reduce_loss, else this shard's partial (the trainer sums
+        the partials inside its gradient all-reduce instead of a collective of its own).  One rank
+        holding every speaker uses the fused 3-launch kernel (ops.ge2e_train); sharded runs take
+        the exchange protocol above."""
         if self.world == 1 and isinstance(self.k, HipShardKernels):
             from .ops import ge2e_train
             loss, _, dE, dwdb = ge2e_train(E_local, w, b)
             return loss, dE, dwdb
-        loss, _, st = self.forward(E_local, w, b)
+        loss, _, st = self.forward(E_local, w, b, reduce_loss=reduce_loss)
         dE, dwdb = self.backward(st, w, b)
         return loss, dE, dwdb
 

@@ -68,6 +68,9 @@ class SpeechEmbedder(nn.Module):
         self.precision = "f32"
         # fp32 product mode of the f32 path: "mfma_f32" (exact) or "bf16x6" (ops.F32_PRODUCT_MODES)
         self.f32_products = "mfma_f32"
+        # bf16 stack schedule: "auto" (measured default), "per_layer", "per_step" or "persist"
+        # (the SV_SCHED_* flags of include/sv_ge2e.h, passed on every call)
+        self.schedule = "auto"
 
     def flat_params(self):
         """Parameters in kernel order: (w_ih, w_hh, b_ih, b_hh) per layer, then w_p, b_p."""
@@ -82,7 +85,7 @@ class SpeechEmbedder(nn.Module):
         if host is not None:  # CPU-resident module: differentiable copies to the GPU and back
             params = [p.to(dev) for p in params]
         out = EmbedderFunction.apply(x.float().to(dev).contiguous(), self.LSTM_stack.num_layers, self.precision,
-                                     self.f32_products, *params)
+                                     self.f32_products, self.schedule, *params)
         return out if host is None else out.to(host)
 
 

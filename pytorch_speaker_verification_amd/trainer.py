@@ -11,7 +11,10 @@ Parameters are flattened into one device buffer (the module's nn.Parameters beco
 of it, so state_dict(), optimizers and checkpoints keep working) so that the gradient
 all-reduce and the clip+SGD update each touch one contiguous buffer:
 
-    flat_p = [ net params (n, padded to n_pad = 4k) | w | b | pad ]   flat_g likewise.
+    flat_p = [ net params (n, padded to n_pad = 4k) | w | b | pad pad | 4 words ]   flat_g likewise;
+    the last 4 words of flat_g ride along the head all-reduce bucket (data parallel): the two
+    status flags of the persistent recurrences and this rank's loss partial (summed, the
+    global loss), so neither needs a collective of its own.
 
 Data parallel: one process per GPU; rank r holds speakers [r*N, (r+1)*N) of a global
 batch of world*N speakers (ShardedGE2E), so the step is the single-GPU step of that
@@ -26,7 +29,10 @@ the persistent bf16 recurrences synchronise through this trainer's own sync bloc
 (``self.status``, include/sv_ge2e.h).  If a hand-off wait times out, the block's sticky status
 is set, the clip + SGD kernels skip the update on the device, the returned loss is NaN, and the
 next ``step()`` (or ``check()``) raises PersistentRecurrenceError -- read through an async
-device-to-pinned copy, so the steady state never synchronises the host.
+device-to-pinned copy, so the steady state never synchronises the host.  Data parallel: each
+rank's status bits travel as flags in the head gradient bucket (SUM all-reduce) and are merged
+back into every rank's status before clip + SGD, so a timeout on one rank skips the update on
+all ranks and every rank raises.  After handling the error, ``reset_status()`` clears the block.
 """
 from __future__ import annotations
 
@@ -47,8 +53,14 @@ class GE2ETrainer:
         self.group = group
         self.write_grads = write_grads
         self.ge2e = ShardedGE2E(group=group)
+        self.status = None
         self._flatten()
-        self.status = PersistStatus(self.flat_p.device)
+        if self.ge2e.world > 1:
+            # every rank starts from rank 0's parameters (as DDP does), so SUM-reduced gradients
+            # update identical replicas even if the ranks' inits differed; only here, where every
+            # rank takes part (a later re-flatten after a device move is rank-local)
+            dist.broadcast(self.flat_p, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0,
+                           group=self.group)
 
     # -------------------------------------------------------------------------------------
     def _flatten(self):
@@ -57,8 +69,8 @@ class GE2ETrainer:
         n = sum(p.numel() for p in params)
         n_pad = (n + 3) // 4 * 4
         self.n, self.n_pad = n, n_pad
-        flat_p = torch.zeros(n_pad + 4, dtype=torch.float32, device=dev)
-        flat_g = torch.zeros(n_pad + 4, dtype=torch.float32, device=dev)
+        flat_p = torch.zeros(n_pad + 8, dtype=torch.float32, device=dev)
+        flat_g = torch.zeros(n_pad + 8, dtype=torch.float32, device=dev)
         off = 0
         self.grad_views = []
         with torch.no_grad():
@@ -80,11 +92,10 @@ class GE2ETrainer:
                 w.grad = flat_g[n_pad:n_pad + 1].view(())
                 b.grad = flat_g[n_pad + 1:n_pad + 2].view(())
         self.flat_p, self.flat_g = flat_p, flat_g
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
-            # every rank starts from rank 0's parameters (as DDP does), so SUM-reduced gradients
-            # update identical replicas even if the ranks' inits differed
-            dist.broadcast(flat_p, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0,
-                           group=self.group)
+        self.flags = flat_g[n_pad + 4:n_pad + 6]      # status flags (sv_status_to_flag / _merge)
+        self.loss_word = flat_g[n_pad + 6:n_pad + 7]  # this rank's loss partial -> the global loss
+        if self.status is None or self.status.block.device != dev:
+            self.status = PersistStatus(dev)
         self._ptrs = [p.data_ptr() for p in params]
         # all-reduce buckets: [off(layer l), off(layer l+1)) per layer; the head bucket runs
         # from the projection weight to the end (proj w, proj b, pad, w, b, pad)
@@ -92,7 +103,7 @@ class GE2ETrainer:
         for p in params:
             offs.append(offs[-1] + p.numel())
         L = len(params) // 4
-        self.buckets = [(offs[4 * l], offs[4 * l + 4]) for l in range(L)] + [(offs[4 * L], n_pad + 4)]
+        self.buckets = [(offs[4 * l], offs[4 * l + 4]) for l in range(L)] + [(offs[4 * L], n_pad + 8)]
         self._comm = None
 
     def _check_layout(self):
@@ -104,6 +115,13 @@ class GE2ETrainer:
         """Wait for every step enqueued so far and raise PersistentRecurrenceError if one of
         them had a persistent-recurrence timeout."""
         self.status.poll(wait=True)
+
+    def reset_status(self):
+        """After a PersistentRecurrenceError: wait for the device, then clear the sticky status so
+        the next step() updates again (the skipped step is not replayed).  Data parallel: every
+        rank calls it (each raised)."""
+        torch.cuda.synchronize(self.flat_p.device)
+        self.status.clear()
 
     def step(self, x, N, M, probe=None):
         """x: [N*M, T, nmels] float32 on this rank's GPU (this rank's N speakers x M
@@ -119,17 +137,21 @@ class GE2ETrainer:
         w, b = self.loss_mod.w, self.loss_mod.b
         bf16 = getattr(net, "precision", "f32") == "bf16"
         products = getattr(net, "f32_products", "mfma_f32")
+        schedule = getattr(net, "schedule", "auto")
         if bf16:
             emb, st = embedder_forward_bf16(x.float().contiguous(), layers, w_p, b_p, status=self.status,
-                                            probe=probe.get("fwd"))
+                                            probe=probe.get("fwd"), schedule=schedule)
         else:
             emb, st = embedder_forward(x.float().contiguous(), layers, w_p, b_p, products=products)
         E = emb.view(N, M, emb.shape[1])
-        loss, dE, dwdb = self.ge2e.train(E, w, b)
+        dp = self.ge2e.world > 1
+        # data parallel: the local loss partial goes to the head bucket's all-reduce (no collective)
+        loss, dE, dwdb = self.ge2e.train(E, w, b, reduce_loss=not dp)
         self.flat_g[self.n_pad:self.n_pad + 2].copy_(dwdb)
         works = []
         ready = None
-        if self.ge2e.world > 1:
+        if dp:
+            self.loss_word.copy_(loss.reshape(1))
             main = torch.cuda.current_stream(x.device)
             if self._comm is None:
                 self._comm = torch.cuda.Stream(device=x.device)
@@ -137,6 +159,10 @@ class GE2ETrainer:
 
             def ready(k, event):
                 lo, hi = self.buckets[k]
+                if k == len(self.buckets) - 1 and bf16:
+                    # the head bucket is enqueued behind the whole stack backward (bf16): the
+                    # status word is final, its bits go along as flags
+                    call("sv_status_to_flag", self.status.ptr(), ptr(self.flags), stream_of(self.flags))
                 if event is None:
                     comm.wait_stream(main)
                 else:
@@ -145,17 +171,24 @@ class GE2ETrainer:
                     works.append(dist.all_reduce(self.flat_g[lo:hi], group=self.group, async_op=True))
         if bf16:
             embedder_backward_bf16(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views, grad_ready=ready,
-                                   status=self.status, probe=probe.get("bwd"))
+                                   status=self.status, probe=probe.get("bwd"), schedule=schedule)
         else:
             embedder_backward(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views, grad_ready=ready,
                               products=products, probe=probe.get("bwd"), kstamp=probe.get("kstamp"))
         for wk in works:
             wk.wait()  # the current (main) stream waits for every bucket
+        if dp:
+            loss = self.loss_word.reshape(())  # the sum of every rank's partial
+            if bf16:  # any rank's timeout -> this rank's status too: every rank skips the update
+                call("sv_status_merge", self.status.ptr(), ptr(self.flags), stream_of(self.flags))
         n = self.n_pad
         st_ = self.status if bf16 else None  # (the fp32 path has no persistent recurrences)
         clip_sgd_step_(self.flat_p[:n], self.flat_g[:n], self.clip_net, self.lr, self.write_grads, status=st_)
         clip_sgd_step_(self.flat_p[n:n + 4], self.flat_g[n:n + 4], self.clip_wb, self.lr, self.write_grads, status=st_)
         if bf16:
+            loss = loss.clone() if dp else loss  # (not a view of flat_g, which the next step reuses)
             call("sv_status_poison", self.status.ptr(), ptr(loss), 1, stream_of(loss))
             self.status.arm()
+        elif dp:
+            loss = loss.clone()
         return loss

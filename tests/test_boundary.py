@@ -40,7 +40,8 @@ def test_c_abi_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(h, s), s
         assert s in _lib.SIGNATURES, f"{s} missing from the ctypes signature table"
-    assert h.sv_abi_version() == 3
+    assert h.sv_abi_version() == _lib.ABI_VERSION == 4
+    assert not hasattr(h, "sv_test_set_fault")  # the fault injector exists only in the test build
     # workspace queries are host-only and callable without a GPU
     assert h.sv_ge2e_workspace_size(64, 10, 256, 64) > 0
     assert h.sv_lstm_layer_bwd_workspace(160, 640, 768, 768) > 0
@@ -93,3 +94,18 @@ def test_ops_refuse_cpu_tensors():
         net(torch.zeros(4, 3, 40))
     with pytest.raises(RuntimeError, match="GPU only"):
         GE2ELoss("cpu")(torch.randn(2, 2, 8))
+
+
+def test_shipped_library_reads_no_environment():
+    """Modes are explicit arguments (include/sv_ge2e.h): no getenv in the product sources, so
+    nothing outside a call's arguments changes what it computes."""
+    import glob
+    for f in glob.glob(os.path.join(ROOT, "pytorch_speaker_verification_amd", "csrc", "*")):
+        assert "getenv" not in open(f).read(), f
+
+
+def test_fault_injection_build_exports_the_test_hook():
+    import ctypes
+    from pytorch_speaker_verification_amd import _lib
+    h = ctypes.CDLL(_lib.FAULT_LIB_PATH)
+    assert hasattr(h, "sv_test_set_fault") and h.sv_abi_version() == _lib.ABI_VERSION

@@ -221,3 +221,52 @@ def test_f32_products_bf16x6_accuracy_and_step():
     (l0, p0), (l1, p1) = res["mfma_f32"], res["bf16x6"]
     assert abs(l1 - l0) <= 1e-5 * abs(l0), (l0, l1)
     assert np.abs(p1 - p0).max() <= 1e-5 * np.abs(p0).max()
+
+
+@pytest.mark.parametrize("tag", ["n8m10_wb", "n4m5", "n3m2"])
+@pytest.mark.parametrize("where", ["cuda", "cpu"])
+def test_dropin_helpers_compose_and_train(tag, where):
+    """GE2E composed from the re-exported drop-in helpers exactly as GE2ELoss.forward does
+    (speech_embedder_net.py:45-48: centroids -> cossim -> w*cos+b -> calc_loss) and
+    differentiated by autograd through the helpers' HIP backward kernels (sv_ge2e_*_bwd) matches
+    the reference-generated golden dE / dw / db; 'cpu': the CPU-resident round trip."""
+    from pytorch_speaker_verification_amd import speech_embedder_net as sen
+    g = golden(f"ge2e_{tag}.npz")
+    E0 = recipe.make_embeddings(int(g["seed"]), int(g["n"]), int(g["m"]), int(g["d"]), bool(g["clustered"]))
+    E = torch.tensor(E0, device=where, requires_grad=True)
+    w = torch.tensor(float(g["w"]), device=where, requires_grad=True)
+    b = torch.tensor(float(g["b"]), device=where, requires_grad=True)
+    centroids = sen.get_centroids(E)
+    cossim = sen.get_cossim(E, centroids)
+    sim_matrix = w * cossim + b
+    loss, per = sen.calc_loss(sim_matrix)
+    loss.backward()
+    ref_loss = float(g["loss"])
+    assert abs(float(loss) - ref_loss) <= 1e-4 * abs(ref_loss)
+    np.testing.assert_allclose(per.detach().cpu().numpy(), g["per"], atol=1e-4)
+    dE = E.grad.cpu().numpy()
+    scale = np.abs(g["dE"]).max()
+    err = float(np.abs(dE - g["dE"]).max() / scale)
+    print(f"\nMEASURED helpers_autograd.{tag}.{where}.dE_rel {err:.3e}")
+    assert err <= 1e-4, err
+    assert abs(float(w.grad) - float(g["dw"])) <= 1e-4 * max(1.0, abs(float(g["dw"])))
+    assert abs(float(b.grad) - float(g["db"])) <= 1e-4 * max(1.0, abs(float(g["db"])))
+
+
+def test_dropin_calc_loss_per_embedding_gradient():
+    """calc_loss's second output is differentiable too (a loss on per-embedding values):
+    against torch autograd of the reference formula (utils.py:126-132) on the same S."""
+    from pytorch_speaker_verification_amd.utils import calc_loss
+    gen = torch.Generator().manual_seed(3)
+    S = (torch.randn(5, 4, 7, generator=gen) * 3).double()
+    wts = torch.randn(5, 4, generator=gen).double()
+    Sr = S.clone().requires_grad_(True)
+    idx = list(range(5))
+    pos = Sr[idx, :, idx]
+    neg = (torch.exp(Sr).sum(dim=2) + 1e-6).log()
+    per_r = -(pos - neg)
+    (per_r.sum() + (per_r * wts).sum()).backward()
+    Sg = S.float().to(DEV).requires_grad_(True)
+    loss, per = calc_loss(Sg)
+    (loss + (per * wts.float().to(DEV)).sum()).backward()
+    np.testing.assert_allclose(Sg.grad.cpu().numpy(), Sr.grad.numpy(), atol=2e-5)

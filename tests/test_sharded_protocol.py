@@ -1,7 +1,7 @@
 """Speaker-sharded GE2E exchange protocol under gloo, world size 2, on CPU.
 
-The product's ShardedGE2E runs its real collective sequence (all_gather of speaker sums,
-SUM all_reduce of the centroid-gradient buffer) with the oracle's per-shard numpy kernels
+The product's ShardedGE2E runs its real collective sequence (all_gather_into_tensor of speaker
+sums, SUM all_reduce of the centroid-gradient buffer) with the oracle's per-shard numpy kernels
 plugged in; the concatenated shard results must equal the unsharded oracle."""
 import os
 import socket
@@ -37,7 +37,12 @@ def _worker(rank, world, port, N, M, D, w, b, q):
         loss, per, st = sh.forward(El, torch.tensor(w), torch.tensor(b))
         dE, dwdb = sh.backward(st, torch.tensor(w), torch.tensor(b))
         dist.all_reduce(dwdb)
-        q.put((rank, float(loss), per.numpy(), dE.numpy(), dwdb.numpy()))
+        # the trainer's form: the loss partial (no reporting collective), summed by the caller
+        part, dE2, _ = sh.train(El, torch.tensor(w), torch.tensor(b), reduce_loss=False)
+        part = part.reshape(1).clone()
+        dist.all_reduce(part)
+        assert np.array_equal(dE2.numpy(), dE.numpy())
+        q.put((rank, float(loss), per.numpy(), dE.numpy(), dwdb.numpy(), float(part[0])))
     finally:
         dist.destroy_process_group()
 
@@ -60,6 +65,7 @@ def test_sharded_ge2e_gloo_world2():
     dE, dw, db = ge2e_np.ge2e_backward(E, w, b)
     for r in range(world):
         assert abs(res[r][1] - loss) < 1e-9 * max(1, abs(loss))  # all-reduced global loss
+        assert abs(res[r][5] - loss) < 1e-9 * max(1, abs(loss))  # summed partials
     np.testing.assert_allclose(np.concatenate([r[2] for r in res]), per, atol=1e-10)
     np.testing.assert_allclose(np.concatenate([r[3] for r in res]), dE, atol=1e-10)
     np.testing.assert_allclose(res[0][4], [dw, db], atol=1e-10)
