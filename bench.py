@@ -310,11 +310,26 @@ def dvector_inference(net, dev, S=16384, T=24, reps=3):
         res.update(ms_per_batch=round(ms, 3), windows_per_sec=round(S / (ms * 1e-3), 1),
                    tflops=round(flops / (ms * 1e-3) / 1e12, 2),
                    mfma_frac=round(flops / (ms * 1e-3) / 1e12 / MI355X_FP32_MFMA_TFLOPS, 4))
-        # the c3 mixed-precision forward on the same windows (bf16 operands, fp32 state)
-        ms16 = _timed(lambda: embed_windows(net, xw, batch=S, precision="bf16"), dev, reps)
+        # the c3 mixed-precision forward on the same windows (bf16 operands, fp32 state), in calls of
+        # the largest co-resident persistent batch (dvector.bf16_batch)
+        from pytorch_speaker_verification_amd.dvector import bf16_batch
+        bb = bf16_batch(H)
+        ms16 = _timed(lambda: embed_windows(net, xw, precision="bf16"), dev, reps)
         res["bf16"] = {"ms_per_batch": round(ms16, 3), "windows_per_sec": round(S / (ms16 * 1e-3), 1),
-                       "tflops": round(flops / (ms16 * 1e-3) / 1e12, 2),
+                       "windows_per_call": bb, "tflops": round(flops / (ms16 * 1e-3) / 1e12, 2),
                        "mfma_frac": round(flops / (ms16 * 1e-3) / 1e12 / MI355X_BF16_MFMA_TFLOPS, 4)}
+        # the reference's call shape: one file's windows per call (dvector_create.py:96-100, tens
+        # to hundreds of windows); 128 windows, per call (kernels + host), fp32 and bf16
+        Sf = 128
+        xf = xw[:Sf].contiguous()
+        flops_f = flops * Sf / S
+        per_file = {"windows": Sf}
+        for prec in ("f32", "bf16"):
+            msf = _timed(lambda: embed_windows(net, xf, precision=prec), dev, max(reps, 10))
+            peak = MI355X_BF16_MFMA_TFLOPS if prec == "bf16" else MI355X_FP32_MFMA_TFLOPS
+            per_file[prec] = {"ms_per_call": round(msf, 3), "windows_per_sec": round(Sf / (msf * 1e-3), 1),
+                              "mfma_frac": round(flops_f / (msf * 1e-3) / 1e12 / peak, 4)}
+        res["per_file_call"] = per_file
         try:
             lstm = torch.nn.LSTM(F, H, num_layers=L, batch_first=True).to(dev)
             proj = torch.nn.Linear(H, P).to(dev)

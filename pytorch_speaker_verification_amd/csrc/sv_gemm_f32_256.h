@@ -1,0 +1,167 @@
+// 256 x BN x 32 exact-fp32 GEMM tile for the big NT GEMMs of the fp32 path (K1 input projection,
+// dx, dW at c2): C[M,N] fp32 = A[M,K] . B[N,K]^T (+ bias0 + bias1 + beta C, or split-K slabs).
+//
+// Why a second fp32 kernel: the 128 x 128 register-staged kernel (gemm_km_kernel) moves every
+// operand through VGPRs and ds_write, and re-reads the A panel once per column sweep (K1: 7.1 GB
+// of HBM traffic per launch against 1.58 GB algorithmic).  Here:
+//   * operands go global -> LDS by LDS-DMA (global_load_lds, 16 B per lane, no VGPR round trip),
+//     two stages of [256][32] fp32 per operand; a row is 128 B = 8 slots of 16 B and row `row`
+//     holds logical slot s at physical slot s ^ ((row >> 1) & 7) (the swizzle is applied to the
+//     per-lane global source, as in sv_gemm256.h), so the MFMA fragment reads below are
+//     conflict-free;
+//   * 8 waves as 2 (M) x 4 (N); a 256 x 256 tile halves the operand bytes per FLOP of 128 x 128;
+//   * exact fp32 products on v_mfma_f32_32x32x2_f32 (MF = 32) or v_mfma_f32_16x16x4_f32 (MF = 16),
+//     B fragment as the MFMA's first operand, so each lane's accumulator holds 4 consecutive C
+//     columns of one row (16-B stores).
+// A k-tile is 32 k = 8192 MFMA cycles per wave: the next tile's DMA (8 instructions per wave) is
+// issued before the current tile's MFMAs and waited for (vmcnt(0) + one barrier) after them.
+// Reduction order: per k-tile, k-groups in order; within a group the MFMA sequence of the fp32
+// k-major tiles (mfma_ktile_km / _km16 in sv_gemm.h): a fixed permutation, deterministic.
+#pragma once
+#include <type_traits>
+#include "sv_gemm.h"
+
+#define GF_BM 256
+#define GF_BK 32
+
+typedef __attribute__((address_space(3))) void* gf_lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gf_glb_ptr_t;
+
+__device__ __forceinline__ int gf_phys_slot(int row, int slot) { return slot ^ ((row >> 1) & 7); }
+
+// one operand's R x 32 fp32 k-tile: thread chunk q = tid + 512 i -> LDS byte q * 16 = row q >> 3,
+// physical slot q & 7, holding logical slot (q & 7) ^ ((row >> 1) & 7) of that row
+template <int R>
+struct GfStage {
+  static constexpr int NI = R * 8 / 512;
+  const float* src[NI];
+  __device__ __forceinline__ void init(const float* base, long ld, int row0, int k0, int tid) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = tid + 512 * i, row = q >> 3, ls = gf_phys_slot(row, q & 7);
+      src[i] = base + (long)(row0 + row) * ld + k0 + ls * 4;
+    }
+  }
+  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      __builtin_amdgcn_global_load_lds((gf_glb_ptr_t)(src[i] + kt * GF_BK),
+                                       (gf_lds_ptr_t)(lds + (wave * 64 + 512 * i) * 16), 16, 0, 0);
+  }
+};
+
+enum { GF_STORE = 0, GF_SLAB = 1 };
+
+template <int BN, int MF, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __restrict__ A, long lda,
+                                                             const float* __restrict__ B, long ldb,
+                                                             float* __restrict__ C, long ldc, long slab, int M, int N,
+                                                             int K, int kchunk, const float* __restrict__ bias0,
+                                                             const float* __restrict__ bias1, float beta) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int WN = BN / 4;                 // wave's columns (64 or 32)
+  constexpr int TM = 128 / MF, TN = WN / MF;  // MFMA blocks per wave
+  using Acc = typename std::conditional<MF == 32, f32x16, f32x4>::type;
+  constexpr int NR = MF == 32 ? 16 : 4;
+  constexpr int OPA = GF_BM * GF_BK * 4, OPB = BN * GF_BK * 4;  // bytes per operand per stage
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tiles_n = N / BN;
+  const int nwg = tiles_n * (M / GF_BM);
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int tn = id % tiles_n, tm = id / tiles_n;
+  const int kbeg = blockIdx.y * kchunk;
+  const int nk = (min(K, kbeg + kchunk) - kbeg) / GF_BK;
+  const int wr = w >> 2, wc = w & 3;
+  GfStage<GF_BM> sa;
+  GfStage<BN> sb;
+  sa.init(A, lda, tm * GF_BM, kbeg, tid);
+  sb.init(B, ldb, tn * BN, kbeg, tid);
+  auto stage = [&](int kt) { return smem + (kt & 1) * (OPA + OPB); };
+  Acc acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < NR; ++e) acc[i][j][e] = 0.f;
+  if (nk > 0) {
+    sa.issue(stage(0), 0, w);
+    sb.issue(stage(0) + OPA, 0, w);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // fragment reads: MF = 32 -> lane (r = lane & 31, h = lane >> 5), k-group g of 8: slot 2 g + h;
+  // MF = 16 -> lane (r = lane & 15, q = lane >> 4), k-group g of 16: slot 4 g + q
+  constexpr int RM = MF == 32 ? 31 : 15;
+  const int fr = lane & RM, fh = MF == 32 ? lane >> 5 : lane >> 4;
+  constexpr int NG = MF == 32 ? GF_BK / 8 : GF_BK / 16;  // k-groups per k-tile
+  auto rd = [&](const char* As, const char* Bs, int g, f32x4 (&a)[TM], f32x4 (&b)[TN]) {
+    const int sl = MF == 32 ? 2 * g + fh : 4 * g + fh;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wr * 128 + MF * i + fr;
+      a[i] = *reinterpret_cast<const f32x4*>(As + row * 128 + gf_phys_slot(row, sl) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wc * WN + MF * j + fr;
+      b[j] = *reinterpret_cast<const f32x4*>(Bs + row * 128 + gf_phys_slot(row, sl) * 16);
+    }
+  };
+  auto mm = [&](const f32x4 (&a)[TM], const f32x4 (&b)[TN]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (MF == 32)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[j][c], a[i][c], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j][c], a[i][c], acc[i][j], 0, 0, 0);
+        }
+  };
+  f32x4 a0[TM], b0[TN], a1[TM], b1[TN];
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* As = stage(kt);
+    const char* Bs = As + OPA;
+    if (kt + 1 < nk) {
+      sa.issue(stage(kt + 1), kt + 1, w);
+      sb.issue(stage(kt + 1) + OPA, kt + 1, w);
+    }
+    rd(As, Bs, 0, a0, b0);
+#pragma unroll
+    for (int g = 0; g < NG; g += 2) {
+      rd(As, Bs, g + 1, a1, b1);
+      mm(a0, b0);
+      if (g + 2 < NG) rd(As, Bs, g + 2, a0, b0);
+      mm(a1, b1);
+    }
+    // the next k-tile landed (this wave's DMA) and every wave is done with this one
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // epilogue: acc[i][j][e] = C[row][4 consecutive cols]
+  float* Cz = C + (EPI == GF_SLAB ? (long)blockIdx.y * slab : 0);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const long row = (long)tm * GF_BM + wr * 128 + MF * i + fr;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < NR / 4; ++q) {
+        // MF = 32: elements 4 q .. 4 q + 3 are columns (4 q & 3) + 8 (q) + 4 h .. + 3 of the block,
+        // i.e. 8 q' + 4 h with q' = q; MF = 16: columns 4 fq .. 4 fq + 3
+        const int c0 = MF == 32 ? 8 * q + 4 * fh : 4 * fh;
+        const int col = tn * BN + wc * WN + MF * j + c0;
+        f32x4 v = f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        float* dst = Cz + row * ldc + col;
+        if (EPI == GF_STORE) {
+          if (bias0) v += *reinterpret_cast<const f32x4*>(bias0 + col);
+          if (bias1) v += *reinterpret_cast<const f32x4*>(bias1 + col);
+          if (beta != 0.f) v += beta * *reinterpret_cast<const f32x4*>(dst);
+        }
+        *reinterpret_cast<f32x4*>(dst) = v;
+      }
+  }
+}

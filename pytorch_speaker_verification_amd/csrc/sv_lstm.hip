@@ -16,6 +16,7 @@
 #include <type_traits>
 #include "sv_common.h"
 #include "sv_gemm.h"
+#include "sv_gemm_f32_256.h"
 #include "../../include/sv_ge2e.h"
 
 #define SV_BKM 32
@@ -540,14 +541,78 @@ GemmPlan plan_gemm(int M, int N, int K) {
   return p;
 }
 
+// ---- 256 x BN LDS-DMA tile (sv_gemm_f32_256.h) for the exact-fp32 NT GEMMs that tile exactly ----
+#ifndef SV_F32_MF
+#define SV_F32_MF 32  // MFMA shape of the 256-tile kernel (16: v_mfma_f32_16x16x4_f32, A/B builds)
+#endif
+int gf256_bn(int N) { return N % 256 == 0 ? 256 : 128; }
+bool gf256_ok(int M, int N, int K, const float* C, long ldc, const float* b0, const float* b1) {
+  return M % GF_BM == 0 && N % 128 == 0 && K % GF_BK == 0 && ldc % 4 == 0 &&
+         !(((uintptr_t)C | (uintptr_t)b0 | (uintptr_t)b1) & 15);
+}
+// one workgroup per CU: split K only to fill the CUs (dW: 36 tiles x 7 slabs at c2)
+GemmPlan plan_gf256(int M, int N, int K) {
+  GemmPlan p;
+  p.bm = GF_BM;
+  p.bn = gf256_bn(N);
+  const long tiles = (long)(M / GF_BM) * (N / p.bn);
+  int sk = 1;
+  if (tiles < 256) sk = (int)std::max(1L, std::min(256L / tiles, (long)K / 1024));
+  p.kchunk = ((K + sk - 1) / sk + GF_BK - 1) / GF_BK * GF_BK;
+  p.splitk = (K + p.kchunk - 1) / p.kchunk;
+  return p;
+}
+template <int BN, int EPI>
+void launch_gf256(dim3 grid, hipStream_t s, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
+                  long slab, int M, int N, int K, int kchunk, const float* b0, const float* b1, float beta) {
+  constexpr size_t lds = 2 * (size_t)(GF_BM + BN) * GF_BK * 4;
+  hipLaunchKernelGGL((gemm_f32_256_kernel<BN, SV_F32_MF, EPI>), grid, dim3(512), lds, s, A, lda, B, ldb, C, ldc, slab,
+                     M, N, K, kchunk, b0, b1, beta);
+}
+int gemm_f32_256(const float* A, long lda, const float* B, long ldb, float* C, long ldc, int M, int N, int K,
+                 const float* bias0, const float* bias1, float beta, float* workspace, hipStream_t stream) {
+  const GemmPlan p = plan_gf256(M, N, K);
+  const int tiles = (M / GF_BM) * (N / p.bn);
+  if (p.splitk == 1) {
+    if (p.bn == 256)
+      launch_gf256<256, GF_STORE>(dim3(tiles, 1), stream, A, lda, B, ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1,
+                                  beta);
+    else
+      launch_gf256<128, GF_STORE>(dim3(tiles, 1), stream, A, lda, B, ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1,
+                                  beta);
+    SV_LAUNCH_CHECK();
+    return SV_OK;
+  }
+  if (!workspace) return SV_EARG;
+  const long slab = (long)M * N;
+  if (p.bn == 256)
+    launch_gf256<256, GF_SLAB>(dim3(tiles, p.splitk), stream, A, lda, B, ldb, workspace, (long)N, slab, M, N, K,
+                               p.kchunk, nullptr, nullptr, 0.f);
+  else
+    launch_gf256<128, GF_SLAB>(dim3(tiles, p.splitk), stream, A, lda, B, ldb, workspace, (long)N, slab, M, N, K,
+                               p.kchunk, nullptr, nullptr, 0.f);
+  SV_LAUNCH_CHECK();
+  const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, stream, workspace, p.splitk, slab, C, ldc, M, N, beta,
+                     bias0, bias1);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
 }  // namespace
 
 F32ProductScope::F32ProductScope(int mode) : prev(t_f32_mode) { t_f32_mode = mode; }
 F32ProductScope::~F32ProductScope() { t_f32_mode = prev; }
 
 extern "C" size_t sv_gemm_f32_workspace(int M, int N, int K) {
+  // the larger of the two kernels' split-K slabs (which one runs depends on pointers and mode)
   const GemmPlan p = plan_gemm(M, N, K);
-  return p.splitk > 1 ? (size_t)p.splitk * M * N * sizeof(float) : 0;
+  size_t ws = p.splitk > 1 ? (size_t)p.splitk * M * N * sizeof(float) : 0;
+  if (M % GF_BM == 0 && N % 128 == 0 && K % GF_BK == 0) {
+    const GemmPlan q = plan_gf256(M, N, K);
+    if (q.splitk > 1) ws = std::max(ws, (size_t)q.splitk * M * N * sizeof(float));
+  }
+  return ws;
 }
 
 extern "C" int sv_gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, const float* A, long lda, const float* B,
@@ -565,6 +630,8 @@ int gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, const float* A, 
   if (a_kcontig ? (K % 4 || lda % 4) : (M % 4 || lda % 4)) return SV_EALIGN;
   if (b_kcontig ? (K % 4 || ldb % 4) : (N % 4 || ldb % 4)) return SV_EALIGN;
   if (((uintptr_t)A | (uintptr_t)B) & 15) return SV_EALIGN;
+  if (a_kcontig && b_kcontig && gemm_x() == 0 && gf256_ok(M, N, K, C, ldc, bias0, bias1))
+    return gemm_f32_256(A, lda, B, ldb, C, ldc, M, N, K, bias0, bias1, beta, workspace, stream);
   const GemmPlan p = plan_gemm(M, N, K);
   const bool ak = a_kcontig != 0, bk = b_kcontig != 0;
   if (p.splitk == 1) {

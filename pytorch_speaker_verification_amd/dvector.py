@@ -27,16 +27,30 @@ def window_frames(logmel, win=WIN, hop=HOP):
     return np.stack([logmel[:, j:j + win].T for j in starts]).astype(np.float32)
 
 
+def bf16_batch(H, limit=16384):
+    """Windows per call of the bf16 forward: the largest multiple of 32 (<= limit) whose whole
+    recurrence grid is co-resident, so each call runs the persistent W-stationary kernels (c3's)
+    instead of one launch per timestep (a 16384-window call does not fit: 0.14 of the bf16 peak)."""
+    from ._lib import lib
+    b = max(32, min(limit, 4096) // 32 * 32)
+    while b > 32 and not lib().sv_persist_fwd_ok(b, H):
+        b -= 32
+    return b if lib().sv_persist_fwd_ok(b, H) else limit
+
+
 @torch.no_grad()
-def embed_windows(net, windows, batch=16384, precision="f32"):
-    """Embeddings [S, proj] of windows [S, win, nmels] with the module's weights (GPU).
-    precision "bf16": the c3 mixed-precision forward (bf16 GEMM operands, fp32 accumulation and
-    state), no activations saved; raises PersistentRecurrenceError if one of its persistent
-    recurrences timed out."""
+def embed_windows(net, windows, batch=None, precision="f32"):
+    """Embeddings [S, proj] of windows [S, win, nmels] with the module's weights (GPU), `batch`
+    windows per call (None: 16384 in fp32; bf16: bf16_batch(), the largest co-resident
+    persistent batch).  precision "bf16": the c3 mixed-precision forward (bf16 GEMM operands,
+    fp32 accumulation and state), no activations saved; raises PersistentRecurrenceError if one
+    of its persistent recurrences timed out."""
     if precision not in ("f32", "bf16"):
         raise ValueError(f"precision must be 'f32' or 'bf16', got {precision!r}")
     dev = next(net.parameters()).device
     layers = net.LSTM_stack.layer_params()
+    if batch is None:
+        batch = bf16_batch(layers[0][1].shape[1]) if precision == "bf16" else 16384
     out = []
     x = torch.as_tensor(windows, dtype=torch.float32)
     for i in range(0, x.shape[0], batch):

@@ -71,23 +71,25 @@ def check_persistent_status(wait=False):
 
 
 class _StreamPool:
-    """Side streams + events for the layer-pipelined schedules (one set per device)."""
+    """Side streams + events for the layer-pipelined schedules, one set per (device, role): the
+    forward and the backward of a step keep separate sets, and a set only ever grows -- an event
+    a call recorded is never destroyed while later work on `main` may still wait on it."""
     _pools = {}
 
     @classmethod
-    def get(cls, device, n_streams, n_events):
-        key = (device.index, n_streams)
+    def get(cls, device, role, n_streams, n_events):
+        key = (device.index, role, n_streams)
         p = cls._pools.get(key)
-        if p is None or len(p[1]) < n_events:
-            streams = [torch.cuda.Stream(device=device) for _ in range(n_streams)]
-            events = []
+        if p is None:
+            p = ([torch.cuda.Stream(device=device) for _ in range(n_streams)], [])
+            cls._pools[key] = p
+        streams, events = p
+        if len(events) < n_events:
             with torch.cuda.device(device):
-                for _ in range(n_events):
+                for _ in range(n_events - len(events)):
                     e = torch.cuda.Event()
                     e.record()  # materialise the native event
                     events.append(e)
-            p = (streams, events)
-            cls._pools[key] = p
         return p
 
 
@@ -155,7 +157,7 @@ def embedder_forward(x, layers, w_p, b_p, save=True, products="mfma_f32"):
         hs = [torch.empty((T + 1, B, H), dtype=torch.float32, device=dev) for _ in range(L)]
         hTs = [torch.empty((H, (T + 1) * Bp), dtype=torch.float32, device=dev) if save else None for _ in range(L)]
         nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
-        streams, events = _StreamPool.get(dev, L, L * nch + 1)
+        streams, events = _StreamPool.get(dev, "fwd", L, L * nch + 1)
         sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * (L * nch + 1))(*[e.cuda_event for e in events[:L * nch + 1]])
         call("sv_lstm_stack_fwd", L, T, B, F, H, ptr(x_tm), _parr([l[0] for l in layers]),
@@ -242,7 +244,7 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
         ld = [T * Bp] + [(T + 1) * Bp] * (L - 1)
         nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
         nev = L * nch + L + 1
-        streams, events = _StreamPool.get(dev, L, nev)
+        streams, events = _StreamPool.get(dev, "bwd", L, nev)
         sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
         call("sv_lstm_stack_bwd", L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
@@ -333,7 +335,7 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=Non
     hTs = [_bf((H, (T + 1) * Bp), dev) if save else None for _ in range(L)]
     if PIPELINE_CHUNK > 0 and L > 1:
         nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
-        streams, events = _StreamPool.get(dev, L, L * nch + 1)
+        streams, events = _StreamPool.get(dev, "fwd", L, L * nch + 1)
         sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * (L * nch + 1))(*[e.cuda_event for e in events[:L * nch + 1]])
         sync, own = _own_status(status, dev)
@@ -394,7 +396,7 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
         ld = [T * Bp] + [(T + 1) * Bp] * (L - 1)
         nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
         nev = L * nch + L + 1
-        streams, events = _StreamPool.get(dev, L, nev)
+        streams, events = _StreamPool.get(dev, "bwd", L, nev)
         sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
         sync, own = _own_status(status, dev)

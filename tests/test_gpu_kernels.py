@@ -14,7 +14,8 @@ DEV = "cuda"
 
 
 @pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 1), (0, 0)])
-@pytest.mark.parametrize("M,N,K", [(100, 72, 40), (256, 768, 640), (3072, 40, 2048), (640, 3072, 768), (8, 4, 4)])
+@pytest.mark.parametrize("M,N,K", [(100, 72, 40), (256, 768, 640), (3072, 40, 2048), (640, 3072, 768), (8, 4, 4),
+                                   (512, 256, 8192), (512, 384, 1024)])   # 256-tile: split-K, BN = 128
 def test_gemm_f32_layouts(ak, bk, M, N, K):
     from pytorch_speaker_verification_amd.ops import gemm_f32
     g = torch.Generator().manual_seed(M * 7 + N * 3 + K + ak * 2 + bk)

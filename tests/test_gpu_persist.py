@@ -22,10 +22,10 @@ def test_persistent_fwd_bf16_equals_per_step(dims, N, M, T):
     a = _run("step", "per_step", dims, N, M, T)
     b = _run("persist", "persist", dims, N, M, T)
     assert int(b["status"][0]) == 0
+    # the forward's outputs; the step's gradients and update are the backward test's
     for k in a:
-        if k == "status":
-            continue
-        np.testing.assert_array_equal(b[k], a[k], err_msg=k)
+        if k in ("emb", "h_last", "loss") or k.startswith(("gates", "c")):
+            np.testing.assert_array_equal(b[k], a[k], err_msg=k)
 
 
 @pytest.mark.parametrize("dims,N,M,T", [((40, 768, 3, 256), 64, 10, 12),   # c3 grid: 24 x 10 workgroups
