@@ -331,9 +331,12 @@ void launch_g256(bool g8, dim3 grid, hipStream_t stream, const bf16_t* A, long l
 BPlan plan_bf16(int M, int N, int K) {
   BPlan p;
   if (gemm256_ok(M, N, K)) {  // one workgroup per CU: split K only to fill the 256 CUs
+    // ... and only for the long weight-gradient reductions (K = T B): a dx GEMM (K = 4H) then sums
+    // K in one order whether it runs per 32-step chunk (per-step schedule) or over all T (the
+    // persistent schedule's fragment-order form), so the two schedules stay bit-identical
     const long tiles = (long)(M / G256_BM) * (N / G256_BM);
     int sk = 1;
-    if (tiles < 256) sk = (int)std::max(1L, std::min(256L / tiles, (long)K / 1024));
+    if (tiles < 256 && K >= 8192) sk = (int)std::max(1L, std::min(256L / tiles, (long)K / 1024));
     p.bm = p.bn = G256_BM;
     p.kchunk = ((K + sk - 1) / sk + G256_BK - 1) / G256_BK * G256_BK;
     p.splitk = (K + p.kchunk - 1) / p.kchunk;
