@@ -170,6 +170,23 @@ int sv_ge2e_train_ok(int N, int M, int D);
 int sv_ge2e_train(const float* E, int N, int M, int D, const float* w, const float* b, float* loss, float* per,
                   float* dE, float* dwdb, float* workspace, hipStream_t stream);
 
+/* the fused kernels in the speaker-sharded form (data parallel; same shape limits as
+ * sv_ge2e_train_ok(N, M, D) for the GLOBAL N):
+ *   sv_ge2e_shard_prep      this shard's per-speaker sums ssum_local [N_local, D] (all-gather them
+ *                           into ssum_all [N, D]) and its rows' normalised state (workspace);
+ *   sv_ge2e_shard_rows      rows against all N centroids, softmax, row backward, then this shard's
+ *                           contribution to red [Np*D + N] (dC^ before the norm Jacobian, beta;
+ *                           SUM-all-reduce it) and its loss / (dw, db) partials;
+ *   sv_ge2e_shard_finalize  this shard's dE from the reduced red.
+ * workspace: sv_ge2e_workspace_size(N_local, M, D, N), kept across the three calls. */
+int sv_ge2e_shard_prep(const float* E, int N_local, int M, int D, float* ssum_local, float* workspace,
+                       hipStream_t stream);
+int sv_ge2e_shard_rows(int N_local, int M, int D, int spk_offset, int N, const float* ssum_all, const float* w,
+                       const float* b, float* per, float* red, float* loss_local, float* dwdb_local, float* workspace,
+                       hipStream_t stream);
+int sv_ge2e_shard_finalize(int N_local, int M, int D, int spk_offset, int N, const float* red, float* dE,
+                           float* workspace, hipStream_t stream);
+
 /* stand-alone helpers (utils.py): C = E.mean(1) [N,D]; cos [N,M,Nc] = get_cossim(E, C) with the
  * diagonal from E's own leave-one-out centroids (utils.py:75,91,113), +1e-6; calc_loss on S [N,M,K]. */
 int sv_ge2e_centroids(const float* E, int N, int M, int D, float* C, hipStream_t stream);

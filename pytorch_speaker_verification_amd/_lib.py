@@ -75,6 +75,9 @@ SIGNATURES = {
     "sv_ge2e_bwd": (_c_int, [_c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_ge2e_train_ok": (_c_int, [_c_int, _c_int, _c_int]),
     "sv_ge2e_train": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "sv_ge2e_shard_prep": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _P, _P]),
+    "sv_ge2e_shard_rows": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "sv_ge2e_shard_finalize": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P]),
     "sv_ge2e_centroids": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _P]),
     "sv_ge2e_cossim_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
     "sv_ge2e_cossim": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _c_int, _P, _P, _P]),

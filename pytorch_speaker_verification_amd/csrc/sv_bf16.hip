@@ -518,9 +518,13 @@ extern "C" int sv_gemm_bf16_bf(int M, int N, int K, const bf16_t* A, long lda, c
   const BPlan p = plan_bf16(M, N, K);
   if (p.bm == G256_BM && p.splitk == 1 && g8_ok(nullptr, 0, bias0, bias1) && ldc % 8 == 0 &&
       !((uintptr_t)C & 15)) {
+    // persistent form: one workgroup per CU walks the tiles, each tile's store tail overlapping
+    // the next tile's first fill
     const int tiles = (M / G256_BM) * (N / G256_BM);
-    launch_g8<G8_STORE_BF16, 0>(dim3(tiles, 1), stream, A, lda, B, ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1,
-                                0.f);
+    const int cus = sv_stream_cus(stream);
+    const int grid = std::min(tiles, cus > 0 ? cus : 256);
+    hipLaunchKernelGGL((gemm_bf16_8qp_kernel<G8_STORE_BF16>), dim3(grid), dim3(512), G256_LDS, stream, A, lda, B, ldb,
+                       (void*)C, ldc, M, N, K, bias0, bias1, 0.f);
   } else if ((long)((M + 127) / 128) * ((N + 127) / 128) < 128) {
     launch_bf<64, 64, BEPI_STORE_BF16>(A, lda, B, ldb, C, ldc, 0, M, N, K, 1, ((K + BBK - 1) / BBK) * BBK, bias0,
                                        bias1, 0.f, stream);

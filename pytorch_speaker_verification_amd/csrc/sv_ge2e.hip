@@ -445,11 +445,13 @@ extern "C" int sv_ge2e_bwd(int N, int M, int D, const float* w, const float* b, 
 #define GF_DMAX 256
 #define GF_MMAX 16
 
+// ssum (sharded form): the speaker's sum goes out for the all-gather instead of C^ / |C| (the
+// centroids of every rank's speakers are formed after it by ge2e_centroid_kernel)
 __global__ __launch_bounds__(256) void ge2e_prep_kernel(const float* __restrict__ E, int M, int D,
                                                         float* __restrict__ Chat, float* __restrict__ Cn,
                                                         float* __restrict__ Ehat, float* __restrict__ Uhat,
                                                         float* __restrict__ En, float* __restrict__ Un,
-                                                        float* __restrict__ rawd) {
+                                                        float* __restrict__ rawd, float* __restrict__ ssum) {
   // one pass over the speaker's rows: wave w holds rows w, w + 4, ... (lane: d = 4 lane .. + 3,
   // D <= 256), their per-wave partial sums meet in LDS (added in wave order, rows in order)
   constexpr int RW = (GF_MMAX + 3) / 4;
@@ -501,7 +503,9 @@ __global__ __launch_bounds__(256) void ge2e_prep_kernel(const float* __restrict_
   }
   const float cn = sqrtf(v[3 * RW]);
   const float icn = 1.0f / fmaxf(cn, EPS_COS);
-  if (w == 0) {
+  if (w == 0 && ssum) {
+    if (dok) *reinterpret_cast<float4*>(ssum + (long)j * D + 4 * lane) = sum;
+  } else if (w == 0) {
     if (dok) *reinterpret_cast<float4*>(Chat + (long)j * D + 4 * lane) = float4{c.x * icn, c.y * icn, c.z * icn, c.w * icn};
     if (lane == 0) Cn[j] = cn;
   }
@@ -533,7 +537,7 @@ __global__ __launch_bounds__(256) void ge2e_prep_kernel(const float* __restrict_
 #define GF_ROWW 4
 __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __restrict__ Chat, const float* __restrict__ Ehat,
                                                         const float* __restrict__ rawd, int Bl, int M, int N, int D,
-                                                        int ldc, const float* __restrict__ wp,
+                                                        int ldc, int s0, const float* __restrict__ wp,
                                                         const float* __restrict__ bp, float* __restrict__ per,
                                                         float* __restrict__ cos, float* __restrict__ dcos,
                                                         float* __restrict__ alpha, float* __restrict__ dcd,
@@ -558,7 +562,7 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
   __syncthreads();
   if (r >= Bl) return;
   const float wv = *wp, bv = *bp;
-  const int sg = r / M;
+  const int sg = s0 + r / M;  // global speaker of this row (s0: the shard's first)
   const float rd = rawd[r];
   // cosines: KS speaker lanes x DS d-slices (DS = 1 for N > 32: lane k and k + 64 over all of
   // D; small N splits D so the wave's lanes all work, the slices then meet by a butterfly), E^
@@ -669,8 +673,12 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
 // 4 consecutive d (16-B loads), s one of 4 row sub-groups, so a wave's batch of GF_COLU loads
 // spans 4 GF_COLU rows and the whole c2 batch (640 rows) is one round trip to L2; rows in a fixed
 // order per (wave, sub-group), the sub-groups then the waves added in a fixed order.
+// PARTIAL (sharded form): k runs over all N speakers, the rows are this shard's; beta_k and dC^_k
+// (before the norm Jacobian) go to the reduce buffer [Np][D] + [N] for the all-reduce, and the
+// shard's dE is formed after it (ge2e_finalize_kernel); loss / dw / db are this shard's sums.
 #define GF_COLW 16
 #define GF_COLU 10
+template <bool PARTIAL>
 __global__ __launch_bounds__(64 * GF_COLW) void ge2e_cols_kernel(int Bl, int M, int N, int D, int ldc,
                                                         const float* __restrict__ Chat, const float* __restrict__ Cn,
                                                         const float* __restrict__ Ehat, const float* __restrict__ Uhat,
@@ -680,7 +688,8 @@ __global__ __launch_bounds__(64 * GF_COLW) void ge2e_cols_kernel(int Bl, int M, 
                                                         const float* __restrict__ alpha, const float* __restrict__ dcd,
                                                         const float* __restrict__ G1, const float* __restrict__ per,
                                                         const float* __restrict__ dwdb_rows, float* __restrict__ dE,
-                                                        float* __restrict__ loss, float* __restrict__ dwdb) {
+                                                        float* __restrict__ loss, float* __restrict__ dwdb,
+                                                        float* __restrict__ red_dchat, float* __restrict__ red_beta) {
   constexpr int NW = GF_COLW, U = GF_COLU;
   __shared__ __attribute__((aligned(16))) float part[NW][64];
   __shared__ float bpart[NW];
@@ -724,6 +733,21 @@ __global__ __launch_bounds__(64 * GF_COLW) void ge2e_cols_kernel(int Bl, int M, 
   }
   if (lane < 16) *reinterpret_cast<float4*>(&part[w][4 * t]) = acc;
   if (lane == 0) bpart[w] = bsum;
+  if constexpr (PARTIAL) {
+    __syncthreads();
+    if (tid < 64 && q * 64 + tid < D) {
+      float dch = 0.f;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) dch += part[i][tid];
+      red_dchat[(long)k * D + q * 64 + tid] = dch;
+    }
+    if (tid == 0 && q == 0) {
+      float beta = 0.f;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) beta += bpart[i];
+      red_beta[k] = beta;
+    }
+  } else {
   // this wave's dE row (speaker k's utterance w): operands loaded before the barrier, dU shared
   // through LDS so the sum over the speaker's M rows needs no second trip to memory
   const int d = q * 64 + lane;
@@ -764,6 +788,7 @@ __global__ __launch_bounds__(64 * GF_COLW) void ge2e_cols_kernel(int Bl, int M, 
     for (int i = 0; i < M; ++i) sumdU += dUs[i][lane];
     dE[rdx] = gE + dCs[lane] * invM + (sumdU - dU) * invm1;
   }
+  }  // !PARTIAL
   if (k == 0 && q == 0) {  // loss = sum per, dw, db: fixed-order block sums (block-uniform branch)
     float l = 0.f, a = 0.f, b = 0.f;
     for (int i = tid; i < Bl; i += 64 * NW) {
@@ -809,15 +834,73 @@ extern "C" int sv_ge2e_train(const float* E, int N, int M, int D, const float* w
   const Ge2eWs ws = carve(workspace, N, M, D, N);
   const int Bl = N * M, Np = (N + 3) & ~3;
   hipLaunchKernelGGL(ge2e_prep_kernel, dim3(N), dim3(256), 0, stream, E, M, D, ws.Chat, ws.Cn, ws.Ehat, ws.Uhat,
-                     ws.En, ws.Un, ws.rawd);
+                     ws.En, ws.Un, ws.rawd, nullptr);
   SV_LAUNCH_CHECK();
   const size_t lds = ((size_t)N * (D + 4) + GF_ROWW * (size_t)D + GF_ROWW * (size_t)N) * sizeof(float);
   hipLaunchKernelGGL(ge2e_rows_kernel, dim3((Bl + GF_ROWW - 1) / GF_ROWW), dim3(64 * GF_ROWW), lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N,
-                     D, Np, w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1);
+                     D, Np, 0, w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1);
   SV_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ge2e_cols_kernel, dim3(N, (D + 63) / 64), dim3(64 * GF_COLW), 0, stream, Bl, M, N, D, Np, ws.Chat, ws.Cn,
+  hipLaunchKernelGGL(ge2e_cols_kernel<false>, dim3(N, (D + 63) / 64), dim3(64 * GF_COLW), 0, stream, Bl, M, N, D, Np, ws.Chat, ws.Cn,
                      ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.G1, per,
-                     ws.dwdb_rows, dE, loss, dwdb);
+                     ws.dwdb_rows, dE, loss, dwdb, nullptr, nullptr);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+// ---- the fused kernels in the speaker-sharded form (data parallel, sharded_ge2e.py) ----
+// shard_prep: this shard's per-speaker sums (for the all-gather) and its rows' E^, U^, norms and
+// diagonal cosines.  shard_rows: every speaker's C^ from the gathered sums, this shard's rows of
+// the similarity matrix against all N (global speaker of local row r: spk_offset + r / M), the
+// softmax and row backward, then per speaker k the shard's dC^_k and beta_k into the reduce
+// buffer red [Np*D + N] (the caller SUM-all-reduces it) and the shard's loss / (dw, db)
+// partials.  shard_finalize: this shard's dE from the reduced buffer.  The workspace carries the
+// state between the three calls (sv_ge2e_workspace_size(N_local, M, D, N)).
+extern "C" int sv_ge2e_shard_prep(const float* E, int N_local, int M, int D, float* ssum_local, float* workspace,
+                                  hipStream_t stream) {
+  if (!E || !ssum_local || !workspace || N_local <= 0) return SV_EARG;
+  if (!sv_ge2e_train_ok(N_local, M, D)) return SV_ESHAPE;
+  if (((uintptr_t)E | (uintptr_t)workspace | (uintptr_t)ssum_local) & 15) return SV_EALIGN;
+  const Ge2eWs ws = carve(workspace, N_local, M, D, N_local);
+  hipLaunchKernelGGL(ge2e_prep_kernel, dim3(N_local), dim3(256), 0, stream, E, M, D, nullptr, nullptr, ws.Ehat, ws.Uhat,
+                     ws.En, ws.Un, ws.rawd, ssum_local);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_ge2e_shard_rows(int N_local, int M, int D, int spk_offset, int N, const float* ssum_all,
+                                  const float* w, const float* b, float* per, float* red, float* loss_local,
+                                  float* dwdb_local, float* workspace, hipStream_t stream) {
+  if (!ssum_all || !w || !b || !per || !red || !loss_local || !dwdb_local || !workspace) return SV_EARG;
+  if (!sv_ge2e_train_ok(N, M, D) || N_local <= 0 || spk_offset < 0 || spk_offset + N_local > N) return SV_ESHAPE;
+  const Ge2eWs ws = carve(workspace, N_local, M, D, N);
+  const int Bl = N_local * M, Np = (N + 3) & ~3;
+  hipLaunchKernelGGL(ge2e_centroid_kernel, dim3(Np), dim3(256), 0, stream, ssum_all, N, M, D, ws.Chat, ws.Cn);
+  SV_LAUNCH_CHECK();
+  const size_t lds = ((size_t)N * (D + 4) + GF_ROWW * (size_t)D + GF_ROWW * (size_t)N) * sizeof(float);
+  hipLaunchKernelGGL(ge2e_rows_kernel, dim3((Bl + GF_ROWW - 1) / GF_ROWW), dim3(64 * GF_ROWW), lds, stream, ws.Chat,
+                     ws.Ehat, ws.rawd, Bl, M, N, D, Np, spk_offset, w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd,
+                     ws.dwdb_rows, ws.G1);
+  SV_LAUNCH_CHECK();
+  // the padding rows of dC^ (speakers N .. Np-1) stay zero through the all-reduce
+  if (Np > N) {
+    hipError_t e = hipMemsetAsync(red + (size_t)N * D, 0, (size_t)(Np - N) * D * sizeof(float), stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(ge2e_cols_kernel<true>, dim3(N, (D + 63) / 64), dim3(64 * GF_COLW), 0, stream, Bl, M, N, D, Np,
+                     ws.Chat, ws.Cn, ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.G1,
+                     per, ws.dwdb_rows, nullptr, loss_local, dwdb_local, red, red + (size_t)Np * D);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_ge2e_shard_finalize(int N_local, int M, int D, int spk_offset, int N, const float* red, float* dE,
+                                      float* workspace, hipStream_t stream) {
+  if (!red || !dE || !workspace || N_local <= 0 || M < 2 || D <= 0) return SV_EARG;
+  const Ge2eWs ws = carve(workspace, N_local, M, D, N);
+  const int Np = (N + 3) & ~3;
+  hipLaunchKernelGGL(ge2e_finalize_kernel, dim3(N_local), dim3(256), 0, stream, M, D, spk_offset, red,
+                     red + (size_t)Np * D, ws.Chat, ws.Cn, ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, ws.dcd, ws.alpha,
+                     ws.G1, dE);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }

@@ -474,3 +474,209 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
   else
     g8_epilogue<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
 }
+
+// ---- persistent form of the 8-phase kernel (G8_STORE_BF16 / G8_STORE, no split-K) ----
+// The K1 shape (K = 768: 12 k-tiles per 256 x 256 tile, 4800 tiles) spent ~40 % of each tile in
+// its prologue (k-tile 0's fill latency) and its store tail.  Here a grid of one workgroup per CU
+// walks the tiles (virtual block v = blockIdx.x + i * gridDim.x, the same xcd_remap as the
+// one-shot kernel), and the next tile's k-tile 0 is filled while this tile's C is stored: its
+// fills go to the stage the last k-tile did not use, and the bf16 C tile goes through the other
+// stage in two 64-row halves (8 KB per wave), after which k-tile 1's first fills go there.  The
+// stage of k-tile kt is (kt + base) & 1, base advancing by nk per tile.  Same MFMA order per tile
+// as gemm_bf16_8q_kernel (bit-identical results).
+__device__ __forceinline__ void g8_epilogue_bf16_half(g8_f32x4 (&acc)[8][4], int hlf, bf16_t* C, long ldc, int tm,
+                                                      int tn, int wr, int wc, int lane, const float* bias0,
+                                                      const float* bias1, char* tile) {
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int col = tn * G256_BM + wc * 64 + 16 * nt + 4 * fq;
+    g8_f32x4 badd = {0.f, 0.f, 0.f, 0.f};
+    if (bias0) badd += *reinterpret_cast<const g8_f32x4*>(bias0 + col);
+    if (bias1) badd += *reinterpret_cast<const g8_f32x4*>(bias1 + col);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const g8_f32x4 v = acc[4 * hlf + m][nt] + badd;
+      const unsigned lo = (unsigned)to_bf(v[0]) | ((unsigned)to_bf(v[1]) << 16);
+      const unsigned hi = (unsigned)to_bf(v[2]) | ((unsigned)to_bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(tile + (16 * m + fr) * 128 + (16 * nt + 4 * fq) * 2) = uint2{lo, hi};
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = 8 * i + (lane >> 3), c = lane & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(tile + row * 128 + c * 16);
+    *reinterpret_cast<uint4*>(C + ((long)tm * G256_BM + wr * 128 + 64 * hlf + row) * ldc + tn * G256_BM + wc * 64 +
+                              8 * c) = v;
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_8qp_kernel(const bf16_t* __restrict__ A, long lda,
+                                                              const bf16_t* __restrict__ B, long ldb, void* __restrict__ C,
+                                                              long ldc, int M, int N, int K,
+                                                              const float* __restrict__ bias0,
+                                                              const float* __restrict__ bias1, float beta) {
+  static_assert(EPI == G8_STORE_BF16 || EPI == G8_STORE, "persistent form: plain stores");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int tiles_n = N / G256_BM;
+  const int nwg = tiles_n * (M / G256_BM);
+  const int nk = K / G256_BK;
+  const int wr = w >> 2, wc = w & 3;
+  constexpr int OPB = G256_BM * G256_BK * 2;
+  int v = blockIdx.x;
+  if (v >= nwg) return;
+  int base = 0;
+  auto tile_of = [&](int vv, int& tm_, int& tn_) {
+    const int id = xcd_remap(vv, nwg);
+    tn_ = id % tiles_n;
+    tm_ = id / tiles_n;
+  };
+  int tm, tn;
+  tile_of(v, tm, tn);
+  G256Stage sa, sb;
+  sa.init(A, lda, tm * G256_BM, 0, tid);
+  sb.init(B, ldb, tn * G256_BM, 0, tid);
+  auto stage = [&](int kt) { return smem + ((kt + base) & 1) * 2 * OPB; };
+  auto fill_a = [&](int kt, int i) {
+    __builtin_amdgcn_global_load_lds((glb_vptr_t)(sa.src[i] + kt * G256_BK), (lds_vptr_t)(stage(kt) + (w * 64 + 512 * i) * 16),
+                                     16, 0, 0);
+  };
+  auto fill_b = [&](int kt, int i) {
+    __builtin_amdgcn_global_load_lds((glb_vptr_t)(sb.src[i] + kt * G256_BK),
+                                     (lds_vptr_t)(stage(kt) + OPB + (w * 64 + 512 * i) * 16), 16, 0, 0);
+  };
+  auto read_a = [&](const char* As, int mt, int ks) -> bf16x8_t {
+    const int row = wr * 128 + 16 * mt + fr;
+    return *reinterpret_cast<const bf16x8_t*>(As + row * 128 + g256_phys_slot(row, 4 * ks + fq) * 16);
+  };
+  auto read_b = [&](const char* Bs, int nt, int ks) -> bf16x8_t {
+    const int row = wc * 64 + 16 * nt + fr;
+    return *reinterpret_cast<const bf16x8_t*>(Bs + row * 128 + g256_phys_slot(row, 4 * ks + fq) * 16);
+  };
+  // first tile: k-tile 0 whole (the later tiles get it during the previous tile's store tail)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) fill_b(0, i);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) fill_a(0, i);
+  g8_f32x4 acc[8][4];
+  bf16x8_t a[4][2], b0[2][2], b1[2][2];
+  auto mma = [&](int mh, int nh, const bf16x8_t (&bq)[2][2]) {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 * mh + i][2 * nh + j] = mfma16_bf16(bq[j][ks], a[i][ks], acc[4 * mh + i][2 * nh + j]);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  while (true) {
+    // prologue remainder: k-tile 1's fills that the steady state issues in the phases of k-tile -1
+    if (nk > 1) {
+      fill_a(1, 0);
+      fill_a(1, 2);
+      fill_b(1, 0);
+      fill_b(1, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (wr == 1) {
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = g8_f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* As = stage(kt);
+      const char* Bs = As + OPB;
+      const bool m1 = kt + 1 < nk, m2 = kt + 2 < nk;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) b0[j][ks] = read_b(Bs, j, ks);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) a[i][ks] = read_a(As, i, ks);
+      if (m1) {
+        fill_b(kt + 1, 2);
+        fill_b(kt + 1, 3);
+      }
+      mma(0, 0, b0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) b1[j][ks] = read_b(Bs, 2 + j, ks);
+      if (m1)
+        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (m1) fill_a(kt + 1, 1);
+      if (m2) fill_a(kt + 2, 0);
+      mma(0, 1, b1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) a[i][ks] = read_a(As, 4 + i, ks);
+      if (m1) fill_a(kt + 1, 3);
+      if (m2) fill_a(kt + 2, 2);
+      mma(1, 1, b1);
+      if (m2)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (m1)
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (m2) {
+        fill_b(kt + 2, 0);
+        fill_b(kt + 2, 1);
+      }
+      mma(1, 0, b0);
+    }
+    if (wr == 0) {
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // every wave is past its last read of both stages.  The next tile's k-tile 0 goes to the
+    // stage k-tile nk - 1 did not use, behind this tile's stores
+    const int tm0 = tm, tn0 = tn;
+    char* tail = stage(nk - 1);  // the C staging area (bf16 output)
+    const int vn = v + gridDim.x;
+    const bool more = vn < nwg;
+    if (more) {
+      tile_of(vn, tm, tn);
+      sa.init(A, lda, tm * G256_BM, 0, tid);
+      sb.init(B, ldb, tn * G256_BM, 0, tid);
+      base = (base + nk) & 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fill_b(0, i);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fill_a(0, i);
+    }
+    if constexpr (EPI == G8_STORE_BF16) {
+      char* wt = tail + w * 8192;  // [64 rows][128 B] per wave
+      g8_epilogue_bf16_half(acc, 0, reinterpret_cast<bf16_t*>(C), ldc, tm0, tn0, wr, wc, lane, bias0, bias1, wt);
+      g8_epilogue_bf16_half(acc, 1, reinterpret_cast<bf16_t*>(C), ldc, tm0, tn0, wr, wc, lane, bias0, bias1, wt);
+      __syncthreads();  // every wave's reads of the C staging area done before k-tile 1 refills it
+    } else {
+      g8_epilogue<EPI>(acc, C, ldc, 0L, tm0, tn0, wr, wc, lane, bias0, bias1, beta);
+    }
+    if (!more) break;
+    v = vn;
+  }
+}

@@ -11,7 +11,10 @@ leave-one-out centroids stay local.  Per step:
 
 With world size 1 this is exactly the single-GPU GE2ELoss.  The per-shard arithmetic is
 a pluggable ``kernels`` object: the HIP kernels (``HipShardKernels``) in production; the
-CPU tests plug in a numpy restatement so the exchange protocol runs under gloo.
+CPU tests plug in a numpy restatement so the exchange protocol runs under gloo.  For the
+training step (``train``) with global N <= 128 the HIP kernels run in their fused sharded form
+(``HipFusedShard``: prep, rows, finalize around the same two exchanges); larger N (c5's 256)
+take the split kernels.
 """
 from __future__ import annotations
 
@@ -58,6 +61,41 @@ class HipShardKernels:
         dE = torch.empty((Nl, M, D), dtype=torch.float32, device=red.device)
         call("sv_ge2e_bwd_finalize", Nl, M, D, st["s0"], N, ptr(red), ptr(red[Np * D:]), ptr(dE), ptr(st["ws"]),
              stream_of(red))
+        return dE
+
+
+class HipFusedShard:
+    """The fused GE2E kernels in the speaker-sharded form (sv_ge2e_shard_prep / _rows /
+    _finalize): 3 launches + the centroid pass around the two exchanges, for global N <= 128
+    (sv_ge2e_train_ok); the split kernels above for the rest."""
+
+    @staticmethod
+    def ok(N, M, D):
+        return bool(lib().sv_ge2e_train_ok(N, M, D))
+
+    def prep(self, E, N):
+        Nl, M, D = E.shape
+        ws = torch.empty(lib().sv_ge2e_workspace_size(Nl, M, D, N) // 4 + 64, dtype=torch.float32, device=E.device)
+        ssum = torch.empty((Nl, D), dtype=torch.float32, device=E.device)
+        call("sv_ge2e_shard_prep", ptr(E), Nl, M, D, ptr(ssum), ptr(ws), stream_of(E))
+        return ssum, ws
+
+    def rows(self, E, s0, N, ssum_all, w, b, ws):
+        Nl, M, D = E.shape
+        Np = (N + 3) // 4 * 4
+        dev = E.device
+        per = torch.empty((Nl, M), dtype=torch.float32, device=dev)
+        red = torch.empty(Np * D + N, dtype=torch.float32, device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        dwdb = torch.empty(2, dtype=torch.float32, device=dev)
+        call("sv_ge2e_shard_rows", Nl, M, D, s0, N, ptr(ssum_all), ptr(w), ptr(b), ptr(per), ptr(red), ptr(loss),
+             ptr(dwdb), ptr(ws), stream_of(E))
+        return loss, per, red, dwdb
+
+    def finalize(self, E, s0, N, red, ws):
+        Nl, M, D = E.shape
+        dE = torch.empty((Nl, M, D), dtype=torch.float32, device=E.device)
+        call("sv_ge2e_shard_finalize", Nl, M, D, s0, N, ptr(red), ptr(dE), ptr(ws), stream_of(E))
         return dE
 
 
@@ -111,6 +149,22 @@ class ShardedGE2E:
         if self.world == 1 and isinstance(self.k, HipShardKernels):
             from .ops import ge2e_train
             loss, _, dE, dwdb = ge2e_train(E_local, w, b)
+            return loss, dE, dwdb
+        Nl, M, D = E_local.shape
+        N = Nl * self.world
+        if isinstance(self.k, HipShardKernels) and D % 4 == 0 and HipFusedShard.ok(N, M, D):
+            # fused sharded form: prep -> all-gather sums -> rows -> all-reduce(dC^, beta) -> dE
+            f = HipFusedShard()
+            E = E_local.contiguous()
+            s0 = Nl * self.rank
+            ssum_local, ws = f.prep(E, N)
+            ssum_all = all_gather_rows(ssum_local, self.rank, self.world, self.group)
+            loss, _, red, dwdb = f.rows(E, s0, N, ssum_all, w.contiguous(), b.contiguous(), ws)
+            dist.all_reduce(red, group=self.group)
+            dE = f.finalize(E, s0, N, red, ws)
+            if reduce_loss:
+                loss = loss.clone()
+                dist.all_reduce(loss, group=self.group)
             return loss, dE, dwdb
         loss, _, st = self.forward(E_local, w, b, reduce_loss=reduce_loss)
         dE, dwdb = self.backward(st, w, b)
