@@ -31,7 +31,18 @@ $(LIB): $(OBJ)
 $(FAULT_LIB): $(FAULT_OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(FAULT_OBJ)
 
+# A/B build (not loaded by tests or the bench): the 256-tile fp32 GEMM on v_mfma_f32_16x16x4_f32
+M16_OBJ := $(patsubst build/sv_lstm.o,build/m16/sv_lstm.o,$(OBJ))
+M16_LIB := scripts/ab/libsv_ge2e_m16.so
+build/m16/sv_lstm.o: $(PKG)/csrc/sv_lstm.hip $(wildcard $(PKG)/csrc/*.h) include/sv_ge2e.h
+	@mkdir -p build/m16
+	$(HIPCC) $(CXXFLAGS) -DSV_F32_MF=16 -c $< -o $@
+$(M16_LIB): $(M16_OBJ)
+	@mkdir -p scripts/ab
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(M16_OBJ)
+ab: $(M16_LIB)
+
 clean:
 	rm -rf build $(LIB) $(FAULT_LIB)
 
-.PHONY: all clean
+.PHONY: all clean ab

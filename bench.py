@@ -216,7 +216,8 @@ def time_step_kernel(B, H, dev, reps=64):
 
 
 def time_gemm_kernel(M, N, K, dev, reps=5):
-    """gemm_km_kernel<128,128> at the K1 shape of layers 1-2 in isolation, HIP events on its stream."""
+    """The fp32 NT GEMM (sv_gemm_f32: gemm_f32_256_kernel, the 256 x 256 LDS-DMA tile, at this shape)
+    at the K1 shape of layers 1-2 in isolation, HIP events on its stream."""
     from pytorch_speaker_verification_amd._lib import call, ptr, stream_of
     g = torch.Generator(device="cpu").manual_seed(8)
     A = torch.randn(M, K, generator=g).to(dev)
@@ -665,8 +666,9 @@ def main():
     if rank == 0:
         ms_g, fl_g, by_g = time_gemm_kernel(160 * 640, 4 * H, H, dev)
         out["roofline_gemm"] = dict(roofline_entry(
-            f"gemm_km_kernel<128,128> (K1/dW/dx NT GEMM, fp32 MFMA 32x32x2), K1 shape M={160 * 640} N={4 * H} K={H}",
-            fl_g, ms_g, MI355X_FP32_MFMA_TFLOPS, pmc_traffic("gemm_km_kernel<128,128>"), 5,
+            f"gemm_f32_256_kernel<256,32,0> (K1/dW/dx NT GEMM, 256x256 LDS-DMA tile, fp32 MFMA 32x32x2), K1 shape "
+            f"M={160 * 640} N={4 * H} K={H}",
+            fl_g, ms_g, MI355X_FP32_MFMA_TFLOPS, pmc_traffic("gemm_f32_256_kernel<256,32,0>"), 5,
             "isolated launches, HIP events on its stream"), algorithmic_bytes=by_g)
         ms_k, fl_k = time_step_kernel(640, H, dev)
         out["roofline_step_kernel"] = roofline_entry(

@@ -236,7 +236,9 @@ int sv_transpose_cast_bf16(const float* src, long ld_src, int R, int C, sv_bf16*
 int sv_lstm_layer_fwd_bf16(const sv_bf16* x_bf, int T, int B, int F, int H, const sv_bf16* w_ih_bf,
                            const sv_bf16* w_hh_bf, const float* b_ih, const float* b_hh, sv_bf16* gates, float* c_tm,
                            float* h_tm, sv_bf16* h_bf, sv_bf16* hT, hipStream_t stream);
-/* stack forward in bf16 (as sv_lstm_stack_fwd; h_bf per layer [T+1,B,H]) under `schedule`
+/* stack forward in bf16 (as sv_lstm_stack_fwd; h_bf per layer [T+1,B,H]; of the fp32 h_tm only
+ * slot T = h_{T-1}, the projection's input, is guaranteed -- the persistent schedules write no
+ * other slot, the next layer and the backward read the bf16 copies) under `schedule`
  * (SV_SCHED_*).  sync: the caller's sync block (below; required when the persistent recurrences run).
  * probe (may be NULL): 2*L caller events recorded around each layer's persistent recurrence
  * launch (before / after; only when the persistent schedule runs) -- in-step kernel timing. */

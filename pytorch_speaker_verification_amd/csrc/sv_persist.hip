@@ -468,7 +468,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
 #pragma unroll
         for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(gp + q * H) = act[k][q];
         *reinterpret_cast<float4*>(c_tm + (long)t * BH + gb * H + j0 + u4) = cv[k];
-        *reinterpret_cast<float4*>(h_tm + (long)(t + 1) * BH + gb * H + j0 + u4) = hv[k];
+        // fp32 h: only h_{T-1} is read (the projection); the next layer and the backward take
+        // the bf16 copies
+        if (t == T - 1) *reinterpret_cast<float4*>(h_tm + (long)(t + 1) * BH + gb * H + j0 + u4) = hv[k];
       }
     }
     if (hT) {  // 32 unit rows x BM/8 chunks of 8 batch columns (padding columns get zeros)

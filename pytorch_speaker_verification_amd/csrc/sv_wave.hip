@@ -247,7 +247,7 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
 #pragma unroll
       for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(gp + q * H) = act[q];
       *reinterpret_cast<float4*>(a.c[l] + (long)t * BH + gb * H + j0 + u4) = cv;
-      *reinterpret_cast<float4*>(a.h[l] + (long)(t + 1) * BH + gb * H + j0 + u4) = hv;
+      if (t == T - 1) *reinterpret_cast<float4*>(a.h[l] + (long)(t + 1) * BH + gb * H + j0 + u4) = hv;  // h_{T-1} only
     }
     if (a.hT[l] && tid < BF_U * (WV_BM / 8)) {
       const int u = tid >> 2, c = tid & 3, gc = b0 + 8 * c;

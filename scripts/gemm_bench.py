@@ -18,7 +18,11 @@ ap.add_argument("--reps", type=int, default=8)
 ap.add_argument("--check", action="store_true", help="bf16: error vs fp32 torch on the same bf16 inputs, "
                 "and bitwise repeatability over --reps runs (a race screen)")
 ap.add_argument("--shapes", default="Gx,dW,dx")
+ap.add_argument("--lib", default=None, help="load this build of the library instead (A/B builds)")
 args = ap.parse_args()
+if args.lib:
+    from pytorch_speaker_verification_amd import _lib
+    _lib.use_library(args.lib)
 dev = torch.device("cuda", 0)
 s = torch.cuda.current_stream(dev).cuda_stream
 B, T, H = 640, 160, 768
@@ -38,7 +42,7 @@ def timeit(fn, reps, warm=2):
     return e0.elapsed_time(e1) / reps * 1e3
 
 
-res = {"env": {k: v for k, v in os.environ.items() if k.startswith("SV_")}}
+res = {"lib": args.lib or "libsv_ge2e.so"}
 for name, (M, N, K) in SHAPES.items():
     if name not in args.shapes.split(","):
         continue
