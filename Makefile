@@ -31,16 +31,21 @@ $(LIB): $(OBJ)
 $(FAULT_LIB): $(FAULT_OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(FAULT_OBJ)
 
-# A/B build (not loaded by tests or the bench): the 256-tile fp32 GEMM on v_mfma_f32_16x16x4_f32
-M16_OBJ := $(patsubst build/sv_lstm.o,build/m16/sv_lstm.o,$(OBJ))
-M16_LIB := scripts/ab/libsv_ge2e_m16.so
-build/m16/sv_lstm.o: $(PKG)/csrc/sv_lstm.hip $(wildcard $(PKG)/csrc/*.h) include/sv_ge2e.h
-	@mkdir -p build/m16
-	$(HIPCC) $(CXXFLAGS) -DSV_F32_MF=16 -c $< -o $@
-$(M16_LIB): $(M16_OBJ)
+# A/B builds (never loaded by tests or the bench): `make ab NAME=x FLAGS="-DSV_..."` compiles every
+# source with FLAGS into scripts/ab/libsv_ge2e_x.so (e.g. -DSV_F32_MF=16: the 256-tile fp32 GEMM on
+# v_mfma_f32_16x16x4_f32; -DSV_PBWD_DEBUG=32: phase stamps of the persistent backward)
+NAME ?= m16
+FLAGS ?= -DSV_F32_MF=16
+AB_OBJ := $(patsubst build/%.o,build/ab_$(NAME)/%.o,$(OBJ))
+AB_LIB := scripts/ab/libsv_ge2e_$(NAME).so
+build/ab_$(NAME)/sv_persist3.o: EXTRA := -mllvm -amdgpu-mfma-vgpr-form=1
+build/ab_$(NAME)/%.o: $(PKG)/csrc/%.hip $(wildcard $(PKG)/csrc/*.h) include/sv_ge2e.h
+	@mkdir -p build/ab_$(NAME)
+	$(HIPCC) $(CXXFLAGS) $(EXTRA) $(FLAGS) -c $< -o $@
+$(AB_LIB): $(AB_OBJ)
 	@mkdir -p scripts/ab
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(M16_OBJ)
-ab: $(M16_LIB)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(AB_OBJ)
+ab: $(AB_LIB)
 
 clean:
 	rm -rf build $(LIB) $(FAULT_LIB)

@@ -512,6 +512,8 @@ def main():
     ap.add_argument("--no-bf16", action="store_true", help="skip the bf16 side measurements (c3/c4/c5)")
     ap.add_argument("--no-f32x", action="store_true", help="skip the fp32-via-bf16x6 side measurement")
     ap.add_argument("--no-vendor", action="store_true", help="skip the nn.LSTM/MIOpen same-GPU baseline")
+    ap.add_argument("--no-extras", action="store_true", help="skip the isolated-kernel, HBM-kernel and d-vector "
+                    "lines (profiling runs that want only the training steps)")
     ap.add_argument("--preset", choices=["c2", "c3", "c4", "c5"], default=None,
                     help="headline config: c2 = N64 M10 T160 f32 per GPU (default), c3 = the same in bf16, "
                          "c4 = N64 M10 T160 bf16 split over the GPUs (strong scaling), c5 = N256 M10 T180 bf16 "
@@ -663,7 +665,7 @@ def main():
                     "same workload, fp32 products formed as six bf16 MFMA products of a three-way bf16 split (fp32 "
                     "accumulation); opt-in per module: net.f32_products = 'bf16x6'", products="bf16x6")
         o["gemm_error_vs_fp64"] = f32_product_accuracy(dev)
-    if rank == 0:
+    if rank == 0 and not args.no_extras:
         ms_g, fl_g, by_g = time_gemm_kernel(160 * 640, 4 * H, H, dev)
         out["roofline_gemm"] = dict(roofline_entry(
             f"gemm_f32_256_kernel<256,32,0> (K1/dW/dx NT GEMM, 256x256 LDS-DMA tile, fp32 MFMA 32x32x2), K1 shape "
@@ -683,8 +685,9 @@ def main():
                 out["vendor_baseline"] = vendor_baseline(N, M, T, dev, dtype=dtype)
                 if "bf16" in out:
                     out["bf16"]["vendor_baseline"] = vendor_baseline(N, M, T, dev, dtype="bf16")
-            if not args.no_cpu_baseline:
-                out["cpu_baseline"] = cpu_baseline(N, M, T)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(N, M, T)
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -980,7 +980,12 @@ constexpr size_t pbwd_lds(int bm) {
   return (size_t)4 * bm * (BF_U + 4) * 4 + (size_t)bm * (4 * BF_U + 8) * 2 + (size_t)4 * BF_U * (bm + 8) * 2 +
          (size_t)bm * 512;  // + the LDS-DMA operand image (EWD)
 }
-constexpr int kPbwdDebug = 0;  // the kernels' diagnostic skips, all off in the product library
+#ifndef SV_PBWD_DEBUG
+#define SV_PBWD_DEBUG 0
+#endif
+// the backward kernels' diagnostic bits: 0 in the product library; A/B builds only (Makefile `ab`:
+// 32 = per-phase cycle stamps into the caller's sync block, read by scripts/persist_ab.py)
+constexpr int kPbwdDebug = SV_PBWD_DEBUG;
 template <int NS, int P>
 void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
                  const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B,

@@ -77,8 +77,10 @@ for name, (M, N, K) in SHAPES.items():
             res["sv_bf16_bfout_Gx"] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
             if args.check:
                 ref = torch.matmul(Ab.float(), Bb.float().t())
-                res["sv_bf16_bfout_err_Gx"] = float(((Cb.float() - ref).abs() / (ref.abs() + 1e-3)).max())
-                del ref
+                sc = torch.matmul(Ab.float().abs(), Bb.float().abs().t())
+                res["sv_bf16_bfout_err_Gx"] = float(((Cb.float() - ref).abs() / sc).max())
+                del ref, sc
+                Cbf = Cb
             del Cb
         if args.check:
             call("sv_gemm_bf16", M, N, K, ptr(Ab), K, ptr(Bb), K, ptr(C), N, None, None, 0.0, ptr(wb), s)
@@ -94,6 +96,9 @@ for name, (M, N, K) in SHAPES.items():
             sc = torch.matmul(Ab.float().abs(), Bb.float().abs().t())
             res["sv_bf16_err_" + name] = float(((first - ref).abs() / sc).max())
             res["sv_bf16_repeat_" + name] = same
+            if name == "Gx":  # the bf16-output kernel rounds the same fp32 sums once (RNE)
+                res["sv_bf16_bfout_is_rne_of_f32out"] = bool(torch.equal(Cbf, first.bfloat16()))
+                del Cbf
             del ref, sc, first
         if args.torch:
             us = timeit(lambda: torch.matmul(Ab, Bb.t()), args.reps)

@@ -5,8 +5,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 D=gpurun_out/pmc_traffic
 mkdir -p $D
 export TMPDIR=/tmp
-ARGS_F32="--steps 2 --warmup 1 --no-cpu-baseline --no-vendor --no-bf16 --no-f32x --fwd-steps 1"
-ARGS_BF16="--steps 2 --warmup 1 --no-cpu-baseline --no-vendor --preset c3 --fwd-steps 1"
+ARGS_F32="--steps 2 --warmup 1 --no-cpu-baseline --no-vendor --no-bf16 --no-f32x --no-extras --fwd-steps 1"
+ARGS_BF16="--steps 2 --warmup 1 --no-cpu-baseline --no-vendor --no-extras --preset c3 --fwd-steps 1"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/f32_fetch -o p -- python3 bench.py $ARGS_F32 > $D/f32_fetch.log 2>&1 || { echo "f32 fetch rc=$?"; tail -5 $D/f32_fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/f32_write -o p -- python3 bench.py $ARGS_F32 > $D/f32_write.log 2>&1 || { echo "f32 write rc=$?"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/bf16_fetch -o p -- python3 bench.py $ARGS_BF16 > $D/bf16_fetch.log 2>&1 || { echo "bf16 fetch rc=$?"; exit 1; }

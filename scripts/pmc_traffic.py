@@ -1,7 +1,8 @@
 """Fold rocprofv3 FETCH_SIZE / WRITE_SIZE passes (separate runs, gpurun_out/pmc_traffic/*) into
 bench_pmc_traffic.json: per kernel family, the average HBM bytes per launch corrected as
 MI355X_MICROARCH.md prescribes (2 x FETCH_SIZE + WRITE_SIZE, counters in KiB).
-Usage: python scripts/pmc_traffic.py <dir with f32_fetch/f32_write/bf16_fetch/bf16_write csvs>"""
+Usage: python scripts/pmc_traffic.py <dir with f32_fetch/f32_write/bf16_fetch/bf16_write csvs>
+       python scripts/pmc_traffic.py --gemm <dir with fetch/write csvs of scripts/gemm_traffic.py>"""
 import csv
 import glob
 import json
@@ -16,31 +17,75 @@ FAMILIES = {  # json key -> kernel-name prefix
     "lstm_persist2_fwd_bf16_kernel": "void lstm_persist2_fwd_bf16_kernel<48, 64, 0>",
     "lstm_persist3_bwd_bf16_kernel": "void lstm_persist3_bwd_bf16_kernel<",
     "lstm_persist3_fwd_bf16_kernel": "void lstm_persist3_fwd_bf16_kernel<",
-    "gemm_bf16_8q_kernel": "void gemm_bf16_8q_kernel<",
+    # in-step GEMMs, per shape (c2 fp32 / c3 bf16, B = 640, T = 160, H = 768): (prefix, grid threads)
+    "gemm_f32_256_kernel<256,32,0>@K1.in_step": ("void gemm_f32_256_kernel<256, 32, 0>", 400 * 12 * 512),
+    "gemm_f32_256_kernel<256,32,0>@dx.in_step": ("void gemm_f32_256_kernel<256, 32, 0>", 400 * 3 * 512),
+    "gemm_f32_256_kernel<256,32,1>@dW.in_step": ("void gemm_f32_256_kernel<256, 32, 1>", 36 * 7 * 512),
+    "gemm_bf16_8qp_kernel<2>@K1.in_step": "void gemm_bf16_8qp_kernel<2>",
+    "gemm_bf16_8q_kernel<0,1>@dx.in_step": "void gemm_bf16_8q_kernel<0, 1>",
+    "gemm_bf16_8q_kernel<1,0>@dW.in_step": "void gemm_bf16_8q_kernel<1, 0>",
+}
+B_, T_, H_ = 640, 160, 768
+# scripts/gemm_traffic.py's isolated launches: key -> (prefix, grid or None, algorithmic bytes)
+GEMM = {
+    "gemm_f32_256_kernel<256,32,0>": ("void gemm_f32_256_kernel<256, 32, 0>", 400 * 12 * 512,
+                                      4 * (T_ * B_ * H_ + 4 * H_ * H_ + T_ * B_ * 4 * H_)),
+    "gemm_f32_256_kernel<256,32,0>@dx": ("void gemm_f32_256_kernel<256, 32, 0>", 400 * 3 * 512,
+                                         4 * (T_ * B_ * 4 * H_ + 4 * H_ * H_ + T_ * B_ * H_)),
+    "gemm_f32_256_kernel<256,32,1>@dW": ("void gemm_f32_256_kernel<256, 32, 1>", None,
+                                         4 * (T_ * B_ * 4 * H_ + T_ * B_ * H_ + 4 * H_ * H_)),
+    "gemm_bf16_8qp_kernel<2>@K1": ("void gemm_bf16_8qp_kernel<2>", None,
+                                   2 * (T_ * B_ * H_ + 4 * H_ * H_ + T_ * B_ * 4 * H_)),
+    "gemm_bf16_8q_kernel<0,0>@dx": ("void gemm_bf16_8q_kernel<0, 0>", None,
+                                    2 * (T_ * B_ * 4 * H_ + 4 * H_ * H_) + 4 * T_ * B_ * H_),
+    "gemm_bf16_8q_kernel<1,0>@dW": ("void gemm_bf16_8q_kernel<1, 0>", None,
+                                    2 * (T_ * B_ * 4 * H_ + T_ * B_ * H_) + 4 * 4 * H_ * H_),
 }
 
 
-def per_launch(path, counter):
+def _grid(r):
+    for c in ("Grid_Size", "Grid_Size_X"):
+        if r.get(c):
+            return int(r[c])
+    return None
+
+
+def per_launch(path, counter, families):
     acc = {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        for key, pre in FAMILIES.items():
-            if r["Kernel_Name"].startswith(pre):
+        for key, spec in families.items():
+            pre, grid = (spec, None) if isinstance(spec, str) else spec[:2]
+            if r["Kernel_Name"].startswith(pre) and (grid is None or _grid(r) == grid):
                 s, n = acc.get(key, (0.0, 0))
                 acc[key] = (s + float(r["Counter_Value"]), n + 1)
     return {k: s / n for k, (s, n) in acc.items()}
 
 
-def main(d):
+def gemm_main(d, data):
+    fs = glob.glob(os.path.join(d, "fetch*", "**", "*counter_collection.csv"), recursive=True)
+    ws = glob.glob(os.path.join(d, "write*", "**", "*counter_collection.csv"), recursive=True)
+    fetch, write = per_launch(fs[0], "FETCH_SIZE", GEMM), per_launch(ws[0], "WRITE_SIZE", GEMM)
+    for k, (_, _, alg) in GEMM.items():
+        if k in fetch and k in write:
+            hbm = int(1024 * (2 * fetch[k] + write[k]))
+            data[k] = {"FETCH_SIZE_KiB": round(fetch[k], 1), "WRITE_SIZE_KiB": round(write[k], 1),
+                       "hbm_bytes_per_launch": hbm, "algorithmic_bytes": alg, "ratio": round(hbm / alg, 3),
+                       "source": "rocprofv3 --pmc over scripts/gemm_traffic.py (isolated launches, c2/c3 shapes)"}
+
+
+def main(d, gemm=False):
     out_path = os.path.join(ROOT, "bench_pmc_traffic.json")  # read by bench.py (profiles/ stays here)
     data = json.load(open(out_path)) if os.path.exists(out_path) else {}
-    for tag in ("f32", "bf16"):
+    if gemm:
+        gemm_main(d, data)
+    for tag in () if gemm else ("f32", "bf16"):
         fs = glob.glob(os.path.join(d, f"{tag}_fetch*", "**", "*counter_collection.csv"), recursive=True)
         ws = glob.glob(os.path.join(d, f"{tag}_write*", "**", "*counter_collection.csv"), recursive=True)
         if not fs or not ws:
             continue
-        fetch, write = per_launch(fs[0], "FETCH_SIZE"), per_launch(ws[0], "WRITE_SIZE")
+        fetch, write = per_launch(fs[0], "FETCH_SIZE", FAMILIES), per_launch(ws[0], "WRITE_SIZE", FAMILIES)
         for k in fetch:
             if k in write:
                 data[k] = {"FETCH_SIZE_KiB": round(fetch[k], 1), "WRITE_SIZE_KiB": round(write[k], 1),
@@ -54,4 +99,7 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    if sys.argv[1] == "--gemm":
+        main(sys.argv[2], gemm=True)
+    else:
+        main(sys.argv[1])
