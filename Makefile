@@ -16,6 +16,7 @@ all: $(LIB) $(FAULT_LIB)
 
 # the wide-tile persistent backward keeps its MFMA accumulators in VGPRs (all AGPRs hold weights)
 build/sv_persist3.o: EXTRA := -mllvm -amdgpu-mfma-vgpr-form=1
+build/sv_persist_f32.o: EXTRA := -mllvm -amdgpu-mfma-vgpr-form=1
 
 build/%.o: $(PKG)/csrc/%.hip $(wildcard $(PKG)/csrc/*.h) include/sv_ge2e.h
 	@mkdir -p build
@@ -39,6 +40,7 @@ FLAGS ?= -DSV_F32_MF=16
 AB_OBJ := $(patsubst build/%.o,build/ab_$(NAME)/%.o,$(OBJ))
 AB_LIB := scripts/ab/libsv_ge2e_$(NAME).so
 build/ab_$(NAME)/sv_persist3.o: EXTRA := -mllvm -amdgpu-mfma-vgpr-form=1
+build/ab_$(NAME)/sv_persist_f32.o: EXTRA := -mllvm -amdgpu-mfma-vgpr-form=1
 build/ab_$(NAME)/%.o: $(PKG)/csrc/%.hip $(wildcard $(PKG)/csrc/*.h) include/sv_ge2e.h
 	@mkdir -p build/ab_$(NAME)
 	$(HIPCC) $(CXXFLAGS) $(EXTRA) $(FLAGS) -c $< -o $@

@@ -544,8 +544,12 @@ def main():
         Ng, M, T = args.N, args.M, args.T
     N = max(1, Ng // world) if strong else Ng
     B = N * M
+    from pytorch_speaker_verification_amd._lib import lib as _svlib
+    # fp32: the persistent recurrences where the library picks them (c2: 240 of 256 CUs), else
+    # the per-step kernels with their in-kernel stamps
+    f32_persist = dtype == "f32" and bool(_svlib().sv_lstm_f32_persist_ok(B, H, 0))
     dt, loss, host, probes, tr = run_steps(ctx, N, M, T, dtype, args.steps, args.warmup, 1235,
-                                           probe="bwd_chunks" if dtype == "f32" else "fwd_bwd")
+                                           probe="bwd_chunks" if dtype == "f32" and not f32_persist else "fwd_bwd")
     ms_step = dt / args.steps * 1e3
     fwd_fl, st_fl = step_flops(B, T, F, H, P, L)
     peak = MI355X_FP32_MFMA_TFLOPS if dtype == "f32" else MI355X_BF16_MFMA_TFLOPS
@@ -574,7 +578,18 @@ def main():
         "step_tflops_per_gpu": round(st_fl / (ms_step * 1e-3) / 1e12, 2),
         "step_mfma_frac": round(st_fl / (ms_step * 1e-3) / 1e12 / peak, 4),
     }
-    if dtype == "f32":
+    if f32_persist:
+        fl = 2.0 * B * T * H * 4 * H
+        out["roofline"] = roofline_entry(
+            "lstm_persist_bwd_f32_kernel (persistent fp32 backward recurrence, one launch per layer, W_hh in "
+            "registers, fp32 MFMA 32x32x2)", fl, probe_ms(probes, "bwd") / L, MI355X_FP32_MFMA_TFLOPS,
+            pmc_traffic("lstm_persist_bwd_f32_kernel"), L * args.steps,
+            "in-step: HIP events around each layer's launch inside the timed steps (on its stream, main)")
+        out["roofline_fwd"] = roofline_entry(
+            "lstm_persist_fwd_f32_kernel (persistent fp32 forward recurrence)", fl, probe_ms(probes, "fwd") / L,
+            MI355X_FP32_MFMA_TFLOPS, pmc_traffic("lstm_persist_fwd_f32_kernel"), L * args.steps,
+            "in-step, as roofline (average over the L layers' launches)")
+    elif dtype == "f32":
         # K3, the headline step's dominant kernel: per-chunk HIP-event spans on its own stream over
         # the timed steps / its L*T launches per step
         from pytorch_speaker_verification_amd.ops import PIPELINE_CHUNK

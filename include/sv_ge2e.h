@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SV_ABI_VERSION 4
+#define SV_ABI_VERSION 5
 int sv_abi_version(void);
 
 /* ---- fp32 product modes (`products` argument of sv_gemm_f32 / sv_lstm_stack_fwd / _bwd; every
@@ -40,8 +40,12 @@ int sv_abi_version(void);
 #define SV_F32_EXACT 0
 #define SV_F32_BF16X6 1
 
-/* ---- schedule flags of the bf16 stack entry points (`schedule` argument of
- * sv_lstm_stack_fwd_bf16 / sv_lstm_stack_bwd_bf16; 0 = the measured default):
+/* ---- schedule flags (`schedule` argument of the stack entry points; 0 = the measured default).
+ * fp32 (sv_lstm_stack_fwd / _bwd): the W-stationary persistent recurrences (one launch per layer,
+ * W_hh in registers, H = 768) under SV_SCHED_AUTO where their grid fills >= 3/4 of the device and
+ * under SV_SCHED_PERSIST wherever it fits; SV_SCHED_PER_STEP keeps the layer-pipelined per-step
+ * kernels (K2 / K3).  The two agree to fp32 rounding (different summation order).
+ * bf16 (sv_lstm_stack_fwd_bf16 / _bwd_bf16):
  *   SV_SCHED_AUTO       the layer wavefront (all layers in one launch) where every layer's grid
  *                       fits co-resident, else one persistent recurrence launch per layer at
  *                       H = 768, else per-step launches;
@@ -92,19 +96,29 @@ int sv_lstm_step_fwd(const float* h_prev, const float* w_hh, float* gates_t, con
 int sv_lstm_step_bwd(const float* dg_next, const float* w_hhT, const float* dh_up, const float* dcf_next,
                      const float* acts_t, const float* c_t, const float* c_prev, float* dg_t, float* dcf_t, int B,
                      int H, hipStream_t stream);
-/* Whole stack, layer-pipelined over streams: layer l runs on side[l] in chunks of `chunk`
- * timesteps (chunk input-projection GEMM, then its steps) and waits only for layer l-1's same
- * chunk, so the layers' kernels overlap.  Per-layer pointers come in host arrays of length L
+/* Whole stack.  Per-step schedule: layer-pipelined over streams, layer l on side[l] in chunks of
+ * `chunk` timesteps (chunk input-projection GEMM, then its steps), waiting only for layer l-1's
+ * same chunk, so the layers' kernels overlap.  Persistent schedule (`schedule`, above): per layer on
+ * `main`, the whole-T input projection, then one persistent recurrence launch (needs `sync`, the
+ * caller's sync block below; probe (may be NULL): 2*L caller events recorded around layer l's
+ * launch, probe[2l] before, [2l+1] after).  Per-layer pointers come in host arrays of length L
  * (layer 0 input width F, others H); ev = L*ceil(T/chunk)+1 caller-created events.  Starts after
  * and joins back into `main` (all work ordered before the next op on `main`). */
 int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float* x_tm, const float* const* w_ih,
                       const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                       float* const* gates, float* const* c_tm, float* const* h_tm, float* const* hT, int chunk,
-                      hipStream_t main, const hipStream_t* side, hipEvent_t* ev, int products);
+                      hipStream_t main, const hipStream_t* side, hipEvent_t* ev, int products, int schedule,
+                      unsigned* sync, hipEvent_t* probe);
+/* 1 if the fp32 stack functions take the persistent recurrences for this batch under `schedule`
+ * on the current device */
+int sv_lstm_f32_persist_ok(int B, int H, int schedule);
 size_t sv_lstm_layer_bwd_workspace(int T, int B, int F, int H);
-/* Whole-stack backward, layer-pipelined over streams (top layer first): each layer's reverse
- * chunks of steps on side[l], then (l > 0) the chunk's dx = dG W_ih GEMM that feeds layer l-1;
- * then the layer's whole-T dW_hh / dW_ih GEMMs and bias row sums on side[l].  side: L streams.
+/* Whole-stack backward (top layer first).  Per-step schedule, layer-pipelined over streams: each
+ * layer's reverse chunks of steps on side[l], then (l > 0) the chunk's dx = dG W_ih GEMM that feeds
+ * layer l-1; then the layer's whole-T dW_hh / dW_ih GEMMs and bias row sums on side[l].  side: L
+ * streams.  Persistent schedule (`schedule`, `sync` as sv_lstm_stack_fwd): per layer on `main`, one
+ * persistent recurrence launch (probe[2l] / [2l+1] around it; kstamp unused), then the whole-T dx,
+ * dW GEMMs and row sums; ev[L*nch + l] recorded after layer l's gradients.
  * xT/ld_xT: per-layer transposed inputs; dx[l] [T,B,H] for l > 0;
  * ev = L*ceil(T/chunk) + L + 1 caller events (ev[L*nch + l] = layer l's gradients done);
  * joins back into `main`.  probe (may be NULL): 2*L*ceil(T/chunk) caller events recorded on the
@@ -120,7 +134,7 @@ int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float* const* xT,
                       float* const* dgT, float* const* dx, float* const* dw_ih, float* const* dw_hh,
                       float* const* db_ih, float* const* db_hh, float* workspace, int chunk, hipStream_t main,
                       const hipStream_t* side, hipEvent_t* ev, int products, hipEvent_t* probe,
-                      unsigned long long* kstamp);
+                      unsigned long long* kstamp, int schedule, unsigned* sync);
 /* xT: the layer input transposed, [F, >= T*Bp] with row stride ld_xT (layer 0: the frames;
  * layer l > 0: hT of layer l-1 offset by Bp columns).  hT: this layer's [H, (T+1)Bp] from the fwd.
  * dh_up: gradient w.r.t. this layer's outputs; dh_up_full=1 -> [T,B,H], 0 -> [B,H] for t=T-1 only.

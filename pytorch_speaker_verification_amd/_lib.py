@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libsv_ge2e.so")
 # the fault-injection test build (Makefile `faultinj`): the same library plus sv_test_set_fault;
 # only tests load it, through use_library() before the first call
 FAULT_LIB_PATH = os.path.join(_HERE, "libsv_ge2e_faultinj.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # schedule flags of the bf16 stack (include/sv_ge2e.h SV_SCHED_*), by name
 SCHEDULES = {"auto": 0, "per_layer": 1, "per_step": 2, "persist": 5}  # persist: per-layer persistent, any H
@@ -56,10 +56,11 @@ SIGNATURES = {
     "sv_lstm_step_fwd": (_c_int, [_P, _P, _P, _P, _P, _P, _c_int, _c_int, _P]),
     "sv_lstm_step_bwd": (_c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _c_int, _c_int, _P]),
     "sv_lstm_stack_fwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                   _c_int, _P, _P, _P, _c_int]),
+                                   _c_int, _P, _P, _P, _c_int, _c_int, _P, _P]),
+    "sv_lstm_f32_persist_ok": (_c_int, [_c_int, _c_int, _c_int]),
     "sv_lstm_stack_bwd_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "sv_lstm_stack_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P, _c_int,
-                                                                                          _P, _P]),
+                                                                                          _P, _P, _c_int, _P]),
     "sv_lstm_layer_bwd_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int]),
     "sv_lstm_layer_bwd": (_c_int, [_c_int, _c_int, _c_int, _c_int, _P, _c_long, _P, _P, _P, _P, _P, _P, _c_int, _P,
                                    _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -848,9 +848,10 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       if ((rc = sv_gemm_bf16_dual(4 * H, H, Fl, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, xT[l], ld_xT[l], dw_ih[l],
                                   Fl, ws.gws, main)))
         return rc;
-    }
-    for (int l = 0; l < L; ++l)
+      // layer l's gradients are complete: its all-reduce bucket (grad_ready) overlaps the lower
+      // layers' weight-gradient GEMMs (the recurrences are all done)
       if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
+    }
     return SV_OK;
   }
   if (sched_persist(schedule, H) && sv_persist_bwd_fits(B, H, sv_stream_cus(main))) {
@@ -874,6 +875,12 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
                                     dgT[l], dgf, main, sync, db_ih[l], db_hh ? db_hh[l] : nullptr,
                                     probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr)))
         return rc;
+      // the completion events of layers >= 1 (grad_ready: a caller's bucketed all-reduce) fire once
+      // the last recurrence is done, so collectives never share the device with a persistent launch
+      // (whose grid must be co-resident; a concurrent RCCL kernel would hold CUs it waits for) but
+      // overlap layer 0's weight-gradient GEMMs
+      for (int k = 1; l == 0 && k < L; ++k)
+        if ((e = hipEventRecord(ev[L * nch + k], main)) != hipSuccess) return (int)e;
       if (afr) {
         if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H, sv_stream_cus(main)), ws.wihT, 4L * H, dx[l],
                                   Fl, ws.gws, main)))
@@ -887,11 +894,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
                              ws.gws, main);
       if (rc) return rc;
     }
-    // the per-layer completion events (grad_ready: a caller's bucketed all-reduce) all fire after
-    // the last recurrence, so collectives never share the device with a persistent launch (whose
-    // grid must be co-resident; a concurrent RCCL kernel would hold CUs it waits for)
-    for (int l = 0; l < L; ++l)
-      if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
+    if ((e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
     return SV_OK;
   }
   // per-step schedule, layer-pipelined (sv_lstm_stack_bwd, sv_lstm.hip): each layer on side[l]

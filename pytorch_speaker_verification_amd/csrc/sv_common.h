@@ -28,6 +28,16 @@ struct F32ProductScope {
   ~F32ProductScope();
 };
 
+// fp32 W-stationary persistent recurrences of one layer (sv_persist_f32.hip): H = 768, 64-row x
+// 32-unit tiles co-resident on `cus` CUs; dgf: sv_persist_f32_bwd_scratch bytes (16-B aligned)
+int sv_persist_f32_fits(int B, int H, int cus);
+int sv_stream_cus(hipStream_t stream);  // CUs of the stream's device (sv_persist.hip)
+size_t sv_persist_f32_bwd_scratch(int T, int B, int H);
+int sv_persist_fwd_f32(int T, int B, int H, const float* whh, float* gates, float* c_tm, float* h_tm, float* hT,
+                       hipStream_t stream, unsigned* sync, int chan, hipEvent_t pre, hipEvent_t post);
+int sv_persist_bwd_f32(int T, int B, int H, const float* whhT, const float* acts, const float* c_tm,
+                       const float* dhup, int up_full, float* dg, float* dgT, float* dgf, hipStream_t stream,
+                       unsigned* sync, hipEvent_t pre, hipEvent_t post);
 #define SV_LAUNCH_CHECK()                                  \
   do {                                                     \
     hipError_t e__ = hipGetLastError();                    \

@@ -887,21 +887,54 @@ extern "C" int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* xT, lo
 // Host arrays (length L) carry the per-layer device pointers; ev needs L*ceil(T/chunk) + 1
 // caller-created events.
 // ============================================================================
+// the fp32 W-stationary persistent recurrences (sv_persist_f32.hip) instead of the per-step
+// kernels: never under SV_SCHED_PER_STEP; where they fit co-resident, under SV_SCHED_PERSIST
+// always, under SV_SCHED_AUTO when the grid fills at least 3/4 of the device (c2: 240 of 256 CUs;
+// a half-empty grid leaves the chip to per-step kernels that share it with the GEMMs)
+static bool f32_persist(int schedule, int B, int H, hipStream_t s) {
+  if (schedule & SV_SCHED_PER_STEP) return false;
+  const int cus = sv_stream_cus(s);
+  if (!sv_persist_f32_fits(B, H, cus)) return false;
+  return (schedule & SV_SCHED_PERSIST) || 4L * (H / 32) * ((B + 63) / 64) >= 3L * cus;
+}
+
+extern "C" int sv_lstm_f32_persist_ok(int B, int H, int schedule) { return f32_persist(schedule, B, H, nullptr); }
+
 extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float* x_tm, const float* const* w_ih,
                                  const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                                  float* const* gates, float* const* c_tm, float* const* h_tm, float* const* hT,
                                  int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev,
-                                 int products) {
+                                 int products, int schedule, unsigned* sync, hipEvent_t* probe) {
   if (L <= 0 || !x_tm || !w_ih || !w_hh || !gates || !c_tm || !h_tm || !side || !ev || chunk <= 0) return SV_EARG;
-  if (products < 0 || products > 3) return SV_EARG;
+  if (products < 0 || products > 3 || schedule < 0 || schedule > SV_SCHED_MASK) return SV_EARG;
   F32ProductScope scope(products);
   if (!lstm_dims_ok(T, B, F, H)) return SV_ESHAPE;
   const int nch = (T + chunk - 1) / chunk;
   const long BH = (long)B * H, BG = 4L * B * H;
   const int Bp = (B + 3) & ~3;
   const long ldhT = (long)(T + 1) * Bp;
+  hipError_t e;
+  if (f32_persist(schedule, B, H, main)) {
+    // one layer after another on `main`: the whole-T input projection (K1), then ONE persistent
+    // launch for the layer's recurrence (the persistent grid needs the whole chip)
+    if (!sync) return SV_EARG;
+    for (int l = 0; l < L; ++l) {
+      const int Fl = l == 0 ? F : H;
+      const float* in = l == 0 ? x_tm : h_tm[l - 1] + BH;
+      if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), main)) != hipSuccess) return (int)e;
+      if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(float), main)) != hipSuccess)
+        return (int)e;
+      int rc = gemm_f32(1, 1, T * B, 4 * H, Fl, in, Fl, w_ih[l], Fl, gates[l], 4L * H, b_ih[l], b_hh[l], 0.f, nullptr,
+                        main);
+      if (rc) return rc;
+      rc = sv_persist_fwd_f32(T, B, H, w_hh[l], gates[l], c_tm[l], h_tm[l], hT[l], main, sync, 0,
+                              probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr);
+      if (rc) return rc;
+    }
+    return SV_OK;
+  }
   hipEvent_t ev_start = ev[L * nch];
-  hipError_t e = hipEventRecord(ev_start, main);
+  e = hipEventRecord(ev_start, main);
   if (e != hipSuccess) return (int)e;
   for (int l = 0; l < L; ++l) {
     hipStream_t s = side[l];
@@ -951,7 +984,9 @@ extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float*
 //   ev: L*ceil(T/chunk) + L + 1 caller-created events.  Joins back into `main`.
 // ============================================================================
 extern "C" size_t sv_lstm_stack_bwd_workspace(int L, int T, int B, int F, int H) {
-  return (size_t)L * ((carve_bwd(nullptr, T, B, std::max(F, H), H).total + 255) & ~size_t(255));
+  // + the persistent backward's fragment-order hand-off (shared by the layers, one after another)
+  const size_t dgf = H == 768 ? sv_persist_f32_bwd_scratch(T, B, H) : 0;
+  return (size_t)L * ((carve_bwd(nullptr, T, B, std::max(F, H), H).total + 255) & ~size_t(255)) + dgf;
 }
 
 extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float* const* xT, const long* ld_xT,
@@ -960,11 +995,12 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
                                  float* const* dgates, float* const* dgT, float* const* dx, float* const* dw_ih,
                                  float* const* dw_hh, float* const* db_ih, float* const* db_hh, float* workspace,
                                  int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev,
-                                 int products, hipEvent_t* probe, unsigned long long* kstamp) {
+                                 int products, hipEvent_t* probe, unsigned long long* kstamp, int schedule,
+                                 unsigned* sync) {
   if (L <= 0 || !xT || !ld_xT || !w_ih || !w_hh || !gates || !c_tm || !hT || !dh_last || !dgates || !dgT || !dx ||
       !dw_ih || !dw_hh || !db_ih || !workspace || !side || !ev || chunk <= 0)
     return SV_EARG;
-  if (products < 0 || products > 3) return SV_EARG;
+  if (products < 0 || products > 3 || schedule < 0 || schedule > SV_SCHED_MASK) return SV_EARG;
   F32ProductScope scope(products);
   if (!lstm_dims_ok(T, B, F, H)) return SV_ESHAPE;
   const int nch = (T + chunk - 1) / chunk;
@@ -973,8 +1009,46 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
   const int TBp = T * Bp;
   const long ldhT = (long)(T + 1) * Bp;
   const size_t per = (carve_bwd(nullptr, T, B, std::max(F, H), H).total + 255) & ~size_t(255);
+  hipError_t e;
+  if (f32_persist(schedule, B, H, main)) {
+    // per layer, top first, all on `main`: ONE persistent launch for the recurrence, then the
+    // whole-T dx = dG W_ih GEMM (the next layer's dh_up), the dW GEMMs and the bias row sums
+    if (!sync) return SV_EARG;
+    float* dgf = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + per * L);
+    for (int l = L - 1; l >= 0; --l) {
+      const int Fl = l == 0 ? F : H;
+      const BwdWs ws = carve_bwd((float*)((char*)workspace + per * l), T, B, std::max(F, H), H);
+      int rc = sv_transpose(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, main);
+      if (rc) return rc;
+      if (l > 0 && (rc = sv_transpose(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, main))) return rc;
+      const float* up = l == L - 1 ? dh_last : dx[l + 1];
+      rc = sv_persist_bwd_f32(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1, dgates[l], dgT[l], dgf, main, sync,
+                              probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr);
+      if (rc) return rc;
+      // the completion events of layers >= 1 (grad_ready: a caller's bucketed all-reduce) fire once
+      // the last recurrence is done, so a collective never shares the device with a persistent
+      // launch (a concurrent RCCL kernel would hold CUs its grid waits for) but overlaps layer 0's
+      // weight-gradient GEMMs
+      for (int k = 1; l == 0 && k < L; ++k)
+        if ((e = hipEventRecord(ev[L * nch + k], main)) != hipSuccess) return (int)e;
+      if (l > 0 && (rc = gemm_f32(1, 1, T * B, Fl, 4 * H, dgates[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr,
+                                  nullptr, 0.f, ws.gws, main)))
+        return rc;
+      if ((rc = gemm_f32(1, 1, 4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws,
+                         main)))
+        return rc;
+      if ((rc = gemm_f32(1, 1, 4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f,
+                         ws.gws, main)))
+        return rc;
+      hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(RS_T), 0, main, dgT[l], (long)TBp, TBp, db_ih[l],
+                         db_hh ? db_hh[l] : nullptr);
+      SV_LAUNCH_CHECK();
+    }
+    if ((e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
+    return SV_OK;
+  }
   hipEvent_t ev_start = ev[L * nch + L];
-  hipError_t e = hipEventRecord(ev_start, main);
+  e = hipEventRecord(ev_start, main);
   if (e != hipSuccess) return (int)e;
   const dim3 grid((H + BWD_U - 1) / BWD_U, (B + BWD_BM - 1) / BWD_BM);
   for (int l = L - 1; l >= 0; --l) {

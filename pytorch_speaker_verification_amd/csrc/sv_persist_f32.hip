@@ -1,0 +1,569 @@
+// W-stationary persistent recurrences of the fp32 path (config c2: exact fp32 MFMA products).
+//
+// Why: the per-step fp32 kernels (K2 lstm_step_fwd_v2_kernel / K3 lstm_step_bwd_v2_kernel) stream
+// their W_hh tile (393 KB per workgroup) from L2 every timestep and run at 53 % / 45 % of the fp32
+// MFMA rate alone, less beside the layer pipeline's GEMMs.  Here ONE launch per layer runs all T
+// steps with each workgroup's W_hh slice held in registers for the whole sequence, so a step is
+// bound by its MFMAs (v_mfma_f32_32x32x2_f32, 64 cycles each) plus one hand-off.
+//
+// Tile (H = 768): 64 batch rows x 32 hidden units x 4 gates; grid (H / 32) x ceil(B / 64) = 240
+// workgroups at B = 640, one per CU (4 waves, 512 registers each).  Wave g holds gate g's weights
+// for its 32 units over K = H: 96 k-groups of 8 = 384 fp32 registers per lane (256 AGPRs + 128
+// VGPRs).  A k-group's 4 MFMAs take k = 8 kg + 4 h + c (c = 0..3) from lane half h: a fixed
+// permutation of the summation order applied to both operands, so every operand fetch is 16 B.
+//
+// Forward: h_{t-1} of the 64 rows (196 KB) is staged through a 4-slot LDS ring of 64-k chunks by
+// LDS-DMA (global_load_lds, sc1), two chunks ahead, one barrier per chunk; the four waves share each
+// chunk.  The x-projection of step t (K1 output incl. biases, in `gates`) arrives by the same DMA.
+// Hand-off: h_t through h_tm[t + 1] (16-B sc1 stores, vmcnt(0), one arrival per workgroup on the row
+// block's counter; MI355X_MICROARCH.md hand-off table row 1), read back with sc1 DMA.
+// Backward: dh_rec = dG_{t+1} W_hh: wave g streams gate g's K = H slice of dG_{t+1} (64 rows) from a
+// fragment-order hand-off buffer straight into registers (1 KB per load instruction), P k-groups
+// ahead; the per-gate partials meet in LDS and are summed in gate order (K3's order).
+// Outputs are the per-step kernels' buffers (activations, c, h, h^T / dG, dG^T), so either direction
+// composes with the other schedule; results agree with the per-step kernels to fp32 rounding.
+#include "sv_persist_dev.h"
+#include "../../include/sv_ge2e.h"
+
+namespace {
+constexpr int PF_BM = 64, PF_U = 32;
+constexpr int PF_KC = 64;                  // k per forward A chunk
+constexpr int PF_CH = PF_BM * PF_KC * 4;   // 16 KB
+constexpr int PF_NB = 4;                   // ring slots (chunk c + 2 is issued while c is consumed)
+constexpr int PF_NA = 64;                  // weight k-groups in AGPRs (4 x 64 = 256 registers)
+constexpr int PF_XCD = 1;                  // XCD-grouped tile order (persist_tile)
+typedef __attribute__((address_space(3))) void* pf_lds_t;
+typedef __attribute__((address_space(1))) void* pf_glb_t;
+
+// LDS slot of 16-B chunk s of row `row` in a [64][64 k] fp32 ring chunk (an involution)
+__device__ __forceinline__ int pf_slot(int row, int s) { return s ^ (row & 15); }
+
+// a lane's weight k-groups (16 B each, k-group kg at w + stride kg): the first PF_NA into AGPRs
+// (pinned element by element), NV into VGPRs, NL into the wave's LDS slots (lane-strided 1 KB)
+template <int NV, int NL>
+__device__ __forceinline__ void pf_load_w(const float* w, int stride, float (&wa)[4 * PF_NA], float (&wv)[4 * NV],
+                                          char* wl) {
+#pragma unroll
+  for (int s = 0; s < PF_NA; ++s) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(w + stride * s);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wa[4 * s + c] = x[c];
+  }
+#pragma unroll
+  for (int s = 0; s < NV; ++s) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(w + stride * (PF_NA + s));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wv[4 * s + c] = x[c];
+  }
+#pragma unroll
+  for (int s = 0; s < NL; ++s)
+    *reinterpret_cast<f32x4*>(wl + s * 1024) = *reinterpret_cast<const f32x4*>(w + stride * (PF_NA + NV + s));
+#pragma unroll
+  for (int i = 0; i < 4 * PF_NA; ++i) asm volatile("" : "+a"(wa[i]));
+}
+
+template <int N>
+__device__ __forceinline__ void pf_vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+}  // namespace
+
+// ============================================================================
+// forward
+// ============================================================================
+// NV / NL: weight k-groups kept in VGPRs / in LDS (after the PF_NA in AGPRs)
+template <int NKG, int NV, int NL>
+__global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
+    const float* __restrict__ whh, float* gates, float* __restrict__ c_tm, float* h_tm, float* __restrict__ hT,
+    long ldhT, int T, int Bp, int B, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit, int fault) {
+  constexpr int H = 8 * NKG, NCH = H / PF_KC, KGC = PF_KC / 8;
+  static_assert(NCH >= 4 && H % PF_KC == 0 && PF_NA + NV + NL == NKG, "chunk schedule / weight split");
+  constexpr int LDP = 4 * PF_U + 4;  // pre [64][LDP] fp32
+  constexpr int LDH = PF_BM + 4;     // hts [32][LDH] fp32
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ring = smem;                                            // [NB][64 rows][256 B]
+  float* gxs = reinterpret_cast<float*>(smem + PF_NB * PF_CH);  // [64][4 * 32] x-projection of step t
+  char* wl = smem + PF_NB * PF_CH + PF_BM * 4 * PF_U * 4;       // [4 waves][NL][64 lanes][16 B]
+  float* pre = reinterpret_cast<float*>(smem);                  // after the k-loop: aliases the ring
+  float* hts = pre + PF_BM * LDP;                               // (aliases the ring too)
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  int ub, rb;
+  persist_tile(xcd, nub, ub, rb);
+  const int j0 = ub * PF_U, b0 = rb * PF_BM;
+  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
+  unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
+  // W_hh of gate g, units j0 + r: lane (r, hh) of k-group kg holds W[g H + j0 + r][8 kg + 4 hh .. + 3]
+  // (one scalar per register: pinned element by element to AGPRs, the MFMAs read them in place)
+  float wa[4 * PF_NA], wv[4 * NV];
+  {
+    const float* wr = whh + ((long)g * H + j0 + r) * H + 4 * hh;
+    pf_load_w<NV, NL>(wr, 8, wa, wv, wl + (g * NL * 64 + lane) * 16);
+  }
+  auto wfrag = [&](int kg) -> f32x4 {  // (kg a compile-time constant after unrolling)
+    if (kg < PF_NA) {
+      const int b = 4 * (kg < PF_NA ? kg : 0);
+      return f32x4{wa[b], wa[b + 1], wa[b + 2], wa[b + 3]};
+    }
+    if (kg < PF_NA + NV) {
+      const int b = 4 * (kg < PF_NA + NV && kg >= PF_NA ? kg - PF_NA : 0);
+      return f32x4{wv[b], wv[b + 1], wv[b + 2], wv[b + 3]};
+    }
+    return *reinterpret_cast<const f32x4*>(wl + ((g * NL + (kg - PF_NA - NV)) * 64 + lane) * 16);
+  };
+  // elementwise map: thread -> units 4 quad .. + 3 of rows 2 rp, 2 rp + 1
+  const int quad = tid & 7, rp = tid >> 3;
+  float cs[2][4];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) cs[k][v] = 0.f;
+  for (int t = 0; t < T; ++t) {
+    // an opaque zero: keeps the DMA address arithmetic inside the step (hoisted out of the time
+    // loop, the per-lane addresses would hold registers the weights need)
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    const int gz = g + z;
+    // ring chunk DMA: wave g fills rows 16 g .. 16 g + 15 (4 instructions of 4 rows); lane -> row
+    // 16 g + 4 j + (lane >> 4), physical slot lane & 15 holding logical slot pf_slot(row, lane & 15).
+    // Rows past B read row B - 1 (finite; rows never mix in the products and are not stored).
+    auto dma_chunk = [&](int ch, int slot) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = 16 * gz + 4 * j + (lane >> 4);
+        const float* src = h_tm + ((long)t * B + min(b0 + row, B - 1)) * H + ch * PF_KC + 4 * pf_slot(row, lane & 15);
+        __builtin_amdgcn_global_load_lds((pf_glb_t)src, (pf_lds_t)(ring + slot * PF_CH + (16 * g + 4 * j) * 256), 16,
+                                         0, 16 /* sc1 */);
+      }
+    };
+    // x-projection of step t: gxs[row][q 32 + u] = gates[t][b0 + row][q H + j0 + u]
+    auto dma_gx = [&]() {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int q = (8 * gz + j) * 64 + lane, row = q >> 5, s = q & 31;
+        const float* src = gates + (long)t * BG + (long)min(b0 + row, B - 1) * G + (s >> 3) * H + j0 + 4 * (s & 7);
+        __builtin_amdgcn_global_load_lds((pf_glb_t)src, (pf_lds_t)(gxs + (8 * g + j) * 256), 16, 0, 0);
+      }
+    };
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+    if (t > 0) {
+      if (tid == 0) persist_wait(my_cnt, (unsigned)nub * (unsigned)t, status, limit, 1u);
+      __syncthreads();
+      dma_chunk(0, 0);
+      dma_chunk(1, 1);
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        if (ch + 2 < NCH) dma_chunk(ch + 2, (ch + 2) % PF_NB);
+        if (ch == 0) dma_gx();
+        // chunk ch landed (this wave's part): the younger DMAs stay in flight
+        if (ch <= 2)
+          pf_vmwait<16>();
+        else if (ch + 2 < NCH)
+          pf_vmwait<8>();
+        else if (ch + 2 == NCH)
+          pf_vmwait<4>();
+        else
+          pf_vmwait<0>();
+        __builtin_amdgcn_s_barrier();  // ... every wave's part; slot (ch + 2) % 4 was last read at ch - 2
+        __builtin_amdgcn_sched_barrier(0);
+        const char* cbase = ring + (ch % PF_NB) * PF_CH;
+        const char* a0p = cbase + r * 256;
+        const char* a1p = cbase + (32 + r) * 256;
+        f32x4 a0 = *reinterpret_cast<const f32x4*>(a0p + 16 * pf_slot(r, hh));
+        f32x4 a1 = *reinterpret_cast<const f32x4*>(a1p + 16 * pf_slot(32 + r, hh));
+        f32x4 w = wfrag(ch * KGC);
+#pragma unroll
+        for (int kk = 0; kk < KGC; ++kk) {
+          const int kg = ch * KGC + kk;
+          f32x4 n0 = a0, n1 = a1, nw = w;
+          if (kk + 1 < KGC) {  // the next k-group's fragments, one k-group ahead
+            n0 = *reinterpret_cast<const f32x4*>(a0p + 16 * pf_slot(r, 2 * (kk + 1) + hh));
+            n1 = *reinterpret_cast<const f32x4*>(a1p + 16 * pf_slot(32 + r, 2 * (kk + 1) + hh));
+            nw = wfrag(kg + 1);
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[c], w[c], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[c], w[c], acc1, 0, 0, 0);
+          }
+          a0 = n0;
+          a1 = n1;
+          w = nw;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else {
+      dma_gx();
+      pf_vmwait<0>();
+    }
+    __syncthreads();  // every wave done with the ring (pre aliases it) and its gxs part landed
+    // pre-activation exchange: wave g's row halves -> pre[row][g 32 + unit]
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      pre[acc_row(i, lane) * LDP + g * PF_U + r] = acc0[i];
+      pre[(32 + acc_row(i, lane)) * LDP + g * PF_U + r] = acc1[i];
+    }
+    __syncthreads();
+    // cell update; the activations go back into pre and c into gxs's gate-0 slot, in place (each
+    // thread rewrites only the positions it read), for the stores after the arrival
+    f32x4 hv[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int row = 2 * rp + k;
+      f32x4 p[4], x[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        p[q] = *reinterpret_cast<const f32x4*>(pre + row * LDP + q * PF_U + 4 * quad);
+        x[q] = *reinterpret_cast<const f32x4*>(gxs + row * (4 * PF_U) + q * PF_U + 4 * quad);
+      }
+      f32x4 cv;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {  // the per-step kernel's cell (lstm_step_fwd_v2_kernel)
+        const float i_ = sv_sigmoid(p[0][v] + x[0][v]);
+        const float f_ = sv_sigmoid(p[1][v] + x[1][v]);
+        const float g_ = tanhf(p[2][v] + x[2][v]);
+        const float o_ = sv_sigmoid(p[3][v] + x[3][v]);
+        const float c = f_ * cs[k][v] + i_ * g_;
+        cs[k][v] = c;
+        cv[v] = c;
+        hv[k][v] = o_ * tanhf(c);
+        p[0][v] = i_;
+        p[1][v] = f_;
+        p[2][v] = g_;
+        p[3][v] = o_;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4*>(pre + row * LDP + q * PF_U + 4 * quad) = p[q];
+      *reinterpret_cast<f32x4*>(gxs + row * (4 * PF_U) + 4 * quad) = cv;
+    }
+    // the hand-off: h_t into h_tm[t + 1], 16-B sc1 stores, drained before the arrival
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int gb = b0 + 2 * rp + k;
+      if (gb < B) {
+        const __amdgpu_buffer_rsrc_t rw = sv_rsrc(h_tm + (long)(t + 1) * BH, (unsigned)(BH * 4));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, hv[k]), rw,
+                                               ((unsigned)gb * (unsigned)H + (unsigned)(j0 + 4 * quad)) * 4u, 0,
+                                               16 /* sc1 */);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0 && persist_arrive_ok(fault, t == 0))
+      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // off the chain: activations, c, h^T of step t
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int row = 2 * rp + k;
+      const long gb = b0 + row;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) hts[(4 * quad + v) * LDH + row] = gb < B ? hv[k][v] : 0.f;
+      if (gb < B) {
+        float* gp = gates + (long)t * BG + gb * G + j0 + 4 * quad;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<f32x4*>(gp + q * H) = *reinterpret_cast<const f32x4*>(pre + row * LDP + q * PF_U + 4 * quad);
+        *reinterpret_cast<f32x4*>(c_tm + (long)t * BH + gb * H + j0 + 4 * quad) =
+            *reinterpret_cast<const f32x4*>(gxs + row * (4 * PF_U) + 4 * quad);
+      }
+    }
+    if (hT) {
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {  // 32 unit rows x 16 pieces of 4 batch columns
+        const int p = tid + 256 * i, u = p >> 4, c = p & 15, gb = b0 + 4 * c;
+        if (gb < Bp) {
+          float* row = hT + (long)(j0 + u) * ldhT;
+          *reinterpret_cast<f32x4*>(row + (long)(t + 1) * Bp + gb) = *reinterpret_cast<const f32x4*>(hts + u * LDH + 4 * c);
+          if (t == 0) *reinterpret_cast<f32x4*>(row + gb) = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+  }
+}
+
+// ============================================================================
+// backward
+// ============================================================================
+// fragment-order hand-off of dG (fp32): [t][row block][gate q][row half][k-group][64 lanes][4];
+// lane (r, h) of block (q, rh, kg) holds dG[32 rh + r][q H + 8 kg + 4 h .. + 3]
+template <int NKG, int P, int NV, int NL>
+__global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_kernel(
+    const float* __restrict__ whhT, const float* __restrict__ acts, const float* __restrict__ c_tm,
+    const float* __restrict__ dhup, int up_full, float* __restrict__ dg, float* __restrict__ dgT, long lddgT,
+    float* dgf, int T, int Bp, int B, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit, int fault) {
+  constexpr int H = 8 * NKG;
+  static_assert(PF_NA + NV + NL == NKG, "weight split");
+  constexpr int LDR = PF_U + 4;      // red [4][64][LDR]
+  constexpr int LDG = 4 * PF_U + 4;  // dgs [64][LDG] row-major dG tile
+  constexpr int LDT = PF_BM + 4;     // gts [128][LDT] transposed dG tile (aliases red)
+  constexpr int FBLK = NKG * 256;    // floats of one (gate, row half) fragment run
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* ea = reinterpret_cast<float*>(smem);  // [64][128] activations of step t (LDS-DMA image)
+  float* ec = ea + PF_BM * 4 * PF_U;           // [64][32] c_{t-1}
+  float* eu = ec + PF_BM * PF_U;               // [64][32] dh_up of step t
+  float* red = eu + PF_BM * PF_U;              // [4][64][LDR]
+  float* gts = red;                            // [128][LDT], written once red has been read
+  float* dgs = red + 4 * PF_BM * LDR;          // [64][LDG]
+  char* wl = reinterpret_cast<char*>(dgs + PF_BM * LDG);  // [4 waves][NL][64 lanes][16 B]
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  int ub, rb;
+  persist_tile(xcd, nub, ub, rb);
+  const int j0 = ub * PF_U, b0 = rb * PF_BM;
+  const int nrb = gridDim.x / nub;
+  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
+  const long FS = (long)nrb * 4 * 2 * FBLK;  // floats of one step's hand-off slot
+  unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
+  // W_hh^T of gate g, units j0 + r: lane (r, hh) of k-group kg holds W_hh[g H + 8 kg + 4 hh .. + 3][j0 + r]
+  float wa[4 * PF_NA], wv[4 * NV];
+  {
+    const float* wr = whhT + (long)(j0 + r) * G + (long)g * H + 4 * hh;
+    pf_load_w<NV, NL>(wr, 8, wa, wv, wl + (g * NL * 64 + lane) * 16);
+  }
+  auto wfrag = [&](int kg) -> f32x4 {
+    if (kg < PF_NA) {
+      const int b = 4 * (kg < PF_NA ? kg : 0);
+      return f32x4{wa[b], wa[b + 1], wa[b + 2], wa[b + 3]};
+    }
+    if (kg < PF_NA + NV) {
+      const int b = 4 * (kg < PF_NA + NV && kg >= PF_NA ? kg - PF_NA : 0);
+      return f32x4{wv[b], wv[b + 1], wv[b + 2], wv[b + 3]};
+    }
+    return *reinterpret_cast<const f32x4*>(wl + ((g * NL + (kg - PF_NA - NV)) * 64 + lane) * 16);
+  };
+  const int quad = tid & 7, rp = tid >> 3;
+  // step tt's elementwise operands -> LDS (global_load_lds; rows past B read row B - 1).  Wave g:
+  // 8 activation pieces (rows 16 g ..), 2 of c_{t-1}, 2 of dh_up; an absent operand (c_{-1}, dh_up
+  // of a step without one) is written as zeros into the same lanes' slots instead.
+  auto load_ew = [&](int tt) {
+    int z = 0;  // opaque zero: the address arithmetic stays here (see the forward)
+    asm volatile("" : "+v"(z));
+    const int gz = g + z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int q = (8 * gz + j) * 64 + lane, row = q >> 5, s = q & 31;
+      const float* src = acts + (long)tt * BG + (long)min(b0 + row, B - 1) * G + (s >> 3) * H + j0 + 4 * (s & 7);
+      __builtin_amdgcn_global_load_lds((pf_glb_t)src, (pf_lds_t)(ea + (8 * g + j) * 256), 16, 0, 0);
+    }
+    const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int q = (2 * gz + j) * 64 + lane, row = q >> 3, c = q & 7;
+      const long off = (long)min(b0 + row, B - 1) * H + j0 + 4 * c;
+      if (tt > 0)
+        __builtin_amdgcn_global_load_lds((pf_glb_t)(c_tm + (long)(tt - 1) * BH + off),
+                                         (pf_lds_t)(ec + (2 * g + j) * 256), 16, 0, 0);
+      else
+        *reinterpret_cast<f32x4*>(ec + 4 * q) = zero;
+      if (up)
+        __builtin_amdgcn_global_load_lds((pf_glb_t)(up + off), (pf_lds_t)(eu + (2 * g + j) * 256), 16, 0, 0);
+      else
+        *reinterpret_cast<f32x4*>(eu + 4 * q) = zero;
+    }
+  };
+  // c_{T-1} of the thread's cells; the cell-gradient carry
+  f32x4 cv[2], dcf[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int gb = min(b0 + 2 * rp + k, B - 1);
+    cv[k] = *reinterpret_cast<const f32x4*>(c_tm + (long)(T - 1) * BH + (long)gb * H + j0 + 4 * quad);
+    dcf[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  load_ew(T - 1);
+  for (int t = T - 1; t >= 0; --t) {
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+    if (t < T - 1) {
+      if (tid == 0) persist_wait(my_cnt, (unsigned)nub * (unsigned)(T - 1 - t), status, limit, 2u);
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t ra = sv_rsrc(dgf + (long)(t + 1) * FS, (unsigned)(FS * 4));
+      const unsigned base = ((unsigned)((rb * 4 + g) * 2) * (unsigned)FBLK + (unsigned)lane * 4u) * 4u;
+      constexpr unsigned HALF = FBLK * 4u;  // bytes from row half 0 to row half 1
+      u32x4_t f0[P], f1[P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        f0[p] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + 1024u * p, 0, 16 /* sc1 */);
+        f1[p] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + HALF + 1024u * p, 0, 16 /* sc1 */);
+      }
+      f32x4 w = wfrag(0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kg = 0; kg < NKG; ++kg) {
+        const f32x4 a0 = __builtin_bit_cast(f32x4, f0[kg % P]), a1 = __builtin_bit_cast(f32x4, f1[kg % P]);
+        const f32x4 nw = kg + 1 < NKG ? wfrag(kg + 1) : w;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[c], w[c], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[c], w[c], acc1, 0, 0, 0);
+        }
+        if (kg + P < NKG) {
+          f0[kg % P] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + 1024u * (kg + P), 0, 16);
+          f1[kg % P] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + HALF + 1024u * (kg + P), 0, 16);
+        }
+        w = nw;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // per-gate partials -> red[g][row][unit]
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      red[(g * PF_BM + acc_row(i, lane)) * LDR + r] = acc0[i];
+      red[(g * PF_BM + 32 + acc_row(i, lane)) * LDR + r] = acc1[i];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
+    __syncthreads();
+    // dh = the partials in gate order + dh_up (K3's order); then red is free for the dG^T tile
+    f32x4 dh[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int row = 2 * rp + k;
+      dh[k] = *reinterpret_cast<const f32x4*>(red + (0 * PF_BM + row) * LDR + 4 * quad);
+      dh[k] += *reinterpret_cast<const f32x4*>(red + (1 * PF_BM + row) * LDR + 4 * quad);
+      dh[k] += *reinterpret_cast<const f32x4*>(red + (2 * PF_BM + row) * LDR + 4 * quad);
+      dh[k] += *reinterpret_cast<const f32x4*>(red + (3 * PF_BM + row) * LDR + 4 * quad);
+      dh[k] += *reinterpret_cast<const f32x4*>(eu + row * PF_U + 4 * quad);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int row = 2 * rp + k;
+      const f32x4 cpv = *reinterpret_cast<const f32x4*>(ec + row * PF_U + 4 * quad);
+      f32x4 a[4], dq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] = *reinterpret_cast<const f32x4*>(ea + row * (4 * PF_U) + q * PF_U + 4 * quad);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {  // the per-step kernel's cell backward (lstm_step_bwd_v2_kernel)
+        const float d = dh[k][v];
+        const float i_ = a[0][v], f_ = a[1][v], g_ = a[2][v], o_ = a[3][v];
+        const float tc = tanhf(cv[k][v]);
+        const float dc = d * o_ * (1.f - tc * tc) + dcf[k][v];
+        dq[0][v] = dc * g_ * i_ * (1.f - i_);
+        dq[1][v] = dc * cpv[v] * f_ * (1.f - f_);
+        dq[2][v] = dc * i_ * (1.f - g_ * g_);
+        dq[3][v] = d * tc * o_ * (1.f - o_);
+        dcf[k][v] = dc * f_;
+      }
+      cv[k] = cpv;  // c_{t-1} is the next step's c_t
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        *reinterpret_cast<f32x4*>(dgs + row * LDG + q * PF_U + 4 * quad) = dq[q];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) gts[(q * PF_U + 4 * quad + v) * LDT + row] = dq[q][v];
+      }
+    }
+    __syncthreads();
+    // the hand-off: 32 fragment blocks of 1 KB (gate q, row half rh, k-group 4 ub + kl), sc1 stores
+    if (t > 0) {
+      const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 4));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int p = tid + 256 * i, blk = p >> 6, L = p & 63;
+        const int q = blk >> 3, rh = (blk >> 2) & 1, kl = blk & 3;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(dgs + (32 * rh + (L & 31)) * LDG + q * PF_U + 8 * kl + 4 * (L >> 5));
+        const unsigned off = ((unsigned)(((rb * 4 + q) * 2 + rh) * FBLK) + (unsigned)(4 * ub + kl) * 256u + (unsigned)L * 4u) * 4u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rw, off, 0, 16 /* sc1 */);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
+        __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // off the chain: row-major dG (the dx GEMM's operand) and dG^T (the dW GEMMs' and bias sums')
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int row = 2 * rp + k;
+      const long gb = b0 + row;
+      if (gb < B) {
+        float* dp = dg + (long)t * BG + gb * G + j0 + 4 * quad;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<f32x4*>(dp + q * H) = *reinterpret_cast<const f32x4*>(dgs + row * LDG + q * PF_U + 4 * quad);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // 128 gate-unit rows x 16 pieces of 4 batch columns
+      const int p = tid + 256 * i, gu = p >> 4, c = p & 15, gb = b0 + 4 * c;
+      if (gb < Bp) {
+        f32x4 v = *reinterpret_cast<const f32x4*>(gts + gu * LDT + 4 * c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (gb + e >= B) v[e] = 0.f;
+        *reinterpret_cast<f32x4*>(dgT + ((long)(gu >> 5) * H + j0 + (gu & 31)) * lddgT + (long)t * Bp + gb) = v;
+      }
+    }
+    if (t > 0) {
+      __syncthreads();  // ea / ec / eu read by every wave before the next step's operands land there
+      load_ew(t - 1);   // in flight during the next hand-off wait
+    }
+  }
+}
+
+// ============================================================================
+// host side
+// ============================================================================
+namespace {
+// weight k-groups (of 96 at H = 768) in VGPRs / LDS beside the 64 in AGPRs
+constexpr int PF_FWD_NV = 16, PF_FWD_NL = 16, PF_BWD_NV = 22, PF_BWD_NL = 10, PF_BWD_P = 3;
+constexpr size_t pf_fwd_lds() {
+  return (size_t)PF_NB * PF_CH + (size_t)PF_BM * 4 * PF_U * 4 + (size_t)4 * PF_FWD_NL * 1024;
+}
+constexpr size_t pf_bwd_lds() {
+  return (size_t)PF_BM * 4 * PF_U * 4 + 2 * (size_t)PF_BM * PF_U * 4 + (size_t)4 * PF_BM * (PF_U + 4) * 4 +
+         (size_t)PF_BM * (4 * PF_U + 4) * 4 + (size_t)4 * PF_BWD_NL * 1024;
+}
+static_assert(pf_fwd_lds() <= 160 * 1024 && pf_bwd_lds() <= 160 * 1024, "LDS");
+static_assert((size_t)4 * PF_U * (PF_BM + 4) <= (size_t)4 * PF_BM * (PF_U + 4), "gts fits in red");
+}  // namespace
+
+// the fp32 persistent recurrences fit: H = 768, (H / 32) x ceil(B / 64) workgroups co-resident
+int sv_persist_f32_fits(int B, int H, int cus) {
+  const long nrb = (B + PF_BM - 1) / PF_BM;
+  return H == 768 && B > 0 && nrb <= SV_PCNT_ROWS && (H / PF_U) * nrb <= cus && (long)B * 4 * H * 4 < (1L << 31);
+}
+
+// bytes of the backward's fragment-order hand-off: T slots of ceil(B / 64) x 64 rows x 4H fp32
+size_t sv_persist_f32_bwd_scratch(int T, int B, int H) {
+  return (size_t)T * (size_t)((B + PF_BM - 1) / PF_BM) * PF_BM * 4 * H * sizeof(float);
+}
+
+int sv_persist_fwd_f32(int T, int B, int H, const float* whh, float* gates, float* c_tm, float* h_tm, float* hT,
+                       hipStream_t stream, unsigned* sync, int chan, hipEvent_t pre, hipEvent_t post) {
+  if (!sv_persist_f32_fits(B, H, sv_stream_cus(stream))) return SV_ESHAPE;
+  if (!sync || chan < 0 || chan >= SV_SYNC_CHANNELS || !whh || !gates || !c_tm || !h_tm) return SV_EARG;
+  unsigned* cnt = sync + SV_SYNC_CNT + (size_t)chan * SV_PCNT_ROWS * SV_PCNT_STRIDE;
+  const int nub = H / PF_U, nrb = (B + PF_BM - 1) / PF_BM;
+  const int Bp = (B + 3) & ~3;
+  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
+  if (e != hipSuccess) return (int)e;
+  if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
+  hipLaunchKernelGGL((lstm_persist_fwd_f32_kernel<96, PF_FWD_NV, PF_FWD_NL>), dim3(nub * nrb), dim3(256), pf_fwd_lds(), stream, whh, gates,
+                     c_tm, h_tm, hT, (long)(T + 1) * Bp, T, Bp, B, cnt, nub, PF_XCD, sync, sv_persist_limit(),
+                     sv_persist_fault(0));
+  SV_LAUNCH_CHECK();
+  if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
+  return SV_OK;
+}
+
+int sv_persist_bwd_f32(int T, int B, int H, const float* whhT, const float* acts, const float* c_tm,
+                       const float* dhup, int up_full, float* dg, float* dgT, float* dgf, hipStream_t stream,
+                       unsigned* sync, hipEvent_t pre, hipEvent_t post) {
+  if (!sv_persist_f32_fits(B, H, sv_stream_cus(stream))) return SV_ESHAPE;
+  if (!sync || !whhT || !acts || !c_tm || !dg || !dgT || !dgf || ((uintptr_t)dgf & 15)) return SV_EARG;
+  unsigned* cnt = sync + SV_SYNC_CNT;  // channel 0
+  const int nub = H / PF_U, nrb = (B + PF_BM - 1) / PF_BM;
+  const int Bp = (B + 3) & ~3;
+  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
+  if (e != hipSuccess) return (int)e;
+  if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
+  hipLaunchKernelGGL((lstm_persist_bwd_f32_kernel<96, PF_BWD_P, PF_BWD_NV, PF_BWD_NL>), dim3(nub * nrb), dim3(256), pf_bwd_lds(), stream, whhT,
+                     acts, c_tm, dhup, up_full, dg, dgT, (long)T * Bp, dgf, T, Bp, B, cnt, nub, PF_XCD, sync,
+                     sv_persist_limit(), sv_persist_fault(1));
+  SV_LAUNCH_CHECK();
+  if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
+  return SV_OK;
+}

@@ -126,10 +126,15 @@ class EmbedderState:
         self.bf16 = False
 
 
-def embedder_forward(x, layers, w_p, b_p, save=True, products="mfma_f32"):
+def embedder_forward(x, layers, w_p, b_p, save=True, products="mfma_f32", status=None, probe=None, schedule="auto"):
     """x [B,T,F] float32 (batch_first); layers = [(w_ih, w_hh, b_ih, b_hh)] * L.
-    Returns (emb [B,P], state).  products: fp32 product mode of the stack (F32_PRODUCT_MODES)."""
+    Returns (emb [B,P], state).  products: fp32 product mode of the stack (F32_PRODUCT_MODES).
+    schedule: 'auto' (the persistent recurrences where they fill the device, sv_lstm_f32_persist_ok),
+    'per_step' (layer-pipelined K2 steps) or 'persist'; status: the caller's PersistStatus (sync
+    block of the persistent recurrences; None = a fresh one, checked at the next call / by
+    check_persistent_status()); probe: 2*L events around the layers' persistent launches."""
     prod = _products(products)
+    sched = schedule_flags(schedule)
     require_device(x, w_p, b_p, *[t for l in layers for t in l])
     B, T, F = x.shape
     H = layers[0][1].shape[1]
@@ -160,9 +165,12 @@ def embedder_forward(x, layers, w_p, b_p, save=True, products="mfma_f32"):
         streams, events = _StreamPool.get(dev, "fwd", L, L * nch + 1)
         sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * (L * nch + 1))(*[e.cuda_event for e in events[:L * nch + 1]])
+        ps, own = _own_status(status, dev)
         call("sv_lstm_stack_fwd", L, T, B, F, H, ptr(x_tm), _parr([l[0] for l in layers]),
              _parr([l[1] for l in layers]), _parr([l[2] for l in layers]), _parr([l[3] for l in layers]),
-             _parr(gs), _parr(cs), _parr(hs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep, prod)
+             _parr(gs), _parr(cs), _parr(hs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep, prod, sched, ps.ptr(),
+             _evarr(probe))
+        _release_status(ps, own)
         if save:
             st.x_tm = [x_tm] + [h[1:] for h in hs[:-1]]
             st.gates, st.c_tm, st.h_tm, st.hT = gs, cs, hs, hTs
@@ -198,7 +206,7 @@ def embedder_forward(x, layers, w_p, b_p, save=True, products="mfma_f32"):
 
 
 def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_ready=None, products="mfma_f32",
-                      probe=None, kstamp=None):
+                      probe=None, kstamp=None, status=None, schedule="auto"):
     """Backward of embedder_forward.  ``grads`` (optional) is a list of preallocated
     output tensors in parameter order [w_ih, w_hh, b_ih, b_hh]*L + [w_p, b_p]; returns it
     (and dx [B,T,F] if need_dx).
@@ -211,8 +219,11 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
     ``probe`` (optional): 2*L*ceil(T/chunk) timing events recorded around one recurrent-step
     launch per chunk; ``kstamp`` (optional): int64 device tensor of 2*L*T slots, pairs preset
     to (-1, 0), set by every recurrent-step launch (l, t) to its start / end on the GPU's 100 MHz
-    real-time clock (include/sv_ge2e.h, sv_lstm_stack_bwd)."""
+    real-time clock (include/sv_ge2e.h, sv_lstm_stack_bwd).  Under the persistent schedule
+    (``schedule``, ``status`` as embedder_forward) probe[2l] / [2l+1] bracket layer l's launch and
+    kstamp is not written."""
     prod = _products(products)
+    sched = schedule_flags(schedule)
     demb = demb.contiguous()
     require_device(demb)
     T, B, H, P = st.T, st.B, st.H, st.P
@@ -228,13 +239,17 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
     ws = _ws(lib().sv_proj_norm_workspace(B, H, P), dev)
     call("sv_proj_norm_bwd", ptr(demb), ptr(st.emb), ptr(st.ynorm), ptr(st.h_last), B, H, P, ptr(w_p),
          ptr(grads[4 * L]), ptr(grads[4 * L + 1]), ptr(dh_last), ptr(ws), s)
-    if grad_ready:
+    stacked = PIPELINE_CHUNK > 0 and L > 1 and not need_dx
+    # under the persistent schedule the projection bucket is enqueued behind the stack backward
+    # (a collective must not run beside a persistent launch); else it overlaps the BPTT
+    late_head = stacked and bool(lib().sv_lstm_f32_persist_ok(B, H, sched))
+    if grad_ready and not late_head:
         grad_ready(L, None)
-    if prod and not (PIPELINE_CHUNK > 0 and L > 1 and not need_dx):
+    if prod and not stacked:
         raise ValueError("the bf16x6 product mode runs on the layer-pipelined stack only")
     Fmax = max(st.x_tm[l].shape[2] for l in range(L))
     Bp = (B + 3) // 4 * 4
-    if PIPELINE_CHUNK > 0 and L > 1 and not need_dx:
+    if stacked:
         F0 = st.x_tm[0].shape[2]
         ws = _ws(lib().sv_lstm_stack_bwd_workspace(L, T, B, F0, H), dev)
         dgs = [torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev) for _ in range(L)]
@@ -245,6 +260,7 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
         nch = (T + PIPELINE_CHUNK - 1) // PIPELINE_CHUNK
         nev = L * nch + L + 1
         streams, events = _StreamPool.get(dev, "bwd", L, nev)
+        ps, own = _own_status(status, dev)
         sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
         call("sv_lstm_stack_bwd", L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
@@ -252,8 +268,12 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
              _parr(st.hT), ptr(dh_last), _parr(dgs), _parr(dgTs), _parr(dxs),
              _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
              _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
-             PIPELINE_CHUNK, s, sp, ep, prod, _evarr(probe), ptr(kstamp) if kstamp is not None else None)
+             PIPELINE_CHUNK, s, sp, ep, prod, _evarr(probe), ptr(kstamp) if kstamp is not None else None, sched,
+             ps.ptr())
+        _release_status(ps, own)
         if grad_ready:
+            if late_head:
+                grad_ready(L, None)
             for l in range(L - 1, -1, -1):
                 grad_ready(l, events[L * nch + l])
         return grads
@@ -455,8 +475,8 @@ def _flat_grads(params, dev):
 class EmbedderFunction(torch.autograd.Function):
     """emb = SpeechEmbedder.forward(x) with params (w_ih, w_hh, b_ih, b_hh)*L, w_p, b_p.
 
-    bf16: the forward and backward share one sync block; if a persistent recurrence of either
-    timed out, every returned gradient is NaN (sv_status_poison), so an optimizer step on them
+    The forward and backward share one sync block; if a persistent recurrence of either timed
+    out, every returned gradient is NaN (sv_status_poison), so an optimizer step on them
     cannot pass unnoticed, and check_persistent_status() raises."""
 
     @staticmethod
@@ -464,13 +484,13 @@ class EmbedderFunction(torch.autograd.Function):
         L = num_layers
         layers = [tuple(params[4 * l:4 * l + 4]) for l in range(L)]
         w_p, b_p = params[4 * L], params[4 * L + 1]
-        ctx.status = None
+        ctx.status = PersistStatus(x.device)
         if precision == "bf16":
-            ctx.status = PersistStatus(x.device)
             emb, st = embedder_forward_bf16(x.contiguous(), layers, w_p, b_p, save=True, status=ctx.status,
                                             schedule=schedule)
         else:
-            emb, st = embedder_forward(x.contiguous(), layers, w_p, b_p, save=True, products=products)
+            emb, st = embedder_forward(x.contiguous(), layers, w_p, b_p, save=True, products=products,
+                                       status=ctx.status, schedule=schedule)
         ctx.precision, ctx.products, ctx.schedule = precision, products, schedule
         ctx.st = st
         ctx.L = L
@@ -483,18 +503,19 @@ class EmbedderFunction(torch.autograd.Function):
         L = ctx.L
         layers = [tuple(params[4 * l:4 * l + 4]) for l in range(L)]
         need_dx = ctx.needs_input_grad[0]
+        grads, flat = _flat_grads(params, demb.device)
         if ctx.precision == "bf16":
             if need_dx:
                 raise NotImplementedError("input gradients are only produced by the fp32 path")
-            grads, flat = _flat_grads(params, demb.device)
             out = embedder_backward_bf16(ctx.st, demb, layers, params[4 * L], grads=grads, status=ctx.status,
                                          schedule=ctx.schedule)
-            call("sv_status_poison", ctx.status.ptr(), ptr(flat), flat.numel(), stream_of(flat))
-            ctx.status.arm()
-            _UNCHECKED.append(ctx.status)
-            ctx.status = None
         else:
-            out = embedder_backward(ctx.st, demb, layers, params[4 * L], need_dx=need_dx, products=ctx.products)
+            out = embedder_backward(ctx.st, demb, layers, params[4 * L], grads=grads, need_dx=need_dx,
+                                    products=ctx.products, status=ctx.status, schedule=ctx.schedule)
+        call("sv_status_poison", ctx.status.ptr(), ptr(flat), flat.numel(), stream_of(flat))
+        ctx.status.arm()
+        _UNCHECKED.append(ctx.status)
+        ctx.status = None
         ctx.st = None
         if need_dx:
             grads, dx = out

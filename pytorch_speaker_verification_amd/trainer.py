@@ -19,13 +19,15 @@ all-reduce and the clip+SGD update each touch one contiguous buffer:
 Data parallel: one process per GPU; rank r holds speakers [r*N, (r+1)*N) of a global
 batch of world*N speakers (ShardedGE2E), so the step is the single-GPU step of that
 global batch.  The gradient SUM all-reduce is bucketed by readiness:
-bucket L = projection + pad + {w, b} (ready before the BPTT starts), then one bucket per
-LSTM layer, top layer first, each launched on a communication stream as soon as the
-backward's per-layer completion event fires, so RCCL traffic overlaps the lower layers'
-BPTT; the clip + SGD kernel waits for all buckets.
+bucket L = projection + pad + {w, b}, then one bucket per LSTM layer, top layer first, each
+launched on a communication stream as soon as the backward's per-layer completion event
+fires; the clip + SGD kernel waits for all buckets.  Per-step schedules: bucket L goes before
+the BPTT starts and RCCL traffic overlaps the lower layers' BPTT.  Persistent schedules (no
+collective may run beside a persistent grid): bucket L and the upper layers' buckets go once
+the last recurrence is done, overlapping layer 0's weight-gradient GEMMs.
 
 Failure surfacing (the reference never steps on wrong gradients, train_speech_embedder.py:61-65):
-the persistent bf16 recurrences synchronise through this trainer's own sync block
+the persistent recurrences (fp32 and bf16) synchronise through this trainer's own sync block
 (``self.status``, include/sv_ge2e.h).  If a hand-off wait times out, the block's sticky status
 is set, the clip + SGD kernels skip the update on the device, the returned loss is NaN, and the
 next ``step()`` (or ``check()``) raises PersistentRecurrenceError -- read through an async
@@ -126,8 +128,8 @@ class GE2ETrainer:
     def step(self, x, N, M, probe=None):
         """x: [N*M, T, nmels] float32 on this rank's GPU (this rank's N speakers x M
         utterances, speaker-major).  Returns the (global) loss as a 0-dim device tensor.
-        probe (bench only): {"fwd": events, "bwd": events} timing events handed to the stack
-        forward (bf16) / backward (include/sv_ge2e.h)."""
+        probe (bench only): {"fwd": events, "bwd": events, "kstamp": tensor} timing probes handed
+        to the stack forward / backward (include/sv_ge2e.h)."""
         probe = probe or {}
         self.status.poll()  # raises if an earlier step's recurrences timed out
         self._check_layout()
@@ -142,7 +144,8 @@ class GE2ETrainer:
             emb, st = embedder_forward_bf16(x.float().contiguous(), layers, w_p, b_p, status=self.status,
                                             probe=probe.get("fwd"), schedule=schedule)
         else:
-            emb, st = embedder_forward(x.float().contiguous(), layers, w_p, b_p, products=products)
+            emb, st = embedder_forward(x.float().contiguous(), layers, w_p, b_p, products=products,
+                                       status=self.status, probe=probe.get("fwd"), schedule=schedule)
         E = emb.view(N, M, emb.shape[1])
         dp = self.ge2e.world > 1
         # data parallel: the local loss partial goes to the head bucket's all-reduce (no collective)
@@ -159,9 +162,10 @@ class GE2ETrainer:
 
             def ready(k, event):
                 lo, hi = self.buckets[k]
-                if k == len(self.buckets) - 1 and bf16:
-                    # the head bucket is enqueued behind the whole stack backward (bf16): the
-                    # status word is final, its bits go along as flags
+                if k == len(self.buckets) - 1:
+                    # the status bits go along as flags: under the persistent schedules the head
+                    # bucket is enqueued behind the whole stack backward, so the word is final
+                    # (the per-step schedules never set it)
                     call("sv_status_to_flag", self.status.ptr(), ptr(self.flags), stream_of(self.flags))
                 if event is None:
                     comm.wait_stream(main)
@@ -174,21 +178,19 @@ class GE2ETrainer:
                                    status=self.status, probe=probe.get("bwd"), schedule=schedule)
         else:
             embedder_backward(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views, grad_ready=ready,
-                              products=products, probe=probe.get("bwd"), kstamp=probe.get("kstamp"))
+                              products=products, probe=probe.get("bwd"), kstamp=probe.get("kstamp"),
+                              status=self.status, schedule=schedule)
         for wk in works:
             wk.wait()  # the current (main) stream waits for every bucket
         if dp:
             loss = self.loss_word.reshape(())  # the sum of every rank's partial
-            if bf16:  # any rank's timeout -> this rank's status too: every rank skips the update
-                call("sv_status_merge", self.status.ptr(), ptr(self.flags), stream_of(self.flags))
+            # any rank's timeout -> this rank's status too: every rank skips the update
+            call("sv_status_merge", self.status.ptr(), ptr(self.flags), stream_of(self.flags))
         n = self.n_pad
-        st_ = self.status if bf16 else None  # (the fp32 path has no persistent recurrences)
-        clip_sgd_step_(self.flat_p[:n], self.flat_g[:n], self.clip_net, self.lr, self.write_grads, status=st_)
-        clip_sgd_step_(self.flat_p[n:n + 4], self.flat_g[n:n + 4], self.clip_wb, self.lr, self.write_grads, status=st_)
-        if bf16:
-            loss = loss.clone() if dp else loss  # (not a view of flat_g, which the next step reuses)
-            call("sv_status_poison", self.status.ptr(), ptr(loss), 1, stream_of(loss))
-            self.status.arm()
-        elif dp:
-            loss = loss.clone()
+        clip_sgd_step_(self.flat_p[:n], self.flat_g[:n], self.clip_net, self.lr, self.write_grads, status=self.status)
+        clip_sgd_step_(self.flat_p[n:n + 4], self.flat_g[n:n + 4], self.clip_wb, self.lr, self.write_grads,
+                       status=self.status)
+        loss = loss.clone() if dp else loss  # (not a view of flat_g, which the next step reuses)
+        call("sv_status_poison", self.status.ptr(), ptr(loss), 1, stream_of(loss))
+        self.status.arm()
         return loss

@@ -43,10 +43,19 @@ with open(os.path.join(prof, f"{tag}_roofline_check.txt"), "w") as f:
     f.write("rocprofv3 kernel traces of `bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-vendor --no-bf16 "
             "--fwd-steps 1` (f32, c2) and `... --dtype bf16` (c3) against the bench line of the same tree\n")
     rf = pf["f32"]["roofline"]
-    # the headline run's timed steps: launches [warmup, warmup + steps) x L*T of the first run
-    d = durations("f32", "void lstm_step_bwd_v2_kernel")
-    line(f, "roofline (c2 headline): lstm_step_bwd_v2_kernel (K3), the 3 timed steps' launches",
-         d[480:4 * 480], rf["avg_launch_us"], 2.0 * B * H * 4 * H)
+    if rf["kernel"].startswith("lstm_persist_bwd_f32_kernel"):
+        # one launch per layer: the headline run's timed steps are its launches [L, 4 L)
+        d = durations("f32", "void lstm_persist_bwd_f32_kernel")
+        line(f, "roofline (c2 headline): lstm_persist_bwd_f32_kernel, the 3 timed steps' launches", d[3:12],
+             rf["avg_launch_us"], 2.0 * B * T * H * 4 * H)
+        d = durations("f32", "void lstm_persist_fwd_f32_kernel")
+        line(f, "roofline_fwd (c2 headline): lstm_persist_fwd_f32_kernel, the 3 timed steps' launches", d[3:12],
+             pf["f32"]["roofline_fwd"]["avg_launch_us"], 2.0 * B * T * H * 4 * H)
+    else:
+        # the headline run's timed steps: launches [warmup, warmup + steps) x L*T of the first run
+        d = durations("f32", "void lstm_step_bwd_v2_kernel")
+        line(f, "roofline (c2 headline): lstm_step_bwd_v2_kernel (K3), the 3 timed steps' launches",
+             d[480:4 * 480], rf["avg_launch_us"], 2.0 * B * H * 4 * H)
     rg = pf["f32"].get("roofline_gemm")
     if rg:
         # bench.py times 5 isolated launches at the K1 shape after the steps: the last 5 of that grid

@@ -78,16 +78,22 @@ def test_small_net_fused_trainer_matches_reference():
     np.testing.assert_allclose([ge2e.w.item(), ge2e.b.item()], s["wb_final"], atol=1e-5)
 
 
-def test_full_dims_c1_matches_reference():
+@pytest.mark.parametrize("schedule", ["auto", "persist"])
+def test_full_dims_c1_matches_reference(schedule):
+    """The reference's own full-dims step at c1 (B = 20, T = 160): under 'auto' the per-step
+    kernels (the persistent grid would fill 24 of 256 CUs), under 'persist' the fp32
+    W-stationary persistent recurrences (sv_persist_f32.hip) against the same golden."""
     s = golden("net_full_c1.npz")
     dims = tuple(int(v) for v in s["dims"])
     net, ge2e = _build(dims, recipe.make_weights(int(s["wseed"]), *dims, scale=float(s["wscale"])))
+    net.schedule = schedule
+    tag = "c1" if schedule == "auto" else "c1_persist"
     N, M, T = int(s["N"]), int(s["M"]), int(s["T"])
     x = torch.tensor(recipe.make_frames(int(s["xseed"]), N * M, T, dims[0]), device=DEV)
     emb = net(x).reshape(N, M, -1)
-    _check("c1.emb_abs", float(np.abs(emb.detach().cpu().numpy() - s["emb"]).max()), 2e-6)
+    _check(f"{tag}.emb_abs", float(np.abs(emb.detach().cpu().numpy() - s["emb"]).max()), 2e-6)
     loss = ge2e(emb)
-    _check("c1.loss_rel", abs(loss.item() - float(s["loss"])) / abs(float(s["loss"])), 2e-6)
+    _check(f"{tag}.loss_rel", abs(loss.item() - float(s["loss"])) / abs(float(s["loss"])), 2e-6)
     loss.backward()
     gn, gh = 0.0, 0.0
     for k, p in net.named_parameters():
@@ -96,35 +102,39 @@ def test_full_dims_c1_matches_reference():
         head = g.reshape(g.shape[0], -1)[:8, :8].numpy() if g.dim() == 2 else g[:64].numpy()
         ref = s["ghead." + k]
         gh = max(gh, float(np.abs(head - ref).max()) / max(np.abs(ref).max(), 1e-6))
-    _check("c1.grad_norm_rel", gn, 2e-5)
-    _check("c1.grad_head_rel", gh, 5e-5)
+    _check(f"{tag}.grad_norm_rel", gn, 2e-5)
+    _check(f"{tag}.grad_head_rel", gh, 5e-5)
 
 
-def test_full_size_c2_against_torch_gpu():
-    """c2 (N=64 x M=10, T=160) vs the stock-PyTorch fp32 port of the reference on the same GPU."""
+@pytest.mark.parametrize("schedule", ["auto", "per_step"])
+def test_full_size_c2_against_torch_gpu(schedule):
+    """c2 (N=64 x M=10, T=160) vs the stock-PyTorch fp32 port of the reference on the same GPU:
+    'auto' runs the fp32 persistent recurrences at this batch, 'per_step' the K2 / K3 kernels."""
     dims, N, M, T = (40, 768, 3, 256), 64, 10, 160
     sd = recipe.make_weights(2024, *dims, scale=3.0)
     net, ge2e = _build(dims, sd)
+    net.schedule = schedule
+    tag = "c2" if schedule == "auto" else "c2_per_step"
     port = torch_port.SpeechEmbedderPort(*dims)
     torch_port.load_recipe_weights(port, sd)
     port = port.to(DEV)
     x = torch.tensor(recipe.make_frames(1236, N * M, T, dims[0]), device=DEV)
     emb = net(x).reshape(N, M, -1)
     emb_ref = port(x).reshape(N, M, -1)
-    _check("c2.emb_rel_vs_miopen", _rel(emb.detach().cpu().numpy(), emb_ref.detach().cpu().numpy()), 1e-5)
+    _check(f"{tag}.emb_rel_vs_miopen", _rel(emb.detach().cpu().numpy(), emb_ref.detach().cpu().numpy()), 1e-5)
     # unit-norm rows (size-independent property of the projection + L2 norm)
     np.testing.assert_allclose(emb.norm(dim=2).detach().cpu().numpy(), 1.0, atol=1e-5)
     loss = ge2e(emb)
     w = torch.tensor(10.0, device=DEV, requires_grad=True)
     b = torch.tensor(-5.0, device=DEV, requires_grad=True)
     loss_ref = torch_port.ge2e_loss(emb_ref, w, b)
-    _check("c2.loss_rel_vs_miopen", abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()), 1e-6)
+    _check(f"{tag}.loss_rel_vs_miopen", abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()), 1e-6)
     loss.backward()
     loss_ref.backward()
     pr = dict(port.named_parameters())
     g = max(_rel(p.grad.cpu().numpy(), pr[k].grad.cpu().numpy()) for k, p in net.named_parameters())
-    _check("c2.grad_rel_vs_miopen", g, 4e-5)
-    _check("c2.dw_vs_miopen", abs(ge2e.w.grad.item() - w.grad.item()) / max(1, abs(w.grad.item())), 2.5e-5)
+    _check(f"{tag}.grad_rel_vs_miopen", g, 4e-5)
+    _check(f"{tag}.dw_vs_miopen", abs(ge2e.w.grad.item() - w.grad.item()) / max(1, abs(w.grad.item())), 2.5e-5)
 
 
 def test_batch_permutation_invariance():
@@ -235,3 +245,30 @@ def test_ragged_training_step_bf16(dims, N, M, T):
         out[prec] = [float(tr.step(xd, N, M)) for _ in range(2)]
         assert all(torch.isfinite(p).all() for p in net.parameters())
     np.testing.assert_allclose(out["bf16"], out["f32"], rtol=1e-2)
+
+
+@pytest.mark.parametrize("N,M,T", [(10, 10, 37),   # B = 100: a partial second row block, T > pipeline chunk
+                                   (3, 3, 2)])     # B = 9, T = 2
+def test_f32_persistent_ragged_against_torch_gpu(N, M, T):
+    """The fp32 persistent recurrences (forced: schedule 'persist') at ragged batch sizes: one
+    fused trainer step against the stock-PyTorch port on the same GPU (loss, parameters)."""
+    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+    dims = (40, 768, 3, 256)
+    sd = recipe.make_weights(N * 13 + T, *dims, scale=3.0)
+    xh = recipe.make_frames(N + 7 * T, N * M, T, dims[0])
+    net, ge = _build(dims, sd)
+    net.schedule = "persist"
+    tr = GE2ETrainer(net, ge, lr=0.01)
+    loss = float(tr.step(torch.tensor(xh, device=DEV), N, M))
+    tr.check()
+    port = torch_port.SpeechEmbedderPort(*dims)
+    torch_port.load_recipe_weights(port, sd)
+    port = port.to(DEV)
+    w = torch.nn.Parameter(torch.tensor(10.0, device=DEV))
+    b = torch.nn.Parameter(torch.tensor(-5.0, device=DEV))
+    opt = torch.optim.SGD([{"params": port.parameters()}, {"params": [w, b]}], lr=0.01)
+    ref = float(torch_port.train_step(port, w, b, opt, torch.tensor(xh, device=DEV), N, M))
+    _check(f"f32_persist_B{N * M}_T{T}.loss_rel_vs_miopen", abs(loss - ref) / abs(ref), 1e-5)
+    got = {k: v.detach() for k, v in net.state_dict().items()}
+    d = max(float((got[k] - v.detach()).abs().max()) for k, v in port.state_dict().items())
+    _check(f"f32_persist_B{N * M}_T{T}.param_abs_vs_miopen", d, 1e-6)

@@ -34,7 +34,7 @@ from pytorch_speaker_verification_amd import PersistentRecurrenceError
 from pytorch_speaker_verification_amd.speech_embedder_net import GE2ELoss, SpeechEmbedder
 from pytorch_speaker_verification_amd.trainer import GE2ETrainer
 
-def make(dims):
+def make(dims, precision="bf16"):
     with model_dims(*dims):
         net = SpeechEmbedder()
     sd = recipe.make_weights(7, *dims, scale=3.0)
@@ -42,7 +42,7 @@ def make(dims):
         for k, v in net.state_dict().items():
             v.copy_(torch.as_tensor(sd[k]))
     net = net.to("cuda:0")
-    net.precision = "bf16"
+    net.precision = precision
     net.schedule = "persist"   # the persistent recurrences at these small dims
     return net
 
@@ -70,8 +70,10 @@ def faulty_step(tr, x, N, M, mode):
 '''
 
 SINGLE = COMMON + r'''
-dims, N, M, T = (40, 96, 2, 32), 4, 5, 6
-net = make(dims)
+prec = sys.argv[2]
+# the fp32 persistent recurrences exist at H = 768 only
+dims, N, M, T = ((40, 96, 2, 32) if prec == "bf16" else (40, 768, 2, 64)), 4, 5, 6
+net = make(dims, prec)
 tr = GE2ETrainer(net, GE2ELoss("cuda:0"), lr=0.01)
 x = torch.tensor(recipe.make_frames(11, N * M, T, dims[0]), device="cuda:0")
 print("RESULT", *faulty_step(tr, x, N, M, int(sys.argv[1])))
@@ -108,19 +110,21 @@ def _script(body):
     return f"ROOT = {ROOT!r}\nHERE = {HERE!r}\n" + body
 
 
+@pytest.mark.parametrize("precision", ["bf16", "f32"])
 @pytest.mark.parametrize("fault,bit", [(1, 1), (2, 2)])
-def test_persistent_timeout_is_reported_and_step_skipped(fault, bit):
-    r = subprocess.run([sys.executable, "-c", _script(SINGLE), str(fault)], env=_env(), capture_output=True, text=True,
-                       timeout=300)
+def test_persistent_timeout_is_reported_and_step_skipped(fault, bit, precision):
+    r = subprocess.run([sys.executable, "-c", _script(SINGLE), str(fault), precision], env=_env(), capture_output=True,
+                       text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     status, nan_loss, unchanged, raised, recovered = _parse(r.stdout)
     assert int(status) == bit   # the first launch that timed out; later waits drained at once
     assert nan_loss == "True" and unchanged == "True" and raised == "True" and recovered == "True"
 
 
-def test_no_fault_no_status():
-    r = subprocess.run([sys.executable, "-c", _script(SINGLE), "0"], env=_env(), capture_output=True, text=True,
-                       timeout=300)
+@pytest.mark.parametrize("precision", ["bf16", "f32"])
+def test_no_fault_no_status(precision):
+    r = subprocess.run([sys.executable, "-c", _script(SINGLE), "0", precision], env=_env(), capture_output=True,
+                       text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     status, nan_loss, unchanged, raised, recovered = _parse(r.stdout)
     assert status == "0" and nan_loss == "False" and unchanged == "False" and raised == "False"
