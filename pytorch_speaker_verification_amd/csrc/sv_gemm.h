@@ -155,6 +155,21 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
 }
 
+// Column-grouped tile order for the one-shot (no split-K) GEMM tiles: position id (after
+// xcd_remap, so each XCD owns a contiguous run of positions) walks the tile grid column group by
+// column group -- G column tiles (the largest divisor of tiles_n <= gmax), every row, then the next
+// group.  An XCD's concurrent tiles then share G panels of B (resident in its L2 for the whole
+// run) and each row panel of A is fetched once per group instead of the B panels once per few
+// rows: at the K1 shape (12 column tiles) B panels were re-fetched by every XCD for every 32 tiles.
+__device__ __forceinline__ void grouped_tile(int id, int tiles_m, int tiles_n, int gmax, int& tm, int& tn) {
+  int G = gmax < tiles_n ? gmax : tiles_n;
+  while (tiles_n % G) --G;
+  const int per = tiles_m * G;
+  const int cg = id / per, rem = id - cg * per;
+  tm = rem / G;
+  tn = cg * G + rem % G;
+}
+
 // XCD-aware 2-D tile map for the per-step kernels (grid nbx unit-blocks x nby row-blocks):
 // the dispatcher deals linear block L to XCD L % 8; give each XCD a compact rectangle of
 // (nby/2) x (nbx/4) tiles so the operand panels it reads (row-blocks of the left operand,

@@ -530,6 +530,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qp_kernel(const bf16_t* __r
   if (v >= nwg) return;
   int base = 0;
   auto tile_of = [&](int vv, int& tm_, int& tn_) {
+    // (row-major tile order: the column-grouped order of the fp32 kernel measured slower here,
+    // K1 bf16 out 547 -> 574 us, fp32 out 658 -> 753 us)
     const int id = xcd_remap(vv, nwg);
     tn_ = id % tiles_n;
     tm_ = id / tiles_n;

@@ -68,7 +68,10 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
   const int tiles_n = N / BN;
   const int nwg = tiles_n * (M / GF_BM);
   const int id = xcd_remap(blockIdx.x, nwg);
-  const int tn = id % tiles_n, tm = id / tiles_n;
+  int tn = id % tiles_n, tm = id / tiles_n;
+  // one-shot launches: column-grouped tile order (4 fp32 B panels of 256 x 768 = 3.1 MB per XCD L2
+  // at the K1 shape); split-K launches keep the plain order
+  if (gridDim.y == 1) grouped_tile(id, M / GF_BM, tiles_n, 4, tm, tn);
   const int kbeg = blockIdx.y * kchunk;
   const int nk = (min(K, kbeg + kchunk) - kbeg) / GF_BK;
   const int wr = w >> 2, wc = w & 3;

@@ -167,6 +167,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
         else
           pf_vmwait<0>();
         __builtin_amdgcn_s_barrier();  // ... every wave's part; slot (ch + 2) % 4 was last read at ch - 2
+        asm volatile("" ::: "memory");  // (the barrier intrinsic is no memory op: keep the LDS reads behind it)
         __builtin_amdgcn_sched_barrier(0);
         const char* cbase = ring + (ch % PF_NB) * PF_CH;
         const char* a0p = cbase + r * 256;
@@ -301,13 +302,15 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_kernel(
   constexpr int LDT = PF_BM + 4;     // gts [128][LDT] transposed dG tile (aliases red)
   constexpr int FBLK = NKG * 256;    // floats of one (gate, row half) fragment run
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // the operand images (ea, ec, eu) and the partials (red) are read into registers at the start
+  // of the epilogue; behind a barrier the dG tiles take their place (dgs over ea + ec, gts over red)
   float* ea = reinterpret_cast<float*>(smem);  // [64][128] activations of step t (LDS-DMA image)
   float* ec = ea + PF_BM * 4 * PF_U;           // [64][32] c_{t-1}
   float* eu = ec + PF_BM * PF_U;               // [64][32] dh_up of step t
   float* red = eu + PF_BM * PF_U;              // [4][64][LDR]
-  float* gts = red;                            // [128][LDT], written once red has been read
-  float* dgs = red + 4 * PF_BM * LDR;          // [64][LDG]
-  char* wl = reinterpret_cast<char*>(dgs + PF_BM * LDG);  // [4 waves][NL][64 lanes][16 B]
+  float* gts = red;                            // [128][LDT]
+  float* dgs = ea;                             // [64][LDG]
+  char* wl = reinterpret_cast<char*>(red + 4 * PF_BM * LDR);  // [4 waves][NL][64 lanes][16 B]
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   int ub, rb;
@@ -417,8 +420,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_kernel(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
     __syncthreads();
-    // dh = the partials in gate order + dh_up (K3's order); then red is free for the dG^T tile
-    f32x4 dh[2];
+    // dh = the partials in gate order + dh_up (K3's order), the step's operands: all into
+    // registers, then the images and red are free for the dG tiles
+    f32x4 dh[2], cpv[2], a[2][4];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int row = 2 * rp + k;
@@ -427,28 +431,29 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_kernel(
       dh[k] += *reinterpret_cast<const f32x4*>(red + (2 * PF_BM + row) * LDR + 4 * quad);
       dh[k] += *reinterpret_cast<const f32x4*>(red + (3 * PF_BM + row) * LDR + 4 * quad);
       dh[k] += *reinterpret_cast<const f32x4*>(eu + row * PF_U + 4 * quad);
+      cpv[k] = *reinterpret_cast<const f32x4*>(ec + row * PF_U + 4 * quad);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        a[k][q] = *reinterpret_cast<const f32x4*>(ea + row * (4 * PF_U) + q * PF_U + 4 * quad);
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int row = 2 * rp + k;
-      const f32x4 cpv = *reinterpret_cast<const f32x4*>(ec + row * PF_U + 4 * quad);
-      f32x4 a[4], dq[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a[q] = *reinterpret_cast<const f32x4*>(ea + row * (4 * PF_U) + q * PF_U + 4 * quad);
+      f32x4 dq[4];
 #pragma unroll
       for (int v = 0; v < 4; ++v) {  // the per-step kernel's cell backward (lstm_step_bwd_v2_kernel)
         const float d = dh[k][v];
-        const float i_ = a[0][v], f_ = a[1][v], g_ = a[2][v], o_ = a[3][v];
+        const float i_ = a[k][0][v], f_ = a[k][1][v], g_ = a[k][2][v], o_ = a[k][3][v];
         const float tc = tanhf(cv[k][v]);
         const float dc = d * o_ * (1.f - tc * tc) + dcf[k][v];
         dq[0][v] = dc * g_ * i_ * (1.f - i_);
-        dq[1][v] = dc * cpv[v] * f_ * (1.f - f_);
+        dq[1][v] = dc * cpv[k][v] * f_ * (1.f - f_);
         dq[2][v] = dc * i_ * (1.f - g_ * g_);
         dq[3][v] = d * tc * o_ * (1.f - o_);
         dcf[k][v] = dc * f_;
       }
-      cv[k] = cpv;  // c_{t-1} is the next step's c_t
+      cv[k] = cpv[k];  // c_{t-1} is the next step's c_t
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         *reinterpret_cast<f32x4*>(dgs + row * LDG + q * PF_U + 4 * quad) = dq[q];
@@ -497,7 +502,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_kernel(
       }
     }
     if (t > 0) {
-      __syncthreads();  // ea / ec / eu read by every wave before the next step's operands land there
+      __syncthreads();  // dgs (over ea / ec) and gts read by every wave before the next operands land
       load_ew(t - 1);   // in flight during the next hand-off wait
     }
   }
@@ -508,16 +513,27 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_kernel(
 // ============================================================================
 namespace {
 // weight k-groups (of 96 at H = 768) in VGPRs / LDS beside the 64 in AGPRs
-constexpr int PF_FWD_NV = 16, PF_FWD_NL = 16, PF_BWD_NV = 22, PF_BWD_NL = 10, PF_BWD_P = 3;
+#ifndef SV_PF32_BWD_NL
+#define SV_PF32_BWD_NL 18
+#endif
+#ifndef SV_PF32_BWD_P
+#define SV_PF32_BWD_P 7
+#endif
+// backward: dG_{t+1} A fragments P k-groups ahead (Little's law: ~10 KB in flight per wave to
+// stream 196 KB per wave per step from L2 / the fabric); the registers for them come from NL
+// weight k-groups held in LDS
+constexpr int PF_FWD_NV = 16, PF_FWD_NL = 16, PF_BWD_NL = SV_PF32_BWD_NL, PF_BWD_NV = 96 - PF_NA - PF_BWD_NL,
+              PF_BWD_P = SV_PF32_BWD_P;
 constexpr size_t pf_fwd_lds() {
   return (size_t)PF_NB * PF_CH + (size_t)PF_BM * 4 * PF_U * 4 + (size_t)4 * PF_FWD_NL * 1024;
 }
 constexpr size_t pf_bwd_lds() {
   return (size_t)PF_BM * 4 * PF_U * 4 + 2 * (size_t)PF_BM * PF_U * 4 + (size_t)4 * PF_BM * (PF_U + 4) * 4 +
-         (size_t)PF_BM * (4 * PF_U + 4) * 4 + (size_t)4 * PF_BWD_NL * 1024;
+         (size_t)4 * PF_BWD_NL * 1024;
 }
 static_assert(pf_fwd_lds() <= 160 * 1024 && pf_bwd_lds() <= 160 * 1024, "LDS");
 static_assert((size_t)4 * PF_U * (PF_BM + 4) <= (size_t)4 * PF_BM * (PF_U + 4), "gts fits in red");
+static_assert((size_t)PF_BM * (4 * PF_U + 4) <= (size_t)PF_BM * 5 * PF_U, "dgs fits in ea + ec");
 }  // namespace
 
 // the fp32 persistent recurrences fit: H = 768, (H / 32) x ceil(B / 64) workgroups co-resident

@@ -1,0 +1,80 @@
+"""A/B of the fp32 stack at c2 (B = 640, T = 160): forward and backward under the persistent
+recurrences vs the layer-pipelined per-step kernels, HIP events on the stream, plus the per-layer
+persistent launch times from the probes, and a full trainer step under each schedule.
+Usage: python scripts/f32_step_ab.py [--iters 3] [--B 640] [--T 160]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if "--lib" in sys.argv:  # an A/B build (Makefile `ab`) instead of the product library
+    from pytorch_speaker_verification_amd import _lib  # noqa: E402
+    _lib.use_library(sys.argv[sys.argv.index("--lib") + 1])
+from pytorch_speaker_verification_amd import ops  # noqa: E402
+from pytorch_speaker_verification_amd._lib import PersistStatus  # noqa: E402
+from pytorch_speaker_verification_amd.speech_embedder_net import GE2ELoss, SpeechEmbedder  # noqa: E402
+from pytorch_speaker_verification_amd.trainer import GE2ETrainer  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--iters", type=int, default=3)
+ap.add_argument("--B", type=int, default=640)
+ap.add_argument("--T", type=int, default=160)
+ap.add_argument("--lib", default=None)
+ap.add_argument("--only", default=None, help="one schedule only")
+args = ap.parse_args()
+dev = torch.device("cuda", 0)
+torch.manual_seed(0)
+net = SpeechEmbedder().to(dev)
+x = torch.randn(args.B, args.T, 40, device=dev)
+layers = net.LSTM_stack.layer_params()
+wp, bp = net.projection.weight, net.projection.bias
+L = len(layers)
+
+
+def ev(n):
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
+    for q in e:
+        q.record()
+    return e
+
+
+def timed(f):
+    for _ in range(1):
+        f()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.iters):
+        f()
+    e1.record()
+    e1.synchronize()
+    return round(e0.elapsed_time(e1) / args.iters, 3)
+
+
+out = {"B": args.B, "T": args.T, "lib": args.lib or "libsv_ge2e.so"}
+for sched in ((args.only,) if args.only else ("auto", "per_step")):
+    ps = PersistStatus(dev)
+    # (probe arrays: 2 L events under the persistent schedule; the per-step one takes 2 L nch)
+    pers = sched != "per_step"
+    pf, pb = (ev(2 * L), ev(2 * L)) if pers else (None, None)
+    emb, st = ops.embedder_forward(x, layers, wp, bp, status=ps, schedule=sched, probe=pf)
+    demb = torch.randn_like(emb) * 0.1
+    ops.embedder_backward(st, demb, layers, wp, status=ps, schedule=sched, probe=pb)
+    torch.cuda.synchronize()
+    o = {"fwd_ms": timed(lambda: ops.embedder_forward(x, layers, wp, bp, status=ps, schedule=sched)),
+         "bwd_ms": timed(lambda: ops.embedder_backward(st, demb, layers, wp, status=ps, schedule=sched))}
+    if pers:
+        o["fwd_layer_us"] = [round(pf[2 * l].elapsed_time(pf[2 * l + 1]) * 1e3, 1) for l in range(L)]
+        o["bwd_layer_us"] = [round(pb[2 * l].elapsed_time(pb[2 * l + 1]) * 1e3, 1) for l in range(L)]
+    net.schedule = sched
+    tr = GE2ETrainer(net, GE2ELoss(dev), lr=0.01)
+    N = args.B // 10
+    o["step_ms"] = timed(lambda: tr.step(x, N, 10))
+    tr.check()
+    o["status"] = int(ps.block[0])
+    out[sched] = o
+    print(json.dumps({sched: o}), flush=True)
+print(json.dumps(out), flush=True)
