@@ -581,9 +581,9 @@ def main():
     if f32_persist:
         fl = 2.0 * B * T * H * 4 * H
         out["roofline"] = roofline_entry(
-            "lstm_persist_bwd_f32_kernel (persistent fp32 backward recurrence, one launch per layer, W_hh in "
+            "lstm_persist_bwd_f32_h2_kernel (persistent fp32 backward recurrence, one launch per layer, two 32-row chains, W_hh in "
             "registers, fp32 MFMA 32x32x2)", fl, probe_ms(probes, "bwd") / L, MI355X_FP32_MFMA_TFLOPS,
-            pmc_traffic("lstm_persist_bwd_f32_kernel"), L * args.steps,
+            pmc_traffic("lstm_persist_bwd_f32_h2_kernel"), L * args.steps,
             "in-step: HIP events around each layer's launch inside the timed steps (on its stream, main)")
         out["roofline_fwd"] = roofline_entry(
             "lstm_persist_fwd_f32_kernel (persistent fp32 forward recurrence)", fl, probe_ms(probes, "fwd") / L,

@@ -17,9 +17,10 @@
 // chunk.  The x-projection of step t (K1 output incl. biases, in `gates`) arrives by the same DMA.
 // Hand-off: h_t through h_tm[t + 1] (16-B sc1 stores, vmcnt(0), one arrival per workgroup on the row
 // block's counter; MI355X_MICROARCH.md hand-off table row 1), read back with sc1 DMA.
-// Backward: dh_rec = dG_{t+1} W_hh: wave g streams gate g's K = H slice of dG_{t+1} (64 rows) from a
-// fragment-order hand-off buffer straight into registers (1 KB per load instruction), P k-groups
-// ahead; the per-gate partials meet in LDS and are summed in gate order (K3's order).
+// Backward: dh_rec = dG_{t+1} W_hh: wave g streams gate g's K = H slice of dG_{t+1} from a
+// fragment-order hand-off buffer straight into registers (1 KB per load instruction), 12 k-groups
+// ahead, as two 32-row half chains (below); the per-gate partials meet in LDS and are summed in
+// gate order (K3's order).
 // Outputs are the per-step kernels' buffers (activations, c, h, h^T / dG, dG^T), so either direction
 // composes with the other schedule; results agree with the per-step kernels to fp32 rounding.
 #include "sv_persist_dev.h"
@@ -286,41 +287,45 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
 }
 
 // ============================================================================
-// backward
+// backward, half-step form: the two 32-row halves of a workgroup's row block run as two
+// independent recurrence chains, each with its own arrival counter ((row block, half) pair).  A
+// workgroup does half 0's step t, then half 1's: while it runs half 1's k-loop, half 0's hand-off
+// reaches the other workgroups, so one chain's epilogue + hand-off latency hides behind the other
+// chain's MFMAs (c2: 4.89 -> 4.79 ms per layer; the same form of the forward measured slower,
+// 4.33 -> 4.46 ms, so the forward keeps the 64-row tile).  Its smaller tiles leave LDS for 24
+// weight k-groups, so the A fragments (the half's dG_{t+1}, from the fragment-order hand-off) can
+// run 12 k-groups ahead.  Each half's k-group products are summed in two accumulators (c even /
+// odd), added at the end; per half the partials meet in LDS and are summed in gate order.
 // ============================================================================
-// fragment-order hand-off of dG (fp32): [t][row block][gate q][row half][k-group][64 lanes][4];
-// lane (r, h) of block (q, rh, kg) holds dG[32 rh + r][q H + 8 kg + 4 h .. + 3]
+constexpr int PH_BM = 32;                      // rows of a half
+
 template <int NKG, int P, int NV, int NL>
-__global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_kernel(
+__global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
     const float* __restrict__ whhT, const float* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, float* __restrict__ dg, float* __restrict__ dgT, long lddgT,
     float* dgf, int T, int Bp, int B, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit, int fault) {
   constexpr int H = 8 * NKG;
   static_assert(PF_NA + NV + NL == NKG, "weight split");
-  constexpr int LDR = PF_U + 4;      // red [4][64][LDR]
-  constexpr int LDG = 4 * PF_U + 4;  // dgs [64][LDG] row-major dG tile
-  constexpr int LDT = PF_BM + 4;     // gts [128][LDT] transposed dG tile (aliases red)
-  constexpr int FBLK = NKG * 256;    // floats of one (gate, row half) fragment run
+  constexpr int LDR = PF_U + 4;      // red [4][32][LDR]
+  constexpr int LDG = 4 * PF_U + 4;  // dgs [32][LDG] (over ea + ec)
+  constexpr int LDT = PH_BM + 4;     // gts [128][LDT] (over red)
+  constexpr int FBLK = NKG * 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // the operand images (ea, ec, eu) and the partials (red) are read into registers at the start
-  // of the epilogue; behind a barrier the dG tiles take their place (dgs over ea + ec, gts over red)
-  float* ea = reinterpret_cast<float*>(smem);  // [64][128] activations of step t (LDS-DMA image)
-  float* ec = ea + PF_BM * 4 * PF_U;           // [64][32] c_{t-1}
-  float* eu = ec + PF_BM * PF_U;               // [64][32] dh_up of step t
-  float* red = eu + PF_BM * PF_U;              // [4][64][LDR]
-  float* gts = red;                            // [128][LDT]
-  float* dgs = ea;                             // [64][LDG]
-  char* wl = reinterpret_cast<char*>(red + 4 * PF_BM * LDR);  // [4 waves][NL][64 lanes][16 B]
+  float* ea = reinterpret_cast<float*>(smem);  // [32][128] activations of the half-step
+  float* ec = ea + PH_BM * 4 * PF_U;           // [32][32] c_{t-1}
+  float* eu = ec + PH_BM * PF_U;               // [32][32] dh_up
+  float* red = eu + PH_BM * PF_U;              // [4][32][LDR]
+  float* gts = red;
+  float* dgs = ea;
+  char* wl = reinterpret_cast<char*>(red + 4 * PH_BM * LDR);
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   int ub, rb;
   persist_tile(xcd, nub, ub, rb);
-  const int j0 = ub * PF_U, b0 = rb * PF_BM;
+  const int j0 = ub * PF_U;
   const int nrb = gridDim.x / nub;
   const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
-  const long FS = (long)nrb * 4 * 2 * FBLK;  // floats of one step's hand-off slot
-  unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
-  // W_hh^T of gate g, units j0 + r: lane (r, hh) of k-group kg holds W_hh[g H + 8 kg + 4 hh .. + 3][j0 + r]
+  const long FS = (long)nrb * 4 * 2 * FBLK;
   float wa[4 * PF_NA], wv[4 * NV];
   {
     const float* wr = whhT + (long)(j0 + r) * G + (long)g * H + 4 * hh;
@@ -337,173 +342,149 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_kernel(
     }
     return *reinterpret_cast<const f32x4*>(wl + ((g * NL + (kg - PF_NA - NV)) * 64 + lane) * 16);
   };
-  const int quad = tid & 7, rp = tid >> 3;
-  // step tt's elementwise operands -> LDS (global_load_lds; rows past B read row B - 1).  Wave g:
-  // 8 activation pieces (rows 16 g ..), 2 of c_{t-1}, 2 of dh_up; an absent operand (c_{-1}, dh_up
-  // of a step without one) is written as zeros into the same lanes' slots instead.
-  auto load_ew = [&](int tt) {
-    int z = 0;  // opaque zero: the address arithmetic stays here (see the forward)
+  const int quad = tid & 7, erow = tid >> 3;
+  // half-step (tt, hf)'s operands -> LDS: wave g: 4 activation pieces (rows 8 g ..), 1 of c_{t-1}, 1
+  // of dh_up; absent operands written as zeros into the same slots
+  auto load_ew = [&](int tt, int hf) {
+    int z = 0;
     asm volatile("" : "+v"(z));
-    const int gz = g + z;
+    const int gz = g + z, b0 = rb * PF_BM + hf * PH_BM;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int q = (8 * gz + j) * 64 + lane, row = q >> 5, s = q & 31;
+    for (int j = 0; j < 4; ++j) {
+      const int q = (4 * gz + j) * 64 + lane, row = q >> 5, s = q & 31;
       const float* src = acts + (long)tt * BG + (long)min(b0 + row, B - 1) * G + (s >> 3) * H + j0 + 4 * (s & 7);
-      __builtin_amdgcn_global_load_lds((pf_glb_t)src, (pf_lds_t)(ea + (8 * g + j) * 256), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((pf_glb_t)src, (pf_lds_t)(ea + (4 * g + j) * 256), 16, 0, 0);
     }
     const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
+    const int q = gz * 64 + lane, row = q >> 3, c = q & 7;
+    const long off = (long)min(b0 + row, B - 1) * H + j0 + 4 * c;
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int q = (2 * gz + j) * 64 + lane, row = q >> 3, c = q & 7;
-      const long off = (long)min(b0 + row, B - 1) * H + j0 + 4 * c;
-      if (tt > 0)
-        __builtin_amdgcn_global_load_lds((pf_glb_t)(c_tm + (long)(tt - 1) * BH + off),
-                                         (pf_lds_t)(ec + (2 * g + j) * 256), 16, 0, 0);
-      else
-        *reinterpret_cast<f32x4*>(ec + 4 * q) = zero;
-      if (up)
-        __builtin_amdgcn_global_load_lds((pf_glb_t)(up + off), (pf_lds_t)(eu + (2 * g + j) * 256), 16, 0, 0);
-      else
-        *reinterpret_cast<f32x4*>(eu + 4 * q) = zero;
-    }
+    if (tt > 0)
+      __builtin_amdgcn_global_load_lds((pf_glb_t)(c_tm + (long)(tt - 1) * BH + off), (pf_lds_t)(ec + g * 256), 16, 0,
+                                       0);
+    else
+      *reinterpret_cast<f32x4*>(ec + 4 * q) = zero;
+    if (up)
+      __builtin_amdgcn_global_load_lds((pf_glb_t)(up + off), (pf_lds_t)(eu + g * 256), 16, 0, 0);
+    else
+      *reinterpret_cast<f32x4*>(eu + 4 * q) = zero;
   };
-  // c_{T-1} of the thread's cells; the cell-gradient carry
   f32x4 cv[2], dcf[2];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int gb = min(b0 + 2 * rp + k, B - 1);
-    cv[k] = *reinterpret_cast<const f32x4*>(c_tm + (long)(T - 1) * BH + (long)gb * H + j0 + 4 * quad);
-    dcf[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int hf = 0; hf < 2; ++hf) {
+    const int gb = min(rb * PF_BM + hf * PH_BM + erow, B - 1);
+    cv[hf] = *reinterpret_cast<const f32x4*>(c_tm + (long)(T - 1) * BH + (long)gb * H + j0 + 4 * quad);
+    dcf[hf] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  load_ew(T - 1);
+  load_ew(T - 1, 0);
   for (int t = T - 1; t >= 0; --t) {
-    f32x16 acc0, acc1;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
-    if (t < T - 1) {
-      if (tid == 0) persist_wait(my_cnt, (unsigned)nub * (unsigned)(T - 1 - t), status, limit, 2u);
-      __syncthreads();
-      const __amdgpu_buffer_rsrc_t ra = sv_rsrc(dgf + (long)(t + 1) * FS, (unsigned)(FS * 4));
-      const unsigned base = ((unsigned)((rb * 4 + g) * 2) * (unsigned)FBLK + (unsigned)lane * 4u) * 4u;
-      constexpr unsigned HALF = FBLK * 4u;  // bytes from row half 0 to row half 1
-      u32x4_t f0[P], f1[P];
+    for (int hf = 0; hf < 2; ++hf) {
+      const int b0 = rb * PF_BM + hf * PH_BM;
+      unsigned* my_cnt = cnt + (rb * 2 + hf) * SV_PCNT_STRIDE;
+      f32x16 acc0, acc1;
 #pragma unroll
-      for (int p = 0; p < P; ++p) {
-        f0[p] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + 1024u * p, 0, 16 /* sc1 */);
-        f1[p] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + HALF + 1024u * p, 0, 16 /* sc1 */);
-      }
-      f32x4 w = wfrag(0);
-      __builtin_amdgcn_sched_barrier(0);
+      for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+      if (t < T - 1) {
+        if (tid == 0) persist_wait(my_cnt, (unsigned)nub * (unsigned)(T - 1 - t), status, limit, 2u);
+        __syncthreads();
+        const __amdgpu_buffer_rsrc_t ra = sv_rsrc(dgf + (long)(t + 1) * FS, (unsigned)(FS * 4));
+        const unsigned base = ((unsigned)(((rb * 4 + g) * 2 + hf) * FBLK) + (unsigned)lane * 4u) * 4u;
+        u32x4_t fa[P];
 #pragma unroll
-      for (int kg = 0; kg < NKG; ++kg) {
-        const f32x4 a0 = __builtin_bit_cast(f32x4, f0[kg % P]), a1 = __builtin_bit_cast(f32x4, f1[kg % P]);
-        const f32x4 nw = kg + 1 < NKG ? wfrag(kg + 1) : w;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[c], w[c], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[c], w[c], acc1, 0, 0, 0);
-        }
-        if (kg + P < NKG) {
-          f0[kg % P] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + 1024u * (kg + P), 0, 16);
-          f1[kg % P] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + HALF + 1024u * (kg + P), 0, 16);
-        }
-        w = nw;
+        for (int p = 0; p < P; ++p) fa[p] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + 1024u * p, 0, 16 /* sc1 */);
+        f32x4 w = wfrag(0);
         __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kg = 0; kg < NKG; ++kg) {
+          const f32x4 a = __builtin_bit_cast(f32x4, fa[kg % P]);
+          const f32x4 nw = kg + 1 < NKG ? wfrag(kg + 1) : w;
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0], w[0], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1], w[1], acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2], w[2], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[3], w[3], acc1, 0, 0, 0);
+          if (kg + P < NKG) fa[kg % P] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + 1024u * (kg + P), 0, 16);
+          w = nw;
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
-    }
-    // per-gate partials -> red[g][row][unit]
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      red[(g * PF_BM + acc_row(i, lane)) * LDR + r] = acc0[i];
-      red[(g * PF_BM + 32 + acc_row(i, lane)) * LDR + r] = acc1[i];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
-    __syncthreads();
-    // dh = the partials in gate order + dh_up (K3's order), the step's operands: all into
-    // registers, then the images and red are free for the dG tiles
-    f32x4 dh[2], cpv[2], a[2][4];
+      for (int i = 0; i < 16; ++i) red[(g * PH_BM + acc_row(i, lane)) * LDR + r] = acc0[i] + acc1[i];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
+      __syncthreads();
+      f32x4 dh, cpv, a4[4];
+      dh = *reinterpret_cast<const f32x4*>(red + (0 * PH_BM + erow) * LDR + 4 * quad);
+      dh += *reinterpret_cast<const f32x4*>(red + (1 * PH_BM + erow) * LDR + 4 * quad);
+      dh += *reinterpret_cast<const f32x4*>(red + (2 * PH_BM + erow) * LDR + 4 * quad);
+      dh += *reinterpret_cast<const f32x4*>(red + (3 * PH_BM + erow) * LDR + 4 * quad);
+      dh += *reinterpret_cast<const f32x4*>(eu + erow * PF_U + 4 * quad);
+      cpv = *reinterpret_cast<const f32x4*>(ec + erow * PF_U + 4 * quad);
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int row = 2 * rp + k;
-      dh[k] = *reinterpret_cast<const f32x4*>(red + (0 * PF_BM + row) * LDR + 4 * quad);
-      dh[k] += *reinterpret_cast<const f32x4*>(red + (1 * PF_BM + row) * LDR + 4 * quad);
-      dh[k] += *reinterpret_cast<const f32x4*>(red + (2 * PF_BM + row) * LDR + 4 * quad);
-      dh[k] += *reinterpret_cast<const f32x4*>(red + (3 * PF_BM + row) * LDR + 4 * quad);
-      dh[k] += *reinterpret_cast<const f32x4*>(eu + row * PF_U + 4 * quad);
-      cpv[k] = *reinterpret_cast<const f32x4*>(ec + row * PF_U + 4 * quad);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        a[k][q] = *reinterpret_cast<const f32x4*>(ea + row * (4 * PF_U) + q * PF_U + 4 * quad);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int row = 2 * rp + k;
+      for (int q = 0; q < 4; ++q) a4[q] = *reinterpret_cast<const f32x4*>(ea + erow * (4 * PF_U) + q * PF_U + 4 * quad);
+      __syncthreads();  // the images and red are free: the dG tiles take their place
       f32x4 dq[4];
 #pragma unroll
       for (int v = 0; v < 4; ++v) {  // the per-step kernel's cell backward (lstm_step_bwd_v2_kernel)
-        const float d = dh[k][v];
-        const float i_ = a[k][0][v], f_ = a[k][1][v], g_ = a[k][2][v], o_ = a[k][3][v];
-        const float tc = tanhf(cv[k][v]);
-        const float dc = d * o_ * (1.f - tc * tc) + dcf[k][v];
+        const float d = dh[v];
+        const float i_ = a4[0][v], f_ = a4[1][v], g_ = a4[2][v], o_ = a4[3][v];
+        const float tc = tanhf(cv[hf][v]);
+        const float dc = d * o_ * (1.f - tc * tc) + dcf[hf][v];
         dq[0][v] = dc * g_ * i_ * (1.f - i_);
-        dq[1][v] = dc * cpv[k][v] * f_ * (1.f - f_);
+        dq[1][v] = dc * cpv[v] * f_ * (1.f - f_);
         dq[2][v] = dc * i_ * (1.f - g_ * g_);
         dq[3][v] = d * tc * o_ * (1.f - o_);
-        dcf[k][v] = dc * f_;
+        dcf[hf][v] = dc * f_;
       }
-      cv[k] = cpv[k];  // c_{t-1} is the next step's c_t
+      cv[hf] = cpv;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        *reinterpret_cast<f32x4*>(dgs + row * LDG + q * PF_U + 4 * quad) = dq[q];
+        *reinterpret_cast<f32x4*>(dgs + erow * LDG + q * PF_U + 4 * quad) = dq[q];
 #pragma unroll
-        for (int v = 0; v < 4; ++v) gts[(q * PF_U + 4 * quad + v) * LDT + row] = dq[q][v];
+        for (int v = 0; v < 4; ++v) gts[(q * PF_U + 4 * quad + v) * LDT + erow] = dq[q][v];
       }
-    }
-    __syncthreads();
-    // the hand-off: 32 fragment blocks of 1 KB (gate q, row half rh, k-group 4 ub + kl), sc1 stores
-    if (t > 0) {
-      const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 4));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int p = tid + 256 * i, blk = p >> 6, L = p & 63;
-        const int q = blk >> 3, rh = (blk >> 2) & 1, kl = blk & 3;
-        const f32x4 v = *reinterpret_cast<const f32x4*>(dgs + (32 * rh + (L & 31)) * LDG + q * PF_U + 8 * kl + 4 * (L >> 5));
-        const unsigned off = ((unsigned)(((rb * 4 + q) * 2 + rh) * FBLK) + (unsigned)(4 * ub + kl) * 256u + (unsigned)L * 4u) * 4u;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rw, off, 0, 16 /* sc1 */);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
-        __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // off the chain: row-major dG (the dx GEMM's operand) and dG^T (the dW GEMMs' and bias sums')
+      if (t > 0) {  // the hand-off: 16 fragment blocks of 1 KB (gate q, this half, k-group 4 ub + kl)
+        const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 4));
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int row = 2 * rp + k;
-      const long gb = b0 + row;
+        for (int i = 0; i < 4; ++i) {
+          const int p = tid + 256 * i, blk = p >> 6, L = p & 63;
+          const int q = blk >> 2, kl = blk & 3;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(dgs + (L & 31) * LDG + q * PF_U + 8 * kl + 4 * (L >> 5));
+          const unsigned off =
+              ((unsigned)(((rb * 4 + q) * 2 + hf) * FBLK) + (unsigned)(4 * ub + kl) * 256u + (unsigned)L * 4u) * 4u;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rw, off, 0, 16 /* sc1 */);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
+          __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // off the chain: row-major dG and dG^T of the half-step
+      const long gb = b0 + erow;
       if (gb < B) {
         float* dp = dg + (long)t * BG + gb * G + j0 + 4 * quad;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          *reinterpret_cast<f32x4*>(dp + q * H) = *reinterpret_cast<const f32x4*>(dgs + row * LDG + q * PF_U + 4 * quad);
+          *reinterpret_cast<f32x4*>(dp + q * H) = *reinterpret_cast<const f32x4*>(dgs + erow * LDG + q * PF_U + 4 * quad);
       }
-    }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {  // 128 gate-unit rows x 16 pieces of 4 batch columns
-      const int p = tid + 256 * i, gu = p >> 4, c = p & 15, gb = b0 + 4 * c;
-      if (gb < Bp) {
-        f32x4 v = *reinterpret_cast<const f32x4*>(gts + gu * LDT + 4 * c);
+      for (int i = 0; i < 4; ++i) {  // 128 gate-unit rows x 8 pieces of 4 batch columns
+        const int p = tid + 256 * i, gu = p >> 3, c = p & 7, gbc = b0 + 4 * c;
+        if (gbc < Bp) {
+          f32x4 v = *reinterpret_cast<const f32x4*>(gts + gu * LDT + 4 * c);
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (gb + e >= B) v[e] = 0.f;
-        *reinterpret_cast<f32x4*>(dgT + ((long)(gu >> 5) * H + j0 + (gu & 31)) * lddgT + (long)t * Bp + gb) = v;
+          for (int e = 0; e < 4; ++e)
+            if (gbc + e >= B) v[e] = 0.f;
+          *reinterpret_cast<f32x4*>(dgT + ((long)(gu >> 5) * H + j0 + (gu & 31)) * lddgT + (long)t * Bp + gbc) = v;
+        }
       }
-    }
-    if (t > 0) {
-      __syncthreads();  // dgs (over ea / ec) and gts read by every wave before the next operands land
-      load_ew(t - 1);   // in flight during the next hand-off wait
+      if (hf == 0 || t > 0) {
+        __syncthreads();  // dgs / gts read by every wave before the next half-step's operands land
+        if (hf == 0)
+          load_ew(t, 1);
+        else
+          load_ew(t - 1, 0);
+      }
     }
   }
 }
@@ -513,33 +494,23 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_kernel(
 // ============================================================================
 namespace {
 // weight k-groups (of 96 at H = 768) in VGPRs / LDS beside the 64 in AGPRs
-#ifndef SV_PF32_BWD_NL
-#define SV_PF32_BWD_NL 18
-#endif
-#ifndef SV_PF32_BWD_P
-#define SV_PF32_BWD_P 7
-#endif
-// backward: dG_{t+1} A fragments P k-groups ahead (Little's law: ~10 KB in flight per wave to
-// stream 196 KB per wave per step from L2 / the fabric); the registers for them come from NL
-// weight k-groups held in LDS
-constexpr int PF_FWD_NV = 16, PF_FWD_NL = 16, PF_BWD_NL = SV_PF32_BWD_NL, PF_BWD_NV = 96 - PF_NA - PF_BWD_NL,
-              PF_BWD_P = SV_PF32_BWD_P;
+constexpr int PF_FWD_NV = 16, PF_FWD_NL = 16, PH_BWD_NL = 24, PH_BWD_NV = 96 - PF_NA - PH_BWD_NL, PH_BWD_P = 12;
 constexpr size_t pf_fwd_lds() {
   return (size_t)PF_NB * PF_CH + (size_t)PF_BM * 4 * PF_U * 4 + (size_t)4 * PF_FWD_NL * 1024;
 }
-constexpr size_t pf_bwd_lds() {
-  return (size_t)PF_BM * 4 * PF_U * 4 + 2 * (size_t)PF_BM * PF_U * 4 + (size_t)4 * PF_BM * (PF_U + 4) * 4 +
-         (size_t)4 * PF_BWD_NL * 1024;
+constexpr size_t ph_bwd_lds() {
+  return (size_t)PH_BM * 4 * PF_U * 4 + 2 * (size_t)PH_BM * PF_U * 4 + (size_t)4 * PH_BM * (PF_U + 4) * 4 +
+         (size_t)4 * PH_BWD_NL * 1024;
 }
-static_assert(pf_fwd_lds() <= 160 * 1024 && pf_bwd_lds() <= 160 * 1024, "LDS");
-static_assert((size_t)4 * PF_U * (PF_BM + 4) <= (size_t)4 * PF_BM * (PF_U + 4), "gts fits in red");
-static_assert((size_t)PF_BM * (4 * PF_U + 4) <= (size_t)PF_BM * 5 * PF_U, "dgs fits in ea + ec");
+static_assert(pf_fwd_lds() <= 160 * 1024 && ph_bwd_lds() <= 160 * 1024, "LDS");
+static_assert((size_t)4 * PF_U * (PH_BM + 4) <= (size_t)4 * PH_BM * (PF_U + 4), "gts fits in red");
+static_assert((size_t)PH_BM * (4 * PF_U + 4) <= (size_t)PH_BM * 5 * PF_U, "dgs fits in ea + ec");
 }  // namespace
 
 // the fp32 persistent recurrences fit: H = 768, (H / 32) x ceil(B / 64) workgroups co-resident
 int sv_persist_f32_fits(int B, int H, int cus) {
-  const long nrb = (B + PF_BM - 1) / PF_BM;
-  return H == 768 && B > 0 && nrb <= SV_PCNT_ROWS && (H / PF_U) * nrb <= cus && (long)B * 4 * H * 4 < (1L << 31);
+  const long nrb = (B + PF_BM - 1) / PF_BM;  // (two counters per row block: one per half)
+  return H == 768 && B > 0 && 2 * nrb <= SV_PCNT_ROWS && (H / PF_U) * nrb <= cus && (long)B * 4 * H * 4 < (1L << 31);
 }
 
 // bytes of the backward's fragment-order hand-off: T slots of ceil(B / 64) x 64 rows x 4H fp32
@@ -557,9 +528,9 @@ int sv_persist_fwd_f32(int T, int B, int H, const float* whh, float* gates, floa
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
-  hipLaunchKernelGGL((lstm_persist_fwd_f32_kernel<96, PF_FWD_NV, PF_FWD_NL>), dim3(nub * nrb), dim3(256), pf_fwd_lds(), stream, whh, gates,
-                     c_tm, h_tm, hT, (long)(T + 1) * Bp, T, Bp, B, cnt, nub, PF_XCD, sync, sv_persist_limit(),
-                     sv_persist_fault(0));
+  hipLaunchKernelGGL((lstm_persist_fwd_f32_kernel<96, PF_FWD_NV, PF_FWD_NL>), dim3(nub * nrb), dim3(256),
+                     pf_fwd_lds(), stream, whh, gates, c_tm, h_tm, hT, (long)(T + 1) * Bp, T, Bp, B, cnt, nub, PF_XCD,
+                     sync, sv_persist_limit(), sv_persist_fault(0));
   SV_LAUNCH_CHECK();
   if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
   return SV_OK;
@@ -573,12 +544,12 @@ int sv_persist_bwd_f32(int T, int B, int H, const float* whhT, const float* acts
   unsigned* cnt = sync + SV_SYNC_CNT;  // channel 0
   const int nub = H / PF_U, nrb = (B + PF_BM - 1) / PF_BM;
   const int Bp = (B + 3) & ~3;
-  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
+  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)2 * nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
-  hipLaunchKernelGGL((lstm_persist_bwd_f32_kernel<96, PF_BWD_P, PF_BWD_NV, PF_BWD_NL>), dim3(nub * nrb), dim3(256), pf_bwd_lds(), stream, whhT,
-                     acts, c_tm, dhup, up_full, dg, dgT, (long)T * Bp, dgf, T, Bp, B, cnt, nub, PF_XCD, sync,
-                     sv_persist_limit(), sv_persist_fault(1));
+  hipLaunchKernelGGL((lstm_persist_bwd_f32_h2_kernel<96, PH_BWD_P, PH_BWD_NV, PH_BWD_NL>), dim3(nub * nrb),
+                     dim3(256), ph_bwd_lds(), stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, (long)T * Bp, dgf, T,
+                     Bp, B, cnt, nub, PF_XCD, sync, sv_persist_limit(), sv_persist_fault(1));
   SV_LAUNCH_CHECK();
   if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
   return SV_OK;

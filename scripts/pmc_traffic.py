@@ -17,7 +17,7 @@ FAMILIES = {  # json key -> kernel-name prefix
     "lstm_persist2_fwd_bf16_kernel": "void lstm_persist2_fwd_bf16_kernel<48, 64, 0>",
     "lstm_persist3_bwd_bf16_kernel": "void lstm_persist3_bwd_bf16_kernel<",
     "lstm_persist3_fwd_bf16_kernel": "void lstm_persist3_fwd_bf16_kernel<",
-    "lstm_persist_bwd_f32_kernel": "void lstm_persist_bwd_f32_kernel<",
+    "lstm_persist_bwd_f32_h2_kernel": "void lstm_persist_bwd_f32_h2_kernel<",
     "lstm_persist_fwd_f32_kernel": "void lstm_persist_fwd_f32_kernel<",
     # in-step GEMMs, per shape (c2 fp32 / c3 bf16, B = 640, T = 160, H = 768): (prefix, grid threads)
     "gemm_f32_256_kernel<256,32,0>@K1.in_step": ("void gemm_f32_256_kernel<256, 32, 0>", 400 * 12 * 512),

@@ -43,10 +43,10 @@ with open(os.path.join(prof, f"{tag}_roofline_check.txt"), "w") as f:
     f.write("rocprofv3 kernel traces of `bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-vendor --no-bf16 "
             "--fwd-steps 1` (f32, c2) and `... --dtype bf16` (c3) against the bench line of the same tree\n")
     rf = pf["f32"]["roofline"]
-    if rf["kernel"].startswith("lstm_persist_bwd_f32_kernel"):
+    if rf["kernel"].startswith("lstm_persist_bwd_f32_h2_kernel"):
         # one launch per layer: the headline run's timed steps are its launches [L, 4 L)
-        d = durations("f32", "void lstm_persist_bwd_f32_kernel")
-        line(f, "roofline (c2 headline): lstm_persist_bwd_f32_kernel, the 3 timed steps' launches", d[3:12],
+        d = durations("f32", "void lstm_persist_bwd_f32_h2_kernel")
+        line(f, "roofline (c2 headline): lstm_persist_bwd_f32_h2_kernel, the 3 timed steps' launches", d[3:12],
              rf["avg_launch_us"], 2.0 * B * T * H * 4 * H)
         d = durations("f32", "void lstm_persist_fwd_f32_kernel")
         line(f, "roofline_fwd (c2 headline): lstm_persist_fwd_f32_kernel, the 3 timed steps' launches", d[3:12],
