@@ -170,6 +170,17 @@ __device__ __forceinline__ void grouped_tile(int id, int tiles_m, int tiles_n, i
   tn = cg * G + rem % G;
 }
 
+// Split-K launches (grid tiles x slabs): slab-major positions dealt to the XCDs in contiguous runs,
+// so each XCD works on (mostly) one K slab and its tiles share that slab's A / B panels through its
+// L2; the plain map gave every XCD pieces of every slab (dW at c2: 2.8x the algorithmic bytes).
+// Every (tile, slab) computes what it did before: the results are bit-identical.
+__device__ __forceinline__ void splitk_tile(int nwg, int& id, int& slab) {
+  const int L = blockIdx.x + blockIdx.y * gridDim.x;
+  const int pos = xcd_remap(L, gridDim.x * gridDim.y);
+  slab = pos / nwg;
+  id = pos - slab * nwg;
+}
+
 // XCD-aware 2-D tile map for the per-step kernels (grid nbx unit-blocks x nby row-blocks):
 // the dispatcher deals linear block L to XCD L % 8; give each XCD a compact rectangle of
 // (nby/2) x (nbx/4) tiles so the operand panels it reads (row-blocks of the left operand,

@@ -244,7 +244,7 @@ __device__ __forceinline__ void g8_epilogue(g8_f32x4 (&acc)[8][4], void* Cv, lon
         const unsigned hi = (unsigned)to_bf(v[2]) | ((unsigned)to_bf(v[3]) << 16);
         *reinterpret_cast<uint2*>(dst) = uint2{lo, hi};
       } else {
-        float* dst = reinterpret_cast<float*>(Cv) + (EPI == G8_SLAB ? (long)blockIdx.y * slab : 0) + row * ldc + col;
+        float* dst = reinterpret_cast<float*>(Cv) + (EPI == G8_SLAB ? slab : 0) + row * ldc + col;  // slab: offset
         if (EPI == G8_STORE) {
           v += badd;
           if (beta != 0.f) v += beta * *reinterpret_cast<const g8_f32x4*>(dst);
@@ -314,9 +314,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
   const int fr = lane & 15, fq = lane >> 4;
   const int tiles_n = N / G256_BM;
   const int nwg = tiles_n * (M / G256_BM);
-  const int id = xcd_remap(blockIdx.x, nwg);
+  int id = xcd_remap(blockIdx.x, nwg), sl = 0;
+  if (gridDim.y > 1) splitk_tile(nwg, id, sl);
   const int tn = id % tiles_n, tm = id / tiles_n;
-  const int kbeg = blockIdx.y * kchunk;
+  const int kbeg = sl * kchunk;
   const int nk = (min(K, kbeg + kchunk) - kbeg) / G256_BK;
   const int wr = w >> 2, wc = w & 3;
   G256Stage sa, sb;
@@ -472,7 +473,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
   if constexpr (EPI == G8_STORE_BF16)
     g8_epilogue_bf16_lds(acc, reinterpret_cast<bf16_t*>(C), ldc, tm, tn, wr, wc, w, lane, bias0, bias1, smem);
   else
-    g8_epilogue<EPI>(acc, C, ldc, slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
+    g8_epilogue<EPI>(acc, C, ldc, (long)sl * slab, tm, tn, wr, wc, lane, bias0, bias1, beta);
 }
 
 // ---- persistent form of the 8-phase kernel (G8_STORE_BF16 / G8_STORE, no split-K) ----

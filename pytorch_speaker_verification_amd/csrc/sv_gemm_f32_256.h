@@ -22,6 +22,9 @@
 #include "sv_gemm.h"
 
 #define GF_BM 256
+#ifndef SV_GF_GROUP
+#define SV_GF_GROUP 4  // column tiles per group of the one-shot tile order (grouped_tile)
+#endif
 #define GF_BK 32
 
 typedef __attribute__((address_space(3))) void* gf_lds_ptr_t;
@@ -67,12 +70,18 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tiles_n = N / BN;
   const int nwg = tiles_n * (M / GF_BM);
-  const int id = xcd_remap(blockIdx.x, nwg);
-  int tn = id % tiles_n, tm = id / tiles_n;
-  // one-shot launches: column-grouped tile order (4 fp32 B panels of 256 x 768 = 3.1 MB per XCD L2
-  // at the K1 shape); split-K launches keep the plain order
-  if (gridDim.y == 1) grouped_tile(id, M / GF_BM, tiles_n, 4, tm, tn);
-  const int kbeg = blockIdx.y * kchunk;
+  int id, sl = 0, tn, tm;
+  if (gridDim.y == 1) {
+    // one-shot launches: column-grouped tile order (4 fp32 B panels of 256 x 768 = 3.1 MB per XCD
+    // L2 at the K1 shape)
+    id = xcd_remap(blockIdx.x, nwg);
+    grouped_tile(id, M / GF_BM, tiles_n, SV_GF_GROUP, tm, tn);
+  } else {
+    splitk_tile(nwg, id, sl);
+    tn = id % tiles_n;
+    tm = id / tiles_n;
+  }
+  const int kbeg = sl * kchunk;
   const int nk = (min(K, kbeg + kchunk) - kbeg) / GF_BK;
   const int wr = w >> 2, wc = w & 3;
   GfStage<GF_BM> sa;
@@ -145,7 +154,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
     __syncthreads();
   }
   // epilogue: acc[i][j][e] = C[row][4 consecutive cols]
-  float* Cz = C + (EPI == GF_SLAB ? (long)blockIdx.y * slab : 0);
+  float* Cz = C + (EPI == GF_SLAB ? (long)sl * slab : 0);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const long row = (long)tm * GF_BM + wr * 128 + MF * i + fr;

@@ -15,6 +15,9 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if "--lib" in sys.argv:  # an A/B build (Makefile `ab`)
+    from pytorch_speaker_verification_amd import _lib  # noqa: E402
+    _lib.use_library(sys.argv[sys.argv.index("--lib") + 1])
 from pytorch_speaker_verification_amd._lib import call, lib, ptr  # noqa: E402
 
 REPS = 3
