@@ -66,7 +66,7 @@ out = {"lib": args.lib or "libsv_ge2e.so", "B": args.B, "T": args.T, "fwd_ms": t
 out["status"] = int(ps.block[0])
 # stamps: u64 [SV_NSTAMP_WG][SV_NSTAMP] at word SV_SYNC_STAMP = 32 + 4 * 64 * 32 of the sync block
 stamp0 = 32 + 4 * 64 * 32
-st64 = ps.block[stamp0:stamp0 + 2 * 1024 * 8].view(torch.int64).view(1024, 8)[:, :5].cpu().double()
+st64 = ps.block[stamp0:stamp0 + 2 * 1024 * 8].view(torch.int64).view(1024, 8)[:512, :5].cpu().double()
 if st64.abs().sum() > 0:
     nwg = int((st64.sum(1) > 0).sum())
     per = st64[:nwg].mean(0) / (args.T - 1)
@@ -74,4 +74,13 @@ if st64.abs().sum() > 0:
     out["bwd_cycles_per_step"] = {k: round(float(v), 1) for k, v in zip(names, per)}
     out["bwd_cycles_total"] = round(float(per.sum()), 1)
     out["stamped_wgs"] = nwg
+# forward stamps (FLAGS=-DSV_PFWD_DEBUG=32): workgroup slots 512 .. of the same area, the last
+# forward layer launch of the timed forwards
+fw = ps.block[stamp0:stamp0 + 2 * 1024 * 8].view(torch.int64).view(1024, 8)[512:, :6].cpu().double()
+if fw.abs().sum() > 0:
+    nwg = int((fw.sum(1) > 0).sum())
+    per = fw[:nwg].mean(0) / (args.T - 1)
+    names = ["wait", "stage h + x-proj issue", "MFMA", "exchange+epilogue", "hand-off+arrive", "post-arrival"]
+    out["fwd_cycles_per_step"] = {k: round(float(v), 1) for k, v in zip(names, per)}
+    out["fwd_cycles_total"] = round(float(per.sum()), 1)
 print(json.dumps(out), flush=True)

@@ -30,6 +30,7 @@ def test_persistent_fwd_bf16_equals_per_step(dims, N, M, T):
 
 @pytest.mark.parametrize("dims,N,M,T", [((40, 768, 3, 256), 64, 10, 12),   # c3 grid: 24 x 10 workgroups
                                         ((40, 768, 3, 256), 64, 10, 40),   # c3, hand-off slots past T = 33
+                                        ((40, 768, 3, 256), 56, 10, 9),    # B = 560: wide tiles, row-major dG
                                         ((40, 768, 2, 256), 16, 10, 7),    # B = 160: 32-row tiles
                                         ((40, 96, 2, 32), 7, 5, 9),        # ragged rows (B = 35)
                                         ((40, 64, 3, 32), 4, 5, 7)])       # H = 64: 2 unit blocks
