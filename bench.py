@@ -311,14 +311,21 @@ def dvector_inference(net, dev, S=16384, T=24, reps=3):
         res.update(ms_per_batch=round(ms, 3), windows_per_sec=round(S / (ms * 1e-3), 1),
                    tflops=round(flops / (ms * 1e-3) / 1e12, 2),
                    mfma_frac=round(flops / (ms * 1e-3) / 1e12 / MI355X_FP32_MFMA_TFLOPS, 4))
-        # the c3 mixed-precision forward on the same windows (bf16 operands, fp32 state), in calls of
-        # the largest co-resident persistent batch (dvector.bf16_batch)
+        # the c3 mixed-precision forward on the same windows (bf16 operands, fp32 state): the default
+        # large-batch path (sv_dvector_embed_bf16: one 256 x 256 GEMM launch per timestep and layer
+        # with the cell in its epilogue) and, beside it, calls of the largest co-resident persistent
+        # batch (dvector.bf16_batch)
         from pytorch_speaker_verification_amd.dvector import bf16_batch
         bb = bf16_batch(H)
         ms16 = _timed(lambda: embed_windows(net, xw, precision="bf16"), dev, reps)
+        ms16p = _timed(lambda: embed_windows(net, xw, precision="bf16", path="persist"), dev, reps)
         res["bf16"] = {"ms_per_batch": round(ms16, 3), "windows_per_sec": round(S / (ms16 * 1e-3), 1),
-                       "windows_per_call": bb, "tflops": round(flops / (ms16 * 1e-3) / 1e12, 2),
-                       "mfma_frac": round(flops / (ms16 * 1e-3) / 1e12 / MI355X_BF16_MFMA_TFLOPS, 4)}
+                       "path": "per-timestep 256x256 GEMM + fused cell (sv_dvector_embed_bf16)",
+                       "tflops": round(flops / (ms16 * 1e-3) / 1e12, 2),
+                       "mfma_frac": round(flops / (ms16 * 1e-3) / 1e12 / MI355X_BF16_MFMA_TFLOPS, 4),
+                       "persistent_batches": {"ms_per_batch": round(ms16p, 3), "windows_per_call": bb,
+                                              "mfma_frac": round(flops / (ms16p * 1e-3) / 1e12 /
+                                                                 MI355X_BF16_MFMA_TFLOPS, 4)}}
         # the reference's call shape: one file's windows per call (dvector_create.py:96-100, tens
         # to hundreds of windows); 128 windows, per call (kernels + host), fp32 and bf16
         Sf = 128

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SV_ABI_VERSION 5
+#define SV_ABI_VERSION 6
 int sv_abi_version(void);
 
 /* ---- fp32 product modes (`products` argument of sv_gemm_f32 / sv_lstm_stack_fwd / _bwd; every
@@ -307,6 +307,22 @@ int sv_status_poison(const void* sync, float* x, int n, hipStream_t stream);
  * skips the update on every rank alike. */
 int sv_status_to_flag(const void* sync, float* flag, hipStream_t stream);
 int sv_status_merge(void* sync, const float* flag, hipStream_t stream);
+
+/* ---- large-batch d-vector inference (dvector_create.py:96-101; SpeechEmbedder.forward of every
+ * 24-frame window of a file, speech_embedder_net.py:27-33), bf16 GEMM operands / fp32 accumulation
+ * and state as the c3 forward (the input projection rounded to bf16 with its biases).  One launch per
+ * timestep and layer: the 256 x 256 bf16 GEMM over [x_t | h_{t-1}] . [W_ih | W_hh]^T with the LSTM
+ * cell in its epilogue, so no co-residency requirement at any B.  x [B][T][F] fp32 (batch-first
+ * windows; F <= 64), layer l's w_ih [4H][F_l] (F_0 = F, else H), w_hh [4H][H], b_ih / b_hh [4H]
+ * (the arrays of b_ih / b_hh may be NULL), w_p [P][H], b_p [P] (may be NULL), all fp32 device
+ * pointers; emb [B][P] = normalize(h_{T-1} w_p^T + b_p).  H % 64 == 0, 4H % 256 == 0; workspace
+ * of sv_dvector_bf16_workspace bytes, 256-B aligned.  Replaces embedder_net(windows) at
+ * dvector_create.py:100 for the bf16 precision of embed_windows (dvector.py). */
+size_t sv_dvector_bf16_workspace(int B, int T, int F, int H, int L, int P);
+int sv_dvector_embed_bf16(int B, int T, int F, int H, int L, const float* x, const float* const* w_ih,
+                          const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
+                          const float* w_p, const float* b_p, int P, float* emb, void* workspace,
+                          hipStream_t stream);
 
 /* ---- clip_grad_norm_ + SGD step over one flat parameter group (train_speech_embedder.py:63-65)
  * p -= lr * min(1, max_norm / (|g|_2 + 1e-6)) * g; write_grad=1 also scales g in place.

@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libsv_ge2e.so")
 # the fault-injection test build (Makefile `faultinj`): the same library plus sv_test_set_fault;
 # only tests load it, through use_library() before the first call
 FAULT_LIB_PATH = os.path.join(_HERE, "libsv_ge2e_faultinj.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # schedule flags of the bf16 stack (include/sv_ge2e.h SV_SCHED_*), by name
 SCHEDULES = {"auto": 0, "per_layer": 1, "per_step": 2, "persist": 5}  # persist: per-layer persistent, any H
@@ -110,6 +110,9 @@ SIGNATURES = {
     "sv_status_poison": (_c_int, [_P, _P, _c_int, _P]),
     "sv_status_to_flag": (_c_int, [_P, _P, _P]),
     "sv_status_merge": (_c_int, [_P, _P, _P]),
+    "sv_dvector_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int]),
+    "sv_dvector_embed_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _c_int, _P,
+                                       _P, _P]),
     "sv_clip_sgd_workspace": (_c_size_t, []),
     "sv_clip_sgd_step": (_c_int, [_P, _P, _c_long, _c_float, _c_float, _c_int, _P, _P, _P, _P]),
 }

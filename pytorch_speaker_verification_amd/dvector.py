@@ -12,9 +12,13 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .ops import check_persistent_status, embedder_forward, embedder_forward_bf16
+from .ops import check_persistent_status, embedder_forward, embedder_forward_bf16, embedder_forward_dvec_bf16
 
 WIN, HOP = 24, 12  # frames: int(.24/.01), int(.12/.01)
+# bf16: from this many windows on, one pass of per-timestep GEMM launches with the cell in their
+# epilogue (sv_dvector_embed_bf16) instead of co-resident persistent batches (bf16_batch)
+DVEC_MIN = 3072
+DVEC_CHUNK = 16384
 
 
 def window_frames(logmel, win=WIN, hop=HOP):
@@ -39,20 +43,29 @@ def bf16_batch(H, limit=16384):
 
 
 @torch.no_grad()
-def embed_windows(net, windows, batch=None, precision="f32"):
+def embed_windows(net, windows, batch=None, precision="f32", path=None):
     """Embeddings [S, proj] of windows [S, win, nmels] with the module's weights (GPU), `batch`
     windows per call (None: 16384 in fp32; bf16: bf16_batch(), the largest co-resident
     persistent batch).  precision "bf16": the c3 mixed-precision forward (bf16 GEMM operands,
     fp32 accumulation and state), no activations saved; raises PersistentRecurrenceError if one
-    of its persistent recurrences timed out."""
+    of its persistent recurrences timed out.  path (bf16 only): "persist" (batches of the
+    training forward's persistent recurrences), "dvec" (sv_dvector_embed_bf16, DVEC_CHUNK windows
+    per call) or None: "dvec" from DVEC_MIN windows on when no batch is given."""
     if precision not in ("f32", "bf16"):
         raise ValueError(f"precision must be 'f32' or 'bf16', got {precision!r}")
+    if path not in (None, "persist", "dvec") or (path is not None and precision != "bf16"):
+        raise ValueError(f"path must be None, 'persist' or 'dvec' (bf16 only), got {path!r}")
     dev = next(net.parameters()).device
     layers = net.LSTM_stack.layer_params()
+    x = torch.as_tensor(windows, dtype=torch.float32)
+    if precision == "bf16" and (path == "dvec" or (path is None and batch is None and x.shape[0] >= DVEC_MIN)):
+        out = [embedder_forward_dvec_bf16(x[i:i + (batch or DVEC_CHUNK)].to(dev).contiguous(), layers,
+                                          net.projection.weight, net.projection.bias)
+               for i in range(0, x.shape[0], batch or DVEC_CHUNK)]
+        return torch.cat(out) if out else torch.zeros((0, net.projection.weight.shape[0]), device=dev)
     if batch is None:
         batch = bf16_batch(layers[0][1].shape[1]) if precision == "bf16" else 16384
     out = []
-    x = torch.as_tensor(windows, dtype=torch.float32)
     for i in range(0, x.shape[0], batch):
         xb = x[i:i + batch].to(dev).contiguous()
         fwd = embedder_forward_bf16 if precision == "bf16" else embedder_forward

@@ -384,6 +384,27 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=Non
     return emb, st
 
 
+def embedder_forward_dvec_bf16(x, layers, w_p, b_p):
+    """Embeddings [B, P] of B windows x [B, T, F] (fp32, batch-first) by sv_dvector_embed_bf16:
+    the c3 forward's numerics (bf16 GEMM operands, bf16 input projection with its biases, fp32
+    accumulation / state / projection) as one 256 x 256 GEMM launch per timestep and layer with the
+    LSTM cell in its epilogue -- the large-batch d-vector path (dvector_create.py:96-101), no
+    activations saved and no co-residency requirement."""
+    require_device(x, w_p, *[t for l in layers for t in l if t is not None])
+    B, T, F = x.shape
+    H = layers[0][1].shape[1]
+    P = w_p.shape[0]
+    L = len(layers)
+    x = x.contiguous()
+    emb = torch.empty((B, P), dtype=torch.float32, device=x.device)
+    ws = _ws(lib().sv_dvector_bf16_workspace(B, T, F, H, L, P), x.device)
+    ts = [[l[i].contiguous() if l[i] is not None else None for l in layers] for i in range(4)]  # kept alive
+    wih, whh, bih, bhh = (_parr(t) for t in ts)
+    call("sv_dvector_embed_bf16", B, T, F, H, L, ptr(x), wih, whh, bih, bhh, ptr(w_p.contiguous()),
+         ptr(b_p) if b_p is not None else None, P, ptr(emb), ptr(ws), stream_of(x))
+    return emb
+
+
 def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, status=None, probe=None,
                            schedule="auto"):
     """Backward of embedder_forward_bf16 (same ``grads`` / ``grad_ready`` contract as

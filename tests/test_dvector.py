@@ -86,3 +86,54 @@ def test_embed_windows_rejects_unknown_precision():
     """The precision switch is validated before any device work (CPU-only check)."""
     with pytest.raises(ValueError):
         dvector.embed_windows(None, np.zeros((1, 24, 40), np.float32), precision="fp16")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [512, 300])
+def test_embed_windows_dvec_path_against_bf16_oracle(S):
+    """The large-batch bf16 path (sv_dvector_embed_bf16: one 256 x 256 GEMM launch per timestep
+    and layer over [x_t | h_{t-1}] with the LSTM cell in its epilogue; S = 300 pads the rows to
+    512) against the bf16-operand oracle (oracle/lstm_bf16.py: the same bf16 rounding of the
+    operands and of the input projection with its biases) and against the persistent bf16 path.
+    The only difference from the oracle is the fp32 order of the h part's sum (MFMA k-steps added
+    onto the rounded input projection), amplified through 24 steps x 3 layers."""
+    import recipe
+    from conftest import model_dims
+    from oracle import lstm_bf16
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    dims = (40, 768, 3, 256)
+    sd = recipe.make_weights(9, *dims, scale=2.0)
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    net = net.cuda()
+    x = recipe.make_frames(12, S, 24, 40)
+    ed = dvector.embed_windows(net, x, precision="bf16", path="dvec").cpu().numpy()
+    ep = dvector.embed_windows(net, x, precision="bf16", path="persist").cpu().numpy()
+    eo, _ = lstm_bf16.embedder_forward(sd, x, 3, bf16=True)
+    eo = eo.numpy()
+    assert ed.shape == (S, 256) and np.isfinite(ed).all()
+    d_or = float(np.abs(ed - eo).max())
+    d_p = float(np.abs(ed - ep).max())
+    print(f"\nMEASURED dvector_dvec_bf16[S={S}] vs bf16 oracle max-abs {d_or:.2e}; vs persistent bf16 {d_p:.2e}")
+    assert d_or <= 5e-3 and d_p <= 5e-3, (d_or, d_p)
+    np.testing.assert_allclose(np.linalg.norm(ed, axis=1), 1.0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_embed_windows_dvec_auto_large_batch():
+    """From DVEC_MIN windows on, embed_windows(precision='bf16') takes the per-step GEMM path;
+    4096 windows of a random-init net against the fp32 path (bf16-level agreement)."""
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    torch.manual_seed(3)
+    net = SpeechEmbedder().cuda()
+    x = np.random.default_rng(4).standard_normal((4096, 24, 40)).astype(np.float32)
+    assert x.shape[0] >= dvector.DVEC_MIN
+    e16 = dvector.embed_windows(net, x, precision="bf16").cpu().numpy()
+    e32 = dvector.embed_windows(net, x).cpu().numpy()
+    d = float(np.abs(e16 - e32).max())
+    cos = float((e16 * e32).sum(1).min())
+    print(f"\nMEASURED dvector_dvec_bf16[4096] vs fp32 max-abs {d:.2e}, min cosine {cos:.7f}")
+    assert d <= 5e-3 and cos > 0.9999, (d, cos)
