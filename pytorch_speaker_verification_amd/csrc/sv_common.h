@@ -37,7 +37,10 @@ int sv_persist_fwd_f32(int T, int B, int H, const float* whh, float* gates, floa
                        hipStream_t stream, unsigned* sync, int chan, hipEvent_t pre, hipEvent_t post);
 int sv_persist_bwd_f32(int T, int B, int H, const float* whhT, const float* acts, const float* c_tm,
                        const float* dhup, int up_full, float* dg, float* dgT, float* dgf, hipStream_t stream,
-                       unsigned* sync, hipEvent_t pre, hipEvent_t post);
+                       unsigned* sync, hipEvent_t pre, hipEvent_t post, float* db_ih = nullptr,
+                       float* db_hh = nullptr);
+// db_ih (= db_hh when given) = sum over nrb row blocks, in order, of the partials dbp [nrb][G]
+int sv_persist_db_finalize(const float* dbp, int nrb, int G, float* db_ih, float* db_hh, hipStream_t stream);
 #define SV_LAUNCH_CHECK()                                  \
   do {                                                     \
     hipError_t e__ = hipGetLastError();                    \

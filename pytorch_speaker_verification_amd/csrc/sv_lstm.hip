@@ -1023,7 +1023,8 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
       if (l > 0 && (rc = sv_transpose(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, main))) return rc;
       const float* up = l == L - 1 ? dh_last : dx[l + 1];
       rc = sv_persist_bwd_f32(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1, dgates[l], dgT[l], dgf, main, sync,
-                              probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr);
+                              probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr, db_ih[l],
+                              db_hh ? db_hh[l] : nullptr);
       if (rc) return rc;
       // the completion events of layers >= 1 (grad_ready: a caller's bucketed all-reduce) fire once
       // the last recurrence is done, so a collective never shares the device with a persistent
@@ -1040,9 +1041,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
       if ((rc = gemm_f32(1, 1, 4 * H, Fl, TBp, dgT[l], TBp, xT[l], ld_xT[l], dw_ih[l], Fl, nullptr, nullptr, 0.f,
                          ws.gws, main)))
         return rc;
-      hipLaunchKernelGGL(rowsum_kernel, dim3(4 * H), dim3(RS_T), 0, main, dgT[l], (long)TBp, TBp, db_ih[l],
-                         db_hh ? db_hh[l] : nullptr);
-      SV_LAUNCH_CHECK();
+      // (bias gradients: summed inside the persistent recurrence, finalized after it)
     }
     if ((e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
     return SV_OK;

@@ -825,6 +825,13 @@ __global__ void persist_db_finalize_kernel(const float* __restrict__ dbp, int nr
   if (db_hh) db_hh[c] = s;
 }
 
+int sv_persist_db_finalize(const float* dbp, int nrb, int G, float* db_ih, float* db_hh, hipStream_t stream) {
+  if (!dbp || !db_ih || nrb <= 0 || G <= 0) return SV_EARG;
+  hipLaunchKernelGGL(persist_db_finalize_kernel, dim3((G + 255) / 256), dim3(256), 0, stream, dbp, nrb, G, db_ih, db_hh);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
 // ============================================================================
 // host side
 // ============================================================================

@@ -303,7 +303,8 @@ template <int NKG, int P, int NV, int NL>
 __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
     const float* __restrict__ whhT, const float* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, float* __restrict__ dg, float* __restrict__ dgT, long lddgT,
-    float* dgf, int T, int Bp, int B, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit, int fault) {
+    float* dgf, int T, int Bp, int B, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit, int fault,
+    float* __restrict__ dbp) {
   constexpr int H = 8 * NKG;
   static_assert(PF_NA + NV + NL == NKG, "weight split");
   constexpr int LDR = PF_U + 4;      // red [4][32][LDR]
@@ -377,6 +378,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
     dcf[hf] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   load_ew(T - 1, 0);
+  float dbs = 0.f;  // threads < 128: bias-gradient partial of gate column tid over t and the row block
   for (int t = T - 1; t >= 0; --t) {
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
@@ -443,6 +445,18 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         for (int v = 0; v < 4; ++v) gts[(q * PF_U + 4 * quad + v) * LDT + erow] = dq[q][v];
       }
       __syncthreads();
+      if (dbp && tid < 4 * PF_U) {  // bias partials: gate column tid, this half's rows in order (rows past B: 0)
+        const int nv = min(PH_BM, B - b0);
+        float s = 0.f;
+#pragma unroll
+        for (int e4 = 0; e4 < PH_BM / 4; ++e4) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(gts + tid * LDT + 4 * e4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (4 * e4 + e < nv) s += v[e];
+        }
+        dbs += s;
+      }
       if (t > 0) {  // the hand-off: 16 fragment blocks of 1 KB (gate q, this half, k-group 4 ub + kl)
         const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 4));
 #pragma unroll
@@ -487,6 +501,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
       }
     }
   }
+  if (dbp && tid < 4 * PF_U) dbp[(long)rb * 4 * H + (long)(tid >> 5) * H + j0 + (tid & 31)] = dbs;
 }
 
 // ============================================================================
@@ -514,8 +529,9 @@ int sv_persist_f32_fits(int B, int H, int cus) {
 }
 
 // bytes of the backward's fragment-order hand-off: T slots of ceil(B / 64) x 64 rows x 4H fp32
-size_t sv_persist_f32_bwd_scratch(int T, int B, int H) {
-  return (size_t)T * (size_t)((B + PF_BM - 1) / PF_BM) * PF_BM * 4 * H * sizeof(float);
+size_t sv_persist_f32_bwd_scratch(int T, int B, int H) {  // hand-off slots + bias partials
+  const size_t nrb = (size_t)((B + PF_BM - 1) / PF_BM);
+  return ((size_t)T * nrb * PF_BM + nrb) * 4 * H * sizeof(float);
 }
 
 int sv_persist_fwd_f32(int T, int B, int H, const float* whh, float* gates, float* c_tm, float* h_tm, float* hT,
@@ -538,19 +554,22 @@ int sv_persist_fwd_f32(int T, int B, int H, const float* whh, float* gates, floa
 
 int sv_persist_bwd_f32(int T, int B, int H, const float* whhT, const float* acts, const float* c_tm,
                        const float* dhup, int up_full, float* dg, float* dgT, float* dgf, hipStream_t stream,
-                       unsigned* sync, hipEvent_t pre, hipEvent_t post) {
+                       unsigned* sync, hipEvent_t pre, hipEvent_t post, float* db_ih, float* db_hh) {
   if (!sv_persist_f32_fits(B, H, sv_stream_cus(stream))) return SV_ESHAPE;
   if (!sync || !whhT || !acts || !c_tm || !dg || !dgT || !dgf || ((uintptr_t)dgf & 15)) return SV_EARG;
   unsigned* cnt = sync + SV_SYNC_CNT;  // channel 0
   const int nub = H / PF_U, nrb = (B + PF_BM - 1) / PF_BM;
   const int Bp = (B + 3) & ~3;
+  // bias partials [nrb][4H] after the hand-off slots (db_ih NULL: not computed here)
+  float* dbp = db_ih ? dgf + (size_t)T * nrb * PF_BM * 4 * H : nullptr;
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)2 * nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
   hipLaunchKernelGGL((lstm_persist_bwd_f32_h2_kernel<96, PH_BWD_P, PH_BWD_NV, PH_BWD_NL>), dim3(nub * nrb),
                      dim3(256), ph_bwd_lds(), stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, (long)T * Bp, dgf, T,
-                     Bp, B, cnt, nub, PF_XCD, sync, sv_persist_limit(), sv_persist_fault(1));
+                     Bp, B, cnt, nub, PF_XCD, sync, sv_persist_limit(), sv_persist_fault(1), dbp);
   SV_LAUNCH_CHECK();
   if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
-  return SV_OK;
+  // bias gradients: the row blocks' partials summed in order (no row-sum pass over dG^T)
+  return dbp ? sv_persist_db_finalize(dbp, nrb, 4 * H, db_ih, db_hh, stream) : SV_OK;
 }
