@@ -445,18 +445,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         for (int v = 0; v < 4; ++v) gts[(q * PF_U + 4 * quad + v) * LDT + erow] = dq[q][v];
       }
       __syncthreads();
-      if (dbp && tid < 4 * PF_U) {  // bias partials: gate column tid, this half's rows in order (rows past B: 0)
-        const int nv = min(PH_BM, B - b0);
-        float s = 0.f;
-#pragma unroll
-        for (int e4 = 0; e4 < PH_BM / 4; ++e4) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(gts + tid * LDT + 4 * e4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (4 * e4 + e < nv) s += v[e];
-        }
-        dbs += s;
-      }
       if (t > 0) {  // the hand-off: 16 fragment blocks of 1 KB (gate q, this half, k-group 4 ub + kl)
         const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 4));
 #pragma unroll
@@ -473,7 +461,20 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
           __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      // off the chain: row-major dG and dG^T of the half-step
+      // off the chain: the bias partials (gate column tid: this half's rows in order, rows past B
+      // excluded), row-major dG and dG^T of the half-step
+      if (dbp && tid < 4 * PF_U) {
+        const int nv = min(PH_BM, B - b0);
+        float s = 0.f;
+#pragma unroll
+        for (int e4 = 0; e4 < PH_BM / 4; ++e4) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(gts + tid * LDT + 4 * e4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (4 * e4 + e < nv) s += v[e];
+        }
+        dbs += s;
+      }
       const long gb = b0 + erow;
       if (gb < B) {
         float* dp = dg + (long)t * BG + gb * G + j0 + 4 * quad;
