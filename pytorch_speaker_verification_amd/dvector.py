@@ -31,6 +31,12 @@ def window_frames(logmel, win=WIN, hop=HOP):
     return np.stack([logmel[:, j:j + win].T for j in starts]).astype(np.float32)
 
 
+def dvec_ok(F, H):
+    """Dimensions sv_dvector_embed_bf16 takes (include/sv_ge2e.h): the x part one padded k-tile,
+    whole 256-column tiles of the unit-interleaved 4H gate columns."""
+    return 0 < F <= 64 and H % 64 == 0 and (4 * H) % 256 == 0
+
+
 def bf16_batch(H, limit=16384):
     """Windows per call of the bf16 forward: the largest multiple of 32 (<= limit) whose whole
     recurrence grid is co-resident, so each call runs the persistent W-stationary kernels (c3's)
@@ -58,7 +64,11 @@ def embed_windows(net, windows, batch=None, precision="f32", path=None):
     dev = next(net.parameters()).device
     layers = net.LSTM_stack.layer_params()
     x = torch.as_tensor(windows, dtype=torch.float32)
-    if precision == "bf16" and (path == "dvec" or (path is None and batch is None and x.shape[0] >= DVEC_MIN)):
+    F, H = x.shape[-1], layers[0][1].shape[1]
+    if path == "dvec" and not dvec_ok(F, H):
+        raise ValueError(f"the per-timestep GEMM path needs F <= 64, H % 64 == 0 and 4H % 256 == 0 (F={F}, H={H})")
+    if precision == "bf16" and (path == "dvec" or (path is None and batch is None and x.shape[0] >= DVEC_MIN
+                                                    and dvec_ok(F, H))):
         out = [embedder_forward_dvec_bf16(x[i:i + (batch or DVEC_CHUNK)].to(dev).contiguous(), layers,
                                           net.projection.weight, net.projection.bias)
                for i in range(0, x.shape[0], batch or DVEC_CHUNK)]

@@ -137,3 +137,12 @@ def test_embed_windows_dvec_auto_large_batch():
     cos = float((e16 * e32).sum(1).min())
     print(f"\nMEASURED dvector_dvec_bf16[4096] vs fp32 max-abs {d:.2e}, min cosine {cos:.7f}")
     assert d <= 5e-3 and cos > 0.9999, (d, cos)
+
+
+def test_dvec_path_dimension_rule():
+    """The large-batch bf16 path's dimension rule mirrors sv_dvector_embed_bf16's argument checks
+    (include/sv_ge2e.h): model dims it cannot take fall back to the persistent batches."""
+    assert dvector.dvec_ok(40, 768)
+    assert not dvector.dvec_ok(80, 768)   # x part wider than one 64-column k-tile
+    assert not dvector.dvec_ok(40, 96)    # 4H = 384: not whole 256-column tiles
+    assert dvector.dvec_ok(40, 64)
