@@ -35,6 +35,8 @@ struct DvecStep {
 };
 }  // namespace
 
+// LAST: the last step of the last layer, which also writes h_{T-1} in fp32 (p.hlast)
+template <bool LAST>
 __global__ __launch_bounds__(512, 1) void lstm_dvec_step_bf16_kernel(const DvecStep p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -73,6 +75,12 @@ __global__ __launch_bounds__(512, 1) void lstm_dvec_step_bf16_kernel(const DvecS
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = g8_f32x4{0.f, 0.f, 0.f, 0.f};
+  // the biases of this lane's 16 gate columns, loaded before the fills (a load inside the k-loop
+  // would wait, in the in-order vmcnt, for every fill in flight)
+  g8_f32x4 bs[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+    bs[nt] = *reinterpret_cast<const g8_f32x4*>(p.bsum + tn * G256_BM + wc * 64 + 16 * nt + 4 * fq);
   // the 8-phase schedule of gemm_bf16_8q_kernel (sv_gemm256.h: fills two per phase, counted waits,
   // the two wave groups one barrier apart)
 #pragma unroll
@@ -162,10 +170,9 @@ __global__ __launch_bounds__(512, 1) void lstm_dvec_step_bf16_kernel(const DvecS
       // the x part is complete: bf16(x W_ih^T + (b_ih + b_hh)), as the c3 path's K1 stores it
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        const g8_f32x4 bs = *reinterpret_cast<const g8_f32x4*>(p.bsum + tn * G256_BM + wc * 64 + 16 * nt + 4 * fq);
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt) {
-          const g8_f32x4 v = acc[mt][nt] + bs;
+          const g8_f32x4 v = acc[mt][nt] + bs[nt];
           acc[mt][nt] = g8_f32x4{round_bf(v[0]), round_bf(v[1]), round_bf(v[2]), round_bf(v[3])};
         }
       }
@@ -181,9 +188,15 @@ __global__ __launch_bounds__(512, 1) void lstm_dvec_step_bf16_kernel(const DvecS
   char* tile = smem + w * 4096;  // [128 rows][16 units] bf16, after every wave's last stage read
   __syncthreads();
   const int ug = tn * 64 + wc * 16;  // first unit of this wave's 16
+  // all eight c_{t-1} loads in flight at once, unconditionally (a load per branch waited for each;
+  // at t = 0 the state is not yet written and the loaded values are discarded)
+  float4 cps[8];
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) cps[mt] = cw[mt * 64];
+  const bool first = p.first;
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt) {
-    float4 cp = p.first ? float4{0.f, 0.f, 0.f, 0.f} : cw[mt * 64];
+    const float4 cp = first ? float4{0.f, 0.f, 0.f, 0.f} : cps[mt];
     float cn[4], hn[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
@@ -193,7 +206,7 @@ __global__ __launch_bounds__(512, 1) void lstm_dvec_step_bf16_kernel(const DvecS
       const float cprev = nt == 0 ? cp.x : nt == 1 ? cp.y : nt == 2 ? cp.z : cp.w;
       cn[nt] = lstm_cell_fwd(pv, zx, cprev, av, hn[nt]);
       *reinterpret_cast<bf16_t*>(tile + (16 * mt + fr) * 32 + (4 * nt + fq) * 2) = to_bf(hn[nt]);
-      if (p.hlast) p.hlast[((long)tm * G256_BM + wr * 128 + 16 * mt + fr) * p.H + ug + 4 * nt + fq] = hn[nt];
+      if constexpr (LAST) p.hlast[((long)tm * G256_BM + wr * 128 + 16 * mt + fr) * p.H + ug + 4 * nt + fq] = hn[nt];
     }
     cw[mt * 64] = float4{cn[0], cn[1], cn[2], cn[3]};
   }
@@ -303,7 +316,10 @@ extern "C" int sv_dvector_embed_bf16(int B, int T, int F, int H, int L, const fl
       s.hlast = (l == L - 1 && t == T - 1) ? hlast : nullptr;
       s.H = H;
       s.first = t == 0;
-      hipLaunchKernelGGL(lstm_dvec_step_bf16_kernel, dim3(grid), dim3(512), lds, stream, s);
+      if (s.hlast)
+        hipLaunchKernelGGL(lstm_dvec_step_bf16_kernel<true>, dim3(grid), dim3(512), lds, stream, s);
+      else
+        hipLaunchKernelGGL(lstm_dvec_step_bf16_kernel<false>, dim3(grid), dim3(512), lds, stream, s);
       SV_LAUNCH_CHECK();
     }
   }
