@@ -109,3 +109,26 @@ def test_fault_injection_build_exports_the_test_hook():
     from pytorch_speaker_verification_amd import _lib
     h = ctypes.CDLL(_lib.FAULT_LIB_PATH)
     assert hasattr(h, "sv_test_set_fault") and h.sv_abi_version() == _lib.ABI_VERSION
+
+
+def test_graft_build_entry_point():
+    """__graft_entry__.build(): the driver's build check (make + import + the library's ABI equal to
+    the binding's; a stale ABI assertion there once failed every build)."""
+    import importlib
+    import sys
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    g = importlib.import_module("__graft_entry__")
+    g.build()
+
+
+@pytest.mark.gpu
+def test_graft_smoke_entry_point():
+    """__graft_entry__.smoke(): one small training step on cuda:0 against the numpy oracle."""
+    import importlib
+    import sys
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    importlib.import_module("__graft_entry__").smoke()
