@@ -4,6 +4,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 import torch
 
 from conftest import GOLDEN, ROOT, golden, model_dims
@@ -116,11 +117,8 @@ def test_graft_build_entry_point():
     the binding's; a stale ABI assertion there once failed every build)."""
     import importlib
     import sys
-    import os
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path.insert(0, root)
-    g = importlib.import_module("__graft_entry__")
-    g.build()
+    sys.path.insert(0, ROOT)
+    importlib.import_module("__graft_entry__").build()
 
 
 @pytest.mark.gpu
@@ -128,7 +126,5 @@ def test_graft_smoke_entry_point():
     """__graft_entry__.smoke(): one small training step on cuda:0 against the numpy oracle."""
     import importlib
     import sys
-    import os
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path.insert(0, root)
+    sys.path.insert(0, ROOT)
     importlib.import_module("__graft_entry__").smoke()
