@@ -40,17 +40,26 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16_t* __restrict
   gemm_mainloop_bf<BM, BN, 256, BBK, TM, TN>(A, lda, RowMapLinear{tm * BM, M}, B, ldb, RowMapLinear{tn * BN, N}, kbeg,
                                              kend, ldsb, tid, wm0, wn0, acc);
   float* Cz = reinterpret_cast<float*>(Cv) + (EPI == BEPI_SLAB ? (long)blockIdx.y * slab : 0);
+  // bias sums of the lane's columns, loaded before any store (a load between stores waits for
+  // every store issued before it)
+  float bsum[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = tn * BN + wn0 + 32 * j + (lane & 31);
+    float badd = 0.f;
+    if (EPI != BEPI_SLAB && col < N) {
+      if (bias0) badd += bias0[col];
+      if (bias1) badd += bias1[col];
+    }
+    bsum[j] = badd;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = tn * BN + wn0 + 32 * j + (lane & 31);
       if (col >= N) continue;
-      float badd = 0.f;
-      if (EPI != BEPI_SLAB) {
-        if (bias0) badd += bias0[col];
-        if (bias1) badd += bias1[col];
-      }
+      const float badd = bsum[j];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = tm * BM + wm0 + 32 * i + acc_row(r, lane);
@@ -517,13 +526,14 @@ extern "C" int sv_gemm_bf16_bf(int M, int N, int K, const bf16_t* A, long lda, c
   if (K % 8 || lda % 8 || ldb % 8 || (((uintptr_t)A | (uintptr_t)B) & 15)) return SV_EALIGN;
   const BPlan p = plan_bf16(M, N, K);
   if (p.bm == G256_BM && p.splitk == 1 && g8_ok(nullptr, 0, bias0, bias1) && ldc % 8 == 0 &&
-      !((uintptr_t)C & 15)) {
+      !((uintptr_t)C & 15) && (size_t)N * 4 <= G8P_BIAS_LDS) {
     // persistent form: one workgroup per CU walks the tiles, each tile's store tail overlapping
     // the next tile's first fill
     const int tiles = (M / G256_BM) * (N / G256_BM);
     const int cus = sv_stream_cus(stream);
     const int grid = std::min(tiles, cus > 0 ? cus : 256);
-    hipLaunchKernelGGL((gemm_bf16_8qp_kernel<G8_STORE_BF16>), dim3(grid), dim3(512), G256_LDS, stream, A, lda, B, ldb,
+    const size_t lds = G256_LDS + ((bias0 || bias1) ? (size_t)N * 4 : 0);
+    hipLaunchKernelGGL((gemm_bf16_8qp_kernel<G8_STORE_BF16>), dim3(grid), dim3(512), lds, stream, A, lda, B, ldb,
                        (void*)C, ldc, M, N, K, bias0, bias1, 0.f);
   } else if ((long)((M + 127) / 128) * ((N + 127) / 128) < 128) {
     launch_bf<64, 64, BEPI_STORE_BF16>(A, lda, B, ldb, C, ldc, 0, M, N, K, 1, ((K + BBK - 1) / BBK) * BBK, bias0,

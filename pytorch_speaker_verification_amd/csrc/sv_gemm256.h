@@ -73,6 +73,7 @@ __device__ __forceinline__ void g256_epilogue_impl(f32x16 (&acc)[4][2], float* C
                                                    float beta) {
   const int r = lane & 31;
   float* Cz = C + (EPI == G256_SLAB ? (long)blockIdx.y * slab : 0);
+  float bsum[2];  // loaded before any store (see g8_bias)
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int col = tn * G256_BM + wc * 64 + 32 * j + r;
@@ -81,6 +82,12 @@ __device__ __forceinline__ void g256_epilogue_impl(f32x16 (&acc)[4][2], float* C
       if (bias0) badd += bias0[col];
       if (bias1) badd += bias1[col];
     }
+    bsum[j] = badd;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = tn * G256_BM + wc * 64 + 32 * j + r;
+    const float badd = bsum[j];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -220,19 +227,43 @@ __device__ __forceinline__ g8_f32x4 mfma16_bf16(bf16x8_t a, bf16x8_t b, g8_f32x4
 
 enum { G8_STORE = 0, G8_SLAB = 1, G8_STORE_BF16 = 2 };
 
+// 0 + bias0 + bias1 of a lane's 4 column groups (column tn 256 + wc 64 + 16 nt + 4 fq), every load
+// issued before any store: a null test around each load interleaved with the stores made the
+// compiler wait for each load on its own, and each such wait also for every store before it
+__device__ __forceinline__ void g8_bias(const float* bias0, const float* bias1, int tn, int wc, int fq,
+                                        g8_f32x4 (&bsum)[4]) {
+  g8_f32x4 b0[4], b1[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) b0[nt] = b1[nt] = g8_f32x4{0.f, 0.f, 0.f, 0.f};
+  const int col = tn * G256_BM + wc * 64 + 4 * fq;
+  if (bias0) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) b0[nt] = *reinterpret_cast<const g8_f32x4*>(bias0 + col + 16 * nt);
+  }
+  if (bias1) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) b1[nt] = *reinterpret_cast<const g8_f32x4*>(bias1 + col + 16 * nt);
+  }
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    g8_f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (bias0) v += b0[nt];
+    if (bias1) v += b1[nt];
+    bsum[nt] = v;
+  }
+}
+
 template <int EPI>
 __device__ __forceinline__ void g8_epilogue(g8_f32x4 (&acc)[8][4], void* Cv, long ldc, long slab, int tm, int tn,
                                             int wr, int wc, int lane, const float* bias0, const float* bias1,
                                             float beta) {
   const int fr = lane & 15, fq = lane >> 4;
+  g8_f32x4 bsum[4];
+  if (EPI != G8_SLAB) g8_bias(bias0, bias1, tn, wc, fq, bsum);
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
     const int col = tn * G256_BM + wc * 64 + 16 * nt + 4 * fq;
-    g8_f32x4 badd = {0.f, 0.f, 0.f, 0.f};
-    if (EPI != G8_SLAB) {
-      if (bias0) badd += *reinterpret_cast<const g8_f32x4*>(bias0 + col);
-      if (bias1) badd += *reinterpret_cast<const g8_f32x4*>(bias1 + col);
-    }
+    const g8_f32x4 badd = EPI != G8_SLAB ? bsum[nt] : g8_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) {
       const long row = (long)tm * G256_BM + wr * 128 + 16 * mt + fr;
@@ -278,16 +309,14 @@ __device__ __forceinline__ void g8_epilogue_bf16_lds(g8_f32x4 (&acc)[8][4], bf16
                                                      const float* bias1, char* smem) {
   const int fr = lane & 15, fq = lane >> 4;
   char* tile = smem + w * 16384;  // [128 rows][128 B]
+  g8_f32x4 bsum[4];
+  g8_bias(bias0, bias1, tn, wc, fq, bsum);
   __syncthreads();                // every wave's last stage reads retired
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
-    const int col = tn * G256_BM + wc * 64 + 16 * nt + 4 * fq;
-    g8_f32x4 badd = {0.f, 0.f, 0.f, 0.f};
-    if (bias0) badd += *reinterpret_cast<const g8_f32x4*>(bias0 + col);
-    if (bias1) badd += *reinterpret_cast<const g8_f32x4*>(bias1 + col);
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) {
-      const g8_f32x4 v = acc[mt][nt] + badd;
+      const g8_f32x4 v = acc[mt][nt] + bsum[nt];
       const unsigned lo = (unsigned)to_bf(v[0]) | ((unsigned)to_bf(v[1]) << 16);
       const unsigned hi = (unsigned)to_bf(v[2]) | ((unsigned)to_bf(v[3]) << 16);
       *reinterpret_cast<uint2*>(tile + (16 * mt + fr) * 128 + (16 * nt + 4 * fq) * 2) = uint2{lo, hi};
@@ -486,15 +515,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
 // stage of k-tile kt is (kt + base) & 1, base advancing by nk per tile.  Same MFMA order per tile
 // as gemm_bf16_8q_kernel (bit-identical results).
 __device__ __forceinline__ void g8_epilogue_bf16_half(g8_f32x4 (&acc)[8][4], int hlf, bf16_t* C, long ldc, int tm,
-                                                      int tn, int wr, int wc, int lane, const float* bias0,
-                                                      const float* bias1, char* tile) {
+                                                      int tn, int wr, int wc, int lane, const float* bl, char* tile) {
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
     const int col = tn * G256_BM + wc * 64 + 16 * nt + 4 * fq;
-    g8_f32x4 badd = {0.f, 0.f, 0.f, 0.f};
-    if (bias0) badd += *reinterpret_cast<const g8_f32x4*>(bias0 + col);
-    if (bias1) badd += *reinterpret_cast<const g8_f32x4*>(bias1 + col);
+    const g8_f32x4 badd = bl ? *reinterpret_cast<const g8_f32x4*>(bl + col) : g8_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const g8_f32x4 v = acc[4 * hlf + m][nt] + badd;
@@ -511,6 +537,8 @@ __device__ __forceinline__ void g8_epilogue_bf16_half(g8_f32x4 (&acc)[8][4], int
                               8 * c) = v;
   }
 }
+
+#define G8P_BIAS_LDS (32 * 1024)  // LDS bytes for the persistent kernel's bias sums (N <= 8192)
 
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_8qp_kernel(const bf16_t* __restrict__ A, long lda,
@@ -529,6 +557,21 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qp_kernel(const bf16_t* __r
   constexpr int OPB = G256_BM * G256_BK * 2;
   int v = blockIdx.x;
   if (v >= nwg) return;
+  // bf16 out: 0 + bias0 + bias1 of every column staged in LDS behind the two stages (G8P_BIAS_LDS;
+  // the host checks N fits), so the store tail reads it without a global load (a load there waits
+  // for the next tile's fills issued before it, and for the stores)
+  const float* bl = nullptr;
+  if (EPI == G8_STORE_BF16 && (bias0 || bias1)) {
+    float* b = reinterpret_cast<float*>(smem + 2 * 2 * G256_BM * G256_BK * 2);
+    for (int c = tid; c < N; c += 512) {
+      float x = 0.f;
+      if (bias0) x += bias0[c];
+      if (bias1) x += bias1[c];
+      b[c] = x;
+    }
+    __syncthreads();
+    bl = b;
+  }
   int base = 0;
   auto tile_of = [&](int vv, int& tm_, int& tn_) {
     // (row-major tile order: the column-grouped order of the fp32 kernel measured slower here,
@@ -673,8 +716,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qp_kernel(const bf16_t* __r
     }
     if constexpr (EPI == G8_STORE_BF16) {
       char* wt = tail + w * 8192;  // [64 rows][128 B] per wave
-      g8_epilogue_bf16_half(acc, 0, reinterpret_cast<bf16_t*>(C), ldc, tm0, tn0, wr, wc, lane, bias0, bias1, wt);
-      g8_epilogue_bf16_half(acc, 1, reinterpret_cast<bf16_t*>(C), ldc, tm0, tn0, wr, wc, lane, bias0, bias1, wt);
+      g8_epilogue_bf16_half(acc, 0, reinterpret_cast<bf16_t*>(C), ldc, tm0, tn0, wr, wc, lane, bl, wt);
+      g8_epilogue_bf16_half(acc, 1, reinterpret_cast<bf16_t*>(C), ldc, tm0, tn0, wr, wc, lane, bl, wt);
       __syncthreads();  // every wave's reads of the C staging area done before k-tile 1 refills it
     } else {
       g8_epilogue<EPI>(acc, C, ldc, 0L, tm0, tn0, wr, wc, lane, bias0, bias1, beta);

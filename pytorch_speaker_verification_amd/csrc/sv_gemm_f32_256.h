@@ -55,6 +55,46 @@ struct GfStage {
 
 enum { GF_STORE = 0, GF_SLAB = 1 };
 
+// MFMA geometry of a wave's 128 x BN/4 block
+template <int BN, int MF>
+struct GfGeom {
+  static constexpr int WN = BN / 4;                 // wave's columns (64 or 32)
+  static constexpr int TM = 128 / MF, TN = WN / MF;  // MFMA blocks per wave
+  static constexpr int NR = MF == 32 ? 16 : 4;
+  static constexpr int OPA = GF_BM * GF_BK * 4, OPB = BN * GF_BK * 4;  // bytes per operand per stage
+  using Acc = typename std::conditional<MF == 32, f32x16, f32x4>::type;
+};
+
+// bias0 / bias1 of a lane's C columns (column of (j, q): tn BN + wc WN + MF j + c0(q)), loaded in
+// one batch per pointer (zeros for a null one): a null test around each load made the compiler
+// wait for every load on its own (64 serial round trips per tile, each also waiting for the stores
+// issued before it).  Added as (acc + bias0) + bias1, the order of the other fp32 kernels.
+template <int BN, int MF>
+struct GfBias {
+  using Gm = GfGeom<BN, MF>;
+  f32x4 b0[Gm::TN][Gm::NR / 4], b1[Gm::TN][Gm::NR / 4];
+  __device__ __forceinline__ void load(const float* bias0, const float* bias1, int tn, int wc, int fh) {
+    auto col = [&](int j, int q) { return tn * BN + wc * Gm::WN + MF * j + (MF == 32 ? 8 * q + 4 * fh : 4 * fh); };
+    ld(bias0, b0, col);
+    ld(bias1, b1, col);
+  }
+  template <class F>
+  __device__ __forceinline__ static void ld(const float* p, f32x4 (&d)[Gm::TN][Gm::NR / 4], F col) {
+    if (p) {
+#pragma unroll
+      for (int j = 0; j < Gm::TN; ++j)
+#pragma unroll
+        for (int q = 0; q < Gm::NR / 4; ++q) d[j][q] = *reinterpret_cast<const f32x4*>(p + col(j, q));
+    } else {
+#pragma unroll
+      for (int j = 0; j < Gm::TN; ++j)
+#pragma unroll
+        for (int q = 0; q < Gm::NR / 4; ++q) d[j][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __device__ __forceinline__ f32x4 add(f32x4 v, int j, int q) const { return v + b0[j][q] + b1[j][q]; }
+};
+
 template <int BN, int MF, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __restrict__ A, long lda,
                                                              const float* __restrict__ B, long ldb,
@@ -155,6 +195,8 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
   }
   // epilogue: acc[i][j][e] = C[row][4 consecutive cols]
   float* Cz = C + (EPI == GF_SLAB ? (long)sl * slab : 0);
+  GfBias<BN, MF> bias;
+  if (EPI == GF_STORE) bias.load(bias0, bias1, tn, wc, fh);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const long row = (long)tm * GF_BM + wr * 128 + MF * i + fr;
@@ -169,11 +211,147 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
         f32x4 v = f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
         float* dst = Cz + row * ldc + col;
         if (EPI == GF_STORE) {
-          if (bias0) v += *reinterpret_cast<const f32x4*>(bias0 + col);
-          if (bias1) v += *reinterpret_cast<const f32x4*>(bias1 + col);
+          v = bias.add(v, j, q);
           if (beta != 0.f) v += beta * *reinterpret_cast<const f32x4*>(dst);
         }
         *reinterpret_cast<f32x4*>(dst) = v;
       }
+  }
+}
+
+// ---- persistent form (plain stores, no split-K, beta = 0) ----
+// At the K1 shape (4800 tiles of 24 k-tiles) the one-shot launch ran at 0.76 of the fp32 peak
+// against 0.88 for the split-K dW launches of the same k-loop: its CUs finish their tiles in lock
+// step, so every round starts with a cold, chip-wide k-tile-0 fill and ends in a chip-wide store
+// burst (256 KB per CU).  Here one workgroup per CU walks the tiles in the one-shot order (virtual
+// block v = blockIdx.x + i gridDim.x); the next tile's k-tile 0 is DMA'd during this tile's last
+// k-tile (into the stage that k-tile leaves idle), so the next tile starts on landed data and its
+// first k-tile runs while this tile's stores drain.  Same k-loop and summation order as
+// gemm_f32_256_kernel: bit-identical results.
+template <int BN, int MF>
+__global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __restrict__ A, long lda,
+                                                              const float* __restrict__ B, long ldb,
+                                                              float* __restrict__ C, long ldc, int M, int N, int K,
+                                                              const float* __restrict__ bias0,
+                                                              const float* __restrict__ bias1) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using Gm = GfGeom<BN, MF>;
+  constexpr int TM = Gm::TM, TN = Gm::TN, WN = Gm::WN, NR = Gm::NR, OPA = Gm::OPA;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const int tiles_m = M / GF_BM, tiles_n = N / BN;
+  const int nwg = tiles_n * tiles_m;
+  const int nk = K / GF_BK;
+  constexpr int RM = MF == 32 ? 31 : 15;
+  const int fr = lane & RM, fh = MF == 32 ? lane >> 5 : lane >> 4;
+  int v = blockIdx.x;
+  if (v >= nwg || nk <= 0) return;
+  int tm, tn;
+  grouped_tile(xcd_remap(v, nwg), tiles_m, tiles_n, SV_GF_GROUP, tm, tn);
+  GfStage<GF_BM> sa;
+  GfStage<BN> sb;
+  sa.init(A, lda, tm * GF_BM, 0, tid);
+  sb.init(B, ldb, tn * BN, 0, tid);
+  sa.issue(smem, 0, w);
+  sb.issue(smem + OPA, 0, w);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // fragment reads and MFMAs: gemm_f32_256_kernel's, verbatim (same order: bit-identical)
+  constexpr int OPB = Gm::OPB;
+  constexpr int NG = MF == 32 ? GF_BK / 8 : GF_BK / 16;  // k-groups per k-tile
+  int base = 0;
+  auto stage = [&](int kt) { return smem + ((kt + base) & 1) * (OPA + OPB); };
+  typename Gm::Acc acc[TM][TN];
+  auto rd = [&](const char* As, const char* Bs, int g, f32x4 (&a)[TM], f32x4 (&b)[TN]) {
+    const int sl = MF == 32 ? 2 * g + fh : 4 * g + fh;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wr * 128 + MF * i + fr;
+      a[i] = *reinterpret_cast<const f32x4*>(As + row * 128 + gf_phys_slot(row, sl) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wc * WN + MF * j + fr;
+      b[j] = *reinterpret_cast<const f32x4*>(Bs + row * 128 + gf_phys_slot(row, sl) * 16);
+    }
+  };
+  auto mm = [&](const f32x4 (&a)[TM], const f32x4 (&b)[TN]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (MF == 32)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[j][c], a[i][c], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j][c], a[i][c], acc[i][j], 0, 0, 0);
+        }
+  };
+  f32x4 a0[TM], b0[TN], a1[TM], b1[TN];
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < NR; ++e) acc[i][j][e] = 0.f;
+    const int vn = v + gridDim.x;
+    const bool more = vn < nwg;
+    int tmn = 0, tnn = 0;
+    if (more) grouped_tile(xcd_remap(vn, nwg), tiles_m, tiles_n, SV_GF_GROUP, tmn, tnn);
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* As = stage(kt);
+      const char* Bs = As + OPA;
+      if (kt + 1 < nk) {
+        sa.issue(stage(kt + 1), kt + 1, w);
+        sb.issue(stage(kt + 1) + OPA, kt + 1, w);
+      } else if (more) {
+        // the next tile's k-tile 0, into the stage this last k-tile leaves idle (stage pointers
+        // formed here: held across the loop they would take registers)
+        GfStage<GF_BM> na;
+        GfStage<BN> nb;
+        na.init(A, lda, tmn * GF_BM, 0, tid);
+        nb.init(B, ldb, tnn * BN, 0, tid);
+        na.issue(stage(kt + 1), 0, w);
+        nb.issue(stage(kt + 1) + OPA, 0, w);
+      }
+      rd(As, Bs, 0, a0, b0);
+#pragma unroll
+      for (int g = 0; g < NG; g += 2) {
+        rd(As, Bs, g + 1, a1, b1);
+        mm(a0, b0);
+        if (g + 2 < NG) rd(As, Bs, g + 2, a0, b0);
+        mm(a1, b1);
+      }
+      // the next k-tile landed (this wave's DMA) and every wave is done with this one
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    GfBias<BN, MF> bias;
+    bias.load(bias0, bias1, tn, wc, fh);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const long row = (long)tm * GF_BM + wr * 128 + MF * i + fr;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < NR / 4; ++q) {
+          const int col = tn * BN + wc * WN + MF * j + (MF == 32 ? 8 * q + 4 * fh : 4 * fh);
+          const f32x4 val =
+              bias.add(f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]}, j, q);
+#ifdef SV_GF_NOSTORE  // A/B diagnostic builds only: the k-loop's rate without the store traffic
+          if (val[0] != val[0])
+#endif
+          *reinterpret_cast<f32x4*>(C + row * ldc + col) = val;
+        }
+    }
+    if (!more) break;
+    v = vn;
+    tm = tmn;
+    tn = tnn;
+    sa.init(A, lda, tm * GF_BM, 0, tid);
+    sb.init(B, ldb, tn * BN, 0, tid);
+    base = (base + nk) & 1;
   }
 }

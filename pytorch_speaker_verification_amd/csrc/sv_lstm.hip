@@ -49,17 +49,26 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   gemm_mainloop<BM, BN, 256, AK, BKC, TM, TN>(A, lda, RowMapLinear{tm * BM, M}, B, ldb, RowMapLinear{tn * BN, N},
                                               kbeg, kend, lds, tid, wm0, wn0, acc);
   float* Cz = C + (EPI == EPI_SLAB ? (long)blockIdx.y * slab : 0);
+  // bias sums of the lane's columns, loaded before any store (a load between stores waits for
+  // every store issued before it)
+  float bsum[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = tn * BN + wn0 + 32 * j + (lane & 31);
+    float badd = 0.f;
+    if (EPI == EPI_STORE && col < N) {
+      if (bias0) badd += bias0[col];
+      if (bias1) badd += bias1[col];
+    }
+    bsum[j] = badd;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = tn * BN + wn0 + 32 * j + (lane & 31);
       if (col >= N) continue;
-      float badd = 0.f;
-      if (EPI == EPI_STORE) {
-        if (bias0) badd += bias0[col];
-        if (bias1) badd += bias1[col];
-      }
+      const float badd = bsum[j];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = tm * BM + wm0 + 32 * i + acc_row(r, lane);
@@ -154,17 +163,26 @@ __global__ __launch_bounds__(256) void gemm_km_kernel(const float* __restrict__ 
                                                                 RowMapLinear{tn * BN, N}, kbeg, kend, lds, tid, wm0,
                                                                 wn0, acc);
   float* Cz = C + (EPI == EPI_SLAB ? (long)blockIdx.y * slab : 0);
+  // bias sums of the lane's columns, loaded before any store (a load between stores waits for
+  // every store issued before it)
+  float bsum[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = tn * BN + wn0 + BLK * j + (lane & (BLK - 1));
+    float badd = 0.f;
+    if (EPI == EPI_STORE && col < N) {
+      if (bias0) badd += bias0[col];
+      if (bias1) badd += bias1[col];
+    }
+    bsum[j] = badd;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = tn * BN + wn0 + BLK * j + (lane & (BLK - 1));
       if (col >= N) continue;
-      float badd = 0.f;
-      if (EPI == EPI_STORE) {
-        if (bias0) badd += bias0[col];
-        if (bias1) badd += bias1[col];
-      }
+      const float badd = bsum[j];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = tm * BM + wm0 + BLK * i + acc_row(r, lane);
@@ -545,6 +563,9 @@ GemmPlan plan_gemm(int M, int N, int K) {
 #ifndef SV_F32_MF
 #define SV_F32_MF 32  // MFMA shape of the 256-tile kernel (16: v_mfma_f32_16x16x4_f32, A/B builds)
 #endif
+#ifndef SV_GF_PERS
+#define SV_GF_PERS 1  // persistent form of the one-shot launches with more tiles than CUs (0: A/B builds)
+#endif
 int gf256_bn(int N) { return N % 256 == 0 ? 256 : 128; }
 bool gf256_ok(int M, int N, int K, const float* C, long ldc, const float* b0, const float* b1) {
   return M % GF_BM == 0 && N % 128 == 0 && K % GF_BK == 0 && ldc % 4 == 0 &&
@@ -574,7 +595,13 @@ int gemm_f32_256(const float* A, long lda, const float* B, long ldb, float* C, l
   const GemmPlan p = plan_gf256(M, N, K);
   const int tiles = (M / GF_BM) * (N / p.bn);
   if (p.splitk == 1) {
-    if (p.bn == 256)
+    const int cus = sv_stream_cus(stream);
+    if (SV_GF_PERS && p.bn == 256 && beta == 0.f && cus > 0 && tiles > cus && K / GF_BK <= 32) {
+      // more tiles than CUs, short K (K1; dx's 96 k-tiles measured slower persistent, 3.80 vs
+      // 3.73 ms): the persistent form (each tile's k-tile 0 fetched during the previous tile)
+      hipLaunchKernelGGL((gemm_f32_256p_kernel<256, SV_F32_MF>), dim3(cus), dim3(512),
+                         2 * (size_t)(GF_BM + 256) * GF_BK * 4, stream, A, lda, B, ldb, C, ldc, M, N, K, bias0, bias1);
+    } else if (p.bn == 256)
       launch_gf256<256, GF_STORE>(dim3(tiles, 1), stream, A, lda, B, ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1,
                                   beta);
     else

@@ -71,8 +71,8 @@ for sched in ((args.only,) if args.only else ("auto", "per_step")):
         o["bwd_layer_us"] = [round(pb[2 * l].elapsed_time(pb[2 * l + 1]) * 1e3, 1) for l in range(L)]
     net.schedule = sched
     tr = GE2ETrainer(net, GE2ELoss(dev), lr=0.01)
-    N = args.B // 10
-    o["step_ms"] = timed(lambda: tr.step(x, N, 10))
+    M = 10 if args.B % 10 == 0 else 8
+    o["step_ms"] = timed(lambda: tr.step(x, args.B // M, M))
     tr.check()
     o["status"] = int(ps.block[0])
     out[sched] = o

@@ -19,6 +19,7 @@ ap.add_argument("--check", action="store_true", help="bf16: error vs fp32 torch 
                 "and bitwise repeatability over --reps runs (a race screen)")
 ap.add_argument("--shapes", default="Gx,dW,dx")
 ap.add_argument("--lib", default=None, help="load this build of the library instead (A/B builds)")
+ap.add_argument("--bias", action="store_true", help="Gx with the two bias vectors, as K1 runs in the stack")
 args = ap.parse_args()
 if args.lib:
     from pytorch_speaker_verification_amd import _lib
@@ -50,7 +51,9 @@ for name, (M, N, K) in SHAPES.items():
     Bm = torch.randn(N, K, device=dev)
     C = torch.empty(M, N, device=dev)
     w = torch.empty(lib().sv_gemm_f32_workspace(M, N, K) // 4 + 1, device=dev)
-    f = lambda: call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, ptr(w), 0, s)  # noqa: E731
+    b0, b1 = (torch.randn(N, device=dev), torch.randn(N, device=dev)) if args.bias and name == "Gx" else (None, None)
+    pb0, pb1 = (ptr(b0), ptr(b1)) if b0 is not None else (None, None)
+    f = lambda: call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, pb0, pb1, 0.0, ptr(w), 0, s)  # noqa: E731
     us = timeit(f, args.reps)
     res["sv_f32_" + name] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
     if args.torch:
@@ -72,7 +75,7 @@ for name, (M, N, K) in SHAPES.items():
         res["sv_bf16_" + name] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
         if name == "Gx":  # the bf16 path's K1: bf16 output incl. biases
             Cb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-            us = timeit(lambda: call("sv_gemm_bf16_bf", M, N, K, ptr(Ab), K, ptr(Bb), K, ptr(Cb), N, None, None, s),
+            us = timeit(lambda: call("sv_gemm_bf16_bf", M, N, K, ptr(Ab), K, ptr(Bb), K, ptr(Cb), N, pb0, pb1, s),
                         args.reps)
             res["sv_bf16_bfout_Gx"] = [round(us, 1), round(2.0 * M * N * K / us / 1e6, 1)]
             if args.check:

@@ -161,6 +161,48 @@ def test_gemm_f32_bias_and_split_k(M, N, K):
     assert (C - ref).abs().max().item() <= 2e-6 * K ** 0.5 * ref.abs().max().item() + 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(9216, 2048, 96), (16640, 1024, 32), (10240, 3072, 768)])
+def test_gemm_f32_persistent_tiles_two_biases(M, N, K):
+    """More 256 x 256 tiles than CUs: the persistent form (gemm_f32_256p_kernel: next tile's first
+    DMA ahead of the stores, counted wait), both bias vectors as K1 passes them; nk = 1 included."""
+    from pytorch_speaker_verification_amd._lib import call, ptr
+    g = torch.Generator().manual_seed(M + N + K)
+    A, B = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
+    b0, b1 = torch.randn(N, generator=g), torch.randn(N, generator=g)
+    Ad, Bd, b0d, b1d = A.to(DEV), B.to(DEV), b0.to(DEV), b1.to(DEV)
+    C = torch.full((M, N), float("nan"), device=DEV)
+    call("sv_gemm_f32", 1, 1, M, N, K, ptr(Ad), K, ptr(Bd), K, ptr(C), N, ptr(b0d), ptr(b1d), 0.0, None, 0,
+         torch.cuda.current_stream().cuda_stream)
+    ref = A.double() @ B.double().T + b0.double() + b1.double()
+    err = (C.cpu().double() - ref).abs().max().item()
+    assert err <= 2e-6 * K ** 0.5 * ref.abs().max().item() + 1e-5, err
+    # repeatable bit for bit (the counted wait orders every tile's first k-tile)
+    C2 = torch.full_like(C, float("nan"))
+    call("sv_gemm_f32", 1, 1, M, N, K, ptr(Ad), K, ptr(Bd), K, ptr(C2), N, ptr(b0d), ptr(b1d), 0.0, None, 0,
+         torch.cuda.current_stream().cuda_stream)
+    assert torch.equal(C, C2)
+
+
+@pytest.mark.parametrize("M,N,K", [(9216, 2048, 64), (5120, 3072, 768), (10240, 3072, 768)])
+def test_gemm_bf16_bfout_two_biases(M, N, K):
+    """The bf16-output K1 (persistent gemm_bf16_8qp_kernel, bias sums staged in LDS) is the RNE
+    rounding of the fp32-output kernel's sums (same k-loop, same bias order) bit for bit."""
+    from pytorch_speaker_verification_amd._lib import call, lib, ptr
+    g = torch.Generator().manual_seed(M + 5 * N + K)
+    A = torch.randn(M, K, generator=g).bfloat16().to(DEV)
+    B = torch.randn(N, K, generator=g).bfloat16().to(DEV)
+    b0, b1 = torch.randn(N, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV)
+    s = torch.cuda.current_stream().cuda_stream
+    Cb = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    call("sv_gemm_bf16_bf", M, N, K, ptr(A), K, ptr(B), K, ptr(Cb), N, ptr(b0), ptr(b1), s)
+    C = torch.empty(M, N, device=DEV)
+    ws = torch.empty(lib().sv_gemm_bf16_workspace(M, N, K) // 4 + 1, device=DEV)
+    call("sv_gemm_bf16", M, N, K, ptr(A), K, ptr(B), K, ptr(C), N, ptr(b0), ptr(b1), 0.0, ptr(ws), s)
+    assert torch.equal(Cb, C.bfloat16())
+    ref = A.double() @ B.double().T + b0.double() + b1.double()
+    assert (C.double() - ref).abs().max().item() <= 2e-6 * K ** 0.5 * ref.abs().max().item() + 1e-5
+
+
 @pytest.mark.parametrize("M,N,K", [(640, 3072, 768), (3072, 768, 10240), (100, 40, 72), (640, 256, 768),
                                    (1024, 768, 3072), (2560, 3072, 768), (512, 256, 4096)])
 def test_gemm_bf16(M, N, K):
