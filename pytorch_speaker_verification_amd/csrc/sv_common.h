@@ -47,7 +47,16 @@ int sv_persist_db_finalize(const float* dbp, int nrb, int G, float* db_ih, float
     if (e__ != hipSuccess) return (int)e__;                \
   } while (0)
 
-__device__ __forceinline__ float sv_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// The fp32 path's LSTM cell activations (every fp32 cell: per-step K2 / K3 and the persistent
+// recurrences, so the schedules stay bit-identical).  v_exp_f32 + v_rcp_f32 forms: the libm tanhf
+// and an IEEE divide made the persistent forward's cell phase 5.1k cycles per step (of 62.6k;
+// stamps).  Error: sigmoid a few fp32 ulps; tanh within ~1e-7 absolute (the
+// 1 - e cancellation near 0), far inside the fp32 path's tolerances (north_star: 1e-4 on the loss).
+__device__ __forceinline__ float sv_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float sv_tanh(float x) {
+  const float e = __expf(-2.0f * fabsf(x));  // (0, 1]
+  return copysignf((1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e), x);
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

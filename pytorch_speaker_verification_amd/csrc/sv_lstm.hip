@@ -335,10 +335,10 @@ __global__ __launch_bounds__(512) void lstm_step_fwd_v2_kernel(const float* __re
     const float* pr = pre + b * LDP + u;
     const float i = sv_sigmoid(pr[0] + xg[k][0]);
     const float f = sv_sigmoid(pr[FWD_U] + xg[k][1]);
-    const float g = tanhf(pr[2 * FWD_U] + xg[k][2]);
+    const float g = sv_tanh(pr[2 * FWD_U] + xg[k][2]);
     const float o = sv_sigmoid(pr[3 * FWD_U] + xg[k][3]);
     const float c = f * cpv[k] + i * g;
-    const float h = o * tanhf(c);
+    const float h = o * sv_tanh(c);
     gp[0] = i;
     gp[H] = f;
     gp[2 * H] = g;
@@ -425,7 +425,7 @@ __global__ __launch_bounds__(512) void lstm_step_bwd_v2_kernel(
     dh += red[(3 * BWD_BM + b) * LDR + u];
     dh += upv[k];
     const float i = av[k][0], f = av[k][1], g = av[k][2], o = av[k][3];
-    const float tc = tanhf(cv[k]);
+    const float tc = sv_tanh(cv[k]);
     const float dc = dh * o * (1.f - tc * tc) + dcfv[k];
     const float d0 = dc * g * i * (1.f - i), d1 = dc * cpv[k] * f * (1.f - f);
     const float d2 = dc * i * (1.f - g * g), d3 = dh * tc * o * (1.f - o);

@@ -119,7 +119,19 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
   for (int k = 0; k < 2; ++k)
 #pragma unroll
     for (int v = 0; v < 4; ++v) cs[k][v] = 0.f;
+#ifdef SV_PF32_STAMP  // A/B stamp builds only: wave 0's cycles per phase, summed over steps 1 .. T-1
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tl = 0;
+  auto stamp = [&](int i) {
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    if (i >= 0) ph[i] += n - tl;
+    tl = n;
+  };
+#define PF_STAMP(i) if (t > 0) stamp(i)
+#else
+#define PF_STAMP(i)
+#endif
   for (int t = 0; t < T; ++t) {
+    PF_STAMP(-1);
     // an opaque zero: keeps the DMA address arithmetic inside the step (hoisted out of the time
     // loop, the per-lane addresses would hold registers the weights need)
     int z = 0;
@@ -152,6 +164,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
     if (t > 0) {
       if (tid == 0) persist_wait(my_cnt, (unsigned)nub * (unsigned)t, status, limit, 1u);
       __syncthreads();
+      PF_STAMP(0);  // 0: hand-off wait
       dma_chunk(0, 0);
       dma_chunk(1, 1);
 #pragma unroll
@@ -170,6 +183,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
         __builtin_amdgcn_s_barrier();  // ... every wave's part; slot (ch + 2) % 4 was last read at ch - 2
         asm volatile("" ::: "memory");  // (the barrier intrinsic is no memory op: keep the LDS reads behind it)
         __builtin_amdgcn_sched_barrier(0);
+        if (ch == 0) {
+          PF_STAMP(1);  // 1: first chunk's DMA latency
+        }
         const char* cbase = ring + (ch % PF_NB) * PF_CH;
         const char* a0p = cbase + r * 256;
         const char* a1p = cbase + (32 + r) * 256;
@@ -200,6 +216,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
       dma_gx();
       pf_vmwait<0>();
     }
+    PF_STAMP(2);  // 2: k-loop after the first chunk
     __syncthreads();  // every wave done with the ring (pre aliases it) and its gxs part landed
     // pre-activation exchange: wave g's row halves -> pre[row][g 32 + unit]
 #pragma unroll
@@ -225,12 +242,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
       for (int v = 0; v < 4; ++v) {  // the per-step kernel's cell (lstm_step_fwd_v2_kernel)
         const float i_ = sv_sigmoid(p[0][v] + x[0][v]);
         const float f_ = sv_sigmoid(p[1][v] + x[1][v]);
-        const float g_ = tanhf(p[2][v] + x[2][v]);
+        const float g_ = sv_tanh(p[2][v] + x[2][v]);
         const float o_ = sv_sigmoid(p[3][v] + x[3][v]);
         const float c = f_ * cs[k][v] + i_ * g_;
         cs[k][v] = c;
         cv[v] = c;
-        hv[k][v] = o_ * tanhf(c);
+        hv[k][v] = o_ * sv_tanh(c);
         p[0][v] = i_;
         p[1][v] = f_;
         p[2][v] = g_;
@@ -240,6 +257,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
       for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4*>(pre + row * LDP + q * PF_U + 4 * quad) = p[q];
       *reinterpret_cast<f32x4*>(gxs + row * (4 * PF_U) + 4 * quad) = cv;
     }
+    PF_STAMP(3);  // 3: exchange + cell
     // the hand-off: h_t into h_tm[t + 1], 16-B sc1 stores, drained before the arrival
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -255,6 +273,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
     __syncthreads();
     if (tid == 0 && persist_arrive_ok(fault, t == 0))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    PF_STAMP(4);  // 4: hand-off stores + drain + arrival
     // off the chain: activations, c, h^T of step t
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -283,7 +302,15 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
         }
       }
     }
+    PF_STAMP(5);  // 5: off-chain stores
   }
+#ifdef SV_PF32_STAMP
+  if (tid == 0 && blockIdx.x < SV_NSTAMP_WG / 2) {
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(status + SV_SYNC_STAMP) + blockIdx.x * SV_NSTAMP;
+    for (int i = 0; i < 6; ++i) st[i] = ph[i];
+  }
+#endif
+#undef PF_STAMP
 }
 
 // ============================================================================
@@ -429,7 +456,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
       for (int v = 0; v < 4; ++v) {  // the per-step kernel's cell backward (lstm_step_bwd_v2_kernel)
         const float d = dh[v];
         const float i_ = a4[0][v], f_ = a4[1][v], g_ = a4[2][v], o_ = a4[3][v];
-        const float tc = tanhf(cv[hf][v]);
+        const float tc = sv_tanh(cv[hf][v]);
         const float dc = d * o_ * (1.f - tc * tc) + dcf[hf][v];
         dq[0][v] = dc * g_ * i_ * (1.f - i_);
         dq[1][v] = dc * cpv[v] * f_ * (1.f - f_);

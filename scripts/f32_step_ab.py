@@ -24,6 +24,8 @@ ap.add_argument("--B", type=int, default=640)
 ap.add_argument("--T", type=int, default=160)
 ap.add_argument("--lib", default=None)
 ap.add_argument("--only", default=None, help="one schedule only")
+ap.add_argument("--stamps", action="store_true", help="a -DSV_PF32_STAMP build: the persistent forward's "
+                "cycles per step by phase (last forward layer launch, mean and max over workgroups)")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 torch.manual_seed(0)
@@ -75,6 +77,18 @@ for sched in ((args.only,) if args.only else ("auto", "per_step")):
     o["step_ms"] = timed(lambda: tr.step(x, args.B // M, M))
     tr.check()
     o["status"] = int(ps.block[0])
+    if args.stamps:
+        # u64 [SV_NSTAMP_WG][SV_NSTAMP] at word 32 + 4 * 64 * 32 of the sync block, written by the
+        # last forward launch: wait, first-chunk DMA, rest of k-loop, exchange + cell, hand-off, off-chain
+        ops.embedder_forward(x, layers, wp, bp, status=ps, schedule=sched)
+        torch.cuda.synchronize()
+        stamp0 = 32 + 4 * 64 * 32
+        nwg = 24 * ((args.B + 63) // 64)
+        st = ps.block[stamp0:stamp0 + 2 * 1024 * 8].view(torch.int64).view(1024, 8)[:nwg, :6].cpu().double()
+        st = st / (args.T - 1)
+        names = ["wait", "dma0", "kloop", "cell", "handoff", "offchain"]
+        o["fwd_stamps_per_step_mean"] = {k: round(float(v), 1) for k, v in zip(names, st.mean(0))}
+        o["fwd_stamps_per_step_max"] = {k: round(float(v), 1) for k, v in zip(names, st.max(0).values)}
     out[sched] = o
     print(json.dumps({sched: o}), flush=True)
 print(json.dumps(out), flush=True)
