@@ -47,6 +47,29 @@ from .ops import (clip_sgd_step_, embedder_backward, embedder_backward_bf16, emb
 from .sharded_ge2e import ShardedGE2E
 
 
+def bf16_row_chunks(B, H, schedule="auto"):
+    """Row ranges of the bf16 LSTM stack.  A batch too large for the co-resident persistent
+    recurrences (sv_persist_fwd_ok / sv_persist_bwd_ok: B > 672 at H = 768, e.g. c5 split over 2
+    GPUs = 1280 rows per rank) runs as k equal row chunks that each fit, one after another (every
+    chunk's recurrences have the whole chip), instead of the per-step kernels (c5 at 2 GPUs: 48.3
+    ms per step on those, profiles/r03_v6_rank_shapes.txt).  Rows are independent in the LSTM, so
+    only the weight gradients change: their sums over rows split into k partial sums (bf16-level,
+    tested against the bf16 oracle).  Under schedule 'auto' only; [(0, B)] when B fits or no
+    chunking helps."""
+    from ._lib import lib
+    if schedule != "auto" or B <= 0:
+        return [(0, B)]
+    L = lib()
+    fits = lambda b: bool(L.sv_persist_fwd_ok(b, H)) and bool(L.sv_persist_bwd_ok(b, H))  # noqa: E731
+    if fits(B):
+        return [(0, B)]
+    for k in range(2, 9):
+        c = (B + k - 1) // k
+        if fits(c):
+            return [(i * c, min(B, (i + 1) * c)) for i in range(k) if i * c < B]
+    return [(0, B)]
+
+
 class GE2ETrainer:
     def __init__(self, embedder, ge2e_loss, lr=0.01, clip_net=3.0, clip_wb=1.0, group=None, write_grads=True):
         self.net = embedder
@@ -140,7 +163,15 @@ class GE2ETrainer:
         bf16 = getattr(net, "precision", "f32") == "bf16"
         products = getattr(net, "f32_products", "mfma_f32")
         schedule = getattr(net, "schedule", "auto")
-        if bf16:
+        chunks = bf16_row_chunks(x.shape[0], layers[0][1].shape[1], schedule) if bf16 else [(0, x.shape[0])]
+        if bf16 and len(chunks) > 1:
+            xf = x.float()
+            outs = [embedder_forward_bf16(xf[r0:r1].contiguous(), layers, w_p, b_p, status=self.status,
+                                          probe=probe.get("fwd") if i == 0 else None, schedule=schedule)
+                    for i, (r0, r1) in enumerate(chunks)]
+            emb = torch.cat([o[0] for o in outs])
+            st = [o[1] for o in outs]
+        elif bf16:
             emb, st = embedder_forward_bf16(x.float().contiguous(), layers, w_p, b_p, status=self.status,
                                             probe=probe.get("fwd"), schedule=schedule)
         else:
@@ -173,7 +204,27 @@ class GE2ETrainer:
                     comm.wait_event(event)
                 with torch.cuda.stream(comm):  # SUM, never mean (SURVEY §7 hard part 4)
                     works.append(dist.all_reduce(self.flat_g[lo:hi], group=self.group, async_op=True))
-        if bf16:
+        if bf16 and len(chunks) > 1:
+            # chunk 0 writes the gradient buffer, the others a scratch copy added into it; the
+            # buckets go once the sum is complete
+            dEf = dE.view(N * M, -1)
+            if getattr(self, "_gtmp", None) is None or self._gtmp.shape != self.flat_g.shape:
+                self._gtmp = torch.zeros_like(self.flat_g)
+                off, self._gtmp_views = 0, []
+                for g in self.grad_views:
+                    self._gtmp_views.append(self._gtmp[off:off + g.numel()].view_as(g))
+                    off += g.numel()
+            for i, (r0, r1) in enumerate(chunks):
+                embedder_backward_bf16(st[i], dEf[r0:r1], layers, w_p,
+                                       grads=self.grad_views if i == 0 else self._gtmp_views,
+                                       status=self.status, probe=probe.get("bwd") if i == 0 else None,
+                                       schedule=schedule)
+                if i > 0:
+                    self.flat_g[:self.n].add_(self._gtmp[:self.n])
+            if ready:
+                for k in range(len(self.buckets) - 1, -1, -1):
+                    ready(k, None)
+        elif bf16:
             embedder_backward_bf16(st, dE.view(N * M, -1), layers, w_p, grads=self.grad_views, grad_ready=ready,
                                    status=self.status, probe=probe.get("bwd"), schedule=schedule)
         else:

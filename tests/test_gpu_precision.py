@@ -120,3 +120,16 @@ def test_bf16_vs_fp32_gap_matches_oracle_gap():
     ora_gap = float((o16 - o32).abs().max())
     _check("c4_rank.hip_bf16_fp32_emb_gap", hip_gap, 2e-2)
     _check("c4_rank.gap_mismatch", abs(hip_gap - ora_gap), 3e-4)
+
+
+def test_c5_two_rank_shape_bf16_row_chunks_against_oracle():
+    """c5 split over 2 GPUs: 128 x 10 = 1280 rows per rank at T = 180, more than the co-resident
+    persistent recurrences take (<= 672 rows), so the trainer runs the bf16 stack as two 640-row
+    chunks on the persistent kernels and sums their weight gradients (trainer.bf16_row_chunks);
+    against the bf16 oracle run on the GPU."""
+    from pytorch_speaker_verification_amd.trainer import bf16_row_chunks
+    dims, N, M, T = (40, 768, 3, 256), 128, 10, 180
+    assert bf16_row_chunks(N * M, 768) == [(0, 640), (640, 1280)]
+    assert bf16_row_chunks(640, 768) == [(0, 640)] and bf16_row_chunks(1280, 768, "per_step") == [(0, 1280)]
+    _compare("c5_2rank_chunked", dims, N, M, T, 5151, dict(emb=5e-3, loss=5e-4, grad=5e-2, param=2e-5),
+             oracle_device=DEV)
