@@ -690,9 +690,10 @@ def main():
     if rank == 0 and not args.no_extras:
         ms_g, fl_g, by_g = time_gemm_kernel(160 * 640, 4 * H, H, dev)
         out["roofline_gemm"] = dict(roofline_entry(
-            f"gemm_f32_256_kernel<256,32,0> (K1/dW/dx NT GEMM, 256x256 LDS-DMA tile, fp32 MFMA 32x32x2), K1 shape "
+            f"gemm_f32_256p_kernel<256,32> (K1/dx NT GEMM: persistent, one workgroup per CU walking 256x256 LDS-DMA "
+            f"tiles, fp32 MFMA 32x32x2), K1 shape "
             f"M={160 * 640} N={4 * H} K={H}",
-            fl_g, ms_g, MI355X_FP32_MFMA_TFLOPS, pmc_traffic("gemm_f32_256_kernel<256,32,0>"), 5,
+            fl_g, ms_g, MI355X_FP32_MFMA_TFLOPS, pmc_traffic("gemm_f32_256p_kernel<256,32>@K1"), 5,
             "isolated launches, HIP events on its stream"), algorithmic_bytes=by_g)
         ms_k, fl_k = time_step_kernel(640, H, dev)
         out["roofline_step_kernel"] = roofline_entry(

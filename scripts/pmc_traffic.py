@@ -36,6 +36,12 @@ GEMM = {
                                          4 * (T_ * B_ * 4 * H_ + 4 * H_ * H_ + T_ * B_ * H_)),
     "gemm_f32_256_kernel<256,32,1>@dW": ("void gemm_f32_256_kernel<256, 32, 1>", None,
                                          4 * (T_ * B_ * 4 * H_ + T_ * B_ * H_ + 4 * H_ * H_)),
+    # the persistent fp32 NT GEMM (one workgroup per CU: K1 and dx have the same grid) -- told apart
+    # by launch order: gemm_traffic.py runs 1 + REPS launches of K1 (Gx), later 1 + REPS of dx
+    "gemm_f32_256p_kernel<256,32>@K1": ("void gemm_f32_256p_kernel<256, 32>", None,
+                                        4 * (T_ * B_ * H_ + 4 * H_ * H_ + T_ * B_ * 4 * H_), (0, 4)),
+    "gemm_f32_256p_kernel<256,32>@dx": ("void gemm_f32_256p_kernel<256, 32>", None,
+                                        4 * (T_ * B_ * 4 * H_ + 4 * H_ * H_ + T_ * B_ * H_), (4, 8)),
     "gemm_bf16_8qp_kernel<2>@K1": ("void gemm_bf16_8qp_kernel<2>", None,
                                    2 * (T_ * B_ * H_ + 4 * H_ * H_ + T_ * B_ * 4 * H_)),
     "gemm_bf16_8q_kernel<0,0>@dx": ("void gemm_bf16_8q_kernel<0, 0>", None,
@@ -53,15 +59,26 @@ def _grid(r):
 
 
 def per_launch(path, counter, families):
-    acc = {}
-    for r in csv.DictReader(open(path)):
+    """Average counter value per launch of each family; a spec's optional 4th item (lo, hi) keeps only
+    the family's matching launches lo .. hi - 1 in dispatch order."""
+    acc, seen = {}, {}
+    rows = list(csv.DictReader(open(path)))
+    if rows and "Dispatch_Id" in rows[0]:
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    for r in rows:
         if r["Counter_Name"] != counter:
             continue
         for key, spec in families.items():
             pre, grid = (spec, None) if isinstance(spec, str) else spec[:2]
             if r["Kernel_Name"].startswith(pre) and (grid is None or _grid(r) == grid):
+                i = seen.get(pre, 0) if len(spec) > 3 and not isinstance(spec, str) else None
+                if i is not None and not (spec[3][0] <= i < spec[3][1]):
+                    continue
                 s, n = acc.get(key, (0.0, 0))
                 acc[key] = (s + float(r["Counter_Value"]), n + 1)
+        for pre in {(sp if isinstance(sp, str) else sp[0]) for sp in families.values()}:
+            if r["Kernel_Name"].startswith(pre):
+                seen[pre] = seen.get(pre, 0) + 1
     return {k: s / n for k, (s, n) in acc.items()}
 
 
@@ -69,7 +86,8 @@ def gemm_main(d, data):
     fs = glob.glob(os.path.join(d, "fetch*", "**", "*counter_collection.csv"), recursive=True)
     ws = glob.glob(os.path.join(d, "write*", "**", "*counter_collection.csv"), recursive=True)
     fetch, write = per_launch(fs[0], "FETCH_SIZE", GEMM), per_launch(ws[0], "WRITE_SIZE", GEMM)
-    for k, (_, _, alg) in GEMM.items():
+    for k, spec in GEMM.items():
+        alg = spec[2]
         if k in fetch and k in write:
             hbm = int(1024 * (2 * fetch[k] + write[k]))
             data[k] = {"FETCH_SIZE_KiB": round(fetch[k], 1), "WRITE_SIZE_KiB": round(write[k], 1),

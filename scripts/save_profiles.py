@@ -59,8 +59,11 @@ with open(os.path.join(prof, f"{tag}_roofline_check.txt"), "w") as f:
     rg = pf["f32"].get("roofline_gemm")
     if rg:
         # bench.py times 5 isolated launches at the K1 shape after the steps: the last 5 of that grid
-        d = durations("f32", "void gemm_f32_256_kernel<256, 32, 0>", (T * B // 256) * (4 * H // 256) * 512)
-        line(f, "roofline_gemm: gemm_f32_256_kernel<256,32,0> at the K1 shape, the 5 isolated launches", d[-5:],
+        # (the 5 launches right before roofline_step_kernel's first lstm_step_fwd_v2_kernel: the
+        # persistent GEMM's grid is one workgroup per CU for every shape, and d-vector runs follow)
+        t_k2 = min(st for st, _ in durations("f32", "void lstm_step_fwd_v2_kernel", start=True))
+        d = [us for st, us in durations("f32", "void gemm_f32_256p_kernel<256, 32>", start=True) if st < t_k2]
+        line(f, "roofline_gemm: gemm_f32_256p_kernel<256,32> at the K1 shape, the 5 isolated launches", d[-5:],
              rg["avg_launch_us"], 2.0 * T * B * 4 * H * H)
     for key, pre in (("roofline", "void lstm_persist3_bwd_bf16_kernel"),
                      ("roofline_fwd", "void lstm_persist")):
