@@ -298,6 +298,9 @@ int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* con
 size_t sv_sync_size(void);
 int sv_persist_fwd_ok(int B, int H);
 int sv_persist_bwd_ok(int B, int H);
+/* the bf16 layer-wavefront schedule (all L layers in one forward and one backward launch) fits
+ * B rows on the current device (L = 3, F = 40, H = 768: B <= 96 on 256 CUs) */
+int sv_wave_ok(int L, int T, int B, int F, int H);
 size_t sv_persist_bwd_scratch(int T, int B, int H);
 int sv_status_poison(const void* sync, float* x, int n, hipStream_t stream);
 /* data-parallel status agreement (a rank whose recurrence timed out must stop every rank's

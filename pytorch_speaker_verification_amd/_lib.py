@@ -106,6 +106,7 @@ SIGNATURES = {
     "sv_sync_size": (_c_size_t, []),
     "sv_persist_fwd_ok": (_c_int, [_c_int, _c_int]),
     "sv_persist_bwd_ok": (_c_int, [_c_int, _c_int]),
+    "sv_wave_ok": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "sv_persist_bwd_scratch": (_c_size_t, [_c_int, _c_int, _c_int]),
     "sv_status_poison": (_c_int, [_P, _P, _c_int, _P]),
     "sv_status_to_flag": (_c_int, [_P, _P, _P]),

@@ -904,6 +904,10 @@ int sv_persist_bwd_fits(int B, int H, int cus) {
 }
 // ... on the current device
 extern "C" int sv_persist_fwd_ok(int B, int H) { return sv_persist_fwd_fits(B, H, current_cus()); }
+extern "C" int sv_wave_ok(int L, int T, int B, int F, int H) {
+  const int cus = current_cus();
+  return sv_wave_fwd_fits(L, T, B, F, H, cus) && sv_wave_bwd_fits(L, B, H, cus);
+}
 
 namespace {
 // row tile of the W-stationary kernels: 32 rows when twice the 64-row grid still fits on the

@@ -47,20 +47,27 @@ from .ops import (clip_sgd_step_, embedder_backward, embedder_backward_bf16, emb
 from .sharded_ge2e import ShardedGE2E
 
 
-def bf16_row_chunks(B, H, schedule="auto"):
+def bf16_row_chunks(B, H, schedule="auto", L=3, T=160, F=40):
     """Row ranges of the bf16 LSTM stack.  A batch too large for the co-resident persistent
     recurrences (sv_persist_fwd_ok / sv_persist_bwd_ok: B > 672 at H = 768, e.g. c5 split over 2
     GPUs = 1280 rows per rank) runs as k equal row chunks that each fit, one after another (every
     chunk's recurrences have the whole chip), instead of the per-step kernels (c5 at 2 GPUs: 48.3
     ms per step on those, profiles/r03_v6_rank_shapes.txt).  Rows are independent in the LSTM, so
     only the weight gradients change: their sums over rows split into k partial sums (bf16-level,
-    tested against the bf16 oracle).  Under schedule 'auto' only; [(0, B)] when B fits or no
-    chunking helps."""
+    tested against the bf16 oracle).  A batch up to twice what the one-launch layer wavefront takes
+    (sv_wave_ok: 96 rows) runs as two wavefront halves: c4 over 4 GPUs, 160 rows, otherwise takes the
+    per-layer persistent kernels on 120 of the 256 CUs.  Under schedule 'auto' only; [(0, B)] when B
+    fits or no chunking helps."""
     from ._lib import lib
     if schedule != "auto" or B <= 0:
         return [(0, B)]
-    L = lib()
-    fits = lambda b: bool(L.sv_persist_fwd_ok(b, H)) and bool(L.sv_persist_bwd_ok(b, H))  # noqa: E731
+    lb = lib()
+    wave = lambda b: bool(lb.sv_wave_ok(L, T, b, F, H))  # noqa: E731
+    fits = lambda b: bool(lb.sv_persist_fwd_ok(b, H)) and bool(lb.sv_persist_bwd_ok(b, H))  # noqa: E731
+    if wave(B):
+        return [(0, B)]
+    if wave((B + 1) // 2):
+        return [(0, (B + 1) // 2), ((B + 1) // 2, B)]
     if fits(B):
         return [(0, B)]
     for k in range(2, 9):
@@ -163,7 +170,8 @@ class GE2ETrainer:
         bf16 = getattr(net, "precision", "f32") == "bf16"
         products = getattr(net, "f32_products", "mfma_f32")
         schedule = getattr(net, "schedule", "auto")
-        chunks = bf16_row_chunks(x.shape[0], layers[0][1].shape[1], schedule) if bf16 else [(0, x.shape[0])]
+        chunks = (bf16_row_chunks(x.shape[0], layers[0][1].shape[1], schedule, len(layers), x.shape[1], x.shape[2])
+                  if bf16 else [(0, x.shape[0])])
         if bf16 and len(chunks) > 1:
             xf = x.float()
             outs = [embedder_forward_bf16(xf[r0:r1].contiguous(), layers, w_p, b_p, status=self.status,

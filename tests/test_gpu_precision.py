@@ -129,7 +129,20 @@ def test_c5_two_rank_shape_bf16_row_chunks_against_oracle():
     against the bf16 oracle run on the GPU."""
     from pytorch_speaker_verification_amd.trainer import bf16_row_chunks
     dims, N, M, T = (40, 768, 3, 256), 128, 10, 180
-    assert bf16_row_chunks(N * M, 768) == [(0, 640), (640, 1280)]
+    assert bf16_row_chunks(N * M, 768, T=T) == [(0, 640), (640, 1280)]
     assert bf16_row_chunks(640, 768) == [(0, 640)] and bf16_row_chunks(1280, 768, "per_step") == [(0, 1280)]
+    # the layer wavefront: 80 rows whole, 160 rows as two halves, 320 rows on the persistent kernels
+    assert bf16_row_chunks(80, 768) == [(0, 80)] and bf16_row_chunks(160, 768) == [(0, 80), (80, 160)]
+    assert bf16_row_chunks(320, 768) == [(0, 320)]
     _compare("c5_2rank_chunked", dims, N, M, T, 5151, dict(emb=5e-3, loss=5e-4, grad=5e-2, param=2e-5),
+             oracle_device=DEV)
+
+
+def test_c4_four_rank_shape_bf16_wavefront_halves_against_oracle():
+    """c4 split over 4 GPUs: 16 x 10 = 160 rows per rank at T = 160, run as two 80-row halves on the
+    one-launch layer wavefront (trainer.bf16_row_chunks); against the bf16 oracle on the GPU."""
+    from pytorch_speaker_verification_amd.trainer import bf16_row_chunks
+    dims, N, M, T = (40, 768, 3, 256), 16, 10, 160
+    assert bf16_row_chunks(N * M, 768, T=T) == [(0, 80), (80, 160)]
+    _compare("c4_4rank_halves", dims, N, M, T, 4141, dict(emb=5e-3, loss=2e-3, grad=5e-2, param=2e-5),
              oracle_device=DEV)
