@@ -297,7 +297,7 @@ def dvector_inference(net, dev, S=16384, T=24, reps=3):
     """d-vector extraction (dvector_create.py:96-101): S windows of T = 24 frames
     (240 ms at a 10 ms hop) embedded by the trained net, no autograd state (dvector.embed_windows,
     fp32 MFMA path), windows already in HBM; MIOpen nn.LSTM + Linear on the same windows beside it."""
-    from pytorch_speaker_verification_amd.dvector import embed_windows
+    from pytorch_speaker_verification_amd.dvector import GraphedEmbedder, embed_windows
     F, H, L, P = DIMS
     g = torch.Generator(device="cpu").manual_seed(24)
     xw = torch.randn(S, T, F, generator=g).to(dev)
@@ -337,6 +337,11 @@ def dvector_inference(net, dev, S=16384, T=24, reps=3):
             peak = MI355X_BF16_MFMA_TFLOPS if prec == "bf16" else MI355X_FP32_MFMA_TFLOPS
             per_file[prec] = {"ms_per_call": round(msf, 3), "windows_per_sec": round(Sf / (msf * 1e-3), 1),
                               "mfma_frac": round(flops_f / (msf * 1e-3) / 1e12 / peak, 4)}
+            # the same call replayed from a HIP graph (dvector.GraphedEmbedder: one launch per call)
+            ge = GraphedEmbedder(net, precision=prec)
+            msg = _timed(lambda: ge(xf), dev, max(reps, 10))
+            per_file[prec]["graph"] = {"ms_per_call": round(msg, 3), "windows_per_sec": round(Sf / (msg * 1e-3), 1),
+                                       "mfma_frac": round(flops_f / (msg * 1e-3) / 1e12 / peak, 4)}
         res["per_file_call"] = per_file
         try:
             lstm = torch.nn.LSTM(F, H, num_layers=L, batch_first=True).to(dev)

@@ -88,6 +88,75 @@ def embed_windows(net, windows, batch=None, precision="f32", path=None):
     return torch.cat(out) if out else torch.zeros((0, net.projection.weight.shape[0]), device=dev)
 
 
+class GraphedEmbedder:
+    """Per-file d-vector calls (dvector_create.py:96-101: one file's windows per
+    ``embedder_net(windows)`` call, tens to hundreds of windows) replayed from HIP graphs.  Such a
+    call is bound by its ~20 kernel launches and their host work (~0.3 ms), not by the kernels;
+    here the whole forward -- frame transpose, casts, input projections, the recurrences, the
+    projection and norm -- is captured once per window-count bucket (S rounded up to `bucket`;
+    padding rows are zeros, rows are independent, and only the first S are returned) and each
+    call is one copy in, one graph launch, one copy out.  Same kernels and numerics as
+    embed_windows(..., batch=S); the weights are read through their pointers at every replay
+    (in-place updates are seen; a module whose parameters were re-allocated is re-captured).
+    precision: "f32" or "bf16".  Raises PersistentRecurrenceError like embed_windows."""
+
+    def __init__(self, net, precision="bf16", bucket=32, max_windows=640):
+        if precision not in ("f32", "bf16"):
+            raise ValueError(f"precision must be 'f32' or 'bf16', got {precision!r}")
+        self.net, self.precision, self.bucket, self.max_windows = net, precision, bucket, max_windows
+        self._graphs = {}
+
+    def _key(self, S, T, F):
+        ptrs = tuple(p.data_ptr() for p in self.net.parameters())
+        return (-(-S // self.bucket) * self.bucket, T, F, ptrs)
+
+    def _capture(self, Sp, T, F, dev):
+        from ._lib import PersistStatus
+        layers = self.net.LSTM_stack.layer_params()
+        wp, bp = self.net.projection.weight, self.net.projection.bias
+        status = PersistStatus(dev)  # caller-owned: nothing polled or allocated during the capture
+        x = torch.zeros((Sp, T, F), dtype=torch.float32, device=dev)
+
+        def fwd():
+            if self.precision == "bf16":
+                return embedder_forward_bf16(x, layers, wp, bp, save=False, status=status)[0]
+            return embedder_forward(x, layers, wp, bp, save=False, status=status)[0]
+
+        side = torch.cuda.Stream(dev)  # warm-up off the capture (allocator, lazy init)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            fwd()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            emb = fwd()
+        return g, x, emb, status
+
+    @torch.no_grad()
+    def __call__(self, windows):
+        dev = next(self.net.parameters()).device
+        x = torch.as_tensor(windows, dtype=torch.float32)
+        S, T, F = x.shape
+        if S == 0:
+            return torch.zeros((0, self.net.projection.weight.shape[0]), device=dev)
+        if S > self.max_windows:  # a long file: the batched path
+            return embed_windows(self.net, x, precision=self.precision)
+        key = self._key(S, T, F)
+        if key not in self._graphs:
+            self._graphs = {k: v for k, v in self._graphs.items() if k[3] == key[3]}  # drop stale weights
+            self._graphs[key] = self._capture(key[0], T, F, dev)
+        g, xs, emb, status = self._graphs[key]
+        xs[:S].copy_(x.to(dev, non_blocking=True))
+        if S < xs.shape[0]:
+            xs[S:].zero_()
+        g.replay()
+        out = emb[:S].clone()
+        status.arm()
+        status.poll(wait=True)
+        return out
+
+
 def partitions(n_windows, win_s=0.24, hop_s=0.12, seg_s=0.401):
     """[start, end) window ranges averaged into one segment (dvector_create.py:56-69): a window i
     joins segment j while it ends (i*hop + win) before j*seg; the loop's else appends the last."""

@@ -146,3 +146,39 @@ def test_dvec_path_dimension_rule():
     assert not dvector.dvec_ok(80, 768)   # x part wider than one 64-column k-tile
     assert not dvector.dvec_ok(40, 96)    # 4H = 384: not whole 256-column tiles
     assert dvector.dvec_ok(40, 64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_graphed_per_file_calls_match_embed_windows(precision):
+    """Per-file calls replayed from HIP graphs (dvector.GraphedEmbedder): the same kernels as
+    embed_windows(..., batch=S), so a file whose window count is a whole bucket is bit-identical;
+    one padded up to its bucket (zero rows, rows independent) agrees to fp32 rounding; repeated
+    replays of one graph with new windows stay right; an in-place weight update is seen."""
+    import recipe
+    from conftest import model_dims
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    dims = (40, 768, 3, 256)
+    sd = recipe.make_weights(19, *dims, scale=2.0)
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    net = net.cuda()
+    ge = dvector.GraphedEmbedder(net, precision=precision)
+    for seed, S in ((20, 128), (21, 128), (22, 100), (23, 37)):
+        x = recipe.make_frames(seed, S, 24, 40)
+        got = ge(x).cpu()
+        ref = dvector.embed_windows(net, x, batch=S, precision=precision).cpu()
+        assert got.shape == ref.shape
+        dev = float((got - ref).abs().max())
+        print(f"\nMEASURED graphed_{precision}_S{S} {dev:.3e}")
+        if S % 32 == 0:
+            assert dev == 0.0, (S, dev)
+        else:
+            assert dev <= (5e-3 if precision == "bf16" else 1e-5), (S, dev)
+    with torch.no_grad():
+        net.projection.bias.add_(0.5)
+    x = recipe.make_frames(24, 128, 24, 40)
+    assert float((ge(x).cpu() - dvector.embed_windows(net, x, batch=128, precision=precision).cpu()).abs().max()) == 0.0
