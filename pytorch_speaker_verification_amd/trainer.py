@@ -216,7 +216,8 @@ class GE2ETrainer:
             # chunk 0 writes the gradient buffer, the others a scratch copy added into it; the
             # buckets go once the sum is complete
             dEf = dE.view(N * M, -1)
-            if getattr(self, "_gtmp", None) is None or self._gtmp.shape != self.flat_g.shape:
+            if (getattr(self, "_gtmp", None) is None or self._gtmp.shape != self.flat_g.shape
+                    or self._gtmp.device != self.flat_g.device):
                 self._gtmp = torch.zeros_like(self.flat_g)
                 off, self._gtmp_views = 0, []
                 for g in self.grad_views:
