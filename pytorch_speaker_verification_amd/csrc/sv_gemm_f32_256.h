@@ -95,12 +95,26 @@ struct GfBias {
   __device__ __forceinline__ f32x4 add(f32x4 v, int j, int q) const { return v + b0[j][q] + b1[j][q]; }
 };
 
-template <int BN, int MF, int EPI>
+// A operand in the fp32 persistent backward's fragment-order hand-off layout (sv_persist_f32.hip,
+// dgf): row m = t * bsl + b of A is (slot t, batch row b); its 32-row group (row block b / 64, half
+// (b / 32) & 1) and 8-wide k-group of gate q form one contiguous KB [64 lanes][4] -- lane r + 32 h
+// holds row r at k 8 kg + 4 h .. + 3, exactly this kernel's 32x32x2 A fragment -- at slot t, block
+// ((b / 64) * 4 + q) * 2 + half, k-group kg.  A 256 x 32 k-tile is 8 row groups x 4 k-groups = 32
+// whole KB, copied to LDS as is (wave w: row group w); every fragment read is lane-linear.
+struct GfAFrag {
+  const float* base;  // dgf
+  long fs;            // slot size (floats)
+  int bsl, kh;        // batch rows per slot (a multiple of 32), gate width H (k per gate)
+};
+
+template <int BN, int MF, int EPI, int AF = 0>
 __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __restrict__ A, long lda,
                                                              const float* __restrict__ B, long ldb,
                                                              float* __restrict__ C, long ldc, long slab, int M, int N,
                                                              int K, int kchunk, const float* __restrict__ bias0,
-                                                             const float* __restrict__ bias1, float beta) {
+                                                             const float* __restrict__ bias1, float beta,
+                                                             GfAFrag af = GfAFrag{}) {
+  static_assert(!AF || MF == 32, "fragment-order A: the 32x32x2 fragment layout");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int WN = BN / 4;                 // wave's columns (64 or 32)
   constexpr int TM = 128 / MF, TN = WN / MF;  // MFMA blocks per wave
@@ -126,9 +140,27 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
   const int wr = w >> 2, wc = w & 3;
   GfStage<GF_BM> sa;
   GfStage<BN> sb;
-  sa.init(A, lda, tm * GF_BM, kbeg, tid);
+  if constexpr (!AF) sa.init(A, lda, tm * GF_BM, kbeg, tid);
   sb.init(B, ldb, tn * BN, kbeg, tid);
   auto stage = [&](int kt) { return smem + (kt & 1) * (OPA + OPB); };
+  // fragment-order A: wave w copies row group w's 4 k-groups of each k-tile (KB c = 4 w + i)
+  long af_row = 0;
+  if constexpr (AF) {
+    const int m0 = tm * GF_BM + 32 * w, t = m0 / af.bsl, b = m0 % af.bsl;
+    af_row = (long)t * af.fs + (long)((b / 64) * 8 + ((b / 32) & 1)) * (af.kh / 8 * 256) + lane * 4;
+  }
+  auto issue_a = [&](char* lds, int kt) {
+    if constexpr (AF) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = kbeg + kt * GF_BK + 8 * i, q = k / af.kh, kg = (k - q * af.kh) / 8;
+        __builtin_amdgcn_global_load_lds((gf_glb_ptr_t)(af.base + af_row + (long)q * 2 * (af.kh / 8 * 256) + kg * 256),
+                                         (gf_lds_ptr_t)(lds + (4 * w + i) * 1024), 16, 0, 0);
+      }
+    } else {
+      sa.issue(lds, kt, w);
+    }
+  };
   Acc acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -137,7 +169,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
 #pragma unroll
       for (int e = 0; e < NR; ++e) acc[i][j][e] = 0.f;
   if (nk > 0) {
-    sa.issue(stage(0), 0, w);
+    issue_a(stage(0), 0);
     sb.issue(stage(0) + OPA, 0, w);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -152,7 +184,10 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row = wr * 128 + MF * i + fr;
-      a[i] = *reinterpret_cast<const f32x4*>(As + row * 128 + gf_phys_slot(row, sl) * 16);
+      if constexpr (AF)
+        a[i] = *reinterpret_cast<const f32x4*>(As + ((wr * 4 + i) * 4 + g) * 1024 + lane * 16);
+      else
+        a[i] = *reinterpret_cast<const f32x4*>(As + row * 128 + gf_phys_slot(row, sl) * 16);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -178,7 +213,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
     const char* As = stage(kt);
     const char* Bs = As + OPA;
     if (kt + 1 < nk) {
-      sa.issue(stage(kt + 1), kt + 1, w);
+      issue_a(stage(kt + 1), kt + 1);
       sb.issue(stage(kt + 1) + OPA, kt + 1, w);
     }
     rd(As, Bs, 0, a0, b0);

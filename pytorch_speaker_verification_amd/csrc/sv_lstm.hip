@@ -626,6 +626,31 @@ int gemm_f32_256(const float* A, long lda, const float* B, long ldb, float* C, l
   return SV_OK;
 }
 
+// dx = dG W_ih of the fp32 persistent backward with A read from its fragment-order hand-off
+// (gemm_f32_256_kernel AF, GfAFrag): the recurrence then writes no row-major dG.  Exact products,
+// whole 256-row tiles, whole 32-row groups per slot, one k-split; else -1 (use the row-major dG).
+int dx_afrag_bn(int T, int B, int H, int Fl) {
+  if (gemm_x() != 0 || SV_F32_MF != 32 || B % 32 || H % 32 || ((long)T * B) % GF_BM) return -1;
+  const int bn = gf256_bn(Fl);
+  if (Fl % bn || plan_gf256(T * B, Fl, 4 * H).splitk != 1) return -1;
+  return bn;
+}
+int gemm_f32_dx_afrag(int bn, const float* dgf, int T, int B, int H, const float* wihT, int Fl, float* dx,
+                      hipStream_t s) {
+  const long nrb = (B + 63) / 64, fs = nrb * 8 * (H / 8) * 256;
+  const GfAFrag af{dgf, fs, B, H};
+  const int M = T * B, K = 4 * H, tiles = (M / GF_BM) * (Fl / bn);
+  const size_t lds = 2 * (size_t)(GF_BM + bn) * GF_BK * 4;
+  if (bn == 256)
+    hipLaunchKernelGGL((gemm_f32_256_kernel<256, SV_F32_MF, GF_STORE, 1>), dim3(tiles, 1), dim3(512), lds, s, nullptr,
+                       0L, wihT, (long)K, dx, (long)Fl, 0L, M, Fl, K, K, nullptr, nullptr, 0.f, af);
+  else
+    hipLaunchKernelGGL((gemm_f32_256_kernel<128, SV_F32_MF, GF_STORE, 1>), dim3(tiles, 1), dim3(512), lds, s, nullptr,
+                       0L, wihT, (long)K, dx, (long)Fl, 0L, M, Fl, K, K, nullptr, nullptr, 0.f, af);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
 }  // namespace
 
 F32ProductScope::F32ProductScope(int mode) : prev(t_f32_mode) { t_f32_mode = mode; }
@@ -1049,9 +1074,12 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
       if (rc) return rc;
       if (l > 0 && (rc = sv_transpose(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, main))) return rc;
       const float* up = l == L - 1 ? dh_last : dx[l + 1];
-      rc = sv_persist_bwd_f32(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1, dgates[l], dgT[l], dgf, main, sync,
-                              probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr, db_ih[l],
-                              db_hh ? db_hh[l] : nullptr);
+      // the row-major dG only where a dx GEMM needs it and cannot read the fragment-order hand-off
+      // (layer 0 computes no dx here)
+      const int abn = l > 0 ? dx_afrag_bn(T, B, H, Fl) : 0;
+      rc = sv_persist_bwd_f32(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1, abn < 0 ? dgates[l] : nullptr,
+                              dgT[l], dgf, main, sync, probe ? probe[2 * l] : nullptr,
+                              probe ? probe[2 * l + 1] : nullptr, db_ih[l], db_hh ? db_hh[l] : nullptr);
       if (rc) return rc;
       // the completion events of layers >= 1 (grad_ready: a caller's bucketed all-reduce) fire once
       // the last recurrence is done, so a collective never shares the device with a persistent
@@ -1059,8 +1087,10 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
       // weight-gradient GEMMs
       for (int k = 1; l == 0 && k < L; ++k)
         if ((e = hipEventRecord(ev[L * nch + k], main)) != hipSuccess) return (int)e;
-      if (l > 0 && (rc = gemm_f32(1, 1, T * B, Fl, 4 * H, dgates[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr,
-                                  nullptr, 0.f, ws.gws, main)))
+      if (l > 0 && abn > 0 && (rc = gemm_f32_dx_afrag(abn, dgf, T, B, H, ws.wihT, Fl, dx[l], main))) return rc;
+      if (l > 0 && abn < 0 &&
+          (rc = gemm_f32(1, 1, T * B, Fl, 4 * H, dgates[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr, nullptr, 0.f,
+                         ws.gws, main)))
         return rc;
       if ((rc = gemm_f32(1, 1, 4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws,
                          main)))

@@ -406,6 +406,17 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
   }
   load_ew(T - 1, 0);
   float dbs = 0.f;  // threads < 128: bias-gradient partial of gate column tid over t and the row block
+#ifdef SV_PF32_STAMP  // A/B stamp builds only: wave 0's cycles per phase, summed over the half-steps of t < T-1
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tl = 0;
+  auto stamp = [&](int i) {
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    if (i >= 0) ph[i] += n - tl;
+    tl = n;
+  };
+#define PB_STAMP(i) if (t < T - 1) stamp(i)
+#else
+#define PB_STAMP(i)
+#endif
   for (int t = T - 1; t >= 0; --t) {
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
@@ -414,9 +425,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
       f32x16 acc0, acc1;
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+      PB_STAMP(-1);
       if (t < T - 1) {
         if (tid == 0) persist_wait(my_cnt, (unsigned)nub * (unsigned)(T - 1 - t), status, limit, 2u);
         __syncthreads();
+        PB_STAMP(0);  // 0: hand-off wait
         const __amdgpu_buffer_rsrc_t ra = sv_rsrc(dgf + (long)(t + 1) * FS, (unsigned)(FS * 4));
         const unsigned base = ((unsigned)(((rb * 4 + g) * 2 + hf) * FBLK) + (unsigned)lane * 4u) * 4u;
         u32x4_t fa[P];
@@ -437,10 +450,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      PB_STAMP(1);  // 1: k-loop (A fragments from the hand-off + MFMAs)
 #pragma unroll
       for (int i = 0; i < 16; ++i) red[(g * PH_BM + acc_row(i, lane)) * LDR + r] = acc0[i] + acc1[i];
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
       __syncthreads();
+      PB_STAMP(2);  // 2: partial exchange + operand DMA wait
       f32x4 dh, cpv, a4[4];
       dh = *reinterpret_cast<const f32x4*>(red + (0 * PH_BM + erow) * LDR + 4 * quad);
       dh += *reinterpret_cast<const f32x4*>(red + (1 * PH_BM + erow) * LDR + 4 * quad);
@@ -472,7 +487,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         for (int v = 0; v < 4; ++v) gts[(q * PF_U + 4 * quad + v) * LDT + erow] = dq[q][v];
       }
       __syncthreads();
-      if (t > 0) {  // the hand-off: 16 fragment blocks of 1 KB (gate q, this half, k-group 4 ub + kl)
+      PB_STAMP(3);  // 3: cell + dG tiles into LDS
+      // the hand-off: 16 fragment blocks of 1 KB (gate q, this half, k-group 4 ub + kl); slot 0 (no
+      // consumer step) only when the dx GEMM reads the fragment-order image (dg == nullptr)
+      if (t > 0 || !dg) {
         const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 4));
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -483,11 +501,14 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
               ((unsigned)(((rb * 4 + q) * 2 + hf) * FBLK) + (unsigned)(4 * ub + kl) * 256u + (unsigned)L * 4u) * 4u;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rw, off, 0, 16 /* sc1 */);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
-          __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t > 0) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
+            __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
+      PB_STAMP(4);  // 4: hand-off stores + drain + arrival
       // off the chain: the bias partials (gate column tid: this half's rows in order, rows past B
       // excluded), row-major dG and dG^T of the half-step
       if (dbp && tid < 4 * PF_U) {
@@ -503,7 +524,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         dbs += s;
       }
       const long gb = b0 + erow;
-      if (gb < B) {
+      if (dg && gb < B) {  // (dg == nullptr: the dx GEMM reads the fragment-order hand-off instead)
         float* dp = dg + (long)t * BG + gb * G + j0 + 4 * quad;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -527,9 +548,18 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         else
           load_ew(t - 1, 0);
       }
+      PB_STAMP(5);  // 5: off-chain (bias partials, dG / dG^T stores, next operand DMA issue)
     }
   }
   if (dbp && tid < 4 * PF_U) dbp[(long)rb * 4 * H + (long)(tid >> 5) * H + j0 + (tid & 31)] = dbs;
+#ifdef SV_PF32_STAMP
+  if (tid == 0 && blockIdx.x < SV_NSTAMP_WG / 2) {  // second half of the stamp slots (the forward uses the first)
+    unsigned long long* st =
+        reinterpret_cast<unsigned long long*>(status + SV_SYNC_STAMP) + (SV_NSTAMP_WG / 2 + blockIdx.x) * SV_NSTAMP;
+    for (int i = 0; i < 6; ++i) st[i] = ph[i];
+  }
+#endif
+#undef PB_STAMP
 }
 
 // ============================================================================
@@ -584,7 +614,8 @@ int sv_persist_bwd_f32(int T, int B, int H, const float* whhT, const float* acts
                        const float* dhup, int up_full, float* dg, float* dgT, float* dgf, hipStream_t stream,
                        unsigned* sync, hipEvent_t pre, hipEvent_t post, float* db_ih, float* db_hh) {
   if (!sv_persist_f32_fits(B, H, sv_stream_cus(stream))) return SV_ESHAPE;
-  if (!sync || !whhT || !acts || !c_tm || !dg || !dgT || !dgf || ((uintptr_t)dgf & 15)) return SV_EARG;
+  // dg may be null: the row-major dG is then not written and slot 0 of dgf holds dG_0 as well
+  if (!sync || !whhT || !acts || !c_tm || !dgT || !dgf || ((uintptr_t)dgf & 15)) return SV_EARG;
   unsigned* cnt = sync + SV_SYNC_CNT;  // channel 0
   const int nub = H / PF_U, nrb = (B + PF_BM - 1) / PF_BM;
   const int Bp = (B + 3) & ~3;

@@ -89,6 +89,15 @@ for sched in ((args.only,) if args.only else ("auto", "per_step")):
         names = ["wait", "dma0", "kloop", "cell", "handoff", "offchain"]
         o["fwd_stamps_per_step_mean"] = {k: round(float(v), 1) for k, v in zip(names, st.mean(0))}
         o["fwd_stamps_per_step_max"] = {k: round(float(v), 1) for k, v in zip(names, st.max(0).values)}
+        # the backward's (slots 512 + workgroup, wave 0, summed over both halves of steps t < T - 1)
+        st_ = ops.embedder_forward(x, layers, wp, bp, status=ps, schedule=sched)[1]
+        ops.embedder_backward(st_, demb, layers, wp, status=ps, schedule=sched)
+        torch.cuda.synchronize()
+        sb = ps.block[stamp0:stamp0 + 2 * 1024 * 8].view(torch.int64).view(1024, 8)[512:512 + nwg, :6].cpu().double()
+        sb = sb / (args.T - 1)
+        nb = ["wait", "kloop", "exchange", "cell", "handoff", "offchain"]
+        o["bwd_stamps_per_step_mean"] = {k: round(float(v), 1) for k, v in zip(nb, sb.mean(0))}
+        o["bwd_stamps_per_step_max"] = {k: round(float(v), 1) for k, v in zip(nb, sb.max(0).values)}
     out[sched] = o
     print(json.dumps({sched: o}), flush=True)
 print(json.dumps(out), flush=True)
