@@ -35,8 +35,9 @@ $(FAULT_LIB): $(FAULT_OBJ)
 # A/B builds (never loaded by tests or the bench): `make ab NAME=x FLAGS="-DSV_..."` compiles every
 # source with FLAGS into scripts/ab/libsv_ge2e_x.so (e.g. -DSV_F32_MF=16: the 256-tile fp32 GEMM on
 # v_mfma_f32_16x16x4_f32; -DSV_PBWD_DEBUG=32: phase stamps of the persistent backward)
-NAME ?= m16
-FLAGS ?= -DSV_F32_MF=16
+# (no default FLAGS: a baseline A/B build of another commit is `make ab NAME=base FLAGS=`)
+NAME ?= ab
+FLAGS ?=
 AB_OBJ := $(patsubst build/%.o,build/ab_$(NAME)/%.o,$(OBJ))
 AB_LIB := scripts/ab/libsv_ge2e_$(NAME).so
 build/ab_$(NAME)/sv_persist3.o: EXTRA := -mllvm -amdgpu-mfma-vgpr-form=1
