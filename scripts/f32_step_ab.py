@@ -24,6 +24,8 @@ ap.add_argument("--B", type=int, default=640)
 ap.add_argument("--T", type=int, default=160)
 ap.add_argument("--lib", default=None)
 ap.add_argument("--only", default=None, help="one schedule only")
+ap.add_argument("--wave-stamps", action="store_true", help="with --stamps: a -DSV_PF32_WAVE_STAMP build, "
+                "the backward's phases of every wave (workgroups 0-127)")
 ap.add_argument("--stamps", action="store_true", help="a -DSV_PF32_STAMP build: the persistent forward's "
                 "cycles per step by phase (last forward layer launch, mean and max over workgroups)")
 args = ap.parse_args()
@@ -98,6 +100,11 @@ for sched in ((args.only,) if args.only else ("auto", "per_step")):
         nb = ["wait", "kloop", "exchange", "cell", "handoff", "offchain"]
         o["bwd_stamps_per_step_mean"] = {k: round(float(v), 1) for k, v in zip(nb, sb.mean(0))}
         o["bwd_stamps_per_step_max"] = {k: round(float(v), 1) for k, v in zip(nb, sb.max(0).values)}
+        if args.wave_stamps:  # a -DSV_PF32_WAVE_STAMP build: slots 512 + 4 wg + wave, workgroups 0-127
+            sw = ps.block[stamp0:stamp0 + 2 * 1024 * 8].view(torch.int64).view(1024, 8)[512:1024, :6]
+            sw = sw.cpu().double().view(128, 4, 6) / (args.T - 1)
+            o["bwd_stamps_per_wave_mean"] = {f"wave{w}": {k: round(float(v), 1) for k, v in zip(nb, sw[:, w].mean(0))}
+                                             for w in range(4)}
     out[sched] = o
     print(json.dumps({sched: o}), flush=True)
 print(json.dumps(out), flush=True)
