@@ -553,11 +553,19 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
   }
   if (dbp && tid < 4 * PF_U) dbp[(long)rb * 4 * H + (long)(tid >> 5) * H + j0 + (tid & 31)] = dbs;
 #ifdef SV_PF32_STAMP
+#ifdef SV_PF32_WAVE_STAMP  // every wave's phases, workgroups 0-127: slot 512 + 4 wg + wave
+  if (lane == 0 && blockIdx.x < SV_NSTAMP_WG / 8) {
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(status + SV_SYNC_STAMP) +
+                             (SV_NSTAMP_WG / 2 + 4 * blockIdx.x + g) * SV_NSTAMP;
+    for (int i = 0; i < 6; ++i) st[i] = ph[i];
+  }
+#else
   if (tid == 0 && blockIdx.x < SV_NSTAMP_WG / 2) {  // second half of the stamp slots (the forward uses the first)
     unsigned long long* st =
         reinterpret_cast<unsigned long long*>(status + SV_SYNC_STAMP) + (SV_NSTAMP_WG / 2 + blockIdx.x) * SV_NSTAMP;
     for (int i = 0; i < 6; ++i) st[i] = ph[i];
   }
+#endif
 #endif
 #undef PB_STAMP
 }
