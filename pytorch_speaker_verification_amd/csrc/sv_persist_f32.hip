@@ -575,7 +575,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
 // ============================================================================
 namespace {
 // weight k-groups (of 96 at H = 768) in VGPRs / LDS beside the 64 in AGPRs
-constexpr int PF_FWD_NV = 16, PF_FWD_NL = 16, PH_BWD_NL = 24, PH_BWD_NV = 96 - PF_NA - PH_BWD_NL, PH_BWD_P = 12;
+#ifndef SV_PH_BWD_P  // A/B builds: the backward's A-fragment prefetch depth
+#define SV_PH_BWD_P 12
+#endif
+constexpr int PF_FWD_NV = 16, PF_FWD_NL = 16, PH_BWD_NL = 24, PH_BWD_NV = 96 - PF_NA - PH_BWD_NL,
+              PH_BWD_P = SV_PH_BWD_P;
 constexpr size_t pf_fwd_lds() {
   return (size_t)PF_NB * PF_CH + (size_t)PF_BM * 4 * PF_U * 4 + (size_t)4 * PF_FWD_NL * 1024;
 }
