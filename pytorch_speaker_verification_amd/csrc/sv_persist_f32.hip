@@ -581,7 +581,11 @@ namespace {
 #ifndef SV_PF_FWD_NV  // A/B builds: the forward's weight k-groups in VGPRs (the rest of 32 in LDS)
 #define SV_PF_FWD_NV 16
 #endif
-constexpr int PF_FWD_NV = SV_PF_FWD_NV, PF_FWD_NL = 32 - SV_PF_FWD_NV, PH_BWD_NL = 24, PH_BWD_NV = 96 - PF_NA - PH_BWD_NL,
+#ifndef SV_PH_BWD_NL  // A/B builds: the backward's weight k-groups in LDS (the rest of 32 in VGPRs)
+#define SV_PH_BWD_NL 24
+#endif
+constexpr int PF_FWD_NV = SV_PF_FWD_NV, PF_FWD_NL = 32 - SV_PF_FWD_NV, PH_BWD_NL = SV_PH_BWD_NL,
+              PH_BWD_NV = 96 - PF_NA - PH_BWD_NL,
               PH_BWD_P = SV_PH_BWD_P;
 constexpr size_t pf_fwd_lds() {
   return (size_t)PF_NB * PF_CH + (size_t)PF_BM * 4 * PF_U * 4 + (size_t)4 * PF_FWD_NL * 1024;
