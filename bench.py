@@ -18,11 +18,14 @@ Side measurements in the same line:
                   strong scaling, value = 640 * steps / time
   c5              (world > 1) N = 256 x M = 10, T = 180 split over the ranks, bf16 (strong)
   c4_rank_shape / c5_rank_shape   (world = 1) one rank's share of c4 / c5 at 8 GPUs, alone
-  roofline        the in-step dominant kernel of the headline step: the fp32 backward
-                  recurrent step K3 (lstm_step_bwd_v2_kernel), timed by HIP event pairs recorded
-                  on its own stream around one launch per chunk INSIDE the timed steps
+  roofline        the worst-fraction in-step kernel of the headline step: at c2 the persistent
+                  fp32 backward recurrence (lstm_persist_bwd_f32_h2_kernel; the per-step
+                  schedule: K3), timed by HIP event pairs on its stream INSIDE the timed steps
   roofline_bf16   the same for c3's dominant kernels, the persistent bf16 recurrences
   roofline_gemm / roofline_step_kernel   secondary: the K1-shape fp32 GEMM and K2 in isolation
+  roofline_dw_gemm  the fp32 dW GEMM (the c2 step's largest kernel by busy time) in isolation
+  dropin_loop     the reference's own loop body (train_speech_embedder.py:46-65) run unchanged on
+                  the dropin/ modules (autograd + torch clip + torch SGD), beside the fused trainer
   cpu_baseline    the reference's CPU path (oracle/torch_port.py, nn.LSTM on oneDNN) on every
                   host CPU this process may use, median of 3 steps at c2, plus c1
 """
@@ -31,6 +34,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import random
 import socket
 import subprocess
 import sys
@@ -190,9 +194,12 @@ def pmc_traffic(kernel):
         return None
 
 
-def _timed(f, dev, reps):
+def _timed(f, dev, reps, warm=3):
+    """Average ms per call of f over `reps` calls, HIP events on the current stream, after `warm`
+    untimed calls (first launches pay code-object load and cold caches)."""
     s = torch.cuda.current_stream(dev)
-    f()
+    for _ in range(warm):
+        f()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(reps):
@@ -226,6 +233,75 @@ def time_gemm_kernel(M, N, K, dev, reps=5):
     f = lambda: call("sv_gemm_f32", 1, 1, M, N, K, ptr(A), K, ptr(Bm), K, ptr(C), N, None, None, 0.0, None, 0,  # noqa
                      stream_of(C))
     return _timed(f, dev, reps), 2.0 * M * N * K, 4.0 * (M * K + N * K + M * N)
+
+
+def time_dw_gemm(T, B, H, dev, reps=5):
+    """The fp32 weight-gradient GEMM of the persistent backward (dW_hh = dG^T h: M = 4H, N = H,
+    K = T * B, split-K slabs; gemm_f32_256_kernel through sv_gemm_f32 with both operands
+    k-contiguous, as sv_lstm_stack_bwd calls it) in isolation: by busy time the c2 step's largest
+    kernel (3 launches of it and 3 of dW_ih per step)."""
+    from pytorch_speaker_verification_amd._lib import call, lib, ptr, stream_of
+    g = torch.Generator(device="cpu").manual_seed(10)
+    K = T * B
+    A = (torch.randn(4 * H, K, generator=g) * 0.01).to(dev)
+    Bm = torch.randn(H, K, generator=g).to(dev)
+    C = torch.empty(4 * H, H, device=dev)
+    ws = torch.empty(int(lib().sv_gemm_f32_workspace(4 * H, H, K)) // 4 + 1, device=dev)
+    f = lambda: call("sv_gemm_f32", 1, 1, 4 * H, H, K, ptr(A), K, ptr(Bm), K, ptr(C), H, None, None, 0.0,  # noqa
+                     ptr(ws), 0, stream_of(C))
+    return _timed(f, dev, reps), 2.0 * 4 * H * H * K, 4.0 * (4 * H * K + H * K + 4 * H * H)
+
+
+def reference_loop_body(embedder_net, ge2e_loss, optimizer, mel_db_batch, N, M):
+    """The reference's training-loop body, train_speech_embedder.py:46-65, as user code: whatever
+    modules it is handed (this package's through dropin/, or the stock-PyTorch port) run through
+    it unchanged -- reshape, random perm / unperm, zero_grad, forward, GE2E loss, loss.backward()
+    (autograd through EmbedderFunction / GE2EFunction), torch clip_grad_norm_ x2, SGD.step."""
+    mel_db_batch = torch.reshape(mel_db_batch, (N * M, mel_db_batch.size(2), mel_db_batch.size(3)))
+    perm = random.sample(range(0, N * M), N * M)
+    unperm = list(perm)
+    for i, j in enumerate(perm):
+        unperm[j] = i
+    mel_db_batch = mel_db_batch[perm]
+    optimizer.zero_grad()
+    embeddings = embedder_net(mel_db_batch)
+    embeddings = embeddings[unperm]
+    embeddings = torch.reshape(embeddings, (N, M, embeddings.size(1)))
+    loss = ge2e_loss(embeddings)
+    loss.backward()
+    torch.nn.utils.clip_grad_norm_(embedder_net.parameters(), 3.0)
+    torch.nn.utils.clip_grad_norm_(ge2e_loss.parameters(), 1.0)
+    optimizer.step()
+    return loss
+
+
+def dropin_loop(ctx, N, M, T, steps, warmup, precision="f32"):
+    """ms per step of the reference's own loop body (reference_loop_body) on this package's
+    modules imported the reference's way (dropin/: `from speech_embedder_net import ...`), the
+    same synthetic batch as the headline, beside the fused GE2ETrainer."""
+    if os.path.join(ROOT, "dropin") not in sys.path:
+        sys.path.append(os.path.join(ROOT, "dropin"))
+    from speech_embedder_net import GE2ELoss, SpeechEmbedder  # noqa: E402  (dropin/ shim)
+    torch.manual_seed(0)
+    net = SpeechEmbedder().to(ctx.dev)
+    net.precision = precision
+    ge2e = GE2ELoss(ctx.dev)
+    opt = torch.optim.SGD([{"params": net.parameters()}, {"params": ge2e.parameters()}], lr=0.01)
+    g = torch.Generator(device="cpu").manual_seed(1235 + ctx.rank)
+    x = torch.randn(N, M, T, DIMS[0], generator=g).to(ctx.dev)
+    random.seed(0)
+    for _ in range(warmup):
+        reference_loop_body(net, ge2e, opt, x, N, M)
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = reference_loop_body(net, ge2e, opt, x, N, M)
+    ctx.barrier()
+    dt = ctx.max_over_ranks(time.perf_counter() - t0)
+    return {"config": f"train_speech_embedder.py:46-65 loop body unchanged on dropin/ modules (autograd forward / "
+                      f"backward, torch clip_grad_norm_ x2, torch SGD), N={N}xM={M}, T={T}, {precision}",
+            "ms_per_step": round(dt / steps * 1e3, 3), "value": round(N * M * ctx.world * steps / dt, 3),
+            "unit": "embeddings/s", "loss": round(float(loss), 5)}
 
 
 def hbm_kernels(tr, N, M, D, dev, reps=50):
@@ -593,8 +669,9 @@ def main():
     if f32_persist:
         fl = 2.0 * B * T * H * 4 * H
         out["roofline"] = roofline_entry(
-            "lstm_persist_bwd_f32_h2_kernel (persistent fp32 backward recurrence, one launch per layer, two 32-row chains, W_hh in "
-            "registers, fp32 MFMA 32x32x2)", fl, probe_ms(probes, "bwd") / L, MI355X_FP32_MFMA_TFLOPS,
+            "lstm_persist_bwd_f32_h2_kernel (the c2 step's worst-fraction in-step kernel, not its largest by busy time "
+            "-- that is the dW GEMM, roofline_dw_gemm: persistent fp32 backward recurrence, one launch per layer, two "
+            "32-row chains, W_hh in registers, fp32 MFMA 32x32x2)", fl, probe_ms(probes, "bwd") / L, MI355X_FP32_MFMA_TFLOPS,
             pmc_traffic("lstm_persist_bwd_f32_h2_kernel"), L * args.steps,
             "in-step: HIP events around each layer's launch inside the timed steps (on its stream, main)")
         out["roofline_fwd"] = roofline_entry(
@@ -699,7 +776,13 @@ def main():
             f"tiles, fp32 MFMA 32x32x2), K1 shape "
             f"M={160 * 640} N={4 * H} K={H}",
             fl_g, ms_g, MI355X_FP32_MFMA_TFLOPS, pmc_traffic("gemm_f32_256p_kernel<256,32>@K1"), 5,
-            "isolated launches, HIP events on its stream"), algorithmic_bytes=by_g)
+            "isolated launches after 3 untimed ones, HIP events on its stream"), algorithmic_bytes=by_g)
+        ms_w, fl_w, by_w = time_dw_gemm(T, B, H, dev)
+        out["roofline_dw_gemm"] = dict(roofline_entry(
+            f"gemm_f32_256_kernel<256,32,1,0> (dW_hh = dG^T h of the persistent fp32 backward: split-K slabs, the c2 "
+            f"step's largest kernel by busy time), M={4 * H} N={H} K={T * B}", fl_w, ms_w, MI355X_FP32_MFMA_TFLOPS,
+            pmc_traffic("gemm_f32_256_kernel<256,32,1,0>@dW"), 5,
+            "isolated launches after 3 untimed ones, HIP events on its stream"), algorithmic_bytes=by_w)
         ms_k, fl_k = time_step_kernel(640, H, dev)
         out["roofline_step_kernel"] = roofline_entry(
             "lstm_step_fwd_v2_kernel (K2, fp32 forward recurrent step) at B=640", fl_k, ms_k,
@@ -713,6 +796,10 @@ def main():
                 out["vendor_baseline"] = vendor_baseline(N, M, T, dev, dtype=dtype)
                 if "bf16" in out:
                     out["bf16"]["vendor_baseline"] = vendor_baseline(N, M, T, dev, dtype="bf16")
+    if world == 1 and not args.no_extras and not strong:
+        log("drop-in loop body")
+        out["dropin_loop"] = dropin_loop(ctx, N, M, T, args.steps, args.warmup, dtype)
+        out["dropin_loop"]["vs_fused_trainer"] = round(out["dropin_loop"]["ms_per_step"] / ms_step, 4)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, M, T)
     if rank == 0:

@@ -62,3 +62,16 @@ def train_step(net, w, b, opt, x, N, M):
     torch.nn.utils.clip_grad_norm_([w, b], 1.0)
     opt.step()
     return loss
+
+
+class GE2ELossPort(nn.Module):
+    """GE2ELoss (speech_embedder_net.py:35-49) as a module with learnable w = 10, b = -5, for the
+    reference's own loop body (its optimizer takes ge2e_loss.parameters())."""
+
+    def __init__(self, device):
+        super().__init__()
+        self.w = nn.Parameter(torch.tensor(10.0, device=device))
+        self.b = nn.Parameter(torch.tensor(-5.0, device=device))
+
+    def forward(self, embeddings):
+        return ge2e_loss(embeddings, self.w, self.b)

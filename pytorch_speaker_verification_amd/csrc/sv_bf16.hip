@@ -602,14 +602,14 @@ extern "C" int sv_lstm_layer_fwd_bf16(const bf16_t* x_bf, int T, int B, int F, i
   const long BH = (long)B * H, BG = 4L * B * H;
   int rc = sv_gemm_bf16_bf(T * B, 4 * H, F, x_bf, F, w_ih_bf, F, gates, 4L * H, b_ih, b_hh, stream);
   if (rc) return rc;
-  hipError_t e = hipMemsetAsync(h_tm, 0, BH * sizeof(float), stream);
+  hipError_t e = sv_memset0(h_tm, BH * sizeof(float), stream);
   if (e != hipSuccess) return (int)e;
-  e = hipMemsetAsync(h_bf, 0, BH * sizeof(bf16_t), stream);
+  e = sv_memset0(h_bf, BH * sizeof(bf16_t), stream);
   if (e != hipSuccess) return (int)e;
   const int Bp = (B + 7) & ~7;
   const long ldhT = (long)(T + 1) * Bp;
   if (hT && Bp != B) {
-    e = hipMemsetAsync(hT, 0, (size_t)H * ldhT * sizeof(bf16_t), stream);
+    e = sv_memset0(hT, (size_t)H * ldhT * sizeof(bf16_t), stream);
     if (e != hipSuccess) return (int)e;
   }
   const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
@@ -647,7 +647,7 @@ extern "C" int sv_lstm_layer_bwd_bf16(int T, int B, int F, int H, const bf16_t* 
   float* dcf1 = workspace + dcfsz;
   float* gws = workspace + 2 * dcfsz;
   if (Bp != B) {
-    hipError_t e = hipMemsetAsync(dgT_bf, 0, (size_t)4 * H * TBp * sizeof(bf16_t), stream);
+    hipError_t e = sv_memset0(dgT_bf, (size_t)4 * H * TBp * sizeof(bf16_t), stream);
     if (e != hipSuccess) return (int)e;
   }
   const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
@@ -697,9 +697,9 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
   const long ldhT = (long)(T + 1) * Bp;
   hipError_t e;
   auto zero_state = [&](int l, hipStream_t s) -> int {
-    if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), s)) != hipSuccess) return (int)e;
-    if ((e = hipMemsetAsync(h_bf[l], 0, BH * sizeof(bf16_t), s)) != hipSuccess) return (int)e;
-    if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(bf16_t), s)) != hipSuccess)
+    if ((e = sv_memset0(h_tm[l], BH * sizeof(float), s)) != hipSuccess) return (int)e;
+    if ((e = sv_memset0(h_bf[l], BH * sizeof(bf16_t), s)) != hipSuccess) return (int)e;
+    if (hT[l] && Bp != B && (e = sv_memset0(hT[l], (size_t)H * ldhT * sizeof(bf16_t), s)) != hipSuccess)
       return (int)e;
     return SV_OK;
   };
@@ -917,7 +917,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     int rc = sv_transpose_cast_bf16(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, s);
     if (rc) return rc;
     if (l > 0 && (rc = sv_transpose_cast_bf16(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, s))) return rc;
-    if (Bp != B && (e = hipMemsetAsync(dgT[l], 0, (size_t)4 * H * TBp * sizeof(bf16_t), s)) != hipSuccess)
+    if (Bp != B && (e = sv_memset0(dgT[l], (size_t)4 * H * TBp * sizeof(bf16_t), s)) != hipSuccess)
       return (int)e;
     for (int c = nch - 1; c >= 0; --c) {
       const int t0 = c * chunk, t1 = std::min(T, t0 + chunk);

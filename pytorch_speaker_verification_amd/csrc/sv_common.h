@@ -32,6 +32,18 @@ struct F32ProductScope {
 // 32-unit tiles co-resident on `cus` CUs; dgf: sv_persist_f32_bwd_scratch bytes (16-B aligned)
 int sv_persist_f32_fits(int B, int H, int cus);
 int sv_stream_cus(hipStream_t stream);  // CUs of the stream's device (sv_persist.hip)
+// zero `words` arrival-counter words in each of `nchan` channels (channel c at cnt + c * chan_stride)
+// with ONE kernel on `stream` (sv_persist.hip).  Never hipMemsetAsync for the counters: replayed
+// from a HIP graph, a memset node's reset was not reliably seen by the persistent kernel's
+// agent-scope atomics and polls (scripts/f32_replay_diag.py)
+int sv_zero_counters(unsigned* cnt, int nchan, long chan_stride, int words, hipStream_t stream);
+// zero `bytes` bytes at p with a kernel on `stream` (0 or a hipError_t).  Used for every zeroing
+// in the library instead of hipMemsetAsync: replayed from a HIP graph, memset nodes left junk
+// behind (the initial-state slots and the arrival counters; scripts/f32_replay_diag.py)
+int sv_zero_bytes(void* p, size_t bytes, hipStream_t stream);
+inline hipError_t sv_memset0(void* p, size_t bytes, hipStream_t stream) {
+  return (hipError_t)sv_zero_bytes(p, bytes, stream);
+}
 size_t sv_persist_f32_bwd_scratch(int T, int B, int H);
 int sv_persist_fwd_f32(int T, int B, int H, const float* whh, float* gates, float* c_tm, float* h_tm, float* hT,
                        hipStream_t stream, unsigned* sync, int chan, hipEvent_t pre, hipEvent_t post);

@@ -883,7 +883,7 @@ extern "C" int sv_ge2e_shard_rows(int N_local, int M, int D, int spk_offset, int
   SV_LAUNCH_CHECK();
   // the padding rows of dC^ (speakers N .. Np-1) stay zero through the all-reduce
   if (Np > N) {
-    hipError_t e = hipMemsetAsync(red + (size_t)N * D, 0, (size_t)(Np - N) * D * sizeof(float), stream);
+    hipError_t e = sv_memset0(red + (size_t)N * D, (size_t)(Np - N) * D * sizeof(float), stream);
     if (e != hipSuccess) return (int)e;
   }
   hipLaunchKernelGGL(ge2e_cols_kernel<true>, dim3(N, (D + 63) / 64), dim3(64 * GF_COLW), 0, stream, Bl, M, N, D, Np,

@@ -833,13 +833,13 @@ extern "C" int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, 
   // K1: all-timestep input projection  gates = x W_ih^T + b_ih + b_hh
   int rc = gemm_f32(1, 1, T * B, 4 * H, F, x_tm, F, w_ih, F, gates, 4L * H, b_ih, b_hh, 0.f, nullptr, stream);
   if (rc) return rc;
-  hipError_t e = hipMemsetAsync(h_tm, 0, BH * sizeof(float), stream);
+  hipError_t e = sv_memset0(h_tm, BH * sizeof(float), stream);
   if (e != hipSuccess) return (int)e;
   const dim3 grid = fwd_step_grid(B, H);
   const int Bp = (B + 3) & ~3;
   const long ldhT = (long)(T + 1) * Bp;
   if (hT && Bp != B) {  // zero the padding columns of the transposed layout
-    e = hipMemsetAsync(hT, 0, (size_t)H * ldhT * sizeof(float), stream);
+    e = sv_memset0(hT, (size_t)H * ldhT * sizeof(float), stream);
     if (e != hipSuccess) return (int)e;
   }
   for (int t = 0; t < T; ++t) {
@@ -896,7 +896,7 @@ extern "C" int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* xT, lo
   if (rc) return rc;
   const dim3 grid((H + BWD_U - 1) / BWD_U, (B + BWD_BM - 1) / BWD_BM);
   if (Bp != B) {
-    hipError_t e = hipMemsetAsync(dgT, 0, (size_t)4 * H * TBp * sizeof(float), stream);
+    hipError_t e = sv_memset0(dgT, (size_t)4 * H * TBp * sizeof(float), stream);
     if (e != hipSuccess) return (int)e;
   }
   for (int t = T - 1; t >= 0; --t) {
@@ -973,8 +973,8 @@ extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float*
     for (int l = 0; l < L; ++l) {
       const int Fl = l == 0 ? F : H;
       const float* in = l == 0 ? x_tm : h_tm[l - 1] + BH;
-      if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), main)) != hipSuccess) return (int)e;
-      if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(float), main)) != hipSuccess)
+      if ((e = sv_memset0(h_tm[l], BH * sizeof(float), main)) != hipSuccess) return (int)e;
+      if (hT[l] && Bp != B && (e = sv_memset0(hT[l], (size_t)H * ldhT * sizeof(float), main)) != hipSuccess)
         return (int)e;
       int rc = gemm_f32(1, 1, T * B, 4 * H, Fl, in, Fl, w_ih[l], Fl, gates[l], 4L * H, b_ih[l], b_hh[l], 0.f, nullptr,
                         main);
@@ -991,8 +991,8 @@ extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float*
   for (int l = 0; l < L; ++l) {
     hipStream_t s = side[l];
     if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
-    if ((e = hipMemsetAsync(h_tm[l], 0, BH * sizeof(float), s)) != hipSuccess) return (int)e;
-    if (hT[l] && Bp != B && (e = hipMemsetAsync(hT[l], 0, (size_t)H * ldhT * sizeof(float), s)) != hipSuccess)
+    if ((e = sv_memset0(h_tm[l], BH * sizeof(float), s)) != hipSuccess) return (int)e;
+    if (hT[l] && Bp != B && (e = sv_memset0(hT[l], (size_t)H * ldhT * sizeof(float), s)) != hipSuccess)
       return (int)e;
   }
   const dim3 grid = fwd_step_grid(B, H);
@@ -1115,7 +1115,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
     int rc = sv_transpose(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, s);
     if (rc) return rc;
     if (l > 0 && (rc = sv_transpose(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, s))) return rc;
-    if (Bp != B && (e = hipMemsetAsync(dgT[l], 0, (size_t)4 * H * TBp * sizeof(float), s)) != hipSuccess) return (int)e;
+    if (Bp != B && (e = sv_memset0(dgT[l], (size_t)4 * H * TBp * sizeof(float), s)) != hipSuccess) return (int)e;
     for (int c = nch - 1; c >= 0; --c) {
       const int t0 = c * chunk, t1 = std::min(T, t0 + chunk);
       if (l < L - 1 && (e = hipStreamWaitEvent(s, ev[(l + 1) * nch + c], 0)) != hipSuccess) return (int)e;

@@ -886,6 +886,35 @@ extern "C" int sv_test_set_fault(int mode) {
 unsigned sv_persist_limit() { return persist_limit(); }
 int sv_persist_fault(int bwd) { return bwd ? persist_fault() != 0 : fwd_fault(); }
 
+__global__ void sv_zero_counters_kernel(unsigned* cnt, int nchan, long chan_stride, int words) {
+  for (int i = threadIdx.x; i < nchan * words; i += blockDim.x) cnt[(i / words) * chan_stride + i % words] = 0u;
+}
+
+int sv_zero_counters(unsigned* cnt, int nchan, long chan_stride, int words, hipStream_t stream) {
+  if (!cnt || nchan <= 0 || words <= 0) return SV_EARG;
+  hipLaunchKernelGGL(sv_zero_counters_kernel, dim3(1), dim3(256), 0, stream, cnt, nchan, chan_stride, words);
+  return (int)hipGetLastError();
+}
+
+// head bytes up to 16-B alignment, 16-B body, tail bytes
+__global__ void sv_zero_bytes_kernel(char* p, size_t head, size_t n16, size_t tail) {
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+  if (i0 < head) p[i0] = 0;
+  uint4* b = reinterpret_cast<uint4*>(p + head);
+  for (size_t i = i0; i < n16; i += stride) b[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (i0 < tail) p[head + 16 * n16 + i0] = 0;
+}
+
+int sv_zero_bytes(void* p, size_t bytes, hipStream_t stream) {
+  if (!bytes) return SV_OK;
+  if (!p) return SV_EARG;
+  const size_t head = std::min(bytes, (size_t)((16 - ((uintptr_t)p & 15)) & 15));
+  const size_t n16 = (bytes - head) / 16, tail = bytes - head - 16 * n16;
+  const size_t blocks = std::max<size_t>(1, std::min<size_t>(2048, (n16 + 255) / 256));
+  hipLaunchKernelGGL(sv_zero_bytes_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (char*)p, head, n16, tail);
+  return (int)hipGetLastError();
+}
+
 int sv_stream_cus(hipStream_t stream) {
   int dev = -1;
   if (stream && hipStreamGetDevice(stream, &dev) == hipSuccess) return device_cus(dev);
@@ -943,7 +972,7 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
   const bool wide = wst && pbwd3_ok(B, H, cus);
   const int bm = wide ? 32 : wst ? persist_bm(B, H, cus) : BF_BM;
   const dim3 grid(wide ? H / 64 : (H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
-  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)grid.y * SV_PCNT_STRIDE * sizeof(unsigned), stream);
+  hipError_t e = (hipError_t)sv_zero_counters(cnt, 1, 0, grid.y * SV_PCNT_STRIDE, stream);
   if (e != hipSuccess) return (int)e;
   const unsigned limit = persist_limit();
   const int fault = fwd_fault();
@@ -1058,7 +1087,7 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
   float* dbp = db_ih ? reinterpret_cast<float*>(reinterpret_cast<char*>(dgf) +
                                                 (size_t)T * ((B + BF_BM - 1) / BF_BM) * BF_BM * 4 * H * sizeof(bf16_t))
                      : nullptr;
-  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)grid.y * SV_PCNT_STRIDE * sizeof(unsigned), stream);
+  hipError_t e = (hipError_t)sv_zero_counters(cnt, 1, 0, grid.y * SV_PCNT_STRIDE, stream);
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   // A-fragment prefetch depth 8 at H = 768 (measured: 4 / 16 no better)
@@ -1131,9 +1160,9 @@ int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, cons
     a.dbp[l] = db_ih ? reinterpret_cast<float*>(p) : nullptr;
     p += wave_dbp_bytes(B, H);
     a.cnt[l] = sync_cnt(sync, l);
-    hipError_t e = hipMemsetAsync(a.cnt[l], 0, (size_t)a.nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
-    if (e != hipSuccess) return (int)e;
   }
+  if (int rc = sv_zero_counters(a.cnt[0], L, (long)SV_PCNT_ROWS * SV_PCNT_STRIDE, a.nrb * SV_PCNT_STRIDE, stream))
+    return rc;
   a.dh_last = dh_last;
   a.status = sync;
   a.limit = persist_limit();

@@ -26,6 +26,12 @@
 #include "sv_persist_dev.h"
 #include "../../include/sv_ge2e.h"
 
+#ifndef SV_PF32_ACQ  // A/B diagnostic builds only (0: the product's relaxed poll)
+#define SV_PF32_ACQ 0
+#endif
+#ifndef SV_PF32_GXAUX  // A/B diagnostic: cache-policy bits of the x-projection DMA
+#define SV_PF32_GXAUX 0
+#endif
 namespace {
 constexpr int PF_BM = 64, PF_U = 32;
 constexpr int PF_KC = 64;                  // k per forward A chunk
@@ -130,6 +136,26 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
 #else
 #define PF_STAMP(i)
 #endif
+#ifdef SV_PF32_CHKCNT  // A/B diagnostic: the counter at the start of the launch (>= nub: not reset yet)
+  if (tid == 0) {
+    const unsigned c0 = __hip_atomic_load(cnt + rb * SV_PCNT_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c0 >= (unsigned)nub) __hip_atomic_fetch_or(status, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c0 >= (unsigned)nub) __hip_atomic_fetch_max(status + 1, c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#endif
+#if SV_PF32_ACQ == 1  // A/B diagnostic: one agent-scope acquire per CU at the start of the launch
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+#elif SV_PF32_ACQ == 3  // A/B diagnostic: a system-scope acquire at the start
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+#endif
   for (int t = 0; t < T; ++t) {
     PF_STAMP(-1);
     // an opaque zero: keeps the DMA address arithmetic inside the step (hoisted out of the time
@@ -155,14 +181,20 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
       for (int j = 0; j < 8; ++j) {
         const int q = (8 * gz + j) * 64 + lane, row = q >> 5, s = q & 31;
         const float* src = gates + (long)t * BG + (long)min(b0 + row, B - 1) * G + (s >> 3) * H + j0 + 4 * (s & 7);
-        __builtin_amdgcn_global_load_lds((pf_glb_t)src, (pf_lds_t)(gxs + (8 * g + j) * 256), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((pf_glb_t)src, (pf_lds_t)(gxs + (8 * g + j) * 256), 16, 0, SV_PF32_GXAUX);
       }
     };
     f32x16 acc0, acc1;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
     if (t > 0) {
-      if (tid == 0) persist_wait(my_cnt, (unsigned)nub * (unsigned)t, status, limit, 1u);
+      if (tid == 0) {
+        persist_wait(my_cnt, (unsigned)nub * (unsigned)t, status, limit, 1u);
+#if SV_PF32_ACQ == 2  // A/B diagnostic: an agent-scope acquire after every poll
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      }
       __syncthreads();
       PF_STAMP(0);  // 0: hand-off wait
       dma_chunk(0, 0);
@@ -271,6 +303,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#ifdef SV_PF32_CHKCNT  // A/B diagnostic: a counter >= nub before this workgroup's first arrival was not reset
+    if (tid == 0 && t == 0 &&
+        __hip_atomic_load(my_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nub)
+      __hip_atomic_fetch_or(status, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     if (tid == 0 && persist_arrive_ok(fault, t == 0))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     PF_STAMP(4);  // 4: hand-off stores + drain + arrival
@@ -404,6 +441,13 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
     cv[hf] = *reinterpret_cast<const f32x4*>(c_tm + (long)(T - 1) * BH + (long)gb * H + j0 + 4 * quad);
     dcf[hf] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+#if SV_PF32_ACQ == 1
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+#endif
   load_ew(T - 1, 0);
   float dbs = 0.f;  // threads < 128: bias-gradient partial of gate column tid over t and the row block
 #ifdef SV_PF32_STAMP  // A/B stamp builds only: wave 0's cycles per phase, summed over the half-steps of t < T-1
@@ -427,7 +471,13 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
       for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
       PB_STAMP(-1);
       if (t < T - 1) {
-        if (tid == 0) persist_wait(my_cnt, (unsigned)nub * (unsigned)(T - 1 - t), status, limit, 2u);
+        if (tid == 0) {
+          persist_wait(my_cnt, (unsigned)nub * (unsigned)(T - 1 - t), status, limit, 2u);
+#if SV_PF32_ACQ == 2
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        }
         __syncthreads();
         PB_STAMP(0);  // 0: hand-off wait
         const __amdgpu_buffer_rsrc_t ra = sv_rsrc(dgf + (long)(t + 1) * FS, (unsigned)(FS * 4));
@@ -618,7 +668,11 @@ int sv_persist_fwd_f32(int T, int B, int H, const float* whh, float* gates, floa
   unsigned* cnt = sync + SV_SYNC_CNT + (size_t)chan * SV_PCNT_ROWS * SV_PCNT_STRIDE;
   const int nub = H / PF_U, nrb = (B + PF_BM - 1) / PF_BM;
   const int Bp = (B + 3) & ~3;
+#ifdef SV_PF32_MEMSET  // A/B diagnostic only: the memset reset that fails under HIP-graph replay
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
+#else
+  hipError_t e = (hipError_t)sv_zero_counters(cnt, 1, 0, nrb * SV_PCNT_STRIDE, stream);
+#endif
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
   hipLaunchKernelGGL((lstm_persist_fwd_f32_kernel<96, PF_FWD_NV, PF_FWD_NL>), dim3(nub * nrb), dim3(256),
@@ -640,7 +694,7 @@ int sv_persist_bwd_f32(int T, int B, int H, const float* whhT, const float* acts
   const int Bp = (B + 3) & ~3;
   // bias partials [nrb][4H] after the hand-off slots (db_ih NULL: not computed here)
   float* dbp = db_ih ? dgf + (size_t)T * nrb * PF_BM * 4 * H : nullptr;
-  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)2 * nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
+  hipError_t e = (hipError_t)sv_zero_counters(cnt, 1, 0, 2 * nrb * SV_PCNT_STRIDE, stream);
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
   hipLaunchKernelGGL((lstm_persist_bwd_f32_h2_kernel<96, PH_BWD_P, PH_BWD_NV, PH_BWD_NL>), dim3(nub * nrb),

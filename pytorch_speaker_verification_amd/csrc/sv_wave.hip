@@ -326,9 +326,9 @@ int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, cons
     a.hb[l] = h_bf[l];
     a.hT[l] = hT[l];
     a.cnt[l] = sync + SV_SYNC_CNT + (size_t)l * SV_PCNT_ROWS * SV_PCNT_STRIDE;
-    hipError_t e = hipMemsetAsync(a.cnt[l], 0, (size_t)a.nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
-    if (e != hipSuccess) return (int)e;
   }
+  if (int rc = sv_zero_counters(a.cnt[0], L, (long)SV_PCNT_ROWS * SV_PCNT_STRIDE, a.nrb * SV_PCNT_STRIDE, stream))
+    return rc;
   a.x_bf = x_bf;
   a.status = sync;
   a.limit = limit;

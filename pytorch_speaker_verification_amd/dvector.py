@@ -49,14 +49,15 @@ def bf16_batch(H, limit=16384):
 
 
 @torch.no_grad()
-def embed_windows(net, windows, batch=None, precision="f32", path=None):
+def embed_windows(net, windows, batch=None, precision="f32", path=None, schedule="auto"):
     """Embeddings [S, proj] of windows [S, win, nmels] with the module's weights (GPU), `batch`
     windows per call (None: 16384 in fp32; bf16: bf16_batch(), the largest co-resident
     persistent batch).  precision "bf16": the c3 mixed-precision forward (bf16 GEMM operands,
-    fp32 accumulation and state), no activations saved; raises PersistentRecurrenceError if one
-    of its persistent recurrences timed out.  path (bf16 only): "persist" (batches of the
-    training forward's persistent recurrences), "dvec" (sv_dvector_embed_bf16, DVEC_CHUNK windows
-    per call) or None: "dvec" from DVEC_MIN windows on when no batch is given."""
+    fp32 accumulation and state), no activations saved.  Raises PersistentRecurrenceError if a
+    persistent recurrence of the call timed out (either precision).  path (bf16 only): "persist"
+    (batches of the training forward's persistent recurrences), "dvec" (sv_dvector_embed_bf16, DVEC_CHUNK windows
+    per call) or None: "dvec" from DVEC_MIN windows on when no batch is given.  schedule: the
+    recurrence schedule of the stack ('auto', 'per_step', 'persist', ...; ops.embedder_forward)."""
     if precision not in ("f32", "bf16"):
         raise ValueError(f"precision must be 'f32' or 'bf16', got {precision!r}")
     if path not in (None, "persist", "dvec") or (path is not None and precision != "bf16"):
@@ -79,12 +80,12 @@ def embed_windows(net, windows, batch=None, precision="f32", path=None):
     for i in range(0, x.shape[0], batch):
         xb = x[i:i + batch].to(dev).contiguous()
         fwd = embedder_forward_bf16 if precision == "bf16" else embedder_forward
-        emb, _ = fwd(xb, layers, net.projection.weight, net.projection.bias, save=False)
+        emb, _ = fwd(xb, layers, net.projection.weight, net.projection.bias, save=False, schedule=schedule)
         out.append(emb)
-    if precision == "bf16":
-        # a persistent recurrence that timed out (its grid not co-resident) must not return
-        # silently wrong embeddings: wait for this call's status words and raise
-        check_persistent_status(wait=True)
+    # a persistent recurrence that timed out (its grid not co-resident) must not return silently
+    # wrong embeddings: wait for this call's status words and raise (both precisions: the fp32
+    # forward takes its persistent recurrences too where a batch fills the device)
+    check_persistent_status(wait=True)
     return torch.cat(out) if out else torch.zeros((0, net.projection.weight.shape[0]), device=dev)
 
 
@@ -98,12 +99,14 @@ class GraphedEmbedder:
     call is one copy in, one graph launch, one copy out.  Same kernels and numerics as
     embed_windows(..., batch=S); the weights are read through their pointers at every replay
     (in-place updates are seen; a module whose parameters were re-allocated is re-captured).
-    precision: "f32" or "bf16".  Raises PersistentRecurrenceError like embed_windows."""
+    precision: "f32" or "bf16"; schedule as embed_windows.  Raises PersistentRecurrenceError like
+    embed_windows."""
 
-    def __init__(self, net, precision="bf16", bucket=32, max_windows=640):
+    def __init__(self, net, precision="bf16", bucket=32, max_windows=640, schedule="auto"):
         if precision not in ("f32", "bf16"):
             raise ValueError(f"precision must be 'f32' or 'bf16', got {precision!r}")
         self.net, self.precision, self.bucket, self.max_windows = net, precision, bucket, max_windows
+        self.schedule = schedule
         self._graphs = {}
 
     def _key(self, S, T, F):
@@ -119,8 +122,8 @@ class GraphedEmbedder:
 
         def fwd():
             if self.precision == "bf16":
-                return embedder_forward_bf16(x, layers, wp, bp, save=False, status=status)[0]
-            return embedder_forward(x, layers, wp, bp, save=False, status=status)[0]
+                return embedder_forward_bf16(x, layers, wp, bp, save=False, status=status, schedule=self.schedule)[0]
+            return embedder_forward(x, layers, wp, bp, save=False, status=status, schedule=self.schedule)[0]
 
         side = torch.cuda.Stream(dev)  # warm-up off the capture (allocator, lazy init)
         side.wait_stream(torch.cuda.current_stream(dev))
@@ -141,7 +144,7 @@ class GraphedEmbedder:
         if S == 0:
             return torch.zeros((0, self.net.projection.weight.shape[0]), device=dev)
         if S > self.max_windows:  # a long file: the batched path
-            return embed_windows(self.net, x, precision=self.precision)
+            return embed_windows(self.net, x, precision=self.precision, schedule=self.schedule)
         key = self._key(S, T, F)
         if key not in self._graphs:
             self._graphs = {k: v for k, v in self._graphs.items() if k[3] == key[3]}  # drop stale weights

@@ -242,7 +242,8 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
     stacked = PIPELINE_CHUNK > 0 and L > 1 and not need_dx
     # under the persistent schedule the projection bucket is enqueued behind the stack backward
     # (a collective must not run beside a persistent launch); else it overlaps the BPTT
-    late_head = stacked and bool(lib().sv_lstm_f32_persist_ok(B, H, sched))
+    with torch.cuda.device(dev):  # (the library answers for the current device)
+        late_head = stacked and bool(lib().sv_lstm_f32_persist_ok(B, H, sched))
     if grad_ready and not late_head:
         grad_ready(L, None)
     if prod and not stacked:
@@ -273,7 +274,10 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
         _release_status(ps, own)
         if grad_ready:
             if late_head:
-                grad_ready(L, None)
+                # behind the event the library records right after the last recurrence (the status
+                # word is final there), not behind all of main: the buckets then overlap layer 0's
+                # dx / dW GEMMs
+                grad_ready(L, events[L * nch + L - 1] if L > 1 else None)
             for l in range(L - 1, -1, -1):
                 grad_ready(l, events[L * nch + l])
         return grads
@@ -450,8 +454,9 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
         _release_status(sync, own)
         if grad_ready:
             # the projection bucket is enqueued behind the stack backward: with the persistent
-            # recurrences a collective must not run beside them (sv_lstm_stack_bwd_bf16)
-            grad_ready(L, None)
+            # recurrences a collective must not run beside them (sv_lstm_stack_bwd_bf16): behind the
+            # event recorded once every recurrence (and layer L-1's gradients) is done
+            grad_ready(L, events[L * nch + L - 1] if L > 1 else None)
             for l in range(L - 1, -1, -1):
                 grad_ready(l, events[L * nch + l])
         return grads
@@ -512,6 +517,10 @@ class EmbedderFunction(torch.autograd.Function):
         else:
             emb, st = embedder_forward(x.contiguous(), layers, w_p, b_p, save=True, products=products,
                                        status=ctx.status, schedule=schedule)
+        # checked even if no backward follows (eval, d-vectors, anything under no_grad): a hand-off
+        # timeout in this forward raises at the next call / check_persistent_status()
+        ctx.status.arm()
+        _UNCHECKED.append(ctx.status)
         ctx.precision, ctx.products, ctx.schedule = precision, products, schedule
         ctx.st = st
         ctx.L = L
@@ -535,7 +544,8 @@ class EmbedderFunction(torch.autograd.Function):
                                     products=ctx.products, status=ctx.status, schedule=ctx.schedule)
         call("sv_status_poison", ctx.status.ptr(), ptr(flat), flat.numel(), stream_of(flat))
         ctx.status.arm()
-        _UNCHECKED.append(ctx.status)
+        if ctx.status not in _UNCHECKED:
+            _UNCHECKED.append(ctx.status)
         ctx.status = None
         ctx.st = None
         if need_dx:

@@ -201,16 +201,16 @@ class GE2ETrainer:
 
             def ready(k, event):
                 lo, hi = self.buckets[k]
-                if k == len(self.buckets) - 1:
-                    # the status bits go along as flags: under the persistent schedules the head
-                    # bucket is enqueued behind the whole stack backward, so the word is final
-                    # (the per-step schedules never set it)
-                    call("sv_status_to_flag", self.status.ptr(), ptr(self.flags), stream_of(self.flags))
                 if event is None:
                     comm.wait_stream(main)
                 else:
                     comm.wait_event(event)
                 with torch.cuda.stream(comm):  # SUM, never mean (SURVEY §7 hard part 4)
+                    if k == len(self.buckets) - 1:
+                        # the status bits go along as flags, converted on the comm stream behind the
+                        # head bucket's event: under the persistent schedules that event follows the
+                        # last recurrence, so the word is final (the per-step schedules never set it)
+                        call("sv_status_to_flag", self.status.ptr(), ptr(self.flags), stream_of(self.flags))
                     works.append(dist.all_reduce(self.flat_g[lo:hi], group=self.group, async_op=True))
         if bf16 and len(chunks) > 1:
             # chunk 0 writes the gradient buffer, the others a scratch copy added into it; the

@@ -1,6 +1,6 @@
 """Copy a gpu_checkpoint.sh run (gpurun_out/ckpt) into profiles/<tag>_*: kernel stats, timelines,
 the bench line and the roofline cross-check (rocprof average of the K1-shape GEMM vs the bench's
-live HIP-event number).  Usage: python scripts/save_profiles.py r01_v7"""
+live HIP-event number).  Usage: python scripts/save_profiles.py r01_v7 [gpurun_out subdirectory, default ckpt]"""
 import csv
 import json
 import os
@@ -10,7 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
-ck = os.path.join(ROOT, "gpurun_out", "ckpt")
+ck = os.path.join(ROOT, "gpurun_out", sys.argv[2] if len(sys.argv) > 2 else "ckpt")
 prof = os.path.join(ROOT, "profiles")
 for d in ("f32", "bf16"):
     shutil.copy(os.path.join(ck, f"prof_{d}", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_{d}_kernel_stats.csv"))

@@ -182,3 +182,42 @@ def test_graphed_per_file_calls_match_embed_windows(precision):
         net.projection.bias.add_(0.5)
     x = recipe.make_frames(24, 128, 24, 40)
     assert float((ge(x).cpu() - dvector.embed_windows(net, x, batch=128, precision=precision).cpu()).abs().max()) == 0.0
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_graphed_persistent_replays_interleaved_with_eager(precision):
+    """Regression for r03's graph-replay mismatch: GraphedEmbedder with the persistent recurrences
+    forced (schedule 'persist'), replays of three bucket graphs (128, 64, 640 windows) interleaved
+    with eager persistent calls of the same shapes, twice over, each checked bit for bit against
+    the per-step schedule (bit-identical by construction) -- and the eager calls too.  With the
+    arrival counters reset by a hipMemsetAsync, 16-22 of 24 such replays came out wrong (one XCD's
+    workgroups read a hand-off early; scripts/f32_replay_diag.py); the counters are now zeroed by a
+    kernel (sv_zero_counters).  Padded buckets (100, 37 windows) agree to fp32 rounding."""
+    import recipe
+    from conftest import model_dims
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    dims = (40, 768, 3, 256)
+    sd = recipe.make_weights(19, *dims, scale=2.0)
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    net = net.cuda()
+    ge = dvector.GraphedEmbedder(net, precision=precision, schedule="persist")
+    worst = 0.0
+    for rep in range(2):
+        for seed, S in ((20, 128), (21, 128), (22, 100), (23, 37), (25, 640), (26, 640)):
+            x = recipe.make_frames(seed + 100 * rep, S, 24, 40)
+            got = ge(x).cpu()
+            eager = dvector.embed_windows(net, x, batch=S, precision=precision, schedule="persist").cpu()
+            ref = dvector.embed_windows(net, x, batch=S, precision=precision, schedule="per_step").cpu()
+            d_eager = float((eager - ref).abs().max())
+            d_graph = float((got - ref).abs().max())
+            worst = max(worst, d_graph)
+            assert d_eager == 0.0, (rep, S, d_eager)
+            if S % 32 == 0:
+                assert d_graph == 0.0, (rep, S, d_graph)
+            else:
+                assert d_graph <= (5e-3 if precision == "bf16" else 1e-5), (rep, S, d_graph)
+    print(f"\nMEASURED graphed_persist_{precision} worst vs per-step {worst:.3e}")

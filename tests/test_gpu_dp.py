@@ -28,7 +28,7 @@ def _model():
     return net.to("cuda:0"), GE2ELoss("cuda:0")
 
 
-def _worker(rank, world, port, q, precision):
+def _worker(rank, world, port, q, precision, NL=NL, M=M):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -46,10 +46,12 @@ def _worker(rank, world, port, q, precision):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("precision", ["f32", "bf16"])
-def test_dp_two_ranks_equal_single_process(precision):
+@pytest.mark.parametrize("precision,NL,M", [("f32", NL, M), ("bf16", NL, M), ("f32", 128, 2)])
+def test_dp_two_ranks_equal_single_process(precision, NL, M):
     """Also exercises the bucketed, event-driven gradient all-reduce (trainer.py): the
-    per-layer buckets are launched from the backward's completion events."""
+    per-layer buckets are launched from the backward's completion events.  NL = 128: a global
+    N = 256 as in config c5, so the ranks take the split sharded GE2E kernels with a speaker
+    offset (rank 1: s0 = 128) and the single process the split kernels with s0 = 0."""
     from pytorch_speaker_verification_amd.trainer import GE2ETrainer
     world = 2
     net, ge2e = _model()
@@ -64,7 +66,7 @@ def test_dp_two_ranks_equal_single_process(precision):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, precision)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, precision, NL, M)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -81,7 +83,7 @@ def test_dp_two_ranks_equal_single_process(precision):
     p_atol = 1e-5 if precision == "f32" else 5e-5
     for rank, losses, sd, wb in res:
         dev_p = max(float(np.abs(sd[k] - ref_sd[k]).max()) for k in ref_sd)
-        print(f"\nMEASURED dp2_vs_single.{precision} rank {rank} params max-abs {dev_p:.2e} "
+        print(f"\nMEASURED dp2_vs_single.{precision}.N{world * NL} rank {rank} params max-abs {dev_p:.2e} "
               f"loss rel {float(np.max(np.abs(np.array(losses) / np.array(ref_losses) - 1))):.2e}")
         np.testing.assert_allclose(losses[:1], ref_losses[:1], rtol=1e-5)
         np.testing.assert_allclose(losses, ref_losses, rtol=loss_rtol)

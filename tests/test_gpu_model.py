@@ -137,6 +137,46 @@ def test_full_size_c2_against_torch_gpu(schedule):
     _check(f"{tag}.dw_vs_miopen", abs(ge2e.w.grad.item() - w.grad.item()) / max(1, abs(w.grad.item())), 2.5e-5)
 
 
+def test_dropin_loop_body_c2_against_torch_gpu():
+    """The reference's own training-loop body (train_speech_embedder.py:46-65: random perm /
+    unperm, zero_grad, forward, GE2E loss, loss.backward(), torch clip_grad_norm_ x2, SGD.step)
+    run unchanged -- as bench.reference_loop_body -- on this package's modules imported the
+    reference's way (dropin/) and on the stock-PyTorch port (MIOpen nn.LSTM) on the same GPU, at
+    c2 (N = 64 x M = 10, T = 160), two steps from the same weights and the same perms."""
+    import os
+    import random
+    import sys
+    import bench
+    sys.path.append(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dropin"))
+    from speech_embedder_net import GE2ELoss, SpeechEmbedder  # noqa: E402  (the dropin/ shim)
+    dims, N, M, T = (40, 768, 3, 256), 64, 10, 160
+    sd = recipe.make_weights(2025, *dims, scale=1.0)
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    torch_port.load_recipe_weights(net, sd)
+    net = net.to(DEV)
+    ge2e = GE2ELoss(DEV)
+    port = torch_port.SpeechEmbedderPort(*dims)
+    torch_port.load_recipe_weights(port, sd)
+    port = port.to(DEV)
+    ge2e_ref = torch_port.GE2ELossPort(DEV)
+    opt = torch.optim.SGD([{"params": net.parameters()}, {"params": ge2e.parameters()}], lr=0.01)
+    opt_ref = torch.optim.SGD([{"params": port.parameters()}, {"params": ge2e_ref.parameters()}], lr=0.01)
+    x = torch.tensor(recipe.make_frames(1237, N * M, T, dims[0]), device=DEV).reshape(N, M, T, dims[0])
+    for step in range(2):
+        random.seed(step)
+        loss = bench.reference_loop_body(net, ge2e, opt, x, N, M)
+        random.seed(step)
+        loss_ref = bench.reference_loop_body(port, ge2e_ref, opt_ref, x, N, M)
+        _check(f"dropin_loop_c2.step{step}.loss_rel_vs_miopen",
+               abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()), 1e-5)
+    pr = dict(port.named_parameters())
+    dp = max(float((p.detach() - pr[k].detach()).abs().max()) for k, p in net.named_parameters())
+    _check("dropin_loop_c2.params_after_2_steps_vs_miopen", dp, 3e-6)
+    _check("dropin_loop_c2.wb_vs_miopen", max(abs(ge2e.w.item() - ge2e_ref.w.item()),
+                                              abs(ge2e.b.item() - ge2e_ref.b.item())), 1e-5)
+
+
 def test_batch_permutation_invariance():
     """The reference permutes rows around the forward (train_speech_embedder.py:48-57);
     rows are independent, so perm -> embed -> unperm equals embed."""

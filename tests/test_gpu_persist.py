@@ -99,3 +99,68 @@ def test_wavefront_bwd_bf16_against_per_layer(N, M, T):
         print(f"\nMEASURED wave_bwd_vs_layer.{k} {d:.3e}")
         assert d < 2e-2, (k, d)
     print(f"\nMEASURED wave_bwd_vs_layer.worst {worst:.3e}")
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+@pytest.mark.parametrize("B", [128, 640])
+def test_graph_replayed_persistent_forward_state_bit_exact(precision, B):
+    """The persistent forward captured in a HIP graph (save=True, so every layer's h_tm / gates /
+    c_tm stays reachable), replayed with new frames, each replay followed by an eager persistent
+    call of the same shape: every layer's h_tm (including slot 0, the zero initial state), gates
+    and c_tm must equal the per-step schedule's bit for bit.  Before every zeroing in the library
+    went through a kernel (sv_zero_bytes / sv_zero_counters), the replays left junk in the
+    memset-zeroed arrival counters and h_tm slot 0, and one XCD's workgroups read a hand-off
+    early (scripts/f32_replay_diag.py)."""
+    import torch
+    import recipe
+    from conftest import model_dims
+    from pytorch_speaker_verification_amd import ops
+    from pytorch_speaker_verification_amd._lib import PersistStatus
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    dev = torch.device("cuda", 0)
+    dims = (40, 768, 3, 256)
+    sd = recipe.make_weights(19, *dims, scale=2.0)
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    net = net.to(dev)
+    layers = net.LSTM_stack.layer_params()
+    wp, bp = net.projection.weight, net.projection.bias
+    fwd = ops.embedder_forward_bf16 if precision == "bf16" else ops.embedder_forward
+    st_ = PersistStatus(dev)
+    xs = torch.zeros((B, 24, 40), device=dev)
+
+    def f():
+        return fwd(xs, layers, wp, bp, save=True, schedule="persist", status=st_)
+
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        f()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        emb, st = f()
+    for rep in range(4):
+        x = torch.as_tensor(recipe.make_frames(300 + rep, B, 24, 40)).to(dev)
+        xs.copy_(x)
+        g.replay()
+        fwd(x, layers, wp, bp, save=False, schedule="persist")
+        ref, rst = fwd(x, layers, wp, bp, save=True, schedule="per_step")
+        torch.cuda.synchronize()
+        assert int(st_.block[0]) == 0
+        assert torch.equal(emb, ref), (rep, float((emb - ref).abs().max()))
+        for l in range(3):
+            # (bf16: the persistent kernels keep fp32 h only for the last step; the bf16 copies of
+            # h, the next layer's input, are x_tm[l + 1])
+            if precision == "f32":
+                assert torch.equal(st.h_tm[l], rst.h_tm[l]), (rep, l, "h_tm")
+                assert float(st.h_tm[l][0].abs().max()) == 0.0
+            elif l + 1 < 3:
+                assert torch.equal(st.x_tm[l + 1], rst.x_tm[l + 1]), (rep, l, "h_bf")
+            assert torch.equal(st.gates[l], rst.gates[l]), (rep, l, "gates")
+            assert torch.equal(st.c_tm[l], rst.c_tm[l]), (rep, l, "c_tm")
+        assert torch.equal(st.h_last, rst.h_last), (rep, "h_last")
