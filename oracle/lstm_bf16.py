@@ -124,6 +124,7 @@ def embedder_backward(params, demb, cache, L, bf16=True, device="cpu"):
         grads[f"LSTM_stack.bias_ih_l{l}"] = db
         grads[f"LSTM_stack.bias_hh_l{l}"] = db.clone()
         dhs = (dG2 @ qWih).reshape(B, T, -1)
+    grads["input"] = dhs  # d loss / d x [B, T, F]: layer 0's dx_t = q(dG_t) q(W_ih)
     return grads
 
 

@@ -976,7 +976,10 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
   if (e != hipSuccess) return (int)e;
   const unsigned limit = persist_limit();
   const int fault = fwd_fault();
-  constexpr int dbg = 0, pipe = 1;  // no diagnostic skips; LDS-pipelined A fragments
+#ifndef SV_PFWD_DEBUG  // A/B diagnostic builds only (persist3 forward: 16 = x-projection always step 0's, cache-hot)
+#define SV_PFWD_DEBUG 0
+#endif
+  constexpr int dbg = SV_PFWD_DEBUG, pipe = 1;  // (product: no diagnostic skips); LDS-pipelined A fragments
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   if (wide) {
     const int rc = sv_persist3_fwd_launch(dim3(grid.x * grid.y), (int)grid.x, stream, whh_bf, gates, c_tm, h_tm, h_bf,

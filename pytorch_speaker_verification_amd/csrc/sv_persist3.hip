@@ -1,7 +1,13 @@
 // Wide-tile persistent backward recurrence (see the kernel comment).  Its own translation unit:
 // built with -mllvm -amdgpu-mfma-vgpr-form=1 (Makefile) so the two accumulators are VGPRs and
 // all 256 AGPRs hold W_hh fragments.
+#include <algorithm>
+
 #include "sv_persist_dev.h"
+
+#ifndef SV_P3_PREFETCH  // operand-prefetch helper workgroups beside the wide persistent backward (A/B: 0 = none)
+#define SV_P3_PREFETCH 0
+#endif
 #include "../../include/sv_ge2e.h"
 
 // ============================================================================
@@ -18,12 +24,78 @@
 // NL: the last NL k-steps of the second W_hh half are read from LDS (staged once, 16 B per lane per
 // fragment, prefetched two k-steps ahead) -- the registers cannot hold all 2 x NS fragments beside
 // the step's working set
+// the helper (prefetch) workgroups of the wide backward: step s's operands (bf16 activations,
+// c_{s-1}, dh_up) of the XCD group's tiles, once that group's first row block has finished step
+// s + 2 -- a step ahead of the compute waves' own LDS-DMA of them (issued at the end of step s + 1;
+// persist_prefetch16, sv_persist_dev.h)
+__device__ void p3_bwd_prefetch(const bf16_t* acts, const float* c_tm, const float* dhup, int up_full, int T, int B,
+                                int H, const unsigned* cnt, int nub, int ncomp, int npf, const unsigned* status,
+                                unsigned limit) {
+  constexpr int BM = 32, U = 64, TB = 4;  // tiles per batch: 8 x 4 = 32 loads (128 KB) in flight
+  const int tid = threadIdx.x;
+  const int p = blockIdx.x - ncomp, x = blockIdx.x & 7, k = p >> 3, nk = npf >> 3;
+  int l0, l1;
+  persist_xcd_tiles(x, ncomp, l0, l1);
+  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
+  const unsigned* c0 = cnt + (l0 / nub) * SV_PCNT_STRIDE;
+  __shared__ int skip;
+  for (int s = T - 1; s >= 0; --s) {
+    if (tid == 0) {
+      if (s + 2 <= T - 1) {
+        unsigned spins = 0;
+        const unsigned target = (unsigned)nub * (unsigned)(T - 1 - (s + 2) + 1);
+        while (__hip_atomic_load(c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+               !__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) && ++spins < limit)
+          __builtin_amdgcn_s_sleep(2);
+      }
+      // too late for step s (its consumers have finished step s + 1 and issued their own DMA of
+      // it): skip it, so a slow helper never holds the launch open
+      skip = __hip_atomic_load(c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nub * (unsigned)(T - 1 - s);
+    }
+    __syncthreads();
+    const bool sk = skip;
+    __syncthreads();
+    if (sk) continue;
+    const float* up = dhup ? (up_full ? dhup + (long)s * BH : (s == T - 1 ? dhup : nullptr)) : nullptr;
+    const __amdgpu_buffer_rsrc_t ra = sv_rsrc(acts + (long)s * BG, (unsigned)(BG * 2));
+    const __amdgpu_buffer_rsrc_t rc = sv_rsrc(c_tm + (long)(s > 0 ? s - 1 : 0) * BH, s > 0 ? (unsigned)(BH * 4) : 0u);
+    const __amdgpu_buffer_rsrc_t ru = sv_rsrc(up ? up : c_tm, up ? (unsigned)(BH * 4) : 0u);
+    // a tile's 16-B pieces: activations 32 rows x 4 gates x 8, c_{s-1} and dh_up 32 rows x 16 each;
+    // thread tid takes pieces tid + 256 i; loads into registers, TB tiles in flight (an absent
+    // operand's range is empty: its loads return zeros without a memory access)
+    for (int L0 = l0 + k; L0 < l1; L0 += TB * nk) {
+      u32x4_t v[TB][8];
+#pragma unroll
+      for (int b = 0; b < TB; ++b) {
+        const int L = min(L0 + b * nk, l1 - 1), ub = L % nub, rb = L / nub, j0 = ub * U;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int e = tid + 256 * i;
+          if (i < 4) {
+            const int row = min(rb * BM + (e >> 5), B - 1), q = (e >> 3) & 3, c = e & 7;
+            v[b][i] = __builtin_amdgcn_raw_buffer_load_b128(
+                ra, (unsigned)(((long)row * G + (long)q * H + j0 + 8 * c) * 2), 0, 0);
+          } else {
+            const int f = e & 511, row = min(rb * BM + (f >> 4), B - 1), c = f & 15;
+            v[b][i] = __builtin_amdgcn_raw_buffer_load_b128(i < 6 ? rc : ru,
+                                                            (unsigned)(((long)row * H + j0 + 4 * c) * 4), 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < TB; ++b)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(v[b][i]));
+    }
+  }
+}
+
 template <int NS, int P, int NL, bool DEFER>
 __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     const bf16_t* __restrict__ whhT, const bf16_t* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
     bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit,
-    int fault, int dbg, float* __restrict__ dbp, unsigned long long* __restrict__ stamps) {
+    int fault, int dbg, float* __restrict__ dbp, unsigned long long* __restrict__ stamps, int ncomp, int npf) {
   constexpr int BM = 32, U = 64, KR = 2;  // rows, units, row passes of the epilogue (16 rows each)
   constexpr int LDR = U + 4;              // red [4][BM][LDR] fp32
   constexpr int LDG = 4 * U + 8;          // dgs [BM][LDG] bf16 (row-major dG tile)
@@ -38,12 +110,16 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
   float* ewc = reinterpret_cast<float*>(ewa + BM * 512);    // [BM][U] c_{t-1}
   float* ewu = ewc + BM * U;                                // [BM][U] dh_up
   char* wl = reinterpret_cast<char*>(ewu + BM * U);         // [4 waves][NL][64 lanes][16 B]
+  if ((int)blockIdx.x >= ncomp) {  // a helper workgroup: operand prefetch only
+    p3_bwd_prefetch(acts, c_tm, dhup, up_full, T, B, H, cnt, nub, ncomp, npf, status, limit);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   int ub, rb;
-  persist_tile(xcd, nub, ub, rb);
+  persist_tile(xcd, nub, ub, rb, ncomp);
   const int j0 = ub * U, b0 = rb * BM;
-  const int nrb = gridDim.x / nub;
+  const int nrb = ncomp / nub;
   const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
   const long FS = (long)nrb * BM * G;
   unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
@@ -84,6 +160,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
   // step tt's operands into LDS (buffer_load ... lds; rows past B and absent operands read zeros)
   // piece i (0..7) of step tt's operand DMA: 0-3 activations, 4-5 c_{t-1}, 6-7 dh_up
   auto ew_piece = [&](int tt, int i) {
+    if (dbg & 512) tt = T - 1;  // (profiling only: every step reads step T-1's operands, cache-hot)
     if (i < 4) {
       const __amdgpu_buffer_rsrc_t ra_ = sv_rsrc(acts + (long)tt * BG, (unsigned)(BG * 2));
       const int p = (g * 4 + i) * 64 + lane, row = p >> 5, sl = p & 31;
@@ -308,9 +385,11 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + SV_SYNC_STAMP);
   // (the DEFER form -- the operand DMA and the dG / dG^T stores inside the next step's k-loop --
   // measured slower: c3 bwd 1205 vs 1086 us per layer; the fragment waits count the older stores)
-  hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL, false>), grid, dim3(256), lds, stream, whhT, acts, c_tm,
-                     dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbg, dbp,
-                     stamps);
+  // operand-prefetch helper workgroups on the CUs the grid leaves free, the same number per XCD
+  const int ncomp = (int)grid.x, npf = SV_P3_PREFETCH ? std::min(16, (sv_stream_cus(stream) - ncomp) / 8 * 8) : 0;
+  hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL, false>), dim3(ncomp + npf), dim3(256), lds, stream, whhT,
+                     acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault,
+                     dbg, dbp, stamps, ncomp, npf);
   return (int)hipGetLastError();
 }
 
@@ -425,6 +504,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
   constexpr int HALF = K / 2, CH = BM * HALF / 8 / 256;
   uint2 xg[KR][4];
   auto load_xg = [&](int tt) {
+    if (dbg & 16) tt = 0;  // (profiling only: every step reads step 0's x-projection, cache-hot)
     if constexpr (XF > 0) {
       load_x(tt);
       return;
@@ -780,6 +860,17 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
   }
   load_ew(T - 1);
   const int t_end = has_dx ? -1 : 0;
+#ifdef SV_WB_STAMP  // A/B stamp builds only: wave 0's cycles per phase, summed over t = T-2 .. 0
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tl = __builtin_amdgcn_s_memtime();
+  auto wmark = [&](int i, int t_) {
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    if (t_ < T - 1 && t_ >= 0) ph[i] += n - tl;
+    tl = n;
+  };
+#define WB_MARK(i) wmark(i, t)
+#else
+#define WB_MARK(i)
+#endif
   for (int t = T - 1; t >= t_end; --t) {
     f32x16 acc0, acc1;
 #pragma unroll
@@ -789,6 +880,18 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
       if (has_up && t >= 0) persist_wait(up_cnt, producers * (unsigned)(T - t + 1), a.status, a.limit, 2u);
     }
     __syncthreads();
+    WB_MARK(0);  // 0: hand-off waits (own layer, layer above) + the previous step's operand DMA
+    // dh_up_t (hand-off from the layer above, sc1 loads) or the top layer's dh_last: issued before
+    // the k-loop, so its round trip overlaps the MFMAs instead of opening the epilogue (the layer
+    // above's counter was polled just now)
+    float4 upv = float4{0.f, 0.f, 0.f, 0.f};
+#ifndef SV_WB_LATE_UP
+    u32x4_t upx = u32x4_t{0u, 0u, 0u, 0u};
+    const float* upp = t >= 0 ? (has_up ? a.dx[l + 1] + (long)t * BH : (t == T - 1 ? a.dh_last : nullptr)) : nullptr;
+    if (upp)
+      upx = __builtin_amdgcn_raw_buffer_load_b128(sv_rsrc(upp, (unsigned)(BH * 4)), (unsigned)((gbv * H + j0 + u4) * 4),
+                                                  0, 16 /* sc1: hand-off */);
+#endif
     if (t < T - 1) {
       // A fragments of dG_{t+1} (this layer's hand-off slot): k-step s at (rb 4 + g) FRAG + s 512
       const __amdgpu_buffer_rsrc_t ra = sv_rsrc(a.dgf[l] + (long)(t + 1) * FS, (unsigned)(FS * 2));
@@ -818,6 +921,7 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
         }
       }
     }
+    WB_MARK(1);  // 1: k-loop (A fragments of dG_{t+1} from the hand-off + MFMAs)
     // per-gate partials: red0 = dh_rec, red1 = dx
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -826,8 +930,7 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
     __syncthreads();
-    // dh_up_t (hand-off from the layer above, sc1 loads) or the top layer's dh_last
-    float4 upv = float4{0.f, 0.f, 0.f, 0.f};
+#ifdef SV_WB_LATE_UP  // A/B: the r03 placement (loaded here, after the k-loop)
     if (t >= 0) {
       const float* up = has_up ? a.dx[l + 1] + (long)t * BH : (t == T - 1 ? a.dh_last : nullptr);
       if (up) {
@@ -837,6 +940,9 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
         upv = float4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
       }
     }
+#else
+    upv = float4{__uint_as_float(upx.x), __uint_as_float(upx.y), __uint_as_float(upx.z), __uint_as_float(upx.w)};
+#endif
     // dx_{t+1} of this layer: gate partials summed in gate order, 16-B sc1 stores (hand-off)
     if (has_dx && t < T - 1) {
       const int b = brow;
@@ -894,6 +1000,7 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
       cv = cpv;
     }
     __syncthreads();
+    WB_MARK(2);  // 2: exchange, dh_up, dx_{t+1} hand-off stores, cell backward, dG tiles
     // the dG_t hand-off: 8 KB per workgroup in fragment order (gate, 2 k-steps), 16-B sc1 stores
     if (t >= 0) {
       const __amdgpu_buffer_rsrc_t rw = sv_rsrc(a.dgf[l] + (long)t * FS, (unsigned)(FS * 2));
@@ -911,6 +1018,7 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
     __syncthreads();
     if (tid == 0 && persist_arrive_ok(a.fault, t == T - 1))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    WB_MARK(3);  // 3: dG_t hand-off stores + drain + arrival
     if (t >= 0 && a.dgT[l]) {  // dG_t^T (the dW GEMMs' operand), then the next step's operands
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -922,7 +1030,17 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
       }
     }
     if (t > 0) load_ew(t - 1);
+    WB_MARK(4);  // 4: dG^T stores + next operand DMA issue
   }
+#ifdef SV_WB_STAMP
+  if (tid == 0 && blockIdx.x < SV_NSTAMP_WG / 2) {  // second half of the stamp slots (the forward's use the first)
+    unsigned long long* st =
+        reinterpret_cast<unsigned long long*>(a.status + SV_SYNC_STAMP) + (SV_NSTAMP_WG / 2 + blockIdx.x) * SV_NSTAMP;
+    for (int i = 0; i < 5; ++i) st[i] = ph[i];
+    st[5] = (unsigned long long)l;
+  }
+#endif
+#undef WB_MARK
   // bias gradients: this tile's column sums over its rows (in order), one partial per row block
   if (a.dbp[l]) {
     __syncthreads();

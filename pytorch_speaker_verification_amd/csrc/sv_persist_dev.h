@@ -15,8 +15,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t sv_rsrc(const void* p, unsigne
 // dispatched to XCD i % 8; with xcd = 1 each XCD gets a contiguous range of logical tiles, so
 // the workgroups that share a row block (and read the same handed-off rows) sit mostly on one
 // XCD and the second and later readers hit that XCD's L2 instead of the fabric.
-__device__ __forceinline__ void persist_tile(int xcd, int nub, int& ub, int& rb) {
-  const int i = blockIdx.x, n = gridDim.x;
+// ncomp: the compute workgroups (blocks past them, if any, are helper workgroups)
+__device__ __forceinline__ void persist_tile(int xcd, int nub, int& ub, int& rb, int ncomp = 0) {
+  const int i = blockIdx.x, n = ncomp ? ncomp : gridDim.x;
   int L = i;
   if (xcd) {
     const int x = i & 7, q = n >> 3, r = n & 7;
@@ -102,3 +103,22 @@ struct W3Frag {
     return *reinterpret_cast<const bf16x8_t*>(pb + ((unsigned)(32 * (s - 32)) ^ fb));
   }
 };
+
+// The logical tiles [l0, l1) that persist_tile (xcd = 1) gives the blocks of XCD group x (blocks
+// b with b % 8 == x) of an n-block grid
+__device__ __forceinline__ void persist_xcd_tiles(int x, int n, int& l0, int& l1) {
+  const int q = n >> 3, r = n & 7;
+  l0 = x * q + min(x, r);
+  l1 = l0 + q + (x < r ? 1 : 0);
+}
+
+// Operand prefetch by the helper workgroups of a persistent grid (blocks ncomp .. ncomp + npf - 1,
+// npf a multiple of 8, so every XCD group gets npf / 8 of them): pull 16-B pieces of the bytes the
+// XCD group's compute workgroups will DMA a few steps later into that XCD's L2 (and the
+// Infinity Cache) by LDS-DMA into a scratch LDS slot -- no registers, no waits on the compute
+// waves' in-order vmcnt.  Speed only: nothing reads the scratch slot, and a prefetch that comes
+// late (or never) changes no result.
+__device__ __forceinline__ void persist_prefetch16(const void* p, char* lds_scratch) {
+  typedef __attribute__((address_space(1))) void* glb_ptr_t;
+  __builtin_amdgcn_global_load_lds((glb_ptr_t)p, (lds_ptr_t)lds_scratch, 16, 0, 0);
+}

@@ -23,9 +23,14 @@
 // gate order (K3's order).
 // Outputs are the per-step kernels' buffers (activations, c, h, h^T / dG, dG^T), so either direction
 // composes with the other schedule; results agree with the per-step kernels to fp32 rounding.
+#include <algorithm>
+
 #include "sv_persist_dev.h"
 #include "../../include/sv_ge2e.h"
 
+#ifndef SV_PF32_PREFETCH  // operand-prefetch helper workgroups beside the persistent backward (A/B: 0 = none)
+#define SV_PF32_PREFETCH 1
+#endif
 #ifndef SV_PF32_ACQ  // A/B diagnostic builds only (0: the product's relaxed poll)
 #define SV_PF32_ACQ 0
 #endif
@@ -363,12 +368,63 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
 // ============================================================================
 constexpr int PH_BM = 32;                      // rows of a half
 
+// the helper (prefetch) workgroups of the backward: step s's operands (activations, c_{s-1}, dh_up)
+// of the XCD group's tiles, once that group's first row block has finished half 0 of step s + 2 --
+// a step ahead of the compute waves' own LDS-DMA of them (issued at the end of step s + 1)
+__device__ void pf32_bwd_prefetch(const float* acts, const float* c_tm, const float* dhup, int up_full, int T, int B,
+                                  int H, const unsigned* cnt, int nub, int ncomp, int npf, const unsigned* status,
+                                  unsigned limit, char* scratch) {
+  const int tid = threadIdx.x, g = tid >> 6;
+  const int p = blockIdx.x - ncomp, x = blockIdx.x & 7, k = p >> 3, nk = npf >> 3;
+  int l0, l1;
+  persist_xcd_tiles(x, ncomp, l0, l1);
+  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
+  const unsigned* c0 = cnt + (l0 / nub) * 2 * SV_PCNT_STRIDE;  // (row block, half 0) of the group's first tile
+  char* dst = scratch + g * 1024;
+  int* skip = reinterpret_cast<int*>(scratch + 4096);
+  for (int s = T - 1; s >= 0; --s) {
+    if (tid == 0) {
+      if (s + 2 <= T - 1) {
+        unsigned spins = 0;
+        const unsigned target = (unsigned)nub * (unsigned)(T - 1 - (s + 2) + 1);
+        while (__hip_atomic_load(c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+               !__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) && ++spins < limit)
+          __builtin_amdgcn_s_sleep(8);
+      }
+      // too late for step s (the group's first row block is past half 0 of step s + 1): skip it, so
+      // a slow helper never holds the launch open
+      *skip = __hip_atomic_load(c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nub * (unsigned)(T - 1 - s);
+    }
+    __syncthreads();
+    const bool sk = *skip;
+    __syncthreads();
+    if (sk) continue;
+    const float* up = dhup ? (up_full ? dhup + (long)s * BH : (s == T - 1 ? dhup : nullptr)) : nullptr;
+    // a tile's pieces: 64 rows x (4 gates of activations + c_{s-1} + dh_up) x 8 pieces of 16 B
+    for (int L = l0 + k; L < l1; L += nk) {
+      const int ub = L % nub, rb = L / nub, j0 = ub * PF_U;
+      for (int i = tid; i < 6 * 64 * 8; i += 256) {
+        const int kind = i >> 9, r2 = min(rb * PF_BM + ((i >> 3) & 63), B - 1), pc = i & 7;
+        const float* src = nullptr;
+        if (kind < 4)
+          src = acts + (long)s * BG + (long)r2 * G + (long)kind * H + j0 + 4 * pc;
+        else if (kind == 4 && s > 0)
+          src = c_tm + (long)(s - 1) * BH + (long)r2 * H + j0 + 4 * pc;
+        else if (kind == 5 && up)
+          src = up + (long)r2 * H + j0 + 4 * pc;
+        if (src) persist_prefetch16(src, dst);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
 template <int NKG, int P, int NV, int NL>
 __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
     const float* __restrict__ whhT, const float* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, float* __restrict__ dg, float* __restrict__ dgT, long lddgT,
     float* dgf, int T, int Bp, int B, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit, int fault,
-    float* __restrict__ dbp) {
+    float* __restrict__ dbp, int ncomp, int npf) {
   constexpr int H = 8 * NKG;
   static_assert(PF_NA + NV + NL == NKG, "weight split");
   constexpr int LDR = PF_U + 4;      // red [4][32][LDR]
@@ -383,12 +439,16 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
   float* gts = red;
   float* dgs = ea;
   char* wl = reinterpret_cast<char*>(red + 4 * PH_BM * LDR);
+  if ((int)blockIdx.x >= ncomp) {  // a helper workgroup: operand prefetch only
+    pf32_bwd_prefetch(acts, c_tm, dhup, up_full, T, B, 8 * NKG, cnt, nub, ncomp, npf, status, limit, smem);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   int ub, rb;
-  persist_tile(xcd, nub, ub, rb);
+  persist_tile(xcd, nub, ub, rb, ncomp);
   const int j0 = ub * PF_U;
-  const int nrb = gridDim.x / nub;
+  const int nrb = ncomp / nub;
   const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
   const long FS = (long)nrb * 4 * 2 * FBLK;
   float wa[4 * PF_NA], wv[4 * NV];
@@ -411,6 +471,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
   // half-step (tt, hf)'s operands -> LDS: wave g: 4 activation pieces (rows 8 g ..), 1 of c_{t-1}, 1
   // of dh_up; absent operands written as zeros into the same slots
   auto load_ew = [&](int tt, int hf) {
+#ifdef SV_PF32_HOTOPS  // A/B diagnostic (results invalid): every step reads step T-1's operands, cache-hot
+    tt = T - 1;
+#endif
     int z = 0;
     asm volatile("" : "+v"(z));
     const int gz = g + z, b0 = rb * PF_BM + hf * PH_BM;
@@ -480,6 +543,16 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         }
         __syncthreads();
         PB_STAMP(0);  // 0: hand-off wait
+#ifndef SV_PF32_STAMP
+        // a scalar-memory op here keeps hipcc's wait for the first A fragment counted (vmcnt(P - 1));
+        // without one it emitted vmcnt(0) before half 0's first MFMA, so every half-step waited for
+        // all P fragments before its k-loop started (+0.35 ms per c2 step; the stamp builds, whose
+        // s_memtime sits here, never had it)
+        {
+          const unsigned long long t_ = __builtin_amdgcn_s_memtime();
+          asm volatile("" ::"s"(t_));
+        }
+#endif
         const __amdgpu_buffer_rsrc_t ra = sv_rsrc(dgf + (long)(t + 1) * FS, (unsigned)(FS * 4));
         const unsigned base = ((unsigned)(((rb * 4 + g) * 2 + hf) * FBLK) + (unsigned)lane * 4u) * 4u;
         u32x4_t fa[P];
@@ -580,6 +653,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         for (int q = 0; q < 4; ++q)
           *reinterpret_cast<f32x4*>(dp + q * H) = *reinterpret_cast<const f32x4*>(dgs + erow * LDG + q * PF_U + 4 * quad);
       }
+#ifndef SV_PF32_NODGT  // A/B diagnostic (results invalid): no dG^T stores
 #pragma unroll
       for (int i = 0; i < 4; ++i) {  // 128 gate-unit rows x 8 pieces of 4 batch columns
         const int p = tid + 256 * i, gu = p >> 3, c = p & 7, gbc = b0 + 4 * c;
@@ -591,6 +665,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
           *reinterpret_cast<f32x4*>(dgT + ((long)(gu >> 5) * H + j0 + (gu & 31)) * lddgT + (long)t * Bp + gbc) = v;
         }
       }
+#endif
       if (hf == 0 || t > 0) {
         __syncthreads();  // dgs / gts read by every wave before the next half-step's operands land
         if (hf == 0)
@@ -697,9 +772,11 @@ int sv_persist_bwd_f32(int T, int B, int H, const float* whhT, const float* acts
   hipError_t e = (hipError_t)sv_zero_counters(cnt, 1, 0, 2 * nrb * SV_PCNT_STRIDE, stream);
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
-  hipLaunchKernelGGL((lstm_persist_bwd_f32_h2_kernel<96, PH_BWD_P, PH_BWD_NV, PH_BWD_NL>), dim3(nub * nrb),
+  // helper workgroups on the CUs the grid leaves free, the same number per XCD (c2: 16)
+  const int ncomp = nub * nrb, npf = SV_PF32_PREFETCH ? std::min(16, (sv_stream_cus(stream) - ncomp) / 8 * 8) : 0;
+  hipLaunchKernelGGL((lstm_persist_bwd_f32_h2_kernel<96, PH_BWD_P, PH_BWD_NV, PH_BWD_NL>), dim3(ncomp + npf),
                      dim3(256), ph_bwd_lds(), stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, (long)T * Bp, dgf, T,
-                     Bp, B, cnt, nub, PF_XCD, sync, sv_persist_limit(), sv_persist_fault(1), dbp);
+                     Bp, B, cnt, nub, PF_XCD, sync, sv_persist_limit(), sv_persist_fault(1), dbp, ncomp, npf);
   SV_LAUNCH_CHECK();
   if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
   // bias gradients: the row blocks' partials summed in order (no row-sum pass over dG^T)

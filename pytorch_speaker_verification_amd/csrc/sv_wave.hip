@@ -267,6 +267,7 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
   if (STAMP && tid == 0 && blockIdx.x < SV_NSTAMP_WG) {
     unsigned long long* st = reinterpret_cast<unsigned long long*>(a.status + SV_SYNC_STAMP) + blockIdx.x * SV_NSTAMP;
     for (int i = 0; i < 7; ++i) st[i] = ph[i];
+    st[7] = (unsigned long long)l;
   }
 }
 
@@ -343,9 +344,14 @@ int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, cons
   // LDS-DMA staging of both A tiles (wave3).  The register-staged form (wave2: eight dependent
   // global round trips per step, same products in the same order) measured 1.20 vs 0.85 ms for
   // the c4 rank-shape forward.
-  a.stamp = 0;
   a.dbg = 0;
+#ifdef SV_WAVE3_STAMP  // A/B stamp builds only: per-phase cycle sums of wave 0, workgroups < 512
+  a.stamp = 1;
+  hipLaunchKernelGGL(lstm_wave3_fwd_bf16_kernel<true>, dim3(L * a.nub * a.nrb), dim3(WV_NT), 0, stream, a);
+#else
+  a.stamp = 0;
   hipLaunchKernelGGL(lstm_wave3_fwd_bf16_kernel<false>, dim3(L * a.nub * a.nrb), dim3(WV_NT), 0, stream, a);
+#endif
   SV_LAUNCH_CHECK();
   if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
   return SV_OK;

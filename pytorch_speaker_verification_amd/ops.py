@@ -410,9 +410,12 @@ def embedder_forward_dvec_bf16(x, layers, w_p, b_p):
 
 
 def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, status=None, probe=None,
-                           schedule="auto"):
+                           schedule="auto", need_dx=False):
     """Backward of embedder_forward_bf16 (same ``grads`` / ``grad_ready`` contract as
-    embedder_backward; ``status`` and ``schedule`` as embedder_forward_bf16)."""
+    embedder_backward; ``status`` and ``schedule`` as embedder_forward_bf16).  need_dx: also the
+    input gradient dx [B,T,F] (returns (grads, dx)), formed by the per-layer kernels, whose layer-0
+    step adds the dx = dG W_ih GEMM (bf16 operands, fp32 accumulation) the stacked schedules skip;
+    the per-layer per-step kernels are bit-identical to the persistent ones."""
     sched = schedule_flags(schedule)
     demb = demb.contiguous()
     require_device(demb)
@@ -431,7 +434,7 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
     call("sv_proj_norm_bwd", ptr(demb), ptr(st.emb), ptr(st.ynorm), ptr(st.h_last), B, H, P, ptr(w_p),
          ptr(grads[4 * L]), ptr(grads[4 * L + 1]), ptr(dh_last), ptr(ws), s)
     Fmax = max(st.x_tm[l].shape[2] for l in range(L))
-    if PIPELINE_CHUNK > 0 and L > 1:
+    if PIPELINE_CHUNK > 0 and L > 1 and not need_dx:
         F0 = st.x_tm[0].shape[2]
         ws = _ws(lib().sv_lstm_stack_bwd_bf16_workspace(L, T, B, F0, H), dev)
         dgs = [_bf((T, B, 4 * H), dev) for _ in range(L)]
@@ -473,7 +476,7 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
         wihT = _bf((Fl, 4 * H), dev)
         call("sv_transpose_cast_bf16", ptr(w_ih), Fl, 4 * H, Fl, ptr(wihT), 4 * H, s)
         call("sv_transpose_cast_bf16", ptr(w_hh), H, 4 * H, H, ptr(whhT), 4 * H, s)
-        dx = torch.empty((T, B, Fl), dtype=torch.float32, device=dev) if l > 0 else None
+        dx = torch.empty((T, B, Fl), dtype=torch.float32, device=dev) if (l > 0 or need_dx) else None
         if l == 0:
             xT, ld_xT = ptr(st.xT0), T * Bp
         else:
@@ -484,6 +487,10 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
         if grad_ready:
             grad_ready(l, None)
         dh_up, full = dx, 1
+    if need_dx:
+        dxb = torch.empty((B, T, dh_up.shape[2]), dtype=torch.float32, device=dev)
+        call("sv_frames_to_time_major", ptr(dh_up), ptr(dxb), T, B, dh_up.shape[2], s)  # [T,B,F] -> [B,T,F]
+        return grads, dxb
     return grads
 
 
@@ -535,10 +542,8 @@ class EmbedderFunction(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         grads, flat = _flat_grads(params, demb.device)
         if ctx.precision == "bf16":
-            if need_dx:
-                raise NotImplementedError("input gradients are only produced by the fp32 path")
             out = embedder_backward_bf16(ctx.st, demb, layers, params[4 * L], grads=grads, status=ctx.status,
-                                         schedule=ctx.schedule)
+                                         schedule=ctx.schedule, need_dx=need_dx)
         else:
             out = embedder_backward(ctx.st, demb, layers, params[4 * L], grads=grads, need_dx=need_dx,
                                     products=ctx.products, status=ctx.status, schedule=ctx.schedule)

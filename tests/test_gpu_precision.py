@@ -146,3 +146,32 @@ def test_c4_four_rank_shape_bf16_wavefront_halves_against_oracle():
     assert bf16_row_chunks(N * M, 768, T=T) == [(0, 80), (80, 160)]
     _compare("c4_4rank_halves", dims, N, M, T, 4141, dict(emb=5e-3, loss=2e-3, grad=5e-2, param=2e-5),
              oracle_device=DEV)
+
+
+@pytest.mark.parametrize("precision", ["bf16", "f32"])
+def test_input_gradient_through_embedder_function(precision):
+    """loss.backward() with frames that require grad: EmbedderFunction returns dx [B,T,F] in both
+    precisions (bf16: the per-layer kernels with the layer-0 dx = dG W_ih GEMM).  Against the bf16
+    oracle's layer-0 dx (fp32 mode for f32) for d emb = a fixed random direction, c4 rank dims at
+    T = 24."""
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    dims, B, T, seed = (40, 768, 3, 256), 80, 24, 5151
+    sd = recipe.make_weights(seed, *dims, scale=3.0)
+    x = recipe.make_frames(seed + 1, B, T, dims[0])
+    g = np.random.default_rng(seed + 2).standard_normal((B, dims[3])).astype(np.float32)
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    net = net.to(DEV)
+    net.precision = precision
+    xt = torch.tensor(x, device=DEV, requires_grad=True)
+    emb = net(xt)
+    emb.backward(torch.tensor(g, device=DEV))
+    dx = xt.grad.detach().cpu().numpy()
+    bf = precision == "bf16"
+    r_emb, cache = lstm_bf16.embedder_forward(sd, x, dims[2], bf16=bf)
+    r_dx = lstm_bf16.embedder_backward(sd, g, cache, dims[2], bf16=bf)["input"].numpy()
+    assert dx.shape == r_dx.shape == (B, T, dims[0])
+    _check(f"dx_{precision}.rel_vs_oracle", _rel(dx, r_dx), 5e-2 if bf else 1e-4)
