@@ -781,7 +781,7 @@ def main():
         out["roofline_dw_gemm"] = dict(roofline_entry(
             f"gemm_f32_256_kernel<256,32,1,0> (dW_hh = dG^T h of the persistent fp32 backward: split-K slabs, the c2 "
             f"step's largest kernel by busy time), M={4 * H} N={H} K={T * B}", fl_w, ms_w, MI355X_FP32_MFMA_TFLOPS,
-            pmc_traffic("gemm_f32_256_kernel<256,32,1,0>@dW"), 5,
+            pmc_traffic("gemm_f32_256_kernel<256,32,1,0>@dW.in_step"), 5,
             "isolated launches after 3 untimed ones, HIP events on its stream"), algorithmic_bytes=by_w)
         ms_k, fl_k = time_step_kernel(640, H, dev)
         out["roofline_step_kernel"] = roofline_entry(

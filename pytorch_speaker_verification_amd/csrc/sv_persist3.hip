@@ -1,13 +1,7 @@
 // Wide-tile persistent backward recurrence (see the kernel comment).  Its own translation unit:
 // built with -mllvm -amdgpu-mfma-vgpr-form=1 (Makefile) so the two accumulators are VGPRs and
 // all 256 AGPRs hold W_hh fragments.
-#include <algorithm>
-
 #include "sv_persist_dev.h"
-
-#ifndef SV_P3_PREFETCH  // operand-prefetch helper workgroups beside the wide persistent backward (A/B: 0 = none)
-#define SV_P3_PREFETCH 0
-#endif
 #include "../../include/sv_ge2e.h"
 
 // ============================================================================
@@ -24,78 +18,12 @@
 // NL: the last NL k-steps of the second W_hh half are read from LDS (staged once, 16 B per lane per
 // fragment, prefetched two k-steps ahead) -- the registers cannot hold all 2 x NS fragments beside
 // the step's working set
-// the helper (prefetch) workgroups of the wide backward: step s's operands (bf16 activations,
-// c_{s-1}, dh_up) of the XCD group's tiles, once that group's first row block has finished step
-// s + 2 -- a step ahead of the compute waves' own LDS-DMA of them (issued at the end of step s + 1;
-// persist_prefetch16, sv_persist_dev.h)
-__device__ void p3_bwd_prefetch(const bf16_t* acts, const float* c_tm, const float* dhup, int up_full, int T, int B,
-                                int H, const unsigned* cnt, int nub, int ncomp, int npf, const unsigned* status,
-                                unsigned limit) {
-  constexpr int BM = 32, U = 64, TB = 4;  // tiles per batch: 8 x 4 = 32 loads (128 KB) in flight
-  const int tid = threadIdx.x;
-  const int p = blockIdx.x - ncomp, x = blockIdx.x & 7, k = p >> 3, nk = npf >> 3;
-  int l0, l1;
-  persist_xcd_tiles(x, ncomp, l0, l1);
-  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
-  const unsigned* c0 = cnt + (l0 / nub) * SV_PCNT_STRIDE;
-  __shared__ int skip;
-  for (int s = T - 1; s >= 0; --s) {
-    if (tid == 0) {
-      if (s + 2 <= T - 1) {
-        unsigned spins = 0;
-        const unsigned target = (unsigned)nub * (unsigned)(T - 1 - (s + 2) + 1);
-        while (__hip_atomic_load(c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
-               !__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) && ++spins < limit)
-          __builtin_amdgcn_s_sleep(2);
-      }
-      // too late for step s (its consumers have finished step s + 1 and issued their own DMA of
-      // it): skip it, so a slow helper never holds the launch open
-      skip = __hip_atomic_load(c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nub * (unsigned)(T - 1 - s);
-    }
-    __syncthreads();
-    const bool sk = skip;
-    __syncthreads();
-    if (sk) continue;
-    const float* up = dhup ? (up_full ? dhup + (long)s * BH : (s == T - 1 ? dhup : nullptr)) : nullptr;
-    const __amdgpu_buffer_rsrc_t ra = sv_rsrc(acts + (long)s * BG, (unsigned)(BG * 2));
-    const __amdgpu_buffer_rsrc_t rc = sv_rsrc(c_tm + (long)(s > 0 ? s - 1 : 0) * BH, s > 0 ? (unsigned)(BH * 4) : 0u);
-    const __amdgpu_buffer_rsrc_t ru = sv_rsrc(up ? up : c_tm, up ? (unsigned)(BH * 4) : 0u);
-    // a tile's 16-B pieces: activations 32 rows x 4 gates x 8, c_{s-1} and dh_up 32 rows x 16 each;
-    // thread tid takes pieces tid + 256 i; loads into registers, TB tiles in flight (an absent
-    // operand's range is empty: its loads return zeros without a memory access)
-    for (int L0 = l0 + k; L0 < l1; L0 += TB * nk) {
-      u32x4_t v[TB][8];
-#pragma unroll
-      for (int b = 0; b < TB; ++b) {
-        const int L = min(L0 + b * nk, l1 - 1), ub = L % nub, rb = L / nub, j0 = ub * U;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int e = tid + 256 * i;
-          if (i < 4) {
-            const int row = min(rb * BM + (e >> 5), B - 1), q = (e >> 3) & 3, c = e & 7;
-            v[b][i] = __builtin_amdgcn_raw_buffer_load_b128(
-                ra, (unsigned)(((long)row * G + (long)q * H + j0 + 8 * c) * 2), 0, 0);
-          } else {
-            const int f = e & 511, row = min(rb * BM + (f >> 4), B - 1), c = f & 15;
-            v[b][i] = __builtin_amdgcn_raw_buffer_load_b128(i < 6 ? rc : ru,
-                                                            (unsigned)(((long)row * H + j0 + 4 * c) * 4), 0, 0);
-          }
-        }
-      }
-#pragma unroll
-      for (int b = 0; b < TB; ++b)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(v[b][i]));
-    }
-  }
-}
-
 template <int NS, int P, int NL, bool DEFER>
 __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     const bf16_t* __restrict__ whhT, const bf16_t* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
     bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit,
-    int fault, int dbg, float* __restrict__ dbp, unsigned long long* __restrict__ stamps, int ncomp, int npf) {
+    int fault, int dbg, float* __restrict__ dbp, unsigned long long* __restrict__ stamps) {
   constexpr int BM = 32, U = 64, KR = 2;  // rows, units, row passes of the epilogue (16 rows each)
   constexpr int LDR = U + 4;              // red [4][BM][LDR] fp32
   constexpr int LDG = 4 * U + 8;          // dgs [BM][LDG] bf16 (row-major dG tile)
@@ -110,16 +38,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
   float* ewc = reinterpret_cast<float*>(ewa + BM * 512);    // [BM][U] c_{t-1}
   float* ewu = ewc + BM * U;                                // [BM][U] dh_up
   char* wl = reinterpret_cast<char*>(ewu + BM * U);         // [4 waves][NL][64 lanes][16 B]
-  if ((int)blockIdx.x >= ncomp) {  // a helper workgroup: operand prefetch only
-    p3_bwd_prefetch(acts, c_tm, dhup, up_full, T, B, H, cnt, nub, ncomp, npf, status, limit);
-    return;
-  }
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   int ub, rb;
-  persist_tile(xcd, nub, ub, rb, ncomp);
+  persist_tile(xcd, nub, ub, rb);
   const int j0 = ub * U, b0 = rb * BM;
-  const int nrb = ncomp / nub;
+  const int nrb = gridDim.x / nub;
   const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
   const long FS = (long)nrb * BM * G;
   unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
@@ -385,11 +309,11 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + SV_SYNC_STAMP);
   // (the DEFER form -- the operand DMA and the dG / dG^T stores inside the next step's k-loop --
   // measured slower: c3 bwd 1205 vs 1086 us per layer; the fragment waits count the older stores)
-  // operand-prefetch helper workgroups on the CUs the grid leaves free, the same number per XCD
-  const int ncomp = (int)grid.x, npf = SV_P3_PREFETCH ? std::min(16, (sv_stream_cus(stream) - ncomp) / 8 * 8) : 0;
-  hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL, false>), dim3(ncomp + npf), dim3(256), lds, stream, whhT,
-                     acts, c_tm, dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault,
-                     dbg, dbp, stamps, ncomp, npf);
+  // (operand-prefetch helper workgroups on the 16 free CUs, as the fp32 backward has them, measured
+  // no gain here: DESIGN §4)
+  hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL, false>), grid, dim3(256), lds, stream, whhT, acts, c_tm,
+                     dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbg, dbp,
+                     stamps);
   return (int)hipGetLastError();
 }
 

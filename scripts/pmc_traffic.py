@@ -20,9 +20,11 @@ FAMILIES = {  # json key -> kernel-name prefix
     "lstm_persist_bwd_f32_h2_kernel": "void lstm_persist_bwd_f32_h2_kernel<",
     "lstm_persist_fwd_f32_kernel": "void lstm_persist_fwd_f32_kernel<",
     # in-step GEMMs, per shape (c2 fp32 / c3 bf16, B = 640, T = 160, H = 768): (prefix, grid threads)
-    "gemm_f32_256_kernel<256,32,0>@K1.in_step": ("void gemm_f32_256_kernel<256, 32, 0>", 400 * 12 * 512),
-    "gemm_f32_256_kernel<256,32,0>@dx.in_step": ("void gemm_f32_256_kernel<256, 32, 0>", 400 * 3 * 512),
-    "gemm_f32_256_kernel<256,32,1>@dW.in_step": ("void gemm_f32_256_kernel<256, 32, 1>", 36 * 7 * 512),
+    # (r04 names: the K1 is the persistent 256p kernel, the dx GEMM reads the fragment-order A (AF = 1),
+    # the dW GEMMs are split-K slabs (EPI = 1); the template's 4th argument is AF)
+    "gemm_f32_256p_kernel<256,32>@K1.in_step": "void gemm_f32_256p_kernel<256, 32>",
+    "gemm_f32_256_kernel<256,32,0,1>@dx.in_step": "void gemm_f32_256_kernel<256, 32, 0, 1>",
+    "gemm_f32_256_kernel<256,32,1,0>@dW.in_step": "void gemm_f32_256_kernel<256, 32, 1, 0>",
     "gemm_bf16_8qp_kernel<2>@K1.in_step": "void gemm_bf16_8qp_kernel<2>",
     "gemm_bf16_8q_kernel<0,1>@dx.in_step": "void gemm_bf16_8q_kernel<0, 1>",
     "gemm_bf16_8q_kernel<1,0>@dW.in_step": "void gemm_bf16_8q_kernel<1, 0>",
