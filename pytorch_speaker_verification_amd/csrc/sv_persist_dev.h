@@ -87,6 +87,29 @@ __device__ __forceinline__ void w3_dma(__amdgpu_buffer_rsrc_t ra, int ts, int B,
   }
 }
 
+// piece i (0 .. W3_DMA - 1) of w3_dma alone (the same addresses), for issue spread over a k-loop
+__device__ __forceinline__ void w3_dma_piece(__amdgpu_buffer_rsrc_t ra, int ts, int B, int H, int b0, char* tile, int g,
+                                             int lane, int i) {
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  int z = 0;  // (the opaque zero of w3_dma: no address hoisted out of the time loop)
+  asm volatile("" : "+v"(z));
+  g += z;
+  const unsigned slot = (unsigned)ts * (unsigned)B * (unsigned)H * 2u;
+  auto row_base = [&](int row) {
+    return b0 + row < B ? slot + (unsigned)(b0 + row) * (unsigned)H * 2u : 0xFFFFE000u;
+  };
+  if (i < 8) {
+    const int row = g * 8 + i;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + row * W3_RA), 16, row_base(row) + 16u * lane, 0,
+                                             0, 16 /* sc1 */);
+  } else {
+    const int p = g * 4 + (i - 8), row = 2 * p + (lane >> 5), sl = lane & 31;
+    const unsigned c = 64u + (unsigned)(sl ^ (row & 15));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + 32 * W3_RA + p * 1024), 16,
+                                             row_base(row) + 16u * c, 0, 0, 16 /* sc1 */);
+  }
+}
+
 // byte offset of A fragment s (k-step, 16 bf16) of lane (r, hh) in a w3_dma tile image
 struct W3Frag {
   const char* pa;

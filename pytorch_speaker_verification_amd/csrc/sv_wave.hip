@@ -94,6 +94,30 @@ __device__ __forceinline__ void w3_mfma_lds(const char* tile, int lane, const bf
   }
 }
 
+// the same, with the 12 pieces of the next step's x-tile DMA (into `dtile`, slot ts of `rd`) issued
+// one per 4 k-steps between the MFMAs (an LDS-DMA issue costs least among bare MFMAs:
+// MI355X_MICROARCH.md, "LDS-DMA piece")
+__device__ __forceinline__ void w3_mfma_lds_dma(const char* tile, int lane, const bf16x8_t (&W)[WV_NS], f32x16& acc,
+                                                __amdgpu_buffer_rsrc_t rd, int ts, int B, int H, int b0, char* dtile,
+                                                int g) {
+  const W3Frag frag(tile, lane);
+  constexpr int P = 4;
+  bf16x8_t f[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) f[j] = frag(j);
+#pragma unroll
+  for (int s = 0; s < WV_NS; ++s) {
+    acc = mfma_bf16(f[s % P], W[s], acc);
+    if (s + P < WV_NS) f[s % P] = frag(s + P);
+    if (s % 4 == 1) w3_dma_piece(rd, ts, B, H, b0, dtile, g, lane, s / 4);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+#ifndef SV_W3_EARLY_X  // the next x tile's DMA inside the h-part when the layer below is ready
+#define SV_W3_EARLY_X 1
+#endif
+
 template <bool L0, bool STAMP>
 __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int rb, char* tile_x, char* tile_h,
                                        float* pre, bf16_t* hsb, bf16_t* hts) {
@@ -166,10 +190,18 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#if SV_W3_EARLY_X
+    unsigned xpoll = 0;
+#endif
     if constexpr (!L0) {
       // this wave's x DMA and everything older (the 12 h DMAs are the newest), then all waves'
       asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
       raw_barrier();
+#if SV_W3_EARLY_X
+      // the layer below's counter for step t + 1's x tile, read now: its round trip runs under the
+      // x-part, and the answer decides at the h-part whether that DMA goes there
+      if (tid == 0 && t + 1 < T) xpoll = __hip_atomic_load(below, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
       w3_mfma_lds(tile_x, lane, wx, acc);
     } else {
       u32x4_t xa[WV_XS];
@@ -188,8 +220,20 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
     for (int i = 0; i < 16; ++i) acc[i] = round_bf(acc[i] + xbias);
     mark(2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    raw_barrier();
-    w3_mfma_lds(tile_h, lane, wh, acc);
+#if SV_W3_EARLY_X
+    __shared__ int xflag;
+    if (!L0 && tid == 0) xflag = (t + 1 < T && xpoll >= producers * (unsigned)(t + 2) && !(a.dbg & 2)) ? 1 : 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+    raw_barrier();  // every wave past the x-part: tile_x is free
+    bool xe = false;
+#if SV_W3_EARLY_X
+    if constexpr (!L0) xe = xflag != 0;
+#endif
+    if (xe)
+      w3_mfma_lds_dma(tile_h, lane, wh, acc, rbel, t + 2, B, H, b0, tile_x, g);
+    else
+      w3_mfma_lds(tile_h, lane, wh, acc);
     mark(3);
 #pragma unroll
     for (int i = 0; i < 16; ++i) pre[acc_row(i, lane) * WV_LDP + g * BF_U + r] = acc[i];
@@ -257,7 +301,7 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
         if (t == 0) *reinterpret_cast<uint4*>(row + gc) = uint4{0u, 0u, 0u, 0u};
       }
     }
-    if (!L0 && t + 1 < T) {  // x_{t+1}: tile_x is free (every wave is past this step's x-part)
+    if (!L0 && t + 1 < T && !xe) {  // x_{t+1}: tile_x is free (every wave is past this step's x-part)
       if (tid == 0) wv_wait(below, producers * (unsigned)(t + 2), a.status, a.limit);
       raw_barrier();
       w3_dma(rbel, t + 2, B, H, b0, tile_x, g, lane);

@@ -19,6 +19,7 @@ ap.add_argument("--check", action="store_true", help="bf16: error vs fp32 torch 
                 "and bitwise repeatability over --reps runs (a race screen)")
 ap.add_argument("--shapes", default="Gx,dW,dx")
 ap.add_argument("--lib", default=None, help="load this build of the library instead (A/B builds)")
+ap.add_argument("--fill", default="randn", help="operand data: randn | zeros (power / clock upper bound)")
 ap.add_argument("--bias", action="store_true", help="Gx with the two bias vectors, as K1 runs in the stack")
 args = ap.parse_args()
 if args.lib:
@@ -47,8 +48,8 @@ res = {"lib": args.lib or "libsv_ge2e.so"}
 for name, (M, N, K) in SHAPES.items():
     if name not in args.shapes.split(","):
         continue
-    A = torch.randn(M, K, device=dev)
-    Bm = torch.randn(N, K, device=dev)
+    A = torch.randn(M, K, device=dev) if args.fill == "randn" else torch.zeros(M, K, device=dev)
+    Bm = torch.randn(N, K, device=dev) if args.fill == "randn" else torch.zeros(N, K, device=dev)
     C = torch.empty(M, N, device=dev)
     w = torch.empty(lib().sv_gemm_f32_workspace(M, N, K) // 4 + 1, device=dev)
     b0, b1 = (torch.randn(N, device=dev), torch.randn(N, device=dev)) if args.bias and name == "Gx" else (None, None)
