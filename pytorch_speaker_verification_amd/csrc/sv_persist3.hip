@@ -4,11 +4,6 @@
 #include "sv_persist_dev.h"
 #include "../../include/sv_ge2e.h"
 
-// the wide backward issues the next step's operand DMA ahead of the hand-off drain (kernel body)
-#ifndef SV_P3B_EARLY_EW
-#define SV_P3B_EARLY_EW 1
-#endif
-
 // ============================================================================
 // Wide-tile W-stationary backward (H = 768, default; SV_PBWD3=0 keeps the 32-unit tile above).
 // Tile: 32 batch rows x 64 hidden units, so the grid is (H / 64) x (B / 32) -- 240 workgroups at
@@ -118,39 +113,27 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     for (int i = 0; i < 8; ++i) ew_piece(tt, i);
   };
   // store i (0..7) of step tt's dG tile from LDS: 0-3 row-major dG (when dg), 4-7 dG^T (when dgT)
-  // store i (0..7) split into its LDS read (store_read: the value, the byte offset, whether it is
-  // stored) and its buffer store (store_issue), so the values can be read before an operand DMA is
-  // issued and stored after it
-  auto store_read = [&](int i, u32x4_t& v, unsigned& off) -> bool {
+  auto store_piece = [&](int tt, int i) {
+    // buffer stores with 32-bit offsets (no 64-bit addresses kept live across the k-loop)
     if (i < 4) {
-      if (!dg) return false;
+      if (!dg) return;
+      const __amdgpu_buffer_rsrc_t rs = sv_rsrc(dg + (long)tt * BG, (unsigned)(BG * 2));
       const int q = tid + 256 * i, row = q >> 5, gq = (q >> 3) & 3, c = q & 7;
       const int gb = b0 + row, gj = j0 + 8 * c;
-      const uint4 x = *reinterpret_cast<const uint4*>(dgs + row * LDG + gq * U + 8 * c);
-      v = u32x4_t{x.x, x.y, x.z, x.w};
-      off = (unsigned)(((long)gb * G + (long)gq * H + gj) * 2);
-      return gb < B && gj < H;
+      const uint4 v = *reinterpret_cast<const uint4*>(dgs + row * LDG + gq * U + 8 * c);
+      if (gb < B && gj < H)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rs,
+                                               (unsigned)(((long)gb * G + (long)gq * H + gj) * 2), 0, 0);
+    } else {
+      if (!dgT) return;
+      const __amdgpu_buffer_rsrc_t rs = sv_rsrc(dgT + (long)tt * Bp, (unsigned)(4L * H * lddgT * 2 - (long)tt * Bp * 2));
+      const int q = tid + 256 * (i - 4), gu = q >> 2, c = q & 3;
+      const int gq = gu / U, gj = j0 + gu % U, gb = b0 + 8 * c;
+      const uint4 v = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * (c ^ ((gu % U) >> 4 & 3)));
+      if (gb < Bp && gj < H)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rs,
+                                               (unsigned)((((long)gq * H + gj) * lddgT + gb) * 2), 0, 0);
     }
-    if (!dgT) return false;
-    const int q = tid + 256 * (i - 4), gu = q >> 2, c = q & 3;
-    const int gq = gu / U, gj = j0 + gu % U, gb = b0 + 8 * c;
-    const uint4 x = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * (c ^ ((gu % U) >> 4 & 3)));
-    v = u32x4_t{x.x, x.y, x.z, x.w};
-    off = (unsigned)((((long)gq * H + gj) * lddgT + gb) * 2);
-    return gb < Bp && gj < H;
-  };
-  auto store_issue = [&](int tt, int i, u32x4_t v, unsigned off) {
-    // buffer stores with 32-bit offsets (no 64-bit addresses kept live across the k-loop)
-    if (i < 4)
-      __builtin_amdgcn_raw_buffer_store_b128(v, sv_rsrc(dg + (long)tt * BG, (unsigned)(BG * 2)), off, 0, 0);
-    else
-      __builtin_amdgcn_raw_buffer_store_b128(
-          v, sv_rsrc(dgT + (long)tt * Bp, (unsigned)(4L * H * lddgT * 2 - (long)tt * Bp * 2)), off, 0, 0);
-  };
-  auto store_piece = [&](int tt, int i) {
-    u32x4_t v;
-    unsigned off;
-    if (store_read(i, v, off)) store_issue(tt, i, v, off);
   };
   {
     const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(T - 1) * BH, (unsigned)(BH * 4));
@@ -269,21 +252,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     }
     __syncthreads();
     mark(2);
-#if SV_P3B_EARLY_EW
-    // (not DEFER) the next step's operand DMA is issued right behind the hand-off stores, before
-    // their drain: the counted wait below leaves its 8 LDS-DMA ops in flight, so their HBM latency
-    // runs under the drain, the arrival and the next poll instead of opening the next step.  Every
-    // LDS read of this step (the dG / dG^T store values) happens before that issue: a ds_read
-    // behind an outstanding LDS-DMA gets a compiler vmcnt(0).  (The cell's reads of ewa / ewc /
-    // ewu ended at the barrier above, so the DMA may overwrite them.)
-    u32x4_t stv[8];
-    unsigned sto[8];
-    bool stk[8];
-    const bool st_on = !DEFER && !(dbg & 8) && !(dbg & 128);
-    const bool ew_early = !DEFER && t > 0 && !(dbg & 64);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) stk[i] = st_on && store_read(i, stv[i], sto[i]);
-#endif
     // the hand-off: 16 KB of dG_t per workgroup in fragment order (gate, k-step), 16-B sc1 stores
     if (!(dbg & 8)) {
       const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 2));
@@ -297,33 +265,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
       }
     }
-#if SV_P3B_EARLY_EW
-    if (ew_early) {
-      load_ew(t - 1);
-      // the 8 youngest ops are the DMA: every older one (the hand-off stores) is done
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();  // raw: __syncthreads() may wait for the DMA too
-    __builtin_amdgcn_sched_barrier(0);
-    if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
-      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    mark(3);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      if (stk[i]) store_issue(t, i, stv[i], sto[i]);
-    if (DEFER && t == 0 && !(dbg & 8) && !(dbg & 128))
-#pragma unroll
-      for (int i = 0; i < 8; ++i) store_piece(t, i);
-#else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     mark(3);
-#endif
-    if (!SV_P3B_EARLY_EW && (!DEFER || t == 0)) {  // DEFER: all but the last step's leftovers go into the next k-loop
+    if (!DEFER || t == 0) {  // DEFER: all but the last step's leftovers go into the next k-loop
       // (dbg, profiling only: 64 skips the operand DMA, 128 the dG / dG^T stores).  The stores
       // first: their LDS reads issued behind an LDS-DMA would wait for it to land (the compiler
       // cannot tell the DMA's LDS range from the tiles', so it puts vmcnt(0) before every read)
@@ -979,22 +926,6 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
     }
     __syncthreads();
     WB_MARK(2);  // 2: exchange, dh_up, dx_{t+1} hand-off stores, cell backward, dG tiles
-#if SV_P3B_EARLY_EW
-    // as in the wide backward: the dG^T values leave LDS before the next step's operand DMA is
-    // issued behind the hand-off stores (the DMA then runs under the drain, the arrival and the
-    // next poll)
-    uint4 tv[2];
-    bool tk[2];
-    long to[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = tid + 256 * i, gu = q >> 2, c = q & 3;
-      const int gq = gu / U, gj = j0 + gu % U, gc = b0 + 8 * c;
-      tk[i] = t >= 0 && a.dgT[l] && gc < a.Bp && gj < H;
-      to[i] = ((long)gq * H + gj) * a.lddgT + (long)t * a.Bp + gc;
-      tv[i] = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
-    }
-#endif
     // the dG_t hand-off: 8 KB per workgroup in fragment order (gate, 2 k-steps), 16-B sc1 stores
     if (t >= 0) {
       const __amdgpu_buffer_rsrc_t rw = sv_rsrc(a.dgf[l] + (long)t * FS, (unsigned)(FS * 2));
@@ -1008,23 +939,6 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
       }
     }
-#if SV_P3B_EARLY_EW
-    if (t > 0) {
-      load_ew(t - 1);
-      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // the 3 youngest ops are the DMA
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (tid == 0 && persist_arrive_ok(a.fault, t == T - 1))
-      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    WB_MARK(3);  // 3: dG_t hand-off stores + next operand DMA issue + drain + arrival
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      if (tk[i]) *reinterpret_cast<uint4*>(a.dgT[l] + to[i]) = tv[i];
-    WB_MARK(4);  // 4: dG^T stores
-#else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0 && persist_arrive_ok(a.fault, t == T - 1))
@@ -1042,7 +956,6 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
     }
     if (t > 0) load_ew(t - 1);
     WB_MARK(4);  // 4: dG^T stores + next operand DMA issue
-#endif
   }
 #ifdef SV_WB_STAMP
   if (tid == 0 && blockIdx.x < SV_NSTAMP_WG / 2) {  // second half of the stamp slots (the forward's use the first)

@@ -34,9 +34,6 @@
 #ifndef SV_PF32_ACQ  // A/B diagnostic builds only (0: the product's relaxed poll)
 #define SV_PF32_ACQ 0
 #endif
-#ifndef SV_PF32_EARLY_EW  // the backward issues the next half-step's operand DMA ahead of the hand-off drain
-#define SV_PF32_EARLY_EW 1
-#endif
 #ifndef SV_PF32_GXAUX  // A/B diagnostic: cache-policy bits of the x-projection DMA
 #define SV_PF32_GXAUX 0
 #endif
@@ -489,17 +486,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
     const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
     const int q = gz * 64 + lane, row = q >> 3, c = q & 7;
     const long off = (long)min(b0 + row, B - 1) * H + j0 + 4 * c;
-#if SV_PF32_EARLY_EW
-    // always six DMA ops per wave (an absent operand reads zeros through an empty buffer range), so
-    // the early issue in the step body can leave exactly six in flight
-    // (readfirstlane: hipcc formed tt - 1 clamped on the VALU and wrapped the load in a waterfall loop)
-    const int tm1 = __builtin_amdgcn_readfirstlane(tt > 0 ? tt - 1 : 0);
-    const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)tm1 * BH, tt > 0 ? (unsigned)(BH * 4) : 0u);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rc_, (lds_ptr_t)(ec + g * 256), 16, (unsigned)(off * 4), 0, 0, 0);
-    const __amdgpu_buffer_rsrc_t ru_ = sv_rsrc(up ? up : c_tm, up ? (unsigned)(BH * 4) : 0u);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ru_, (lds_ptr_t)(eu + g * 256), 16, (unsigned)(off * 4), 0, 0, 0);
-    return;
-#endif
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
     if (tt > 0)
       __builtin_amdgcn_global_load_lds((pf_glb_t)(c_tm + (long)(tt - 1) * BH + off), (pf_lds_t)(ec + g * 256), 16, 0,
@@ -625,86 +611,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
       }
       __syncthreads();
       PB_STAMP(3);  // 3: cell + dG tiles into LDS
-#if SV_PF32_EARLY_EW
-      // every LDS read of the half-step's dG tiles first (hand-off, bias partial, dG / dG^T store
-      // values into registers), then the hand-off stores, then the next half-step's operand DMA
-      // (into the images the tiles alias) BEFORE the drain: the counted wait leaves its six ops in
-      // flight, so its latency runs under the drain, the arrival and the next poll
-      {
-        const bool ho = t > 0 || !dg, ew_next = hf == 0 || t > 0;
-        f32x4 hv[4];
-        unsigned hoff[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int p = tid + 256 * i, blk = p >> 6, L = p & 63;
-          const int q = blk >> 2, kl = blk & 3;
-          hv[i] = *reinterpret_cast<const f32x4*>(dgs + (L & 31) * LDG + q * PF_U + 8 * kl + 4 * (L >> 5));
-          hoff[i] = ((unsigned)(((rb * 4 + q) * 2 + hf) * FBLK) + (unsigned)(4 * ub + kl) * 256u + (unsigned)L * 4u) * 4u;
-        }
-        float bsum = 0.f;
-        if (dbp && tid < 4 * PF_U) {
-          const int nv = min(PH_BM, B - b0);
-#pragma unroll
-          for (int e4 = 0; e4 < PH_BM / 4; ++e4) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(gts + tid * LDT + 4 * e4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (4 * e4 + e < nv) bsum += v[e];
-          }
-        }
-        const long gb = b0 + erow;
-        const bool dok = dg && gb < B;
-        f32x4 dv[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) dv[q] = *reinterpret_cast<const f32x4*>(dgs + erow * LDG + q * PF_U + 4 * quad);
-        f32x4 tv[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int p = tid + 256 * i, gu = p >> 3, c = p & 7, gbc = b0 + 4 * c;
-          tv[i] = *reinterpret_cast<const f32x4*>(gts + gu * LDT + 4 * c);
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (gbc + e >= B) tv[i][e] = 0.f;
-        }
-        __syncthreads();  // every wave's tile reads done: the DMA may overwrite the images
-        if (ho) {
-          const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 4));
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, hv[i]), rw, hoff[i], 0, 16 /* sc1 */);
-        }
-        if (ew_next) {
-          if (hf == 0)
-            load_ew(t, 1);
-          else
-            load_ew(t - 1, 0);
-          asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // the six youngest ops are the DMA
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();  // raw: __syncthreads() may wait for the DMA as well
-        __builtin_amdgcn_sched_barrier(0);
-        if (t > 0 && tid == 0 && persist_arrive_ok(fault, t == T - 1))
-          __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        PB_STAMP(4);  // 4: hand-off stores + next operand DMA issue + drain + arrival
-        dbs += bsum;
-        if (dok) {
-          float* dp = dg + (long)t * BG + gb * G + j0 + 4 * quad;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4*>(dp + q * H) = dv[q];
-        }
-#ifndef SV_PF32_NODGT
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int p = tid + 256 * i, gu = p >> 3, c = p & 7, gbc = b0 + 4 * c;
-          if (gbc < Bp)
-            *reinterpret_cast<f32x4*>(dgT + ((long)(gu >> 5) * H + j0 + (gu & 31)) * lddgT + (long)t * Bp + gbc) = tv[i];
-        }
-#endif
-        PB_STAMP(5);  // 5: off-chain (bias partials, dG / dG^T stores)
-        continue;
-      }
-#endif
       // the hand-off: 16 fragment blocks of 1 KB (gate q, this half, k-group 4 ub + kl); slot 0 (no
       // consumer step) only when the dx GEMM reads the fragment-order image (dg == nullptr)
       if (t > 0 || !dg) {
