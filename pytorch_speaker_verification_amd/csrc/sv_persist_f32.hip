@@ -34,6 +34,9 @@
 #ifndef SV_PF32_ACQ  // A/B diagnostic builds only (0: the product's relaxed poll)
 #define SV_PF32_ACQ 0
 #endif
+#ifndef SV_PF32_FWD_AHEAD2  // forward k-loop: A / W fragments two k-groups ahead across chunks
+#define SV_PF32_FWD_AHEAD2 1
+#endif
 #ifndef SV_PF32_GXAUX  // A/B diagnostic: cache-policy bits of the x-projection DMA
 #define SV_PF32_GXAUX 0
 #endif
@@ -204,6 +207,68 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
       PF_STAMP(0);  // 0: hand-off wait
       dma_chunk(0, 0);
       dma_chunk(1, 1);
+#if SV_PF32_FWD_AHEAD2
+      // fragments two k-groups ahead, across chunk boundaries: chunk ch + 1's wait and barrier come
+      // before the last two k-groups of chunk ch, so its first fragments are read while those run.
+      // Waits (this wave's ops younger than chunk c + 1's four): chunk c + 2's and, for c <= 1, the
+      // x-projection's eight (issued at chunk 0, behind chunk 2's) -- c = 0, 1: 12; then 4; last: 0.
+      pf_vmwait<4>();  // chunk 0 (chunk 1 in flight)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      PF_STAMP(1);  // 1: first chunk's DMA latency
+      auto afrag = [&](int kg, f32x4& x0, f32x4& x1) {
+        const char* cb = ring + ((kg / KGC) % PF_NB) * PF_CH;
+        const int kk = kg % KGC;
+        x0 = *reinterpret_cast<const f32x4*>(cb + r * 256 + 16 * pf_slot(r, 2 * kk + hh));
+        x1 = *reinterpret_cast<const f32x4*>(cb + (32 + r) * 256 + 16 * pf_slot(32 + r, 2 * kk + hh));
+      };
+      f32x4 a0, a1, b0_, b1_, w = wfrag(0), wn = wfrag(1);
+      afrag(0, a0, a1);
+      afrag(1, b0_, b1_);
+#pragma unroll
+      for (int kg = 0; kg < NKG; ++kg) {
+        const int ch = kg / KGC, kk = kg % KGC;
+        if (kk == 0 && ch + 2 < NCH) dma_chunk(ch + 2, (ch + 2) % PF_NB);
+        if (kg == 0) dma_gx();
+        if (kk == KGC - 2 && ch + 1 < NCH) {  // chunk ch + 1 landed, every wave's part
+          if (ch <= 1)
+            pf_vmwait<12>();
+          else if (ch + 2 < NCH)
+            pf_vmwait<4>();
+          else
+            pf_vmwait<0>();
+          __builtin_amdgcn_s_barrier();  // (slot (ch + 3) % 4's last reads, chunk ch - 1's, are done)
+          asm volatile("" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // the first MFMA pair, then k-group kg + 2's reads, then the rest: hipcc waits lgkmcnt(0)
+        // before a k-group's first MFMA (every outstanding LDS read), so reads issued after it have
+        // the group's other six MFMAs before the next such wait
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[0], w[0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[0], w[0], acc1, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 n0 = a0, n1 = a1, nw = w;
+        if (kg + 2 < NKG) {
+          afrag(kg + 2, n0, n1);
+          nw = wfrag(kg + 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 1; c < 4; ++c) {
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[c], w[c], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[c], w[c], acc1, 0, 0, 0);
+        }
+        a0 = b0_;
+        a1 = b1_;
+        w = wn;
+        b0_ = n0;
+        b1_ = n1;
+        wn = nw;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      pf_vmwait<0>();  // the x-projection (already waited for by the chunk waits; kept explicit)
+#else
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
         if (ch + 2 < NCH) dma_chunk(ch + 2, (ch + 2) % PF_NB);
@@ -249,6 +314,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+#endif
     } else {
       dma_gx();
       pf_vmwait<0>();
