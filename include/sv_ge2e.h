@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SV_ABI_VERSION 6
+#define SV_ABI_VERSION 7
 int sv_abi_version(void);
 
 /* ---- fp32 product modes (`products` argument of sv_gemm_f32 / sv_lstm_stack_fwd / _bwd; every
@@ -280,6 +280,31 @@ int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const sv_bf16* con
                            float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace, int chunk,
                            hipStream_t main, const hipStream_t* side, hipEvent_t* ev, void* sync, hipEvent_t* probe,
                            int schedule);
+
+/* ---- dtype-enum form of the stack entry points (SURVEY.md §8 b: `lstm_fwd` = K1 + K2 and
+ * `lstm_bwd` = K3 + K4 with a dtype argument; replaces the nn.LSTM forward / autograd backward at
+ * speech_embedder_net.py:28 and train_speech_embedder.py:62).  One entry point per direction:
+ *   SV_DTYPE_F32   -> sv_lstm_stack_fwd / _bwd: the `void` operands are float; h_bf is ignored
+ *                     (pass NULL);
+ *   SV_DTYPE_BF16  -> sv_lstm_stack_fwd_bf16 / _bwd_bf16: the `void` operands are sv_bf16
+ *                     (x, w_ih, w_hh, gates, h_bf, hT; in the backward xT, gates, hT, dg, dgT);
+ *                     `products` and `kstamp` are ignored (pass 0 / NULL).
+ * Every other argument means what it means in the dtype-specific entry point; the backward takes
+ * the fp32 master weights in both dtypes.  An unknown dtype returns SV_EARG. */
+#define SV_DTYPE_F32 0
+#define SV_DTYPE_BF16 1
+int sv_lstm_fwd(int dtype, int L, int T, int B, int F, int H, const void* x, const void* const* w_ih,
+                const void* const* w_hh, const float* const* b_ih, const float* const* b_hh, void* const* gates,
+                float* const* c_tm, float* const* h_tm, void* const* h_bf, void* const* hT, int chunk,
+                hipStream_t main, const hipStream_t* side, hipEvent_t* ev, int products, int schedule, void* sync,
+                hipEvent_t* probe);
+size_t sv_lstm_bwd_workspace(int dtype, int L, int T, int B, int F, int H);
+int sv_lstm_bwd(int dtype, int L, int T, int B, int F, int H, const void* const* xT, const long* ld_xT,
+                const float* const* w_ih, const float* const* w_hh, const void* const* gates, const float* const* c_tm,
+                const void* const* hT, const float* dh_last, void* const* dg, void* const* dgT, float* const* dx,
+                float* const* dw_ih, float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace,
+                int chunk, hipStream_t main, const hipStream_t* side, hipEvent_t* ev, int products, hipEvent_t* probe,
+                unsigned long long* kstamp, int schedule, void* sync);
 
 /* ---- persistent recurrences (one launch per layer for all T; sv_persist.hip).  The bf16 stack
  * forward uses them (by default when H = 768: W_hh held in registers) when the grid is

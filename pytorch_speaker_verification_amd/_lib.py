@@ -16,7 +16,8 @@ LIB_PATH = os.path.join(_HERE, "libsv_ge2e.so")
 # the fault-injection test build (Makefile `faultinj`): the same library plus sv_test_set_fault;
 # only tests load it, through use_library() before the first call
 FAULT_LIB_PATH = os.path.join(_HERE, "libsv_ge2e_faultinj.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
+SV_DTYPE_F32, SV_DTYPE_BF16 = 0, 1  # include/sv_ge2e.h
 
 # schedule flags of the bf16 stack (include/sv_ge2e.h SV_SCHED_*), by name
 SCHEDULES = {"auto": 0, "per_layer": 1, "per_step": 2, "persist": 5}  # persist: per-layer persistent, any H
@@ -103,6 +104,10 @@ SIGNATURES = {
     "sv_lstm_stack_bwd_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "sv_lstm_stack_bwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int] + [_P] * 16 + [_c_int, _P, _P, _P, _P,
                                                                                                _P, _c_int]),
+    # dtype-enum form of the stack entry points (SV_DTYPE_F32 / SV_DTYPE_BF16)
+    "sv_lstm_fwd": (_c_int, [_c_int] * 6 + [_P] * 10 + [_c_int, _P, _P, _P, _c_int, _c_int, _P, _P]),
+    "sv_lstm_bwd_workspace": (_c_size_t, [_c_int] * 6),
+    "sv_lstm_bwd": (_c_int, [_c_int] * 6 + [_P] * 16 + [_c_int, _P, _P, _P, _c_int, _P, _P, _c_int, _P]),
     "sv_sync_size": (_c_size_t, []),
     "sv_persist_fwd_ok": (_c_int, [_c_int, _c_int]),
     "sv_persist_bwd_ok": (_c_int, [_c_int, _c_int]),

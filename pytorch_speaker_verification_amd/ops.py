@@ -15,7 +15,7 @@ import ctypes
 
 import torch
 
-from ._lib import PersistStatus, call, lib, ptr, require_device, schedule_flags, stream_of
+from ._lib import SV_DTYPE_BF16, SV_DTYPE_F32, PersistStatus, call, lib, ptr, require_device, schedule_flags, stream_of
 
 # timesteps per chunk of the layer-pipelined schedules (measured at c2: 16 / 24 / 32 / 48 / 64 ->
 # 69.3 / 69.7 / 69.1 / 69.5 / 69.6 ms per step)
@@ -166,9 +166,9 @@ def embedder_forward(x, layers, w_p, b_p, save=True, products="mfma_f32", status
         sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * (L * nch + 1))(*[e.cuda_event for e in events[:L * nch + 1]])
         ps, own = _own_status(status, dev)
-        call("sv_lstm_stack_fwd", L, T, B, F, H, ptr(x_tm), _parr([l[0] for l in layers]),
+        call("sv_lstm_fwd", SV_DTYPE_F32, L, T, B, F, H, ptr(x_tm), _parr([l[0] for l in layers]),
              _parr([l[1] for l in layers]), _parr([l[2] for l in layers]), _parr([l[3] for l in layers]),
-             _parr(gs), _parr(cs), _parr(hs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep, prod, sched, ps.ptr(),
+             _parr(gs), _parr(cs), _parr(hs), None, _parr(hTs), PIPELINE_CHUNK, s, sp, ep, prod, sched, ps.ptr(),
              _evarr(probe))
         _release_status(ps, own)
         if save:
@@ -252,7 +252,7 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
     Bp = (B + 3) // 4 * 4
     if stacked:
         F0 = st.x_tm[0].shape[2]
-        ws = _ws(lib().sv_lstm_stack_bwd_workspace(L, T, B, F0, H), dev)
+        ws = _ws(lib().sv_lstm_bwd_workspace(SV_DTYPE_F32, L, T, B, F0, H), dev)
         dgs = [torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev) for _ in range(L)]
         dgTs = [torch.empty((4 * H, T * Bp), dtype=torch.float32, device=dev) for _ in range(L)]
         dxs = [None] + [torch.empty((T, B, H), dtype=torch.float32, device=dev) for _ in range(L - 1)]
@@ -264,7 +264,7 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
         ps, own = _own_status(status, dev)
         sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
-        call("sv_lstm_stack_bwd", L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
+        call("sv_lstm_bwd", SV_DTYPE_F32, L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
              _parr([l[0] for l in layers]), _parr([l[1] for l in layers]), _parr(st.gates), _parr(st.c_tm),
              _parr(st.hT), ptr(dh_last), _parr(dgs), _parr(dgTs), _parr(dxs),
              _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
@@ -363,10 +363,10 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=Non
         sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * (L * nch + 1))(*[e.cuda_event for e in events[:L * nch + 1]])
         sync, own = _own_status(status, dev)
-        call("sv_lstm_stack_fwd_bf16", L, T, B, F, H, ptr(x_bf), _parr([w[0] for w in wbf]),
+        call("sv_lstm_fwd", SV_DTYPE_BF16, L, T, B, F, H, ptr(x_bf), _parr([w[0] for w in wbf]),
              _parr([w[1] for w in wbf]), _parr([l[2] for l in layers]), _parr([l[3] for l in layers]),
-             _parr(gs), _parr(cs), _parr(hs), _parr(hbs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep, sync.ptr(),
-             _evarr(probe), sched)
+             _parr(gs), _parr(cs), _parr(hs), _parr(hbs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep, 0, sched,
+             sync.ptr(), _evarr(probe))
         _release_status(sync, own)
     else:
         for l, (w_ih, w_hh, b_ih, b_hh) in enumerate(layers):
@@ -436,7 +436,7 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
     Fmax = max(st.x_tm[l].shape[2] for l in range(L))
     if PIPELINE_CHUNK > 0 and L > 1 and not need_dx:
         F0 = st.x_tm[0].shape[2]
-        ws = _ws(lib().sv_lstm_stack_bwd_bf16_workspace(L, T, B, F0, H), dev)
+        ws = _ws(lib().sv_lstm_bwd_workspace(SV_DTYPE_BF16, L, T, B, F0, H), dev)
         dgs = [_bf((T, B, 4 * H), dev) for _ in range(L)]
         dgTs = [_bf((4 * H, T * Bp), dev) for _ in range(L)]
         dxs = [None] + [torch.empty((T, B, H), dtype=torch.float32, device=dev) for _ in range(L - 1)]
@@ -448,12 +448,12 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
         sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
         sync, own = _own_status(status, dev)
-        call("sv_lstm_stack_bwd_bf16", L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
+        call("sv_lstm_bwd", SV_DTYPE_BF16, L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
              _parr([l[0] for l in layers]), _parr([l[1] for l in layers]), _parr(st.gates), _parr(st.c_tm),
              _parr(st.hT), ptr(dh_last), _parr(dgs), _parr(dgTs), _parr(dxs),
              _parr([grads[4 * l] for l in range(L)]), _parr([grads[4 * l + 1] for l in range(L)]),
              _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
-             PIPELINE_CHUNK, s, sp, ep, sync.ptr(), _evarr(probe), sched)
+             PIPELINE_CHUNK, s, sp, ep, 0, _evarr(probe), None, sched, sync.ptr())
         _release_status(sync, own)
         if grad_ready:
             # the projection bucket is enqueued behind the stack backward: with the persistent

@@ -1,15 +1,8 @@
 #!/bin/bash
-# r04 checkpoint: bf16 helper A/B (skip statistics), then pytest -m gpu (verbose, MEASURED lines),
+# r04 checkpoint: pytest -m gpu (verbose, MEASURED lines),
 # the full bench line, rocprofv3 kernel-trace summaries (fp32 c2, bf16 c3) and the HBM-traffic PMC
 # passes.  Stops at the first failure.
 cd "$GRAFT_REPO_ROOT"; export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp; O=gpurun_out/${TAG:-r412}; mkdir -p $O
-for r in 1 2; do
-for v in prod p3pf p3pf8; do
-  L="--lib scripts/ab/libsv_ge2e_$v.so"; [ $v = prod ] && L=""
-  timeout -k 10 200 python -u scripts/persist_ab.py $L --iters 5 >> $O/bf16.log 2>&1 || { echo "$v rc=$?"; tail -5 $O/bf16.log; exit 1; }
-done
-done
-grep '^{' $O/bf16.log | cut -c1-250
 timeout -k 10 1500 python -u -m pytest tests -m gpu -v -s -rA --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error" $O/pytest_gpu.log | head -20; tail -5 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
 timeout -k 10 900 python -u bench.py > $O/bench.log 2>&1 || { echo "bench failed"; tail -20 $O/bench.log; exit 1; }

@@ -41,13 +41,28 @@ def test_c_abi_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(h, s), s
         assert s in _lib.SIGNATURES, f"{s} missing from the ctypes signature table"
-    assert h.sv_abi_version() == _lib.ABI_VERSION == 6
+    assert h.sv_abi_version() == _lib.ABI_VERSION == 7
     assert not hasattr(h, "sv_test_set_fault")  # the fault injector exists only in the test build
     # workspace queries are host-only and callable without a GPU
     assert h.sv_ge2e_workspace_size(64, 10, 256, 64) > 0
     assert h.sv_lstm_layer_bwd_workspace(160, 640, 768, 768) > 0
     ws = h.sv_gemm_f32_workspace(3072, 768, 102400)  # split-K slabs
     assert ws > 0 and ws % (3072 * 768 * 4) == 0
+
+
+def test_dtype_enum_entry_points_dispatch():
+    """SURVEY §8 b's dtype argument: sv_lstm_fwd / sv_lstm_bwd forward to the fp32 or bf16 stack
+    functions (ops.py calls only these); host-side checks, no launch: the workspace query of each
+    dtype is the dtype-specific one, and an unknown dtype is an argument error before any work."""
+    from pytorch_speaker_verification_amd import _lib
+    h = _lib.lib()
+    for dims in ((3, 160, 640, 40, 768), (3, 24, 32, 40, 64)):
+        assert h.sv_lstm_bwd_workspace(_lib.SV_DTYPE_F32, *dims) == h.sv_lstm_stack_bwd_workspace(*dims)
+        assert h.sv_lstm_bwd_workspace(_lib.SV_DTYPE_BF16, *dims) == h.sv_lstm_stack_bwd_bf16_workspace(*dims)
+        assert h.sv_lstm_bwd_workspace(2, *dims) == 0
+    nul = [None] * 10
+    assert h.sv_lstm_fwd(2, 3, 4, 8, 40, 64, *nul, 0, None, None, None, 0, 0, None, None) == -1  # SV_EARG
+    assert h.sv_lstm_bwd(-1, 3, 4, 8, 40, 64, *([None] * 16), 0, None, None, None, 0, None, None, 0, None) == -1
 
 
 def test_library_binds_torch_hip_runtime():
