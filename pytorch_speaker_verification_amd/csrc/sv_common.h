@@ -45,8 +45,12 @@ inline hipError_t sv_memset0(void* p, size_t bytes, hipStream_t stream) {
   return (hipError_t)sv_zero_bytes(p, bytes, stream);
 }
 size_t sv_persist_f32_bwd_scratch(int T, int B, int H);
+// x_tm (may be NULL): layer 0's input [T,B,F] (F = 40): the input projection x W_ih^T + b_ih + b_hh
+// is formed inside the recurrence (no K1 GEMM; `gates` is then output only)
 int sv_persist_fwd_f32(int T, int B, int H, const float* whh, float* gates, float* c_tm, float* h_tm, float* hT,
-                       hipStream_t stream, unsigned* sync, int chan, hipEvent_t pre, hipEvent_t post);
+                       hipStream_t stream, unsigned* sync, int chan, hipEvent_t pre, hipEvent_t post,
+                       const float* x_tm = nullptr, int F = 0, const float* wih = nullptr,
+                       const float* b_ih = nullptr, const float* b_hh = nullptr);
 int sv_persist_bwd_f32(int T, int B, int H, const float* whhT, const float* acts, const float* c_tm,
                        const float* dhup, int up_full, float* dg, float* dgT, float* dgf, hipStream_t stream,
                        unsigned* sync, hipEvent_t pre, hipEvent_t post, float* db_ih = nullptr,

@@ -19,6 +19,10 @@
 #include "sv_gemm_f32_256.h"
 #include "../../include/sv_ge2e.h"
 
+#ifndef SV_PF32_FUSE_X0  // fp32 persistent forward: layer 0's input projection inside the recurrence
+#define SV_PF32_FUSE_X0 1
+#endif
+
 #define SV_BKM 32
 
 // ============================================================================
@@ -976,11 +980,18 @@ extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float*
       if ((e = sv_memset0(h_tm[l], BH * sizeof(float), main)) != hipSuccess) return (int)e;
       if (hT[l] && Bp != B && (e = sv_memset0(hT[l], (size_t)H * ldhT * sizeof(float), main)) != hipSuccess)
         return (int)e;
-      int rc = gemm_f32(1, 1, T * B, 4 * H, Fl, in, Fl, w_ih[l], Fl, gates[l], 4L * H, b_ih[l], b_hh[l], 0.f, nullptr,
-                        main);
-      if (rc) return rc;
+      // layer 0 at F = 40: the input projection inside the recurrence (SV_PF32_FUSE_X0; c2 layer 0:
+      // the K=40 GEMM wrote 1.26 GB that the recurrence read back)
+      const bool fuse = SV_PF32_FUSE_X0 && l == 0 && F == 40;
+      int rc = 0;
+      if (!fuse) {
+        rc = gemm_f32(1, 1, T * B, 4 * H, Fl, in, Fl, w_ih[l], Fl, gates[l], 4L * H, b_ih[l], b_hh[l], 0.f, nullptr,
+                      main);
+        if (rc) return rc;
+      }
       rc = sv_persist_fwd_f32(T, B, H, w_hh[l], gates[l], c_tm[l], h_tm[l], hT[l], main, sync, 0,
-                              probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr);
+                              probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr,
+                              fuse ? x_tm : nullptr, F, w_ih[l], b_ih[l], b_hh[l]);
       if (rc) return rc;
     }
     return SV_OK;

@@ -87,11 +87,22 @@ __device__ __forceinline__ void pf_vmwait() {
 // forward
 // ============================================================================
 // NV / NL: weight k-groups kept in VGPRs / in LDS (after the PF_NA in AGPRs)
-template <int NKG, int NV, int NL>
+// XKG > 0 (layer 0, F = 8 XKG input features): the input projection x_t W_ih^T is formed in the
+// kernel (no K1 GEMM, no x-projection round trip through HBM): W_ih fragments, the x_t tile and
+// b_ih + b_hh live in the x-projection's LDS region; the x-part's MFMAs run at the top of each step,
+// before the hand-off wait (they need no h_{t-1}), and start the accumulators the h-part adds to.
+template <int NKG, int NV, int NL, int XKG = 0>
 __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
     const float* __restrict__ whh, float* gates, float* __restrict__ c_tm, float* h_tm, float* __restrict__ hT,
-    long ldhT, int T, int Bp, int B, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit, int fault) {
+    long ldhT, int T, int Bp, int B, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit, int fault,
+    const float* __restrict__ x_tm = nullptr, const float* __restrict__ wih = nullptr,
+    const float* __restrict__ b_ih = nullptr, const float* __restrict__ b_hh = nullptr) {
   constexpr int H = 8 * NKG, NCH = H / PF_KC, KGC = PF_KC / 8;
+  constexpr int XF = 8 * XKG, XLD = XF + 4;  // x tile [64][XLD] fp32 (an odd 16-B row stride: conflict-free)
+  constexpr int XSL = XLD / 4;               // 16-B slots per x-tile row
+  constexpr int GXN = XKG ? 0 : 8;           // x-projection DMA ops per wave in the k-loop's counted waits
+  static_assert(XKG == 0 || (PF_BM * XLD * 4 + 4 * XKG * 1024 + 4 * PF_U * 4 <= PF_BM * 4 * PF_U * 4 && XSL % 2 == 1),
+                "x tile + W_ih + biases fit the x-projection region");
   static_assert(NCH >= 4 && H % PF_KC == 0 && PF_NA + NV + NL == NKG, "chunk schedule / weight split");
   constexpr int LDP = 4 * PF_U + 4;  // pre [64][LDP] fp32
   constexpr int LDH = PF_BM + 4;     // hts [32][LDH] fp32
@@ -101,6 +112,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
   char* wl = smem + PF_NB * PF_CH + PF_BM * 4 * PF_U * 4;       // [4 waves][NL][64 lanes][16 B]
   float* pre = reinterpret_cast<float*>(smem);                  // after the k-loop: aliases the ring
   float* hts = pre + PF_BM * LDP;                               // (aliases the ring too)
+  // XKG: x tile, W_ih fragments and biases in the x-projection region; c staged in the ring
+  float* xs = gxs;                                                  // [64][XLD]
+  char* wil = reinterpret_cast<char*>(gxs + PF_BM * XLD);           // [4 waves][XKG][64 lanes][16 B]
+  float* bsl = reinterpret_cast<float*>(wil + 4 * XKG * 1024);      // [4 gates][32 units] b_ih + b_hh
+  float* cst = XKG ? hts + PF_U * (PF_BM + 4) : gxs;                // c_t of the step (row stride CLD)
+  constexpr int CLD = XKG ? PF_U : 4 * PF_U;
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   int ub, rb;
@@ -108,6 +125,39 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
   const int j0 = ub * PF_U, b0 = rb * PF_BM;
   const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
   unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
+  // x_t's tile by LDS-DMA: 64 rows x XSL slots lane-linear, wave g issuing instructions g, g + 4, ...;
+  // the pad slot of a row re-reads its last data slot (never read back)
+  auto dma_x = [&](int tt) {
+    if constexpr (XKG > 0) {
+      constexpr int NI = (PF_BM * XSL + 63) / 64;
+      int z = 0;  // (an opaque zero: no per-lane offset hoisted out of the time loop into registers)
+      asm volatile("" : "+v"(z));
+      const __amdgpu_buffer_rsrc_t rx = sv_rsrc(x_tm + (long)tt * B * XF, (unsigned)((long)B * XF * 4));
+#pragma unroll
+      for (int jj = 0; jj < (NI + 3) / 4; ++jj) {
+        const int j = 4 * jj + g;
+        if (j < NI) {  // (wave-uniform)
+          const int q = 64 * j + lane + z, row = min(q / XSL, PF_BM - 1), sl = min(q % XSL, XSL - 2);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(reinterpret_cast<char*>(xs) + j * 1024), 16,
+                                                   (unsigned)((min(b0 + row, B - 1) * XF + 4 * sl) * 4), 0, 0, 0);
+        }
+      }
+    }
+  };
+  if constexpr (XKG > 0) {
+    // W_ih of gate g, units j0 + r: lane (r, hh) of k-group kg holds W_ih[g H + j0 + r][8 kg + 4 hh .. + 3]
+#pragma unroll
+    for (int kg = 0; kg < XKG; ++kg)
+      *reinterpret_cast<f32x4*>(wil + ((g * XKG + kg) * 64 + lane) * 16) =
+          *reinterpret_cast<const f32x4*>(wih + ((long)g * H + j0 + r) * XF + 8 * kg + 4 * hh);
+    if (tid < 4 * PF_U) {
+      const long col = (long)(tid >> 5) * H + j0 + (tid & 31);
+      bsl[tid] = (b_ih ? b_ih[col] : 0.f) + (b_hh ? b_hh[col] : 0.f);
+    }
+    dma_x(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   // W_hh of gate g, units j0 + r: lane (r, hh) of k-group kg holds W[g H + j0 + r][8 kg + 4 hh .. + 3]
   // (one scalar per register: pinned element by element to AGPRs, the MFMAs read them in place)
   float wa[4 * PF_NA], wv[4 * NV];
@@ -195,6 +245,19 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
     f32x16 acc0, acc1;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+    if constexpr (XKG > 0) {  // x_t W_ih^T (x_t landed and visible: the previous step's drain + barrier)
+#pragma unroll
+      for (int kg = 0; kg < XKG; ++kg) {
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(xs + r * XLD + 8 * kg + 4 * hh);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(xs + (32 + r) * XLD + 8 * kg + 4 * hh);
+        const f32x4 wx = *reinterpret_cast<const f32x4*>(wil + ((g * XKG + kg) * 64 + lane) * 16);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0[c], wx[c], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1[c], wx[c], acc1, 0, 0, 0);
+        }
+      }
+    }
     if (t > 0) {
       if (tid == 0) {
         persist_wait(my_cnt, (unsigned)nub * (unsigned)t, status, limit, 1u);
@@ -230,10 +293,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
       for (int kg = 0; kg < NKG; ++kg) {
         const int ch = kg / KGC, kk = kg % KGC;
         if (kk == 0 && ch + 2 < NCH) dma_chunk(ch + 2, (ch + 2) % PF_NB);
-        if (kg == 0) dma_gx();
+        if (XKG == 0 && kg == 0) dma_gx();
         if (kk == KGC - 2 && ch + 1 < NCH) {  // chunk ch + 1 landed, every wave's part
           if (ch <= 1)
-            pf_vmwait<12>();
+            pf_vmwait<4 + GXN>();
           else if (ch + 2 < NCH)
             pf_vmwait<4>();
           else
@@ -316,8 +379,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
       }
 #endif
     } else {
-      dma_gx();
-      pf_vmwait<0>();
+      if constexpr (XKG == 0) {
+        dma_gx();
+        pf_vmwait<0>();
+      }
     }
     PF_STAMP(2);  // 2: k-loop after the first chunk
     __syncthreads();  // every wave done with the ring (pre aliases it) and its gxs part landed
@@ -338,7 +403,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         p[q] = *reinterpret_cast<const f32x4*>(pre + row * LDP + q * PF_U + 4 * quad);
-        x[q] = *reinterpret_cast<const f32x4*>(gxs + row * (4 * PF_U) + q * PF_U + 4 * quad);
+        x[q] = *reinterpret_cast<const f32x4*>(XKG ? bsl + q * PF_U + 4 * quad
+                                                   : gxs + row * (4 * PF_U) + q * PF_U + 4 * quad);
       }
       f32x4 cv;
 #pragma unroll
@@ -358,7 +424,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4*>(pre + row * LDP + q * PF_U + 4 * quad) = p[q];
-      *reinterpret_cast<f32x4*>(gxs + row * (4 * PF_U) + 4 * quad) = cv;
+      *reinterpret_cast<f32x4*>(cst + row * CLD + 4 * quad) = cv;
     }
     PF_STAMP(3);  // 3: exchange + cell
     // the hand-off: h_t into h_tm[t + 1], 16-B sc1 stores, drained before the arrival
@@ -395,7 +461,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
         for (int q = 0; q < 4; ++q)
           *reinterpret_cast<f32x4*>(gp + q * H) = *reinterpret_cast<const f32x4*>(pre + row * LDP + q * PF_U + 4 * quad);
         *reinterpret_cast<f32x4*>(c_tm + (long)t * BH + gb * H + j0 + 4 * quad) =
-            *reinterpret_cast<const f32x4*>(gxs + row * (4 * PF_U) + 4 * quad);
+            *reinterpret_cast<const f32x4*>(cst + row * CLD + 4 * quad);
       }
     }
     if (hT) {
@@ -408,6 +474,16 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
           *reinterpret_cast<f32x4*>(row + (long)(t + 1) * Bp + gb) = *reinterpret_cast<const f32x4*>(hts + u * LDH + 4 * c);
           if (t == 0) *reinterpret_cast<f32x4*>(row + gb) = f32x4{0.f, 0.f, 0.f, 0.f};
         }
+      }
+    }
+    if constexpr (XKG > 0) {
+      // x_{t+1} (xs was last read by this step's x-part, before the barriers since; an LDS-DMA
+      // issued inside the k-loop made hipcc wait vmcnt(0) before the ring reads behind it), then
+      // landed and visible before the next step's x-part
+      if (t + 1 < T) {
+        dma_x(t + 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
       }
     }
     PF_STAMP(5);  // 5: off-chain stores
@@ -803,7 +879,8 @@ size_t sv_persist_f32_bwd_scratch(int T, int B, int H) {  // hand-off slots + bi
 }
 
 int sv_persist_fwd_f32(int T, int B, int H, const float* whh, float* gates, float* c_tm, float* h_tm, float* hT,
-                       hipStream_t stream, unsigned* sync, int chan, hipEvent_t pre, hipEvent_t post) {
+                       hipStream_t stream, unsigned* sync, int chan, hipEvent_t pre, hipEvent_t post,
+                       const float* x_tm, int F, const float* wih, const float* b_ih, const float* b_hh) {
   if (!sv_persist_f32_fits(B, H, sv_stream_cus(stream))) return SV_ESHAPE;
   if (!sync || chan < 0 || chan >= SV_SYNC_CHANNELS || !whh || !gates || !c_tm || !h_tm) return SV_EARG;
   unsigned* cnt = sync + SV_SYNC_CNT + (size_t)chan * SV_PCNT_ROWS * SV_PCNT_STRIDE;
@@ -816,9 +893,16 @@ int sv_persist_fwd_f32(int T, int B, int H, const float* whh, float* gates, floa
 #endif
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
-  hipLaunchKernelGGL((lstm_persist_fwd_f32_kernel<96, PF_FWD_NV, PF_FWD_NL>), dim3(nub * nrb), dim3(256),
-                     pf_fwd_lds(), stream, whh, gates, c_tm, h_tm, hT, (long)(T + 1) * Bp, T, Bp, B, cnt, nub, PF_XCD,
-                     sync, sv_persist_limit(), sv_persist_fault(0));
+  if (x_tm) {  // layer 0: the input projection inside the recurrence (F = 40 only)
+    if (F != 40 || !wih) return SV_EARG;
+    hipLaunchKernelGGL((lstm_persist_fwd_f32_kernel<96, PF_FWD_NV, PF_FWD_NL, 5>), dim3(nub * nrb), dim3(256),
+                       pf_fwd_lds(), stream, whh, gates, c_tm, h_tm, hT, (long)(T + 1) * Bp, T, Bp, B, cnt, nub,
+                       PF_XCD, sync, sv_persist_limit(), sv_persist_fault(0), x_tm, wih, b_ih, b_hh);
+  } else {
+    hipLaunchKernelGGL((lstm_persist_fwd_f32_kernel<96, PF_FWD_NV, PF_FWD_NL>), dim3(nub * nrb), dim3(256),
+                       pf_fwd_lds(), stream, whh, gates, c_tm, h_tm, hT, (long)(T + 1) * Bp, T, Bp, B, cnt, nub,
+                       PF_XCD, sync, sv_persist_limit(), sv_persist_fault(0), nullptr, nullptr, nullptr, nullptr);
+  }
   SV_LAUNCH_CHECK();
   if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
   return SV_OK;

@@ -188,8 +188,10 @@ def test_graphed_per_file_calls_match_embed_windows(precision):
 def test_graphed_persistent_replays_interleaved_with_eager(precision):
     """Regression for r03's graph-replay mismatch: GraphedEmbedder with the persistent recurrences
     forced (schedule 'persist'), replays of three bucket graphs (128, 64, 640 windows) interleaved
-    with eager persistent calls of the same shapes, twice over, each checked bit for bit against
-    the per-step schedule (bit-identical by construction) -- and the eager calls too.  With the
+    with eager persistent calls of the same shapes, twice over, each replay checked bit for bit
+    against the eager persistent call, and both against the per-step schedule (bf16: bit-identical
+    by construction; fp32: within 1e-5, its persistent layer 0 forms the input projection in the
+    recurrence).  With the
     arrival counters reset by a hipMemsetAsync, 16-22 of 24 such replays came out wrong (one XCD's
     workgroups read a hand-off early; scripts/f32_replay_diag.py); the counters are now zeroed by a
     kernel (sv_zero_counters).  Padded buckets (100, 37 windows) agree to fp32 rounding."""
@@ -215,9 +217,12 @@ def test_graphed_persistent_replays_interleaved_with_eager(precision):
             d_eager = float((eager - ref).abs().max())
             d_graph = float((got - ref).abs().max())
             worst = max(worst, d_graph)
-            assert d_eager == 0.0, (rep, S, d_eager)
+            # bf16: persistent and per-step are bit-identical; fp32: they agree to rounding (the
+            # persistent layer 0 forms its input projection in the recurrence), and the replay must
+            # equal the eager persistent call bit for bit
+            assert d_eager <= (0.0 if precision == "bf16" else 1e-5), (rep, S, d_eager)
             if S % 32 == 0:
-                assert d_graph == 0.0, (rep, S, d_graph)
+                assert torch.equal(got, eager), (rep, S, float((got - eager).abs().max()))
             else:
                 assert d_graph <= (5e-3 if precision == "bf16" else 1e-5), (rep, S, d_graph)
     print(f"\nMEASURED graphed_persist_{precision} worst vs per-step {worst:.3e}")

@@ -107,7 +107,8 @@ def test_graph_replayed_persistent_forward_state_bit_exact(precision, B):
     """The persistent forward captured in a HIP graph (save=True, so every layer's h_tm / gates /
     c_tm stays reachable), replayed with new frames, each replay followed by an eager persistent
     call of the same shape: every layer's h_tm (including slot 0, the zero initial state), gates
-    and c_tm must equal the per-step schedule's bit for bit.  Before every zeroing in the library
+    and c_tm must equal, bit for bit, the per-step schedule's (bf16) or the eager persistent call's
+    (fp32, whose layer 0 forms its input projection in the recurrence; per-step within 1e-5).  Before every zeroing in the library
     went through a kernel (sv_zero_bytes / sv_zero_counters), the replays left junk in the
     memset-zeroed arrival counters and h_tm slot 0, and one XCD's workgroups read a hand-off
     early (scripts/f32_replay_diag.py)."""
@@ -148,8 +149,17 @@ def test_graph_replayed_persistent_forward_state_bit_exact(precision, B):
         x = torch.as_tensor(recipe.make_frames(300 + rep, B, 24, 40)).to(dev)
         xs.copy_(x)
         g.replay()
-        fwd(x, layers, wp, bp, save=False, schedule="persist")
-        ref, rst = fwd(x, layers, wp, bp, save=True, schedule="per_step")
+        eag, est = fwd(x, layers, wp, bp, save=True, schedule="persist")
+        if precision == "f32":
+            # fp32: the persistent forward forms layer 0's input projection inside the recurrence
+            # (a different summation order from the per-step schedule's K1 GEMM + K2), so the bit-exact
+            # reference is the eager persistent call, and the per-step schedule agrees to rounding
+            per, _ = fwd(x, layers, wp, bp, save=False, schedule="per_step")
+            torch.cuda.synchronize()
+            assert float((eag - per).abs().max()) < 1e-5, (rep, float((eag - per).abs().max()))
+            ref, rst = eag, est
+        else:
+            ref, rst = fwd(x, layers, wp, bp, save=True, schedule="per_step")
         torch.cuda.synchronize()
         assert int(st_.block[0]) == 0
         assert torch.equal(emb, ref), (rep, float((emb - ref).abs().max()))
