@@ -101,8 +101,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
   constexpr int XF = 8 * XKG, XLD = XF + 4;  // x tile [64][XLD] fp32 (an odd 16-B row stride: conflict-free)
   constexpr int XSL = XLD / 4;               // 16-B slots per x-tile row
   constexpr int GXN = XKG ? 0 : 8;           // x-projection DMA ops per wave in the k-loop's counted waits
-  static_assert(XKG == 0 || (PF_BM * XLD * 4 + 4 * XKG * 1024 + 4 * PF_U * 4 <= PF_BM * 4 * PF_U * 4 && XSL % 2 == 1),
-                "x tile + W_ih + biases fit the x-projection region");
+  static_assert(XKG == 0 || (4 * XKG * 1024 + 4 * PF_U * 4 + PF_BM * PF_U * 4 <= PF_BM * 4 * PF_U * 4 &&
+                             PF_BM * XLD * 4 <= PF_CH && XSL % 2 == 1 &&
+                             (PF_BM * (4 * PF_U + 4) + PF_U * (PF_BM + 4)) * 4 <= 3 * PF_CH),
+                "W_ih + biases + c fit the x-projection region; the x tile ring slot 3, above pre + hts");
   static_assert(NCH >= 4 && H % PF_KC == 0 && PF_NA + NV + NL == NKG, "chunk schedule / weight split");
   constexpr int LDP = 4 * PF_U + 4;  // pre [64][LDP] fp32
   constexpr int LDH = PF_BM + 4;     // hts [32][LDH] fp32
@@ -113,10 +115,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
   float* pre = reinterpret_cast<float*>(smem);                  // after the k-loop: aliases the ring
   float* hts = pre + PF_BM * LDP;                               // (aliases the ring too)
   // XKG: x tile, W_ih fragments and biases in the x-projection region; c staged in the ring
-  float* xs = gxs;                                                  // [64][XLD]
-  char* wil = reinterpret_cast<char*>(gxs + PF_BM * XLD);           // [4 waves][XKG][64 lanes][16 B]
+  // (the x tile lives in ring slot 3, free from the end of one k-loop to the next step's chunk-3 DMA,
+  // above pre + hts; W_ih, the biases and the step's c in the x-projection region)
+  float* xs = reinterpret_cast<float*>(ring + 3 * PF_CH);           // [64][XLD]
+  char* wil = reinterpret_cast<char*>(gxs);                         // [4 waves][XKG][64 lanes][16 B]
   float* bsl = reinterpret_cast<float*>(wil + 4 * XKG * 1024);      // [4 gates][32 units] b_ih + b_hh
-  float* cst = XKG ? hts + PF_U * (PF_BM + 4) : gxs;                // c_t of the step (row stride CLD)
+  float* cst = XKG ? bsl + 4 * PF_U : gxs;                          // c_t of the step (row stride CLD)
   constexpr int CLD = XKG ? PF_U : 4 * PF_U;
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -386,6 +390,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
     }
     PF_STAMP(2);  // 2: k-loop after the first chunk
     __syncthreads();  // every wave done with the ring (pre aliases it) and its gxs part landed
+    // XKG: x_{t+1} into ring slot 3 now (this step's x-part read x_t there before the poll barrier;
+    // the hand-off drain below waits for it, the cell's 2-3k cycles after its issue)
+    if (XKG > 0 && t + 1 < T) dma_x(t + 1);
     // pre-activation exchange: wave g's row halves -> pre[row][g 32 + unit]
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -474,16 +481,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
           *reinterpret_cast<f32x4*>(row + (long)(t + 1) * Bp + gb) = *reinterpret_cast<const f32x4*>(hts + u * LDH + 4 * c);
           if (t == 0) *reinterpret_cast<f32x4*>(row + gb) = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-      }
-    }
-    if constexpr (XKG > 0) {
-      // x_{t+1} (xs was last read by this step's x-part, before the barriers since; an LDS-DMA
-      // issued inside the k-loop made hipcc wait vmcnt(0) before the ring reads behind it), then
-      // landed and visible before the next step's x-part
-      if (t + 1 < T) {
-        dma_x(t + 1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
       }
     }
     PF_STAMP(5);  // 5: off-chain stores
