@@ -28,6 +28,7 @@
 #define GF_BK 32
 
 typedef __attribute__((address_space(3))) void* gf_lds_ptr_t;
+typedef unsigned int gf_u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) void* gf_glb_ptr_t;
 
 __device__ __forceinline__ int gf_phys_slot(int row, int slot) { return slot ^ ((row >> 1) & 7); }
@@ -107,36 +108,19 @@ struct GfAFrag {
   int bsl, kh;        // batch rows per slot (a multiple of 32), gate width H (k per gate)
 };
 
-template <int BN, int MF, int EPI, int AF = 0>
-__global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __restrict__ A, long lda,
-                                                             const float* __restrict__ B, long ldb,
-                                                             float* __restrict__ C, long ldc, long slab, int M, int N,
-                                                             int K, int kchunk, const float* __restrict__ bias0,
-                                                             const float* __restrict__ bias1, float beta,
-                                                             GfAFrag af = GfAFrag{}) {
-  static_assert(!AF || MF == 32, "fragment-order A: the 32x32x2 fragment layout");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+// the k-loop of one tile (rows tm GF_BM, columns tn BN, k-tiles [kbeg / GF_BK, + nk)) into acc
+// (zeroed here); shared by the one-shot and stream-K kernels.  Ends with every wave past its last
+// LDS read (the stages may be refilled).
+template <int BN, int MF, int AF>
+__device__ __forceinline__ void gf_mainloop(const float* __restrict__ A, long lda, const float* __restrict__ B,
+                                            long ldb, int tm, int tn, int kbeg, int nk, const GfAFrag& af,
+                                            char* smem,
+                                            typename GfGeom<BN, MF>::Acc (&acc)[128 / MF][BN / 4 / MF]) {
   constexpr int WN = BN / 4;                 // wave's columns (64 or 32)
   constexpr int TM = 128 / MF, TN = WN / MF;  // MFMA blocks per wave
-  using Acc = typename std::conditional<MF == 32, f32x16, f32x4>::type;
   constexpr int NR = MF == 32 ? 16 : 4;
   constexpr int OPA = GF_BM * GF_BK * 4, OPB = BN * GF_BK * 4;  // bytes per operand per stage
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int tiles_n = N / BN;
-  const int nwg = tiles_n * (M / GF_BM);
-  int id, sl = 0, tn, tm;
-  if (gridDim.y == 1) {
-    // one-shot launches: column-grouped tile order (4 fp32 B panels of 256 x 768 = 3.1 MB per XCD
-    // L2 at the K1 shape)
-    id = xcd_remap(blockIdx.x, nwg);
-    grouped_tile(id, M / GF_BM, tiles_n, SV_GF_GROUP, tm, tn);
-  } else {
-    splitk_tile(nwg, id, sl);
-    tn = id % tiles_n;
-    tm = id / tiles_n;
-  }
-  const int kbeg = sl * kchunk;
-  const int nk = (min(K, kbeg + kchunk) - kbeg) / GF_BK;
   const int wr = w >> 2, wc = w & 3;
   GfStage<GF_BM> sa;
   GfStage<BN> sb;
@@ -161,7 +145,6 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
       sa.issue(lds, kt, w);
     }
   };
-  Acc acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -228,7 +211,19 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  // epilogue: acc[i][j][e] = C[row][4 consecutive cols]
+}
+
+// C tile store of acc: acc[i][j][e] = C[row][4 consecutive cols] (+ bias0 + bias1 + beta C for
+// GF_STORE; slab `sl` of the split-K workspace for GF_SLAB)
+template <int BN, int MF, int EPI>
+__device__ __forceinline__ void gf_store_tile(const typename GfGeom<BN, MF>::Acc (&acc)[128 / MF][BN / 4 / MF],
+                                              float* __restrict__ C, long ldc, long slab, int sl, int tm, int tn,
+                                              const float* __restrict__ bias0, const float* __restrict__ bias1,
+                                              float beta) {
+  constexpr int WN = BN / 4, TM = 128 / MF, TN = WN / MF, NR = MF == 32 ? 16 : 4;
+  constexpr int RM = MF == 32 ? 31 : 15;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
+  const int fr = lane & RM, fh = MF == 32 ? lane >> 5 : lane >> 4;
   float* Cz = C + (EPI == GF_SLAB ? (long)sl * slab : 0);
   GfBias<BN, MF> bias;
   if (EPI == GF_STORE) bias.load(bias0, bias1, tn, wc, fh);
@@ -251,6 +246,137 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
         }
         *reinterpret_cast<f32x4*>(dst) = v;
       }
+  }
+}
+
+template <int BN, int MF, int EPI, int AF = 0>
+__global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __restrict__ A, long lda,
+                                                             const float* __restrict__ B, long ldb,
+                                                             float* __restrict__ C, long ldc, long slab, int M, int N,
+                                                             int K, int kchunk, const float* __restrict__ bias0,
+                                                             const float* __restrict__ bias1, float beta,
+                                                             GfAFrag af = GfAFrag{}) {
+  static_assert(!AF || MF == 32, "fragment-order A: the 32x32x2 fragment layout");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles_n = N / BN;
+  const int nwg = tiles_n * (M / GF_BM);
+  int id, sl = 0, tn, tm;
+  if (gridDim.y == 1) {
+    // one-shot launches: column-grouped tile order (4 fp32 B panels of 256 x 768 = 3.1 MB per XCD
+    // L2 at the K1 shape)
+    id = xcd_remap(blockIdx.x, nwg);
+    grouped_tile(id, M / GF_BM, tiles_n, SV_GF_GROUP, tm, tn);
+  } else {
+    splitk_tile(nwg, id, sl);
+    tn = id % tiles_n;
+    tm = id / tiles_n;
+  }
+  const int kbeg = sl * kchunk;
+  const int nk = (min(K, kbeg + kchunk) - kbeg) / GF_BK;
+  typename GfGeom<BN, MF>::Acc acc[128 / MF][BN / 4 / MF];
+  gf_mainloop<BN, MF, AF>(A, lda, B, ldb, tm, tn, kbeg, nk, af, smem, acc);
+  gf_store_tile<BN, MF, EPI>(acc, C, ldc, slab, sl, tm, tn, bias0, bias1, beta);
+}
+
+// ---- stream-K form (C = A . B^T, plain stores, no bias / beta; 32x32x2 MFMA) ----
+// A one-shot launch with tiles % CUs != 0 leaves the last round partly idle: the c2 dx GEMM
+// (fragment-order A) is 1200 tiles of 96 k-tiles on 256 CUs, 4.69 rounds run as 5.  Here a grid of
+// G workgroups (one per CU) first runs R = tiles / G whole tiles each (data-parallel part, the
+// one-shot kernel's tile order), then the remaining rem tiles' rem x nk k-tiles, cut into G equal
+// contiguous ranges of L k-tiles (tile-major, k-minor).  A range's pieces of a tile are partial
+// sums; each is written (sc1, drained) to the workgroup's partial slot and counted on the tile's
+// arrival counter, and the workgroup that arrives last reads the others (sc1 loads) and stores the
+// tile's sum -- summed in segment order (k order), so the result is deterministic.  No workgroup
+// ever waits for another (no co-residency requirement).  The counters are left at zero.
+struct GfSK {
+  int R, rem, L;   // whole-tile rounds, stream-K tiles, k-tiles per workgroup range
+  float* part;     // 2 G partial slots of 512 threads x 128 fp32 (slot 2 i: the piece opening i's range)
+  unsigned* cnt;   // [rem] arrival counters, zero at the launch
+};
+constexpr int GF_SK_MAXSEG = 4;  // segments per stream-K tile (the host checks)
+
+template <int BN, int AF>
+__global__ __launch_bounds__(512, 1) void gemm_f32_256sk_kernel(const float* __restrict__ A, long lda,
+                                                               const float* __restrict__ B, long ldb,
+                                                               float* __restrict__ C, long ldc, int M, int N, int K,
+                                                               GfSK sk, GfAFrag af = GfAFrag{}) {
+  constexpr int MF = 32, TM = 128 / MF, TN = BN / 4 / MF, NR = 16, NV = TM * TN * NR;
+  constexpr unsigned SLOT = 512u * NV * 4u;  // bytes per partial slot
+  using Acc = typename GfGeom<BN, MF>::Acc;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ unsigned arrived;
+  const int tid = threadIdx.x, G = gridDim.x, i = blockIdx.x;
+  const int tiles_m = M / GF_BM, tiles_n = N / BN, nk = K / GF_BK;
+  const long S = (long)sk.rem * nk, p1 = min(S, (long)(i + 1) * sk.L);
+  long p = (long)i * sk.L;  // stream-K cursor (tile-major, k-minor)
+  // partial slots: one buffer descriptor over all of them (uniform); lane offset (chunk 512 + tid) 16
+  const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(sk.part, 0, 2u * G * SLOT, 0x00020000);
+  Acc acc[TM][TN];
+  // work items: R whole tiles (positions i + G r of [0, R G), the one-shot kernel's order), then
+  // this workgroup's stream-K range -- one call site of the k-loop
+  for (int r = 0;; ++r) {
+    int tm, tn, ka = 0, kb = nk, j = -1;
+    if (r < sk.R) {
+      grouped_tile(xcd_remap(i + G * r, sk.R * G), tiles_m, tiles_n, SV_GF_GROUP, tm, tn);
+    } else {
+      if (p >= p1) break;
+      j = (int)(p / nk);
+      ka = (int)(p - (long)j * nk);
+      kb = (int)min((long)nk, p1 - (long)j * nk);
+      p = (long)j * nk + kb;
+      grouped_tile(sk.R * G + j, tiles_m, tiles_n, SV_GF_GROUP, tm, tn);
+    }
+    gf_mainloop<BN, MF, AF>(A, lda, B, ldb, tm, tn, ka * GF_BK, kb - ka, af, smem, acc);
+    if (ka == 0 && kb == nk) {  // a whole tile
+      gf_store_tile<BN, MF, GF_STORE>(acc, C, ldc, 0L, 0, tm, tn, nullptr, nullptr, 0.f);
+      continue;
+    }
+    // a piece of stream-K tile j: the tile's pieces are workgroups s0 .. s1's (k order)
+    const int s0 = (int)(((long)j * nk) / sk.L), s1 = (int)(((long)j * nk + nk - 1) / sk.L);
+    auto slot = [&](int wg) {  // slot of workgroup wg's piece of tile j: 0 if it opens wg's range
+      return (unsigned)(2 * wg + ((long)wg * sk.L >= (long)j * nk ? 0 : 1)) * SLOT;
+    };
+    {
+      const unsigned base = slot(i);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+          for (int q = 0; q < NR / 4; ++q) {
+            const unsigned off = base + (unsigned)((((a * TN + b) * (NR / 4) + q) * 512 + tid) * 16);
+            const f32x4 v = {acc[a][b][4 * q], acc[a][b][4 * q + 1], acc[a][b][4 * q + 2], acc[a][b][4 * q + 3]};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gf_u32x4, v), rpart, off, 0, 16 /* sc1 */);
+          }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) arrived = __hip_atomic_fetch_add(sk.cnt + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (arrived != (unsigned)(s1 - s0)) continue;  // not the last piece to arrive
+    // the last piece: the tile's pieces summed in segment order (this one from registers)
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int q = 0; q < NR / 4; ++q) {
+          const unsigned off = (unsigned)((((a * TN + b) * (NR / 4) + q) * 512 + tid) * 16);
+          const f32x4 own = {acc[a][b][4 * q], acc[a][b][4 * q + 1], acc[a][b][4 * q + 2], acc[a][b][4 * q + 3]};
+          f32x4 sum = own;
+          for (int wg = s0; wg <= s1; ++wg) {
+            const f32x4 v = wg == i ? own
+                                    : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                    rpart, slot(wg) + off, 0, 16 /* sc1 */));
+            sum = wg == s0 ? v : sum + v;
+          }
+          acc[a][b][4 * q] = sum[0];
+          acc[a][b][4 * q + 1] = sum[1];
+          acc[a][b][4 * q + 2] = sum[2];
+          acc[a][b][4 * q + 3] = sum[3];
+        }
+    gf_store_tile<BN, MF, GF_STORE>(acc, C, ldc, 0L, 0, tm, tn, nullptr, nullptr, 0.f);
+    if (tid == 0) __hip_atomic_store(sk.cnt + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

@@ -639,12 +639,38 @@ int dx_afrag_bn(int T, int B, int H, int Fl) {
   if (Fl % bn || plan_gf256(T * B, Fl, 4 * H).splitk != 1) return -1;
   return bn;
 }
+// stream-K scratch of the dx GEMM (gemm_f32_256sk_kernel): two partial slots of 512 threads x 128
+// fp32 per workgroup (grid capped at GF_SK_GRID) + the stream-K tiles' arrival counters
+constexpr int GF_SK_GRID = 256;
+constexpr size_t GF_SK_SLOT = (size_t)512 * 128 * sizeof(float);
+size_t gf_sk_bytes() { return 2 * GF_SK_GRID * GF_SK_SLOT + GF_SK_GRID * sizeof(unsigned) * 4; }
+#ifndef SV_GF_SK
+#define SV_GF_SK 1  // the dx GEMM's stream-K form where its tiles leave the last round part-idle (0: A/B)
+#endif
 int gemm_f32_dx_afrag(int bn, const float* dgf, int T, int B, int H, const float* wihT, int Fl, float* dx,
-                      hipStream_t s) {
+                      hipStream_t s, void* skws = nullptr) {
   const long nrb = (B + 63) / 64, fs = nrb * 8 * (H / 8) * 256;
   const GfAFrag af{dgf, fs, B, H};
   const int M = T * B, K = 4 * H, tiles = (M / GF_BM) * (Fl / bn);
   const size_t lds = 2 * (size_t)(GF_BM + bn) * GF_BK * 4;
+  const int G = std::min(sv_stream_cus(s), GF_SK_GRID), nk = K / GF_BK;
+  if (SV_GF_SK && skws && bn == 256 && G > 0 && tiles > G && tiles % G) {
+    // c2 dx: 1200 tiles on 256 CUs = 4 whole rounds + 176 tiles as 66 k-tiles per workgroup
+    GfSK sk;
+    sk.R = tiles / G;
+    sk.rem = tiles % G;
+    sk.L = (int)(((long)sk.rem * nk + G - 1) / G);
+    if (sk.L * 3 >= nk) {  // <= GF_SK_MAXSEG pieces per tile
+      sk.part = static_cast<float*>(skws);
+      sk.cnt = reinterpret_cast<unsigned*>(static_cast<char*>(skws) + 2 * GF_SK_GRID * GF_SK_SLOT);
+      hipError_t e = (hipError_t)sv_zero_counters(sk.cnt, 1, 0, sk.rem, s);
+      if (e != hipSuccess) return (int)e;
+      hipLaunchKernelGGL((gemm_f32_256sk_kernel<256, 1>), dim3(G), dim3(512), lds, s, nullptr, 0L, wihT, (long)K, dx,
+                         (long)Fl, M, Fl, K, sk, af);
+      SV_LAUNCH_CHECK();
+      return SV_OK;
+    }
+  }
   if (bn == 256)
     hipLaunchKernelGGL((gemm_f32_256_kernel<256, SV_F32_MF, GF_STORE, 1>), dim3(tiles, 1), dim3(512), lds, s, nullptr,
                        0L, wihT, (long)K, dx, (long)Fl, 0L, M, Fl, K, K, nullptr, nullptr, 0.f, af);
@@ -1048,7 +1074,8 @@ extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float*
 // ============================================================================
 extern "C" size_t sv_lstm_stack_bwd_workspace(int L, int T, int B, int F, int H) {
   // + the persistent backward's fragment-order hand-off (shared by the layers, one after another)
-  const size_t dgf = H == 768 ? sv_persist_f32_bwd_scratch(T, B, H) : 0;
+  // + the dx GEMM's stream-K scratch behind it
+  const size_t dgf = H == 768 ? ((sv_persist_f32_bwd_scratch(T, B, H) + 255) & ~size_t(255)) + gf_sk_bytes() : 0;
   return (size_t)L * ((carve_bwd(nullptr, T, B, std::max(F, H), H).total + 255) & ~size_t(255)) + dgf;
 }
 
@@ -1078,6 +1105,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
     // whole-T dx = dG W_ih GEMM (the next layer's dh_up), the dW GEMMs and the bias row sums
     if (!sync) return SV_EARG;
     float* dgf = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + per * L);
+    void* skws = reinterpret_cast<char*>(dgf) + ((sv_persist_f32_bwd_scratch(T, B, H) + 255) & ~size_t(255));
     for (int l = L - 1; l >= 0; --l) {
       const int Fl = l == 0 ? F : H;
       const BwdWs ws = carve_bwd((float*)((char*)workspace + per * l), T, B, std::max(F, H), H);
@@ -1098,7 +1126,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
       // weight-gradient GEMMs
       for (int k = 1; l == 0 && k < L; ++k)
         if ((e = hipEventRecord(ev[L * nch + k], main)) != hipSuccess) return (int)e;
-      if (l > 0 && abn > 0 && (rc = gemm_f32_dx_afrag(abn, dgf, T, B, H, ws.wihT, Fl, dx[l], main))) return rc;
+      if (l > 0 && abn > 0 && (rc = gemm_f32_dx_afrag(abn, dgf, T, B, H, ws.wihT, Fl, dx[l], main, skws))) return rc;
       if (l > 0 && abn < 0 &&
           (rc = gemm_f32(1, 1, T * B, Fl, 4 * H, dgates[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr, nullptr, 0.f,
                          ws.gws, main)))
