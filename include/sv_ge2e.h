@@ -244,6 +244,8 @@ int sv_gemm_bf16(int M, int N, int K, const sv_bf16* A, long lda, const sv_bf16*
 int sv_gemm_bf16_bf(int M, int N, int K, const sv_bf16* A, long lda, const sv_bf16* B, long ldb, sv_bf16* C,
                     long ldc, const float* bias0, const float* bias1, hipStream_t stream);
 int sv_cast_bf16(const float* x, sv_bf16* y, long n, hipStream_t stream);
+/* n <= 8 such casts in one launch (y[i] = bf16(x[i]), count[i] elements each; host arrays) */
+int sv_cast_bf16_batch(int n, const float* const* x, sv_bf16* const* y, const long* count, hipStream_t stream);
 int sv_transpose_cast_bf16(const float* src, long ld_src, int R, int C, sv_bf16* dst, long ld_dst,
                            hipStream_t stream);
 /* x_bf [T,B,F]; writes gates (bf16), c_tm/h_tm (fp32) plus h_bf [T+1,B,H] and hT [H,(T+1)Bp] (bf16) */

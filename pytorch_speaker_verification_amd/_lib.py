@@ -93,6 +93,7 @@ SIGNATURES = {
                               _P]),
     "sv_gemm_bf16_bf": (_c_int, [_c_int, _c_int, _c_int, _P, _c_long, _P, _c_long, _P, _c_long, _P, _P, _P]),
     "sv_cast_bf16": (_c_int, [_P, _P, _c_long, _P]),
+    "sv_cast_bf16_batch": (_c_int, [_c_int, _P, _P, _P, _P]),
     "sv_transpose_cast_bf16": (_c_int, [_P, _c_long, _c_int, _c_int, _P, _c_long, _P]),
     "sv_lstm_layer_fwd_bf16": (_c_int, [_P, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_lstm_stack_fwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,

@@ -125,6 +125,54 @@ __global__ __launch_bounds__(256) void transpose_cast_kernel(const float* __rest
   }
 }
 
+// up to 8 casts / transpose-casts in ONE launch (the per-step weight copies of the bf16 path: at
+// the c4 rank shape each of the 13 separate launches took ~5 us for ~1 us of traffic)
+struct CastBatch {
+  const float* x[8];
+  bf16_t* y[8];
+  long start[9];  // element prefix sums
+  int n;
+};
+__global__ void cast_bf16_batch_kernel(const CastBatch cb) {
+  const long total = cb.start[cb.n];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int b = 0;
+#pragma unroll
+    for (int k = 1; k < 8; ++k) b += (k < cb.n && i >= cb.start[k]) ? 1 : 0;
+    const long j = i - cb.start[b];
+    cb.y[b][j] = to_bf(cb.x[b][j]);
+  }
+}
+struct TCastBatch {
+  const float* src[8];
+  bf16_t* dst[8];
+  long lds[8], ldd[8];
+  int R[8], C[8], tx[8];  // column tiles per matrix
+  int tile0[9];           // 32 x 32 tile prefix sums
+  int n;
+};
+__global__ __launch_bounds__(256) void transpose_cast_batch_kernel(const TCastBatch tb) {
+  __shared__ float tile[32][33];
+  int b = 0;
+#pragma unroll
+  for (int k = 1; k < 8; ++k) b += (k < tb.n && (int)blockIdx.x >= tb.tile0[k]) ? 1 : 0;
+  const int t = blockIdx.x - tb.tile0[b];
+  const int R = tb.R[b], C = tb.C[b];
+  const int c0 = (t % tb.tx[b]) * 32, r0 = (t / tb.tx[b]) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const float* src = tb.src[b];
+  for (int i = ty; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? src[(long)r * tb.lds[b] + c] : 0.f;
+  }
+  __syncthreads();
+  bf16_t* dst = tb.dst[b];
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) dst[(long)c * tb.ldd[b] + r] = to_bf(tile[tx][i]);
+  }
+}
+
 // row sums of a bf16 matrix, fp32 accumulation, one block per row, fixed order
 __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const bf16_t* __restrict__ X, long ld, int C,
                                                           float* __restrict__ out0, float* __restrict__ out1) {
@@ -585,6 +633,45 @@ extern "C" int sv_cast_bf16(const float* x, bf16_t* y, long n, hipStream_t strea
   return SV_OK;
 }
 
+extern "C" int sv_cast_bf16_batch(int n, const float* const* x, bf16_t* const* y, const long* count,
+                                  hipStream_t stream) {
+  if (n <= 0 || n > 8 || !x || !y || !count) return SV_EARG;
+  CastBatch cb{};
+  cb.n = n;
+  for (int i = 0; i < n; ++i) {
+    if (!x[i] || !y[i] || count[i] <= 0) return SV_EARG;
+    cb.x[i] = x[i];
+    cb.y[i] = y[i];
+    cb.start[i + 1] = cb.start[i] + count[i];
+  }
+  const int grid = (int)std::min<long>((cb.start[n] + 255) / 256, 8192);
+  hipLaunchKernelGGL(cast_bf16_batch_kernel, dim3(grid), dim3(256), 0, stream, cb);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+// the transpose-casts of up to 8 matrices in one launch (dst[c ldd + r] = bf16(src[r lds + c]))
+int transpose_cast_bf16_batch(int n, const float* const* src, const long* lds, const int* R, const int* C,
+                              bf16_t* const* dst, const long* ldd, hipStream_t stream) {
+  if (n <= 0 || n > 8) return SV_EARG;
+  TCastBatch tb{};
+  tb.n = n;
+  for (int i = 0; i < n; ++i) {
+    if (!src[i] || !dst[i] || R[i] <= 0 || C[i] <= 0) return SV_EARG;
+    tb.src[i] = src[i];
+    tb.dst[i] = dst[i];
+    tb.lds[i] = lds[i];
+    tb.ldd[i] = ldd[i];
+    tb.R[i] = R[i];
+    tb.C[i] = C[i];
+    tb.tx[i] = (C[i] + 31) / 32;
+    tb.tile0[i + 1] = tb.tile0[i] + tb.tx[i] * ((R[i] + 31) / 32);
+  }
+  hipLaunchKernelGGL(transpose_cast_batch_kernel, dim3(tb.tile0[n]), dim3(256), 0, stream, tb);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
 extern "C" int sv_transpose_cast_bf16(const float* src, long ld_src, int R, int C, bf16_t* dst, long ld_dst,
                                       hipStream_t stream) {
   if (!src || !dst || R <= 0 || C <= 0) return SV_EARG;
@@ -703,13 +790,28 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
       return (int)e;
     return SV_OK;
   };
+  // every layer's state reset in one launch (the schedules that run on `main`)
+  auto zero_states = [&](hipStream_t s) -> int {
+    void* p[8];
+    size_t b[8];
+    int n = 0;
+    for (int l = 0; l < L; ++l) {
+      if (n + 3 > 8) {
+        if (int rc = sv_zero_bytes_multi(n, p, b, s)) return rc;
+        n = 0;
+      }
+      p[n] = h_tm[l], b[n++] = BH * sizeof(float);
+      p[n] = h_bf[l], b[n++] = BH * sizeof(bf16_t);
+      if (hT[l] && Bp != B) p[n] = hT[l], b[n++] = (size_t)H * ldhT * sizeof(bf16_t);
+    }
+    return sv_zero_bytes_multi(n, p, b, s);
+  };
   int rc;
   if (sched_wave(schedule, H) && sv_wave_fwd_fits(L, T, B, F, H, sv_stream_cus(main))) {
     // layer-wavefront schedule (sv_wave.hip): every layer's recurrence and input projection in
     // one launch on `main`
     if (!sync) return SV_EARG;
-    for (int l = 0; l < L; ++l)
-      if ((rc = zero_state(l, main))) return rc;
+    if ((rc = zero_states(main))) return rc;
     return sv_wave_fwd_bf16(L, T, B, F, H, x_bf, w_ih_bf, w_hh_bf, b_ih, b_hh, gates, c_tm, h_tm, h_bf, hT, sync, main,
                             sv_persist_limit(), sv_persist_fault(0), probe ? probe[0] : nullptr,
                             probe ? probe[1] : nullptr);
@@ -718,8 +820,8 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
     if (!sync) return SV_EARG;
     // persistent schedule on `main`: per layer the whole-T K1 GEMM, then one launch for the
     // recurrence (sv_persist.hip); layers run one after another
+    if ((rc = zero_states(main))) return rc;
     for (int l = 0; l < L; ++l) {
-      if ((rc = zero_state(l, main))) return rc;
       const int Fl = l == 0 ? F : H;
       const bf16_t* in = l == 0 ? x_bf : h_bf[l - 1] + BH;
       if (l == 0 && sv_persist_fwd_fusex_ok(H, F)) {  // layer 0's input projection inside the recurrence
@@ -805,6 +907,35 @@ BBwdWs carve_bbwd(char* base, int T, int B, int F, int H) {
 
 // L per-layer regions, then the persistent backward's hand-off scratch (shared by the layers,
 // whose recurrences run one after another)
+// W_hh^T of every layer and W_ih^T of layers >= 1 (bf16 [K, 4H]) in one or two launches
+static int wbf_transposes(int L, int F, int H, const float* const* w_ih, const float* const* w_hh,
+                          const bf16_t* const* whhT, const bf16_t* const* wihT, hipStream_t s) {
+  const float* src[8];
+  bf16_t* dst[8];
+  long lds[8], ldd[8];
+  int R[8], C[8], n = 0;
+  auto flush = [&]() -> int {
+    const int rc = n ? transpose_cast_bf16_batch(n, src, lds, R, C, dst, ldd, s) : 0;
+    n = 0;
+    return rc;
+  };
+  for (int l = 0; l < L; ++l) {
+    for (int m = 0; m < (l > 0 ? 2 : 1); ++m) {
+      if (n == 8)
+        if (int rc = flush()) return rc;
+      const int K = m == 0 ? H : (l == 0 ? F : H);
+      src[n] = m == 0 ? w_hh[l] : w_ih[l];
+      dst[n] = const_cast<bf16_t*>(m == 0 ? whhT[l] : wihT[l]);
+      lds[n] = K;
+      ldd[n] = 4L * H;
+      R[n] = 4 * H;
+      C[n] = K;
+      ++n;
+    }
+  }
+  return flush();
+}
+
 extern "C" size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H) {
   const size_t per = (size_t)L * carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
   size_t scratch = sv_persist_bwd_fits(B, H, 1 << 30) ? sv_persist_bwd_scratch(T, B, H) : 0;
@@ -843,13 +974,12 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     const bf16_t* wihT_l[WB_L];
     for (int l = 0; l < L; ++l) {
       const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
-      int rc = sv_transpose_cast_bf16(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, main);
-      if (rc) return rc;
-      if (l > 0 && (rc = sv_transpose_cast_bf16(w_ih[l], H, 4 * H, H, ws.wihT, 4L * H, main))) return rc;
       whhT_l[l] = ws.whhT;
       wihT_l[l] = l > 0 ? ws.wihT : nullptr;
     }
-    int rc = sv_wave_bwd_bf16(L, T, B, H, whhT_l, wihT_l, gates, c_tm, dh_last, dx, dgT, (char*)workspace + per * L,
+    int rc = wbf_transposes(L, F, H, w_ih, w_hh, whhT_l, wihT_l, main);
+    if (rc) return rc;
+    rc = sv_wave_bwd_bf16(L, T, B, H, whhT_l, wihT_l, gates, c_tm, dh_last, dx, dgT, (char*)workspace + per * L,
                               sync, main, db_ih, db_hh, probe ? probe[0] : nullptr, probe ? probe[1] : nullptr);
     if (rc) return rc;
     for (int l = L - 1; l >= 0; --l) {
@@ -871,12 +1001,20 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     // fragment-order hand-off, then the layer's weight gradients (measured: on a side stream
     // beside the next layer's recurrence 16.8 vs 16.6 ms at c3 -- the GEMM workgroups contend
     // with the co-resident recurrence)
+    {  // every layer's W_hh^T / W_ih^T (bf16) in one launch
+      const bf16_t* whhT_l[8];
+      const bf16_t* wihT_l[8];
+      for (int l = 0; l < L && l < 8; ++l) {
+        const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
+        whhT_l[l] = ws.whhT;
+        wihT_l[l] = l > 0 ? ws.wihT : nullptr;
+      }
+      if (int rc = wbf_transposes(L, F, H, w_ih, w_hh, whhT_l, wihT_l, main)) return rc;
+    }
     for (int l = L - 1; l >= 0; --l) {
       const int Fl = l == 0 ? F : H;
       const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
-      int rc = sv_transpose_cast_bf16(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, main);
-      if (rc) return rc;
-      if (l > 0 && (rc = sv_transpose_cast_bf16(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, main))) return rc;
+      int rc = 0;
       const float* up = l == L - 1 ? dh_last : dx[l + 1];
       bf16_t* dgf = (bf16_t*)((char*)workspace + per * L);
       const bool afr = l > 0 && gemm_afrag_ok(T, B, Fl, H);  // dx reads dgf: no row-major dG

@@ -41,6 +41,8 @@ int sv_zero_counters(unsigned* cnt, int nchan, long chan_stride, int words, hipS
 // in the library instead of hipMemsetAsync: replayed from a HIP graph, memset nodes left junk
 // behind (the initial-state slots and the arrival counters; scripts/f32_replay_diag.py)
 int sv_zero_bytes(void* p, size_t bytes, hipStream_t stream);
+// up to 8 zeroings in one launch (n buffers of bytes[i] bytes each)
+int sv_zero_bytes_multi(int n, void* const* ptrs, const size_t* bytes, hipStream_t stream);
 inline hipError_t sv_memset0(void* p, size_t bytes, hipStream_t stream) {
   return (hipError_t)sv_zero_bytes(p, bytes, stream);
 }

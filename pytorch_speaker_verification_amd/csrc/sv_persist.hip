@@ -915,6 +915,39 @@ int sv_zero_bytes(void* p, size_t bytes, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// up to 8 zeroings in one launch (blockIdx.y = buffer): the per-step state resets of the bf16 stack
+struct ZeroBatch {
+  char* p[8];
+  size_t head[8], n16[8], tail[8];
+};
+__global__ void sv_zero_bytes_multi_kernel(const ZeroBatch zb) {
+  const int b = blockIdx.y;
+  char* p = zb.p[b];
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+  if (i0 < zb.head[b]) p[i0] = 0;
+  uint4* q = reinterpret_cast<uint4*>(p + zb.head[b]);
+  for (size_t i = i0; i < zb.n16[b]; i += stride) q[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (i0 < zb.tail[b]) p[zb.head[b] + 16 * zb.n16[b] + i0] = 0;
+}
+int sv_zero_bytes_multi(int n, void* const* ptrs, const size_t* bytes, hipStream_t stream) {
+  if (n <= 0) return SV_OK;
+  if (n > 8) return SV_EARG;
+  ZeroBatch zb{};
+  size_t most = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!ptrs[i] && bytes[i]) return SV_EARG;
+    char* p = static_cast<char*>(ptrs[i]);
+    zb.p[i] = p;
+    zb.head[i] = std::min(bytes[i], (size_t)((16 - ((uintptr_t)p & 15)) & 15));
+    zb.n16[i] = (bytes[i] - zb.head[i]) / 16;
+    zb.tail[i] = bytes[i] - zb.head[i] - 16 * zb.n16[i];
+    most = std::max(most, zb.n16[i]);
+  }
+  const size_t blocks = std::max<size_t>(1, std::min<size_t>(2048, (most + 255) / 256));
+  hipLaunchKernelGGL(sv_zero_bytes_multi_kernel, dim3((unsigned)blocks, n), dim3(256), 0, stream, zb);
+  return (int)hipGetLastError();
+}
+
 int sv_stream_cus(hipStream_t stream) {
   int dev = -1;
   if (stream && hipStreamGetDevice(stream, &dev) == hipSuccess) return device_cus(dev);

@@ -336,7 +336,16 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=Non
     x_tm = torch.empty((T, B, F), dtype=torch.float32, device=dev)
     call("sv_frames_to_time_major", ptr(x), ptr(x_tm), B, T, F, s)
     x_bf = _bf((T, B, F), dev)
-    call("sv_cast_bf16", ptr(x_tm), ptr(x_bf), x_tm.numel(), s)
+    L = len(layers)
+    # the frames' and every layer's weight casts in one launch (sv_cast_bf16_batch)
+    wbf = [(_bf(w_ih.shape, dev), _bf(w_hh.shape, dev)) for (w_ih, w_hh, _, _) in layers]
+    srcs = [x_tm] + [w for (w_ih, w_hh, _, _) in layers for w in (w_ih, w_hh)]
+    dsts = [x_bf] + [w for pair in wbf for w in pair]
+    for i in range(0, len(srcs), 8):
+        n = min(8, len(srcs) - i)
+        call("sv_cast_bf16_batch", n, (ctypes.c_void_p * n)(*[ptr(t) for t in srcs[i:i + n]]),
+             (ctypes.c_void_p * n)(*[ptr(t) for t in dsts[i:i + n]]),
+             (ctypes.c_long * n)(*[t.numel() for t in srcs[i:i + n]]), s)
     if save:
         st.xT0 = (torch.zeros if Bp != B else torch.empty)((F, T * Bp), dtype=torch.bfloat16, device=dev)
         if Bp == B:
@@ -345,13 +354,6 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=Non
             for t in range(T):
                 call("sv_transpose_cast_bf16", ptr(x_tm[t]), F, B, F, ptr(st.xT0) + 2 * t * Bp, T * Bp, s)
     inp = x_bf
-    L = len(layers)
-    wbf = []
-    for (w_ih, w_hh, b_ih, b_hh) in layers:
-        wih_bf, whh_bf = _bf(w_ih.shape, dev), _bf(w_hh.shape, dev)
-        call("sv_cast_bf16", ptr(w_ih), ptr(wih_bf), w_ih.numel(), s)
-        call("sv_cast_bf16", ptr(w_hh), ptr(whh_bf), w_hh.numel(), s)
-        wbf.append((wih_bf, whh_bf))
     gs = [_bf((T, B, 4 * H), dev) for _ in range(L)]  # bf16 x-projection in, bf16 activations out
     cs = [torch.empty((T, B, H), dtype=torch.float32, device=dev) for _ in range(L)]
     hs = [torch.empty((T + 1, B, H), dtype=torch.float32, device=dev) for _ in range(L)]
