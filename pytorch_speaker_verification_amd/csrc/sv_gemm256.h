@@ -514,6 +514,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
 // stage in two 64-row halves (8 KB per wave), after which k-tile 1's first fills go there.  The
 // stage of k-tile kt is (kt + base) & 1, base advancing by nk per tile.  Same MFMA order per tile
 // as gemm_bf16_8q_kernel (bit-identical results).
+// The bf16 C tile goes out with non-temporal stores (SV_G8P_NT, default on): with plain stores the
+// 128 KB per tile pushed the B panels out of the XCD's L2 (K1 at c3: 571 -> 550 us, A/B in
+// profiles/r04_v6_bf16_k1_order_ab.txt; non-temporal A fills measured slower, 569 us)
+#ifndef SV_G8P_NT
+#define SV_G8P_NT 1
+#endif
 __device__ __forceinline__ void g8_epilogue_bf16_half(g8_f32x4 (&acc)[8][4], int hlf, bf16_t* C, long ldc, int tm,
                                                       int tn, int wr, int wc, int lane, const float* bl, char* tile) {
   const int fr = lane & 15, fq = lane >> 4;
@@ -533,12 +539,25 @@ __device__ __forceinline__ void g8_epilogue_bf16_half(g8_f32x4 (&acc)[8][4], int
   for (int i = 0; i < 8; ++i) {
     const int row = 8 * i + (lane >> 3), c = lane & 7;
     const uint4 v = *reinterpret_cast<const uint4*>(tile + row * 128 + c * 16);
-    *reinterpret_cast<uint4*>(C + ((long)tm * G256_BM + wr * 128 + 64 * hlf + row) * ldc + tn * G256_BM + wc * 64 +
-                              8 * c) = v;
+    uint4* dst = reinterpret_cast<uint4*>(C + ((long)tm * G256_BM + wr * 128 + 64 * hlf + row) * ldc + tn * G256_BM +
+                                          wc * 64 + 8 * c);
+    if (SV_G8P_NT) {
+      typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_t*>(dst));
+    } else {
+      *dst = v;
+    }
   }
 }
 
 #define G8P_BIAS_LDS (32 * 1024)  // LDS bytes for the persistent kernel's bias sums (N <= 8192)
+// Tile order: column groups of SV_G8P_GROUP tiles (grouped_tile, 0: row-major).  K1 at c3 (12
+// column tiles): groups of 4 with non-temporal C stores 540-545 us and 0.66 GB of corrected FETCH
+// per launch against row-major 548-553 us / 0.89 GB (groups of 6: 538-551 us / 0.64 GB; 3: no
+// faster).  Without the non-temporal stores the grouping alone gained nothing (547 -> 574 us in r03)
+#ifndef SV_G8P_GROUP
+#define SV_G8P_GROUP 4
+#endif
 
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_8qp_kernel(const bf16_t* __restrict__ A, long lda,
@@ -574,9 +593,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qp_kernel(const bf16_t* __r
   }
   int base = 0;
   auto tile_of = [&](int vv, int& tm_, int& tn_) {
-    // (row-major tile order: the column-grouped order of the fp32 kernel measured slower here,
-    // K1 bf16 out 547 -> 574 us, fp32 out 658 -> 753 us)
     const int id = xcd_remap(vv, nwg);
+    if (SV_G8P_GROUP > 0) {
+      grouped_tile(id, M / G256_BM, tiles_n, SV_G8P_GROUP, tm_, tn_);
+      return;
+    }
     tn_ = id % tiles_n;
     tm_ = id / tiles_n;
   };
