@@ -23,7 +23,7 @@ FAMILIES = {  # json key -> kernel-name prefix
     # (r04 names: the K1 is the persistent 256p kernel, the dx GEMM reads the fragment-order A (AF = 1),
     # the dW GEMMs are split-K slabs (EPI = 1); the template's 4th argument is AF)
     "gemm_f32_256p_kernel<256,32>@K1.in_step": "void gemm_f32_256p_kernel<256, 32>",
-    "gemm_f32_256_kernel<256,32,0,1>@dx.in_step": "void gemm_f32_256_kernel<256, 32, 0, 1>",
+    "gemm_f32_256sk_kernel<256,1>@dx.in_step": "void gemm_f32_256sk_kernel<256, 1>",  # stream-K dx (r04)
     "gemm_f32_256_kernel<256,32,1,0>@dW.in_step": "void gemm_f32_256_kernel<256, 32, 1, 0>",
     "gemm_bf16_8qp_kernel<2>@K1.in_step": "void gemm_bf16_8qp_kernel<2>",
     "gemm_bf16_8q_kernel<0,1>@dx.in_step": "void gemm_bf16_8q_kernel<0, 1>",
@@ -100,6 +100,7 @@ def gemm_main(d, data):
 def main(d, gemm=False):
     out_path = os.path.join(ROOT, "bench_pmc_traffic.json")  # read by bench.py (profiles/ stays here)
     data = json.load(open(out_path)) if os.path.exists(out_path) else {}
+    data.pop("gemm_f32_256_kernel<256,32,0,1>@dx.in_step", None)  # the one-shot dx, replaced in-step by stream-K
     if gemm:
         gemm_main(d, data)
     for tag in () if gemm else ("f32", "bf16"):
@@ -112,7 +113,8 @@ def main(d, gemm=False):
             if k in write:
                 data[k] = {"FETCH_SIZE_KiB": round(fetch[k], 1), "WRITE_SIZE_KiB": round(write[k], 1),
                            "hbm_bytes_per_launch": int(1024 * (2 * fetch[k] + write[k])),
-                           "source": f"rocprofv3 --pmc over bench.py ({tag} step, in-step launches)"}
+                           "source": f"rocprofv3 --pmc over bench.py ({tag} step, in-step launches; "
+                                     f"{os.path.basename(os.path.normpath(os.path.join(d, '..')))})"}
     data["_note"] = ("rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE in separate runs; hbm_bytes = 2*FETCH_SIZE + "
                      "WRITE_SIZE (gfx950 halves wide reads, MI355X_MICROARCH.md §HBM); FETCH_SIZE counts L2 misses "
                      "incl. Infinity-Cache hits.  In-step entries: scripts/gpu_pmc_traffic.sh + scripts/pmc_traffic.py")
