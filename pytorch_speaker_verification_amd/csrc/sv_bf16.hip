@@ -103,36 +103,18 @@ __global__ void slab_reduce_bf_kernel(const float* __restrict__ slab, int nz, lo
   }
 }
 
-// x (fp32, n) -> y (bf16)
-__global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) y[i] = to_bf(x[i]);
-}
-
-// dst[c*ldd + r] = bf16(src[r*lds + c])
-__global__ __launch_bounds__(256) void transpose_cast_kernel(const float* __restrict__ src, long lds_, int R, int C,
-                                                             bf16_t* __restrict__ dst, long ldd) {
-  __shared__ float tile[32][33];
-  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int i = ty; i < 32; i += 8) {
-    const int r = r0 + i, c = c0 + tx;
-    tile[i][tx] = (r < R && c < C) ? src[(long)r * lds_ + c] : 0.f;
-  }
-  __syncthreads();
-  for (int i = ty; i < 32; i += 8) {
-    const int c = c0 + i, r = r0 + tx;
-    if (c < C && r < R) dst[(long)c * ldd + r] = to_bf(tile[tx][i]);
-  }
-}
-
 // up to 8 casts / transpose-casts in ONE launch (the per-step weight copies of the bf16 path: at
-// the c4 rank shape each of the 13 separate launches took ~5 us for ~1 us of traffic)
+// the c4 rank shape each of the 13 separate launches took ~5 us for ~1 us of traffic); the
+// single-matrix entry points (sv_cast_bf16, sv_transpose_cast_bf16) are batches of one
 struct CastBatch {
   const float* x[8];
   bf16_t* y[8];
   long start[9];  // element prefix sums
   int n;
 };
+// VEC: start[] counts groups of 4 elements (every count % 4 == 0, every pointer 16-B aligned):
+// one float4 load and one 8-B store per thread-iteration
+template <bool VEC>
 __global__ void cast_bf16_batch_kernel(const CastBatch cb) {
   const long total = cb.start[cb.n];
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -140,7 +122,12 @@ __global__ void cast_bf16_batch_kernel(const CastBatch cb) {
 #pragma unroll
     for (int k = 1; k < 8; ++k) b += (k < cb.n && i >= cb.start[k]) ? 1 : 0;
     const long j = i - cb.start[b];
-    cb.y[b][j] = to_bf(cb.x[b][j]);
+    if constexpr (VEC) {
+      const float4 v = reinterpret_cast<const float4*>(cb.x[b])[j];
+      reinterpret_cast<uint2*>(cb.y[b])[j] = pack_bf4(v.x, v.y, v.z, v.w);
+    } else {
+      cb.y[b][j] = to_bf(cb.x[b][j]);
+    }
   }
 }
 struct TCastBatch {
@@ -148,28 +135,60 @@ struct TCastBatch {
   bf16_t* dst[8];
   long lds[8], ldd[8];
   int R[8], C[8], tx[8];  // column tiles per matrix
-  int tile0[9];           // 32 x 32 tile prefix sums
+  int tile0[9];           // 64 x 64 tile prefix sums
   int n;
+  unsigned vec;           // bit b: matrix b takes the 16-B paths (lds % 4, ldd % 8, aligned bases)
 };
+// 64 x 64 tiles: float4 loads along a source row (16 threads per row, 16 rows per pass) and 16-B
+// bf16 stores along a destination row (8 threads per row, 32 rows per pass) where the matrix's
+// leading dimensions and base pointers allow (tb.vec bit b), element-wise at the edges
 __global__ __launch_bounds__(256) void transpose_cast_batch_kernel(const TCastBatch tb) {
-  __shared__ float tile[32][33];
+  __shared__ float tile[64][65];
   int b = 0;
 #pragma unroll
   for (int k = 1; k < 8; ++k) b += (k < tb.n && (int)blockIdx.x >= tb.tile0[k]) ? 1 : 0;
   const int t = blockIdx.x - tb.tile0[b];
   const int R = tb.R[b], C = tb.C[b];
-  const int c0 = (t % tb.tx[b]) * 32, r0 = (t / tb.tx[b]) * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c0 = (t % tb.tx[b]) * 64, r0 = (t / tb.tx[b]) * 64;
+  const bool vec = (tb.vec >> b) & 1;
   const float* src = tb.src[b];
-  for (int i = ty; i < 32; i += 8) {
-    const int r = r0 + i, c = c0 + tx;
-    tile[i][tx] = (r < R && c < C) ? src[(long)r * tb.lds[b] + c] : 0.f;
+  {
+    const int lc = (threadIdx.x & 15) * 4, lr = threadIdx.x >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + lr + 16 * i, c = c0 + lc;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (r < R) {
+        if (vec && c + 3 < C) {
+          const float4 q = *reinterpret_cast<const float4*>(src + (long)r * tb.lds[b] + c);
+          v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (c + e < C) v[e] = src[(long)r * tb.lds[b] + c + e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tile[lr + 16 * i][lc + e] = v[e];
+    }
   }
   __syncthreads();
   bf16_t* dst = tb.dst[b];
-  for (int i = ty; i < 32; i += 8) {
-    const int c = c0 + i, r = r0 + tx;
-    if (c < C && r < R) dst[(long)c * tb.ldd[b] + r] = to_bf(tile[tx][i]);
+  const int lr8 = (threadIdx.x & 7) * 8, lcr = threadIdx.x >> 3;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int cc = lcr + 32 * i, c = c0 + cc, r = r0 + lr8;
+    if (c >= C) continue;
+    bf16_t* d = dst + (long)c * tb.ldd[b] + r;
+    if (vec && r + 7 < R) {
+      const uint2 lo = pack_bf4(tile[lr8][cc], tile[lr8 + 1][cc], tile[lr8 + 2][cc], tile[lr8 + 3][cc]);
+      const uint2 hi = pack_bf4(tile[lr8 + 4][cc], tile[lr8 + 5][cc], tile[lr8 + 6][cc], tile[lr8 + 7][cc]);
+      *reinterpret_cast<uint4*>(d) = uint4{lo.x, lo.y, hi.x, hi.y};
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (r + e < R) d[e] = to_bf(tile[lr8 + e][cc]);
+    }
   }
 }
 
@@ -625,12 +644,11 @@ int gemm_bf16_afrag(int T, int B, int H, int N, const bf16_t* dgf, int bm, const
   return SV_OK;
 }
 
+extern "C" int sv_cast_bf16_batch(int n, const float* const* x, bf16_t* const* y, const long* count,
+                                  hipStream_t stream);
 extern "C" int sv_cast_bf16(const float* x, bf16_t* y, long n, hipStream_t stream) {
   if (!x || !y || n <= 0) return SV_EARG;
-  const int grid = (int)std::min<long>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid), dim3(256), 0, stream, x, y, n);
-  SV_LAUNCH_CHECK();
-  return SV_OK;
+  return sv_cast_bf16_batch(1, &x, &y, &n, stream);
 }
 
 extern "C" int sv_cast_bf16_batch(int n, const float* const* x, bf16_t* const* y, const long* count,
@@ -638,14 +656,19 @@ extern "C" int sv_cast_bf16_batch(int n, const float* const* x, bf16_t* const* y
   if (n <= 0 || n > 8 || !x || !y || !count) return SV_EARG;
   CastBatch cb{};
   cb.n = n;
+  bool vec = true;
   for (int i = 0; i < n; ++i) {
     if (!x[i] || !y[i] || count[i] <= 0) return SV_EARG;
     cb.x[i] = x[i];
     cb.y[i] = y[i];
-    cb.start[i + 1] = cb.start[i] + count[i];
+    vec = vec && count[i] % 4 == 0 && !((uintptr_t)x[i] & 15) && !((uintptr_t)y[i] & 7);
   }
+  for (int i = 0; i < n; ++i) cb.start[i + 1] = cb.start[i] + (vec ? count[i] / 4 : count[i]);
   const int grid = (int)std::min<long>((cb.start[n] + 255) / 256, 8192);
-  hipLaunchKernelGGL(cast_bf16_batch_kernel, dim3(grid), dim3(256), 0, stream, cb);
+  if (vec)
+    hipLaunchKernelGGL(cast_bf16_batch_kernel<true>, dim3(grid), dim3(256), 0, stream, cb);
+  else
+    hipLaunchKernelGGL(cast_bf16_batch_kernel<false>, dim3(grid), dim3(256), 0, stream, cb);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }
@@ -664,8 +687,9 @@ int transpose_cast_bf16_batch(int n, const float* const* src, const long* lds, c
     tb.ldd[i] = ldd[i];
     tb.R[i] = R[i];
     tb.C[i] = C[i];
-    tb.tx[i] = (C[i] + 31) / 32;
-    tb.tile0[i + 1] = tb.tile0[i] + tb.tx[i] * ((R[i] + 31) / 32);
+    tb.tx[i] = (C[i] + 63) / 64;
+    tb.tile0[i + 1] = tb.tile0[i] + tb.tx[i] * ((R[i] + 63) / 64);
+    if (lds[i] % 4 == 0 && ldd[i] % 8 == 0 && !((uintptr_t)src[i] & 15) && !((uintptr_t)dst[i] & 15)) tb.vec |= 1u << i;
   }
   hipLaunchKernelGGL(transpose_cast_batch_kernel, dim3(tb.tile0[n]), dim3(256), 0, stream, tb);
   SV_LAUNCH_CHECK();
@@ -675,10 +699,7 @@ int transpose_cast_bf16_batch(int n, const float* const* src, const long* lds, c
 extern "C" int sv_transpose_cast_bf16(const float* src, long ld_src, int R, int C, bf16_t* dst, long ld_dst,
                                       hipStream_t stream) {
   if (!src || !dst || R <= 0 || C <= 0) return SV_EARG;
-  hipLaunchKernelGGL(transpose_cast_kernel, dim3((C + 31) / 32, (R + 31) / 32), dim3(256), 0, stream, src, ld_src, R, C,
-                     dst, ld_dst);
-  SV_LAUNCH_CHECK();
-  return SV_OK;
+  return transpose_cast_bf16_batch(1, &src, &ld_src, &R, &C, &dst, &ld_dst, stream);
 }
 
 extern "C" int sv_lstm_layer_fwd_bf16(const bf16_t* x_bf, int T, int B, int F, int H, const bf16_t* w_ih_bf,

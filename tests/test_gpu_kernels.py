@@ -313,3 +313,44 @@ def test_dropin_calc_loss_per_embedding_gradient():
     loss, per = calc_loss(Sg)
     (loss + (per * wts.float().to(DEV)).sum()).backward()
     np.testing.assert_allclose(Sg.grad.cpu().numpy(), Sr.grad.numpy(), atol=2e-5)
+
+
+@pytest.mark.parametrize("counts,offset", [((4096, 123, 8, 1, 3072 * 40), 0),             # scalar path (odd counts)
+                                           ((640 * 160 * 40, 3072 * 40, 3072 * 768), 0),  # the bf16 forward's casts
+                                           ((3072 * 768, 4096), 1)])                      # misaligned base: scalar
+def test_cast_bf16_batch_is_rne(counts, offset):
+    """sv_cast_bf16_batch (and sv_cast_bf16, a batch of one) = torch's round-to-nearest-even bf16
+    cast, bit for bit, on the vectorised and the element-wise paths."""
+    import ctypes
+    from pytorch_speaker_verification_amd._lib import call, ptr
+    g = torch.Generator().manual_seed(sum(counts))
+    xs = [(torch.randn(n + offset, generator=g) * 3.0).to(DEV)[offset:] for n in counts]
+    xs[0][:4] = torch.tensor([float("inf"), -0.0, 1.2e-38, 3.3895314e38])  # inf, signed zero, near min, bf16 max
+    ys = [torch.empty(n, dtype=torch.bfloat16, device=DEV) for n in counts]
+    n = len(xs)
+    s = torch.cuda.current_stream().cuda_stream
+    call("sv_cast_bf16_batch", n, (ctypes.c_void_p * n)(*[ptr(t) for t in xs]),
+         (ctypes.c_void_p * n)(*[ptr(t) for t in ys]), (ctypes.c_long * n)(*[t.numel() for t in xs]), s)
+    one = torch.empty(counts[-1], dtype=torch.bfloat16, device=DEV)
+    call("sv_cast_bf16", ptr(xs[-1]), ptr(one), counts[-1], s)
+    torch.cuda.synchronize()
+    for x, y in zip(xs, ys):
+        assert torch.equal(y.view(torch.int16), x.bfloat16().view(torch.int16))
+    assert torch.equal(one.view(torch.int16), xs[-1].bfloat16().view(torch.int16))
+
+
+@pytest.mark.parametrize("R,C,lds,ldd", [(3072, 768, 768, 3072), (3072, 40, 40, 3072), (40, 102400, 102400, 40),
+                                         (100, 77, 80, 104), (3, 5, 5, 3)])
+def test_transpose_cast_bf16(R, C, lds, ldd):
+    """sv_transpose_cast_bf16 (the batched 64 x 64 tile kernel, one matrix): dst[c ldd + r] =
+    bf16(src[r lds + c]) bit for bit, full and edge tiles, the 16-B and the element-wise paths."""
+    from pytorch_speaker_verification_amd._lib import call, ptr
+    g = torch.Generator().manual_seed(R * 31 + C)
+    src = torch.randn(R, lds, generator=g).to(DEV)
+    dst = torch.full((C, ldd), -7.0, dtype=torch.bfloat16, device=DEV)
+    call("sv_transpose_cast_bf16", ptr(src), lds, R, C, ptr(dst), ldd, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = src[:, :C].t().bfloat16()
+    assert torch.equal(dst[:, :R].view(torch.int16), ref.view(torch.int16))
+    if ldd > R:  # padding columns untouched
+        assert bool((dst[:, R:].float() == -7.0).all())
