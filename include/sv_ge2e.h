@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SV_ABI_VERSION 7
+#define SV_ABI_VERSION 8
 int sv_abi_version(void);
 
 /* ---- fp32 product modes (`products` argument of sv_gemm_f32 / sv_lstm_stack_fwd / _bwd; every
@@ -361,6 +361,13 @@ int sv_dvector_embed_bf16(int B, int T, int F, int H, int L, const float* x, con
 size_t sv_clip_sgd_workspace(void);
 int sv_clip_sgd_step(float* params, float* grads, long n, float max_norm, float lr, int write_grad,
                      float* total_norm_out, const void* sync, float* workspace, hipStream_t stream);
+/* the reference's two parameter groups in one pair of launches (ABI v8): the network's
+ * (clip_grad_norm_(net, 3.0), train_speech_embedder.py:63) and the GE2E loss's {w, b}
+ * (clip_grad_norm_(ge2e, 1.0), :64), each exactly as sv_clip_sgd_step computes it (bit-identical);
+ * total_norm_out (may be NULL): float[2]; workspace: sv_clip_sgd_workspace() * 2 bytes */
+int sv_clip_sgd_step2(float* params0, float* grads0, long n0, float max_norm0, float* params1, float* grads1,
+                      long n1, float max_norm1, float lr, int write_grad, float* total_norm_out, const void* sync,
+                      float* workspace, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libsv_ge2e.so")
 # the fault-injection test build (Makefile `faultinj`): the same library plus sv_test_set_fault;
 # only tests load it, through use_library() before the first call
 FAULT_LIB_PATH = os.path.join(_HERE, "libsv_ge2e_faultinj.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 SV_DTYPE_F32, SV_DTYPE_BF16 = 0, 1  # include/sv_ge2e.h
 
 # schedule flags of the bf16 stack (include/sv_ge2e.h SV_SCHED_*), by name
@@ -122,6 +122,8 @@ SIGNATURES = {
                                        _P, _P]),
     "sv_clip_sgd_workspace": (_c_size_t, []),
     "sv_clip_sgd_step": (_c_int, [_P, _P, _c_long, _c_float, _c_float, _c_int, _P, _P, _P, _P]),
+    "sv_clip_sgd_step2": (_c_int, [_P, _P, _c_long, _c_float, _P, _P, _c_long, _c_float, _c_float, _c_int, _P, _P, _P,
+                                   _P]),
 }
 
 ERRORS = {-1: "invalid argument (SV_EARG)", -2: "misaligned pointer/leading dim (SV_EALIGN)",

@@ -72,33 +72,52 @@ extern "C" int sv_proj_norm_bwd(const float* demb, const float* emb, const float
 // fused clip_grad_norm_(max_norm) + SGD(lr) over one flat parameter group.
 // pass 1: per-block partial sums of squares (fixed grid, fixed order)
 #define CLIP_BLOCKS 512
-__global__ __launch_bounds__(256) void sqsum_partial_kernel(const float* __restrict__ g, long n,
-                                                            float* __restrict__ partial) {
+// One group = one parameter group of the reference; the two-group launches (sv_clip_sgd_step2)
+// give group 1 the blocks after group 0's, each group's blocks doing exactly what they do alone.
+struct ClipGroup {
+  float* p;
+  float* g;
+  long n;
+  float max_norm;
+  int blocks;   // this group's grid (the single-group formula of sv_clip_sgd_step)
+  int first;    // its first block in the launch
+};
+__device__ __forceinline__ void sqsum_partial_body(const float* __restrict__ g, long n, int bid, int nb,
+                                                   float* __restrict__ partial) {
   __shared__ float red[4];
   float s = 0.f;
   const long n4 = n / 4;
   const f32x4* g4 = reinterpret_cast<const f32x4*>(g);
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+  for (long i = bid * 256L + threadIdx.x; i < n4; i += (long)nb * 256) {
     const f32x4 v = g4[i];
     s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
   }
-  for (long i = n4 * 4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) s += g[i] * g[i];
+  for (long i = n4 * 4 + bid * 256L + threadIdx.x; i < n; i += (long)nb * 256) s += g[i] * g[i];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (threadIdx.x == 0) partial[bid] = red[0] + red[1] + red[2] + red[3];
+}
+__global__ __launch_bounds__(256) void sqsum_partial_kernel(const float* __restrict__ g, long n,
+                                                            float* __restrict__ partial) {
+  sqsum_partial_body(g, n, blockIdx.x, gridDim.x, partial);
+}
+__global__ __launch_bounds__(256) void sqsum_partial2_kernel(ClipGroup g0, ClipGroup g1, float* __restrict__ partial) {
+  const bool one = (int)blockIdx.x >= g1.first;
+  const ClipGroup& c = one ? g1 : g0;
+  sqsum_partial_body(c.g, c.n, blockIdx.x - c.first, c.blocks, partial + (one ? CLIP_BLOCKS : 0));
 }
 
 // pass 2: every block re-reduces the partials (fixed order, fp64), computes
 // coef = min(1, max_norm / (|g| + 1e-6)) and updates p -= lr * coef * g (optionally g *= coef).
 // status (optional, a persistent-recurrence sync block's status word): nonzero -> the gradients
 // came from a timed-out recurrence: no update at all (parameters and gradients untouched).
-__global__ __launch_bounds__(256) void clip_sgd_kernel(float* __restrict__ p, float* __restrict__ g, long n,
-                                                       const float* __restrict__ partial, int npart, float max_norm,
-                                                       float lr, int write_grad, float* __restrict__ norm_out,
-                                                       const unsigned* __restrict__ status) {
+__device__ __forceinline__ void clip_sgd_body(float* __restrict__ p, float* __restrict__ g, long n, int bid, int nb,
+                                              const float* __restrict__ partial, int npart, float max_norm, float lr,
+                                              int write_grad, float* __restrict__ norm_out,
+                                              const unsigned* __restrict__ status) {
   if (status && *status) {
-    if (norm_out && blockIdx.x == 0 && threadIdx.x == 0) norm_out[0] = __builtin_nanf("");
+    if (norm_out && bid == 0 && threadIdx.x == 0) norm_out[0] = __builtin_nanf("");
     return;
   }
   __shared__ double redd[4];
@@ -112,7 +131,7 @@ __global__ __launch_bounds__(256) void clip_sgd_kernel(float* __restrict__ p, fl
     const float total = (float)sqrt(redd[0] + redd[1] + redd[2] + redd[3]);
     const float c = max_norm / (total + 1e-6f);
     coef_s = c < 1.0f ? c : 1.0f;
-    if (norm_out && blockIdx.x == 0) norm_out[0] = total;
+    if (norm_out && bid == 0) norm_out[0] = total;
   }
   __syncthreads();
   const float k = coef_s;
@@ -120,16 +139,30 @@ __global__ __launch_bounds__(256) void clip_sgd_kernel(float* __restrict__ p, fl
   const long n4 = n / 4;
   f32x4* p4 = reinterpret_cast<f32x4*>(p);
   f32x4* g4 = reinterpret_cast<f32x4*>(g);
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+  for (long i = bid * 256L + threadIdx.x; i < n4; i += (long)nb * 256) {
     const f32x4 gv = g4[i];
     p4[i] = p4[i] - step * gv;
     if (write_grad) g4[i] = gv * k;
   }
-  for (long i = n4 * 4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+  for (long i = n4 * 4 + bid * 256L + threadIdx.x; i < n; i += (long)nb * 256) {
     const float gv = g[i];
     p[i] -= step * gv;
     if (write_grad) g[i] = gv * k;
   }
+}
+__global__ __launch_bounds__(256) void clip_sgd_kernel(float* __restrict__ p, float* __restrict__ g, long n,
+                                                       const float* __restrict__ partial, int npart, float max_norm,
+                                                       float lr, int write_grad, float* __restrict__ norm_out,
+                                                       const unsigned* __restrict__ status) {
+  clip_sgd_body(p, g, n, blockIdx.x, gridDim.x, partial, npart, max_norm, lr, write_grad, norm_out, status);
+}
+__global__ __launch_bounds__(256) void clip_sgd2_kernel(ClipGroup g0, ClipGroup g1, const float* __restrict__ partial,
+                                                        float lr, int write_grad, float* __restrict__ norm_out,
+                                                        const unsigned* __restrict__ status) {
+  const bool one = (int)blockIdx.x >= g1.first;
+  const ClipGroup& c = one ? g1 : g0;
+  clip_sgd_body(c.p, c.g, c.n, blockIdx.x - c.first, c.blocks, partial + (one ? CLIP_BLOCKS : 0), c.blocks,
+                c.max_norm, lr, write_grad, norm_out ? norm_out + (one ? 1 : 0) : nullptr, status);
 }
 
 extern "C" size_t sv_clip_sgd_workspace(void) { return CLIP_BLOCKS * sizeof(float); }
@@ -143,6 +176,23 @@ extern "C" int sv_clip_sgd_step(float* params, float* grads, long n, float max_n
   SV_LAUNCH_CHECK();
   hipLaunchKernelGGL(clip_sgd_kernel, dim3(blocks), dim3(256), 0, stream, params, grads, n, workspace, blocks, max_norm,
                      lr, write_grad, total_norm_out, reinterpret_cast<const unsigned*>(sync));
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+extern "C" int sv_clip_sgd_step2(float* params0, float* grads0, long n0, float max_norm0, float* params1,
+                                 float* grads1, long n1, float max_norm1, float lr, int write_grad,
+                                 float* total_norm_out, const void* sync, float* workspace, hipStream_t stream) {
+  if (!params0 || !grads0 || !params1 || !grads1 || !workspace || n0 <= 0 || n1 <= 0) return SV_EARG;
+  if (((uintptr_t)params0 | (uintptr_t)grads0 | (uintptr_t)params1 | (uintptr_t)grads1) & 15) return SV_EALIGN;
+  ClipGroup g0{params0, grads0, n0, max_norm0, (int)std::min<long>(CLIP_BLOCKS, (n0 / 4 + 255) / 256 + 1), 0};
+  ClipGroup g1{params1, grads1, n1, max_norm1, (int)std::min<long>(CLIP_BLOCKS, (n1 / 4 + 255) / 256 + 1), 0};
+  g1.first = g0.blocks;
+  const int blocks = g0.blocks + g1.blocks;
+  hipLaunchKernelGGL(sqsum_partial2_kernel, dim3(blocks), dim3(256), 0, stream, g0, g1, workspace);
+  SV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(clip_sgd2_kernel, dim3(blocks), dim3(256), 0, stream, g0, g1, workspace, lr, write_grad,
+                     total_norm_out, reinterpret_cast<const unsigned*>(sync));
   SV_LAUNCH_CHECK();
   return SV_OK;
 }

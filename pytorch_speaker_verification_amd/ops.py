@@ -8,6 +8,7 @@ plumbing; every FLOP of the path runs in the HIP kernels of libsv_ge2e.so.
   ge2e_forward / ge2e_backward           GE2ELoss.forward (speech_embedder_net.py:43-49)
   EmbedderFunction, GE2EFunction         autograd.Function glue (loss.backward() works)
   clip_sgd_step_                         clip_grad_norm_ + SGD.step (train_speech_embedder.py:63-65)
+  clip_sgd_step2_                        the same over both parameter groups in one launch pair
 """
 from __future__ import annotations
 
@@ -667,6 +668,16 @@ def clip_sgd_step_(flat_params, flat_grads, max_norm, lr, write_grad=False, norm
     call("sv_clip_sgd_step", ptr(flat_params), ptr(flat_grads), flat_params.numel(), float(max_norm), float(lr),
          int(write_grad), ptr(norm_out), status.ptr() if status is not None else None, ptr(ws),
          stream_of(flat_params))
+
+
+def clip_sgd_step2_(p0, g0, max_norm0, p1, g1, max_norm1, lr, write_grad=False, norm_out=None, status=None):
+    """clip_sgd_step_ over two flat parameter groups (the network's and the loss's {w, b},
+    train_speech_embedder.py:63-65) in one pair of launches; bit-identical to two calls."""
+    require_device(p0, g0, p1, g1)
+    ws = _ws(2 * lib().sv_clip_sgd_workspace(), p0.device)
+    call("sv_clip_sgd_step2", ptr(p0), ptr(g0), p0.numel(), float(max_norm0), ptr(p1), ptr(g1), p1.numel(),
+         float(max_norm1), float(lr), int(write_grad), ptr(norm_out), status.ptr() if status is not None else None,
+         ptr(ws), stream_of(p0))
 
 
 def gemm_f32(A, B, a_kcontig=True, b_kcontig=True, bias=None, products="mfma_f32"):

@@ -42,7 +42,7 @@ import torch
 import torch.distributed as dist
 
 from ._lib import PersistStatus, call, ptr, stream_of
-from .ops import (clip_sgd_step_, embedder_backward, embedder_backward_bf16, embedder_forward,
+from .ops import (clip_sgd_step2_, embedder_backward, embedder_backward_bf16, embedder_forward,
                   embedder_forward_bf16)
 from .sharded_ge2e import ShardedGE2E
 
@@ -247,9 +247,9 @@ class GE2ETrainer:
             # any rank's timeout -> this rank's status too: every rank skips the update
             call("sv_status_merge", self.status.ptr(), ptr(self.flags), stream_of(self.flags))
         n = self.n_pad
-        clip_sgd_step_(self.flat_p[:n], self.flat_g[:n], self.clip_net, self.lr, self.write_grads, status=self.status)
-        clip_sgd_step_(self.flat_p[n:n + 4], self.flat_g[n:n + 4], self.clip_wb, self.lr, self.write_grads,
-                       status=self.status)
+        # clip_grad_norm_ x2 + SGD (train_speech_embedder.py:63-65): both groups in one launch pair
+        clip_sgd_step2_(self.flat_p[:n], self.flat_g[:n], self.clip_net, self.flat_p[n:n + 4], self.flat_g[n:n + 4],
+                        self.clip_wb, self.lr, self.write_grads, status=self.status)
         loss = loss.clone() if dp else loss  # (not a view of flat_g, which the next step reuses)
         call("sv_status_poison", self.status.ptr(), ptr(loss), 1, stream_of(loss))
         self.status.arm()

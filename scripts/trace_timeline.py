@@ -13,13 +13,19 @@ def short(name):
     return n.replace("void ", "")
 
 
+def step_ends(ks):
+    """End of each training step: its clip_sgd2_kernel (both parameter groups in one launch, ABI
+    v8), or the second clip_sgd_kernel of each step (net group, then w/b group) in older traces."""
+    two = [k[1] for k in ks if k[2].startswith("clip_sgd2")]
+    return two if two else [k[1] for k in ks if k[2].startswith("clip_sgd")][1::2]
+
+
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     which = int(sys.argv[2]) if len(sys.argv) > 2 else -1
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), r["Queue_Id"])
                  for r in rows), key=lambda x: x[0])
-    # step ends: the second clip_sgd of each step (two per step: net group, w/b group)
-    ends = [k[1] for k in ks if k[2].startswith("clip_sgd")][1::2]
+    ends = step_ends(ks)
     starts = [ks[0][0]] + ends[:-1]
     s0, s1 = starts[which], ends[which]
     sel = [k for k in ks if k[0] >= s0 and k[1] <= s1]
@@ -50,7 +56,7 @@ if __name__ == "__main__":
 def phases(path, which=-1):
     rows = list(csv.DictReader(open(path)))
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in rows))
-    ends = [k[1] for k in ks if k[2].startswith("clip_sgd")][1::2]
+    ends = step_ends(ks)
     starts = [ks[0][0]] + ends[:-1]
     s0, s1 = starts[which], ends[which]
     sel = [k for k in ks if k[0] >= s0 and k[1] <= s1]

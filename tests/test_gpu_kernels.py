@@ -150,6 +150,37 @@ def test_clip_sgd_matches_torch():
         assert abs(float(out) - float(norm)) <= 1e-5 * float(norm)
 
 
+@pytest.mark.parametrize("write_grad", [False, True])
+@pytest.mark.parametrize("n0,n1", [(12134656, 4), (1003, 2), (4096, 8192)])
+def test_clip_sgd_step2_is_two_steps(n0, n1, write_grad):
+    """sv_clip_sgd_step2 (both groups in one launch pair, what the trainer runs) = two
+    sv_clip_sgd_step calls, bit for bit: parameters, gradients and both norms; and the status word
+    skips both groups."""
+    from pytorch_speaker_verification_amd._lib import PersistStatus
+    from pytorch_speaker_verification_amd.ops import clip_sgd_step2_, clip_sgd_step_
+    g = torch.Generator().manual_seed(n0 + n1)
+    p0, g0 = torch.randn(n0, generator=g).to(DEV), (torch.randn(n0, generator=g) * 0.1).to(DEV)
+    p1, g1 = torch.randn(n1, generator=g).to(DEV), (torch.randn(n1, generator=g) * 3.0).to(DEV)
+    a = [t.clone() for t in (p0, g0, p1, g1)]
+    na, nb = torch.zeros(2, device=DEV), torch.zeros(2, device=DEV)
+    clip_sgd_step_(a[0], a[1], 3.0, 0.01, write_grad=write_grad, norm_out=na[0:1])
+    clip_sgd_step_(a[2], a[3], 1.0, 0.01, write_grad=write_grad, norm_out=na[1:2])
+    b = [t.clone() for t in (p0, g0, p1, g1)]
+    clip_sgd_step2_(b[0], b[1], 3.0, b[2], b[3], 1.0, 0.01, write_grad=write_grad, norm_out=nb)
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert torch.equal(na, nb)
+    st = PersistStatus(torch.device(DEV))
+    st.block[0] = 1  # a timed-out recurrence: nothing may change
+    c = [t.clone() for t in (p0, g0, p1, g1)]
+    clip_sgd_step2_(c[0], c[1], 3.0, c[2], c[3], 1.0, 0.01, write_grad=True, norm_out=nb, status=st)
+    torch.cuda.synchronize()
+    for x, y in zip(c, (p0, g0, p1, g1)):
+        assert torch.equal(x, y)
+    assert bool(torch.isnan(nb).all())
+
+
 @pytest.mark.parametrize("M,N,K", [(640, 256, 768), (100, 36, 1024), (3000, 3072, 40)])
 def test_gemm_f32_bias_and_split_k(M, N, K):
     """Bias epilogue on both the direct and the split-K (slab reduce) paths."""
