@@ -825,6 +825,22 @@ __global__ void persist_db_finalize_kernel(const float* __restrict__ dbp, int nr
   if (db_hh) db_hh[c] = s;
 }
 
+// the same for up to 4 layers in one launch (grid y = layer): the layer wavefront's biases
+struct DbMulti {
+  const float* dbp[4];
+  float* db_ih[4];
+  float* db_hh[4];
+};
+__global__ void persist_db_finalize_multi_kernel(const DbMulti m, int nrb, int G) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x, l = blockIdx.y;
+  if (c >= G) return;
+  const float* dbp = m.dbp[l];
+  float s = 0.f;
+  for (int r = 0; r < nrb; ++r) s += dbp[(long)r * G + c];
+  m.db_ih[l][c] = s;
+  if (m.db_hh[l]) m.db_hh[l][c] = s;
+}
+
 int sv_persist_db_finalize(const float* dbp, int nrb, int G, float* db_ih, float* db_hh, hipStream_t stream) {
   if (!dbp || !db_ih || nrb <= 0 || G <= 0) return SV_EARG;
   hipLaunchKernelGGL(persist_db_finalize_kernel, dim3((G + 255) / 256), dim3(256), 0, stream, dbp, nrb, G, db_ih, db_hh);
@@ -1213,9 +1229,15 @@ int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, cons
   const int rc = sv_wave_bwd_launch(a, stream);
   if (rc) return rc;
   if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
-  for (int l = 0; l < L && db_ih; ++l) {
-    hipLaunchKernelGGL(persist_db_finalize_kernel, dim3((4 * H + 255) / 256), dim3(256), 0, stream, a.dbp[l], a.nrb,
-                       4 * H, db_ih[l], db_hh ? db_hh[l] : nullptr);
+  if (db_ih) {  // every layer's bias gradients in one launch
+    DbMulti m{};
+    for (int l = 0; l < L; ++l) {
+      m.dbp[l] = a.dbp[l];
+      m.db_ih[l] = db_ih[l];
+      m.db_hh[l] = db_hh ? db_hh[l] : nullptr;
+    }
+    hipLaunchKernelGGL(persist_db_finalize_multi_kernel, dim3((4 * H + 255) / 256, L), dim3(256), 0, stream, m, a.nrb,
+                       4 * H);
     SV_LAUNCH_CHECK();
   }
   return SV_OK;

@@ -616,10 +616,11 @@ def ge2e_backward(st, w, b, gloss=None):
     return dE, dwdb[0], dwdb[1]
 
 
-def ge2e_train(E, w, b):
+def ge2e_train(E, w, b, dwdb_out=None):
     """Fused GE2E forward + closed-form backward for one GPU holding all N speakers (the training
     step's gloss = 1): returns (loss 0-dim, per [N,M], dE [N,M,D], dwdb [2]) from three launches
-    (include/sv_ge2e.h, sv_ge2e_train).  Shapes outside sv_ge2e_train_ok take the split path."""
+    (include/sv_ge2e.h, sv_ge2e_train); dwdb_out (2 contiguous fp32 on the device): written in
+    place of a new dwdb tensor.  Shapes outside sv_ge2e_train_ok take the split path."""
     require_device(E, w, b)
     Ep, D0 = _pad_d(E)
     N, M, D = Ep.shape
@@ -634,7 +635,9 @@ def ge2e_train(E, w, b):
     loss = torch.empty((), dtype=torch.float32, device=dev)
     per = torch.empty((N, M), dtype=torch.float32, device=dev)
     dE = torch.empty((N, M, D), dtype=torch.float32, device=dev)
-    dwdb = torch.empty((2,), dtype=torch.float32, device=dev)
+    dwdb = torch.empty((2,), dtype=torch.float32, device=dev) if dwdb_out is None else dwdb_out
+    if dwdb.numel() != 2 or dwdb.dtype != torch.float32 or not dwdb.is_contiguous() or dwdb.device != dev:
+        raise ValueError("ge2e_train: dwdb_out must be 2 contiguous fp32 values on the embeddings' device")
     call("sv_ge2e_train", ptr(Ep), N, M, D, ptr(w.contiguous()), ptr(b.contiguous()), ptr(loss), ptr(per), ptr(dE),
          ptr(dwdb), ptr(ws), stream_of(Ep))
     if D0 != D:

@@ -140,15 +140,16 @@ class ShardedGE2E:
             dist.all_reduce(loss, group=self.group)
         return loss, per, st
 
-    def train(self, E_local, w, b, reduce_loss=True):
+    def train(self, E_local, w, b, reduce_loss=True, dwdb_out=None):
         """Forward + backward for the training step (gloss = 1): (loss, dE_local, dwdb_partial[2]);
         the loss is the global sum when reduce_loss, else this shard's partial (the trainer sums
         the partials inside its gradient all-reduce instead of a collective of its own).  One rank
-        holding every speaker uses the fused 3-launch kernel (ops.ge2e_train); sharded runs take
-        the exchange protocol above."""
+        holding every speaker uses the fused 3-launch kernel (ops.ge2e_train), which writes dwdb
+        straight into ``dwdb_out`` when given (the trainer's gradient slot); sharded runs take the
+        exchange protocol above."""
         if self.world == 1 and isinstance(self.k, HipShardKernels):
             from .ops import ge2e_train
-            loss, _, dE, dwdb = ge2e_train(E_local, w, b)
+            loss, _, dE, dwdb = ge2e_train(E_local, w, b, dwdb_out=dwdb_out)
             return loss, dE, dwdb
         Nl, M, D = E_local.shape
         N = Nl * self.world

@@ -188,8 +188,10 @@ class GE2ETrainer:
         E = emb.view(N, M, emb.shape[1])
         dp = self.ge2e.world > 1
         # data parallel: the local loss partial goes to the head bucket's all-reduce (no collective)
-        loss, dE, dwdb = self.ge2e.train(E, w, b, reduce_loss=not dp)
-        self.flat_g[self.n_pad:self.n_pad + 2].copy_(dwdb)
+        gslot = self.flat_g[self.n_pad:self.n_pad + 2]  # dL/dw, dL/db
+        loss, dE, dwdb = self.ge2e.train(E, w, b, reduce_loss=not dp, dwdb_out=gslot)
+        if dwdb.data_ptr() != gslot.data_ptr():  # (the split / sharded paths return their own)
+            gslot.copy_(dwdb)
         works = []
         ready = None
         if dp:
