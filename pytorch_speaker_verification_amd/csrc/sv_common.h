@@ -19,9 +19,11 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
 // fp32 GEMM of the C ABI's sv_gemm_f32 (include/sv_ge2e.h) under the calling thread's current
 // product mode; F32ProductScope sets that mode for one entry point's duration
+// fine: split K in chunks down to 128 when the tiles leave most of the chip idle (the projection's
+// GEMMs; their workspace comes from sv_gemm_f32_workspace, which covers both plans)
 int gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
              float* C, long ldc, const float* bias0, const float* bias1, float beta, float* workspace,
-             hipStream_t stream);
+             hipStream_t stream, bool fine = false);
 struct F32ProductScope {
   int prev;
   explicit F32ProductScope(int mode);

@@ -533,7 +533,7 @@ struct GemmPlan {
 // traffic of the split (sk x M x N x 4 B written and read back), over sk <= 32 with K chunks of
 // at least 512.  At the dW shape (144 tiles, K = 102400) this picks 32 splits = 9 full rounds of
 // 512 blocks (the old 512/144 = 3 left 80 CUs with one block and the rest with two).
-GemmPlan plan_gemm(int M, int N, int K) {
+GemmPlan plan_gemm(int M, int N, int K, bool fine = false) {
   GemmPlan p;
   const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
   const bool small = t128 < 128;
@@ -545,7 +545,10 @@ GemmPlan plan_gemm(int M, int N, int K) {
   if (tiles < slots) {
     // per-block rate at ~120 TF/s shared by all resident blocks; HBM ~5 TB/s for the slabs
     const double rate = 120e12 / (double)slots, hbm = 5e12;
-    const int kmax = std::max(1, std::min(32, K / 512));
+    // K chunks of at least 512, or with `fine` 128 when the tiles alone would leave most of the
+    // chip idle (the projection GEMMs: 8-48 tiles of 64 x 64 over K = 256-768 ran 12-24 us on 8-48
+    // CUs)
+    const int kmax = std::max(1, std::min(32, K / (fine && tiles * 8 < slots ? 128 : 512)));
     double best = 1e30;
     for (int c = 1; c <= kmax; ++c) {
       const long rounds = (tiles * c + slots - 1) / slots;
@@ -688,8 +691,9 @@ F32ProductScope::~F32ProductScope() { t_f32_mode = prev; }
 
 extern "C" size_t sv_gemm_f32_workspace(int M, int N, int K) {
   // the larger of the two kernels' split-K slabs (which one runs depends on pointers and mode)
-  const GemmPlan p = plan_gemm(M, N, K);
+  const GemmPlan p = plan_gemm(M, N, K), pf = plan_gemm(M, N, K, true);  // both plans (gemm_f32's `fine`)
   size_t ws = p.splitk > 1 ? (size_t)p.splitk * M * N * sizeof(float) : 0;
+  if (pf.splitk > 1) ws = std::max(ws, (size_t)pf.splitk * M * N * sizeof(float));
   if (M % GF_BM == 0 && N % 128 == 0 && K % GF_BK == 0) {
     const GemmPlan q = plan_gf256(M, N, K);
     if (q.splitk > 1) ws = std::max(ws, (size_t)q.splitk * M * N * sizeof(float));
@@ -707,14 +711,14 @@ extern "C" int sv_gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, co
 
 int gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
              float* C, long ldc, const float* bias0, const float* bias1, float beta, float* workspace,
-             hipStream_t stream) {
+             hipStream_t stream, bool fine) {
   if (M <= 0 || N <= 0 || K <= 0 || !A || !B || !C) return SV_EARG;
   if (a_kcontig ? (K % 4 || lda % 4) : (M % 4 || lda % 4)) return SV_EALIGN;
   if (b_kcontig ? (K % 4 || ldb % 4) : (N % 4 || ldb % 4)) return SV_EALIGN;
   if (((uintptr_t)A | (uintptr_t)B) & 15) return SV_EALIGN;
   if (a_kcontig && b_kcontig && gemm_x() == 0 && gf256_ok(M, N, K, C, ldc, bias0, bias1))
     return gemm_f32_256(A, lda, B, ldb, C, ldc, M, N, K, bias0, bias1, beta, workspace, stream);
-  const GemmPlan p = plan_gemm(M, N, K);
+  const GemmPlan p = plan_gemm(M, N, K, fine && workspace != nullptr);
   const bool ak = a_kcontig != 0, bk = b_kcontig != 0;
   if (p.splitk == 1) {
     if (p.bm == 64)

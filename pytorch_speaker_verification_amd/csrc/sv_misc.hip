@@ -44,7 +44,7 @@ extern "C" size_t sv_proj_norm_workspace(int B, int H, int P) {
 extern "C" int sv_proj_norm_fwd(const float* h_last, int B, int H, int P, const float* w_p, const float* b_p, float* y,
                                 float* emb, float* ynorm, float* workspace, hipStream_t stream) {
   if (!h_last || !w_p || !y || !emb || !ynorm || B <= 0 || H <= 0 || P <= 0) return SV_EARG;
-  int rc = gemm_f32(1, 1, B, P, H, h_last, H, w_p, H, y, P, b_p, nullptr, 0.f, workspace, stream);
+  int rc = gemm_f32(1, 1, B, P, H, h_last, H, w_p, H, y, P, b_p, nullptr, 0.f, workspace, stream, true);
   if (rc) return rc;
   hipLaunchKernelGGL(rownorm_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, y, B, P, emb, ynorm);
   SV_LAUNCH_CHECK();
@@ -60,12 +60,12 @@ extern "C" int sv_proj_norm_bwd(const float* demb, const float* emb, const float
   hipLaunchKernelGGL(rownorm_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, demb, emb, ynorm, B, P, dy);
   SV_LAUNCH_CHECK();
   // dWp [P,H] = dy^T h_last  (A = dy as [K=B][M=P], B = h_last as [K=B][N=H])
-  int rc = gemm_f32(0, 0, P, H, B, dy, P, h_last, H, dw_p, H, nullptr, nullptr, 0.f, gws, stream);
+  int rc = gemm_f32(0, 0, P, H, B, dy, P, h_last, H, dw_p, H, nullptr, nullptr, 0.f, gws, stream, true);
   if (rc) return rc;
   rc = sv_colsum(dy, B, P, db_p, gws, stream);
   if (rc) return rc;
   // dh_last [B,H] = dy Wp  (A = dy [B, K=P] k-contig, B = Wp as [K=P][N=H])
-  return gemm_f32(1, 0, B, H, P, dy, P, w_p, H, dh_last, H, nullptr, nullptr, 0.f, gws, stream);
+  return gemm_f32(1, 0, B, H, P, dy, P, w_p, H, dh_last, H, nullptr, nullptr, 0.f, gws, stream, true);
 }
 
 // ---------------------------------------------------------------------------
