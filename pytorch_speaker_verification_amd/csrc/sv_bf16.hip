@@ -4,6 +4,7 @@
 // GE2E loss and the optimizer stay fp32.  Same algorithm, layouts and epilogues
 // as sv_lstm.hip; transposed layouts use column blocks of Bp = B rounded up to 8 so every
 // bf16 row stays 16-byte aligned.
+#include <vector>
 #include <algorithm>
 #include "sv_common.h"
 #include "sv_gemm.h"
@@ -1023,14 +1024,13 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     // beside the next layer's recurrence 16.8 vs 16.6 ms at c3 -- the GEMM workgroups contend
     // with the co-resident recurrence)
     {  // every layer's W_hh^T / W_ih^T (bf16) in one launch
-      const bf16_t* whhT_l[8];
-      const bf16_t* wihT_l[8];
-      for (int l = 0; l < L && l < 8; ++l) {
+      std::vector<const bf16_t*> whhT_l(L), wihT_l(L);  // any L (wbf_transposes batches 8 at a time)
+      for (int l = 0; l < L; ++l) {
         const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
         whhT_l[l] = ws.whhT;
         wihT_l[l] = l > 0 ? ws.wihT : nullptr;
       }
-      if (int rc = wbf_transposes(L, F, H, w_ih, w_hh, whhT_l, wihT_l, main)) return rc;
+      if (int rc = wbf_transposes(L, F, H, w_ih, w_hh, whhT_l.data(), wihT_l.data(), main)) return rc;
     }
     for (int l = L - 1; l >= 0; --l) {
       const int Fl = l == 0 ? F : H;

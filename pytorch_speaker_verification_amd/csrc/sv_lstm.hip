@@ -1012,7 +1012,11 @@ extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float*
         return (int)e;
       // layer 0 at F = 40: the input projection inside the recurrence (SV_PF32_FUSE_X0; c2 layer 0:
       // the K=40 GEMM wrote 1.26 GB that the recurrence read back)
-      const bool fuse = SV_PF32_FUSE_X0 && l == 0 && F == 40;
+      // (exact fp32 products only: the bf16x6 mode keeps the GEMM, whose products it splits; and 16-B
+      // aligned x_tm / W_ih only: the kernel reads them by LDS-DMA / f32x4 -- else the GEMM path
+      // rejects the misaligned pointer with SV_EALIGN)
+      const bool fuse = SV_PF32_FUSE_X0 && l == 0 && F == 40 && products == 0 &&
+                        !(((uintptr_t)x_tm | (uintptr_t)w_ih[0]) & 15);
       int rc = 0;
       if (!fuse) {
         rc = gemm_f32(1, 1, T * B, 4 * H, Fl, in, Fl, w_ih[l], Fl, gates[l], 4L * H, b_ih[l], b_hh[l], 0.f, nullptr,

@@ -520,6 +520,9 @@ class EmbedderFunction(torch.autograd.Function):
         L = num_layers
         layers = [tuple(params[4 * l:4 * l + 4]) for l in range(L)]
         w_p, b_p = params[4 * L], params[4 * L + 1]
+        # earlier calls' completed checks: raise on a timeout there, drop the finished entries (so
+        # a forward-only loop keeps _UNCHECKED bounded)
+        check_persistent_status()
         ctx.status = PersistStatus(x.device)
         if precision == "bf16":
             emb, st = embedder_forward_bf16(x.contiguous(), layers, w_p, b_p, save=True, status=ctx.status,

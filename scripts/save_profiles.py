@@ -9,6 +9,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if len(sys.argv) < 2 or sys.argv[1].startswith("-"):
+    sys.exit(__doc__)
 tag = sys.argv[1]
 ck = os.path.join(ROOT, "gpurun_out", sys.argv[2] if len(sys.argv) > 2 else "ckpt")
 prof = os.path.join(ROOT, "profiles")

@@ -17,6 +17,8 @@ What is recorded (inputs + expected outputs; no reference source is copied):
   net_small.npz       -- full training step (fwd, GE2E, bwd, clip 3.0/1.0, SGD) of the
                          reference SpeechEmbedder at small dims, 3 steps.
   net_full_c1.npz     -- one step at the full dims (40->768x3->256), N=4 x M=5, T=160.
+  net_full_c2.npz     -- one step at the headline config c2 (N=64 x M=10, T=160, full dims).
+  net_fwd_c5.npz      -- forward + loss at c5's global batch (N=256 x M=10, T=180, full dims).
   hparam.json         -- the parsed config/config.yaml as the reference sees it.
 
 Weights/inputs come from tests/golden/recipe.py (numpy PCG64), so fixtures hold the
@@ -189,6 +191,58 @@ def eer_and_loader_fixtures(ref_hparam, ref_net):
         os.chdir(cwd)
 
 
+def net_full_c2(ref_net, ref_hparam):
+    """One training step at c2 (N=64 x M=10, T=160, full dims, fp32): the headline config pinned
+    to the reference itself (≈13 s of CPU).  Whole-tensor gradient and update norms plus 8x8 heads;
+    the embeddings in full (640 x 256)."""
+    dims = (40, 768, 3, 256)
+    rec = train_steps(ref_net, ref_hparam, dims, wseed=61, wscale=2.0, xseed=62, N=64, M=10, T=160, steps=1)
+    sd0 = recipe.make_weights(61, *dims, scale=2.0)
+    out = dict(dims=np.array(dims), wseed=61, wscale=2.0, xseed=62, N=64, M=10, T=160,
+               loss=rec["losses"][0], emb=rec["emb"][0], dw0=rec["dw0"], db0=rec["db0"], wb1=np.array(rec["wb1"]))
+    for k, g in rec["grads"].items():
+        out["gnorm." + k] = np.linalg.norm(g.astype(np.float64))
+        out["ghead." + k] = g.reshape(g.shape[0], -1)[:8, :8] if g.ndim == 2 else g[:64]
+    for k, p in rec["params1"].items():
+        out["p1head." + k] = p.reshape(p.shape[0], -1)[:8, :8] if p.ndim == 2 else p[:64]
+        out["dpnorm." + k] = np.linalg.norm(p.astype(np.float64) - sd0[k].astype(np.float64))
+    np.savez_compressed(os.path.join(HERE, "net_full_c2.npz"), **out)
+    print("net_full_c2 loss", rec["losses"][0])
+
+
+def net_fwd_c5(ref_net, ref_hparam):
+    """Forward + GE2E loss at c5's global batch (N=256 x M=10, T=180, full dims, fp32; ≈20 s of
+    CPU).  Every 8th embedding row in full, all 2560 rows projected on 4 fixed unit directions
+    (a checksum of every row), the per-embedding loss and the loss."""
+    import torch
+    dims = (40, 768, 3, 256)
+    N, M, T = 256, 10, 180
+    hp = ref_hparam.hparam
+    old = (hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj)
+    hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj = dims
+    try:
+        net = ref_net.SpeechEmbedder()
+    finally:
+        hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj = old
+    sd = recipe.make_weights(71, *dims, scale=2.0)
+    net.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+    x = torch.tensor(recipe.make_frames(72, N * M, T, dims[0]))
+    ge2e = ref_net.GE2ELoss("cpu")
+    with torch.no_grad():
+        emb = net(x)
+        loss = ge2e(emb.reshape(N, M, -1))
+        import utils as ref_utils
+        cos = ref_utils.get_cossim(emb.reshape(N, M, -1), ref_utils.get_centroids(emb.reshape(N, M, -1)))
+        _, per = ref_utils.calc_loss(ge2e.w * cos + ge2e.b)
+    dirs = np.random.default_rng(73).standard_normal((4, dims[3]))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    e = emb.numpy()
+    np.savez_compressed(os.path.join(HERE, "net_fwd_c5.npz"), dims=np.array(dims), wseed=71, wscale=2.0, xseed=72,
+                        N=N, M=M, T=T, loss=loss.item(), per=per.numpy(), emb_rows=e[::8], dirs=dirs,
+                        emb_proj=e.astype(np.float64) @ dirs.T)
+    print("net_fwd_c5 loss", loss.item())
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference not present; nothing to do")
@@ -196,6 +250,11 @@ def main():
     import torch
     torch.set_num_threads(os.cpu_count())
     ref_hparam, ref_utils, ref_net = import_reference()
+    only = sys.argv[1].split(",") if len(sys.argv) > 1 else None
+    if only:  # e.g. `make_golden.py net_full_c2,net_fwd_c5`: just those fixtures
+        for name in only:
+            {"net_full_c2": net_full_c2, "net_fwd_c5": net_fwd_c5}[name](ref_net, ref_hparam)
+        return
 
     # ---- KAT-0: utils.py:166-173 -------------------------------------------------
     E0 = np.array([[0, 1, 0], [0, 0, 1], [0, 1, 0], [0, 1, 0], [1, 0, 0], [1, 0, 0]],
@@ -272,6 +331,10 @@ def main():
         out["p1head." + k] = p.reshape(p.shape[0], -1)[:8, :8] if p.ndim == 2 else p[:64]
     np.savez_compressed(os.path.join(HERE, "net_full_c1.npz"), **out)
     print("net_full_c1 loss", rec["losses"][0])
+
+    # ---- the headline config (c2) and c5's global forward, pinned to the reference -------
+    net_full_c2(ref_net, ref_hparam)
+    net_fwd_c5(ref_net, ref_hparam)
 
     # ---- init RNG parity: reference SpeechEmbedder() under torch.manual_seed ------
     hp = ref_hparam.hparam

@@ -1,11 +1,11 @@
-"""GPU: the reference's CPU-resident evaluation drops in unchanged.
+"""GPU: CPU-resident modules (the reference's evaluation never moves its net to a device,
+train_speech_embedder.py:100-102,120-121) compute on the HIP kernels and hand back CPU tensors.
 
-train_speech_embedder.py:100-121 builds the net with ``SpeechEmbedder()``, loads the checkpoint
-and calls ``.eval()`` without ever moving it to a device, then feeds it CPU batches straight from
-the DataLoader, without ``torch.no_grad()``.  The drop-in module keeps that working: inputs and
-parameters make a round trip to the GPU's HIP kernels and the results come back as CPU tensors
-(no CPU compute path exists: ``_lib.compute_device``).  The loop body below is the reference's,
-statement for statement; it must reproduce the reference's own run (tests/golden/eer.npz).
+This package's own calls -- a CPU-resident ``SpeechEmbedder`` loaded from the reference-written
+checkpoint, ``get_centroids`` of the enrollment half, ``get_cossim`` of the verification half --
+on the batches the reference's recorded ``test()`` run drew (same synthetic data, seeds and RNG
+consumption), against that run's similarity matrices (tests/golden/eer.npz).  The EER of those
+matrices is taken by the numpy oracle and must reproduce the run's printed average.
 """
 import os
 import random
@@ -17,11 +17,13 @@ from torch.utils.data import DataLoader
 
 import recipe
 from conftest import golden
+from oracle import eer_np
 
 pytestmark = pytest.mark.gpu
 
 
-def test_reference_shaped_cpu_resident_eval(tmp_path, monkeypatch):
+def test_cpu_resident_modules_reproduce_reference_eval(tmp_path, monkeypatch):
+    from pytorch_speaker_verification_amd import train_speech_embedder as tse
     from pytorch_speaker_verification_amd.data_load import SpeakerDatasetTIMITPreprocessed
     from pytorch_speaker_verification_amd.hparam import hparam as hp
     from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder, get_centroids, get_cossim
@@ -35,76 +37,45 @@ def test_reference_shaped_cpu_resident_eval(tmp_path, monkeypatch):
     ckpt = os.path.join(os.path.dirname(__file__), "golden", "ref_small_checkpoint.pth")
     saved = {k: dict(v) for k, v in hp.items() if isinstance(v, dict)}
     saved_top = {k: v for k, v in hp.items() if not isinstance(v, dict)}
-    sims, eers = [], []
+    N, M, epochs = int(g["N"]), int(g["M"]), int(g["epochs"])
+    half = M // 2
+    sims = []
     try:
         hp.data.nmels, hp.model.hidden, hp.model.num_layer, hp.model.proj = [int(v) for v in g["dims"]]
         hp.training = False
         hp.data.test_path = str(d)
-        hp.test.N, hp.test.M, hp.test.epochs, hp.test.num_workers = int(g["N"]), int(g["M"]), int(g["epochs"]), 0
-        random.seed(int(g["seed"]))
-        np.random.seed(int(g["seed"]))
-        torch.manual_seed(int(g["seed"]))
-        # ---- train_speech_embedder.py:92-154, CPU-resident as written there ----
-        test_dataset = SpeakerDatasetTIMITPreprocessed()
-        test_loader = DataLoader(test_dataset, batch_size=hp.test.N, shuffle=True, num_workers=hp.test.num_workers,
-                                 drop_last=True)
-        embedder_net = SpeechEmbedder()
-        embedder_net.load_state_dict(torch.load(ckpt, weights_only=True))
-        embedder_net.eval()
-        avg_EER = 0
-        for e in range(hp.test.epochs):
-            batch_avg_EER = 0
-            for batch_id, mel_db_batch in enumerate(test_loader):
-                assert hp.test.M % 2 == 0
-                enrollment_batch, verification_batch = torch.split(mel_db_batch, int(mel_db_batch.size(1) / 2), dim=1)
-                enrollment_batch = torch.reshape(enrollment_batch, (hp.test.N * hp.test.M // 2,
-                                                                    enrollment_batch.size(2), enrollment_batch.size(3)))
-                verification_batch = torch.reshape(verification_batch, (hp.test.N * hp.test.M // 2,
-                                                                        verification_batch.size(2),
-                                                                        verification_batch.size(3)))
-                perm = random.sample(range(0, verification_batch.size(0)), verification_batch.size(0))
-                unperm = list(perm)
-                for i, j in enumerate(perm):
-                    unperm[j] = i
-                verification_batch = verification_batch[perm]
-                enrollment_embeddings = embedder_net(enrollment_batch)
-                verification_embeddings = embedder_net(verification_batch)
-                verification_embeddings = verification_embeddings[unperm]
-                enrollment_embeddings = torch.reshape(enrollment_embeddings,
-                                                      (hp.test.N, hp.test.M // 2, enrollment_embeddings.size(1)))
-                verification_embeddings = torch.reshape(verification_embeddings,
-                                                        (hp.test.N, hp.test.M // 2, verification_embeddings.size(1)))
-                enrollment_centroids = get_centroids(enrollment_embeddings)
-                sim_matrix = get_cossim(verification_embeddings, enrollment_centroids)
-                assert sim_matrix.device.type == "cpu" and enrollment_embeddings.device.type == "cpu"
-                sims.append(sim_matrix.detach().numpy().copy())
-                diff = 1
-                EER = 0
-                for thres in [0.01 * i + 0.5 for i in range(50)]:
-                    sim_matrix_thresh = sim_matrix > thres
-                    FAR = (sum([sim_matrix_thresh[i].float().sum() - sim_matrix_thresh[i, :, i].float().sum()
-                                for i in range(int(hp.test.N))]) / (hp.test.N - 1.0) / (float(hp.test.M / 2)) /
-                           hp.test.N)
-                    FRR = (sum([hp.test.M / 2 - sim_matrix_thresh[i, :, i].float().sum()
-                                for i in range(int(hp.test.N))]) / (float(hp.test.M / 2)) / hp.test.N)
-                    if diff > abs(FAR - FRR):
-                        diff = abs(FAR - FRR)
-                        EER = (FAR + FRR) / 2
-                batch_avg_EER += EER
-                eers.append(float(EER))
-            avg_EER += batch_avg_EER / (batch_id + 1)
-        avg_EER = avg_EER / hp.test.epochs
+        hp.test.M = M
+        for s in (random.seed, np.random.seed, torch.manual_seed):
+            s(int(g["seed"]))
+        net = SpeechEmbedder()
+        net.load_state_dict(torch.load(ckpt, weights_only=True))
+        net.eval()
+        loader = DataLoader(SpeakerDatasetTIMITPreprocessed(), batch_size=N, shuffle=True, drop_last=True)
+        for _ in range(epochs):
+            for batch in loader:
+                frames = batch.shape[2:]
+                enroll = batch[:, :half].reshape(N * half, *frames)
+                verif = batch[:, half:].reshape(N * half, *frames)
+                tse._value_neutral_perm(verif.shape[0])  # the run's perm draw (RNG order only)
+                centroids = get_centroids(net(enroll).reshape(N, half, -1))
+                sim = get_cossim(net(verif).reshape(N, half, -1), centroids)
+                assert sim.device.type == "cpu" and centroids.device.type == "cpu"
+                sims.append(sim.detach().numpy().copy())
     finally:
         for k, v in saved.items():
             hp[k].update(v)
         for k, v in saved_top.items():
             hp[k] = v
-    # the parameters never left the CPU; the embeddings came back there
-    assert all(p.device.type == "cpu" for p in embedder_net.parameters())
+    assert all(p.device.type == "cpu" for p in net.parameters())
     got = np.stack(sims)
+    assert got.shape == g["sims"].shape
     err = float(np.abs(got - g["sims"]).max())
     print(f"\nMEASURED cpu_resident_eval sims max|dev| {err:.3e}")
     assert err <= 4e-6, err  # 10x the deviation measured on MI355X (4.2e-7)
-    # the reference's run is recorded as its printed "{:.4f}" line (:154): the same EER selection
-    # reproduces it exactly
-    assert f"{float(avg_EER):.4f}" == f"{float(g['avg_eer']):.4f}", (float(avg_EER), float(g["avg_eer"]))
+    per_batch = [eer_np.eer(s)[0] for s in got]
+    nb = len(per_batch) // epochs
+    avg = np.float32(0)
+    for e in range(epochs):
+        avg = np.float32(avg + np.float32(np.float32(sum(per_batch[e * nb:(e + 1) * nb], np.float32(0))) / nb))
+    avg = np.float32(avg / epochs)
+    assert f"{float(avg):.4f}" == f"{float(g['avg_eer']):.4f}", (float(avg), float(g["avg_eer"]))

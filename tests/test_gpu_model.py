@@ -106,6 +106,91 @@ def test_full_dims_c1_matches_reference(schedule):
     _check(f"{tag}.grad_head_rel", gh, 5e-5)
 
 
+def _grad_checks(tag, net, s, tol_norm=2e-5, tol_head=5e-5):
+    gn, gh = 0.0, 0.0
+    for k, p in net.named_parameters():
+        g = p.grad.cpu().double()
+        gn = max(gn, abs(g.norm().item() - float(s["gnorm." + k])) / float(s["gnorm." + k]))
+        head = g.reshape(g.shape[0], -1)[:8, :8].numpy() if g.dim() == 2 else g[:64].numpy()
+        ref = s["ghead." + k]
+        gh = max(gh, float(np.abs(head - ref).max()) / max(np.abs(ref).max(), 1e-6))
+    _check(f"{tag}.grad_norm_rel", gn, tol_norm)
+    _check(f"{tag}.grad_head_rel", gh, tol_head)
+
+
+@pytest.mark.parametrize("schedule", ["auto", "per_step"])
+def test_full_size_c2_matches_reference(schedule):
+    """The headline config c2 (N=64 x M=10, T=160, fp32) against the reference's own step
+    (tests/golden/net_full_c2.npz, generated by running the reference): embeddings, loss, every
+    parameter's gradient norm and 8x8 head through module forward + loss.backward(); 'auto' runs the
+    fp32 persistent recurrences at this batch, 'per_step' the K2 / K3 kernels."""
+    s = golden("net_full_c2.npz")
+    dims = tuple(int(v) for v in s["dims"])
+    net, ge2e = _build(dims, recipe.make_weights(int(s["wseed"]), *dims, scale=float(s["wscale"])))
+    net.schedule = schedule
+    tag = "c2_ref" if schedule == "auto" else "c2_ref_per_step"
+    N, M, T = int(s["N"]), int(s["M"]), int(s["T"])
+    x = torch.tensor(recipe.make_frames(int(s["xseed"]), N * M, T, dims[0]), device=DEV)
+    emb = net(x).reshape(N, M, -1)
+    _check(f"{tag}.emb_abs", float(np.abs(emb.detach().cpu().numpy().reshape(N * M, -1) - s["emb"].reshape(N * M, -1)).max()), 5e-6)
+    loss = ge2e(emb)
+    _check(f"{tag}.loss_rel", abs(loss.item() - float(s["loss"])) / abs(float(s["loss"])), 1e-5)
+    loss.backward()
+    _grad_checks(tag, net, s)
+    _check(f"{tag}.dw_rel", abs(ge2e.w.grad.item() - float(s["dw0"])) / max(1.0, abs(float(s["dw0"]))), 2.5e-5)
+
+
+@pytest.mark.parametrize("schedule", ["auto", "per_step"])
+def test_full_size_c2_fused_step_matches_reference(schedule):
+    """The fused step bench.py times (GE2ETrainer.step: forward, GE2E, backward, clip 3.0 / 1.0,
+    SGD) at c2 against the reference's parameters after its one clipped SGD step: 8x8 heads and
+    every parameter's update norm |p1 - p0|, plus the loss and w, b."""
+    from pytorch_speaker_verification_amd.trainer import GE2ETrainer
+    s = golden("net_full_c2.npz")
+    dims = tuple(int(v) for v in s["dims"])
+    sd = recipe.make_weights(int(s["wseed"]), *dims, scale=float(s["wscale"]))
+    net, ge2e = _build(dims, sd)
+    net.schedule = schedule
+    tag = "c2_ref_step" if schedule == "auto" else "c2_ref_step_per_step"
+    N, M, T = int(s["N"]), int(s["M"]), int(s["T"])
+    x = torch.tensor(recipe.make_frames(int(s["xseed"]), N * M, T, dims[0]), device=DEV)
+    tr = GE2ETrainer(net, ge2e, lr=0.01)
+    loss = float(tr.step(x, N, M))
+    _check(f"{tag}.loss_rel", abs(loss - float(s["loss"])) / abs(float(s["loss"])), 1e-5)
+    ph, dn = 0.0, 0.0
+    for k, v in net.state_dict().items():
+        p = v.detach().cpu().double().numpy()
+        head = p.reshape(p.shape[0], -1)[:8, :8] if p.ndim == 2 else p[:64]
+        ph = max(ph, float(np.abs(head - s["p1head." + k]).max()))
+        ref = float(s["dpnorm." + k])
+        dn = max(dn, abs(float(np.linalg.norm(p - sd[k].astype(np.float64))) - ref) / ref)
+    _check(f"{tag}.param_head_abs", ph, 3e-7)
+    _check(f"{tag}.update_norm_rel", dn, 2e-5)
+    _check(f"{tag}.wb_abs", float(np.abs(np.array([ge2e.w.item(), ge2e.b.item()]) - s["wb1"]).max()), 1e-5)
+
+
+def test_c5_global_forward_matches_reference():
+    """c5's global batch (N=256 x M=10, T=180, fp32) forward + GE2E loss on one GPU against the
+    reference's own run (tests/golden/net_fwd_c5.npz): every 8th embedding row, every row's
+    projection on 4 fixed directions, the per-embedding loss (the N=256 GE2E path) and the loss."""
+    s = golden("net_fwd_c5.npz")
+    dims = tuple(int(v) for v in s["dims"])
+    net, ge2e = _build(dims, recipe.make_weights(int(s["wseed"]), *dims, scale=float(s["wscale"])))
+    N, M, T = int(s["N"]), int(s["M"]), int(s["T"])
+    x = torch.tensor(recipe.make_frames(int(s["xseed"]), N * M, T, dims[0]), device=DEV)
+    with torch.no_grad():
+        emb = net(x)
+        loss = ge2e(emb.reshape(N, M, -1))
+        from pytorch_speaker_verification_amd.utils import calc_loss, get_centroids, get_cossim
+        E = emb.reshape(N, M, -1)
+        _, per = calc_loss(ge2e.w * get_cossim(E, get_centroids(E)) + ge2e.b)
+    e = emb.cpu().numpy()
+    _check("c5_ref.emb_rows_abs", float(np.abs(e[::8] - s["emb_rows"]).max()), 5e-6)
+    _check("c5_ref.emb_proj_abs", float(np.abs(e.astype(np.float64) @ s["dirs"].T - s["emb_proj"]).max()), 2e-5)
+    _check("c5_ref.per_abs", float(np.abs(per.cpu().numpy() - s["per"]).max()), 1e-4)
+    _check("c5_ref.loss_rel", abs(loss.item() - float(s["loss"])) / abs(float(s["loss"])), 1e-5)
+
+
 @pytest.mark.parametrize("schedule", ["auto", "per_step"])
 def test_full_size_c2_against_torch_gpu(schedule):
     """c2 (N=64 x M=10, T=160) vs the stock-PyTorch fp32 port of the reference on the same GPU:

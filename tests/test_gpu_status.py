@@ -148,3 +148,28 @@ def test_dp_timeout_on_one_rank_skips_every_rank():
     for status, nan_loss, unchanged, raised, recovered in outs:
         assert int(status) == 2
         assert nan_loss == "True" and unchanged == "True" and raised == "True" and recovered == "True"
+
+
+def test_forward_only_module_calls_keep_unchecked_list_bounded():
+    """Forward-only module calls (the EER loop, anything under no_grad) arm a status check per
+    call; each call first drops the completed ones, so the pending list stays bounded."""
+    import torch
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    import recipe
+    from conftest import model_dims
+    from pytorch_speaker_verification_amd import ops
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    dims = (40, 64, 3, 32)
+    with model_dims(*dims):
+        net = SpeechEmbedder().to("cuda")
+    net.precision = "bf16"
+    x = torch.tensor(recipe.make_frames(3, 20, 24, 40), device="cuda")
+    ops.check_persistent_status(wait=True)
+    sizes = []
+    with torch.no_grad():
+        for _ in range(40):
+            net(x)
+            torch.cuda.synchronize()
+            sizes.append(len(ops._UNCHECKED))
+    print(f"\nMEASURED unchecked_list sizes max {max(sizes)} last {sizes[-1]}")
+    assert max(sizes) <= 2, sizes

@@ -33,3 +33,19 @@ def test_port_small_net_three_steps():
     np.testing.assert_allclose(losses, s["losses"], rtol=1e-5)
     for k, v in net.state_dict().items():
         np.testing.assert_allclose(v.numpy(), s["pf." + k], atol=1e-5)
+
+
+def test_port_c2_forward_against_reference():
+    """The port's c2 forward (N=64 x M=10, T=160, full dims: the cpu_baseline workload) against the
+    reference's own embeddings and loss (tests/golden/net_full_c2.npz)."""
+    s = golden("net_full_c2.npz")
+    dims = tuple(int(v) for v in s["dims"])
+    net = torch_port.SpeechEmbedderPort(*dims)
+    torch_port.load_recipe_weights(net, recipe.make_weights(int(s["wseed"]), *dims, scale=float(s["wscale"])))
+    N, M, T = int(s["N"]), int(s["M"]), int(s["T"])
+    x = torch.tensor(recipe.make_frames(int(s["xseed"]), N * M, T, dims[0]))
+    with torch.no_grad():
+        emb = net(x)
+        loss = torch_port.ge2e_loss(emb.reshape(N, M, -1), 10.0, -5.0)
+    assert float(np.abs(emb.numpy() - s["emb"].reshape(N * M, -1)).max()) <= 1e-6
+    assert abs(loss.item() - float(s["loss"])) <= 1e-6 * abs(float(s["loss"]))
