@@ -174,13 +174,37 @@ def probe_ms(probes, key):
 
 
 def persist_kernels(B, H=768, cus=256):
-    """(bwd, fwd) names of the persistent bf16 recurrence kernels the library picks for the upper
-    layers at batch B (sv_persist.hip: the wide 32 x 64 tile where the 32-unit tile would need
-    64-row blocks)."""
+    """(bwd, fwd) names of the per-layer persistent bf16 recurrence kernels the library picks for
+    the upper layers at batch B (sv_persist.hip: the wide 32 x 64 tile where the 32-unit tile would
+    need 64-row blocks)."""
     wide = H == 768 and (B + 31) // 32 * (H // 32) > cus and (B + 31) // 32 * (H // 64) <= cus
     bwd = "lstm_persist3_bwd_bf16_kernel" if wide else "lstm_persist2_bwd_bf16_kernel"
     fwd = "lstm_persist3_fwd_bf16_kernel" if wide else "lstm_persist2_fwd_bf16_kernel"
     return bwd, fwd
+
+
+def bf16_recurrences(B, T):
+    """What the bf16 trainer step runs for its recurrences at batch B under schedule 'auto', and
+    how its probe events must be read.  The trainer probes only the first row chunk
+    (trainer.bf16_row_chunks: equal persistent chunks past 672 rows, two wavefront halves up to
+    192), so the FLOPs are that chunk's.  Returns dict(kind, bwd, fwd, launches (per direction per
+    step), fwd_flops / bwd_flops (per launch), rows)."""
+    from pytorch_speaker_verification_amd._lib import lib
+    from pytorch_speaker_verification_amd.trainer import bf16_row_chunks
+    F, H, L, _ = DIMS
+    r0, r1 = bf16_row_chunks(B, H, "auto", L, T, F)[0]
+    b = r1 - r0
+    G = 4 * H
+    if lib().sv_wave_ok(L, T, b, F, H):
+        # one launch for all layers: the forward contracts every layer's input and recurrent
+        # operands, the backward every layer's dh_rec and the upper layers' dx
+        return {"kind": "wave", "bwd": "lstm_wave_bwd_bf16_kernel", "fwd": "lstm_wave3_fwd_bf16_kernel",
+                "launches": 1, "rows": b,
+                "fwd_flops": float(sum(2 * b * T * G * ((F if l == 0 else H) + H) for l in range(L))),
+                "bwd_flops": float(2 * b * T * G * H * (2 * L - 1))}
+    kb, kf = persist_kernels(b, H)
+    fl = float(2 * b * T * H * G)
+    return {"kind": "persist", "bwd": kb, "fwd": kf, "launches": L, "rows": b, "fwd_flops": fl, "bwd_flops": fl}
 
 
 def pmc_traffic(kernel):
@@ -350,6 +374,49 @@ def hbm_kernels(tr, N, M, D, dev, reps=50):
                                      "graph launch); launch- and L2-latency bound at this size"},
             "clip_sgd": {"avg_us": round(ms_cl * 1e3, 2), "algorithmic_bytes": by_cl,
                          "achieved_GBps": r(by_cl, ms_cl), "peak_GBps": MI355X_HBM_GBPS}}
+
+
+def c5_rank_ge2e(dev, world=8, reps=50):
+    """The GE2E of one c5 rank at 8 GPUs as ShardedGE2E.train runs it (sharded_ge2e.py): this
+    rank's N_local = 32 speakers x M = 10 against all N = 256 centroids, the last rank (speaker
+    offset s0 = 224), the fused sharded kernels (sv_ge2e_shard_prep / _rows / _finalize) with the
+    two exchanges left out (the all-gathered sums and the all-reduced buffer are synthetic); the
+    split kernels of the same shard beside it."""
+    from pytorch_speaker_verification_amd.sharded_ge2e import HipFusedShard, HipShardKernels
+    N, M, D = 256, 10, 256
+    Nl = N // world
+    s0 = N - Nl
+    g = torch.Generator(device="cpu").manual_seed(25)
+    E = torch.nn.functional.normalize(torch.randn(Nl, M, D, generator=g), dim=2).to(dev)
+    others = torch.nn.functional.normalize(torch.randn(N, M, D, generator=g), dim=2).sum(1).to(dev)
+    w = torch.tensor(10.0, device=dev)
+    b = torch.tensor(-5.0, device=dev)
+    f = HipFusedShard()
+    assert f.ok(N, M, D)
+    ssum_local, ws = f.prep(E, N)
+    ssum_all = others.clone()
+    ssum_all[s0:] = ssum_local
+
+    def fused():
+        sl, wsp = f.prep(E, N)
+        _, _, red, _ = f.rows(E, s0, N, ssum_all, w, b, wsp)
+        f.finalize(E, s0, N, red, wsp)
+    k = HipShardKernels()
+
+    def split():
+        k.speaker_sums(E)
+        _, _, st = k.fwd_rows(E, s0, N, ssum_all, w, b)
+        red, _ = k.bwd_rows(st, w, b, None)
+        k.finalize(st, red)
+    ms_f = _timed(fused, dev, reps)
+    ms_s = _timed(split, dev, reps)
+    by = 3.0 * Nl * M * D * 4
+    return {"workload": f"one c5 rank's GE2E at {world} GPUs: N_local={Nl}xM={M} rows against N={N} centroids, "
+                        f"s0={s0}, D={D} (exchanges excluded)",
+            "fused_us": round(ms_f * 1e3, 2), "split_us": round(ms_s * 1e3, 2), "algorithmic_bytes": by,
+            "note": "fused: sv_ge2e_shard_prep + _rows (centroids of all 256 speakers in two fp32 LDS tiles) + "
+                    "_finalize; split: the sv_ge2e_speaker_sums / fwd_rows / bwd_rows / bwd_finalize kernels; "
+                    "eager per-call loop (host path included), launch- and L2-latency bound"}
 
 
 def _ge2e_torch(E, w, b):
@@ -580,6 +647,30 @@ def _launch_ranks(args):
     return subprocess.run(cmd, env=env).returncode
 
 
+def bf16_roofline(probes, B, T, steps, where):
+    """(backward, forward) roofline entries of the bf16 step's recurrences from its probe events:
+    per-layer persistent launches (one event pair per layer) or the one-launch layer wavefront (its
+    first pair spans the whole launch)."""
+    r = bf16_recurrences(B, T)
+    n = r["launches"]
+    if r["kind"] == "wave":
+        what = ("one launch for all {L} layers (layer wavefront, sv_wave.hip / sv_persist3.hip); FLOPs = every "
+                "layer's {part} at {rows} rows").format(L=DIMS[2], rows=r["rows"], part="{part}")
+        nb = what.format(part="dh_rec and the upper layers' dx contractions")
+        nf = what.format(part="input and recurrent gate contractions")
+    else:
+        nb = f"persistent backward recurrence, one launch per layer, {r['rows']} rows per launch"
+        nf = (f"persistent forward recurrence, one launch per layer, {r['rows']} rows; layer 0: "
+              "lstm_persist2_fwd_bf16_kernel with the fused input projection")
+    chunk = "" if r["rows"] == B else f" (the first of the step's row chunks: {r['rows']} of {B} rows)"
+    note = f"in-step: HIP events around each launch inside the {where}{chunk}"
+    bwd = roofline_entry(f"{r['bwd']} ({nb})", r["bwd_flops"], probe_ms(probes, "bwd") / n, MI355X_BF16_MFMA_TFLOPS,
+                         pmc_traffic(r["bwd"]), n * steps, note)
+    fwd = roofline_entry(f"{r['fwd']} ({nf})", r["fwd_flops"], probe_ms(probes, "fwd") / n, MI355X_BF16_MFMA_TFLOPS,
+                         pmc_traffic(r["fwd"]), n * steps, note + " (average over the launches)")
+    return bwd, fwd
+
+
 def roofline_entry(kernel, flops, ms, peak, traffic, launches, note):
     ach = flops / (ms * 1e-3) / 1e12
     return {"kernel": kernel, "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
@@ -693,17 +784,7 @@ def main():
             "32-step chunk)")
         out["roofline"]["stream_span_us"] = round(ms_ev * 1e3, 2)
     else:
-        fl = 2.0 * B * T * H * 4 * H
-        kb, kf = persist_kernels(B)
-        out["roofline"] = roofline_entry(
-            f"{kb} (persistent backward recurrence, one launch per layer, bf16 MFMA)", fl,
-            probe_ms(probes, "bwd") / L, MI355X_BF16_MFMA_TFLOPS, pmc_traffic(kb),
-            L * args.steps, "in-step: HIP events around each layer's launch inside the timed steps")
-        out["roofline_fwd"] = roofline_entry(
-            f"{kf} (persistent forward recurrence; layer 0: lstm_persist2_fwd_bf16_kernel with the fused input "
-            "projection)", fl, probe_ms(probes, "fwd") / L,
-            MI355X_BF16_MFMA_TFLOPS, pmc_traffic(kf), L * args.steps,
-            "in-step, as roofline (average over the L layers' launches)")
+        out["roofline"], out["roofline_fwd"] = bf16_roofline(probes, B, T, args.steps, "timed steps")
 
     # forward-only (inference) embeddings/s at the headline shape
     from pytorch_speaker_verification_amd.ops import embedder_forward, embedder_forward_bf16
@@ -742,28 +823,23 @@ def main():
     if not args.no_bf16 and args.preset is None and dtype == "f32":
         o, pr = side("bf16", N, M, T, "bf16", False, "c3: the headline workload with bf16 GEMM operands, fp32 "
                      "accumulate/state/loss", probe="fwd_bwd")
-        fl = 2.0 * B * T * H * 4 * H
-        kb, kf = persist_kernels(B)
-        out["roofline_bf16"] = roofline_entry(
-            f"{kb} (c3's dominant kernel: persistent backward recurrence)", fl,
-            probe_ms(pr, "bwd") / L, MI355X_BF16_MFMA_TFLOPS, pmc_traffic(kb),
-            L * args.steps, "in-step: HIP events around each layer's launch inside the timed c3 steps")
-        out["roofline_bf16_fwd"] = roofline_entry(
-            f"{kf} (persistent forward recurrence; layer 0: the fused-projection 32-unit kernel)", fl,
-            probe_ms(pr, "fwd") / L, MI355X_BF16_MFMA_TFLOPS, pmc_traffic(kf), L * args.steps,
-            "in-step (average over the L layers' launches)")
+        out["roofline_bf16"], out["roofline_bf16_fwd"] = bf16_roofline(pr, B, T, args.steps, "timed c3 steps")
+        def side_rl(name, Nl, Tl, descr):
+            o, pr = side(name, Nl, 10, Tl, "bf16", True, descr, probe="fwd_bwd")
+            o["roofline"], o["roofline_fwd"] = bf16_roofline(pr, Nl * 10, Tl, args.steps, f"timed {name} steps")
         if world > 1:
-            side("c4", max(1, 64 // world), 10, 160, "bf16", True,
-                 f"c4: N=64xM=10, T=160, bf16, split over {world} GPUs ({max(1, 64 // world)} speakers per rank); "
-                 "value = 640 embeddings per step / time")
-            side("c5", max(1, 256 // world), 10, 180, "bf16", True,
-                 f"c5: N=256xM=10, T=180, bf16, split over {world} GPUs ({max(1, 256 // world)} speakers per rank)")
+            side_rl("c4", max(1, 64 // world), 160,
+                    f"c4: N=64xM=10, T=160, bf16, split over {world} GPUs ({max(1, 64 // world)} speakers per rank); "
+                    "value = 640 embeddings per step / time")
+            side_rl("c5", max(1, 256 // world), 180,
+                    f"c5: N=256xM=10, T=180, bf16, split over {world} GPUs ({max(1, 256 // world)} speakers per rank)")
         else:
-            side("c4_rank_shape", 8, 10, 160, "bf16", True,
-                 "one rank's share of c4 at 8 GPUs (N=8xM=10, T=160, bf16) run alone on this GPU: the per-rank "
-                 "step time of the 8-GPU strong-scaling config (value counts this GPU's 80 embeddings)")
-            side("c5_rank_shape", 32, 10, 180, "bf16", True,
-                 "one rank's share of c5 at 8 GPUs (N=32xM=10, T=180, bf16) run alone on this GPU")
+            side_rl("c4_rank_shape", 8, 160,
+                    "one rank's share of c4 at 8 GPUs (N=8xM=10, T=160, bf16) run alone on this GPU: the per-rank "
+                    "step time of the 8-GPU strong-scaling config (value counts this GPU's 80 embeddings)")
+            side_rl("c5_rank_shape", 32, 180,
+                    "one rank's share of c5 at 8 GPUs (N=32xM=10, T=180, bf16) run alone on this GPU; its GE2E runs "
+                    "the single-GPU fused kernel at N=32 (the real rank's sharded GE2E: c5_rank_ge2e)")
     if not args.no_f32x and dtype == "f32" and world == 1:
         o, _ = side("f32_bf16x6", N, M, T, "f32", False,
                     "same workload, fp32 products formed as six bf16 MFMA products of a three-way bf16 split (fp32 "
@@ -790,6 +866,7 @@ def main():
         if world == 1:
             log("hbm kernels / vendor baseline")
             out["hbm_kernels"] = hbm_kernels(tr, N, M, P, dev)
+            out["c5_rank_ge2e"] = c5_rank_ge2e(dev)
             log("d-vector inference")
             out["dvector_inference"] = dvector_inference(tr.net, dev)
             if not args.no_vendor:

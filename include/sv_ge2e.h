@@ -176,9 +176,10 @@ int sv_ge2e_bwd(int N, int M, int D, const float* w, const float* b, const float
                 float* dchat, float* beta, float* workspace, hipStream_t stream);
 
 /* fused single-GPU training form (all N speakers local, gloss = 1): forward + closed-form
- * backward in three launches (per-speaker prep; a wave per row with every centroid staged in LDS:
- * cosines, shuffle softmax, row backward; a workgroup per (speaker, 64-wide d slice): centroid
- * gradients and the speaker's dE).  Needs N <= 128, 2 <= M <= 16, D <= 256, D % 4 == 0 (sv_ge2e_train_ok);
+ * backward in three launches (per-speaker prep; a wave per row with the centroids staged in LDS,
+ * fp32, in one tile up to 128 speakers and two tiles of 128 above: cosines, shuffle softmax, row
+ * backward; a workgroup per (speaker, 64-wide d slice): centroid gradients and the speaker's dE).
+ * Needs N <= 256, 2 <= M <= 16, D <= 256, D % 4 == 0 (sv_ge2e_train_ok);
  * workspace: sv_ge2e_workspace_size(N, M, D, N). */
 int sv_ge2e_train_ok(int N, int M, int D);
 int sv_ge2e_train(const float* E, int N, int M, int D, const float* w, const float* b, float* loss, float* per,

@@ -619,14 +619,44 @@ extern "C" int sv_gemm_bf16_bf(int M, int N, int K, const bf16_t* A, long lda, c
 bool gemm_afrag_ok(int T, int B, int N, int H) {
   return gemm256_ok(T * B, N, 4 * H) && B % 32 == 0 && H % G256_BK == 0;
 }
-// (the split-K plan of sv_gemm_bf16 for the same shape, so both forms sum in the same order)
+// stream-K scratch of the dx GEMM's persistent form (gemm_bf16_8qsk_kernel): two partial slots of
+// 512 threads x 128 fp32 per workgroup (grid capped at G8_SK_GRID) + the stream-K tiles' counters
+constexpr int G8_SK_GRID = 256;
+constexpr size_t G8_SK_SLOT = (size_t)512 * 128 * sizeof(float);
+size_t g8_sk_bytes() { return 2 * G8_SK_GRID * G8_SK_SLOT + G8_SK_GRID * sizeof(unsigned) * 4; }
+#ifndef SV_G8_SK
+#define SV_G8_SK 1  // the dx GEMM's persistent + stream-K form where its tiles exceed one round (0: A/B)
+#endif
+// (the split-K plan of sv_gemm_bf16 for the same shape).  More tiles than one round of CUs (the c3
+// dx: 1200 tiles): the persistent + stream-K kernel when `skws` (g8_sk_bytes) is given -- its
+// stream-K tiles sum K in pieces, so at those shapes the per-step schedule's chunked dx GEMMs
+// (one round each) no longer sum bit-identically; within the bf16 tolerance of the oracle
 int gemm_bf16_afrag(int T, int B, int H, int N, const bf16_t* dgf, int bm, const bf16_t* Bop, long ldb, float* C,
-                    long ldc, float* workspace, hipStream_t stream) {
+                    long ldc, float* workspace, hipStream_t stream, void* skws = nullptr) {
   const int M = T * B, K = 4 * H;
   const int tiles = (M / G256_BM) * (N / G256_BM);
   const long fs = (long)((B + bm - 1) / bm) * bm * 4 * H;
   const G256AFrag af{dgf, fs, B, bm, H};
   const BPlan p = plan_bf16(M, N, K);
+  const int G = std::min(sv_stream_cus(stream), G8_SK_GRID), nk = K / G256_BK;
+  if (SV_G8_SK && p.splitk == 1 && skws && G > 0 && tiles > G && g8_ok(C, ldc, nullptr, nullptr)) {
+    G8SK sk;
+    sk.R = tiles / G;
+    sk.rem = tiles % G;
+    sk.L = sk.rem ? (int)(((long)sk.rem * nk + G - 1) / G) : 0;
+    if (sk.rem == 0 || (long)sk.L * (G8_SK_MAXSEG - 1) >= nk) {  // <= G8_SK_MAXSEG pieces per stream-K tile
+      sk.part = static_cast<float*>(skws);
+      sk.cnt = reinterpret_cast<unsigned*>(static_cast<char*>(skws) + 2 * G8_SK_GRID * G8_SK_SLOT);
+      if (sk.rem) {
+        hipError_t e = (hipError_t)sv_zero_counters(sk.cnt, 1, 0, sk.rem, stream);
+        if (e != hipSuccess) return (int)e;
+      }
+      hipLaunchKernelGGL((gemm_bf16_8qsk_kernel<1>), dim3(G), dim3(512), G256_LDS, stream, nullptr, 0L, Bop, ldb, C,
+                         ldc, M, N, K, sk, af);
+      SV_LAUNCH_CHECK();
+      return SV_OK;
+    }
+  }
   if (p.splitk == 1) {
     launch_g256<G256_STORE, 1>(g8_ok(C, ldc, nullptr, nullptr), dim3(tiles, 1), stream, nullptr, 0L, Bop, ldb, C,
                                ldc, 0L, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
@@ -958,11 +988,16 @@ static int wbf_transposes(int L, int F, int H, const float* const* w_ih, const f
   return flush();
 }
 
-extern "C" size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H) {
-  const size_t per = (size_t)L * carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
+// the hand-off scratch shared by the layers (persistent or wavefront backward), behind the L
+// per-layer regions; then the dx GEMM's stream-K scratch (persistent schedule)
+static size_t bbwd_scratch(int L, int T, int B, int H) {
   size_t scratch = sv_persist_bwd_fits(B, H, 1 << 30) ? sv_persist_bwd_scratch(T, B, H) : 0;
   if (sv_wave_bwd_fits(L, B, H, 1 << 30)) scratch = std::max(scratch, sv_wave_bwd_scratch(L, T, B, H));
-  return per + scratch;
+  return (scratch + 255) & ~size_t(255);
+}
+extern "C" size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H) {
+  const size_t per = (size_t)L * carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
+  return per + bbwd_scratch(L, T, B, H) + (sv_persist_bwd_fits(B, H, 1 << 30) ? g8_sk_bytes() : 0);
 }
 
 extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const bf16_t* const* xT, const long* ld_xT,
@@ -1052,7 +1087,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
         if ((e = hipEventRecord(ev[L * nch + k], main)) != hipSuccess) return (int)e;
       if (afr) {
         if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H, sv_stream_cus(main)), ws.wihT, 4L * H, dx[l],
-                                  Fl, ws.gws, main)))
+                                  Fl, ws.gws, main, (char*)workspace + per * L + bbwd_scratch(L, T, B, H))))
           return rc;
       } else if (l > 0 && (rc = sv_gemm_bf16(T * B, Fl, 4 * H, dg[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr,
                                               nullptr, 0.f, ws.gws, main))) {

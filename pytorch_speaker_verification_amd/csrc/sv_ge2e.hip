@@ -165,11 +165,11 @@ __global__ __launch_bounds__(256) void ge2e_rowloss_kernel(float* __restrict__ c
   float z = 0.f;
   for (int k = lane; k < N; k += 64) {
     const float cr = (k == sg) ? rawd[r] : c[k];
-    z += __expf(w * (cr + EPS_SIM) + b - mx);
+    z += expf(w * (cr + EPS_SIM) + b - mx);
   }
   z = wave_sum(z);
   // log(sum_k e^S + 1e-6) = mx + log(sum_k e^{S-mx} + 1e-6 e^{-mx}), mx >= 0
-  const float lz = mx + logf(z + EPS_LOG * __expf(-mx));
+  const float lz = mx + logf(z + EPS_LOG * expf(-mx));
   if (lane == 0) {
     const float spos = w * (rawd[r] + EPS_SIM) + b;
     per[r] = lz - spos;
@@ -203,26 +203,28 @@ __global__ __launch_bounds__(256) void ge2e_rowbwd_kernel(const float* __restric
   const float lz = logz[r];
   const float* c = cos + (long)r * ldc;
   float* dc = dcos + (long)r * ldc;
-  float a = 0.f, dw = 0.f, db = 0.f;
+  // sum_k dS_k x_k with dS = p - delta is a difference of two O(1) sums (sum_k p_k = 1 - 1e-6 e^-lz):
+  // summed as sum_k p_k (x_k - x_d) - x_d 1e-6 e^-lz, i.e. only the small differences accumulate
+  // (the reference's fp32 dw is within 5e-8 of fp64 at c2; the direct form was 5e-5 off)
+  const float cd = c[sg];
+  const float tail = EPS_LOG * expf(-lz);  // 1 - sum_k p_k
+  float a = 0.f, dw = 0.f;
   for (int k = lane; k < N; k += 64) {
     const float cr = c[k];
-    const float cp = cr + EPS_SIM;
-    const float p = __expf(w * cp + b - lz);
+    const float p = expf(w * (cr + EPS_SIM) + b - lz);
     const float ds = g * (p - (k == sg ? 1.0f : 0.0f));
-    const float dcv = w * ds;
-    a += dcv * cr;
-    dw += ds * cp;
-    db += ds;
-    dc[k] = (k == sg) ? 0.f : dcv;
+    const float pd = p * (cr - cd);
+    a += pd;
+    dw += pd;
+    dc[k] = (k == sg) ? 0.f : w * ds;
   }
   for (int k = N + lane; k < ldc; k += 64) dc[k] = 0.f;
   a = wave_sum(a);
   dw = wave_sum(dw);
-  db = wave_sum(db);
   if (lane == 0) {
-    alpha[r] = a;
-    dwdb[r] = dw;
-    dwdb[Bl + r] = db;
+    alpha[r] = w * g * (a - cd * tail);
+    dwdb[r] = g * (dw - (cd + EPS_SIM) * tail);
+    dwdb[Bl + r] = -g * tail;
   }
 }
 
@@ -319,7 +321,7 @@ __global__ void ge2e_dcd_kernel(const float* __restrict__ rawd, const float* __r
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= Bl) return;
   const float w = *wp, b = *bp, g = gl ? *gl : 1.0f;
-  const float p = __expf(w * (rawd[r] + EPS_SIM) + b - logz[r]);
+  const float p = expf(w * (rawd[r] + EPS_SIM) + b - logz[r]);
   dcd[r] = w * g * (p - 1.0f);
 }
 
@@ -425,7 +427,8 @@ extern "C" int sv_ge2e_bwd(int N, int M, int D, const float* w, const float* b, 
 
 // ============================================================================
 // Fused single-GPU training path: GE2E forward + closed-form backward in three launches
-// (sv_ge2e_train), for N <= 128 speakers, M <= 16, D <= 256 (every c1-c5 single-GPU shape):
+// (sv_ge2e_train), for N <= 256 speakers, M <= 16, D <= 256 (every c1-c5 shape, c5's global N = 256
+// included):
 //   F1 ge2e_prep_kernel   one workgroup per speaker: its sum, centroid C^ and |C| (LDS
 //                         reduction), and per utterance row E^, U^ (leave-one-out), the norms and
 //                         the diagonal cosine (a wave per row, shuffle reductions)
@@ -441,7 +444,7 @@ extern "C" int sv_ge2e_bwd(int N, int M, int D, const float* w, const float* b, 
 // The arithmetic is the split path's (same formulas, fixed-order sums; the cosines by FMA dot
 // products instead of the MFMA GEMM), so results agree to fp32 rounding.
 // ============================================================================
-#define GF_NMAX 128
+#define GF_NMAX 256
 #define GF_DMAX 256
 #define GF_MMAX 16
 
@@ -532,9 +535,15 @@ __global__ __launch_bounds__(256) void ge2e_prep_kernel(const float* __restrict_
 
 // F2: GF_ROWW rows per workgroup, one per wave (160 workgroups of 4 waves at c2: each row's
 // serial work in its own wave; 8 waves per workgroup measured slower, 11.2 vs 10.0 us at c2).
-// Cs [N][D + 4] fp32 in LDS (16-B padded rows: the 16 lanes of a ds_read_b128 group hit
+// Cs [NT][D + 4] fp32 in LDS (16-B padded rows: the 16 lanes of a ds_read_b128 group hit
 // disjoint banks); the rows' E^ in Es [GF_ROWW][D]; per-row dcos in Vs [GF_ROWW][N].
+// NH = 64-speaker groups per lane: 2 for N <= 128 (C^ staged once, NT = N), 4 for N <= 256 (c5's
+// "centroid LDS stress": 256 fp32 rows of C^ are 266 KB, over the 160 KB LDS), where C^ is staged
+// in two tiles of GF_TILE = 128 speakers (133 KB): tile 0, then tile 1 for the cosines, G1 over
+// tile 1 while it is resident, then tile 0 again -- still fp32 throughout.
 #define GF_ROWW 4
+#define GF_TILE 128
+template <int NH>
 __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __restrict__ Chat, const float* __restrict__ Ehat,
                                                         const float* __restrict__ rawd, int Bl, int M, int N, int D,
                                                         int ldc, int s0, const float* __restrict__ wp,
@@ -542,111 +551,131 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
                                                         float* __restrict__ cos, float* __restrict__ dcos,
                                                         float* __restrict__ alpha, float* __restrict__ dcd,
                                                         float* __restrict__ dwdb_rows, float* __restrict__ G1) {
+  static_assert(NH == 2 || NH == 4, "NH: 64-speaker groups per lane");
   extern __shared__ __attribute__((aligned(16))) float gsm[];
   const int LDC = D + 4;
-  float* Cs = gsm;                    // [N][LDC]
-  float* Es = Cs + (size_t)N * LDC;   // [GF_ROWW][D]
-  float* Vs = Es + GF_ROWW * D;       // [GF_ROWW][N]
+  const int NT = NH == 2 ? N : GF_TILE;  // speakers per LDS tile
+  float* Cs = gsm;                       // [NT][LDC]
+  float* Es = Cs + (size_t)NT * LDC;     // [GF_ROWW][D]
+  float* Vs = Es + GF_ROWW * D;          // [GF_ROWW][N]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int D4 = D / 4, NQ = N * D4;
-  // global -> LDS copy of C^ (distinct address spaces: the unrolled loads issue back to back)
+  const int D4 = D / 4;
+  // global -> LDS copy of C^ rows k0 .. (distinct address spaces: the unrolled loads issue back to back)
+  auto stage = [&](int k0) {
+    const int NQ = min(NT, N - k0) * D4;
 #pragma unroll 8
-  for (int q = tid; q < NQ; q += 64 * GF_ROWW) {
-    const int row = q / D4, col = (q - row * D4) * 4;
-    *reinterpret_cast<float4*>(Cs + row * LDC + col) = *reinterpret_cast<const float4*>(Chat + (long)row * D + col);
-  }
+    for (int q = tid; q < NQ; q += 64 * GF_ROWW) {
+      const int row = q / D4, col = (q - row * D4) * 4;
+      *reinterpret_cast<float4*>(Cs + row * LDC + col) =
+          *reinterpret_cast<const float4*>(Chat + (long)(k0 + row) * D + col);
+    }
+  };
+  stage(0);
   const int r = blockIdx.x * GF_ROWW + w;   // this wave's row
-  if (r < Bl)
+  const bool live = r < Bl;
+  if (live)
     for (int c = lane * 4; c < D; c += 256)
       *reinterpret_cast<float4*>(Es + w * D + c) = *reinterpret_cast<const float4*>(Ehat + (long)r * D + c);
   __syncthreads();
-  if (r >= Bl) return;
+  if constexpr (NH == 2) {
+    if (!live) return;  // (no later workgroup barrier)
+  }
   const float wv = *wp, bv = *bp;
   const int sg = s0 + r / M;  // global speaker of this row (s0: the shard's first)
-  const float rd = rawd[r];
+  const float rd = live ? rawd[r] : 0.f;
   // cosines: KS speaker lanes x DS d-slices (DS = 1 for N > 32: lane k and k + 64 over all of
   // D; small N splits D so the wave's lanes all work, the slices then meet by a butterfly), E^
-  // broadcast; four independent partial sums (d mod 4), added pairwise at the end
+  // broadcast; four independent partial sums (d mod 4), added pairwise at the end.  Speaker
+  // lane + 64 h is cv[h].
   int DS = N <= 8 ? 8 : N <= 16 ? 4 : N <= 32 ? 2 : 1;
   while (DS > 1 && D % (4 * DS)) DS >>= 1;
   const int KS = 64 / DS, dlen = D / DS;
   const int kl = lane & (KS - 1), d0 = (lane / KS) * dlen;
-  float cv[2] = {0.f, 0.f};
+  float cv[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) cv[h] = 0.f;
   const float* e0 = Es + w * D;
 #pragma unroll
-  for (int hk = 0; hk < 2; ++hk) {
-    const int k = kl + 64 * hk;
-    if (k < N) {
-      float4 a = float4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < NH / 2; ++t) {
+    if (t > 0) {  // NH == 4: the second tile
+      __syncthreads();
+      stage(t * GF_TILE);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int hk = 0; hk < 2; ++hk) {
+      const int kt = kl + 64 * hk;  // speaker within the tile
+      if (live && t * GF_TILE + kt < N) {
+        float4 a = float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
-      for (int c = d0; c < d0 + dlen; c += 4) {
-        const float4 cc = *reinterpret_cast<const float4*>(Cs + k * LDC + c);
-        const float4 x0 = *reinterpret_cast<const float4*>(e0 + c);
-        a.x += x0.x * cc.x;
-        a.y += x0.y * cc.y;
-        a.z += x0.z * cc.z;
-        a.w += x0.w * cc.w;
+        for (int c = d0; c < d0 + dlen; c += 4) {
+          const float4 cc = *reinterpret_cast<const float4*>(Cs + kt * LDC + c);
+          const float4 x0 = *reinterpret_cast<const float4*>(e0 + c);
+          a.x += x0.x * cc.x;
+          a.y += x0.y * cc.y;
+          a.z += x0.z * cc.z;
+          a.w += x0.w * cc.w;
+        }
+        cv[2 * t + hk] = (a.x + a.y) + (a.z + a.w);
       }
-      cv[hk] = (a.x + a.y) + (a.z + a.w);
     }
   }
   for (int o = KS; o < 64; o <<= 1) cv[0] += __shfl_xor(cv[0], o, 64);  // lane k < KS: speaker k
 #pragma unroll
-  for (int hk = 0; hk < 2; ++hk)
-    if (lane + 64 * hk == sg) cv[hk] = rd;  // get_cossim's diagonal overwrite (utils.py:112-113)
+  for (int h = 0; h < NH; ++h)
+    if (lane + 64 * h == sg) cv[h] = rd;  // get_cossim's diagonal overwrite (utils.py:112-113)
   // row softmax: S = w (cos + 1e-6) + b;  lz = log(sum_k e^S + 1e-6)
   float mx = -INFINITY;
 #pragma unroll
-  for (int hk = 0; hk < 2; ++hk)
-    if (lane + 64 * hk < N) mx = fmaxf(mx, wv * (cv[hk] + EPS_SIM) + bv);
+  for (int h = 0; h < NH; ++h)
+    if (lane + 64 * h < N) mx = fmaxf(mx, wv * (cv[h] + EPS_SIM) + bv);
   mx = fmaxf(wave_max(mx), 0.f);
   float z = 0.f;
 #pragma unroll
-  for (int hk = 0; hk < 2; ++hk)
-    if (lane + 64 * hk < N) z += __expf(wv * (cv[hk] + EPS_SIM) + bv - mx);
+  for (int h = 0; h < NH; ++h)
+    if (lane + 64 * h < N) z += expf(wv * (cv[h] + EPS_SIM) + bv - mx);
   z = wave_sum(z);
-  const float lz = mx + logf(z + EPS_LOG * __expf(-mx));
-  // row backward (gloss = 1): dS = p - delta, dcos = w dS
-  float a = 0.f, dw = 0.f, db = 0.f;
+  const float lz = mx + logf(z + EPS_LOG * expf(-mx));
+  // row backward (gloss = 1): dS = p - delta, dcos = w dS; alpha, dw, db as sums of the small
+  // differences p_k (x_k - x_d) and the analytic 1 - sum_k p_k = 1e-6 e^-lz (ge2e_rowbwd_kernel)
+  const float tail = EPS_LOG * expf(-lz);
+  float pdsum = 0.f;
 #pragma unroll
-  for (int hk = 0; hk < 2; ++hk) {
-    const int k = lane + 64 * hk;
-    if (k < N) {
-      const float cp = cv[hk] + EPS_SIM;
-      const float p = __expf(wv * cp + bv - lz);
+  for (int h = 0; h < NH; ++h) {
+    const int k = lane + 64 * h;
+    if (live && k < N) {
+      const float p = expf(wv * (cv[h] + EPS_SIM) + bv - lz);
       const float ds = p - (k == sg ? 1.0f : 0.0f);
       const float dcv = wv * ds;
-      a += dcv * cv[hk];
-      dw += ds * cp;
-      db += ds;
+      pdsum += p * (cv[h] - rd);
       const float off = (k == sg) ? 0.f : dcv;
       Vs[w * N + k] = off;
-      cos[(long)r * ldc + k] = cv[hk];
+      cos[(long)r * ldc + k] = cv[h];
       dcos[(long)r * ldc + k] = off;
       if (k == sg) dcd[r] = dcv;
     }
   }
-  a = wave_sum(a);
-  dw = wave_sum(dw);
-  db = wave_sum(db);
-  if (lane == 0) {
+  pdsum = wave_sum(pdsum);
+  if (live && lane == 0) {
     per[r] = lz - (wv * (rd + EPS_SIM) + bv);
-    alpha[r] = a;
-    dwdb_rows[r] = dw;
-    dwdb_rows[Bl + r] = db;
+    alpha[r] = wv * (pdsum - rd * tail);
+    dwdb_rows[r] = pdsum - (rd + EPS_SIM) * tail;
+    dwdb_rows[Bl + r] = -tail;
   }
-  // G1_r = sum_k dcos_off[r,k] C^_k: lanes over d (4 each), even / odd speakers in two
+  // G1_r = sum_k dcos_off[r,k] C^_k: lanes over d (4 each, D <= 256), even / odd speakers in two
   // accumulators, added at the end
   __builtin_amdgcn_wave_barrier();
   const float* vr = Vs + w * N;
-  for (int c = lane * 4; c < D; c += 256) {
-    float4 g0 = float4{0.f, 0.f, 0.f, 0.f}, g1 = g0;
-    int k = 0;
+  const int c = lane * 4;
+  const bool cok = live && c < D;
+  float4 g0 = float4{0.f, 0.f, 0.f, 0.f}, g1 = g0;
+  auto g1_acc = [&](int ka, int kb, int k0) {  // speakers [ka, kb), tile in LDS from speaker k0
+    int k = ka;
 #pragma unroll 4
-    for (; k + 1 < N; k += 2) {
+    for (; k + 1 < kb; k += 2) {
       const float d0 = vr[k], d1 = vr[k + 1];
-      const float4 c0 = *reinterpret_cast<const float4*>(Cs + k * LDC + c);
-      const float4 c1 = *reinterpret_cast<const float4*>(Cs + (k + 1) * LDC + c);
+      const float4 c0 = *reinterpret_cast<const float4*>(Cs + (k - k0) * LDC + c);
+      const float4 c1 = *reinterpret_cast<const float4*>(Cs + (k + 1 - k0) * LDC + c);
       g0.x += d0 * c0.x;
       g0.y += d0 * c0.y;
       g0.z += d0 * c0.z;
@@ -656,16 +685,39 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
       g1.z += d1 * c1.z;
       g1.w += d1 * c1.w;
     }
-    if (k < N) {
+    if (k < kb) {
       const float d0 = vr[k];
-      const float4 c0 = *reinterpret_cast<const float4*>(Cs + k * LDC + c);
+      const float4 c0 = *reinterpret_cast<const float4*>(Cs + (k - k0) * LDC + c);
       g0.x += d0 * c0.x;
       g0.y += d0 * c0.y;
       g0.z += d0 * c0.z;
       g0.w += d0 * c0.w;
     }
-    *reinterpret_cast<float4*>(G1 + (long)r * D + c) = float4{g0.x + g1.x, g0.y + g1.y, g0.z + g1.z, g0.w + g1.w};
+  };
+  if constexpr (NH == 2) {
+    if (cok) g1_acc(0, N, 0);
+  } else {
+    if (cok) g1_acc(GF_TILE, N, GF_TILE);  // tile 1 is resident
+    __syncthreads();
+    stage(0);
+    __syncthreads();
+    if (cok) g1_acc(0, GF_TILE, 0);
   }
+  if (cok) *reinterpret_cast<float4*>(G1 + (long)r * D + c) = float4{g0.x + g1.x, g0.y + g1.y, g0.z + g1.z, g0.w + g1.w};
+}
+
+// launch F2 for N speakers (<= GF_NMAX)
+static void launch_rows(int Bl, int M, int N, int D, int Np, int s0, const Ge2eWs& ws, const float* w, const float* b,
+                        float* per, hipStream_t stream) {
+  const int NT = N <= GF_TILE ? N : GF_TILE;
+  const size_t lds = ((size_t)NT * (D + 4) + GF_ROWW * (size_t)D + GF_ROWW * (size_t)N) * sizeof(float);
+  const dim3 grid((Bl + GF_ROWW - 1) / GF_ROWW), block(64 * GF_ROWW);
+  if (N <= GF_TILE)
+    hipLaunchKernelGGL(ge2e_rows_kernel<2>, grid, block, lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N, D, Np, s0,
+                       w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1);
+  else
+    hipLaunchKernelGGL(ge2e_rows_kernel<4>, grid, block, lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N, D, Np, s0,
+                       w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1);
 }
 
 // F3: workgroup (speaker k, d slice q of 64), GF_COLW waves: beta_k, dC^_k[slice], dC_k[slice],
@@ -836,9 +888,7 @@ extern "C" int sv_ge2e_train(const float* E, int N, int M, int D, const float* w
   hipLaunchKernelGGL(ge2e_prep_kernel, dim3(N), dim3(256), 0, stream, E, M, D, ws.Chat, ws.Cn, ws.Ehat, ws.Uhat,
                      ws.En, ws.Un, ws.rawd, nullptr);
   SV_LAUNCH_CHECK();
-  const size_t lds = ((size_t)N * (D + 4) + GF_ROWW * (size_t)D + GF_ROWW * (size_t)N) * sizeof(float);
-  hipLaunchKernelGGL(ge2e_rows_kernel, dim3((Bl + GF_ROWW - 1) / GF_ROWW), dim3(64 * GF_ROWW), lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N,
-                     D, Np, 0, w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1);
+  launch_rows(Bl, M, N, D, Np, 0, ws, w, b, per, stream);
   SV_LAUNCH_CHECK();
   hipLaunchKernelGGL(ge2e_cols_kernel<false>, dim3(N, (D + 63) / 64), dim3(64 * GF_COLW), 0, stream, Bl, M, N, D, Np, ws.Chat, ws.Cn,
                      ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.G1, per,
@@ -876,10 +926,7 @@ extern "C" int sv_ge2e_shard_rows(int N_local, int M, int D, int spk_offset, int
   const int Bl = N_local * M, Np = (N + 3) & ~3;
   hipLaunchKernelGGL(ge2e_centroid_kernel, dim3(Np), dim3(256), 0, stream, ssum_all, N, M, D, ws.Chat, ws.Cn);
   SV_LAUNCH_CHECK();
-  const size_t lds = ((size_t)N * (D + 4) + GF_ROWW * (size_t)D + GF_ROWW * (size_t)N) * sizeof(float);
-  hipLaunchKernelGGL(ge2e_rows_kernel, dim3((Bl + GF_ROWW - 1) / GF_ROWW), dim3(64 * GF_ROWW), lds, stream, ws.Chat,
-                     ws.Ehat, ws.rawd, Bl, M, N, D, Np, spk_offset, w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd,
-                     ws.dwdb_rows, ws.G1);
+  launch_rows(Bl, M, N, D, Np, spk_offset, ws, w, b, per, stream);
   SV_LAUNCH_CHECK();
   // the padding rows of dC^ (speakers N .. Np-1) stay zero through the all-reduce
   if (Np > N) {
@@ -935,9 +982,9 @@ __global__ __launch_bounds__(256) void ge2e_calc_loss_kernel(const float* __rest
   for (int k = lane; k < K; k += 64) mx = fmaxf(mx, s[k]);
   mx = fmaxf(wave_max(mx), 0.f);
   float z = 0.f;
-  for (int k = lane; k < K; k += 64) z += __expf(s[k] - mx);
+  for (int k = lane; k < K; k += 64) z += expf(s[k] - mx);
   z = wave_sum(z);
-  if (lane == 0) per[r] = mx + logf(z + EPS_LOG * __expf(-mx)) - s[r / M];
+  if (lane == 0) per[r] = mx + logf(z + EPS_LOG * expf(-mx)) - s[r / M];
 }
 
 extern "C" int sv_ge2e_centroids(const float* E, int N, int M, int D, float* C, hipStream_t stream) {
@@ -1099,11 +1146,11 @@ __global__ __launch_bounds__(256) void ge2e_calc_loss_bwd_kernel(const float* __
   for (int k = lane; k < K; k += 64) mx = fmaxf(mx, s[k]);
   mx = fmaxf(wave_max(mx), 0.f);
   float z = 0.f;
-  for (int k = lane; k < K; k += 64) z += __expf(s[k] - mx);
+  for (int k = lane; k < K; k += 64) z += expf(s[k] - mx);
   z = wave_sum(z);
-  const float inv = 1.0f / (z + EPS_LOG * __expf(-mx));
+  const float inv = 1.0f / (z + EPS_LOG * expf(-mx));
   const float g = (gloss ? *gloss : 0.f) + (gper ? gper[r] : 0.f);
-  for (int k = lane; k < K; k += 64) dS[(long)r * K + k] = g * (__expf(s[k] - mx) * inv - (k == j ? 1.f : 0.f));
+  for (int k = lane; k < K; k += 64) dS[(long)r * K + k] = g * (expf(s[k] - mx) * inv - (k == j ? 1.f : 0.f));
 }
 
 extern "C" int sv_ge2e_centroids_bwd(const float* dC, int N, int M, int D, float* dE, hipStream_t stream) {

@@ -508,8 +508,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
 constexpr int PH_BM = 32;                      // rows of a half
 
 // the helper (prefetch) workgroups of the backward: step s's operands (activations, c_{s-1}, dh_up)
-// of the XCD group's tiles, once that group's first row block has finished half 0 of step s + 2 --
-// a step ahead of the compute waves' own LDS-DMA of them (issued at the end of step s + 1)
+// of the XCD group's tiles, once that group's first row block has finished half 0 of step
+// s + SV_PF32_AHEAD -- ahead of the compute waves' own LDS-DMA of them (issued at the end of step s + 1)
+#ifndef SV_PF32_AHEAD
+#define SV_PF32_AHEAD 2
+#endif
 __device__ void pf32_bwd_prefetch(const float* acts, const float* c_tm, const float* dhup, int up_full, int T, int B,
                                   int H, const unsigned* cnt, int nub, int ncomp, int npf, const unsigned* status,
                                   unsigned limit, char* scratch) {
@@ -523,9 +526,9 @@ __device__ void pf32_bwd_prefetch(const float* acts, const float* c_tm, const fl
   int* skip = reinterpret_cast<int*>(scratch + 4096);
   for (int s = T - 1; s >= 0; --s) {
     if (tid == 0) {
-      if (s + 2 <= T - 1) {
+      if (s + SV_PF32_AHEAD <= T - 1) {
         unsigned spins = 0;
-        const unsigned target = (unsigned)nub * (unsigned)(T - 1 - (s + 2) + 1);
+        const unsigned target = (unsigned)nub * (unsigned)(T - 1 - (s + SV_PF32_AHEAD) + 1);
         while (__hip_atomic_load(c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
                !__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) && ++spins < limit)
           __builtin_amdgcn_s_sleep(8);
@@ -651,7 +654,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
   __syncthreads();
 #endif
   load_ew(T - 1, 0);
-  float dbs = 0.f;  // threads < 128: bias-gradient partial of gate column tid over t and the row block
+  // threads < 128: bias-gradient partial of gate column tid over t and the row block, accumulated in
+  // fp64 (320 fp32 half-step sums of a cancelling sum: in fp32 the c2 bias gradients were 8e-6 off)
+  double dbs = 0.0;
 #ifdef SV_PF32_STAMP  // A/B stamp builds only: wave 0's cycles per phase, summed over the half-steps of t < T-1
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tl = 0;
   auto stamp = [&](int i) {
@@ -815,7 +820,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
       PB_STAMP(5);  // 5: off-chain (bias partials, dG / dG^T stores, next operand DMA issue)
     }
   }
-  if (dbp && tid < 4 * PF_U) dbp[(long)rb * 4 * H + (long)(tid >> 5) * H + j0 + (tid & 31)] = dbs;
+  if (dbp && tid < 4 * PF_U) dbp[(long)rb * 4 * H + (long)(tid >> 5) * H + j0 + (tid & 31)] = (float)dbs;
 #ifdef SV_PF32_STAMP
 #ifdef SV_PF32_WAVE_STAMP  // every wave's phases, workgroups 0-127: slot 512 + 4 wg + wave
   if (lane == 0 && blockIdx.x < SV_NSTAMP_WG / 8) {

@@ -12,9 +12,9 @@ leave-one-out centroids stay local.  Per step:
 With world size 1 this is exactly the single-GPU GE2ELoss.  The per-shard arithmetic is
 a pluggable ``kernels`` object: the HIP kernels (``HipShardKernels``) in production; the
 CPU tests plug in a numpy restatement so the exchange protocol runs under gloo.  For the
-training step (``train``) with global N <= 128 the HIP kernels run in their fused sharded form
-(``HipFusedShard``: prep, rows, finalize around the same two exchanges); larger N (c5's 256)
-take the split kernels.
+training step (``train``) with global N <= 256 the HIP kernels run in their fused sharded form
+(``HipFusedShard``: prep, rows, finalize around the same two exchanges; c5's N = 256 stages the
+centroids in two LDS tiles); larger N take the split kernels.
 """
 from __future__ import annotations
 
@@ -66,7 +66,7 @@ class HipShardKernels:
 
 class HipFusedShard:
     """The fused GE2E kernels in the speaker-sharded form (sv_ge2e_shard_prep / _rows /
-    _finalize): 3 launches + the centroid pass around the two exchanges, for global N <= 128
+    _finalize): 3 launches + the centroid pass around the two exchanges, for global N <= 256
     (sv_ge2e_train_ok); the split kernels above for the rest."""
 
     @staticmethod

@@ -62,7 +62,7 @@ def test_ge2e_golden(tag):
     assert abs(db - o_db) <= 1e-5 * E.shape[0] * E.shape[1]
 
 
-@pytest.mark.parametrize("tag", ["kat0", "n4m5", "n4m5_flat", "n8m10_wb", "n64m10", "n3m2"])
+@pytest.mark.parametrize("tag", ["kat0", "n4m5", "n4m5_flat", "n8m10_wb", "n64m10", "n3m2", "n256m10"])
 def test_ge2e_fused_train_golden(tag):
     """The fused 3-launch training form (sv_ge2e_train) against the reference's golden vectors
     and the split path: loss, per-row loss, dE, dw, db."""

@@ -46,12 +46,27 @@ def test_persistent_bwd_bf16_equals_per_step(dims, N, M, T):
     np.testing.assert_array_equal(b["loss"], a["loss"])
     grads = [k for k in a if k.startswith("grad_")]
     assert len(grads) == 4 * dims[2] + 2
+    # where the dx GEMM over all T (T * B / 256 * H / 256 tiles) exceeds one round of the 256 CUs it
+    # runs in the persistent + stream-K form (gemm_bf16_8qsk_kernel), whose stream-K tiles sum K in
+    # pieces: the layers below the top then differ from the per-step schedule's chunked GEMMs by
+    # fp32 summation order, amplified by their bf16 roundings (bf16-level agreement, as against the
+    # oracle); the top layer, the projection and the loss stay bit-identical
+    H = dims[1]
+    sk = H == 768 and (T * N * M) % 256 == 0 and (T * N * M // 256) * (H // 256) > 256
+    top = f"_l{dims[2] - 1}"
+    worst = 0.0
     for k in grads:
-        if ".bias_" in k:
+        if sk and top not in k and "projection" not in k:
+            dev = float(np.abs(b[k] - a[k]).max()) / max(float(np.abs(a[k]).max()), 1e-30)
+            worst = max(worst, dev)
+            assert dev <= 2e-2, (k, dev)
+        elif ".bias_" in k:
             np.testing.assert_allclose(b[k], a[k], rtol=1e-5, atol=1e-6 * np.abs(a[k]).max(), err_msg=k)
         else:
             np.testing.assert_array_equal(b[k], a[k], err_msg=k)
-    np.testing.assert_allclose(b["flat_p"], a["flat_p"], rtol=0, atol=1e-7)
+    if sk:
+        print(f"\nMEASURED persist_vs_per_step_bf16.T{T}.lower_layer_grad_rel {worst:.2e} (stream-K dx)")
+    np.testing.assert_allclose(b["flat_p"], a["flat_p"], rtol=0, atol=1e-6 if sk else 1e-7)
 
 
 @pytest.mark.parametrize("N,M,T", [(8, 10, 20),    # c4's per-rank shape: 3 x 3 x 24 = 216 workgroups

@@ -4,9 +4,9 @@ ShardedGE2E (sharded_ge2e.py) runs the GE2E kernels per rank around two exchange
 all-gather of the per-speaker sums and a SUM all-reduce of the [dC^ | beta] buffer.  Here the
 ranks are virtual: one process runs every shard's kernels on its own slice of the speakers with
 the shard's speaker offset s0 > 0, and the exchanges are done by hand (concatenation of the
-sums, a plain sum of the reduce buffers).  So the per-shard arithmetic that c5 runs on 8 GPUs
-(global N = 256 > 128: the split kernels sv_ge2e_fwd_rows / bwd_rows / bwd_finalize) and that
-c4 runs (global N = 64: the fused sv_ge2e_shard_prep / _rows / _finalize) is checked against
+sums, a plain sum of the reduce buffers).  So the per-shard arithmetic that c4 and c5 run on 8
+GPUs (global N = 64 and 256: the fused sv_ge2e_shard_prep / _rows / _finalize) and the split
+kernels (sv_ge2e_fwd_rows / bwd_rows / bwd_finalize, any N) are checked against
 the reference's golden vectors (tests/golden/ge2e_n256m10.npz, ge2e_n64m10.npz; reference math
 utils.py:72-132) and the numpy oracle.  Tolerances: loss 1e-4 relative (north_star), dE 1e-4 of
 its largest entry, dw 1e-4, db 1e-5 per row."""
@@ -74,12 +74,14 @@ def test_split_shard_kernels_n256(world):
     _check("n256m10", g, E, w, b, loss, per, dE, dw, db, f"ge2e_split_shards{world}")
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_fused_shard_kernels_n64(world):
+@pytest.mark.parametrize("tag,world", [("n64m10", 2), ("n64m10", 4), ("n64m10", 8),
+                                       ("n256m10", 2), ("n256m10", 4), ("n256m10", 8)])
+def test_fused_shard_kernels(tag, world):
     """The fused sharded form (HipFusedShard: sv_ge2e_shard_prep / _rows / _finalize) that
-    ShardedGE2E.train takes for global N <= 128 (c4: N = 64 over 8 GPUs, 8 speakers per rank)."""
+    ShardedGE2E.train takes for global N <= 256: c4 (N = 64 over 8 GPUs, 8 speakers per rank) and
+    c5 (N = 256: 32 speakers per rank at 8 GPUs, s0 up to 224; the centroids in two LDS tiles)."""
     from pytorch_speaker_verification_amd.sharded_ge2e import HipFusedShard
-    g, E, w, b = _inputs("n64m10")
+    g, E, w, b = _inputs(tag)
     N, M, D = E.shape
     Nl = N // world
     assert HipFusedShard.ok(N, M, D)
@@ -97,4 +99,4 @@ def test_fused_shard_kernels_n64(world):
     dE = torch.cat([f.finalize(shards[r], r * Nl, N, red.clone(), prep[r][1]) for r in range(world)]).cpu().numpy()
     dw = sum(float(r_[3][0]) for r_ in rows)
     db = sum(float(r_[3][1]) for r_ in rows)
-    _check("n64m10", g, E, w, b, loss, per, dE, dw, db, f"ge2e_fused_shards{world}")
+    _check(tag, g, E, w, b, loss, per, dE, dw, db, f"ge2e_fused_shards{world}")

@@ -1,4 +1,6 @@
-"""Speaker-sharded GE2E exchange protocol under gloo, world size 2, on CPU.
+"""Speaker-sharded GE2E exchange protocol under gloo on CPU, at world sizes 2, 4
+and 8: c4's shape (global N = 64, 8 speakers per rank at world 8) and c5's (N = 256, 32 per rank,
+speaker offsets s0 up to 224).
 
 The product's ShardedGE2E runs its real collective sequence (all_gather_into_tensor of speaker
 sums, SUM all_reduce of the centroid-gradient buffer) with the oracle's per-shard numpy kernels
@@ -7,6 +9,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -47,16 +50,16 @@ def _worker(rank, world, port, N, M, D, w, b, q):
         dist.destroy_process_group()
 
 
-def test_sharded_ge2e_gloo_world2():
-    N, M, D, w, b = 8, 5, 16, 7.5, -2.5
-    world = 2
+@pytest.mark.parametrize("world,N,M,D", [(2, 8, 5, 16), (4, 64, 10, 256), (8, 64, 10, 256), (8, 256, 10, 256)])
+def test_sharded_ge2e_gloo(world, N, M, D):
+    w, b = 7.5, -2.5
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, N, M, D, w, b, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
