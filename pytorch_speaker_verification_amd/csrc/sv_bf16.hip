@@ -444,6 +444,49 @@ BPlan plan_bf16(int M, int N, int K) {
   return p;
 }
 
+// stream-K scratch of the persistent + stream-K 8-phase kernel (gemm_bf16_8qsk_kernel): two partial
+// slots of 512 threads x 128 fp32 per workgroup (grid capped at G8_SK_GRID) + the tiles' counters
+constexpr int G8_SK_GRID = 256;
+constexpr size_t G8_SK_SLOT = (size_t)512 * 128 * sizeof(float);
+size_t g8_sk_bytes() { return 2 * G8_SK_GRID * G8_SK_SLOT + G8_SK_GRID * sizeof(unsigned) * 4; }
+// Measured slower and off by default (A/B builds: -DSV_G8_SK=1 / -DSV_G8_SK_DW=1):
+// the dx GEMM's persistent + stream-K form where its tiles exceed one round, and the weight-gradient
+// GEMMs' stream-K form in place of split-K slabs + reduce
+#ifndef SV_G8_SK
+#define SV_G8_SK 0
+#endif
+#ifndef SV_G8_SK_DW
+#define SV_G8_SK_DW 0
+#endif
+#if SV_G8_SK_DW
+// the split-K shapes of plan_bf16 (K = T B weight gradients, fewer tiles than CUs) as ONE stream-K
+// launch: every CU gets an equal run of k-tiles (tile-major), a tile's pieces are summed by its last
+// arriving piece -- no slab buffer, no reduce launch, no idle CUs in a last round (the split-K plan
+// of 7 slabs ran 2 rounds of 252 + 252 workgroups at c3 / c4, then a reduce over 7 slabs)
+template <bool DUAL>
+int launch_g8sk(int M, int N, int K, const bf16_t* A, long lda, const bf16_t* B, long ldb, float* C, long ldc,
+                G256Dual dual, float* C2, long ldc2, void* ws, hipStream_t stream) {
+  const int tiles = (M / G256_BM) * (N / G256_BM), nk = K / G256_BK;
+  const int G = std::min(sv_stream_cus(stream), G8_SK_GRID);
+  if (G <= 0) return -1;
+  G8SK sk;
+  sk.R = tiles / G;
+  sk.rem = tiles % G;
+  sk.L = sk.rem ? (int)(((long)sk.rem * nk + G - 1) / G) : 0;
+  if (sk.rem && (long)sk.L * (G8_SK_MAXSEG - 1) < nk) return -1;  // too many pieces per tile
+  sk.part = static_cast<float*>(ws);
+  sk.cnt = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + 2 * G8_SK_GRID * G8_SK_SLOT);
+  if (sk.rem) {
+    hipError_t e = (hipError_t)sv_zero_counters(sk.cnt, 1, 0, sk.rem, stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL((gemm_bf16_8qsk_kernel<0, DUAL>), dim3(G), dim3(512), G256_LDS, stream, A, lda, B, ldb, C, ldc, M,
+                     N, K, sk, G256AFrag{}, dual, C2, ldc2);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+#endif
+
 template <int BM, int BN, int EPI>
 void launch_bf(const bf16_t* A, long lda, const bf16_t* B, long ldb, void* C, long ldc, long slab, int M, int N, int K,
                int splitk, int kchunk, const float* b0, const float* b1, float beta, hipStream_t s) {
@@ -500,7 +543,8 @@ extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, cons
 // workspace: sv_gemm_bf16_dual_workspace bytes
 size_t sv_gemm_bf16_dual_workspace(int M, int N1, int N2, int K) {
   const BPlan p = plan_bf16(M, N1, K);
-  const size_t fused = p.splitk > 1 ? (size_t)p.splitk * M * (N1 + N2) * sizeof(float) : 0;
+  size_t fused = p.splitk > 1 ? (size_t)p.splitk * M * (N1 + N2) * sizeof(float) : 0;
+  if (SV_G8_SK_DW && p.splitk > 1 && p.bm == G256_BM) fused = std::max(fused, g8_sk_bytes());
   return std::max(fused, std::max(sv_gemm_bf16_workspace(M, N1, K), sv_gemm_bf16_workspace(M, N2, K)));
 }
 int sv_gemm_bf16_dual(int M, int N1, int N2, int K, const bf16_t* A, long lda, const bf16_t* B1, long ldb1, float* C1,
@@ -516,6 +560,13 @@ int sv_gemm_bf16_dual(int M, int N1, int N2, int K, const bf16_t* A, long lda, c
     return sv_gemm_bf16(M, N2, K, A, lda, B2, ldb2, C2, ldc2, nullptr, nullptr, 0.f, workspace, stream);
   }
   const int N = N1 + N2;
+#if SV_G8_SK_DW
+  if (g8_ok(C1, ldc1, nullptr, nullptr) && g8_ok(C2, ldc2, nullptr, nullptr)) {
+    const int rc = launch_g8sk<true>(M, N, K, A, lda, B1, ldb1, C1, ldc1, G256Dual{B2, ldb2, N1}, C2, ldc2, workspace,
+                                     stream);
+    if (rc >= 0) return rc;
+  }
+#endif
   const int tiles = (M / G256_BM) * (N / G256_BM);
   const long slab = (long)M * N;
   hipLaunchKernelGGL((gemm_bf16_8q_kernel<G8_SLAB, 0>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream, A, lda, B1,
@@ -531,7 +582,9 @@ int sv_gemm_bf16_dual(int M, int N1, int N2, int K, const bf16_t* A, long lda, c
 
 extern "C" size_t sv_gemm_bf16_workspace(int M, int N, int K) {
   const BPlan p = plan_bf16(M, N, K);
-  return p.splitk > 1 ? (size_t)p.splitk * M * N * sizeof(float) : 0;
+  if (p.splitk <= 1) return 0;
+  const size_t slabs = (size_t)p.splitk * M * N * sizeof(float);
+  return SV_G8_SK_DW && p.bm == G256_BM ? std::max(slabs, g8_sk_bytes()) : slabs;  // (+ stream-K scratch)
 }
 
 extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, const bf16_t* B, long ldb, float* C,
@@ -550,6 +603,12 @@ extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, cons
       return SV_OK;
     }
     if (!workspace) return SV_EARG;
+#if SV_G8_SK_DW
+    if (beta == 0.f && !bias0 && !bias1 && g8_ok(C, ldc, nullptr, nullptr)) {
+      const int rc = launch_g8sk<false>(M, N, K, A, lda, B, ldb, C, ldc, G256Dual{}, nullptr, 0L, workspace, stream);
+      if (rc >= 0) return rc;
+    }
+#endif
     launch_g256<G256_SLAB, 0>(g8_ok(workspace, N, nullptr, nullptr), dim3(tiles, p.splitk), stream, A, lda, B,
                               ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr, 0.f);
     SV_LAUNCH_CHECK();
@@ -619,14 +678,6 @@ extern "C" int sv_gemm_bf16_bf(int M, int N, int K, const bf16_t* A, long lda, c
 bool gemm_afrag_ok(int T, int B, int N, int H) {
   return gemm256_ok(T * B, N, 4 * H) && B % 32 == 0 && H % G256_BK == 0;
 }
-// stream-K scratch of the dx GEMM's persistent form (gemm_bf16_8qsk_kernel): two partial slots of
-// 512 threads x 128 fp32 per workgroup (grid capped at G8_SK_GRID) + the stream-K tiles' counters
-constexpr int G8_SK_GRID = 256;
-constexpr size_t G8_SK_SLOT = (size_t)512 * 128 * sizeof(float);
-size_t g8_sk_bytes() { return 2 * G8_SK_GRID * G8_SK_SLOT + G8_SK_GRID * sizeof(unsigned) * 4; }
-#ifndef SV_G8_SK
-#define SV_G8_SK 1  // the dx GEMM's persistent + stream-K form where its tiles exceed one round (0: A/B)
-#endif
 // (the split-K plan of sv_gemm_bf16 for the same shape).  More tiles than one round of CUs (the c3
 // dx: 1200 tiles): the persistent + stream-K kernel when `skws` (g8_sk_bytes) is given -- its
 // stream-K tiles sum K in pieces, so at those shapes the per-step schedule's chunked dx GEMMs
@@ -638,8 +689,9 @@ int gemm_bf16_afrag(int T, int B, int H, int N, const bf16_t* dgf, int bm, const
   const long fs = (long)((B + bm - 1) / bm) * bm * 4 * H;
   const G256AFrag af{dgf, fs, B, bm, H};
   const BPlan p = plan_bf16(M, N, K);
+#if SV_G8_SK
   const int G = std::min(sv_stream_cus(stream), G8_SK_GRID), nk = K / G256_BK;
-  if (SV_G8_SK && p.splitk == 1 && skws && G > 0 && tiles > G && g8_ok(C, ldc, nullptr, nullptr)) {
+  if (p.splitk == 1 && skws && G > 0 && tiles > G && g8_ok(C, ldc, nullptr, nullptr)) {
     G8SK sk;
     sk.R = tiles / G;
     sk.rem = tiles % G;
@@ -657,6 +709,9 @@ int gemm_bf16_afrag(int T, int B, int H, int N, const bf16_t* dgf, int bm, const
       return SV_OK;
     }
   }
+#else
+  (void)skws;
+#endif
   if (p.splitk == 1) {
     launch_g256<G256_STORE, 1>(g8_ok(C, ldc, nullptr, nullptr), dim3(tiles, 1), stream, nullptr, 0L, Bop, ldb, C,
                                ldc, 0L, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
@@ -997,7 +1052,7 @@ static size_t bbwd_scratch(int L, int T, int B, int H) {
 }
 extern "C" size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H) {
   const size_t per = (size_t)L * carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
-  return per + bbwd_scratch(L, T, B, H) + (sv_persist_bwd_fits(B, H, 1 << 30) ? g8_sk_bytes() : 0);
+  return per + bbwd_scratch(L, T, B, H) + (SV_G8_SK && sv_persist_bwd_fits(B, H, 1 << 30) ? g8_sk_bytes() : 0);
 }
 
 extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const bf16_t* const* xT, const long* ld_xT,

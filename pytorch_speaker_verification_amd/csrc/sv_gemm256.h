@@ -768,13 +768,17 @@ struct G8SK {
   float* part;      // 2 G partial slots of 512 threads x 128 fp32 (slot 2 i: the piece opening i's range)
   unsigned* cnt;    // [rem] arrival counters, zero at the launch
 };
-constexpr int G8_SK_MAXSEG = 4;  // pieces per stream-K tile (the host checks: L * (MAXSEG - 1) >= nk)
+constexpr int G8_SK_MAXSEG = 8;  // pieces per stream-K tile (the host checks: L * (MAXSEG - 1) >= nk)
 
-template <int AF>
+// DUAL: C = A . [B ; B2]^T over N = n1 + n2 columns, column tiles at and past n1 reading B2 and
+// stored to C2 (ldc2) -- the backward's dW_hh and dW_ih of one layer in one pass over dG^T
+template <int AF, bool DUAL = false>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_8qsk_kernel(const bf16_t* __restrict__ A, long lda,
                                                                const bf16_t* __restrict__ B, long ldb,
                                                                float* __restrict__ C, long ldc, int M, int N, int K,
-                                                               G8SK sk, G256AFrag af = G256AFrag{}) {
+                                                               G8SK sk, G256AFrag af = G256AFrag{},
+                                                               G256Dual dual = G256Dual{}, float* __restrict__ C2 = nullptr,
+                                                               long ldc2 = 0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ unsigned arrived;
   constexpr unsigned SLOT = 512u * 128u * 4u;  // bytes per partial slot
@@ -826,7 +830,22 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qsk_kernel(const bf16_t* __
     } else {
       sa.init(A, lda, tm * G256_BM, ka * G256_BK, tid);
     }
-    sb.init(B, ldb, tn * G256_BM, ka * G256_BK, tid);
+    if (DUAL && tn * G256_BM >= dual.n1)
+      sb.init(dual.B2, dual.ldb2, tn * G256_BM - dual.n1, ka * G256_BK, tid);
+    else
+      sb.init(B, ldb, tn * G256_BM, ka * G256_BK, tid);
+  };
+  // output of column tile tn_: C (tile tn_) or, past n1 in the DUAL form, C2 (tile tn_ - n1 / 256)
+  auto out_of = [&](int tn_, float*& Co, long& ldco, int& tno) {
+    if (DUAL && tn_ * G256_BM >= dual.n1) {
+      Co = C2;
+      ldco = ldc2;
+      tno = tn_ - dual.n1 / G256_BM;
+    } else {
+      Co = C;
+      ldco = ldc;
+      tno = tn_;
+    }
   };
   auto stage = [&](int kt) { return smem + ((kt + base) & 1) * 2 * OPB; };
   auto fill_a = [&](int kt, int i) {
@@ -968,8 +987,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qsk_kernel(const bf16_t* __
 #pragma unroll
       for (int i = 0; i < 4; ++i) fill_a(0, i);
     }
+    float* Co;
+    long ldco;
+    int tno;
+    out_of(tn0, Co, ldco, tno);
     if (ka0 == 0 && kb0 == nk) {  // a whole tile
-      g8_epilogue<G8_STORE>(acc, C, ldc, 0L, tm0, tn0, wr, wc, lane, nullptr, nullptr, 0.f);
+      g8_epilogue<G8_STORE>(acc, Co, ldco, 0L, tm0, tno, wr, wc, lane, nullptr, nullptr, 0.f);
     } else {
       // a piece of stream-K tile j0: the tile's pieces are workgroups s0 .. s1's (k order)
       const int s0 = (int)(((long)j0 * nk) / sk.L), s1 = (int)(((long)j0 * nk + nk - 1) / sk.L);
@@ -1001,8 +1024,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qsk_kernel(const bf16_t* __
             for (int wg = s0 + 1; wg <= s1; ++wg)
               sum += __builtin_bit_cast(g8_f32x4, __builtin_amdgcn_raw_buffer_load_b128(rpart, slot(wg) + off, 0, 16));
             const long row = (long)tm0 * G256_BM + wr * 128 + 16 * i + fr;
-            const int col = tn0 * G256_BM + wc * 64 + 16 * jj + 4 * fq;
-            *reinterpret_cast<g8_f32x4*>(C + row * ldc + col) = sum;
+            const int col = tno * G256_BM + wc * 64 + 16 * jj + 4 * fq;
+            *reinterpret_cast<g8_f32x4*>(Co + row * ldco + col) = sum;
           }
         if (tid == 0) __hip_atomic_store(sk.cnt + j0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }

@@ -513,6 +513,13 @@ constexpr int PH_BM = 32;                      // rows of a half
 #ifndef SV_PF32_AHEAD
 #define SV_PF32_AHEAD 2
 #endif
+#ifndef SV_PF32_DGT_SC1  // the backward's dG^T stores written through with sc1 (r05: 7.62 -> 7.39 GB per
+#define SV_PF32_DGT_SC1 1   // launch of fetch + write, time unchanged; 0: A/B)
+#endif
+#ifndef SV_PF32_PF_HALF  // the helpers' trigger: half 1 of step s + SV_PF32_AHEAD (r05: 7.42 -> 6.74 GB per launch,
+                         // time unchanged: the lines land closer to their use and fewer are evicted first; 0: A/B)
+#define SV_PF32_PF_HALF 1
+#endif
 __device__ void pf32_bwd_prefetch(const float* acts, const float* c_tm, const float* dhup, int up_full, int T, int B,
                                   int H, const unsigned* cnt, int nub, int ncomp, int npf, const unsigned* status,
                                   unsigned limit, char* scratch) {
@@ -521,7 +528,7 @@ __device__ void pf32_bwd_prefetch(const float* acts, const float* c_tm, const fl
   int l0, l1;
   persist_xcd_tiles(x, ncomp, l0, l1);
   const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
-  const unsigned* c0 = cnt + (l0 / nub) * 2 * SV_PCNT_STRIDE;  // (row block, half 0) of the group's first tile
+  const unsigned* c0 = cnt + ((l0 / nub) * 2 + SV_PF32_PF_HALF) * SV_PCNT_STRIDE;  // (row block, half) of the group's first tile
   char* dst = scratch + g * 1024;
   int* skip = reinterpret_cast<int*>(scratch + 4096);
   for (int s = T - 1; s >= 0; --s) {
@@ -798,6 +805,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
           *reinterpret_cast<f32x4*>(dp + q * H) = *reinterpret_cast<const f32x4*>(dgs + erow * LDG + q * PF_U + 4 * quad);
       }
 #ifndef SV_PF32_NODGT  // A/B diagnostic (results invalid): no dG^T stores
+#if SV_PF32_DGT_SC1
+      // sc1 stores: written through and dropped from this XCD's L2 (MI355X_MICROARCH.md, stores of
+      // each flavour), so the 48 KB per tile per step the dW GEMMs read back much later do not evict
+      // the lines the helper workgroups prefetched
+      const __amdgpu_buffer_rsrc_t rdt = sv_rsrc(dgT, (unsigned)((long)4 * H * lddgT * 4));
+#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) {  // 128 gate-unit rows x 8 pieces of 4 batch columns
         const int p = tid + 256 * i, gu = p >> 3, c = p & 7, gbc = b0 + 4 * c;
@@ -806,7 +819,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (gbc + e >= B) v[e] = 0.f;
-          *reinterpret_cast<f32x4*>(dgT + ((long)(gu >> 5) * H + j0 + (gu & 31)) * lddgT + (long)t * Bp + gbc) = v;
+          const long eo = ((long)(gu >> 5) * H + j0 + (gu & 31)) * lddgT + (long)t * Bp + gbc;
+#if SV_PF32_DGT_SC1
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rdt, (unsigned)(eo * 4), 0, 16 /* sc1 */);
+#else
+          *reinterpret_cast<f32x4*>(dgT + eo) = v;
+#endif
         }
       }
 #endif
