@@ -277,7 +277,8 @@ __global__ __launch_bounds__(256) void ge2e_dwdb_kernel(const float* __restrict_
 //   dE_r  = (G1_r + dcos_d U^_r - alpha_r E^_r [|E|>eps]) / max(|E_r|, eps)
 //           + dC_j / M + (sum_i' dU_ji' - dU_r) / (M - 1)
 // where dcos_d = w dS[r, s(r)] is recovered from alpha_r's definition inputs.
-__global__ __launch_bounds__(256) void ge2e_finalize_kernel(
+// any M (the split path's general form): one thread per d walks the speaker's M rows twice
+__global__ __launch_bounds__(256) void ge2e_finalize_serial_kernel(
     int M, int D, int s0, const float* __restrict__ dchat, const float* __restrict__ beta,
     const float* __restrict__ Chat, const float* __restrict__ Cn, const float* __restrict__ Ehat,
     const float* __restrict__ Uhat, const float* __restrict__ En, const float* __restrict__ Un,
@@ -312,6 +313,61 @@ __global__ __launch_bounds__(256) void ge2e_finalize_kernel(
       dE[rd] = gE + dC * invM + (sumdU - dU) * invm1;
     }
   }
+}
+
+#define GF_MMAX_FIN 16  // utterances per speaker of the one-pass finalize (one wave each)
+__global__ __launch_bounds__(1024) void ge2e_finalize_kernel(
+    int M, int D, int s0, const float* __restrict__ dchat, const float* __restrict__ beta,
+    const float* __restrict__ Chat, const float* __restrict__ Cn, const float* __restrict__ Ehat,
+    const float* __restrict__ Uhat, const float* __restrict__ En, const float* __restrict__ Un,
+    const float* __restrict__ rawd, const float* __restrict__ dcd, const float* __restrict__ alpha,
+    const float* __restrict__ G1, float* __restrict__ dE) {
+  // workgroup (speaker j, 64-wide d slice q), wave i = the speaker's utterance i (M <= 16 waves):
+  // every (row, d) of the slice in one pass, the leave-one-out sum of dU through LDS (the cols
+  // kernel's epilogue; the former one-thread-per-d form walked the M rows twice, serially)
+  __shared__ float dUs[GF_MMAX_FIN][64];
+  const int j = blockIdx.x, q = blockIdx.y;
+  const int lane = threadIdx.x & 63, i = threadIdx.x >> 6;
+  const int sg = s0 + j;
+  const int d = q * 64 + lane;
+  const bool mine = d < D && i < M;
+  const int r = j * M + i;
+  const long rd = (long)r * D + d;
+  float dU = 0.f, gE = 0.f;
+  if (mine) {
+    const float un = Un[r], en = En[r], dd = dcd[r];
+    const float iu = 1.0f / fmaxf(un, EPS_COS);
+    const float pu = un > EPS_COS ? 1.f : 0.f;
+    const float eh = Ehat[rd], uh = Uhat[rd];
+    dU = dd * (eh - rawd[r] * uh * pu) * iu;
+    const float ie = 1.0f / fmaxf(en, EPS_COS);
+    const float pe = en > EPS_COS ? 1.f : 0.f;
+    gE = (G1[rd] + dd * uh - alpha[r] * eh * pe) * ie;
+    dUs[i][lane] = dU;
+  }
+  __syncthreads();
+  if (!mine) return;
+  const float cn = Cn[sg];
+  const float icn = 1.0f / fmaxf(cn, EPS_COS);
+  const float pc = cn > EPS_COS ? 1.f : 0.f;
+  const long cd = (long)sg * D + d;
+  const float dC = (dchat[cd] - beta[sg] * Chat[cd] * pc) * icn;
+  float sumdU = 0.f;
+  for (int k = 0; k < M; ++k) sumdU += dUs[k][lane];
+  const float invM = 1.0f / (float)M, invm1 = 1.0f / (float)(M - 1);
+  dE[rd] = gE + dC * invM + (sumdU - dU) * invm1;
+}
+
+// dE of a shard's speakers from the reduced [dC^ | beta]: the one-pass 2-D form up to GF_MMAX_FIN
+// utterances per speaker, else the serial form
+static void launch_finalize(int N_local, int M, int D, int s0, const float* dchat, const float* beta, const Ge2eWs& ws,
+                            const float* dcd, float* dE, hipStream_t stream) {
+  if (M <= GF_MMAX_FIN)
+    hipLaunchKernelGGL(ge2e_finalize_kernel, dim3(N_local, (D + 63) / 64), dim3(64 * M), 0, stream, M, D, s0, dchat, beta,
+                       ws.Chat, ws.Cn, ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, dcd, ws.alpha, ws.G1, dE);
+  else
+    hipLaunchKernelGGL(ge2e_finalize_serial_kernel, dim3(N_local), dim3(256), 0, stream, M, D, s0, dchat, beta, ws.Chat,
+                       ws.Cn, ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, dcd, ws.alpha, ws.G1, dE);
 }
 
 // dcos on the diagonal (w dS[r, s(r)]) for the finalize step, recomputed from logz
@@ -412,8 +468,7 @@ extern "C" int sv_ge2e_bwd_finalize(int N_local, int M, int D, int spk_offset, i
                                     const float* beta, float* dE, float* workspace, hipStream_t stream) {
   if (N_local <= 0 || M < 2 || D <= 0 || !dchat || !beta || !dE || !workspace) return SV_EARG;
   const Ge2eWs ws = carve(workspace, N_local, M, D, N);
-  hipLaunchKernelGGL(ge2e_finalize_kernel, dim3(N_local), dim3(256), 0, stream, M, D, spk_offset, dchat, beta, ws.Chat,
-                     ws.Cn, ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, ws.dwdb_rows, ws.alpha, ws.G1, dE);
+  launch_finalize(N_local, M, D, spk_offset, dchat, beta, ws, ws.dwdb_rows, dE, stream);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }
@@ -560,9 +615,20 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
   float* Vs = Es + GF_ROWW * D;          // [GF_ROWW][N]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int D4 = D / 4;
-  // global -> LDS copy of C^ rows k0 .. (distinct address spaces: the unrolled loads issue back to back)
+  // global -> LDS copy of C^ rows k0 .. .  D = 256 (every c1-c5 shape): by LDS-DMA, one 1 KB row per
+  // wave instruction (no VGPR round trip, every row in flight at once; the register copy below kept
+  // ~8 loads per lane in flight and took ~12 us per 128-speaker tile at c5's rank shape), waited for
+  // by the caller's vmcnt(0) + barrier; else through registers (distinct address spaces: the unrolled
+  // loads issue back to back)
   auto stage = [&](int k0) {
-    const int NQ = min(NT, N - k0) * D4;
+    const int nk = min(NT, N - k0);
+    if (D == 256) {
+      for (int row = w; row < nk; row += GF_ROWW)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(Chat + (long)(k0 + row) * D + lane * 4),
+                                         (__attribute__((address_space(3))) void*)(Cs + row * LDC), 16, 0, 0);
+      return;
+    }
+    const int NQ = nk * D4;
 #pragma unroll 8
     for (int q = tid; q < NQ; q += 64 * GF_ROWW) {
       const int row = q / D4, col = (q - row * D4) * 4;
@@ -576,6 +642,7 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
   if (live)
     for (int c = lane * 4; c < D; c += 256)
       *reinterpret_cast<float4*>(Es + w * D + c) = *reinterpret_cast<const float4*>(Ehat + (long)r * D + c);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA of C^ landed
   __syncthreads();
   if constexpr (NH == 2) {
     if (!live) return;  // (no later workgroup barrier)
@@ -600,6 +667,7 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
     if (t > 0) {  // NH == 4: the second tile
       __syncthreads();
       stage(t * GF_TILE);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
 #pragma unroll
@@ -700,6 +768,7 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
     if (cok) g1_acc(GF_TILE, N, GF_TILE);  // tile 1 is resident
     __syncthreads();
     stage(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (cok) g1_acc(0, GF_TILE, 0);
   }
@@ -945,9 +1014,7 @@ extern "C" int sv_ge2e_shard_finalize(int N_local, int M, int D, int spk_offset,
   if (!red || !dE || !workspace || N_local <= 0 || M < 2 || D <= 0) return SV_EARG;
   const Ge2eWs ws = carve(workspace, N_local, M, D, N);
   const int Np = (N + 3) & ~3;
-  hipLaunchKernelGGL(ge2e_finalize_kernel, dim3(N_local), dim3(256), 0, stream, M, D, spk_offset, red,
-                     red + (size_t)Np * D, ws.Chat, ws.Cn, ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, ws.dcd, ws.alpha,
-                     ws.G1, dE);
+  launch_finalize(N_local, M, D, spk_offset, red, red + (size_t)Np * D, ws, ws.dcd, dE, stream);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }
