@@ -598,6 +598,9 @@ __global__ __launch_bounds__(256) void ge2e_prep_kernel(const float* __restrict_
 // tile 1 while it is resident, then tile 0 again -- still fp32 throughout.
 #define GF_ROWW 4
 #define GF_TILE 128
+#ifndef SV_GE2E_DIAG  // A/B diagnostics (results invalid): 1 = no G1 pass, 2 = no tile-0 restage
+#define SV_GE2E_DIAG 0
+#endif
 template <int NH>
 __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __restrict__ Chat, const float* __restrict__ Ehat,
                                                         const float* __restrict__ rawd, int Bl, int M, int N, int D,
@@ -764,10 +767,10 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
   };
   if constexpr (NH == 2) {
     if (cok) g1_acc(0, N, 0);
-  } else {
+  } else if (SV_GE2E_DIAG != 1) {
     if (cok) g1_acc(GF_TILE, N, GF_TILE);  // tile 1 is resident
     __syncthreads();
-    stage(0);
+    if (SV_GE2E_DIAG != 2) stage(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (cok) g1_acc(0, GF_TILE, 0);
@@ -775,9 +778,201 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
   if (cok) *reinterpret_cast<float4*>(G1 + (long)r * D + c) = float4{g0.x + g1.x, g0.y + g1.y, g0.z + g1.z, g0.w + g1.w};
 }
 
+// F2 for 128 < N <= 256 and D = 256 (c5's global N): 4 rows per workgroup, FOUR waves per row
+// (16 waves), so each wave walks a quarter of the row's work -- the one-wave-per-row form above
+// (ge2e_rows_kernel<4>) is latency-bound at a c5 rank's 320 rows (25 us: 256 cosine dot products
+// and 256 G1 terms in one wave, plus a third tile staging).  The speakers pass through LDS in two
+// chunks of 128 (fp32, 133 KB), each staged once by LDS-DMA; per chunk the cosines, then the
+// chunk's share of
+// G1 = sum_{k != j} dcos_k C^_k accumulated online (flash-attention style: weights e^{S_k - m}
+// against the running row max m, the partial sum rescaled by e^{m_old - m} when a chunk raises it,
+// finally scaled by w e^{m - lz}).
+//   cosines: wave p of the row takes speakers 128 c + 32 p + (lane & 31), the two lane halves
+//     taking d halves, joined by one shuffle (lanes < 32 hold the speaker);
+//   row max / sums: per-wave partials met in LDS; G1: wave p takes d = 64 p + lane.
+// FUSEC (sharded form): the chunks hold the all-gathered speaker SUMS s_k; the centroid scale
+// c_k = 1 / (M max(|s_k / M|, eps)) comes from |s_k|^2 summed in the same loop as the cosine, so
+// cos = (E^ . s_k) c_k and the G1 weights carry c_k -- no normalisation pass and no centroid
+// launch; the workgroups also write C^ and |C| of the shard's own speakers for the finalize step.
+// (Measured: 64-speaker chunks double-buffered, the next chunk's DMA under the current chunk's
+// work: 27.3 us against 24.3 at the c5 rank shape -- the chunks' extra barriers cost more than the
+// staging latency they hide; a third staging of the first tile for G1 instead of the online sum:
+// 19.5 us + the centroid launch.)
+constexpr int GF_CH = 128;  // speakers per chunk
+template <bool FUSEC>
+__global__ __launch_bounds__(1024) void ge2e_rows16_kernel(const float* __restrict__ Csrc,
+                                                          const float* __restrict__ Ehat,
+                                                          const float* __restrict__ rawd, int Bl, int M, int N,
+                                                          int ldc, int s0, const float* __restrict__ wp,
+                                                          const float* __restrict__ bp, float* __restrict__ per,
+                                                          float* __restrict__ cos, float* __restrict__ dcos,
+                                                          float* __restrict__ alpha, float* __restrict__ dcd,
+                                                          float* __restrict__ dwdb_rows, float* __restrict__ G1,
+                                                          float* __restrict__ Chat_out, float* __restrict__ Cn_out) {
+  constexpr int D = 256, LDC = D + 4, RW = 4, NCM = GF_NMAX / GF_CH;
+  extern __shared__ __attribute__((aligned(16))) float gsm[];
+  float* Cb = gsm;                    // [GF_CH][LDC]
+  float* Es = Cb + GF_CH * LDC;       // [RW][D]
+  float* Vs = Es + RW * D;            // [RW][GF_CH] G1 weights of the current chunk
+  float* red = Vs + RW * GF_CH;       // [RW][4 waves][4]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = w >> 2, pq = w & 3;   // row of the workgroup, quarter
+  const int r = blockIdx.x * RW + i;
+  const bool live = r < Bl;
+  const int nc = (N + GF_CH - 1) / GF_CH;
+  auto rows_of = [&](int c) { return min(GF_CH, N - c * GF_CH); };
+  auto stage = [&](int c) {  // chunk c -> LDS: this wave's rows w, w + 16, ...
+    const int nk = rows_of(c);
+    for (int row = w; row < nk; row += 16)
+      __builtin_amdgcn_global_load_lds(
+          (__attribute__((address_space(1))) void*)(Csrc + (long)(c * GF_CH + row) * D + lane * 4),
+          (__attribute__((address_space(3))) void*)(Cb + row * LDC), 16, 0, 0);
+  };
+  float* rr = red + (i * 4 + pq) * 4;
+  auto row_sum = [&](float v, int slot) {  // the row's 4 waves' values, added in wave order
+    if (lane == 0) rr[slot] = v;
+    __syncthreads();
+    return (red[(i * 4) * 4 + slot] + red[(i * 4 + 1) * 4 + slot]) + (red[(i * 4 + 2) * 4 + slot] + red[(i * 4 + 3) * 4 + slot]);
+  };
+  if (live) Es[i * D + pq * 64 + lane] = Ehat[(long)r * D + pq * 64 + lane];
+  const float wv = *wp, bv = *bp;
+  const int sg = s0 + (live ? r : 0) / M;
+  const float rd = live ? rawd[r] : 0.f;
+  const int kq = 32 * pq + (lane & 31), dq = (lane >> 5) * 128;
+  const bool own = lane < 32;
+  const float* e0 = Es + i * D;
+  const int d = pq * 64 + lane;  // this lane's G1 column
+  float cv[NCM];
+#pragma unroll
+  for (int c = 0; c < NCM; ++c) cv[c] = 0.f;
+  float m = 0.f, zsum = 0.f, acc0 = 0.f, acc1 = 0.f;  // running max (>= 0), sum of e^{S - m}, G1 partial
+#pragma unroll
+  for (int c = 0; c < NCM; ++c) {
+    if (c >= nc) break;
+    if (c > 0) __syncthreads();  // every wave done with the previous chunk (its G1 terms, Vs)
+    stage(c);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const float* buf = Cb;
+    const int k = c * GF_CH + kq;
+    float ck = 1.f;  // centroid scale (FUSEC)
+    {
+      float4 a = float4{0.f, 0.f, 0.f, 0.f}, q = a;
+      if (k < N) {
+#pragma unroll 8
+        for (int cc0 = dq; cc0 < dq + 128; cc0 += 4) {
+          const float4 cc = *reinterpret_cast<const float4*>(buf + kq * LDC + cc0);
+          const float4 x0 = *reinterpret_cast<const float4*>(e0 + cc0);
+          a.x += x0.x * cc.x;
+          a.y += x0.y * cc.y;
+          a.z += x0.z * cc.z;
+          a.w += x0.w * cc.w;
+          if constexpr (FUSEC) {
+            q.x += cc.x * cc.x;
+            q.y += cc.y * cc.y;
+            q.z += cc.z * cc.z;
+            q.w += cc.w * cc.w;
+          }
+        }
+      }
+      float v = (a.x + a.y) + (a.z + a.w);
+      v += __shfl_xor(v, 32, 64);
+      cv[c] = v;
+      if constexpr (FUSEC) {  // |C_k| = |s_k| / M, C^_k = s_k / (M max(|C_k|, eps))
+        float qq = (q.x + q.y) + (q.z + q.w);
+        qq += __shfl_xor(qq, 32, 64);
+        ck = 1.0f / ((float)M * fmaxf(sqrtf(qq) / (float)M, EPS_COS));
+        cv[c] *= ck;
+      }
+    }
+    if (k == sg) cv[c] = rd;  // get_cossim's diagonal overwrite (utils.py:112-113)
+    const bool valid = own && k < N;
+    const float sk = wv * (cv[c] + EPS_SIM) + bv;
+    const float tm = wave_max(valid ? sk : -INFINITY);
+    if (lane == 0) rr[0] = tm;
+    __syncthreads();
+    const float tmax = fmaxf(fmaxf(red[(i * 4) * 4], red[(i * 4 + 1) * 4]), fmaxf(red[(i * 4 + 2) * 4], red[(i * 4 + 3) * 4]));
+    const float mn = fmaxf(m, tmax);  // (m starts at 0: the row max is clamped at 0 as in ge2e_rows_kernel)
+    const float resc = expf(m - mn);
+    const float e = valid ? expf(sk - mn) : 0.f;
+    zsum = zsum * resc + row_sum(wave_sum(e), 1);
+    // the chunk's G1 weights (the diagonal excluded: its gradient goes to U, utils.py:112-113)
+    if (own) Vs[i * GF_CH + kq] = (valid && k != sg) ? e * ck : 0.f;
+    if constexpr (FUSEC) {
+      // C^ and |C| of this shard's own speakers in this chunk, for the finalize step: speaker s0 + j
+      // by workgroup j % gridDim.x, wave (j / gridDim.x) % 16
+      const int nl = Bl / M, nkc = rows_of(c);
+      for (int j = (int)blockIdx.x + (int)gridDim.x * w; j < nl; j += (int)gridDim.x * 16) {
+        const int kt = s0 + j - c * GF_CH;
+        if (kt < 0 || kt >= nkc) continue;
+        float4 v = *reinterpret_cast<const float4*>(buf + kt * LDC + 4 * lane);
+        const float cn = sqrtf(wave_sum(v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w)) / (float)M;
+        const float inv = 1.0f / ((float)M * fmaxf(cn, EPS_COS));
+        v = float4{v.x * inv, v.y * inv, v.z * inv, v.w * inv};
+        *reinterpret_cast<float4*>(Chat_out + (long)(s0 + j) * D + 4 * lane) = v;
+        if (lane == 0) Cn_out[s0 + j] = cn;
+      }
+    }
+    __syncthreads();
+    acc0 *= resc;
+    acc1 *= resc;
+    const float* vr = Vs + i * GF_CH;
+    const int nk = rows_of(c);
+    int kk = 0;
+#pragma unroll 4
+    for (; kk + 1 < nk; kk += 2) {
+      acc0 += vr[kk] * buf[kk * LDC + d];
+      acc1 += vr[kk + 1] * buf[(kk + 1) * LDC + d];
+    }
+    if (kk < nk) acc0 += vr[kk] * buf[kk * LDC + d];
+    m = mn;
+  }
+  const float lz = m + logf(zsum + EPS_LOG * expf(-m));
+  // row backward (gloss = 1): as ge2e_rows_kernel (the small differences p_k (x_k - x_d) and the
+  // analytic tail 1 - sum_k p_k = 1e-6 e^-lz)
+  const float tail = EPS_LOG * expf(-lz);
+  float pdsum = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCM; ++c) {
+    const int k = c * GF_CH + kq;
+    if (c < nc && own && live && k < N) {
+      const float p = expf(wv * (cv[c] + EPS_SIM) + bv - lz);
+      const float ds = p - (k == sg ? 1.0f : 0.0f);
+      const float dcv = wv * ds;
+      pdsum += p * (cv[c] - rd);
+      const float off = (k == sg) ? 0.f : dcv;
+      cos[(long)r * ldc + k] = cv[c];
+      dcos[(long)r * ldc + k] = off;
+      if (k == sg) dcd[r] = dcv;
+    }
+  }
+  const float ps = row_sum(wave_sum(pdsum), 2);
+  if (live && pq == 0 && lane == 0) {
+    per[r] = lz - (wv * (rd + EPS_SIM) + bv);
+    alpha[r] = wv * (ps - rd * tail);
+    dwdb_rows[r] = ps - (rd + EPS_SIM) * tail;
+    dwdb_rows[Bl + r] = -tail;
+  }
+  if (live) G1[(long)r * D + d] = (acc0 + acc1) * (wv * expf(m - lz));
+}
+
 // launch F2 for N speakers (<= GF_NMAX)
+// (ssum != nullptr: the sharded form's all-gathered sums -- the 16-wave kernel forms C^ itself and
+// returns true; false: the caller must run ge2e_centroid_kernel first)
+static bool rows_fuse_centroids(int N, int D) { return N > GF_TILE && N <= GF_NMAX && D == 256; }
 static void launch_rows(int Bl, int M, int N, int D, int Np, int s0, const Ge2eWs& ws, const float* w, const float* b,
-                        float* per, hipStream_t stream) {
+                        float* per, hipStream_t stream, const float* ssum = nullptr) {
+  if (N > GF_TILE && D == 256) {
+    const size_t lds = ((size_t)GF_CH * (D + 4) + 4 * (size_t)D + 4 * GF_CH + 64) * sizeof(float);
+    const dim3 grid((Bl + 3) / 4), block(1024);
+    if (ssum)
+      hipLaunchKernelGGL(ge2e_rows16_kernel<true>, grid, block, lds, stream, ssum, ws.Ehat, ws.rawd, Bl, M, N, Np, s0, w,
+                         b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1, ws.Chat, ws.Cn);
+    else
+      hipLaunchKernelGGL(ge2e_rows16_kernel<false>, grid, block, lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N, Np,
+                         s0, w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1, nullptr, nullptr);
+    return;
+  }
   const int NT = N <= GF_TILE ? N : GF_TILE;
   const size_t lds = ((size_t)NT * (D + 4) + GF_ROWW * (size_t)D + GF_ROWW * (size_t)N) * sizeof(float);
   const dim3 grid((Bl + GF_ROWW - 1) / GF_ROWW), block(64 * GF_ROWW);
@@ -940,6 +1135,88 @@ __global__ __launch_bounds__(64 * GF_COLW) void ge2e_cols_kernel(int Bl, int M, 
   }
 }
 
+// F3 in the sharded form for D <= 256 (the c4 / c5 ranks' small row counts): one workgroup per
+// speaker k over all of D (lane: d = 4 lane .. + 3), 16 waves over the shard's rows (row w, w + 16,
+// ...: dcos[r,k] and cos[r,k] are one broadcast load per row and wave, E^_r one 1-KB coalesced
+// load), the waves' partials added in LDS in wave order.  Writes this shard's dC^_k and beta_k to
+// the reduce buffer, and workgroup 0 the shard's loss / dw / db partials (ge2e_cols_kernel<true>
+// ran (N, D / 64) workgroups of 16 waves: 2 rounds of 512 at c5's rank shape, 11 us).
+__global__ __launch_bounds__(1024) void ge2e_cols_partial_kernel(int Bl, int N, int D, int ldc,
+                                                                 const float* __restrict__ Ehat,
+                                                                 const float* __restrict__ cos,
+                                                                 const float* __restrict__ dcos,
+                                                                 const float* __restrict__ per,
+                                                                 const float* __restrict__ dwdb_rows,
+                                                                 float* __restrict__ loss, float* __restrict__ dwdb,
+                                                                 float* __restrict__ red_dchat,
+                                                                 float* __restrict__ red_beta) {
+  constexpr int NW = 16;
+  __shared__ __attribute__((aligned(16))) float4 part[NW][64];
+  __shared__ float bpart[NW];
+  __shared__ float red3[3][NW];
+  const int k = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bool dok = 4 * lane < D;
+  float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+#pragma unroll 4
+  for (int r = w; r < Bl; r += NW) {
+    const float dc = dcos[(long)r * ldc + k];
+    const float cv = cos[(long)r * ldc + k];
+    const float4 e = dok ? *reinterpret_cast<const float4*>(Ehat + (long)r * D + 4 * lane) : float4{0.f, 0.f, 0.f, 0.f};
+    acc.x += dc * e.x;
+    acc.y += dc * e.y;
+    acc.z += dc * e.z;
+    acc.w += dc * e.w;
+    bsum += dc * cv;
+  }
+  part[w][lane] = acc;
+  if (lane == 0) bpart[w] = bsum;
+  __syncthreads();
+  if (w == 0) {
+    float4 t = part[0][lane];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) {
+      const float4 v = part[i][lane];
+      t = float4{t.x + v.x, t.y + v.y, t.z + v.z, t.w + v.w};
+    }
+    if (dok) *reinterpret_cast<float4*>(red_dchat + (long)k * D + 4 * lane) = t;
+    if (lane == 0) {
+      float b = 0.f;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) b += bpart[i];
+      red_beta[k] = b;
+    }
+  }
+  if (k == 0) {  // loss = sum per, dw, db: fixed-order block sums (block-uniform branch)
+    float l = 0.f, a = 0.f, b = 0.f;
+    for (int i = tid; i < Bl; i += 64 * NW) {
+      l += per[i];
+      a += dwdb_rows[i];
+      b += dwdb_rows[Bl + i];
+    }
+    l = wave_sum(l);
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) {
+      red3[0][w] = l;
+      red3[1][w] = a;
+      red3[2][w] = b;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+      for (int i = 0; i < NW; ++i) {
+        s0 += red3[0][i];
+        s1 += red3[1][i];
+        s2 += red3[2][i];
+      }
+      loss[0] = s0;
+      dwdb[0] = s1;
+      dwdb[1] = s2;
+    }
+  }
+}
+
 // can the fused 3-launch path run this shape?
 extern "C" int sv_ge2e_train_ok(int N, int M, int D) {
   return N > 0 && N <= GF_NMAX && M >= 2 && M <= GF_MMAX && D > 0 && D <= GF_DMAX && D % 4 == 0;
@@ -993,18 +1270,29 @@ extern "C" int sv_ge2e_shard_rows(int N_local, int M, int D, int spk_offset, int
   if (!sv_ge2e_train_ok(N, M, D) || N_local <= 0 || spk_offset < 0 || spk_offset + N_local > N) return SV_ESHAPE;
   const Ge2eWs ws = carve(workspace, N_local, M, D, N);
   const int Bl = N_local * M, Np = (N + 3) & ~3;
-  hipLaunchKernelGGL(ge2e_centroid_kernel, dim3(Np), dim3(256), 0, stream, ssum_all, N, M, D, ws.Chat, ws.Cn);
-  SV_LAUNCH_CHECK();
-  launch_rows(Bl, M, N, D, Np, spk_offset, ws, w, b, per, stream);
+#ifndef SV_GE2E_FUSEC
+#define SV_GE2E_FUSEC 1
+#endif
+  if (SV_GE2E_FUSEC && rows_fuse_centroids(N, D) && Np == N) {  // (C^ formed inside the rows kernel)
+    launch_rows(Bl, M, N, D, Np, spk_offset, ws, w, b, per, stream, ssum_all);
+  } else {
+    hipLaunchKernelGGL(ge2e_centroid_kernel, dim3(Np), dim3(256), 0, stream, ssum_all, N, M, D, ws.Chat, ws.Cn);
+    SV_LAUNCH_CHECK();
+    launch_rows(Bl, M, N, D, Np, spk_offset, ws, w, b, per, stream);
+  }
   SV_LAUNCH_CHECK();
   // the padding rows of dC^ (speakers N .. Np-1) stay zero through the all-reduce
   if (Np > N) {
     hipError_t e = sv_memset0(red + (size_t)N * D, (size_t)(Np - N) * D * sizeof(float), stream);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL(ge2e_cols_kernel<true>, dim3(N, (D + 63) / 64), dim3(64 * GF_COLW), 0, stream, Bl, M, N, D, Np,
-                     ws.Chat, ws.Cn, ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.G1,
-                     per, ws.dwdb_rows, nullptr, loss_local, dwdb_local, red, red + (size_t)Np * D);
+  if (D <= 256)
+    hipLaunchKernelGGL(ge2e_cols_partial_kernel, dim3(N), dim3(1024), 0, stream, Bl, N, D, Np, ws.Ehat, ws.cos, ws.dcos,
+                       per, ws.dwdb_rows, loss_local, dwdb_local, red, red + (size_t)Np * D);
+  else
+    hipLaunchKernelGGL(ge2e_cols_kernel<true>, dim3(N, (D + 63) / 64), dim3(64 * GF_COLW), 0, stream, Bl, M, N, D, Np,
+                       ws.Chat, ws.Cn, ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, ws.cos, ws.dcos, ws.alpha, ws.dcd,
+                       ws.G1, per, ws.dwdb_rows, nullptr, loss_local, dwdb_local, red, red + (size_t)Np * D);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }
