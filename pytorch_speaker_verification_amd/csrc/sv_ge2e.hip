@@ -540,8 +540,8 @@ __global__ __launch_bounds__(256) void ge2e_prep_kernel(const float* __restrict_
   const float fm = (float)M;
   const float4 c = float4{sum.x / fm, sum.y / fm, sum.z / fm, sum.w / fm};
   const float invm1 = 1.0f / (float)(M - 1);
-  // every lane-partial first (|c|^2; per row |e|^2, |u|^2, e.u), then ONE butterfly over all of
-  // them: the 3 RW + 1 shuffle chains are independent, so their LDS latencies overlap
+  // every lane-partial first (|c|^2; per row |e|^2, |u|^2, e.u), then the wave sums by DPP
+  // (independent chains, no LDS round trips; the sums are wave-uniform)
   float v[3 * RW + 1];
   float4 uu[RW];
   v[3 * RW] = c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w;
@@ -555,10 +555,7 @@ __global__ __launch_bounds__(256) void ge2e_prep_kernel(const float* __restrict_
     v[3 * q + 2] = x.x * u.x + x.y * u.y + x.z * u.z + x.w * u.w;
   }
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-#pragma unroll
-    for (int i = 0; i < 3 * RW + 1; ++i) v[i] += __shfl_xor(v[i], o, 64);
-  }
+  for (int i = 0; i < 3 * RW + 1; ++i) v[i] = wave_sum_dpp(v[i]);
   const float cn = sqrtf(v[3 * RW]);
   const float icn = 1.0f / fmaxf(cn, EPS_COS);
   if (w == 0 && ssum) {
@@ -799,6 +796,12 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
 // staging latency they hide; a third staging of the first tile for G1 instead of the online sum:
 // 19.5 us + the centroid launch.)
 constexpr int GF_CH = 128;  // speakers per chunk
+#ifndef SV_GE2E_ROWS4R      // 8 / 16: ge2e_rows4r_kernel below on that many waves; 0: this kernel (A/B)
+#define SV_GE2E_ROWS4R 8
+#endif
+#ifndef SV_GE2E_R4ROWS      // rows per workgroup of ge2e_rows4r_kernel (2 or 4)
+#define SV_GE2E_R4ROWS 2
+#endif
 template <bool FUSEC>
 __global__ __launch_bounds__(1024) void ge2e_rows16_kernel(const float* __restrict__ Csrc,
                                                           const float* __restrict__ Ehat,
@@ -956,12 +959,317 @@ __global__ __launch_bounds__(1024) void ge2e_rows16_kernel(const float* __restri
   if (live) G1[(long)r * D + d] = (acc0 + acc1) * (wv * expf(m - lz));
 }
 
+// ge2e_rows4r_kernel's centroid tile stride: 288 = 32 mod 64 banks, so the two speakers of a 16-lane
+// LDS pass (8-lane groups reading 32 consecutive floats each) fall on disjoint banks
+constexpr int GF_R4LDC = 288;
+#ifndef SV_GE2E_R4GL  // lanes per speaker in ge2e_rows4r_kernel's cosine step (8 or 16)
+#define SV_GE2E_R4GL 8
+#endif
+
+// SV_GE2E_PROBE (A/B builds only): phase timestamps of ge2e_rows4r_kernel (100 MHz wall clock)
+// printed by thread 0 of the first and last workgroups
+#ifndef SV_GE2E_PROBE
+#define SV_GE2E_PROBE 0
+#endif
+#if SV_GE2E_PROBE
+#define GPROBE(n) \
+  if (threadIdx.x == 0) tp[n] = wall_clock64()
+#else
+#define GPROBE(n)
+#endif
+
+// a workgroup-uniform value (read from LDS) kept in an SGPR
+__device__ __forceinline__ float uniform_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
+// F2, register-blocked form of the kernel above (same arguments, outputs and FUSEC meaning), the
+// product's for 128 < N <= 256 and D = 256: RW rows per workgroup of NWV waves (8 waves, 2 rows:
+// 160 workgroups at a c5 rank's 320 rows).  Every centroid value leaves LDS once per WORKGROUP and
+// feeds the RW rows from registers:
+//   cosines: lane = GL s + g (GL = 8-lane groups) holds E^[RW rows][32 j + 4 g .. +3] (j < 8); group
+//     s takes one speaker per step, reads its 256 values as 8 conflict-free float4 per lane (tile
+//     stride GF_R4LDC), and the RW dot products (+ |s_k|^2 under FUSEC) are summed over the group
+//     by DPP; the steps are branch-free so their reads, FMAs and sums interleave;
+//   softmax: one thread per (row, speaker of the chunk), online max / sum per row as above;
+//   G1: wave w takes speakers KW w .. KW w + KW - 1 of the chunk (KW = 128 / NWV), lane 4-column
+//     slice d = 4 lane, its RW weights per speaker one broadcast LDS read; the
+//     waves' [RW][256] partials meet once, in LDS, after the last chunk;
+//   row backward: one thread per (row, speaker), cos / dcos stored coalesced.
+// Measured at the c5 rank shape (scripts/ge2e_c5rank.py, kernel trace): 23.4 us for the kernel
+// above, 22.9 here with 16 waves x 4 rows and 16-lane groups (the FUSEC form spilled), 17.1 with
+// 8 waves x 2 rows, 14.5 with branch-free steps, 13.4 with 8-lane groups.  Phase probes
+// (SV_GE2E_PROBE, 2.3 GHz shader clock): staging a chunk ~1.9 us (256 KB of sums per workgroup
+// from L2, the per-CU fill rate), cosines 1.2 us, softmax 0.9 us and G1 ~0.9 us per chunk.
+template <bool FUSEC, int NWV, int RW>
+__global__ __launch_bounds__(64 * NWV) void ge2e_rows4r_kernel(const float* __restrict__ Csrc,
+                                                          const float* __restrict__ Ehat,
+                                                          const float* __restrict__ rawd, int Bl, int M, int N,
+                                                          int ldc, int s0, const float* __restrict__ wp,
+                                                          const float* __restrict__ bp, float* __restrict__ per,
+                                                          float* __restrict__ cos, float* __restrict__ dcos,
+                                                          float* __restrict__ alpha, float* __restrict__ dcd,
+                                                          float* __restrict__ dwdb_rows, float* __restrict__ G1,
+                                                          float* __restrict__ Chat_out, float* __restrict__ Cn_out) {
+  constexpr int D = 256, LDC = GF_R4LDC, NCM = GF_NMAX / GF_CH, NT = 64 * NWV, KW = GF_CH / NWV;
+  constexpr int GL = SV_GE2E_R4GL, SPS = 64 / GL, JN = D / (4 * GL), NS = KW / SPS;  // lanes per speaker, ...
+  static_assert((GL == 8 || GL == 16) && KW % SPS == 0, "whole cosine steps");
+  static_assert((NWV == 8 || NWV == 16) && (RW == 2 || RW == 4) && 2 * RW <= NWV && GF_CH / NWV * RW <= 64,
+                "RW rows x 128 speakers of the softmax step on waves 0 .. 2 RW - 1");
+  static_assert(256 * RW % NT == 0, "whole (row, speaker) items per thread in the row backward");
+  auto sel = [](const auto* a, int i) {  // a[i] for a workgroup-uniform i, without dynamic indexing
+    auto v = a[0];
+#pragma unroll
+    for (int q = 1; q < RW; ++q)
+      if (i == q) v = a[q];
+    return v;
+  };
+  extern __shared__ __attribute__((aligned(16))) float gsm[];
+  float* Cb = gsm;                     // [GF_CH][LDC]; after the last chunk: [NWV waves][RW][D] G1 partials
+  float* Ss = Cb + GF_CH * LDC;        // [RW][GF_NMAX] cosines (diagonal overwritten)
+  float* Vs = Ss + RW * GF_NMAX;       // [GF_CH][RW] G1 weights of the current chunk
+  float* Kc = Vs + GF_CH * RW;         // [GF_CH] centroid scales of the current chunk
+  float* red = Kc + GF_CH;             // [2][16]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane % GL, s = lane / GL;
+#if SV_GE2E_PROBE
+  unsigned long long tp[16] = {};
+  const unsigned long long cy0 = __builtin_amdgcn_s_memtime();
+#endif
+  GPROBE(0);
+  const int r0 = blockIdx.x * RW;
+  const float wv = *wp, bv = *bp;
+  int sg[RW];
+  float rd[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const bool lv = r0 + i < Bl;
+    sg[i] = s0 + (lv ? r0 + i : 0) / M;
+    rd[i] = lv ? rawd[r0 + i] : 0.f;
+  }
+  float4 ev[RW][JN];
+#pragma unroll
+  for (int i = 0; i < RW; ++i)
+#pragma unroll
+    for (int j = 0; j < JN; ++j)
+      ev[i][j] = *reinterpret_cast<const float4*>(Ehat + (long)min(r0 + i, Bl - 1) * D + 4 * GL * j + 4 * g);
+  // (a row past Bl computes on a copy of the last row: its results are never stored; all 4 RW
+  // loads in flight at once, no per-row branch)
+  const int nc = (N + GF_CH - 1) / GF_CH;
+  float m[RW], zsum[RW];
+  float4 acc[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    m[i] = 0.f;  // (the row max is clamped at 0 as in ge2e_rows_kernel)
+    zsum[i] = 0.f;
+    acc[i] = float4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int c = 0; c < NCM; ++c) {
+    if (c >= nc) break;
+    const int nk = min(GF_CH, N - c * GF_CH);
+    if (c > 0) __syncthreads();  // every wave done with the previous chunk
+    for (int row = w; row < nk; row += NWV)
+      __builtin_amdgcn_global_load_lds(
+          (__attribute__((address_space(1))) void*)(Csrc + (long)(c * GF_CH + row) * D + lane * 4),
+          (__attribute__((address_space(3))) void*)(Cb + row * LDC), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    GPROBE(1 + 4 * c);
+    // cosines of the chunk: wave w, step t, lane group s -> speaker KW w + SPS t + s; the steps are
+    // independent and branch-free (a speaker past the chunk reads the chunk's last row and is not
+    // stored), so their LDS reads, FMAs and DPP sums interleave
+    {
+      float a[NS][RW], q[NS];
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        const int kr = min(KW * w + SPS * t + s, nk - 1);
+        q[t] = 0.f;
+#pragma unroll
+        for (int i = 0; i < RW; ++i) a[t][i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+          const float4 cc = *reinterpret_cast<const float4*>(Cb + kr * LDC + 4 * GL * j + 4 * g);
+#pragma unroll
+          for (int i = 0; i < RW; ++i)
+            a[t][i] += (ev[i][j].x * cc.x + ev[i][j].y * cc.y) + (ev[i][j].z * cc.z + ev[i][j].w * cc.w);
+          if constexpr (FUSEC) q[t] += (cc.x * cc.x + cc.y * cc.y) + (cc.z * cc.z + cc.w * cc.w);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+#pragma unroll
+        for (int i = 0; i < RW; ++i) a[t][i] = dpp_group_sum<GL>(a[t][i]);
+        if constexpr (FUSEC) q[t] = dpp_group_sum<GL>(q[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        const int kl = KW * w + SPS * t + s;
+        float ck = 1.f;
+        if constexpr (FUSEC)  // |C_k| = |s_k| / M, C^_k = s_k / (M max(|C_k|, eps))
+          ck = __builtin_amdgcn_rcpf(fmaxf(__builtin_amdgcn_sqrtf(q[t]), (float)M * EPS_COS));  // (1 ulp ops)
+        if (g == 0 && kl < nk) {
+          const int k = c * GF_CH + kl;
+          Kc[kl] = ck;
+#pragma unroll
+          for (int i = 0; i < RW; ++i) Ss[i * GF_NMAX + k] = (k == sg[i]) ? rd[i] : a[t][i] * ck;  // utils.py:112-113
+        }
+      }
+    }
+    if constexpr (FUSEC) {  // C^ and |C| of the shard's own speakers in this chunk (for the finalize step)
+      const int nl = Bl / M;
+      for (int j = (int)blockIdx.x + (int)gridDim.x * w; j < nl; j += (int)gridDim.x * NWV) {
+        const int kt = s0 + j - c * GF_CH;
+        if (kt < 0 || kt >= nk) continue;
+        float4 v = *reinterpret_cast<const float4*>(Cb + kt * LDC + 4 * lane);
+        const float cn = sqrtf(wave_sum_dpp(v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w)) / (float)M;
+        const float inv = 1.0f / ((float)M * fmaxf(cn, EPS_COS));
+        v = float4{v.x * inv, v.y * inv, v.z * inv, v.w * inv};
+        *reinterpret_cast<float4*>(Chat_out + (long)(s0 + j) * D + 4 * lane) = v;
+        if (lane == 0) Cn_out[s0 + j] = cn;
+      }
+    }
+    __syncthreads();
+    GPROBE(2 + 4 * c);
+    // online softmax over the chunk: thread -> (row i = tid / 128, speaker kl = tid % 128), waves 0..7
+    const int si = tid >> 7, skl = tid & 127, sk_g = c * GF_CH + skl;
+    const bool sval = tid < 128 * RW && skl < nk && r0 + si < Bl;
+    float sk = -INFINITY;
+    if (sval) sk = wv * (Ss[si * GF_NMAX + sk_g] + EPS_SIM) + bv;
+    if (w < 2 * RW) {
+      const float tm = wave_max_dpp(sk);
+      if (lane == 0) red[w] = tm;
+    }
+    __syncthreads();
+    float resc[RW];
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+      const float mn = fmaxf(m[i], uniform_f(fmaxf(red[2 * i], red[2 * i + 1])));
+      resc[i] = expf(m[i] - mn);
+      m[i] = mn;
+    }
+    if (w < 2 * RW) {
+      const int i = si;
+      const float mi = sel(m, i);
+      const int sgi = sel(sg, i);
+      const float e = sval ? expf(sk - mi) : 0.f;
+      // the diagonal is excluded from G1 (its gradient goes to U, utils.py:112-113)
+      Vs[skl * RW + i] = (sval && sk_g != sgi) ? e * Kc[skl] : 0.f;
+      const float es = wave_sum_dpp(e);
+      if (lane == 0) red[16 + w] = es;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+      zsum[i] = zsum[i] * resc[i] + uniform_f(red[16 + 2 * i] + red[16 + 2 * i + 1]);
+      acc[i].x *= resc[i];
+      acc[i].y *= resc[i];
+      acc[i].z *= resc[i];
+      acc[i].w *= resc[i];
+    }
+    GPROBE(3 + 4 * c);
+    // G1 partials: wave w, speakers KW w .. KW w + KW - 1, columns 4 lane .. 4 lane + 3
+#pragma unroll
+    for (int kk = 0; kk < KW; ++kk) {  // (past the chunk: the last row again, with weight 0)
+      const int kr = min(KW * w + kk, nk - 1);
+      const float4 cc = *reinterpret_cast<const float4*>(Cb + kr * LDC + 4 * lane);
+      float vk[RW];  // the speaker's RW weights: one broadcast LDS read
+      if constexpr (RW == 2) {
+        const float2 t2 = *reinterpret_cast<const float2*>(Vs + (KW * w + kk) * RW);
+        vk[0] = t2.x;
+        vk[1] = t2.y;
+      } else {
+#pragma unroll
+        for (int i = 0; i < RW; ++i) vk[i] = Vs[(KW * w + kk) * RW + i];
+      }
+#pragma unroll
+      for (int i = 0; i < RW; ++i) {
+        const float vs = vk[i];
+        acc[i].x += vs * cc.x;
+        acc[i].y += vs * cc.y;
+        acc[i].z += vs * cc.z;
+        acc[i].w += vs * cc.w;
+      }
+    }
+  }
+  float lz[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) lz[i] = m[i] + logf(zsum[i] + EPS_LOG * expf(-m[i]));
+  __syncthreads();  // Cb free: the G1 partials meet there
+  GPROBE(9);
+#pragma unroll
+  for (int i = 0; i < RW; ++i) *reinterpret_cast<float4*>(Cb + (w * RW + i) * D + 4 * lane) = acc[i];
+  __syncthreads();
+  // items (row i, speaker / column k) = (item / 256, item % 256), item = tid + NT it
+  float pdv[256 * RW / NT];
+#pragma unroll
+  for (int it = 0; it < 256 * RW / NT; ++it) {
+    const int item = tid + NT * it, i = item >> 8, k = item & 255, r = r0 + i;
+    const bool live = r < Bl;
+    const float lzi = sel(lz, i), mi = sel(m, i), rdi = sel(rd, i);
+    const int sgi = sel(sg, i);
+    float gs = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NWV; ++ww) gs += Cb[(ww * RW + i) * D + k];
+    if (live) G1[(long)r * D + k] = gs * (wv * expf(mi - lzi));
+    // row backward (gloss = 1): the small differences p_k (x_k - x_d), as ge2e_rows_kernel
+    float pd = 0.f;
+    if (live && k < N) {
+      const float cv = Ss[i * GF_NMAX + k];
+      const float p = expf(wv * (cv + EPS_SIM) + bv - lzi);
+      const float dcv = wv * (p - (k == sgi ? 1.0f : 0.0f));
+      pd = p * (cv - rdi);
+      cos[(long)r * ldc + k] = cv;
+      dcos[(long)r * ldc + k] = (k == sgi) ? 0.f : dcv;
+      if (k == sgi) dcd[r] = dcv;
+    }
+    pdv[it] = wave_sum_dpp(pd);
+  }
+  GPROBE(10);
+#pragma unroll
+  for (int it = 0; it < 256 * RW / NT; ++it)
+    if (lane == 0) red[w + NWV * it] = pdv[it];  // slot = item / 64: row i owns slots 4 i .. 4 i + 3
+  __syncthreads();
+  if (tid < RW) {
+    const int i = tid, r = r0 + i;
+    if (r < Bl) {
+      const float lzi = sel(lz, i), rdi = sel(rd, i);
+      // the analytic tail 1 - sum_k p_k = 1e-6 e^-lz
+      const float tail = EPS_LOG * expf(-lzi);
+      const float ps = (red[4 * i] + red[4 * i + 1]) + (red[4 * i + 2] + red[4 * i + 3]);
+      per[r] = lzi - (wv * (rdi + EPS_SIM) + bv);
+      alpha[r] = wv * (ps - rdi * tail);
+      dwdb_rows[r] = ps - (rdi + EPS_SIM) * tail;
+      dwdb_rows[Bl + r] = -tail;
+    }
+  }
+#if SV_GE2E_PROBE
+  GPROBE(11);
+  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
+    printf("PROBE wg %d: %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu cycles %llu\n", (int)blockIdx.x,
+           tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[5] - tp[3], tp[6] - tp[5], tp[7] - tp[6], tp[9] - tp[7],
+           tp[10] - tp[9], tp[11] - tp[10], tp[11] - tp[0], tp[0], __builtin_amdgcn_s_memtime() - cy0);
+#endif
+}
+
 // launch F2 for N speakers (<= GF_NMAX)
 // (ssum != nullptr: the sharded form's all-gathered sums -- the 16-wave kernel forms C^ itself and
 // returns true; false: the caller must run ge2e_centroid_kernel first)
 static bool rows_fuse_centroids(int N, int D) { return N > GF_TILE && N <= GF_NMAX && D == 256; }
 static void launch_rows(int Bl, int M, int N, int D, int Np, int s0, const Ge2eWs& ws, const float* w, const float* b,
                         float* per, hipStream_t stream, const float* ssum = nullptr) {
+  if (N > GF_TILE && D == 256 && SV_GE2E_ROWS4R) {
+    const size_t lds = ((size_t)GF_CH * GF_R4LDC + 4 * GF_NMAX + 4 * GF_CH + GF_CH + 32) * sizeof(float);
+    constexpr int R4W = SV_GE2E_ROWS4R == 16 ? 16 : 8, R4R = SV_GE2E_R4ROWS == 4 ? 4 : 2;
+    const dim3 grid((Bl + R4R - 1) / R4R), block(64 * R4W);
+    if (ssum)
+      hipLaunchKernelGGL((ge2e_rows4r_kernel<true, R4W, R4R>), grid, block, lds, stream, ssum, ws.Ehat, ws.rawd, Bl, M, N, Np, s0, w,
+                         b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1, ws.Chat, ws.Cn);
+    else
+      hipLaunchKernelGGL((ge2e_rows4r_kernel<false, R4W, R4R>), grid, block, lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N, Np,
+                         s0, w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1, nullptr, nullptr);
+    return;
+  }
   if (N > GF_TILE && D == 256) {
     const size_t lds = ((size_t)GF_CH * (D + 4) + 4 * (size_t)D + 4 * GF_CH + 64) * sizeof(float);
     const dim3 grid((Bl + 3) / 4), block(1024);
@@ -1158,16 +1466,29 @@ __global__ __launch_bounds__(1024) void ge2e_cols_partial_kernel(int Bl, int N, 
   const bool dok = 4 * lane < D;
   float4 acc = float4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
-#pragma unroll 4
-  for (int r = w; r < Bl; r += NW) {
-    const float dc = dcos[(long)r * ldc + k];
-    const float cv = cos[(long)r * ldc + k];
-    const float4 e = dok ? *reinterpret_cast<const float4*>(Ehat + (long)r * D + 4 * lane) : float4{0.f, 0.f, 0.f, 0.f};
-    acc.x += dc * e.x;
-    acc.y += dc * e.y;
-    acc.z += dc * e.z;
-    acc.w += dc * e.w;
-    bsum += dc * cv;
+  // RB rows per wave in flight at once (loads first, then the FMAs): a c5 rank's 320 rows are two
+  // batches, not one memory latency per 4 rows
+  constexpr int RB = 16;
+  for (int rb = w; rb < Bl; rb += NW * RB) {
+    float dc[RB], cv[RB];
+    float4 e[RB];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int r = rb + NW * u;
+      const bool ok = r < Bl;
+      const long rr = ok ? r : 0;
+      dc[u] = ok ? dcos[rr * ldc + k] : 0.f;
+      cv[u] = cos[rr * ldc + k];
+      e[u] = dok ? *reinterpret_cast<const float4*>(Ehat + rr * D + 4 * lane) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      acc.x += dc[u] * e[u].x;
+      acc.y += dc[u] * e[u].y;
+      acc.z += dc[u] * e[u].z;
+      acc.w += dc[u] * e[u].w;
+      bsum += dc[u] * cv[u];
+    }
   }
   part[w][lane] = acc;
   if (lane == 0) bpart[w] = bsum;
