@@ -1444,11 +1444,17 @@ __global__ __launch_bounds__(64 * GF_COLW) void ge2e_cols_kernel(int Bl, int M, 
 }
 
 // F3 in the sharded form for D <= 256 (the c4 / c5 ranks' small row counts): one workgroup per
-// speaker k over all of D (lane: d = 4 lane .. + 3), 16 waves over the shard's rows (row w, w + 16,
-// ...: dcos[r,k] and cos[r,k] are one broadcast load per row and wave, E^_r one 1-KB coalesced
-// load), the waves' partials added in LDS in wave order.  Writes this shard's dC^_k and beta_k to
-// the reduce buffer, and workgroup 0 the shard's loss / dw / db partials (ge2e_cols_kernel<true>
-// ran (N, D / 64) workgroups of 16 waves: 2 rounds of 512 at c5's rank shape, 11 us).
+// KB speakers k0 .. k0 + KB - 1 over all of D (lane: d = 4 lane .. + 3), 16 waves over the shard's
+// rows (row w, w + 16, ...: the KB speakers' dcos[r,k] and cos[r,k] are one broadcast load each per
+// row and wave, E^_r one 1-KB coalesced load, read once for KB speakers), the waves' partials added
+// in LDS in wave order -- every speaker's sums in the same order for any KB.  Writes this shard's
+// dC^_k and beta_k to the reduce buffer, and workgroup 0 the shard's loss / dw / db partials
+// (r05: KB = 1 ran 256 workgroups that each streamed all of E^ from L2, 84 MB at c5's rank shape,
+// 7.5-9.4 us; ge2e_cols_kernel<true> before it ran (N, D / 64) workgroups, 11 us).
+#ifndef SV_GE2E_COLRB  // rows per wave in flight at KB = 1
+#define SV_GE2E_COLRB 16
+#endif
+template <int KB>
 __global__ __launch_bounds__(1024) void ge2e_cols_partial_kernel(int Bl, int N, int D, int ldc,
                                                                  const float* __restrict__ Ehat,
                                                                  const float* __restrict__ cos,
@@ -1459,55 +1465,84 @@ __global__ __launch_bounds__(1024) void ge2e_cols_partial_kernel(int Bl, int N, 
                                                                  float* __restrict__ red_dchat,
                                                                  float* __restrict__ red_beta) {
   constexpr int NW = 16;
-  __shared__ __attribute__((aligned(16))) float4 part[NW][64];
-  __shared__ float bpart[NW];
+  __shared__ __attribute__((aligned(16))) float4 part[KB][NW][64];
+  __shared__ float bpart[KB][NW];
   __shared__ float red3[3][NW];
-  const int k = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int k0 = blockIdx.x * KB, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const bool dok = 4 * lane < D;
-  float4 acc = float4{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;
-  // RB rows per wave in flight at once (loads first, then the FMAs): a c5 rank's 320 rows are two
+  float4 acc[KB];
+  float bsum[KB];
+#pragma unroll
+  for (int j = 0; j < KB; ++j) {
+    acc[j] = float4{0.f, 0.f, 0.f, 0.f};
+    bsum[j] = 0.f;
+  }
+  // RB rows per wave in flight at once (loads first, then the FMAs): a c5 rank's 320 rows are a few
   // batches, not one memory latency per 4 rows
-  constexpr int RB = 16;
+  constexpr int RB = KB == 1 ? SV_GE2E_COLRB : KB == 2 ? 10 : 6;
   for (int rb = w; rb < Bl; rb += NW * RB) {
-    float dc[RB], cv[RB];
+    float dc[RB][KB], cv[RB][KB];
     float4 e[RB];
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const int r = rb + NW * u;
       const bool ok = r < Bl;
       const long rr = ok ? r : 0;
-      dc[u] = ok ? dcos[rr * ldc + k] : 0.f;
-      cv[u] = cos[rr * ldc + k];
+      if constexpr (KB == 4) {  // (k0 % 4 == 0, ldc % 4 == 0: one 16-B broadcast load)
+        const float4 d4 = *reinterpret_cast<const float4*>(dcos + rr * ldc + k0);
+        const float4 c4 = *reinterpret_cast<const float4*>(cos + rr * ldc + k0);
+        dc[u][0] = ok ? d4.x : 0.f, dc[u][1] = ok ? d4.y : 0.f, dc[u][2] = ok ? d4.z : 0.f, dc[u][3] = ok ? d4.w : 0.f;
+        cv[u][0] = c4.x, cv[u][1] = c4.y, cv[u][2] = c4.z, cv[u][3] = c4.w;
+      } else if constexpr (KB == 2) {
+        const float2 d2 = *reinterpret_cast<const float2*>(dcos + rr * ldc + k0);
+        const float2 c2 = *reinterpret_cast<const float2*>(cos + rr * ldc + k0);
+        dc[u][0] = ok ? d2.x : 0.f, dc[u][1] = ok ? d2.y : 0.f;
+        cv[u][0] = c2.x, cv[u][1] = c2.y;
+      } else {
+#pragma unroll
+        for (int j = 0; j < KB; ++j) {
+          dc[u][j] = ok ? dcos[rr * ldc + k0 + j] : 0.f;
+          cv[u][j] = cos[rr * ldc + k0 + j];
+        }
+      }
       e[u] = dok ? *reinterpret_cast<const float4*>(Ehat + rr * D + 4 * lane) : float4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int u = 0; u < RB; ++u) {
-      acc.x += dc[u] * e[u].x;
-      acc.y += dc[u] * e[u].y;
-      acc.z += dc[u] * e[u].z;
-      acc.w += dc[u] * e[u].w;
-      bsum += dc[u] * cv[u];
-    }
+    for (int u = 0; u < RB; ++u)
+#pragma unroll
+      for (int j = 0; j < KB; ++j) {
+        acc[j].x += dc[u][j] * e[u].x;
+        acc[j].y += dc[u][j] * e[u].y;
+        acc[j].z += dc[u][j] * e[u].z;
+        acc[j].w += dc[u][j] * e[u].w;
+        bsum[j] += dc[u][j] * cv[u][j];
+      }
   }
-  part[w][lane] = acc;
-  if (lane == 0) bpart[w] = bsum;
+#pragma unroll
+  for (int j = 0; j < KB; ++j) {
+    part[j][w][lane] = acc[j];
+    if (lane == 0) bpart[j][w] = bsum[j];
+  }
   __syncthreads();
-  if (w == 0) {
-    float4 t = part[0][lane];
+  if (w < KB) {  // wave j sums speaker k0 + j's partials in wave order
+    const int k = k0 + w;
+    float4 t = part[w][0][lane];
 #pragma unroll
     for (int i = 1; i < NW; ++i) {
-      const float4 v = part[i][lane];
+      const float4 v = part[w][i][lane];
       t = float4{t.x + v.x, t.y + v.y, t.z + v.z, t.w + v.w};
     }
-    if (dok) *reinterpret_cast<float4*>(red_dchat + (long)k * D + 4 * lane) = t;
-    if (lane == 0) {
-      float b = 0.f;
+    if (k < N) {
+      if (dok) *reinterpret_cast<float4*>(red_dchat + (long)k * D + 4 * lane) = t;
+      if (lane == 0) {
+        float b = 0.f;
 #pragma unroll
-      for (int i = 0; i < NW; ++i) b += bpart[i];
-      red_beta[k] = b;
+        for (int i = 0; i < NW; ++i) b += bpart[w][i];
+        red_beta[k] = b;
+      }
     }
   }
+  const int k = blockIdx.x;
   if (k == 0) {  // loss = sum per, dw, db: fixed-order block sums (block-uniform branch)
     float l = 0.f, a = 0.f, b = 0.f;
     for (int i = tid; i < Bl; i += 64 * NW) {
@@ -1594,6 +1629,9 @@ extern "C" int sv_ge2e_shard_rows(int N_local, int M, int D, int spk_offset, int
 #ifndef SV_GE2E_FUSEC
 #define SV_GE2E_FUSEC 1
 #endif
+#ifndef SV_GE2E_COLKB  // speakers per workgroup of ge2e_cols_partial_kernel (1, 2 or 4; Np % 4 == 0)
+#define SV_GE2E_COLKB 1
+#endif
   if (SV_GE2E_FUSEC && rows_fuse_centroids(N, D) && Np == N) {  // (C^ formed inside the rows kernel)
     launch_rows(Bl, M, N, D, Np, spk_offset, ws, w, b, per, stream, ssum_all);
   } else {
@@ -1608,8 +1646,9 @@ extern "C" int sv_ge2e_shard_rows(int N_local, int M, int D, int spk_offset, int
     if (e != hipSuccess) return (int)e;
   }
   if (D <= 256)
-    hipLaunchKernelGGL(ge2e_cols_partial_kernel, dim3(N), dim3(1024), 0, stream, Bl, N, D, Np, ws.Ehat, ws.cos, ws.dcos,
-                       per, ws.dwdb_rows, loss_local, dwdb_local, red, red + (size_t)Np * D);
+    hipLaunchKernelGGL(ge2e_cols_partial_kernel<SV_GE2E_COLKB>, dim3((N + SV_GE2E_COLKB - 1) / SV_GE2E_COLKB),
+                       dim3(1024), 0, stream, Bl, N, D, Np, ws.Ehat, ws.cos, ws.dcos, per, ws.dwdb_rows, loss_local,
+                       dwdb_local, red, red + (size_t)Np * D);
   else
     hipLaunchKernelGGL(ge2e_cols_kernel<true>, dim3(N, (D + 63) / 64), dim3(64 * GF_COLW), 0, stream, Bl, M, N, D, Np,
                        ws.Chat, ws.Cn, ws.Ehat, ws.Uhat, ws.En, ws.Un, ws.rawd, ws.cos, ws.dcos, ws.alpha, ws.dcd,

@@ -520,6 +520,9 @@ constexpr int PH_BM = 32;                      // rows of a half
                          // time unchanged: the lines land closer to their use and fewer are evicted first; 0: A/B)
 #define SV_PF32_PF_HALF 1
 #endif
+#ifndef SV_PF32_PF_SPLIT  // per-half triggers: half h's rows of step s once half h of step s + 1 is done (0: A/B)
+#define SV_PF32_PF_SPLIT 1
+#endif
 __device__ void pf32_bwd_prefetch(const float* acts, const float* c_tm, const float* dhup, int up_full, int T, int B,
                                   int H, const unsigned* cnt, int nub, int ncomp, int npf, const unsigned* status,
                                   unsigned limit, char* scratch) {
@@ -528,9 +531,57 @@ __device__ void pf32_bwd_prefetch(const float* acts, const float* c_tm, const fl
   int l0, l1;
   persist_xcd_tiles(x, ncomp, l0, l1);
   const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
-  const unsigned* c0 = cnt + ((l0 / nub) * 2 + SV_PF32_PF_HALF) * SV_PCNT_STRIDE;  // (row block, half) of the group's first tile
   char* dst = scratch + g * 1024;
   int* skip = reinterpret_cast<int*>(scratch + 4096);
+#if SV_PF32_PF_SPLIT
+  // The compute workgroups DMA half 0's operands of step s at the end of half 1 of step s + 1 and
+  // half 1's at the end of half 0 of step s (load_ew).  Each half's 32 rows are prefetched half a
+  // step before that: half 0's once the group's first row block has finished half 0 of step s + 1,
+  // half 1's once it has finished half 1 of step s + 1 -- so about one half-step of operands per
+  // XCD is in flight in L2 (r05: the whole-step trigger two steps ahead held 1-1.5 steps, and part
+  // of it was evicted before its DMA and fetched twice).
+  const unsigned* ch[2] = {cnt + ((l0 / nub) * 2 + 0) * SV_PCNT_STRIDE, cnt + ((l0 / nub) * 2 + 1) * SV_PCNT_STRIDE};
+  for (int s = T - 1; s >= 0; --s) {
+    for (int hf = 0; hf < 2; ++hf) {
+      if (tid == 0) {
+        if (s + 1 <= T - 1) {  // trigger: half hf of step s + 1 done (T - 1 - s steps counted)
+          unsigned spins = 0;
+          const unsigned target = (unsigned)nub * (unsigned)(T - 1 - s);
+          while (__hip_atomic_load(ch[hf], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+                 !__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) && ++spins < limit)
+            __builtin_amdgcn_s_sleep(8);
+        }
+        // too late (the compute waves have issued their own DMA of these operands): half 0's once
+        // half 1 of step s + 1 is done, half 1's once half 0 of step s is done -- skip, so a slow
+        // helper never holds the launch open
+        *skip = hf == 0 ? __hip_atomic_load(ch[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nub * (unsigned)(T - 1 - s)
+                        : __hip_atomic_load(ch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nub * (unsigned)(T - s);
+      }
+      __syncthreads();
+      const bool sk = *skip;
+      __syncthreads();
+      if (sk) continue;
+      const float* up = dhup ? (up_full ? dhup + (long)s * BH : (s == T - 1 ? dhup : nullptr)) : nullptr;
+      // a tile half's pieces: 32 rows x (4 gates of activations + c_{s-1} + dh_up) x 8 pieces of 16 B
+      for (int L = l0 + k; L < l1; L += nk) {
+        const int ub = L % nub, rb = L / nub, j0 = ub * PF_U;
+        for (int i = tid; i < 6 * PH_BM * 8; i += 256) {
+          const int kind = i >> 8, r2 = min(rb * PF_BM + hf * PH_BM + ((i >> 3) & 31), B - 1), pc = i & 7;
+          const float* src = nullptr;
+          if (kind < 4)
+            src = acts + (long)s * BG + (long)r2 * G + (long)kind * H + j0 + 4 * pc;
+          else if (kind == 4 && s > 0)
+            src = c_tm + (long)(s - 1) * BH + (long)r2 * H + j0 + 4 * pc;
+          else if (kind == 5 && up)
+            src = up + (long)r2 * H + j0 + 4 * pc;
+          if (src) persist_prefetch16(src, dst);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+#else
+  const unsigned* c0 = cnt + ((l0 / nub) * 2 + SV_PF32_PF_HALF) * SV_PCNT_STRIDE;  // (row block, half) of the group's first tile
   for (int s = T - 1; s >= 0; --s) {
     if (tid == 0) {
       if (s + SV_PF32_AHEAD <= T - 1) {
@@ -566,6 +617,7 @@ __device__ void pf32_bwd_prefetch(const float* acts, const float* c_tm, const fl
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+#endif
 }
 
 template <int NKG, int P, int NV, int NL>
