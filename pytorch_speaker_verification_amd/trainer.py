@@ -85,6 +85,10 @@ class GE2ETrainer:
         self.group = group
         self.write_grads = write_grads
         self.ge2e = ShardedGE2E(group=group)
+        # the data-parallel machinery (comm stream, bucketed SUM all-reduce from the backward's
+        # events, status flags): on whenever the group has more than one rank; a world-1 process
+        # group may switch it on to run the collectives on one GPU (tests/test_gpu_rccl.py)
+        self.dp = self.ge2e.world > 1
         self.status = None
         self._flatten()
         if self.ge2e.world > 1:
@@ -186,7 +190,7 @@ class GE2ETrainer:
             emb, st = embedder_forward(x.float().contiguous(), layers, w_p, b_p, products=products,
                                        status=self.status, probe=probe.get("fwd"), schedule=schedule)
         E = emb.view(N, M, emb.shape[1])
-        dp = self.ge2e.world > 1
+        dp = self.dp
         # data parallel: the local loss partial goes to the head bucket's all-reduce (no collective)
         gslot = self.flat_g[self.n_pad:self.n_pad + 2]  # dL/dw, dL/db
         loss, dE, dwdb = self.ge2e.train(E, w, b, reduce_loss=not dp, dwdb_out=gslot)
