@@ -399,6 +399,15 @@ int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, cons
 // layer-wavefront backward (sv_persist3.hip / sv_persist.hip): all L = 3 layers' recurrences and
 // their upstream gradients dx in one launch, for the small per-GPU batches (B <= 80 at H = 768)
 constexpr int WB_L = 3;
+// A/B builds only (measured slower): the weight gradients beside the backward
+// wavefront (sv_bf16.hip, gemm_bf16_8qw_kernel), which needs the wavefront's dG^T stores written
+// through (sc1); SV_WAVE_DGT_SC1: those stores alone (diagnostic)
+#ifndef SV_WAVE_DW_SIDE
+#define SV_WAVE_DW_SIDE 0
+#endif
+#ifndef SV_WAVE_DGT_SC1
+#define SV_WAVE_DGT_SC1 0
+#endif
 struct WaveBwdArgs {
   const bf16_t* whhT[WB_L];  // [H][4H] bf16 (W_hh^T)
   const bf16_t* wihT[WB_L];  // [H][4H] bf16 (W_ih^T; layers >= 1)
@@ -414,6 +423,7 @@ struct WaveBwdArgs {
   unsigned limit;
   long lddgT;
   int T, Bp, B, H, nub, nrb, fault;
+  int dgt_sc1;  // dG^T stores written through (sc1): the weight-gradient GEMM reads them in-launch
 };
 int sv_wave_bwd_launch(const WaveBwdArgs& a, hipStream_t stream);
 int sv_wave_bwd_fits(int L, int B, int H, int cus);
@@ -421,4 +431,4 @@ size_t sv_wave_bwd_scratch(int L, int T, int B, int H);
 int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, const bf16_t* const* wihT,
                      const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
                      bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
-                     float* const* db_hh, hipEvent_t pre, hipEvent_t post);
+                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, int dgt_sc1 = 0);

@@ -11,6 +11,7 @@
 #include "../../include/sv_ge2e.h"
 #include "sv_bf16.h"
 #include "sv_gemm256.h"
+#include "sv_persist_dev.h"
 
 
 // ============================================================================
@@ -529,6 +530,121 @@ void launch_bwd_bf16(dim3 grid, hipStream_t s, const bf16_t* dgn, const bf16_t* 
                      bf16_t* dgT, long lddgT, int t, int Bp, int B, int H) {
   hipLaunchKernelGGL(lstm_step_bwd_bf16_kernel<6>, grid, dim3(512), BBWD_LDS, s, dgn, whhT, up, dcfi, acts, ct, cp,
                      dg, dcfo, dgT, lddgT, t, Bp, B, H);
+}
+
+// ---- the layer wavefront's weight gradients beside it (c4 rank) ----
+// The backward wavefront (every layer's recurrence in one launch, sv_persist3.hip) holds 216 of
+// the 256 CUs for ~0.9 ms at the c4 rank shape; its dW GEMMs (dual dW_hh | dW_ih per upper layer,
+// layer 0's dW_hh: K = T Bp split into S slabs of kchunk) used to run after it.  Here the same
+// (layer, slab, 256 x 256 tile) items -- the split-K plan and 8-phase tile body of
+// sv_gemm_bf16_dual / sv_gemm_bf16, so every slab partial is bit-identical -- are pulled from a
+// queue by two launches of one kernel: WAIT = 1 on the CUs the wavefront leaves free, beside it,
+// polling the wavefront's arrival counters until the slab's time steps are final (dG^T_t is
+// stored, sc1, after iteration t's arrival and covered by iteration t - 1's: counter >= nub (T -
+// t_lo + 1) on every row block); WAIT = 0 on every CU once the wavefront is done, for what is
+// left.  Items go in readiness order: slabs from the last time steps down, in each the top layer
+// first (it runs ahead); queue 0 holds the items a counter can prove ready, queue 1 the rest
+// (layer 0's first slab: its dG^T_0 is final only when the launch ends).
+struct G8QLayer {
+  const bf16_t* A;    // dG^T [4H][T Bp]
+  const bf16_t* B;    // h^T (time-shifted), B rows = units
+  const bf16_t* B2;   // x^T (dual: columns past n1), or null
+  const unsigned* cnt;
+  float* ws;          // split-K slabs [S][M][N]
+  long lda, ldb, ldb2;
+  int N, n1, tiles;
+};
+struct G8Queue {
+  G8QLayer lay[WB_L];
+  unsigned* heads;  // [0]: queue 0, [SV_PCNT_STRIDE]: queue 1
+  unsigned* status;
+  unsigned limit;
+  int M, K, kchunk, S, P, nA, n1q;  // P: items per slab (all layers); nA / n1q: items in queue 0 / 1
+  int Bp, T, nub, nrb;
+};
+#ifndef SV_WAVE_DW_NT  // cache-policy bits added to the side launch's fills (2: non-temporal)
+#define SV_WAVE_DW_NT 0
+#endif
+#ifndef SV_WAVE_DW_SLEEP  // s_sleep argument between the side launch's polls (64 cycles each)
+#define SV_WAVE_DW_SLEEP 64
+#endif
+#ifndef SV_WAVE_DW_GRID  // most workgroups of the side launch
+#define SV_WAVE_DW_GRID 40
+#endif
+template <int WAIT>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_8qw_kernel(const G8Queue q) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int item;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  while (true) {
+    if (tid == 0) {
+      int i = -1;
+      const unsigned v = __hip_atomic_fetch_add(q.heads, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v < (unsigned)q.nA) {
+        i = (int)v;
+      } else if (!WAIT) {
+        const unsigned u = __hip_atomic_fetch_add(q.heads + SV_PCNT_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (u < (unsigned)q.n1q) i = q.nA + (int)u;
+      }
+      item = i;
+    }
+    __syncthreads();
+    const int i = item;
+    if (i < 0) break;
+    int l, s, tile;
+    if (i < q.nA) {  // slab S-1-i/P; in it the top layer's tiles first
+      const int sb = i / q.P, r = i - sb * q.P;
+      s = q.S - 1 - sb;
+      l = r < q.lay[2].tiles ? 2 : r < q.lay[2].tiles + q.lay[1].tiles ? 1 : 0;
+      tile = l == 2 ? r : l == 1 ? r - q.lay[2].tiles : r - q.lay[2].tiles - q.lay[1].tiles;
+    } else {
+      l = 0, s = 0, tile = i - q.nA;
+    }
+    // (field-wise selects: a dynamic index into the kernel-argument struct would copy it to scratch)
+    const G8QLayer& L2 = q.lay[2];
+    const G8QLayer& L1 = q.lay[1];
+    const G8QLayer& L0 = q.lay[0];
+    const bf16_t* A = l == 2 ? L2.A : l == 1 ? L1.A : L0.A;
+    const bf16_t* Bm = l == 2 ? L2.B : l == 1 ? L1.B : L0.B;
+    const bf16_t* B2 = l == 2 ? L2.B2 : l == 1 ? L1.B2 : L0.B2;
+    const unsigned* cnt = l == 2 ? L2.cnt : l == 1 ? L1.cnt : L0.cnt;
+    float* ws = l == 2 ? L2.ws : l == 1 ? L1.ws : L0.ws;
+    const long lda = l == 2 ? L2.lda : l == 1 ? L1.lda : L0.lda;
+    const long ldb = l == 2 ? L2.ldb : l == 1 ? L1.ldb : L0.ldb;
+    const long ldb2 = l == 2 ? L2.ldb2 : l == 1 ? L1.ldb2 : L0.ldb2;
+    const int N = l == 2 ? L2.N : l == 1 ? L1.N : L0.N;
+    const int n1 = l == 2 ? L2.n1 : l == 1 ? L1.n1 : L0.n1;
+    const int tiles_n = N / G256_BM;
+    const int tn = tile % tiles_n, tm = tile / tiles_n;
+    const int kbeg = s * q.kchunk;
+    const int nk = (min(q.K, kbeg + q.kchunk) - kbeg) / G256_BK;
+    if (WAIT) {
+      // a slow poll (~2 us between reads): a slab's steps finish ~0.1 ms apart, and 40 pollers at
+      // the recurrence's own rate (s_sleep 2) on the lines its arrivals and hand-off waits use slowed
+      // it by 8 % (r05)
+      if (tid == 0) {
+        const unsigned target = (unsigned)q.nub * (unsigned)(q.T - kbeg / q.Bp + 1);
+        for (int rb = 0; rb < q.nrb; ++rb) {
+          const unsigned* c = cnt + rb * SV_PCNT_STRIDE;
+          unsigned spins = 0;
+          while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load(q.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+            __builtin_amdgcn_s_sleep(SV_WAVE_DW_SLEEP);
+            if (++spins > (q.limit >> 5)) {
+              __hip_atomic_fetch_or(q.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+    g8_f32x4 acc[8][4];
+    g8_tile<0, WAIT ? 16 | SV_WAVE_DW_NT : 0, WAIT ? SV_WAVE_DW_NT : 0>(A, lda, Bm, ldb, G256AFrag{},
+                                                                        G256Dual{B2, ldb2, n1}, tm, tn, kbeg, nk, smem, acc);
+    g8_epilogue<G8_SLAB>(acc, ws, N, (long)s * q.M * N, tm, tn, wr, wc, lane, nullptr, nullptr, 0.f);
+  }
 }
 
 }  // namespace
@@ -1091,9 +1207,91 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     }
     int rc = wbf_transposes(L, F, H, w_ih, w_hh, whhT_l, wihT_l, main);
     if (rc) return rc;
+    // the weight gradients beside the wavefront on the CUs it leaves free (gemm_bf16_8qw_kernel)
+    const int cus = sv_stream_cus(main);
+    const int side_grid = std::min(SV_WAVE_DW_GRID, cus - L * (H / 32) * ((B + 31) / 32));
+    const BPlan p = plan_bf16(4 * H, H, TBp);
+    bool beside = SV_WAVE_DW_SIDE && L == WB_L && side_grid >= 8 && side[0] && p.bm == G256_BM && p.splitk > 1 &&
+                  gemm256_ok(4 * H, 2 * H, TBp) && 4L * H * TBp * 2 < (1L << 32) && TBp % 8 == 0 && ldhT % 8 == 0;
+    G8Queue q{};
+    if (beside) {
+      for (int l = 0; l < L; ++l) {
+        const int Fl = l == 0 ? F : H;
+        const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
+        const bool dual = l > 0;  // layer 0: dW_hh only (its N = F dW_ih runs after, as before)
+        if ((dual && (Fl % G256_BM || ld_xT[l] % 8 || ((uintptr_t)xT[l] & 15))) || ((uintptr_t)dgT[l] & 15) ||
+            ((uintptr_t)hT[l] & 15) || !g8_ok(ws.gws, dual ? H + Fl : H, nullptr, nullptr))
+          beside = false;
+        G8QLayer& ql = q.lay[l];
+        ql.A = dgT[l];
+        ql.lda = TBp;
+        ql.B = hT[l];
+        ql.ldb = ldhT;
+        ql.B2 = dual ? xT[l] : nullptr;
+        ql.ldb2 = dual ? ld_xT[l] : 0;
+        ql.n1 = H;
+        ql.N = dual ? H + Fl : H;
+        ql.tiles = (4 * H / G256_BM) * (ql.N / G256_BM);
+        ql.ws = ws.gws;
+        ql.cnt = sync + SV_SYNC_CNT + (size_t)l * SV_PCNT_ROWS * SV_PCNT_STRIDE;
+      }
+    }
+    if (beside) {
+      q.heads = sync + SV_SYNC_CNT + (size_t)WB_L * SV_PCNT_ROWS * SV_PCNT_STRIDE;  // channel 3, rows 0-1
+      q.status = sync;
+      q.limit = sv_persist_limit();
+      q.M = 4 * H;
+      q.K = TBp;
+      q.kchunk = p.kchunk;
+      q.S = p.splitk;
+      q.P = q.lay[0].tiles + q.lay[1].tiles + q.lay[2].tiles;
+      q.n1q = q.lay[0].tiles;
+      q.nA = q.S * q.P - q.n1q;
+      q.Bp = Bp;
+      q.T = T;
+      q.nub = H / 32;
+      q.nrb = (B + 31) / 32;
+      // every counter the side launch reads is zero before it starts (the wavefront zeroes its own
+      // channels again right before its launch, while they still read zero)
+      if ((rc = sv_zero_counters(sync + SV_SYNC_CNT, WB_L + 1, (long)SV_PCNT_ROWS * SV_PCNT_STRIDE,
+                                 std::max(q.nrb, 2) * SV_PCNT_STRIDE, main)))
+        return rc;
+      if ((e = hipEventRecord(ev[0], main)) != hipSuccess) return (int)e;
+      if ((e = hipStreamWaitEvent(side[0], ev[0], 0)) != hipSuccess) return (int)e;
+      hipLaunchKernelGGL(gemm_bf16_8qw_kernel<1>, dim3(side_grid), dim3(512), G256_LDS, side[0], q);
+      SV_LAUNCH_CHECK();
+      if ((e = hipEventRecord(ev[1], side[0])) != hipSuccess) return (int)e;
+    }
     rc = sv_wave_bwd_bf16(L, T, B, H, whhT_l, wihT_l, gates, c_tm, dh_last, dx, dgT, (char*)workspace + per * L,
-                              sync, main, db_ih, db_hh, probe ? probe[0] : nullptr, probe ? probe[1] : nullptr);
+                              sync, main, db_ih, db_hh, probe ? probe[0] : nullptr, probe ? probe[1] : nullptr,
+                              beside || SV_WAVE_DGT_SC1 ? 1 : 0);
     if (rc) return rc;
+    if (beside) {
+      hipLaunchKernelGGL(gemm_bf16_8qw_kernel<0>, dim3(cus), dim3(512), G256_LDS, main, q);
+      SV_LAUNCH_CHECK();
+      if ((e = hipStreamWaitEvent(main, ev[1], 0)) != hipSuccess) return (int)e;
+      const long slab0 = 4L * H * H;
+      for (int l = L - 1; l >= 0; --l) {  // the slabs' sums (sv_gemm_bf16_dual's / sv_gemm_bf16's reduce)
+        const G8QLayer& ql = q.lay[l];
+        const long slab = 4L * H * ql.N;
+        const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
+        if (l > 0)
+          hipLaunchKernelGGL(slab_reduce_bf_kernel, dim3(grid), dim3(256), 0, main, ql.ws, q.S, slab, dw_hh[l], (long)H,
+                             4 * H, ql.N, 0.f, nullptr, nullptr, nullptr, dw_ih[l], (long)H, H);
+        else
+          hipLaunchKernelGGL(slab_reduce_bf_kernel, dim3((int)std::min<long>((slab0 + 255) / 256, 4096)), dim3(256), 0,
+                             main, ql.ws, q.S, slab0, dw_hh[0], (long)H, 4 * H, H, 0.f, nullptr, nullptr);
+        SV_LAUNCH_CHECK();
+        if (l == 0) {
+          const BBwdWs ws = carve_bbwd((char*)workspace, T, B, std::max(F, H), H);
+          if ((rc = sv_gemm_bf16(4 * H, F, TBp, dgT[0], TBp, xT[0], ld_xT[0], dw_ih[0], F, nullptr, nullptr, 0.f,
+                                 ws.gws, main)))
+            return rc;
+        }
+        if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
+      }
+      return SV_OK;
+    }
     for (int l = L - 1; l >= 0; --l) {
       const int Fl = l == 0 ? F : H;
       const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);

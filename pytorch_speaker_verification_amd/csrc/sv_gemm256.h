@@ -331,23 +331,16 @@ __device__ __forceinline__ void g8_epilogue_bf16_lds(g8_f32x4 (&acc)[8][4], bf16
   }
 }
 
-template <int EPI, int AF = 0>
-__global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __restrict__ A, long lda,
-                                                             const bf16_t* __restrict__ B, long ldb, void* __restrict__ C,
-                                                             long ldc, long slab, int M, int N, int K, int kchunk,
-                                                             const float* __restrict__ bias0,
-                                                             const float* __restrict__ bias1, float beta,
-                                                             G256AFrag af = G256AFrag{}, G256Dual dual = G256Dual{}) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+// one 256 x 256 tile (tm, tn) of C = A . B^T (B2 past dual.n1) over the k-tiles [kbeg, kbeg + 64 nk)
+// into acc: gemm_bf16_8q_kernel's prologue and 8-phase k-loop, shared by the queue-driven form.
+// AUXA: cache-policy bits of the A fills (16 = sc1: A written in the same launch window by another
+// kernel, read past the L1)
+template <int AF, int AUXA = 0, int AUXB = 0>
+__device__ __forceinline__ void g8_tile(const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ B, long ldb,
+                                        const G256AFrag& af, const G256Dual& dual, int tm, int tn, int kbeg, int nk,
+                                        char* smem, g8_f32x4 (&acc)[8][4]) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int tiles_n = N / G256_BM;
-  const int nwg = tiles_n * (M / G256_BM);
-  int id = xcd_remap(blockIdx.x, nwg), sl = 0;
-  if (gridDim.y > 1) splitk_tile(nwg, id, sl);
-  const int tn = id % tiles_n, tm = id / tiles_n;
-  const int kbeg = sl * kchunk;
-  const int nk = (min(K, kbeg + kchunk) - kbeg) / G256_BK;
   const int wr = w >> 2, wc = w & 3;
   G256Stage sa, sb;
   if constexpr (!AF) sa.init(A, lda, tm * G256_BM, kbeg, tid);
@@ -378,12 +371,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
                                        (lds_vptr_t)(lds + ((2 * i + (w >> 2)) * 4 + (w & 3)) * 1024), 16, 0, 0);
     } else {
       __builtin_amdgcn_global_load_lds((glb_vptr_t)(sa.src[i] + kt * G256_BK), (lds_vptr_t)(lds + (w * 64 + 512 * i) * 16),
-                                       16, 0, 0);
+                                       16, 0, AUXA);
     }
   };
   auto fill_b = [&](int kt, int i) {
     __builtin_amdgcn_global_load_lds((glb_vptr_t)(sb.src[i] + kt * G256_BK),
-                                     (lds_vptr_t)(stage(kt) + OPB + (w * 64 + 512 * i) * 16), 16, 0, 0);
+                                     (lds_vptr_t)(stage(kt) + OPB + (w * 64 + 512 * i) * 16), 16, 0, AUXB);
   };
   auto read_a = [&](const char* As, int mt, int ks) -> bf16x8_t {
     const int row = wr * 128 + 16 * mt + fr;
@@ -398,7 +391,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
     const int row = wc * 64 + 16 * nt + fr;
     return *reinterpret_cast<const bf16x8_t*>(Bs + row * 128 + g256_phys_slot(row, 4 * ks + fq) * 16);
   };
-  g8_f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -499,6 +491,27 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   }
+}
+
+template <int EPI, int AF = 0>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __restrict__ A, long lda,
+                                                             const bf16_t* __restrict__ B, long ldb, void* __restrict__ C,
+                                                             long ldc, long slab, int M, int N, int K, int kchunk,
+                                                             const float* __restrict__ bias0,
+                                                             const float* __restrict__ bias1, float beta,
+                                                             G256AFrag af = G256AFrag{}, G256Dual dual = G256Dual{}) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tiles_n = N / G256_BM;
+  const int nwg = tiles_n * (M / G256_BM);
+  int id = xcd_remap(blockIdx.x, nwg), sl = 0;
+  if (gridDim.y > 1) splitk_tile(nwg, id, sl);
+  const int tn = id % tiles_n, tm = id / tiles_n;
+  const int kbeg = sl * kchunk;
+  const int nk = (min(K, kbeg + kchunk) - kbeg) / G256_BK;
+  const int wr = w >> 2, wc = w & 3;
+  g8_f32x4 acc[8][4];
+  g8_tile<AF>(A, lda, B, ldb, af, dual, tm, tn, kbeg, nk, smem, acc);
   if constexpr (EPI == G8_STORE_BF16)
     g8_epilogue_bf16_lds(acc, reinterpret_cast<bf16_t*>(C), ldc, tm, tn, wr, wc, w, lane, bias0, bias1, smem);
   else

@@ -1191,7 +1191,7 @@ size_t sv_wave_bwd_scratch(int L, int T, int B, int H) {
 int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, const bf16_t* const* wihT,
                      const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
                      bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
-                     float* const* db_hh, hipEvent_t pre, hipEvent_t post) {
+                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, int dgt_sc1) {
   if (!sv_wave_bwd_fits(L, B, H, sv_stream_cus(stream))) return SV_ESHAPE;
   if (!scratch || ((uintptr_t)scratch & 15) || !sync || !dh_last || !whhT || !wihT || !acts || !c_tm || !dx || !dgT)
     return SV_EARG;
@@ -1224,6 +1224,7 @@ int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, cons
   a.Bp = (B + 7) & ~7;
   a.H = H;
   a.lddgT = (long)T * a.Bp;
+  a.dgt_sc1 = dgt_sc1 && 4L * H * a.lddgT * 2 < (1L << 32);  // (one buffer descriptor per layer)
   hipError_t e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
   const int rc = sv_wave_bwd_launch(a, stream);

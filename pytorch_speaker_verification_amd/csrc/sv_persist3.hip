@@ -945,13 +945,21 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     WB_MARK(3);  // 3: dG_t hand-off stores + drain + arrival
     if (t >= 0 && a.dgT[l]) {  // dG_t^T (the dW GEMMs' operand), then the next step's operands
+      // dgt_sc1: written through (16-B sc1 stores), because the weight-gradient GEMM beside this
+      // launch reads them once iteration t - 1 has arrived (its vmcnt(0) covers these stores)
+      const __amdgpu_buffer_rsrc_t rt = sv_rsrc(a.dgT[l], a.dgt_sc1 ? (unsigned)(4L * H * a.lddgT * 2) : 0u);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int q = tid + 256 * i, gu = q >> 2, c = q & 3;
         const int gq = gu / U, gj = j0 + gu % U, gc = b0 + 8 * c;
-        if (gc < a.Bp && gj < H)
-          *reinterpret_cast<uint4*>(a.dgT[l] + ((long)gq * H + gj) * a.lddgT + (long)t * a.Bp + gc) =
-              *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
+        if (gc < a.Bp && gj < H) {
+          const long eo = ((long)gq * H + gj) * a.lddgT + (long)t * a.Bp + gc;
+          const uint4 v = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
+          if ((SV_WAVE_DW_SIDE || SV_WAVE_DGT_SC1) && a.dgt_sc1)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rt, (unsigned)(eo * 2), 0, 16 /* sc1 */);
+          else
+            *reinterpret_cast<uint4*>(a.dgT[l] + eo) = v;
+        }
       }
     }
     if (t > 0) load_ew(t - 1);
