@@ -565,6 +565,9 @@ struct G8Queue {
 #ifndef SV_WAVE_DW_NT  // cache-policy bits added to the side launch's fills (2: non-temporal)
 #define SV_WAVE_DW_NT 0
 #endif
+#ifndef SV_WAVE_DW_QUEUE  // A/B: the wavefront's weight gradients as one queue-driven launch after it (r05:
+#define SV_WAVE_DW_QUEUE 0   // 319 us against 310 for the three per-layer launches)
+#endif
 #ifndef SV_WAVE_DW_SLEEP  // s_sleep argument between the side launch's polls (64 cycles each)
 #define SV_WAVE_DW_SLEEP 64
 #endif
@@ -1211,17 +1214,17 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     const int cus = sv_stream_cus(main);
     const int side_grid = std::min(SV_WAVE_DW_GRID, cus - L * (H / 32) * ((B + 31) / 32));
     const BPlan p = plan_bf16(4 * H, H, TBp);
-    bool beside = SV_WAVE_DW_SIDE && L == WB_L && side_grid >= 8 && side[0] && p.bm == G256_BM && p.splitk > 1 &&
-                  gemm256_ok(4 * H, 2 * H, TBp) && 4L * H * TBp * 2 < (1L << 32) && TBp % 8 == 0 && ldhT % 8 == 0;
+    bool queued = (SV_WAVE_DW_QUEUE || SV_WAVE_DW_SIDE) && L == WB_L && p.bm == G256_BM && p.splitk > 1 &&
+                  gemm256_ok(4 * H, 2 * H, TBp) && TBp % 8 == 0 && ldhT % 8 == 0;
     G8Queue q{};
-    if (beside) {
+    if (queued) {
       for (int l = 0; l < L; ++l) {
         const int Fl = l == 0 ? F : H;
         const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
         const bool dual = l > 0;  // layer 0: dW_hh only (its N = F dW_ih runs after, as before)
         if ((dual && (Fl % G256_BM || ld_xT[l] % 8 || ((uintptr_t)xT[l] & 15))) || ((uintptr_t)dgT[l] & 15) ||
             ((uintptr_t)hT[l] & 15) || !g8_ok(ws.gws, dual ? H + Fl : H, nullptr, nullptr))
-          beside = false;
+          queued = false;
         G8QLayer& ql = q.lay[l];
         ql.A = dgT[l];
         ql.lda = TBp;
@@ -1236,7 +1239,8 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
         ql.cnt = sync + SV_SYNC_CNT + (size_t)l * SV_PCNT_ROWS * SV_PCNT_STRIDE;
       }
     }
-    if (beside) {
+    const bool beside = SV_WAVE_DW_SIDE && queued && side_grid >= 8 && side[0] && 4L * H * TBp * 2 < (1L << 32);
+    if (queued) {
       q.heads = sync + SV_SYNC_CNT + (size_t)WB_L * SV_PCNT_ROWS * SV_PCNT_STRIDE;  // channel 3, rows 0-1
       q.status = sync;
       q.limit = sv_persist_limit();
@@ -1253,9 +1257,11 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       q.nrb = (B + 31) / 32;
       // every counter the side launch reads is zero before it starts (the wavefront zeroes its own
       // channels again right before its launch, while they still read zero)
-      if ((rc = sv_zero_counters(sync + SV_SYNC_CNT, WB_L + 1, (long)SV_PCNT_ROWS * SV_PCNT_STRIDE,
-                                 std::max(q.nrb, 2) * SV_PCNT_STRIDE, main)))
+      if ((rc = sv_zero_counters(beside ? sync + SV_SYNC_CNT : q.heads, beside ? WB_L + 1 : 1,
+                                 (long)SV_PCNT_ROWS * SV_PCNT_STRIDE, std::max(q.nrb, 2) * SV_PCNT_STRIDE, main)))
         return rc;
+    }
+    if (beside) {
       if ((e = hipEventRecord(ev[0], main)) != hipSuccess) return (int)e;
       if ((e = hipStreamWaitEvent(side[0], ev[0], 0)) != hipSuccess) return (int)e;
       hipLaunchKernelGGL(gemm_bf16_8qw_kernel<1>, dim3(side_grid), dim3(512), G256_LDS, side[0], q);
@@ -1266,10 +1272,10 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
                               sync, main, db_ih, db_hh, probe ? probe[0] : nullptr, probe ? probe[1] : nullptr,
                               beside || SV_WAVE_DGT_SC1 ? 1 : 0);
     if (rc) return rc;
-    if (beside) {
+    if (queued) {
       hipLaunchKernelGGL(gemm_bf16_8qw_kernel<0>, dim3(cus), dim3(512), G256_LDS, main, q);
       SV_LAUNCH_CHECK();
-      if ((e = hipStreamWaitEvent(main, ev[1], 0)) != hipSuccess) return (int)e;
+      if (beside && (e = hipStreamWaitEvent(main, ev[1], 0)) != hipSuccess) return (int)e;
       const long slab0 = 4L * H * H;
       for (int l = L - 1; l >= 0; --l) {  // the slabs' sums (sv_gemm_bf16_dual's / sv_gemm_bf16's reduce)
         const G8QLayer& ql = q.lay[l];
