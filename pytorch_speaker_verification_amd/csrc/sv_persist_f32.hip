@@ -520,6 +520,9 @@ constexpr int PH_BM = 32;                      // rows of a half
                          // time unchanged: the lines land closer to their use and fewer are evicted first; 0: A/B)
 #define SV_PF32_PF_HALF 1
 #endif
+#ifndef SV_PF32_EDMA  // A/B builds: k-groups before the backward k-loop's end at which the next half-step's
+#define SV_PF32_EDMA 0   // operand DMA is issued into a second operand image set (r05: 12 / 24 measured slower,
+#endif                   // DESIGN §4); 0: after the half-step's hand-off, one set
 #ifndef SV_PF32_PF_SPLIT  // per-half triggers: half h's rows of step s once half h of step s + 1 is done (0: A/B)
 #define SV_PF32_PF_SPLIT 1
 #endif
@@ -633,13 +636,14 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
   constexpr int LDT = PH_BM + 4;     // gts [128][LDT] (over red)
   constexpr int FBLK = NKG * 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* ea = reinterpret_cast<float*>(smem);  // [32][128] activations of the half-step
-  float* ec = ea + PH_BM * 4 * PF_U;           // [32][32] c_{t-1}
-  float* eu = ec + PH_BM * PF_U;               // [32][32] dh_up
-  float* red = eu + PH_BM * PF_U;              // [4][32][LDR]
+  // operand image set(s): [32][128] activations of the half-step, [32][32] c_{t-1}, [32][32] dh_up;
+  // with SV_PF32_EDMA two sets, the next half-step's filled during this one's k-loop
+  constexpr int ESET = PH_BM * 6 * PF_U;       // floats per set
+  float* red = reinterpret_cast<float*>(smem) + ESET;  // [4][32][LDR]
   float* gts = red;
-  float* dgs = ea;
   char* wl = reinterpret_cast<char*>(red + 4 * PH_BM * LDR);
+  float* eset[2] = {reinterpret_cast<float*>(smem),
+                    SV_PF32_EDMA ? reinterpret_cast<float*>(wl + (size_t)4 * NL * 1024) : reinterpret_cast<float*>(smem)};
   if ((int)blockIdx.x >= ncomp) {  // a helper workgroup: operand prefetch only
     pf32_bwd_prefetch(acts, c_tm, dhup, up_full, T, B, 8 * NKG, cnt, nub, ncomp, npf, status, limit, smem);
     return;
@@ -671,10 +675,13 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
   const int quad = tid & 7, erow = tid >> 3;
   // half-step (tt, hf)'s operands -> LDS: wave g: 4 activation pieces (rows 8 g ..), 1 of c_{t-1}, 1
   // of dh_up; absent operands written as zeros into the same slots
-  auto load_ew = [&](int tt, int hf) {
+  auto load_ew = [&](int tt, int hf, int set) {
 #ifdef SV_PF32_HOTOPS  // A/B diagnostic (results invalid): every step reads step T-1's operands, cache-hot
     tt = T - 1;
 #endif
+    float* ea = eset[set];
+    float* ec = ea + PH_BM * 4 * PF_U;
+    float* eu = ec + PH_BM * PF_U;
     int z = 0;
     asm volatile("" : "+v"(z));
     const int gz = g + z, b0 = rb * PF_BM + hf * PH_BM;
@@ -712,7 +719,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
   }
   __syncthreads();
 #endif
-  load_ew(T - 1, 0);
+  load_ew(T - 1, 0, 0);
+  int cs = 0;  // the current half-step's operand image set
   // threads < 128: bias-gradient partial of gate column tid over t and the row block, accumulated in
   // fp64 (320 fp32 half-step sums of a cancelling sum: in fp32 the c2 bias gradients were 8e-6 off)
   double dbs = 0.0;
@@ -763,8 +771,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         for (int p = 0; p < P; ++p) fa[p] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + 1024u * p, 0, 16 /* sc1 */);
         f32x4 w = wfrag(0);
         __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int kg = 0; kg < NKG; ++kg) {
+        auto kstep = [&](int kg) {
           const f32x4 a = __builtin_bit_cast(f32x4, fa[kg % P]);
           const f32x4 nw = kg + 1 < NKG ? wfrag(kg + 1) : w;
           acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0], w[0], acc0, 0, 0, 0);
@@ -774,9 +781,29 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
           if (kg + P < NKG) fa[kg % P] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + 1024u * (kg + P), 0, 16);
           w = nw;
           __builtin_amdgcn_sched_barrier(0);
+        };
+        constexpr int KE = NKG - SV_PF32_EDMA;
+#pragma unroll
+        for (int kg = 0; kg < KE; ++kg) kstep(kg);
+        if (SV_PF32_EDMA) {
+          // the next half-step's operands into the other image set, behind this k-loop's last A
+          // fragment loads: hipcc's counted waits of the last k-groups do not count these LDS-DMA
+          // pieces, so they wait for them ~SV_PF32_EDMA k-groups after the issue (L2-warm: the
+          // helper workgroups fetched them), instead of the next half-step's first barrier waiting
+          if (hf == 0)
+            load_ew(t, 1, cs ^ 1);
+          else if (t > 0)
+            load_ew(t - 1, 0, cs ^ 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int kg = KE; kg < NKG; ++kg) kstep(kg);
         }
       }
       PB_STAMP(1);  // 1: k-loop (A fragments from the hand-off + MFMAs)
+      float* ea = eset[cs];
+      float* ec = ea + PH_BM * 4 * PF_U;
+      float* eu = ec + PH_BM * PF_U;
+      float* dgs = ea;
 #pragma unroll
       for (int i = 0; i < 16; ++i) red[(g * PH_BM + acc_row(i, lane)) * LDR + r] = acc0[i] + acc1[i];
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
@@ -880,13 +907,14 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         }
       }
 #endif
-      if (hf == 0 || t > 0) {
+      if ((hf == 0 || t > 0) && (!SV_PF32_EDMA || t == T - 1)) {  // (SV_PF32_EDMA: issued in the k-loop)
         __syncthreads();  // dgs / gts read by every wave before the next half-step's operands land
         if (hf == 0)
-          load_ew(t, 1);
+          load_ew(t, 1, SV_PF32_EDMA ? cs ^ 1 : 0);
         else
-          load_ew(t - 1, 0);
+          load_ew(t - 1, 0, SV_PF32_EDMA ? cs ^ 1 : 0);
       }
+      if (SV_PF32_EDMA) cs ^= 1;
       PB_STAMP(5);  // 5: off-chain (bias partials, dG / dG^T stores, next operand DMA issue)
     }
   }
@@ -921,7 +949,7 @@ namespace {
 #define SV_PF_FWD_NV 16
 #endif
 #ifndef SV_PH_BWD_NL  // A/B builds: the backward's weight k-groups in LDS (the rest of 32 in VGPRs)
-#define SV_PH_BWD_NL 24
+#define SV_PH_BWD_NL (SV_PF32_EDMA ? 23 : 24)  // (the second operand image set takes 24 KB of LDS)
 #endif
 constexpr int PF_FWD_NV = SV_PF_FWD_NV, PF_FWD_NL = 32 - SV_PF_FWD_NV, PH_BWD_NL = SV_PH_BWD_NL,
               PH_BWD_NV = 96 - PF_NA - PH_BWD_NL,
@@ -930,8 +958,8 @@ constexpr size_t pf_fwd_lds() {
   return (size_t)PF_NB * PF_CH + (size_t)PF_BM * 4 * PF_U * 4 + (size_t)4 * PF_FWD_NL * 1024;
 }
 constexpr size_t ph_bwd_lds() {
-  return (size_t)PH_BM * 4 * PF_U * 4 + 2 * (size_t)PH_BM * PF_U * 4 + (size_t)4 * PH_BM * (PF_U + 4) * 4 +
-         (size_t)4 * PH_BWD_NL * 1024;
+  return (SV_PF32_EDMA ? 2 : 1) * ((size_t)PH_BM * 4 * PF_U * 4 + 2 * (size_t)PH_BM * PF_U * 4) +
+         (size_t)4 * PH_BM * (PF_U + 4) * 4 + (size_t)4 * PH_BWD_NL * 1024;
 }
 static_assert(pf_fwd_lds() <= 160 * 1024 && ph_bwd_lds() <= 160 * 1024, "LDS");
 static_assert((size_t)4 * PF_U * (PH_BM + 4) <= (size_t)4 * PH_BM * (PF_U + 4), "gts fits in red");
