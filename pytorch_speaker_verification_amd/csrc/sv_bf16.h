@@ -376,6 +376,15 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
                            const float* c_tm, const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT,
                            bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int xcd, unsigned* sync,
                            unsigned limit, int fault, int dbg, float* dbp);
+// the 16-row wide-tile backward (sv_persist3.hip; 257..336 rows at H = 768; grid nub x nrb).  A/B
+// builds only: at c5's 320 rows it measured equal to the 32 x 32 tile
+#ifndef SV_PBWD16
+#define SV_PBWD16 0
+#endif
+int sv_persist16_bwd_ok(int B, int H, int cus);
+int sv_persist16_bwd_launch(int nub, int nrb, hipStream_t stream, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
+                            const float* dhup, int up_full, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B,
+                            int H, unsigned* cnt, int xcd, unsigned* sync, unsigned limit, int fault, float* dbp);
 // launcher of the wide-tile persistent forward (sv_persist3.hip; no fused input projection)
 int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whh_bf, bf16_t* gates, float* c_tm,
                            float* h_tm, bf16_t* h_bf, bf16_t* hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt,

@@ -1116,7 +1116,7 @@ extern "C" int sv_persist_bwd_ok(int B, int H) { return sv_persist_bwd_fits(B, H
 // bf16; the 64-row count bounds the 32-row one)
 extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H) {
   const size_t frag = (size_t)T * (size_t)((B + BF_BM - 1) / BF_BM) * BF_BM * 4 * H * sizeof(bf16_t);
-  return frag + (size_t)((B + 31) / 32) * 4 * H * sizeof(float);  // + bias-gradient partials
+  return frag + (size_t)((B + 15) / 16) * 4 * H * sizeof(float);  // + bias-gradient partials (16-row blocks)
 }
 
 // one layer's backward recurrence for all t (reverse), on `stream`: dG (bf16, row-major and
@@ -1133,8 +1133,9 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
   const int Bp = (B + 7) & ~7;
   const long lddgT = (long)T * Bp;
   const bool wide = pbwd3_ok(B, H, cus);
-  const int bm = wide ? 32 : persist_bm(B, H, cus);
-  const dim3 grid(wide ? H / 64 : (H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
+  const bool r16 = !wide && !dg && sv_persist16_bwd_ok(B, H, cus);  // (writes no row-major dG)
+  const int bm = wide ? 32 : r16 ? 16 : persist_bm(B, H, cus);
+  const dim3 grid(wide || r16 ? H / 64 : (H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
   // bias-gradient partials [nrb][4H] after the fragment-order slots (db_ih NULL: not computed)
   float* dbp = db_ih ? reinterpret_cast<float*>(reinterpret_cast<char*>(dgf) +
                                                 (size_t)T * ((B + BF_BM - 1) / BF_BM) * BF_BM * 4 * H * sizeof(bf16_t))
@@ -1143,7 +1144,11 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   // A-fragment prefetch depth 8 at H = 768 (measured: 4 / 16 no better)
-  if (wide) {
+  if (r16) {
+    const int rc = sv_persist16_bwd_launch((int)grid.x, (int)grid.y, stream, whhT, acts, c_tm, dhup, up_full, dgT, lddgT,
+                                           dgf, T, Bp, B, H, cnt, kPersistXcd, sync, persist_limit(), persist_fault(), dbp);
+    if (rc) return rc;
+  } else if (wide) {
     const int rc = sv_persist3_bwd_launch(dim3(grid.x * grid.y), (int)grid.x, stream, whhT, acts, c_tm, dhup, up_full,
                                           dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, kPersistXcd, sync, persist_limit(),
                                           persist_fault(), kPbwdDebug, dbp);
