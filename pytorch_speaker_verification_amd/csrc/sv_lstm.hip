@@ -566,6 +566,104 @@ GemmPlan plan_gemm(int M, int N, int K, bool fine = false) {
   return p;
 }
 
+#ifndef SV_GEMM_NARROW  // 0: the N <= 48 exact NT GEMMs on the 64 x 64 tiles (A/B)
+#define SV_GEMM_NARROW 1
+#endif
+// ---- narrow NT GEMM (N <= 48): layer 0's dW_ih = dG^T x (M = 4H, N = F = 40, K = T B) ----
+// The 64 x 64 tiles (4 waves of v_mfma_f32_32x32x2_f32) padded N = 40 to 64 and ran this shape at
+// 75 TF/s (334 us at c2); it streams dG^T (1.26 GB at c2) once.  Here a workgroup is 128 rows x 48
+// columns (3 blocks of 16) over a K chunk: v_mfma_f32_16x16x4_f32, exact fp32 products, each wave
+// 32 rows (2 x 3 accumulators).  A lane reads 4 consecutive k of its row (one 16-B LDS read) and
+// spends them over 4 MFMAs (MFMA j takes k = 4 q + j of lane group q, for A and B alike, so the 4
+// MFMAs cover 16 k); LDS images are [rows][32 k] with 16-B chunk c of row r at c ^ (r & 7), filled
+// by LDS-DMA (two stages of 32 k).  Split-K slabs, reduced by slab_reduce_kernel.
+constexpr int GN_BM = 128, GN_BN = 48, GN_BK = 32;
+__global__ __launch_bounds__(256) void gemm_f32_narrow_kernel(const float* __restrict__ A, long lda,
+                                                              const float* __restrict__ B, long ldb,
+                                                              float* __restrict__ slab, long slab_stride, int M, int N,
+                                                              int K, int kchunk) {
+  __shared__ __attribute__((aligned(16))) float lds[2][(GN_BM + GN_BN) * GN_BK];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int m0 = blockIdx.x * GN_BM, s = blockIdx.y;
+  const int kbeg = s * kchunk, nk = (min(K, kbeg + kchunk) - kbeg) / GN_BK;
+  // DMA map: chunk q (16 B) of the stage: A rows 0..127 (q < 1024), then B rows 0..47
+  auto fill = [&](int kt, int st) {
+    const int k0 = kbeg + kt * GN_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = tid + 256 * i, row = q >> 3, pc = q & 7, c = pc ^ (row & 7);
+      __builtin_amdgcn_global_load_lds((gf_glb_ptr_t)(A + (long)(m0 + row) * lda + k0 + 4 * c),
+                                       (gf_lds_ptr_t)(&lds[st][0] + 4 * (w * 64 + 256 * i)), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i == 1 && w >= 2) break;  // 384 chunks of B: waves 0-1 issue a second one (wave-uniform)
+      const int q = tid + 256 * i, row = q >> 3, pc = q & 7, c = pc ^ (row & 7);
+      const int n = min(row, N - 1);  // padding columns read row N - 1 (their sums are not stored)
+      __builtin_amdgcn_global_load_lds((gf_glb_ptr_t)(B + (long)n * ldb + k0 + 4 * c),
+                                       (gf_lds_ptr_t)(&lds[st][GN_BM * GN_BK] + 4 * (w * 64 + 256 * i)), 16, 0, 0);
+    }
+  };
+  f32x4 acc[2][3];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) fill(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage st landed for every wave; stage st ^ 1 free
+    if (kt + 1 < nk) fill(kt + 1, st ^ 1);
+    const float* As = &lds[st][0];
+    const float* Bs = &lds[st][GN_BM * GN_BK];
+#pragma unroll
+    for (int ks = 0; ks < GN_BK / 16; ++ks) {
+      const int c = 4 * ks + lq;
+      f32x4 a[2], b[3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = 32 * w + 16 * i + lr;
+        a[i] = *reinterpret_cast<const f32x4*>(As + row * GN_BK + 4 * (c ^ (row & 7)));
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int row = 16 * j + lr;
+        b[j] = *reinterpret_cast<const f32x4*>(Bs + row * GN_BK + 4 * (c ^ (row & 7)));
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
+    }
+  }
+  // lane holds C[4 lq + v][lr] of each 16 x 16 block
+  float* Cz = slab + (long)s * slab_stride;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int col = 16 * j + lr;
+      if (col >= N) continue;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) Cz[(long)(m0 + 32 * w + 16 * i + 4 * lq + v) * N + col] = acc[i][j][v];
+    }
+}
+// the narrow kernel's plan: exact products, NT, N <= 48, whole 128-row tiles and 32-k steps; K
+// chunks of at least 1024 over up to 32 slabs (c2: 24 row tiles x 32 slabs = 768 workgroups)
+bool narrow_ok(int M, int N, int K, long lda, long ldb, int mode) {
+  return mode == 0 && SV_GEMM_NARROW && N <= GN_BN && M % GN_BM == 0 && K % GN_BK == 0 && K >= 4096 && lda % 4 == 0 &&
+         ldb % 4 == 0;
+}
+int narrow_splitk(int K, int& kchunk) {
+  const int sk = std::max(1, std::min(32, K / 1024));
+  kchunk = ((K + sk - 1) / sk + GN_BK - 1) / GN_BK * GN_BK;
+  return (K + kchunk - 1) / kchunk;
+}
+
 // ---- 256 x BN LDS-DMA tile (sv_gemm_f32_256.h) for the exact-fp32 NT GEMMs that tile exactly ----
 #ifndef SV_F32_MF
 #define SV_F32_MF 32  // MFMA shape of the 256-tile kernel (16: v_mfma_f32_16x16x4_f32, A/B builds)
@@ -698,6 +796,10 @@ extern "C" size_t sv_gemm_f32_workspace(int M, int N, int K) {
     const GemmPlan q = plan_gf256(M, N, K);
     if (q.splitk > 1) ws = std::max(ws, (size_t)q.splitk * M * N * sizeof(float));
   }
+  if (narrow_ok(M, N, K, K, K, 0)) {  // (the narrow kernel's slabs)
+    int kchunk;
+    ws = std::max(ws, (size_t)narrow_splitk(K, kchunk) * M * N * sizeof(float));
+  }
   return ws;
 }
 
@@ -718,6 +820,19 @@ int gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, const float* A, 
   if (((uintptr_t)A | (uintptr_t)B) & 15) return SV_EALIGN;
   if (a_kcontig && b_kcontig && gemm_x() == 0 && gf256_ok(M, N, K, C, ldc, bias0, bias1))
     return gemm_f32_256(A, lda, B, ldb, C, ldc, M, N, K, bias0, bias1, beta, workspace, stream);
+  if (a_kcontig && b_kcontig && workspace && narrow_ok(M, N, K, lda, ldb, gemm_x())) {
+    int kchunk;
+    const int sk = narrow_splitk(K, kchunk);
+    const long slab = (long)M * N;
+    hipLaunchKernelGGL(gemm_f32_narrow_kernel, dim3(M / GN_BM, sk), dim3(256), 0, stream, A, lda, B, ldb, workspace,
+                       slab, M, N, K, kchunk);
+    SV_LAUNCH_CHECK();
+    const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, stream, workspace, sk, slab, C, ldc, M, N, beta, bias0,
+                       bias1);
+    SV_LAUNCH_CHECK();
+    return SV_OK;
+  }
   const GemmPlan p = plan_gemm(M, N, K, fine && workspace != nullptr);
   const bool ak = a_kcontig != 0, bk = b_kcontig != 0;
   if (p.splitk == 1) {

@@ -192,6 +192,22 @@ def test_gemm_f32_bias_and_split_k(M, N, K):
     assert (C - ref).abs().max().item() <= 2e-6 * K ** 0.5 * ref.abs().max().item() + 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(3072, 40, 102400), (384, 48, 8192), (256, 17, 4096 + 32 * 5)])
+def test_gemm_f32_narrow_n(M, N, K):
+    """N <= 48 exact NT GEMMs (layer 0's dW_ih = dG^T x at c2: M = 4H, N = 40, K = T B) on the
+    narrow kernel (128 x 48 tiles of v_mfma_f32_16x16x4_f32, split-K slabs): against fp64, with a
+    bias (the slab reduce's epilogue) on the ragged shape."""
+    from pytorch_speaker_verification_amd.ops import gemm_f32
+    g = torch.Generator().manual_seed(M + N + K)
+    A, B = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
+    bias = torch.randn(N, generator=g) if N == 17 else None
+    ref = A.double() @ B.double().T + (bias.double() if bias is not None else 0.0)
+    C = gemm_f32(A.to(DEV), B.to(DEV), True, True, bias=bias.to(DEV) if bias is not None else None).cpu().double()
+    err = (C - ref).abs().max().item() / ref.abs().max().item()
+    print(f"\nMEASURED gemm_f32_narrow.{M}x{N}x{K}.rel_vs_fp64 {err:.2e}")
+    assert err <= 1e-5
+
+
 @pytest.mark.parametrize("M,N,K", [(9216, 2048, 96), (16640, 1024, 32), (10240, 3072, 768)])
 def test_gemm_f32_persistent_tiles_two_biases(M, N, K):
     """More 256 x 256 tiles than CUs: the persistent form (gemm_f32_256p_kernel: next tile's first
