@@ -389,6 +389,16 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256sk_kernel(const float* __r
 // k-tile (into the stage that k-tile leaves idle), so the next tile starts on landed data and its
 // first k-tile runs while this tile's stores drain.  Same k-loop and summation order as
 // gemm_f32_256_kernel: bit-identical results.
+// SV_GF_EARLY (A/B only, measured no faster: DESIGN §4): the next tile's k-tile 1 is DMA'd too,
+// into the stage the last k-tile frees, before this tile's C stores, so k-tile 0's closing wait
+// counts the stores (vmcnt(NST)) instead of draining them: the chip-wide store burst (256 KB per
+// CU, the CUs in lock step) drains under two k-tiles of MFMAs instead of one.
+#ifndef SV_GF_EARLY
+#define SV_GF_EARLY 0
+#endif
+#if SV_GF_EARLY && defined(SV_GF_NOSTORE)
+#error "SV_GF_NOSTORE builds count no stores: build them with -DSV_GF_EARLY=0"
+#endif
 template <int BN, int MF>
 __global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __restrict__ A, long lda,
                                                               const float* __restrict__ B, long ldb,
@@ -450,6 +460,10 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __re
         }
   };
   f32x4 a0[TM], b0[TN], a1[TM], b1[TN];
+  // store instructions per wave between the early k-tile-1 DMA and k-tile 0's closing wait
+  constexpr int NST = TM * TN * (NR / 4);
+  static_assert(NST <= 63, "vmcnt holds 6 bits");
+  bool pre1 = false;  // this tile's k-tile 1 went out before the previous tile's stores
   while (true) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -465,8 +479,10 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __re
       const char* As = stage(kt);
       const char* Bs = As + OPA;
       if (kt + 1 < nk) {
-        sa.issue(stage(kt + 1), kt + 1, w);
-        sb.issue(stage(kt + 1) + OPA, kt + 1, w);
+        if (!(SV_GF_EARLY && kt == 0 && pre1)) {
+          sa.issue(stage(kt + 1), kt + 1, w);
+          sb.issue(stage(kt + 1) + OPA, kt + 1, w);
+        }
       } else if (more) {
         // the next tile's k-tile 0, into the stage this last k-tile leaves idle (stage pointers
         // formed here: held across the loop they would take registers)
@@ -485,12 +501,32 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __re
         if (g + 2 < NG) rd(As, Bs, g + 2, a0, b0);
         mm(a1, b1);
       }
-      // the next k-tile landed (this wave's DMA) and every wave is done with this one
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      // the next k-tile landed (this wave's DMA) and every wave is done with this one; after an
+      // early k-tile 1 the previous tile's NST stores, younger than it, may stay in flight
+      // (a raw barrier there: __syncthreads' release fence would drain the stores)
+      if (SV_GF_EARLY && kt == 0 && pre1) {
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
     }
     GfBias<BN, MF> bias;
     bias.load(bias0, bias1, tn, wc, fh);
+    if (SV_GF_EARLY) {
+      // the bias loads waited for in a form the compiler sees (the builtin, vmcnt(0) alone), so
+      // it places no wait of its own behind the DMA below; then the next tile's k-tile 1 into the
+      // stage the last k-tile freed (after its barrier) -- after the last tile a harmless re-fetch
+      // of this tile's, drained at the end (the host launches this kernel with nk >= 2)
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      GfStage<GF_BM> na;
+      GfStage<BN> nb;
+      na.init(A, lda, (more ? tmn : tm) * GF_BM, 0, tid);
+      nb.init(B, ldb, (more ? tnn : tn) * BN, 0, tid);
+      na.issue(stage(nk + 1), 1, w);
+      nb.issue(stage(nk + 1) + OPA, 1, w);
+      pre1 = true;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const long row = (long)tm * GF_BM + wr * 128 + MF * i + fr;
@@ -515,4 +551,5 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __re
     sb.init(B, ldb, tn * BN, 0, tid);
     base = (base + nk) & 1;
   }
+  if (SV_GF_EARLY) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last re-fetch into LDS
 }

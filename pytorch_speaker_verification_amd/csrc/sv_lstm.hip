@@ -701,7 +701,8 @@ int gemm_f32_256(const float* A, long lda, const float* B, long ldb, float* C, l
   const int tiles = (M / GF_BM) * (N / p.bn);
   if (p.splitk == 1) {
     const int cus = sv_stream_cus(stream);
-    if (SV_GF_PERS && p.bn == 256 && beta == 0.f && cus > 0 && tiles > cus && K / GF_BK <= 32) {
+    if (SV_GF_PERS && p.bn == 256 && beta == 0.f && cus > 0 && tiles > cus && K / GF_BK <= 32 &&
+        K / GF_BK >= 2) {
       // more tiles than CUs, short K (K1; dx's 96 k-tiles measured slower persistent, 3.80 vs
       // 3.73 ms): the persistent form (each tile's k-tile 0 fetched during the previous tile)
       hipLaunchKernelGGL((gemm_f32_256p_kernel<256, SV_F32_MF>), dim3(cus), dim3(512),
