@@ -794,8 +794,12 @@ extern "C" int sv_gemm_bf16_bf(int M, int N, int K, const bf16_t* A, long lda, c
 
 // dx = dG . W_ih with dG read from the persistent backward's fragment-order hand-off buffer
 // (no row-major dG copy): M = T * B rows (t, b), K = 4H; needs B % 32, M % 256, N % 256, H % 64
+#ifndef SV_BF16_AFRAG  // 0: the recurrence writes row-major dG for a row-major dx GEMM (A/B builds)
+#define SV_BF16_AFRAG 1
+#endif
 bool gemm_afrag_ok(int T, int B, int N, int H) {
-  return gemm256_ok(T * B, N, 4 * H) && B % 32 == 0 && H % G256_BK == 0;
+  return SV_BF16_AFRAG && gemm256_ok(T * B, N, 4 * H) && B % 32 == 0 && H % G256_BK == 0 &&
+         4 * H / G256_BK < 4096 && (unsigned long long)T * B * B < (1ull << 32);  // g256_af_koff / _rowoff exact
 }
 // (the split-K plan of sv_gemm_bf16 for the same shape).  More tiles than one round of CUs (the c3
 // dx: 1200 tiles): the persistent + stream-K kernel when `skws` (g8_sk_bytes) is given -- its
@@ -806,7 +810,7 @@ int gemm_bf16_afrag(int T, int B, int H, int N, const bf16_t* dgf, int bm, const
   const int M = T * B, K = 4 * H;
   const int tiles = (M / G256_BM) * (N / G256_BM);
   const long fs = (long)((B + bm - 1) / bm) * bm * 4 * H;
-  const G256AFrag af{dgf, fs, B, bm, H};
+  const G256AFrag af = g256_afrag(dgf, fs, B, bm, H);
   const BPlan p = plan_bf16(M, N, K);
 #if SV_G8_SK
   const int G = std::min(sv_stream_cus(stream), G8_SK_GRID), nk = K / G256_BK;

@@ -63,7 +63,36 @@ struct G256AFrag {
   const bf16_t* base;  // dgf
   long fs;             // slot size (elements)
   int bsl, bm, kg;     // batch rows per slot, row-block size of the layout, gate K (= H)
+  // k-tile kk (64 k) of A lies in gate g = kk / ktg at k-tile s = kk - g ktg of that gate; g is
+  // (kk kdiv) >> 20 with kdiv = ceil(2^20 / ktg), exact for kk < 4096 (the host checks): a runtime
+  // division per fill was ~30 instructions inside the 8-phase loop's phases (dx 17 % slower than on
+  // a row-major A)
+  int ktg;
+  unsigned kdiv;
+  long gstride;  // elements per gate of one row block's layout: (bm / 32) (kg / 16) 512
+  // the row -> (slot, row block) split without division: x / d = umulhi(x, ceil(2^32 / d)),
+  // exact for x d < 2^32 (the host checks T B x B < 2^32)
+  unsigned bsl_div, bm_div;
+  int kr, frag;  // bm / 32 row groups per row block; elements per (row group, gate): kg / 16 x 512
 };
+__host__ inline unsigned g256_magic(unsigned d) { return (unsigned)((((unsigned long long)1 << 32) + d - 1) / d); }
+__host__ inline G256AFrag g256_afrag(const bf16_t* base, long fs, int bsl, int bm, int kg) {
+  const int ktg = kg / 64;
+  return G256AFrag{base, fs, bsl, bm, kg, ktg, (unsigned)(((1u << 20) + ktg - 1) / ktg),
+                   (long)(bm / 32) * (kg / 16 * 512), g256_magic((unsigned)bsl), g256_magic((unsigned)bm),
+                   bm / 32, kg / 16 * 512};
+}
+// element offset of row `row` (= t bsl + b) of the fragment-order A at gate 0, k-step 0
+__device__ __forceinline__ long g256_af_rowoff(const G256AFrag& af, int row) {
+  const unsigned t = __umulhi((unsigned)row, af.bsl_div), b = (unsigned)row - t * (unsigned)af.bsl;
+  const unsigned rb = __umulhi(b, af.bm_div), q = (b >> 5) - rb * (unsigned)af.kr;
+  return (long)t * af.fs + (long)(rb * 4u * (unsigned)af.kr + q) * af.frag;
+}
+// element offset of k-tile kk (64 k) of the fragment-order A, relative to a row group's gate 0
+__device__ __forceinline__ long g256_af_koff(const G256AFrag& af, int kk) {
+  const int g = (int)(((unsigned)kk * af.kdiv) >> 20), s = kk - g * af.ktg;
+  return (long)g * af.gstride + (long)s * 2048;
+}
 
 // C tile store of a wave's 4 x 2 accumulators (bias / beta for G256_STORE, slab per k-split for
 // G256_SLAB)
@@ -129,18 +158,15 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16_t* __r
   // k-step c % 4) of the tile
   long af_row[4];  // element offset of this lane's 16 B in row group c / 4 at gate 0, k-step 0
   if constexpr (AF) {
-    const int KR = af.bm / 32, frag = af.kg / 16 * 512;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int c = 4 * w + i, row = tm * G256_BM + 32 * (c >> 2);
-      const int t = row / af.bsl, b = row % af.bsl;
-      af_row[i] = (long)t * af.fs + (long)(((b / af.bm) * 4) * KR + (b / 32) % KR) * frag + (c & 3) * 512 + lane * 8;
+      af_row[i] = g256_af_rowoff(af, row) + (c & 3) * 512 + lane * 8;
     }
   }
   auto issue_a = [&](char* lds, int kt) {
     if constexpr (AF) {
-      const int k0 = kbeg + kt * G256_BK, g = k0 / af.kg, s0 = (k0 % af.kg) / 16;
-      const long goff = (long)g * (af.bm / 32) * (af.kg / 16 * 512) + (long)s0 * 512;
+      const long goff = g256_af_koff(af, kbeg / G256_BK + kt);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         __builtin_amdgcn_global_load_lds((glb_vptr_t)(af.base + af_row[i] + goff),
@@ -353,20 +379,17 @@ __device__ __forceinline__ void g8_tile(const bf16_t* __restrict__ A, long lda, 
   // k-step w % 4), so a chunk is the 64 rows 64 i .. 64 i + 63 as for the row-major operand
   long af_row[4];
   if constexpr (AF) {
-    const int KR = af.bm / 32, frag = af.kg / 16 * 512;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rg = 2 * i + (w >> 2), row = tm * G256_BM + 32 * rg;
-      const int t = row / af.bsl, b = row % af.bsl;
-      af_row[i] = (long)t * af.fs + (long)(((b / af.bm) * 4) * KR + (b / 32) % KR) * frag + (w & 3) * 512 + lane * 8;
+      af_row[i] = g256_af_rowoff(af, row) + (w & 3) * 512 + lane * 8;
     }
   }
   auto stage = [&](int kt) { return smem + (kt & 1) * 2 * OPB; };
   auto fill_a = [&](int kt, int i) {
     char* lds = stage(kt);
     if constexpr (AF) {
-      const int k0 = kbeg + kt * G256_BK, g = k0 / af.kg, s0 = (k0 % af.kg) / 16;
-      const long goff = (long)g * (af.bm / 32) * (af.kg / 16 * 512) + (long)s0 * 512;
+      const long goff = g256_af_koff(af, kbeg / G256_BK + kt);
       __builtin_amdgcn_global_load_lds((glb_vptr_t)(af.base + af_row[i] + goff),
                                        (lds_vptr_t)(lds + ((2 * i + (w >> 2)) * 4 + (w & 3)) * 1024), 16, 0, 0);
     } else {
@@ -833,12 +856,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qsk_kernel(const bf16_t* __
   long af_row[4];
   auto init_item = [&]() {
     if constexpr (AF) {
-      const int KR = af.bm / 32, frag = af.kg / 16 * 512;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int rg = 2 * i + (w >> 2), row = tm * G256_BM + 32 * rg;
-        const int t = row / af.bsl, b = row % af.bsl;
-        af_row[i] = (long)t * af.fs + (long)(((b / af.bm) * 4) * KR + (b / 32) % KR) * frag + (w & 3) * 512 + lane * 8;
+        af_row[i] = g256_af_rowoff(af, row) + (w & 3) * 512 + lane * 8;
       }
     } else {
       sa.init(A, lda, tm * G256_BM, ka * G256_BK, tid);
@@ -864,8 +885,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qsk_kernel(const bf16_t* __
   auto fill_a = [&](int kt, int i) {
     char* lds = stage(kt);
     if constexpr (AF) {
-      const int k0 = (ka + kt) * G256_BK, g = k0 / af.kg, s0 = (k0 % af.kg) / 16;
-      const long goff = (long)g * (af.bm / 32) * (af.kg / 16 * 512) + (long)s0 * 512;
+      const long goff = g256_af_koff(af, ka + kt);
       __builtin_amdgcn_global_load_lds((glb_vptr_t)(af.base + af_row[i] + goff),
                                        (lds_vptr_t)(lds + ((2 * i + (w >> 2)) * 4 + (w & 3)) * 1024), 16, 0, 0);
     } else {

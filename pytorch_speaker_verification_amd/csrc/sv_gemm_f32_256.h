@@ -106,7 +106,14 @@ struct GfAFrag {
   const float* base;  // dgf
   long fs;            // slot size (floats)
   int bsl, kh;        // batch rows per slot (a multiple of 32), gate width H (k per gate)
+  // x / d as umulhi(x, ceil(2^32 / d)) (exact for x d < 2^32: the host checks T B x B and 4H x H):
+  // a runtime division per k-tile sat in the k-loop (sv_gemm256.h's G256AFrag)
+  unsigned bsl_div, kh_div;
 };
+__host__ inline GfAFrag gf_afrag(const float* base, long fs, int bsl, int kh) {
+  auto magic = [](unsigned d) { return (unsigned)((((unsigned long long)1 << 32) + d - 1) / d); };
+  return GfAFrag{base, fs, bsl, kh, magic((unsigned)bsl), magic((unsigned)kh)};
+}
 
 // the k-loop of one tile (rows tm GF_BM, columns tn BN, k-tiles [kbeg / GF_BK, + nk)) into acc
 // (zeroed here); shared by the one-shot and stream-K kernels.  Ends with every wave past its last
@@ -130,16 +137,18 @@ __device__ __forceinline__ void gf_mainloop(const float* __restrict__ A, long ld
   // fragment-order A: wave w copies row group w's 4 k-groups of each k-tile (KB c = 4 w + i)
   long af_row = 0;
   if constexpr (AF) {
-    const int m0 = tm * GF_BM + 32 * w, t = m0 / af.bsl, b = m0 % af.bsl;
+    const int m0 = tm * GF_BM + 32 * w, t = (int)__umulhi((unsigned)m0, af.bsl_div), b = m0 - t * af.bsl;
     af_row = (long)t * af.fs + (long)((b / 64) * 8 + ((b / 32) & 1)) * (af.kh / 8 * 256) + lane * 4;
   }
   auto issue_a = [&](char* lds, int kt) {
     if constexpr (AF) {
+      // the k-tile's 4 k-groups lie in one gate q (H % 32 == 0: the host checks)
+      const int k0 = kbeg + kt * GF_BK, q = (int)__umulhi((unsigned)k0, af.kh_div), kg0 = (k0 - q * af.kh) / 8;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int k = kbeg + kt * GF_BK + 8 * i, q = k / af.kh, kg = (k - q * af.kh) / 8;
-        __builtin_amdgcn_global_load_lds((gf_glb_ptr_t)(af.base + af_row + (long)q * 2 * (af.kh / 8 * 256) + kg * 256),
-                                         (gf_lds_ptr_t)(lds + (4 * w + i) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(
+            (gf_glb_ptr_t)(af.base + af_row + (long)q * 2 * (af.kh / 8 * 256) + (kg0 + i) * 256),
+            (gf_lds_ptr_t)(lds + (4 * w + i) * 1024), 16, 0, 0);
       }
     } else {
       sa.issue(lds, kt, w);

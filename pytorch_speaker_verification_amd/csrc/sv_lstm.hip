@@ -737,6 +737,7 @@ int gemm_f32_256(const float* A, long lda, const float* B, long ldb, float* C, l
 // whole 256-row tiles, whole 32-row groups per slot, one k-split; else -1 (use the row-major dG).
 int dx_afrag_bn(int T, int B, int H, int Fl) {
   if (gemm_x() != 0 || SV_F32_MF != 32 || B % 32 || H % 32 || ((long)T * B) % GF_BM) return -1;
+  if ((unsigned long long)T * B * B >= (1ull << 32) || 4ull * H * H >= (1ull << 32)) return -1;  // gf_afrag's magic
   const int bn = gf256_bn(Fl);
   if (Fl % bn || plan_gf256(T * B, Fl, 4 * H).splitk != 1) return -1;
   return bn;
@@ -752,7 +753,7 @@ size_t gf_sk_bytes() { return 2 * GF_SK_GRID * GF_SK_SLOT + GF_SK_GRID * sizeof(
 int gemm_f32_dx_afrag(int bn, const float* dgf, int T, int B, int H, const float* wihT, int Fl, float* dx,
                       hipStream_t s, void* skws = nullptr) {
   const long nrb = (B + 63) / 64, fs = nrb * 8 * (H / 8) * 256;
-  const GfAFrag af{dgf, fs, B, H};
+  const GfAFrag af = gf_afrag(dgf, fs, B, H);
   const int M = T * B, K = 4 * H, tiles = (M / GF_BM) * (Fl / bn);
   const size_t lds = 2 * (size_t)(GF_BM + bn) * GF_BK * 4;
   const int G = std::min(sv_stream_cus(s), GF_SK_GRID), nk = K / GF_BK;
