@@ -865,14 +865,20 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
       // off the chain: the bias partials (gate column tid: this half's rows in order, rows past B
       // excluded), row-major dG and dG^T of the half-step
       if (dbp && tid < 4 * PF_U) {
-        const int nv = min(PH_BM, B - b0);
+        // rows in order either way; the partial row block's runtime bound in its own branch (32
+        // per-row predicates of both halves, hoisted out of the step loop, were 128 SGPRs spilled
+        // to VGPR lanes and read back every step)
+        const int nv = B - b0;
         float s = 0.f;
+        if (nv >= PH_BM) {
 #pragma unroll
-        for (int e4 = 0; e4 < PH_BM / 4; ++e4) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(gts + tid * LDT + 4 * e4);
+          for (int e4 = 0; e4 < PH_BM / 4; ++e4) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(gts + tid * LDT + 4 * e4);
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (4 * e4 + e < nv) s += v[e];
+            for (int e = 0; e < 4; ++e) s += v[e];
+          }
+        } else {
+          for (int e = 0; e < nv; ++e) s += gts[tid * LDT + e];
         }
         dbs += s;
       }
