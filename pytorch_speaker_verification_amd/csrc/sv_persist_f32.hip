@@ -863,12 +863,16 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
       }
       PB_STAMP(4);  // 4: hand-off stores + drain + arrival
       // off the chain: the bias partials (gate column tid: this half's rows in order, rows past B
-      // excluded), row-major dG and dG^T of the half-step
+      // excluded), row-major dG and dG^T of the half-step.  The row bounds through an opaque copy
+      // made here, so their predicates are formed here each half-step: hoisted out of the step loop
+      // they were held across the k-loops in SGPRs and spilled to VGPR lanes
+      int Bq = B, Bpq = Bp;
+      asm volatile("" : "+s"(Bq), "+s"(Bpq));
       if (dbp && tid < 4 * PF_U) {
         // rows in order either way; the partial row block's runtime bound in its own branch (32
         // per-row predicates of both halves, hoisted out of the step loop, were 128 SGPRs spilled
         // to VGPR lanes and read back every step)
-        const int nv = B - b0;
+        const int nv = Bq - b0;
         float s = 0.f;
         if (nv >= PH_BM) {
 #pragma unroll
@@ -883,7 +887,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         dbs += s;
       }
       const long gb = b0 + erow;
-      if (dg && gb < B) {  // (dg == nullptr: the dx GEMM reads the fragment-order hand-off instead)
+      if (dg && gb < Bq) {  // (dg == nullptr: the dx GEMM reads the fragment-order hand-off instead)
         float* dp = dg + (long)t * BG + gb * G + j0 + 4 * quad;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -899,11 +903,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) {  // 128 gate-unit rows x 8 pieces of 4 batch columns
         const int p = tid + 256 * i, gu = p >> 3, c = p & 7, gbc = b0 + 4 * c;
-        if (gbc < Bp) {
+        if (gbc < Bpq) {
           f32x4 v = *reinterpret_cast<const f32x4*>(gts + gu * LDT + 4 * c);
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            if (gbc + e >= B) v[e] = 0.f;
+            if (gbc + e >= Bq) v[e] = 0.f;
           const long eo = ((long)(gu >> 5) * H + j0 + (gu & 31)) * lddgT + (long)t * Bp + gbc;
 #if SV_PF32_DGT_SC1
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rdt, (unsigned)(eo * 4), 0, 16 /* sc1 */);
