@@ -59,55 +59,57 @@ constexpr int W3_DMA = 12;  // DMA instructions per wave per tile (8 A + 4 B)
 
 // stage a 32-row tile of slot `ts` of `ra` (a [T+1][B][H] bf16 buffer, H = 768; the descriptor is
 // built once, outside the time loop, so it stays scalar): wave w stages rows 8 w .. 8 w + 7; rows
-// past B read zeros
+// past B read zeros.  The wave index goes through an opaque SGPR copy: the 24 per-instruction
+// addresses are not hoisted out of the time loop (held live across it they pushed weight fragments
+// into scratch) yet stay scalar -- a row's base is SALU arithmetic passed as soffset (region A) or
+// one select per lane (region B) -- where an opaque VGPR zero made every address a VALU chain with
+// a quarter-rate v_mul_lo_u32 and a v_readfirstlane for M0
+struct W3Dma {
+  __amdgpu_buffer_rsrc_t ra;
+  unsigned slot, vl, xs, h2;
+  int B, H, b0, g;
+  char* tile;
+  __device__ __forceinline__ W3Dma(__amdgpu_buffer_rsrc_t ra_, int ts, int B_, int H_, int b0_, char* tile_, int g_,
+                                   int lane)
+      : ra(ra_), B(B_), H(H_), b0(b0_), tile(tile_) {
+    int gz = __builtin_amdgcn_readfirstlane(g_);  // (wave-uniform)
+    asm volatile("" : "+s"(gz));
+    g = gz;
+    slot = (unsigned)ts * (unsigned)B * (unsigned)H * 2u;
+    vl = 16u * (unsigned)lane;
+    const unsigned hh = (unsigned)lane >> 5;
+    xs = ((unsigned)lane & 31u) ^ hh;  // (sl ^ ((2 p + hh) & 15)) = xs ^ (2 p & 14)
+    h2 = hh;
+  }
+  __device__ __forceinline__ unsigned row_base(int row) const {
+    return b0 + row < B ? slot + (unsigned)(b0 + row) * (unsigned)H * 2u : 0xFFFFE000u;
+  }
+  __device__ __forceinline__ void piece(int i) const {
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    if (i < 8) {  // region A: row g 8 + i, one 1-KB row per instruction
+      const int row = g * 8 + i;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + row * W3_RA), 16, vl, row_base(row), 0,
+                                               16 /* sc1 */);
+    } else {  // region B: rows 2 p, 2 p + 1 (lane halves), 512 B each, chunk c at c ^ (row & 15)
+      const int p = g * 4 + (i - 8);
+      const unsigned r0 = row_base(2 * p), r1 = row_base(2 * p + 1);
+      const unsigned c = 64u + (xs ^ (unsigned)((2 * p) & 14));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + 32 * W3_RA + p * 1024), 16,
+                                               (h2 ? r1 : r0) + 16u * c, 0, 0, 16 /* sc1 */);
+    }
+  }
+};
 __device__ __forceinline__ void w3_dma(__amdgpu_buffer_rsrc_t ra, int ts, int B, int H, int b0, char* tile, int g,
                                        int lane) {
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  // an opaque zero keeps the 24 per-instruction addresses from being hoisted out of the time loop
-  // (held live across it they pushed weight fragments into scratch)
-  int z = 0;
-  asm volatile("" : "+v"(z));
-  g += z;
-  const unsigned slot = (unsigned)ts * (unsigned)B * (unsigned)H * 2u;
-  auto row_base = [&](int row) {
-    return b0 + row < B ? slot + (unsigned)(b0 + row) * (unsigned)H * 2u : 0xFFFFE000u;
-  };
+  const W3Dma d(ra, ts, B, H, b0, tile, g, lane);
 #pragma unroll
-  for (int j = 0; j < 32 / 4; ++j) {  // region A: one row per instruction
-    const int row = g * (32 / 4) + j;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + row * W3_RA), 16, row_base(row) + 16u * lane, 0,
-                                             0, 16 /* sc1 */);
-  }
-#pragma unroll
-  for (int j = 0; j < 32 / 8; ++j) {  // region B: rows 2p, 2p + 1 per instruction, swizzled
-    const int p = g * (32 / 8) + j, row = 2 * p + (lane >> 5), sl = lane & 31;
-    const unsigned c = 64u + (unsigned)(sl ^ (row & 15));
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + 32 * W3_RA + p * 1024), 16,
-                                             row_base(row) + 16u * c, 0, 0, 16 /* sc1 */);
-  }
+  for (int i = 0; i < W3_DMA; ++i) d.piece(i);
 }
 
 // piece i (0 .. W3_DMA - 1) of w3_dma alone (the same addresses), for issue spread over a k-loop
 __device__ __forceinline__ void w3_dma_piece(__amdgpu_buffer_rsrc_t ra, int ts, int B, int H, int b0, char* tile, int g,
                                              int lane, int i) {
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  int z = 0;  // (the opaque zero of w3_dma: no address hoisted out of the time loop)
-  asm volatile("" : "+v"(z));
-  g += z;
-  const unsigned slot = (unsigned)ts * (unsigned)B * (unsigned)H * 2u;
-  auto row_base = [&](int row) {
-    return b0 + row < B ? slot + (unsigned)(b0 + row) * (unsigned)H * 2u : 0xFFFFE000u;
-  };
-  if (i < 8) {
-    const int row = g * 8 + i;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + row * W3_RA), 16, row_base(row) + 16u * lane, 0,
-                                             0, 16 /* sc1 */);
-  } else {
-    const int p = g * 4 + (i - 8), row = 2 * p + (lane >> 5), sl = lane & 31;
-    const unsigned c = 64u + (unsigned)(sl ^ (row & 15));
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(tile + 32 * W3_RA + p * 1024), 16,
-                                             row_base(row) + 16u * c, 0, 0, 16 /* sc1 */);
-  }
+  W3Dma(ra, ts, B, H, b0, tile, g, lane).piece(i);
 }
 
 // byte offset of A fragment s (k-step, 16 bf16) of lane (r, hh) in a w3_dma tile image
