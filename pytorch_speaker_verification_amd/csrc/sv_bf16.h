@@ -331,6 +331,28 @@ __device__ __forceinline__ f2_t lstm_cell_bwd2(f2_t dh, f2_t i, f2_t f, f2_t g, 
   d[3] = dh * tc * o * (1.f - o);
   return dc * f;
 }
+// the cell backward of 4 consecutive units as two packed pairs (lstm_cell_bwd2; per element the
+// operations of lstm_cell_bwd, so bit-identical to it): dh (recurrent + upstream), gates i f g o,
+// c_t, c_{t-1}, dcf in / out; dd[v][q] the gate pre-activation gradients of unit v
+template <class V4, class A4>
+__device__ __forceinline__ void lstm_cell_bwd_x4(const V4& dh, const A4& i, const A4& f, const A4& g, const A4& o,
+                                                 const V4& c, const V4& cp, float (&dcf)[4], float (&dd)[4][4]) {
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int v0 = 2 * p, v1 = 2 * p + 1;
+    f2_t d2[4];
+    const f2_t r = lstm_cell_bwd2(f2_t{dh[v0], dh[v1]}, f2_t{i[v0], i[v1]}, f2_t{f[v0], f[v1]}, f2_t{g[v0], g[v1]},
+                                  f2_t{o[v0], o[v1]}, f2_t{c[v0], c[v1]}, f2_t{cp[v0], cp[v1]},
+                                  f2_t{dcf[v0], dcf[v1]}, d2);
+    dcf[v0] = r.x;
+    dcf[v1] = r.y;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      dd[v0][q] = d2[q].x;
+      dd[v1][q] = d2[q].y;
+    }
+  }
+}
 
 // recurrent-step tile: 64 batch rows x 32 hidden units (x 4 gates = 128 gate columns)
 #define BF_BM 64

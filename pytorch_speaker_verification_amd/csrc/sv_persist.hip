@@ -716,15 +716,20 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
       const float a2[4] = {f2.x, f2.y, f2.z, f2.w};
       const float a3[4] = {f3.x, f3.y, f3.z, f3.w};
       unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
+      float dh4[4];  // (elementwise, the scalar order)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        float dh = rs0[v];
-        dh += rs1[v];
-        dh += rs2[v];
-        dh += rs3[v];
-        dh += ups[v];
-        float dd[4];
-        dcf[k][v] = lstm_cell_bwd(dh, a0[v], a1[v], a2[v], a3[v], cs[v], cps[v], dcf[k][v], dd);
+        dh4[v] = rs0[v];
+        dh4[v] += rs1[v];
+        dh4[v] += rs2[v];
+        dh4[v] += rs3[v];
+        dh4[v] += ups[v];
+      }
+      float ddv[4][4];
+      lstm_cell_bwd_x4(dh4, a0, a1, a2, a3, cs, cps, dcf[k], ddv);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float (&dd)[4] = ddv[v];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const bf16_t e = to_bf(dd[q]);

@@ -223,15 +223,16 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
           f[q] = unpack_bf4(*reinterpret_cast<const uint2*>(ewa + b * 512 + ((q + b) & 3) * 128 + (u4 >> 3) * 16 +
                                                             (u4 & 7) * 2));
         unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
+        float4 dh4 = r0;  // (elementwise, the scalar order)
+        dh4 += r1;
+        dh4 += r2;
+        dh4 += r3;
+        dh4 += upv;
+        float ddv[4][4];
+        lstm_cell_bwd_x4(dh4, f[0], f[1], f[2], f[3], cv[k], cpv, dcf[k], ddv);
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          float dh = r0[v];
-          dh += r1[v];
-          dh += r2[v];
-          dh += r3[v];
-          dh += upv[v];
-          float dd[4];
-          dcf[k][v] = lstm_cell_bwd(dh, f[0][v], f[1][v], f[2][v], f[3][v], cv[k][v], cpv[v], dcf[k][v], dd);
+          const float (&dd)[4] = ddv[v];
           const int u = u4 + v, sw = (2 * brow) ^ (((u >> 4) & 3) << 3);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -476,15 +477,16 @@ __global__ __launch_bounds__(256, 1) void lstm_persist16_bwd_bf16_kernel(
       for (int q = 0; q < 4; ++q)
         f[q] = unpack_bf4(*reinterpret_cast<const uint2*>(ewa + b * 512 + ((q + b) & 3) * 128 + (u4 >> 3) * 16 + (u4 & 7) * 2));
       unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
+      float4 dh4 = r0;  // (elementwise, the scalar order)
+      dh4 += r1;
+      dh4 += r2;
+      dh4 += r3;
+      dh4 += upv;
+      float ddv[4][4];
+      lstm_cell_bwd_x4(dh4, f[0], f[1], f[2], f[3], cv, cpv, dcf, ddv);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        float dh = r0[v];
-        dh += r1[v];
-        dh += r2[v];
-        dh += r3[v];
-        dh += upv[v];
-        float dd[4];
-        dcf[v] = lstm_cell_bwd(dh, f[0][v], f[1][v], f[2][v], f[3][v], cv[v], cpv[v], dcf[v], dd);
+        const float (&dd)[4] = ddv[v];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const unsigned e = to_bf(dd[q]);
@@ -1154,15 +1156,16 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
         f[q] = unpack_bf4(*reinterpret_cast<const uint2*>(ewa + b * 256 + ((q + b) & 3) * 64 + (u4 >> 3) * 16 +
                                                           (u4 & 7) * 2));
       unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
+      float4 dh4 = r0;  // (elementwise, the scalar order)
+      dh4 += r1;
+      dh4 += r2;
+      dh4 += r3;
+      dh4 += upv;
+      float ddv[4][4];
+      lstm_cell_bwd_x4(dh4, f[0], f[1], f[2], f[3], cv, cpv, dcf, ddv);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        float dh = r0[v];
-        dh += r1[v];
-        dh += r2[v];
-        dh += r3[v];
-        dh += upv[v];
-        float dd[4];
-        dcf[v] = lstm_cell_bwd(dh, f[0][v], f[1][v], f[2][v], f[3][v], cv[v], cpv[v], dcf[v], dd);
+        const float (&dd)[4] = ddv[v];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const bf16_t e = to_bf(dd[q]);
