@@ -439,6 +439,15 @@ constexpr int WB_L = 3;
 #ifndef SV_WAVE_DGT_SC1
 #define SV_WAVE_DGT_SC1 0
 #endif
+// Row stride (elements) of the library's own W_ih^T copies (bf16 [F][4H]) that the dx GEMMs read
+// as their B operand: 4H + SV_WIHT_PAD.  At 4H = 3072 a row is 6 KB, so the 256 rows of a k-tile
+// fill all fell on one L2 channel; 64 more elements (128 B) spread them: the c3 dx GEMM 569 -> 478 us
+// isolated (scripts/gemm_ld_ab.py).  Values only move: results are bit-identical.
+#ifndef SV_WIHT_PAD
+#define SV_WIHT_PAD 64
+#endif
+inline long bf16_wiht_ld(int H) { return 4L * H + SV_WIHT_PAD; }
+
 struct WaveBwdArgs {
   const bf16_t* whhT[WB_L];  // [H][4H] bf16 (W_hh^T)
   const bf16_t* wihT[WB_L];  // [H][4H] bf16 (W_ih^T; layers >= 1)
@@ -455,6 +464,7 @@ struct WaveBwdArgs {
   long lddgT;
   int T, Bp, B, H, nub, nrb, fault;
   int dgt_sc1;  // dG^T stores written through (sc1): the weight-gradient GEMM reads them in-launch
+  long ldwih;   // row stride of wihT (elements; bf16_wiht_ld)
 };
 int sv_wave_bwd_launch(const WaveBwdArgs& a, hipStream_t stream);
 int sv_wave_bwd_fits(int L, int B, int H, int cus);
@@ -462,4 +472,4 @@ size_t sv_wave_bwd_scratch(int L, int T, int B, int H);
 int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, const bf16_t* const* wihT,
                      const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
                      bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
-                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, int dgt_sc1 = 0);
+                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, int dgt_sc1 = 0, long ldwih = 0);

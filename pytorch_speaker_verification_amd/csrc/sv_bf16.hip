@@ -1123,7 +1123,7 @@ BBwdWs carve_bbwd(char* base, int T, int B, int F, int H) {
   w.dcf0 = (float*)take((size_t)B * H * 4);
   w.dcf1 = (float*)take((size_t)B * H * 4);
   w.whhT = (bf16_t*)take((size_t)4 * H * H * 2);
-  w.wihT = (bf16_t*)take((size_t)4 * H * F * 2);
+  w.wihT = (bf16_t*)take((size_t)bf16_wiht_ld(H) * F * 2);
   const int TBp = T * ((B + 7) & ~7);
   size_t g = sv_gemm_bf16_workspace(4 * H, H, TBp);
   g = std::max(g, sv_gemm_bf16_workspace(4 * H, F, TBp));
@@ -1157,7 +1157,7 @@ static int wbf_transposes(int L, int F, int H, const float* const* w_ih, const f
       src[n] = m == 0 ? w_hh[l] : w_ih[l];
       dst[n] = const_cast<bf16_t*>(m == 0 ? whhT[l] : wihT[l]);
       lds[n] = K;
-      ldd[n] = 4L * H;
+      ldd[n] = m == 0 ? 4L * H : bf16_wiht_ld(H);
       R[n] = 4 * H;
       C[n] = K;
       ++n;
@@ -1274,7 +1274,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     }
     rc = sv_wave_bwd_bf16(L, T, B, H, whhT_l, wihT_l, gates, c_tm, dh_last, dx, dgT, (char*)workspace + per * L,
                               sync, main, db_ih, db_hh, probe ? probe[0] : nullptr, probe ? probe[1] : nullptr,
-                              beside || SV_WAVE_DGT_SC1 ? 1 : 0);
+                              beside || SV_WAVE_DGT_SC1 ? 1 : 0, bf16_wiht_ld(H));
     if (rc) return rc;
     if (queued) {
       hipLaunchKernelGGL(gemm_bf16_8qw_kernel<0>, dim3(cus), dim3(512), G256_LDS, main, q);
@@ -1349,10 +1349,10 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       for (int k = 1; l == 0 && k < L; ++k)
         if ((e = hipEventRecord(ev[L * nch + k], main)) != hipSuccess) return (int)e;
       if (afr) {
-        if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H, sv_stream_cus(main)), ws.wihT, 4L * H, dx[l],
+        if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H, sv_stream_cus(main)), ws.wihT, bf16_wiht_ld(H), dx[l],
                                   Fl, ws.gws, main, (char*)workspace + per * L + bbwd_scratch(L, T, B, H))))
           return rc;
-      } else if (l > 0 && (rc = sv_gemm_bf16(T * B, Fl, 4 * H, dg[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr,
+      } else if (l > 0 && (rc = sv_gemm_bf16(T * B, Fl, 4 * H, dg[l], 4L * H, ws.wihT, bf16_wiht_ld(H), dx[l], Fl, nullptr,
                                               nullptr, 0.f, ws.gws, main))) {
         return rc;
       }
@@ -1373,7 +1373,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
     int rc = sv_transpose_cast_bf16(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, s);
     if (rc) return rc;
-    if (l > 0 && (rc = sv_transpose_cast_bf16(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, s))) return rc;
+    if (l > 0 && (rc = sv_transpose_cast_bf16(w_ih[l], Fl, 4 * H, Fl, ws.wihT, bf16_wiht_ld(H), s))) return rc;
     if (Bp != B && (e = sv_memset0(dgT[l], (size_t)4 * H * TBp * sizeof(bf16_t), s)) != hipSuccess)
       return (int)e;
     for (int c = nch - 1; c >= 0; --c) {
@@ -1389,7 +1389,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
         SV_LAUNCH_CHECK();
       }
       if (l > 0) {
-        rc = sv_gemm_bf16((t1 - t0) * B, Fl, 4 * H, dg[l] + t0 * BG, 4L * H, ws.wihT, 4L * H,
+        rc = sv_gemm_bf16((t1 - t0) * B, Fl, 4 * H, dg[l] + t0 * BG, 4L * H, ws.wihT, bf16_wiht_ld(H),
                           dx[l] + (long)t0 * B * Fl, Fl, nullptr, nullptr, 0.f, ws.gws, s);
         if (rc) return rc;
       }

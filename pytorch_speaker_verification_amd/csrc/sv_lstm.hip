@@ -750,7 +750,7 @@ size_t gf_sk_bytes() { return 2 * GF_SK_GRID * GF_SK_SLOT + GF_SK_GRID * sizeof(
 #ifndef SV_GF_SK
 #define SV_GF_SK 1  // the dx GEMM's stream-K form where its tiles leave the last round part-idle (0: A/B)
 #endif
-int gemm_f32_dx_afrag(int bn, const float* dgf, int T, int B, int H, const float* wihT, int Fl, float* dx,
+int gemm_f32_dx_afrag(int bn, const float* dgf, int T, int B, int H, const float* wihT, long ldw, int Fl, float* dx,
                       hipStream_t s, void* skws = nullptr) {
   const long nrb = (B + 63) / 64, fs = nrb * 8 * (H / 8) * 256;
   const GfAFrag af = gf_afrag(dgf, fs, B, H);
@@ -768,7 +768,7 @@ int gemm_f32_dx_afrag(int bn, const float* dgf, int T, int B, int H, const float
       sk.cnt = reinterpret_cast<unsigned*>(static_cast<char*>(skws) + 2 * GF_SK_GRID * GF_SK_SLOT);
       hipError_t e = (hipError_t)sv_zero_counters(sk.cnt, 1, 0, sk.rem, s);
       if (e != hipSuccess) return (int)e;
-      hipLaunchKernelGGL((gemm_f32_256sk_kernel<256, 1>), dim3(G), dim3(512), lds, s, nullptr, 0L, wihT, (long)K, dx,
+      hipLaunchKernelGGL((gemm_f32_256sk_kernel<256, 1>), dim3(G), dim3(512), lds, s, nullptr, 0L, wihT, ldw, dx,
                          (long)Fl, M, Fl, K, sk, af);
       SV_LAUNCH_CHECK();
       return SV_OK;
@@ -776,10 +776,10 @@ int gemm_f32_dx_afrag(int bn, const float* dgf, int T, int B, int H, const float
   }
   if (bn == 256)
     hipLaunchKernelGGL((gemm_f32_256_kernel<256, SV_F32_MF, GF_STORE, 1>), dim3(tiles, 1), dim3(512), lds, s, nullptr,
-                       0L, wihT, (long)K, dx, (long)Fl, 0L, M, Fl, K, K, nullptr, nullptr, 0.f, af);
+                       0L, wihT, ldw, dx, (long)Fl, 0L, M, Fl, K, K, nullptr, nullptr, 0.f, af);
   else
     hipLaunchKernelGGL((gemm_f32_256_kernel<128, SV_F32_MF, GF_STORE, 1>), dim3(tiles, 1), dim3(512), lds, s, nullptr,
-                       0L, wihT, (long)K, dx, (long)Fl, 0L, M, Fl, K, K, nullptr, nullptr, 0.f, af);
+                       0L, wihT, ldw, dx, (long)Fl, 0L, M, Fl, K, K, nullptr, nullptr, 0.f, af);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }
@@ -1001,6 +1001,14 @@ extern "C" int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, 
   return SV_OK;
 }
 
+// Row stride (floats) of the library's own W_ih^T copies (fp32 [F][4H]), the dx GEMMs' B operand:
+// 4H + SV_WIHT_PAD_F32.  A 12-KB row stride put the 256 rows of a k-tile fill on one L2 channel;
+// 64 more floats spread them (the c2 dx GEMM 3707 -> 3654 us isolated, scripts/gemm_ld_ab.py).
+#ifndef SV_WIHT_PAD_F32
+#define SV_WIHT_PAD_F32 64
+#endif
+static inline long f32_wiht_ld(int H) { return 4L * H + SV_WIHT_PAD_F32; }
+
 namespace {
 struct BwdWs {
   float *dcf0, *dcf1, *whhT, *wihT, *gws;
@@ -1018,7 +1026,7 @@ BwdWs carve_bwd(float* base, int T, int B, int F, int H) {
   w.dcf0 = take((size_t)B * H);
   w.dcf1 = take((size_t)B * H);
   w.whhT = take((size_t)4 * H * H);
-  w.wihT = take((size_t)4 * H * F);
+  w.wihT = take((size_t)f32_wiht_ld(H) * F);
   const int TBp = T * ((B + 3) & ~3);
   size_t g = sv_gemm_f32_workspace(4 * H, H, TBp);
   g = std::max(g, sv_gemm_f32_workspace(4 * H, F, TBp));
@@ -1072,9 +1080,9 @@ extern "C" int sv_lstm_layer_bwd(int T, int B, int F, int H, const float* xT, lo
   SV_LAUNCH_CHECK();
   // dx = dG W_ih: A = dG [TB, 4H], B = W_ih^T [F, 4H]
   if (dx_tm) {
-    rc = sv_transpose(w_ih, F, 4 * H, F, ws.wihT, 4L * H, stream);
+    rc = sv_transpose(w_ih, F, 4 * H, F, ws.wihT, f32_wiht_ld(H), stream);
     if (rc) return rc;
-    rc = gemm_f32(1, 1, TB, F, 4 * H, dgates, 4L * H, ws.wihT, 4L * H, dx_tm, F, nullptr, nullptr, 0.f, ws.gws,
+    rc = gemm_f32(1, 1, TB, F, 4 * H, dgates, 4L * H, ws.wihT, f32_wiht_ld(H), dx_tm, F, nullptr, nullptr, 0.f, ws.gws,
                      stream);
     if (rc) return rc;
   }
@@ -1236,7 +1244,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
       const BwdWs ws = carve_bwd((float*)((char*)workspace + per * l), T, B, std::max(F, H), H);
       int rc = sv_transpose(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, main);
       if (rc) return rc;
-      if (l > 0 && (rc = sv_transpose(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, main))) return rc;
+      if (l > 0 && (rc = sv_transpose(w_ih[l], Fl, 4 * H, Fl, ws.wihT, f32_wiht_ld(H), main))) return rc;
       const float* up = l == L - 1 ? dh_last : dx[l + 1];
       // the row-major dG only where a dx GEMM needs it and cannot read the fragment-order hand-off
       // (layer 0 computes no dx here)
@@ -1251,9 +1259,9 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
       // weight-gradient GEMMs
       for (int k = 1; l == 0 && k < L; ++k)
         if ((e = hipEventRecord(ev[L * nch + k], main)) != hipSuccess) return (int)e;
-      if (l > 0 && abn > 0 && (rc = gemm_f32_dx_afrag(abn, dgf, T, B, H, ws.wihT, Fl, dx[l], main, skws))) return rc;
+      if (l > 0 && abn > 0 && (rc = gemm_f32_dx_afrag(abn, dgf, T, B, H, ws.wihT, f32_wiht_ld(H), Fl, dx[l], main, skws))) return rc;
       if (l > 0 && abn < 0 &&
-          (rc = gemm_f32(1, 1, T * B, Fl, 4 * H, dgates[l], 4L * H, ws.wihT, 4L * H, dx[l], Fl, nullptr, nullptr, 0.f,
+          (rc = gemm_f32(1, 1, T * B, Fl, 4 * H, dgates[l], 4L * H, ws.wihT, f32_wiht_ld(H), dx[l], Fl, nullptr, nullptr, 0.f,
                          ws.gws, main)))
         return rc;
       if ((rc = gemm_f32(1, 1, 4 * H, H, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, nullptr, nullptr, 0.f, ws.gws,
@@ -1278,7 +1286,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
     if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
     int rc = sv_transpose(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, s);
     if (rc) return rc;
-    if (l > 0 && (rc = sv_transpose(w_ih[l], Fl, 4 * H, Fl, ws.wihT, 4L * H, s))) return rc;
+    if (l > 0 && (rc = sv_transpose(w_ih[l], Fl, 4 * H, Fl, ws.wihT, f32_wiht_ld(H), s))) return rc;
     if (Bp != B && (e = sv_memset0(dgT[l], (size_t)4 * H * TBp * sizeof(float), s)) != hipSuccess) return (int)e;
     for (int c = nch - 1; c >= 0; --c) {
       const int t0 = c * chunk, t1 = std::min(T, t0 + chunk);
@@ -1299,7 +1307,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
         if (probe && t == tp && (e = hipEventRecord(probe[2 * (l * nch + c) + 1], s)) != hipSuccess) return (int)e;
       }
       if (l > 0) {  // dh_up of layer l-1 for this chunk: dx = dG W_ih
-        rc = gemm_f32(1, 1, (t1 - t0) * B, Fl, 4 * H, dgates[l] + t0 * BG, 4L * H, ws.wihT, 4L * H,
+        rc = gemm_f32(1, 1, (t1 - t0) * B, Fl, 4 * H, dgates[l] + t0 * BG, 4L * H, ws.wihT, f32_wiht_ld(H),
                       dx[l] + (long)t0 * B * Fl, Fl, nullptr, nullptr, 0.f, ws.gws, s);
         if (rc) return rc;
       }

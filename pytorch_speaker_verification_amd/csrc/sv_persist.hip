@@ -1201,13 +1201,14 @@ size_t sv_wave_bwd_scratch(int L, int T, int B, int H) {
 int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, const bf16_t* const* wihT,
                      const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
                      bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
-                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, int dgt_sc1) {
+                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, int dgt_sc1, long ldwih) {
   if (!sv_wave_bwd_fits(L, B, H, sv_stream_cus(stream))) return SV_ESHAPE;
   if (!scratch || ((uintptr_t)scratch & 15) || !sync || !dh_last || !whhT || !wihT || !acts || !c_tm || !dx || !dgT)
     return SV_EARG;
   WaveBwdArgs a{};
   a.nub = H / 32;
   a.nrb = (B + 31) / 32;
+  a.ldwih = ldwih ? ldwih : 4L * H;
   char* p = static_cast<char*>(scratch);
   for (int l = 0; l < L; ++l) {
     if (!whhT[l] || !acts[l] || !c_tm[l] || !dgT[l] || (l > 0 && (!wihT[l] || !dx[l]))) return SV_EARG;

@@ -982,7 +982,7 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
   bf16x8_t wa[NS], wb[NR];
   {
     const bf16_t* ra = a.whhT[l] + (long)(j0 + r) * G + (long)g * H + 8 * hh;
-    const bf16_t* rbp = has_dx ? a.wihT[l] + (long)(j0 + r) * G + (long)g * H + 8 * hh : ra;
+    const bf16_t* rbp = has_dx ? a.wihT[l] + (long)(j0 + r) * a.ldwih + (long)g * H + 8 * hh : ra;
     const bool ok = j0 + r < H;
     const bf16x8_t z = {};
 #pragma unroll
