@@ -37,6 +37,9 @@
 #ifndef SV_PF32_FWD_AHEAD2  // forward k-loop: A / W fragments two k-groups ahead across chunks
 #define SV_PF32_FWD_AHEAD2 1
 #endif
+#ifndef SV_PF32_BDMA  // the forward's ring / x-projection DMA as buffer loads with scalar bases (0: A/B)
+#define SV_PF32_BDMA 1
+#endif
 #ifndef SV_PF32_GXAUX  // A/B diagnostic: cache-policy bits of the x-projection DMA
 #define SV_PF32_GXAUX 0
 #endif
@@ -220,6 +223,35 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
 #endif
   for (int t = 0; t < T; ++t) {
     PF_STAMP(-1);
+#if SV_PF32_BDMA
+    // the wave index through an opaque SGPR copy: the DMA address arithmetic stays inside the step
+    // (hoisted out of the time loop, the per-lane addresses would hold registers the weights need)
+    // and scalar where it is uniform -- the step's base in a buffer descriptor, a row group's LDS
+    // address (M0) and the chunk offset in SALU, 32-bit per-lane offsets -- where an opaque VGPR
+    // zero made every address a 64-bit VALU chain with a v_readfirstlane for M0
+    int gs = __builtin_amdgcn_readfirstlane(g);
+    asm volatile("" : "+s"(gs));
+    const __amdgpu_buffer_rsrc_t rh = sv_rsrc(h_tm + (long)t * B * H, (unsigned)((long)B * H * 4));
+    const __amdgpu_buffer_rsrc_t rg = sv_rsrc(gates + (long)t * BG, (unsigned)(BG * 4));
+    auto dma_chunk = [&](int ch, int slot) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int rowu = 16 * gs + 4 * j, rl = lane >> 4, row = rowu + rl;
+        const unsigned vo = (unsigned)((min(b0 + row, B - 1) * H + 4 * ((lane & 15) ^ (4 * j + rl))) * 4);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (pf_lds_t)(ring + slot * PF_CH + rowu * 256), 16, vo,
+                                                 (unsigned)(ch * PF_KC * 4), 0, 16 /* sc1 */);
+      }
+    };
+    auto dma_gx = [&]() {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int rowu = 2 * (8 * gs + j), row = rowu + (lane >> 5), s = lane & 31;
+        const unsigned vo = (unsigned)((min(b0 + row, B - 1) * (int)G + (s >> 3) * H + j0 + 4 * (s & 7)) * 4);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (pf_lds_t)(gxs + (8 * gs + j) * 256), 16, vo, 0, 0,
+                                                 SV_PF32_GXAUX);
+      }
+    };
+#else
     // an opaque zero: keeps the DMA address arithmetic inside the step (hoisted out of the time
     // loop, the per-lane addresses would hold registers the weights need)
     int z = 0;
@@ -246,6 +278,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
         __builtin_amdgcn_global_load_lds((pf_glb_t)src, (pf_lds_t)(gxs + (8 * g + j) * 256), 16, 0, SV_PF32_GXAUX);
       }
     };
+#endif
     f32x16 acc0, acc1;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
