@@ -715,6 +715,33 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
     float* ea = eset[set];
     float* ec = ea + PH_BM * 4 * PF_U;
     float* eu = ec + PH_BM * PF_U;
+#if SV_PF32_BDMA
+    // (the forward's dma_chunk form: buffer loads, scalar bases, 32-bit per-lane offsets)
+    int gs = __builtin_amdgcn_readfirstlane(g);
+    asm volatile("" : "+s"(gs));
+    const int b0 = rb * PF_BM + hf * PH_BM;
+    const __amdgpu_buffer_rsrc_t ra_ = sv_rsrc(acts + (long)tt * BG, (unsigned)(BG * 4));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = 2 * (4 * gs + j) + (lane >> 5), s = lane & 31;
+      const unsigned vo = (unsigned)((min(b0 + row, B - 1) * (int)G + (s >> 3) * H + j0 + 4 * (s & 7)) * 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_, (pf_lds_t)(ea + (4 * gs + j) * 256), 16, vo, 0, 0, 0);
+    }
+    const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
+    const int q = g * 64 + lane, row = 8 * gs + (lane >> 3), c = lane & 7;
+    const unsigned vo2 = (unsigned)((min(b0 + row, B - 1) * H + j0 + 4 * c) * 4);
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    if (tt > 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(sv_rsrc(c_tm + (long)(tt - 1) * BH, (unsigned)(BH * 4)),
+                                               (pf_lds_t)(ec + gs * 256), 16, vo2, 0, 0, 0);
+    else
+      *reinterpret_cast<f32x4*>(ec + 4 * q) = zero;
+    if (up)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(sv_rsrc(up, (unsigned)(BH * 4)), (pf_lds_t)(eu + gs * 256), 16, vo2, 0,
+                                               0, 0);
+    else
+      *reinterpret_cast<f32x4*>(eu + 4 * q) = zero;
+#else
     int z = 0;
     asm volatile("" : "+v"(z));
     const int gz = g + z, b0 = rb * PF_BM + hf * PH_BM;
@@ -737,6 +764,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
       __builtin_amdgcn_global_load_lds((pf_glb_t)(up + off), (pf_lds_t)(eu + g * 256), 16, 0, 0);
     else
       *reinterpret_cast<f32x4*>(eu + 4 * q) = zero;
+#endif
   };
   f32x4 cv[2], dcf[2];
 #pragma unroll
