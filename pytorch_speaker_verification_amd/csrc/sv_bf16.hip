@@ -699,10 +699,108 @@ int sv_gemm_bf16_dual(int M, int N1, int N2, int K, const bf16_t* A, long lda, c
   return SV_OK;
 }
 
+// ---- narrow bf16 NT GEMM (N <= 48): layer 0's dW_ih = dG^T x (M = 4H, N = F = 40, K = T B) ----
+// The 64 x 64 tiles padded N = 40 to 64 and streamed dG^T (629 MB at c3) at 4.6 TB/s (138 us).  The
+// fp32 narrow kernel's layout (sv_lstm.hip) in bf16: a workgroup is 128 rows x 48 columns over a K
+// chunk, v_mfma_f32_16x16x32_bf16 (B first: a lane's 4 accumulators are 4 consecutive C columns),
+// each wave 32 rows (2 x 3 blocks); LDS images [rows][64 k] (128 B) with 16-B chunk c of row r at
+// c ^ (r & 7), filled by LDS-DMA, two stages; split-K slabs reduced by slab_reduce_bf_kernel.
+constexpr int GNB_BM = 128, GNB_BN = 48, GNB_BK = 64;
+__global__ __launch_bounds__(256) void gemm_bf16_narrow_kernel(const bf16_t* __restrict__ A, long lda,
+                                                               const bf16_t* __restrict__ B, long ldb,
+                                                               float* __restrict__ slab, long slab_stride, int M,
+                                                               int N, int K, int kchunk) {
+  __shared__ __attribute__((aligned(16))) char lds[2][(GNB_BM + GNB_BN) * 128];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int m0 = blockIdx.x * GNB_BM, s = blockIdx.y;
+  const int kbeg = s * kchunk, nk = (min(K, kbeg + kchunk) - kbeg) / GNB_BK;
+  // DMA map: 16-B chunk q of the stage: A rows 0..127 (q < 1024), then B rows 0..47
+  auto fill = [&](int kt, int st) {
+    const int k0 = kbeg + kt * GNB_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = tid + 256 * i, row = q >> 3, c = (q & 7) ^ (row & 7);
+      __builtin_amdgcn_global_load_lds((glb_vptr_t)(A + (long)(m0 + row) * lda + k0 + 8 * c),
+                                       (lds_vptr_t)(&lds[st][0] + 16 * (w * 64 + 256 * i)), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i == 1 && w >= 2) break;  // 384 chunks of B: waves 0-1 issue a second one (wave-uniform)
+      const int q = tid + 256 * i, row = q >> 3, c = (q & 7) ^ (row & 7);
+      const int n = min(row, N - 1);  // padding columns read row N - 1 (their sums are not stored)
+      __builtin_amdgcn_global_load_lds((glb_vptr_t)(B + (long)n * ldb + k0 + 8 * c),
+                                       (lds_vptr_t)(&lds[st][GNB_BM * 128] + 16 * (w * 64 + 256 * i)), 16, 0, 0);
+    }
+  };
+  g8_f32x4 acc[2][3];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = g8_f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) fill(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage st landed for every wave; stage st ^ 1 free
+    if (kt + 1 < nk) fill(kt + 1, st ^ 1);
+    const char* As = &lds[st][0];
+    const char* Bs = &lds[st][GNB_BM * 128];
+#pragma unroll
+    for (int ks = 0; ks < GNB_BK / 32; ++ks) {
+      const int c = 4 * ks + lq;  // lane group lq: k 8 lq .. 8 lq + 7 of the 32-k step
+      bf16x8_t a[2], b[3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = 32 * w + 16 * i + lr;
+        a[i] = *reinterpret_cast<const bf16x8_t*>(As + row * 128 + 16 * (c ^ (row & 7)));
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int row = 16 * j + lr;
+        b[j] = *reinterpret_cast<const bf16x8_t*>(Bs + row * 128 + 16 * (c ^ (row & 7)));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = mfma16_bf16(b[j], a[i], acc[i][j]);
+    }
+  }
+  // lane holds C[16 i + lr][16 j + 4 lq .. + 3] of its wave's rows
+  float* Cz = slab + (long)s * slab_stride;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int col = 16 * j + 4 * lq;
+      if (col < N)
+        *reinterpret_cast<g8_f32x4*>(Cz + (long)(m0 + 32 * w + 16 * i + lr) * N + col) = acc[i][j];
+    }
+}
+#ifndef SV_GEMM_BF_NARROW  // 0: the N <= 48 bf16 GEMMs on the 64 x 64 tiles (A/B)
+#define SV_GEMM_BF_NARROW 1
+#endif
+// exact plan of the narrow kernel: N <= 48 in whole 4-column groups, whole 128-row tiles, 64-k steps,
+// K chunks of at least 1024 over up to 32 slabs (c3: 24 row tiles x 32 slabs = 768 workgroups)
+static bool narrow_bf_ok(int M, int N, int K, long lda, long ldb) {
+  return SV_GEMM_BF_NARROW && N <= GNB_BN && N % 4 == 0 && M % GNB_BM == 0 && K % GNB_BK == 0 && K >= 4096 &&
+         lda % 8 == 0 && ldb % 8 == 0;
+}
+static int narrow_bf_splitk(int K, int& kchunk) {
+  const int sk = std::max(1, std::min(32, K / 1024));
+  kchunk = ((K + sk - 1) / sk + GNB_BK - 1) / GNB_BK * GNB_BK;
+  return (K + kchunk - 1) / kchunk;
+}
+
 extern "C" size_t sv_gemm_bf16_workspace(int M, int N, int K) {
   const BPlan p = plan_bf16(M, N, K);
-  if (p.splitk <= 1) return 0;
-  const size_t slabs = (size_t)p.splitk * M * N * sizeof(float);
+  size_t nar = 0;
+  if (narrow_bf_ok(M, N, K, K, K)) {  // (the narrow kernel's slabs)
+    int kchunk;
+    nar = (size_t)narrow_bf_splitk(K, kchunk) * M * N * sizeof(float);
+  }
+  if (p.splitk <= 1) return nar;
+  const size_t slabs = std::max(nar, (size_t)p.splitk * M * N * sizeof(float));
   return SV_G8_SK_DW && p.bm == G256_BM ? std::max(slabs, g8_sk_bytes()) : slabs;  // (+ stream-K scratch)
 }
 
@@ -711,6 +809,19 @@ extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, cons
                             hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || !A || !B || !C) return SV_EARG;
   if (K % 8 || lda % 8 || ldb % 8 || (((uintptr_t)A | (uintptr_t)B) & 15)) return SV_EALIGN;
+  if (workspace && !((uintptr_t)workspace & 15) && narrow_bf_ok(M, N, K, lda, ldb)) {
+    int kchunk;
+    const int sk = narrow_bf_splitk(K, kchunk);
+    const long slab = (long)M * N;
+    hipLaunchKernelGGL(gemm_bf16_narrow_kernel, dim3(M / GNB_BM, sk), dim3(256), 0, stream, A, lda, B, ldb, workspace,
+                       slab, M, N, K, kchunk);
+    SV_LAUNCH_CHECK();
+    const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
+    hipLaunchKernelGGL(slab_reduce_bf_kernel, dim3(grid), dim3(256), 0, stream, workspace, sk, slab, C, ldc, M, N,
+                       beta, bias0, bias1);
+    SV_LAUNCH_CHECK();
+    return SV_OK;
+  }
   const BPlan p = plan_bf16(M, N, K);
   if (p.bm == G256_BM) {
     const int tiles = (M / G256_BM) * (N / G256_BM);

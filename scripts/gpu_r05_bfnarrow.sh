@@ -1,0 +1,18 @@
+#!/bin/bash
+# bf16 narrow NT GEMM (layer 0's dW_ih, N = 40) vs the 64 x 64 tiles (head = previous tree): GPU tests,
+# c3 / c4-rank / c5-rank stack A/B (3 interleaved rounds of scripts/persist_ab.py), one c3 kernel trace each
+cd "$GRAFT_REPO_ROOT"; export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp; O=gpurun_out/${TAG:-bfnarrow}; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread -m gpu tests/test_gpu_kernels.py tests/test_gpu_persist.py tests/test_gpu_precision.py tests/test_gpu_model.py > $O/pytest.log 2>&1 || { echo "pytest rc=$?"; grep -E "FAILED|Error|assert" $O/pytest.log | head; tail -5 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log; grep "MEASURED gemm_bf16_narrow" $O/pytest.log
+for r in 1 2 3; do for v in prod head; do
+  L=""; [ $v != prod ] && L="--lib scripts/ab/libsv_ge2e_$v.so"
+  for shp in "" "--B 80 --T 160" "--B 320 --T 180"; do
+    echo "== $v $shp" >> $O/ab.log
+    timeout -k 10 200 python -u scripts/persist_ab.py $L $shp --iters 5 >> $O/ab.log 2>&1 || { echo "$v $shp rc=$?"; tail -5 $O/ab.log; exit 1; }
+  done
+done; done
+for v in prod head; do
+  L=""; [ $v != prod ] && L="--lib scripts/ab/libsv_ge2e_$v.so"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c3_$v -o run -- python3 scripts/persist_ab.py $L --iters 3 > $O/c3_$v.log 2>&1 || { echo "$v trace rc=$?"; exit 1; }
+done
+echo done

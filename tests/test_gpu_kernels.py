@@ -208,6 +208,28 @@ def test_gemm_f32_narrow_n(M, N, K):
     assert err <= 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(3072, 40, 102400), (384, 48, 8192), (256, 16, 4096 + 64)])
+def test_gemm_bf16_narrow_n(M, N, K):
+    """N <= 48 bf16 NT GEMMs (layer 0's dW_ih = dG^T x at c3: M = 4H, N = 40, K = T B) on the narrow
+    kernel (128 x 48 tiles of v_mfma_f32_16x16x32_bf16, split-K slabs): against fp64 on the same
+    bf16 operands, with a bias (the slab reduce's epilogue) on the smallest shape."""
+    from pytorch_speaker_verification_amd._lib import call, lib, ptr
+    g = torch.Generator().manual_seed(M + 3 * N + K)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    B = torch.randn(N, K, generator=g).bfloat16()
+    bias = torch.randn(N, generator=g) if N == 16 else None
+    ref = A.double() @ B.double().T + (bias.double() if bias is not None else 0.0)
+    Ad, Bd = A.to(DEV), B.to(DEV)
+    bd = bias.to(DEV) if bias is not None else None
+    C = torch.full((M, N), float("nan"), device=DEV)
+    ws = torch.empty(lib().sv_gemm_bf16_workspace(M, N, K) // 4 + 1, device=DEV)
+    call("sv_gemm_bf16", M, N, K, ptr(Ad), K, ptr(Bd), K, ptr(C), N, ptr(bd) if bd is not None else None, None, 0.0,
+         ptr(ws), torch.cuda.current_stream().cuda_stream)
+    err = (C.cpu().double() - ref).abs().max().item() / ref.abs().max().item()
+    print(f"\nMEASURED gemm_bf16_narrow.{M}x{N}x{K}.rel_vs_fp64 {err:.2e}")
+    assert err <= 1e-5
+
+
 @pytest.mark.parametrize("M,N,K", [(9216, 2048, 96), (9216, 2048, 64), (16640, 1024, 32), (10240, 3072, 768)])
 def test_gemm_f32_persistent_tiles_two_biases(M, N, K):
     """More 256 x 256 tiles than CUs: the persistent form (gemm_f32_256p_kernel: the next tile's
