@@ -900,6 +900,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
   }
 }
 
+#ifndef SV_P3F_MODE  // h_{t-1} staging of the wide forward (A/B builds; see below)
+#define SV_P3F_MODE 0
+#endif
 int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whh_bf, bf16_t* gates, float* c_tm,
                            float* h_tm, bf16_t* h_bf, bf16_t* hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt,
                            int xcd, unsigned* status, unsigned limit, int fault, const bf16_t* x_bf, int F,
@@ -907,17 +910,18 @@ int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
   constexpr size_t base = (size_t)32 * (768 + 8) * 2 + (size_t)32 * (4 * 64 + 4) * 4 + (size_t)32 * 72 * 2 +
                           (size_t)64 * 40 * 2;
   // MODE 0: h_{t-1} staged through registers in two halves.  Measured alternatives (bit-identical
-  // results): LDS-DMA staging (MODE 2) 921 vs 843 us per layer at c3; the second half in flight
-  // during the first half's MFMAs (MODE 1) 4.77 vs 4.67 ms for the 3-layer forward
+  // results): LDS-DMA staging (MODE 2) 921 vs 843 us per layer at c3 (r05, on the scalar-addressed
+  // W3Dma: 908 vs 854); the second half in flight during the first half's MFMAs (MODE 1) 4.77 vs
+  // 4.67 ms for the 3-layer forward
   if (x_bf) {  // layer 0, F = 40: the W_ih fragments take registers, so more W_hh fragments live in LDS
     if (F != 40 || !wih_bf) return SV_EARG;
     constexpr int NL = 16;
-    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 5>), grid, dim3(256), base + (size_t)4 * NL * 1024,
+    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 5, SV_P3F_MODE>), grid, dim3(256), base + (size_t)4 * NL * 1024,
                        stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
                        fault, x_bf, wih_bf, b_ih, b_hh, dbg);
   } else {
     constexpr int NL = 12;
-    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0>), grid, dim3(256), base + (size_t)4 * NL * 1024,
+    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0, SV_P3F_MODE>), grid, dim3(256), base + (size_t)4 * NL * 1024,
                        stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
                        fault, nullptr, nullptr, nullptr, nullptr, dbg);
   }
