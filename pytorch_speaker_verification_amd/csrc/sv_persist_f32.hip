@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int rowu = 16 * gs + 4 * j, rl = lane >> 4, row = rowu + rl;
-        const unsigned vo = (unsigned)((min(b0 + row, B - 1) * H + 4 * ((lane & 15) ^ (4 * j + rl))) * 4);
+        const unsigned vo = (__umul24((unsigned)min(b0 + row, B - 1), (unsigned)H) + 4u * ((lane & 15) ^ (4 * j + rl))) * 4u;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (pf_lds_t)(ring + slot * PF_CH + rowu * 256), 16, vo,
                                                  (unsigned)(ch * PF_KC * 4), 0, 16 /* sc1 */);
       }
@@ -246,7 +246,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int rowu = 2 * (8 * gs + j), row = rowu + (lane >> 5), s = lane & 31;
-        const unsigned vo = (unsigned)((min(b0 + row, B - 1) * (int)G + (s >> 3) * H + j0 + 4 * (s & 7)) * 4);
+        const unsigned vo =
+            (__umul24((unsigned)min(b0 + row, B - 1), (unsigned)G) + (unsigned)((s >> 3) * H + j0 + 4 * (s & 7))) * 4u;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (pf_lds_t)(gxs + (8 * gs + j) * 256), 16, vo, 0, 0,
                                                  SV_PF32_GXAUX);
       }
@@ -724,12 +725,13 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = 2 * (4 * gs + j) + (lane >> 5), s = lane & 31;
-      const unsigned vo = (unsigned)((min(b0 + row, B - 1) * (int)G + (s >> 3) * H + j0 + 4 * (s & 7)) * 4);
+      const unsigned vo =
+          (__umul24((unsigned)min(b0 + row, B - 1), (unsigned)G) + (unsigned)((s >> 3) * H + j0 + 4 * (s & 7))) * 4u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_, (pf_lds_t)(ea + (4 * gs + j) * 256), 16, vo, 0, 0, 0);
     }
     const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
     const int q = g * 64 + lane, row = 8 * gs + (lane >> 3), c = lane & 7;
-    const unsigned vo2 = (unsigned)((min(b0 + row, B - 1) * H + j0 + 4 * c) * 4);
+    const unsigned vo2 = (__umul24((unsigned)min(b0 + row, B - 1), (unsigned)H) + (unsigned)(j0 + 4 * c)) * 4u;
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
     if (tt > 0)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(sv_rsrc(c_tm + (long)(tt - 1) * BH, (unsigned)(BH * 4)),
