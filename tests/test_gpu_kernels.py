@@ -233,8 +233,8 @@ def test_gemm_bf16_narrow_n(M, N, K):
 @pytest.mark.parametrize("M,N,K", [(9216, 2048, 96), (9216, 2048, 64), (16640, 1024, 32), (10240, 3072, 768)])
 def test_gemm_f32_persistent_tiles_two_biases(M, N, K):
     """More 256 x 256 tiles than CUs: the persistent form (gemm_f32_256p_kernel: the next tile's
-    k-tiles 0 and 1 DMA'd ahead of the stores, k-tile 0's wait counting the stores), both bias
-    vectors as K1 passes them; nk = 2 (k-tile 1 the last) and nk = 1 (the one-shot kernel) included."""
+    k-tile 0 DMA'd during this tile's last k-tile), both bias vectors as K1 passes them; nk = 2 and
+    nk = 1 (the one-shot kernel) included."""
     from pytorch_speaker_verification_amd._lib import call, ptr
     g = torch.Generator().manual_seed(M + N + K)
     A, B = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
