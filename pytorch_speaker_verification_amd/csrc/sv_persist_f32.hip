@@ -547,6 +547,9 @@ constexpr int PH_BM = 32;                      // rows of a half
 #ifndef SV_PF32_AHEAD
 #define SV_PF32_AHEAD 2
 #endif
+#ifndef SV_PF32_OVL  // the backward's bias partials and dG^T stores under the hand-off drain (0: A/B)
+#define SV_PF32_OVL 1
+#endif
 #ifndef SV_PF32_DGT_SC1  // the backward's dG^T stores written through with sc1 (r05: 7.62 -> 7.39 GB per
 #define SV_PF32_DGT_SC1 1   // launch of fetch + write, time unchanged; 0: A/B)
 #endif
@@ -709,6 +712,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
   const int quad = tid & 7, erow = tid >> 3;
   // half-step (tt, hf)'s operands -> LDS: wave g: 4 activation pieces (rows 8 g ..), 1 of c_{t-1}, 1
   // of dh_up; absent operands written as zeros into the same slots
+  // the dG^T buffer fits one 32-bit buffer descriptor with room for the dropped-store offset
+  const bool dgt_fits = dgT && (long)4 * H * lddgT * 4 < (1L << 32) - 64;
   auto load_ew = [&](int tt, int hf, int set) {
 #ifdef SV_PF32_HOTOPS  // A/B diagnostic (results invalid): every step reads step T-1's operands, cache-hot
     tt = T - 1;
@@ -904,8 +909,69 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
       }
       __syncthreads();
       PB_STAMP(3);  // 3: cell + dG tiles into LDS
+      // off-chain pieces of the half-step (the bias partials of gate column tid over this half's rows
+      // in order, rows past B excluded; dG^T of the half-step).  The row bounds through an opaque
+      // copy made here, so their predicates are formed here each half-step: hoisted out of the step
+      // loop they were held across the k-loops in SGPRs and spilled to VGPR lanes
+      int Bq = B, Bpq = Bp;
+      asm volatile("" : "+s"(Bq), "+s"(Bpq));
+      auto bias_part = [&]() {
+        if (dbp && tid < 4 * PF_U) {
+          // rows in order either way; the partial row block's runtime bound in its own branch (32
+          // per-row predicates of both halves, hoisted out of the step loop, were 128 SGPRs spilled
+          // to VGPR lanes and read back every step)
+          const int nv = Bq - b0;
+          float s = 0.f;
+          if (nv >= PH_BM) {
+#pragma unroll
+            for (int e4 = 0; e4 < PH_BM / 4; ++e4) {
+              const f32x4 v = *reinterpret_cast<const f32x4*>(gts + tid * LDT + 4 * e4);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) s += v[e];
+            }
+          } else {
+            for (int e = 0; e < nv; ++e) s += gts[tid * LDT + e];
+          }
+          dbs += s;
+        }
+      };
+      // dG^T stores, 4 per thread (128 gate-unit rows x 8 pieces of 4 batch columns); `exact`: every
+      // thread issues all 4 (pieces past Bp to an offset past the descriptor's range, dropped), so a
+      // counted wait can name them
+      auto dgt_stores = [&](bool exact) {
+#ifndef SV_PF32_NODGT  // A/B diagnostic (results invalid): no dG^T stores
+#if SV_PF32_DGT_SC1
+        // sc1 stores: written through and dropped from this XCD's L2 (MI355X_MICROARCH.md, stores of
+        // each flavour), so the 48 KB per tile per step the dW GEMMs read back much later do not
+        // evict the lines the helper workgroups prefetched
+        const __amdgpu_buffer_rsrc_t rdt = sv_rsrc(dgT, (unsigned)((long)4 * H * lddgT * 4));
+#endif
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int p = tid + 256 * i, gu = p >> 3, c = p & 7, gbc = b0 + 4 * c;
+          if (exact || gbc < Bpq) {
+            f32x4 v = *reinterpret_cast<const f32x4*>(gts + gu * LDT + 4 * c);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (gbc + e >= Bq) v[e] = 0.f;
+            const long eo = ((long)(gu >> 5) * H + j0 + (gu & 31)) * lddgT + (long)t * Bp + gbc;
+#if SV_PF32_DGT_SC1
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rdt,
+                                                   gbc < Bpq ? (unsigned)(eo * 4) : 0xFFFFFFF0u, 0, 16 /* sc1 */);
+#else
+            if (gbc < Bpq) *reinterpret_cast<f32x4*>(dgT + eo) = v;
+#endif
+          }
+        }
+#endif
+      };
       // the hand-off: 16 fragment blocks of 1 KB (gate q, this half, k-group 4 ub + kl); slot 0 (no
       // consumer step) only when the dx GEMM reads the fragment-order image (dg == nullptr)
+      // SV_PF32_OVL: with an arrival to make and dG^T written through one descriptor, the bias
+      // partials and the dG^T stores go out behind the hand-off stores, before their drain, and the
+      // drain counts them (vmcnt(4): this wave's hand-off stores, older, are done; a raw barrier, as
+      // __syncthreads' release fence would drain the dG^T stores too)
+      const bool ovl = SV_PF32_OVL && SV_PF32_DGT_SC1 && t > 0 && !dg && dgt_fits;
       if (t > 0 || !dg) {
         const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 4));
 #pragma unroll
@@ -917,7 +983,16 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
               ((unsigned)(((rb * 4 + q) * 2 + hf) * FBLK) + (unsigned)(4 * ub + kl) * 256u + (unsigned)L * 4u) * 4u;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rw, off, 0, 16 /* sc1 */);
         }
-        if (t > 0) {
+        if (ovl) {
+          asm volatile("" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);  // (the dG^T stores stay younger than the hand-off's)
+          bias_part();
+          dgt_stores(true);
+          asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
+            __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (t > 0) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __syncthreads();
           if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
@@ -925,30 +1000,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         }
       }
       PB_STAMP(4);  // 4: hand-off stores + drain + arrival
-      // off the chain: the bias partials (gate column tid: this half's rows in order, rows past B
-      // excluded), row-major dG and dG^T of the half-step.  The row bounds through an opaque copy
-      // made here, so their predicates are formed here each half-step: hoisted out of the step loop
-      // they were held across the k-loops in SGPRs and spilled to VGPR lanes
-      int Bq = B, Bpq = Bp;
-      asm volatile("" : "+s"(Bq), "+s"(Bpq));
-      if (dbp && tid < 4 * PF_U) {
-        // rows in order either way; the partial row block's runtime bound in its own branch (32
-        // per-row predicates of both halves, hoisted out of the step loop, were 128 SGPRs spilled
-        // to VGPR lanes and read back every step)
-        const int nv = Bq - b0;
-        float s = 0.f;
-        if (nv >= PH_BM) {
-#pragma unroll
-          for (int e4 = 0; e4 < PH_BM / 4; ++e4) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(gts + tid * LDT + 4 * e4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) s += v[e];
-          }
-        } else {
-          for (int e = 0; e < nv; ++e) s += gts[tid * LDT + e];
-        }
-        dbs += s;
-      }
+      if (!ovl) bias_part();
       const long gb = b0 + erow;
       if (dg && gb < Bq) {  // (dg == nullptr: the dx GEMM reads the fragment-order hand-off instead)
         float* dp = dg + (long)t * BG + gb * G + j0 + 4 * quad;
@@ -956,30 +1008,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
         for (int q = 0; q < 4; ++q)
           *reinterpret_cast<f32x4*>(dp + q * H) = *reinterpret_cast<const f32x4*>(dgs + erow * LDG + q * PF_U + 4 * quad);
       }
-#ifndef SV_PF32_NODGT  // A/B diagnostic (results invalid): no dG^T stores
-#if SV_PF32_DGT_SC1
-      // sc1 stores: written through and dropped from this XCD's L2 (MI355X_MICROARCH.md, stores of
-      // each flavour), so the 48 KB per tile per step the dW GEMMs read back much later do not evict
-      // the lines the helper workgroups prefetched
-      const __amdgpu_buffer_rsrc_t rdt = sv_rsrc(dgT, (unsigned)((long)4 * H * lddgT * 4));
-#endif
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {  // 128 gate-unit rows x 8 pieces of 4 batch columns
-        const int p = tid + 256 * i, gu = p >> 3, c = p & 7, gbc = b0 + 4 * c;
-        if (gbc < Bpq) {
-          f32x4 v = *reinterpret_cast<const f32x4*>(gts + gu * LDT + 4 * c);
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (gbc + e >= Bq) v[e] = 0.f;
-          const long eo = ((long)(gu >> 5) * H + j0 + (gu & 31)) * lddgT + (long)t * Bp + gbc;
-#if SV_PF32_DGT_SC1
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rdt, (unsigned)(eo * 4), 0, 16 /* sc1 */);
-#else
-          *reinterpret_cast<f32x4*>(dgT + eo) = v;
-#endif
-        }
-      }
-#endif
+      if (!ovl) dgt_stores(false);
       if ((hf == 0 || t > 0) && (!SV_PF32_EDMA || t == T - 1)) {  // (SV_PF32_EDMA: issued in the k-loop)
         __syncthreads();  // dgs / gts read by every wave before the next half-step's operands land
         if (hf == 0)
