@@ -37,6 +37,12 @@
 #ifndef SV_PF32_FWD_AHEAD2  // forward k-loop: A / W fragments two k-groups ahead across chunks
 #define SV_PF32_FWD_AHEAD2 1
 #endif
+#ifndef SV_PF32_OVL  // the backward's bias partials and dG^T stores under the hand-off drain (0: A/B)
+#define SV_PF32_OVL 1
+#endif
+#ifndef SV_PF32_OVL_FWD  // the forward's off-chain stores under its hand-off drain (A/B: measured slower)
+#define SV_PF32_OVL_FWD 0
+#endif
 #ifndef SV_PF32_BDMA  // the forward's ring / x-projection DMA as buffer loads with scalar bases (0: A/B)
 #define SV_PF32_BDMA 1
 #endif
@@ -479,8 +485,38 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
                                                16 /* sc1 */);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // off the chain: activations, c, h^T of step t.  SV_PF32_OVL_FWD (A/B, measured slower: DESIGN
+    // §4) with a whole row block: the h^T tile (LDS) and the 10 activation / c stores per thread go
+    // out behind the hand-off stores, before their drain, which counts them (vmcnt(10); a raw
+    // barrier: __syncthreads' fence would drain them)
+    auto offchain = [&]() {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int row = 2 * rp + k;
+        const long gb = b0 + row;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) hts[(4 * quad + v) * LDH + row] = gb < B ? hv[k][v] : 0.f;
+        if (gb < B) {
+          float* gp = gates + (long)t * BG + gb * G + j0 + 4 * quad;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<f32x4*>(gp + q * H) = *reinterpret_cast<const f32x4*>(pre + row * LDP + q * PF_U + 4 * quad);
+          *reinterpret_cast<f32x4*>(c_tm + (long)t * BH + gb * H + j0 + 4 * quad) =
+              *reinterpret_cast<const f32x4*>(cst + row * CLD + 4 * quad);
+        }
+      }
+    };
+    const bool ovlf = SV_PF32_OVL_FWD && b0 + PF_BM <= B;  // (uniform: every row of the block valid)
+    if (ovlf) {
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);  // (the off-chain stores stay younger than the hand-off's)
+      offchain();
+      asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
 #ifdef SV_PF32_CHKCNT  // A/B diagnostic: a counter >= nub before this workgroup's first arrival was not reset
     if (tid == 0 && t == 0 &&
         __hip_atomic_load(my_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nub)
@@ -489,22 +525,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
     if (tid == 0 && persist_arrive_ok(fault, t == 0))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     PF_STAMP(4);  // 4: hand-off stores + drain + arrival
-    // off the chain: activations, c, h^T of step t
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int row = 2 * rp + k;
-      const long gb = b0 + row;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) hts[(4 * quad + v) * LDH + row] = gb < B ? hv[k][v] : 0.f;
-      if (gb < B) {
-        float* gp = gates + (long)t * BG + gb * G + j0 + 4 * quad;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          *reinterpret_cast<f32x4*>(gp + q * H) = *reinterpret_cast<const f32x4*>(pre + row * LDP + q * PF_U + 4 * quad);
-        *reinterpret_cast<f32x4*>(c_tm + (long)t * BH + gb * H + j0 + 4 * quad) =
-            *reinterpret_cast<const f32x4*>(cst + row * CLD + 4 * quad);
-      }
-    }
+    if (!ovlf) offchain();
     if (hT) {
       __syncthreads();
 #pragma unroll
@@ -546,9 +567,6 @@ constexpr int PH_BM = 32;                      // rows of a half
 // s + SV_PF32_AHEAD -- ahead of the compute waves' own LDS-DMA of them (issued at the end of step s + 1)
 #ifndef SV_PF32_AHEAD
 #define SV_PF32_AHEAD 2
-#endif
-#ifndef SV_PF32_OVL  // the backward's bias partials and dG^T stores under the hand-off drain (0: A/B)
-#define SV_PF32_OVL 1
 #endif
 #ifndef SV_PF32_DGT_SC1  // the backward's dG^T stores written through with sc1 (r05: 7.62 -> 7.39 GB per
 #define SV_PF32_DGT_SC1 1   // launch of fetch + write, time unchanged; 0: A/B)
