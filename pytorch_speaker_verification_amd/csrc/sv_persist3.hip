@@ -15,6 +15,9 @@
 // per-gate k order and gate-order sum (bit-identical dG), fragment-order hand-off (row blocks of
 // 32), operands staged by LDS-DMA after the arrival, bias partials per row block.
 // ============================================================================
+#ifndef SV_P3B_OVL  // the wide backward's dG^T stores under the hand-off drain (0: A/B)
+#define SV_P3B_OVL 1
+#endif
 // NL: the last NL k-steps of the second W_hh half are read from LDS (staged once, 16 B per lane per
 // fragment, prefetched two k-steps ahead) -- the registers cannot hold all 2 x NS fragments beside
 // the step's working set
@@ -127,10 +130,14 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     } else {
       if (!dgT) return;
       const __amdgpu_buffer_rsrc_t rs = sv_rsrc(dgT + (long)tt * Bp, (unsigned)(4L * H * lddgT * 2 - (long)tt * Bp * 2));
-      const int q = tid + 256 * (i - 4), gu = q >> 2, c = q & 3;
+      const int q = tid + 256 * (i & 3), gu = q >> 2, c = q & 3;
       const int gq = gu / U, gj = j0 + gu % U, gb = b0 + 8 * c;
       const uint4 v = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * (c ^ ((gu % U) >> 4 & 3)));
-      if (gb < Bp && gj < H)
+      if (i >= 8)  // (exact form, i = 8..11: always issued, an invalid piece to a dropped offset)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rs,
+                                               gb < Bp && gj < H ? (unsigned)((((long)gq * H + gj) * lddgT + gb) * 2)
+                                                                 : 0xFFFFFFF0u, 0, 0);
+      else if (gb < Bp && gj < H)
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rs,
                                                (unsigned)((((long)gq * H + gj) * lddgT + gb) * 2), 0, 0);
     }
@@ -266,8 +273,21 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // SV_P3B_OVL: with the dx GEMM on the hand-off (no row-major dG), the step's 4 dG^T stores per
+    // thread go out behind the hand-off stores, before their drain, which counts them (vmcnt(4):
+    // this wave's older hand-off stores done; a raw barrier: __syncthreads' fence would drain them)
+    const bool ovl = SV_P3B_OVL && !DEFER && !dbg && !dg && dgT;
+    if (ovl) {
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);  // (the dG^T stores stay younger than the hand-off's)
+#pragma unroll
+      for (int i = 8; i < 12; ++i) store_piece(t, i);
+      asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
     if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     mark(3);
@@ -275,7 +295,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
       // (dbg, profiling only: 64 skips the operand DMA, 128 the dG / dG^T stores).  The stores
       // first: their LDS reads issued behind an LDS-DMA would wait for it to land (the compiler
       // cannot tell the DMA's LDS range from the tiles', so it puts vmcnt(0) before every read)
-      if (!(dbg & 8) && !(dbg & 128))
+      if (!ovl && !(dbg & 8) && !(dbg & 128))
 #pragma unroll
         for (int i = 0; i < 8; ++i) store_piece(t, i);
       if (!DEFER && t > 0 && !(dbg & 64)) load_ew(t - 1);
