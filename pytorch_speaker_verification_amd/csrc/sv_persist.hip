@@ -28,6 +28,9 @@
 #include "../../include/sv_ge2e.h"
 
 #include "sv_persist_dev.h"
+#ifndef SV_P2B_OVL  // the 32 x 32 persistent backward's dG^T stores under the hand-off drain (0: A/B)
+#define SV_P2B_OVL 1
+#endif
 
 // A-operand tile of a handed-off buffer: [R][BK] bf16 rows (row stride ld elements) read with
 // buffer_load_dwordx4 sc1 (bypasses the CU's L1, L2-served; rows past the buffer end read 0)
@@ -760,9 +763,31 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
       }
     }
-    // publish dG_t: every store of the hand-off drained, barrier, one lane arrives
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // publish dG_t: every store of the hand-off drained, barrier, one lane arrives.  SV_P2B_OVL (no
+    // row-major dG: the dx GEMM reads the hand-off): the BM / 16 dG^T stores per thread (buffer
+    // stores; a piece past Bp to a dropped offset) go out first, and the drain counts them
+    // (vmcnt(BM / 16): this wave's older hand-off stores done; a raw barrier: __syncthreads' fence
+    // would drain them)
+    const bool ovl = SV_P2B_OVL && !dbg && !dg && dgT && 4L * H * lddgT * 2 < (1L << 32) - 64;
+    if (ovl) {
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);  // (the dG^T stores stay younger than the hand-off's)
+      const __amdgpu_buffer_rsrc_t rt = sv_rsrc(dgT, (unsigned)(4L * H * lddgT * 2));
+#pragma unroll
+      for (int i = 0; i < BM / 16; ++i) {
+        const int q = tid + 256 * i, gu = q / (BM / 8), c = q % (BM / 8);
+        const int gq = gu / BF_U, gj = j0 + gu % BF_U, gb = b0 + 8 * c;
+        const uint4 v = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
+        const unsigned off =
+            gb < Bp && gj < H ? (unsigned)((((long)gq * H + gj) * lddgT + (long)t * Bp + gb) * 2) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rt, off, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(BM / 16) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
     if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     mark(3);
@@ -780,7 +805,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
           *reinterpret_cast<uint4*>(dgt + (long)gb * G + (long)gq * H + gj) =
               *reinterpret_cast<const uint4*>(dgs + row * LDG + gq * BF_U + 8 * c);
       }
-      if (dgT) {
+      if (dgT && !ovl) {
 #pragma unroll
         for (int i = 0; i < BM / 16; ++i) {
           const int q = tid + 256 * i, gu = q / (BM / 8), c = q % (BM / 8);

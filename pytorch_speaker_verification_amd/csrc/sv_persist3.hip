@@ -1217,12 +1217,36 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // SV_P3B_OVL: the 2 dG_t^T stores per thread (buffer stores; a piece past Bp to a dropped offset)
+    // behind the hand-off stores, before their drain, which counts them (vmcnt(2): this wave's
+    // older hand-off and dx stores done; a raw barrier: __syncthreads' fence would drain them)
+    const bool ovl = SV_P3B_OVL && t >= 0 && a.dgT[l] && 4L * H * a.lddgT * 2 < (1L << 32) - 64;
+    if (ovl) {
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);  // (the dG^T stores stay younger than the hand-off's)
+      const __amdgpu_buffer_rsrc_t rt = sv_rsrc(a.dgT[l], (unsigned)(4L * H * a.lddgT * 2));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int q = tid + 256 * i, gu = q >> 2, c = q & 3;
+        const int gq = gu / U, gj = j0 + gu % U, gc = b0 + 8 * c;
+        const long eo = ((long)gq * H + gj) * a.lddgT + (long)t * a.Bp + gc;
+        const uint4 v = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
+        const unsigned off = gc < a.Bp && gj < H ? (unsigned)(eo * 2) : 0xFFFFFFF0u;
+        if ((SV_WAVE_DW_SIDE || SV_WAVE_DGT_SC1) && a.dgt_sc1)
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rt, off, 0, 16 /* sc1 */);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rt, off, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
     if (tid == 0 && persist_arrive_ok(a.fault, t == T - 1))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     WB_MARK(3);  // 3: dG_t hand-off stores + drain + arrival
-    if (t >= 0 && a.dgT[l]) {  // dG_t^T (the dW GEMMs' operand), then the next step's operands
+    if (!ovl && t >= 0 && a.dgT[l]) {  // dG_t^T (the dW GEMMs' operand), then the next step's operands
       // dgt_sc1: written through (16-B sc1 stores), because the weight-gradient GEMM beside this
       // launch reads them once iteration t - 1 has arrived (its vmcnt(0) covers these stores)
       const __amdgpu_buffer_rsrc_t rt = sv_rsrc(a.dgT[l], a.dgt_sc1 ? (unsigned)(4L * H * a.lddgT * 2) : 0u);
