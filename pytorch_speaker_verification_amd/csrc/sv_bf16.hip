@@ -650,6 +650,63 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qw_kernel(const G8Queue q) 
   }
 }
 
+// ---- the layer wavefront's weight gradients as whole-K tiles in one launch (c4 rank) ----
+// After the wavefront every layer's dG^T is final.  The per-layer split-K plan (c4 rank: K = T Bp =
+// 12800 in 7 slabs of 29 k-tiles; 504 workgroups per dual GEMM, two rounds) writes 129 MB of fp32
+// slabs per layer and reads them back in a reduce launch; the three layers' 256 x 256 tiles
+// together (72 + 72 dual, 36 for layer 0's dW_hh) fit the CUs as ONE round of whole-K tiles, each
+// stored straight into dW_hh / dW_ih.  Another fp32 summation order than the slabs' (one
+// accumulator over all k-tiles): agreement with the per-layer schedule at fp32 level.
+struct G8FLayer {
+  const bf16_t* A;    // dG^T [4H][T Bp]
+  const bf16_t* B;    // h^T (time-shifted)
+  const bf16_t* B2;   // x^T (dual: columns past n1), or null
+  float* C1;          // dW_hh
+  float* C2;          // dW_ih (dual)
+  long lda, ldb, ldb2, ldc1, ldc2;
+  int N, n1, tiles;
+};
+struct G8Full {
+  G8FLayer lay[WB_L];
+  int K;
+};
+#ifndef SV_WAVE_DW_FULLK
+#define SV_WAVE_DW_FULLK 1
+#endif
+__global__ __launch_bounds__(512, 1) void gemm_bf16_8qf_kernel(const G8Full q) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const G8FLayer& L2 = q.lay[2];
+  const G8FLayer& L1 = q.lay[1];
+  const G8FLayer& L0 = q.lay[0];
+  // position r after xcd_remap: each XCD owns a contiguous run, so a row tile's column tiles (the
+  // same dG^T rows) share an L2; top layer first
+  const int r = xcd_remap(blockIdx.x, (int)gridDim.x);
+  const int l = r < L2.tiles ? 2 : r < L2.tiles + L1.tiles ? 1 : 0;
+  const int tile = l == 2 ? r : l == 1 ? r - L2.tiles : r - L2.tiles - L1.tiles;
+  // (field-wise selects: a dynamic index into the kernel-argument struct would copy it to scratch)
+  const bf16_t* A = l == 2 ? L2.A : l == 1 ? L1.A : L0.A;
+  const bf16_t* Bm = l == 2 ? L2.B : l == 1 ? L1.B : L0.B;
+  const bf16_t* B2 = l == 2 ? L2.B2 : l == 1 ? L1.B2 : L0.B2;
+  float* C1 = l == 2 ? L2.C1 : l == 1 ? L1.C1 : L0.C1;
+  float* C2 = l == 2 ? L2.C2 : l == 1 ? L1.C2 : L0.C2;
+  const long lda = l == 2 ? L2.lda : l == 1 ? L1.lda : L0.lda;
+  const long ldb = l == 2 ? L2.ldb : l == 1 ? L1.ldb : L0.ldb;
+  const long ldb2 = l == 2 ? L2.ldb2 : l == 1 ? L1.ldb2 : L0.ldb2;
+  const long ldc1 = l == 2 ? L2.ldc1 : l == 1 ? L1.ldc1 : L0.ldc1;
+  const long ldc2 = l == 2 ? L2.ldc2 : l == 1 ? L1.ldc2 : L0.ldc2;
+  const int N = l == 2 ? L2.N : l == 1 ? L1.N : L0.N;
+  const int n1 = l == 2 ? L2.n1 : l == 1 ? L1.n1 : L0.n1;
+  const int tiles_n = N / G256_BM;
+  const int tn = tile % tiles_n, tm = tile / tiles_n;
+  g8_f32x4 acc[8][4];
+  g8_tile<0>(A, lda, Bm, ldb, G256AFrag{}, G256Dual{B2, ldb2, n1}, tm, tn, 0, q.K / G256_BK, smem, acc);
+  const bool second = tn * G256_BM >= n1;  // n1 % 256 == 0 (host): a tile is all C1 or all C2
+  g8_epilogue<G8_STORE>(acc, second ? C2 : C1, second ? ldc2 : ldc1, 0, tm, second ? tn - n1 / G256_BM : tn, wr, wc,
+                        lane, nullptr, nullptr, 0.f);
+}
+
 }  // namespace
 
 extern "C" size_t sv_gemm_bf16_workspace(int M, int N, int K);
@@ -1412,6 +1469,46 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
         if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
       }
       return SV_OK;
+    }
+    // every layer's whole-K weight-gradient tiles in one launch where they fit one round of the CUs
+    // (gemm_bf16_8qf_kernel; layer 0's N = F dW_ih after it on the narrow kernel)
+    if (SV_WAVE_DW_FULLK && L == WB_L && gemm256_ok(4 * H, H, TBp) && TBp % 8 == 0 && ldhT % 8 == 0) {
+      G8Full f{};
+      f.K = TBp;
+      bool ok = true;
+      int P = 0;
+      for (int l = 0; l < L; ++l) {
+        const bool dual = l > 0;  // upper layers: input width H
+        G8FLayer& fl = f.lay[l];
+        fl.A = dgT[l];
+        fl.lda = TBp;
+        fl.B = hT[l];
+        fl.ldb = ldhT;
+        fl.B2 = dual ? xT[l] : nullptr;
+        fl.ldb2 = dual ? ld_xT[l] : 0;
+        fl.C1 = dw_hh[l];
+        fl.ldc1 = H;
+        fl.C2 = dual ? dw_ih[l] : nullptr;
+        fl.ldc2 = H;
+        fl.n1 = H;
+        fl.N = dual ? 2 * H : H;
+        fl.tiles = (4 * H / G256_BM) * (fl.N / G256_BM);
+        P += fl.tiles;
+        if (((uintptr_t)dgT[l] | (uintptr_t)hT[l] | (uintptr_t)dw_hh[l]) & 15) ok = false;
+        if (dual && ((((uintptr_t)xT[l] | (uintptr_t)dw_ih[l]) & 15) || ld_xT[l] % 8)) ok = false;
+      }
+      if (ok && P <= cus) {
+        hipLaunchKernelGGL(gemm_bf16_8qf_kernel, dim3(P), dim3(512), G256_LDS, main, f);
+        SV_LAUNCH_CHECK();
+        for (int l = L - 1; l >= 1; --l)
+          if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
+        const BBwdWs ws = carve_bbwd((char*)workspace, T, B, std::max(F, H), H);
+        if ((rc = sv_gemm_bf16(4 * H, F, TBp, dgT[0], TBp, xT[0], ld_xT[0], dw_ih[0], F, nullptr, nullptr, 0.f, ws.gws,
+                               main)))
+          return rc;
+        if ((e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
+        return SV_OK;
+      }
     }
     for (int l = L - 1; l >= 0; --l) {
       const int Fl = l == 0 ? F : H;
