@@ -472,4 +472,5 @@ size_t sv_wave_bwd_scratch(int L, int T, int B, int H);
 int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, const bf16_t* const* wihT,
                      const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
                      bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
-                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, int dgt_sc1 = 0, long ldwih = 0);
+                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, int dgt_sc1 = 0, long ldwih = 0,
+                     int zero_next = 0);

@@ -656,7 +656,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qw_kernel(const G8Queue q) 
 // slabs per layer and reads them back in a reduce launch; the three layers' 256 x 256 tiles
 // together (72 + 72 dual, 36 for layer 0's dW_hh) fit the CUs as ONE round of whole-K tiles, each
 // stored straight into dW_hh / dW_ih.  Another fp32 summation order than the slabs' (one
-// accumulator over all k-tiles): agreement with the per-layer schedule at fp32 level.
+// accumulator over the k-tiles): agreement with the per-layer schedule at fp32 level.
+// Split form (S > 0): the CUs the tiles leave free (nsw workgroups, a multiple of 8, blocks
+// 0 .. nsw - 1) compute every tile's first S k-tiles (tiles b, b + nsw, ...) and store the fp32
+// partial (sc1, per-thread order) and a flag; the tile's own workgroup (block nsw + position)
+// computes k-tiles S .. K/64 - 1, waits for the flag, adds the partial (its own sum first: one
+// fixed order) and stores C.  The waiters are dispatched after every workgroup they wait for.
 struct G8FLayer {
   const bf16_t* A;    // dG^T [4H][T Bp]
   const bf16_t* B;    // h^T (time-shifted)
@@ -668,10 +673,21 @@ struct G8FLayer {
 };
 struct G8Full {
   G8FLayer lay[WB_L];
-  int K;
+  int K;             // T Bp
+  int nsw, S;        // split form: first-piece workgroups and k-tiles (S = 0: whole-K tiles only)
+  float* part;       // [P][256 x 256] fp32 first-piece partials
+  unsigned* flag;    // [P], zero before the launch
+  unsigned* status;  // the sync block's status word
+  unsigned limit;
 };
 #ifndef SV_WAVE_DW_FULLK
 #define SV_WAVE_DW_FULLK 1
+#endif
+#ifndef SV_WAVE_DW_SPLIT  // the split form on the CUs the whole-K tiles leave free
+#define SV_WAVE_DW_SPLIT 1
+#endif
+#ifndef SV_WAVE_DW_SOFF  // the first pieces' k-tiles below an even split (per workgroup: theirs and the tile's)
+#define SV_WAVE_DW_SOFF 2
 #endif
 __global__ __launch_bounds__(512, 1) void gemm_bf16_8qf_kernel(const G8Full q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -680,28 +696,64 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qf_kernel(const G8Full q) {
   const G8FLayer& L2 = q.lay[2];
   const G8FLayer& L1 = q.lay[1];
   const G8FLayer& L0 = q.lay[0];
-  // position r after xcd_remap: each XCD owns a contiguous run, so a row tile's column tiles (the
-  // same dG^T rows) share an L2; top layer first
-  const int r = xcd_remap(blockIdx.x, (int)gridDim.x);
-  const int l = r < L2.tiles ? 2 : r < L2.tiles + L1.tiles ? 1 : 0;
-  const int tile = l == 2 ? r : l == 1 ? r - L2.tiles : r - L2.tiles - L1.tiles;
-  // (field-wise selects: a dynamic index into the kernel-argument struct would copy it to scratch)
-  const bf16_t* A = l == 2 ? L2.A : l == 1 ? L1.A : L0.A;
-  const bf16_t* Bm = l == 2 ? L2.B : l == 1 ? L1.B : L0.B;
-  const bf16_t* B2 = l == 2 ? L2.B2 : l == 1 ? L1.B2 : L0.B2;
+  const int P = L2.tiles + L1.tiles + L0.tiles;
+  // tile r (top layer first) -> its operands (field-wise selects: a dynamic index into the
+  // kernel-argument struct would copy it to scratch)
+  auto run = [&](int r, int kbeg, int nk, g8_f32x4 (&acc)[8][4], int& l, int& tm, int& tn) {
+    l = r < L2.tiles ? 2 : r < L2.tiles + L1.tiles ? 1 : 0;
+    const int tile = l == 2 ? r : l == 1 ? r - L2.tiles : r - L2.tiles - L1.tiles;
+    const bf16_t* A = l == 2 ? L2.A : l == 1 ? L1.A : L0.A;
+    const bf16_t* Bm = l == 2 ? L2.B : l == 1 ? L1.B : L0.B;
+    const bf16_t* B2 = l == 2 ? L2.B2 : l == 1 ? L1.B2 : L0.B2;
+    const long lda = l == 2 ? L2.lda : l == 1 ? L1.lda : L0.lda;
+    const long ldb = l == 2 ? L2.ldb : l == 1 ? L1.ldb : L0.ldb;
+    const long ldb2 = l == 2 ? L2.ldb2 : l == 1 ? L1.ldb2 : L0.ldb2;
+    const int N = l == 2 ? L2.N : l == 1 ? L1.N : L0.N;
+    const int n1 = l == 2 ? L2.n1 : l == 1 ? L1.n1 : L0.n1;
+    const int tiles_n = N / G256_BM;
+    tn = tile % tiles_n;
+    tm = tile / tiles_n;
+    g8_tile<0>(A, lda, Bm, ldb, G256AFrag{}, G256Dual{B2, ldb2, n1}, tm, tn, kbeg, nk, smem, acc);
+  };
+  g8_f32x4 acc[8][4];
+  int l, tm, tn;
+  if ((int)blockIdx.x < q.nsw) {  // first pieces
+    for (int j = blockIdx.x; j < P; j += q.nsw) {
+      run(j, 0, q.S, acc, l, tm, tn);
+      const __amdgpu_buffer_rsrc_t rp = sv_rsrc(q.part + (long)j * G256_BM * G256_BM, G256_BM * G256_BM * 4u);
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        const g8_f32x4 v = acc[i >> 2][i & 3];
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4_t{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])}, rp,
+            (unsigned)(i * 512 + tid) * 16u, 0, 16 /* sc1 */);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(q.flag + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  // position after xcd_remap (nsw % 8 == 0, so blocks nsw + i keep i's XCD): each XCD owns a
+  // contiguous run, so a row tile's column tiles (the same dG^T rows) share an L2
+  const int r = xcd_remap((int)blockIdx.x - q.nsw, P);
+  run(r, q.S * G256_BK, q.K / G256_BK - q.S, acc, l, tm, tn);
+  if (q.S > 0) {
+    if (tid == 0) persist_wait(q.flag + r, 1u, q.status, q.limit, 2u);
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rp = sv_rsrc(q.part + (long)r * G256_BM * G256_BM, G256_BM * G256_BM * 4u);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(rp, (unsigned)(i * 512 + tid) * 16u, 0, 16 /* sc1 */);
+      acc[i >> 2][i & 3] += g8_f32x4{__uint_as_float(x[0]), __uint_as_float(x[1]), __uint_as_float(x[2]),
+                                     __uint_as_float(x[3])};
+    }
+  }
   float* C1 = l == 2 ? L2.C1 : l == 1 ? L1.C1 : L0.C1;
   float* C2 = l == 2 ? L2.C2 : l == 1 ? L1.C2 : L0.C2;
-  const long lda = l == 2 ? L2.lda : l == 1 ? L1.lda : L0.lda;
-  const long ldb = l == 2 ? L2.ldb : l == 1 ? L1.ldb : L0.ldb;
-  const long ldb2 = l == 2 ? L2.ldb2 : l == 1 ? L1.ldb2 : L0.ldb2;
   const long ldc1 = l == 2 ? L2.ldc1 : l == 1 ? L1.ldc1 : L0.ldc1;
   const long ldc2 = l == 2 ? L2.ldc2 : l == 1 ? L1.ldc2 : L0.ldc2;
-  const int N = l == 2 ? L2.N : l == 1 ? L1.N : L0.N;
   const int n1 = l == 2 ? L2.n1 : l == 1 ? L1.n1 : L0.n1;
-  const int tiles_n = N / G256_BM;
-  const int tn = tile % tiles_n, tm = tile / tiles_n;
-  g8_f32x4 acc[8][4];
-  g8_tile<0>(A, lda, Bm, ldb, G256AFrag{}, G256Dual{B2, ldb2, n1}, tm, tn, 0, q.K / G256_BK, smem, acc);
   const bool second = tn * G256_BM >= n1;  // n1 % 256 == 0 (host): a tile is all C1 or all C2
   g8_epilogue<G8_STORE>(acc, second ? C2 : C1, second ? ldc2 : ldc1, 0, tm, second ? tn - n1 / G256_BM : tn, wr, wc,
                         lane, nullptr, nullptr, 0.f);
@@ -1278,7 +1330,7 @@ namespace {
 struct BBwdWs {
   float *dcf0, *dcf1, *gws;
   bf16_t *whhT, *wihT;
-  size_t total;
+  size_t gbytes, total;  // gws bytes; the region's
 };
 BBwdWs carve_bbwd(char* base, int T, int B, int F, int H) {
   BBwdWs w;
@@ -1298,6 +1350,7 @@ BBwdWs carve_bbwd(char* base, int T, int B, int F, int H) {
   g = std::max(g, sv_gemm_bf16_workspace(T * B, F, 4 * H));
   g = std::max(g, sv_gemm_bf16_dual_workspace(4 * H, H, F, TBp));
   w.gws = (float*)take(g);
+  w.gbytes = g;
   w.total = off;
   return w;
 }
@@ -1440,9 +1493,54 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       SV_LAUNCH_CHECK();
       if ((e = hipEventRecord(ev[1], side[0])) != hipSuccess) return (int)e;
     }
+    // every layer's whole-K weight-gradient tiles in one launch where they fit one round of the CUs
+    // (gemm_bf16_8qf_kernel; layer 0's N = F dW_ih after it on the narrow kernel)
+    G8Full f{};
+    int fP = 0;
+    bool fullk = false;
+    if (SV_WAVE_DW_FULLK && !queued && L == WB_L && gemm256_ok(4 * H, H, TBp) && TBp % 8 == 0 && ldhT % 8 == 0) {
+      f.K = TBp;
+      fullk = true;
+      for (int l = 0; l < L; ++l) {
+        const bool dual = l > 0;  // upper layers: input width H
+        G8FLayer& fl = f.lay[l];
+        fl.A = dgT[l];
+        fl.lda = TBp;
+        fl.B = hT[l];
+        fl.ldb = ldhT;
+        fl.B2 = dual ? xT[l] : nullptr;
+        fl.ldb2 = dual ? ld_xT[l] : 0;
+        fl.C1 = dw_hh[l];
+        fl.ldc1 = H;
+        fl.C2 = dual ? dw_ih[l] : nullptr;
+        fl.ldc2 = H;
+        fl.n1 = H;
+        fl.N = dual ? 2 * H : H;
+        fl.tiles = (4 * H / G256_BM) * (fl.N / G256_BM);
+        fP += fl.tiles;
+        if (((uintptr_t)dgT[l] | (uintptr_t)hT[l] | (uintptr_t)dw_hh[l]) & 15) fullk = false;
+        if (dual && ((((uintptr_t)xT[l] | (uintptr_t)dw_ih[l]) & 15) || ld_xT[l] % 8)) fullk = false;
+      }
+      fullk = fullk && fP <= cus;
+      // the split form where at least 8 CUs are left over and the partials fit the GEMM scratch
+      const BBwdWs wsp = carve_bbwd((char*)workspace + per * (L - 1), T, B, std::max(F, H), H);
+      const int KT = TBp / G256_BK;
+      f.nsw = fullk && SV_WAVE_DW_SPLIT ? (cus - fP) / 8 * 8 : 0;
+      if (f.nsw > 0) {
+        const int per_wg = (fP + f.nsw - 1) / f.nsw;  // first pieces per workgroup
+        f.S = KT / (per_wg + 1) - SV_WAVE_DW_SOFF;    // (their stores and prologues: a little less)
+      }
+      if (f.nsw <= 0 || f.S < 4 || (size_t)fP * G256_BM * G256_BM * 4 > wsp.gbytes) f.nsw = f.S = 0;
+      if (f.S > 0) {
+        f.part = wsp.gws;
+        f.flag = sync + SV_SYNC_CNT + (size_t)WB_L * SV_PCNT_ROWS * SV_PCNT_STRIDE;  // channel 3, zeroed with the
+        f.status = sync;                                                             // wavefront's counters
+        f.limit = sv_persist_limit();
+      }
+    }
     rc = sv_wave_bwd_bf16(L, T, B, H, whhT_l, wihT_l, gates, c_tm, dh_last, dx, dgT, (char*)workspace + per * L,
                               sync, main, db_ih, db_hh, probe ? probe[0] : nullptr, probe ? probe[1] : nullptr,
-                              beside || SV_WAVE_DGT_SC1 ? 1 : 0, bf16_wiht_ld(H));
+                              beside || SV_WAVE_DGT_SC1 ? 1 : 0, bf16_wiht_ld(H), f.S > 0 ? fP : 0);
     if (rc) return rc;
     if (queued) {
       hipLaunchKernelGGL(gemm_bf16_8qw_kernel<0>, dim3(cus), dim3(512), G256_LDS, main, q);
@@ -1470,45 +1568,17 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       }
       return SV_OK;
     }
-    // every layer's whole-K weight-gradient tiles in one launch where they fit one round of the CUs
-    // (gemm_bf16_8qf_kernel; layer 0's N = F dW_ih after it on the narrow kernel)
-    if (SV_WAVE_DW_FULLK && L == WB_L && gemm256_ok(4 * H, H, TBp) && TBp % 8 == 0 && ldhT % 8 == 0) {
-      G8Full f{};
-      f.K = TBp;
-      bool ok = true;
-      int P = 0;
-      for (int l = 0; l < L; ++l) {
-        const bool dual = l > 0;  // upper layers: input width H
-        G8FLayer& fl = f.lay[l];
-        fl.A = dgT[l];
-        fl.lda = TBp;
-        fl.B = hT[l];
-        fl.ldb = ldhT;
-        fl.B2 = dual ? xT[l] : nullptr;
-        fl.ldb2 = dual ? ld_xT[l] : 0;
-        fl.C1 = dw_hh[l];
-        fl.ldc1 = H;
-        fl.C2 = dual ? dw_ih[l] : nullptr;
-        fl.ldc2 = H;
-        fl.n1 = H;
-        fl.N = dual ? 2 * H : H;
-        fl.tiles = (4 * H / G256_BM) * (fl.N / G256_BM);
-        P += fl.tiles;
-        if (((uintptr_t)dgT[l] | (uintptr_t)hT[l] | (uintptr_t)dw_hh[l]) & 15) ok = false;
-        if (dual && ((((uintptr_t)xT[l] | (uintptr_t)dw_ih[l]) & 15) || ld_xT[l] % 8)) ok = false;
-      }
-      if (ok && P <= cus) {
-        hipLaunchKernelGGL(gemm_bf16_8qf_kernel, dim3(P), dim3(512), G256_LDS, main, f);
-        SV_LAUNCH_CHECK();
-        for (int l = L - 1; l >= 1; --l)
-          if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
-        const BBwdWs ws = carve_bbwd((char*)workspace, T, B, std::max(F, H), H);
-        if ((rc = sv_gemm_bf16(4 * H, F, TBp, dgT[0], TBp, xT[0], ld_xT[0], dw_ih[0], F, nullptr, nullptr, 0.f, ws.gws,
-                               main)))
-          return rc;
-        if ((e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
-        return SV_OK;
-      }
+    if (fullk) {
+      hipLaunchKernelGGL(gemm_bf16_8qf_kernel, dim3(f.nsw + fP), dim3(512), G256_LDS, main, f);
+      SV_LAUNCH_CHECK();
+      for (int l = L - 1; l >= 1; --l)
+        if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
+      const BBwdWs ws = carve_bbwd((char*)workspace, T, B, std::max(F, H), H);
+      if ((rc = sv_gemm_bf16(4 * H, F, TBp, dgT[0], TBp, xT[0], ld_xT[0], dw_ih[0], F, nullptr, nullptr, 0.f, ws.gws,
+                             main)))
+        return rc;
+      if ((e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
+      return SV_OK;
     }
     for (int l = L - 1; l >= 0; --l) {
       const int Fl = l == 0 ? F : H;

@@ -1226,7 +1226,8 @@ size_t sv_wave_bwd_scratch(int L, int T, int B, int H) {
 int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, const bf16_t* const* wihT,
                      const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
                      bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
-                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, int dgt_sc1, long ldwih) {
+                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, int dgt_sc1, long ldwih,
+                     int zero_next) {
   if (!sv_wave_bwd_fits(L, B, H, sv_stream_cus(stream))) return SV_ESHAPE;
   if (!scratch || ((uintptr_t)scratch & 15) || !sync || !dh_last || !whhT || !wihT || !acts || !c_tm || !dx || !dgT)
     return SV_EARG;
@@ -1249,7 +1250,11 @@ int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, cons
     p += wave_dbp_bytes(B, H);
     a.cnt[l] = sync_cnt(sync, l);
   }
-  if (int rc = sv_zero_counters(a.cnt[0], L, (long)SV_PCNT_ROWS * SV_PCNT_STRIDE, a.nrb * SV_PCNT_STRIDE, stream))
+  if (zero_next > 0 && (L + 1 > SV_SYNC_CHANNELS || zero_next > SV_PCNT_ROWS * SV_PCNT_STRIDE)) return SV_EARG;
+  // zero_next > 0: channel L's first zero_next words too (the flags of the weight-gradient launch
+  // that follows, gemm_bf16_8qf_kernel), in the same launch
+  if (int rc = sv_zero_counters(a.cnt[0], zero_next > 0 ? L + 1 : L, (long)SV_PCNT_ROWS * SV_PCNT_STRIDE,
+                                std::max(a.nrb * SV_PCNT_STRIDE, zero_next), stream))
     return rc;
   a.dh_last = dh_last;
   a.status = sync;
