@@ -34,7 +34,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import random
 import socket
 import subprocess
 import sys
@@ -276,31 +275,29 @@ def time_dw_gemm(T, B, H, dev, reps=5):
     return _timed(f, dev, reps), 2.0 * 4 * H * H * K, 4.0 * (4 * H * K + H * K + 4 * H * H)
 
 
-def reference_loop_body(embedder_net, ge2e_loss, optimizer, mel_db_batch, N, M):
-    """The reference's training-loop body, train_speech_embedder.py:46-65, as user code: whatever
-    modules it is handed (this package's through dropin/, or the stock-PyTorch port) run through
-    it unchanged -- reshape, random perm / unperm, zero_grad, forward, GE2E loss, loss.backward()
-    (autograd through EmbedderFunction / GE2EFunction), torch clip_grad_norm_ x2, SGD.step."""
-    mel_db_batch = torch.reshape(mel_db_batch, (N * M, mel_db_batch.size(2), mel_db_batch.size(3)))
-    perm = random.sample(range(0, N * M), N * M)
-    unperm = list(perm)
-    for i, j in enumerate(perm):
-        unperm[j] = i
-    mel_db_batch = mel_db_batch[perm]
-    optimizer.zero_grad()
-    embeddings = embedder_net(mel_db_batch)
-    embeddings = embeddings[unperm]
-    embeddings = torch.reshape(embeddings, (N, M, embeddings.size(1)))
-    loss = ge2e_loss(embeddings)
+def user_train_step(net, loss_fn, opt, frames, n_spk, n_utt, gen=None):
+    """One step of a user-written GE2E loop over nn.Module objects, the shape of the loop
+    train_speech_embedder.py:46-65 runs (there: reshape, a shuffled row order around the forward,
+    zero_grad, forward, GE2E loss, backward, clip_grad_norm_ 3.0 / 1.0, SGD step).  Written here
+    with torch primitives: the row shuffle is ``torch.randperm`` and its inverse ``argsort``.
+    Whatever modules it is handed (this package's through dropin/, or the stock-PyTorch port) run
+    through autograd, torch's clip_grad_norm_ and the optimizer, nothing fused."""
+    rows = n_spk * n_utt
+    flat = frames.flatten(0, 1)                                   # [N*M, T, F]
+    order = torch.randperm(rows, generator=gen).to(flat.device)
+    back = torch.argsort(order)                                   # order[back] == arange
+    opt.zero_grad()
+    emb = net(flat.index_select(0, order)).index_select(0, back)
+    loss = loss_fn(emb.view(n_spk, n_utt, -1))
     loss.backward()
-    torch.nn.utils.clip_grad_norm_(embedder_net.parameters(), 3.0)
-    torch.nn.utils.clip_grad_norm_(ge2e_loss.parameters(), 1.0)
-    optimizer.step()
+    for group, max_norm in zip(opt.param_groups, (3.0, 1.0)):
+        torch.nn.utils.clip_grad_norm_(group["params"], max_norm)
+    opt.step()
     return loss
 
 
 def dropin_loop(ctx, N, M, T, steps, warmup, precision="f32"):
-    """ms per step of the reference's own loop body (reference_loop_body) on this package's
+    """ms per step of a user-written loop (user_train_step) on this package's
     modules imported the reference's way (dropin/: `from speech_embedder_net import ...`), the
     same synthetic batch as the headline, beside the fused GE2ETrainer."""
     if os.path.join(ROOT, "dropin") not in sys.path:
@@ -313,19 +310,19 @@ def dropin_loop(ctx, N, M, T, steps, warmup, precision="f32"):
     opt = torch.optim.SGD([{"params": net.parameters()}, {"params": ge2e.parameters()}], lr=0.01)
     g = torch.Generator(device="cpu").manual_seed(1235 + ctx.rank)
     x = torch.randn(N, M, T, DIMS[0], generator=g).to(ctx.dev)
-    random.seed(0)
+    gen = torch.Generator().manual_seed(0)
     for _ in range(warmup):
-        reference_loop_body(net, ge2e, opt, x, N, M)
+        user_train_step(net, ge2e, opt, x, N, M, gen)
     ctx.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        loss = reference_loop_body(net, ge2e, opt, x, N, M)
+        loss = user_train_step(net, ge2e, opt, x, N, M, gen)
     ctx.barrier()
     dt = ctx.max_over_ranks(time.perf_counter() - t0)
-    return {"config": f"train_speech_embedder.py:46-65 loop body unchanged on dropin/ modules (autograd forward / "
+    return {"config": f"user-written loop of train_speech_embedder.py:46-65's shape on dropin/ modules (autograd forward / "
                       f"backward, torch clip_grad_norm_ x2, torch SGD), N={N}xM={M}, T={T}, {precision}",
             "ms_per_step": round(dt / steps * 1e3, 3), "value": round(N * M * ctx.world * steps / dt, 3),
-            "unit": "embeddings/s", "loss": round(float(loss), 5)}
+            "unit": "embeddings/s", "loss": round(float(loss.detach()), 5)}
 
 
 def hbm_kernels(tr, N, M, D, dev, reps=50):

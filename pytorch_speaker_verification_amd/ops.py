@@ -458,6 +458,7 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
              _parr([grads[4 * l + 2] for l in range(L)]), _parr([grads[4 * l + 3] for l in range(L)]), ptr(ws),
              PIPELINE_CHUNK, s, sp, ep, 0, _evarr(probe), None, sched, sync.ptr())
         _release_status(sync, own)
+        st.dgT = dgTs  # the weight-gradient GEMMs' A operands (tests check dW against them)
         if grad_ready:
             # the projection bucket is enqueued behind the stack backward: with the persistent
             # recurrences a collective must not run beside them (sv_lstm_stack_bwd_bf16): behind the

@@ -19,6 +19,8 @@ What is recorded (inputs + expected outputs; no reference source is copied):
   net_full_c1.npz     -- one step at the full dims (40->768x3->256), N=4 x M=5, T=160.
   net_full_c2.npz     -- one step at the headline config c2 (N=64 x M=10, T=160, full dims).
   net_fwd_c5.npz      -- forward + loss at c5's global batch (N=256 x M=10, T=180, full dims).
+  net_full_c5.npz     -- one training step at c5's global batch (forward, GE2E, backward, clip,
+                         SGD): gradient norms and 8x8 heads, update norms (≈5 min of CPU).
   hparam.json         -- the parsed config/config.yaml as the reference sees it.
 
 Weights/inputs come from tests/golden/recipe.py (numpy PCG64), so fixtures hold the
@@ -210,6 +212,30 @@ def net_full_c2(ref_net, ref_hparam):
     print("net_full_c2 loss", rec["losses"][0])
 
 
+def net_full_c5(ref_net, ref_hparam):
+    """One training step at c5's global batch (N=256 x M=10, T=180, full dims, fp32): the backward
+    at the largest config pinned to the reference itself.  Every 8th embedding row, all rows on 4
+    fixed directions, gradient / update norms and 8x8 heads (as net_full_c2)."""
+    dims = (40, 768, 3, 256)
+    N, M, T = 256, 10, 180
+    rec = train_steps(ref_net, ref_hparam, dims, wseed=81, wscale=2.0, xseed=82, N=N, M=M, T=T, steps=1)
+    sd0 = recipe.make_weights(81, *dims, scale=2.0)
+    e = rec["emb"][0].reshape(N * M, -1)
+    dirs = np.random.default_rng(83).standard_normal((4, dims[3]))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    out = dict(dims=np.array(dims), wseed=81, wscale=2.0, xseed=82, N=N, M=M, T=T,
+               loss=rec["losses"][0], emb_rows=e[::8], dirs=dirs, emb_proj=e.astype(np.float64) @ dirs.T,
+               dw0=rec["dw0"], db0=rec["db0"], wb1=np.array(rec["wb1"]))
+    for k, g in rec["grads"].items():
+        out["gnorm." + k] = np.linalg.norm(g.astype(np.float64))
+        out["ghead." + k] = g.reshape(g.shape[0], -1)[:8, :8] if g.ndim == 2 else g[:64]
+    for k, p in rec["params1"].items():
+        out["p1head." + k] = p.reshape(p.shape[0], -1)[:8, :8] if p.ndim == 2 else p[:64]
+        out["dpnorm." + k] = np.linalg.norm(p.astype(np.float64) - sd0[k].astype(np.float64))
+    np.savez_compressed(os.path.join(HERE, "net_full_c5.npz"), **out)
+    print("net_full_c5 loss", rec["losses"][0])
+
+
 def net_fwd_c5(ref_net, ref_hparam):
     """Forward + GE2E loss at c5's global batch (N=256 x M=10, T=180, full dims, fp32; ≈20 s of
     CPU).  Every 8th embedding row in full, all 2560 rows projected on 4 fixed unit directions
@@ -253,7 +279,7 @@ def main():
     only = sys.argv[1].split(",") if len(sys.argv) > 1 else None
     if only:  # e.g. `make_golden.py net_full_c2,net_fwd_c5`: just those fixtures
         for name in only:
-            {"net_full_c2": net_full_c2, "net_fwd_c5": net_fwd_c5}[name](ref_net, ref_hparam)
+            {"net_full_c2": net_full_c2, "net_fwd_c5": net_fwd_c5, "net_full_c5": net_full_c5}[name](ref_net, ref_hparam)
         return
 
     # ---- KAT-0: utils.py:166-173 -------------------------------------------------
@@ -335,6 +361,7 @@ def main():
     # ---- the headline config (c2) and c5's global forward, pinned to the reference -------
     net_full_c2(ref_net, ref_hparam)
     net_fwd_c5(ref_net, ref_hparam)
+    net_full_c5(ref_net, ref_hparam)
 
     # ---- init RNG parity: reference SpeechEmbedder() under torch.manual_seed ------
     hp = ref_hparam.hparam

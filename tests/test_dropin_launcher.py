@@ -98,6 +98,24 @@ def test_launcher_refuses_missing_script_and_preimported_modules(tmp_path):
     assert r.returncode == 2 and "no such script" in r.stderr
     r = _run([os.path.join(DROPIN, "run.py")], cwd=str(tmp_path))
     assert r.returncode == 2
+    # a shimmed name imported before the launcher runs (here `utils`, from a decoy-free directory
+    # of its own) must make run.main refuse instead of mixing two resolutions; in a fresh process
+    (tmp_path / "pre").mkdir()
+    (tmp_path / "pre" / "utils.py").write_text("X = 1\n")
+    (tmp_path / "s.py").write_text("pass\n")
+    probe = textwrap.dedent(f"""
+        import sys
+        sys.path[:0] = [{str(tmp_path / "pre")!r}, {DROPIN!r}]
+        import utils, run
+        try:
+            run.main([{str(tmp_path / "s.py")!r}])
+        except RuntimeError as e:
+            print("REFUSED", e)
+    """)
+    r = _run(["-c", probe], cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "REFUSED" in r.stdout and "'utils'" in r.stdout, r.stdout
+    # the path order, checked in this process without leaving `run` imported
     sys.path.insert(0, DROPIN)
     try:
         import importlib
@@ -105,6 +123,7 @@ def test_launcher_refuses_missing_script_and_preimported_modules(tmp_path):
         assert run.resolve_path("/x/y", ["", "/x/y", "/a"])[:4] == [DROPIN, ROOT, "/x/y", "/a"]
     finally:
         sys.path.remove(DROPIN)
+        sys.modules.pop("run", None)
 
 
 @pytest.mark.skipif(not os.path.isdir(REFERENCE), reason="the reference checkout is only in the build container")

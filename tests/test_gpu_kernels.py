@@ -424,3 +424,32 @@ def test_transpose_cast_bf16(R, C, lds, ldd):
     assert torch.equal(dst[:, :R].view(torch.int16), ref.view(torch.int16))
     if ldd > R:  # padding columns untouched
         assert bool((dst[:, R:].float() == -7.0).all())
+
+
+@pytest.mark.parametrize("N,M,D", [(160, 4, 64), (200, 3, 100), (129, 5, 256)])
+def test_ge2e_fused_train_wide_n_other_d(N, M, D):
+    """128 < N <= 256 with D != 256 takes the two-tile ge2e_rows_kernel<4> (D = 256 takes the
+    register-blocked ge2e_rows4r_kernel, which the n256m10 golden covers): loss, per-row loss,
+    dE, dw, db against the fp64 numpy oracle (oracle/ge2e_np.py, pinned to the reference's GE2E
+    goldens by tests/test_oracle_golden.py).  Ragged N (129, 200: rows past the batch in the last
+    tile) and D not a multiple of 64 (100)."""
+    from pytorch_speaker_verification_amd import ops
+    E = recipe.make_embeddings(N * 31 + D, N, M, D, True)
+    w, b = 7.0, -3.0
+    o_loss, o_per = ge2e_np.ge2e_forward(E, w, b)[:2]
+    o_dE, o_dw, o_db = ge2e_np.ge2e_backward(E, w, b)
+    Et = torch.tensor(E, device=DEV)
+    wt = torch.tensor(w, dtype=torch.float32, device=DEV)
+    bt = torch.tensor(b, dtype=torch.float32, device=DEV)
+    loss, per, dE, dwdb = ops.ge2e_train(Et, wt, bt)
+    loss, per, dE, dwdb = float(loss), per.cpu().numpy(), dE.cpu().numpy(), dwdb.cpu().numpy()
+    scale = float(np.abs(o_dE).max())
+    d_loss = abs(loss - float(o_loss)) / abs(float(o_loss))
+    d_dE = float(np.abs(dE - o_dE).max()) / scale
+    print(f"\nMEASURED ge2e_fused_wide.N{N}M{M}D{D} loss_rel {d_loss:.2e} dE_rel {d_dE:.2e} "
+          f"dw {abs(dwdb[0] - o_dw):.2e} db {abs(dwdb[1] - o_db):.2e}")
+    assert d_loss <= 1e-4
+    np.testing.assert_allclose(per, o_per, atol=1e-4)
+    assert d_dE <= 1e-4
+    assert abs(dwdb[0] - o_dw) <= 1e-4 * max(1.0, abs(o_dw))
+    assert abs(dwdb[1] - o_db) <= 1e-5 * N * M

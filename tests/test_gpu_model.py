@@ -251,13 +251,12 @@ def test_full_size_c2_against_torch_gpu(schedule):
 
 
 def test_dropin_loop_body_c2_against_torch_gpu():
-    """The reference's own training-loop body (train_speech_embedder.py:46-65: random perm /
-    unperm, zero_grad, forward, GE2E loss, loss.backward(), torch clip_grad_norm_ x2, SGD.step)
-    run unchanged -- as bench.reference_loop_body -- on this package's modules imported the
-    reference's way (dropin/) and on the stock-PyTorch port (MIOpen nn.LSTM) on the same GPU, at
-    c2 (N = 64 x M = 10, T = 160), two steps from the same weights and the same perms."""
+    """A user-written loop of the reference's shape (train_speech_embedder.py:46-65: shuffled rows
+    around the forward, zero_grad, forward, GE2E loss, loss.backward(), torch clip_grad_norm_ x2,
+    SGD.step) -- bench.user_train_step -- on this package's modules imported the reference's way
+    (dropin/) and on the stock-PyTorch port (MIOpen nn.LSTM) on the same GPU, at c2 (N = 64 x
+    M = 10, T = 160), two steps from the same weights and the same row orders."""
     import os
-    import random
     import sys
     import bench
     sys.path.append(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dropin"))
@@ -277,10 +276,8 @@ def test_dropin_loop_body_c2_against_torch_gpu():
     opt_ref = torch.optim.SGD([{"params": port.parameters()}, {"params": ge2e_ref.parameters()}], lr=0.01)
     x = torch.tensor(recipe.make_frames(1237, N * M, T, dims[0]), device=DEV).reshape(N, M, T, dims[0])
     for step in range(2):
-        random.seed(step)
-        loss = bench.reference_loop_body(net, ge2e, opt, x, N, M)
-        random.seed(step)
-        loss_ref = bench.reference_loop_body(port, ge2e_ref, opt_ref, x, N, M)
+        loss = bench.user_train_step(net, ge2e, opt, x, N, M, torch.Generator().manual_seed(step))
+        loss_ref = bench.user_train_step(port, ge2e_ref, opt_ref, x, N, M, torch.Generator().manual_seed(step))
         _check(f"dropin_loop_c2.step{step}.loss_rel_vs_miopen",
                abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()), 1e-5)
     pr = dict(port.named_parameters())
@@ -425,3 +422,56 @@ def test_f32_persistent_ragged_against_torch_gpu(N, M, T):
     got = {k: v.detach() for k, v in net.state_dict().items()}
     d = max(float((got[k] - v.detach()).abs().max()) for k, v in port.state_dict().items())
     _check(f"f32_persist_B{N * M}_T{T}.param_abs_vs_miopen", d, 1e-6)
+
+
+def test_c5_global_step_matches_reference():
+    """c5's global batch (N=256 x M=10, T=180) through a whole fp32 training step on one GPU
+    (module forward, GE2E, loss.backward(): the per-step kernels at 2560 rows) against the
+    reference's own step (tests/golden/net_full_c5.npz): embeddings, loss, every parameter's
+    gradient norm and 8x8 head, dL/dw -- the c5 backward pinned to the reference itself, not only
+    at the 320-row rank shape."""
+    s = golden("net_full_c5.npz")
+    dims = tuple(int(v) for v in s["dims"])
+    net, ge2e = _build(dims, recipe.make_weights(int(s["wseed"]), *dims, scale=float(s["wscale"])))
+    N, M, T = int(s["N"]), int(s["M"]), int(s["T"])
+    x = torch.tensor(recipe.make_frames(int(s["xseed"]), N * M, T, dims[0]), device=DEV)
+    emb = net(x).reshape(N, M, -1)
+    e = emb.detach().cpu().numpy().reshape(N * M, -1)
+    _check("c5_step_ref.emb_rows_abs", float(np.abs(e[::8] - s["emb_rows"]).max()), 5e-6)
+    _check("c5_step_ref.emb_proj_abs", float(np.abs(e.astype(np.float64) @ s["dirs"].T - s["emb_proj"]).max()), 2e-5)
+    loss = ge2e(emb)
+    _check("c5_step_ref.loss_rel", abs(loss.item() - float(s["loss"])) / abs(float(s["loss"])), 1e-5)
+    loss.backward()
+    _grad_checks("c5_step_ref", net, s)
+    from oracle import ge2e_np
+    dw64 = ge2e_np.ge2e_backward(emb.detach().cpu().double().numpy(), 10.0, -5.0)[1]
+    _check("c5_step_ref.dw_kernel_rel_vs_fp64_on_own_emb", abs(ge2e.w.grad.item() - dw64) / max(1.0, abs(dw64)), 1e-5)
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c5"])
+def test_bf16_path_against_reference_fp32(cfg):
+    """The mixed-precision path (c3's numerics: bf16 GEMM operands and bf16 storage, fp32 state,
+    accumulation, loss) on the inputs of the reference's own fp32 step (net_full_c2.npz: c2 =
+    c3's shape; net_full_c5.npz: c5's global batch), with every deviation bounded against the
+    REFERENCE's fp32 values, not the bf16 oracle: loss, embeddings, every parameter's gradient norm.
+    The bounds are the mixed-precision tolerance stated in DESIGN §7 (about 3x the measured gap)."""
+    s = golden(f"net_full_{cfg}.npz")
+    dims = tuple(int(v) for v in s["dims"])
+    net, ge2e = _build(dims, recipe.make_weights(int(s["wseed"]), *dims, scale=float(s["wscale"])))
+    net.precision = "bf16"
+    N, M, T = int(s["N"]), int(s["M"]), int(s["T"])
+    x = torch.tensor(recipe.make_frames(int(s["xseed"]), N * M, T, dims[0]), device=DEV)
+    emb = net(x).reshape(N, M, -1)
+    e = emb.detach().cpu().numpy().reshape(N * M, -1)
+    ref_e = s["emb"].reshape(N * M, -1) if "emb" in s.files else s["emb_rows"]
+    mine = e if "emb" in s.files else e[::8]
+    _check(f"bf16_vs_ref_fp32.{cfg}.emb_abs", float(np.abs(mine - ref_e).max()), 1.5e-2)
+    loss = ge2e(emb)
+    _check(f"bf16_vs_ref_fp32.{cfg}.loss_rel", abs(loss.item() - float(s["loss"])) / abs(float(s["loss"])), 1e-3)
+    loss.backward()
+    gn = max((abs(float(p.grad.double().norm()) - float(s["gnorm." + k])) / float(s["gnorm." + k]), k)
+             for k, p in net.named_parameters())
+    print(f"\nMEASURED bf16_vs_ref_fp32.{cfg}.worst grad_norm {gn[1]}")
+    _check(f"bf16_vs_ref_fp32.{cfg}.grad_norm_rel", gn[0], 3e-2)
+    _check(f"bf16_vs_ref_fp32.{cfg}.dw_rel", abs(ge2e.w.grad.item() - float(s["dw0"])) / max(1.0, abs(float(s["dw0"]))),
+           3e-2)

@@ -46,11 +46,11 @@ def test_persistent_bwd_bf16_equals_per_step(dims, N, M, T):
     np.testing.assert_array_equal(b["loss"], a["loss"])
     grads = [k for k in a if k.startswith("grad_")]
     assert len(grads) == 4 * dims[2] + 2
-    # where the dx GEMM over all T (T * B / 256 * H / 256 tiles) exceeds one round of the 256 CUs it
-    # runs in the persistent + stream-K form (gemm_bf16_8qsk_kernel), whose stream-K tiles sum K in
-    # pieces: the layers below the top then differ from the per-step schedule's chunked GEMMs by
-    # fp32 summation order, amplified by their bf16 roundings (bf16-level agreement, as against the
-    # oracle); the top layer, the projection and the loss stay bit-identical
+    # where the dx GEMM over all T (T * B / 256 * H / 256 tiles) exceeds one round of the 256 CUs,
+    # the persistent schedule runs it as one whole-T GEMM while the per-step schedule runs it in
+    # time chunks: the layers below the top then see dx summed in another fp32 order (measured
+    # 2.3e-7 relative, r05_v10); the top layer, the projection and the loss stay bit-identical.  The
+    # bound is ~40x that: a dropped or double-counted k-piece moves a gradient by O(1e-2)
     H = dims[1]
     sk = H == 768 and (T * N * M) % 256 == 0 and (T * N * M // 256) * (H // 256) > 256
     top = f"_l{dims[2] - 1}"
@@ -59,7 +59,7 @@ def test_persistent_bwd_bf16_equals_per_step(dims, N, M, T):
         if sk and top not in k and "projection" not in k:
             dev = float(np.abs(b[k] - a[k]).max()) / max(float(np.abs(a[k]).max()), 1e-30)
             worst = max(worst, dev)
-            assert dev <= 2e-2, (k, dev)
+            assert dev <= 1e-5, (k, dev)
         elif ".bias_" in k:
             np.testing.assert_allclose(b[k], a[k], rtol=1e-5, atol=1e-6 * np.abs(a[k]).max(), err_msg=k)
         else:
@@ -72,10 +72,9 @@ def test_persistent_bwd_bf16_equals_per_step(dims, N, M, T):
 @pytest.mark.parametrize("N,M,T", [(32, 10, 9),    # c5's per-rank 320 rows: 20 x 12 workgroups
                                    (33, 9, 7)])    # 297 rows: a partial last 16-row block
 def test_persistent_bwd_bf16_16row_tile_against_per_step(N, M, T):
-    """257..336 rows (c5's rank shape) through the persistent backward: the 32 x 32 tile, or in an
-    A/B build with SV_PBWD16 the 16-row wide tile (lstm_persist16_bwd_bf16_kernel,
-    v_mfma_f32_16x16x32_bf16, dG handed off in the 32-row fragment order the dx GEMM reads: another
-    MFMA shape, so bf16-level agreement -- measured 2.2e-7).  The oracle test of this shape is
+    """257..336 rows (c5's rank shape) through the persistent backward (the 32 x 32 tile) against
+    the per-step schedule: the same products, the dx GEMM's K summed in another order (measured
+    2.2e-7).  The oracle test of this shape is
     test_gpu_precision.py::test_c5_rank_shape_bf16_against_oracle; the loss is bit-identical."""
     dims = (40, 768, 3, 256)
     a = _run("step", "per_step", dims, N, M, T)
@@ -88,7 +87,7 @@ def test_persistent_bwd_bf16_16row_tile_against_per_step(N, M, T):
             continue
         dev = float(np.abs(b[k] - a[k]).max()) / max(float(np.abs(a[k]).max()), 1e-30)
         worst = max(worst, dev)
-        assert dev <= 2e-2, (k, dev)
+        assert dev <= 1e-5, (k, dev)   # measured 2.2e-7 (r05_v10)
     print(f"\nMEASURED persist_c5rows_vs_per_step_bf16.B{N * M}.grad_rel {worst:.2e}")
     np.testing.assert_allclose(b["flat_p"], a["flat_p"], rtol=0, atol=2e-6)
 
@@ -213,3 +212,53 @@ def test_graph_replayed_persistent_forward_state_bit_exact(precision, B):
             assert torch.equal(st.gates[l], rst.gates[l]), (rep, l, "gates")
             assert torch.equal(st.c_tm[l], rst.c_tm[l]), (rep, l, "c_tm")
         assert torch.equal(st.h_last, rst.h_last), (rep, "h_last")
+
+
+@pytest.mark.parametrize("N,M,T", [(8, 10, 160),   # c4's per-rank shape: whole-K tiles + first pieces (split form)
+                                   (8, 10, 40)])
+def test_wavefront_weight_gradients_against_fp64_of_same_operands(N, M, T):
+    """The layer wavefront's weight gradients (gemm_bf16_8qf_kernel: every layer's 256 x 256 tiles
+    in one launch; at the c4 rank shape the free CUs compute each tile's first k-tiles and hand the
+    fp32 partial over through a flag) against an fp64 product of the SAME bf16 operands the launch
+    reads -- dG^T (st.dgT) times the time-shifted h^T / x^T -- bounded at fp32 level per element
+    (1e-5 of the sum of |products|): a stale partial from the previous step, a lost flag, or a wrong
+    first-piece / whole-K k split moves an element by O(1) of that bound.  Two consecutive backward
+    calls on different inputs, so a partial left over from the first would show in the second."""
+    import torch
+    import recipe
+    from conftest import model_dims
+    from pytorch_speaker_verification_amd import ops
+    from pytorch_speaker_verification_amd._lib import lib
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    dev = torch.device("cuda", 0)
+    dims = (40, 768, 3, 256)
+    B, H, F = N * M, dims[1], dims[0]
+    assert lib().sv_wave_ok(3, T, B, F, H)
+    sd = recipe.make_weights(77, *dims, scale=3.0)
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    net = net.to(dev)
+    layers = net.LSTM_stack.layer_params()
+    wp, bp = net.projection.weight, net.projection.bias
+    Bp = (B + 7) // 8 * 8
+    worst = 0.0
+    for rep in range(2):
+        x = torch.as_tensor(recipe.make_frames(500 + rep, B, T, F)).to(dev)
+        demb = torch.as_tensor(np.random.default_rng(600 + rep).standard_normal((B, dims[3])).astype(np.float32)).to(dev)
+        emb, st = ops.embedder_forward_bf16(x, layers, wp, bp, save=True)
+        grads = ops.embedder_backward_bf16(st, demb, layers, wp)
+        torch.cuda.synchronize()
+        for l in range(3):
+            A = st.dgT[l].double()                                   # [4H, T Bp]
+            hprev = st.hT[l][:, :T * Bp].double()                    # column block t = h_{t-1}
+            xin = (st.xT0 if l == 0 else st.hT[l - 1][:, Bp:(T + 1) * Bp]).double()
+            for name, Bop, got in (("w_hh", hprev, grads[4 * l + 1]), ("w_ih", xin, grads[4 * l])):
+                ref = A @ Bop.T
+                bound = A.abs() @ Bop.abs().T
+                err = ((got.double() - ref).abs() / (bound + 1e-30)).max().item()
+                worst = max(worst, err)
+                assert err <= 1e-5, (rep, l, name, err)
+    print(f"\nMEASURED wave_dw_vs_fp64_same_operands.T{T} {worst:.2e} (of sum |products|)")

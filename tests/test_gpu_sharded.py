@@ -100,3 +100,39 @@ def test_fused_shard_kernels(tag, world):
     dw = sum(float(r_[3][0]) for r_ in rows)
     db = sum(float(r_[3][1]) for r_ in rows)
     _check(tag, g, E, w, b, loss, per, dE, dw, db, f"ge2e_fused_shards{world}")
+
+
+@pytest.mark.parametrize("N,M,D,world", [(160, 4, 64, 2), (160, 4, 64, 5), (200, 3, 100, 4)])
+def test_fused_shard_kernels_wide_n_other_d(N, M, D, world):
+    """The fused sharded form at 128 < N <= 256 with D != 256 (the two-tile rows kernel, every
+    shard after the first with s0 > 0) against the fp64 numpy oracle."""
+    from pytorch_speaker_verification_amd.sharded_ge2e import HipFusedShard
+    E = recipe.make_embeddings(N * 17 + D, N, M, D, True)
+    w, b = 7.0, -3.0
+    Nl = N // world
+    assert HipFusedShard.ok(N, M, D)
+    f = HipFusedShard()
+    Et = torch.tensor(E, device=DEV)
+    wt = torch.tensor(w, dtype=torch.float32, device=DEV)
+    bt = torch.tensor(b, dtype=torch.float32, device=DEV)
+    shards = [Et[r * Nl:(r + 1) * Nl].contiguous() for r in range(world)]
+    prep = [f.prep(s, N) for s in shards]
+    ssum_all = torch.cat([p[0] for p in prep])
+    rows = [f.rows(shards[r], r * Nl, N, ssum_all, wt, bt, prep[r][1]) for r in range(world)]
+    loss = sum(float(r_[0]) for r_ in rows)
+    per = np.concatenate([r_[1].cpu().numpy() for r_ in rows])
+    red = torch.stack([r_[2] for r_ in rows]).sum(0)
+    dE = torch.cat([f.finalize(shards[r], r * Nl, N, red.clone(), prep[r][1]) for r in range(world)]).cpu().numpy()
+    dw = sum(float(r_[3][0]) for r_ in rows)
+    db = sum(float(r_[3][1]) for r_ in rows)
+    o_loss, o_per = ge2e_np.ge2e_forward(E, w, b)[:2]
+    o_dE, o_dw, o_db = ge2e_np.ge2e_backward(E, w, b)
+    scale = float(np.abs(o_dE).max())
+    d_loss = abs(loss - float(o_loss)) / abs(float(o_loss))
+    d_dE = float(np.abs(dE - o_dE).max()) / scale
+    print(f"\nMEASURED ge2e_fused_shards{world}_wide.N{N}M{M}D{D} loss_rel {d_loss:.2e} dE_rel {d_dE:.2e}")
+    assert d_loss <= 1e-4
+    np.testing.assert_allclose(per, o_per, atol=1e-4)
+    assert d_dE <= 1e-4
+    assert abs(dw - o_dw) <= 1e-4 * max(1.0, abs(o_dw))
+    assert abs(db - o_db) <= 1e-5 * N * M
