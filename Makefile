@@ -32,10 +32,13 @@ $(LIB): $(OBJ)
 $(FAULT_LIB): $(FAULT_OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(FAULT_OBJ)
 
-# A/B builds (never loaded by tests or the bench): `make ab NAME=x FLAGS="-DSV_..."` compiles every
-# source with FLAGS into scripts/ab/libsv_ge2e_x.so (e.g. -DSV_F32_MF=16: the 256-tile fp32 GEMM on
-# v_mfma_f32_16x16x4_f32; -DSV_PBWD_DEBUG=32: phase stamps of the persistent backward)
-# (no default FLAGS: a baseline A/B build of another commit is `make ab NAME=base FLAGS=`)
+# A/B builds (never loaded by tests or the bench; scripts/ab/ is not sent to the GPU box unless a
+# call un-ignores it): `make ab NAME=x FLAGS="-D..."` compiles every source with FLAGS into
+# scripts/ab/libsv_ge2e_x.so.  The sources keep only the phase-stamp builds as flags
+# (-DSV_PF32_STAMP [-DSV_PF32_WAVE_STAMP], -DSV_WB_STAMP, -DSV_WAVE3_STAMP: scripts/f32_step_ab.py
+# --stamps, scripts/wave_stamps.py); a candidate kernel change is an A/B build of a patched tree
+# against `make ab NAME=base FLAGS=`, timed by scripts/gpu_ab.sh.  Variants measured slower are
+# deleted from the sources (DESIGN §4 keeps the record).
 NAME ?= ab
 FLAGS ?=
 AB_OBJ := $(patsubst build/%.o,build/ab_$(NAME)/%.o,$(OBJ))

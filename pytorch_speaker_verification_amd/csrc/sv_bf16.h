@@ -398,15 +398,6 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
                            const float* c_tm, const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT,
                            bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int xcd, unsigned* sync,
                            unsigned limit, int fault, int dbg, float* dbp);
-// the 16-row wide-tile backward (sv_persist3.hip; 257..336 rows at H = 768; grid nub x nrb).  A/B
-// builds only: at c5's 320 rows it measured equal to the 32 x 32 tile
-#ifndef SV_PBWD16
-#define SV_PBWD16 0
-#endif
-int sv_persist16_bwd_ok(int B, int H, int cus);
-int sv_persist16_bwd_launch(int nub, int nrb, hipStream_t stream, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
-                            const float* dhup, int up_full, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B,
-                            int H, unsigned* cnt, int xcd, unsigned* sync, unsigned limit, int fault, float* dbp);
 // launcher of the wide-tile persistent forward (sv_persist3.hip; no fused input projection)
 int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whh_bf, bf16_t* gates, float* c_tm,
                            float* h_tm, bf16_t* h_bf, bf16_t* hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt,
@@ -430,23 +421,11 @@ int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, cons
 // layer-wavefront backward (sv_persist3.hip / sv_persist.hip): all L = 3 layers' recurrences and
 // their upstream gradients dx in one launch, for the small per-GPU batches (B <= 80 at H = 768)
 constexpr int WB_L = 3;
-// A/B builds only (measured slower): the weight gradients beside the backward
-// wavefront (sv_bf16.hip, gemm_bf16_8qw_kernel), which needs the wavefront's dG^T stores written
-// through (sc1); SV_WAVE_DGT_SC1: those stores alone (diagnostic)
-#ifndef SV_WAVE_DW_SIDE
-#define SV_WAVE_DW_SIDE 0
-#endif
-#ifndef SV_WAVE_DGT_SC1
-#define SV_WAVE_DGT_SC1 0
-#endif
 // Row stride (elements) of the library's own W_ih^T copies (bf16 [F][4H]) that the dx GEMMs read
-// as their B operand: 4H + SV_WIHT_PAD.  At 4H = 3072 a row is 6 KB, so the 256 rows of a k-tile
+// as their B operand: 4H + 64.  At 4H = 3072 a row is 6 KB, so the 256 rows of a k-tile
 // fill all fell on one L2 channel; 64 more elements (128 B) spread them: the c3 dx GEMM 569 -> 478 us
 // isolated (scripts/gemm_ld_ab.py).  Values only move: results are bit-identical.
-#ifndef SV_WIHT_PAD
-#define SV_WIHT_PAD 64
-#endif
-inline long bf16_wiht_ld(int H) { return 4L * H + SV_WIHT_PAD; }
+inline long bf16_wiht_ld(int H) { return 4L * H + 64; }
 
 struct WaveBwdArgs {
   const bf16_t* whhT[WB_L];  // [H][4H] bf16 (W_hh^T)
@@ -463,7 +442,6 @@ struct WaveBwdArgs {
   unsigned limit;
   long lddgT;
   int T, Bp, B, H, nub, nrb, fault;
-  int dgt_sc1;  // dG^T stores written through (sc1): the weight-gradient GEMM reads them in-launch
   long ldwih;   // row stride of wihT (elements; bf16_wiht_ld)
 };
 int sv_wave_bwd_launch(const WaveBwdArgs& a, hipStream_t stream);
@@ -472,5 +450,5 @@ size_t sv_wave_bwd_scratch(int L, int T, int B, int H);
 int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, const bf16_t* const* wihT,
                      const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
                      bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
-                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, int dgt_sc1 = 0, long ldwih = 0,
+                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, long ldwih = 0,
                      int zero_next = 0);

@@ -445,49 +445,6 @@ BPlan plan_bf16(int M, int N, int K) {
   return p;
 }
 
-// stream-K scratch of the persistent + stream-K 8-phase kernel (gemm_bf16_8qsk_kernel): two partial
-// slots of 512 threads x 128 fp32 per workgroup (grid capped at G8_SK_GRID) + the tiles' counters
-constexpr int G8_SK_GRID = 256;
-constexpr size_t G8_SK_SLOT = (size_t)512 * 128 * sizeof(float);
-size_t g8_sk_bytes() { return 2 * G8_SK_GRID * G8_SK_SLOT + G8_SK_GRID * sizeof(unsigned) * 4; }
-// Measured slower and off by default (A/B builds: -DSV_G8_SK=1 / -DSV_G8_SK_DW=1):
-// the dx GEMM's persistent + stream-K form where its tiles exceed one round, and the weight-gradient
-// GEMMs' stream-K form in place of split-K slabs + reduce
-#ifndef SV_G8_SK
-#define SV_G8_SK 0
-#endif
-#ifndef SV_G8_SK_DW
-#define SV_G8_SK_DW 0
-#endif
-#if SV_G8_SK_DW
-// the split-K shapes of plan_bf16 (K = T B weight gradients, fewer tiles than CUs) as ONE stream-K
-// launch: every CU gets an equal run of k-tiles (tile-major), a tile's pieces are summed by its last
-// arriving piece -- no slab buffer, no reduce launch, no idle CUs in a last round (the split-K plan
-// of 7 slabs ran 2 rounds of 252 + 252 workgroups at c3 / c4, then a reduce over 7 slabs)
-template <bool DUAL>
-int launch_g8sk(int M, int N, int K, const bf16_t* A, long lda, const bf16_t* B, long ldb, float* C, long ldc,
-                G256Dual dual, float* C2, long ldc2, void* ws, hipStream_t stream) {
-  const int tiles = (M / G256_BM) * (N / G256_BM), nk = K / G256_BK;
-  const int G = std::min(sv_stream_cus(stream), G8_SK_GRID);
-  if (G <= 0) return -1;
-  G8SK sk;
-  sk.R = tiles / G;
-  sk.rem = tiles % G;
-  sk.L = sk.rem ? (int)(((long)sk.rem * nk + G - 1) / G) : 0;
-  if (sk.rem && (long)sk.L * (G8_SK_MAXSEG - 1) < nk) return -1;  // too many pieces per tile
-  sk.part = static_cast<float*>(ws);
-  sk.cnt = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + 2 * G8_SK_GRID * G8_SK_SLOT);
-  if (sk.rem) {
-    hipError_t e = (hipError_t)sv_zero_counters(sk.cnt, 1, 0, sk.rem, stream);
-    if (e != hipSuccess) return (int)e;
-  }
-  hipLaunchKernelGGL((gemm_bf16_8qsk_kernel<0, DUAL>), dim3(G), dim3(512), G256_LDS, stream, A, lda, B, ldb, C, ldc, M,
-                     N, K, sk, G256AFrag{}, dual, C2, ldc2);
-  SV_LAUNCH_CHECK();
-  return SV_OK;
-}
-#endif
-
 template <int BM, int BN, int EPI>
 void launch_bf(const bf16_t* A, long lda, const bf16_t* B, long ldb, void* C, long ldc, long slab, int M, int N, int K,
                int splitk, int kchunk, const float* b0, const float* b1, float beta, hipStream_t s) {
@@ -532,124 +489,6 @@ void launch_bwd_bf16(dim3 grid, hipStream_t s, const bf16_t* dgn, const bf16_t* 
                      dg, dcfo, dgT, lddgT, t, Bp, B, H);
 }
 
-// ---- the layer wavefront's weight gradients beside it (c4 rank) ----
-// The backward wavefront (every layer's recurrence in one launch, sv_persist3.hip) holds 216 of
-// the 256 CUs for ~0.9 ms at the c4 rank shape; its dW GEMMs (dual dW_hh | dW_ih per upper layer,
-// layer 0's dW_hh: K = T Bp split into S slabs of kchunk) used to run after it.  Here the same
-// (layer, slab, 256 x 256 tile) items -- the split-K plan and 8-phase tile body of
-// sv_gemm_bf16_dual / sv_gemm_bf16, so every slab partial is bit-identical -- are pulled from a
-// queue by two launches of one kernel: WAIT = 1 on the CUs the wavefront leaves free, beside it,
-// polling the wavefront's arrival counters until the slab's time steps are final (dG^T_t is
-// stored, sc1, after iteration t's arrival and covered by iteration t - 1's: counter >= nub (T -
-// t_lo + 1) on every row block); WAIT = 0 on every CU once the wavefront is done, for what is
-// left.  Items go in readiness order: slabs from the last time steps down, in each the top layer
-// first (it runs ahead); queue 0 holds the items a counter can prove ready, queue 1 the rest
-// (layer 0's first slab: its dG^T_0 is final only when the launch ends).
-struct G8QLayer {
-  const bf16_t* A;    // dG^T [4H][T Bp]
-  const bf16_t* B;    // h^T (time-shifted), B rows = units
-  const bf16_t* B2;   // x^T (dual: columns past n1), or null
-  const unsigned* cnt;
-  float* ws;          // split-K slabs [S][M][N]
-  long lda, ldb, ldb2;
-  int N, n1, tiles;
-};
-struct G8Queue {
-  G8QLayer lay[WB_L];
-  unsigned* heads;  // [0]: queue 0, [SV_PCNT_STRIDE]: queue 1
-  unsigned* status;
-  unsigned limit;
-  int M, K, kchunk, S, P, nA, n1q;  // P: items per slab (all layers); nA / n1q: items in queue 0 / 1
-  int Bp, T, nub, nrb;
-};
-#ifndef SV_WAVE_DW_NT  // cache-policy bits added to the side launch's fills (2: non-temporal)
-#define SV_WAVE_DW_NT 0
-#endif
-#ifndef SV_WAVE_DW_QUEUE  // A/B: the wavefront's weight gradients as one queue-driven launch after it (r05:
-#define SV_WAVE_DW_QUEUE 0   // 319 us against 310 for the three per-layer launches)
-#endif
-#ifndef SV_WAVE_DW_SLEEP  // s_sleep argument between the side launch's polls (64 cycles each)
-#define SV_WAVE_DW_SLEEP 64
-#endif
-#ifndef SV_WAVE_DW_GRID  // most workgroups of the side launch
-#define SV_WAVE_DW_GRID 40
-#endif
-template <int WAIT>
-__global__ __launch_bounds__(512, 1) void gemm_bf16_8qw_kernel(const G8Queue q) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ int item;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wr = w >> 2, wc = w & 3;
-  while (true) {
-    if (tid == 0) {
-      int i = -1;
-      const unsigned v = __hip_atomic_fetch_add(q.heads, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (v < (unsigned)q.nA) {
-        i = (int)v;
-      } else if (!WAIT) {
-        const unsigned u = __hip_atomic_fetch_add(q.heads + SV_PCNT_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (u < (unsigned)q.n1q) i = q.nA + (int)u;
-      }
-      item = i;
-    }
-    __syncthreads();
-    const int i = item;
-    if (i < 0) break;
-    int l, s, tile;
-    if (i < q.nA) {  // slab S-1-i/P; in it the top layer's tiles first
-      const int sb = i / q.P, r = i - sb * q.P;
-      s = q.S - 1 - sb;
-      l = r < q.lay[2].tiles ? 2 : r < q.lay[2].tiles + q.lay[1].tiles ? 1 : 0;
-      tile = l == 2 ? r : l == 1 ? r - q.lay[2].tiles : r - q.lay[2].tiles - q.lay[1].tiles;
-    } else {
-      l = 0, s = 0, tile = i - q.nA;
-    }
-    // (field-wise selects: a dynamic index into the kernel-argument struct would copy it to scratch)
-    const G8QLayer& L2 = q.lay[2];
-    const G8QLayer& L1 = q.lay[1];
-    const G8QLayer& L0 = q.lay[0];
-    const bf16_t* A = l == 2 ? L2.A : l == 1 ? L1.A : L0.A;
-    const bf16_t* Bm = l == 2 ? L2.B : l == 1 ? L1.B : L0.B;
-    const bf16_t* B2 = l == 2 ? L2.B2 : l == 1 ? L1.B2 : L0.B2;
-    const unsigned* cnt = l == 2 ? L2.cnt : l == 1 ? L1.cnt : L0.cnt;
-    float* ws = l == 2 ? L2.ws : l == 1 ? L1.ws : L0.ws;
-    const long lda = l == 2 ? L2.lda : l == 1 ? L1.lda : L0.lda;
-    const long ldb = l == 2 ? L2.ldb : l == 1 ? L1.ldb : L0.ldb;
-    const long ldb2 = l == 2 ? L2.ldb2 : l == 1 ? L1.ldb2 : L0.ldb2;
-    const int N = l == 2 ? L2.N : l == 1 ? L1.N : L0.N;
-    const int n1 = l == 2 ? L2.n1 : l == 1 ? L1.n1 : L0.n1;
-    const int tiles_n = N / G256_BM;
-    const int tn = tile % tiles_n, tm = tile / tiles_n;
-    const int kbeg = s * q.kchunk;
-    const int nk = (min(q.K, kbeg + q.kchunk) - kbeg) / G256_BK;
-    if (WAIT) {
-      // a slow poll (~2 us between reads): a slab's steps finish ~0.1 ms apart, and 40 pollers at
-      // the recurrence's own rate (s_sleep 2) on the lines its arrivals and hand-off waits use slowed
-      // it by 8 % (r05)
-      if (tid == 0) {
-        const unsigned target = (unsigned)q.nub * (unsigned)(q.T - kbeg / q.Bp + 1);
-        for (int rb = 0; rb < q.nrb; ++rb) {
-          const unsigned* c = cnt + rb * SV_PCNT_STRIDE;
-          unsigned spins = 0;
-          while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (__hip_atomic_load(q.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-            __builtin_amdgcn_s_sleep(SV_WAVE_DW_SLEEP);
-            if (++spins > (q.limit >> 5)) {
-              __hip_atomic_fetch_or(q.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-          }
-        }
-      }
-      __syncthreads();
-    }
-    g8_f32x4 acc[8][4];
-    g8_tile<0, WAIT ? 16 | SV_WAVE_DW_NT : 0, WAIT ? SV_WAVE_DW_NT : 0>(A, lda, Bm, ldb, G256AFrag{},
-                                                                        G256Dual{B2, ldb2, n1}, tm, tn, kbeg, nk, smem, acc);
-    g8_epilogue<G8_SLAB>(acc, ws, N, (long)s * q.M * N, tm, tn, wr, wc, lane, nullptr, nullptr, 0.f);
-  }
-}
-
 // ---- the layer wavefront's weight gradients as whole-K tiles in one launch (c4 rank) ----
 // After the wavefront every layer's dG^T is final.  The per-layer split-K plan (c4 rank: K = T Bp =
 // 12800 in 7 slabs of 29 k-tiles; 504 workgroups per dual GEMM, two rounds) writes 129 MB of fp32
@@ -680,15 +519,6 @@ struct G8Full {
   unsigned* status;  // the sync block's status word
   unsigned limit;
 };
-#ifndef SV_WAVE_DW_FULLK
-#define SV_WAVE_DW_FULLK 1
-#endif
-#ifndef SV_WAVE_DW_SPLIT  // the split form on the CUs the whole-K tiles leave free
-#define SV_WAVE_DW_SPLIT 1
-#endif
-#ifndef SV_WAVE_DW_SOFF  // the first pieces' k-tiles below an even split (per workgroup: theirs and the tile's)
-#define SV_WAVE_DW_SOFF 2
-#endif
 __global__ __launch_bounds__(512, 1) void gemm_bf16_8qf_kernel(const G8Full q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -772,7 +602,6 @@ extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, cons
 size_t sv_gemm_bf16_dual_workspace(int M, int N1, int N2, int K) {
   const BPlan p = plan_bf16(M, N1, K);
   size_t fused = p.splitk > 1 ? (size_t)p.splitk * M * (N1 + N2) * sizeof(float) : 0;
-  if (SV_G8_SK_DW && p.splitk > 1 && p.bm == G256_BM) fused = std::max(fused, g8_sk_bytes());
   return std::max(fused, std::max(sv_gemm_bf16_workspace(M, N1, K), sv_gemm_bf16_workspace(M, N2, K)));
 }
 int sv_gemm_bf16_dual(int M, int N1, int N2, int K, const bf16_t* A, long lda, const bf16_t* B1, long ldb1, float* C1,
@@ -788,13 +617,6 @@ int sv_gemm_bf16_dual(int M, int N1, int N2, int K, const bf16_t* A, long lda, c
     return sv_gemm_bf16(M, N2, K, A, lda, B2, ldb2, C2, ldc2, nullptr, nullptr, 0.f, workspace, stream);
   }
   const int N = N1 + N2;
-#if SV_G8_SK_DW
-  if (g8_ok(C1, ldc1, nullptr, nullptr) && g8_ok(C2, ldc2, nullptr, nullptr)) {
-    const int rc = launch_g8sk<true>(M, N, K, A, lda, B1, ldb1, C1, ldc1, G256Dual{B2, ldb2, N1}, C2, ldc2, workspace,
-                                     stream);
-    if (rc >= 0) return rc;
-  }
-#endif
   const int tiles = (M / G256_BM) * (N / G256_BM);
   const long slab = (long)M * N;
   hipLaunchKernelGGL((gemm_bf16_8q_kernel<G8_SLAB, 0>), dim3(tiles, p.splitk), dim3(512), G256_LDS, stream, A, lda, B1,
@@ -886,13 +708,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_narrow_kernel(const bf16_t* __r
         *reinterpret_cast<g8_f32x4*>(Cz + (long)(m0 + 32 * w + 16 * i + lr) * N + col) = acc[i][j];
     }
 }
-#ifndef SV_GEMM_BF_NARROW  // 0: the N <= 48 bf16 GEMMs on the 64 x 64 tiles (A/B)
-#define SV_GEMM_BF_NARROW 1
-#endif
 // exact plan of the narrow kernel: N <= 48 in whole 4-column groups, whole 128-row tiles, 64-k steps,
 // K chunks of at least 1024 over up to 32 slabs (c3: 24 row tiles x 32 slabs = 768 workgroups)
 static bool narrow_bf_ok(int M, int N, int K, long lda, long ldb) {
-  return SV_GEMM_BF_NARROW && N <= GNB_BN && N % 4 == 0 && M % GNB_BM == 0 && K % GNB_BK == 0 && K >= 4096 &&
+  return N <= GNB_BN && N % 4 == 0 && M % GNB_BM == 0 && K % GNB_BK == 0 && K >= 4096 &&
          lda % 8 == 0 && ldb % 8 == 0;
 }
 static int narrow_bf_splitk(int K, int& kchunk) {
@@ -909,8 +728,7 @@ extern "C" size_t sv_gemm_bf16_workspace(int M, int N, int K) {
     nar = (size_t)narrow_bf_splitk(K, kchunk) * M * N * sizeof(float);
   }
   if (p.splitk <= 1) return nar;
-  const size_t slabs = std::max(nar, (size_t)p.splitk * M * N * sizeof(float));
-  return SV_G8_SK_DW && p.bm == G256_BM ? std::max(slabs, g8_sk_bytes()) : slabs;  // (+ stream-K scratch)
+  return std::max(nar, (size_t)p.splitk * M * N * sizeof(float));
 }
 
 extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, const bf16_t* B, long ldb, float* C,
@@ -942,12 +760,6 @@ extern "C" int sv_gemm_bf16(int M, int N, int K, const bf16_t* A, long lda, cons
       return SV_OK;
     }
     if (!workspace) return SV_EARG;
-#if SV_G8_SK_DW
-    if (beta == 0.f && !bias0 && !bias1 && g8_ok(C, ldc, nullptr, nullptr)) {
-      const int rc = launch_g8sk<false>(M, N, K, A, lda, B, ldb, C, ldc, G256Dual{}, nullptr, 0L, workspace, stream);
-      if (rc >= 0) return rc;
-    }
-#endif
     launch_g256<G256_SLAB, 0>(g8_ok(workspace, N, nullptr, nullptr), dim3(tiles, p.splitk), stream, A, lda, B,
                               ldb, workspace, (long)N, slab, M, N, K, p.kchunk, nullptr, nullptr, 0.f);
     SV_LAUNCH_CHECK();
@@ -1014,47 +826,18 @@ extern "C" int sv_gemm_bf16_bf(int M, int N, int K, const bf16_t* A, long lda, c
 
 // dx = dG . W_ih with dG read from the persistent backward's fragment-order hand-off buffer
 // (no row-major dG copy): M = T * B rows (t, b), K = 4H; needs B % 32, M % 256, N % 256, H % 64
-#ifndef SV_BF16_AFRAG  // 0: the recurrence writes row-major dG for a row-major dx GEMM (A/B builds)
-#define SV_BF16_AFRAG 1
-#endif
 bool gemm_afrag_ok(int T, int B, int N, int H) {
-  return SV_BF16_AFRAG && gemm256_ok(T * B, N, 4 * H) && B % 32 == 0 && H % G256_BK == 0 &&
+  return gemm256_ok(T * B, N, 4 * H) && B % 32 == 0 && H % G256_BK == 0 &&
          4 * H / G256_BK < 4096 && (unsigned long long)T * B * B < (1ull << 32);  // g256_af_koff / _rowoff exact
 }
-// (the split-K plan of sv_gemm_bf16 for the same shape).  More tiles than one round of CUs (the c3
-// dx: 1200 tiles): the persistent + stream-K kernel when `skws` (g8_sk_bytes) is given -- its
-// stream-K tiles sum K in pieces, so at those shapes the per-step schedule's chunked dx GEMMs
-// (one round each) no longer sum bit-identically; within the bf16 tolerance of the oracle
+// (the split-K plan of sv_gemm_bf16 for the same shape)
 int gemm_bf16_afrag(int T, int B, int H, int N, const bf16_t* dgf, int bm, const bf16_t* Bop, long ldb, float* C,
-                    long ldc, float* workspace, hipStream_t stream, void* skws = nullptr) {
+                    long ldc, float* workspace, hipStream_t stream) {
   const int M = T * B, K = 4 * H;
   const int tiles = (M / G256_BM) * (N / G256_BM);
   const long fs = (long)((B + bm - 1) / bm) * bm * 4 * H;
   const G256AFrag af = g256_afrag(dgf, fs, B, bm, H);
   const BPlan p = plan_bf16(M, N, K);
-#if SV_G8_SK
-  const int G = std::min(sv_stream_cus(stream), G8_SK_GRID), nk = K / G256_BK;
-  if (p.splitk == 1 && skws && G > 0 && tiles > G && g8_ok(C, ldc, nullptr, nullptr)) {
-    G8SK sk;
-    sk.R = tiles / G;
-    sk.rem = tiles % G;
-    sk.L = sk.rem ? (int)(((long)sk.rem * nk + G - 1) / G) : 0;
-    if (sk.rem == 0 || (long)sk.L * (G8_SK_MAXSEG - 1) >= nk) {  // <= G8_SK_MAXSEG pieces per stream-K tile
-      sk.part = static_cast<float*>(skws);
-      sk.cnt = reinterpret_cast<unsigned*>(static_cast<char*>(skws) + 2 * G8_SK_GRID * G8_SK_SLOT);
-      if (sk.rem) {
-        hipError_t e = (hipError_t)sv_zero_counters(sk.cnt, 1, 0, sk.rem, stream);
-        if (e != hipSuccess) return (int)e;
-      }
-      hipLaunchKernelGGL((gemm_bf16_8qsk_kernel<1>), dim3(G), dim3(512), G256_LDS, stream, nullptr, 0L, Bop, ldb, C,
-                         ldc, M, N, K, sk, af);
-      SV_LAUNCH_CHECK();
-      return SV_OK;
-    }
-  }
-#else
-  (void)skws;
-#endif
   if (p.splitk == 1) {
     launch_g256<G256_STORE, 1>(g8_ok(C, ldc, nullptr, nullptr), dim3(tiles, 1), stream, nullptr, 0L, Bop, ldb, C,
                                ldc, 0L, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
@@ -1388,7 +1171,7 @@ static int wbf_transposes(int L, int F, int H, const float* const* w_ih, const f
 }
 
 // the hand-off scratch shared by the layers (persistent or wavefront backward), behind the L
-// per-layer regions; then the dx GEMM's stream-K scratch (persistent schedule)
+// per-layer regions
 static size_t bbwd_scratch(int L, int T, int B, int H) {
   size_t scratch = sv_persist_bwd_fits(B, H, 1 << 30) ? sv_persist_bwd_scratch(T, B, H) : 0;
   if (sv_wave_bwd_fits(L, B, H, 1 << 30)) scratch = std::max(scratch, sv_wave_bwd_scratch(L, T, B, H));
@@ -1396,7 +1179,7 @@ static size_t bbwd_scratch(int L, int T, int B, int H) {
 }
 extern "C" size_t sv_lstm_stack_bwd_bf16_workspace(int L, int T, int B, int F, int H) {
   const size_t per = (size_t)L * carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
-  return per + bbwd_scratch(L, T, B, H) + (SV_G8_SK && sv_persist_bwd_fits(B, H, 1 << 30) ? g8_sk_bytes() : 0);
+  return per + bbwd_scratch(L, T, B, H);
 }
 
 extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const bf16_t* const* xT, const long* ld_xT,
@@ -1435,70 +1218,13 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     }
     int rc = wbf_transposes(L, F, H, w_ih, w_hh, whhT_l, wihT_l, main);
     if (rc) return rc;
-    // the weight gradients beside the wavefront on the CUs it leaves free (gemm_bf16_8qw_kernel)
     const int cus = sv_stream_cus(main);
-    const int side_grid = std::min(SV_WAVE_DW_GRID, cus - L * (H / 32) * ((B + 31) / 32));
-    const BPlan p = plan_bf16(4 * H, H, TBp);
-    bool queued = (SV_WAVE_DW_QUEUE || SV_WAVE_DW_SIDE) && L == WB_L && p.bm == G256_BM && p.splitk > 1 &&
-                  gemm256_ok(4 * H, 2 * H, TBp) && TBp % 8 == 0 && ldhT % 8 == 0;
-    G8Queue q{};
-    if (queued) {
-      for (int l = 0; l < L; ++l) {
-        const int Fl = l == 0 ? F : H;
-        const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
-        const bool dual = l > 0;  // layer 0: dW_hh only (its N = F dW_ih runs after, as before)
-        if ((dual && (Fl % G256_BM || ld_xT[l] % 8 || ((uintptr_t)xT[l] & 15))) || ((uintptr_t)dgT[l] & 15) ||
-            ((uintptr_t)hT[l] & 15) || !g8_ok(ws.gws, dual ? H + Fl : H, nullptr, nullptr))
-          queued = false;
-        G8QLayer& ql = q.lay[l];
-        ql.A = dgT[l];
-        ql.lda = TBp;
-        ql.B = hT[l];
-        ql.ldb = ldhT;
-        ql.B2 = dual ? xT[l] : nullptr;
-        ql.ldb2 = dual ? ld_xT[l] : 0;
-        ql.n1 = H;
-        ql.N = dual ? H + Fl : H;
-        ql.tiles = (4 * H / G256_BM) * (ql.N / G256_BM);
-        ql.ws = ws.gws;
-        ql.cnt = sync + SV_SYNC_CNT + (size_t)l * SV_PCNT_ROWS * SV_PCNT_STRIDE;
-      }
-    }
-    const bool beside = SV_WAVE_DW_SIDE && queued && side_grid >= 8 && side[0] && 4L * H * TBp * 2 < (1L << 32);
-    if (queued) {
-      q.heads = sync + SV_SYNC_CNT + (size_t)WB_L * SV_PCNT_ROWS * SV_PCNT_STRIDE;  // channel 3, rows 0-1
-      q.status = sync;
-      q.limit = sv_persist_limit();
-      q.M = 4 * H;
-      q.K = TBp;
-      q.kchunk = p.kchunk;
-      q.S = p.splitk;
-      q.P = q.lay[0].tiles + q.lay[1].tiles + q.lay[2].tiles;
-      q.n1q = q.lay[0].tiles;
-      q.nA = q.S * q.P - q.n1q;
-      q.Bp = Bp;
-      q.T = T;
-      q.nub = H / 32;
-      q.nrb = (B + 31) / 32;
-      // every counter the side launch reads is zero before it starts (the wavefront zeroes its own
-      // channels again right before its launch, while they still read zero)
-      if ((rc = sv_zero_counters(beside ? sync + SV_SYNC_CNT : q.heads, beside ? WB_L + 1 : 1,
-                                 (long)SV_PCNT_ROWS * SV_PCNT_STRIDE, std::max(q.nrb, 2) * SV_PCNT_STRIDE, main)))
-        return rc;
-    }
-    if (beside) {
-      if ((e = hipEventRecord(ev[0], main)) != hipSuccess) return (int)e;
-      if ((e = hipStreamWaitEvent(side[0], ev[0], 0)) != hipSuccess) return (int)e;
-      hipLaunchKernelGGL(gemm_bf16_8qw_kernel<1>, dim3(side_grid), dim3(512), G256_LDS, side[0], q);
-      SV_LAUNCH_CHECK();
-      if ((e = hipEventRecord(ev[1], side[0])) != hipSuccess) return (int)e;
-    }
     // every layer's whole-K weight-gradient tiles in one launch where they fit one round of the CUs
     // (gemm_bf16_8qf_kernel; layer 0's N = F dW_ih after it on the narrow kernel)
     G8Full f{};
     int fP = 0;
     bool fullk = false;
-    if (SV_WAVE_DW_FULLK && !queued && L == WB_L && gemm256_ok(4 * H, H, TBp) && TBp % 8 == 0 && ldhT % 8 == 0) {
+    if (L == WB_L && gemm256_ok(4 * H, H, TBp) && TBp % 8 == 0 && ldhT % 8 == 0) {
       f.K = TBp;
       fullk = true;
       for (int l = 0; l < L; ++l) {
@@ -1525,10 +1251,10 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       // the split form where at least 8 CUs are left over and the partials fit the GEMM scratch
       const BBwdWs wsp = carve_bbwd((char*)workspace + per * (L - 1), T, B, std::max(F, H), H);
       const int KT = TBp / G256_BK;
-      f.nsw = fullk && SV_WAVE_DW_SPLIT ? (cus - fP) / 8 * 8 : 0;
+      f.nsw = fullk ? (cus - fP) / 8 * 8 : 0;
       if (f.nsw > 0) {
         const int per_wg = (fP + f.nsw - 1) / f.nsw;  // first pieces per workgroup
-        f.S = KT / (per_wg + 1) - SV_WAVE_DW_SOFF;    // (their stores and prologues: a little less)
+        f.S = KT / (per_wg + 1) - 2;    // (their stores and prologues: a little less)
       }
       if (f.nsw <= 0 || f.S < 4 || (size_t)fP * G256_BM * G256_BM * 4 > wsp.gbytes) f.nsw = f.S = 0;
       if (f.S > 0) {
@@ -1540,34 +1266,8 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     }
     rc = sv_wave_bwd_bf16(L, T, B, H, whhT_l, wihT_l, gates, c_tm, dh_last, dx, dgT, (char*)workspace + per * L,
                               sync, main, db_ih, db_hh, probe ? probe[0] : nullptr, probe ? probe[1] : nullptr,
-                              beside || SV_WAVE_DGT_SC1 ? 1 : 0, bf16_wiht_ld(H), f.S > 0 ? fP : 0);
+                              bf16_wiht_ld(H), f.S > 0 ? fP : 0);
     if (rc) return rc;
-    if (queued) {
-      hipLaunchKernelGGL(gemm_bf16_8qw_kernel<0>, dim3(cus), dim3(512), G256_LDS, main, q);
-      SV_LAUNCH_CHECK();
-      if (beside && (e = hipStreamWaitEvent(main, ev[1], 0)) != hipSuccess) return (int)e;
-      const long slab0 = 4L * H * H;
-      for (int l = L - 1; l >= 0; --l) {  // the slabs' sums (sv_gemm_bf16_dual's / sv_gemm_bf16's reduce)
-        const G8QLayer& ql = q.lay[l];
-        const long slab = 4L * H * ql.N;
-        const int grid = (int)std::min<long>((slab + 255) / 256, 4096);
-        if (l > 0)
-          hipLaunchKernelGGL(slab_reduce_bf_kernel, dim3(grid), dim3(256), 0, main, ql.ws, q.S, slab, dw_hh[l], (long)H,
-                             4 * H, ql.N, 0.f, nullptr, nullptr, nullptr, dw_ih[l], (long)H, H);
-        else
-          hipLaunchKernelGGL(slab_reduce_bf_kernel, dim3((int)std::min<long>((slab0 + 255) / 256, 4096)), dim3(256), 0,
-                             main, ql.ws, q.S, slab0, dw_hh[0], (long)H, 4 * H, H, 0.f, nullptr, nullptr);
-        SV_LAUNCH_CHECK();
-        if (l == 0) {
-          const BBwdWs ws = carve_bbwd((char*)workspace, T, B, std::max(F, H), H);
-          if ((rc = sv_gemm_bf16(4 * H, F, TBp, dgT[0], TBp, xT[0], ld_xT[0], dw_ih[0], F, nullptr, nullptr, 0.f,
-                                 ws.gws, main)))
-            return rc;
-        }
-        if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
-      }
-      return SV_OK;
-    }
     if (fullk) {
       hipLaunchKernelGGL(gemm_bf16_8qf_kernel, dim3(f.nsw + fP), dim3(512), G256_LDS, main, f);
       SV_LAUNCH_CHECK();
@@ -1628,7 +1328,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
         if ((e = hipEventRecord(ev[L * nch + k], main)) != hipSuccess) return (int)e;
       if (afr) {
         if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H, sv_stream_cus(main)), ws.wihT, bf16_wiht_ld(H), dx[l],
-                                  Fl, ws.gws, main, (char*)workspace + per * L + bbwd_scratch(L, T, B, H))))
+                                  Fl, ws.gws, main)))
           return rc;
       } else if (l > 0 && (rc = sv_gemm_bf16(T * B, Fl, 4 * H, dg[l], 4L * H, ws.wihT, bf16_wiht_ld(H), dx[l], Fl, nullptr,
                                               nullptr, 0.f, ws.gws, main))) {

@@ -595,9 +595,6 @@ __global__ __launch_bounds__(256) void ge2e_prep_kernel(const float* __restrict_
 // tile 1 while it is resident, then tile 0 again -- still fp32 throughout.
 #define GF_ROWW 4
 #define GF_TILE 128
-#ifndef SV_GE2E_DIAG  // A/B diagnostics (results invalid): 1 = no G1 pass, 2 = no tile-0 restage
-#define SV_GE2E_DIAG 0
-#endif
 template <int NH>
 __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __restrict__ Chat, const float* __restrict__ Ehat,
                                                         const float* __restrict__ rawd, int Bl, int M, int N, int D,
@@ -764,10 +761,10 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
   };
   if constexpr (NH == 2) {
     if (cok) g1_acc(0, N, 0);
-  } else if (SV_GE2E_DIAG != 1) {
+  } else {
     if (cok) g1_acc(GF_TILE, N, GF_TILE);  // tile 1 is resident
     __syncthreads();
-    if (SV_GE2E_DIAG != 2) stage(0);
+    stage(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (cok) g1_acc(0, GF_TILE, 0);
@@ -775,217 +772,27 @@ __global__ __launch_bounds__(64 * GF_ROWW) void ge2e_rows_kernel(const float* __
   if (cok) *reinterpret_cast<float4*>(G1 + (long)r * D + c) = float4{g0.x + g1.x, g0.y + g1.y, g0.z + g1.z, g0.w + g1.w};
 }
 
-// F2 for 128 < N <= 256 and D = 256 (c5's global N): 4 rows per workgroup, FOUR waves per row
-// (16 waves), so each wave walks a quarter of the row's work -- the one-wave-per-row form above
-// (ge2e_rows_kernel<4>) is latency-bound at a c5 rank's 320 rows (25 us: 256 cosine dot products
-// and 256 G1 terms in one wave, plus a third tile staging).  The speakers pass through LDS in two
-// chunks of 128 (fp32, 133 KB), each staged once by LDS-DMA; per chunk the cosines, then the
-// chunk's share of
-// G1 = sum_{k != j} dcos_k C^_k accumulated online (flash-attention style: weights e^{S_k - m}
-// against the running row max m, the partial sum rescaled by e^{m_old - m} when a chunk raises it,
-// finally scaled by w e^{m - lz}).
-//   cosines: wave p of the row takes speakers 128 c + 32 p + (lane & 31), the two lane halves
-//     taking d halves, joined by one shuffle (lanes < 32 hold the speaker);
-//   row max / sums: per-wave partials met in LDS; G1: wave p takes d = 64 p + lane.
-// FUSEC (sharded form): the chunks hold the all-gathered speaker SUMS s_k; the centroid scale
-// c_k = 1 / (M max(|s_k / M|, eps)) comes from |s_k|^2 summed in the same loop as the cosine, so
-// cos = (E^ . s_k) c_k and the G1 weights carry c_k -- no normalisation pass and no centroid
-// launch; the workgroups also write C^ and |C| of the shard's own speakers for the finalize step.
-// (Measured: 64-speaker chunks double-buffered, the next chunk's DMA under the current chunk's
-// work: 27.3 us against 24.3 at the c5 rank shape -- the chunks' extra barriers cost more than the
-// staging latency they hide; a third staging of the first tile for G1 instead of the online sum:
-// 19.5 us + the centroid launch.)
-constexpr int GF_CH = 128;  // speakers per chunk
-#ifndef SV_GE2E_ROWS4R      // 8 / 16: ge2e_rows4r_kernel below on that many waves; 0: this kernel (A/B)
-#define SV_GE2E_ROWS4R 8
-#endif
-#ifndef SV_GE2E_R4ROWS      // rows per workgroup of ge2e_rows4r_kernel (2 or 4)
-#define SV_GE2E_R4ROWS 2
-#endif
-template <bool FUSEC>
-__global__ __launch_bounds__(1024) void ge2e_rows16_kernel(const float* __restrict__ Csrc,
-                                                          const float* __restrict__ Ehat,
-                                                          const float* __restrict__ rawd, int Bl, int M, int N,
-                                                          int ldc, int s0, const float* __restrict__ wp,
-                                                          const float* __restrict__ bp, float* __restrict__ per,
-                                                          float* __restrict__ cos, float* __restrict__ dcos,
-                                                          float* __restrict__ alpha, float* __restrict__ dcd,
-                                                          float* __restrict__ dwdb_rows, float* __restrict__ G1,
-                                                          float* __restrict__ Chat_out, float* __restrict__ Cn_out) {
-  constexpr int D = 256, LDC = D + 4, RW = 4, NCM = GF_NMAX / GF_CH;
-  extern __shared__ __attribute__((aligned(16))) float gsm[];
-  float* Cb = gsm;                    // [GF_CH][LDC]
-  float* Es = Cb + GF_CH * LDC;       // [RW][D]
-  float* Vs = Es + RW * D;            // [RW][GF_CH] G1 weights of the current chunk
-  float* red = Vs + RW * GF_CH;       // [RW][4 waves][4]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int i = w >> 2, pq = w & 3;   // row of the workgroup, quarter
-  const int r = blockIdx.x * RW + i;
-  const bool live = r < Bl;
-  const int nc = (N + GF_CH - 1) / GF_CH;
-  auto rows_of = [&](int c) { return min(GF_CH, N - c * GF_CH); };
-  auto stage = [&](int c) {  // chunk c -> LDS: this wave's rows w, w + 16, ...
-    const int nk = rows_of(c);
-    for (int row = w; row < nk; row += 16)
-      __builtin_amdgcn_global_load_lds(
-          (__attribute__((address_space(1))) void*)(Csrc + (long)(c * GF_CH + row) * D + lane * 4),
-          (__attribute__((address_space(3))) void*)(Cb + row * LDC), 16, 0, 0);
-  };
-  float* rr = red + (i * 4 + pq) * 4;
-  auto row_sum = [&](float v, int slot) {  // the row's 4 waves' values, added in wave order
-    if (lane == 0) rr[slot] = v;
-    __syncthreads();
-    return (red[(i * 4) * 4 + slot] + red[(i * 4 + 1) * 4 + slot]) + (red[(i * 4 + 2) * 4 + slot] + red[(i * 4 + 3) * 4 + slot]);
-  };
-  if (live) Es[i * D + pq * 64 + lane] = Ehat[(long)r * D + pq * 64 + lane];
-  const float wv = *wp, bv = *bp;
-  const int sg = s0 + (live ? r : 0) / M;
-  const float rd = live ? rawd[r] : 0.f;
-  const int kq = 32 * pq + (lane & 31), dq = (lane >> 5) * 128;
-  const bool own = lane < 32;
-  const float* e0 = Es + i * D;
-  const int d = pq * 64 + lane;  // this lane's G1 column
-  float cv[NCM];
-#pragma unroll
-  for (int c = 0; c < NCM; ++c) cv[c] = 0.f;
-  float m = 0.f, zsum = 0.f, acc0 = 0.f, acc1 = 0.f;  // running max (>= 0), sum of e^{S - m}, G1 partial
-#pragma unroll
-  for (int c = 0; c < NCM; ++c) {
-    if (c >= nc) break;
-    if (c > 0) __syncthreads();  // every wave done with the previous chunk (its G1 terms, Vs)
-    stage(c);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const float* buf = Cb;
-    const int k = c * GF_CH + kq;
-    float ck = 1.f;  // centroid scale (FUSEC)
-    {
-      float4 a = float4{0.f, 0.f, 0.f, 0.f}, q = a;
-      if (k < N) {
-#pragma unroll 8
-        for (int cc0 = dq; cc0 < dq + 128; cc0 += 4) {
-          const float4 cc = *reinterpret_cast<const float4*>(buf + kq * LDC + cc0);
-          const float4 x0 = *reinterpret_cast<const float4*>(e0 + cc0);
-          a.x += x0.x * cc.x;
-          a.y += x0.y * cc.y;
-          a.z += x0.z * cc.z;
-          a.w += x0.w * cc.w;
-          if constexpr (FUSEC) {
-            q.x += cc.x * cc.x;
-            q.y += cc.y * cc.y;
-            q.z += cc.z * cc.z;
-            q.w += cc.w * cc.w;
-          }
-        }
-      }
-      float v = (a.x + a.y) + (a.z + a.w);
-      v += __shfl_xor(v, 32, 64);
-      cv[c] = v;
-      if constexpr (FUSEC) {  // |C_k| = |s_k| / M, C^_k = s_k / (M max(|C_k|, eps))
-        float qq = (q.x + q.y) + (q.z + q.w);
-        qq += __shfl_xor(qq, 32, 64);
-        ck = 1.0f / ((float)M * fmaxf(sqrtf(qq) / (float)M, EPS_COS));
-        cv[c] *= ck;
-      }
-    }
-    if (k == sg) cv[c] = rd;  // get_cossim's diagonal overwrite (utils.py:112-113)
-    const bool valid = own && k < N;
-    const float sk = wv * (cv[c] + EPS_SIM) + bv;
-    const float tm = wave_max(valid ? sk : -INFINITY);
-    if (lane == 0) rr[0] = tm;
-    __syncthreads();
-    const float tmax = fmaxf(fmaxf(red[(i * 4) * 4], red[(i * 4 + 1) * 4]), fmaxf(red[(i * 4 + 2) * 4], red[(i * 4 + 3) * 4]));
-    const float mn = fmaxf(m, tmax);  // (m starts at 0: the row max is clamped at 0 as in ge2e_rows_kernel)
-    const float resc = expf(m - mn);
-    const float e = valid ? expf(sk - mn) : 0.f;
-    zsum = zsum * resc + row_sum(wave_sum(e), 1);
-    // the chunk's G1 weights (the diagonal excluded: its gradient goes to U, utils.py:112-113)
-    if (own) Vs[i * GF_CH + kq] = (valid && k != sg) ? e * ck : 0.f;
-    if constexpr (FUSEC) {
-      // C^ and |C| of this shard's own speakers in this chunk, for the finalize step: speaker s0 + j
-      // by workgroup j % gridDim.x, wave (j / gridDim.x) % 16
-      const int nl = Bl / M, nkc = rows_of(c);
-      for (int j = (int)blockIdx.x + (int)gridDim.x * w; j < nl; j += (int)gridDim.x * 16) {
-        const int kt = s0 + j - c * GF_CH;
-        if (kt < 0 || kt >= nkc) continue;
-        float4 v = *reinterpret_cast<const float4*>(buf + kt * LDC + 4 * lane);
-        const float cn = sqrtf(wave_sum(v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w)) / (float)M;
-        const float inv = 1.0f / ((float)M * fmaxf(cn, EPS_COS));
-        v = float4{v.x * inv, v.y * inv, v.z * inv, v.w * inv};
-        *reinterpret_cast<float4*>(Chat_out + (long)(s0 + j) * D + 4 * lane) = v;
-        if (lane == 0) Cn_out[s0 + j] = cn;
-      }
-    }
-    __syncthreads();
-    acc0 *= resc;
-    acc1 *= resc;
-    const float* vr = Vs + i * GF_CH;
-    const int nk = rows_of(c);
-    int kk = 0;
-#pragma unroll 4
-    for (; kk + 1 < nk; kk += 2) {
-      acc0 += vr[kk] * buf[kk * LDC + d];
-      acc1 += vr[kk + 1] * buf[(kk + 1) * LDC + d];
-    }
-    if (kk < nk) acc0 += vr[kk] * buf[kk * LDC + d];
-    m = mn;
-  }
-  const float lz = m + logf(zsum + EPS_LOG * expf(-m));
-  // row backward (gloss = 1): as ge2e_rows_kernel (the small differences p_k (x_k - x_d) and the
-  // analytic tail 1 - sum_k p_k = 1e-6 e^-lz)
-  const float tail = EPS_LOG * expf(-lz);
-  float pdsum = 0.f;
-#pragma unroll
-  for (int c = 0; c < NCM; ++c) {
-    const int k = c * GF_CH + kq;
-    if (c < nc && own && live && k < N) {
-      const float p = expf(wv * (cv[c] + EPS_SIM) + bv - lz);
-      const float ds = p - (k == sg ? 1.0f : 0.0f);
-      const float dcv = wv * ds;
-      pdsum += p * (cv[c] - rd);
-      const float off = (k == sg) ? 0.f : dcv;
-      cos[(long)r * ldc + k] = cv[c];
-      dcos[(long)r * ldc + k] = off;
-      if (k == sg) dcd[r] = dcv;
-    }
-  }
-  const float ps = row_sum(wave_sum(pdsum), 2);
-  if (live && pq == 0 && lane == 0) {
-    per[r] = lz - (wv * (rd + EPS_SIM) + bv);
-    alpha[r] = wv * (ps - rd * tail);
-    dwdb_rows[r] = ps - (rd + EPS_SIM) * tail;
-    dwdb_rows[Bl + r] = -tail;
-  }
-  if (live) G1[(long)r * D + d] = (acc0 + acc1) * (wv * expf(m - lz));
-}
+constexpr int GF_CH = 128;  // speakers per chunk of ge2e_rows4r_kernel
 
 // ge2e_rows4r_kernel's centroid tile stride: 288 = 32 mod 64 banks, so the two speakers of a 16-lane
 // LDS pass (8-lane groups reading 32 consecutive floats each) fall on disjoint banks
 constexpr int GF_R4LDC = 288;
-#ifndef SV_GE2E_R4GL  // lanes per speaker in ge2e_rows4r_kernel's cosine step (8 or 16)
-#define SV_GE2E_R4GL 8
-#endif
-
-// SV_GE2E_PROBE (A/B builds only): phase timestamps of ge2e_rows4r_kernel (100 MHz wall clock)
-// printed by thread 0 of the first and last workgroups
-#ifndef SV_GE2E_PROBE
-#define SV_GE2E_PROBE 0
-#endif
-#if SV_GE2E_PROBE
-#define GPROBE(n) \
-  if (threadIdx.x == 0) tp[n] = wall_clock64()
-#else
-#define GPROBE(n)
-#endif
 
 // a workgroup-uniform value (read from LDS) kept in an SGPR
 __device__ __forceinline__ float uniform_f(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
 }
 
-// F2, register-blocked form of the kernel above (same arguments, outputs and FUSEC meaning), the
-// product's for 128 < N <= 256 and D = 256: RW rows per workgroup of NWV waves (8 waves, 2 rows:
-// 160 workgroups at a c5 rank's 320 rows).  Every centroid value leaves LDS once per WORKGROUP and
+// F2 for 128 < N <= 256 and D = 256 (c5's global N), register-blocked: RW rows per workgroup of NWV
+// waves (8 waves, 2 rows: 160 workgroups at a c5 rank's 320 rows).  The speakers pass through LDS in
+// two chunks of 128 (fp32), each staged once by LDS-DMA; per chunk the cosines, then the chunk's
+// share of G1 = sum_{k != j} dcos_k C^_k accumulated online (flash-attention style: weights
+// e^{S_k - m} against the running row max m, the partial sum rescaled by e^{m_old - m} when a chunk
+// raises it, finally scaled by w e^{m - lz}).
+// FUSEC (sharded form): the chunks hold the all-gathered speaker SUMS s_k; the centroid scale
+// c_k = 1 / (M max(|s_k / M|, eps)) comes from |s_k|^2 summed in the same loop as the cosine, so
+// cos = (E^ . s_k) c_k and the G1 weights carry c_k -- no normalisation pass and no centroid
+// launch; the workgroups also write C^ and |C| of the shard's own speakers for the finalize step.  Every centroid value leaves LDS once per WORKGROUP and
 // feeds the RW rows from registers:
 //   cosines: lane = GL s + g (GL = 8-lane groups) holds E^[RW rows][32 j + 4 g .. +3] (j < 8); group
 //     s takes one speaker per step, reads its 256 values as 8 conflict-free float4 per lane (tile
@@ -996,11 +803,12 @@ __device__ __forceinline__ float uniform_f(float v) {
 //     slice d = 4 lane, its RW weights per speaker one broadcast LDS read; the
 //     waves' [RW][256] partials meet once, in LDS, after the last chunk;
 //   row backward: one thread per (row, speaker), cos / dcos stored coalesced.
-// Measured at the c5 rank shape (scripts/ge2e_c5rank.py, kernel trace): 23.4 us for the kernel
-// above, 22.9 here with 16 waves x 4 rows and 16-lane groups (the FUSEC form spilled), 17.1 with
-// 8 waves x 2 rows, 14.5 with branch-free steps, 13.4 with 8-lane groups.  Phase probes
-// (SV_GE2E_PROBE, 2.3 GHz shader clock): staging a chunk ~1.9 us (256 KB of sums per workgroup
-// from L2, the per-CU fill rate), cosines 1.2 us, softmax 0.9 us and G1 ~0.9 us per chunk.
+// Measured at the c5 rank shape (scripts/ge2e_c5rank.py, kernel trace): 23.4 us for the r05 form
+// with four waves per row (16 waves, 4 rows per workgroup; deleted), 22.9 here with 16 waves x 4 rows
+// and 16-lane groups (the FUSEC form spilled), 17.1 with 8 waves x 2 rows, 14.5 with branch-free
+// steps, 13.4 with 8-lane groups.  Phase probes (2.3 GHz shader clock): staging a chunk ~1.9 us
+// (256 KB of sums per workgroup from L2, the per-CU fill rate), cosines 1.2 us, softmax 0.9 us and
+// G1 ~0.9 us per chunk.
 template <bool FUSEC, int NWV, int RW>
 __global__ __launch_bounds__(64 * NWV) void ge2e_rows4r_kernel(const float* __restrict__ Csrc,
                                                           const float* __restrict__ Ehat,
@@ -1012,7 +820,7 @@ __global__ __launch_bounds__(64 * NWV) void ge2e_rows4r_kernel(const float* __re
                                                           float* __restrict__ dwdb_rows, float* __restrict__ G1,
                                                           float* __restrict__ Chat_out, float* __restrict__ Cn_out) {
   constexpr int D = 256, LDC = GF_R4LDC, NCM = GF_NMAX / GF_CH, NT = 64 * NWV, KW = GF_CH / NWV;
-  constexpr int GL = SV_GE2E_R4GL, SPS = 64 / GL, JN = D / (4 * GL), NS = KW / SPS;  // lanes per speaker, ...
+  constexpr int GL = 8, SPS = 64 / GL, JN = D / (4 * GL), NS = KW / SPS;  // lanes per speaker, ...
   static_assert((GL == 8 || GL == 16) && KW % SPS == 0, "whole cosine steps");
   static_assert((NWV == 8 || NWV == 16) && (RW == 2 || RW == 4) && 2 * RW <= NWV && GF_CH / NWV * RW <= 64,
                 "RW rows x 128 speakers of the softmax step on waves 0 .. 2 RW - 1");
@@ -1032,11 +840,6 @@ __global__ __launch_bounds__(64 * NWV) void ge2e_rows4r_kernel(const float* __re
   float* red = Kc + GF_CH;             // [2][16]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane % GL, s = lane / GL;
-#if SV_GE2E_PROBE
-  unsigned long long tp[16] = {};
-  const unsigned long long cy0 = __builtin_amdgcn_s_memtime();
-#endif
-  GPROBE(0);
   const int r0 = blockIdx.x * RW;
   const float wv = *wp, bv = *bp;
   int sg[RW];
@@ -1075,7 +878,6 @@ __global__ __launch_bounds__(64 * NWV) void ge2e_rows4r_kernel(const float* __re
           (__attribute__((address_space(3))) void*)(Cb + row * LDC), 16, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    GPROBE(1 + 4 * c);
     // cosines of the chunk: wave w, step t, lane group s -> speaker KW w + SPS t + s; the steps are
     // independent and branch-free (a speaker past the chunk reads the chunk's last row and is not
     // stored), so their LDS reads, FMAs and DPP sums interleave
@@ -1130,7 +932,6 @@ __global__ __launch_bounds__(64 * NWV) void ge2e_rows4r_kernel(const float* __re
       }
     }
     __syncthreads();
-    GPROBE(2 + 4 * c);
     // online softmax over the chunk: thread -> (row i = tid / 128, speaker kl = tid % 128), waves 0..7
     const int si = tid >> 7, skl = tid & 127, sk_g = c * GF_CH + skl;
     const bool sval = tid < 128 * RW && skl < nk && r0 + si < Bl;
@@ -1167,7 +968,6 @@ __global__ __launch_bounds__(64 * NWV) void ge2e_rows4r_kernel(const float* __re
       acc[i].z *= resc[i];
       acc[i].w *= resc[i];
     }
-    GPROBE(3 + 4 * c);
     // G1 partials: wave w, speakers KW w .. KW w + KW - 1, columns 4 lane .. 4 lane + 3
 #pragma unroll
     for (int kk = 0; kk < KW; ++kk) {  // (past the chunk: the last row again, with weight 0)
@@ -1196,7 +996,6 @@ __global__ __launch_bounds__(64 * NWV) void ge2e_rows4r_kernel(const float* __re
 #pragma unroll
   for (int i = 0; i < RW; ++i) lz[i] = m[i] + logf(zsum[i] + EPS_LOG * expf(-m[i]));
   __syncthreads();  // Cb free: the G1 partials meet there
-  GPROBE(9);
 #pragma unroll
   for (int i = 0; i < RW; ++i) *reinterpret_cast<float4*>(Cb + (w * RW + i) * D + 4 * lane) = acc[i];
   __syncthreads();
@@ -1225,7 +1024,6 @@ __global__ __launch_bounds__(64 * NWV) void ge2e_rows4r_kernel(const float* __re
     }
     pdv[it] = wave_sum_dpp(pd);
   }
-  GPROBE(10);
 #pragma unroll
   for (int it = 0; it < 256 * RW / NT; ++it)
     if (lane == 0) red[w + NWV * it] = pdv[it];  // slot = item / 64: row i owns slots 4 i .. 4 i + 3
@@ -1243,41 +1041,23 @@ __global__ __launch_bounds__(64 * NWV) void ge2e_rows4r_kernel(const float* __re
       dwdb_rows[Bl + r] = -tail;
     }
   }
-#if SV_GE2E_PROBE
-  GPROBE(11);
-  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
-    printf("PROBE wg %d: %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu cycles %llu\n", (int)blockIdx.x,
-           tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[5] - tp[3], tp[6] - tp[5], tp[7] - tp[6], tp[9] - tp[7],
-           tp[10] - tp[9], tp[11] - tp[10], tp[11] - tp[0], tp[0], __builtin_amdgcn_s_memtime() - cy0);
-#endif
 }
 
 // launch F2 for N speakers (<= GF_NMAX)
-// (ssum != nullptr: the sharded form's all-gathered sums -- the 16-wave kernel forms C^ itself and
-// returns true; false: the caller must run ge2e_centroid_kernel first)
+// (ssum != nullptr: the sharded form's all-gathered sums -- at 128 < N <= 256, D = 256 the rows
+// kernel forms C^ itself, rows_fuse_centroids; else the caller runs ge2e_centroid_kernel first)
 static bool rows_fuse_centroids(int N, int D) { return N > GF_TILE && N <= GF_NMAX && D == 256; }
 static void launch_rows(int Bl, int M, int N, int D, int Np, int s0, const Ge2eWs& ws, const float* w, const float* b,
                         float* per, hipStream_t stream, const float* ssum = nullptr) {
-  if (N > GF_TILE && D == 256 && SV_GE2E_ROWS4R) {
+  if (N > GF_TILE && D == 256) {
     const size_t lds = ((size_t)GF_CH * GF_R4LDC + 4 * GF_NMAX + 4 * GF_CH + GF_CH + 32) * sizeof(float);
-    constexpr int R4W = SV_GE2E_ROWS4R == 16 ? 16 : 8, R4R = SV_GE2E_R4ROWS == 4 ? 4 : 2;
+    constexpr int R4W = 8, R4R = 2;
     const dim3 grid((Bl + R4R - 1) / R4R), block(64 * R4W);
     if (ssum)
       hipLaunchKernelGGL((ge2e_rows4r_kernel<true, R4W, R4R>), grid, block, lds, stream, ssum, ws.Ehat, ws.rawd, Bl, M, N, Np, s0, w,
                          b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1, ws.Chat, ws.Cn);
     else
       hipLaunchKernelGGL((ge2e_rows4r_kernel<false, R4W, R4R>), grid, block, lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N, Np,
-                         s0, w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1, nullptr, nullptr);
-    return;
-  }
-  if (N > GF_TILE && D == 256) {
-    const size_t lds = ((size_t)GF_CH * (D + 4) + 4 * (size_t)D + 4 * GF_CH + 64) * sizeof(float);
-    const dim3 grid((Bl + 3) / 4), block(1024);
-    if (ssum)
-      hipLaunchKernelGGL(ge2e_rows16_kernel<true>, grid, block, lds, stream, ssum, ws.Ehat, ws.rawd, Bl, M, N, Np, s0, w,
-                         b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1, ws.Chat, ws.Cn);
-    else
-      hipLaunchKernelGGL(ge2e_rows16_kernel<false>, grid, block, lds, stream, ws.Chat, ws.Ehat, ws.rawd, Bl, M, N, Np,
                          s0, w, b, per, ws.cos, ws.dcos, ws.alpha, ws.dcd, ws.dwdb_rows, ws.G1, nullptr, nullptr);
     return;
   }
@@ -1450,10 +1230,8 @@ __global__ __launch_bounds__(64 * GF_COLW) void ge2e_cols_kernel(int Bl, int M, 
 // in LDS in wave order -- every speaker's sums in the same order for any KB.  Writes this shard's
 // dC^_k and beta_k to the reduce buffer, and workgroup 0 the shard's loss / dw / db partials
 // (r05: KB = 1 ran 256 workgroups that each streamed all of E^ from L2, 84 MB at c5's rank shape,
-// 7.5-9.4 us; ge2e_cols_kernel<true> before it ran (N, D / 64) workgroups, 11 us).
-#ifndef SV_GE2E_COLRB  // rows per wave in flight at KB = 1
-#define SV_GE2E_COLRB 16
-#endif
+// 7.5-9.4 us; ge2e_cols_kernel<true> before it ran (N, D / 64) workgroups, 11 us; KB = 2 / 4 with
+// 16-B broadcast loads measured 10.2 / 11.8 us: the product launches KB = 1).
 template <int KB>
 __global__ __launch_bounds__(1024) void ge2e_cols_partial_kernel(int Bl, int N, int D, int ldc,
                                                                  const float* __restrict__ Ehat,
@@ -1479,7 +1257,7 @@ __global__ __launch_bounds__(1024) void ge2e_cols_partial_kernel(int Bl, int N, 
   }
   // RB rows per wave in flight at once (loads first, then the FMAs): a c5 rank's 320 rows are a few
   // batches, not one memory latency per 4 rows
-  constexpr int RB = KB == 1 ? SV_GE2E_COLRB : KB == 2 ? 10 : 6;
+  constexpr int RB = KB == 1 ? 16 : KB == 2 ? 10 : 6;
   for (int rb = w; rb < Bl; rb += NW * RB) {
     float dc[RB][KB], cv[RB][KB];
     float4 e[RB];
@@ -1488,22 +1266,10 @@ __global__ __launch_bounds__(1024) void ge2e_cols_partial_kernel(int Bl, int N, 
       const int r = rb + NW * u;
       const bool ok = r < Bl;
       const long rr = ok ? r : 0;
-      if constexpr (KB == 4) {  // (k0 % 4 == 0, ldc % 4 == 0: one 16-B broadcast load)
-        const float4 d4 = *reinterpret_cast<const float4*>(dcos + rr * ldc + k0);
-        const float4 c4 = *reinterpret_cast<const float4*>(cos + rr * ldc + k0);
-        dc[u][0] = ok ? d4.x : 0.f, dc[u][1] = ok ? d4.y : 0.f, dc[u][2] = ok ? d4.z : 0.f, dc[u][3] = ok ? d4.w : 0.f;
-        cv[u][0] = c4.x, cv[u][1] = c4.y, cv[u][2] = c4.z, cv[u][3] = c4.w;
-      } else if constexpr (KB == 2) {
-        const float2 d2 = *reinterpret_cast<const float2*>(dcos + rr * ldc + k0);
-        const float2 c2 = *reinterpret_cast<const float2*>(cos + rr * ldc + k0);
-        dc[u][0] = ok ? d2.x : 0.f, dc[u][1] = ok ? d2.y : 0.f;
-        cv[u][0] = c2.x, cv[u][1] = c2.y;
-      } else {
 #pragma unroll
-        for (int j = 0; j < KB; ++j) {
-          dc[u][j] = ok ? dcos[rr * ldc + k0 + j] : 0.f;
-          cv[u][j] = cos[rr * ldc + k0 + j];
-        }
+      for (int j = 0; j < KB; ++j) {
+        dc[u][j] = ok ? dcos[rr * ldc + k0 + j] : 0.f;
+        cv[u][j] = cos[rr * ldc + k0 + j];
       }
       e[u] = dok ? *reinterpret_cast<const float4*>(Ehat + rr * D + 4 * lane) : float4{0.f, 0.f, 0.f, 0.f};
     }
@@ -1626,13 +1392,7 @@ extern "C" int sv_ge2e_shard_rows(int N_local, int M, int D, int spk_offset, int
   if (!sv_ge2e_train_ok(N, M, D) || N_local <= 0 || spk_offset < 0 || spk_offset + N_local > N) return SV_ESHAPE;
   const Ge2eWs ws = carve(workspace, N_local, M, D, N);
   const int Bl = N_local * M, Np = (N + 3) & ~3;
-#ifndef SV_GE2E_FUSEC
-#define SV_GE2E_FUSEC 1
-#endif
-#ifndef SV_GE2E_COLKB  // speakers per workgroup of ge2e_cols_partial_kernel (1, 2 or 4; Np % 4 == 0)
-#define SV_GE2E_COLKB 1
-#endif
-  if (SV_GE2E_FUSEC && rows_fuse_centroids(N, D) && Np == N) {  // (C^ formed inside the rows kernel)
+  if (rows_fuse_centroids(N, D) && Np == N) {  // (C^ formed inside the rows kernel)
     launch_rows(Bl, M, N, D, Np, spk_offset, ws, w, b, per, stream, ssum_all);
   } else {
     hipLaunchKernelGGL(ge2e_centroid_kernel, dim3(Np), dim3(256), 0, stream, ssum_all, N, M, D, ws.Chat, ws.Cn);
@@ -1646,7 +1406,7 @@ extern "C" int sv_ge2e_shard_rows(int N_local, int M, int D, int spk_offset, int
     if (e != hipSuccess) return (int)e;
   }
   if (D <= 256)
-    hipLaunchKernelGGL(ge2e_cols_partial_kernel<SV_GE2E_COLKB>, dim3((N + SV_GE2E_COLKB - 1) / SV_GE2E_COLKB),
+    hipLaunchKernelGGL(ge2e_cols_partial_kernel<1>, dim3(N),
                        dim3(1024), 0, stream, Bl, N, D, Np, ws.Ehat, ws.cos, ws.dcos, per, ws.dwdb_rows, loss_local,
                        dwdb_local, red, red + (size_t)Np * D);
   else

@@ -550,12 +550,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
 // stage in two 64-row halves (8 KB per wave), after which k-tile 1's first fills go there.  The
 // stage of k-tile kt is (kt + base) & 1, base advancing by nk per tile.  Same MFMA order per tile
 // as gemm_bf16_8q_kernel (bit-identical results).
-// The bf16 C tile goes out with non-temporal stores (SV_G8P_NT, default on): with plain stores the
+// The bf16 C tile goes out with non-temporal stores: with plain stores the
 // 128 KB per tile pushed the B panels out of the XCD's L2 (K1 at c3: 571 -> 550 us, A/B in
 // profiles/r04_v6_bf16_k1_order_ab.txt; non-temporal A fills measured slower, 569 us)
-#ifndef SV_G8P_NT
-#define SV_G8P_NT 1
-#endif
 __device__ __forceinline__ void g8_epilogue_bf16_half(g8_f32x4 (&acc)[8][4], int hlf, bf16_t* C, long ldc, int tm,
                                                       int tn, int wr, int wc, int lane, const float* bl, char* tile) {
   const int fr = lane & 15, fq = lane >> 4;
@@ -577,23 +574,16 @@ __device__ __forceinline__ void g8_epilogue_bf16_half(g8_f32x4 (&acc)[8][4], int
     const uint4 v = *reinterpret_cast<const uint4*>(tile + row * 128 + c * 16);
     uint4* dst = reinterpret_cast<uint4*>(C + ((long)tm * G256_BM + wr * 128 + 64 * hlf + row) * ldc + tn * G256_BM +
                                           wc * 64 + 8 * c);
-    if (SV_G8P_NT) {
-      typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-      __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_t*>(dst));
-    } else {
-      *dst = v;
-    }
+    typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_t*>(dst));
   }
 }
 
 #define G8P_BIAS_LDS (32 * 1024)  // LDS bytes for the persistent kernel's bias sums (N <= 8192)
-// Tile order: column groups of SV_G8P_GROUP tiles (grouped_tile, 0: row-major).  K1 at c3 (12
+// Tile order: column groups of 4 tiles (grouped_tile).  K1 at c3 (12
 // column tiles): groups of 4 with non-temporal C stores 540-545 us and 0.66 GB of corrected FETCH
 // per launch against row-major 548-553 us / 0.89 GB (groups of 6: 538-551 us / 0.64 GB; 3: no
 // faster).  Without the non-temporal stores the grouping alone gained nothing (547 -> 574 us in r03)
-#ifndef SV_G8P_GROUP
-#define SV_G8P_GROUP 4
-#endif
 
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_8qp_kernel(const bf16_t* __restrict__ A, long lda,
@@ -630,12 +620,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qp_kernel(const bf16_t* __r
   int base = 0;
   auto tile_of = [&](int vv, int& tm_, int& tn_) {
     const int id = xcd_remap(vv, nwg);
-    if (SV_G8P_GROUP > 0) {
-      grouped_tile(id, M / G256_BM, tiles_n, SV_G8P_GROUP, tm_, tn_);
-      return;
-    }
-    tn_ = id % tiles_n;
-    tm_ = id / tiles_n;
+    grouped_tile(id, M / G256_BM, tiles_n, 4, tm_, tn_);
   };
   int tm, tn;
   tile_of(v, tm, tn);
@@ -781,288 +766,5 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qp_kernel(const bf16_t* __r
     }
     if (!more) break;
     v = vn;
-  }
-}
-
-// ---- persistent + stream-K form of the 8-phase kernel (fp32 C = A . B^T, plain stores) ----
-// The c3 dx GEMM (M = T B = 102400, N = H = 768, K = 4H = 3072: 1200 tiles of 48 k-tiles) ran one
-// workgroup per tile: every tile paid its k-tile-0 fill latency and its 256 KB fp32 store tail with
-// nothing overlapping them, and 1200 tiles on 256 CUs are 4.69 rounds run as 5.  Here a grid of G
-// workgroups (one per CU) walks work items: R = tiles / G whole tiles each (tile i + G r, the
-// one-shot order), then a stream-K range of the remaining rem tiles' rem x nk k-tiles, cut into G
-// equal contiguous ranges of L (tile-major, k-minor).  The next item's k-tile 0 is filled behind
-// the current item's stores (gemm_bf16_8qp_kernel's overlap: the fills go to the stage its last
-// k-tile did not use; the fp32 epilogue stores from registers).  A range's piece of a tile is a
-// partial sum written (sc1, drained) to the workgroup's partial slot and counted on the tile's
-// arrival counter; the piece that arrives last sums the tile's pieces in k order from the slots
-// (sc1 loads) and stores the tile -- deterministic, and no workgroup waits for another (no
-// co-residency needed; gemm_f32_256sk_kernel's protocol).  The counters are left at zero.  Whole
-// tiles are summed exactly as gemm_bf16_8q_kernel sums them; stream-K tiles in pieces.
-typedef unsigned int g8_u32x4 __attribute__((ext_vector_type(4)));
-struct G8SK {
-  int R, rem, L;    // whole-tile rounds, stream-K tiles, k-tiles per workgroup range
-  float* part;      // 2 G partial slots of 512 threads x 128 fp32 (slot 2 i: the piece opening i's range)
-  unsigned* cnt;    // [rem] arrival counters, zero at the launch
-};
-constexpr int G8_SK_MAXSEG = 8;  // pieces per stream-K tile (the host checks: L * (MAXSEG - 1) >= nk)
-
-// DUAL: C = A . [B ; B2]^T over N = n1 + n2 columns, column tiles at and past n1 reading B2 and
-// stored to C2 (ldc2) -- the backward's dW_hh and dW_ih of one layer in one pass over dG^T
-template <int AF, bool DUAL = false>
-__global__ __launch_bounds__(512, 1) void gemm_bf16_8qsk_kernel(const bf16_t* __restrict__ A, long lda,
-                                                               const bf16_t* __restrict__ B, long ldb,
-                                                               float* __restrict__ C, long ldc, int M, int N, int K,
-                                                               G8SK sk, G256AFrag af = G256AFrag{},
-                                                               G256Dual dual = G256Dual{}, float* __restrict__ C2 = nullptr,
-                                                               long ldc2 = 0) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ unsigned arrived;
-  constexpr unsigned SLOT = 512u * 128u * 4u;  // bytes per partial slot
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int tiles_n = N / G256_BM;
-  const int nk = K / G256_BK;
-  const int wr = w >> 2, wc = w & 3;
-  const int G = gridDim.x, ib = blockIdx.x;
-  constexpr int OPB = G256_BM * G256_BK * 2;
-  const long S = (long)sk.rem * nk, p1 = min(S, (long)(ib + 1) * sk.L);
-  long p = (long)ib * sk.L;  // stream-K cursor
-  int r = 0;
-  // the next work item: (tile tm, tn; k-tiles [ka, kb); stream-K tile index j or -1)
-  auto next_item = [&](int& tm_, int& tn_, int& ka_, int& kb_, int& j_) -> bool {
-    int id;
-    if (r < sk.R) {
-      id = xcd_remap(ib + G * r, sk.R * G);
-      ++r;
-      ka_ = 0;
-      kb_ = nk;
-      j_ = -1;
-    } else {
-      if (p >= p1) return false;
-      j_ = (int)(p / nk);
-      ka_ = (int)(p - (long)j_ * nk);
-      kb_ = (int)min((long)nk, p1 - (long)j_ * nk);
-      p = (long)j_ * nk + kb_;
-      id = sk.R * G + j_;
-    }
-    tn_ = id % tiles_n;
-    tm_ = id / tiles_n;
-    return true;
-  };
-  int tm, tn, ka, kb, j;
-  if (!next_item(tm, tn, ka, kb, j)) return;
-  int base = 0;
-  G256Stage sa, sb;
-  long af_row[4];
-  auto init_item = [&]() {
-    if constexpr (AF) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rg = 2 * i + (w >> 2), row = tm * G256_BM + 32 * rg;
-        af_row[i] = g256_af_rowoff(af, row) + (w & 3) * 512 + lane * 8;
-      }
-    } else {
-      sa.init(A, lda, tm * G256_BM, ka * G256_BK, tid);
-    }
-    if (DUAL && tn * G256_BM >= dual.n1)
-      sb.init(dual.B2, dual.ldb2, tn * G256_BM - dual.n1, ka * G256_BK, tid);
-    else
-      sb.init(B, ldb, tn * G256_BM, ka * G256_BK, tid);
-  };
-  // output of column tile tn_: C (tile tn_) or, past n1 in the DUAL form, C2 (tile tn_ - n1 / 256)
-  auto out_of = [&](int tn_, float*& Co, long& ldco, int& tno) {
-    if (DUAL && tn_ * G256_BM >= dual.n1) {
-      Co = C2;
-      ldco = ldc2;
-      tno = tn_ - dual.n1 / G256_BM;
-    } else {
-      Co = C;
-      ldco = ldc;
-      tno = tn_;
-    }
-  };
-  auto stage = [&](int kt) { return smem + ((kt + base) & 1) * 2 * OPB; };
-  auto fill_a = [&](int kt, int i) {
-    char* lds = stage(kt);
-    if constexpr (AF) {
-      const long goff = g256_af_koff(af, ka + kt);
-      __builtin_amdgcn_global_load_lds((glb_vptr_t)(af.base + af_row[i] + goff),
-                                       (lds_vptr_t)(lds + ((2 * i + (w >> 2)) * 4 + (w & 3)) * 1024), 16, 0, 0);
-    } else {
-      __builtin_amdgcn_global_load_lds((glb_vptr_t)(sa.src[i] + kt * G256_BK), (lds_vptr_t)(lds + (w * 64 + 512 * i) * 16),
-                                       16, 0, 0);
-    }
-  };
-  auto fill_b = [&](int kt, int i) {
-    __builtin_amdgcn_global_load_lds((glb_vptr_t)(sb.src[i] + kt * G256_BK),
-                                     (lds_vptr_t)(stage(kt) + OPB + (w * 64 + 512 * i) * 16), 16, 0, 0);
-  };
-  auto read_a = [&](const char* As, int mt, int ks) -> bf16x8_t {
-    const int row = wr * 128 + 16 * mt + fr;
-    if constexpr (AF) {
-      return *reinterpret_cast<const bf16x8_t*>(As + ((row >> 5) * 4 + 2 * ks + (fq >> 1)) * 1024 +
-                                                ((row & 31) + 32 * (fq & 1)) * 16);
-    } else {
-      return *reinterpret_cast<const bf16x8_t*>(As + row * 128 + g256_phys_slot(row, 4 * ks + fq) * 16);
-    }
-  };
-  auto read_b = [&](const char* Bs, int nt, int ks) -> bf16x8_t {
-    const int row = wc * 64 + 16 * nt + fr;
-    return *reinterpret_cast<const bf16x8_t*>(Bs + row * 128 + g256_phys_slot(row, 4 * ks + fq) * 16);
-  };
-  init_item();
-#pragma unroll
-  for (int i = 0; i < 4; ++i) fill_b(0, i);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) fill_a(0, i);
-  g8_f32x4 acc[8][4];
-  bf16x8_t a[4][2], b0[2][2], b1[2][2];
-  auto mma = [&](int mh, int nh, const bf16x8_t (&bq)[2][2]) {
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_setprio(1);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-          acc[4 * mh + i][2 * nh + jj] = mfma16_bf16(bq[jj][ks], a[i][ks], acc[4 * mh + i][2 * nh + jj]);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  while (true) {
-    const int nki = kb - ka;
-    // prologue remainder (gemm_bf16_8q_kernel's): k-tile 1's first fills, k-tile 0 landed
-    if (nki > 1) {
-      fill_a(1, 0);
-      fill_a(1, 2);
-      fill_b(1, 0);
-      fill_b(1, 1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (wr == 1) {
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) acc[i][jj] = g8_f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nki; ++kt) {
-      const char* As = stage(kt);
-      const char* Bs = As + OPB;
-      const bool m1 = kt + 1 < nki, m2 = kt + 2 < nki;
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) b0[jj][ks] = read_b(Bs, jj, ks);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a[i][ks] = read_a(As, i, ks);
-      if (m1) {
-        fill_b(kt + 1, 2);
-        fill_b(kt + 1, 3);
-      }
-      mma(0, 0, b0);
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) b1[jj][ks] = read_b(Bs, 2 + jj, ks);
-      if (m1)
-        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (m1) fill_a(kt + 1, 1);
-      if (m2) fill_a(kt + 2, 0);
-      mma(0, 1, b1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a[i][ks] = read_a(As, 4 + i, ks);
-      if (m1) fill_a(kt + 1, 3);
-      if (m2) fill_a(kt + 2, 2);
-      mma(1, 1, b1);
-      if (m2)
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else if (m1)
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (m2) {
-        fill_b(kt + 2, 0);
-        fill_b(kt + 2, 1);
-      }
-      mma(1, 0, b0);
-    }
-    if (wr == 0) {
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // every wave is past its last read of both stages: the next item's k-tile 0 goes to the stage
-    // this item's last k-tile did not use, behind this item's stores
-    const int tm0 = tm, tn0 = tn, ka0 = ka, kb0 = kb, j0 = j;
-    const bool more = next_item(tm, tn, ka, kb, j);
-    if (more) {
-      base = (base + nki) & 1;
-      init_item();
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fill_b(0, i);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fill_a(0, i);
-    }
-    float* Co;
-    long ldco;
-    int tno;
-    out_of(tn0, Co, ldco, tno);
-    if (ka0 == 0 && kb0 == nk) {  // a whole tile
-      g8_epilogue<G8_STORE>(acc, Co, ldco, 0L, tm0, tno, wr, wc, lane, nullptr, nullptr, 0.f);
-    } else {
-      // a piece of stream-K tile j0: the tile's pieces are workgroups s0 .. s1's (k order)
-      const int s0 = (int)(((long)j0 * nk) / sk.L), s1 = (int)(((long)j0 * nk + nk - 1) / sk.L);
-      auto slot = [&](int wg) {  // slot of workgroup wg's piece of tile j0: 0 if it opens wg's range
-        return (unsigned)(2 * wg + ((long)wg * sk.L >= (long)j0 * nk ? 0 : 1)) * SLOT;
-      };
-      const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(sk.part, 0, 2u * G * SLOT, 0x00020000);
-      {
-        const unsigned sb0 = slot(ib);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(g8_u32x4, acc[i][jj]), rpart,
-                                                   sb0 + (unsigned)(((i * 4 + jj) * 512 + tid) * 16), 0, 16 /* sc1 */);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) arrived = __hip_atomic_fetch_add(sk.cnt + j0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      if (arrived == (unsigned)(s1 - s0)) {  // the last piece: every piece (its own too) from the slots,
-        // summed in k order, stored straight to C (acc[mt][nt] = C[16 mt + fr][16 nt + 4 fq ..])
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            const unsigned off = (unsigned)(((i * 4 + jj) * 512 + tid) * 16);
-            g8_f32x4 sum = __builtin_bit_cast(g8_f32x4, __builtin_amdgcn_raw_buffer_load_b128(rpart, slot(s0) + off, 0, 16));
-            for (int wg = s0 + 1; wg <= s1; ++wg)
-              sum += __builtin_bit_cast(g8_f32x4, __builtin_amdgcn_raw_buffer_load_b128(rpart, slot(wg) + off, 0, 16));
-            const long row = (long)tm0 * G256_BM + wr * 128 + 16 * i + fr;
-            const int col = tno * G256_BM + wc * 64 + 16 * jj + 4 * fq;
-            *reinterpret_cast<g8_f32x4*>(Co + row * ldco + col) = sum;
-          }
-        if (tid == 0) __hip_atomic_store(sk.cnt + j0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if (!more) break;
   }
 }

@@ -22,9 +22,6 @@
 #include "sv_gemm.h"
 
 #define GF_BM 256
-#ifndef SV_GF_GROUP
-#define SV_GF_GROUP 4  // column tiles per group of the one-shot tile order (grouped_tile)
-#endif
 #define GF_BK 32
 
 typedef __attribute__((address_space(3))) void* gf_lds_ptr_t;
@@ -274,7 +271,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256_kernel(const float* __res
     // one-shot launches: column-grouped tile order (4 fp32 B panels of 256 x 768 = 3.1 MB per XCD
     // L2 at the K1 shape)
     id = xcd_remap(blockIdx.x, nwg);
-    grouped_tile(id, M / GF_BM, tiles_n, SV_GF_GROUP, tm, tn);
+    grouped_tile(id, M / GF_BM, tiles_n, 4, tm, tn);
   } else {
     splitk_tile(nwg, id, sl);
     tn = id % tiles_n;
@@ -326,14 +323,14 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256sk_kernel(const float* __r
   for (int r = 0;; ++r) {
     int tm, tn, ka = 0, kb = nk, j = -1;
     if (r < sk.R) {
-      grouped_tile(xcd_remap(i + G * r, sk.R * G), tiles_m, tiles_n, SV_GF_GROUP, tm, tn);
+      grouped_tile(xcd_remap(i + G * r, sk.R * G), tiles_m, tiles_n, 4, tm, tn);
     } else {
       if (p >= p1) break;
       j = (int)(p / nk);
       ka = (int)(p - (long)j * nk);
       kb = (int)min((long)nk, p1 - (long)j * nk);
       p = (long)j * nk + kb;
-      grouped_tile(sk.R * G + j, tiles_m, tiles_n, SV_GF_GROUP, tm, tn);
+      grouped_tile(sk.R * G + j, tiles_m, tiles_n, 4, tm, tn);
     }
     gf_mainloop<BN, MF, AF>(A, lda, B, ldb, tm, tn, ka * GF_BK, kb - ka, af, smem, acc);
     if (ka == 0 && kb == nk) {  // a whole tile
@@ -398,16 +395,8 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256sk_kernel(const float* __r
 // k-tile (into the stage that k-tile leaves idle), so the next tile starts on landed data and its
 // first k-tile runs while this tile's stores drain.  Same k-loop and summation order as
 // gemm_f32_256_kernel: bit-identical results.
-// SV_GF_EARLY (A/B only, measured no faster: DESIGN §4): the next tile's k-tile 1 is DMA'd too,
-// into the stage the last k-tile frees, before this tile's C stores, so k-tile 0's closing wait
-// counts the stores (vmcnt(NST)) instead of draining them: the chip-wide store burst (256 KB per
-// CU, the CUs in lock step) drains under two k-tiles of MFMAs instead of one.
-#ifndef SV_GF_EARLY
-#define SV_GF_EARLY 0
-#endif
-#if SV_GF_EARLY && defined(SV_GF_NOSTORE)
-#error "SV_GF_NOSTORE builds count no stores: build them with -DSV_GF_EARLY=0"
-#endif
+// (The next tile's k-tile 1 DMA'd too, before this tile's C stores, with k-tile 0's closing wait
+// counting the stores, measured no faster and was deleted: DESIGN §4.)
 template <int BN, int MF>
 __global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __restrict__ A, long lda,
                                                               const float* __restrict__ B, long ldb,
@@ -427,7 +416,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __re
   int v = blockIdx.x;
   if (v >= nwg || nk <= 0) return;
   int tm, tn;
-  grouped_tile(xcd_remap(v, nwg), tiles_m, tiles_n, SV_GF_GROUP, tm, tn);
+  grouped_tile(xcd_remap(v, nwg), tiles_m, tiles_n, 4, tm, tn);
   GfStage<GF_BM> sa;
   GfStage<BN> sb;
   sa.init(A, lda, tm * GF_BM, 0, tid);
@@ -469,10 +458,6 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __re
         }
   };
   f32x4 a0[TM], b0[TN], a1[TM], b1[TN];
-  // store instructions per wave between the early k-tile-1 DMA and k-tile 0's closing wait
-  constexpr int NST = TM * TN * (NR / 4);
-  static_assert(NST <= 63, "vmcnt holds 6 bits");
-  bool pre1 = false;  // this tile's k-tile 1 went out before the previous tile's stores
   while (true) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -483,15 +468,13 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __re
     const int vn = v + gridDim.x;
     const bool more = vn < nwg;
     int tmn = 0, tnn = 0;
-    if (more) grouped_tile(xcd_remap(vn, nwg), tiles_m, tiles_n, SV_GF_GROUP, tmn, tnn);
+    if (more) grouped_tile(xcd_remap(vn, nwg), tiles_m, tiles_n, 4, tmn, tnn);
     for (int kt = 0; kt < nk; ++kt) {
       const char* As = stage(kt);
       const char* Bs = As + OPA;
       if (kt + 1 < nk) {
-        if (!(SV_GF_EARLY && kt == 0 && pre1)) {
-          sa.issue(stage(kt + 1), kt + 1, w);
-          sb.issue(stage(kt + 1) + OPA, kt + 1, w);
-        }
+        sa.issue(stage(kt + 1), kt + 1, w);
+        sb.issue(stage(kt + 1) + OPA, kt + 1, w);
       } else if (more) {
         // the next tile's k-tile 0, into the stage this last k-tile leaves idle (stage pointers
         // formed here: held across the loop they would take registers)
@@ -510,32 +493,12 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __re
         if (g + 2 < NG) rd(As, Bs, g + 2, a0, b0);
         mm(a1, b1);
       }
-      // the next k-tile landed (this wave's DMA) and every wave is done with this one; after an
-      // early k-tile 1 the previous tile's NST stores, younger than it, may stay in flight
-      // (a raw barrier there: __syncthreads' release fence would drain the stores)
-      if (SV_GF_EARLY && kt == 0 && pre1) {
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-      }
+      // the next k-tile landed (this wave's DMA) and every wave is done with this one
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
     }
     GfBias<BN, MF> bias;
     bias.load(bias0, bias1, tn, wc, fh);
-    if (SV_GF_EARLY) {
-      // the bias loads waited for in a form the compiler sees (the builtin, vmcnt(0) alone), so
-      // it places no wait of its own behind the DMA below; then the next tile's k-tile 1 into the
-      // stage the last k-tile freed (after its barrier) -- after the last tile a harmless re-fetch
-      // of this tile's, drained at the end (the host launches this kernel with nk >= 2)
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-      GfStage<GF_BM> na;
-      GfStage<BN> nb;
-      na.init(A, lda, (more ? tmn : tm) * GF_BM, 0, tid);
-      nb.init(B, ldb, (more ? tnn : tn) * BN, 0, tid);
-      na.issue(stage(nk + 1), 1, w);
-      nb.issue(stage(nk + 1) + OPA, 1, w);
-      pre1 = true;
-    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const long row = (long)tm * GF_BM + wr * 128 + MF * i + fr;
@@ -546,9 +509,6 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __re
           const int col = tn * BN + wc * WN + MF * j + (MF == 32 ? 8 * q + 4 * fh : 4 * fh);
           const f32x4 val =
               bias.add(f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]}, j, q);
-#ifdef SV_GF_NOSTORE  // A/B diagnostic builds only: the k-loop's rate without the store traffic
-          if (val[0] != val[0])
-#endif
           *reinterpret_cast<f32x4*>(C + row * ldc + col) = val;
         }
     }
@@ -560,5 +520,4 @@ __global__ __launch_bounds__(512, 1) void gemm_f32_256p_kernel(const float* __re
     sb.init(B, ldb, tn * BN, 0, tid);
     base = (base + nk) & 1;
   }
-  if (SV_GF_EARLY) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last re-fetch into LDS
 }

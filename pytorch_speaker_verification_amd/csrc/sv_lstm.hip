@@ -19,9 +19,6 @@
 #include "sv_gemm_f32_256.h"
 #include "../../include/sv_ge2e.h"
 
-#ifndef SV_PF32_FUSE_X0  // fp32 persistent forward: layer 0's input projection inside the recurrence
-#define SV_PF32_FUSE_X0 1
-#endif
 
 #define SV_BKM 32
 
@@ -566,9 +563,6 @@ GemmPlan plan_gemm(int M, int N, int K, bool fine = false) {
   return p;
 }
 
-#ifndef SV_GEMM_NARROW  // 0: the N <= 48 exact NT GEMMs on the 64 x 64 tiles (A/B)
-#define SV_GEMM_NARROW 1
-#endif
 // ---- narrow NT GEMM (N <= 48): layer 0's dW_ih = dG^T x (M = 4H, N = F = 40, K = T B) ----
 // The 64 x 64 tiles (4 waves of v_mfma_f32_32x32x2_f32) padded N = 40 to 64 and ran this shape at
 // 75 TF/s (334 us at c2); it streams dG^T (1.26 GB at c2) once.  Here a workgroup is 128 rows x 48
@@ -655,7 +649,7 @@ __global__ __launch_bounds__(256) void gemm_f32_narrow_kernel(const float* __res
 // the narrow kernel's plan: exact products, NT, N <= 48, whole 128-row tiles and 32-k steps; K
 // chunks of at least 1024 over up to 32 slabs (c2: 24 row tiles x 32 slabs = 768 workgroups)
 bool narrow_ok(int M, int N, int K, long lda, long ldb, int mode) {
-  return mode == 0 && SV_GEMM_NARROW && N <= GN_BN && M % GN_BM == 0 && K % GN_BK == 0 && K >= 4096 && lda % 4 == 0 &&
+  return mode == 0 && N <= GN_BN && M % GN_BM == 0 && K % GN_BK == 0 && K >= 4096 && lda % 4 == 0 &&
          ldb % 4 == 0;
 }
 int narrow_splitk(int K, int& kchunk) {
@@ -665,12 +659,6 @@ int narrow_splitk(int K, int& kchunk) {
 }
 
 // ---- 256 x BN LDS-DMA tile (sv_gemm_f32_256.h) for the exact-fp32 NT GEMMs that tile exactly ----
-#ifndef SV_F32_MF
-#define SV_F32_MF 32  // MFMA shape of the 256-tile kernel (16: v_mfma_f32_16x16x4_f32, A/B builds)
-#endif
-#ifndef SV_GF_PERS
-#define SV_GF_PERS 1  // persistent form of the one-shot launches with more tiles than CUs (0: A/B builds)
-#endif
 int gf256_bn(int N) { return N % 256 == 0 ? 256 : 128; }
 bool gf256_ok(int M, int N, int K, const float* C, long ldc, const float* b0, const float* b1) {
   return M % GF_BM == 0 && N % 128 == 0 && K % GF_BK == 0 && ldc % 4 == 0 &&
@@ -692,7 +680,7 @@ template <int BN, int EPI>
 void launch_gf256(dim3 grid, hipStream_t s, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
                   long slab, int M, int N, int K, int kchunk, const float* b0, const float* b1, float beta) {
   constexpr size_t lds = 2 * (size_t)(GF_BM + BN) * GF_BK * 4;
-  hipLaunchKernelGGL((gemm_f32_256_kernel<BN, SV_F32_MF, EPI>), grid, dim3(512), lds, s, A, lda, B, ldb, C, ldc, slab,
+  hipLaunchKernelGGL((gemm_f32_256_kernel<BN, 32, EPI>), grid, dim3(512), lds, s, A, lda, B, ldb, C, ldc, slab,
                      M, N, K, kchunk, b0, b1, beta);
 }
 int gemm_f32_256(const float* A, long lda, const float* B, long ldb, float* C, long ldc, int M, int N, int K,
@@ -701,11 +689,11 @@ int gemm_f32_256(const float* A, long lda, const float* B, long ldb, float* C, l
   const int tiles = (M / GF_BM) * (N / p.bn);
   if (p.splitk == 1) {
     const int cus = sv_stream_cus(stream);
-    if (SV_GF_PERS && p.bn == 256 && beta == 0.f && cus > 0 && tiles > cus && K / GF_BK <= 32 &&
+    if (p.bn == 256 && beta == 0.f && cus > 0 && tiles > cus && K / GF_BK <= 32 &&
         K / GF_BK >= 2) {
       // more tiles than CUs, short K (K1; dx's 96 k-tiles measured slower persistent, 3.80 vs
       // 3.73 ms): the persistent form (each tile's k-tile 0 fetched during the previous tile)
-      hipLaunchKernelGGL((gemm_f32_256p_kernel<256, SV_F32_MF>), dim3(cus), dim3(512),
+      hipLaunchKernelGGL((gemm_f32_256p_kernel<256, 32>), dim3(cus), dim3(512),
                          2 * (size_t)(GF_BM + 256) * GF_BK * 4, stream, A, lda, B, ldb, C, ldc, M, N, K, bias0, bias1);
     } else if (p.bn == 256)
       launch_gf256<256, GF_STORE>(dim3(tiles, 1), stream, A, lda, B, ldb, C, ldc, 0L, M, N, K, p.kchunk, bias0, bias1,
@@ -736,7 +724,7 @@ int gemm_f32_256(const float* A, long lda, const float* B, long ldb, float* C, l
 // (gemm_f32_256_kernel AF, GfAFrag): the recurrence then writes no row-major dG.  Exact products,
 // whole 256-row tiles, whole 32-row groups per slot, one k-split; else -1 (use the row-major dG).
 int dx_afrag_bn(int T, int B, int H, int Fl) {
-  if (gemm_x() != 0 || SV_F32_MF != 32 || B % 32 || H % 32 || ((long)T * B) % GF_BM) return -1;
+  if (gemm_x() != 0 || B % 32 || H % 32 || ((long)T * B) % GF_BM) return -1;
   if ((unsigned long long)T * B * B >= (1ull << 32) || 4ull * H * H >= (1ull << 32)) return -1;  // gf_afrag's magic
   const int bn = gf256_bn(Fl);
   if (Fl % bn || plan_gf256(T * B, Fl, 4 * H).splitk != 1) return -1;
@@ -747,9 +735,6 @@ int dx_afrag_bn(int T, int B, int H, int Fl) {
 constexpr int GF_SK_GRID = 256;
 constexpr size_t GF_SK_SLOT = (size_t)512 * 128 * sizeof(float);
 size_t gf_sk_bytes() { return 2 * GF_SK_GRID * GF_SK_SLOT + GF_SK_GRID * sizeof(unsigned) * 4; }
-#ifndef SV_GF_SK
-#define SV_GF_SK 1  // the dx GEMM's stream-K form where its tiles leave the last round part-idle (0: A/B)
-#endif
 int gemm_f32_dx_afrag(int bn, const float* dgf, int T, int B, int H, const float* wihT, long ldw, int Fl, float* dx,
                       hipStream_t s, void* skws = nullptr) {
   const long nrb = (B + 63) / 64, fs = nrb * 8 * (H / 8) * 256;
@@ -757,7 +742,7 @@ int gemm_f32_dx_afrag(int bn, const float* dgf, int T, int B, int H, const float
   const int M = T * B, K = 4 * H, tiles = (M / GF_BM) * (Fl / bn);
   const size_t lds = 2 * (size_t)(GF_BM + bn) * GF_BK * 4;
   const int G = std::min(sv_stream_cus(s), GF_SK_GRID), nk = K / GF_BK;
-  if (SV_GF_SK && skws && bn == 256 && G > 0 && tiles > G && tiles % G) {
+  if (skws && bn == 256 && G > 0 && tiles > G && tiles % G) {
     // c2 dx: 1200 tiles on 256 CUs = 4 whole rounds + 176 tiles as 66 k-tiles per workgroup
     GfSK sk;
     sk.R = tiles / G;
@@ -775,10 +760,10 @@ int gemm_f32_dx_afrag(int bn, const float* dgf, int T, int B, int H, const float
     }
   }
   if (bn == 256)
-    hipLaunchKernelGGL((gemm_f32_256_kernel<256, SV_F32_MF, GF_STORE, 1>), dim3(tiles, 1), dim3(512), lds, s, nullptr,
+    hipLaunchKernelGGL((gemm_f32_256_kernel<256, 32, GF_STORE, 1>), dim3(tiles, 1), dim3(512), lds, s, nullptr,
                        0L, wihT, ldw, dx, (long)Fl, 0L, M, Fl, K, K, nullptr, nullptr, 0.f, af);
   else
-    hipLaunchKernelGGL((gemm_f32_256_kernel<128, SV_F32_MF, GF_STORE, 1>), dim3(tiles, 1), dim3(512), lds, s, nullptr,
+    hipLaunchKernelGGL((gemm_f32_256_kernel<128, 32, GF_STORE, 1>), dim3(tiles, 1), dim3(512), lds, s, nullptr,
                        0L, wihT, ldw, dx, (long)Fl, 0L, M, Fl, K, K, nullptr, nullptr, 0.f, af);
   SV_LAUNCH_CHECK();
   return SV_OK;
@@ -1002,12 +987,9 @@ extern "C" int sv_lstm_layer_fwd(const float* x_tm, int T, int B, int F, int H, 
 }
 
 // Row stride (floats) of the library's own W_ih^T copies (fp32 [F][4H]), the dx GEMMs' B operand:
-// 4H + SV_WIHT_PAD_F32.  A 12-KB row stride put the 256 rows of a k-tile fill on one L2 channel;
+// 4H + 64.  A 12-KB row stride put the 256 rows of a k-tile fill on one L2 channel;
 // 64 more floats spread them (the c2 dx GEMM 3707 -> 3654 us isolated, scripts/gemm_ld_ab.py).
-#ifndef SV_WIHT_PAD_F32
-#define SV_WIHT_PAD_F32 64
-#endif
-static inline long f32_wiht_ld(int H) { return 4L * H + SV_WIHT_PAD_F32; }
+static inline long f32_wiht_ld(int H) { return 4L * H + 64; }
 
 namespace {
 struct BwdWs {
@@ -1135,12 +1117,12 @@ extern "C" int sv_lstm_stack_fwd(int L, int T, int B, int F, int H, const float*
       if ((e = sv_memset0(h_tm[l], BH * sizeof(float), main)) != hipSuccess) return (int)e;
       if (hT[l] && Bp != B && (e = sv_memset0(hT[l], (size_t)H * ldhT * sizeof(float), main)) != hipSuccess)
         return (int)e;
-      // layer 0 at F = 40: the input projection inside the recurrence (SV_PF32_FUSE_X0; c2 layer 0:
+      // layer 0 at F = 40: the input projection inside the recurrence (c2 layer 0:
       // the K=40 GEMM wrote 1.26 GB that the recurrence read back)
       // (exact fp32 products only: the bf16x6 mode keeps the GEMM, whose products it splits; and 16-B
       // aligned x_tm / W_ih only: the kernel reads them by LDS-DMA / f32x4 -- else the GEMM path
       // rejects the misaligned pointer with SV_EALIGN)
-      const bool fuse = SV_PF32_FUSE_X0 && l == 0 && F == 40 && products == 0 &&
+      const bool fuse = l == 0 && F == 40 && products == 0 &&
                         !(((uintptr_t)x_tm | (uintptr_t)w_ih[0]) & 15);
       int rc = 0;
       if (!fuse) {

@@ -28,9 +28,6 @@
 #include "../../include/sv_ge2e.h"
 
 #include "sv_persist_dev.h"
-#ifndef SV_P2B_OVL  // the 32 x 32 persistent backward's dG^T stores under the hand-off drain (0: A/B)
-#define SV_P2B_OVL 1
-#endif
 
 // A-operand tile of a handed-off buffer: [R][BK] bf16 rows (row stride ld elements) read with
 // buffer_load_dwordx4 sc1 (bypasses the CU's L1, L2-served; rows past the buffer end read 0)
@@ -763,12 +760,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
       }
     }
-    // publish dG_t: every store of the hand-off drained, barrier, one lane arrives.  SV_P2B_OVL (no
+    // publish dG_t: every store of the hand-off drained, barrier, one lane arrives.  With no
     // row-major dG: the dx GEMM reads the hand-off): the BM / 16 dG^T stores per thread (buffer
     // stores; a piece past Bp to a dropped offset) go out first, and the drain counts them
     // (vmcnt(BM / 16): this wave's older hand-off stores done; a raw barrier: __syncthreads' fence
     // would drain them)
-    const bool ovl = SV_P2B_OVL && !dbg && !dg && dgT && 4L * H * lddgT * 2 < (1L << 32) - 64;
+    const bool ovl = !dbg && !dg && dgT && 4L * H * lddgT * 2 < (1L << 32) - 64;
     if (ovl) {
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);  // (the dG^T stores stay younger than the hand-off's)
@@ -1055,10 +1052,7 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
   if (e != hipSuccess) return (int)e;
   const unsigned limit = persist_limit();
   const int fault = fwd_fault();
-#ifndef SV_PFWD_DEBUG  // A/B diagnostic builds only (persist3 forward: 16 = x-projection always step 0's, cache-hot)
-#define SV_PFWD_DEBUG 0
-#endif
-  constexpr int dbg = SV_PFWD_DEBUG, pipe = 1;  // (product: no diagnostic skips); LDS-pipelined A fragments
+  constexpr int dbg = 0, pipe = 1;  // (no diagnostic skips: the kernels' dbg bits are for A/B edits); LDS-pipelined A fragments
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   if (wide) {
     const int rc = sv_persist3_fwd_launch(dim3(grid.x * grid.y), (int)grid.x, stream, whh_bf, gates, c_tm, h_tm, h_bf,
@@ -1102,12 +1096,9 @@ constexpr size_t pbwd_lds(int bm) {
   return (size_t)4 * bm * (BF_U + 4) * 4 + (size_t)bm * (4 * BF_U + 8) * 2 + (size_t)4 * BF_U * (bm + 8) * 2 +
          (size_t)bm * 512;  // + the LDS-DMA operand image (EWD)
 }
-#ifndef SV_PBWD_DEBUG
-#define SV_PBWD_DEBUG 0
-#endif
-// the backward kernels' diagnostic bits: 0 in the product library; A/B builds only (Makefile `ab`:
-// 32 = per-phase cycle stamps into the caller's sync block, read by scripts/persist_ab.py)
-constexpr int kPbwdDebug = SV_PBWD_DEBUG;
+// the backward kernels' diagnostic bits: 0 in the product library (an A/B edit sets e.g. 32 = per-phase
+// cycle stamps into the caller's sync block, read by scripts/persist_ab.py)
+constexpr int kPbwdDebug = 0;
 template <int NS, int P>
 void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
                  const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B,
@@ -1163,9 +1154,8 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
   const int Bp = (B + 7) & ~7;
   const long lddgT = (long)T * Bp;
   const bool wide = pbwd3_ok(B, H, cus);
-  const bool r16 = !wide && !dg && sv_persist16_bwd_ok(B, H, cus);  // (writes no row-major dG)
-  const int bm = wide ? 32 : r16 ? 16 : persist_bm(B, H, cus);
-  const dim3 grid(wide || r16 ? H / 64 : (H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
+  const int bm = wide ? 32 : persist_bm(B, H, cus);
+  const dim3 grid(wide ? H / 64 : (H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
   // bias-gradient partials [nrb][4H] after the fragment-order slots (db_ih NULL: not computed)
   float* dbp = db_ih ? reinterpret_cast<float*>(reinterpret_cast<char*>(dgf) +
                                                 (size_t)T * ((B + BF_BM - 1) / BF_BM) * BF_BM * 4 * H * sizeof(bf16_t))
@@ -1174,11 +1164,7 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   // A-fragment prefetch depth 8 at H = 768 (measured: 4 / 16 no better)
-  if (r16) {
-    const int rc = sv_persist16_bwd_launch((int)grid.x, (int)grid.y, stream, whhT, acts, c_tm, dhup, up_full, dgT, lddgT,
-                                           dgf, T, Bp, B, H, cnt, kPersistXcd, sync, persist_limit(), persist_fault(), dbp);
-    if (rc) return rc;
-  } else if (wide) {
+  if (wide) {
     const int rc = sv_persist3_bwd_launch(dim3(grid.x * grid.y), (int)grid.x, stream, whhT, acts, c_tm, dhup, up_full,
                                           dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, kPersistXcd, sync, persist_limit(),
                                           persist_fault(), kPbwdDebug, dbp);
@@ -1226,7 +1212,7 @@ size_t sv_wave_bwd_scratch(int L, int T, int B, int H) {
 int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, const bf16_t* const* wihT,
                      const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
                      bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
-                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, int dgt_sc1, long ldwih,
+                     float* const* db_hh, hipEvent_t pre, hipEvent_t post, long ldwih,
                      int zero_next) {
   if (!sv_wave_bwd_fits(L, B, H, sv_stream_cus(stream))) return SV_ESHAPE;
   if (!scratch || ((uintptr_t)scratch & 15) || !sync || !dh_last || !whhT || !wihT || !acts || !c_tm || !dx || !dgT)
@@ -1265,7 +1251,6 @@ int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, cons
   a.Bp = (B + 7) & ~7;
   a.H = H;
   a.lddgT = (long)T * a.Bp;
-  a.dgt_sc1 = dgt_sc1 && 4L * H * a.lddgT * 2 < (1L << 32);  // (one buffer descriptor per layer)
   hipError_t e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
   const int rc = sv_wave_bwd_launch(a, stream);

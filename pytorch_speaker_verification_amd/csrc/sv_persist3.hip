@@ -15,13 +15,10 @@
 // per-gate k order and gate-order sum (bit-identical dG), fragment-order hand-off (row blocks of
 // 32), operands staged by LDS-DMA after the arrival, bias partials per row block.
 // ============================================================================
-#ifndef SV_P3B_OVL  // the wide backward's dG^T stores under the hand-off drain (0: A/B)
-#define SV_P3B_OVL 1
-#endif
 // NL: the last NL k-steps of the second W_hh half are read from LDS (staged once, 16 B per lane per
 // fragment, prefetched two k-steps ahead) -- the registers cannot hold all 2 x NS fragments beside
 // the step's working set
-template <int NS, int P, int NL, bool DEFER>
+template <int NS, int P, int NL>
 __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     const bf16_t* __restrict__ whhT, const bf16_t* __restrict__ acts, const float* __restrict__ c_tm,
     const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
@@ -188,18 +185,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
         acc1 = mfma_bf16(a, s < NR ? wb[s < NR ? s : 0] : wq[s & 1], acc1);
         if (s + 2 >= NR && s + 2 < NS) wq[s & 1] = wl_read(s + 2 - NR);  // k-step s + 2 (same parity)
         if (s + P < NS) fa[s % P] = __builtin_amdgcn_raw_buffer_load_b128(ra, base0 + kstep * (s + P), 0, 16);
-        // DEFER: the previous step's leftovers ride in this latency-bound loop instead of delaying
-        // the next wait -- this step's operand DMA (k-steps 1-8), step t+1's dG / dG^T stores
-        // (k-steps 10-17, from the LDS tiles the epilogue below overwrites)
-        if (DEFER && s >= 1 && s <= 8) ew_piece(t, s - 1);
-        if (DEFER && s >= 10 && s <= 17 && !(dbg & 8)) store_piece(t + 1, s - 10);
         __builtin_amdgcn_sched_barrier(0);
       }
-    } else if (DEFER && t < T - 1) {  // no recurrent GEMM (dbg & 4): the leftovers here
-      load_ew(t);
-      if (!(dbg & 8))
-#pragma unroll
-        for (int i = 0; i < 8; ++i) store_piece(t + 1, i);
     }
     // per-gate partials -> red[g][row][unit]
 #pragma unroll
@@ -273,10 +260,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
       }
     }
-    // SV_P3B_OVL: with the dx GEMM on the hand-off (no row-major dG), the step's 4 dG^T stores per
+    // with the dx GEMM on the hand-off (no row-major dG), the step's 4 dG^T stores per
     // thread go out behind the hand-off stores, before their drain, which counts them (vmcnt(4):
     // this wave's older hand-off stores done; a raw barrier: __syncthreads' fence would drain them)
-    const bool ovl = SV_P3B_OVL && !DEFER && !dbg && !dg && dgT;
+    const bool ovl = !dbg && !dg && dgT;
     if (ovl) {
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);  // (the dG^T stores stay younger than the hand-off's)
@@ -291,14 +278,14 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     mark(3);
-    if (!DEFER || t == 0) {  // DEFER: all but the last step's leftovers go into the next k-loop
+    {
       // (dbg, profiling only: 64 skips the operand DMA, 128 the dG / dG^T stores).  The stores
       // first: their LDS reads issued behind an LDS-DMA would wait for it to land (the compiler
       // cannot tell the DMA's LDS range from the tiles', so it puts vmcnt(0) before every read)
       if (!ovl && !(dbg & 8) && !(dbg & 128))
 #pragma unroll
         for (int i = 0; i < 8; ++i) store_piece(t, i);
-      if (!DEFER && t > 0 && !(dbg & 64)) load_ew(t - 1);
+      if (t > 0 && !(dbg & 64)) load_ew(t - 1);
     }
     mark(4);
   }
@@ -328,265 +315,13 @@ int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
   constexpr size_t lds = (size_t)4 * 32 * 68 * 4 + (size_t)32 * 264 * 2 + (size_t)256 * 40 * 2 + (size_t)32 * 512 +
                          (size_t)2 * 32 * 64 * 4 + (size_t)4 * NL * 1024;
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + SV_SYNC_STAMP);
-  // (the DEFER form -- the operand DMA and the dG / dG^T stores inside the next step's k-loop --
-  // measured slower: c3 bwd 1205 vs 1086 us per layer; the fragment waits count the older stores)
+  // (the operand DMA and the dG / dG^T stores deferred into the next step's k-loop measured slower
+  // -- c3 bwd 1205 vs 1086 us per layer: the fragment waits count the older stores -- and deleted)
   // (operand-prefetch helper workgroups on the 16 free CUs, as the fp32 backward has them, measured
   // no gain here: DESIGN §4)
-  hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL, false>), grid, dim3(256), lds, stream, whhT, acts, c_tm,
+  hipLaunchKernelGGL((lstm_persist3_bwd_bf16_kernel<48, 8, NL>), grid, dim3(256), lds, stream, whhT, acts, c_tm,
                      dhup, up_full, dg, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbg, dbp,
                      stamps);
-  return (int)hipGetLastError();
-}
-
-// ============================================================================
-// 16-row wide tile (H = 768, batches of 257..336 rows: c5's 320 rows per rank).  The 32 x 32 tile
-// there (240 workgroups) streams 32 rows x 4H of dG_{t+1} (196 KB) per workgroup per step for 48
-// v_mfma_f32_32x32x16_bf16 per wave; this tile is 16 rows x 64 units on the same 240-workgroup
-// grid and streams 16 rows x 4H (98 KB) for 96 v_mfma_f32_16x16x32_bf16 per wave (the same MFMA
-// time): wave g holds gate g's W_hh^T rows for 64 units as 24 k-steps x 4 column blocks of 16
-// (96 fragments: 256 AGPRs + VGPRs + NL in LDS) and every A fragment (16 rows x 32 k) feeds 4 MFMAs.
-// The hand-off is the 32-row fragment order of the other tiles (sv_persist.hip: row block rb32 =
-// b / 32, KB = 32 rows x 16 k, lane = row + 32 * (k / 8)); a 16-row tile writes and reads its half
-// of each KB (lanes 16 h .. 16 h + 15 and 32 + 16 h ..), so the dx GEMM reads it unchanged.  One
-// arrival counter per 16-row block.  bf16-level agreement with the per-step schedule (another MFMA
-// shape: the k sums differ in order).
-// ============================================================================
-__device__ __forceinline__ f32x4 mfma16x32_bf16(bf16x8_t a, bf16x8_t b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-template <int P, int NL>
-__global__ __launch_bounds__(256, 1) void lstm_persist16_bwd_bf16_kernel(
-    const bf16_t* __restrict__ whhT, const bf16_t* __restrict__ acts, const float* __restrict__ c_tm,
-    const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dgT, long lddgT, bf16_t* dgf, int T, int Bp,
-    int B, int H, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit, int fault, float* __restrict__ dbp) {
-  constexpr int BM = 16, U = 64, NKS = 24, NF = 4 * NKS;  // rows, units, k-steps of 32, W fragments
-  constexpr int NA = 64, NV = NF - NA - NL;               // fragments in AGPRs / VGPRs (the rest in LDS)
-  constexpr int LDR = U + 4;                              // red [4][BM][LDR] fp32
-  constexpr int LDG = 4 * U + 8;                          // dgs [BM][LDG] bf16
-  constexpr int LDT = BM + 8;                             // gts [4U][LDT] bf16
-  constexpr int FRAG = 48 * 64 * 8;                       // dgf elements of one (32-row block, gate)
-  static_assert(P >= 1 && P <= NKS && NV >= 0, "prefetch depth / weight split");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem);
-  bf16_t* dgs = reinterpret_cast<bf16_t*>(smem + 4 * BM * LDR * 4);
-  bf16_t* gts = dgs + BM * LDG;
-  char* ewa = reinterpret_cast<char*>(gts + 4 * U * LDT);  // [BM][512 B]: gate q at ((q + row) & 3) * 128
-  float* ewc = reinterpret_cast<float*>(ewa + BM * 512);    // [BM][U] c_{t-1}
-  float* ewu = ewc + BM * U;                                // [BM][U] dh_up
-  char* wl = reinterpret_cast<char*>(ewu + BM * U);         // [4 waves][NL][64 lanes][16 B]
-  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
-  const int lr = lane & 15, lq = lane >> 4;
-  int ub, rb;
-  persist_tile(xcd, nub, ub, rb);
-  const int j0 = ub * U, b0 = rb * BM, rb32 = b0 / 32, hb = (b0 / 16) & 1;
-  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
-  const long nrb32 = (B + 31) / 32;
-  const long FS = nrb32 * 32 * G;
-  unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
-  const unsigned producers = nub;
-  // fragment f = 4 s + cb: B[k][n] = W_hh[g H + 32 s + k][j0 + 16 cb + n], lane (n = lr, k = 8 lq ..)
-  bf16x8_t wa[NA], wv[NV > 0 ? NV : 1];
-  {
-    const bf16x8_t z = {};
-    auto src = [&](int f) {
-      return whhT + (long)(j0 + 16 * (f & 3) + lr) * G + (long)g * H + 32 * (f >> 2) + 8 * lq;
-    };
-#pragma unroll
-    for (int f = 0; f < NA; ++f) wa[f] = *reinterpret_cast<const bf16x8_t*>(src(f));
-#pragma unroll
-    for (int f = 0; f < NV; ++f) wv[f] = *reinterpret_cast<const bf16x8_t*>(src(NA + f));
-#pragma unroll
-    for (int f = 0; f < NL; ++f)
-      *reinterpret_cast<bf16x8_t*>(wl + ((g * NL + f) * 64 + lane) * 16) = *reinterpret_cast<const bf16x8_t*>(src(NA + NV + f));
-    (void)z;
-#pragma unroll
-    for (int f = 0; f < NA; ++f) asm volatile("" : "+a"(wa[f]));
-  }
-  auto wfrag = [&](int f) -> bf16x8_t {
-    if (f < NA) return wa[f < NA ? f : 0];
-    if (f < NA + NV) return wv[f >= NA && f < NA + NV ? f - NA : 0];
-    return *reinterpret_cast<const bf16x8_t*>(wl + ((g * NL + (f - NA - NV)) * 64 + lane) * 16);
-  };
-  // elementwise map: thread -> row brow, 4 consecutive units u4
-  const int u4 = (tid & 15) * 4, brow = tid >> 4;
-  float4 cv;
-  float dcf[4] = {0.f, 0.f, 0.f, 0.f};
-  float dbs[4][4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) dbs[q][v] = 0.f;
-  const long Bv = B;
-  // step tt's operands into LDS: pieces 0-1 activations, 2 c_{t-1}, 3 dh_up (one KB per wave each)
-  auto load_ew = [&](int tt) {
-    {
-      const __amdgpu_buffer_rsrc_t ra_ = sv_rsrc(acts + (long)tt * BG, (unsigned)(BG * 2));
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int p = (g * 2 + i) * 64 + lane, row = p >> 5, sl = p & 31;
-        const int q = ((sl >> 3) - row) & 3, c = sl & 7;
-        const long gb = b0 + row, gbv = gb < Bv ? gb : Bv + 64;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_, (lds_ptr_t)(ewa + (g * 2 + i) * 1024), 16,
-                                                 (unsigned)((gbv * G + q * H + j0 + 8 * c) * 2), 0, 0, 0);
-      }
-    }
-    const int p = g * 64 + lane, row = p >> 4, c = p & 15;
-    const long gb = b0 + row, gbv = gb < Bv ? gb : Bv + 64;
-    const unsigned off = (unsigned)((gbv * H + j0 + 4 * c) * 4);
-    const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(tt > 0 ? tt - 1 : 0) * BH, tt > 0 ? (unsigned)(BH * 4) : 0u);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rc_, (lds_ptr_t)((char*)ewc + g * 1024), 16, off, 0, 0, 0);
-    const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
-    const __amdgpu_buffer_rsrc_t ru_ = sv_rsrc(up ? up : c_tm, up ? (unsigned)(BH * 4) : 0u);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ru_, (lds_ptr_t)((char*)ewu + g * 1024), 16, off, 0, 0, 0);
-  };
-  {
-    const __amdgpu_buffer_rsrc_t rc_ = sv_rsrc(c_tm + (long)(T - 1) * BH, (unsigned)(BH * 4));
-    const long gb = b0 + brow;
-    const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(rc_, (unsigned)(((gb < Bv ? gb : Bv + 64) * H + j0 + u4) * 4), 0, 0);
-    cv = float4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
-  }
-  load_ew(T - 1);
-  // this lane's A fragment of k-step s (16 rows x 32 k): KB 2 s + lq / 2 of (rb32, gate g), lane
-  // 16 hb + lr + 32 (lq & 1) of it
-  const unsigned abase =
-      ((unsigned)(rb32 * 4 + g) * (unsigned)FRAG + (unsigned)(lq >> 1) * 512u + (unsigned)(16 * hb + lr + 32 * (lq & 1)) * 8u) *
-      2u;
-  for (int t = T - 1; t >= 0; --t) {
-    f32x4 acc[4];
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (t < T - 1) {
-      if (tid == 0) persist_wait(my_cnt, producers * (unsigned)(T - 1 - t), status, limit, 2u);
-      __syncthreads();
-      {
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime();  // (keeps the first wait counted)
-        asm volatile("" ::"s"(t_));
-      }
-      const __amdgpu_buffer_rsrc_t ra = sv_rsrc(dgf + (long)(t + 1) * FS, (unsigned)(FS * 2));
-      constexpr unsigned kstep = 2u * 512u * 2u;  // two KBs (bytes)
-      u32x4_t fa[P];
-#pragma unroll
-      for (int s = 0; s < P; ++s) fa[s] = __builtin_amdgcn_raw_buffer_load_b128(ra, abase + kstep * s, 0, 16 /* sc1 */);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int s = 0; s < NKS; ++s) {
-        const bf16x8_t a = __builtin_bit_cast(bf16x8_t, fa[s % P]);
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb) acc[cb] = mfma16x32_bf16(a, wfrag(4 * s + cb), acc[cb]);
-        if (s + P < NKS) fa[s % P] = __builtin_amdgcn_raw_buffer_load_b128(ra, abase + kstep * (s + P), 0, 16);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    // per-gate partials -> red[g][row][unit]: lane holds rows 4 lq + v of column block cb, column lr
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) red[(g * BM + 4 * lq + v) * LDR + 16 * cb + lr] = acc[cb][v];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
-    __syncthreads();
-    {
-      const int b = brow;
-      const float4 r0 = *reinterpret_cast<const float4*>(red + (0 * BM + b) * LDR + u4);
-      const float4 r1 = *reinterpret_cast<const float4*>(red + (1 * BM + b) * LDR + u4);
-      const float4 r2 = *reinterpret_cast<const float4*>(red + (2 * BM + b) * LDR + u4);
-      const float4 r3 = *reinterpret_cast<const float4*>(red + (3 * BM + b) * LDR + u4);
-      const float4 cpv = *reinterpret_cast<const float4*>(ewc + b * U + u4);
-      const float4 upv = *reinterpret_cast<const float4*>(ewu + b * U + u4);
-      float4 f[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        f[q] = unpack_bf4(*reinterpret_cast<const uint2*>(ewa + b * 512 + ((q + b) & 3) * 128 + (u4 >> 3) * 16 + (u4 & 7) * 2));
-      unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
-      float4 dh4 = r0;  // (elementwise, the scalar order)
-      dh4 += r1;
-      dh4 += r2;
-      dh4 += r3;
-      dh4 += upv;
-      float ddv[4][4];
-      lstm_cell_bwd_x4(dh4, f[0], f[1], f[2], f[3], cv, cpv, dcf, ddv);
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const float (&dd)[4] = ddv[v];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const unsigned e = to_bf(dd[q]);
-          pk[q][v >> 1] |= e << (16 * (v & 1));
-          dbs[q][v] += __uint_as_float(e << 16);
-          gts[(q * U + u4 + v) * LDT + b] = (bf16_t)e;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(dgs + b * LDG + q * U + u4) = uint2{pk[q][0], pk[q][1]};
-      cv = cpv;  // c_{t-1} is the next step's c_t
-    }
-    __syncthreads();
-    // the hand-off: this tile's half of 16 KBs (gate q, k-step j0 / 16 + sl) = 8 KB, 16-B sc1 stores
-    {
-      const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 2));
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int p = tid + 256 * i, r = p & 15, kh = (p >> 4) & 1, sl = (p >> 5) & 3, q = p >> 7;
-        const uint4 v = *reinterpret_cast<const uint4*>(dgs + r * LDG + q * U + 16 * sl + 8 * kh);
-        const unsigned off = ((unsigned)(rb32 * 4 + q) * (unsigned)FRAG + (unsigned)(j0 / 16 + sl) * 512u +
-                              (unsigned)(16 * hb + r + 32 * kh) * 8u) *
-                             2u;
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0 && persist_arrive_ok(fault, t == T - 1))
-      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // dG_t^T (the dW GEMMs' operand): 256 gate columns x 16 rows, two 16-B stores per thread
-    if (dgT) {
-      const __amdgpu_buffer_rsrc_t rs = sv_rsrc(dgT + (long)t * Bp, (unsigned)(4L * H * lddgT * 2 - (long)t * Bp * 2));
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int p = tid + 256 * i, gu = p >> 1, c = p & 1;
-        const int gq = gu / U, gj = j0 + gu % U, gb = b0 + 8 * c;
-        const uint4 v = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
-        if (gb < Bp)
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rs,
-                                                 (unsigned)((((long)gq * H + gj) * lddgT + gb) * 2), 0, 0);
-      }
-    }
-    if (t > 0) load_ew(t - 1);
-  }
-  if (dbp) {
-    __syncthreads();
-    float* dsum = red;  // [16][4U] fp32
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      *reinterpret_cast<float4*>(dsum + brow * (4 * U) + q * U + u4) = float4{dbs[q][0], dbs[q][1], dbs[q][2], dbs[q][3]};
-    __syncthreads();
-    {
-      const int q = tid / U, gj = j0 + tid % U;
-      float sum = 0.f;
-      for (int b = 0; b < BM; ++b) sum += dsum[b * (4 * U) + tid];
-      dbp[(long)rb * G + (long)q * H + gj] = sum;
-    }
-  }
-}
-
-// the 16-row tile's grid: (H / 64) x ceil(B / 16) workgroups co-resident, and more rows than one
-// 32-row grid round leaves in a 16-row one (c5's 320 rows: 240 workgroups either way)
-int sv_persist16_bwd_ok(int B, int H, int cus) {
-  return SV_PBWD16 && H == 768 && B > 256 && (long)(H / 64) * ((B + 15) / 16) <= cus && (B + 15) / 16 <= SV_PCNT_ROWS;
-}
-int sv_persist16_bwd_launch(int nub, int nrb, hipStream_t stream, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
-                            const float* dhup, int up_full, bf16_t* dgT, long lddgT, bf16_t* dgf, int T, int Bp, int B,
-                            int H, unsigned* cnt, int xcd, unsigned* sync, unsigned limit, int fault, float* dbp) {
-#ifndef SV_P16_NL  // W fragments in LDS (A/B builds)
-#define SV_P16_NL 16
-#endif
-#ifndef SV_P16_P  // A-fragment prefetch depth (A/B builds)
-#define SV_P16_P 8
-#endif
-  constexpr int NL = SV_P16_NL;
-  constexpr size_t lds = (size_t)4 * 16 * 68 * 4 + (size_t)16 * 264 * 2 + (size_t)256 * 24 * 2 + (size_t)16 * 512 +
-                         (size_t)2 * 16 * 64 * 4 + (size_t)4 * (NL > 0 ? NL : 1) * 1024;
-  hipLaunchKernelGGL((lstm_persist16_bwd_bf16_kernel<SV_P16_P, NL>), dim3(nub * nrb), dim3(256), lds, stream, whhT, acts, c_tm,
-                     dhup, up_full, dgT, lddgT, dgf, T, Bp, B, H, cnt, nub, xcd, sync, limit, fault, dbp);
   return (int)hipGetLastError();
 }
 
@@ -602,12 +337,9 @@ int sv_persist16_bwd_launch(int nub, int nrb, hipStream_t stream, const bf16_t* 
 // XF > 0 (layer 0, F = 8 XF <= 48 features): the input projection formed in the kernel from x_bf
 // [T,B,F] and W_ih [4H,F] (both halves' fragments in registers), rounded to bf16 with its biases as
 // the K1 path stores it -- lstm_persist2_fwd_bf16_kernel's fused form.
-// SPLIT: the second half of h_{t-1} is loaded while the first half's MFMAs run (its registers
-// stay live across them; only where the register budget allows, XF = 0)
-// MODE: 0 register staging of h_{t-1} (two halves), 1 the same with the second half in flight
-// during the first half's MFMAs (SPLIT), 2 LDS-DMA staging into the row-contiguous tile image of
-// sv_persist_dev.h's w3_dma (one batch of 12 DMA instructions per wave, no register round trip)
-template <int NS, int NL, int PA, int XF, int MODE = 0>
+// h_{t-1} is staged through registers in two halves (measured against LDS-DMA staging and the
+// second half in flight during the first half's MFMAs: both slower, sv_persist3_fwd_launch)
+template <int NS, int NL, int PA, int XF>
 __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
     const bf16_t* __restrict__ whh_bf, bf16_t* __restrict__ gates, float* __restrict__ c_tm, float* __restrict__ h_tm,
     bf16_t* h_bf, bf16_t* __restrict__ hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd,
@@ -617,8 +349,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
   // MFMAs, 8 no post-arrival stores
   constexpr int BM = 32, U = 64, KR = 2;
   constexpr int K = NS * 16, LDA = K + 8;
-  constexpr bool SPLIT = MODE == 1, DMA = MODE == 2;
-  static_assert(!DMA || (BM * LDA * 2 == W3_TILE && NS == 48), "DMA tile image = the As region");
   constexpr int LDP = 4 * U + 4;  // pre [BM][LDP] fp32
   constexpr int LDB = U + 8;      // hsb [BM][LDB] bf16
   constexpr int LDT = BM + 8;     // hts [U][LDT] bf16
@@ -718,7 +448,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
       }
     }
   };
-  const __amdgpu_buffer_rsrc_t rh_all = sv_rsrc(h_bf, (unsigned)((long)(T + 1) * BH * 2));
   for (int t = 0; t < T; ++t) {
     f32x16 acc0, acc1;
 #pragma unroll
@@ -744,11 +473,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
         }
       };
       const bf16_t* A0 = As + r * LDA + 8 * hh;
-      const W3Frag dfrag(reinterpret_cast<const char*>(As), lane);
-      auto afrag = [&](int s) {
-        if constexpr (DMA) return dfrag(s);
-        return *reinterpret_cast<const bf16x8_t*>(A0 + 16 * s);
-      };
+      auto afrag = [&](int s) { return *reinterpret_cast<const bf16x8_t*>(A0 + 16 * s); };
       bf16x8_t wq[2];
       // k-steps [s0, s1) from the staged A tile: A fragments PA ahead (within the range), the
       // LDS-resident W fragments two ahead
@@ -768,27 +493,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
           __builtin_amdgcn_sched_barrier(0);
         }
       };
-      if constexpr (DMA) {
-        w3_dma(rh_all, t, B, H, b0, reinterpret_cast<char*>(As), g, lane);
-        load_xg(t);
-        // the tile's DMA (older than the x-projection loads), then every wave's
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XF > 0 ? XS : KR * 4) : "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        if (!(dbg & 2)) mma_range(0, NS);
-      } else if constexpr (SPLIT) {
-        uint4 v0[CH], v1[CH];
-        stage_load(0, v0);
-        stage_store(0, v0);
-        stage_load(1, v1);  // in flight during the first half's MFMAs
-        __syncthreads();
-        load_xg(t);
-        __builtin_amdgcn_sched_barrier(0);
-        if (!(dbg & 2)) mma_range(0, NS / 2);
-        stage_store(1, v1);
-        __syncthreads();
-        if (!(dbg & 2)) mma_range(NS / 2, NS);
-      } else {
+      {
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           uint4 v[CH];
@@ -920,28 +625,25 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
   }
 }
 
-#ifndef SV_P3F_MODE  // h_{t-1} staging of the wide forward (A/B builds; see below)
-#define SV_P3F_MODE 0
-#endif
 int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whh_bf, bf16_t* gates, float* c_tm,
                            float* h_tm, bf16_t* h_bf, bf16_t* hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt,
                            int xcd, unsigned* status, unsigned limit, int fault, const bf16_t* x_bf, int F,
                            const bf16_t* wih_bf, const float* b_ih, const float* b_hh, int dbg) {
   constexpr size_t base = (size_t)32 * (768 + 8) * 2 + (size_t)32 * (4 * 64 + 4) * 4 + (size_t)32 * 72 * 2 +
                           (size_t)64 * 40 * 2;
-  // MODE 0: h_{t-1} staged through registers in two halves.  Measured alternatives (bit-identical
-  // results): LDS-DMA staging (MODE 2) 921 vs 843 us per layer at c3 (r05, on the scalar-addressed
-  // W3Dma: 908 vs 854); the second half in flight during the first half's MFMAs (MODE 1) 4.77 vs
-  // 4.67 ms for the 3-layer forward
+  // h_{t-1} staged through registers in two halves.  Measured alternatives (bit-identical results,
+  // deleted): LDS-DMA staging 921 vs 843 us per layer at c3 (r05, on the scalar-addressed W3Dma: 908
+  // vs 854); the second half in flight during the first half's MFMAs 4.77 vs 4.67 ms for the
+  // 3-layer forward
   if (x_bf) {  // layer 0, F = 40: the W_ih fragments take registers, so more W_hh fragments live in LDS
     if (F != 40 || !wih_bf) return SV_EARG;
     constexpr int NL = 16;
-    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 5, SV_P3F_MODE>), grid, dim3(256), base + (size_t)4 * NL * 1024,
+    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 5>), grid, dim3(256), base + (size_t)4 * NL * 1024,
                        stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
                        fault, x_bf, wih_bf, b_ih, b_hh, dbg);
   } else {
     constexpr int NL = 12;
-    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0, SV_P3F_MODE>), grid, dim3(256), base + (size_t)4 * NL * 1024,
+    hipLaunchKernelGGL((lstm_persist3_fwd_bf16_kernel<48, NL, 4, 0>), grid, dim3(256), base + (size_t)4 * NL * 1024,
                        stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit,
                        fault, nullptr, nullptr, nullptr, nullptr, dbg);
   }
@@ -1087,13 +789,11 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
     // the k-loop, so its round trip overlaps the MFMAs instead of opening the epilogue (the layer
     // above's counter was polled just now)
     float4 upv = float4{0.f, 0.f, 0.f, 0.f};
-#ifndef SV_WB_LATE_UP
     u32x4_t upx = u32x4_t{0u, 0u, 0u, 0u};
     const float* upp = t >= 0 ? (has_up ? a.dx[l + 1] + (long)t * BH : (t == T - 1 ? a.dh_last : nullptr)) : nullptr;
     if (upp)
       upx = __builtin_amdgcn_raw_buffer_load_b128(sv_rsrc(upp, (unsigned)(BH * 4)), (unsigned)((gbv * H + j0 + u4) * 4),
                                                   0, 16 /* sc1: hand-off */);
-#endif
     if (t < T - 1) {
       // A fragments of dG_{t+1} (this layer's hand-off slot): k-step s at (rb 4 + g) FRAG + s 512
       const __amdgpu_buffer_rsrc_t ra = sv_rsrc(a.dgf[l] + (long)(t + 1) * FS, (unsigned)(FS * 2));
@@ -1132,19 +832,7 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's operand DMA landed
     __syncthreads();
-#ifdef SV_WB_LATE_UP  // A/B: the r03 placement (loaded here, after the k-loop)
-    if (t >= 0) {
-      const float* up = has_up ? a.dx[l + 1] + (long)t * BH : (t == T - 1 ? a.dh_last : nullptr);
-      if (up) {
-        const __amdgpu_buffer_rsrc_t ru = sv_rsrc(up, (unsigned)(BH * 4));
-        const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(ru, (unsigned)((gbv * H + j0 + u4) * 4), 0,
-                                                                16 /* sc1: hand-off */);
-        upv = float4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
-      }
-    }
-#else
     upv = float4{__uint_as_float(upx.x), __uint_as_float(upx.y), __uint_as_float(upx.z), __uint_as_float(upx.w)};
-#endif
     // dx_{t+1} of this layer: gate partials summed in gate order, 16-B sc1 stores (hand-off)
     if (has_dx && t < T - 1) {
       const int b = brow;
@@ -1217,10 +905,10 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw, off, 0, 16 /* sc1 */);
       }
     }
-    // SV_P3B_OVL: the 2 dG_t^T stores per thread (buffer stores; a piece past Bp to a dropped offset)
+    // the 2 dG_t^T stores per thread (buffer stores; a piece past Bp to a dropped offset)
     // behind the hand-off stores, before their drain, which counts them (vmcnt(2): this wave's
     // older hand-off and dx stores done; a raw barrier: __syncthreads' fence would drain them)
-    const bool ovl = SV_P3B_OVL && t >= 0 && a.dgT[l] && 4L * H * a.lddgT * 2 < (1L << 32) - 64;
+    const bool ovl = t >= 0 && a.dgT[l] && 4L * H * a.lddgT * 2 < (1L << 32) - 64;
     if (ovl) {
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);  // (the dG^T stores stay younger than the hand-off's)
@@ -1232,10 +920,7 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
         const long eo = ((long)gq * H + gj) * a.lddgT + (long)t * a.Bp + gc;
         const uint4 v = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
         const unsigned off = gc < a.Bp && gj < H ? (unsigned)(eo * 2) : 0xFFFFFFF0u;
-        if ((SV_WAVE_DW_SIDE || SV_WAVE_DGT_SC1) && a.dgt_sc1)
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rt, off, 0, 16 /* sc1 */);
-        else
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rt, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rt, off, 0, 0);
       }
       asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
@@ -1247,9 +932,6 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     WB_MARK(3);  // 3: dG_t hand-off stores + drain + arrival
     if (!ovl && t >= 0 && a.dgT[l]) {  // dG_t^T (the dW GEMMs' operand), then the next step's operands
-      // dgt_sc1: written through (16-B sc1 stores), because the weight-gradient GEMM beside this
-      // launch reads them once iteration t - 1 has arrived (its vmcnt(0) covers these stores)
-      const __amdgpu_buffer_rsrc_t rt = sv_rsrc(a.dgT[l], a.dgt_sc1 ? (unsigned)(4L * H * a.lddgT * 2) : 0u);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int q = tid + 256 * i, gu = q >> 2, c = q & 3;
@@ -1257,10 +939,7 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
         if (gc < a.Bp && gj < H) {
           const long eo = ((long)gq * H + gj) * a.lddgT + (long)t * a.Bp + gc;
           const uint4 v = *reinterpret_cast<const uint4*>(gts + gu * LDT + 8 * c);
-          if ((SV_WAVE_DW_SIDE || SV_WAVE_DGT_SC1) && a.dgt_sc1)
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rt, (unsigned)(eo * 2), 0, 16 /* sc1 */);
-          else
-            *reinterpret_cast<uint4*>(a.dgT[l] + eo) = v;
+          *reinterpret_cast<uint4*>(a.dgT[l] + eo) = v;
         }
       }
     }

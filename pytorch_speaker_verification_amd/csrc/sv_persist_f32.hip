@@ -28,27 +28,6 @@
 #include "sv_persist_dev.h"
 #include "../../include/sv_ge2e.h"
 
-#ifndef SV_PF32_PREFETCH  // operand-prefetch helper workgroups beside the persistent backward (A/B: 0 = none)
-#define SV_PF32_PREFETCH 1
-#endif
-#ifndef SV_PF32_ACQ  // A/B diagnostic builds only (0: the product's relaxed poll)
-#define SV_PF32_ACQ 0
-#endif
-#ifndef SV_PF32_FWD_AHEAD2  // forward k-loop: A / W fragments two k-groups ahead across chunks
-#define SV_PF32_FWD_AHEAD2 1
-#endif
-#ifndef SV_PF32_OVL  // the backward's bias partials and dG^T stores under the hand-off drain (0: A/B)
-#define SV_PF32_OVL 1
-#endif
-#ifndef SV_PF32_OVL_FWD  // the forward's off-chain stores under its hand-off drain (A/B: measured slower)
-#define SV_PF32_OVL_FWD 0
-#endif
-#ifndef SV_PF32_BDMA  // the forward's ring / x-projection DMA as buffer loads with scalar bases (0: A/B)
-#define SV_PF32_BDMA 1
-#endif
-#ifndef SV_PF32_GXAUX  // A/B diagnostic: cache-policy bits of the x-projection DMA
-#define SV_PF32_GXAUX 0
-#endif
 namespace {
 constexpr int PF_BM = 64, PF_U = 32;
 constexpr int PF_KC = 64;                  // k per forward A chunk
@@ -207,29 +186,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
 #else
 #define PF_STAMP(i)
 #endif
-#ifdef SV_PF32_CHKCNT  // A/B diagnostic: the counter at the start of the launch (>= nub: not reset yet)
-  if (tid == 0) {
-    const unsigned c0 = __hip_atomic_load(cnt + rb * SV_PCNT_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (c0 >= (unsigned)nub) __hip_atomic_fetch_or(status, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (c0 >= (unsigned)nub) __hip_atomic_fetch_max(status + 1, c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-#endif
-#if SV_PF32_ACQ == 1  // A/B diagnostic: one agent-scope acquire per CU at the start of the launch
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-#elif SV_PF32_ACQ == 3  // A/B diagnostic: a system-scope acquire at the start
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-#endif
   for (int t = 0; t < T; ++t) {
     PF_STAMP(-1);
-#if SV_PF32_BDMA
     // the wave index through an opaque SGPR copy: the DMA address arithmetic stays inside the step
     // (hoisted out of the time loop, the per-lane addresses would hold registers the weights need)
     // and scalar where it is uniform -- the step's base in a buffer descriptor, a row group's LDS
@@ -254,38 +212,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
         const int rowu = 2 * (8 * gs + j), row = rowu + (lane >> 5), s = lane & 31;
         const unsigned vo =
             (__umul24((unsigned)min(b0 + row, B - 1), (unsigned)G) + (unsigned)((s >> 3) * H + j0 + 4 * (s & 7))) * 4u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (pf_lds_t)(gxs + (8 * gs + j) * 256), 16, vo, 0, 0,
-                                                 SV_PF32_GXAUX);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (pf_lds_t)(gxs + (8 * gs + j) * 256), 16, vo, 0, 0, 0);
       }
     };
-#else
-    // an opaque zero: keeps the DMA address arithmetic inside the step (hoisted out of the time
-    // loop, the per-lane addresses would hold registers the weights need)
-    int z = 0;
-    asm volatile("" : "+v"(z));
-    const int gz = g + z;
-    // ring chunk DMA: wave g fills rows 16 g .. 16 g + 15 (4 instructions of 4 rows); lane -> row
-    // 16 g + 4 j + (lane >> 4), physical slot lane & 15 holding logical slot pf_slot(row, lane & 15).
-    // Rows past B read row B - 1 (finite; rows never mix in the products and are not stored).
-    auto dma_chunk = [&](int ch, int slot) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = 16 * gz + 4 * j + (lane >> 4);
-        const float* src = h_tm + ((long)t * B + min(b0 + row, B - 1)) * H + ch * PF_KC + 4 * pf_slot(row, lane & 15);
-        __builtin_amdgcn_global_load_lds((pf_glb_t)src, (pf_lds_t)(ring + slot * PF_CH + (16 * g + 4 * j) * 256), 16,
-                                         0, 16 /* sc1 */);
-      }
-    };
-    // x-projection of step t: gxs[row][q 32 + u] = gates[t][b0 + row][q H + j0 + u]
-    auto dma_gx = [&]() {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int q = (8 * gz + j) * 64 + lane, row = q >> 5, s = q & 31;
-        const float* src = gates + (long)t * BG + (long)min(b0 + row, B - 1) * G + (s >> 3) * H + j0 + 4 * (s & 7);
-        __builtin_amdgcn_global_load_lds((pf_glb_t)src, (pf_lds_t)(gxs + (8 * g + j) * 256), 16, 0, SV_PF32_GXAUX);
-      }
-    };
-#endif
     f32x16 acc0, acc1;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
@@ -305,16 +234,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
     if (t > 0) {
       if (tid == 0) {
         persist_wait(my_cnt, (unsigned)nub * (unsigned)t, status, limit, 1u);
-#if SV_PF32_ACQ == 2  // A/B diagnostic: an agent-scope acquire after every poll
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
       }
       __syncthreads();
       PF_STAMP(0);  // 0: hand-off wait
       dma_chunk(0, 0);
       dma_chunk(1, 1);
-#if SV_PF32_FWD_AHEAD2
       // fragments two k-groups ahead, across chunk boundaries: chunk ch + 1's wait and barrier come
       // before the last two k-groups of chunk ch, so its first fragments are read while those run.
       // Waits (this wave's ops younger than chunk c + 1's four): chunk c + 2's and, for c <= 1, the
@@ -375,53 +299,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
         __builtin_amdgcn_sched_barrier(0);
       }
       pf_vmwait<0>();  // the x-projection (already waited for by the chunk waits; kept explicit)
-#else
-#pragma unroll
-      for (int ch = 0; ch < NCH; ++ch) {
-        if (ch + 2 < NCH) dma_chunk(ch + 2, (ch + 2) % PF_NB);
-        if (ch == 0) dma_gx();
-        // chunk ch landed (this wave's part): the younger DMAs stay in flight
-        if (ch <= 2)
-          pf_vmwait<16>();
-        else if (ch + 2 < NCH)
-          pf_vmwait<8>();
-        else if (ch + 2 == NCH)
-          pf_vmwait<4>();
-        else
-          pf_vmwait<0>();
-        __builtin_amdgcn_s_barrier();  // ... every wave's part; slot (ch + 2) % 4 was last read at ch - 2
-        asm volatile("" ::: "memory");  // (the barrier intrinsic is no memory op: keep the LDS reads behind it)
-        __builtin_amdgcn_sched_barrier(0);
-        if (ch == 0) {
-          PF_STAMP(1);  // 1: first chunk's DMA latency
-        }
-        const char* cbase = ring + (ch % PF_NB) * PF_CH;
-        const char* a0p = cbase + r * 256;
-        const char* a1p = cbase + (32 + r) * 256;
-        f32x4 a0 = *reinterpret_cast<const f32x4*>(a0p + 16 * pf_slot(r, hh));
-        f32x4 a1 = *reinterpret_cast<const f32x4*>(a1p + 16 * pf_slot(32 + r, hh));
-        f32x4 w = wfrag(ch * KGC);
-#pragma unroll
-        for (int kk = 0; kk < KGC; ++kk) {
-          const int kg = ch * KGC + kk;
-          f32x4 n0 = a0, n1 = a1, nw = w;
-          if (kk + 1 < KGC) {  // the next k-group's fragments, one k-group ahead
-            n0 = *reinterpret_cast<const f32x4*>(a0p + 16 * pf_slot(r, 2 * (kk + 1) + hh));
-            n1 = *reinterpret_cast<const f32x4*>(a1p + 16 * pf_slot(32 + r, 2 * (kk + 1) + hh));
-            nw = wfrag(kg + 1);
-          }
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[c], w[c], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[c], w[c], acc1, 0, 0, 0);
-          }
-          a0 = n0;
-          a1 = n1;
-          w = nw;
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-#endif
     } else {
       if constexpr (XKG == 0) {
         dma_gx();
@@ -485,10 +362,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
                                                16 /* sc1 */);
       }
     }
-    // off the chain: activations, c, h^T of step t.  SV_PF32_OVL_FWD (A/B, measured slower: DESIGN
-    // §4) with a whole row block: the h^T tile (LDS) and the 10 activation / c stores per thread go
-    // out behind the hand-off stores, before their drain, which counts them (vmcnt(10); a raw
-    // barrier: __syncthreads' fence would drain them)
+    // off the chain, after the arrival: activations, c, h^T of step t (issuing them behind the
+    // hand-off stores, before their drain, measured slower: DESIGN §4)
     auto offchain = [&]() {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
@@ -506,26 +381,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
         }
       }
     };
-    const bool ovlf = SV_PF32_OVL_FWD && b0 + PF_BM <= B;  // (uniform: every row of the block valid)
-    if (ovlf) {
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);  // (the off-chain stores stay younger than the hand-off's)
-      offchain();
-      asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-#ifdef SV_PF32_CHKCNT  // A/B diagnostic: a counter >= nub before this workgroup's first arrival was not reset
-    if (tid == 0 && t == 0 &&
-        __hip_atomic_load(my_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nub)
-      __hip_atomic_fetch_or(status, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (tid == 0 && persist_arrive_ok(fault, t == 0))
       __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     PF_STAMP(4);  // 4: hand-off stores + drain + arrival
-    if (!ovlf) offchain();
+    offchain();
     if (hT) {
       __syncthreads();
 #pragma unroll
@@ -563,24 +424,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_fwd_f32_kernel(
 constexpr int PH_BM = 32;                      // rows of a half
 
 // the helper (prefetch) workgroups of the backward: step s's operands (activations, c_{s-1}, dh_up)
-// of the XCD group's tiles, once that group's first row block has finished half 0 of step
-// s + SV_PF32_AHEAD -- ahead of the compute waves' own LDS-DMA of them (issued at the end of step s + 1)
-#ifndef SV_PF32_AHEAD
-#define SV_PF32_AHEAD 2
-#endif
-#ifndef SV_PF32_DGT_SC1  // the backward's dG^T stores written through with sc1 (r05: 7.62 -> 7.39 GB per
-#define SV_PF32_DGT_SC1 1   // launch of fetch + write, time unchanged; 0: A/B)
-#endif
-#ifndef SV_PF32_PF_HALF  // the helpers' trigger: half 1 of step s + SV_PF32_AHEAD (r05: 7.42 -> 6.74 GB per launch,
-                         // time unchanged: the lines land closer to their use and fewer are evicted first; 0: A/B)
-#define SV_PF32_PF_HALF 1
-#endif
-#ifndef SV_PF32_EDMA  // A/B builds: k-groups before the backward k-loop's end at which the next half-step's
-#define SV_PF32_EDMA 0   // operand DMA is issued into a second operand image set (r05: 12 / 24 measured slower,
-#endif                   // DESIGN §4); 0: after the half-step's hand-off, one set
-#ifndef SV_PF32_PF_SPLIT  // per-half triggers: half h's rows of step s once half h of step s + 1 is done (0: A/B)
-#define SV_PF32_PF_SPLIT 1
-#endif
+// of the XCD group's tiles, half a step ahead of the compute waves' own LDS-DMA of them (below)
 __device__ void pf32_bwd_prefetch(const float* acts, const float* c_tm, const float* dhup, int up_full, int T, int B,
                                   int H, const unsigned* cnt, int nub, int ncomp, int npf, const unsigned* status,
                                   unsigned limit, char* scratch) {
@@ -591,7 +435,6 @@ __device__ void pf32_bwd_prefetch(const float* acts, const float* c_tm, const fl
   const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
   char* dst = scratch + g * 1024;
   int* skip = reinterpret_cast<int*>(scratch + 4096);
-#if SV_PF32_PF_SPLIT
   // The compute workgroups DMA half 0's operands of step s at the end of half 1 of step s + 1 and
   // half 1's at the end of half 0 of step s (load_ew).  Each half's 32 rows are prefetched half a
   // step before that: half 0's once the group's first row block has finished half 0 of step s + 1,
@@ -638,44 +481,6 @@ __device__ void pf32_bwd_prefetch(const float* acts, const float* c_tm, const fl
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
-#else
-  const unsigned* c0 = cnt + ((l0 / nub) * 2 + SV_PF32_PF_HALF) * SV_PCNT_STRIDE;  // (row block, half) of the group's first tile
-  for (int s = T - 1; s >= 0; --s) {
-    if (tid == 0) {
-      if (s + SV_PF32_AHEAD <= T - 1) {
-        unsigned spins = 0;
-        const unsigned target = (unsigned)nub * (unsigned)(T - 1 - (s + SV_PF32_AHEAD) + 1);
-        while (__hip_atomic_load(c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
-               !__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) && ++spins < limit)
-          __builtin_amdgcn_s_sleep(8);
-      }
-      // too late for step s (the group's first row block is past half 0 of step s + 1): skip it, so
-      // a slow helper never holds the launch open
-      *skip = __hip_atomic_load(c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nub * (unsigned)(T - 1 - s);
-    }
-    __syncthreads();
-    const bool sk = *skip;
-    __syncthreads();
-    if (sk) continue;
-    const float* up = dhup ? (up_full ? dhup + (long)s * BH : (s == T - 1 ? dhup : nullptr)) : nullptr;
-    // a tile's pieces: 64 rows x (4 gates of activations + c_{s-1} + dh_up) x 8 pieces of 16 B
-    for (int L = l0 + k; L < l1; L += nk) {
-      const int ub = L % nub, rb = L / nub, j0 = ub * PF_U;
-      for (int i = tid; i < 6 * 64 * 8; i += 256) {
-        const int kind = i >> 9, r2 = min(rb * PF_BM + ((i >> 3) & 63), B - 1), pc = i & 7;
-        const float* src = nullptr;
-        if (kind < 4)
-          src = acts + (long)s * BG + (long)r2 * G + (long)kind * H + j0 + 4 * pc;
-        else if (kind == 4 && s > 0)
-          src = c_tm + (long)(s - 1) * BH + (long)r2 * H + j0 + 4 * pc;
-        else if (kind == 5 && up)
-          src = up + (long)r2 * H + j0 + 4 * pc;
-        if (src) persist_prefetch16(src, dst);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-#endif
 }
 
 template <int NKG, int P, int NV, int NL>
@@ -691,14 +496,13 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
   constexpr int LDT = PH_BM + 4;     // gts [128][LDT] (over red)
   constexpr int FBLK = NKG * 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // operand image set(s): [32][128] activations of the half-step, [32][32] c_{t-1}, [32][32] dh_up;
-  // with SV_PF32_EDMA two sets, the next half-step's filled during this one's k-loop
-  constexpr int ESET = PH_BM * 6 * PF_U;       // floats per set
+  // operand image: [32][128] activations of the half-step, [32][32] c_{t-1}, [32][32] dh_up (issuing
+  // the next half-step's into a second image during this one's k-loop measured slower: DESIGN §4)
+  constexpr int ESET = PH_BM * 6 * PF_U;       // floats per image
   float* red = reinterpret_cast<float*>(smem) + ESET;  // [4][32][LDR]
   float* gts = red;
   char* wl = reinterpret_cast<char*>(red + 4 * PH_BM * LDR);
-  float* eset[2] = {reinterpret_cast<float*>(smem),
-                    SV_PF32_EDMA ? reinterpret_cast<float*>(wl + (size_t)4 * NL * 1024) : reinterpret_cast<float*>(smem)};
+  float* const eimg = reinterpret_cast<float*>(smem);
   if ((int)blockIdx.x >= ncomp) {  // a helper workgroup: operand prefetch only
     pf32_bwd_prefetch(acts, c_tm, dhup, up_full, T, B, 8 * NKG, cnt, nub, ncomp, npf, status, limit, smem);
     return;
@@ -732,14 +536,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
   // of dh_up; absent operands written as zeros into the same slots
   // the dG^T buffer fits one 32-bit buffer descriptor with room for the dropped-store offset
   const bool dgt_fits = dgT && (long)4 * H * lddgT * 4 < (1L << 32) - 64;
-  auto load_ew = [&](int tt, int hf, int set) {
-#ifdef SV_PF32_HOTOPS  // A/B diagnostic (results invalid): every step reads step T-1's operands, cache-hot
-    tt = T - 1;
-#endif
-    float* ea = eset[set];
+  auto load_ew = [&](int tt, int hf) {
+    float* ea = eimg;
     float* ec = ea + PH_BM * 4 * PF_U;
     float* eu = ec + PH_BM * PF_U;
-#if SV_PF32_BDMA
     // (the forward's dma_chunk form: buffer loads, scalar bases, 32-bit per-lane offsets)
     int gs = __builtin_amdgcn_readfirstlane(g);
     asm volatile("" : "+s"(gs));
@@ -766,30 +566,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
                                                0, 0);
     else
       *reinterpret_cast<f32x4*>(eu + 4 * q) = zero;
-#else
-    int z = 0;
-    asm volatile("" : "+v"(z));
-    const int gz = g + z, b0 = rb * PF_BM + hf * PH_BM;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = (4 * gz + j) * 64 + lane, row = q >> 5, s = q & 31;
-      const float* src = acts + (long)tt * BG + (long)min(b0 + row, B - 1) * G + (s >> 3) * H + j0 + 4 * (s & 7);
-      __builtin_amdgcn_global_load_lds((pf_glb_t)src, (pf_lds_t)(ea + (4 * g + j) * 256), 16, 0, 0);
-    }
-    const float* up = dhup ? (up_full ? dhup + (long)tt * BH : (tt == T - 1 ? dhup : nullptr)) : nullptr;
-    const int q = gz * 64 + lane, row = q >> 3, c = q & 7;
-    const long off = (long)min(b0 + row, B - 1) * H + j0 + 4 * c;
-    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-    if (tt > 0)
-      __builtin_amdgcn_global_load_lds((pf_glb_t)(c_tm + (long)(tt - 1) * BH + off), (pf_lds_t)(ec + g * 256), 16, 0,
-                                       0);
-    else
-      *reinterpret_cast<f32x4*>(ec + 4 * q) = zero;
-    if (up)
-      __builtin_amdgcn_global_load_lds((pf_glb_t)(up + off), (pf_lds_t)(eu + g * 256), 16, 0, 0);
-    else
-      *reinterpret_cast<f32x4*>(eu + 4 * q) = zero;
-#endif
   };
   f32x4 cv[2], dcf[2];
 #pragma unroll
@@ -798,15 +574,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
     cv[hf] = *reinterpret_cast<const f32x4*>(c_tm + (long)(T - 1) * BH + (long)gb * H + j0 + 4 * quad);
     dcf[hf] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-#if SV_PF32_ACQ == 1
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-#endif
-  load_ew(T - 1, 0, 0);
-  int cs = 0;  // the current half-step's operand image set
+  load_ew(T - 1, 0);
   // threads < 128: bias-gradient partial of gate column tid over t and the row block, accumulated in
   // fp64 (320 fp32 half-step sums of a cancelling sum: in fp32 the c2 bias gradients were 8e-6 off)
   double dbs = 0.0;
@@ -833,10 +601,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
       if (t < T - 1) {
         if (tid == 0) {
           persist_wait(my_cnt, (unsigned)nub * (unsigned)(T - 1 - t), status, limit, 2u);
-#if SV_PF32_ACQ == 2
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
         }
         __syncthreads();
         PB_STAMP(0);  // 0: hand-off wait
@@ -868,25 +632,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
           w = nw;
           __builtin_amdgcn_sched_barrier(0);
         };
-        constexpr int KE = NKG - SV_PF32_EDMA;
 #pragma unroll
-        for (int kg = 0; kg < KE; ++kg) kstep(kg);
-        if (SV_PF32_EDMA) {
-          // the next half-step's operands into the other image set, behind this k-loop's last A
-          // fragment loads: hipcc's counted waits of the last k-groups do not count these LDS-DMA
-          // pieces, so they wait for them ~SV_PF32_EDMA k-groups after the issue (L2-warm: the
-          // helper workgroups fetched them), instead of the next half-step's first barrier waiting
-          if (hf == 0)
-            load_ew(t, 1, cs ^ 1);
-          else if (t > 0)
-            load_ew(t - 1, 0, cs ^ 1);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int kg = KE; kg < NKG; ++kg) kstep(kg);
-        }
+        for (int kg = 0; kg < NKG; ++kg) kstep(kg);
       }
       PB_STAMP(1);  // 1: k-loop (A fragments from the hand-off + MFMAs)
-      float* ea = eset[cs];
+      float* ea = eimg;
       float* ec = ea + PH_BM * 4 * PF_U;
       float* eu = ec + PH_BM * PF_U;
       float* dgs = ea;
@@ -957,13 +707,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
       // thread issues all 4 (pieces past Bp to an offset past the descriptor's range, dropped), so a
       // counted wait can name them
       auto dgt_stores = [&](bool exact) {
-#ifndef SV_PF32_NODGT  // A/B diagnostic (results invalid): no dG^T stores
-#if SV_PF32_DGT_SC1
         // sc1 stores: written through and dropped from this XCD's L2 (MI355X_MICROARCH.md, stores of
         // each flavour), so the 48 KB per tile per step the dW GEMMs read back much later do not
         // evict the lines the helper workgroups prefetched
         const __amdgpu_buffer_rsrc_t rdt = sv_rsrc(dgT, (unsigned)((long)4 * H * lddgT * 4));
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int p = tid + 256 * i, gu = p >> 3, c = p & 7, gbc = b0 + 4 * c;
@@ -973,23 +720,18 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
             for (int e = 0; e < 4; ++e)
               if (gbc + e >= Bq) v[e] = 0.f;
             const long eo = ((long)(gu >> 5) * H + j0 + (gu & 31)) * lddgT + (long)t * Bp + gbc;
-#if SV_PF32_DGT_SC1
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rdt,
                                                    gbc < Bpq ? (unsigned)(eo * 4) : 0xFFFFFFF0u, 0, 16 /* sc1 */);
-#else
-            if (gbc < Bpq) *reinterpret_cast<f32x4*>(dgT + eo) = v;
-#endif
           }
         }
-#endif
       };
       // the hand-off: 16 fragment blocks of 1 KB (gate q, this half, k-group 4 ub + kl); slot 0 (no
       // consumer step) only when the dx GEMM reads the fragment-order image (dg == nullptr)
-      // SV_PF32_OVL: with an arrival to make and dG^T written through one descriptor, the bias
+      // with an arrival to make and dG^T written through one descriptor, the bias
       // partials and the dG^T stores go out behind the hand-off stores, before their drain, and the
       // drain counts them (vmcnt(4): this wave's hand-off stores, older, are done; a raw barrier, as
       // __syncthreads' release fence would drain the dG^T stores too)
-      const bool ovl = SV_PF32_OVL && SV_PF32_DGT_SC1 && t > 0 && !dg && dgt_fits;
+      const bool ovl = t > 0 && !dg && dgt_fits;
       if (t > 0 || !dg) {
         const __amdgpu_buffer_rsrc_t rw = sv_rsrc(dgf + (long)t * FS, (unsigned)(FS * 4));
 #pragma unroll
@@ -1027,14 +769,13 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
           *reinterpret_cast<f32x4*>(dp + q * H) = *reinterpret_cast<const f32x4*>(dgs + erow * LDG + q * PF_U + 4 * quad);
       }
       if (!ovl) dgt_stores(false);
-      if ((hf == 0 || t > 0) && (!SV_PF32_EDMA || t == T - 1)) {  // (SV_PF32_EDMA: issued in the k-loop)
+      if (hf == 0 || t > 0) {
         __syncthreads();  // dgs / gts read by every wave before the next half-step's operands land
         if (hf == 0)
-          load_ew(t, 1, SV_PF32_EDMA ? cs ^ 1 : 0);
+          load_ew(t, 1);
         else
-          load_ew(t - 1, 0, SV_PF32_EDMA ? cs ^ 1 : 0);
+          load_ew(t - 1, 0);
       }
-      if (SV_PF32_EDMA) cs ^= 1;
       PB_STAMP(5);  // 5: off-chain (bias partials, dG / dG^T stores, next operand DMA issue)
     }
   }
@@ -1062,23 +803,14 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_bwd_f32_h2_kernel(
 // ============================================================================
 namespace {
 // weight k-groups (of 96 at H = 768) in VGPRs / LDS beside the 64 in AGPRs
-#ifndef SV_PH_BWD_P  // A/B builds: the backward's A-fragment prefetch depth
-#define SV_PH_BWD_P 12
-#endif
-#ifndef SV_PF_FWD_NV  // A/B builds: the forward's weight k-groups in VGPRs (the rest of 32 in LDS)
-#define SV_PF_FWD_NV 16
-#endif
-#ifndef SV_PH_BWD_NL  // A/B builds: the backward's weight k-groups in LDS (the rest of 32 in VGPRs)
-#define SV_PH_BWD_NL (SV_PF32_EDMA ? 23 : 24)  // (the second operand image set takes 24 KB of LDS)
-#endif
-constexpr int PF_FWD_NV = SV_PF_FWD_NV, PF_FWD_NL = 32 - SV_PF_FWD_NV, PH_BWD_NL = SV_PH_BWD_NL,
-              PH_BWD_NV = 96 - PF_NA - PH_BWD_NL,
-              PH_BWD_P = SV_PH_BWD_P;
+// (measured: 20 / 24 forward k-groups in VGPRs and backward prefetch depths 8 / 16 no faster)
+constexpr int PF_FWD_NV = 16, PF_FWD_NL = 32 - PF_FWD_NV, PH_BWD_NL = 24, PH_BWD_NV = 96 - PF_NA - PH_BWD_NL,
+              PH_BWD_P = 12;
 constexpr size_t pf_fwd_lds() {
   return (size_t)PF_NB * PF_CH + (size_t)PF_BM * 4 * PF_U * 4 + (size_t)4 * PF_FWD_NL * 1024;
 }
 constexpr size_t ph_bwd_lds() {
-  return (SV_PF32_EDMA ? 2 : 1) * ((size_t)PH_BM * 4 * PF_U * 4 + 2 * (size_t)PH_BM * PF_U * 4) +
+  return ((size_t)PH_BM * 4 * PF_U * 4 + 2 * (size_t)PH_BM * PF_U * 4) +
          (size_t)4 * PH_BM * (PF_U + 4) * 4 + (size_t)4 * PH_BWD_NL * 1024;
 }
 static_assert(pf_fwd_lds() <= 160 * 1024 && ph_bwd_lds() <= 160 * 1024, "LDS");
@@ -1106,11 +838,7 @@ int sv_persist_fwd_f32(int T, int B, int H, const float* whh, float* gates, floa
   unsigned* cnt = sync + SV_SYNC_CNT + (size_t)chan * SV_PCNT_ROWS * SV_PCNT_STRIDE;
   const int nub = H / PF_U, nrb = (B + PF_BM - 1) / PF_BM;
   const int Bp = (B + 3) & ~3;
-#ifdef SV_PF32_MEMSET  // A/B diagnostic only: the memset reset that fails under HIP-graph replay
-  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nrb * SV_PCNT_STRIDE * sizeof(unsigned), stream);
-#else
   hipError_t e = (hipError_t)sv_zero_counters(cnt, 1, 0, nrb * SV_PCNT_STRIDE, stream);
-#endif
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
   if (x_tm) {  // layer 0: the input projection inside the recurrence (F = 40 only)
@@ -1143,7 +871,7 @@ int sv_persist_bwd_f32(int T, int B, int H, const float* whhT, const float* acts
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;
   // helper workgroups on the CUs the grid leaves free, the same number per XCD (c2: 16)
-  const int ncomp = nub * nrb, npf = SV_PF32_PREFETCH ? std::min(16, (sv_stream_cus(stream) - ncomp) / 8 * 8) : 0;
+  const int ncomp = nub * nrb, npf = std::min(16, (sv_stream_cus(stream) - ncomp) / 8 * 8);
   hipLaunchKernelGGL((lstm_persist_bwd_f32_h2_kernel<96, PH_BWD_P, PH_BWD_NV, PH_BWD_NL>), dim3(ncomp + npf),
                      dim3(256), ph_bwd_lds(), stream, whhT, acts, c_tm, dhup, up_full, dg, dgT, (long)T * Bp, dgf, T,
                      Bp, B, cnt, nub, PF_XCD, sync, sv_persist_limit(), sv_persist_fault(1), dbp, ncomp, npf);

@@ -114,9 +114,6 @@ __device__ __forceinline__ void w3_mfma_lds_dma(const char* tile, int lane, cons
   }
 }
 
-#ifndef SV_W3_EARLY_X  // the next x tile's DMA inside the h-part when the layer below is ready
-#define SV_W3_EARLY_X 1
-#endif
 
 template <bool L0, bool STAMP>
 __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int rb, char* tile_x, char* tile_h,
@@ -190,18 +187,14 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#if SV_W3_EARLY_X
     unsigned xpoll = 0;
-#endif
     if constexpr (!L0) {
       // this wave's x DMA and everything older (the 12 h DMAs are the newest), then all waves'
       asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
       raw_barrier();
-#if SV_W3_EARLY_X
       // the layer below's counter for step t + 1's x tile, read now: its round trip runs under the
       // x-part, and the answer decides at the h-part whether that DMA goes there
       if (tid == 0 && t + 1 < T) xpoll = __hip_atomic_load(below, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
       w3_mfma_lds(tile_x, lane, wx, acc);
     } else {
       u32x4_t xa[WV_XS];
@@ -220,16 +213,12 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
     for (int i = 0; i < 16; ++i) acc[i] = round_bf(acc[i] + xbias);
     mark(2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if SV_W3_EARLY_X
     __shared__ int xflag;
     if (!L0 && tid == 0) xflag = (t + 1 < T && xpoll >= producers * (unsigned)(t + 2) && !(a.dbg & 2)) ? 1 : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
     raw_barrier();  // every wave past the x-part: tile_x is free
     bool xe = false;
-#if SV_W3_EARLY_X
     if constexpr (!L0) xe = xflag != 0;
-#endif
     if (xe)
       w3_mfma_lds_dma(tile_h, lane, wh, acc, rbel, t + 2, B, H, b0, tile_x, g);
     else

@@ -50,7 +50,10 @@ def split(path):
 def norm(body):
     res = []
     for ln in body:
-        ln = ln.split(";")[0].split("//")[0].rstrip() if not ln.strip().startswith("#desc") else ln
+        if not ln.strip().startswith("#desc"):
+            ln = re.sub(r"\s+#.*$", "", ln.split(";")[0].split("//")[0]).rstrip()  # device ; / host # comments
+            if ln.lstrip().startswith("#"):
+                continue
         if not ln.strip() or ln.strip().startswith(("; %bb", ".loc", ".file", ".cfi")):
             continue
         ln = re.sub(r"\.LBB\d+_(\d+)", r".LBB_\1", ln)
@@ -60,6 +63,7 @@ def norm(body):
         ln = re.sub(r"\.LCPI\d+_(\d+)", r".LCPI_\1", ln)
         ln = re.sub(r"\.L\.str(\.\d+)?", ".L.str", ln)
         ln = re.sub(r"__hip_cuid_\w+", "__hip_cuid", ln)
+        ln = re.sub(r"__hip_gpubin_handle_\w+", "__hip_gpubin_handle", ln)
         res.append(ln)
     return res
 
