@@ -818,6 +818,16 @@ def main():
         ctx.barrier()
         tf = ctx.max_over_ranks((time.perf_counter() - tf0) / args.fwd_steps)
     out["fwd_embeddings_per_sec"] = round(emb_total / tf, 1)
+    # the two readings of the metric side by side, under explicit names: `value` stays the training
+    # step's embeddings/s (the series every round reports); SURVEY §8d defines embeddings/s as
+    # N*M / t(forward, no grad) and GE2E steps/s as 1 / t(full training step)
+    out["metric_readings"] = {
+        "train_step_embeddings_per_sec": out["value"],
+        "forward_only_embeddings_per_sec": out["fwd_embeddings_per_sec"],
+        "ge2e_steps_per_sec": out["steps_per_sec"],
+        "value_is": "train_step_embeddings_per_sec (N*M*world / t(fwd + GE2E + bwd + clip + SGD))",
+        "forward_only_is": "SURVEY 8d embeddings/s: N*M*world / t(forward, no grad, save=False)",
+    }
 
     # ---- side measurements ----------------------------------------------------------------
     def side(name, Nl, Ml, Tl, prec, strong_, descr, probe=None, products="mfma_f32"):

@@ -19,6 +19,10 @@ FAMILIES = {  # json key -> kernel-name prefix
     "lstm_persist3_fwd_bf16_kernel": "void lstm_persist3_fwd_bf16_kernel<",
     "lstm_persist_bwd_f32_h2_kernel": "void lstm_persist_bwd_f32_h2_kernel<",
     "lstm_persist_fwd_f32_kernel": "void lstm_persist_fwd_f32_kernel<",
+    # the rank shapes (scripts/persist_ab.py passes c4: B = 80, T = 160; c5: B = 320, T = 180)
+    "lstm_wave3_fwd_bf16_kernel": "void lstm_wave3_fwd_bf16_kernel<",
+    "lstm_wave_bwd_bf16_kernel": "void lstm_wave_bwd_bf16_kernel<",
+    "gemm_bf16_8qf_kernel@c4": "(anonymous namespace)::gemm_bf16_8qf_kernel",
     # in-step GEMMs, per shape (c2 fp32 / c3 bf16, B = 640, T = 160, H = 768): (prefix, grid threads)
     # (r04 names: the K1 is the persistent 256p kernel, the dx GEMM reads the fragment-order A (AF = 1),
     # the dW GEMMs are split-K slabs (EPI = 1); the template's 4th argument is AF)
@@ -103,7 +107,7 @@ def main(d, gemm=False):
     data.pop("gemm_f32_256_kernel<256,32,0,1>@dx.in_step", None)  # the one-shot dx, replaced in-step by stream-K
     if gemm:
         gemm_main(d, data)
-    for tag in () if gemm else ("f32", "bf16"):
+    for tag in () if gemm else ("f32", "bf16", "c4", "c5"):
         fs = glob.glob(os.path.join(d, f"{tag}_fetch*", "**", "*counter_collection.csv"), recursive=True)
         ws = glob.glob(os.path.join(d, f"{tag}_write*", "**", "*counter_collection.csv"), recursive=True)
         if not fs or not ws:
@@ -113,7 +117,8 @@ def main(d, gemm=False):
             if k in write:
                 data[k] = {"FETCH_SIZE_KiB": round(fetch[k], 1), "WRITE_SIZE_KiB": round(write[k], 1),
                            "hbm_bytes_per_launch": int(1024 * (2 * fetch[k] + write[k])),
-                           "source": f"rocprofv3 --pmc over bench.py ({tag} step, in-step launches; "
+                           "source": f"rocprofv3 --pmc over {'bench.py' if tag in ('f32', 'bf16') else 'scripts/persist_ab.py'} "
+                                     f"({tag} step, in-step launches; "
                                      f"{os.path.basename(os.path.normpath(os.path.join(d, '..')))})"}
     data["_note"] = ("rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE in separate runs; hbm_bytes = 2*FETCH_SIZE + "
                      "WRITE_SIZE (gfx950 halves wide reads, MI355X_MICROARCH.md §HBM); FETCH_SIZE counts L2 misses "
