@@ -47,6 +47,16 @@ def main():
           {k: round(v / 1e6, 3) for k, v in sorted(conc.items())})
     for n, v in sorted(busy.items(), key=lambda x: -x[1])[:14]:
         print(f"  {n[:60]:60s} n={cnt[n]:5d} busy={v / 1e6:8.3f} ms avg={v / cnt[n] / 1e3:8.2f} us")
+    # the step in launch order: each kernel's duration and the idle gap before it (the previous
+    # kernel's end to this one's start, 0 when they overlap)
+    print("in order (gap before, duration, us):")
+    prev, gaps = s0, 0
+    for a, b, n, _ in sel:
+        g = max(0, a - prev)
+        gaps += g
+        print(f"  {g / 1e3:7.2f} {(b - a) / 1e3:9.2f}  {n[:70]}")
+        prev = max(prev, b)
+    print(f"idle gaps total {gaps / 1e3:.1f} us")
 
 
 if __name__ == "__main__":

@@ -454,7 +454,9 @@ def test_bf16_path_against_reference_fp32(cfg):
     accumulation, loss) on the inputs of the reference's own fp32 step (net_full_c2.npz: c2 =
     c3's shape; net_full_c5.npz: c5's global batch), with every deviation bounded against the
     REFERENCE's fp32 values, not the bf16 oracle: loss, embeddings, every parameter's gradient norm.
-    The bounds are the mixed-precision tolerance stated in DESIGN §7 (about 3x the measured gap)."""
+    The bounds are the mixed-precision tolerance stated in DESIGN §7, about 3-4x the gap measured on
+    MI355X (r06: emb 9.4e-4 / 8.2e-4, loss 2.7e-5 / 3.4e-6, grad norms 4.0e-3 / 1.4e-3, dw 3.6e-3 /
+    8.2e-4 at c2 / c5)."""
     s = golden(f"net_full_{cfg}.npz")
     dims = tuple(int(v) for v in s["dims"])
     net, ge2e = _build(dims, recipe.make_weights(int(s["wseed"]), *dims, scale=float(s["wscale"])))
@@ -465,13 +467,13 @@ def test_bf16_path_against_reference_fp32(cfg):
     e = emb.detach().cpu().numpy().reshape(N * M, -1)
     ref_e = s["emb"].reshape(N * M, -1) if "emb" in s.files else s["emb_rows"]
     mine = e if "emb" in s.files else e[::8]
-    _check(f"bf16_vs_ref_fp32.{cfg}.emb_abs", float(np.abs(mine - ref_e).max()), 1.5e-2)
+    _check(f"bf16_vs_ref_fp32.{cfg}.emb_abs", float(np.abs(mine - ref_e).max()), 3e-3)
     loss = ge2e(emb)
-    _check(f"bf16_vs_ref_fp32.{cfg}.loss_rel", abs(loss.item() - float(s["loss"])) / abs(float(s["loss"])), 1e-3)
+    _check(f"bf16_vs_ref_fp32.{cfg}.loss_rel", abs(loss.item() - float(s["loss"])) / abs(float(s["loss"])), 1e-4)
     loss.backward()
     gn = max((abs(float(p.grad.double().norm()) - float(s["gnorm." + k])) / float(s["gnorm." + k]), k)
              for k, p in net.named_parameters())
     print(f"\nMEASURED bf16_vs_ref_fp32.{cfg}.worst grad_norm {gn[1]}")
-    _check(f"bf16_vs_ref_fp32.{cfg}.grad_norm_rel", gn[0], 3e-2)
+    _check(f"bf16_vs_ref_fp32.{cfg}.grad_norm_rel", gn[0], 1.5e-2)
     _check(f"bf16_vs_ref_fp32.{cfg}.dw_rel", abs(ge2e.w.grad.item() - float(s["dw0"])) / max(1.0, abs(float(s["dw0"]))),
-           3e-2)
+           1.5e-2)
