@@ -14,7 +14,7 @@ FAMILIES = {  # json key -> kernel-name prefix
     "lstm_step_bwd_v2_kernel": "void lstm_step_bwd_v2_kernel<",
     "lstm_step_fwd_v2_kernel": "void lstm_step_fwd_v2_kernel<32, 101",
     "lstm_persist2_bwd_bf16_kernel": "void lstm_persist2_bwd_bf16_kernel<",
-    "lstm_persist2_fwd_bf16_kernel": "void lstm_persist2_fwd_bf16_kernel<48, 64, 0>",
+    "lstm_persist2_fwd_bf16_kernel": "void lstm_persist2_fwd_bf16_kernel<48, 32, 0>",  # (c5 rank: 32 x 32 tiles)
     "lstm_persist3_bwd_bf16_kernel": "void lstm_persist3_bwd_bf16_kernel<",
     "lstm_persist3_fwd_bf16_kernel": "void lstm_persist3_fwd_bf16_kernel<",
     "lstm_persist_bwd_f32_h2_kernel": "void lstm_persist_bwd_f32_h2_kernel<",
@@ -113,10 +113,14 @@ def main(d, gemm=False):
         if not fs or not ws:
             continue
         fetch, write = per_launch(fs[0], "FETCH_SIZE", FAMILIES), per_launch(ws[0], "WRITE_SIZE", FAMILIES)
-        for k in fetch:
-            if k in write:
-                data[k] = {"FETCH_SIZE_KiB": round(fetch[k], 1), "WRITE_SIZE_KiB": round(write[k], 1),
-                           "hbm_bytes_per_launch": int(1024 * (2 * fetch[k] + write[k])),
+        for k0 in fetch:
+            if k0 not in write:
+                continue
+            # the rank passes' GEMMs (other shapes than c2 / c3's) under their own keys
+            k = f"{tag}:{k0}" if tag in ("c4", "c5") and "@" in k0 and not k0.endswith("@c4") else k0
+            if True:
+                data[k] = {"FETCH_SIZE_KiB": round(fetch[k0], 1), "WRITE_SIZE_KiB": round(write[k0], 1),
+                           "hbm_bytes_per_launch": int(1024 * (2 * fetch[k0] + write[k0])),
                            "source": f"rocprofv3 --pmc over {'bench.py' if tag in ('f32', 'bf16') else 'scripts/persist_ab.py'} "
                                      f"({tag} step, in-step launches; "
                                      f"{os.path.basename(os.path.normpath(os.path.join(d, '..')))})"}
