@@ -831,8 +831,13 @@ def main():
 
     # ---- side measurements ----------------------------------------------------------------
     def side(name, Nl, Ml, Tl, prec, strong_, descr, probe=None, products="mfma_f32"):
-        d, l_, _, pr, _ = run_steps(ctx, Nl, Ml, Tl, prec, args.steps, args.warmup, 2235, probe=probe,
-                                    products=products)
+        # the step time without timing probes (each probe event record idles the GPU ~6 us between
+        # two kernels: 4 - 12 per step at these shapes), then, for the roofline entries, a second
+        # run of the same steps with the probes (its time is reported beside, probed_ms_per_step)
+        d, l_, _, _, _ = run_steps(ctx, Nl, Ml, Tl, prec, args.steps, args.warmup, 2235, products=products)
+        pr, dp = None, None
+        if probe:
+            dp, _, _, pr, _ = run_steps(ctx, Nl, Ml, Tl, prec, args.steps, 1, 2235, probe=probe, products=products)
         ms = d / args.steps * 1e3
         _, fl = step_flops(Nl * Ml, Tl, F, H, P, L)
         tot = Nl * Ml * world
@@ -842,6 +847,8 @@ def main():
              "step_tflops_per_gpu": round(fl / (ms * 1e-3) / 1e12, 2),
              "step_mfma_frac": round(fl / (ms * 1e-3) / 1e12 /
                                      (MI355X_FP32_MFMA_TFLOPS if prec == "f32" else MI355X_BF16_MFMA_TFLOPS), 4)}
+        if dp is not None:
+            o["probed_ms_per_step"] = round(dp / args.steps * 1e3, 3)
         out[name] = o
         return o, pr
 

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SV_ABI_VERSION 8
+#define SV_ABI_VERSION 9
 int sv_abi_version(void);
 
 /* ---- fp32 product modes (`products` argument of sv_gemm_f32 / sv_lstm_stack_fwd / _bwd; every
@@ -54,12 +54,19 @@ int sv_abi_version(void);
  *   SV_SCHED_PER_STEP   per-step launches, layer-pipelined over the side streams (bit-identical
  *                       to the persistent per-layer schedule);
  *   SV_SCHED_PERSIST    persistent per-layer recurrences for any H they support (64, 96, 768),
- *                       not only H = 768. */
+ *                       not only H = 768.
+ * Both precisions:
+ *   SV_SCHED_NO_EVENTS  (ABI v9) the stack backward's persistent / wavefront schedules record no
+ *                       per-layer completion events into `ev` (set it when nothing waits on them,
+ *                       i.e. no data-parallel gradient buckets: each event record leaves the GPU
+ *                       idle for ~6 us between two kernels); the per-step schedule, whose side
+ *                       streams synchronise through the events, ignores it. */
 #define SV_SCHED_AUTO 0
 #define SV_SCHED_PER_LAYER 1
 #define SV_SCHED_PER_STEP 2
 #define SV_SCHED_PERSIST 4
-#define SV_SCHED_MASK 7
+#define SV_SCHED_NO_EVENTS 8
+#define SV_SCHED_MASK 15
 
 /* ---- dense fp32 MFMA GEMM (used by every op below; exported for tests) -----------------
  * C[M,N] = op(A) op(B) (+ bias0[n] + bias1[n]) (+ beta C).
@@ -331,6 +338,13 @@ int sv_persist_bwd_ok(int B, int H);
 int sv_wave_ok(int L, int T, int B, int F, int H);
 size_t sv_persist_bwd_scratch(int T, int B, int H);
 int sv_status_poison(const void* sync, float* x, int n, hipStream_t stream);
+/* (ABI v9) sv_status_poison's poisoning of x[0..n) (n may be 0) plus a report of the status word
+ * to the host without a copy: one 8-byte store of ((seq << 32) | status) into host_slot_dev, the
+ * device address (sv_host_device_ptr = hipHostGetDevicePointer) of a caller-owned, 8-byte aligned
+ * slot of pinned host memory; the host knows step `seq` is done when the slot's high word equals
+ * seq.  Replaces the device->pinned copy + event of the old check. */
+int sv_status_report(const void* sync, float* x, int n, void* host_slot_dev, unsigned seq, hipStream_t stream);
+int sv_host_device_ptr(void* host, void** dev);
 /* data-parallel status agreement (a rank whose recurrence timed out must stop every rank's
  * update): sv_status_to_flag writes the status's forward / backward bits as 0/1 floats into
  * flag[0..1], two words of the gradient buffer that the SUM all-reduce carries; sv_status_merge

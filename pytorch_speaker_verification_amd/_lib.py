@@ -16,11 +16,12 @@ LIB_PATH = os.path.join(_HERE, "libsv_ge2e.so")
 # the fault-injection test build (Makefile `faultinj`): the same library plus sv_test_set_fault;
 # only tests load it, through use_library() before the first call
 FAULT_LIB_PATH = os.path.join(_HERE, "libsv_ge2e_faultinj.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 SV_DTYPE_F32, SV_DTYPE_BF16 = 0, 1  # include/sv_ge2e.h
 
 # schedule flags of the bf16 stack (include/sv_ge2e.h SV_SCHED_*), by name
 SCHEDULES = {"auto": 0, "per_layer": 1, "per_step": 2, "persist": 5}  # persist: per-layer persistent, any H
+SV_SCHED_NO_EVENTS = 8  # the stack backward records no per-layer completion events (nothing waits on them)
 
 
 def schedule_flags(schedule):
@@ -115,6 +116,8 @@ SIGNATURES = {
     "sv_wave_ok": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "sv_persist_bwd_scratch": (_c_size_t, [_c_int, _c_int, _c_int]),
     "sv_status_poison": (_c_int, [_P, _P, _c_int, _P]),
+    "sv_status_report": (_c_int, [_P, _P, _c_int, _P, ctypes.c_uint, _P]),
+    "sv_host_device_ptr": (_c_int, [_P, _P]),
     "sv_status_to_flag": (_c_int, [_P, _P, _P]),
     "sv_status_merge": (_c_int, [_P, _P, _P]),
     "sv_dvector_bf16_workspace": (_c_size_t, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int]),
@@ -198,35 +201,68 @@ class PersistentRecurrenceError(RuntimeError):
 class PersistStatus:
     """A caller-owned sync block for the persistent recurrences (sv_sync_size bytes, zeroed once)
     plus a non-blocking check of its sticky status word: ``arm()`` after enqueueing work that
-    uses the block issues an async device->pinned copy of the word behind it; ``poll()`` raises
-    PersistentRecurrenceError for any completed copy that saw a nonzero status (``wait=True``
+    uses the block issues an async device->pinned copy of the word behind it; ``report(x)``
+    (the training step's end) instead poisons x on a timeout and has one kernel store the word
+    into a ring of pinned host slots (sv_status_report: no copy, no event); ``poll()`` raises
+    PersistentRecurrenceError for any completed check that saw a nonzero status (``wait=True``
     first waits for all of them)."""
+
+    RING = 64
 
     def __init__(self, device):
         words = (int(lib().sv_sync_size()) + 3) // 4
         self.block = torch.zeros(words, dtype=torch.int32, device=device)
         self._pending = []
+        self._ring = None  # pinned host slots of sv_status_report, set up on first use
+        self._seq = 0
 
     def ptr(self):
         return self.block.data_ptr()
+
+    def report(self, x):
+        """x (fp32, contiguous, on the block's device) := NaN if the status is set, and the status
+        reported into the next host slot, both stream-ordered on x's stream (sv_status_report)."""
+        if self._ring is None:
+            ring = torch.zeros(self.RING, dtype=torch.int64, pin_memory=True)
+            dev = ctypes.c_void_p()
+            rc = lib().sv_host_device_ptr(ctypes.c_void_p(ring.data_ptr()), ctypes.byref(dev))
+            if rc != 0 or not dev.value:
+                raise NativeLibraryError(f"sv_host_device_ptr failed ({rc}): pinned host memory is not mapped")
+            self._ring, self._ring_dev = ring, dev.value
+        if sum(1 for p in self._pending if p[0] == "slot") >= self.RING - 1:
+            self.poll(wait=True)  # every slot in use: the host is a whole ring ahead of the device
+        self._seq = self._seq % 0xFFFFFFFF + 1  # (never 0: a fresh slot reads 0)
+        k = self._seq % self.RING
+        call("sv_status_report", self.ptr(), ptr(x), x.numel(), self._ring_dev + 8 * k, self._seq, stream_of(x))
+        self._pending.append(("slot", k, self._seq))
 
     def arm(self):
         host = torch.empty(1, dtype=torch.int32, pin_memory=True)
         host.copy_(self.block[:1], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.block.device))
-        self._pending.append((ev, host))
+        self._pending.append(("copy", ev, host))
 
     def poll(self, wait=False):
         keep = []
         bad = 0
-        for ev, host in self._pending:
+        if wait and any(p[0] == "slot" for p in self._pending):
+            torch.cuda.synchronize(self.block.device)
+        for p in self._pending:
+            if p[0] == "slot":
+                v = int(self._ring[p[1]])
+                if (v >> 32) == p[2]:
+                    bad |= v & 0xFFFFFFFF
+                else:
+                    keep.append(p)
+                continue
+            _, ev, host = p
             if wait:
                 ev.synchronize()
             if ev.query():
                 bad |= int(host[0])
             else:
-                keep.append((ev, host))
+                keep.append(p)
         self._pending = keep
         if bad:
             which = " and ".join(n for b, n in ((1, "forward"), (2, "backward")) if bad & b)

@@ -1201,9 +1201,10 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
   const int TBp = T * Bp;
   const long ldhT = (long)(T + 1) * Bp;
   const size_t per = carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
-  hipEvent_t ev_start = ev[L * nch + L];
-  hipError_t e = hipEventRecord(ev_start, main);
-  if (e != hipSuccess) return (int)e;
+  hipError_t e;
+  // the per-layer completion events (a caller's gradient buckets wait on them) of the persistent and
+  // wavefront schedules; SV_SCHED_NO_EVENTS: nobody waits, record none (each record idles the GPU)
+  const bool evs = !(schedule & SV_SCHED_NO_EVENTS);
   if (sched_wave(schedule, H) && sv_wave_bwd_fits(L, B, H, sv_stream_cus(main))) {
     if (!sync) return SV_EARG;
     // layer-wavefront schedule: every layer's recurrence and upstream gradient dx in one launch
@@ -1271,13 +1272,13 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     if (fullk) {
       hipLaunchKernelGGL(gemm_bf16_8qf_kernel, dim3(f.nsw + fP), dim3(512), G256_LDS, main, f);
       SV_LAUNCH_CHECK();
-      for (int l = L - 1; l >= 1; --l)
+      for (int l = L - 1; l >= 1 && evs; --l)
         if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
       const BBwdWs ws = carve_bbwd((char*)workspace, T, B, std::max(F, H), H);
       if ((rc = sv_gemm_bf16(4 * H, F, TBp, dgT[0], TBp, xT[0], ld_xT[0], dw_ih[0], F, nullptr, nullptr, 0.f, ws.gws,
                              main)))
         return rc;
-      if ((e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
+      if (evs && (e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
       return SV_OK;
     }
     for (int l = L - 1; l >= 0; --l) {
@@ -1288,7 +1289,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
         return rc;
       // layer l's gradients are complete: its all-reduce bucket (grad_ready) overlaps the lower
       // layers' weight-gradient GEMMs (the recurrences are all done)
-      if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
+      if (evs && (e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
     }
     return SV_OK;
   }
@@ -1324,7 +1325,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       // the last recurrence is done, so collectives never share the device with a persistent launch
       // (whose grid must be co-resident; a concurrent RCCL kernel would hold CUs it waits for) but
       // overlap layer 0's weight-gradient GEMMs
-      for (int k = 1; l == 0 && k < L; ++k)
+      for (int k = 1; l == 0 && k < L && evs; ++k)
         if ((e = hipEventRecord(ev[L * nch + k], main)) != hipSuccess) return (int)e;
       if (afr) {
         if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H, sv_stream_cus(main)), ws.wihT, bf16_wiht_ld(H), dx[l],
@@ -1339,10 +1340,12 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
                              ws.gws, main);
       if (rc) return rc;
     }
-    if ((e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
+    if (evs && (e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
     return SV_OK;
   }
   // per-step schedule, layer-pipelined (sv_lstm_stack_bwd, sv_lstm.hip): each layer on side[l]
+  hipEvent_t ev_start = ev[L * nch + L];
+  if ((e = hipEventRecord(ev_start, main)) != hipSuccess) return (int)e;
   const dim3 grid((H + BF_U - 1) / BF_U, (B + BF_BM - 1) / BF_BM);
   for (int l = L - 1; l >= 0; --l) {
     hipStream_t s = side[l];

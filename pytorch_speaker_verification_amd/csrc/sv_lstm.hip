@@ -1239,7 +1239,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
       // the last recurrence is done, so a collective never shares the device with a persistent
       // launch (a concurrent RCCL kernel would hold CUs its grid waits for) but overlaps layer 0's
       // weight-gradient GEMMs
-      for (int k = 1; l == 0 && k < L; ++k)
+      for (int k = 1; l == 0 && k < L && !(schedule & SV_SCHED_NO_EVENTS); ++k)
         if ((e = hipEventRecord(ev[L * nch + k], main)) != hipSuccess) return (int)e;
       if (l > 0 && abn > 0 && (rc = gemm_f32_dx_afrag(abn, dgf, T, B, H, ws.wihT, f32_wiht_ld(H), Fl, dx[l], main, skws))) return rc;
       if (l > 0 && abn < 0 &&
@@ -1254,7 +1254,7 @@ extern "C" int sv_lstm_stack_bwd(int L, int T, int B, int F, int H, const float*
         return rc;
       // (bias gradients: summed inside the persistent recurrence, finalized after it)
     }
-    if ((e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
+    if (!(schedule & SV_SCHED_NO_EVENTS) && (e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
     return SV_OK;
   }
   hipEvent_t ev_start = ev[L * nch + L];

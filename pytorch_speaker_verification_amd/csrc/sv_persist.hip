@@ -1284,6 +1284,34 @@ extern "C" int sv_status_poison(const void* sync, float* x, int n, hipStream_t s
   return SV_OK;
 }
 
+// sv_status_poison + the status word reported to the host without a copy or an event (ABI v9):
+// thread 0 stores ((seq << 32) | status) into a slot of caller-owned pinned host memory mapped into
+// the device's address space (system scope, release), so the host reads the outcome of step `seq`
+// by comparing the slot's high word -- the device->pinned copy and the event it needed idled the
+// GPU ~10 us per step
+__global__ void status_report_kernel(const unsigned* __restrict__ status, float* __restrict__ x, int n,
+                                     unsigned long long* slot, unsigned seq) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned s = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (i < n && s) x[i] = __builtin_nanf("");
+  if (i == 0)
+    __hip_atomic_store(slot, ((unsigned long long)seq << 32) | s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+extern "C" int sv_status_report(const void* sync, float* x, int n, void* host_slot_dev, unsigned seq,
+                                hipStream_t stream) {
+  if (!sync || !host_slot_dev || n < 0 || (n > 0 && !x) || ((uintptr_t)host_slot_dev & 7)) return SV_EARG;
+  hipLaunchKernelGGL(status_report_kernel, dim3(n > 0 ? (n + 255) / 256 : 1), dim3(256), 0, stream,
+                     reinterpret_cast<const unsigned*>(sync), x, n,
+                     reinterpret_cast<unsigned long long*>(host_slot_dev), seq);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+// the device address of pinned host memory (hipHostGetDevicePointer), for sv_status_report's slot
+extern "C" int sv_host_device_ptr(void* host, void** dev) {
+  if (!host || !dev) return SV_EARG;
+  return (int)hipHostGetDevicePointer(dev, host, 0);
+}
+
 // data-parallel status agreement: flag[0..1] := the status's forward / backward bits as floats
 // (two words of the SUM-reduced gradient buffer: a sum over ranks stays nonzero iff any rank set
 // the bit), then status |= the reduced bits on every rank

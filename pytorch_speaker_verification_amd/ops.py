@@ -16,7 +16,8 @@ import ctypes
 
 import torch
 
-from ._lib import SV_DTYPE_BF16, SV_DTYPE_F32, PersistStatus, call, lib, ptr, require_device, schedule_flags, stream_of
+from ._lib import (SV_DTYPE_BF16, SV_DTYPE_F32, SV_SCHED_NO_EVENTS, PersistStatus, call, lib, ptr, require_device,
+                   schedule_flags, stream_of)
 
 # timesteps per chunk of the layer-pipelined schedules (measured at c2: 16 / 24 / 32 / 48 / 64 ->
 # 69.3 / 69.7 / 69.1 / 69.5 / 69.6 ms per step)
@@ -224,7 +225,9 @@ def embedder_backward(st, demb, layers, w_p, grads=None, need_dx=False, grad_rea
     (``schedule``, ``status`` as embedder_forward) probe[2l] / [2l+1] bracket layer l's launch and
     kstamp is not written."""
     prod = _products(products)
-    sched = schedule_flags(schedule)
+    # no grad_ready: nothing waits on the per-layer completion events, so the persistent
+    # schedule records none (include/sv_ge2e.h SV_SCHED_NO_EVENTS)
+    sched = schedule_flags(schedule) | (0 if grad_ready else SV_SCHED_NO_EVENTS)
     demb = demb.contiguous()
     require_device(demb)
     T, B, H, P = st.T, st.B, st.H, st.P
@@ -419,7 +422,7 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
     input gradient dx [B,T,F] (returns (grads, dx)), formed by the per-layer kernels, whose layer-0
     step adds the dx = dG W_ih GEMM (bf16 operands, fp32 accumulation) the stacked schedules skip;
     the per-layer per-step kernels are bit-identical to the persistent ones."""
-    sched = schedule_flags(schedule)
+    sched = schedule_flags(schedule) | (0 if grad_ready else SV_SCHED_NO_EVENTS)  # (as embedder_backward)
     demb = demb.contiguous()
     require_device(demb)
     T, B, H, P = st.T, st.B, st.H, st.P

@@ -71,6 +71,10 @@ class SpeechEmbedder(nn.Module):
         # bf16 stack schedule: "auto" (measured default), "per_layer", "per_step" or "persist"
         # (the SV_SCHED_* flags of include/sv_ge2e.h, passed on every call)
         self.schedule = "auto"
+        # "function": ops.EmbedderFunction (the backward reads the forward's saved activations);
+        # "library": the torch.library op sv::speech_embedder (library.py: visible to fake tensors,
+        # make_fx and torch.compile; its backward recomputes the forward, fp32 exact products only)
+        self.dispatch = "function"
 
     def flat_params(self):
         """Parameters in kernel order: (w_ih, w_hh, b_ih, b_hh) per layer, then w_p, b_p."""
@@ -84,8 +88,12 @@ class SpeechEmbedder(nn.Module):
         host = None if params[0].is_cuda else params[0].device
         if host is not None:  # CPU-resident module: differentiable copies to the GPU and back
             params = [p.to(dev) for p in params]
-        out = EmbedderFunction.apply(x.float().to(dev).contiguous(), self.LSTM_stack.num_layers, self.precision,
-                                     self.f32_products, self.schedule, *params)
+        if self.dispatch == "library":
+            from . import library
+            out = library.speech_embedder(x.float().to(dev).contiguous(), params, self.precision, self.schedule)
+        else:
+            out = EmbedderFunction.apply(x.float().to(dev).contiguous(), self.LSTM_stack.num_layers, self.precision,
+                                         self.f32_products, self.schedule, *params)
         return out if host is None else out.to(host)
 
 
@@ -100,11 +108,17 @@ class GE2ELoss(nn.Module):
         self.w = nn.Parameter(torch.tensor(10.0).to(device), requires_grad=True)
         self.b = nn.Parameter(torch.tensor(-5.0).to(device), requires_grad=True)
         self.device = device
+        self.dispatch = "function"  # or "library": the torch.library op sv::ge2e_loss (library.py)
 
     def forward(self, embeddings):
         dev = compute_device(self.w)
+        if self.dispatch == "library":
+            from . import library
+            fn = library.ge2e_loss
+        else:
+            fn = GE2EFunction.apply
         if self.w.is_cuda:
-            loss, _ = GE2EFunction.apply(embeddings.to(dev).contiguous(), self.w, self.b)
+            loss, _ = fn(embeddings.to(dev).contiguous(), self.w, self.b)
             return loss
-        loss, _ = GE2EFunction.apply(embeddings.to(dev).contiguous(), self.w.to(dev), self.b.to(dev))
+        loss, _ = fn(embeddings.to(dev).contiguous(), self.w.to(dev), self.b.to(dev))
         return loss.to(self.w.device)

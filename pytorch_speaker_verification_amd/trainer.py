@@ -257,6 +257,6 @@ class GE2ETrainer:
         clip_sgd_step2_(self.flat_p[:n], self.flat_g[:n], self.clip_net, self.flat_p[n:n + 4], self.flat_g[n:n + 4],
                         self.clip_wb, self.lr, self.write_grads, status=self.status)
         loss = loss.clone() if dp else loss  # (not a view of flat_g, which the next step reuses)
-        call("sv_status_poison", self.status.ptr(), ptr(loss), 1, stream_of(loss))
-        self.status.arm()
+        # NaN loss on a timeout, and the status word to a pinned host slot (no copy, no event)
+        self.status.report(loss)
         return loss
