@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SV_ABI_VERSION 9
+#define SV_ABI_VERSION 10
 int sv_abi_version(void);
 
 /* ---- fp32 product modes (`products` argument of sv_gemm_f32 / sv_lstm_stack_fwd / _bwd; every
@@ -60,13 +60,18 @@ int sv_abi_version(void);
  *                       per-layer completion events into `ev` (set it when nothing waits on them,
  *                       i.e. no data-parallel gradient buckets: each event record leaves the GPU
  *                       idle for ~6 us between two kernels); the per-step schedule, whose side
- *                       streams synchronise through the events, ignores it. */
+ *                       streams synchronise through the events, ignores it.
+ * bf16 stack backward only:
+ *   SV_SCHED_WT_READY   (ABI v10) the workspace already holds the bf16 weight transposes, written by
+ *                       sv_lstm_weights_bf16 (below) from the same weights into the same workspace:
+ *                       no transpose launch (the fp32 backward ignores it). */
 #define SV_SCHED_AUTO 0
 #define SV_SCHED_PER_LAYER 1
 #define SV_SCHED_PER_STEP 2
 #define SV_SCHED_PERSIST 4
 #define SV_SCHED_NO_EVENTS 8
-#define SV_SCHED_MASK 15
+#define SV_SCHED_WT_READY 16
+#define SV_SCHED_MASK 31
 
 /* ---- dense fp32 MFMA GEMM (used by every op below; exported for tests) -----------------
  * C[M,N] = op(A) op(B) (+ bias0[n] + bias1[n]) (+ beta C).
@@ -256,6 +261,16 @@ int sv_cast_bf16(const float* x, sv_bf16* y, long n, hipStream_t stream);
 int sv_cast_bf16_batch(int n, const float* const* x, sv_bf16* const* y, const long* count, hipStream_t stream);
 int sv_transpose_cast_bf16(const float* src, long ld_src, int R, int C, sv_bf16* dst, long ld_dst,
                            hipStream_t stream);
+/* (ABI v10) the bf16 stack's input in one launch: frames x [B,T,F] (F <= 64) -> x_bf [T,B,F] and,
+ * if xT != NULL, xT [F][T*Bp] (column t*Bp + b = x[b,t,:], columns b in [B, Bp) zero) */
+int sv_frames_to_bf16(const float* x, int B, int T, int F, sv_bf16* x_bf, sv_bf16* xT, int Bp, hipStream_t stream);
+/* (ABI v10) every layer's bf16 weights in one launch, each fp32 weight read once: w_ih_bf[l] /
+ * w_hh_bf[l] = bf16(w_ih[l]) / bf16(w_hh[l]) (row-major, the stack forward's operands) and, if
+ * bwd_workspace != NULL (sv_lstm_bwd_workspace(SV_DTYPE_BF16, L, T, B, F, H) bytes), the bf16
+ * transposes the stack backward reads, inside that workspace: pass it to sv_lstm_bwd with
+ * SV_SCHED_WT_READY and the backward launches no transposes. */
+int sv_lstm_weights_bf16(int L, int T, int B, int F, int H, const float* const* w_ih, const float* const* w_hh,
+                         sv_bf16* const* w_ih_bf, sv_bf16* const* w_hh_bf, void* bwd_workspace, hipStream_t stream);
 /* x_bf [T,B,F]; writes gates (bf16), c_tm/h_tm (fp32) plus h_bf [T+1,B,H] and hT [H,(T+1)Bp] (bf16) */
 int sv_lstm_layer_fwd_bf16(const sv_bf16* x_bf, int T, int B, int F, int H, const sv_bf16* w_ih_bf,
                            const sv_bf16* w_hh_bf, const float* b_ih, const float* b_hh, sv_bf16* gates, float* c_tm,

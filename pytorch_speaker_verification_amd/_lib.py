@@ -16,12 +16,13 @@ LIB_PATH = os.path.join(_HERE, "libsv_ge2e.so")
 # the fault-injection test build (Makefile `faultinj`): the same library plus sv_test_set_fault;
 # only tests load it, through use_library() before the first call
 FAULT_LIB_PATH = os.path.join(_HERE, "libsv_ge2e_faultinj.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 SV_DTYPE_F32, SV_DTYPE_BF16 = 0, 1  # include/sv_ge2e.h
 
 # schedule flags of the bf16 stack (include/sv_ge2e.h SV_SCHED_*), by name
 SCHEDULES = {"auto": 0, "per_layer": 1, "per_step": 2, "persist": 5}  # persist: per-layer persistent, any H
 SV_SCHED_NO_EVENTS = 8  # the stack backward records no per-layer completion events (nothing waits on them)
+SV_SCHED_WT_READY = 16  # the bf16 backward workspace already holds sv_lstm_weights_bf16's transposes
 
 
 def schedule_flags(schedule):
@@ -96,6 +97,8 @@ SIGNATURES = {
     "sv_cast_bf16": (_c_int, [_P, _P, _c_long, _P]),
     "sv_cast_bf16_batch": (_c_int, [_c_int, _P, _P, _P, _P]),
     "sv_transpose_cast_bf16": (_c_int, [_P, _c_long, _c_int, _c_int, _P, _c_long, _P]),
+    "sv_frames_to_bf16": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _P, _c_int, _P]),
+    "sv_lstm_weights_bf16": (_c_int, [_c_int] * 5 + [_P] * 6),
     "sv_lstm_layer_fwd_bf16": (_c_int, [_P, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_lstm_stack_fwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                         _P, _c_int, _P, _P, _P, _P, _P, _c_int]),

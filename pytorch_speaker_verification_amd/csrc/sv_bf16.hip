@@ -134,7 +134,8 @@ __global__ void cast_bf16_batch_kernel(const CastBatch cb) {
 }
 struct TCastBatch {
   const float* src[8];
-  bf16_t* dst[8];
+  bf16_t* dst[8];   // transposed copy (null: none)
+  bf16_t* dstr[8];  // row-major copy, row stride C (null: none; ABI v10, sv_lstm_weights_bf16)
   long lds[8], ldd[8];
   int R[8], C[8], tx[8];  // column tiles per matrix
   int tile0[9];           // 64 x 64 tile prefix sums
@@ -172,10 +173,21 @@ __global__ __launch_bounds__(256) void transpose_cast_batch_kernel(const TCastBa
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) tile[lr + 16 * i][lc + e] = v[e];
+      if (tb.dstr[b] && r < R) {  // the row-major copy straight from the registers
+        bf16_t* d = tb.dstr[b] + (long)r * C + c;
+        if (vec && c + 3 < C) {
+          *reinterpret_cast<uint2*>(d) = pack_bf4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (c + e < C) d[e] = to_bf(v[e]);
+        }
+      }
     }
   }
-  __syncthreads();
   bf16_t* dst = tb.dst[b];
+  if (!dst) return;  // uniform per workgroup: no barrier skipped by part of it
+  __syncthreads();
   const int lr8 = (threadIdx.x & 7) * 8, lcr = threadIdx.x >> 3;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -885,25 +897,68 @@ extern "C" int sv_cast_bf16_batch(int n, const float* const* x, bf16_t* const* y
   return SV_OK;
 }
 
-// the transpose-casts of up to 8 matrices in one launch (dst[c ldd + r] = bf16(src[r lds + c]))
+// the transpose-casts of up to 8 matrices in one launch (dst[c ldd + r] = bf16(src[r lds + c]));
+// dstr (optional, per matrix): also the row-major cast dstr[r C + c], from the same read; a null
+// dst[i] with a dstr[i]: the row-major cast alone
 int transpose_cast_bf16_batch(int n, const float* const* src, const long* lds, const int* R, const int* C,
-                              bf16_t* const* dst, const long* ldd, hipStream_t stream) {
+                              bf16_t* const* dst, const long* ldd, hipStream_t stream, bf16_t* const* dstr = nullptr) {
   if (n <= 0 || n > 8) return SV_EARG;
   TCastBatch tb{};
   tb.n = n;
   for (int i = 0; i < n; ++i) {
-    if (!src[i] || !dst[i] || R[i] <= 0 || C[i] <= 0) return SV_EARG;
+    if (!src[i] || !(dst[i] || (dstr && dstr[i])) || R[i] <= 0 || C[i] <= 0) return SV_EARG;
     tb.src[i] = src[i];
     tb.dst[i] = dst[i];
+    tb.dstr[i] = dstr ? dstr[i] : nullptr;
     tb.lds[i] = lds[i];
     tb.ldd[i] = ldd[i];
     tb.R[i] = R[i];
     tb.C[i] = C[i];
     tb.tx[i] = (C[i] + 63) / 64;
     tb.tile0[i + 1] = tb.tile0[i] + tb.tx[i] * ((R[i] + 63) / 64);
-    if (lds[i] % 4 == 0 && ldd[i] % 8 == 0 && !((uintptr_t)src[i] & 15) && !((uintptr_t)dst[i] & 15)) tb.vec |= 1u << i;
+    const bool rv = !tb.dstr[i] || (C[i] % 4 == 0 && !((uintptr_t)tb.dstr[i] & 7));
+    if (lds[i] % 4 == 0 && ldd[i] % 8 == 0 && !((uintptr_t)src[i] & 15) && !((uintptr_t)dst[i] & 15) && rv)
+      tb.vec |= 1u << i;
   }
   hipLaunchKernelGGL(transpose_cast_batch_kernel, dim3(tb.tile0[n]), dim3(256), 0, stream, tb);
+  SV_LAUNCH_CHECK();
+  return SV_OK;
+}
+
+// the bf16 stack's input in one launch (ABI v10; was to_time_major + a cast + a transpose-cast, and
+// T transpose-casts when B % 8 != 0): frames x [B,T,F] fp32 -> x_bf [T,B,F] and, when xT is given,
+// xT [F][T Bp] with column t Bp + b = x[b,t,:] (padding columns b in [B, Bp) zero) -- layer 0's
+// dW_ih operand.  Workgroup (t, 64 rows b): the tile goes through LDS so both stores coalesce.
+__global__ __launch_bounds__(256) void frames_to_bf16_kernel(const float* __restrict__ x, int B, int T, int F, int Bp,
+                                                             bf16_t* __restrict__ x_bf, bf16_t* __restrict__ xT) {
+  __shared__ float tile[64][65];  // [b][f], F <= 64
+  const int t = blockIdx.y, b0 = blockIdx.x * 64, tid = threadIdx.x;
+  // 16 predicated loads per thread, all in flight before the first LDS write (a rolled loop
+  // waited for each load on its own); thread -> (row tid / 64 + 4 i, column tid % 64)
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int b = (tid >> 6) + 4 * i, f = tid & 63;
+    v[i] = (f < F && b0 + b < B) ? x[((long)(b0 + b) * T + t) * F + f] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) tile[(tid >> 6) + 4 * i][tid & 63] = v[i];
+  __syncthreads();
+  for (int i = tid; i < 64 * F; i += 256) {
+    const int b = i / F, f = i % F;
+    if (b0 + b < B) x_bf[((long)t * B + b0 + b) * F + f] = to_bf(tile[b][f]);
+  }
+  if (xT)
+    for (int i = tid; i < 64 * F; i += 256) {
+      const int f = i / 64, b = i % 64;
+      if (b0 + b < Bp) xT[(long)f * T * Bp + (long)t * Bp + b0 + b] = to_bf(tile[b][f]);
+    }
+}
+extern "C" int sv_frames_to_bf16(const float* x, int B, int T, int F, bf16_t* x_bf, bf16_t* xT, int Bp,
+                                 hipStream_t stream) {
+  if (!x || !x_bf || B <= 0 || T <= 0 || F <= 0 || F > 64 || (xT && Bp < B)) return SV_EARG;
+  hipLaunchKernelGGL(frames_to_bf16_kernel, dim3((std::max(B, xT ? Bp : B) + 63) / 64, T), dim3(256), 0, stream, x, B,
+                     T, F, Bp, x_bf, xT);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }
@@ -1170,6 +1225,46 @@ static int wbf_transposes(int L, int F, int H, const float* const* w_ih, const f
   return flush();
 }
 
+// ABI v10: every layer's bf16 weights in one launch (transpose_cast_batch_kernel, each fp32 weight
+// read once): the forward's row-major operands w_ih_bf / w_hh_bf and, when bwd_workspace is given
+// (a stack-backward workspace, sv_lstm_bwd_workspace(SV_DTYPE_BF16, ...)), the transposes the stack
+// backward reads -- W_hh^T of every layer, W_ih^T of layers >= 1 -- in that workspace's per-layer
+// regions, so that sv_lstm_bwd with SV_SCHED_WT_READY on the same workspace launches none (at the
+// c4 rank shape: the forward's cast and the backward's transposes, 13 + 20 us, read every weight
+// twice)
+extern "C" int sv_lstm_weights_bf16(int L, int T, int B, int F, int H, const float* const* w_ih,
+                                    const float* const* w_hh, bf16_t* const* w_ih_bf, bf16_t* const* w_hh_bf,
+                                    void* bwd_workspace, hipStream_t stream) {
+  if (L <= 0 || !w_ih || !w_hh || !w_ih_bf || !w_hh_bf) return SV_EARG;
+  if (T <= 0 || B <= 0 || F <= 0 || H <= 0 || F % 8 || H % 8) return SV_ESHAPE;
+  const size_t per = carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
+  const float* src[8];
+  bf16_t *dst[8], *dstr[8];
+  long lds[8], ldd[8];
+  int R[8], C[8], n = 0;
+  for (int l = 0; l < L; ++l) {
+    if (!w_ih[l] || !w_hh[l] || !w_ih_bf[l] || !w_hh_bf[l]) return SV_EARG;
+    BBwdWs ws{};
+    if (bwd_workspace) ws = carve_bbwd((char*)bwd_workspace + per * l, T, B, std::max(F, H), H);
+    for (int m = 0; m < 2; ++m) {  // m = 0: W_ih [4H][F_l], m = 1: W_hh [4H][H]
+      if (n == 8) {
+        if (int rc = transpose_cast_bf16_batch(n, src, lds, R, C, dst, ldd, stream, dstr)) return rc;
+        n = 0;
+      }
+      const int K = (m == 0 && l == 0) ? F : H;
+      src[n] = m == 0 ? w_ih[l] : w_hh[l];
+      dstr[n] = m == 0 ? w_ih_bf[l] : w_hh_bf[l];
+      dst[n] = !bwd_workspace ? nullptr : m == 1 ? ws.whhT : (l > 0 ? ws.wihT : nullptr);
+      ldd[n] = m == 1 ? 4L * H : bf16_wiht_ld(H);
+      lds[n] = K;
+      R[n] = 4 * H;
+      C[n] = K;
+      ++n;
+    }
+  }
+  return transpose_cast_bf16_batch(n, src, lds, R, C, dst, ldd, stream, dstr);
+}
+
 // the hand-off scratch shared by the layers (persistent or wavefront backward), behind the L
 // per-layer regions
 static size_t bbwd_scratch(int L, int T, int B, int H) {
@@ -1205,6 +1300,8 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
   // the per-layer completion events (a caller's gradient buckets wait on them) of the persistent and
   // wavefront schedules; SV_SCHED_NO_EVENTS: nobody waits, record none (each record idles the GPU)
   const bool evs = !(schedule & SV_SCHED_NO_EVENTS);
+  // SV_SCHED_WT_READY: sv_lstm_weights_bf16 already wrote the transposes into this workspace
+  const bool wt_ready = schedule & SV_SCHED_WT_READY;
   if (sched_wave(schedule, H) && sv_wave_bwd_fits(L, B, H, sv_stream_cus(main))) {
     if (!sync) return SV_EARG;
     // layer-wavefront schedule: every layer's recurrence and upstream gradient dx in one launch
@@ -1217,7 +1314,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       whhT_l[l] = ws.whhT;
       wihT_l[l] = l > 0 ? ws.wihT : nullptr;
     }
-    int rc = wbf_transposes(L, F, H, w_ih, w_hh, whhT_l, wihT_l, main);
+    int rc = wt_ready ? 0 : wbf_transposes(L, F, H, w_ih, w_hh, whhT_l, wihT_l, main);
     if (rc) return rc;
     const int cus = sv_stream_cus(main);
     // every layer's whole-K weight-gradient tiles in one launch where they fit one round of the CUs
@@ -1307,7 +1404,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
         whhT_l[l] = ws.whhT;
         wihT_l[l] = l > 0 ? ws.wihT : nullptr;
       }
-      if (int rc = wbf_transposes(L, F, H, w_ih, w_hh, whhT_l.data(), wihT_l.data(), main)) return rc;
+      if (int rc = wt_ready ? 0 : wbf_transposes(L, F, H, w_ih, w_hh, whhT_l.data(), wihT_l.data(), main)) return rc;
     }
     for (int l = L - 1; l >= 0; --l) {
       const int Fl = l == 0 ? F : H;
@@ -1352,9 +1449,10 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     const int Fl = l == 0 ? F : H;
     const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
     if ((e = hipStreamWaitEvent(s, ev_start, 0)) != hipSuccess) return (int)e;
-    int rc = sv_transpose_cast_bf16(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, s);
+    int rc = wt_ready ? 0 : sv_transpose_cast_bf16(w_hh[l], H, 4 * H, H, ws.whhT, 4L * H, s);
     if (rc) return rc;
-    if (l > 0 && (rc = sv_transpose_cast_bf16(w_ih[l], Fl, 4 * H, Fl, ws.wihT, bf16_wiht_ld(H), s))) return rc;
+    if (!wt_ready && l > 0 && (rc = sv_transpose_cast_bf16(w_ih[l], Fl, 4 * H, Fl, ws.wihT, bf16_wiht_ld(H), s)))
+      return rc;
     if (Bp != B && (e = sv_memset0(dgT[l], (size_t)4 * H * TBp * sizeof(bf16_t), s)) != hipSuccess)
       return (int)e;
     for (int c = nch - 1; c >= 0; --c) {

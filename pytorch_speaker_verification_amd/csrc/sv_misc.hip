@@ -35,6 +35,112 @@ __global__ __launch_bounds__(256) void rownorm_bwd_kernel(const float* __restric
   for (int p = lane; p < P; p += 64) dy[(long)r * P + p] = (de[p] - e[p] * dot) * inv;
 }
 
+// ---- the projection backward in one launch (P <= 256, H % 4 == 0, B <= 128) ----
+// The GEMM path takes 5 launches after the row-norm backward (the dWp GEMM, a two-level column
+// sum, the dh GEMM, their slab reduce); at the rank shapes each is a ~5 us latency-bound launch
+// (r06 c4 rank timeline: 27 us for the five).  Here ONE launch: workgroups of PJ_R rows x 64
+// columns of H form dh = dy Wp (K = P, Wp rows read coalesced), workgroups of 8 rows of P x 64
+// columns form dWp = dy^T h (K = B, h rows read coalesced), those of column block 0 also
+// db = colsum(dy); dy's slice staged in LDS, each of the 4 waves a quarter of K, PJ_U loads in
+// flight per lane.  Exact fp32 products, fp32 accumulation in a fixed
+// order (another order than the MFMA GEMMs': results agree to fp32 rounding).  Measured (traces):
+// c4 rank (B = 80) 18-20 us against 27; c5 rank (B = 320) 59 us against 39 -- its K = B loop
+// grows with the batch while the GEMM path's does not, hence B <= 128.
+#define PJ_R 4
+#define PJ_U 32  // loads in flight per thread
+__global__ __launch_bounds__(256) void proj_bwd_small_kernel(const float* __restrict__ dy, const float* __restrict__ h,
+                                                             int B, int H, int P, const float* __restrict__ W,
+                                                             float* __restrict__ dW, float* __restrict__ db,
+                                                             float* __restrict__ dh, int ndh) {
+  // workgroup = 64 columns of H (lane = column) x 4 waves, each wave one quarter of the reduction
+  // dimension; the waves' partials added through LDS in wave order (fixed summation order)
+  extern __shared__ float sm[];  // staged dy slice, then [4 waves][8][64] partials
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, ncb = (H + 63) / 64;
+  if ((int)blockIdx.x < ndh) {  // dh[r][c] = sum_p dy[r][p] W[p][c], r in [r0, r0 + PJ_R)
+    const int r0 = (blockIdx.x / ncb) * PJ_R, c = (blockIdx.x % ncb) * 64 + lane;
+    float* part = sm + PJ_R * P;
+    {  // PJ_R * P <= 1024: four predicated loads per thread in flight at once
+      float v[PJ_R];
+#pragma unroll
+      for (int k = 0; k < PJ_R; ++k) {
+        const int i = tid + 256 * k;
+        v[k] = (i < PJ_R * P && r0 + i / P < B) ? dy[(long)r0 * P + i] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < PJ_R; ++k)
+        if (tid + 256 * k < PJ_R * P) sm[tid + 256 * k] = v[k];
+    }
+    __syncthreads();
+    const int q = (P + 3) / 4, pa = wv * q, pe = min(P, pa + q);
+    float acc[PJ_R];
+#pragma unroll
+    for (int r = 0; r < PJ_R; ++r) acc[r] = 0.f;
+    for (int p0 = pa; p0 < pe; p0 += PJ_U) {
+      float wv_[PJ_U];
+#pragma unroll
+      for (int u = 0; u < PJ_U; ++u) wv_[u] = (p0 + u < pe && c < H) ? W[(long)(p0 + u) * H + c] : 0.f;
+#pragma unroll
+      for (int u = 0; u < PJ_U; ++u)
+#pragma unroll
+        for (int r = 0; r < PJ_R; ++r) acc[r] = fmaf(p0 + u < pe ? sm[r * P + p0 + u] : 0.f, wv_[u], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < PJ_R; ++r) part[(wv * PJ_R + r) * 64 + lane] = acc[r];
+    __syncthreads();
+    if (tid < PJ_R * 64) {
+      const int r = tid >> 6;
+      const float v = part[(0 * PJ_R + r) * 64 + lane] + part[(1 * PJ_R + r) * 64 + lane] +
+                      part[(2 * PJ_R + r) * 64 + lane] + part[(3 * PJ_R + r) * 64 + lane];
+      if (r0 + r < B && c < H) dh[(long)(r0 + r) * H + c] = v;
+    }
+    return;
+  }
+  // dW[p][c] = sum_b dy[b][p] h[b][c], p in [p0, p0 + 8); db[p] = sum_b dy[b][p] (column block 0)
+  const int j = blockIdx.x - ndh, p0 = (j / ncb) * 8, c = (j % ncb) * 64 + lane;
+  float* part = sm + B * 8;
+  for (int i0 = 0; i0 < B * 8; i0 += 256 * 8) {  // 8 predicated loads per thread in flight at once
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = i0 + tid + 256 * k;
+      v[k] = (i < B * 8 && p0 + (i & 7) < P) ? dy[(long)(i >> 3) * P + p0 + (i & 7)] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (i0 + tid + 256 * k < B * 8) sm[i0 + tid + 256 * k] = v[k];
+  }
+  __syncthreads();
+  if (j % ncb == 0 && tid < 8 && p0 + tid < P) {
+    float s_ = 0.f;
+    for (int b = 0; b < B; ++b) s_ += sm[b * 8 + tid];
+    db[p0 + tid] = s_;
+  }
+  const int q = (B + 3) / 4, ba = wv * q, be = min(B, ba + q);
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  for (int b0 = ba; b0 < be; b0 += PJ_U) {
+    float hv[PJ_U];
+#pragma unroll
+    for (int u = 0; u < PJ_U; ++u) hv[u] = (b0 + u < be && c < H) ? h[(long)(b0 + u) * H + c] : 0.f;
+#pragma unroll
+    for (int u = 0; u < PJ_U; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = fmaf(b0 + u < be ? sm[(b0 + u) * 8 + k] : 0.f, hv[u], acc[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) part[(wv * 8 + k) * 64 + lane] = acc[k];
+  __syncthreads();
+  for (int k = wv; k < 8; k += 4) {
+    const float v = part[(0 * 8 + k) * 64 + lane] + part[(1 * 8 + k) * 64 + lane] + part[(2 * 8 + k) * 64 + lane] +
+                    part[(3 * 8 + k) * 64 + lane];
+    if (p0 + k < P && c < H) dW[(long)(p0 + k) * H + c] = v;
+  }
+}
+static bool proj_small_ok(int B, int H, int P, const void* h, const void* W) {
+  return P <= 256 && H % 4 == 0 && B <= 128 && !(((uintptr_t)h | (uintptr_t)W) & 15);
+}
+
 extern "C" size_t sv_proj_norm_workspace(int B, int H, int P) {
   size_t g = std::max(sv_gemm_f32_workspace(B, P, H), std::max(sv_gemm_f32_workspace(P, H, B), sv_gemm_f32_workspace(B, H, P)));
   g = std::max(g, sv_colsum_workspace(B, P));
@@ -59,6 +165,14 @@ extern "C" int sv_proj_norm_bwd(const float* demb, const float* emb, const float
   float* gws = workspace + ((size_t)B * P * sizeof(float) + 255) / 256 * 64;
   hipLaunchKernelGGL(rownorm_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, demb, emb, ynorm, B, P, dy);
   SV_LAUNCH_CHECK();
+  if (proj_small_ok(B, H, P, h_last, w_p)) {
+    const int ncb = (H + 63) / 64, ndh = (B + PJ_R - 1) / PJ_R * ncb, ndw = (P + 7) / 8 * ncb;
+    const size_t lds = std::max((size_t)PJ_R * P + 4 * PJ_R * 64, (size_t)B * 8 + 4 * 8 * 64) * sizeof(float);
+    hipLaunchKernelGGL(proj_bwd_small_kernel, dim3(ndh + ndw), dim3(256), lds, stream, dy, h_last, B, H, P, w_p, dw_p,
+                       db_p, dh_last, ndh);
+    SV_LAUNCH_CHECK();
+    return SV_OK;
+  }
   // dWp [P,H] = dy^T h_last  (A = dy as [K=B][M=P], B = h_last as [K=B][N=H])
   int rc = gemm_f32(0, 0, P, H, B, dy, P, h_last, H, dw_p, H, nullptr, nullptr, 0.f, gws, stream, true);
   if (rc) return rc;

@@ -16,8 +16,8 @@ import ctypes
 
 import torch
 
-from ._lib import (SV_DTYPE_BF16, SV_DTYPE_F32, SV_SCHED_NO_EVENTS, PersistStatus, call, lib, ptr, require_device,
-                   schedule_flags, stream_of)
+from ._lib import (SV_DTYPE_BF16, SV_DTYPE_F32, SV_SCHED_NO_EVENTS, SV_SCHED_WT_READY, PersistStatus, call, lib,
+                   ptr, require_device, schedule_flags, stream_of)
 
 # timesteps per chunk of the layer-pipelined schedules (measured at c2: 16 / 24 / 32 / 48 / 64 ->
 # 69.3 / 69.7 / 69.1 / 69.5 / 69.6 ms per step)
@@ -126,6 +126,7 @@ class EmbedderState:
         self.y = self.emb = self.ynorm = self.h_last = None
         self.T = self.B = self.H = self.P = 0
         self.bf16 = False
+        self.bws = None     # bf16: the stacked backward's workspace, its weight transposes already in
 
 
 def embedder_forward(x, layers, w_p, b_p, save=True, products="mfma_f32", status=None, probe=None, schedule="auto"):
@@ -337,26 +338,34 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=Non
     Bp = (B + 7) // 8 * 8
     st = EmbedderState()
     st.T, st.B, st.H, st.P, st.bf16 = T, B, H, P, True
-    x_tm = torch.empty((T, B, F), dtype=torch.float32, device=dev)
-    call("sv_frames_to_time_major", ptr(x), ptr(x_tm), B, T, F, s)
     x_bf = _bf((T, B, F), dev)
     L = len(layers)
-    # the frames' and every layer's weight casts in one launch (sv_cast_bf16_batch)
+    fused_x = F <= 64
+    if save:  # layer 0's dW_ih operand x^T [F][T Bp] (padding columns zero)
+        st.xT0 = (torch.empty if fused_x or Bp == B else torch.zeros)((F, T * Bp), dtype=torch.bfloat16, device=dev)
+    if fused_x:  # x -> time-major bf16 and x^T in one launch (sv_frames_to_bf16)
+        call("sv_frames_to_bf16", ptr(x), B, T, F, ptr(x_bf), ptr(st.xT0) if save else None, Bp, s)
+        srcs, dsts = [], []
+    else:
+        x_tm = torch.empty((T, B, F), dtype=torch.float32, device=dev)
+        call("sv_frames_to_time_major", ptr(x), ptr(x_tm), B, T, F, s)
+        srcs, dsts = [x_tm], [x_bf]
+        if save:
+            if Bp == B:
+                call("sv_transpose_cast_bf16", ptr(x_tm), F, T * B, F, ptr(st.xT0), T * B, s)
+            else:
+                for t in range(T):
+                    call("sv_transpose_cast_bf16", ptr(x_tm[t]), F, B, F, ptr(st.xT0) + 2 * t * Bp, T * Bp, s)
+    if srcs:  # the time-major frames' cast (F > 64)
+        call("sv_cast_bf16", ptr(srcs[0]), ptr(dsts[0]), srcs[0].numel(), s)
+    # every layer's bf16 weights in one launch (sv_lstm_weights_bf16); when the stacked backward
+    # follows, also its weight transposes, into the backward workspace it will be handed
+    # (SV_SCHED_WT_READY: the backward launches no transposes)
     wbf = [(_bf(w_ih.shape, dev), _bf(w_hh.shape, dev)) for (w_ih, w_hh, _, _) in layers]
-    srcs = [x_tm] + [w for (w_ih, w_hh, _, _) in layers for w in (w_ih, w_hh)]
-    dsts = [x_bf] + [w for pair in wbf for w in pair]
-    for i in range(0, len(srcs), 8):
-        n = min(8, len(srcs) - i)
-        call("sv_cast_bf16_batch", n, (ctypes.c_void_p * n)(*[ptr(t) for t in srcs[i:i + n]]),
-             (ctypes.c_void_p * n)(*[ptr(t) for t in dsts[i:i + n]]),
-             (ctypes.c_long * n)(*[t.numel() for t in srcs[i:i + n]]), s)
-    if save:
-        st.xT0 = (torch.zeros if Bp != B else torch.empty)((F, T * Bp), dtype=torch.bfloat16, device=dev)
-        if Bp == B:
-            call("sv_transpose_cast_bf16", ptr(x_tm), F, T * B, F, ptr(st.xT0), T * B, s)
-        else:
-            for t in range(T):
-                call("sv_transpose_cast_bf16", ptr(x_tm[t]), F, B, F, ptr(st.xT0) + 2 * t * Bp, T * Bp, s)
+    if save and PIPELINE_CHUNK > 0 and L > 1:
+        st.bws = _ws(lib().sv_lstm_bwd_workspace(SV_DTYPE_BF16, L, T, B, F, H), dev)
+    call("sv_lstm_weights_bf16", L, T, B, F, H, _parr([l[0] for l in layers]), _parr([l[1] for l in layers]),
+         _parr([w[0] for w in wbf]), _parr([w[1] for w in wbf]), ptr(st.bws) if st.bws is not None else None, s)
     inp = x_bf
     gs = [_bf((T, B, 4 * H), dev) for _ in range(L)]  # bf16 x-projection in, bf16 activations out
     cs = [torch.empty((T, B, H), dtype=torch.float32, device=dev) for _ in range(L)]
@@ -442,7 +451,10 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
     Fmax = max(st.x_tm[l].shape[2] for l in range(L))
     if PIPELINE_CHUNK > 0 and L > 1 and not need_dx:
         F0 = st.x_tm[0].shape[2]
-        ws = _ws(lib().sv_lstm_bwd_workspace(SV_DTYPE_BF16, L, T, B, F0, H), dev)
+        if st.bws is not None:  # the forward wrote the weight transposes into it (sv_lstm_weights_bf16)
+            ws, sched = st.bws, sched | SV_SCHED_WT_READY
+        else:
+            ws = _ws(lib().sv_lstm_bwd_workspace(SV_DTYPE_BF16, L, T, B, F0, H), dev)
         dgs = [_bf((T, B, 4 * H), dev) for _ in range(L)]
         dgTs = [_bf((4 * H, T * Bp), dev) for _ in range(L)]
         dxs = [None] + [torch.empty((T, B, H), dtype=torch.float32, device=dev) for _ in range(L - 1)]

@@ -262,3 +262,53 @@ def test_wavefront_weight_gradients_against_fp64_of_same_operands(N, M, T):
                 worst = max(worst, err)
                 assert err <= 1e-5, (rep, l, name, err)
     print(f"\nMEASURED wave_dw_vs_fp64_same_operands.T{T} {worst:.2e} (of sum |products|)")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T,schedule", [(80, 24, "auto"), (320, 12, "auto"), (64, 8, "per_step")])
+def test_weights_bf16_transposes_handed_to_the_backward(B, T, schedule):
+    """sv_lstm_weights_bf16 (ABI v10): the forward's one launch writes every layer's bf16 weights
+    and, into the stack backward's workspace, the transposes that backward would otherwise form;
+    SV_SCHED_WT_READY makes the backward use them.  The gradients must be bit-identical to a
+    backward that transposes on its own (st.bws dropped), under the wavefront (B = 80), persistent
+    (B = 320) and per-step schedules; the row-major copies must equal torch's bf16 rounding."""
+    import recipe
+    import torch
+    from conftest import model_dims
+    from pytorch_speaker_verification_amd import ops
+    from pytorch_speaker_verification_amd._lib import call, stream_of
+    from pytorch_speaker_verification_amd.ops import _parr
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    dev = torch.device("cuda", 0)
+    dims = (40, 768, 3, 256)
+    F, H = dims[0], dims[1]
+    sd = recipe.make_weights(91, *dims, scale=3.0)
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    net = net.to(dev)
+    layers = net.LSTM_stack.layer_params()
+    wp, bp = net.projection.weight, net.projection.bias
+    x = torch.as_tensor(recipe.make_frames(700, B, T, F)).to(dev)
+    demb = torch.as_tensor(np.random.default_rng(701).standard_normal((B, dims[3])).astype(np.float32)).to(dev)
+    out = []
+    for handed in (True, False):
+        emb, st = ops.embedder_forward_bf16(x, layers, wp, bp, save=True, schedule=schedule)
+        assert st.bws is not None
+        if not handed:
+            st.bws = None
+        out.append([g.clone() for g in ops.embedder_backward_bf16(st, demb, layers, wp, schedule=schedule)])
+    torch.cuda.synchronize()
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+    # the row-major copies alone (no workspace) against torch's RNE rounding
+    wih = [torch.empty_like(l[0], dtype=torch.bfloat16) for l in layers]
+    whh = [torch.empty_like(l[1], dtype=torch.bfloat16) for l in layers]
+    call("sv_lstm_weights_bf16", 3, T, B, F, H, _parr([l[0] for l in layers]), _parr([l[1] for l in layers]),
+         _parr(wih), _parr(whh), None, stream_of(x))
+    torch.cuda.synchronize()
+    for l in range(3):
+        assert torch.equal(wih[l], layers[l][0].to(torch.bfloat16))
+        assert torch.equal(whh[l], layers[l][1].to(torch.bfloat16))
