@@ -742,7 +742,10 @@ def main():
     # fp32: the persistent recurrences where the library picks them (c2: 240 of 256 CUs), else
     # the per-step kernels with their in-kernel stamps
     f32_persist = dtype == "f32" and bool(_svlib().sv_lstm_f32_persist_ok(B, H, 0))
-    dt, loss, host, probes, tr = run_steps(ctx, N, M, T, dtype, args.steps, args.warmup, 1235,
+    # the step time without timing probes (each probe event record idles the GPU ~6 us between two
+    # kernels: 12 records per c2 step), then the same steps again with the probes for the roofline
+    dt, loss, host, _, tr = run_steps(ctx, N, M, T, dtype, args.steps, args.warmup, 1235)
+    dt_probed, _, _, probes, _ = run_steps(ctx, N, M, T, dtype, args.steps, 1, 1235,
                                            probe="bwd_chunks" if dtype == "f32" and not f32_persist else "fwd_bwd")
     ms_step = dt / args.steps * 1e3
     fwd_fl, st_fl = step_flops(B, T, F, H, P, L)
@@ -768,6 +771,7 @@ def main():
                    "parallelism": f"dp{world} (speaker-sharded GE2E, RCCL grad all-reduce)"},
         "steps_per_sec": round(args.steps / dt, 4),
         "host_enqueue_ms_per_step": round(host / args.steps * 1e3, 3),
+        "probed_ms_per_step": round(dt_probed / args.steps * 1e3, 3),
         "loss": round(loss, 5),
         "step_tflops_per_gpu": round(st_fl / (ms_step * 1e-3) / 1e12, 2),
         "step_mfma_frac": round(st_fl / (ms_step * 1e-3) / 1e12 / peak, 4),
