@@ -417,7 +417,7 @@ int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, cons
                      const bf16_t* const* w_hh_bf, const float* const* b_ih, const float* const* b_hh,
                      bf16_t* const* gates, float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
                      bf16_t* const* hT, unsigned* sync, hipStream_t stream, unsigned limit, int fault, hipEvent_t pre,
-                     hipEvent_t post);
+                     hipEvent_t post, int counters_zeroed = 0);
 // layer-wavefront backward (sv_persist3.hip / sv_persist.hip): all L = 3 layers' recurrences and
 // their upstream gradients dx in one launch, for the small per-GPU batches (B <= 80 at H = 768)
 constexpr int WB_L = 3;

@@ -1078,13 +1078,14 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
       return (int)e;
     return SV_OK;
   };
-  // every layer's state reset in one launch (the schedules that run on `main`)
-  auto zero_states = [&](hipStream_t s) -> int {
-    void* p[8];
-    size_t b[8];
+  // every layer's state reset in one launch (the schedules that run on `main`); cnt: also the
+  // counter channels 0..L-1 of the sync block (the layer wavefront's), in the same launch
+  auto zero_states = [&](hipStream_t s, bool cnt) -> int {
+    void* p[SV_ZB_MAX];
+    size_t b[SV_ZB_MAX];
     int n = 0;
     for (int l = 0; l < L; ++l) {
-      if (n + 3 > 8) {
+      if (n + 3 > SV_ZB_MAX) {
         if (int rc = sv_zero_bytes_multi(n, p, b, s)) return rc;
         n = 0;
       }
@@ -1092,23 +1093,30 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
       p[n] = h_bf[l], b[n++] = BH * sizeof(bf16_t);
       if (hT[l] && Bp != B) p[n] = hT[l], b[n++] = (size_t)H * ldhT * sizeof(bf16_t);
     }
+    if (cnt) {
+      if (n == SV_ZB_MAX) {
+        if (int rc = sv_zero_bytes_multi(n, p, b, s)) return rc;
+        n = 0;
+      }
+      p[n] = sync + SV_SYNC_CNT, b[n++] = (size_t)L * SV_PCNT_ROWS * SV_PCNT_STRIDE * sizeof(unsigned);
+    }
     return sv_zero_bytes_multi(n, p, b, s);
   };
   int rc;
   if (sched_wave(schedule, H) && sv_wave_fwd_fits(L, T, B, F, H, sv_stream_cus(main))) {
     // layer-wavefront schedule (sv_wave.hip): every layer's recurrence and input projection in
     // one launch on `main`
-    if (!sync) return SV_EARG;
-    if ((rc = zero_states(main))) return rc;
+    if (!sync || L > SV_SYNC_CHANNELS) return SV_EARG;
+    if ((rc = zero_states(main, true))) return rc;
     return sv_wave_fwd_bf16(L, T, B, F, H, x_bf, w_ih_bf, w_hh_bf, b_ih, b_hh, gates, c_tm, h_tm, h_bf, hT, sync, main,
                             sv_persist_limit(), sv_persist_fault(0), probe ? probe[0] : nullptr,
-                            probe ? probe[1] : nullptr);
+                            probe ? probe[1] : nullptr, 1);
   }
   if (sched_persist(schedule, H) && sv_persist_fwd_fits(B, H, sv_stream_cus(main))) {
     if (!sync) return SV_EARG;
     // persistent schedule on `main`: per layer the whole-T K1 GEMM, then one launch for the
     // recurrence (sv_persist.hip); layers run one after another
-    if ((rc = zero_states(main))) return rc;
+    if ((rc = zero_states(main, false))) return rc;
     for (int l = 0; l < L; ++l) {
       const int Fl = l == 0 ? F : H;
       const bf16_t* in = l == 0 ? x_bf : h_bf[l - 1] + BH;

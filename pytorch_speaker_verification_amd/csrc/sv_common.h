@@ -24,6 +24,10 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 int gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
              float* C, long ldc, const float* bias0, const float* bias1, float beta, float* workspace,
              hipStream_t stream, bool fine = false);
+// the projection forward with the row norm fused into the split-K reduce (sv_lstm.hip); returns 0
+// where that form does not apply (the caller then runs gemm_f32 and its own norm)
+int proj_norm_fused(const float* h, int B, int K, int P, const float* W, const float* bias, float* y, float* emb,
+                    float* ynorm, float* workspace, hipStream_t stream, int* rc);
 struct F32ProductScope {
   int prev;
   explicit F32ProductScope(int mode);
@@ -43,7 +47,8 @@ int sv_zero_counters(unsigned* cnt, int nchan, long chan_stride, int words, hipS
 // in the library instead of hipMemsetAsync: replayed from a HIP graph, memset nodes left junk
 // behind (the initial-state slots and the arrival counters; scripts/f32_replay_diag.py)
 int sv_zero_bytes(void* p, size_t bytes, hipStream_t stream);
-// up to 8 zeroings in one launch (n buffers of bytes[i] bytes each)
+// up to SV_ZB_MAX zeroings in one launch (n buffers of bytes[i] bytes each)
+#define SV_ZB_MAX 12
 int sv_zero_bytes_multi(int n, void* const* ptrs, const size_t* bytes, hipStream_t stream);
 inline hipError_t sv_memset0(void* p, size_t bytes, hipStream_t stream) {
   return (hipError_t)sv_zero_bytes(p, bytes, stream);

@@ -843,6 +843,76 @@ int gemm_f32(int a_kcontig, int b_kcontig, int M, int N, int K, const float* A, 
   return SV_OK;
 }
 
+// the projection's split-K slabs summed and the rows normalised in one launch (one wave per row,
+// P <= 256): y = sum_z slab[z] + bias in slab_reduce_kernel's order, emb = y / |y| and |y| in
+// rownorm_fwd_kernel's (sv_misc.hip) -- the two launches' results bit for bit, one launch fewer
+#define SR_NZ 8
+__global__ __launch_bounds__(256) void slab_rownorm_kernel(const float* __restrict__ slab, int nz, long zstride, int B,
+                                                           int P, const float* __restrict__ bias, float* __restrict__ y,
+                                                           float* __restrict__ emb, float* __restrict__ ynorm) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= B) return;
+  // every slab value of the lane's 4 columns loaded at once (nz <= SR_NZ: one round trip, where a
+  // loop over z waited for each load in turn), then summed in z order
+  float x[SR_NZ][4], bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = lane + 64 * j;
+    bv[j] = (bias && p < P) ? bias[p] : 0.f;
+#pragma unroll
+    for (int z = 0; z < SR_NZ; ++z) x[z][j] = (z < nz && p < P) ? slab[z * zstride + (long)r * P + p] : 0.f;
+  }
+  float v[4];
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = lane + 64 * j;
+    if (p < P) {
+      float s = 0.f;
+#pragma unroll
+      for (int z = 0; z < SR_NZ; ++z)
+        if (z < nz) s += x[z][j];
+      if (bias) s += bv[j];
+      v[j] = 0.f + s;  // (slab_reduce_kernel's store with beta = 0)
+      y[(long)r * P + p] = v[j];
+      ss += v[j] * v[j];
+    }
+  }
+  const float n = sqrtf(wave_sum(ss));
+  const float inv = 1.0f / n;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = lane + 64 * j;
+    if (p < P) emb[(long)r * P + p] = v[j] * inv;
+  }
+  if (lane == 0) ynorm[r] = n;
+}
+
+// y = h W^T + b (h [B,K], W [P,K], both k-contiguous) with the row norm fused into the split-K
+// reduce where gemm_f32 would take that form (P <= 256, P % 4 == 0); returns 1 if it ran, 0 if
+// the caller should take gemm_f32 + its own norm
+int proj_norm_fused(const float* h, int B, int K, int P, const float* W, const float* bias, float* y, float* emb,
+                    float* ynorm, float* workspace, hipStream_t stream, int* rc) {
+  *rc = SV_OK;
+  if (!workspace || P > 256 || P % 4 || K % 4 || (((uintptr_t)h | (uintptr_t)W) & 15) || gemm_x() != 0) return 0;
+  if (gf256_ok(B, P, K, y, P, bias, nullptr) || narrow_ok(B, P, K, K, K, 0)) return 0;
+  const GemmPlan p = plan_gemm(B, P, K, true);
+  if (p.splitk <= 1 || p.splitk > SR_NZ) return 0;
+  const long slab = (long)B * P;
+  if (p.bm == 64)
+    *rc = dispatch_layout<64, 64, EPI_SLAB>(true, true, h, K, W, K, workspace, P, slab, B, P, K, p.splitk, p.kchunk,
+                                            nullptr, nullptr, 0.f, stream);
+  else
+    *rc = dispatch_layout<128, 128, EPI_SLAB>(true, true, h, K, W, K, workspace, P, slab, B, P, K, p.splitk, p.kchunk,
+                                              nullptr, nullptr, 0.f, stream);
+  if (*rc) return 1;
+  hipLaunchKernelGGL(slab_rownorm_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, workspace, p.splitk, slab, B, P, bias,
+                     y, emb, ynorm);
+  *rc = (int)hipGetLastError();
+  return 1;
+}
+
 extern "C" int sv_frames_to_time_major(const float* x, float* x_tm, int B, int T, int F, hipStream_t stream) {
   if (!x || !x_tm || B <= 0 || T <= 0 || F <= 0) return SV_EARG;
   if (F % 4 || (((uintptr_t)x | (uintptr_t)x_tm) & 15)) return SV_EALIGN;

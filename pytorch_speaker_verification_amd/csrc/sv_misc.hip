@@ -150,7 +150,9 @@ extern "C" size_t sv_proj_norm_workspace(int B, int H, int P) {
 extern "C" int sv_proj_norm_fwd(const float* h_last, int B, int H, int P, const float* w_p, const float* b_p, float* y,
                                 float* emb, float* ynorm, float* workspace, hipStream_t stream) {
   if (!h_last || !w_p || !y || !emb || !ynorm || B <= 0 || H <= 0 || P <= 0) return SV_EARG;
-  int rc = gemm_f32(1, 1, B, P, H, h_last, H, w_p, H, y, P, b_p, nullptr, 0.f, workspace, stream, true);
+  int rc;
+  if (proj_norm_fused(h_last, B, H, P, w_p, b_p, y, emb, ynorm, workspace, stream, &rc)) return rc;
+  rc = gemm_f32(1, 1, B, P, H, h_last, H, w_p, H, y, P, b_p, nullptr, 0.f, workspace, stream, true);
   if (rc) return rc;
   hipLaunchKernelGGL(rownorm_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, y, B, P, emb, ynorm);
   SV_LAUNCH_CHECK();

@@ -958,10 +958,11 @@ int sv_zero_bytes(void* p, size_t bytes, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-// up to 8 zeroings in one launch (blockIdx.y = buffer): the per-step state resets of the bf16 stack
+// up to SV_ZB_MAX zeroings in one launch (blockIdx.y = buffer): the per-step state resets of the
+// bf16 stack (and, for the layer wavefront, its counter channels)
 struct ZeroBatch {
-  char* p[8];
-  size_t head[8], n16[8], tail[8];
+  char* p[SV_ZB_MAX];
+  size_t head[SV_ZB_MAX], n16[SV_ZB_MAX], tail[SV_ZB_MAX];
 };
 __global__ void sv_zero_bytes_multi_kernel(const ZeroBatch zb) {
   const int b = blockIdx.y;
@@ -974,7 +975,7 @@ __global__ void sv_zero_bytes_multi_kernel(const ZeroBatch zb) {
 }
 int sv_zero_bytes_multi(int n, void* const* ptrs, const size_t* bytes, hipStream_t stream) {
   if (n <= 0) return SV_OK;
-  if (n > 8) return SV_EARG;
+  if (n > SV_ZB_MAX) return SV_EARG;
   ZeroBatch zb{};
   size_t most = 0;
   for (int i = 0; i < n; ++i) {

@@ -338,12 +338,12 @@ int sv_wave_fwd_fits(int L, int T, int B, int F, int H, int cus) {
 
 // all L layers' recurrences of the bf16 stack forward in one launch (no K1 GEMMs): writes what the
 // per-layer schedule writes.  h_tm / h_bf slot 0 and padded hT columns must be zero (the caller's
-// memsets).  Counter channels 0..L-1 of `sync`.
+// memsets).  Counter channels 0..L-1 of `sync` (zeroed here unless counters_zeroed).
 int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, const bf16_t* const* w_ih_bf,
                      const bf16_t* const* w_hh_bf, const float* const* b_ih, const float* const* b_hh,
                      bf16_t* const* gates, float* const* c_tm, float* const* h_tm, bf16_t* const* h_bf,
                      bf16_t* const* hT, unsigned* sync, hipStream_t stream, unsigned limit, int fault, hipEvent_t pre,
-                     hipEvent_t post) {
+                     hipEvent_t post, int counters_zeroed) {
   if (!sv_wave_fwd_fits(L, T, B, F, H, sv_stream_cus(stream))) return SV_ESHAPE;
   if (!sync || !x_bf) return SV_EARG;
   WaveFwd2Args a{};
@@ -361,8 +361,10 @@ int sv_wave_fwd_bf16(int L, int T, int B, int F, int H, const bf16_t* x_bf, cons
     a.hT[l] = hT[l];
     a.cnt[l] = sync + SV_SYNC_CNT + (size_t)l * SV_PCNT_ROWS * SV_PCNT_STRIDE;
   }
-  if (int rc = sv_zero_counters(a.cnt[0], L, (long)SV_PCNT_ROWS * SV_PCNT_STRIDE, a.nrb * SV_PCNT_STRIDE, stream))
-    return rc;
+  // counters_zeroed: the caller zeroed channels 0..L-1 in its state-reset launch
+  if (!counters_zeroed)
+    if (int rc = sv_zero_counters(a.cnt[0], L, (long)SV_PCNT_ROWS * SV_PCNT_STRIDE, a.nrb * SV_PCNT_STRIDE, stream))
+      return rc;
   a.x_bf = x_bf;
   a.status = sync;
   a.limit = limit;
