@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SV_ABI_VERSION 10
+#define SV_ABI_VERSION 11
 int sv_abi_version(void);
 
 /* ---- fp32 product modes (`products` argument of sv_gemm_f32 / sv_lstm_stack_fwd / _bwd; every
@@ -271,6 +271,11 @@ int sv_frames_to_bf16(const float* x, int B, int T, int F, sv_bf16* x_bf, sv_bf1
  * SV_SCHED_WT_READY and the backward launches no transposes. */
 int sv_lstm_weights_bf16(int L, int T, int B, int F, int H, const float* const* w_ih, const float* const* w_hh,
                          sv_bf16* const* w_ih_bf, sv_bf16* const* w_hh_bf, void* bwd_workspace, hipStream_t stream);
+/* (ABI v11) sv_frames_to_bf16 (frames x [B,T,F] -> x_bf, xT) and sv_lstm_weights_bf16 in ONE launch:
+ * the bf16 stack forward's whole operand preparation. */
+int sv_lstm_prep_bf16(int L, int T, int B, int F, int H, const float* x, sv_bf16* x_bf, sv_bf16* xT, int Bp,
+                      const float* const* w_ih, const float* const* w_hh, sv_bf16* const* w_ih_bf,
+                      sv_bf16* const* w_hh_bf, void* bwd_workspace, hipStream_t stream);
 /* x_bf [T,B,F]; writes gates (bf16), c_tm/h_tm (fp32) plus h_bf [T+1,B,H] and hT [H,(T+1)Bp] (bf16) */
 int sv_lstm_layer_fwd_bf16(const sv_bf16* x_bf, int T, int B, int F, int H, const sv_bf16* w_ih_bf,
                            const sv_bf16* w_hh_bf, const float* b_ih, const float* b_hh, sv_bf16* gates, float* c_tm,

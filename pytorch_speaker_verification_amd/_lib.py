@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libsv_ge2e.so")
 # the fault-injection test build (Makefile `faultinj`): the same library plus sv_test_set_fault;
 # only tests load it, through use_library() before the first call
 FAULT_LIB_PATH = os.path.join(_HERE, "libsv_ge2e_faultinj.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 SV_DTYPE_F32, SV_DTYPE_BF16 = 0, 1  # include/sv_ge2e.h
 
 # schedule flags of the bf16 stack (include/sv_ge2e.h SV_SCHED_*), by name
@@ -99,6 +99,7 @@ SIGNATURES = {
     "sv_transpose_cast_bf16": (_c_int, [_P, _c_long, _c_int, _c_int, _P, _c_long, _P]),
     "sv_frames_to_bf16": (_c_int, [_P, _c_int, _c_int, _c_int, _P, _P, _c_int, _P]),
     "sv_lstm_weights_bf16": (_c_int, [_c_int] * 5 + [_P] * 6),
+    "sv_lstm_prep_bf16": (_c_int, [_c_int] * 5 + [_P] * 3 + [_c_int] + [_P] * 6),
     "sv_lstm_layer_fwd_bf16": (_c_int, [_P, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "sv_lstm_stack_fwd_bf16": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                         _P, _c_int, _P, _P, _P, _P, _P, _c_int]),

@@ -142,15 +142,56 @@ struct TCastBatch {
   int n;
   unsigned vec;           // bit b: matrix b takes the 16-B paths (lds % 4, ldd % 8, aligned bases)
 };
+// the frames' part of the bf16 stack's input preparation (sv_frames_to_bf16 / sv_lstm_prep_bf16):
+// frames x [B,T,F] fp32 -> x_bf [T,B,F] and, when xT is given, xT [F][T Bp] with column t Bp + b =
+// x[b,t,:] (padding columns b in [B, Bp) zero) -- layer 0's dW_ih operand.  Workgroup (t, 64 rows
+// b): the tile goes through LDS so both stores coalesce.
+struct FramesArgs {
+  const float* x;
+  bf16_t *x_bf, *xT;
+  int B, T, F, Bp, nbx;  // nbx: 64-row blocks per timestep
+};
+__device__ __forceinline__ void frames_tile(const FramesArgs& fa, int bx, int t, float (*tile)[65]) {
+  const int b0 = bx * 64, tid = threadIdx.x, B = fa.B, T = fa.T, F = fa.F, Bp = fa.Bp;
+  // 16 predicated loads per thread, all in flight before the first LDS write (a rolled loop
+  // waited for each load on its own); thread -> (row tid / 64 + 4 i, column tid % 64)
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int b = (tid >> 6) + 4 * i, f = tid & 63;
+    v[i] = (f < F && b0 + b < B) ? fa.x[((long)(b0 + b) * T + t) * F + f] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) tile[(tid >> 6) + 4 * i][tid & 63] = v[i];
+  __syncthreads();
+  for (int i = tid; i < 64 * F; i += 256) {
+    const int b = i / F, f = i % F;
+    if (b0 + b < B) fa.x_bf[((long)t * B + b0 + b) * F + f] = to_bf(tile[b][f]);
+  }
+  if (fa.xT)
+    for (int i = tid; i < 64 * F; i += 256) {
+      const int f = i / 64, b = i % 64;
+      if (b0 + b < Bp) fa.xT[(long)f * T * Bp + (long)t * Bp + b0 + b] = to_bf(tile[b][f]);
+    }
+}
+
 // 64 x 64 tiles: float4 loads along a source row (16 threads per row, 16 rows per pass) and 16-B
 // bf16 stores along a destination row (8 threads per row, 32 rows per pass) where the matrix's
-// leading dimensions and base pointers allow (tb.vec bit b), element-wise at the edges
-__global__ __launch_bounds__(256) void transpose_cast_batch_kernel(const TCastBatch tb) {
+// leading dimensions and base pointers allow (tb.vec bit b), element-wise at the edges.
+// The first nfr workgroups (fa.x given): the frames' part, beside the tiles in the same launch --
+// dispatched first, so that these latency-bound workgroups overlap the tiles instead of forming
+// the launch's tail (placed after the tiles, the launch took the two kernels' sum, 27 us at c4)
+__global__ __launch_bounds__(256) void transpose_cast_batch_kernel(const TCastBatch tb, const FramesArgs fa, int nfr) {
   __shared__ float tile[64][65];
+  if ((int)blockIdx.x < nfr) {
+    frames_tile(fa, blockIdx.x % fa.nbx, blockIdx.x / fa.nbx, tile);
+    return;
+  }
+  const int blk = blockIdx.x - nfr;
   int b = 0;
 #pragma unroll
-  for (int k = 1; k < 8; ++k) b += (k < tb.n && (int)blockIdx.x >= tb.tile0[k]) ? 1 : 0;
-  const int t = blockIdx.x - tb.tile0[b];
+  for (int k = 1; k < 8; ++k) b += (k < tb.n && blk >= tb.tile0[k]) ? 1 : 0;
+  const int t = blk - tb.tile0[b];
   const int R = tb.R[b], C = tb.C[b];
   const int c0 = (t % tb.tx[b]) * 64, r0 = (t / tb.tx[b]) * 64;
   const bool vec = (tb.vec >> b) & 1;
@@ -901,7 +942,8 @@ extern "C" int sv_cast_bf16_batch(int n, const float* const* x, bf16_t* const* y
 // dstr (optional, per matrix): also the row-major cast dstr[r C + c], from the same read; a null
 // dst[i] with a dstr[i]: the row-major cast alone
 int transpose_cast_bf16_batch(int n, const float* const* src, const long* lds, const int* R, const int* C,
-                              bf16_t* const* dst, const long* ldd, hipStream_t stream, bf16_t* const* dstr = nullptr) {
+                              bf16_t* const* dst, const long* ldd, hipStream_t stream, bf16_t* const* dstr = nullptr,
+                              const FramesArgs* frames = nullptr) {
   if (n <= 0 || n > 8) return SV_EARG;
   TCastBatch tb{};
   tb.n = n;
@@ -920,45 +962,27 @@ int transpose_cast_bf16_batch(int n, const float* const* src, const long* lds, c
     if (lds[i] % 4 == 0 && ldd[i] % 8 == 0 && !((uintptr_t)src[i] & 15) && !((uintptr_t)dst[i] & 15) && rv)
       tb.vec |= 1u << i;
   }
-  hipLaunchKernelGGL(transpose_cast_batch_kernel, dim3(tb.tile0[n]), dim3(256), 0, stream, tb);
+  const FramesArgs fa = frames ? *frames : FramesArgs{};
+  const int nfr = frames ? fa.nbx * fa.T : 0;
+  hipLaunchKernelGGL(transpose_cast_batch_kernel, dim3(nfr + tb.tile0[n]), dim3(256), 0, stream, tb, fa, nfr);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }
 
 // the bf16 stack's input in one launch (ABI v10; was to_time_major + a cast + a transpose-cast, and
-// T transpose-casts when B % 8 != 0): frames x [B,T,F] fp32 -> x_bf [T,B,F] and, when xT is given,
-// xT [F][T Bp] with column t Bp + b = x[b,t,:] (padding columns b in [B, Bp) zero) -- layer 0's
-// dW_ih operand.  Workgroup (t, 64 rows b): the tile goes through LDS so both stores coalesce.
-__global__ __launch_bounds__(256) void frames_to_bf16_kernel(const float* __restrict__ x, int B, int T, int F, int Bp,
-                                                             bf16_t* __restrict__ x_bf, bf16_t* __restrict__ xT) {
+// T transpose-casts when B % 8 != 0): frames_tile above, one workgroup per (64 rows, timestep)
+__global__ __launch_bounds__(256) void frames_to_bf16_kernel(const FramesArgs fa) {
   __shared__ float tile[64][65];  // [b][f], F <= 64
-  const int t = blockIdx.y, b0 = blockIdx.x * 64, tid = threadIdx.x;
-  // 16 predicated loads per thread, all in flight before the first LDS write (a rolled loop
-  // waited for each load on its own); thread -> (row tid / 64 + 4 i, column tid % 64)
-  float v[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int b = (tid >> 6) + 4 * i, f = tid & 63;
-    v[i] = (f < F && b0 + b < B) ? x[((long)(b0 + b) * T + t) * F + f] : 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) tile[(tid >> 6) + 4 * i][tid & 63] = v[i];
-  __syncthreads();
-  for (int i = tid; i < 64 * F; i += 256) {
-    const int b = i / F, f = i % F;
-    if (b0 + b < B) x_bf[((long)t * B + b0 + b) * F + f] = to_bf(tile[b][f]);
-  }
-  if (xT)
-    for (int i = tid; i < 64 * F; i += 256) {
-      const int f = i / 64, b = i % 64;
-      if (b0 + b < Bp) xT[(long)f * T * Bp + (long)t * Bp + b0 + b] = to_bf(tile[b][f]);
-    }
+  frames_tile(fa, blockIdx.x, blockIdx.y, tile);
+}
+static FramesArgs frames_args(const float* x, int B, int T, int F, bf16_t* x_bf, bf16_t* xT, int Bp) {
+  return FramesArgs{x, x_bf, xT, B, T, F, Bp, (std::max(B, xT ? Bp : B) + 63) / 64};
 }
 extern "C" int sv_frames_to_bf16(const float* x, int B, int T, int F, bf16_t* x_bf, bf16_t* xT, int Bp,
                                  hipStream_t stream) {
   if (!x || !x_bf || B <= 0 || T <= 0 || F <= 0 || F > 64 || (xT && Bp < B)) return SV_EARG;
-  hipLaunchKernelGGL(frames_to_bf16_kernel, dim3((std::max(B, xT ? Bp : B) + 63) / 64, T), dim3(256), 0, stream, x, B,
-                     T, F, Bp, x_bf, xT);
+  const FramesArgs fa = frames_args(x, B, T, F, x_bf, xT, Bp);
+  hipLaunchKernelGGL(frames_to_bf16_kernel, dim3(fa.nbx, T), dim3(256), 0, stream, fa);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }
@@ -1240,9 +1264,26 @@ static int wbf_transposes(int L, int F, int H, const float* const* w_ih, const f
 // regions, so that sv_lstm_bwd with SV_SCHED_WT_READY on the same workspace launches none (at the
 // c4 rank shape: the forward's cast and the backward's transposes, 13 + 20 us, read every weight
 // twice)
+static int weights_bf16(int L, int T, int B, int F, int H, const float* const* w_ih, const float* const* w_hh,
+                        bf16_t* const* w_ih_bf, bf16_t* const* w_hh_bf, void* bwd_workspace, hipStream_t stream,
+                        const FramesArgs* frames);
 extern "C" int sv_lstm_weights_bf16(int L, int T, int B, int F, int H, const float* const* w_ih,
                                     const float* const* w_hh, bf16_t* const* w_ih_bf, bf16_t* const* w_hh_bf,
                                     void* bwd_workspace, hipStream_t stream) {
+  return weights_bf16(L, T, B, F, H, w_ih, w_hh, w_ih_bf, w_hh_bf, bwd_workspace, stream, nullptr);
+}
+// ABI v11: sv_frames_to_bf16 and sv_lstm_weights_bf16 as ONE launch (the frames' workgroups beside
+// the weight tiles: at the c4 rank shape 10 + 17 us one after the other)
+extern "C" int sv_lstm_prep_bf16(int L, int T, int B, int F, int H, const float* x, bf16_t* x_bf, bf16_t* xT, int Bp,
+                                 const float* const* w_ih, const float* const* w_hh, bf16_t* const* w_ih_bf,
+                                 bf16_t* const* w_hh_bf, void* bwd_workspace, hipStream_t stream) {
+  if (!x || !x_bf || F > 64 || (xT && Bp < B)) return SV_EARG;
+  const FramesArgs fa = frames_args(x, B, T, F, x_bf, xT, Bp);
+  return weights_bf16(L, T, B, F, H, w_ih, w_hh, w_ih_bf, w_hh_bf, bwd_workspace, stream, &fa);
+}
+static int weights_bf16(int L, int T, int B, int F, int H, const float* const* w_ih, const float* const* w_hh,
+                        bf16_t* const* w_ih_bf, bf16_t* const* w_hh_bf, void* bwd_workspace, hipStream_t stream,
+                        const FramesArgs* frames) {
   if (L <= 0 || !w_ih || !w_hh || !w_ih_bf || !w_hh_bf) return SV_EARG;
   if (T <= 0 || B <= 0 || F <= 0 || H <= 0 || F % 8 || H % 8) return SV_ESHAPE;
   const size_t per = carve_bbwd(nullptr, T, B, std::max(F, H), H).total;
@@ -1270,7 +1311,7 @@ extern "C" int sv_lstm_weights_bf16(int L, int T, int B, int F, int H, const flo
       ++n;
     }
   }
-  return transpose_cast_bf16_batch(n, src, lds, R, C, dst, ldd, stream, dstr);
+  return transpose_cast_bf16_batch(n, src, lds, R, C, dst, ldd, stream, dstr, frames);  // frames: the last launch
 }
 
 // the hand-off scratch shared by the layers (persistent or wavefront backward), behind the L

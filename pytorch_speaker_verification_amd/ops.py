@@ -343,8 +343,7 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=Non
     fused_x = F <= 64
     if save:  # layer 0's dW_ih operand x^T [F][T Bp] (padding columns zero)
         st.xT0 = (torch.empty if fused_x or Bp == B else torch.zeros)((F, T * Bp), dtype=torch.bfloat16, device=dev)
-    if fused_x:  # x -> time-major bf16 and x^T in one launch (sv_frames_to_bf16)
-        call("sv_frames_to_bf16", ptr(x), B, T, F, ptr(x_bf), ptr(st.xT0) if save else None, Bp, s)
+    if fused_x:  # x -> time-major bf16 and x^T: in the weights' launch below (sv_lstm_prep_bf16)
         srcs, dsts = [], []
     else:
         x_tm = torch.empty((T, B, F), dtype=torch.float32, device=dev)
@@ -364,8 +363,12 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=Non
     wbf = [(_bf(w_ih.shape, dev), _bf(w_hh.shape, dev)) for (w_ih, w_hh, _, _) in layers]
     if save and PIPELINE_CHUNK > 0 and L > 1:
         st.bws = _ws(lib().sv_lstm_bwd_workspace(SV_DTYPE_BF16, L, T, B, F, H), dev)
-    call("sv_lstm_weights_bf16", L, T, B, F, H, _parr([l[0] for l in layers]), _parr([l[1] for l in layers]),
-         _parr([w[0] for w in wbf]), _parr([w[1] for w in wbf]), ptr(st.bws) if st.bws is not None else None, s)
+    wargs = (_parr([l[0] for l in layers]), _parr([l[1] for l in layers]), _parr([w[0] for w in wbf]),
+             _parr([w[1] for w in wbf]), ptr(st.bws) if st.bws is not None else None, s)
+    if fused_x:  # the frames' part in the same launch (sv_lstm_prep_bf16)
+        call("sv_lstm_prep_bf16", L, T, B, F, H, ptr(x), ptr(x_bf), ptr(st.xT0) if save else None, Bp, *wargs)
+    else:
+        call("sv_lstm_weights_bf16", L, T, B, F, H, *wargs)
     inp = x_bf
     gs = [_bf((T, B, 4 * H), dev) for _ in range(L)]  # bf16 x-projection in, bf16 activations out
     cs = [torch.empty((T, B, H), dtype=torch.float32, device=dev) for _ in range(L)]

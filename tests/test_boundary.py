@@ -41,7 +41,7 @@ def test_c_abi_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(h, s), s
         assert s in _lib.SIGNATURES, f"{s} missing from the ctypes signature table"
-    assert h.sv_abi_version() == _lib.ABI_VERSION == 10
+    assert h.sv_abi_version() == _lib.ABI_VERSION == 11
     assert not hasattr(h, "sv_test_set_fault")  # the fault injector exists only in the test build
     # workspace queries are host-only and callable without a GPU
     assert h.sv_ge2e_workspace_size(64, 10, 256, 64) > 0

@@ -312,3 +312,24 @@ def test_weights_bf16_transposes_handed_to_the_backward(B, T, schedule):
     for l in range(3):
         assert torch.equal(wih[l], layers[l][0].to(torch.bfloat16))
         assert torch.equal(whh[l], layers[l][1].to(torch.bfloat16))
+    # sv_lstm_prep_bf16 (ABI v11): the frames' launch folded into the weights' one -- the same bytes
+    # as sv_frames_to_bf16 + sv_lstm_weights_bf16 (padding columns of x^T included)
+    Bp = (B + 7) // 8 * 8
+    outs = []
+    for fused in (True, False):
+        xb = torch.full((T, B, F), float("nan"), device=dev).bfloat16()
+        xT = torch.full((F, T * Bp), float("nan"), device=dev).bfloat16()
+        wi = [torch.zeros_like(l[0], dtype=torch.bfloat16) for l in layers]
+        wh = [torch.zeros_like(l[1], dtype=torch.bfloat16) for l in layers]
+        wargs = (_parr([l[0] for l in layers]), _parr([l[1] for l in layers]), _parr(wi), _parr(wh), None,
+                 stream_of(x))
+        if fused:
+            call("sv_lstm_prep_bf16", 3, T, B, F, H, x.data_ptr(), xb.data_ptr(), xT.data_ptr(), Bp, *wargs)
+        else:
+            call("sv_frames_to_bf16", x.data_ptr(), B, T, F, xb.data_ptr(), xT.data_ptr(), Bp, stream_of(x))
+            call("sv_lstm_weights_bf16", 3, T, B, F, H, *wargs)
+        torch.cuda.synchronize()
+        outs.append([xb, xT] + wi + wh)
+    for a, b in zip(*outs):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+    assert torch.equal(outs[0][0].float(), x.transpose(0, 1).bfloat16().float())
