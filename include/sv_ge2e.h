@@ -64,14 +64,20 @@ int sv_abi_version(void);
  * bf16 stack backward only:
  *   SV_SCHED_WT_READY   (ABI v10) the workspace already holds the bf16 weight transposes, written by
  *                       sv_lstm_weights_bf16 (below) from the same weights into the same workspace:
- *                       no transpose launch (the fp32 backward ignores it). */
+ *                       no transpose launch (the fp32 backward ignores it).
+ *   SV_SCHED_CNT_READY  (ABI v11) the sync block's backward counter channels are still as the last
+ *                       bf16 stack forward on it left them (it zeroes them) -- no backward has run
+ *                       on the block since: the persistent / wavefront backward launches no
+ *                       counter zeroing (the caller tracks this; passing it wrongly makes the
+ *                       hand-off waits pass early). */
 #define SV_SCHED_AUTO 0
 #define SV_SCHED_PER_LAYER 1
 #define SV_SCHED_PER_STEP 2
 #define SV_SCHED_PERSIST 4
 #define SV_SCHED_NO_EVENTS 8
 #define SV_SCHED_WT_READY 16
-#define SV_SCHED_MASK 31
+#define SV_SCHED_CNT_READY 32
+#define SV_SCHED_MASK 63
 
 /* ---- dense fp32 MFMA GEMM (used by every op below; exported for tests) -----------------
  * C[M,N] = op(A) op(B) (+ bias0[n] + bias1[n]) (+ beta C).
@@ -403,6 +409,12 @@ int sv_clip_sgd_step(float* params, float* grads, long n, float max_norm, float 
 int sv_clip_sgd_step2(float* params0, float* grads0, long n0, float max_norm0, float* params1, float* grads1,
                       long n1, float max_norm1, float lr, int write_grad, float* total_norm_out, const void* sync,
                       float* workspace, hipStream_t stream);
+/* (ABI v11) sv_clip_sgd_step2 with the training step's status report in its update launch: as
+ * sv_status_report(sync, report_x, report_n, host_slot_dev, seq) after it, one launch fewer */
+int sv_clip_sgd_step2_report(float* params0, float* grads0, long n0, float max_norm0, float* params1, float* grads1,
+                             long n1, float max_norm1, float lr, int write_grad, float* total_norm_out,
+                             const void* sync, float* workspace, float* report_x, int report_n, void* host_slot_dev,
+                             unsigned seq, hipStream_t stream);
 
 #ifdef __cplusplus
 }

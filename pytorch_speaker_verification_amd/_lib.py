@@ -23,6 +23,7 @@ SV_DTYPE_F32, SV_DTYPE_BF16 = 0, 1  # include/sv_ge2e.h
 SCHEDULES = {"auto": 0, "per_layer": 1, "per_step": 2, "persist": 5}  # persist: per-layer persistent, any H
 SV_SCHED_NO_EVENTS = 8  # the stack backward records no per-layer completion events (nothing waits on them)
 SV_SCHED_WT_READY = 16  # the bf16 backward workspace already holds sv_lstm_weights_bf16's transposes
+SV_SCHED_CNT_READY = 32  # the bf16 backward's counter channels are as the last stack forward zeroed them
 
 
 def schedule_flags(schedule):
@@ -131,6 +132,8 @@ SIGNATURES = {
     "sv_clip_sgd_step": (_c_int, [_P, _P, _c_long, _c_float, _c_float, _c_int, _P, _P, _P, _P]),
     "sv_clip_sgd_step2": (_c_int, [_P, _P, _c_long, _c_float, _P, _P, _c_long, _c_float, _c_float, _c_int, _P, _P, _P,
                                    _P]),
+    "sv_clip_sgd_step2_report": (_c_int, [_P, _P, _c_long, _c_float, _P, _P, _c_long, _c_float, _c_float, _c_int, _P,
+                                          _P, _P, _P, _c_int, _P, ctypes.c_uint, _P]),
 }
 
 ERRORS = {-1: "invalid argument (SV_EARG)", -2: "misaligned pointer/leading dim (SV_EALIGN)",
@@ -219,6 +222,9 @@ class PersistStatus:
         self._pending = []
         self._ring = None  # pinned host slots of sv_status_report, set up on first use
         self._seq = 0
+        # the bf16 stack forward zeroed the block's backward counter channels and no backward has
+        # run on it since (ops.py: the next bf16 backward passes SV_SCHED_CNT_READY)
+        self.bwd_counters_clean = False
 
     def ptr(self):
         return self.block.data_ptr()
@@ -226,6 +232,13 @@ class PersistStatus:
     def report(self, x):
         """x (fp32, contiguous, on the block's device) := NaN if the status is set, and the status
         reported into the next host slot, both stream-ordered on x's stream (sv_status_report)."""
+        slot, seq = self.next_slot()
+        call("sv_status_report", self.ptr(), ptr(x), x.numel(), slot, seq, stream_of(x))
+
+    def next_slot(self):
+        """(device address, sequence number) of the next host report slot, registered as a pending
+        check: the caller's launch (sv_status_report, or the trainer's sv_clip_sgd_step2_report)
+        must store (seq << 32) | status there."""
         if self._ring is None:
             ring = torch.zeros(self.RING, dtype=torch.int64, pin_memory=True)
             dev = ctypes.c_void_p()
@@ -237,8 +250,8 @@ class PersistStatus:
             self.poll(wait=True)  # every slot in use: the host is a whole ring ahead of the device
         self._seq = self._seq % 0xFFFFFFFF + 1  # (never 0: a fresh slot reads 0)
         k = self._seq % self.RING
-        call("sv_status_report", self.ptr(), ptr(x), x.numel(), self._ring_dev + 8 * k, self._seq, stream_of(x))
         self._pending.append(("slot", k, self._seq))
+        return self._ring_dev + 8 * k, self._seq
 
     def arm(self):
         host = torch.empty(1, dtype=torch.int32, pin_memory=True)

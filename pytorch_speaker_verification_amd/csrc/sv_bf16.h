@@ -365,11 +365,15 @@ __device__ __forceinline__ void lstm_cell_bwd_x4(const V4& dh, const A4& i, cons
 //                             the launch drains; outputs since then are invalid)
 //   [SV_SYNC_CNT ..)          arrival counters: SV_SYNC_CHANNELS channels x SV_PCNT_ROWS row
 //                             blocks x SV_PCNT_STRIDE words (one 128-B line per counter); each
-//                             launch zeroes the rows it uses of its channel
+//                             launch zeroes the rows it uses of its channel, unless the stack
+//                             forward zeroed them all (r06: the forward recurrences' channels
+//                             0 .. L-1 and, from SV_BWD_CH0 on, the backward's, in its state-reset
+//                             launch; a backward with SV_SCHED_CNT_READY then zeroes none)
 //   [SV_SYNC_STAMP ..)        u64 phase stamps of the persistent backward (profiling)
 #define SV_PCNT_ROWS 64
 #define SV_PCNT_STRIDE 32
-#define SV_SYNC_CHANNELS 4
+#define SV_SYNC_CHANNELS 8
+#define SV_BWD_CH0 4  // the backward recurrences' channels: SV_BWD_CH0 + layer (wavefront: + its dW flags at + L)
 #define SV_SYNC_CNT 32
 #define SV_NSTAMP 8
 #define SV_NSTAMP_WG 1024
@@ -384,7 +388,7 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
                         bf16_t* h_bf, bf16_t* hT, hipStream_t stream, unsigned* sync, int chan = 0,
                         const bf16_t* x_bf = nullptr, int F = 0, const bf16_t* wih_bf = nullptr,
                         const float* b_ih = nullptr, const float* b_hh = nullptr, hipEvent_t pre = nullptr,
-                        hipEvent_t post = nullptr);
+                        hipEvent_t post = nullptr, int counters_zeroed = 0);
 // persistent backward recurrence of one layer (sv_persist.hip)
 extern "C" int sv_persist_bwd_ok(int B, int H);
 extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H);
@@ -392,7 +396,7 @@ int sv_persist_bm(int B, int H, int cus);
 int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
                         const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream,
                         unsigned* sync, float* db_ih = nullptr, float* db_hh = nullptr, hipEvent_t pre = nullptr,
-                        hipEvent_t post = nullptr);
+                        hipEvent_t post = nullptr, int chan = 0, int counters_zeroed = 0);
 // launcher of the wide-tile persistent backward (sv_persist3.hip; grid = nub x nrb workgroups)
 int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whhT, const bf16_t* acts,
                            const float* c_tm, const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT,
@@ -451,4 +455,4 @@ int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, cons
                      const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
                      bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
                      float* const* db_hh, hipEvent_t pre, hipEvent_t post, long ldwih = 0,
-                     int zero_next = 0);
+                     int zero_next = 0, int ch0 = 0, int counters_zeroed = 0);

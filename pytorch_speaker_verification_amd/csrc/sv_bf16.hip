@@ -1117,12 +1117,12 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
       p[n] = h_bf[l], b[n++] = BH * sizeof(bf16_t);
       if (hT[l] && Bp != B) p[n] = hT[l], b[n++] = (size_t)H * ldhT * sizeof(bf16_t);
     }
-    if (cnt) {
+    if (cnt) {  // every counter channel: this forward's and the backward's that follows
       if (n == SV_ZB_MAX) {
         if (int rc = sv_zero_bytes_multi(n, p, b, s)) return rc;
         n = 0;
       }
-      p[n] = sync + SV_SYNC_CNT, b[n++] = (size_t)L * SV_PCNT_ROWS * SV_PCNT_STRIDE * sizeof(unsigned);
+      p[n] = sync + SV_SYNC_CNT, b[n++] = (size_t)SV_SYNC_CHANNELS * SV_PCNT_ROWS * SV_PCNT_STRIDE * sizeof(unsigned);
     }
     return sv_zero_bytes_multi(n, p, b, s);
   };
@@ -1139,27 +1139,37 @@ extern "C" int sv_lstm_stack_fwd_bf16(int L, int T, int B, int F, int H, const b
   if (sched_persist(schedule, H) && sv_persist_fwd_fits(B, H, sv_stream_cus(main))) {
     if (!sync) return SV_EARG;
     // persistent schedule on `main`: per layer the whole-T K1 GEMM, then one launch for the
-    // recurrence (sv_persist.hip); layers run one after another
-    if ((rc = zero_states(main, false))) return rc;
+    // recurrence (sv_persist.hip); layers run one after another, layer l on counter channel l
+    // (zeroed, with the backward's, in the state-reset launch) where L <= SV_BWD_CH0, else all on
+    // channel 0, each launch zeroing it
+    const bool own = L <= SV_BWD_CH0;
+    if ((rc = zero_states(main, true))) return rc;
     for (int l = 0; l < L; ++l) {
       const int Fl = l == 0 ? F : H;
       const bf16_t* in = l == 0 ? x_bf : h_bf[l - 1] + BH;
       if (l == 0 && sv_persist_fwd_fusex_ok(H, F)) {  // layer 0's input projection inside the recurrence
-        if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, sync, 0,
-                                      x_bf, F, w_ih_bf[l], b_ih[l], b_hh[l], probe ? probe[2 * l] : nullptr,
-                                      probe ? probe[2 * l + 1] : nullptr)))
+        if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, sync,
+                                      own ? l : 0, x_bf, F, w_ih_bf[l], b_ih[l], b_hh[l],
+                                      probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr, own)))
           return rc;
         continue;
       }
       rc = sv_gemm_bf16_bf(T * B, 4 * H, Fl, in, Fl, w_ih_bf[l], Fl, gates[l], 4L * H, b_ih[l], b_hh[l], main);
       if (rc) return rc;
-      if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, sync, 0,
-                                    nullptr, 0, nullptr, nullptr, nullptr, probe ? probe[2 * l] : nullptr,
-                                    probe ? probe[2 * l + 1] : nullptr)))
+      if ((rc = sv_persist_fwd_bf16(T, B, H, w_hh_bf[l], gates[l], c_tm[l], h_tm[l], h_bf[l], hT[l], main, sync,
+                                    own ? l : 0, nullptr, 0, nullptr, nullptr, nullptr,
+                                    probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr, own)))
         return rc;
     }
     return SV_OK;
   }
+  // per-step schedule: no counters of its own, but the backward's zeroed all the same (the
+  // caller may pass SV_SCHED_CNT_READY to a persistent backward after any stack forward)
+  if (sync && (rc = sv_zero_bytes(sync + SV_SYNC_CNT + (size_t)SV_BWD_CH0 * SV_PCNT_ROWS * SV_PCNT_STRIDE,
+                                  (size_t)(SV_SYNC_CHANNELS - SV_BWD_CH0) * SV_PCNT_ROWS * SV_PCNT_STRIDE *
+                                      sizeof(unsigned),
+                                  main)))
+    return rc;
   hipEvent_t ev_start = ev[L * nch];
   e = hipEventRecord(ev_start, main);
   if (e != hipSuccess) return (int)e;
@@ -1351,6 +1361,9 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
   const bool evs = !(schedule & SV_SCHED_NO_EVENTS);
   // SV_SCHED_WT_READY: sv_lstm_weights_bf16 already wrote the transposes into this workspace
   const bool wt_ready = schedule & SV_SCHED_WT_READY;
+  // SV_SCHED_CNT_READY: the stack forward zeroed the backward's counter channels and no backward
+  // has used this sync block since (the caller tracks that): no zeroing launches here
+  const bool cnt_ready = schedule & SV_SCHED_CNT_READY;
   if (sched_wave(schedule, H) && sv_wave_bwd_fits(L, B, H, sv_stream_cus(main))) {
     if (!sync) return SV_EARG;
     // layer-wavefront schedule: every layer's recurrence and upstream gradient dx in one launch
@@ -1406,14 +1419,14 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       if (f.nsw <= 0 || f.S < 4 || (size_t)fP * G256_BM * G256_BM * 4 > wsp.gbytes) f.nsw = f.S = 0;
       if (f.S > 0) {
         f.part = wsp.gws;
-        f.flag = sync + SV_SYNC_CNT + (size_t)WB_L * SV_PCNT_ROWS * SV_PCNT_STRIDE;  // channel 3, zeroed with the
+        f.flag = sync + SV_SYNC_CNT + (size_t)(SV_BWD_CH0 + WB_L) * SV_PCNT_ROWS * SV_PCNT_STRIDE;  // zeroed with the
         f.status = sync;                                                             // wavefront's counters
         f.limit = sv_persist_limit();
       }
     }
     rc = sv_wave_bwd_bf16(L, T, B, H, whhT_l, wihT_l, gates, c_tm, dh_last, dx, dgT, (char*)workspace + per * L,
                               sync, main, db_ih, db_hh, probe ? probe[0] : nullptr, probe ? probe[1] : nullptr,
-                              bf16_wiht_ld(H), f.S > 0 ? fP : 0);
+                              bf16_wiht_ld(H), f.S > 0 ? fP : 0, SV_BWD_CH0, cnt_ready);
     if (rc) return rc;
     if (fullk) {
       hipLaunchKernelGGL(gemm_bf16_8qf_kernel, dim3(f.nsw + fP), dim3(512), G256_LDS, main, f);
@@ -1462,10 +1475,14 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       const float* up = l == L - 1 ? dh_last : dx[l + 1];
       bf16_t* dgf = (bf16_t*)((char*)workspace + per * L);
       const bool afr = l > 0 && gemm_afrag_ok(T, B, Fl, H);  // dx reads dgf: no row-major dG
+      // layer l on channel SV_BWD_CH0 + l, pre-zeroed by the forward (cnt_ready) where the layers fit
+      // the channels, else each launch zeroing its own
+      const bool own = L <= SV_SYNC_CHANNELS - SV_BWD_CH0;
       if ((rc = sv_persist_bwd_bf16(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1,
                                     (afr || l == 0) ? nullptr : dg[l],  // layer 0 has no dx GEMM
                                     dgT[l], dgf, main, sync, db_ih[l], db_hh ? db_hh[l] : nullptr,
-                                    probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr)))
+                                    probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr,
+                                    SV_BWD_CH0 + (own ? l : 0), own && cnt_ready)))
         return rc;
       // the completion events of layers >= 1 (grad_ready: a caller's bucketed all-reduce) fire once
       // the last recurrence is done, so collectives never share the device with a persistent launch

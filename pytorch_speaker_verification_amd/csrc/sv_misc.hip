@@ -272,9 +272,25 @@ __global__ __launch_bounds__(256) void clip_sgd_kernel(float* __restrict__ p, fl
                                                        const unsigned* __restrict__ status) {
   clip_sgd_body(p, g, n, blockIdx.x, gridDim.x, partial, npart, max_norm, lr, write_grad, norm_out, status);
 }
+// the training step's status report (sv_status_report's kernel) folded into the update launch
+// (ABI v11, sv_clip_sgd_step2_report): workgroup 0 poisons x[0..n) when the status is set and
+// stores (seq << 32) | status into the pinned host slot (slot null: no report)
+struct ClipReport {
+  float* x;
+  int n;
+  unsigned long long* slot;
+  unsigned seq;
+};
 __global__ __launch_bounds__(256) void clip_sgd2_kernel(ClipGroup g0, ClipGroup g1, const float* __restrict__ partial,
                                                         float lr, int write_grad, float* __restrict__ norm_out,
-                                                        const unsigned* __restrict__ status) {
+                                                        const unsigned* __restrict__ status, const ClipReport rep) {
+  if (rep.slot && blockIdx.x == 0) {
+    const unsigned st = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = threadIdx.x; i < rep.n && st; i += blockDim.x) rep.x[i] = __builtin_nanf("");
+    if (threadIdx.x == 0)
+      __hip_atomic_store(rep.slot, ((unsigned long long)rep.seq << 32) | st, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   const bool one = (int)blockIdx.x >= g1.first;
   const ClipGroup& c = one ? g1 : g0;
   clip_sgd_body(c.p, c.g, c.n, blockIdx.x - c.first, c.blocks, partial + (one ? CLIP_BLOCKS : 0), c.blocks,
@@ -296,9 +312,29 @@ extern "C" int sv_clip_sgd_step(float* params, float* grads, long n, float max_n
   return SV_OK;
 }
 
+static int clip_sgd_step2(float* params0, float* grads0, long n0, float max_norm0, float* params1, float* grads1,
+                          long n1, float max_norm1, float lr, int write_grad, float* total_norm_out, const void* sync,
+                          float* workspace, hipStream_t stream, const ClipReport& rep);
 extern "C" int sv_clip_sgd_step2(float* params0, float* grads0, long n0, float max_norm0, float* params1,
                                  float* grads1, long n1, float max_norm1, float lr, int write_grad,
                                  float* total_norm_out, const void* sync, float* workspace, hipStream_t stream) {
+  return clip_sgd_step2(params0, grads0, n0, max_norm0, params1, grads1, n1, max_norm1, lr, write_grad, total_norm_out,
+                        sync, workspace, stream, ClipReport{nullptr, 0, nullptr, 0});
+}
+extern "C" int sv_clip_sgd_step2_report(float* params0, float* grads0, long n0, float max_norm0, float* params1,
+                                        float* grads1, long n1, float max_norm1, float lr, int write_grad,
+                                        float* total_norm_out, const void* sync, float* workspace,
+                                        float* report_x, int report_n, void* host_slot_dev, unsigned seq,
+                                        hipStream_t stream) {
+  if (!sync || !host_slot_dev || report_n < 0 || (report_n > 0 && !report_x) || ((uintptr_t)host_slot_dev & 7))
+    return SV_EARG;
+  return clip_sgd_step2(params0, grads0, n0, max_norm0, params1, grads1, n1, max_norm1, lr, write_grad, total_norm_out,
+                        sync, workspace, stream,
+                        ClipReport{report_x, report_n, reinterpret_cast<unsigned long long*>(host_slot_dev), seq});
+}
+static int clip_sgd_step2(float* params0, float* grads0, long n0, float max_norm0, float* params1, float* grads1,
+                          long n1, float max_norm1, float lr, int write_grad, float* total_norm_out, const void* sync,
+                          float* workspace, hipStream_t stream, const ClipReport& rep) {
   if (!params0 || !grads0 || !params1 || !grads1 || !workspace || n0 <= 0 || n1 <= 0) return SV_EARG;
   if (((uintptr_t)params0 | (uintptr_t)grads0 | (uintptr_t)params1 | (uintptr_t)grads1) & 15) return SV_EALIGN;
   ClipGroup g0{params0, grads0, n0, max_norm0, (int)std::min<long>(CLIP_BLOCKS, (n0 / 4 + 255) / 256 + 1), 0};
@@ -308,7 +344,7 @@ extern "C" int sv_clip_sgd_step2(float* params0, float* grads0, long n0, float m
   hipLaunchKernelGGL(sqsum_partial2_kernel, dim3(blocks), dim3(256), 0, stream, g0, g1, workspace);
   SV_LAUNCH_CHECK();
   hipLaunchKernelGGL(clip_sgd2_kernel, dim3(blocks), dim3(256), 0, stream, g0, g1, workspace, lr, write_grad,
-                     total_norm_out, reinterpret_cast<const unsigned*>(sync));
+                     total_norm_out, reinterpret_cast<const unsigned*>(sync), rep);
   SV_LAUNCH_CHECK();
   return SV_OK;
 }

@@ -1034,7 +1034,7 @@ int pbwd3_ok(int B, int H, int cus);
 int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates, float* c_tm, float* h_tm,
                         bf16_t* h_bf, bf16_t* hT, hipStream_t stream, unsigned* sync, int chan, const bf16_t* x_bf,
                         int F, const bf16_t* wih_bf, const float* b_ih, const float* b_hh, hipEvent_t pre,
-                        hipEvent_t post) {
+                        hipEvent_t post, int counters_zeroed) {
   const int cus = sv_stream_cus(stream);
   if (!sv_persist_fwd_fits(B, H, cus)) return SV_ESHAPE;
   if (!sync || chan < 0 || chan >= SV_SYNC_CHANNELS) return SV_EARG;
@@ -1049,7 +1049,7 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
   const bool wide = wst && pbwd3_ok(B, H, cus);
   const int bm = wide ? 32 : wst ? persist_bm(B, H, cus) : BF_BM;
   const dim3 grid(wide ? H / 64 : (H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
-  hipError_t e = (hipError_t)sv_zero_counters(cnt, 1, 0, grid.y * SV_PCNT_STRIDE, stream);
+  hipError_t e = counters_zeroed ? hipSuccess : (hipError_t)sv_zero_counters(cnt, 1, 0, grid.y * SV_PCNT_STRIDE, stream);
   if (e != hipSuccess) return (int)e;
   const unsigned limit = persist_limit();
   const int fault = fwd_fault();
@@ -1144,14 +1144,16 @@ extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H) {
 // one layer's backward recurrence for all t (reverse), on `stream`: dG (bf16, row-major and
 // transposed) from the activations, cell states and the upstream dh (dhup [T,B,H] if up_full,
 // else [B,H] at t = T-1 only, or NULL).  dgT: [4H][T*Bp] (padding columns written as zeros).
-// dgf: sv_persist_bwd_scratch(T, B, H) bytes.  Counter channel 0 of `sync`.
+// dgf: sv_persist_bwd_scratch(T, B, H) bytes.  Counter channel `chan` of `sync` (zeroed here unless
+// counters_zeroed).
 int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
                         const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream,
-                        unsigned* sync, float* db_ih, float* db_hh, hipEvent_t pre, hipEvent_t post) {
+                        unsigned* sync, float* db_ih, float* db_hh, hipEvent_t pre, hipEvent_t post, int chan,
+                        int counters_zeroed) {
   const int cus = sv_stream_cus(stream);
   if (!sv_persist_bwd_fits(B, H, cus)) return SV_ESHAPE;
-  if (!dgf || ((uintptr_t)dgf & 15) || !sync) return SV_EARG;
-  unsigned* cnt = sync_cnt(sync, 0);
+  if (!dgf || ((uintptr_t)dgf & 15) || !sync || chan < 0 || chan >= SV_SYNC_CHANNELS) return SV_EARG;
+  unsigned* cnt = sync_cnt(sync, chan);
   const int Bp = (B + 7) & ~7;
   const long lddgT = (long)T * Bp;
   const bool wide = pbwd3_ok(B, H, cus);
@@ -1161,7 +1163,7 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
   float* dbp = db_ih ? reinterpret_cast<float*>(reinterpret_cast<char*>(dgf) +
                                                 (size_t)T * ((B + BF_BM - 1) / BF_BM) * BF_BM * 4 * H * sizeof(bf16_t))
                      : nullptr;
-  hipError_t e = (hipError_t)sv_zero_counters(cnt, 1, 0, grid.y * SV_PCNT_STRIDE, stream);
+  hipError_t e = counters_zeroed ? hipSuccess : (hipError_t)sv_zero_counters(cnt, 1, 0, grid.y * SV_PCNT_STRIDE, stream);
   if (e != hipSuccess) return (int)e;
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
   // A-fragment prefetch depth 8 at H = 768 (measured: 4 / 16 no better)
@@ -1209,12 +1211,13 @@ size_t sv_wave_bwd_scratch(int L, int T, int B, int H) {
 }
 // dx[l] (l >= 1): layer l's upstream gradient for layer l-1, [T][B][H] fp32 (written whole);
 // dgT[l]: [4H][T*Bp] (padding columns written as zeros); db_ih NULL: bias gradients not computed.
-// Counter channels 0..L-1 of `sync`.
+// Counter channels ch0 .. ch0 + L - 1 of `sync` (+ channel ch0 + L for zero_next), zeroed here unless
+// counters_zeroed.
 int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, const bf16_t* const* wihT,
                      const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
                      bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
                      float* const* db_hh, hipEvent_t pre, hipEvent_t post, long ldwih,
-                     int zero_next) {
+                     int zero_next, int ch0, int counters_zeroed) {
   if (!sv_wave_bwd_fits(L, B, H, sv_stream_cus(stream))) return SV_ESHAPE;
   if (!scratch || ((uintptr_t)scratch & 15) || !sync || !dh_last || !whhT || !wihT || !acts || !c_tm || !dx || !dgT)
     return SV_EARG;
@@ -1235,14 +1238,17 @@ int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, cons
     p += wave_frag_bytes(T, B, H);
     a.dbp[l] = db_ih ? reinterpret_cast<float*>(p) : nullptr;
     p += wave_dbp_bytes(B, H);
-    a.cnt[l] = sync_cnt(sync, l);
+    a.cnt[l] = sync_cnt(sync, ch0 + l);
   }
-  if (zero_next > 0 && (L + 1 > SV_SYNC_CHANNELS || zero_next > SV_PCNT_ROWS * SV_PCNT_STRIDE)) return SV_EARG;
-  // zero_next > 0: channel L's first zero_next words too (the flags of the weight-gradient launch
-  // that follows, gemm_bf16_8qf_kernel), in the same launch
-  if (int rc = sv_zero_counters(a.cnt[0], zero_next > 0 ? L + 1 : L, (long)SV_PCNT_ROWS * SV_PCNT_STRIDE,
-                                std::max(a.nrb * SV_PCNT_STRIDE, zero_next), stream))
-    return rc;
+  if (ch0 < 0 || ch0 + L + (zero_next > 0 ? 1 : 0) > SV_SYNC_CHANNELS ||
+      zero_next > SV_PCNT_ROWS * SV_PCNT_STRIDE)
+    return SV_EARG;
+  // zero_next > 0: channel ch0 + L's first zero_next words too (the flags of the weight-gradient
+  // launch that follows, gemm_bf16_8qf_kernel), in the same launch
+  if (!counters_zeroed)
+    if (int rc = sv_zero_counters(a.cnt[0], zero_next > 0 ? L + 1 : L, (long)SV_PCNT_ROWS * SV_PCNT_STRIDE,
+                                  std::max(a.nrb * SV_PCNT_STRIDE, zero_next), stream))
+      return rc;
   a.dh_last = dh_last;
   a.status = sync;
   a.limit = persist_limit();

@@ -16,8 +16,8 @@ import ctypes
 
 import torch
 
-from ._lib import (SV_DTYPE_BF16, SV_DTYPE_F32, SV_SCHED_NO_EVENTS, SV_SCHED_WT_READY, PersistStatus, call, lib,
-                   ptr, require_device, schedule_flags, stream_of)
+from ._lib import (SV_DTYPE_BF16, SV_DTYPE_F32, SV_SCHED_CNT_READY, SV_SCHED_NO_EVENTS, SV_SCHED_WT_READY,
+                   PersistStatus, call, lib, ptr, require_device, schedule_flags, stream_of)
 
 # timesteps per chunk of the layer-pipelined schedules (measured at c2: 16 / 24 / 32 / 48 / 64 ->
 # 69.3 / 69.7 / 69.1 / 69.5 / 69.6 ms per step)
@@ -385,6 +385,7 @@ def embedder_forward_bf16(x, layers, w_p, b_p, save=True, status=None, probe=Non
              _parr([w[1] for w in wbf]), _parr([l[2] for l in layers]), _parr([l[3] for l in layers]),
              _parr(gs), _parr(cs), _parr(hs), _parr(hbs), _parr(hTs), PIPELINE_CHUNK, s, sp, ep, 0, sched,
              sync.ptr(), _evarr(probe))
+        sync.bwd_counters_clean = True  # (the stack forward zeroes the backward's channels, every schedule)
         _release_status(sync, own)
     else:
         for l, (w_ih, w_hh, b_ih, b_hh) in enumerate(layers):
@@ -469,6 +470,9 @@ def embedder_backward_bf16(st, demb, layers, w_p, grads=None, grad_ready=None, s
         sp = (ctypes.c_void_p * L)(*[st_.cuda_stream for st_ in streams])
         ep = (ctypes.c_void_p * nev)(*[e.cuda_event for e in events[:nev]])
         sync, own = _own_status(status, dev)
+        if sync.bwd_counters_clean:  # the forward zeroed the backward's counters, none used since
+            sched |= SV_SCHED_CNT_READY
+        sync.bwd_counters_clean = False
         call("sv_lstm_bwd", SV_DTYPE_BF16, L, T, B, F0, H, (ctypes.c_void_p * L)(*xT), (ctypes.c_long * L)(*ld),
              _parr([l[0] for l in layers]), _parr([l[1] for l in layers]), _parr(st.gates), _parr(st.c_tm),
              _parr(st.hT), ptr(dh_last), _parr(dgs), _parr(dgTs), _parr(dxs),
@@ -695,14 +699,24 @@ def clip_sgd_step_(flat_params, flat_grads, max_norm, lr, write_grad=False, norm
          stream_of(flat_params))
 
 
-def clip_sgd_step2_(p0, g0, max_norm0, p1, g1, max_norm1, lr, write_grad=False, norm_out=None, status=None):
+def clip_sgd_step2_(p0, g0, max_norm0, p1, g1, max_norm1, lr, write_grad=False, norm_out=None, status=None,
+                    report=None):
     """clip_sgd_step_ over two flat parameter groups (the network's and the loss's {w, b},
-    train_speech_embedder.py:63-65) in one pair of launches; bit-identical to two calls."""
+    train_speech_embedder.py:63-65) in one pair of launches; bit-identical to two calls.
+    report: a tensor x for ``status.report(x)`` done inside the update launch
+    (sv_clip_sgd_step2_report: the training step's status report without a launch of its own)."""
     require_device(p0, g0, p1, g1)
     ws = _ws(2 * lib().sv_clip_sgd_workspace(), p0.device)
-    call("sv_clip_sgd_step2", ptr(p0), ptr(g0), p0.numel(), float(max_norm0), ptr(p1), ptr(g1), p1.numel(),
-         float(max_norm1), float(lr), int(write_grad), ptr(norm_out), status.ptr() if status is not None else None,
-         ptr(ws), stream_of(p0))
+    args = (ptr(p0), ptr(g0), p0.numel(), float(max_norm0), ptr(p1), ptr(g1), p1.numel(), float(max_norm1), float(lr),
+            int(write_grad), ptr(norm_out), status.ptr() if status is not None else None, ptr(ws))
+    if report is not None:
+        if status is None:
+            raise ValueError("clip_sgd_step2_: report needs the status block")
+        require_device(report)
+        slot, seq = status.next_slot()
+        call("sv_clip_sgd_step2_report", *args, ptr(report), report.numel(), slot, seq, stream_of(p0))
+    else:
+        call("sv_clip_sgd_step2", *args, stream_of(p0))
 
 
 def gemm_f32(A, B, a_kcontig=True, b_kcontig=True, bias=None, products="mfma_f32"):

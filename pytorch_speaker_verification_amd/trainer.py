@@ -253,10 +253,10 @@ class GE2ETrainer:
             # any rank's timeout -> this rank's status too: every rank skips the update
             call("sv_status_merge", self.status.ptr(), ptr(self.flags), stream_of(self.flags))
         n = self.n_pad
-        # clip_grad_norm_ x2 + SGD (train_speech_embedder.py:63-65): both groups in one launch pair
-        clip_sgd_step2_(self.flat_p[:n], self.flat_g[:n], self.clip_net, self.flat_p[n:n + 4], self.flat_g[n:n + 4],
-                        self.clip_wb, self.lr, self.write_grads, status=self.status)
+        # clip_grad_norm_ x2 + SGD (train_speech_embedder.py:63-65): both groups in one launch pair,
+        # the second also the step's report -- NaN loss on a timeout, and the status word to a pinned
+        # host slot (no copy, no event, no launch of its own)
         loss = loss.clone() if dp else loss  # (not a view of flat_g, which the next step reuses)
-        # NaN loss on a timeout, and the status word to a pinned host slot (no copy, no event)
-        self.status.report(loss)
+        clip_sgd_step2_(self.flat_p[:n], self.flat_g[:n], self.clip_net, self.flat_p[n:n + 4], self.flat_g[n:n + 4],
+                        self.clip_wb, self.lr, self.write_grads, status=self.status, report=loss)
         return loss
