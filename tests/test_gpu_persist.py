@@ -333,3 +333,44 @@ def test_weights_bf16_transposes_handed_to_the_backward(B, T, schedule):
     for a, b in zip(*outs):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16))
     assert torch.equal(outs[0][0].float(), x.transpose(0, 1).bfloat16().float())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,schedule", [(80, "auto"), (320, "per_layer")])
+def test_second_backward_zeroes_its_own_counters(B, schedule):
+    """SV_SCHED_CNT_READY (ABI v11): the stack forward zeroes the backward's counter channels, so the
+    first backward on its sync block launches no zeroing; a second backward of the same forward on
+    the same block (as retain_graph would run it) must zero them itself -- with stale counters its
+    hand-off waits would pass at once.  Both backwards must give the same gradients bit for bit."""
+    import recipe
+    import torch
+    from conftest import model_dims
+    from pytorch_speaker_verification_amd.speech_embedder_net import SpeechEmbedder
+    dev = torch.device("cuda", 0)
+    dims = (40, 768, 3, 256)
+    sd = recipe.make_weights(23, *dims, scale=3.0)
+    with model_dims(*dims):
+        net = SpeechEmbedder()
+    with torch.no_grad():
+        for k, v in net.state_dict().items():
+            v.copy_(torch.as_tensor(sd[k]))
+    net = net.to(dev)
+    from pytorch_speaker_verification_amd import ops
+    from pytorch_speaker_verification_amd._lib import PersistStatus
+    layers = net.LSTM_stack.layer_params()
+    wp, bp = net.projection.weight, net.projection.bias
+    x = torch.as_tensor(recipe.make_frames(24, B, 12, 40)).to(dev)
+    demb = torch.as_tensor(np.random.default_rng(25).standard_normal((B, 256)).astype(np.float32)).to(dev)
+    status = PersistStatus(dev)  # one caller-owned sync block for the forward and both backwards
+    _, st = ops.embedder_forward_bf16(x, layers, wp, bp, save=True, status=status, schedule=schedule)
+    assert status.bwd_counters_clean
+    g = []
+    for _ in range(2):
+        g.append([t.clone() for t in ops.embedder_backward_bf16(st, demb, layers, wp, status=status,
+                                                                 schedule=schedule)])
+        assert not status.bwd_counters_clean
+    torch.cuda.synchronize()
+    status.poll(wait=True)
+    assert int(status.block[0]) == 0
+    for a, b in zip(*g):
+        assert torch.equal(a, b)
