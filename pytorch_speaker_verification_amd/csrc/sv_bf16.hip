@@ -1324,6 +1324,9 @@ static int weights_bf16(int L, int T, int B, int F, int H, const float* const* w
   return transpose_cast_bf16_batch(n, src, lds, R, C, dst, ldd, stream, dstr, frames);  // frames: the last launch
 }
 
+#ifndef SV_PERSIST_FULLK
+#define SV_PERSIST_FULLK 1  // the persistent schedule's weight gradients as one whole-K launch (A/B)
+#endif
 // the hand-off scratch shared by the layers (persistent or wavefront backward), behind the L
 // per-layer regions
 static size_t bbwd_scratch(int L, int T, int B, int H) {
@@ -1364,6 +1367,67 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
   // SV_SCHED_CNT_READY: the stack forward zeroed the backward's counter channels and no backward
   // has used this sync block since (the caller tracks that): no zeroing launches here
   const bool cnt_ready = schedule & SV_SCHED_CNT_READY;
+  // every layer's whole-K weight-gradient tiles in one launch where they fit one round of the CUs
+  // (gemm_bf16_8qf_kernel; layer 0's N = F dW_ih after it on the narrow kernel), the split form
+  // (first pieces on the CUs the tiles leave free, their flags on channel SV_BWD_CH0 + WB_L) where
+  // at least 8 CUs are left over and the partials fit the GEMM scratch
+  auto plan_fullk = [&](G8Full& f, int& fP) -> bool {
+    const int cus = sv_stream_cus(main);
+    f = G8Full{};
+    fP = 0;
+    if (!(L == WB_L && gemm256_ok(4 * H, H, TBp) && TBp % 8 == 0 && ldhT % 8 == 0)) return false;
+    bool fullk = true;
+    f.K = TBp;
+    for (int l = 0; l < L; ++l) {
+      const bool dual = l > 0;  // upper layers: input width H
+      G8FLayer& fl = f.lay[l];
+      fl.A = dgT[l];
+      fl.lda = TBp;
+      fl.B = hT[l];
+      fl.ldb = ldhT;
+      fl.B2 = dual ? xT[l] : nullptr;
+      fl.ldb2 = dual ? ld_xT[l] : 0;
+      fl.C1 = dw_hh[l];
+      fl.ldc1 = H;
+      fl.C2 = dual ? dw_ih[l] : nullptr;
+      fl.ldc2 = H;
+      fl.n1 = H;
+      fl.N = dual ? 2 * H : H;
+      fl.tiles = (4 * H / G256_BM) * (fl.N / G256_BM);
+      fP += fl.tiles;
+      if (((uintptr_t)dgT[l] | (uintptr_t)hT[l] | (uintptr_t)dw_hh[l]) & 15) fullk = false;
+      if (dual && ((((uintptr_t)xT[l] | (uintptr_t)dw_ih[l]) & 15) || ld_xT[l] % 8)) fullk = false;
+    }
+    fullk = fullk && fP <= cus;
+    const BBwdWs wsp = carve_bbwd((char*)workspace + per * (L - 1), T, B, std::max(F, H), H);
+    const int KT = TBp / G256_BK;
+    f.nsw = fullk ? (cus - fP) / 8 * 8 : 0;
+    if (f.nsw > 0) {
+      const int per_wg = (fP + f.nsw - 1) / f.nsw;  // first pieces per workgroup
+      f.S = KT / (per_wg + 1) - 2;    // (their stores and prologues: a little less)
+    }
+    if (f.nsw <= 0 || f.S < 4 || (size_t)fP * G256_BM * G256_BM * 4 > wsp.gbytes) f.nsw = f.S = 0;
+    if (f.S > 0) {
+      f.part = wsp.gws;
+      f.flag = sync + SV_SYNC_CNT + (size_t)(SV_BWD_CH0 + WB_L) * SV_PCNT_ROWS * SV_PCNT_STRIDE;
+      f.status = sync;
+      f.limit = sv_persist_limit();
+    }
+    return fullk;
+  };
+  // the whole-K launch, then layer 0's dW_ih and the layers' completion events
+  auto run_fullk = [&](const G8Full& f, int fP) -> int {
+    hipLaunchKernelGGL(gemm_bf16_8qf_kernel, dim3(f.nsw + fP), dim3(512), G256_LDS, main, f);
+    SV_LAUNCH_CHECK();
+    for (int l = L - 1; l >= 1 && evs; --l)
+      if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
+    const BBwdWs ws = carve_bbwd((char*)workspace, T, B, std::max(F, H), H);
+    if (int rc = sv_gemm_bf16(4 * H, F, TBp, dgT[0], TBp, xT[0], ld_xT[0], dw_ih[0], F, nullptr, nullptr, 0.f, ws.gws,
+                              main))
+      return rc;
+    if (evs && (e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
+    return SV_OK;
+  };
   if (sched_wave(schedule, H) && sv_wave_bwd_fits(L, B, H, sv_stream_cus(main))) {
     if (!sync) return SV_EARG;
     // layer-wavefront schedule: every layer's recurrence and upstream gradient dx in one launch
@@ -1378,68 +1442,14 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     }
     int rc = wt_ready ? 0 : wbf_transposes(L, F, H, w_ih, w_hh, whhT_l, wihT_l, main);
     if (rc) return rc;
-    const int cus = sv_stream_cus(main);
-    // every layer's whole-K weight-gradient tiles in one launch where they fit one round of the CUs
-    // (gemm_bf16_8qf_kernel; layer 0's N = F dW_ih after it on the narrow kernel)
-    G8Full f{};
-    int fP = 0;
-    bool fullk = false;
-    if (L == WB_L && gemm256_ok(4 * H, H, TBp) && TBp % 8 == 0 && ldhT % 8 == 0) {
-      f.K = TBp;
-      fullk = true;
-      for (int l = 0; l < L; ++l) {
-        const bool dual = l > 0;  // upper layers: input width H
-        G8FLayer& fl = f.lay[l];
-        fl.A = dgT[l];
-        fl.lda = TBp;
-        fl.B = hT[l];
-        fl.ldb = ldhT;
-        fl.B2 = dual ? xT[l] : nullptr;
-        fl.ldb2 = dual ? ld_xT[l] : 0;
-        fl.C1 = dw_hh[l];
-        fl.ldc1 = H;
-        fl.C2 = dual ? dw_ih[l] : nullptr;
-        fl.ldc2 = H;
-        fl.n1 = H;
-        fl.N = dual ? 2 * H : H;
-        fl.tiles = (4 * H / G256_BM) * (fl.N / G256_BM);
-        fP += fl.tiles;
-        if (((uintptr_t)dgT[l] | (uintptr_t)hT[l] | (uintptr_t)dw_hh[l]) & 15) fullk = false;
-        if (dual && ((((uintptr_t)xT[l] | (uintptr_t)dw_ih[l]) & 15) || ld_xT[l] % 8)) fullk = false;
-      }
-      fullk = fullk && fP <= cus;
-      // the split form where at least 8 CUs are left over and the partials fit the GEMM scratch
-      const BBwdWs wsp = carve_bbwd((char*)workspace + per * (L - 1), T, B, std::max(F, H), H);
-      const int KT = TBp / G256_BK;
-      f.nsw = fullk ? (cus - fP) / 8 * 8 : 0;
-      if (f.nsw > 0) {
-        const int per_wg = (fP + f.nsw - 1) / f.nsw;  // first pieces per workgroup
-        f.S = KT / (per_wg + 1) - 2;    // (their stores and prologues: a little less)
-      }
-      if (f.nsw <= 0 || f.S < 4 || (size_t)fP * G256_BM * G256_BM * 4 > wsp.gbytes) f.nsw = f.S = 0;
-      if (f.S > 0) {
-        f.part = wsp.gws;
-        f.flag = sync + SV_SYNC_CNT + (size_t)(SV_BWD_CH0 + WB_L) * SV_PCNT_ROWS * SV_PCNT_STRIDE;  // zeroed with the
-        f.status = sync;                                                             // wavefront's counters
-        f.limit = sv_persist_limit();
-      }
-    }
+    G8Full f;
+    int fP;
+    const bool fullk = plan_fullk(f, fP);
     rc = sv_wave_bwd_bf16(L, T, B, H, whhT_l, wihT_l, gates, c_tm, dh_last, dx, dgT, (char*)workspace + per * L,
                               sync, main, db_ih, db_hh, probe ? probe[0] : nullptr, probe ? probe[1] : nullptr,
                               bf16_wiht_ld(H), f.S > 0 ? fP : 0, SV_BWD_CH0, cnt_ready);
     if (rc) return rc;
-    if (fullk) {
-      hipLaunchKernelGGL(gemm_bf16_8qf_kernel, dim3(f.nsw + fP), dim3(512), G256_LDS, main, f);
-      SV_LAUNCH_CHECK();
-      for (int l = L - 1; l >= 1 && evs; --l)
-        if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
-      const BBwdWs ws = carve_bbwd((char*)workspace, T, B, std::max(F, H), H);
-      if ((rc = sv_gemm_bf16(4 * H, F, TBp, dgT[0], TBp, xT[0], ld_xT[0], dw_ih[0], F, nullptr, nullptr, 0.f, ws.gws,
-                             main)))
-        return rc;
-      if (evs && (e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
-      return SV_OK;
-    }
+    if (fullk) return run_fullk(f, fP);
     for (int l = L - 1; l >= 0; --l) {
       const int Fl = l == 0 ? F : H;
       const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
@@ -1468,6 +1478,14 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       }
       if (int rc = wt_ready ? 0 : wbf_transposes(L, F, H, w_ih, w_hh, whhT_l.data(), wihT_l.data(), main)) return rc;
     }
+    // the weight gradients of every layer after the last recurrence, as the layer wavefront's one
+    // whole-K launch (plan_fullk), where it applies; else per layer, split-K, after its recurrence
+    G8Full f;
+    int fP;
+    const bool fullk = SV_PERSIST_FULLK && plan_fullk(f, fP);
+    if (fullk && f.S > 0 && !cnt_ready) {  // the first pieces' flags (else zeroed by the forward)
+      if (int rc = sv_zero_counters(f.flag, 1, 0, fP, main)) return rc;
+    }
     for (int l = L - 1; l >= 0; --l) {
       const int Fl = l == 0 ? F : H;
       const BBwdWs ws = carve_bbwd((char*)workspace + per * l, T, B, std::max(F, H), H);
@@ -1488,7 +1506,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       // the last recurrence is done, so collectives never share the device with a persistent launch
       // (whose grid must be co-resident; a concurrent RCCL kernel would hold CUs it waits for) but
       // overlap layer 0's weight-gradient GEMMs
-      for (int k = 1; l == 0 && k < L && evs; ++k)
+      for (int k = 1; l == 0 && k < L && evs && !fullk; ++k)
         if ((e = hipEventRecord(ev[L * nch + k], main)) != hipSuccess) return (int)e;
       if (afr) {
         if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H, sv_stream_cus(main)), ws.wihT, bf16_wiht_ld(H), dx[l],
@@ -1498,11 +1516,13 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
                                               nullptr, 0.f, ws.gws, main))) {
         return rc;
       }
+      if (fullk) continue;
       // dW_hh and dW_ih in one pass over dG^T (falls back to two GEMMs for layer 0's F = 40)
       rc = sv_gemm_bf16_dual(4 * H, H, Fl, TBp, dgT[l], TBp, hT[l], ldhT, dw_hh[l], H, xT[l], ld_xT[l], dw_ih[l], Fl,
                              ws.gws, main);
       if (rc) return rc;
     }
+    if (fullk) return run_fullk(f, fP);
     if (evs && (e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
     return SV_OK;
   }

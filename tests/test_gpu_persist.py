@@ -37,7 +37,8 @@ def test_persistent_fwd_bf16_equals_per_step(dims, N, M, T):
 def test_persistent_bwd_bf16_equals_per_step(dims, N, M, T):
     """W-stationary persistent backward recurrence (one launch per layer, dG handed off through
     HBM) vs per-step launches: the same per-gate MFMA order and the same gate-order sum, so dG,
-    the weight gradients and dx are bit-identical.  The bias gradients are summed inside the
+    the weight gradients and dx are bit-identical (the weight gradients: where both schedules sum
+    K = T Bp in one order, see below).  The bias gradients are summed inside the
     persistent kernel (over t per element, then rows, then row blocks) instead of by a row-sum
     kernel over dG^T: the same bf16 values in another fp32 order."""
     a = _run("step", "per_step", dims, N, M, T)
@@ -53,20 +54,31 @@ def test_persistent_bwd_bf16_equals_per_step(dims, N, M, T):
     # bound is ~40x that: a dropped or double-counted k-piece moves a gradient by O(1e-2)
     H = dims[1]
     sk = H == 768 and (T * N * M) % 256 == 0 and (T * N * M // 256) * (H // 256) > 256
+    # r06: with 3 layers at H = 768 the persistent schedule forms every layer's weight gradients
+    # after the last recurrence as ONE whole-K launch (one accumulator over K = T Bp); where the
+    # per-step schedule splits that K (K >= 8192: split-K slabs) the weight gradients are the same
+    # products summed in another fp32 order (bound 1e-5 relative, measured in the MEASURED line)
+    Bp = (N * M + 7) // 8 * 8
+    fk = dims[2] == 3 and H == 768 and (T * Bp) % 64 == 0 and T * Bp >= 8192
     top = f"_l{dims[2] - 1}"
-    worst = 0.0
+    worst = worst_w = 0.0
     for k in grads:
+        rel = float(np.abs(b[k] - a[k]).max()) / max(float(np.abs(a[k]).max()), 1e-30)
         if sk and top not in k and "projection" not in k:
-            dev = float(np.abs(b[k] - a[k]).max()) / max(float(np.abs(a[k]).max()), 1e-30)
-            worst = max(worst, dev)
-            assert dev <= 1e-5, (k, dev)
+            worst = max(worst, rel)
+            assert rel <= 1e-5, (k, rel)
         elif ".bias_" in k:
             np.testing.assert_allclose(b[k], a[k], rtol=1e-5, atol=1e-6 * np.abs(a[k]).max(), err_msg=k)
+        elif fk and ".weight_" in k and "projection" not in k:
+            worst_w = max(worst_w, rel)
+            assert rel <= 1e-5, (k, rel)
         else:
             np.testing.assert_array_equal(b[k], a[k], err_msg=k)
     if sk:
         print(f"\nMEASURED persist_vs_per_step_bf16.T{T}.lower_layer_grad_rel {worst:.2e} (stream-K dx)")
-    np.testing.assert_allclose(b["flat_p"], a["flat_p"], rtol=0, atol=1e-6 if sk else 1e-7)
+    if fk:
+        print(f"\nMEASURED persist_vs_per_step_bf16.T{T}.weight_grad_rel {worst_w:.2e} (whole-K dW)")
+    np.testing.assert_allclose(b["flat_p"], a["flat_p"], rtol=0, atol=1e-6 if (sk or fk) else 1e-7)
 
 
 @pytest.mark.parametrize("N,M,T", [(32, 10, 9),    # c5's per-rank 320 rows: 20 x 12 workgroups
