@@ -562,6 +562,7 @@ struct G8FLayer {
   float* C2;          // dW_ih (dual)
   long lda, ldb, ldb2, ldc1, ldc2;
   int N, n1, tiles;
+  int f2;             // dW_ih columns (rows of x^T): layer 0's F = 40 in one partial 256-wide tile
 };
 struct G8Full {
   G8FLayer lay[WB_L];
@@ -593,10 +594,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qf_kernel(const G8Full q) {
     const long ldb2 = l == 2 ? L2.ldb2 : l == 1 ? L1.ldb2 : L0.ldb2;
     const int N = l == 2 ? L2.N : l == 1 ? L1.N : L0.N;
     const int n1 = l == 2 ? L2.n1 : l == 1 ? L1.n1 : L0.n1;
+    const int f2 = l == 2 ? L2.f2 : l == 1 ? L1.f2 : L0.f2;
     const int tiles_n = N / G256_BM;
     tn = tile % tiles_n;
     tm = tile / tiles_n;
-    g8_tile<0>(A, lda, Bm, ldb, G256AFrag{}, G256Dual{B2, ldb2, n1}, tm, tn, kbeg, nk, smem, acc);
+    g8_tile<0>(A, lda, Bm, ldb, G256AFrag{}, G256Dual{B2, ldb2, n1, f2}, tm, tn, kbeg, nk, smem, acc);
   };
   g8_f32x4 acc[8][4];
   int l, tm, tn;
@@ -637,9 +639,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qf_kernel(const G8Full q) {
   const long ldc1 = l == 2 ? L2.ldc1 : l == 1 ? L1.ldc1 : L0.ldc1;
   const long ldc2 = l == 2 ? L2.ldc2 : l == 1 ? L1.ldc2 : L0.ldc2;
   const int n1 = l == 2 ? L2.n1 : l == 1 ? L1.n1 : L0.n1;
+  const int f2 = l == 2 ? L2.f2 : l == 1 ? L1.f2 : L0.f2;
   const bool second = tn * G256_BM >= n1;  // n1 % 256 == 0 (host): a tile is all C1 or all C2
   g8_epilogue<G8_STORE>(acc, second ? C2 : C1, second ? ldc2 : ldc1, 0, tm, second ? tn - n1 / G256_BM : tn, wr, wc,
-                        lane, nullptr, nullptr, 0.f);
+                        lane, nullptr, nullptr, 0.f, second && f2 > 0 ? f2 : 1 << 30);
 }
 
 }  // namespace
@@ -1379,7 +1382,11 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     bool fullk = true;
     f.K = TBp;
     for (int l = 0; l < L; ++l) {
-      const bool dual = l > 0;  // upper layers: input width H
+      // upper layers: dW_ih beside dW_hh (input width H, 3 column tiles); layer 0 too (x0 tile):
+      // its F <= 256 columns as one partial column tile (x^T rows clamped, F columns stored) --
+      // the narrow GEMM after the launch re-read all of dG^T_0 for them (c5 rank 76 + 10 us)
+      const bool x0 = l == 0 && F <= G256_BM && F % 4 == 0;
+      const bool dual = l > 0 || x0;
       G8FLayer& fl = f.lay[l];
       fl.A = dgT[l];
       fl.lda = TBp;
@@ -1390,13 +1397,14 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       fl.C1 = dw_hh[l];
       fl.ldc1 = H;
       fl.C2 = dual ? dw_ih[l] : nullptr;
-      fl.ldc2 = H;
+      fl.ldc2 = l > 0 ? H : F;
       fl.n1 = H;
-      fl.N = dual ? 2 * H : H;
+      fl.N = l > 0 ? 2 * H : x0 ? H + G256_BM : H;
+      fl.f2 = x0 ? F : 0;
       fl.tiles = (4 * H / G256_BM) * (fl.N / G256_BM);
       fP += fl.tiles;
       if (((uintptr_t)dgT[l] | (uintptr_t)hT[l] | (uintptr_t)dw_hh[l]) & 15) fullk = false;
-      if (dual && ((((uintptr_t)xT[l] | (uintptr_t)dw_ih[l]) & 15) || ld_xT[l] % 8)) fullk = false;
+      if (dual && ((((uintptr_t)xT[l] | (uintptr_t)dw_ih[l]) & 15) || ld_xT[l] % 8 || fl.ldc2 % 4)) fullk = false;
     }
     fullk = fullk && fP <= cus;
     const BBwdWs wsp = carve_bbwd((char*)workspace + per * (L - 1), T, B, std::max(F, H), H);
@@ -1421,10 +1429,12 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     SV_LAUNCH_CHECK();
     for (int l = L - 1; l >= 1 && evs; --l)
       if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
-    const BBwdWs ws = carve_bbwd((char*)workspace, T, B, std::max(F, H), H);
-    if (int rc = sv_gemm_bf16(4 * H, F, TBp, dgT[0], TBp, xT[0], ld_xT[0], dw_ih[0], F, nullptr, nullptr, 0.f, ws.gws,
-                              main))
-      return rc;
+    if (!f.lay[0].f2) {  // layer 0's dW_ih (F > 256) on its own
+      const BBwdWs ws = carve_bbwd((char*)workspace, T, B, std::max(F, H), H);
+      if (int rc = sv_gemm_bf16(4 * H, F, TBp, dgT[0], TBp, xT[0], ld_xT[0], dw_ih[0], F, nullptr, nullptr, 0.f, ws.gws,
+                                main))
+        return rc;
+    }
     if (evs && (e = hipEventRecord(ev[L * nch], main)) != hipSuccess) return (int)e;
     return SV_OK;
   };

@@ -28,11 +28,14 @@ __device__ __forceinline__ int g256_phys_slot(int row, int slot) { return slot ^
 // row q >> 3, physical slot q & 7, holding logical slot (q & 7) ^ ((row >> 1) & 7) of that row
 struct G256Stage {
   const bf16_t* src[4];
-  __device__ __forceinline__ void init(const bf16_t* base, long ld, int row0, int k0, int tid) {
+  // rmax > 0: source rows clamped to rmax - 1 (a partial last tile: its padding rows' products
+  // land only in C columns the epilogue does not store)
+  __device__ __forceinline__ void init(const bf16_t* base, long ld, int row0, int k0, int tid, int rmax = 0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int q = tid + 512 * i, row = q >> 3, ls = g256_phys_slot(row, q & 7);
-      src[i] = base + (long)(row0 + row) * ld + k0 + ls * 8;
+      const int r = rmax > 0 ? min(row0 + row, rmax - 1) : row0 + row;
+      src[i] = base + (long)r * ld + k0 + ls * 8;
     }
   }
   // DMA k-tile kt into `lds` (this operand's 32 KB of one stage); wave-uniform destination
@@ -58,6 +61,7 @@ struct G256Dual {
   const bf16_t* B2;
   long ldb2;
   int n1;
+  int rows2;  // rows of B2 (0: whole tiles); the rows past it read its last row (results unused)
 };
 struct G256AFrag {
   const bf16_t* base;  // dgf
@@ -279,16 +283,18 @@ __device__ __forceinline__ void g8_bias(const float* bias0, const float* bias1, 
   }
 }
 
+// ncol: C columns stored (the rest of a partial last tile dropped; a multiple of 4)
 template <int EPI>
 __device__ __forceinline__ void g8_epilogue(g8_f32x4 (&acc)[8][4], void* Cv, long ldc, long slab, int tm, int tn,
                                             int wr, int wc, int lane, const float* bias0, const float* bias1,
-                                            float beta) {
+                                            float beta, int ncol = 1 << 30) {
   const int fr = lane & 15, fq = lane >> 4;
   g8_f32x4 bsum[4];
   if (EPI != G8_SLAB) g8_bias(bias0, bias1, tn, wc, fq, bsum);
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
     const int col = tn * G256_BM + wc * 64 + 16 * nt + 4 * fq;
+    if (col >= ncol) continue;
     const g8_f32x4 badd = EPI != G8_SLAB ? bsum[nt] : g8_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) {
@@ -371,7 +377,7 @@ __device__ __forceinline__ void g8_tile(const bf16_t* __restrict__ A, long lda, 
   G256Stage sa, sb;
   if constexpr (!AF) sa.init(A, lda, tm * G256_BM, kbeg, tid);
   if (dual.B2 && tn * G256_BM >= dual.n1)
-    sb.init(dual.B2, dual.ldb2, tn * G256_BM - dual.n1, kbeg, tid);
+    sb.init(dual.B2, dual.ldb2, tn * G256_BM - dual.n1, kbeg, tid, dual.rows2);
   else
     sb.init(B, ldb, tn * G256_BM, kbeg, tid);
   constexpr int OPB = G256_BM * G256_BK * 2;

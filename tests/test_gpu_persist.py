@@ -55,11 +55,12 @@ def test_persistent_bwd_bf16_equals_per_step(dims, N, M, T):
     H = dims[1]
     sk = H == 768 and (T * N * M) % 256 == 0 and (T * N * M // 256) * (H // 256) > 256
     # r06: with 3 layers at H = 768 the persistent schedule forms every layer's weight gradients
-    # after the last recurrence as ONE whole-K launch (one accumulator over K = T Bp); where the
-    # per-step schedule splits that K (K >= 8192: split-K slabs) the weight gradients are the same
+    # after the last recurrence as ONE whole-K launch (one accumulator over K = T Bp, layer 0's
+    # dW_ih as a partial tile of it); where the per-step schedule splits that K (split-K slabs:
+    # dW_hh / dW_ih of the upper layers at K >= 8192, layer 0's narrow dW_ih always) they are the same
     # products summed in another fp32 order (bound 1e-5 relative, measured in the MEASURED line)
     Bp = (N * M + 7) // 8 * 8
-    fk = dims[2] == 3 and H == 768 and (T * Bp) % 64 == 0 and T * Bp >= 8192
+    fk = dims[2] == 3 and H == 768 and (T * Bp) % 64 == 0
     top = f"_l{dims[2] - 1}"
     worst = worst_w = 0.0
     for k in grads:
