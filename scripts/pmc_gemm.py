@@ -10,7 +10,7 @@ import sys
 from collections import defaultdict
 
 d = sys.argv[1]
-PREFIX = ("gemm_f32_256", "gemm_f32_narrow", "gemm_bf16_8q", "gemm_bf16_kernel")
+PREFIX = ("gemm_f32_256", "gemm_f32_narrow", "gemm_bf16_8q", "gemm_bf16_kernel", "gemm_bf16_narrow")
 
 
 def grid(r):
@@ -21,16 +21,17 @@ def grid(r):
 
 def key(r):
     n = r["Kernel_Name"]
-    if not n.startswith("void "):
-        return None
-    short = n[5:].split("(")[0]
+    for pre in ("void ", "(anonymous namespace)::"):
+        if n.startswith(pre):
+            n = n[len(pre):]
+    short = n.split("(")[0]
     if not short.startswith(PREFIX):
         return None
     return f"{short} grid={grid(r)}"
 
 
 out = {}
-for w in ("f32", "bf16"):
+for w in ("f32", "bf16", "c4", "c5"):
     tr = glob.glob(os.path.join(d, f"{w}_trace", "**", "*kernel_trace.csv"), recursive=True)
     pm = glob.glob(os.path.join(d, f"{w}_pmc", "**", "*counter_collection.csv"), recursive=True)
     if not tr or not pm:
