@@ -294,6 +294,23 @@ __device__ __forceinline__ float lstm_cell_bwd(float dh, float i, float f, float
 // the same per-element operations in the same order as lstm_cell_bwd (contraction off, the
 // transcendentals per element), so results are bit-identical to it.
 typedef float f2_t __attribute__((ext_vector_type(2)));
+// x + b for a pair, each rounded to bf16 (nearest even) and back: one v_pk_add_f32 and one
+// v_cvt_pk_bf16_f32 for both (round_bf(x.x + b), round_bf(x.y + b), bit for bit)
+__device__ __forceinline__ f2_t round_bf2(f2_t x, float b) {
+  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+  const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(x + b, bf2_t));
+  return f2_t{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+// acc[i] += round_bf(x[i] + b) over 16 accumulator elements, in pairs
+template <typename V>
+__device__ __forceinline__ void add_round_bf16x(V& acc, const V& x, float b) {
+#pragma unroll
+  for (int i = 0; i < 16; i += 2) {
+    const f2_t s = f2_t{acc[i], acc[i + 1]} + round_bf2(f2_t{x[i], x[i + 1]}, b);
+    acc[i] = s.x;
+    acc[i + 1] = s.y;
+  }
+}
 __device__ __forceinline__ f2_t bf_tanh2(f2_t x) {
 #pragma clang fp contract(off)
   const f2_t y = -2.0f * x;

@@ -389,11 +389,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
         x0 = mfma_bf16(__builtin_bit_cast(bf16x8_t, xa[s2][0]), wx[s2], x0);
         if constexpr (BM == 64) x1 = mfma_bf16(__builtin_bit_cast(bf16x8_t, xa[s2][1]), wx[s2], x1);
       }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        acc0[i] += round_bf(x0[i] + xbias);
-        if constexpr (BM == 64) acc1[i] += round_bf(x1[i] + xbias);
-      }
+      add_round_bf16x(acc0, x0, xbias);
+      if constexpr (BM == 64) add_round_bf16x(acc1, x1, xbias);
     }
     // gate exchange: wave g's [BM rows][32 units] -> pre[row][g * 32 + unit]
 #pragma unroll

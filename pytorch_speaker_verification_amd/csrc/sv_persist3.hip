@@ -517,11 +517,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
         x0 = mfma_bf16(__builtin_bit_cast(bf16x8_t, xa[s2]), wxa[s2], x0);
         x1 = mfma_bf16(__builtin_bit_cast(bf16x8_t, xa[s2]), wxb[s2], x1);
       }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        acc0[i] += round_bf(x0[i] + xba);
-        acc1[i] += round_bf(x1[i] + xbb);
-      }
+      add_round_bf16x(acc0, x0, xba);
+      add_round_bf16x(acc1, x1, xbb);
     }
     // gate exchange: wave g's [32 rows][64 units] -> pre[row][g * 64 + unit]
 #pragma unroll

@@ -210,7 +210,11 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
       for (int s = 0; s < WV_XS; ++s) acc = mfma_bf16(__builtin_bit_cast(bf16x8_t, xa[s]), wx[s], acc);
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = round_bf(acc[i] + xbias);
+    for (int i = 0; i < 16; i += 2) {
+      const f2_t v = round_bf2(f2_t{acc[i], acc[i + 1]}, xbias);
+      acc[i] = v.x;
+      acc[i + 1] = v.y;
+    }
     mark(2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __shared__ int xflag;
