@@ -301,6 +301,22 @@ __device__ __forceinline__ f2_t round_bf2(f2_t x, float b) {
   const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(x + b, bf2_t));
   return f2_t{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
 }
+// the cell backward's dG of 4 units x 4 gates (ddv[unit][gate]) as bf16 pairs, pr[gate][p] = units
+// 2p (low half) and 2p + 1 (high half), one v_cvt_pk_bf16_f32 per pair; dbs[gate][unit] (the bias
+// partials) += the rounded values, two per v_pk_add_f32 (the per-element form's sums, bit for bit)
+__device__ __forceinline__ void pack_dg4(const float (&ddv)[4][4], unsigned (&pr)[4][2], float (&dbs)[4][4]) {
+  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(f2_t{ddv[2 * p][q], ddv[2 * p + 1][q]}, bf2_t));
+      pr[q][p] = u;
+      const f2_t d = f2_t{dbs[q][2 * p], dbs[q][2 * p + 1]} + f2_t{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+      dbs[q][2 * p] = d.x;
+      dbs[q][2 * p + 1] = d.y;
+    }
+}
 // acc[i] += round_bf(x[i] + b) over 16 accumulator elements, in pairs
 template <typename V>
 __device__ __forceinline__ void add_round_bf16x(V& acc, const V& x, float b) {

@@ -712,7 +712,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
       const float a1[4] = {f1.x, f1.y, f1.z, f1.w};
       const float a2[4] = {f2.x, f2.y, f2.z, f2.w};
       const float a3[4] = {f3.x, f3.y, f3.z, f3.w};
-      unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
+      unsigned pk[4][2];
       float dh4[4];  // (elementwise, the scalar order)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
@@ -724,17 +724,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
       }
       float ddv[4][4];
       lstm_cell_bwd_x4(dh4, a0, a1, a2, a3, cs, cps, dcf[k], ddv);
+      pack_dg4(ddv, pk, dbs[k]);
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const float (&dd)[4] = ddv[v];
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bf16_t e = to_bf(dd[q]);
-          gts[(q * BF_U + u4 + v) * LDT + b] = e;
-          pk[q][v >> 1] |= (unsigned)e << (16 * (v & 1));
-          dbs[k][q][v] += __uint_as_float((unsigned)e << 16);
-        }
-      }
+        for (int v = 0; v < 4; ++v) gts[(q * BF_U + u4 + v) * LDT + b] = (bf16_t)(pk[q][v >> 1] >> (16 * (v & 1)));
 #pragma unroll
       for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(dgs + b * LDG + q * BF_U + u4) = uint2{pk[q][0], pk[q][1]};
       cv[k] = cpv[k];  // c_{t-1} is the next step's c_t

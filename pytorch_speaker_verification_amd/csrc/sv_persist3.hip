@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
         for (int q = 0; q < 4; ++q)
           f[q] = unpack_bf4(*reinterpret_cast<const uint2*>(ewa + b * 512 + ((q + b) & 3) * 128 + (u4 >> 3) * 16 +
                                                             (u4 & 7) * 2));
-        unsigned pk[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
+        unsigned pk[4][2];
         float4 dh4 = r0;  // (elementwise, the scalar order)
         dh4 += r1;
         dh4 += r2;
@@ -224,22 +224,20 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
         dh4 += upv;
         float ddv[4][4];
         lstm_cell_bwd_x4(dh4, f[0], f[1], f[2], f[3], cv[k], cpv, dcf[k], ddv);
+        pack_dg4(ddv, pk, dbs);
+        const int sw = (2 * brow) ^ (((u4 >> 4) & 3) << 3);  // (the same for the 4 units)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const float (&dd)[4] = ddv[v];
-          const int u = u4 + v, sw = (2 * brow) ^ (((u >> 4) & 3) << 3);
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const unsigned e = to_bf(dd[q]);
-            pk[q][v >> 1] |= e << (16 * (v & 1));
-            dbs[q][v] += __uint_as_float(e << 16);
-            if (k == 0)
-              e0s[q][v >> 1] |= e << (16 * (v & 1));
-            else if (!(dbg & 256))  // (profiling: 256 skips the transposed-tile writes)
-              *reinterpret_cast<unsigned*>(gts + (q * U + u) * LDT + sw) =
-                  ((e0s[q][v >> 1] >> (16 * (v & 1))) & 0xffffu) | (e << 16);
+          for (int p = 0; p < 2; ++p) {
+            if (k == 0) {
+              e0s[q][p] = pk[q][p];
+            } else {
+              const int u = u4 + 2 * p;
+              *reinterpret_cast<unsigned*>(gts + (q * U + u) * LDT + sw) = (e0s[q][p] & 0xffffu) | (pk[q][p] << 16);
+              *reinterpret_cast<unsigned*>(gts + (q * U + u + 1) * LDT + sw) = (e0s[q][p] >> 16) | (pk[q][p] & 0xffff0000u);
+            }
           }
-        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(dgs + b * LDG + q * U + u4) = uint2{pk[q][0], pk[q][1]};
         cv[k] = cpv;  // c_{t-1} is the next step's c_t
@@ -872,6 +870,7 @@ __global__ __launch_bounds__(256, 1) void lstm_wave_bwd_bf16_kernel(const WaveBw
       dh4 += upv;
       float ddv[4][4];
       lstm_cell_bwd_x4(dh4, f[0], f[1], f[2], f[3], cv, cpv, dcf, ddv);
+      // (per element here: the packed pairs of pack_dg4 measured +10 us per c4 rank step)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const float (&dd)[4] = ddv[v];
