@@ -240,8 +240,14 @@ __device__ __forceinline__ float from_bf(bf16_t x) { return __uint_as_float((uns
 // x rounded to bf16 (nearest even) and back: the stored x-projection of the bf16 path
 __device__ __forceinline__ float round_bf(float x) { return from_bf(to_bf(x)); }
 // 4 consecutive bf16 <-> 4 floats (8-B loads / stores of activations and x-projections)
+// a (low half) and b (high half) rounded to bf16 in one v_cvt_pk_bf16_f32 (to_bf's rounding, bit for bit)
+__device__ __forceinline__ unsigned pack_bf2(float a, float b) {
+  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+  typedef float fl2_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(fl2_t{a, b}, bf2_t));
+}
 __device__ __forceinline__ uint2 pack_bf4(float a, float b, float c, float d) {
-  return uint2{(unsigned)to_bf(a) | ((unsigned)to_bf(b) << 16), (unsigned)to_bf(c) | ((unsigned)to_bf(d) << 16)};
+  return uint2{pack_bf2(a, b), pack_bf2(c, d)};
 }
 __device__ __forceinline__ float4 unpack_bf4(uint2 p) {
   return float4{__uint_as_float(p.x << 16), __uint_as_float(p.x & 0xffff0000u), __uint_as_float(p.y << 16),

@@ -303,8 +303,8 @@ __device__ __forceinline__ void g8_epilogue(g8_f32x4 (&acc)[8][4], void* Cv, lon
       if constexpr (EPI == G8_STORE_BF16) {
         v += badd;
         bf16_t* dst = reinterpret_cast<bf16_t*>(Cv) + row * ldc + col;
-        const unsigned lo = (unsigned)to_bf(v[0]) | ((unsigned)to_bf(v[1]) << 16);
-        const unsigned hi = (unsigned)to_bf(v[2]) | ((unsigned)to_bf(v[3]) << 16);
+        const unsigned lo = pack_bf2(v[0], v[1]);
+        const unsigned hi = pack_bf2(v[2], v[3]);
         *reinterpret_cast<uint2*>(dst) = uint2{lo, hi};
       } else {
         float* dst = reinterpret_cast<float*>(Cv) + (EPI == G8_SLAB ? slab : 0) + row * ldc + col;  // slab: offset
@@ -349,8 +349,8 @@ __device__ __forceinline__ void g8_epilogue_bf16_lds(g8_f32x4 (&acc)[8][4], bf16
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) {
       const g8_f32x4 v = acc[mt][nt] + bsum[nt];
-      const unsigned lo = (unsigned)to_bf(v[0]) | ((unsigned)to_bf(v[1]) << 16);
-      const unsigned hi = (unsigned)to_bf(v[2]) | ((unsigned)to_bf(v[3]) << 16);
+      const unsigned lo = pack_bf2(v[0], v[1]);
+      const unsigned hi = pack_bf2(v[2], v[3]);
       *reinterpret_cast<uint2*>(tile + (16 * mt + fr) * 128 + (16 * nt + 4 * fq) * 2) = uint2{lo, hi};
     }
   }
@@ -569,8 +569,8 @@ __device__ __forceinline__ void g8_epilogue_bf16_half(g8_f32x4 (&acc)[8][4], int
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const g8_f32x4 v = acc[4 * hlf + m][nt] + badd;
-      const unsigned lo = (unsigned)to_bf(v[0]) | ((unsigned)to_bf(v[1]) << 16);
-      const unsigned hi = (unsigned)to_bf(v[2]) | ((unsigned)to_bf(v[3]) << 16);
+      const unsigned lo = pack_bf2(v[0], v[1]);
+      const unsigned hi = pack_bf2(v[2], v[3]);
       *reinterpret_cast<uint2*>(tile + (16 * m + fr) * 128 + (16 * nt + 4 * fq) * 2) = uint2{lo, hi};
     }
   }

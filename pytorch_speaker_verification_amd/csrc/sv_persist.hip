@@ -429,10 +429,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
         for (int q = 0; q < 4; ++q) ao[q][v] = a4[q];
         co[v] = c;
         ho[v] = h;
-        const bf16_t e = to_bf(h);
-        hts[(u4 + v) * LDT + b] = e;
-        pk[v >> 1] |= (unsigned)e << (16 * (v & 1));
       }
+      pk[0] = pack_bf2(ho[0], ho[1]);
+      pk[1] = pack_bf2(ho[2], ho[3]);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) hts[(u4 + v) * LDT + b] = (bf16_t)(pk[v >> 1] >> (16 * (v & 1)));
       *reinterpret_cast<uint2*>(hsb + b * LDB + u4) = uint2{pk[0], pk[1]};
 #pragma unroll
       for (int q = 0; q < 4; ++q) act[k][q] = pack_bf4(ao[q][0], ao[q][1], ao[q][2], ao[q][3]);

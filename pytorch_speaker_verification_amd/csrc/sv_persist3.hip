@@ -559,8 +559,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
         co[v1] = c.y;
         ho[v0] = h.x;
         ho[v1] = h.y;
-        const bf16_t e0 = to_bf(h.x), e1 = to_bf(h.y);
-        pk[vp] = (unsigned)e0 | ((unsigned)e1 << 16);
+        pk[vp] = pack_bf2(h.x, h.y);
+        const bf16_t e0 = (bf16_t)pk[vp], e1 = (bf16_t)(pk[vp] >> 16);
         if (k == 0) {
           hk0[vp] = pk[vp];
         } else {  // a unit's two rows as one 4-B write into the transposed tile (chunk swizzle)
