@@ -299,6 +299,12 @@ __device__ __forceinline__ float lstm_cell_bwd(float dh, float i, float f, float
 // Two elements at once in packed fp32 (v_pk_mul_f32 / v_pk_add_f32: one VALU issue for both):
 // the same per-element operations in the same order as lstm_cell_bwd (contraction off, the
 // transcendentals per element), so results are bit-identical to it.
+// the persistent bf16 kernels' diagnostic bits (dbg, profiling only, results invalid) are honoured
+// only in A/B builds with -DSV_PDBG=-1; product builds fold every such branch away (the runtime
+// value in per-element code cost scheduling: DESIGN §4)
+#ifndef SV_PDBG
+#define SV_PDBG 0
+#endif
 typedef float f2_t __attribute__((ext_vector_type(2)));
 // x + b for a pair, each rounded to bf16 (nearest even) and back: one v_pk_add_f32 and one
 // v_cvt_pk_bf16_f32 for both (round_bf(x.x + b), round_bf(x.y + b), bit for bit)

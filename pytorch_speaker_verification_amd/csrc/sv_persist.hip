@@ -229,6 +229,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_fwd_bf16_kernel(const bf
                                                                        const bf16_t* __restrict__ wih_bf,
                                                                        const float* __restrict__ b_ih,
                                                                        const float* __restrict__ b_hh) {
+  if (!SV_PDBG) pipe = 1;  // (the non-pipelined k-loop: A/B builds only)
   constexpr int K = NS * 16, LDA = K + 8, HALF = NS / 2 * 16;
   constexpr int LDP = 4 * BF_U + 4;      // pre [BM][LDP] fp32
   constexpr int LDB = BF_U + 8;          // hsb [BM][LDB] bf16 (h tile, row-major)
@@ -509,6 +510,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist2_bwd_bf16_kernel(
     const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
     bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit,
     int fault, int dbg, float* __restrict__ dbp, unsigned long long* __restrict__ stamps) {
+  dbg &= SV_PDBG;
   constexpr int LDR = BF_U + 4;          // red [4][BM][LDR] fp32 (16-B aligned rows)
   constexpr int LDG = 4 * BF_U + 8;      // dgs [BM][LDG] bf16 (row-major dG tile)
   constexpr int LDT = BM + 8;            // gts [128][LDT] bf16 (transposed dG tile)

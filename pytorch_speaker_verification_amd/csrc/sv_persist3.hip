@@ -24,6 +24,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_bwd_bf16_kernel(
     const float* __restrict__ dhup, int up_full, bf16_t* __restrict__ dg, bf16_t* __restrict__ dgT, long lddgT,
     bf16_t* dgf, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd, unsigned* status, unsigned limit,
     int fault, int dbg, float* __restrict__ dbp, unsigned long long* __restrict__ stamps) {
+  dbg &= SV_PDBG;
   constexpr int BM = 32, U = 64, KR = 2;  // rows, units, row passes of the epilogue (16 rows each)
   constexpr int LDR = U + 4;              // red [4][BM][LDR] fp32
   constexpr int LDG = 4 * U + 8;          // dgs [BM][LDG] bf16 (row-major dG tile)
@@ -343,6 +344,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist3_fwd_bf16_kernel(
     bf16_t* h_bf, bf16_t* __restrict__ hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd,
     unsigned* status, unsigned limit, int fault, const bf16_t* __restrict__ x_bf, const bf16_t* __restrict__ wih_bf,
     const float* __restrict__ b_ih, const float* __restrict__ b_hh, int dbg) {
+  dbg &= SV_PDBG;
   // dbg (SV_PERSIST_DEBUG, profiling only, results invalid): 1 no hand-off waits, 2 no recurrent
   // MFMAs, 8 no post-arrival stores
   constexpr int BM = 32, U = 64, KR = 2;
