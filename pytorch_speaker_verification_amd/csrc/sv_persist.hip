@@ -1092,7 +1092,8 @@ constexpr size_t pbwd_lds(int bm) {
          (size_t)bm * 512;  // + the LDS-DMA operand image (EWD)
 }
 // the backward kernels' diagnostic bits: 0 in the product library (an A/B edit sets e.g. 32 = per-phase
-// cycle stamps into the caller's sync block, read by scripts/persist_ab.py)
+// cycle stamps into the caller's sync block, read by scripts/persist_ab.py, in a build with
+// FLAGS=-DSV_PDBG=-1: the kernels fold the bits away otherwise)
 constexpr int kPbwdDebug = 0;
 template <int NS, int P>
 void launch_pbwd(dim3 grid, int bm, hipStream_t s, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,

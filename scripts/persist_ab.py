@@ -1,6 +1,6 @@
 """A/B timing of the bf16 stack forward and backward at c3 (B = 640, T = 160, H = 768), HIP events
 on the stream, for the product library or an A/B build (`make ab NAME=x FLAGS=...`, --lib).
-With a stamp build (FLAGS=-DSV_PBWD_DEBUG=32) it also prints the persistent backward's cycles per
+With a stamp build (kPbwdDebug = 32 in sv_persist.hip, FLAGS=-DSV_PDBG=-1) it also prints the persistent backward's cycles per
 step by phase (workgroup 0..N of the last backward layer launch: wait, A stream + MFMA + partial
 exchange, cell epilogue, hand-off stores + arrival, post-arrival issue).
 Usage: python scripts/persist_ab.py [--lib scripts/ab/libsv_ge2e_x.so] [--iters 5] [--B 640]"""
@@ -74,7 +74,7 @@ if st64.abs().sum() > 0:
     out["bwd_cycles_per_step"] = {k: round(float(v), 1) for k, v in zip(names, per)}
     out["bwd_cycles_total"] = round(float(per.sum()), 1)
     out["stamped_wgs"] = nwg
-# forward stamps (FLAGS=-DSV_PFWD_DEBUG=32): workgroup slots 512 .. of the same area, the last
+# forward stamps (the forward launcher's dbg = 32, FLAGS=-DSV_PDBG=-1): workgroup slots 512 .. of the same area, the last
 # forward layer launch of the timed forwards
 fw = ps.block[stamp0:stamp0 + 2 * 1024 * 8].view(torch.int64).view(1024, 8)[512:, :6].cpu().double()
 if fw.abs().sum() > 0:
