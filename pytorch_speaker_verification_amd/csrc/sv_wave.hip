@@ -126,6 +126,7 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
   unsigned* my_cnt = a.cnt[l] + rb * SV_PCNT_STRIDE;
   unsigned* below = L0 ? nullptr : a.cnt[l - 1] + rb * SV_PCNT_STRIDE;
   const unsigned producers = nub;
+  const int dbg = a.dbg & SV_PDBG;  // (diagnostic bits: A/B builds with -DSV_PDBG=-1 only)
   const bool wok = j0 + r < H;
   bf16x8_t wh[WV_NS], wx[WV_NS];
   {
@@ -177,7 +178,7 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
     // h_{t-1} (t = 0: slot 0, zeros -- the h-part then adds exact zeros, so every step has the
     // same DMA / wait shape and the compiler can count the waits)
     if (tid == 0 && t > 0) wv_wait(my_cnt, producers * (unsigned)t, a.status, a.limit);
-    if (a.dbg & 1)
+    if (dbg & 1)
       __syncthreads();  // debug: drain everything (the x DMA too) here
     else
       raw_barrier();
@@ -218,7 +219,7 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
     mark(2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __shared__ int xflag;
-    if (!L0 && tid == 0) xflag = (t + 1 < T && xpoll >= producers * (unsigned)(t + 2) && !(a.dbg & 2)) ? 1 : 0;
+    if (!L0 && tid == 0) xflag = (t + 1 < T && xpoll >= producers * (unsigned)(t + 2) && !(dbg & 2)) ? 1 : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();  // every wave past the x-part: tile_x is free
     bool xe = false;
@@ -250,10 +251,11 @@ __device__ __forceinline__ void w3_run(const WaveFwd2Args& a, int l, int ub, int
         for (int q = 0; q < 4; ++q) ao[q][v] = a4[q];
         co[v] = c;
         ho[v] = h;
-        const bf16_t e = to_bf(h);
-        hts[(u4 + v) * WV_LDT + brow] = e;
-        pk[v >> 1] |= (unsigned)e << (16 * (v & 1));
       }
+      pk[0] = pack_bf2(ho[0], ho[1]);
+      pk[1] = pack_bf2(ho[2], ho[3]);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) hts[(u4 + v) * WV_LDT + brow] = (bf16_t)(pk[v >> 1] >> (16 * (v & 1)));
       *reinterpret_cast<uint2*>(hsb + brow * WV_LDB + u4) = uint2{pk[0], pk[1]};
 #pragma unroll
       for (int q = 0; q < 4; ++q) act[q] = pack_bf4(ao[q][0], ao[q][1], ao[q][2], ao[q][3]);
