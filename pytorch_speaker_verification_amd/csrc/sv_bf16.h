@@ -306,6 +306,12 @@ __device__ __forceinline__ float lstm_cell_bwd(float dh, float i, float f, float
 #define SV_PDBG 0
 #endif
 typedef float f2_t __attribute__((ext_vector_type(2)));
+// a pair rounded to bf16 (nearest even) and back: one v_cvt_pk_bf16_f32 (round_bf, bit for bit)
+__device__ __forceinline__ f2_t round_bf2(f2_t x) {
+  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+  const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf2_t));
+  return f2_t{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
 // x + b for a pair, each rounded to bf16 (nearest even) and back: one v_pk_add_f32 and one
 // v_cvt_pk_bf16_f32 for both (round_bf(x.x + b), round_bf(x.y + b), bit for bit)
 __device__ __forceinline__ f2_t round_bf2(f2_t x, float b) {
@@ -453,6 +459,13 @@ int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
                            int xcd, unsigned* status, unsigned limit, int fault, const bf16_t* x_bf = nullptr,
                            int F = 0, const bf16_t* wih_bf = nullptr, const float* b_ih = nullptr,
                            const float* b_hh = nullptr, int dbg = 0);
+// launcher of the 16-row wide persistent forward (sv_persist3.hip; nrb x nub workgroups, H = 768,
+// B % 16 == 0; x_bf: layer 0's input projection in the kernel, F = 40)
+int sv_persist16_fwd_launch(int nrb, int nub, hipStream_t stream, const bf16_t* whh_bf, bf16_t* gates, float* c_tm,
+                            float* h_tm, bf16_t* h_bf, bf16_t* hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt,
+                            int xcd, unsigned* status, unsigned limit, int fault, const bf16_t* x_bf = nullptr,
+                            int F = 0, const bf16_t* wih_bf = nullptr, const float* b_ih = nullptr,
+                            const float* b_hh = nullptr);
 // CUs of the device `stream` belongs to (cached per device); dims fit co-resident on `cus` CUs
 int sv_stream_cus(hipStream_t stream);
 int sv_persist_fwd_fits(int B, int H, int cus);

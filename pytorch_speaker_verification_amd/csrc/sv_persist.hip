@@ -1019,6 +1019,12 @@ int persist_bm(int B, int H, int cus) {
 }
 }  // namespace
 
+// the 16-row wide forward (sv_persist16_fwd_launch): H = 768, whole 16-row blocks, B > 256 (below, the
+// 32 x 32 tile keeps its bit-identity with the per-step schedule), (B / 16) x (H / 64) co-resident
+int pfwd16_ok(int B, int H, int cus) {
+  return H == 768 && B % 16 == 0 && B > 256 && B / 16 <= SV_PCNT_ROWS && (long)(B / 16) * (H / 64) <= cus;
+}
+
 // can the persistent forward compute layer 0's input projection in-kernel (F = 40 features)?
 int sv_persist_fwd_fusex_ok(int H, int F) { return H == 768 && F == 40; }
 
@@ -1041,15 +1047,23 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
   // wide tile (32 rows x 64 units, sv_persist3.hip) where the wide backward runs, with or without
   // the fused layer-0 projection
   const bool wide = wst && pbwd3_ok(B, H, cus);
-  const int bm = wide ? 32 : wst ? persist_bm(B, H, cus) : BF_BM;
-  const dim3 grid(wide ? H / 64 : (H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
+  // 16-row wide tile (sv_persist3.hip, with or without the fused layer-0 projection) where it keeps
+  // the 32-row tile's workgroup count (B in (256, 320] at H = 768 on 256 CUs: c5's rank shape)
+  const bool p16 = wst && !wide && pfwd16_ok(B, H, cus);
+  const int bm = wide ? 32 : p16 ? 16 : wst ? persist_bm(B, H, cus) : BF_BM;
+  const dim3 grid(wide || p16 ? H / 64 : (H + BF_U - 1) / BF_U, (B + bm - 1) / bm);
   hipError_t e = counters_zeroed ? hipSuccess : (hipError_t)sv_zero_counters(cnt, 1, 0, grid.y * SV_PCNT_STRIDE, stream);
   if (e != hipSuccess) return (int)e;
   const unsigned limit = persist_limit();
   const int fault = fwd_fault();
   constexpr int dbg = 0, pipe = 1;  // (no diagnostic skips: the kernels' dbg bits are for A/B edits); LDS-pipelined A fragments
   if (pre && (e = hipEventRecord(pre, stream)) != hipSuccess) return (int)e;  // timing probe
-  if (wide) {
+  if (p16) {
+    const int rc = sv_persist16_fwd_launch((int)grid.y, (int)grid.x, stream, whh_bf, gates, c_tm, h_tm, h_bf, hT, ldhT,
+                                           T, Bp, B, H, cnt, kPersistXcd, status, limit, fault, x_bf, F, wih_bf, b_ih,
+                                           b_hh);
+    if (rc) return rc;
+  } else if (wide) {
     const int rc = sv_persist3_fwd_launch(dim3(grid.x * grid.y), (int)grid.x, stream, whh_bf, gates, c_tm, h_tm, h_bf,
                                           hT, ldhT, T, Bp, B, H, cnt, kPersistXcd, status, limit, fault, x_bf, F,
                                           wih_bf, b_ih, b_hh, dbg);

@@ -648,6 +648,292 @@ int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
 }
 
 // ============================================================================
+// 16-row wide forward (c5's per-rank batch: 320 rows = 20 x 12 workgroups, layers without the
+// fused input projection).  Tile: 16 batch rows x 64 units x 4 gates.  Against the 32 x 32 tile
+// (the same 240 workgroups) each workgroup stages half the h_{t-1} bytes per step (24 KB) and
+// reads half the A fragments from LDS, for the same MFMA time: v_mfma_f32_16x16x32_bf16 with
+// wave g's W_hh rows of the 64 units (4 column tiles x 24 k-steps = 96 fragments: 64 in AGPRs, the
+// rest in VGPRs and NL in LDS, one per k-step of the last NL) as the first operand, so a lane's
+// 4 accumulators are 4 consecutive units of one row (16-B exchange writes).  Same cell helper,
+// hand-off (bf16 h rows, 16-B sc1 stores, one counter per 16-row block) and outputs (activations,
+// c, h^T, fp32 h_{T-1}) as the 32-row kernels.  The MFMA's k-blocking differs (32 per instruction
+// against 16); the tests hold this shape to the per-step schedule at fp32 level
+// (tests/test_gpu_persist.py; its losses came out bit-identical).  Measured: c5 rank step 6.58-6.62
+// vs 6.67-6.69 ms.
+// ============================================================================
+// XF > 0 (layer 0, F = 8 XF <= 64 features): the input projection formed in the kernel from x_bf [T,B,F] and W_ih
+// [4H,F] (two k-steps of 32, zero past F), rounded to bf16 with its biases as the K1 path stores it, then
+// added to the recurrent part (the 32-row kernels' fused form)
+template <int NL, int PA, int XF>
+__global__ __launch_bounds__(256, 1) void lstm_persist16_fwd_bf16_kernel(
+    const bf16_t* __restrict__ whh_bf, bf16_t* __restrict__ gates, float* __restrict__ c_tm, float* __restrict__ h_tm,
+    bf16_t* h_bf, bf16_t* __restrict__ hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt, int nub, int xcd,
+    unsigned* status, unsigned limit, int fault, const bf16_t* __restrict__ x_bf, const bf16_t* __restrict__ wih_bf,
+    const float* __restrict__ b_ih, const float* __restrict__ b_hh) {
+  constexpr int BM = 16, U = 64, K = 768, KS = K / 32;  // 24 k-steps of 32
+  constexpr int NLS = KS - NL;                          // k-steps whose 4 fragments are all in registers
+  constexpr int NRF = 4 * NLS + 3 * NL;                 // register fragments (84 at NL = 12)
+  constexpr int NA = 64;                                // ... of which in AGPRs
+  constexpr int LDA = K + 8;                            // As [BM][LDA] bf16
+  constexpr int LDP = 4 * U + 4;                        // pre [BM][LDP] fp32
+  constexpr int LDB = U + 8;                            // hsb [BM][LDB] bf16
+  constexpr int LDT = BM + 8;                           // hts [U][LDT] bf16
+  static_assert(NRF > NA && PA >= 1 && PA <= KS, "register plan");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);
+  float* pre = reinterpret_cast<float*>(smem + BM * LDA * 2);
+  bf16_t* hsb = reinterpret_cast<bf16_t*>(pre + BM * LDP);
+  bf16_t* hts = hsb + BM * LDB;
+  char* wl = reinterpret_cast<char*>(hts + U * LDT);  // [4 waves][NL][64 lanes][16 B]
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  int ub, rb;
+  persist_tile(xcd, nub, ub, rb);
+  const int j0 = ub * U, b0 = rb * BM;
+  const long G = 4L * H, BH = (long)B * H, BG = (long)B * G;
+  unsigned* my_cnt = cnt + rb * SV_PCNT_STRIDE;
+  const unsigned producers = nub;
+  // fragment (k-step s, column tile nt) of gate g: lane -> W_hh row g H + j0 + 16 nt + fr, k = 32 s +
+  // 8 fq.  Register index: 4 s + nt for s < NLS, then 3 per k-step (nt = 0..2); nt = 3 of the last NL
+  // k-steps in LDS
+  constexpr auto ridx = [](int s_, int nt_) { return s_ < NLS ? 4 * s_ + nt_ : 4 * NLS + 3 * (s_ - NLS) + nt_; };
+  bf16x8_t wr[NRF];
+  {
+    const bf16_t* base = whh_bf + ((long)g * H + j0 + fr) * K + 8 * fq;
+    const bf16x8_t z = {};
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const bf16x8_t v = j0 + 16 * nt + fr < H ? *reinterpret_cast<const bf16x8_t*>(base + (long)16 * nt * K + 32 * s_) : z;
+        if (s_ >= NLS && nt == 3)
+          *reinterpret_cast<bf16x8_t*>(wl + ((g * NL + s_ - NLS) * 64 + lane) * 16) = v;
+        else
+          wr[ridx(s_, nt)] = v;
+      }
+#pragma unroll
+    for (int f = 0; f < NA; ++f) asm volatile("" : "+a"(wr[f]));
+  }
+  auto wl_read = [&](int j) { return *reinterpret_cast<const bf16x8_t*>(wl + ((g * NL + j) * 64 + lane) * 16); };
+  // fused input projection (XF > 0): W_ih fragments of the 4 column tiles (k = 32 s2 + 8 fq, zero
+  // past F) and the biases of the lane's accumulator columns (unit 16 nt + 4 fq + v)
+  constexpr int F = 8 * XF;
+  static_assert(F <= 64, "two k-steps of 32");
+  bf16x8_t wx[XF > 0 ? 2 : 1][4];
+  float xb[XF > 0 ? 4 : 1][4];
+  if constexpr (XF > 0) {
+    const bf16x8_t z = {};
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int row = g * H + j0 + 16 * nt + fr, k = 32 * s2 + 8 * fq;
+        wx[s2][nt] = (k < F && j0 + 16 * nt + fr < H) ? *reinterpret_cast<const bf16x8_t*>(wih_bf + (long)row * F + k) : z;
+      }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int c = g * H + j0 + 16 * nt + 4 * fq + v;
+        xb[nt][v] = j0 + 16 * nt + 4 * fq + v < H ? (b_ih ? b_ih[c] : 0.f) + (b_hh ? b_hh[c] : 0.f) : 0.f;
+      }
+  }
+  u32x4_t xa[2];
+  auto load_x = [&](int tt) {  // x_t rows b0 + fr, k = 32 s2 + 8 fq (zeros past F)
+    const __amdgpu_buffer_rsrc_t rxs = sv_rsrc(x_bf + (long)tt * B * F, (unsigned)((long)B * F * 2));
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int k = 32 * s2 + 8 * fq;
+      xa[s2] = __builtin_amdgcn_raw_buffer_load_b128(rxs, k < F ? ((unsigned)(b0 + fr) * (unsigned)F + k) * 2u : 0xFFFFFFF0u,
+                                                     0, 0);
+    }
+  };
+  // elementwise map: thread -> row brow, 4 consecutive units u4
+  const int u4 = (tid & 15) * 4, brow = tid >> 4;
+  float cst[4] = {0.f, 0.f, 0.f, 0.f};
+  uint2 xg[4];
+  auto load_xg = [&](int tt) {  // bf16(x W_ih^T + b) of step tt (K1 output), rows past B read zeros
+    if constexpr (XF > 0) {
+      load_x(tt);
+      return;
+    }
+    const __amdgpu_buffer_rsrc_t rx = sv_rsrc(gates + (long)tt * BG, (unsigned)(BG * 2));
+    const long gb = b0 + brow, gbv = gb < B ? gb : (long)B + 64;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const u32x2_t x = __builtin_amdgcn_raw_buffer_load_b64(rx, (unsigned)((gbv * G + q * H + j0 + u4) * 2), 0, 0);
+      xg[q] = uint2{x.x, x.y};
+    }
+  };
+  constexpr int CH = BM * K / 8 / 256;  // 16-B staging chunks per thread (6)
+  for (int t = 0; t < T; ++t) {
+    f32x4 acc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (t > 0) {
+      if (tid == 0) persist_wait(my_cnt, producers * (unsigned)t, status, limit, 1u);
+      __syncthreads();
+      {  // h_{t-1} of the 16 rows into LDS (sc1 loads: written by other workgroups this launch)
+        const __amdgpu_buffer_rsrc_t ra = sv_rsrc(h_bf + (long)t * BH, (unsigned)(BH * 2));
+        uint4 v[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int q = tid + 256 * i, row = q / (K / 8), c = (q % (K / 8)) * 8;
+          const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(
+              ra, ((unsigned)(b0 + row) * (unsigned)H + (unsigned)c) * 2u, 0, 16 /* sc1 */);
+          v[i] = uint4{x.x, x.y, x.z, x.w};
+        }
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int q = tid + 256 * i, row = q / (K / 8), c = (q % (K / 8)) * 8;
+          *reinterpret_cast<uint4*>(As + row * LDA + c) = v[i];
+        }
+      }
+      __syncthreads();
+      load_xg(t);
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16_t* A0 = As + fr * LDA + 8 * fq;
+      auto afrag = [&](int s_) { return *reinterpret_cast<const bf16x8_t*>(A0 + 32 * s_); };
+      bf16x8_t fa[PA], wq[2];
+#pragma unroll
+      for (int p_ = 0; p_ < PA; ++p_) fa[p_] = afrag(p_);
+#pragma unroll
+      for (int s_ = 0; s_ < KS; ++s_) {
+        const bf16x8_t a = fa[s_ % PA];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(s_ >= NLS && nt == 3 ? wq[s_ & 1] : wr[ridx(s_, nt < 3 || s_ < NLS ? nt : 0)],
+                                                            a, acc[nt], 0, 0, 0);
+        if (s_ + PA < KS) fa[s_ % PA] = afrag(s_ + PA);
+        if (s_ + 2 >= NLS && s_ + 2 < KS) wq[s_ & 1] = wl_read(s_ + 2 - NLS);  // two k-steps ahead
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+      load_xg(0);
+    }
+    if constexpr (XF > 0) {  // pre-activation = recurrent part + bf16(x_t W_ih^T + b_ih + b_hh)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        f32x4 x = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wx[s2][nt], __builtin_bit_cast(bf16x8_t, xa[s2]), x, 0, 0, 0);
+#pragma unroll
+        for (int v = 0; v < 4; v += 2) {
+          const f2_t r = round_bf2(f2_t{x[v], x[v + 1]} + f2_t{xb[nt][v], xb[nt][v + 1]});
+          const f2_t sm = f2_t{acc[nt][v], acc[nt][v + 1]} + r;
+          acc[nt][v] = sm.x;
+          acc[nt][v + 1] = sm.y;
+        }
+      }
+    }
+    // gate exchange: wave g's [16 rows][64 units] -> pre[row][g * 64 + unit]
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) *reinterpret_cast<f32x4*>(pre + fr * LDP + g * U + 16 * nt + 4 * fq) = acc[nt];
+    __syncthreads();
+    uint2 act[4];
+    float4 cv, hv;
+    {
+      const int b = brow;
+      float4 pq[4], xf[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        pq[q] = *reinterpret_cast<const float4*>(pre + b * LDP + q * U + u4);
+        xf[q] = XF > 0 ? float4{0.f, 0.f, 0.f, 0.f} : unpack_bf4(xg[q]);
+      }
+      float ao[4][4], co[4], ho[4];
+#pragma unroll
+      for (int vp = 0; vp < 2; ++vp) {  // unit pairs in packed fp32
+        const int v0 = 2 * vp, v1 = v0 + 1;
+        const f2_t pv[4] = {f2_t{pq[0][v0], pq[0][v1]}, f2_t{pq[1][v0], pq[1][v1]}, f2_t{pq[2][v0], pq[2][v1]},
+                            f2_t{pq[3][v0], pq[3][v1]}};
+        const f2_t xv[4] = {f2_t{xf[0][v0], xf[0][v1]}, f2_t{xf[1][v0], xf[1][v1]}, f2_t{xf[2][v0], xf[2][v1]},
+                            f2_t{xf[3][v0], xf[3][v1]}};
+        f2_t a4[4], h;
+        const f2_t c = lstm_cell_fwd2(pv, xv, f2_t{cst[v0], cst[v1]}, a4, h);
+        cst[v0] = c.x;
+        cst[v1] = c.y;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          ao[q][v0] = a4[q].x;
+          ao[q][v1] = a4[q].y;
+        }
+        co[v0] = c.x;
+        co[v1] = c.y;
+        ho[v0] = h.x;
+        ho[v1] = h.y;
+      }
+      const unsigned pk0 = pack_bf2(ho[0], ho[1]), pk1 = pack_bf2(ho[2], ho[3]);
+      *reinterpret_cast<uint2*>(hsb + b * LDB + u4) = uint2{pk0, pk1};
+      hts[(u4 + 0) * LDT + b] = (bf16_t)pk0;
+      hts[(u4 + 1) * LDT + b] = (bf16_t)(pk0 >> 16);
+      hts[(u4 + 2) * LDT + b] = (bf16_t)pk1;
+      hts[(u4 + 3) * LDT + b] = (bf16_t)(pk1 >> 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) act[q] = pack_bf4(ao[q][0], ao[q][1], ao[q][2], ao[q][3]);
+      cv = float4{co[0], co[1], co[2], co[3]};
+      hv = float4{ho[0], ho[1], ho[2], ho[3]};
+    }
+    __syncthreads();  // hsb, hts complete
+    // the hand-off: h_t bf16, 16 rows x 8 chunks of 8 units, one 16-B sc1 store per thread of 128
+    if (tid < BM * 8) {
+      const int row = tid >> 3, c = tid & 7, gb = b0 + row;
+      const __amdgpu_buffer_rsrc_t rw = sv_rsrc(h_bf + (long)(t + 1) * BH, (unsigned)(BH * 2));
+      if (gb < B && j0 + 8 * c < H) {
+        const uint4 v = *reinterpret_cast<const uint4*>(hsb + row * LDB + 8 * c);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rw,
+                                               ((unsigned)gb * (unsigned)H + (unsigned)(j0 + 8 * c)) * 2u, 0,
+                                               16 /* sc1 */);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0 && persist_arrive_ok(fault, t == 0))
+      __hip_atomic_fetch_add(my_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // off the critical chain: activations, c, h and h^T of step t
+    {
+      const long gb = b0 + brow;
+      if (gb < B) {
+        bf16_t* gp = gates + (long)t * BG + gb * G + j0 + u4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(gp + q * H) = act[q];
+        *reinterpret_cast<float4*>(c_tm + (long)t * BH + gb * H + j0 + u4) = cv;
+        if (t == T - 1) *reinterpret_cast<float4*>(h_tm + (long)(t + 1) * BH + gb * H + j0 + u4) = hv;
+      }
+    }
+    if (hT && tid < U * 2) {  // 64 unit rows x 2 chunks of 8 batch columns
+      const int u = tid >> 1, c = tid & 1, gb = b0 + 8 * c;
+      if (gb < Bp && j0 + u < H) {
+        bf16_t* row = hT + (long)(j0 + u) * ldhT;
+        *reinterpret_cast<uint4*>(row + (long)(t + 1) * Bp + gb) = *reinterpret_cast<const uint4*>(hts + u * LDT + 8 * c);
+        if (t == 0) *reinterpret_cast<uint4*>(row + gb) = uint4{0u, 0u, 0u, 0u};
+      }
+    }
+  }
+}
+
+int sv_persist16_fwd_launch(int nrb, int nub, hipStream_t stream, const bf16_t* whh_bf, bf16_t* gates, float* c_tm,
+                            float* h_tm, bf16_t* h_bf, bf16_t* hT, long ldhT, int T, int Bp, int B, int H, unsigned* cnt,
+                            int xcd, unsigned* status, unsigned limit, int fault, const bf16_t* x_bf, int F,
+                            const bf16_t* wih_bf, const float* b_ih, const float* b_hh) {
+  constexpr int NL = 12;
+  constexpr size_t lds = (size_t)16 * (768 + 8) * 2 + (size_t)16 * (4 * 64 + 4) * 4 + (size_t)16 * 72 * 2 +
+                         (size_t)64 * 24 * 2 + (size_t)4 * NL * 1024;
+  if (H != 768 || B % 16 || nub != H / 64) return SV_EARG;
+  if (x_bf) {  // layer 0, F = 40
+    if (F != 40 || !wih_bf) return SV_EARG;
+    hipLaunchKernelGGL((lstm_persist16_fwd_bf16_kernel<NL, 4, 5>), dim3(nrb * nub), dim3(256), lds, stream, whh_bf,
+                       gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, x_bf, wih_bf,
+                       b_ih, b_hh);
+  } else {
+    hipLaunchKernelGGL((lstm_persist16_fwd_bf16_kernel<NL, 4, 0>), dim3(nrb * nub), dim3(256), lds, stream, whh_bf,
+                       gates, c_tm, h_tm, h_bf, hT, ldhT, T, Bp, B, H, cnt, nub, xcd, status, limit, fault, nullptr,
+                       nullptr, nullptr, nullptr);
+  }
+  return (int)hipGetLastError();
+}
+
+// ============================================================================
 // Layer-wavefront backward for small per-GPU batches (c4's 80 rows per rank): ONE launch runs the
 // backward recurrences of all L layers.  The per-layer schedule at B = 80 runs 72 workgroups per
 // layer, one layer after another, each followed by its dx = dG W_ih GEMM; here workgroup (l, ub,
