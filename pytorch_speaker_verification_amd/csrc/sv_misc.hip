@@ -2,6 +2,7 @@
 // fused gradient-clip + SGD update (train_speech_embedder.py:63-65, SURVEY §8 a-I).
 #include <algorithm>
 #include "sv_common.h"
+#include "sv_gemm.h"
 #include "../../include/sv_ge2e.h"
 
 // emb = y / |y|_2 (torch.norm, no eps).  One wave per row.
@@ -137,6 +138,66 @@ __global__ __launch_bounds__(256) void proj_bwd_small_kernel(const float* __rest
     if (p0 + k < P && c < H) dW[(long)(p0 + k) * H + c] = v;
   }
 }
+// ---- the projection backward in one launch at larger B (B > 128: c2 / c3 / c5 rank) ----
+// The GEMM path's 6 launches (the dWp GEMM + its split-K reduce, a two-level column sum, the dh
+// GEMM + reduce) cost ~37 us at B = 640 for ~0.5 GFLOP.  Here one launch: 64 x 64 tiles of
+// dWp = dy^T h (K = B) and of dh = dy Wp (K = P) on the fp32 MFMA main loop (sv_gemm.h; exact fp32
+// products, one accumulator over K), and db = colsum(dy) in PB_DBW workgroups of 64 columns x 4
+// row quarters (PB_U loads in flight per thread, the quarters added in order).
+#define PB_DBW_COLS 64
+#define PB_U 16
+__global__ __launch_bounds__(256) void proj_bwd_tiles_kernel(const float* __restrict__ dy, const float* __restrict__ h,
+                                                             int B, int H, int P, const float* __restrict__ W,
+                                                             float* __restrict__ dW, float* __restrict__ db,
+                                                             float* __restrict__ dh, int ndw, int ndh) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tiles_h = (H + 63) / 64;
+  const int wm0 = (w >> 1) * 32, wn0 = (w & 1) * 32;
+  int id = blockIdx.x;
+  if (id < ndw + ndh) {
+    const bool isdw = id < ndw;
+    if (!isdw) id -= ndw;
+    const int tm = id / tiles_h, tn = id % tiles_h;
+    f32x16 acc[1][1];
+    zero_acc(acc);
+    const int M = isdw ? P : B;
+    if (isdw)  // A = dy as [K = B][M = P], B = h as [K = B][N = H]
+      gemm_mainloop<64, 64, 256, false, false, 1, 1>(dy, P, RowMapLinear{tm * 64, P}, h, H, RowMapLinear{tn * 64, H}, 0,
+                                                     B, lds, tid, wm0, wn0, acc);
+    else       // A = dy [M = B][K = P] k-contiguous, B = Wp as [K = P][N = H]
+      gemm_mainloop<64, 64, 256, true, false, 1, 1>(dy, P, RowMapLinear{tm * 64, B}, W, H, RowMapLinear{tn * 64, H}, 0,
+                                                    P, lds, tid, wm0, wn0, acc);
+    float* C = isdw ? dW : dh;
+    const int col = tn * 64 + wn0 + (lane & 31);
+    if (col < H) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = tm * 64 + wm0 + acc_row(r, lane);
+        if (row < M) C[(long)row * H + col] = acc[0][0][r];
+      }
+    }
+    return;
+  }
+  // db[c] = sum_b dy[b][c]: lane = column, wave = row quarter
+  const int c = (id - ndw - ndh) * PB_DBW_COLS + lane;
+  const int q = (B + 3) / 4, ba = w * q, be = min(B, ba + q);
+  float s_ = 0.f;
+  for (int b0 = ba; b0 < be; b0 += PB_U) {
+    float v[PB_U];
+#pragma unroll
+    for (int u = 0; u < PB_U; ++u) v[u] = (b0 + u < be && c < P) ? dy[(long)(b0 + u) * P + c] : 0.f;
+#pragma unroll
+    for (int u = 0; u < PB_U; ++u) s_ += v[u];
+  }
+  lds[w * 64 + lane] = s_;
+  __syncthreads();
+  if (w == 0 && c < P) db[c] = lds[lane] + lds[64 + lane] + lds[128 + lane] + lds[192 + lane];
+}
+static bool proj_tiles_ok(int B, int H, int P, const void* h, const void* W, const void* dy) {
+  return B > 128 && H % 4 == 0 && P % 4 == 0 && !(((uintptr_t)h | (uintptr_t)W | (uintptr_t)dy) & 15);
+}
+
 static bool proj_small_ok(int B, int H, int P, const void* h, const void* W) {
   return P <= 256 && H % 4 == 0 && B <= 128 && !(((uintptr_t)h | (uintptr_t)W) & 15);
 }
@@ -172,6 +233,16 @@ extern "C" int sv_proj_norm_bwd(const float* demb, const float* emb, const float
     const size_t lds = std::max((size_t)PJ_R * P + 4 * PJ_R * 64, (size_t)B * 8 + 4 * 8 * 64) * sizeof(float);
     hipLaunchKernelGGL(proj_bwd_small_kernel, dim3(ndh + ndw), dim3(256), lds, stream, dy, h_last, B, H, P, w_p, dw_p,
                        db_p, dh_last, ndh);
+    SV_LAUNCH_CHECK();
+    return SV_OK;
+  }
+  if (proj_tiles_ok(B, H, P, h_last, w_p, dy)) {
+    const int th = (H + 63) / 64, ndw = (P + 63) / 64 * th, ndh = (B + 63) / 64 * th;
+    const int ndb = (P + PB_DBW_COLS - 1) / PB_DBW_COLS;
+    constexpr size_t lds = 2 * SV_BK * (TileLd<false, 64>::value + TileLd<false, 64>::value) * sizeof(float);
+    static_assert(2 * SV_BK * (TileLd<true, 64>::value + TileLd<false, 64>::value) * sizeof(float) <= lds, "lds");
+    hipLaunchKernelGGL(proj_bwd_tiles_kernel, dim3(ndw + ndh + ndb), dim3(256), lds, stream, dy, h_last, B, H, P, w_p,
+                       dw_p, db_p, dh_last, ndw, ndh);
     SV_LAUNCH_CHECK();
     return SV_OK;
   }
