@@ -657,9 +657,9 @@ int sv_persist3_fwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t*
 // 4 accumulators are 4 consecutive units of one row (16-B exchange writes).  Same cell helper,
 // hand-off (bf16 h rows, 16-B sc1 stores, one counter per 16-row block) and outputs (activations,
 // c, h^T, fp32 h_{T-1}) as the 32-row kernels.  The MFMA's k-blocking differs (32 per instruction
-// against 16); the tests hold this shape to the per-step schedule at fp32 level
-// (tests/test_gpu_persist.py; its losses came out bit-identical).  Measured: c5 rank step 6.58-6.62
-// vs 6.67-6.69 ms.
+// against 16) but not the k order, and the outputs are bit-identical to the per-step schedule's
+// (tests/test_gpu_persist.py asserts it at 320 and 288 rows).  Measured: c5 rank step 6.58-6.62 vs
+// 6.67-6.69 ms.
 // ============================================================================
 // XF > 0 (layer 0, F = 8 XF <= 64 features): the input projection formed in the kernel from x_bf [T,B,F] and W_ih
 // [4H,F] (two k-steps of 32, zero past F), rounded to bf16 with its biases as the K1 path stores it, then

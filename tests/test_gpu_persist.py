@@ -28,6 +28,22 @@ def test_persistent_fwd_bf16_equals_per_step(dims, N, M, T):
             np.testing.assert_array_equal(b[k], a[k], err_msg=k)
 
 
+@pytest.mark.parametrize("N,M,T", [(32, 10, 9),    # c5's per-rank 320 rows: 20 x 12 workgroups
+                                   (32, 9, 7)])    # 288 rows: 18 row blocks
+def test_persistent_fwd_bf16_16row_tile_against_per_step(N, M, T):
+    """The 16-row wide forward (lstm_persist16_fwd_bf16_kernel, chosen for 257..320 rows, layer 0's
+    x-projection fused) against the per-step schedule, bit for bit: its v_mfma_f32_16x16x32_bf16 sums
+    each pre-activation over 32-wide k blocks where the per-step kernels' 32x32x16 sums 16-wide ones,
+    in the same k order -- measured identical on gfx950 (r06), and asserted so."""
+    dims = (40, 768, 3, 256)
+    a = _run("step", "per_step", dims, N, M, T)
+    b = _run("persist", "persist", dims, N, M, T)
+    assert int(b["status"][0]) == 0
+    for k in a:
+        if k in ("emb", "h_last", "loss") or k.startswith(("gates", "c")):
+            np.testing.assert_array_equal(b[k], a[k], err_msg=k)
+
+
 @pytest.mark.parametrize("dims,N,M,T", [((40, 768, 3, 256), 64, 10, 12),   # c3 grid: 24 x 10 workgroups
                                         ((40, 768, 3, 256), 64, 10, 40),   # c3, hand-off slots past T = 33
                                         ((40, 768, 3, 256), 56, 10, 9),    # B = 560: wide tiles, row-major dG
