@@ -444,10 +444,41 @@ int sv_persist_fwd_bf16(int T, int B, int H, const bf16_t* whh_bf, bf16_t* gates
 extern "C" int sv_persist_bwd_ok(int B, int H);
 extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H);
 int sv_persist_bm(int B, int H, int cus);
+struct DbFin;  // (below)
 int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
                         const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream,
                         unsigned* sync, float* db_ih = nullptr, float* db_hh = nullptr, hipEvent_t pre = nullptr,
-                        hipEvent_t post = nullptr, int chan = 0, int counters_zeroed = 0);
+                        hipEvent_t post = nullptr, int chan = 0, int counters_zeroed = 0,
+                        DbFin* defer = nullptr);
+// a persistent backward's bias-gradient finalize (db[c] = sum over the nrb row-block partials of
+// column c, rows in order; db_hh gets the same sums), deferred into the launch that follows the
+// recurrence (the dx GEMM, or the whole-K weight-gradient launch) as extra workgroups past its tiles:
+// up to SV_DBF_MAX layers, G columns each
+#define SV_DBF_MAX 3
+struct DbFin {
+  const float* dbp[SV_DBF_MAX];
+  float* db_ih[SV_DBF_MAX];
+  float* db_hh[SV_DBF_MAX];
+  int n, nrb, G;
+};
+// workgroups of `threads` threads the finalize needs
+__host__ __device__ inline int dbfin_blocks(const DbFin& f, int threads) {
+  return f.n > 0 ? f.n * ((f.G + threads - 1) / threads) : 0;
+}
+// finalize workgroup `blk` (0 .. dbfin_blocks - 1) with blockDim.x threads
+__device__ __forceinline__ void dbfin_run(const DbFin& f, int blk) {
+  const int per = (f.G + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int l = blk / per, c = (blk % per) * (int)blockDim.x + (int)threadIdx.x;
+  if (l >= f.n || c >= f.G) return;
+  const float* p = l == 0 ? f.dbp[0] : l == 1 ? f.dbp[1] : f.dbp[2];
+  float* o1 = l == 0 ? f.db_ih[0] : l == 1 ? f.db_ih[1] : f.db_ih[2];
+  float* o2 = l == 0 ? f.db_hh[0] : l == 1 ? f.db_hh[1] : f.db_hh[2];
+  float s = 0.f;
+  for (int r = 0; r < f.nrb; ++r) s += p[(long)r * f.G + c];
+  o1[c] = s;
+  if (o2) o2[c] = s;
+}
+int sv_dbfin_launch(const DbFin& f, hipStream_t stream);  // as its own launch (sv_persist.hip)
 // launcher of the wide-tile persistent backward (sv_persist3.hip; grid = nub x nrb workgroups)
 int sv_persist3_bwd_launch(dim3 grid, int nub, hipStream_t stream, const bf16_t* whhT, const bf16_t* acts,
                            const float* c_tm, const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, long lddgT,

@@ -572,6 +572,7 @@ struct G8Full {
   unsigned* flag;    // [P], zero before the launch
   unsigned* status;  // the sync block's status word
   unsigned limit;
+  DbFin fin;         // a deferred bias finalize: workgroups past the tiles (dbfin_blocks(fin, 512))
 };
 __global__ __launch_bounds__(512, 1) void gemm_bf16_8qf_kernel(const G8Full q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -581,6 +582,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8qf_kernel(const G8Full q) {
   const G8FLayer& L1 = q.lay[1];
   const G8FLayer& L0 = q.lay[0];
   const int P = L2.tiles + L1.tiles + L0.tiles;
+  if ((int)blockIdx.x >= q.nsw + P) {  // the deferred bias finalize (the highest blocks: nobody waits on them)
+    dbfin_run(q.fin, blockIdx.x - q.nsw - P);
+    return;
+  }
   // tile r (top layer first) -> its operands (field-wise selects: a dynamic index into the
   // kernel-argument struct would copy it to scratch)
   auto run = [&](int r, int kbeg, int nk, g8_f32x4 (&acc)[8][4], int& l, int& tm, int& tn) {
@@ -887,16 +892,26 @@ bool gemm_afrag_ok(int T, int B, int N, int H) {
          4 * H / G256_BK < 4096 && (unsigned long long)T * B * B < (1ull << 32);  // g256_af_koff / _rowoff exact
 }
 // (the split-K plan of sv_gemm_bf16 for the same shape)
+// fin: a deferred bias finalize (sv_persist_bwd_bf16's `defer`) done by extra workgroups of the
+// one-shot 8-phase launch, else by its own launch after the GEMM
 int gemm_bf16_afrag(int T, int B, int H, int N, const bf16_t* dgf, int bm, const bf16_t* Bop, long ldb, float* C,
-                    long ldc, float* workspace, hipStream_t stream) {
+                    long ldc, float* workspace, hipStream_t stream, const DbFin& fin) {
   const int M = T * B, K = 4 * H;
   const int tiles = (M / G256_BM) * (N / G256_BM);
   const long fs = (long)((B + bm - 1) / bm) * bm * 4 * H;
   const G256AFrag af = g256_afrag(dgf, fs, B, bm, H);
   const BPlan p = plan_bf16(M, N, K);
+  if (p.splitk == 1 && g8_ok(C, ldc, nullptr, nullptr)) {
+    hipLaunchKernelGGL((gemm_bf16_8q_kernel<G256_STORE, 1>), dim3(tiles + dbfin_blocks(fin, 512)), dim3(512), G256_LDS,
+                       stream, nullptr, 0L, Bop, ldb, (void*)C, ldc, 0L, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af,
+                       G256Dual{}, fin);
+    SV_LAUNCH_CHECK();
+    return SV_OK;
+  }
+  if (int rc = sv_dbfin_launch(fin, stream)) return rc;
   if (p.splitk == 1) {
-    launch_g256<G256_STORE, 1>(g8_ok(C, ldc, nullptr, nullptr), dim3(tiles, 1), stream, nullptr, 0L, Bop, ldb, C,
-                               ldc, 0L, M, N, K, p.kchunk, nullptr, nullptr, 0.f, af);
+    launch_g256<G256_STORE, 1>(false, dim3(tiles, 1), stream, nullptr, 0L, Bop, ldb, C, ldc, 0L, M, N, K, p.kchunk,
+                               nullptr, nullptr, 0.f, af);
     SV_LAUNCH_CHECK();
     return SV_OK;
   }
@@ -1425,7 +1440,7 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
   };
   // the whole-K launch, then layer 0's dW_ih and the layers' completion events
   auto run_fullk = [&](const G8Full& f, int fP) -> int {
-    hipLaunchKernelGGL(gemm_bf16_8qf_kernel, dim3(f.nsw + fP), dim3(512), G256_LDS, main, f);
+    hipLaunchKernelGGL(gemm_bf16_8qf_kernel, dim3(f.nsw + fP + dbfin_blocks(f.fin, 512)), dim3(512), G256_LDS, main, f);
     SV_LAUNCH_CHECK();
     for (int l = L - 1; l >= 1 && evs; --l)
       if ((e = hipEventRecord(ev[L * nch + l], main)) != hipSuccess) return (int)e;
@@ -1506,11 +1521,14 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
       // layer l on channel SV_BWD_CH0 + l, pre-zeroed by the forward (cnt_ready) where the layers fit
       // the channels, else each launch zeroing its own
       const bool own = L <= SV_SYNC_CHANNELS - SV_BWD_CH0;
+      // the bias-gradient finalize rides on the next launch (the dx GEMM; layer 0's: the whole-K
+      // weight-gradient launch), before the next recurrence reuses the partials' slots in dgf
+      DbFin fin{};
       if ((rc = sv_persist_bwd_bf16(T, B, H, ws.whhT, gates[l], c_tm[l], up, l < L - 1,
                                     (afr || l == 0) ? nullptr : dg[l],  // layer 0 has no dx GEMM
                                     dgT[l], dgf, main, sync, db_ih[l], db_hh ? db_hh[l] : nullptr,
                                     probe ? probe[2 * l] : nullptr, probe ? probe[2 * l + 1] : nullptr,
-                                    SV_BWD_CH0 + (own ? l : 0), own && cnt_ready)))
+                                    SV_BWD_CH0 + (own ? l : 0), own && cnt_ready, &fin)))
         return rc;
       // the completion events of layers >= 1 (grad_ready: a caller's bucketed all-reduce) fire once
       // the last recurrence is done, so collectives never share the device with a persistent launch
@@ -1520,11 +1538,15 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
         if ((e = hipEventRecord(ev[L * nch + k], main)) != hipSuccess) return (int)e;
       if (afr) {
         if ((rc = gemm_bf16_afrag(T, B, H, Fl, dgf, sv_persist_bm(B, H, sv_stream_cus(main)), ws.wihT, bf16_wiht_ld(H), dx[l],
-                                  Fl, ws.gws, main)))
+                                  Fl, ws.gws, main, fin)))
           return rc;
-      } else if (l > 0 && (rc = sv_gemm_bf16(T * B, Fl, 4 * H, dg[l], 4L * H, ws.wihT, bf16_wiht_ld(H), dx[l], Fl, nullptr,
-                                              nullptr, 0.f, ws.gws, main))) {
-        return rc;
+      } else if (l == 0 && fullk) {
+        f.fin = fin;
+      } else {
+        if ((rc = sv_dbfin_launch(fin, main))) return rc;
+        if (l > 0 && (rc = sv_gemm_bf16(T * B, Fl, 4 * H, dg[l], 4L * H, ws.wihT, bf16_wiht_ld(H), dx[l], Fl, nullptr,
+                                        nullptr, 0.f, ws.gws, main)))
+          return rc;
       }
       if (fullk) continue;
       // dW_hh and dW_ih in one pass over dG^T (falls back to two GEMMs for layer 0's F = 40)

@@ -528,11 +528,16 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_8q_kernel(const bf16_t* __re
                                                              long ldc, long slab, int M, int N, int K, int kchunk,
                                                              const float* __restrict__ bias0,
                                                              const float* __restrict__ bias1, float beta,
-                                                             G256AFrag af = G256AFrag{}, G256Dual dual = G256Dual{}) {
+                                                             G256AFrag af = G256AFrag{}, G256Dual dual = G256Dual{},
+                                                             DbFin fin = DbFin{}) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tiles_n = N / G256_BM;
   const int nwg = tiles_n * (M / G256_BM);
+  if (fin.n > 0 && (int)blockIdx.x >= nwg) {  // a deferred bias finalize (one-shot grids only)
+    dbfin_run(fin, blockIdx.x - nwg);
+    return;
+  }
   int id = xcd_remap(blockIdx.x, nwg), sl = 0;
   if (gridDim.y > 1) splitk_tile(nwg, id, sl);
   const int tn = id % tiles_n, tm = id / tiles_n;

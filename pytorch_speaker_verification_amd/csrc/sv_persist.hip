@@ -1158,7 +1158,7 @@ extern "C" size_t sv_persist_bwd_scratch(int T, int B, int H) {
 int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* acts, const float* c_tm,
                         const float* dhup, int up_full, bf16_t* dg, bf16_t* dgT, bf16_t* dgf, hipStream_t stream,
                         unsigned* sync, float* db_ih, float* db_hh, hipEvent_t pre, hipEvent_t post, int chan,
-                        int counters_zeroed) {
+                        int counters_zeroed, DbFin* defer) {
   const int cus = sv_stream_cus(stream);
   if (!sv_persist_bwd_fits(B, H, cus)) return SV_ESHAPE;
   if (!dgf || ((uintptr_t)dgf & 15) || !sync || chan < 0 || chan >= SV_SYNC_CHANNELS) return SV_EARG;
@@ -1192,12 +1192,27 @@ int sv_persist_bwd_bf16(int T, int B, int H, const bf16_t* whhT, const bf16_t* a
                       dbp);
   SV_LAUNCH_CHECK();
   if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
-  if (dbp) {
+  if (dbp && defer) {  // the caller's next launch sums the partials (dbfin_run)
+    *defer = DbFin{};
+    defer->dbp[0] = dbp;
+    defer->db_ih[0] = db_ih;
+    defer->db_hh[0] = db_hh;
+    defer->n = 1;
+    defer->nrb = (int)grid.y;
+    defer->G = 4 * H;
+  } else if (dbp) {
     hipLaunchKernelGGL(persist_db_finalize_kernel, dim3((4 * H + 255) / 256), dim3(256), 0, stream, dbp, (int)grid.y,
                        4 * H, db_ih, db_hh);
     SV_LAUNCH_CHECK();
   }
   return SV_OK;
+}
+
+__global__ void dbfin_kernel(const DbFin f) { dbfin_run(f, blockIdx.x); }
+int sv_dbfin_launch(const DbFin& f, hipStream_t stream) {
+  if (f.n <= 0) return SV_OK;
+  hipLaunchKernelGGL(dbfin_kernel, dim3(dbfin_blocks(f, 256)), dim3(256), 0, stream, f);
+  return (int)hipGetLastError();
 }
 
 // ---- layer-wavefront backward (lstm_wave_bwd_bf16_kernel, sv_persist3.hip) ----
