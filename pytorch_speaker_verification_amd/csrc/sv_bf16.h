@@ -544,4 +544,4 @@ int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, cons
                      const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
                      bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
                      float* const* db_hh, hipEvent_t pre, hipEvent_t post, long ldwih = 0,
-                     int zero_next = 0, int ch0 = 0, int counters_zeroed = 0);
+                     int zero_next = 0, int ch0 = 0, int counters_zeroed = 0, DbFin* defer = nullptr);

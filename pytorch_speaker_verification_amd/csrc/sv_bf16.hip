@@ -1470,9 +1470,10 @@ extern "C" int sv_lstm_stack_bwd_bf16(int L, int T, int B, int F, int H, const b
     G8Full f;
     int fP;
     const bool fullk = plan_fullk(f, fP);
+    // with the whole-K launch after it, the bias finalize rides on that launch (G8Full::fin)
     rc = sv_wave_bwd_bf16(L, T, B, H, whhT_l, wihT_l, gates, c_tm, dh_last, dx, dgT, (char*)workspace + per * L,
                               sync, main, db_ih, db_hh, probe ? probe[0] : nullptr, probe ? probe[1] : nullptr,
-                              bf16_wiht_ld(H), f.S > 0 ? fP : 0, SV_BWD_CH0, cnt_ready);
+                              bf16_wiht_ld(H), f.S > 0 ? fP : 0, SV_BWD_CH0, cnt_ready, fullk ? &f.fin : nullptr);
     if (rc) return rc;
     if (fullk) return run_fullk(f, fP);
     for (int l = L - 1; l >= 0; --l) {

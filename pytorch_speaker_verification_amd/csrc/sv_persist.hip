@@ -1241,7 +1241,7 @@ int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, cons
                      const bf16_t* const* acts, const float* const* c_tm, const float* dh_last, float* const* dx,
                      bf16_t* const* dgT, void* scratch, unsigned* sync, hipStream_t stream, float* const* db_ih,
                      float* const* db_hh, hipEvent_t pre, hipEvent_t post, long ldwih,
-                     int zero_next, int ch0, int counters_zeroed) {
+                     int zero_next, int ch0, int counters_zeroed, DbFin* defer) {
   if (!sv_wave_bwd_fits(L, B, H, sv_stream_cus(stream))) return SV_ESHAPE;
   if (!scratch || ((uintptr_t)scratch & 15) || !sync || !dh_last || !whhT || !wihT || !acts || !c_tm || !dx || !dgT)
     return SV_EARG;
@@ -1287,7 +1287,17 @@ int sv_wave_bwd_bf16(int L, int T, int B, int H, const bf16_t* const* whhT, cons
   const int rc = sv_wave_bwd_launch(a, stream);
   if (rc) return rc;
   if (post && (e = hipEventRecord(post, stream)) != hipSuccess) return (int)e;
-  if (db_ih) {  // every layer's bias gradients in one launch
+  if (db_ih && defer && L <= SV_DBF_MAX) {  // the caller's next launch sums the partials (dbfin_run)
+    *defer = DbFin{};
+    for (int l = 0; l < L; ++l) {
+      defer->dbp[l] = a.dbp[l];
+      defer->db_ih[l] = db_ih[l];
+      defer->db_hh[l] = db_hh ? db_hh[l] : nullptr;
+    }
+    defer->n = L;
+    defer->nrb = a.nrb;
+    defer->G = 4 * H;
+  } else if (db_ih) {  // every layer's bias gradients in one launch
     DbMulti m{};
     for (int l = 0; l < L; ++l) {
       m.dbp[l] = a.dbp[l];
