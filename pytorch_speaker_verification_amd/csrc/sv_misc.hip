@@ -46,7 +46,8 @@ __global__ __launch_bounds__(256) void rownorm_bwd_kernel(const float* __restric
 // flight per lane.  Exact fp32 products, fp32 accumulation in a fixed
 // order (another order than the MFMA GEMMs': results agree to fp32 rounding).  Measured (traces):
 // c4 rank (B = 80) 18-20 us against 27; c5 rank (B = 320) 59 us against 39 -- its K = B loop
-// grows with the batch while the GEMM path's does not, hence B <= 128.
+// grows with the batch while the GEMM path's does not, hence B <= 128.  Since r06 the MFMA-tile
+// kernel below is faster at every B; this one serves unaligned operands.
 #define PJ_R 4
 #define PJ_U 32  // loads in flight per thread
 __global__ __launch_bounds__(256) void proj_bwd_small_kernel(const float* __restrict__ dy, const float* __restrict__ h,
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(256) void proj_bwd_small_kernel(const float* __rest
     if (p0 + k < P && c < H) dW[(long)(p0 + k) * H + c] = v;
   }
 }
-// ---- the projection backward in one launch at larger B (B > 128: c2 / c3 / c5 rank) ----
+// ---- the projection backward in one launch (16-B aligned operands, any B: every config) ----
 // The GEMM path's 6 launches (the dWp GEMM + its split-K reduce, a two-level column sum, the dh
 // GEMM + reduce) cost ~37 us at B = 640 for ~0.5 GFLOP.  Here one launch: 64 x 64 tiles of
 // dWp = dy^T h (K = B) and of dh = dy Wp (K = P) on the fp32 MFMA main loop (sv_gemm.h; exact fp32
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(256) void proj_bwd_tiles_kernel(const float* __rest
   if (w == 0 && c < P) db[c] = lds[lane] + lds[64 + lane] + lds[128 + lane] + lds[192 + lane];
 }
 static bool proj_tiles_ok(int B, int H, int P, const void* h, const void* W, const void* dy) {
-  return B > 128 && H % 4 == 0 && P % 4 == 0 && !(((uintptr_t)h | (uintptr_t)W | (uintptr_t)dy) & 15);
+  return H % 4 == 0 && P % 4 == 0 && !(((uintptr_t)h | (uintptr_t)W | (uintptr_t)dy) & 15);
 }
 
 static bool proj_small_ok(int B, int H, int P, const void* h, const void* W) {
@@ -228,7 +229,7 @@ extern "C" int sv_proj_norm_bwd(const float* demb, const float* emb, const float
   float* gws = workspace + ((size_t)B * P * sizeof(float) + 255) / 256 * 64;
   hipLaunchKernelGGL(rownorm_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, demb, emb, ynorm, B, P, dy);
   SV_LAUNCH_CHECK();
-  if (proj_small_ok(B, H, P, h_last, w_p)) {
+  if (proj_small_ok(B, H, P, h_last, w_p) && !proj_tiles_ok(B, H, P, h_last, w_p, dy)) {
     const int ncb = (H + 63) / 64, ndh = (B + PJ_R - 1) / PJ_R * ncb, ndw = (P + 7) / 8 * ncb;
     const size_t lds = std::max((size_t)PJ_R * P + 4 * PJ_R * 64, (size_t)B * 8 + 4 * 8 * 64) * sizeof(float);
     hipLaunchKernelGGL(proj_bwd_small_kernel, dim3(ndh + ndw), dim3(256), lds, stream, dy, h_last, B, H, P, w_p, dw_p,
